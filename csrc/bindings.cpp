@@ -1,0 +1,379 @@
+// Python bindings: mlapi_amd._C
+//
+// Kernels take raw device pointers (ints) + a hipStream_t (int), so torch tensors are passed as
+// tensor.data_ptr() / torch.cuda.current_stream().cuda_stream without linking libtorch.
+// Blocking calls release the GIL.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <sys/eventfd.h>
+#include <unistd.h>
+
+#include <cmath>
+#include <mutex>
+
+#include "http/loadgen.h"
+#include "http/server.h"
+#include "mlapi/common.h"
+#include "mlapi/kernels.h"
+#include "runtime/engine.h"
+#include "runtime/float_repr.h"
+
+namespace py = pybind11;
+using namespace mlapi;
+
+namespace {
+
+template <typename T>
+T* ptr(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+hipStream_t stream_of(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Completion sink for Python/asyncio: the engine's completer thread appends and signals an
+// eventfd; Python watches the fd (loop.add_reader) and drains.
+class PySink : public Sink {
+ public:
+  PySink() {
+    fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (fd_ < 0) throw std::runtime_error("eventfd failed");
+  }
+  ~PySink() override { close(fd_); }
+  void on_complete(const Completion* c, size_t n, const std::shared_ptr<const Model>& m) override {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (size_t i = 0; i < n; ++i) {
+        items_.push_back(c[i]);
+        versions_.push_back(m ? m->version : 0);
+      }
+    }
+    const uint64_t one = 1;
+    ssize_t r = write(fd_, &one, sizeof one);
+    (void)r;
+  }
+  int fd() const { return fd_; }
+  py::list drain() {
+    std::vector<Completion> items;
+    std::vector<uint64_t> vers;
+    {
+      uint64_t v;
+      ssize_t r = read(fd_, &v, sizeof v);
+      (void)r;
+      std::lock_guard<std::mutex> lk(mu_);
+      items.swap(items_);
+      vers.swap(versions_);
+    }
+    py::list out;
+    for (size_t i = 0; i < items.size(); ++i)
+      out.append(py::make_tuple(items[i].tag, items[i].idx, items[i].status, items[i].p, items[i].latency_ns,
+                                vers[i]));
+    return out;
+  }
+
+ private:
+  int fd_;
+  std::mutex mu_;
+  std::vector<Completion> items_;
+  std::vector<uint64_t> versions_;
+};
+
+py::dict stats_dict(const EngineStats& s) {
+  py::dict d;
+  d["requests"] = s.requests;
+  d["batches"] = s.batches;
+  d["errors"] = s.errors;
+  py::list bh, lh;
+  for (auto v : s.batch_hist) bh.append(v);
+  for (auto v : s.latency_hist) lh.append(v);
+  d["batch_hist"] = bh;
+  d["latency_hist_us_pow2"] = lh;
+  d["latency_sum_us"] = s.latency_sum_us;
+  d["device_us_sum"] = s.device_us_sum;
+  d["queue_depth"] = s.queue_depth;
+  d["model_version"] = s.model_version;
+  d["healthy"] = s.healthy;
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "mlapi_amd native runtime: gfx950 HIP kernels, batching engine, HTTP server, load generator";
+
+  m.attr("KIND_BINARY") = (int)KIND_BINARY;
+  m.attr("KIND_BINARY_SOFTMAX") = (int)KIND_BINARY_SOFTMAX;
+  m.attr("KIND_MULTINOMIAL") = (int)KIND_MULTINOMIAL;
+  m.attr("KIND_OVR") = (int)KIND_OVR;
+  m.attr("DT_F64") = (int)DT_F64;
+  m.attr("DT_F32") = (int)DT_F32;
+  m.attr("DT_BF16") = (int)DT_BF16;
+
+  m.def("device_count", [] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("py_float_repr", [](double v) {
+    std::string s;
+    if (!append_py_float(s, v)) throw std::invalid_argument("non-finite");
+    return s;
+  });
+  m.def("parse_predict_body", [](const std::string& body, const std::vector<std::string>& names) -> py::object {
+    std::vector<double> out(names.size());
+    if (!parse_predict_body(body.data(), body.size(), names, out.data())) return py::none();
+    return py::cast(out);
+  });
+
+  // ---------------------------------------------------------------- kernels
+  m.def(
+      "linear_small",
+      [](int dt, uintptr_t X, int64_t ldx, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind,
+         uintptr_t out_idx, uintptr_t out_p, uintptr_t stream) {
+        launch_linear_small(dt, ptr<void>(X), ldx, ptr<void>(W), ptr<void>(b), B, F, K, kind, ptr<int32_t>(out_idx),
+                            ptr<void>(out_p), stream_of(stream));
+      },
+      py::arg("dt"), py::arg("X"), py::arg("ldx"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"),
+      py::arg("K"), py::arg("kind"), py::arg("out_idx"), py::arg("out_p"), py::arg("stream") = 0);
+  m.def(
+      "gemv_binary",
+      [](int dt, uintptr_t X, uintptr_t w, float bias, int64_t B, int F, int kind, uintptr_t out_idx,
+         uintptr_t out_p, uintptr_t stream) {
+        launch_gemv_binary(dt, ptr<void>(X), ptr<void>(w), bias, B, F, kind, ptr<int32_t>(out_idx),
+                           ptr<float>(out_p), stream_of(stream));
+      },
+      py::arg("dt"), py::arg("X"), py::arg("w"), py::arg("bias"), py::arg("B"), py::arg("F"), py::arg("kind"),
+      py::arg("out_idx"), py::arg("out_p"), py::arg("stream") = 0);
+  m.def("gemm_softmax_workspace", &gemm_softmax_workspace);
+  m.def(
+      "gemm_softmax",
+      [](uintptr_t X, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind, uintptr_t out_idx,
+         uintptr_t out_p, uintptr_t ws, size_t ws_bytes, uintptr_t stream) {
+        launch_gemm_softmax(ptr<void>(X), ptr<void>(W), ptr<float>(b), B, F, K, kind, ptr<int32_t>(out_idx),
+                            ptr<float>(out_p), ptr<void>(ws), ws_bytes, stream_of(stream));
+      },
+      py::arg("X"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"), py::arg("K"), py::arg("kind"),
+      py::arg("out_idx"), py::arg("out_p"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream") = 0);
+  m.def(
+      "gemm_logits",
+      [](uintptr_t X, uintptr_t W, uintptr_t b, int64_t B, int F, int K, uintptr_t Z, uintptr_t stream) {
+        launch_gemm_logits(ptr<void>(X), ptr<void>(W), ptr<float>(b), B, F, K, ptr<float>(Z), stream_of(stream));
+      },
+      py::arg("X"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"), py::arg("K"), py::arg("Z"),
+      py::arg("stream") = 0);
+  m.def("train_binary_workspace", &train_binary_workspace);
+  m.def(
+      "train_binary_grad",
+      [](int dt, uintptr_t X, uintptr_t y, uintptr_t w, uintptr_t b, int64_t B, int F, uintptr_t out, uintptr_t ws,
+         size_t ws_bytes, uintptr_t stream) {
+        launch_train_binary_grad(dt, ptr<void>(X), ptr<float>(y), ptr<float>(w), 0.f, ptr<float>(b), B, F,
+                                 ptr<float>(out), ptr<void>(ws), ws_bytes, stream_of(stream));
+      },
+      py::arg("dt"), py::arg("X"), py::arg("y"), py::arg("w"), py::arg("b"), py::arg("B"), py::arg("F"),
+      py::arg("out"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream") = 0);
+  m.def("train_small_workspace", &train_small_workspace);
+  m.def(
+      "train_small_grad",
+      [](int dt, uintptr_t X, uintptr_t y, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind,
+         uintptr_t out, uintptr_t ws, size_t ws_bytes, uintptr_t stream) {
+        launch_train_small_grad(dt, ptr<void>(X), ptr<int32_t>(y), ptr<void>(W), ptr<void>(b), B, F, K, kind,
+                                ptr<void>(out), ptr<void>(ws), ws_bytes, stream_of(stream));
+      },
+      py::arg("dt"), py::arg("X"), py::arg("y"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"),
+      py::arg("K"), py::arg("kind"), py::arg("out"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream") = 0);
+  m.def(
+      "sgd_update",
+      [](uintptr_t params, uintptr_t grad, uintptr_t mom, int64_t n, int64_t n_pen, float lr, float inv_n, float l2,
+         float momentum, uintptr_t stream) {
+        launch_sgd_update(ptr<float>(params), ptr<float>(grad), ptr<float>(mom), n, n_pen, lr, inv_n, l2, momentum,
+                          stream_of(stream));
+      },
+      py::arg("params"), py::arg("grad"), py::arg("mom"), py::arg("n"), py::arg("n_pen"), py::arg("lr"),
+      py::arg("inv_n"), py::arg("l2"), py::arg("momentum"), py::arg("stream") = 0);
+  m.def(
+      "cast",
+      [](int src_dt, uintptr_t src, int dst_dt, uintptr_t dst, int64_t n, uintptr_t stream) {
+        launch_cast(src_dt, ptr<void>(src), dst_dt, ptr<void>(dst), n, stream_of(stream));
+      },
+      py::arg("src_dt"), py::arg("src"), py::arg("dst_dt"), py::arg("dst"), py::arg("n"), py::arg("stream") = 0);
+
+  // ---------------------------------------------------------------- engine
+  py::class_<EngineConfig>(m, "EngineConfig")
+      .def(py::init<>())
+      .def_readwrite("device", &EngineConfig::device)
+      .def_readwrite("max_batch", &EngineConfig::max_batch)
+      .def_readwrite("max_wait_us", &EngineConfig::max_wait_us)
+      .def_readwrite("slots", &EngineConfig::slots)
+      .def_readwrite("dtype", &EngineConfig::dtype)
+      .def_readwrite("max_features", &EngineConfig::max_features)
+      .def_readwrite("watchdog_ms", &EngineConfig::watchdog_ms)
+      .def_readwrite("fail_every", &EngineConfig::fail_every)
+      .def_readwrite("delay_us", &EngineConfig::delay_us);
+
+  py::class_<PySink>(m, "PySink").def(py::init<>()).def("fd", &PySink::fd).def("drain", &PySink::drain);
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<const EngineConfig&>(), py::call_guard<py::gil_scoped_release>())
+      .def(
+          "load_model",
+          [](Engine& e, int kind, py::array_t<double, py::array::c_style | py::array::forcecast> W,
+             py::array_t<double, py::array::c_style | py::array::forcecast> b, std::vector<std::string> labels) {
+            if (W.ndim() != 2) throw std::invalid_argument("W must be 2-D");
+            const int K = (int)W.shape(0), F = (int)W.shape(1);
+            if (b.size() != K) throw std::invalid_argument("b must have K entries");
+            const double* wp = W.data();
+            const double* bp = b.data();
+            py::gil_scoped_release rel;
+            return e.load_model(kind, F, K, wp, bp, labels);
+          },
+          py::arg("kind"), py::arg("W"), py::arg("b"), py::arg("labels"))
+      .def("unload_model", &Engine::unload_model)
+      .def("model_version",
+           [](Engine& e) -> uint64_t {
+             auto mm = e.model();
+             return mm ? mm->version : 0;
+           })
+      .def("n_features",
+           [](Engine& e) -> int {
+             auto mm = e.model();
+             return mm ? mm->F : 0;
+           })
+      .def(
+          "submit",
+          [](Engine& e, py::array_t<double, py::array::c_style | py::array::forcecast> x, uint64_t tag, PySink& sink) {
+            return e.submit(x.data(), (int)x.size(), tag, &sink);
+          },
+          py::arg("x"), py::arg("tag"), py::arg("sink"))
+      .def(
+          "submit_many",
+          [](Engine& e, py::array_t<double, py::array::c_style | py::array::forcecast> X, uint64_t tag0,
+             PySink& sink) {
+            if (X.ndim() != 2) throw std::invalid_argument("X must be 2-D");
+            const int64_t B = X.shape(0);
+            const int F = (int)X.shape(1);
+            const double* xp = X.data();
+            int64_t ok = 0;
+            for (int64_t r = 0; r < B; ++r) ok += e.submit(xp + r * F, F, tag0 + (uint64_t)r, &sink);
+            return ok;
+          },
+          py::arg("X"), py::arg("tag0"), py::arg("sink"))
+      .def("predict",
+           [](Engine& e, py::array_t<double, py::array::c_style | py::array::forcecast> X) {
+             if (X.ndim() != 2) throw std::invalid_argument("X must be 2-D");
+             const int64_t B = X.shape(0);
+             const int F = (int)X.shape(1);
+             py::array_t<int32_t> idx(B), st(B);
+             py::array_t<double> p(B);
+             const double* xp = X.data();
+             int32_t* ip = idx.mutable_data();
+             double* pp = p.mutable_data();
+             int32_t* sp = st.mutable_data();
+             {
+               py::gil_scoped_release rel;
+               e.predict(xp, B, F, ip, pp, sp);
+             }
+             return py::make_tuple(idx, p, st);
+           })
+      .def("stats", [](Engine& e) { return stats_dict(e.stats()); })
+      .def("healthy", &Engine::healthy)
+      .def("stop", &Engine::stop, py::call_guard<py::gil_scoped_release>());
+
+  // ---------------------------------------------------------------- HTTP server
+  py::class_<ServerConfig>(m, "ServerConfig")
+      .def(py::init<>())
+      .def_readwrite("host", &ServerConfig::host)
+      .def_readwrite("port", &ServerConfig::port)
+      .def_readwrite("io_threads", &ServerConfig::io_threads)
+      .def_readwrite("reuseport", &ServerConfig::reuseport)
+      .def_readwrite("feature_names", &ServerConfig::feature_names)
+      .def_readwrite("predict_path", &ServerConfig::predict_path)
+      .def_readwrite("server_header", &ServerConfig::server_header)
+      .def_readwrite("fast_path", &ServerConfig::fast_path)
+      .def_readwrite("max_body", &ServerConfig::max_body)
+      .def_readwrite("backlog", &ServerConfig::backlog);
+
+  py::class_<HttpServer>(m, "HttpServer")
+      .def(py::init<Engine*, const ServerConfig&>(), py::keep_alive<1, 2>())
+      .def("start", &HttpServer::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &HttpServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def("port", &HttpServer::port)
+      .def(
+          "next_slow",
+          [](HttpServer& s, int timeout_ms) -> py::object {
+            SlowRequest r;
+            bool got;
+            {
+              py::gil_scoped_release rel;
+              got = s.next_slow(&r, timeout_ms);
+            }
+            if (!got) return py::none();
+            py::list headers;
+            for (auto& h : r.headers) headers.append(py::make_tuple(py::bytes(h.first), py::bytes(h.second)));
+            py::dict d;
+            d["token"] = r.token;
+            d["method"] = r.method;
+            d["target"] = py::bytes(r.target);
+            d["http_version"] = r.http_version;
+            d["headers"] = headers;
+            d["body"] = py::bytes(r.body);
+            d["client"] = py::make_tuple(r.client_host, r.client_port);
+            d["server"] = py::make_tuple(r.server_host, r.server_port);
+            return d;
+          },
+          py::arg("timeout_ms") = 100)
+      .def(
+          "respond",
+          [](HttpServer& s, uint64_t token, int status, const std::string& reason, py::list headers, py::bytes body,
+             bool close) {
+            std::vector<std::pair<std::string, std::string>> hs;
+            for (auto h : headers) {
+              auto t = h.cast<py::tuple>();
+              hs.emplace_back(t[0].cast<std::string>(), t[1].cast<std::string>());
+            }
+            std::string b = body;
+            py::gil_scoped_release rel;
+            s.respond(token, status, reason, hs, b, close);
+          },
+          py::arg("token"), py::arg("status"), py::arg("reason"), py::arg("headers"), py::arg("body"),
+          py::arg("close") = false)
+      .def("stats", [](HttpServer& s) {
+        const ServerStats st = s.stats();
+        py::dict d;
+        d["fast"] = st.fast;
+        d["slow"] = st.slow;
+        d["responses"] = st.responses;
+        d["connections"] = st.connections;
+        d["errors"] = st.errors;
+        d["bad_requests"] = st.bad_requests;
+        return d;
+      });
+
+  // ---------------------------------------------------------------- load generator
+  py::class_<Loadgen>(m, "Loadgen")
+      .def(py::init<const std::string&, int, const std::string&, int, int, double>(), py::arg("host"), py::arg("port"),
+           py::arg("request"), py::arg("conns"), py::arg("threads"), py::arg("timeout_s") = 30.0)
+      .def(
+          "run",
+          [](Loadgen& lg, int64_t n, bool record) {
+            LoadgenResult r;
+            {
+              py::gil_scoped_release rel;
+              r = lg.run(n, record);
+            }
+            py::dict d;
+            d["elapsed_s"] = r.elapsed_s;
+            d["completed"] = r.completed;
+            d["errors"] = r.errors;
+            d["failed"] = r.failed;
+            py::array_t<int64_t> lat((py::ssize_t)r.latencies_ns.size());
+            if (!r.latencies_ns.empty())
+              std::memcpy(lat.mutable_data(), r.latencies_ns.data(), r.latencies_ns.size() * sizeof(int64_t));
+            d["latencies_ns"] = lat;
+            py::dict sc;
+            for (int s = 0; s < 600; ++s)
+              if (r.status_counts[s]) sc[py::int_(s)] = r.status_counts[s];
+            d["status_counts"] = sc;
+            return d;
+          },
+          py::arg("requests_per_conn"), py::arg("record") = true)
+      .def("close", &Loadgen::close_all);
+}

@@ -1,0 +1,897 @@
+// Native HTTP/1.1 server (see server.h).
+#include "server.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <stdexcept>
+#include <unordered_map>
+
+#include "../runtime/float_repr.h"
+
+namespace mlapi {
+
+// ------------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------------
+std::string http_date_now() {
+  thread_local time_t cached_t = 0;
+  thread_local std::string cached;
+  const time_t t = time(nullptr);
+  if (t != cached_t) {
+    struct tm g;
+    gmtime_r(&t, &g);
+    char buf[64];
+    strftime(buf, sizeof buf, "%a, %d %b %Y %H:%M:%S GMT", &g);
+    cached = buf;
+    cached_t = t;
+  }
+  return cached;
+}
+
+static inline bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+static inline void lower_inplace(std::string& s) {
+  for (char& c : s)
+    if (c >= 'A' && c <= 'Z') c = (char)(c - 'A' + 'a');
+}
+
+static inline std::string trim(const std::string& s) {
+  size_t a = 0, b = s.size();
+  while (a < b && (s[a] == ' ' || s[a] == '\t')) ++a;
+  while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t')) --b;
+  return s.substr(a, b - a);
+}
+
+namespace {
+
+// Skip one JSON value starting at p[i]; returns false on malformed input.
+bool skip_value(const char* p, size_t n, size_t& i, int depth) {
+  if (depth > 64) return false;
+  while (i < n && is_ws(p[i])) ++i;
+  if (i >= n) return false;
+  const char c = p[i];
+  if (c == '"') {
+    ++i;
+    while (i < n) {
+      const unsigned char ch = (unsigned char)p[i];
+      if (ch == '\\') {
+        i += 2;
+        continue;
+      }
+      if (ch < 0x20) return false;
+      if (ch == '"') {
+        ++i;
+        return true;
+      }
+      ++i;
+    }
+    return false;
+  }
+  if (c == '{' || c == '[') {
+    const char close = c == '{' ? '}' : ']';
+    ++i;
+    while (i < n && is_ws(p[i])) ++i;
+    if (i < n && p[i] == close) {
+      ++i;
+      return true;
+    }
+    for (;;) {
+      if (c == '{') {
+        while (i < n && is_ws(p[i])) ++i;
+        if (i >= n || p[i] != '"') return false;
+        if (!skip_value(p, n, i, depth + 1)) return false;
+        while (i < n && is_ws(p[i])) ++i;
+        if (i >= n || p[i] != ':') return false;
+        ++i;
+      }
+      if (!skip_value(p, n, i, depth + 1)) return false;
+      while (i < n && is_ws(p[i])) ++i;
+      if (i >= n) return false;
+      if (p[i] == ',') {
+        ++i;
+        continue;
+      }
+      if (p[i] == close) {
+        ++i;
+        return true;
+      }
+      return false;
+    }
+  }
+  // literals / numbers: consume a token of allowed characters; strictness only matters for the
+  // required keys (parsed separately), an odd extra value just needs to be skippable.
+  if (c == 't' && n - i >= 4 && memcmp(p + i, "true", 4) == 0) { i += 4; return true; }
+  if (c == 'f' && n - i >= 5 && memcmp(p + i, "false", 5) == 0) { i += 5; return true; }
+  if (c == 'n' && n - i >= 4 && memcmp(p + i, "null", 4) == 0) { i += 4; return true; }
+  if (c == '-' || (c >= '0' && c <= '9')) {
+    ++i;
+    while (i < n && ((p[i] >= '0' && p[i] <= '9') || p[i] == '.' || p[i] == 'e' || p[i] == 'E' || p[i] == '+' ||
+                     p[i] == '-'))
+      ++i;
+    return true;
+  }
+  return false;  // NaN / Infinity / garbage -> slow path
+}
+
+// Strict JSON number (RFC 8259 grammar) -> finite double.
+bool parse_number(const char* p, size_t n, size_t& i, double* out) {
+  const size_t s = i;
+  if (i < n && p[i] == '-') ++i;
+  if (i >= n) return false;
+  if (p[i] == '0') {
+    ++i;
+  } else if (p[i] >= '1' && p[i] <= '9') {
+    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
+  } else {
+    return false;
+  }
+  if (i < n && p[i] == '.') {
+    ++i;
+    if (i >= n || !(p[i] >= '0' && p[i] <= '9')) return false;
+    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
+  }
+  if (i < n && (p[i] == 'e' || p[i] == 'E')) {
+    ++i;
+    if (i < n && (p[i] == '+' || p[i] == '-')) ++i;
+    if (i >= n || !(p[i] >= '0' && p[i] <= '9')) return false;
+    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
+  }
+  const size_t len = i - s;
+  if (len > 400) return false;  // absurd literals: let Python decide
+  char buf[416];
+  memcpy(buf, p + s, len);
+  buf[len] = '\0';
+  char* end = nullptr;
+  const double v = strtod(buf, &end);
+  if (end != buf + len || !std::isfinite(v)) return false;
+  *out = v;
+  return true;
+}
+
+}  // namespace
+
+bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>& names, double* out) {
+  const size_t nk = names.size();
+  if (nk > 4096) return false;
+  std::vector<char> seen(nk, 0);
+  size_t i = 0;
+  while (i < n && is_ws(p[i])) ++i;
+  if (i >= n || p[i] != '{') return false;
+  ++i;
+  while (i < n && is_ws(p[i])) ++i;
+  if (i < n && p[i] == '}') {
+    ++i;
+  } else {
+    for (;;) {
+      while (i < n && is_ws(p[i])) ++i;
+      if (i >= n || p[i] != '"') return false;
+      ++i;
+      const size_t ks = i;
+      while (i < n && p[i] != '"') {
+        if (p[i] == '\\' || (unsigned char)p[i] < 0x20) return false;  // escaped keys -> slow path
+        ++i;
+      }
+      if (i >= n) return false;
+      const size_t klen = i - ks;
+      ++i;
+      while (i < n && is_ws(p[i])) ++i;
+      if (i >= n || p[i] != ':') return false;
+      ++i;
+      while (i < n && is_ws(p[i])) ++i;
+      int which = -1;
+      for (size_t k = 0; k < nk; ++k) {
+        if (names[k].size() == klen && memcmp(names[k].data(), p + ks, klen) == 0) {
+          which = (int)k;
+          break;
+        }
+      }
+      if (which >= 0) {
+        double v;
+        if (!parse_number(p, n, i, &v)) return false;
+        out[which] = v;
+        seen[which] = 1;
+      } else {
+        if (!skip_value(p, n, i, 0)) return false;
+      }
+      while (i < n && is_ws(p[i])) ++i;
+      if (i >= n) return false;
+      if (p[i] == ',') {
+        ++i;
+        continue;
+      }
+      if (p[i] == '}') {
+        ++i;
+        break;
+      }
+      return false;
+    }
+  }
+  while (i < n && is_ws(p[i])) ++i;
+  if (i != n) return false;
+  for (size_t k = 0; k < nk; ++k)
+    if (!seen[k]) return false;
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------------
+// IO thread
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+constexpr uint64_t ID_LISTEN = 0;
+constexpr uint64_t ID_EVENT = 1;
+
+struct Conn {
+  int fd = -1;
+  uint64_t id = 0;
+  std::string in;
+  size_t in_pos = 0;
+  std::string out;
+  size_t out_pos = 0;
+  bool waiting = false;       // a request is outstanding (engine or Python)
+  bool close_after = false;   // close once `out` is flushed
+  bool sent_continue = false;
+  bool epollout = false;
+  std::string client_host, server_host;
+  int client_port = 0, server_port = 0;
+};
+
+struct FastBatch {
+  std::shared_ptr<const Model> model;
+  std::vector<Completion> c;
+};
+
+struct SlowResp {
+  uint64_t conn_id;
+  std::string bytes;
+  bool close;
+};
+
+void addr_to_str(const sockaddr_storage& ss, std::string& host, int& port) {
+  char buf[INET6_ADDRSTRLEN] = {0};
+  if (ss.ss_family == AF_INET) {
+    const auto* a = reinterpret_cast<const sockaddr_in*>(&ss);
+    inet_ntop(AF_INET, &a->sin_addr, buf, sizeof buf);
+    port = ntohs(a->sin_port);
+  } else {
+    const auto* a = reinterpret_cast<const sockaddr_in6*>(&ss);
+    inet_ntop(AF_INET6, &a->sin6_addr, buf, sizeof buf);
+    port = ntohs(a->sin6_port);
+  }
+  host = buf;
+}
+
+int make_listener(const std::string& host, int port, bool reuseport, int backlog, int* bound_port) {
+  addrinfo hints{};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  hints.ai_flags = AI_PASSIVE | AI_NUMERICSERV;
+  addrinfo* res = nullptr;
+  const std::string ps = std::to_string(port);
+  if (getaddrinfo(host.empty() ? nullptr : host.c_str(), ps.c_str(), &hints, &res) != 0 || !res)
+    throw std::runtime_error("getaddrinfo failed for " + host);
+  int fd = socket(res->ai_family, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, IPPROTO_TCP);
+  if (fd < 0) {
+    freeaddrinfo(res);
+    throw std::runtime_error("socket() failed");
+  }
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  if (reuseport) setsockopt(fd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
+  if (bind(fd, res->ai_addr, res->ai_addrlen) != 0) {
+    const int e = errno;
+    freeaddrinfo(res);
+    close(fd);
+    throw std::runtime_error("bind(" + host + ":" + ps + ") failed: " + strerror(e));
+  }
+  freeaddrinfo(res);
+  if (listen(fd, backlog) != 0) {
+    close(fd);
+    throw std::runtime_error("listen() failed");
+  }
+  sockaddr_storage ss{};
+  socklen_t sl = sizeof ss;
+  getsockname(fd, reinterpret_cast<sockaddr*>(&ss), &sl);
+  std::string h;
+  addr_to_str(ss, h, *bound_port);
+  return fd;
+}
+
+}  // namespace
+
+class IoThread : public Sink {
+ public:
+  IoThread(HttpServer* srv, int index, int listen_fd) : srv_(srv), index_(index), lfd_(listen_fd) {
+    epfd_ = epoll_create1(EPOLL_CLOEXEC);
+    evfd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (epfd_ < 0 || evfd_ < 0) throw std::runtime_error("epoll/eventfd creation failed");
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = ID_LISTEN;
+    epoll_ctl(epfd_, EPOLL_CTL_ADD, lfd_, &ev);
+    ev.data.u64 = ID_EVENT;
+    epoll_ctl(epfd_, EPOLL_CTL_ADD, evfd_, &ev);
+    const auto& cfg = srv_->config();
+    nfeat_ = cfg.feature_names.size();
+  }
+  ~IoThread() override {
+    for (auto& kv : conns_) close(kv.second->fd);
+    if (lfd_ >= 0) close(lfd_);
+    close(evfd_);
+    close(epfd_);
+  }
+
+  void start() { th_ = std::thread([this] { loop(); }); }
+  void stop() {
+    stop_.store(true);
+    wake();
+    if (th_.joinable()) th_.join();
+  }
+
+  // Sink: engine completer thread -> this IO thread.
+  void on_complete(const Completion* c, size_t n, const std::shared_ptr<const Model>& model) override {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fast_.push_back(FastBatch{model, std::vector<Completion>(c, c + n)});
+    }
+    wake();
+  }
+
+  void post_slow(uint64_t conn_id, std::string&& bytes, bool close) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      slow_.push_back(SlowResp{conn_id, std::move(bytes), close});
+    }
+    wake();
+  }
+
+  std::atomic<uint64_t> n_fast{0}, n_slow{0}, n_resp{0}, n_conn{0}, n_err{0}, n_bad{0};
+
+ private:
+  void wake() {
+    if (!signaled_.exchange(true)) {
+      const uint64_t one = 1;
+      ssize_t r = write(evfd_, &one, sizeof one);
+      (void)r;
+    }
+  }
+
+  void loop() {
+    epoll_event evs[256];
+    while (!stop_.load()) {
+      const int n = epoll_wait(epfd_, evs, 256, 200);
+      for (int i = 0; i < n; ++i) {
+        const uint64_t id = evs[i].data.u64;
+        if (id == ID_LISTEN) {
+          accept_all();
+        } else if (id == ID_EVENT) {
+          uint64_t v;
+          ssize_t r = read(evfd_, &v, sizeof v);
+          (void)r;
+          signaled_.store(false);
+          drain_pending();
+        } else {
+          auto it = conns_.find(id);
+          if (it == conns_.end()) continue;
+          Conn* c = it->second.get();
+          bool alive = true;
+          if (evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR | EPOLLRDHUP)) alive = on_readable(c);
+          if (alive && (evs[i].events & EPOLLOUT)) alive = flush(c);
+        }
+      }
+    }
+  }
+
+  void accept_all() {
+    for (;;) {
+      sockaddr_storage ss{};
+      socklen_t sl = sizeof ss;
+      const int fd = accept4(lfd_, reinterpret_cast<sockaddr*>(&ss), &sl, SOCK_NONBLOCK | SOCK_CLOEXEC);
+      if (fd < 0) return;
+      int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);  // never Nagle
+      auto c = std::make_unique<Conn>();
+      c->fd = fd;
+      c->id = next_id_++;
+      addr_to_str(ss, c->client_host, c->client_port);
+      sockaddr_storage ls{};
+      socklen_t ll = sizeof ls;
+      getsockname(fd, reinterpret_cast<sockaddr*>(&ls), &ll);
+      addr_to_str(ls, c->server_host, c->server_port);
+      epoll_event ev{};
+      ev.events = EPOLLIN | EPOLLRDHUP;
+      ev.data.u64 = c->id;
+      epoll_ctl(epfd_, EPOLL_CTL_ADD, fd, &ev);
+      conns_.emplace(c->id, std::move(c));
+      n_conn.fetch_add(1, std::memory_order_relaxed);
+    }
+  }
+
+  void close_conn(Conn* c) {
+    epoll_ctl(epfd_, EPOLL_CTL_DEL, c->fd, nullptr);
+    close(c->fd);
+    conns_.erase(c->id);  // destroys c
+  }
+
+  // returns false if the connection was closed
+  bool on_readable(Conn* c) {
+    char buf[65536];
+    bool eof = false;
+    for (;;) {
+      const ssize_t r = recv(c->fd, buf, sizeof buf, 0);
+      if (r > 0) {
+        c->in.append(buf, (size_t)r);
+        if ((size_t)r < sizeof buf) break;
+      } else if (r == 0) {
+        eof = true;
+        break;
+      } else {
+        if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+        if (errno == EINTR) continue;
+        eof = true;
+        break;
+      }
+    }
+    if (eof) {
+      close_conn(c);
+      return false;
+    }
+    return process(c);
+  }
+
+  bool flush(Conn* c) {
+    while (c->out_pos < c->out.size()) {
+      const ssize_t w = send(c->fd, c->out.data() + c->out_pos, c->out.size() - c->out_pos, MSG_NOSIGNAL);
+      if (w > 0) {
+        c->out_pos += (size_t)w;
+      } else if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        if (!c->epollout) {
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLRDHUP | EPOLLOUT;
+          ev.data.u64 = c->id;
+          epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev);
+          c->epollout = true;
+        }
+        return true;
+      } else if (w < 0 && errno == EINTR) {
+        continue;
+      } else {
+        close_conn(c);
+        return false;
+      }
+    }
+    c->out.clear();
+    c->out_pos = 0;
+    if (c->epollout) {
+      epoll_event ev{};
+      ev.events = EPOLLIN | EPOLLRDHUP;
+      ev.data.u64 = c->id;
+      epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev);
+      c->epollout = false;
+    }
+    if (c->close_after && !c->waiting) {
+      close_conn(c);
+      return false;
+    }
+    return true;
+  }
+
+  void append_response(Conn* c, int status, const char* reason, const char* ctype, const std::string& body) {
+    std::string& o = c->out;
+    o.reserve(o.size() + 160 + body.size());
+    o += "HTTP/1.1 ";
+    o += std::to_string(status);
+    o += ' ';
+    o += reason;
+    o += "\r\ndate: ";
+    o += http_date_now();
+    o += "\r\nserver: ";
+    o += srv_->config().server_header;
+    o += "\r\ncontent-length: ";
+    o += std::to_string(body.size());
+    o += "\r\ncontent-type: ";
+    o += ctype;
+    if (c->close_after) o += "\r\nconnection: close";
+    o += "\r\n\r\n";
+    o += body;
+    n_resp.fetch_add(1, std::memory_order_relaxed);
+  }
+
+  void internal_error(Conn* c) {
+    append_response(c, 500, "Internal Server Error", "text/plain; charset=utf-8", "Internal Server Error");
+    n_err.fetch_add(1, std::memory_order_relaxed);
+  }
+
+  void bad_request(Conn* c, int status, const char* reason) {
+    c->close_after = true;
+    append_response(c, status, reason, "text/plain; charset=utf-8", reason);
+    n_bad.fetch_add(1, std::memory_order_relaxed);
+  }
+
+  void drain_pending() {
+    std::vector<FastBatch> fast;
+    std::vector<SlowResp> slow;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fast.swap(fast_);
+      slow.swap(slow_);
+    }
+    std::string body;
+    for (FastBatch& fb : fast) {
+      for (const Completion& cp : fb.c) {
+        auto it = conns_.find(cp.tag);
+        if (it == conns_.end()) continue;  // client went away
+        Conn* c = it->second.get();
+        c->waiting = false;
+        bool ok = cp.status == ST_OK && fb.model && cp.idx >= 0 && (size_t)cp.idx < fb.model->label_json.size();
+        if (ok) {
+          body.clear();
+          body += "{\"prediction\":";
+          body += fb.model->label_json[cp.idx];
+          body += ",\"probability\":";
+          ok = append_py_float(body, cp.p);
+          body += '}';
+        }
+        if (ok)
+          append_response(c, 200, "OK", "application/json", body);
+        else
+          internal_error(c);
+        process(c);  // dispatches pipelined requests, then flushes (may close c)
+      }
+    }
+    for (SlowResp& sr : slow) {
+      auto it = conns_.find(sr.conn_id);
+      if (it == conns_.end()) continue;
+      Conn* c = it->second.get();
+      c->waiting = false;
+      c->out += sr.bytes;
+      if (sr.close) c->close_after = true;
+      n_resp.fetch_add(1, std::memory_order_relaxed);
+      process(c);  // dispatches pipelined requests, then flushes (may close c)
+    }
+  }
+
+  // Parse and dispatch as many complete requests as possible (one outstanding at a time).
+  // Returns false if the connection was closed.
+  bool process(Conn* c) {
+    while (!c->waiting && !c->close_after) {
+      const int r = parse_one(c);
+      if (r == 0) break;  // need more bytes
+      if (r < 0) break;   // error response queued, close_after set
+    }
+    if (c->in_pos > 0 && (c->in_pos == c->in.size() || c->in_pos > (1u << 16))) {
+      c->in.erase(0, c->in_pos);
+      c->in_pos = 0;
+    }
+    return flush(c);
+  }
+
+  // 1 = dispatched a request, 0 = incomplete, -1 = protocol error (response queued)
+  int parse_one(Conn* c) {
+    const auto& cfg = srv_->config();
+    const char* base = c->in.data() + c->in_pos;
+    const size_t avail = c->in.size() - c->in_pos;
+    if (avail == 0) return 0;
+    // tolerate stray CRLFs between requests (RFC 7230 3.5)
+    size_t lead = 0;
+    while (lead < avail && (base[lead] == '\r' || base[lead] == '\n')) ++lead;
+    if (lead) {
+      c->in_pos += lead;
+      return avail > lead ? 1 : 0;
+    }
+    const void* hend_p = memmem(base, avail, "\r\n\r\n", 4);
+    if (!hend_p) {
+      if (avail > cfg.max_header) {
+        bad_request(c, 431, "Request Header Fields Too Large");
+        return -1;
+      }
+      return 0;
+    }
+    const size_t hlen = (size_t)(static_cast<const char*>(hend_p) - base) + 4;
+    // request line
+    const char* le = static_cast<const char*>(memmem(base, hlen, "\r\n", 2));
+    std::string line(base, (size_t)(le - base));
+    const size_t s1 = line.find(' ');
+    const size_t s2 = s1 == std::string::npos ? std::string::npos : line.find(' ', s1 + 1);
+    if (s1 == std::string::npos || s2 == std::string::npos) {
+      bad_request(c, 400, "Bad Request");
+      return -1;
+    }
+    std::string method = line.substr(0, s1), target = line.substr(s1 + 1, s2 - s1 - 1),
+                version = line.substr(s2 + 1);
+    if (version != "HTTP/1.1" && version != "HTTP/1.0") {
+      bad_request(c, 400, "Bad Request");
+      return -1;
+    }
+    // headers
+    std::vector<std::pair<std::string, std::string>> headers;
+    int64_t clen = -1;
+    bool chunked = false, expect100 = false;
+    std::string conn_hdr, ctype;
+    const char* hp = le + 2;
+    const char* hlim = base + hlen - 2;
+    while (hp < hlim) {
+      const char* e = static_cast<const char*>(memmem(hp, (size_t)(hlim - hp) + 2, "\r\n", 2));
+      if (!e) break;
+      const char* colon = static_cast<const char*>(memchr(hp, ':', (size_t)(e - hp)));
+      if (!colon) {
+        bad_request(c, 400, "Bad Request");
+        return -1;
+      }
+      std::string name(hp, (size_t)(colon - hp)), value(colon + 1, (size_t)(e - colon - 1));
+      lower_inplace(name);
+      value = trim(value);
+      if (name == "content-length") {
+        char* endp = nullptr;
+        const long long v = strtoll(value.c_str(), &endp, 10);
+        if (value.empty() || *endp != '\0' || v < 0 || (clen >= 0 && clen != v)) {
+          bad_request(c, 400, "Bad Request");
+          return -1;
+        }
+        clen = v;
+      } else if (name == "transfer-encoding") {
+        std::string v = value;
+        lower_inplace(v);
+        if (v.find("chunked") != std::string::npos) chunked = true;
+      } else if (name == "connection") {
+        conn_hdr = value;
+        lower_inplace(conn_hdr);
+      } else if (name == "content-type") {
+        ctype = value;
+      } else if (name == "expect") {
+        std::string v = value;
+        lower_inplace(v);
+        expect100 = v == "100-continue";
+      }
+      headers.emplace_back(std::move(name), std::move(value));
+      hp = e + 2;
+    }
+    // body
+    std::string body;
+    size_t consumed = hlen;
+    if (chunked) {
+      size_t pos = hlen;
+      for (;;) {
+        const void* ce = memmem(base + pos, avail - pos, "\r\n", 2);
+        if (!ce) {
+          if (expect100 && !c->sent_continue) send_continue(c);
+          return 0;
+        }
+        const std::string szs(base + pos, (size_t)(static_cast<const char*>(ce) - (base + pos)));
+        char* endp = nullptr;
+        const unsigned long long sz = strtoull(szs.c_str(), &endp, 16);
+        if (endp == szs.c_str()) {
+          bad_request(c, 400, "Bad Request");
+          return -1;
+        }
+        pos = (size_t)(static_cast<const char*>(ce) - base) + 2;
+        if (sz == 0) {
+          // trailers until empty line
+          const void* te = memmem(base + pos, avail - pos, "\r\n", 2);
+          if (!te) return 0;
+          while (static_cast<const char*>(te) != base + pos) {
+            pos = (size_t)(static_cast<const char*>(te) - base) + 2;
+            te = memmem(base + pos, avail - pos, "\r\n", 2);
+            if (!te) return 0;
+          }
+          pos += 2;
+          break;
+        }
+        if (body.size() + sz > cfg.max_body) {
+          bad_request(c, 413, "Payload Too Large");
+          return -1;
+        }
+        if (avail - pos < sz + 2) {
+          if (expect100 && !c->sent_continue) send_continue(c);
+          return 0;
+        }
+        body.append(base + pos, sz);
+        pos += sz + 2;
+      }
+      consumed = pos;
+    } else if (clen > 0) {
+      if ((size_t)clen > cfg.max_body) {
+        bad_request(c, 413, "Payload Too Large");
+        return -1;
+      }
+      if (avail - hlen < (size_t)clen) {
+        if (expect100 && !c->sent_continue) send_continue(c);
+        return 0;
+      }
+      body.assign(base + hlen, (size_t)clen);
+      consumed = hlen + (size_t)clen;
+    }
+    c->in_pos += consumed;
+    c->sent_continue = false;
+    const bool keep_alive = version == "HTTP/1.1" ? conn_hdr.find("close") == std::string::npos
+                                                  : conn_hdr.find("keep-alive") != std::string::npos;
+    if (!keep_alive) c->close_after = true;
+
+    // ---- fast path
+    if (cfg.fast_path && method == "POST") {
+      const size_t q = target.find('?');
+      const std::string path = q == std::string::npos ? target : target.substr(0, q);
+      if (path == cfg.predict_path && json_ctype(ctype) && nfeat_ > 0) {
+        double x[256];
+        if (nfeat_ <= 256 && parse_predict_body(body.data(), body.size(), cfg.feature_names, x)) {
+          Engine* eng = srv_->engine();
+          c->waiting = true;
+          if (!eng->submit(x, (int)nfeat_, c->id, this)) {
+            c->waiting = false;
+            internal_error(c);
+          }
+          n_fast.fetch_add(1, std::memory_order_relaxed);
+          return 1;
+        }
+      }
+    }
+    // ---- slow path: hand to the Python ASGI app
+    SlowRequest sr;
+    sr.token = ((uint64_t)index_ << 56) | c->id;
+    sr.method = std::move(method);
+    sr.target = std::move(target);
+    sr.http_version = version.substr(5);
+    sr.headers = std::move(headers);
+    sr.body = std::move(body);
+    sr.client_host = c->client_host;
+    sr.client_port = c->client_port;
+    sr.server_host = c->server_host;
+    sr.server_port = c->server_port;
+    c->waiting = true;
+    n_slow.fetch_add(1, std::memory_order_relaxed);
+    srv_->push_slow(std::move(sr));
+    return 1;
+  }
+
+  static bool json_ctype(const std::string& ct) {
+    // FastAPI: maintype 'application' and subtype 'json' or '*+json' (routing.py), params ignored.
+    std::string v = ct.substr(0, ct.find(';'));
+    v = trim(v);
+    lower_inplace(v);
+    if (v.compare(0, 12, "application/") != 0) return false;
+    const std::string sub = v.substr(12);
+    return sub == "json" || (sub.size() > 5 && sub.compare(sub.size() - 5, 5, "+json") == 0);
+  }
+
+  void send_continue(Conn* c) {
+    c->sent_continue = true;
+    static const char kCont[] = "HTTP/1.1 100 Continue\r\n\r\n";
+    ssize_t w = send(c->fd, kCont, sizeof(kCont) - 1, MSG_NOSIGNAL);
+    (void)w;
+  }
+
+  HttpServer* srv_;
+  int index_;
+  int lfd_;
+  int epfd_ = -1, evfd_ = -1;
+  size_t nfeat_ = 0;
+  std::thread th_;
+  std::atomic<bool> stop_{false};
+  std::atomic<bool> signaled_{false};
+  std::mutex mu_;
+  std::vector<FastBatch> fast_;
+  std::vector<SlowResp> slow_;
+  std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns_;
+  uint64_t next_id_ = 16;
+};
+
+// ------------------------------------------------------------------------------------------------
+HttpServer::HttpServer(Engine* engine, const ServerConfig& cfg) : engine_(engine), cfg_(cfg) {
+  if (cfg_.io_threads < 1) cfg_.io_threads = 1;
+  if (cfg_.io_threads > 64) cfg_.io_threads = 64;
+}
+
+HttpServer::~HttpServer() { stop(); }
+
+void HttpServer::start() {
+  if (started_) return;
+  int port = cfg_.port;
+  std::vector<int> fds;
+  try {
+    for (int i = 0; i < cfg_.io_threads; ++i) {
+      int bp = 0;
+      fds.push_back(make_listener(cfg_.host, port, cfg_.reuseport || cfg_.io_threads > 1, cfg_.backlog, &bp));
+      if (i == 0) {
+        bound_port_ = bp;
+        port = bp;
+      }
+    }
+  } catch (...) {
+    for (int fd : fds) close(fd);
+    throw;
+  }
+  for (int i = 0; i < cfg_.io_threads; ++i) threads_.push_back(std::make_unique<IoThread>(this, i, fds[i]));
+  for (auto& t : threads_) t->start();
+  started_ = true;
+}
+
+void HttpServer::stop() {
+  {
+    std::lock_guard<std::mutex> lk(slow_mu_);
+    if (stopping_) return;
+    stopping_ = true;
+  }
+  slow_cv_.notify_all();
+  for (auto& t : threads_) t->stop();
+  threads_.clear();
+}
+
+void HttpServer::push_slow(SlowRequest&& r) {
+  {
+    std::lock_guard<std::mutex> lk(slow_mu_);
+    slow_q_.push_back(std::move(r));
+  }
+  slow_cv_.notify_one();
+}
+
+bool HttpServer::next_slow(SlowRequest* out, int timeout_ms) {
+  std::unique_lock<std::mutex> lk(slow_mu_);
+  if (!slow_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return stopping_ || !slow_q_.empty(); }))
+    return false;
+  if (slow_q_.empty()) return false;
+  *out = std::move(slow_q_.front());
+  slow_q_.pop_front();
+  return true;
+}
+
+void HttpServer::respond(uint64_t token, int status, const std::string& reason,
+                         const std::vector<std::pair<std::string, std::string>>& headers, const std::string& body,
+                         bool close) {
+  const int ti = (int)(token >> 56);
+  const uint64_t cid = token & ((uint64_t(1) << 56) - 1);
+  if (ti < 0 || ti >= (int)threads_.size()) return;
+  std::string o;
+  o.reserve(256 + body.size());
+  o += "HTTP/1.1 ";
+  o += std::to_string(status);
+  o += ' ';
+  o += reason;
+  o += "\r\ndate: ";
+  o += http_date_now();
+  o += "\r\nserver: ";
+  o += cfg_.server_header;
+  bool has_len = false;
+  for (const auto& h : headers) {
+    if (h.first == "content-length") has_len = true;
+    o += "\r\n";
+    o += h.first;
+    o += ": ";
+    o += h.second;
+  }
+  if (!has_len) {
+    o += "\r\ncontent-length: ";
+    o += std::to_string(body.size());
+  }
+  if (close) o += "\r\nconnection: close";
+  o += "\r\n\r\n";
+  o += body;
+  threads_[ti]->post_slow(cid, std::move(o), close);
+}
+
+ServerStats HttpServer::stats() const {
+  ServerStats s;
+  for (const auto& t : threads_) {
+    s.fast += t->n_fast.load();
+    s.slow += t->n_slow.load();
+    s.responses += t->n_resp.load();
+    s.connections += t->n_conn.load();
+    s.errors += t->n_err.load();
+    s.bad_requests += t->n_bad.load();
+  }
+  return s;
+}
+
+}  // namespace mlapi

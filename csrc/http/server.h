@@ -1,0 +1,99 @@
+// Native HTTP/1.1 front end for the serving engine.
+//
+// The reference spends ~80% of every request in uvicorn/h11 + FastAPI + pydantic,
+// and its multi-worker mode stalls 44 ms per response on Nagle/delayed-ACK. This
+// server keeps the reference's HTTP surface but moves the hot path native:
+//
+//  * N IO threads, each with its own SO_REUSEPORT listener + epoll loop (the kernel spreads
+//    connections; DP ranks can share one port the same way), TCP_NODELAY on every socket, every
+//    response emitted with a single send();
+//  * fast path: `POST /predict`, JSON content type, body that is a plain JSON object whose
+//    required keys are finite JSON numbers (extra keys ignored) -> parsed straight into the
+//    engine queue; the response {"prediction":...,"probability":repr(p)} is rendered natively,
+//    byte-identical to FastAPI's JSONResponse;
+//  * everything else (validation errors, /files/, /docs, /openapi.json, 404/405, anything a
+//    strict parser would have to guess about) is handed to the Python ASGI app through
+//    next_slow()/respond(), so error bodies stay exactly FastAPI's.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+
+#include "../runtime/engine.h"
+
+namespace mlapi {
+
+struct ServerConfig {
+  std::string host = "127.0.0.1";
+  int port = 8000;
+  int io_threads = 2;
+  bool reuseport = true;
+  std::vector<std::string> feature_names;  // JSON keys of the /predict body, in W's column order
+  std::string predict_path = "/predict";
+  std::string server_header = "uvicorn";
+  bool fast_path = true;
+  size_t max_body = 64u << 20;
+  size_t max_header = 64u << 10;
+  int backlog = 4096;
+};
+
+struct SlowRequest {
+  uint64_t token = 0;
+  std::string method, target, http_version;
+  std::vector<std::pair<std::string, std::string>> headers;  // names lower-cased
+  std::string body;
+  std::string client_host, server_host;
+  int client_port = 0, server_port = 0;
+};
+
+struct ServerStats {
+  uint64_t fast = 0, slow = 0, responses = 0, connections = 0, errors = 0, bad_requests = 0;
+};
+
+class IoThread;
+
+class HttpServer {
+ public:
+  HttpServer(Engine* engine, const ServerConfig& cfg);
+  ~HttpServer();
+  void start();
+  void stop();
+  int port() const { return bound_port_; }
+  bool next_slow(SlowRequest* out, int timeout_ms);
+  void respond(uint64_t token, int status, const std::string& reason,
+               const std::vector<std::pair<std::string, std::string>>& headers, const std::string& body,
+               bool close);
+  ServerStats stats() const;
+  const ServerConfig& config() const { return cfg_; }
+  Engine* engine() const { return engine_; }
+
+  // internal, used by IoThread
+  void push_slow(SlowRequest&& r);
+
+ private:
+  Engine* engine_;
+  ServerConfig cfg_;
+  int bound_port_ = 0;
+  std::vector<std::unique_ptr<IoThread>> threads_;
+  std::mutex slow_mu_;
+  std::condition_variable slow_cv_;
+  std::deque<SlowRequest> slow_q_;
+  bool stopping_ = false;
+  bool started_ = false;
+};
+
+// Strict parser for the fast path. Returns true only for a JSON object in which every name in
+// `names` appears with a finite JSON-number value (last duplicate wins, like json.loads); extra
+// keys may hold any JSON value. Anything else returns false (-> slow path decides).
+bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>& names, double* out);
+
+// HTTP date (RFC 7231 IMF-fixdate), cached per second.
+std::string http_date_now();
+
+}  // namespace mlapi

@@ -1,0 +1,54 @@
+// Host-side launchers for the HIP kernels in csrc/kernels/*.hip.
+// Every pointer is a device-accessible address (device memory, or host-pinned mapped memory for
+// the zero-copy serving path). All launchers are asynchronous on `stream` and capture-safe
+// (no allocation, no synchronization) so they can be recorded into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace mlapi {
+
+// ---- linear_small.hip: fused  z = x W^T + b  -> (argmax label, p_max)  for small F, K ----------
+// X: [B, F] (ld = ldx elements) in dtype `dt` (F64 or F32); W: [K, F]; b: [K] (same dtype).
+// out_idx: int32[B]; out_p: dtype[B]. K = rows of W (1 for binary kinds).
+void launch_linear_small(int dt, const void* X, int64_t ldx, const void* W, const void* b, int64_t B, int F,
+                         int K, int kind, int32_t* out_idx, void* out_p, hipStream_t stream);
+
+// ---- gemv_binary.hip: binary LR predict, HBM-streaming GEMV + sigmoid epilogue ----------------
+// X: [B, F] bf16 or f32 row-major; w: [F] same dtype; bias: scalar f32.
+// out_idx: int32[B] (z > 0), out_p: f32[B] = sigmoid(|z|) (kind BINARY) or sigmoid(2|z|).
+void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_t B, int F, int kind,
+                        int32_t* out_idx, float* out_p, hipStream_t stream);
+
+// ---- gemm_softmax.hip: multiclass predict, bf16 MFMA GEMM + online softmax/argmax epilogue ----
+// X: [B, F] bf16; W: [K, F] bf16; b: [K] f32. F % 32 == 0. Workspace: gemm_softmax_workspace().
+size_t gemm_softmax_workspace(int64_t B, int K, int F);
+void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind,
+                         int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream);
+// Full logits (for tests / decision_function): Z[B, K] f32.
+void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B, int F, int K, float* Z,
+                        hipStream_t stream);
+
+// ---- train kernels (train.hip) -----------------------------------------------------------------
+// Binary logistic regression, one pass over X: accumulates grad (F w-entries, 1 bias) and stats
+// [loss_sum, n_correct] into per-block slabs, then reduce_slabs() folds them into out[F + 3]:
+// out = [gW(F) | gb | loss_sum | n_correct]  (sums over the batch, not means).
+size_t train_binary_workspace(int64_t B, int F);
+void launch_train_binary_grad(int dt, const void* X, const float* y, const float* w, float bias_unused,
+                              const float* bptr, int64_t B, int F, float* out, void* workspace, size_t ws_bytes,
+                              hipStream_t stream);
+// Small multiclass / binary (F*K <= 1024): fp64 or fp32, exact loss+grad of sklearn's objective
+// terms. out = [gW (K*F, row-major) | gb (K) | loss_sum | n_correct].
+size_t train_small_workspace(int64_t B, int F, int K);
+void launch_train_small_grad(int dt, const void* X, const int32_t* y, const void* W, const void* b, int64_t B,
+                             int F, int K, int kind, void* out, void* workspace, size_t ws_bytes,
+                             hipStream_t stream);
+// SGD (+momentum) update: p -= lr * (g * inv_n + l2 * p) for the first n_penalized entries,
+// p -= lr * g * inv_n for the rest (intercepts are not penalized, like sklearn).
+void launch_sgd_update(float* params, const float* grad, float* momentum_buf, int64_t n, int64_t n_penalized,
+                       float lr, float inv_n, float l2, float momentum, hipStream_t stream);
+
+// ---- pack.hip ----------------------------------------------------------------------------------
+void launch_cast(int src_dt, const void* src, int dst_dt, void* dst, int64_t n, hipStream_t stream);
+
+}  // namespace mlapi

@@ -1,0 +1,215 @@
+// Binary logistic-regression predict over a large batch: z = X w + b, label = z > 0,
+// p_max = sigmoid(|z|)  (BASELINE config 2: 1M x 256 bf16; reference op K1+K3+K5).
+//
+// Roofline: 1M x 256 bf16 = 512 MiB read once (> 256 MiB Infinity Cache) vs 8 B/row written,
+// ~1 FLOP/byte -> HBM-bound; target ~6 TB/s => ~85 us. Design (cdna_hip_programming.md
+// "GEMV / M <= 16" row: no LDS round trip):
+//  * a row is split into 16-byte chunks; LPR lanes cover one row (F=256 bf16: 32 lanes, so one
+//    global_load_dwordx4 wave-instruction reads 2 full rows = 1 KiB, perfectly coalesced);
+//  * each lane keeps its weight chunk in registers for the whole kernel (w read once per wave);
+//  * U rows per lane-group are loaded back-to-back (U x 16 B in flight per lane, non-temporal:
+//    X is streamed exactly once) before any is consumed -> latency hidden by ILP + 8 waves/SIMD;
+//  * bf16 products use v_dot2_f32_bf16 (2 MACs per instruction, f32 accumulate);
+//  * the U partial dot products are reduced across the LPR lanes with a butterfly
+//    reduce-scatter: log2(U) halving steps + the remaining xor steps (9 shuffles for U=8,
+//    LPR=32 instead of 40), after which lane groups own whole rows and one lane per row writes.
+#include <hip/hip_runtime.h>
+
+#include "mlapi/common.h"
+#include "mlapi/kernels.h"
+#include "mlapi/device.h"
+
+namespace mlapi {
+namespace {
+
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+
+template <typename T>
+struct Chunk;  // 16 bytes of one row
+template <>
+struct Chunk<uint16_t> {
+  static constexpr int N = 8;
+  __device__ static __forceinline__ float dot(const uint4& x, const uint4& w, float acc) {
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x.x), __builtin_bit_cast(bf16x2_t, w.x), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x.y), __builtin_bit_cast(bf16x2_t, w.y), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x.z), __builtin_bit_cast(bf16x2_t, w.z), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x.w), __builtin_bit_cast(bf16x2_t, w.w), acc, false);
+    return acc;
+  }
+};
+template <>
+struct Chunk<float> {
+  static constexpr int N = 4;
+  __device__ static __forceinline__ float dot(const uint4& x, const uint4& w, float acc) {
+    acc = fmaf(__uint_as_float(x.x), __uint_as_float(w.x), acc);
+    acc = fmaf(__uint_as_float(x.y), __uint_as_float(w.y), acc);
+    acc = fmaf(__uint_as_float(x.z), __uint_as_float(w.z), acc);
+    acc = fmaf(__uint_as_float(x.w), __uint_as_float(w.w), acc);
+    return acc;
+  }
+};
+
+// Butterfly reduce-scatter of U per-lane partials over groups of LPR lanes.
+// On return p[0] holds the full sum of row slot `slot` for this lane; see slot_of().
+template <int LPR, int U>
+__device__ __forceinline__ float reduce_scatter(float (&p)[U], int lane) {
+  int cnt = U;
+#pragma unroll
+  for (int off = LPR / 2; off >= 1; off >>= 1) {
+    if (cnt > 1) {
+      const int half = cnt / 2;
+      const bool upper = (lane & off) != 0;
+#pragma unroll
+      for (int j = 0; j < half; ++j) {
+        const float mine = upper ? p[j + half] : p[j];
+        const float other = upper ? p[j] : p[j + half];
+        p[j] = mine + __shfl_xor(other, off, 64);
+      }
+      cnt = half;
+    } else {
+      p[0] += __shfl_xor(p[0], off, 64);
+    }
+  }
+  return p[0];
+}
+
+template <int LPR, int U>
+__device__ __forceinline__ int slot_of(int lane) {
+  int slot = 0, cnt = U;
+#pragma unroll
+  for (int off = LPR / 2; off >= 1; off >>= 1) {
+    if (cnt > 1) {
+      const int half = cnt / 2;
+      if (lane & off) slot += half;
+      cnt = half;
+    }
+  }
+  return slot;
+}
+
+// Lowest lane offset used by the reduce-scatter phase; lanes whose bits below it are zero write.
+template <int LPR, int U>
+constexpr int writer_mask() {
+  int cnt = U, last = LPR;
+  for (int off = LPR / 2; off >= 1; off >>= 1) {
+    if (cnt > 1) { cnt /= 2; last = off; }
+  }
+  return last - 1;
+}
+
+template <typename T, int LPR, int CPL, int U>
+__global__ __launch_bounds__(256) void gemv_binary_kernel(const T* __restrict__ X, const T* __restrict__ w, float bias,
+                                                          int64_t B, int F, int kind, int32_t* __restrict__ out_idx,
+                                                          float* __restrict__ out_p) {
+  static_assert(U <= LPR, "reduce-scatter needs U <= LPR");
+  constexpr int RPW = 64 / LPR;  // rows per wave-instruction
+  constexpr int NE = Chunk<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / LPR;       // row within the wave-instruction
+  const int cl = lane % LPR;        // chunk lane
+  const int chunks = F / NE;        // 16-byte chunks per row
+  const int64_t ld16 = chunks;      // row stride in uint4
+
+  uint4 wv[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = cl + c * LPR;
+    wv[c] = ch < chunks ? reinterpret_cast<const uint4*>(w)[ch] : make_uint4(0, 0, 0, 0);
+  }
+  const float scale = kind == KIND_BINARY_SOFTMAX ? 2.f : 1.f;
+  const int slot = slot_of<LPR, U>(lane % LPR);
+  const bool writer = ((lane % LPR) & writer_mask<LPR, U>()) == 0;
+
+  const int64_t rows_per_wave_iter = (int64_t)U * RPW;
+  const int64_t waves_total = (int64_t)gridDim.x * (blockDim.x / 64);
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const uint4* X16 = reinterpret_cast<const uint4*>(X);
+
+  for (int64_t base = wave_id * rows_per_wave_iter; base < B; base += waves_total * rows_per_wave_iter) {
+    uint4 xv[U][CPL];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t row = base + (int64_t)u * RPW + sub;
+      row = row < B ? row : B - 1;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) {
+        const int ch = cl + c * LPR;
+        xv[u][c] = (CPL == 1 || ch < chunks) ? load_nt16(X16 + row * ld16 + (ch < chunks ? ch : 0))
+                                              : make_uint4(0, 0, 0, 0);
+        if (CPL == 1 && ch >= chunks) xv[u][c] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    float part[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) acc = Chunk<T>::dot(xv[u][c], wv[c], acc);
+      part[u] = acc;
+    }
+    const float z0 = reduce_scatter<LPR, U>(part, lane % LPR);
+    const int64_t row = base + (int64_t)slot * RPW + sub;
+    if (writer && row < B) {
+      const float z = z0 + bias;
+      const float a = scale * fabsf(z);
+      out_idx[row] = z > 0.f;
+      out_p[row] = 1.f / (1.f + __expf(-a));
+    }
+  }
+}
+
+template <typename T, int LPR, int CPL, int U>
+void launch(const void* X, const void* w, float bias, int64_t B, int F, int kind, int32_t* out_idx, float* out_p,
+            hipStream_t stream) {
+  constexpr int rows_per_block_iter = 4 * U * (64 / LPR);
+  int64_t blocks = (B + rows_per_block_iter - 1) / rows_per_block_iter;
+  const int64_t cap = 256 * 8;  // 256 CUs x 8 resident blocks: grid-stride beyond that
+  if (blocks > cap) blocks = cap;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((gemv_binary_kernel<T, LPR, CPL, U>), dim3((unsigned)blocks), dim3(256), 0, stream,
+                     static_cast<const T*>(X), static_cast<const T*>(w), bias, B, F, kind, out_idx, out_p);
+  MLAPI_HIP_CHECK(hipGetLastError());
+}
+
+template <typename T>
+void dispatch(const void* X, const void* w, float bias, int64_t B, int F, int kind, int32_t* out_idx, float* out_p,
+              hipStream_t stream) {
+  constexpr int NE = Chunk<T>::N;
+  if (F % NE != 0) throw std::invalid_argument("gemv_binary: F must be a multiple of 16 bytes of elements");
+  const int chunks = F / NE;
+  if (chunks <= 4)
+    launch<T, 4, 1, 4>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+  else if (chunks <= 8)
+    launch<T, 8, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+  else if (chunks <= 16)
+    launch<T, 16, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+  else if (chunks <= 32)
+    launch<T, 32, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+  else if (chunks <= 64)
+    launch<T, 64, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+  else if (chunks <= 128)
+    launch<T, 64, 2, 4>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+  else if (chunks <= 256)
+    launch<T, 64, 4, 2>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+  else if (chunks <= 512)
+    launch<T, 64, 8, 1>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+  else
+    throw std::invalid_argument("gemv_binary: F too large (max 4096 bf16 / 2048 f32)");
+}
+
+}  // namespace
+
+void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_t B, int F, int kind,
+                        int32_t* out_idx, float* out_p, hipStream_t stream) {
+  if (B <= 0) return;
+  if (reinterpret_cast<uintptr_t>(X) % 16 || reinterpret_cast<uintptr_t>(w) % 16)
+    throw std::invalid_argument("gemv_binary: X and w must be 16-byte aligned");
+  if (dt == DT_BF16)
+    dispatch<uint16_t>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+  else if (dt == DT_F32)
+    dispatch<float>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+  else
+    throw std::invalid_argument("gemv_binary: dtype must be bf16 or f32");
+}
+
+}  // namespace mlapi

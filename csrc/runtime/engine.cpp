@@ -1,0 +1,490 @@
+// Serving engine implementation (see engine.h for the design).
+#include "engine.h"
+
+#include <immintrin.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+#include "mlapi/kernels.h"
+#include "trace.h"
+
+namespace mlapi {
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+Model::~Model() {
+  if (device >= 0) {
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device);
+    if (dW) (void)hipFree(dW);
+    if (db) (void)hipFree(db);
+    (void)hipSetDevice(prev);
+  }
+}
+
+// Same epilogue formulas as linear_small.hip (float64).
+void cpu_linear_predict(const Model& m, const double* X, int64_t B, int32_t* idx, double* p) {
+  const int F = m.F, K = m.K;
+  std::vector<double> z((size_t)K);
+  for (int64_t r = 0; r < B; ++r) {
+    const double* x = X + r * F;
+    for (int k = 0; k < K; ++k) {
+      double acc = 0.0;
+      for (int f = 0; f < F; ++f) acc = std::fma(x[f], m.W[(size_t)k * F + f], acc);
+      z[k] = acc + m.b[k];
+    }
+    int32_t id = 0;
+    double pm;
+    if (m.kind == KIND_BINARY) {
+      const double p1 = 1.0 / (1.0 + std::exp(-z[0]));
+      const double p0 = 1.0 - p1;
+      id = z[0] > 0.0;
+      pm = std::isnan(p1) ? p1 : (p0 > p1 ? p0 : p1);
+    } else if (m.kind == KIND_BINARY_SOFTMAX) {
+      const double zz = z[0], mm = std::fabs(zz);
+      const double e0 = std::exp(-zz - mm), e1 = std::exp(zz - mm), s = e0 + e1;
+      const double q0 = e0 / s, q1 = e1 / s;
+      id = zz > 0.0;
+      pm = std::isnan(s) ? s : (q0 > q1 ? q0 : q1);
+    } else if (m.kind == KIND_MULTINOMIAL) {
+      double mx = z[0];
+      bool nan = std::isnan(z[0]);
+      for (int k = 1; k < K; ++k) {
+        nan |= std::isnan(z[k]);
+        if (z[k] > mx) { mx = z[k]; id = k; }
+      }
+      double s = 0.0;
+      for (int k = 0; k < K; ++k) s += std::exp(z[k] - mx);
+      pm = nan ? std::nan("") : 1.0 / s;
+    } else {
+      double mx = z[0];
+      for (int k = 1; k < K; ++k)
+        if (z[k] > mx) { mx = z[k]; id = k; }
+      double s = 0.0, smax = 0.0;
+      for (int k = 0; k < K; ++k) {
+        const double sg = 1.0 / (1.0 + std::exp(-z[k]));
+        s += sg;
+        smax = sg > smax ? sg : smax;
+      }
+      pm = smax / s;
+    }
+    idx[r] = id;
+    p[r] = pm;
+  }
+}
+
+Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
+  if (cfg_.max_batch < 1) cfg_.max_batch = 1;
+  if (cfg_.slots < 1) cfg_.slots = 1;
+  if (cfg_.dtype != DT_F64 && cfg_.dtype != DT_F32) throw std::invalid_argument("engine dtype must be f64 or f32");
+  q_meta_.reserve(4096);
+  q_x_.reserve(4096 * 8);
+  if (cfg_.device >= 0) {
+    MLAPI_HIP_CHECK(hipSetDevice(cfg_.device));
+    int lo = 0, hi = 0;
+    MLAPI_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    MLAPI_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
+    slots_.resize(cfg_.slots);
+    const size_t xb = (size_t)cfg_.max_batch * cfg_.max_features * sizeof(double);
+    for (int i = 0; i < cfg_.slots; ++i) {
+      Slot& s = slots_[i];
+      MLAPI_HIP_CHECK(hipHostMalloc(&s.hx, xb, hipHostMallocMapped));
+      MLAPI_HIP_CHECK(hipHostGetDevicePointer(&s.dx, s.hx, 0));
+      MLAPI_HIP_CHECK(hipHostMalloc((void**)&s.hidx, (size_t)cfg_.max_batch * sizeof(int32_t), hipHostMallocMapped));
+      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.didx, s.hidx, 0));
+      MLAPI_HIP_CHECK(hipHostMalloc(&s.hp, (size_t)cfg_.max_batch * sizeof(double), hipHostMallocMapped));
+      MLAPI_HIP_CHECK(hipHostGetDevicePointer(&s.dp, s.hp, 0));
+      MLAPI_HIP_CHECK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+      s.metas.reserve(cfg_.max_batch);
+      free_slots_.push_back(i);
+    }
+  }
+  batcher_ = std::thread([this] { batcher_loop(); });
+  if (cfg_.device >= 0) completer_ = std::thread([this] { completer_loop(); });
+}
+
+Engine::~Engine() {
+  stop();
+  if (cfg_.device >= 0) {
+    (void)hipSetDevice(cfg_.device);
+    for (Slot& s : slots_) {
+      if (s.ev) (void)hipEventDestroy(s.ev);
+      if (s.hx) (void)hipHostFree(s.hx);
+      if (s.hidx) (void)hipHostFree(s.hidx);
+      if (s.hp) (void)hipHostFree(s.hp);
+    }
+    {
+      std::lock_guard<std::mutex> lk(model_mu_);
+      model_.reset();
+    }
+    if (stream_) (void)hipStreamDestroy(stream_);
+  }
+}
+
+void Engine::stop() {
+  {
+    std::lock_guard<std::mutex> lk(q_mu_);
+    stopping_ = true;
+  }
+  q_cv_.notify_all();
+  if (batcher_.joinable()) batcher_.join();
+  s_cv_.notify_all();
+  if (completer_.joinable()) completer_.join();
+}
+
+uint64_t Engine::load_model(int kind, int F, int K, const double* W, const double* b,
+                            const std::vector<std::string>& label_json) {
+  if (F <= 0 || K <= 0) throw std::invalid_argument("load_model: empty model");
+  if (F > cfg_.max_features) throw std::invalid_argument("load_model: F exceeds engine max_features");
+  auto m = std::make_shared<Model>();
+  m->kind = kind;
+  m->F = F;
+  m->K = K;
+  m->dtype = cfg_.dtype;
+  m->W.assign(W, W + (size_t)K * F);
+  m->b.assign(b, b + K);
+  m->label_json = label_json;
+  m->version = next_version_.fetch_add(1);
+  if (cfg_.device >= 0) {
+    MLAPI_HIP_CHECK(hipSetDevice(cfg_.device));
+    m->device = cfg_.device;
+    const size_t es = dtype_size(cfg_.dtype);
+    MLAPI_HIP_CHECK(hipMalloc(&m->dW, (size_t)K * F * es));
+    MLAPI_HIP_CHECK(hipMalloc(&m->db, (size_t)K * es));
+    if (cfg_.dtype == DT_F64) {
+      MLAPI_HIP_CHECK(hipMemcpy(m->dW, m->W.data(), (size_t)K * F * 8, hipMemcpyHostToDevice));
+      MLAPI_HIP_CHECK(hipMemcpy(m->db, m->b.data(), (size_t)K * 8, hipMemcpyHostToDevice));
+    } else {
+      std::vector<float> wf(m->W.begin(), m->W.end()), bf(m->b.begin(), m->b.end());
+      MLAPI_HIP_CHECK(hipMemcpy(m->dW, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
+      MLAPI_HIP_CHECK(hipMemcpy(m->db, bf.data(), bf.size() * 4, hipMemcpyHostToDevice));
+    }
+  }
+  std::shared_ptr<const Model> cm = m;
+  {
+    std::lock_guard<std::mutex> lk(model_mu_);
+    model_.swap(cm);
+  }
+  {
+    std::lock_guard<std::mutex> lk(st_mu_);
+    stats_.model_version = m->version;
+  }
+  return m->version;  // old model (cm) released here unless an in-flight batch still holds it
+}
+
+void Engine::unload_model() {
+  std::lock_guard<std::mutex> lk(model_mu_);
+  model_.reset();
+}
+
+std::shared_ptr<const Model> Engine::model() const {
+  std::lock_guard<std::mutex> lk(model_mu_);
+  return model_;
+}
+
+bool Engine::submit(const double* x, int nf, uint64_t tag, Sink* sink) {
+  if (nf < 0 || nf > cfg_.max_features) return false;
+  const int64_t t = now_ns();
+  {
+    std::lock_guard<std::mutex> lk(q_mu_);
+    if (stopping_) return false;
+    const int32_t off = (int32_t)q_x_.size();
+    q_x_.insert(q_x_.end(), x, x + nf);
+    q_meta_.push_back(Meta{tag, sink, t, nf, off});
+  }
+  q_cv_.notify_one();
+  return true;
+}
+
+namespace {
+struct BlockingSink : Sink {
+  std::mutex mu;
+  std::condition_variable cv;
+  int64_t remaining = 0;
+  int32_t* idx;
+  double* p;
+  int32_t* st;
+  void on_complete(const Completion* c, size_t n, const std::shared_ptr<const Model>&) override {
+    std::lock_guard<std::mutex> lk(mu);
+    for (size_t i = 0; i < n; ++i) {
+      idx[c[i].tag] = c[i].idx;
+      p[c[i].tag] = c[i].p;
+      st[c[i].tag] = c[i].status;
+    }
+    remaining -= (int64_t)n;
+    if (remaining == 0) cv.notify_all();
+  }
+};
+}  // namespace
+
+void Engine::predict(const double* X, int64_t B, int F, int32_t* idx, double* p, int32_t* status) {
+  BlockingSink sink;
+  sink.idx = idx;
+  sink.p = p;
+  sink.st = status;
+  sink.remaining = B;
+  int64_t submitted = 0;
+  for (int64_t r = 0; r < B; ++r) {
+    if (!submit(X + r * F, F, (uint64_t)r, &sink)) {
+      idx[r] = 0;
+      p[r] = std::nan("");
+      status[r] = ST_SHUTDOWN;
+    } else {
+      ++submitted;
+    }
+  }
+  std::unique_lock<std::mutex> lk(sink.mu);
+  sink.remaining -= (B - submitted);
+  sink.cv.wait(lk, [&] { return sink.remaining <= 0; });
+}
+
+void Engine::record_batch(size_t n) {
+  int b = 0;
+  while ((size_t(1) << (b + 1)) <= n && b < 11) ++b;
+  std::lock_guard<std::mutex> lk(st_mu_);
+  stats_.batches++;
+  stats_.batch_hist[b]++;
+}
+
+void Engine::deliver(std::vector<Meta>& metas, const int32_t* idx, const double* p, const int32_t* st,
+                     const std::shared_ptr<const Model>& m, int64_t now) {
+  const size_t n = metas.size();
+  uint64_t errors = 0;
+  uint64_t lat_hist[24] = {0};
+  double lat_sum = 0;
+  // group by sink, preserving submission order inside each sink
+  std::vector<Completion> buf;
+  buf.reserve(n);
+  std::vector<char> done(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    if (done[i]) continue;
+    Sink* sk = metas[i].sink;
+    buf.clear();
+    for (size_t j = i; j < n; ++j) {
+      if (done[j] || metas[j].sink != sk) continue;
+      done[j] = 1;
+      const int64_t lat = now - metas[j].t_enq;
+      int32_t s = st[j];
+      if (s == ST_OK && !std::isfinite(p[j])) s = ST_NONFINITE;
+      if (s != ST_OK) ++errors;
+      buf.push_back(Completion{metas[j].tag, idx[j], s, p[j], lat});
+      const double us = (double)lat * 1e-3;
+      lat_sum += us;
+      int bkt = 0;
+      while (bkt < 23 && (double)(int64_t(1) << bkt) <= us) ++bkt;
+      lat_hist[bkt]++;
+    }
+    if (sk) sk->on_complete(buf.data(), buf.size(), m);
+  }
+  std::lock_guard<std::mutex> lk(st_mu_);
+  stats_.requests += n;
+  stats_.errors += errors;
+  stats_.latency_sum_us += lat_sum;
+  for (int b = 0; b < 24; ++b) stats_.latency_hist[b] += lat_hist[b];
+}
+
+void Engine::run_cpu(std::vector<Meta>& metas, const std::vector<double>& xs, const std::shared_ptr<const Model>& m) {
+  const size_t n = metas.size();
+  std::vector<int32_t> idx(n, 0), st(n, ST_OK);
+  std::vector<double> p(n, 0.0);
+  if (!m) {
+    std::fill(st.begin(), st.end(), (int32_t)ST_NO_MODEL);
+  } else {
+    std::vector<double> X((size_t)n * m->F, 0.0);
+    for (size_t i = 0; i < n; ++i) {
+      if (metas[i].nf != m->F) {
+        st[i] = ST_SHAPE;
+        continue;
+      }
+      std::memcpy(&X[i * m->F], &xs[metas[i].off], sizeof(double) * m->F);
+    }
+    cpu_linear_predict(*m, X.data(), (int64_t)n, idx.data(), p.data());
+    if (cfg_.fail_every > 0 && (++batch_counter_ % (uint64_t)cfg_.fail_every) == 0)
+      std::fill(st.begin(), st.end(), (int32_t)ST_DEVICE_ERROR);
+  }
+  if (cfg_.delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(cfg_.delay_us));
+  record_batch(n);
+  deliver(metas, idx.data(), p.data(), st.data(), m, now_ns());
+}
+
+void Engine::batcher_loop() {
+  if (cfg_.device >= 0) (void)hipSetDevice(cfg_.device);
+  std::vector<Meta> metas;
+  std::vector<double> xs;
+  metas.reserve(4096);
+  xs.reserve(4096 * 8);
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(q_mu_);
+      q_cv_.wait(lk, [&] { return stopping_ || !q_meta_.empty(); });
+      if (q_meta_.empty() && stopping_) break;
+      if (cfg_.max_wait_us > 0 && (int)q_meta_.size() < cfg_.max_batch && !stopping_) {
+        q_cv_.wait_for(lk, std::chrono::microseconds(cfg_.max_wait_us),
+                       [&] { return stopping_ || (int)q_meta_.size() >= cfg_.max_batch; });
+      }
+      metas.swap(q_meta_);
+      xs.swap(q_x_);
+      q_meta_.clear();
+      q_x_.clear();
+    }
+    const std::shared_ptr<const Model> m = model();
+    size_t pos = 0;
+    while (pos < metas.size()) {
+      const size_t n = std::min(metas.size() - pos, (size_t)cfg_.max_batch);
+      std::vector<Meta> chunk(metas.begin() + pos, metas.begin() + pos + n);
+      pos += n;
+      if (cfg_.device < 0 || !m) {
+        run_cpu(chunk, xs, m);
+        continue;
+      }
+      // ---- GPU path: acquire a slot, pack, launch
+      int si;
+      {
+        std::unique_lock<std::mutex> lk(s_mu_);
+        s_cv_.wait(lk, [&] { return !free_slots_.empty(); });
+        si = free_slots_.front();
+        free_slots_.pop_front();
+      }
+      Slot& s = slots_[si];
+      TraceRange tr("mlapi.batch.launch");
+      s.metas.swap(chunk);
+      s.model = m;
+      s.n = (int)n;
+      s.failed = false;
+      s.launched = false;
+      s.pre_status.assign(n, ST_OK);
+      const int F = m->F;
+      if (m->dtype == DT_F64) {
+        double* hx = static_cast<double*>(s.hx);
+        for (size_t i = 0; i < n; ++i) {
+          if (s.metas[i].nf != F) {
+            s.pre_status[i] = ST_SHAPE;
+            std::memset(hx + i * F, 0, sizeof(double) * F);
+          } else {
+            std::memcpy(hx + i * F, &xs[s.metas[i].off], sizeof(double) * F);
+          }
+        }
+      } else {
+        float* hx = static_cast<float*>(s.hx);
+        for (size_t i = 0; i < n; ++i) {
+          const bool ok = s.metas[i].nf == F;
+          if (!ok) s.pre_status[i] = ST_SHAPE;
+          for (int f = 0; f < F; ++f) hx[i * F + f] = ok ? (float)xs[s.metas[i].off + f] : 0.f;
+        }
+      }
+      if (cfg_.fail_every > 0 && (++batch_counter_ % (uint64_t)cfg_.fail_every) == 0) {
+        s.failed = true;
+      } else {
+        try {
+          launch_linear_small(m->dtype, s.dx, F, m->dW, m->db, (int64_t)n, F, m->K, m->kind, s.didx, s.dp,
+                              stream_);
+          MLAPI_HIP_CHECK(hipEventRecord(s.ev, stream_));
+          s.launched = true;
+        } catch (const std::exception&) {
+          s.failed = true;
+          healthy_.store(false);
+        }
+      }
+      s.t_launch = now_ns();
+      {
+        std::lock_guard<std::mutex> lk(s_mu_);
+        inflight_.push_back(si);
+      }
+      s_cv_.notify_all();
+    }
+    metas.clear();
+    xs.clear();
+  }
+  {
+    std::lock_guard<std::mutex> lk(s_mu_);
+    batcher_done_ = true;
+  }
+  s_cv_.notify_all();
+}
+
+void Engine::completer_loop() {
+  (void)hipSetDevice(cfg_.device);
+  std::vector<int32_t> st;
+  std::vector<double> pd;
+  for (;;) {
+    int si;
+    {
+      std::unique_lock<std::mutex> lk(s_mu_);
+      s_cv_.wait(lk, [&] { return !inflight_.empty() || batcher_done_; });
+      if (inflight_.empty()) break;  // batcher has exited and nothing is in flight
+      si = inflight_.front();
+      inflight_.pop_front();
+    }
+    Slot& s = slots_[si];
+    if (s.launched) {
+      // Poll the event: spin briefly (sub-10us kernels), then back off.
+      const int64_t t0 = now_ns();
+      int spins = 0;
+      for (;;) {
+        const hipError_t e = hipEventQuery(s.ev);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) {
+          s.failed = true;
+          healthy_.store(false);
+          break;
+        }
+        if (++spins < 2000) {
+          _mm_pause();
+        } else {
+          std::this_thread::sleep_for(std::chrono::microseconds(20));
+          if (cfg_.watchdog_ms > 0 && now_ns() - t0 > (int64_t)cfg_.watchdog_ms * 1000000) healthy_.store(false);
+        }
+      }
+    }
+    if (cfg_.delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(cfg_.delay_us));
+    const int64_t now = now_ns();
+    const size_t n = (size_t)s.n;
+    st.assign(s.pre_status.begin(), s.pre_status.end());
+    pd.resize(n);
+    if (s.failed) {
+      std::fill(st.begin(), st.end(), (int32_t)ST_DEVICE_ERROR);
+      std::fill(pd.begin(), pd.end(), 0.0);
+    } else if (s.model->dtype == DT_F64) {
+      std::memcpy(pd.data(), s.hp, n * sizeof(double));
+    } else {
+      const float* pf = static_cast<const float*>(s.hp);
+      for (size_t i = 0; i < n; ++i) pd[i] = pf[i];
+    }
+    {
+      std::lock_guard<std::mutex> lk(st_mu_);
+      stats_.device_us_sum += (double)(now - s.t_launch) * 1e-3;
+    }
+    record_batch(n);
+    std::shared_ptr<const Model> m = std::move(s.model);
+    deliver(s.metas, s.hidx, pd.data(), st.data(), m, now);
+    s.metas.clear();
+    {
+      std::lock_guard<std::mutex> lk(s_mu_);
+      free_slots_.push_back(si);
+    }
+    s_cv_.notify_all();
+  }
+}
+
+EngineStats Engine::stats() const {
+  EngineStats s;
+  {
+    std::lock_guard<std::mutex> lk(st_mu_);
+    s = stats_;
+  }
+  {
+    std::lock_guard<std::mutex> lk(const_cast<std::mutex&>(q_mu_));
+    s.queue_depth = q_meta_.size();
+  }
+  s.healthy = healthy_.load();
+  return s;
+}
+
+}  // namespace mlapi

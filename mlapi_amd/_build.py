@@ -1,0 +1,114 @@
+"""Build the native extension ``mlapi_amd._C`` in-tree with hipcc for gfx950.
+
+Every source (HIP kernels, C++ runtime, HTTP server, bindings) is compiled by ``hipcc
+--offload-arch=gfx950`` in parallel and linked into ``mlapi_amd/_C<ext-suffix>.so``. No hipify,
+no torch cpp_extension: the extension links only libamdhip64 (resolved at import time to the
+HIP runtime torch already loaded, see :mod:`mlapi_amd._native`).
+
+Usage: ``python -m mlapi_amd._build [--force] [--jobs N]``.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+BUILD = ROOT / "build" / "native"
+ARCH = os.environ.get("MLAPI_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = [
+    "kernels/linear_small.hip",
+    "kernels/gemv_binary.hip",
+    "kernels/gemm_softmax.hip",
+    "kernels/train.hip",
+    "kernels/pack.hip",
+    "runtime/engine.cpp",
+    "http/server.cpp",
+    "http/loadgen.cpp",
+    "bindings.cpp",
+]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (ROCm required to build mlapi_amd._C)")
+
+
+def ext_path() -> Path:
+    return ROOT / "mlapi_amd" / ("_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _includes() -> list:
+    import pybind11
+
+    return [f"-I{CSRC}", f"-I{CSRC / 'include'}", f"-I{pybind11.get_include()}",
+            f"-I{sysconfig.get_paths()['include']}"]
+
+
+def _flags() -> list:
+    return ["-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}",
+            "-Wno-unused-result", "-Wno-unused-command-line-argument"]
+
+
+def _headers_mtime() -> float:
+    m = 0.0
+    for p in CSRC.rglob("*.h"):
+        m = max(m, p.stat().st_mtime)
+    return m
+
+
+def _compile(src: str, force: bool, hmt: float) -> Path:
+    s = CSRC / src
+    obj = BUILD / (src.replace("/", "__") + ".o")
+    if not force and obj.exists() and obj.stat().st_mtime >= max(s.stat().st_mtime, hmt):
+        return obj
+    cmd = [hipcc()] + _flags() + _includes()
+    if s.suffix == ".cpp":
+        cmd += ["-x", "hip"] if src == "bindings.cpp" else []
+    cmd += ["-c", str(s), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+    return obj
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    hmt = _headers_mtime()
+    jobs = jobs or min(len(SOURCES), max(1, min(8, os.cpu_count() or 1)))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force, hmt), SOURCES))
+    out = ext_path()
+    newest = max(o.stat().st_mtime for o in objs)
+    if force or not out.exists() or out.stat().st_mtime < newest:
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out) + ".tmp"] + \
+              [str(o) for o in objs] + ["-lpthread"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+        os.replace(str(out) + ".tmp", out)
+        if verbose:
+            print(f"[mlapi_amd] built {out.relative_to(ROOT)}", file=sys.stderr)
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=None)
+    a = ap.parse_args(argv)
+    build(force=a.force, jobs=a.jobs)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

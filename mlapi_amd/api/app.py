@@ -1,0 +1,205 @@
+"""The FastAPI application: the reference's HTTP surface on top of the native engine.
+
+Route-for-route parity with `main.py`:
+
+* ``POST /predict`` (`main.py:16-27`): body ``IrisSpecies`` (4 required floats), response
+  ``{"prediction": <label>, "probability": <max class probability>}``. The reference unpickles
+  the checkpoint and runs sklearn twice per request; here the request is awaited on the batching
+  engine (HIP kernel on a GPU, or the C++ CPU backend) and the checkpoint is hot-reloaded only
+  when the file changes.
+* ``POST /files/`` (`main.py:29-39`): multipart ``file`` + ``token`` -> CSV parsed with pandas,
+  ``print(df)``, echoed back as ``{"file": {col: {row: value}}, "token": token}``.
+* ``/docs``, ``/redoc``, ``/openapi.json``: FastAPI defaults; the schema matches the reference's
+  (title "FastAPI", version "0.1.0", same operation ids and component schemas).
+
+Extra routes (excluded from the OpenAPI schema so it stays identical): ``/healthz``,
+``/readyz``, ``/metrics``, ``POST /admin/reload``.
+
+Error behaviour follows the reference: validation errors are FastAPI's 422 bodies, any failure
+in the model path is an HTTP 500 ``Internal Server Error`` (text/plain).
+"""
+import io
+import logging
+import math
+from typing import Optional
+
+from fastapi import FastAPI, Request
+from fastapi.exceptions import RequestValidationError
+from fastapi.responses import JSONResponse, PlainTextResponse, Response
+from pydantic import BaseModel, create_model
+
+from mlapi_amd.api.multipart import MultipartError, parse_form
+from mlapi_amd.utils.config import IRIS_FEATURES, Config
+
+log = logging.getLogger("mlapi_amd.api")
+
+
+class IrisSpecies(BaseModel):
+    """Request schema of `POST /predict` (`main.py:10-14`)."""
+
+    sepal_length: float
+    sepal_width: float
+    petal_length: float
+    petal_width: float
+
+
+def request_model(feature_names) -> type:
+    if list(feature_names) == IRIS_FEATURES:
+        return IrisSpecies
+    return create_model("FeatureRecord", **{n: (float, ...) for n in feature_names})
+
+
+FILES_OPENAPI = {
+    "requestBody": {
+        "content": {"multipart/form-data": {"schema": {"$ref": "#/components/schemas/Body_create_file_files__post"}}},
+        "required": True,
+    },
+    "responses": {
+        "422": {
+            "description": "Validation Error",
+            "content": {"application/json": {"schema": {"$ref": "#/components/schemas/HTTPValidationError"}}},
+        }
+    },
+}
+FILES_BODY_SCHEMA = {
+    "properties": {
+        "file": {"contentMediaType": "application/octet-stream", "title": "File", "type": "string"},
+        "token": {"title": "Token", "type": "string"},
+    },
+    "required": ["file", "token"],
+    "title": "Body_create_file_files__post",
+    "type": "object",
+}
+
+
+def _missing(name: str) -> dict:
+    return {"type": "missing", "loc": ["body", name], "msg": "Field required", "input": None}
+
+
+def dataframe_payload(df, strict_parity: bool = True):
+    """``jsonable_encoder(df)`` as the reference sees it: ``dict(df)`` -> {col: {row: value}}.
+
+    With ``strict_parity`` (default) cells that FastAPI cannot encode (numpy ints / bools, NaN)
+    raise -> HTTP 500, exactly like the reference. Otherwise they are converted.
+    """
+    import numpy as np
+
+    out = {}
+    for col in df.columns:
+        colmap = {}
+        for idx, v in df[col].items():
+            if isinstance(v, (np.bool_, bool)) or (isinstance(v, np.integer)):
+                if strict_parity:
+                    raise ValueError(f"{type(v)} is not JSON serializable")
+                v = v.item()
+            elif isinstance(v, float) and not math.isfinite(v):
+                if strict_parity:
+                    raise ValueError("Out of range float values are not JSON compliant")
+                v = None
+            elif isinstance(v, np.generic):
+                v = v.item()
+            colmap[idx if not isinstance(idx, np.generic) else idx.item()] = v
+        out[col if not isinstance(col, np.generic) else col.item()] = colmap
+    return out
+
+
+def create_app(config: Optional[Config] = None, *, runtime=None) -> FastAPI:
+    """Build the app. ``runtime`` is a :class:`mlapi_amd.serve.service.ServingRuntime`; when
+    omitted one is created lazily from ``config`` on first use (so `uvicorn main:app` works)."""
+    config = config or Config.from_env()
+    app = FastAPI()  # no title/version: OpenAPI info stays {"title": "FastAPI", "version": "0.1.0"}
+    app.state.config = config
+    app.state.runtime = runtime
+    Record = request_model(config.feature_names)
+    names = list(config.feature_names)
+
+    def rt():
+        if app.state.runtime is None:
+            from mlapi_amd.serve.service import ServingRuntime
+
+            app.state.runtime = ServingRuntime(config)
+        return app.state.runtime
+
+    @app.post("/predict")
+    async def predict_species(iris: Record):  # type: ignore[valid-type]
+        data = iris.model_dump()
+        r = rt()
+        if not r.store.check():  # per-request checkpoint semantics (main.py:19), via stat()
+            raise RuntimeError(r.store.last_error or "no model loaded")
+        label, probability = await r.client.predict_one([data[n] for n in names])
+        return {"prediction": label, "probability": probability}
+
+    @app.post("/files/", openapi_extra=FILES_OPENAPI)
+    async def create_file(request: Request):
+        body = await request.body()
+        try:
+            parts = parse_form(body, request.headers.get("content-type"))
+        except MultipartError:  # Starlette: MultiPartException -> 400 (fastapi/routing.py)
+            return JSONResponse({"detail": "There was an error parsing the body"}, status_code=400)
+        fields = {}
+        for p in parts:
+            fields[p.name] = p  # last one wins, like FormData.get
+        errors = []
+        fpart, tpart = fields.get("file"), fields.get("token")
+        if fpart is None or (not fpart.is_file and fpart.data == b""):
+            errors.append(_missing("file"))
+        if tpart is None or (not tpart.is_file and tpart.data == b""):
+            errors.append(_missing("token"))
+        if errors:
+            raise RequestValidationError(errors)
+        import pandas as pd
+
+        s = str(fpart.data, "utf-8")  # main.py:31
+        df = pd.read_csv(io.StringIO(s))  # main.py:32-33
+        print(df)  # main.py:34
+        token = tpart.data.decode("utf-8")
+        return {"file": dataframe_payload(df, strict_parity=config.files_strict_parity), "token": token}
+
+    # ---- operational endpoints (not part of the reference schema)
+    @app.get("/healthz", include_in_schema=False)
+    async def healthz():
+        r = app.state.runtime
+        ok = r is None or r.healthy()
+        return JSONResponse({"status": "ok" if ok else "unhealthy"}, status_code=200 if ok else 503)
+
+    @app.get("/readyz", include_in_schema=False)
+    async def readyz():
+        r = rt()
+        ready = r.store.check() and r.healthy()
+        return JSONResponse({"ready": bool(ready), "model_version": r.handle.version, "backend": r.handle.backend,
+                             "error": r.store.last_error}, status_code=200 if ready else 503)
+
+    @app.get("/metrics", include_in_schema=False)
+    async def metrics():
+        return PlainTextResponse(rt().metrics_text(), media_type="text/plain; version=0.0.4")
+
+    @app.post("/admin/reload", include_in_schema=False)
+    async def admin_reload():
+        r = rt()
+        r.store._key = ("force",)  # next check() re-reads the file
+        ok = r.store.check()
+        r.on_admin_reload()
+        return JSONResponse({"reloaded": ok, "model_version": r.handle.version, "error": r.store.last_error},
+                            status_code=200 if ok else 500)
+
+    _orig_openapi = app.openapi
+
+    def openapi():
+        if app.openapi_schema:
+            return app.openapi_schema
+        schema = _orig_openapi()
+        schema.setdefault("components", {}).setdefault("schemas", {})["Body_create_file_files__post"] = \
+            FILES_BODY_SCHEMA
+        schemas = schema["components"]["schemas"]
+        schema["components"]["schemas"] = {k: schemas[k] for k in sorted(schemas)}
+        app.openapi_schema = schema
+        return schema
+
+    app.openapi = openapi  # type: ignore[method-assign]
+
+    @app.on_event("shutdown")
+    async def _shutdown():  # pragma: no cover - exercised by uvicorn
+        if app.state.runtime is not None and getattr(app.state.runtime, "owned_by_app", False):
+            app.state.runtime.close()
+
+    return app

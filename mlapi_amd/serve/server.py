@@ -1,0 +1,84 @@
+"""NativeServer: the production front end (native HTTP fast path + ASGI slow path).
+
+    python -m mlapi_amd.serve --port 8000                 # one process, one GPU (or CPU backend)
+    torchrun --nproc-per-node 8 -m mlapi_amd.serve ...    # DP=8 replicas sharing one port
+
+Compared with `uvicorn main:app` (which also works and serves the same app), the native server
+parses/answers valid `/predict` requests in C++ IO threads and only hands the remaining traffic
+to FastAPI; the model runs in the same batching engine either way.
+"""
+from __future__ import annotations
+
+import logging
+import signal
+import threading
+from typing import Optional
+
+from mlapi_amd._native import C
+from mlapi_amd.api.app import create_app
+from mlapi_amd.serve.asgi_bridge import AsgiBridge
+from mlapi_amd.serve.service import ServingRuntime
+from mlapi_amd.utils.config import Config
+
+log = logging.getLogger("mlapi_amd.serve")
+
+
+class NativeServer:
+    def __init__(self, config: Config, runtime: Optional[ServingRuntime] = None, app=None):
+        self.config = config
+        self.runtime = runtime or ServingRuntime(config)
+        self.runtime.owned_by_app = False
+        self.app = app or create_app(config, runtime=self.runtime)
+        c = C()
+        sc = c.ServerConfig()
+        sc.host = config.host
+        sc.port = int(config.port)
+        sc.io_threads = int(config.io_threads)
+        sc.reuseport = bool(config.reuseport)
+        sc.feature_names = list(config.feature_names)
+        sc.server_header = config.server_header
+        sc.fast_path = bool(config.fast_path)
+        self.http = c.HttpServer(self.runtime.handle.engine, sc)
+        self.runtime.http = self.http
+        self.bridge = AsgiBridge(self.app, self.http, workers=config.slow_workers)
+        self._started = False
+
+    @property
+    def port(self) -> int:
+        return int(self.http.port())
+
+    def start(self) -> "NativeServer":
+        self.runtime.store.start_watcher(self.config.reload_interval_ms)
+        self.http.start()
+        self.bridge.start()
+        self._started = True
+        log.info("serving on %s:%d (backend %s)", self.config.host, self.port, self.runtime.handle.backend)
+        return self
+
+    def stop(self) -> None:
+        if not self._started:
+            return
+        self._started = False
+        self.http.stop()
+        self.bridge.stop()
+        self.runtime.close()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+
+    def serve_forever(self) -> None:
+        stop = threading.Event()
+        for sig in (signal.SIGINT, signal.SIGTERM):
+            try:
+                signal.signal(sig, lambda *_: stop.set())
+            except ValueError:  # not main thread
+                pass
+        self.start()
+        try:
+            while not stop.wait(0.5):
+                pass
+        finally:
+            self.stop()

@@ -1,0 +1,112 @@
+"""Typed configuration from environment variables and CLI flags.
+
+The reference has no configuration: the checkpoint path 'LRClassifier.pkl' is hard-coded and
+resolved against the CWD on every request (`main.py:19`), the feature order is hard-coded
+(`main.py:20`) and the only knobs are uvicorn's CLI flags (`README.md:16`). Defaults here keep
+every one of those behaviours; everything else is opt-in.
+
+Every field ``foo`` can be set with the environment variable ``MLAPI_FOO``.
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+IRIS_FEATURES = ["sepal_length", "sepal_width", "petal_length", "petal_width"]  # main.py:11-14,20
+
+
+@dataclass
+class Config:
+    # model / checkpoint
+    model_path: str = "LRClassifier.pkl"      # main.py:19 (relative to the CWD, like the reference)
+    reload: str = "mtime"                     # "mtime": hot-reload when the file changes; "off"
+    reload_interval_ms: int = 50              # watcher period for the native fast path
+    missing_model: str = "error"              # "error": HTTP 500 while the file is absent (A16); "keep"
+    feature_names: List[str] = field(default_factory=lambda: list(IRIS_FEATURES))
+    int_labels: str = "json"                  # "json": render int labels as numbers; "error": 500 like A17
+    files_strict_parity: bool = True          # /files/: 500 on int/bool/NaN cells like the reference (R4d)
+    # device / engine
+    device: str = "auto"                      # "auto" | "cpu" | "cuda" | "cuda:N" | "N"
+    dtype: str = "f64"                        # serving compute dtype: f64 (sklearn parity) | f32
+    max_batch: int = 256
+    max_wait_us: int = 0                      # 0 = continuous batching
+    slots: int = 4
+    watchdog_ms: int = 2000
+    fail_every: int = 0                       # fault injection (tests): fail every N-th batch
+    delay_us: int = 0                         # fault injection: delay every batch
+    # HTTP
+    host: str = "127.0.0.1"
+    port: int = 8000
+    io_threads: int = 2
+    reuseport: bool = True
+    fast_path: bool = True
+    server_header: str = "uvicorn"
+    slow_workers: int = 1
+    log_level: str = "warning"
+    access_log: bool = False
+    # observability
+    metrics: bool = True
+
+    @classmethod
+    def from_env(cls, **overrides) -> "Config":
+        cfg = cls()
+        for f in dataclasses.fields(cls):
+            env = os.environ.get("MLAPI_" + f.name.upper())
+            if env is not None:
+                setattr(cfg, f.name, _coerce(f, env))
+        for k, v in overrides.items():
+            if v is not None:
+                setattr(cfg, k, v)
+        return cfg
+
+    @classmethod
+    def add_arguments(cls, ap: argparse.ArgumentParser) -> None:
+        for f in dataclasses.fields(cls):
+            flag = "--" + f.name.replace("_", "-")
+            if f.type in ("bool", bool):
+                ap.add_argument(flag, dest=f.name, default=None, type=_parse_bool)
+            elif f.name == "feature_names":
+                ap.add_argument(flag, dest=f.name, default=None, type=lambda s: [x for x in s.split(",") if x])
+            else:
+                typ = int if f.type in ("int", int) else str
+                ap.add_argument(flag, dest=f.name, default=None, type=typ)
+
+    @classmethod
+    def from_args(cls, ns: argparse.Namespace) -> "Config":
+        return cls.from_env(**{f.name: getattr(ns, f.name, None) for f in dataclasses.fields(cls)})
+
+    def device_index(self) -> Optional[int]:
+        """None -> CPU backend; int -> HIP device ordinal."""
+        d = str(self.device).strip().lower()
+        if d == "cpu":
+            return None
+        if d in ("cuda", "gpu", "hip"):
+            return int(os.environ.get("LOCAL_RANK", "0"))
+        if d.startswith("cuda:"):
+            return int(d.split(":", 1)[1])
+        if d.isdigit():
+            return int(d)
+        # auto: a GPU if one is visible (LOCAL_RANK selects it under torchrun), else CPU
+        from mlapi_amd._native import gpu_count
+
+        n = gpu_count()
+        if n == 0:
+            return None
+        return int(os.environ.get("LOCAL_RANK", "0")) % n
+
+
+def _parse_bool(s: str) -> bool:
+    return str(s).strip().lower() in ("1", "true", "yes", "on")
+
+
+def _coerce(f: dataclasses.Field, s: str):
+    if f.type in ("bool", bool):
+        return _parse_bool(s)
+    if f.type in ("int", int):
+        return int(s)
+    if f.name == "feature_names":
+        return [x for x in s.split(",") if x]
+    return s

@@ -1,0 +1,70 @@
+"""Prometheus text exposition for ``GET /metrics``.
+
+The reference's only observability is ``print(df)`` (`main.py:34`) and uvicorn's access log.
+Here the native engine and HTTP server keep lock-cheap counters and histograms (requests,
+batches, batch-size histogram, queue depth, latency histogram, device time, health) and this
+module renders them (plus the rank's identity) in the Prometheus 0.0.4 text format. No global
+registry: it is rendered on demand from the live objects.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, Optional
+
+
+def _line(out: list, name: str, value, labels: Optional[Dict[str, str]] = None) -> None:
+    if labels:
+        lab = ",".join(f'{k}="{v}"' for k, v in labels.items())
+        out.append(f"{name}{{{lab}}} {value}")
+    else:
+        out.append(f"{name} {value}")
+
+
+def render(engine_stats: Optional[dict] = None, server_stats: Optional[dict] = None,
+           labels: Optional[Dict[str, str]] = None, extra: Iterable[tuple] = ()) -> str:
+    labels = dict(labels or {})
+    out: list = []
+    if engine_stats:
+        es = engine_stats
+        out += ["# HELP mlapi_requests_total Requests completed by the batching engine.",
+                "# TYPE mlapi_requests_total counter"]
+        _line(out, "mlapi_requests_total", es["requests"], labels)
+        out += ["# TYPE mlapi_request_errors_total counter"]
+        _line(out, "mlapi_request_errors_total", es["errors"], labels)
+        out += ["# HELP mlapi_batches_total Kernel launches (batches).", "# TYPE mlapi_batches_total counter"]
+        _line(out, "mlapi_batches_total", es["batches"], labels)
+        out += ["# HELP mlapi_batch_size Rows per launch.", "# TYPE mlapi_batch_size histogram"]
+        cum = 0
+        for i, c in enumerate(es["batch_hist"]):
+            cum += c
+            _line(out, "mlapi_batch_size_bucket", cum, {**labels, "le": str(2 ** (i + 1) - 1)})
+        _line(out, "mlapi_batch_size_bucket", cum, {**labels, "le": "+Inf"})
+        _line(out, "mlapi_batch_size_count", es["batches"], labels)
+        out += ["# HELP mlapi_request_latency_seconds Submit-to-completion latency inside the engine.",
+                "# TYPE mlapi_request_latency_seconds histogram"]
+        cum = 0
+        for i, c in enumerate(es["latency_hist_us_pow2"]):
+            cum += c
+            _line(out, "mlapi_request_latency_seconds_bucket", cum, {**labels, "le": f"{(2 ** i) * 1e-6:.6g}"})
+        _line(out, "mlapi_request_latency_seconds_bucket", cum, {**labels, "le": "+Inf"})
+        _line(out, "mlapi_request_latency_seconds_sum", f"{es['latency_sum_us'] * 1e-6:.9g}", labels)
+        _line(out, "mlapi_request_latency_seconds_count", es["requests"], labels)
+        out += ["# TYPE mlapi_device_seconds_total counter"]
+        _line(out, "mlapi_device_seconds_total", f"{es['device_us_sum'] * 1e-6:.9g}", labels)
+        out += ["# TYPE mlapi_queue_depth gauge"]
+        _line(out, "mlapi_queue_depth", es["queue_depth"], labels)
+        out += ["# TYPE mlapi_model_version gauge"]
+        _line(out, "mlapi_model_version", es["model_version"], labels)
+        out += ["# TYPE mlapi_engine_healthy gauge"]
+        _line(out, "mlapi_engine_healthy", 1 if es["healthy"] else 0, labels)
+    if server_stats:
+        out += ["# HELP mlapi_http_requests_total HTTP requests by path taken.",
+                "# TYPE mlapi_http_requests_total counter"]
+        _line(out, "mlapi_http_requests_total", server_stats["fast"], {**labels, "path": "fast"})
+        _line(out, "mlapi_http_requests_total", server_stats["slow"], {**labels, "path": "slow"})
+        out += ["# TYPE mlapi_http_connections_total counter"]
+        _line(out, "mlapi_http_connections_total", server_stats["connections"], labels)
+        out += ["# TYPE mlapi_http_internal_errors_total counter"]
+        _line(out, "mlapi_http_internal_errors_total", server_stats["errors"], labels)
+    for name, value, lab in extra:
+        _line(out, name, value, {**labels, **(lab or {})})
+    return "\n".join(out) + "\n"
