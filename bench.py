@@ -1,0 +1,230 @@
+"""Benchmark driver (BASELINE.json metric: "requests/sec (whole node) + p50 latency, logistic
+/predict at batch=1/64").
+
+    python bench.py --gpus N --steps K --warmup W            # default: --mode serve
+    torchrun --nproc-per-node N bench.py --gpus N ...        # one rank per GPU (RCCL)
+
+serve (flagship, BASELINE config 1/4): every rank runs the full production stack on its GPU -
+native HTTP server -> batching engine -> fused fp64 HIP kernel -> JSON response - with the Iris
+LogisticRegression architecture (F=4 features, K=3 classes; random-init weights, seeded,
+broadcast from rank 0 over RCCL = collective C1), and a native closed-loop load generator with
+64 keep-alive connections ("batch=64": 64 concurrent single-row POST /predict requests).
+  step  = each of the 64 connections completes --reqs-per-conn (16) requests = 1024 requests/rank
+  value = whole-node requests/s = N * K * 1024 / max-over-ranks elapsed
+  p50/p99 at concurrency 64 come from the timed run; batch=1 latency (concurrency 1) is measured
+  afterwards on every rank and reported as extra fields.
+Other modes (extra evidence, not the headline): gemv (config 2: 1M x 256 bf16 binary predict),
+gemm (config 3: B=1024, F=256, K=1000 bf16 multiclass predict), train (config 5: binary LR
+mini-batch SGD, F=256 bf16, DP gradient all-reduce).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+# Reference numbers (measured on the reference itself, CPU, no published numbers):
+BASELINES = {
+    "serve": 1494.0,       # req/s, 1 uvicorn worker, concurrency 64
+    "gemv": 1.00e6,        # rows/s, sklearn binary 1M x 256 predict+proba
+    "gemm": 87075.0,       # rows/s, sklearn 1000-class B=1024 F=256
+    "train": 3.73e6,       # sample-gradients/s, sklearn lbfgs binary 100k x 256
+}
+IRIS_LABELS = ["Iris-setosa", "Iris-versicolor", "Iris-virginica"]
+
+
+def _sync(info):
+    import torch
+
+    if info.device is not None:
+        torch.cuda.synchronize(info.device)
+
+
+def _timed(info, fn):
+    """barrier + sync on both sides of fn(); returns max-over-ranks seconds."""
+    from mlapi_amd.parallel.comm import all_reduce_max, barrier
+
+    barrier(info)
+    _sync(info)
+    t0 = time.perf_counter()
+    out = fn()
+    _sync(info)
+    t1 = time.perf_counter()
+    barrier(info)
+    return all_reduce_max(t1 - t0, info), out
+
+
+def bench_serve(args, info):
+    from mlapi_amd._native import C
+    from mlapi_amd.models.linear import LinearModel
+    from mlapi_amd.parallel.comm import all_gather_floats, barrier, broadcast_model
+    from mlapi_amd.serve.server import NativeServer
+    from mlapi_amd.utils.config import Config
+
+    model = LinearModel.random(4, 3, seed=0, labels=IRIS_LABELS) if info.is_main else None
+    model = broadcast_model(model, info)  # C1 over RCCL
+    device = "cpu" if info.device is None else f"cuda:{info.device.index}"
+    cfg = Config.from_env(port=0, device=device, reload="off", missing_model="keep", io_threads=args.io_threads,
+                          max_batch=args.max_batch, model_path="/nonexistent/bench.pkl")
+    srv = NativeServer(cfg)
+    srv.runtime.handle.load(model)
+    srv.start()
+    body = json.dumps({"sepal_length": 5.1, "sepal_width": 3.5, "petal_length": 1.4, "petal_width": 0.2},
+                      separators=(",", ":")).encode()
+    req = (b"POST /predict HTTP/1.1\r\nHost: 127.0.0.1\r\nContent-Type: application/json\r\n"
+           b"Content-Length: %d\r\n\r\n%s" % (len(body), body)).decode()
+    try:
+        lg = C().Loadgen("127.0.0.1", srv.port, req, args.conns, args.client_threads, 60.0)
+        if args.warmup:
+            w = lg.run(args.warmup * args.reqs_per_conn, False)
+            if w["failed"]:
+                raise RuntimeError(f"warmup failed: {w}")
+        s0 = srv.runtime.handle.stats()
+        elapsed, res = _timed(info, lambda: lg.run(args.steps * args.reqs_per_conn, True))
+        s1 = srv.runtime.handle.stats()
+        lg.close()
+        if res["failed"] or res["status_counts"].get(200, 0) != args.steps * args.reqs_per_conn * args.conns:
+            raise RuntimeError(f"load generator saw errors: {res['status_counts']} failed={res['failed']}")
+        lat = res["latencies_ns"] / 1e6
+        # batch=1: one connection, closed loop
+        lg1 = C().Loadgen("127.0.0.1", srv.port, req, 1, 1, 60.0)
+        lg1.run(200, False)
+        r1 = lg1.run(args.c1_requests, True)
+        lg1.close()
+        lat1 = r1["latencies_ns"] / 1e6
+        per_rank = all_gather_floats([np.percentile(lat, 50), np.percentile(lat, 99), np.percentile(lat1, 50),
+                                      np.percentile(lat1, 99), r1["completed"] / r1["elapsed_s"],
+                                      (s1["requests"] - s0["requests"]) / max(1, s1["batches"] - s0["batches"])],
+                                     info)
+        barrier(info)
+    finally:
+        srv.stop()
+    total = info.world * args.steps * args.reqs_per_conn * args.conns
+    value = total / elapsed
+    extra = {
+        "p50_latency_ms_c64": float(np.max(per_rank[:, 0])),
+        "p99_latency_ms_c64": float(np.max(per_rank[:, 1])),
+        "p50_latency_ms_batch1": float(np.max(per_rank[:, 2])),
+        "p99_latency_ms_batch1": float(np.max(per_rank[:, 3])),
+        "req_per_s_batch1_per_rank": float(np.min(per_rank[:, 4])),
+        "mean_gpu_batch_rows": float(np.mean(per_rank[:, 5])),
+        "backend": srv.runtime.handle.backend,
+        "requests_per_step": args.reqs_per_conn * args.conns * info.world,
+        "baseline_note": "reference uvicorn+sklearn, 1 worker, c=64: 1494 req/s, p50 41.8 ms; c=1 p50 0.881 ms",
+    }
+    return ("requests_per_sec_whole_node", value, "req/s", elapsed, extra,
+            {"model": "sklearn LogisticRegression (Iris: F=4, K=3) via POST /predict", "global_batch": args.conns * info.world,
+             "seq_len": 1, "features": 4, "parallelism": f"dp{info.world}", "concurrency_per_gpu": args.conns})
+
+
+def bench_gemv(args, info):
+    import torch
+
+    from mlapi_amd.ops import linear as ops
+
+    B, F = args.rows, 256
+    g = torch.Generator(device=info.device).manual_seed(info.rank)
+    X = torch.randn(B, F, device=info.device, generator=g).to(torch.bfloat16)
+    w = (torch.randn(F, device=info.device, generator=g) / 16).to(torch.bfloat16)
+    idx = torch.empty(B, dtype=torch.int32, device=info.device)
+    p = torch.empty(B, dtype=torch.float32, device=info.device)
+    for _ in range(args.warmup):
+        ops.gemv_binary(X, w, 0.1)
+    elapsed, _ = _timed(info, lambda: [ops.gemv_binary(X, w, 0.1) for _ in range(args.steps)])
+    value = info.world * B * args.steps / elapsed
+    gbps = B * F * 2 * args.steps / (elapsed) / 1e9
+    return ("rows_per_sec_binary_predict", value, "rows/s", elapsed, {"hbm_GBps_per_gpu": gbps},
+            {"model": "binary LogisticRegression F=256", "global_batch": B * info.world, "seq_len": 1,
+             "features": F, "parallelism": f"dp{info.world}"})
+
+
+def bench_gemm(args, info):
+    import torch
+
+    from mlapi_amd.ops import linear as ops
+
+    B, F, K = args.batch, 256, 1000
+    g = torch.Generator(device=info.device).manual_seed(info.rank)
+    X = torch.randn(B, F, device=info.device, generator=g).to(torch.bfloat16)
+    W = (torch.randn(K, F, device=info.device, generator=g) / 16).to(torch.bfloat16)
+    b = torch.randn(K, device=info.device, generator=g) * 0.1
+    op = ops.GemmSoftmax(B, K, F, info.device)
+    out = (torch.empty(B, dtype=torch.int32, device=info.device), torch.empty(B, device=info.device))
+    for _ in range(args.warmup):
+        op(X, W, b, out=out)
+    elapsed, _ = _timed(info, lambda: [op(X, W, b, out=out) for _ in range(args.steps)])
+    value = info.world * B * args.steps / elapsed
+    tflops = 2 * B * F * K * args.steps / elapsed / 1e12
+    return ("rows_per_sec_softmax_predict", value, "rows/s", elapsed, {"tflops_per_gpu": tflops},
+            {"model": "softmax regression F=256 K=1000", "global_batch": B * info.world, "seq_len": 1,
+             "features": F, "parallelism": f"dp{info.world}"})
+
+
+def bench_train(args, info):
+    from mlapi_amd.train.sgd import BinarySGDTrainer, synthetic_binary
+
+    F = 256
+    X, y = synthetic_binary(args.train_batch * args.shards, F, seed=1234 + info.rank, device=info.device)
+    tr = BinarySGDTrainer(F, info=info, lr=0.5, l2=1e-4, device=info.device)
+    nb = args.shards
+
+    def run(n):
+        for s in range(n):
+            j = s % nb
+            tr.step(X[j * args.train_batch:(j + 1) * args.train_batch], y[j * args.train_batch:(j + 1) * args.train_batch])
+
+    run(args.warmup)
+    elapsed, _ = _timed(info, lambda: run(args.steps))
+    value = info.world * args.train_batch * args.steps / elapsed
+    return ("train_samples_per_sec", value, "samples/s", elapsed, {"final_loss": tr.last_loss()},
+            {"model": "binary LogisticRegression F=256 (mini-batch SGD)", "global_batch": args.train_batch * info.world,
+             "seq_len": 1, "features": F, "parallelism": f"dp{info.world}"})
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--mode", default="serve", choices=["serve", "gemv", "gemm", "train"])
+    ap.add_argument("--conns", type=int, default=64)
+    ap.add_argument("--reqs-per-conn", type=int, default=16)
+    ap.add_argument("--client-threads", type=int, default=3)
+    ap.add_argument("--io-threads", type=int, default=3)
+    ap.add_argument("--max-batch", type=int, default=256)
+    ap.add_argument("--c1-requests", type=int, default=3000)
+    ap.add_argument("--rows", type=int, default=1 << 20)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--train-batch", type=int, default=1 << 16)
+    ap.add_argument("--shards", type=int, default=8)
+    ap.add_argument("--cpu", action="store_true", help="force the CPU backend (testing without a GPU)")
+    args = ap.parse_args(argv)
+
+    from mlapi_amd.parallel.comm import init_distributed, shutdown
+
+    info = init_distributed(use_gpu=False if args.cpu else None)
+    if args.mode != "serve" and info.device is None:
+        print(f"mode {args.mode} needs a GPU", file=sys.stderr)
+        return 2
+    fn = {"serve": bench_serve, "gemv": bench_gemv, "gemm": bench_gemm, "train": bench_train}[args.mode]
+    metric, value, unit, elapsed, extra, config = fn(args, info)
+    if info.is_main:
+        line = {
+            "metric": metric, "value": value, "unit": unit, "n_gpus": info.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": value / BASELINES[args.mode],
+            "dtype": "fp64" if args.mode == "serve" else "bf16",
+            "data": "synthetic (random-init weights, fixed synthetic inputs)", "config": config,
+        }
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    shutdown(info)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

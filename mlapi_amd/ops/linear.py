@@ -1,0 +1,160 @@
+"""torch-facing wrappers of the HIP kernels (csrc/kernels/*.hip).
+
+Every op takes device tensors and launches on ``torch.cuda.current_stream()``; there is no
+silent CPU / PyTorch fallback: a CPU tensor or a missing extension raises. Pure-PyTorch oracles
+for tests live in :mod:`mlapi_amd.ops.reference`.
+
+Dispatch for ``predict`` (the reference's ``predict`` + ``predict_proba().max()``,
+`main.py:21-22`):
+  * f64 / f32 inputs with small F, K  -> ``linear_small`` (fused, one row per lane);
+  * binary (K == 1) bf16 / f32        -> ``gemv_binary`` (HBM-streaming GEMV + sigmoid);
+  * multiclass bf16                   -> ``gemm_softmax`` (MFMA + online softmax/argmax).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from mlapi_amd._native import C
+from mlapi_amd.models.linear import Kind
+
+_DT = {torch.float64: 0, torch.float32: 1, torch.bfloat16: 2}
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check(*ts: torch.Tensor) -> None:
+    for t in ts:
+        if not isinstance(t, torch.Tensor) or not t.is_cuda:
+            raise ValueError("mlapi_amd.ops: inputs must be GPU tensors (no CPU fallback)")
+        if not t.is_contiguous():
+            raise ValueError("mlapi_amd.ops: inputs must be contiguous")
+
+
+def linear_small(X: torch.Tensor, W: torch.Tensor, b: torch.Tensor, kind: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Fused z = X W^T + b -> (int32 label index, p_max) in X's dtype (f64 or f32)."""
+    _check(X, W, b)
+    if X.dtype not in (torch.float64, torch.float32) or W.dtype != X.dtype or b.dtype != X.dtype:
+        raise TypeError("linear_small: X, W, b must share dtype f64 or f32")
+    B, F = X.shape
+    K = W.shape[0]
+    if W.shape[1] != F or b.numel() != K:
+        raise ValueError("linear_small: shape mismatch")
+    idx = torch.empty(B, dtype=torch.int32, device=X.device)
+    p = torch.empty(B, dtype=X.dtype, device=X.device)
+    C().linear_small(_DT[X.dtype], X.data_ptr(), F, W.data_ptr(), b.data_ptr(), B, F, K, int(kind), idx.data_ptr(),
+                     p.data_ptr(), _stream())
+    return idx, p
+
+
+def gemv_binary(X: torch.Tensor, w: torch.Tensor, bias: float, kind: int = Kind.BINARY):
+    """Binary LR over a large batch: (int32 z>0, f32 sigmoid(|z|)). X: [B, F] bf16/f32."""
+    _check(X, w)
+    if X.dtype not in (torch.bfloat16, torch.float32) or w.dtype != X.dtype:
+        raise TypeError("gemv_binary: X and w must share dtype bf16 or f32")
+    B, F = X.shape
+    if w.numel() != F:
+        raise ValueError("gemv_binary: w must have F entries")
+    idx = torch.empty(B, dtype=torch.int32, device=X.device)
+    p = torch.empty(B, dtype=torch.float32, device=X.device)
+    C().gemv_binary(_DT[X.dtype], X.data_ptr(), w.data_ptr(), float(bias), B, F, int(kind), idx.data_ptr(),
+                    p.data_ptr(), _stream())
+    return idx, p
+
+
+class GemmSoftmax:
+    """Multiclass predict with a cached workspace (capture-safe launches after construction)."""
+
+    def __init__(self, max_batch: int, n_classes: int, n_features: int, device):
+        self.max_batch, self.K, self.F = max_batch, n_classes, n_features
+        nbytes = C().gemm_softmax_workspace(max_batch, n_classes, n_features)
+        self.ws = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
+
+    def __call__(self, X, W, b, kind: int = Kind.MULTINOMIAL, out=None):
+        _check(X, W, b)
+        if X.dtype != torch.bfloat16 or W.dtype != torch.bfloat16 or b.dtype != torch.float32:
+            raise TypeError("gemm_softmax: X, W bf16 and b f32")
+        B, F = X.shape
+        K = W.shape[0]
+        if F % 32 or F > 512 or W.shape[1] != F or b.numel() != K:
+            raise ValueError("gemm_softmax: need F % 32 == 0, F <= 512 and matching W/b")
+        need = C().gemm_softmax_workspace(B, K, F)
+        if need > self.ws.numel():
+            self.ws = torch.empty(need, dtype=torch.uint8, device=X.device)
+        if out is None:
+            out = (torch.empty(B, dtype=torch.int32, device=X.device), torch.empty(B, dtype=torch.float32, device=X.device))
+        idx, p = out
+        C().gemm_softmax(X.data_ptr(), W.data_ptr(), b.data_ptr(), B, F, K, int(kind), idx.data_ptr(), p.data_ptr(),
+                         self.ws.data_ptr(), self.ws.numel(), _stream())
+        return idx, p
+
+
+def gemm_softmax(X, W, b, kind: int = Kind.MULTINOMIAL):
+    return GemmSoftmax(X.shape[0], W.shape[0], X.shape[1], X.device)(X, W, b, kind)
+
+
+def gemm_logits(X, W, b) -> torch.Tensor:
+    _check(X, W, b)
+    B, F = X.shape
+    K = W.shape[0]
+    Z = torch.empty(B, K, dtype=torch.float32, device=X.device)
+    C().gemm_logits(X.data_ptr(), W.data_ptr(), b.data_ptr(), B, F, K, Z.data_ptr(), _stream())
+    return Z
+
+
+def predict(X: torch.Tensor, W: torch.Tensor, b: torch.Tensor, kind: int):
+    """Dispatching predict: returns (int32 index, p_max)."""
+    K, F = W.shape
+    if X.dtype in (torch.float64,) or (X.dtype == torch.float32 and F <= 32 and K <= 16):
+        return linear_small(X, W.to(X.dtype).contiguous(), b.to(X.dtype).contiguous(), kind)
+    if K == 1:
+        return gemv_binary(X, W.reshape(-1).to(X.dtype).contiguous(), float(b.reshape(-1)[0]), kind)
+    return gemm_softmax(X.to(torch.bfloat16).contiguous(), W.to(torch.bfloat16).contiguous(),
+                        b.to(torch.float32).contiguous(), kind)
+
+
+# ------------------------------------------------------------------------------------------ train
+def train_binary_grad(X: torch.Tensor, y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, ws: torch.Tensor = None,
+                      out: torch.Tensor = None) -> torch.Tensor:
+    """Sums over the batch: out = [dL/dw (F) | dL/db | loss_sum | n_correct] (f32)."""
+    _check(X, y, w, b)
+    B, F = X.shape
+    if ws is None:
+        ws = torch.empty(C().train_binary_workspace(B, F), dtype=torch.uint8, device=X.device)
+    if out is None:
+        out = torch.empty(F + 3, dtype=torch.float32, device=X.device)
+    C().train_binary_grad(_DT[X.dtype], X.data_ptr(), y.data_ptr(), w.data_ptr(), b.data_ptr(), B, F, out.data_ptr(),
+                          ws.data_ptr(), ws.numel(), _stream())
+    return out
+
+
+def train_small_grad(X: torch.Tensor, y: torch.Tensor, W: torch.Tensor, b: torch.Tensor, kind: int,
+                     ws: torch.Tensor = None, out: torch.Tensor = None) -> torch.Tensor:
+    """out = [dL/dW (K*F row-major) | dL/db (K) | loss_sum | n_correct] in X's dtype (f64/f32)."""
+    _check(X, y, W, b)
+    B, F = X.shape
+    K = W.shape[0]
+    if ws is None:
+        ws = torch.empty(C().train_small_workspace(B, F, K), dtype=torch.uint8, device=X.device)
+    if out is None:
+        out = torch.empty(K * F + K + 2, dtype=X.dtype, device=X.device)
+    C().train_small_grad(_DT[X.dtype], X.data_ptr(), y.data_ptr(), W.data_ptr(), b.data_ptr(), B, F, K, int(kind),
+                         out.data_ptr(), ws.data_ptr(), ws.numel(), _stream())
+    return out
+
+
+def sgd_update(params: torch.Tensor, grad: torch.Tensor, n_penalized: int, lr: float, inv_n: float, l2: float,
+               momentum: float = 0.0, mom_buf: torch.Tensor = None) -> None:
+    _check(params, grad)
+    C().sgd_update(params.data_ptr(), grad.data_ptr(), 0 if mom_buf is None else mom_buf.data_ptr(), params.numel(),
+                   n_penalized, float(lr), float(inv_n), float(l2), float(momentum), _stream())
+
+
+def cast(src: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    _check(src)
+    dst = torch.empty(src.shape, dtype=dtype, device=src.device)
+    C().cast(_DT[src.dtype], src.data_ptr(), _DT[dtype], dst.data_ptr(), src.numel(), _stream())
+    return dst

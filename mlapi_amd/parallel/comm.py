@@ -1,0 +1,137 @@
+"""Process-group setup and the framework's collectives (RCCL over xGMI via torch.distributed).
+
+One process per GPU. On ROCm the ``"nccl"`` backend of torch.distributed IS RCCL; CPU tests use
+``"gloo"`` with the same code. Collectives used by the framework:
+
+* C1 ``broadcast_model`` - rank 0's checkpoint to every replica at startup and on reload: the
+  (kind, K, F, n_classes) header and the label JSON go first (tiny), then W|b packed into ONE
+  flat float64 buffer so the weights cross xGMI in a single broadcast;
+* C2 ``all_reduce_sum`` of the fused gradient buffer [gW | gb | loss | n_correct] per training
+  step (C3 - the loss/accuracy scalars - piggyback on the same buffer);
+* C4 ``barrier``.
+
+All messages are <= ~1 MiB, i.e. latency-bound on xGMI: one fused buffer per step, never one
+collective per tensor.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from mlapi_amd.models.linear import Kind, LinearModel
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: Optional[torch.device] = None  # None -> CPU
+    backend: str = "none"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None) -> DistInfo:
+    """Initialise from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); no-op for 1 process."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available() and torch.cuda.device_count() > 0
+    device = None
+    if use_gpu:
+        device = torch.device("cuda", local_rank % torch.cuda.device_count())
+        torch.cuda.set_device(device)
+    info = DistInfo(rank, world, local_rank, device, "none")
+    if world > 1:
+        if not dist.is_initialized():
+            backend = backend or ("nccl" if use_gpu else "gloo")
+            kw = {"device_id": device} if backend == "nccl" else {}
+            dist.init_process_group(backend=backend, **kw)
+        info.backend = dist.get_backend()
+    return info
+
+
+def _coll_device(info: DistInfo) -> torch.device:
+    return info.device if (info.backend == "nccl" and info.device is not None) else torch.device("cpu")
+
+
+def barrier(info: DistInfo) -> None:
+    if info.world > 1:
+        if info.backend == "nccl":
+            dist.barrier(device_ids=[info.device.index])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(value: float, info: DistInfo) -> float:
+    if info.world == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=_coll_device(info))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_gather_floats(values, info: DistInfo) -> np.ndarray:
+    t = torch.tensor(list(values), dtype=torch.float64, device=_coll_device(info))
+    if info.world == 1:
+        return t.cpu().numpy()[None, :]
+    out = [torch.empty_like(t) for _ in range(info.world)]
+    dist.all_gather(out, t)
+    return torch.stack(out).cpu().numpy()
+
+
+def all_reduce_sum_(t: torch.Tensor, info: DistInfo) -> torch.Tensor:
+    """In-place sum over ranks (C2). ``t`` must live on the collective's device."""
+    if info.world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
+def _broadcast_bytes(payload: Optional[bytes], info: DistInfo, src: int = 0) -> bytes:
+    dev = _coll_device(info)
+    n = torch.tensor([len(payload) if payload is not None else 0], dtype=torch.int64, device=dev)
+    dist.broadcast(n, src)
+    buf = torch.empty(int(n.item()), dtype=torch.uint8, device=dev)
+    if info.rank == src:
+        buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
+    dist.broadcast(buf, src)
+    return bytes(buf.cpu().numpy().tobytes())
+
+
+def broadcast_model(model: Optional[LinearModel], info: DistInfo, src: int = 0) -> LinearModel:
+    """C1: replicate ``model`` from ``src`` to every rank (RCCL broadcast over xGMI on GPUs)."""
+    if info.world == 1:
+        assert model is not None
+        return model
+    header = None
+    if info.rank == src:
+        header = json.dumps({
+            "kind": int(model.kind), "K": model.n_outputs, "F": model.n_features,
+            "classes": model.classes.tolist(),
+            "classes_dtype": "object" if model.classes.dtype == object else model.classes.dtype.str,
+        }).encode()
+    h = json.loads(_broadcast_bytes(header, info, src))
+    K, F = h["K"], h["F"]
+    dev = _coll_device(info)
+    flat = torch.empty(K * F + K, dtype=torch.float64, device=dev)
+    if info.rank == src:
+        flat.copy_(torch.from_numpy(np.concatenate([model.W.reshape(-1), model.b])))
+    dist.broadcast(flat, src)  # the one weight collective
+    arr = flat.cpu().numpy()
+    classes = np.array(h["classes"], dtype=object if h["classes_dtype"] == "object" else np.dtype(h["classes_dtype"]))
+    return LinearModel(arr[:K * F].reshape(K, F), arr[K * F:], classes, Kind(h["kind"]))
+
+
+def shutdown(info: DistInfo) -> None:
+    if info.world > 1 and dist.is_initialized():
+        dist.destroy_process_group()

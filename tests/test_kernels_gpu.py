@@ -1,0 +1,176 @@
+"""T3: every HIP kernel vs a plain PyTorch fp64/fp32 reference of the same op."""
+import numpy as np
+import pytest
+import torch
+
+from mlapi_amd.models.linear import Kind
+from mlapi_amd.ops import linear as ops
+from mlapi_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _rand(shape, dtype, seed, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(shape, generator=g, dtype=torch.float64) * scale).to(dtype).to(DEV)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("kind,K", [(Kind.BINARY, 1), (Kind.BINARY_SOFTMAX, 1), (Kind.MULTINOMIAL, 3),
+                                    (Kind.OVR, 3), (Kind.MULTINOMIAL, 16), (Kind.OVR, 7)])
+@pytest.mark.parametrize("B,F", [(1, 4), (64, 4), (1000, 4), (333, 31)])
+def test_linear_small(dtype, kind, K, B, F):
+    X, W, b = _rand((B, F), dtype, 1), _rand((K, F), dtype, 2), _rand((K,), dtype, 3)
+    idx, p = ops.linear_small(X, W, b, kind)
+    ridx, rp = ref.predict_ref(X, W, b, kind)
+    torch.cuda.synchronize()
+    tol = 1e-12 if dtype == torch.float64 else 2e-6
+    assert torch.equal(idx.cpu(), ridx.cpu())
+    torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=tol, atol=tol)
+
+
+def test_linear_generic_wide():
+    X, W, b = _rand((257, 100), torch.float64, 4), _rand((40, 100), torch.float64, 5), _rand((40,), torch.float64, 6)
+    for kind in (Kind.MULTINOMIAL, Kind.OVR):
+        idx, p = ops.linear_small(X, W, b, kind)
+        ridx, rp = ref.predict_ref(X, W, b, kind)
+        assert torch.equal(idx.cpu(), ridx.cpu())
+        torch.testing.assert_close(p.cpu(), rp.cpu(), rtol=1e-12, atol=1e-12)
+
+
+def test_linear_small_iris_parity(iris_sklearn_model, iris_data):
+    """fp64 GPU path reproduces sklearn's predict / predict_proba().max() (main.py:21-22)."""
+    m = iris_sklearn_model
+    _, Xte, _, yte = iris_data
+    X = torch.tensor(Xte, device=DEV)
+    W = torch.tensor(m.coef_, device=DEV)
+    b = torch.tensor(m.intercept_, device=DEV)
+    idx, p = ops.linear_small(X, W, b, Kind.MULTINOMIAL)
+    pred = m.classes_[idx.cpu().numpy()]
+    np.testing.assert_array_equal(pred, m.predict(Xte))
+    np.testing.assert_allclose(p.cpu().numpy(), m.predict_proba(Xte).max(1), rtol=1e-14, atol=0)
+    assert np.mean(pred == yte) == pytest.approx(0.9666666666666667, abs=0)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,F", [(1, 256), (17, 256), (4099, 256), (1000, 64), (513, 128), (300, 1024), (77, 8)])
+@pytest.mark.parametrize("kind", [Kind.BINARY, Kind.BINARY_SOFTMAX])
+def test_gemv_binary(dtype, B, F, kind):
+    if dtype == torch.float32 and F == 8:
+        F = 8
+    X, w = _rand((B, F), dtype, 7), _rand((F,), dtype, 8, scale=1 / np.sqrt(F))
+    bias = 0.125
+    idx, p = ops.gemv_binary(X, w, bias, kind)
+    z = X.double() @ w.double() + bias
+    ridx = (z > 0).to(torch.int32)
+    rp = torch.sigmoid(z.abs() * (2 if kind == Kind.BINARY_SOFTMAX else 1))
+    torch.cuda.synchronize()
+    near = z.abs() < 1e-4  # sign of a near-zero logit may flip under f32 accumulation
+    assert torch.equal(idx[~near].cpu(), ridx[~near].cpu())
+    torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=1e-5, atol=1e-5)
+
+
+def test_gemv_binary_large_stream():
+    B, F = 1 << 20, 256
+    X = torch.randn(B, F, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(F, device=DEV) / 16).to(torch.bfloat16)
+    idx, p = ops.gemv_binary(X, w, -0.5)
+    z = X.float() @ w.float() - 0.5
+    near = z.abs() < 1e-3
+    assert torch.equal(idx[~near], (z > 0).to(torch.int32)[~near])
+    torch.testing.assert_close(p, torch.sigmoid(z.abs()), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("B,F,K", [(1024, 256, 1000), (1, 256, 1000), (130, 64, 10), (2048, 128, 37),
+                                   (4096, 256, 3), (100, 512, 200), (37, 32, 65)])
+@pytest.mark.parametrize("kind", [Kind.MULTINOMIAL, Kind.OVR])
+def test_gemm_softmax(B, F, K, kind):
+    X = _rand((B, F), torch.bfloat16, 9)
+    W = _rand((K, F), torch.bfloat16, 10, scale=1 / np.sqrt(F))
+    b = _rand((K,), torch.float32, 11, scale=0.1)
+    idx, p = ops.gemm_softmax(X, W, b, kind)
+    Z = ref.logits_ref(X, W, b, dtype=torch.float64)
+    ridx, rp = ref.predict_ref(X, W, b, kind)
+    top2 = torch.topk(Z, min(2, K), dim=1).values
+    clear = (top2[:, 0] - top2[:, -1]) > 1e-3 if K > 1 else torch.ones(B, dtype=torch.bool, device=DEV)
+    torch.cuda.synchronize()
+    assert torch.equal(idx[clear].cpu(), ridx[clear].cpu())
+    torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=2e-4, atol=2e-5)
+
+
+def test_gemm_logits_asymmetric():
+    """A = I-style check with an asymmetric operand: catches a transposed C write (guide S3)."""
+    B, F, K = 64, 64, 48
+    X = torch.zeros(B, F, device=DEV, dtype=torch.bfloat16)
+    X[torch.arange(B), torch.arange(B) % F] = 1
+    W = (torch.arange(K * F, device=DEV, dtype=torch.float32).reshape(K, F) % 13 - 6).to(torch.bfloat16)
+    b = torch.arange(K, device=DEV, dtype=torch.float32) * 0.5
+    Z = ops.gemm_logits(X, W, b)
+    torch.testing.assert_close(Z, ref.logits_ref(X, W, b), rtol=0, atol=0)
+
+
+def test_gemm_ties_first_max():
+    B, F, K = 256, 32, 130
+    X = torch.ones(B, F, device=DEV, dtype=torch.bfloat16)
+    W = torch.zeros(K, F, device=DEV, dtype=torch.bfloat16)
+    b = torch.zeros(K, device=DEV)
+    b[[5, 77, 129]] = 1.0  # three-way tie for the max
+    idx, p = ops.gemm_softmax(X, W, b)
+    assert (idx == 5).all()
+    torch.testing.assert_close(p, torch.full_like(p, float(torch.softmax(b.double(), 0).max())), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,F", [(1, 256), (5000, 256), (1 << 16, 256), (999, 64), (333, 1024)])
+def test_train_binary_grad(dtype, B, F):
+    X = _rand((B, F), dtype, 12)
+    y = (torch.rand(B, device=DEV) > 0.5).float()
+    w = _rand((F,), torch.float32, 13, scale=0.05)
+    b = torch.tensor([0.1], device=DEV)
+    out = ops.train_binary_grad(X, y, w, b)
+    r = ref.train_binary_ref(X, y, w, b)
+    torch.testing.assert_close(out.double().cpu(), r.cpu(), rtol=2e-4, atol=2e-3 * max(1.0, np.sqrt(B) / 30))
+    out2 = ops.train_binary_grad(X, y, w, b)
+    assert torch.equal(out, out2), "gradient must be bitwise deterministic"
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("kind,K", [(Kind.MULTINOMIAL, 3), (Kind.BINARY, 1), (Kind.BINARY_SOFTMAX, 1),
+                                    (Kind.OVR, 3), (Kind.MULTINOMIAL, 16)])
+@pytest.mark.parametrize("B,F", [(120, 4), (5000, 10), (64, 64)])
+def test_train_small_grad(dtype, kind, K, B, F):
+    if K * F > 1024:
+        pytest.skip("outside train_small range")
+    X = _rand((B, F), dtype, 14)
+    W = _rand((K, F), dtype, 15, scale=0.3)
+    b = _rand((K,), dtype, 16, scale=0.3)
+    ncls = 2 if K == 1 else K
+    y = torch.randint(0, ncls, (B,), device=DEV, dtype=torch.int32)
+    out = ops.train_small_grad(X, y, W, b, kind)
+    r = ref.train_small_ref(X, y, W, b, kind)
+    tol = 1e-10 if dtype == torch.float64 else 3e-4
+    torch.testing.assert_close(out.double().cpu(), r.cpu(), rtol=tol, atol=tol * max(1, B / 100))
+
+
+def test_sgd_update():
+    p = torch.randn(1001, device=DEV)
+    g = torch.randn(1001, device=DEV)
+    exp = p.clone()
+    exp[:1000] -= 0.1 * (g[:1000] / 8 + 0.01 * exp[:1000])
+    exp[1000:] -= 0.1 * g[1000:] / 8
+    ops.sgd_update(p, g, 1000, 0.1, 1 / 8, 0.01)
+    torch.testing.assert_close(p, exp)
+
+
+@pytest.mark.parametrize("src,dst", [(torch.float64, torch.float32), (torch.float32, torch.bfloat16),
+                                     (torch.bfloat16, torch.float32), (torch.float64, torch.bfloat16)])
+def test_cast(src, dst):
+    x = _rand((4097,), src, 17, scale=100)
+    torch.testing.assert_close(ops.cast(x, dst), x.to(dst), rtol=0, atol=0)
+
+
+def test_ops_reject_cpu_tensors():
+    with pytest.raises(ValueError):
+        ops.linear_small(torch.zeros(2, 4, dtype=torch.float64), torch.zeros(3, 4, dtype=torch.float64),
+                         torch.zeros(3, dtype=torch.float64), Kind.MULTINOMIAL)
