@@ -212,14 +212,50 @@ __global__ __launch_bounds__(256) void train_binary_grad_kernel(const T* __restr
   }
 }
 
+// Deterministic slab reduction: 32 columns x 8 partitions per 256-thread block. Partition p sums
+// slabs p, p+8, p+16, ... in increasing order (each wave-row reads 32 consecutive columns = one
+// coalesced 128-B segment per slab), then the 8 partials are added in fixed order through LDS.
+// A single thread per column walking all slabs serially was the bottleneck of the training step
+// (232 us vs 22 us for the fused gradient kernel: profiles/r1_first/train_kernel_stats.csv).
+constexpr int RED_COLS = 32;
+constexpr int RED_PARTS = 8;
 template <typename T>
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(const T* __restrict__ slabs, int nslabs, int width,
                                                            T* __restrict__ out) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= width) return;
+  __shared__ T part[RED_PARTS][RED_COLS];
+  const int c = threadIdx.x % RED_COLS;
+  const int p = threadIdx.x / RED_COLS;
+  const int j = blockIdx.x * RED_COLS + c;
   T s = T(0);
-  for (int i = 0; i < nslabs; ++i) s += slabs[(int64_t)i * width + j];
-  out[j] = s;
+  if (j < width) {
+    int i = p;
+    for (; i + 3 * RED_PARTS < nslabs; i += 4 * RED_PARTS) {  // 4 independent loads in flight
+      const T a0 = slabs[(int64_t)i * width + j];
+      const T a1 = slabs[(int64_t)(i + RED_PARTS) * width + j];
+      const T a2 = slabs[(int64_t)(i + 2 * RED_PARTS) * width + j];
+      const T a3 = slabs[(int64_t)(i + 3 * RED_PARTS) * width + j];
+      s += a0;
+      s += a1;
+      s += a2;
+      s += a3;
+    }
+    for (; i < nslabs; i += RED_PARTS) s += slabs[(int64_t)i * width + j];
+  }
+  part[p][c] = s;
+  __syncthreads();
+  if (p == 0 && j < width) {
+    T t = part[0][c];
+#pragma unroll
+    for (int q = 1; q < RED_PARTS; ++q) t += part[q][c];
+    out[j] = t;
+  }
+}
+
+template <typename T>
+void launch_reduce_slabs(const T* slabs, int nslabs, int width, T* out, hipStream_t stream) {
+  hipLaunchKernelGGL(reduce_slabs_kernel<T>, dim3((unsigned)((width + RED_COLS - 1) / RED_COLS)), dim3(256), 0,
+                     stream, slabs, nslabs, width, out);
+  MLAPI_HIP_CHECK(hipGetLastError());
 }
 
 struct BinPlan {
@@ -238,7 +274,7 @@ BinPlan bin_plan(int chunks) {
 
 int64_t bin_blocks(int64_t B, const BinPlan& p) {
   int64_t blocks = (B + p.rows_per_block - 1) / p.rows_per_block;
-  const int64_t cap = 256 * 4;
+  const int64_t cap = 256 * 2;  // 2 blocks per CU: enough bytes in flight, few slabs to reduce
   return blocks < 1 ? 1 : (blocks > cap ? cap : blocks);
 }
 
@@ -447,9 +483,7 @@ void launch_train_binary_grad(int dt, const void* X, const float* y, const float
 #undef MLAPI_TB_ALL
 #undef MLAPI_TB
   MLAPI_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(reduce_slabs_kernel<float>, dim3((unsigned)((F + 3 + 255) / 256)), dim3(256), 0, stream,
-                     slabs, (int)blocks, F + 3, out);
-  MLAPI_HIP_CHECK(hipGetLastError());
+  launch_reduce_slabs<float>(slabs, (int)blocks, F + 3, out, stream);
 }
 
 size_t train_small_workspace(int64_t B, int F, int K) {
@@ -470,15 +504,15 @@ void launch_train_small_grad(int dt, const void* X, const int32_t* y, const void
                        static_cast<const double*>(X), y, static_cast<const double*>(W),
                        static_cast<const double*>(b), B, F, K, kind, static_cast<double*>(workspace));
     MLAPI_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(reduce_slabs_kernel<double>, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, stream,
-                       static_cast<const double*>(workspace), (int)blocks, width, static_cast<double*>(out));
+    launch_reduce_slabs<double>(static_cast<const double*>(workspace), (int)blocks, width, static_cast<double*>(out),
+                                stream);
   } else if (dt == DT_F32) {
     hipLaunchKernelGGL(train_small_grad_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, stream,
                        static_cast<const float*>(X), y, static_cast<const float*>(W), static_cast<const float*>(b),
                        B, F, K, kind, static_cast<float*>(workspace));
     MLAPI_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(reduce_slabs_kernel<float>, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, stream,
-                       static_cast<const float*>(workspace), (int)blocks, width, static_cast<float*>(out));
+    launch_reduce_slabs<float>(static_cast<const float*>(workspace), (int)blocks, width, static_cast<float*>(out),
+                               stream);
   } else {
     throw std::invalid_argument("train_small: dtype must be f64 or f32");
   }

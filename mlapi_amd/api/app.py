@@ -18,6 +18,7 @@ Extra routes (excluded from the OpenAPI schema so it stays identical): ``/health
 Error behaviour follows the reference: validation errors are FastAPI's 422 bodies, any failure
 in the model path is an HTTP 500 ``Internal Server Error`` (text/plain).
 """
+import contextlib
 import io
 import logging
 import math
@@ -34,9 +35,9 @@ from mlapi_amd.utils.config import IRIS_FEATURES, Config
 log = logging.getLogger("mlapi_amd.api")
 
 
+# Request schema of `POST /predict` (`main.py:10-14`). No docstring on purpose: pydantic would
+# publish it as the schema "description" and /openapi.json would no longer match the reference.
 class IrisSpecies(BaseModel):
-    """Request schema of `POST /predict` (`main.py:10-14`)."""
-
     sepal_length: float
     sepal_width: float
     petal_length: float
@@ -77,20 +78,22 @@ def _missing(name: str) -> dict:
 
 
 def dataframe_payload(df, strict_parity: bool = True):
-    """``jsonable_encoder(df)`` as the reference sees it: ``dict(df)`` -> {col: {row: value}}.
+    """``jsonable_encoder(df)`` as the reference sees it: ``dict(df)`` -> {col: dict(series)}.
 
-    With ``strict_parity`` (default) cells that FastAPI cannot encode (numpy ints / bools, NaN)
-    raise -> HTTP 500, exactly like the reference. Otherwise they are converted.
+    ``dict(series)`` yields numpy scalars, exactly what FastAPI's encoder receives in the reference:
+    numpy ints / bools are not JSON-encodable and NaN is rejected by ``json.dumps(allow_nan=False)``,
+    so with ``strict_parity`` (default) those cells raise -> HTTP 500 like the reference.
+    Otherwise they are converted (ints/bools to JSON numbers/booleans, NaN to null).
     """
     import numpy as np
 
     out = {}
-    for col in df.columns:
+    for col, series in dict(df).items():
         colmap = {}
-        for idx, v in df[col].items():
-            if isinstance(v, (np.bool_, bool)) or (isinstance(v, np.integer)):
+        for idx, v in dict(series).items():
+            if isinstance(v, (np.bool_, np.integer)):
                 if strict_parity:
-                    raise ValueError(f"{type(v)} is not JSON serializable")
+                    raise ValueError(f"{type(v).__name__} is not JSON serializable")
                 v = v.item()
             elif isinstance(v, float) and not math.isfinite(v):
                 if strict_parity:
@@ -98,8 +101,8 @@ def dataframe_payload(df, strict_parity: bool = True):
                 v = None
             elif isinstance(v, np.generic):
                 v = v.item()
-            colmap[idx if not isinstance(idx, np.generic) else idx.item()] = v
-        out[col if not isinstance(col, np.generic) else col.item()] = colmap
+            colmap[idx.item() if isinstance(idx, np.generic) else idx] = v
+        out[col.item() if isinstance(col, np.generic) else col] = colmap
     return out
 
 
@@ -107,7 +110,16 @@ def create_app(config: Optional[Config] = None, *, runtime=None) -> FastAPI:
     """Build the app. ``runtime`` is a :class:`mlapi_amd.serve.service.ServingRuntime`; when
     omitted one is created lazily from ``config`` on first use (so `uvicorn main:app` works)."""
     config = config or Config.from_env()
-    app = FastAPI()  # no title/version: OpenAPI info stays {"title": "FastAPI", "version": "0.1.0"}
+    @contextlib.asynccontextmanager
+    async def lifespan(_app):
+        yield
+        r = _app.state.runtime
+        if r is not None and getattr(r, "owned_by_app", False):  # uvicorn main:app owns its runtime
+            r.close()
+            _app.state.runtime = None
+
+    # no title/version: OpenAPI info stays {"title": "FastAPI", "version": "0.1.0"} like the reference
+    app = FastAPI(lifespan=lifespan)
     app.state.config = config
     app.state.runtime = runtime
     Record = request_model(config.feature_names)
@@ -196,10 +208,5 @@ def create_app(config: Optional[Config] = None, *, runtime=None) -> FastAPI:
         return schema
 
     app.openapi = openapi  # type: ignore[method-assign]
-
-    @app.on_event("shutdown")
-    async def _shutdown():  # pragma: no cover - exercised by uvicorn
-        if app.state.runtime is not None and getattr(app.state.runtime, "owned_by_app", False):
-            app.state.runtime.close()
 
     return app

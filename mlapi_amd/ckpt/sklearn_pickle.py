@@ -102,6 +102,31 @@ def _safe_reconstructor(cls, base, state):
     return copyreg._reconstructor(cls, base, state)
 
 
+def _safe_codecs_encode(obj, encoding="utf-8"):
+    """Protocol-2 pickles store numpy array bytes as ``_codecs.encode(str, 'latin1')``."""
+    if not isinstance(obj, str) or encoding not in ("latin1", "latin-1", "utf-8", "utf8"):
+        raise UnsafeCheckpointError("_codecs.encode with unexpected arguments")
+    return obj.encode(encoding)
+
+
+class _InertLoss:
+    """Stand-in for sklearn's Cython loss objects inside SGDClassifier pickles (inert data)."""
+
+    def __init__(self, *args, **kwargs):
+        self.args = args
+
+    def __setstate__(self, state):
+        pass
+
+
+def _safe_frombuffer(buf, dtype, shape, order):
+    dtype = np.dtype(dtype)
+    if dtype.hasobject:
+        raise UnsafeCheckpointError("object arrays cannot come from a raw buffer")
+    arr = np.frombuffer(buf, dtype=dtype)
+    return arr.reshape(shape, order=order).copy()
+
+
 class SafeUnpickler(pickle.Unpickler):
     """``pickle.Unpickler`` whose ``find_class`` only resolves the allow-list above."""
 
@@ -114,14 +139,21 @@ class SafeUnpickler(pickle.Unpickler):
                 return _np_reconstruct()
             if name == "scalar":
                 return _np_scalar()
+        if (module in ("_loss", "sklearn._loss._loss", "sklearn.linear_model._sgd_fast",
+                       "sklearn.linear_model.sgd_fast") and name.isidentifier()):
+            return _InertLoss  # SGDClassifier's Cython loss object: never used for predict
+        if module in ("numpy.core.numeric", "numpy._core.numeric") and name == "_frombuffer":
+            return _safe_frombuffer  # pickle protocol 5 arrays
         if module == "numpy" and name == "ndarray":
             return np.ndarray
         if module == "numpy" and name == "dtype":
             return np.dtype
-        if module == "copyreg" and name == "_reconstructor":
+        if module in ("copyreg", "copy_reg") and name == "_reconstructor":  # copy_reg: py2 name (proto 0/1)
             return _safe_reconstructor
         if module in ("builtins", "__builtin__") and name == "object":
             return object
+        if module == "_codecs" and name == "encode":
+            return _safe_codecs_encode
         raise UnsafeCheckpointError(f"global '{module}.{name}' is not allowed in a checkpoint")
 
 
@@ -186,12 +218,12 @@ def export_sklearn_pickle(model, dst: Union[str, os.PathLike, None] = None, *,
     if "multi_class" not in (hparams or {}):
         state["multi_class"] = model.sklearn_multi_class()
 
-    inner = pickle.dumps(state, protocol=2)
-    assert inner[:2] == b"\x80\x02" and inner[-1:] == b"."
+    inner = pickle.dumps(state, protocol=3)  # protocol 3: raw bytes opcodes (readable by Python >= 3.0)
+    assert inner[:2] == b"\x80\x03" and inner[-1:] == b"."
     body = inner[2:-1]
     if numpy_compat == "1.x":
         body = body.replace(b"cnumpy._core.multiarray\n", b"cnumpy.core.multiarray\n")
-    out = (b"\x80\x02"
+    out = (b"\x80\x03"
            + b"csklearn.linear_model._logistic\nLogisticRegression\n"
            + b")\x81"  # EMPTY_TUPLE, NEWOBJ
            + body

@@ -101,7 +101,7 @@ class ModelStore:
         self.path = path
         self.reload = reload
         self.missing = missing
-        self._key = None
+        self._key = ("unchecked",)  # sentinel: the first check() always looks at the file
         self._lock = threading.Lock()
         self._watcher: Optional[threading.Thread] = None
         self._stop = threading.Event()
@@ -117,7 +117,7 @@ class ModelStore:
 
     def check(self) -> bool:
         """Sync with the file; returns True when a model is being served."""
-        if self.reload == "off" and self._key is not None:
+        if self.reload == "off" and self._key != ("unchecked",):
             return self.handle.version != 0
         key = self._stat_key()
         if key == self._key:
@@ -184,7 +184,7 @@ class AsyncEngine:
     def _state(self):
         loop = asyncio.get_running_loop()
         st = self._per_loop.get(id(loop))
-        if st is None:
+        if st is None or st[2] is not loop:  # a new loop may reuse a dead loop's id()
             sink = C().PySink()
             futures: dict = {}
 

@@ -43,8 +43,9 @@ class BinarySGDTrainer:
         self.F = n_features
         self.info = info or DistInfo(device=device)
         self.device = device if device is not None else self.info.device
+        self.on_gpu = self.device is not None and torch.device(self.device).type == "cuda"
         if self.device is None:
-            raise ValueError("BinarySGDTrainer runs on a GPU (use mlapi_amd.train.cpu for the CPU path)")
+            self.device = torch.device("cpu")  # explicit CPU path (gloo tests / GPU-less hosts)
         self.lr, self.l2, self.momentum = lr, l2, momentum
         # params = [w (F) | b]; grad buffer = [gw | gb | loss | correct]
         self.params = torch.zeros(n_features + 1, dtype=torch.float32, device=self.device)
@@ -70,14 +71,35 @@ class BinarySGDTrainer:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         return self._ws
 
-    def step(self, X: torch.Tensor, y: torch.Tensor) -> None:
-        from mlapi_amd.ops.linear import sgd_update, train_binary_grad
+    def _grad_cpu(self, X: torch.Tensor, y: torch.Tensor) -> None:
+        """Same sums as the fused kernel, in float32 PyTorch (CPU path)."""
+        Xf = X.float()
+        z = Xf @ self.w + self.b
+        g = torch.sigmoid(z) - y
+        self.grad[: self.F] = Xf.T @ g
+        self.grad[self.F] = g.sum()
+        self.grad[self.F + 1] = (torch.clamp(z, min=0) - z * y + torch.log1p(torch.exp(-z.abs()))).sum()
+        self.grad[self.F + 2] = ((z > 0) == (y > 0.5)).sum()
 
+    def step(self, X: torch.Tensor, y: torch.Tensor) -> None:
         B = X.shape[0]
-        train_binary_grad(X, y, self.w, self.b, ws=self._workspace(B), out=self.grad)
+        if self.on_gpu:
+            from mlapi_amd.ops.linear import sgd_update, train_binary_grad
+
+            train_binary_grad(X, y, self.w, self.b, ws=self._workspace(B), out=self.grad)
+        else:
+            self._grad_cpu(X, y)
         all_reduce_sum_(self.grad, self.info)
         n_global = B * self.info.world
-        sgd_update(self.params, self.grad, self.F, self.lr, 1.0 / n_global, self.l2, self.momentum, self.mom)
+        if self.on_gpu:
+            sgd_update(self.params, self.grad, self.F, self.lr, 1.0 / n_global, self.l2, self.momentum, self.mom)
+        else:
+            d = self.grad[: self.F + 1] / n_global
+            d[: self.F] += self.l2 * self.params[: self.F]
+            if self.mom is not None:
+                self.mom.mul_(self.momentum).add_(d)
+                d = self.mom
+            self.params.sub_(self.lr * d)
         self.steps += 1
         self._n_seen = n_global
 
@@ -111,8 +133,13 @@ class BinarySGDTrainer:
 
     def evaluate(self, X: torch.Tensor, y: torch.Tensor) -> Tuple[float, float]:
         """(mean loss, accuracy) on (X, y) without updating."""
-        from mlapi_amd.ops.linear import train_binary_grad
+        saved = self.grad.clone()
+        if self.on_gpu:
+            from mlapi_amd.ops.linear import train_binary_grad
 
-        out = train_binary_grad(X, y, self.w, self.b, ws=self._workspace(X.shape[0]))
-        o = out.cpu()
+            train_binary_grad(X, y, self.w, self.b, ws=self._workspace(X.shape[0]), out=self.grad)
+        else:
+            self._grad_cpu(X, y)
+        o = self.grad.cpu().clone()
+        self.grad.copy_(saved)
         return float(o[self.F + 1]) / X.shape[0], float(o[self.F + 2]) / X.shape[0]

@@ -1,0 +1,202 @@
+"""Native HTTP front end (CPU backend): wire-level parity with FastAPI, HTTP/1.1 edge cases, load."""
+import json
+import socket
+import threading
+import time
+
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from conftest import FIXTURES
+from test_contract import assert_same_body
+
+GOLDEN = json.loads((FIXTURES / "reference_contract.json").read_text())
+NAMES = ["sepal_length", "sepal_width", "petal_length", "petal_width"]
+A1 = b'{"sepal_length":5.1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}'
+
+
+@pytest.fixture
+def server(iris_cwd):
+    from mlapi_amd.serve.server import NativeServer
+    from mlapi_amd.utils.config import Config
+
+    srv = NativeServer(Config.from_env(port=0, device="cpu", io_threads=2)).start()
+    yield srv
+    srv.stop()
+
+
+def raw(port, data: bytes, n_responses=1, timeout=5.0) -> list:
+    """Send raw bytes, read n complete responses -> [(status, headers, body)]."""
+    s = socket.create_connection(("127.0.0.1", port), timeout=timeout)
+    s.sendall(data)
+    buf = b""
+    out = []
+    while len(out) < n_responses:
+        while b"\r\n\r\n" not in buf:
+            chunk = s.recv(65536)
+            if not chunk:
+                s.close()
+                return out
+            buf += chunk
+        head, rest = buf.split(b"\r\n\r\n", 1)
+        lines = head.decode("latin-1").split("\r\n")
+        status = int(lines[0].split()[1])
+        headers = {k.lower(): v.strip() for k, v in (l.split(":", 1) for l in lines[1:])}
+        if status == 100:
+            buf = rest
+            continue
+        n = int(headers.get("content-length", 0))
+        while len(rest) < n:
+            rest += s.recv(65536)
+        out.append((status, headers, rest[:n]))
+        buf = rest[n:]
+    s.close()
+    return out
+
+
+def post(body: bytes, ctype=b"application/json", extra=b"") -> bytes:
+    h = b"POST /predict HTTP/1.1\r\nHost: t\r\n"
+    if ctype is not None:
+        h += b"Content-Type: " + ctype + b"\r\n"
+    return h + extra + b"Content-Length: %d\r\n\r\n" % len(body) + body
+
+
+@pytest.mark.parametrize("case", [c for c in GOLDEN if c["name"] != "A18"], ids=lambda c: c["name"])
+def test_golden_over_the_wire(server, case):
+    req = case["request"]
+    if req["method"] == "GET":
+        data = f"GET {req['path']} HTTP/1.1\r\nHost: t\r\n\r\n".encode()
+    else:
+        body = req["content"].encode() if "content" in req else json.dumps(req["json"]).encode()
+        ctype = req.get("headers", {}).get("content-type", "application/json")
+        data = post(body, ctype.encode())
+    (status, headers, body), = raw(server.port, data)
+    assert status == case["status"]
+    assert headers["content-type"] == case["content_type"]
+    assert_same_body(body.decode(), case["body"], status)
+    assert headers["server"] == "uvicorn" and "date" in headers
+
+
+def test_fast_path_is_taken(server):
+    raw(server.port, post(A1))
+    assert server.http.stats()["fast"] >= 1
+
+
+def test_keepalive_and_pipelining(server):
+    reqs = post(A1) * 5 + b"GET /nope HTTP/1.1\r\nHost: t\r\n\r\n" + post(A1)
+    res = raw(server.port, reqs, n_responses=7)
+    assert [r[0] for r in res] == [200] * 5 + [404, 200]
+
+
+def test_chunked_and_expect_continue(server):
+    body = A1
+    chunked = b"%x\r\n%s\r\n%x\r\n%s\r\n0\r\n\r\n" % (10, body[:10], len(body) - 10, body[10:])
+    data = (b"POST /predict HTTP/1.1\r\nHost: t\r\nContent-Type: application/json\r\n"
+            b"Transfer-Encoding: chunked\r\n\r\n" + chunked)
+    (status, _, b), = raw(server.port, data)
+    assert status == 200 and json.loads(b)["prediction"] == "Iris-setosa"
+    (status, _, _), = raw(server.port, post(A1, extra=b"Expect: 100-continue\r\n"))
+    assert status == 200
+
+
+def test_http10_closes(server):
+    s = socket.create_connection(("127.0.0.1", server.port))
+    s.sendall(b"POST /predict HTTP/1.0\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n%s"
+              % (len(A1), A1))
+    data = b""
+    while True:
+        c = s.recv(4096)
+        if not c:
+            break
+        data += c
+    assert data.startswith(b"HTTP/1.1 200") and b"connection: close" in data
+
+
+def test_malformed_requests(server):
+    (status, _, _), = raw(server.port, b"GARBAGE\r\n\r\n")
+    assert status == 400
+    (status, _, _), = raw(server.port, b"POST /predict HTTP/1.1\r\nContent-Length: x\r\n\r\n")
+    assert status == 400
+    (status, _, _), = raw(server.port, b"POST /predict HTTP/1.1\r\nContent-Length: 999999999999\r\n\r\n")
+    assert status == 413
+
+
+def test_files_via_slow_path(server):
+    from mlapi_amd.api.multipart import encode_multipart
+
+    body, ctype = encode_multipart({"token": "abc"}, {"file": ("x.csv", b"c\n0.5\n", "text/csv")})
+    data = (b"POST /files/ HTTP/1.1\r\nHost: t\r\nContent-Type: " + ctype.encode() +
+            b"\r\nContent-Length: %d\r\n\r\n" % len(body) + body)
+    (status, _, b), = raw(server.port, data)
+    assert status == 200 and json.loads(b) == {"file": {"c": {"0": 0.5}}, "token": "abc"}
+
+
+def test_loadgen_concurrency_and_batching(server, native):
+    req = post(A1).decode()
+    lg = native.Loadgen("127.0.0.1", server.port, req, 32, 2)
+    r = lg.run(100, True)
+    lg.close()
+    assert r["status_counts"] == {200: 3200} and r["failed"] == 0
+    assert len(r["latencies_ns"]) == 3200
+
+
+def test_client_disconnect_mid_request(server):
+    s = socket.create_connection(("127.0.0.1", server.port))
+    s.sendall(post(A1)[:-5])
+    s.close()
+    time.sleep(0.05)
+    (status, _, _), = raw(server.port, post(A1))
+    assert status == 200
+
+
+# ------------------------------------------------------------------ fast-path parser units
+def _parse(native, body: str):
+    return native.parse_predict_body(body, NAMES)
+
+
+def test_parser_accepts_plain_numbers(native):
+    assert _parse(native, '{"sepal_length":5.1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}') == \
+        [5.1, 3.5, 1.4, 0.2]
+    assert _parse(native, ' { "petal_width" : -0e0 , "sepal_length":1E2,"sepal_width":0,"petal_length":12345678901234567890 } ') \
+        == [100.0, 0.0, 12345678901234567890.0, -0.0]
+    assert _parse(native, '{"x":{"a":[1,"}",{"b":null}]},"sepal_length":1,"sepal_width":2,"petal_length":3,'
+                          '"petal_width":4,"y":true}') == [1, 2, 3, 4]
+
+
+@pytest.mark.parametrize("body", [
+    '{"sepal_length":"5.1","sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',  # string -> pydantic coerces
+    '{"sepal_length":NaN,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"sepal_length":1e400,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',  # inf
+    '{"sepal_length":01,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"sepal_length":1.,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"sepal_length":null,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"sepal_length":true,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"sepal_length":1,"sepal_width":3.5,"petal_length":1.4}',
+    '{"sepal\\u005flength":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '[1,2,3,4]', 'hello', '', '{"sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2} x',
+    '{"sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2,}',
+])
+def test_parser_delegates_everything_else(native, body):
+    assert _parse(native, body) is None
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(st.floats(allow_nan=False, allow_infinity=False), min_size=4, max_size=4),
+       st.dictionaries(st.text(min_size=1, max_size=5), st.integers() | st.text(max_size=5) | st.none(), max_size=3))
+def test_parser_matches_json_loads(native, vals, extra):
+    d = dict(extra)
+    d.update(zip(NAMES, vals))
+    body = json.dumps(d)
+    got = _parse(native, body)
+    if got is None:  # only acceptable when an extra key needed escapes (delegated, still correct)
+        assert "\\" in body
+    else:
+        assert got == [json.loads(body)[n] for n in NAMES]
+
+
+@settings(max_examples=2000, deadline=None)
+@given(st.floats(allow_nan=False, allow_infinity=False))
+def test_float_repr_matches_python(native, v):
+    assert native.py_float_repr(v) == repr(v) == json.dumps(v)

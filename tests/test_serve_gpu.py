@@ -37,11 +37,14 @@ def test_engine_gpu_matches_oracle(native, dtype, kind, K):
 
 
 def test_engine_gpu_nonfinite_and_shape(native):
-    m = LinearModel.random(4, 3, seed=0)
+    # logits overflow to +inf for two classes -> inf - inf = NaN probability -> status 1 (A13)
+    m = LinearModel(np.array([[1.0, 1, 1, 1], [-1, -1, -1, -1], [0.5, 0.5, 0.5, 0.5]]), np.zeros(3),
+                    np.array(["a", "b", "c"], dtype=object), Kind.MULTINOMIAL)
     e = _engine(native)
     try:
         e.load_model(int(m.kind), m.W, m.b, m.label_json())
-        idx, p, st = e.predict(np.array([[1e308, 1e308, -1e308, 1e308], [1.0, 2.0, 3.0, 4.0]]))
+        idx, p, st = e.predict(np.array([[1e308, 1e308, 1e308, 1e308], [1.0, 2.0, 3.0, 4.0]]))
+        assert not np.isfinite(m.predict_max(np.array([[1e308] * 4]))[1][0])
         assert st[0] == 1 and st[1] == 0
         idx, p, st = e.predict(np.ones((3, 5)))
         assert (st == 3).all()

@@ -91,7 +91,7 @@ def main(ref_main: str) -> None:
                     "content_type": r.headers.get("content-type"), "body": r.content.decode()})
     dst = REPO / "tests" / "fixtures" / "reference_contract.json"
     dst.parent.mkdir(parents=True, exist_ok=True)
-    dst.write_text(json.dumps(out, indent=1, sort_keys=True) + "\n")
+    dst.write_text(json.dumps(out, indent=1) + "\n")  # key order preserved: 422 bodies echo it
     print(f"wrote {len(out)} cases to {dst}")
 
 
