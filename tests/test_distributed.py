@@ -1,0 +1,118 @@
+"""T5: multi-process semantics on CPU with gloo (world_size 2), via torchrun."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+ENV = {**os.environ, "PYTHONPATH": str(ROOT), "OMP_NUM_THREADS": "1", "CUDA_VISIBLE_DEVICES": "",
+       "HIP_VISIBLE_DEVICES": ""}
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def torchrun(nproc: int, script: str, env: dict, cwd=None, timeout=240, args=()):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", script, *args]
+    return subprocess.Popen(cmd, env={**ENV, **env}, cwd=cwd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                            text=True)
+
+
+def run(nproc, script, env, timeout=240, args=(), cwd=None):
+    p = torchrun(nproc, script, env, args=args, cwd=cwd)
+    try:
+        out, _ = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        out, _ = p.communicate()
+        raise AssertionError("torchrun timed out:\n" + out[-3000:])
+    assert p.returncode == 0, out[-3000:]
+    return out
+
+
+def test_broadcast_and_dp_sgd_determinism(tmp_path):
+    script = str(ROOT / "tests" / "dist" / "bcast_train.py")
+    run(1, script, {"OUT": str(tmp_path)})
+    run(2, script, {"OUT": str(tmp_path)})
+    b0 = json.loads((tmp_path / "bcast_2_0.json").read_text())
+    b1 = json.loads((tmp_path / "bcast_2_1.json").read_text())
+    assert b0["W"] == b1["W"] and b0["b"] == b1["b"] and b0["classes"] == b1["classes"] == list("abcde")
+    p0, p1 = np.load(tmp_path / "params_2_0.npy"), np.load(tmp_path / "params_2_1.npy")
+    assert np.array_equal(p0, p1), "DP replicas must stay bitwise identical"
+    single = np.load(tmp_path / "params_1_0.npy")
+    np.testing.assert_allclose(p0, single, rtol=1e-4, atol=1e-5)  # DP == single-process on the global batch
+    assert b0["acc"] > 0.8
+
+
+def test_dp_serving_reload(tmp_path, iris_pickle_bytes):
+    import httpx
+
+    from mlapi_amd.ckpt import export_sklearn_pickle, load_sklearn_pickle
+
+    (tmp_path / "LRClassifier.pkl").write_bytes(iris_pickle_bytes)
+    base = free_port()
+    while base + 1 == 0:
+        base = free_port()
+    p = torchrun(2, str(ROOT / "tests" / "dist" / "dp_serve.py"), {"OUT": str(tmp_path), "BASE_PORT": str(base)},
+                 cwd=str(tmp_path))
+    try:
+        t0 = time.time()
+        while not all((tmp_path / f"ready_{r}").exists() for r in (0, 1)):
+            assert p.poll() is None, p.stdout.read()
+            assert time.time() - t0 < 90
+            time.sleep(0.1)
+        a1 = {"sepal_length": 5.1, "sepal_width": 3.5, "petal_length": 1.4, "petal_width": 0.2}
+        for r in (0, 1):
+            res = httpx.post(f"http://127.0.0.1:{base + r}/predict", json=a1)
+            assert res.json()["prediction"] == "Iris-setosa"
+        m = load_sklearn_pickle(iris_pickle_bytes)
+        m.b = m.b + np.array([-100.0, 0.0, 100.0])
+        export_sklearn_pickle(m, tmp_path / "LRClassifier.pkl")
+        deadline = time.time() + 20
+        seen = set()
+        while time.time() < deadline and len(seen) < 2:
+            for r in (0, 1):
+                if httpx.post(f"http://127.0.0.1:{base + r}/predict", json=a1).json()["prediction"] == "Iris-virginica":
+                    seen.add(r)
+            time.sleep(0.05)
+        assert seen == {0, 1}, "both replicas must switch to the new weights (broadcast from rank 0)"
+        os.remove(tmp_path / "LRClassifier.pkl")
+        deadline = time.time() + 20
+        codes = set()
+        while time.time() < deadline and codes != {500}:
+            codes = {httpx.post(f"http://127.0.0.1:{base + r}/predict", json=a1).status_code for r in (0, 1)}
+            time.sleep(0.05)
+        assert codes == {500}
+    finally:
+        (tmp_path / "stop").touch()
+        try:
+            out, _ = p.communicate(timeout=60)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+    assert p.returncode == 0, out[-3000:]
+
+
+def test_bench_contract_two_ranks():
+    out = run(2, str(ROOT / "bench.py"), {}, args=["--cpu", "--gpus", "2", "--steps", "10", "--warmup", "2",
+                                                   "--c1-requests", "200"])
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
