@@ -4,16 +4,22 @@
 // MFMA layout (v_mfma_f32_16x16x32_bf16, cdna_hip_programming.md S3): the class dimension is the
 // MFMA "M" (A operand = W rows) and the batch row is "N" (B operand = X rows), so the C/D tile
 // puts ONE batch row on each lane (col = lane & 15) and 4 classes in its registers
-// (row = (lane >> 4) * 4 + reg). The softmax reduction over classes is then lane-local: each lane
-// keeps an online (max, sum-exp, argmax) state over the classes it owns and the 4 lanes that
-// share a batch row merge once at the very end (2 xor-shuffles) - no LDS, no per-tile shuffles.
+// (row = (lane >> 4) * 4 + reg). The softmax reduction over classes is lane-local: each lane keeps
+// an online (max, sum-exp, argmax) state over the classes it owns; the 4 lanes sharing a batch
+// row merge once at the end (2 xor-shuffles). No LDS is needed for the epilogue.
 //
-// Work split: a 256-thread block = 4 waves x 32 batch rows (2 N-tiles). Each wave keeps its X
-// fragments for the whole F in registers (F=256: 64 VGPRs) and streams W fragments (L2-resident,
-// 500 KiB at K=1000) for 64 classes (4 M-tiles) per chunk. For small batches (B=1024 -> only 8
-// row-blocks) the class range is split over gridDim.y so the launch still fills the chip; each
-// split writes a partial (max, sum, argmax) per row and a tiny merge kernel combines them in
-// split order (deterministic). For large B there is one split and no merge.
+// Data movement (v2, after profiles/r1_first/gemm_kernel_stats.csv showed the v1 kernel exposing
+// one L2/HBM latency per k-step by loading W fragments straight to registers):
+//  * X: each wave loads its NT x 16 batch rows for the whole F once, straight to registers;
+//  * W: 64-class chunks are staged cooperatively by all 4 waves into a double-buffered LDS image
+//    [64 classes][F] with a 16-byte-chunk XOR swizzle (chunk ^ (class & 15)), which makes the
+//    ds_read_b128 fragment reads (16 classes x 16 B at one k-offset per lane group) conflict-free;
+//    the global loads for chunk c+1 are issued before the MFMAs of chunk c and written to LDS
+//    after them (T14 issue-early / write-late), one barrier per chunk;
+//  * small batches (B=1024 -> 16 row blocks) split the class range over gridDim.y so the launch
+//    fills the chip; the splits are merged IN THE SAME LAUNCH by the last-arriving block of each
+//    row block (agent-scope release fence + relaxed ticket, acquire fence in the reducer:
+//    Guideline 16), replacing v1's separate merge kernel (7.3 us of a 18.6 us total).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -26,15 +32,15 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 
-constexpr int ROWS_PER_WAVE = 32;
-constexpr int ROWS_PER_BLOCK = 4 * ROWS_PER_WAVE;
 constexpr int CLASS_CHUNK = 64;
+constexpr int COUNTER_BYTES = 4096;  // per-row-block arrival counters live at the start of the workspace
 
 struct RowState {
-  float m;   // running max logit (-inf if nothing seen yet)
-  float s;   // softmax: sum exp(z - m);  OvR: sum sigmoid(z)
-  int bi;    // argmax class (first max wins)
+  float m;  // running max logit (-inf if nothing seen yet)
+  float s;  // softmax: sum exp(z - m);  OvR: sum sigmoid(z)
+  int bi;   // argmax class (first max wins)
 };
 
 __device__ __forceinline__ float sigmoidf_(float z) { return 1.f / (1.f + __expf(-z)); }
@@ -55,35 +61,51 @@ __device__ __forceinline__ RowState merge_state(RowState a, RowState b, bool ovr
 }
 
 __device__ __forceinline__ RowState shfl_state(RowState a, int off) {
-  RowState r;
-  r.m = __shfl_xor(a.m, off, 64);
-  r.s = __shfl_xor(a.s, off, 64);
-  r.bi = __shfl_xor(a.bi, off, 64);
-  return r;
+  return RowState{__shfl_xor(a.m, off, 64), __shfl_xor(a.s, off, 64), __shfl_xor(a.bi, off, 64)};
 }
 
-// MODE 0: fused argmax/p_max epilogue (partials when gridDim.y > 1). MODE 1: write logits Z.
-template <int KS, int MODE>
+// LDS byte offset of 16-byte chunk `ch` of class row `r` in a [64][F] bf16 image.
+__device__ __forceinline__ int lds_off(int r, int ch, int row_bytes, int swz_mask) {
+  return r * row_bytes + ((ch ^ (r & swz_mask)) << 4);
+}
+
+// KS = F/32 upper bound (registers), NT = 16-row N-tiles per wave, MODE 0 = fused epilogue,
+// MODE 1 = write logits.
+template <int KS, int NT, int MODE>
 __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __restrict__ X,
                                                            const uint16_t* __restrict__ W,
                                                            const float* __restrict__ bias, int64_t B, int F, int K,
                                                            int kind, int classes_per_split,
                                                            int32_t* __restrict__ out_idx, float* __restrict__ out_p,
+                                                           unsigned int* __restrict__ counters,
                                                            float4* __restrict__ partials, float* __restrict__ Z) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int q = lane >> 4;   // k-group of the operand fragments / class quad of the C tile
+  constexpr int ROWS_PER_WAVE = 16 * NT;
+  constexpr int ROWS_PER_BLOCK = 4 * ROWS_PER_WAVE;
+  constexpr int MAX_ROW_BYTES = KS * 64;              // F * 2 bytes
+  constexpr int BUF_BYTES = CLASS_CHUNK * MAX_ROW_BYTES;
+  constexpr int PIECES = BUF_BYTES / 16 / 256;         // 16-byte pieces per thread per chunk (upper bound)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF_BYTES + 16];
+  int* const flag = reinterpret_cast<int*>(smem + 2 * BUF_BYTES);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int q = lane >> 4;
   const int col = lane & 15;
-  const int ksr = F / 32;    // runtime k-steps (<= KS)
+  const int ksr = F / 32;
+  const int row_bytes = F * 2;
+  const int nch = F / 8;                               // 16-byte chunks per W row
+  const int swz_mask = (nch & -nch) >= 16 ? 15 : (nch & -nch) - 1;
   const bool ovr = kind == KIND_OVR;
   const int64_t row0 = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wave * ROWS_PER_WAVE;
   const int c_begin = blockIdx.y * classes_per_split;
   const int c_end = min(K, c_begin + classes_per_split);
+  const int pieces = CLASS_CHUNK * nch;                // actual pieces per chunk
 
-  // X fragments for the whole feature range stay in registers.
-  bf16x8_t xf[2][KS];
+  // ---- X fragments for the whole feature range, straight to registers (issued first)
+  bf16x8_t xf[NT][KS];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < NT; ++t) {
     int64_t r = row0 + t * 16 + col;
     r = r < B ? r : B - 1;
     const uint16_t* xr = X + r * F + 8 * q;
@@ -92,39 +114,65 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
       xf[t][ks] = ks < ksr ? *reinterpret_cast<const bf16x8_t*>(xr + ks * 32) : bf16x8_t{};
   }
 
-  RowState st[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) st[t] = RowState{-INFINITY, 0.f, 0x7fffffff};
+  // ---- W chunk staging: global -> registers (issue early) -> LDS (write late). Plain unrolled
+  // code, not lambdas: a lambda capturing `stage` by reference forces it into scratch memory.
+  u32x4_t stage[PIECES];
+#define MLAPI_LOAD_CHUNK(C0)                                                         \
+  _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                               \
+    const int p = tid + i * 256;                                                     \
+    if (p < pieces) {                                                                \
+      const int r = p / nch, ch = p % nch;                                           \
+      int cls = (C0) + r;                                                            \
+      cls = cls < K ? cls : K - 1;                                                   \
+      stage[i] = *reinterpret_cast<const u32x4_t*>(W + (int64_t)cls * F + ch * 8);  \
+    }                                                                                \
+  }
+#define MLAPI_WRITE_CHUNK(BUF)                                                                         \
+  _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                                                 \
+    const int p = tid + i * 256;                                                                       \
+    if (p < pieces) {                                                                                  \
+      const int r = p / nch, ch = p % nch;                                                             \
+      *reinterpret_cast<u32x4_t*>(smem + (BUF) * BUF_BYTES + lds_off(r, ch, row_bytes, swz_mask)) = stage[i]; \
+    }                                                                                                  \
+  }
 
-  for (int c0 = c_begin; c0 < c_end; c0 += CLASS_CHUNK) {
-    f32x4_t acc[2][4];
+  RowState st[NT];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < NT; ++t) st[t] = RowState{-INFINITY, 0.f, 0x7fffffff};
+
+  MLAPI_LOAD_CHUNK(c_begin)
+  MLAPI_WRITE_CHUNK(0)
+  __syncthreads();
+
+  int buf = 0;
+  for (int c0 = c_begin; c0 < c_end; c0 += CLASS_CHUNK) {
+    const bool has_next = c0 + CLASS_CHUNK < c_end;
+    if (has_next) {
+      MLAPI_LOAD_CHUNK(c0 + CLASS_CHUNK)
+    }
+
+    f32x4_t acc[NT][4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) acc[t][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-    const uint16_t* wrow[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      int cls = c0 + mt * 16 + col;
-      cls = cls < K ? cls : K - 1;
-      wrow[mt] = W + (int64_t)cls * F + 8 * q;
-    }
+    const unsigned char* wb = smem + buf * BUF_BYTES;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       if (ks < ksr) {
         bf16x8_t wf[4];
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) wf[mt] = *reinterpret_cast<const bf16x8_t*>(wrow[mt] + ks * 32);
+        for (int mt = 0; mt < 4; ++mt)
+          wf[mt] = *reinterpret_cast<const bf16x8_t*>(wb + lds_off(mt * 16 + col, ks * 4 + q, row_bytes, swz_mask));
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)
             acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt], xf[t][ks], acc[t][mt], 0, 0, 0);
       }
     }
 
-    // Epilogue for this chunk: lane owns classes c0 + mt*16 + q*4 + reg of batch row (t, col).
+    // epilogue for this chunk: lane owns classes c0 + mt*16 + q*4 + r of batch row (t, col)
     float bv[4][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -134,7 +182,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
         bv[mt][r] = cls < c_end ? bias[cls] : 0.f;
       }
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < NT; ++t) {
       if constexpr (MODE == 1) {
         const int64_t row = row0 + t * 16 + col;
         if (row < B) {
@@ -175,79 +223,128 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
         S.s += add;
       }
     }
+    if (has_next) {
+      MLAPI_WRITE_CHUNK(buf ^ 1)
+    }
+    __syncthreads();
+    buf ^= 1;
   }
 
+#undef MLAPI_LOAD_CHUNK
+#undef MLAPI_WRITE_CHUNK
   if constexpr (MODE == 0) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < NT; ++t) {
       RowState S = st[t];
       S = merge_state(S, shfl_state(S, 16), ovr);
       S = merge_state(S, shfl_state(S, 32), ovr);
-      const int64_t row = row0 + t * 16 + col;
-      if (q == 0 && row < B) {
-        if (gridDim.y == 1) {
-          out_idx[row] = S.bi;
-          out_p[row] = ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s;
-        } else {
-          partials[(int64_t)blockIdx.y * B + row] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
+      st[t] = S;
+    }
+    if (gridDim.y == 1) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int64_t row = row0 + t * 16 + col;
+        if (q == 0 && row < B) {
+          out_idx[row] = st[t].bi;
+          out_p[row] = ovr ? sigmoidf_(st[t].m) / st[t].s : 1.f / st[t].s;
         }
+      }
+      return;
+    }
+    // ---- split classes: publish partials, last-arriving block of this row block merges them
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int64_t row = row0 + t * 16 + col;
+      if (q == 0 && row < B)
+        partials[(int64_t)blockIdx.y * B + row] = make_float4(st[t].m, st[t].s, __int_as_float(st[t].bi), 0.f);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: ROCm 7.2 may drop the fence's own wait
+      const unsigned ticket =
+          __hip_atomic_fetch_add(&counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = ticket == gridDim.y - 1;
+    }
+    __syncthreads();
+    if (*flag == 0) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    __syncthreads();
+    if (tid < ROWS_PER_BLOCK) {
+      const int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + tid;
+      if (row < B) {
+        float4 p0 = partials[row];
+        RowState S{p0.x, p0.y, __float_as_int(p0.z)};
+        for (unsigned sp = 1; sp < gridDim.y; ++sp) {  // fixed split order: deterministic
+          const float4 p = partials[(int64_t)sp * B + row];
+          S = merge_state(S, RowState{p.x, p.y, __float_as_int(p.z)}, ovr);
+        }
+        out_idx[row] = S.bi;
+        out_p[row] = ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s;
       }
     }
   }
 }
 
-__global__ __launch_bounds__(256) void merge_partials_kernel(const float4* __restrict__ partials, int splits,
-                                                             int64_t B, int kind, int32_t* __restrict__ out_idx,
-                                                             float* __restrict__ out_p) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= B) return;
-  const bool ovr = kind == KIND_OVR;
-  float4 p0 = partials[row];
-  RowState S{p0.x, p0.y, __float_as_int(p0.z)};
-  for (int sp = 1; sp < splits; ++sp) {
-    const float4 p = partials[(int64_t)sp * B + row];
-    S = merge_state(S, RowState{p.x, p.y, __float_as_int(p.z)}, ovr);
-  }
-  out_idx[row] = S.bi;
-  out_p[row] = ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s;
-}
-
 struct Plan {
+  int nt;                 // 16-row tiles per wave
   int splits;
   int classes_per_split;
+  int64_t row_blocks;
 };
 
 Plan make_plan(int64_t B, int K) {
-  const int64_t row_blocks = (B + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
+  Plan p;
+  const int64_t rb2 = (B + 127) / 128;
+  p.nt = rb2 >= 512 ? 2 : 1;  // large batches: 32 rows/wave (W re-read from L2 half as often)
+  const int rows_per_block = 64 * p.nt;
+  p.row_blocks = (B + rows_per_block - 1) / rows_per_block;
   const int chunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
-  int64_t want = (512 + row_blocks - 1) / row_blocks;  // aim for >= 512 blocks (2 per CU)
+  int64_t want = (256 + p.row_blocks - 1) / p.row_blocks;  // aim for >= 256 blocks (1 per CU)
   int splits = (int)(want < 1 ? 1 : (want > chunks ? chunks : want));
   const int chunks_per_split = (chunks + splits - 1) / splits;
-  Plan p;
   p.classes_per_split = chunks_per_split * CLASS_CHUNK;
   p.splits = (K + p.classes_per_split - 1) / p.classes_per_split;
+  if (p.splits > 1 && p.row_blocks * 4 > COUNTER_BYTES) {  // counters do not fit: no split
+    p.splits = 1;
+    p.classes_per_split = chunks * CLASS_CHUNK;
+  }
   return p;
 }
 
 template <int MODE>
 void launch_mode(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind, int32_t* out_idx,
-                 float* out_p, float4* partials, float* Z, const Plan& plan, hipStream_t stream) {
+                 float* out_p, void* ws, float* Z, const Plan& plan, hipStream_t stream) {
   if (F % 32 != 0 || F > 512) throw std::invalid_argument("gemm_softmax: F must be a multiple of 32 and <= 512");
-  const dim3 grid((unsigned)((B + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), (unsigned)plan.splits);
+  const dim3 grid((unsigned)plan.row_blocks, (unsigned)plan.splits);
   auto x = static_cast<const uint16_t*>(X);
   auto w = static_cast<const uint16_t*>(W);
-#define MLAPI_GEMM_LAUNCH(KSV)                                                                                    \
-  hipLaunchKernelGGL((gemm_softmax_kernel<KSV, MODE>), grid, dim3(256), 0, stream, x, w, b, B, F, K, kind,       \
-                     plan.classes_per_split, out_idx, out_p, partials, Z)
+  auto counters = static_cast<unsigned int*>(ws);
+  auto partials = ws ? reinterpret_cast<float4*>(static_cast<unsigned char*>(ws) + COUNTER_BYTES) : nullptr;
+#define MLAPI_GEMM_LAUNCH(KSV, NTV)                                                                              \
+  hipLaunchKernelGGL((gemm_softmax_kernel<KSV, NTV, MODE>), grid, dim3(256), 0, stream, x, w, b, B, F, K, kind, \
+                     plan.classes_per_split, out_idx, out_p, counters, partials, Z)
+#define MLAPI_GEMM_NT(KSV)           \
+  if (plan.nt == 2)                  \
+    MLAPI_GEMM_LAUNCH(KSV, 2);       \
+  else                               \
+    MLAPI_GEMM_LAUNCH(KSV, 1);
   const int ks = F / 32;
-  if (ks <= 2)
-    MLAPI_GEMM_LAUNCH(2);
-  else if (ks <= 4)
-    MLAPI_GEMM_LAUNCH(4);
-  else if (ks <= 8)
-    MLAPI_GEMM_LAUNCH(8);
-  else
-    MLAPI_GEMM_LAUNCH(16);
+  if (ks <= 2) {
+    MLAPI_GEMM_NT(2)
+  } else if (ks <= 4) {
+    MLAPI_GEMM_NT(4)
+  } else if (ks <= 8) {
+    MLAPI_GEMM_NT(8)
+  } else {
+    MLAPI_GEMM_NT(16)
+  }
+#undef MLAPI_GEMM_NT
 #undef MLAPI_GEMM_LAUNCH
   MLAPI_HIP_CHECK(hipGetLastError());
 }
@@ -257,7 +354,7 @@ void launch_mode(const void* X, const void* W, const float* b, int64_t B, int F,
 size_t gemm_softmax_workspace(int64_t B, int K, int F) {
   (void)F;
   const Plan p = make_plan(B, K);
-  return p.splits > 1 ? (size_t)p.splits * (size_t)B * sizeof(float4) : 0;
+  return p.splits > 1 ? (size_t)COUNTER_BYTES + (size_t)p.splits * (size_t)B * sizeof(float4) : 0;
 }
 
 void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind,
@@ -266,20 +363,17 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("gemm_softmax: multiclass kinds only (binary models use gemv_binary)");
   const Plan plan = make_plan(B, K);
-  if (plan.splits > 1 && ws_bytes < (size_t)plan.splits * (size_t)B * sizeof(float4))
-    throw std::invalid_argument("gemm_softmax: workspace too small");
-  launch_mode<0>(X, W, b, B, F, K, kind, out_idx, out_p, static_cast<float4*>(workspace), nullptr, plan, stream);
-  if (plan.splits > 1) {
-    hipLaunchKernelGGL(merge_partials_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, stream,
-                       static_cast<const float4*>(workspace), plan.splits, B, kind, out_idx, out_p);
-    MLAPI_HIP_CHECK(hipGetLastError());
-  }
+  if (plan.splits > 1 && ws_bytes < gemm_softmax_workspace(B, K, F))
+    throw std::invalid_argument("gemm_softmax: workspace too small (must be zero-initialised once)");
+  launch_mode<0>(X, W, b, B, F, K, kind, out_idx, out_p, plan.splits > 1 ? workspace : nullptr, nullptr, plan,
+                 stream);
 }
 
 void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B, int F, int K, float* Z,
                         hipStream_t stream) {
   if (B <= 0) return;
-  const Plan plan = make_plan(B, K);
+  Plan plan = make_plan(B, K);
+  plan.splits = (K + plan.classes_per_split - 1) / plan.classes_per_split;  // no merge needed for logits
   launch_mode<1>(X, W, b, B, F, K, KIND_MULTINOMIAL, nullptr, nullptr, nullptr, Z, plan, stream);
 }
 

@@ -71,7 +71,9 @@ class GemmSoftmax:
     def __init__(self, max_batch: int, n_classes: int, n_features: int, device):
         self.max_batch, self.K, self.F = max_batch, n_classes, n_features
         nbytes = C().gemm_softmax_workspace(max_batch, n_classes, n_features)
-        self.ws = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
+        # zero-initialised once: the in-kernel split merge uses arrival counters at the start of
+        # the workspace, which the last-arriving block re-arms to 0 after every launch.
+        self.ws = torch.zeros(max(nbytes, 16), dtype=torch.uint8, device=device)
 
     def __call__(self, X, W, b, kind: int = Kind.MULTINOMIAL, out=None):
         _check(X, W, b)
@@ -83,7 +85,7 @@ class GemmSoftmax:
             raise ValueError("gemm_softmax: need F % 32 == 0, F <= 512 and matching W/b")
         need = C().gemm_softmax_workspace(B, K, F)
         if need > self.ws.numel():
-            self.ws = torch.empty(need, dtype=torch.uint8, device=X.device)
+            self.ws = torch.zeros(need, dtype=torch.uint8, device=X.device)
         if out is None:
             out = (torch.empty(B, dtype=torch.int32, device=X.device), torch.empty(B, dtype=torch.float32, device=X.device))
         idx, p = out
