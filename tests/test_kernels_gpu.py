@@ -99,6 +99,25 @@ def test_gemm_softmax(B, F, K, kind):
     torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=2e-4, atol=2e-5)
 
 
+def test_gemm_softmax_large_batch_and_rearm():
+    """NT=2 multi-chunk path (double-buffered LDS) and the split path launched repeatedly on one
+    workspace (the in-kernel merge counters must re-arm themselves)."""
+    F, K = 256, 1000
+    W = _rand((K, F), torch.bfloat16, 21, scale=1 / 16)
+    b = _rand((K,), torch.float32, 22, scale=0.1)
+    for B in (70000, 1024):
+        X = _rand((B, F), torch.bfloat16, 20)
+        op = ops.GemmSoftmax(B, K, F, DEV)
+        Z = ref.logits_ref(X, W, b, dtype=torch.float32)
+        top2 = torch.topk(Z, 2, dim=1).values
+        clear = (top2[:, 0] - top2[:, 1]) > 1e-3
+        rp = torch.softmax(Z.double(), dim=1).max(dim=1).values
+        for _ in range(3):
+            idx, p = op(X, W, b)
+            assert torch.equal(idx[clear], torch.argmax(Z, dim=1).to(torch.int32)[clear])
+            torch.testing.assert_close(p.double(), rp, rtol=2e-4, atol=2e-5)
+
+
 def test_gemm_logits_asymmetric():
     """A = I-style check with an asymmetric operand: catches a transposed C write (guide S3)."""
     B, F, K = 64, 64, 48
