@@ -193,13 +193,13 @@ def main(argv=None) -> int:
     ap.add_argument("--mode", default="serve", choices=["serve", "gemv", "gemm", "train"])
     ap.add_argument("--conns", type=int, default=64)
     ap.add_argument("--reqs-per-conn", type=int, default=16)
-    ap.add_argument("--client-threads", type=int, default=3)
-    ap.add_argument("--io-threads", type=int, default=3)
+    ap.add_argument("--client-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
+    ap.add_argument("--io-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--max-batch", type=int, default=256)
     ap.add_argument("--c1-requests", type=int, default=3000)
     ap.add_argument("--rows", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=1024)
-    ap.add_argument("--train-batch", type=int, default=1 << 16)
+    ap.add_argument("--train-batch", type=int, default=1 << 18)
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--cpu", action="store_true", help="force the CPU backend (testing without a GPU)")
     args = ap.parse_args(argv)
@@ -207,6 +207,18 @@ def main(argv=None) -> int:
     from mlapi_amd.parallel.comm import init_distributed, shutdown
 
     info = init_distributed(use_gpu=False if args.cpu else None)
+    if args.io_threads <= 0 or args.client_threads <= 0:
+        # Server IO threads and load-generator threads share this rank's CPUs (sweep on a 16-CPU
+        # MI355X box share: 6 + 6 threads -> 519k req/s vs 3 + 3 -> 270k; tools/serve_sweep.sh).
+        try:
+            cpus = len(os.sched_getaffinity(0))
+        except AttributeError:  # pragma: no cover
+            cpus = os.cpu_count() or 8
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", info.world))
+        per_rank = max(4, cpus // max(1, local))
+        auto = max(2, min(6, (per_rank - 3) // 2))
+        args.io_threads = args.io_threads if args.io_threads > 0 else auto
+        args.client_threads = args.client_threads if args.client_threads > 0 else auto
     if args.mode != "serve" and info.device is None:
         print(f"mode {args.mode} needs a GPU", file=sys.stderr)
         return 2

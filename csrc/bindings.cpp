@@ -144,6 +144,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("dt"), py::arg("X"), py::arg("w"), py::arg("bias"), py::arg("B"), py::arg("F"), py::arg("kind"),
       py::arg("out_idx"), py::arg("out_p"), py::arg("stream") = 0);
   m.def("gemm_softmax_workspace", &gemm_softmax_workspace);
+  m.def("gemm_softmax_force_plan", &gemm_softmax_force_plan, py::arg("nt") = 0, py::arg("splits") = 0);
   m.def(
       "gemm_softmax",
       [](uintptr_t X, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind, uintptr_t out_idx,
@@ -170,6 +171,17 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("dt"), py::arg("X"), py::arg("y"), py::arg("w"), py::arg("b"), py::arg("B"), py::arg("F"),
       py::arg("out"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream") = 0);
+  m.def(
+      "train_binary_step",
+      [](int dt, uintptr_t X, uintptr_t y, uintptr_t params, uintptr_t mom, int64_t B, int F, uintptr_t grad_out,
+         uintptr_t ws, size_t ws_bytes, float lr, float inv_n, float l2, float momentum, uintptr_t stream) {
+        launch_train_binary_step(dt, ptr<void>(X), ptr<float>(y), ptr<float>(params), ptr<float>(mom), B, F,
+                                 ptr<float>(grad_out), ptr<void>(ws), ws_bytes, lr, inv_n, l2, momentum,
+                                 stream_of(stream));
+      },
+      py::arg("dt"), py::arg("X"), py::arg("y"), py::arg("params"), py::arg("mom"), py::arg("B"), py::arg("F"),
+      py::arg("grad_out"), py::arg("ws"), py::arg("ws_bytes"), py::arg("lr"), py::arg("inv_n"), py::arg("l2"),
+      py::arg("momentum"), py::arg("stream") = 0);
   m.def("train_small_workspace", &train_small_workspace);
   m.def(
       "train_small_grad",

@@ -23,6 +23,8 @@ void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_
 // ---- gemm_softmax.hip: multiclass predict, bf16 MFMA GEMM + online softmax/argmax epilogue ----
 // X: [B, F] bf16; W: [K, F] bf16; b: [K] f32. F % 32 == 0. Workspace: gemm_softmax_workspace().
 size_t gemm_softmax_workspace(int64_t B, int K, int F);
+// Benchmark hook: force the (rows-per-wave tiles, class splits) plan; (0, 0) = automatic.
+void gemm_softmax_force_plan(int nt, int splits);
 void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind,
                          int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream);
 // Full logits (for tests / decision_function): Z[B, K] f32.
@@ -37,6 +39,12 @@ size_t train_binary_workspace(int64_t B, int F);
 void launch_train_binary_grad(int dt, const void* X, const float* y, const float* w, float bias_unused,
                               const float* bptr, int64_t B, int F, float* out, void* workspace, size_t ws_bytes,
                               hipStream_t stream);
+// Single-replica fused step: gradient (as above, into grad_out) + deterministic reduce + SGD update
+// of params = [w (F) | b] in place (2 launches total). DP training uses launch_train_binary_grad,
+// an all-reduce, then launch_sgd_update.
+void launch_train_binary_step(int dt, const void* X, const float* y, float* params, float* mom, int64_t B, int F,
+                              float* grad_out, void* workspace, size_t ws_bytes, float lr, float inv_n, float l2,
+                              float momentum, hipStream_t stream);
 // Small multiclass / binary (F*K <= 1024): fp64 or fp32, exact loss+grad of sklearn's objective
 // terms. out = [gW (K*F, row-major) | gb (K) | loss_sum | n_correct].
 size_t train_small_workspace(int64_t B, int F, int K);

@@ -298,10 +298,23 @@ struct Plan {
   int64_t row_blocks;
 };
 
+// Benchmark hook (tools/gemm_plan_sweep.py): force (nt, splits); 0 = automatic.
+int g_force_nt = 0, g_force_splits = 0;
+
 Plan make_plan(int64_t B, int K) {
   Plan p;
   const int64_t rb2 = (B + 127) / 128;
   p.nt = rb2 >= 512 ? 2 : 1;  // large batches: 32 rows/wave (W re-read from L2 half as often)
+  if (g_force_nt == 1 || g_force_nt == 2) p.nt = g_force_nt;
+  if (g_force_splits > 0) {
+    const int rows_per_block = 64 * p.nt;
+    p.row_blocks = (B + rows_per_block - 1) / rows_per_block;
+    const int chunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
+    const int sp = g_force_splits > chunks ? chunks : g_force_splits;
+    p.classes_per_split = ((chunks + sp - 1) / sp) * CLASS_CHUNK;
+    p.splits = (K + p.classes_per_split - 1) / p.classes_per_split;
+    if (!(p.splits > 1 && p.row_blocks * 4 > COUNTER_BYTES)) return p;
+  }
   const int rows_per_block = 64 * p.nt;
   p.row_blocks = (B + rows_per_block - 1) / rows_per_block;
   const int chunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
@@ -350,6 +363,11 @@ void launch_mode(const void* X, const void* W, const float* b, int64_t B, int F,
 }
 
 }  // namespace
+
+void gemm_softmax_force_plan(int nt, int splits) {
+  g_force_nt = nt;
+  g_force_splits = splits;
+}
 
 size_t gemm_softmax_workspace(int64_t B, int K, int F) {
   (void)F;

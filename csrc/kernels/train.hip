@@ -212,16 +212,25 @@ __global__ __launch_bounds__(256) void train_binary_grad_kernel(const T* __restr
   }
 }
 
-// Deterministic slab reduction: 32 columns x 8 partitions per 256-thread block. Partition p sums
-// slabs p, p+8, p+16, ... in increasing order (each wave-row reads 32 consecutive columns = one
-// coalesced 128-B segment per slab), then the 8 partials are added in fixed order through LDS.
+// Deterministic slab reduction: 16 columns x 16 partitions per 256-thread block. Partition p sums
+// slabs p, p+16, p+32, ... in increasing order (each partition row reads 16 consecutive columns =
+// one coalesced 64-B segment per slab), then the 16 partials are added in fixed order through LDS.
 // A single thread per column walking all slabs serially was the bottleneck of the training step
 // (232 us vs 22 us for the fused gradient kernel: profiles/r1_first/train_kernel_stats.csv).
-constexpr int RED_COLS = 32;
-constexpr int RED_PARTS = 8;
-template <typename T>
+// FUSE_SGD: when no all-reduce separates them (one replica), the SGD update of the parameter
+// vector is applied by the same thread that produced the column's gradient sum (saves a launch).
+constexpr int RED_COLS = 16;
+constexpr int RED_PARTS = 16;
+struct SgdArgs {
+  float* params = nullptr;
+  float* mom = nullptr;
+  int64_t n_params = 0, n_pen = 0;
+  float lr = 0.f, inv_n = 0.f, l2 = 0.f, momentum = 0.f;
+};
+
+template <typename T, bool FUSE_SGD>
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(const T* __restrict__ slabs, int nslabs, int width,
-                                                           T* __restrict__ out) {
+                                                           T* __restrict__ out, SgdArgs sgd) {
   __shared__ T part[RED_PARTS][RED_COLS];
   const int c = threadIdx.x % RED_COLS;
   const int p = threadIdx.x / RED_COLS;
@@ -248,13 +257,29 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const T* __restrict__
 #pragma unroll
     for (int q = 1; q < RED_PARTS; ++q) t += part[q][c];
     out[j] = t;
+    if constexpr (FUSE_SGD) {
+      if (j < sgd.n_params) {
+        float d = (float)t * sgd.inv_n + (j < sgd.n_pen ? sgd.l2 * sgd.params[j] : 0.f);
+        if (sgd.mom != nullptr) {
+          const float v = sgd.momentum * sgd.mom[j] + d;
+          sgd.mom[j] = v;
+          d = v;
+        }
+        sgd.params[j] -= sgd.lr * d;
+      }
+    }
   }
 }
 
 template <typename T>
-void launch_reduce_slabs(const T* slabs, int nslabs, int width, T* out, hipStream_t stream) {
-  hipLaunchKernelGGL(reduce_slabs_kernel<T>, dim3((unsigned)((width + RED_COLS - 1) / RED_COLS)), dim3(256), 0,
-                     stream, slabs, nslabs, width, out);
+void launch_reduce_slabs(const T* slabs, int nslabs, int width, T* out, hipStream_t stream,
+                         const SgdArgs* sgd = nullptr) {
+  const dim3 grid((unsigned)((width + RED_COLS - 1) / RED_COLS));
+  if (sgd != nullptr)
+    hipLaunchKernelGGL((reduce_slabs_kernel<T, true>), grid, dim3(256), 0, stream, slabs, nslabs, width, out, *sgd);
+  else
+    hipLaunchKernelGGL((reduce_slabs_kernel<T, false>), grid, dim3(256), 0, stream, slabs, nslabs, width, out,
+                       SgdArgs{});
   MLAPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -274,7 +299,7 @@ BinPlan bin_plan(int chunks) {
 
 int64_t bin_blocks(int64_t B, const BinPlan& p) {
   int64_t blocks = (B + p.rows_per_block - 1) / p.rows_per_block;
-  const int64_t cap = 256 * 2;  // 2 blocks per CU: enough bytes in flight, few slabs to reduce
+  const int64_t cap = 256;  // one fat block per CU: enough bytes in flight, few slabs to reduce
   return blocks < 1 ? 1 : (blocks > cap ? cap : blocks);
 }
 
@@ -452,9 +477,9 @@ size_t train_binary_workspace(int64_t B, int F) {
   return (size_t)256 * 4 * (size_t)(F + 3) * sizeof(float);  // upper bound: cap blocks
 }
 
-void launch_train_binary_grad(int dt, const void* X, const float* y, const float* w, float /*bias_unused*/,
-                              const float* bptr, int64_t B, int F, float* out, void* workspace, size_t ws_bytes,
-                              hipStream_t stream) {
+namespace {
+void train_binary_impl(int dt, const void* X, const float* y, const float* w, const float* bptr, int64_t B, int F,
+                       float* out, void* workspace, size_t ws_bytes, hipStream_t stream, const SgdArgs* sgd) {
   if (B <= 0) return;
   const int ne = dt == DT_BF16 ? 8 : 4;
   if (F % ne != 0) throw std::invalid_argument("train_binary: F must be a multiple of 16 bytes of elements");
@@ -483,7 +508,29 @@ void launch_train_binary_grad(int dt, const void* X, const float* y, const float
 #undef MLAPI_TB_ALL
 #undef MLAPI_TB
   MLAPI_HIP_CHECK(hipGetLastError());
-  launch_reduce_slabs<float>(slabs, (int)blocks, F + 3, out, stream);
+  launch_reduce_slabs<float>(slabs, (int)blocks, F + 3, out, stream, sgd);
+}
+}  // namespace
+
+void launch_train_binary_grad(int dt, const void* X, const float* y, const float* w, float /*bias_unused*/,
+                              const float* bptr, int64_t B, int F, float* out, void* workspace, size_t ws_bytes,
+                              hipStream_t stream) {
+  train_binary_impl(dt, X, y, w, bptr, B, F, out, workspace, ws_bytes, stream, nullptr);
+}
+
+void launch_train_binary_step(int dt, const void* X, const float* y, float* params, float* mom, int64_t B, int F,
+                              float* grad_out, void* workspace, size_t ws_bytes, float lr, float inv_n, float l2,
+                              float momentum, hipStream_t stream) {
+  SgdArgs a;
+  a.params = params;
+  a.mom = mom;
+  a.n_params = F + 1;
+  a.n_pen = F;
+  a.lr = lr;
+  a.inv_n = inv_n;
+  a.l2 = l2;
+  a.momentum = momentum;
+  train_binary_impl(dt, X, y, params, params + F, B, F, grad_out, workspace, ws_bytes, stream, &a);
 }
 
 size_t train_small_workspace(int64_t B, int F, int K) {

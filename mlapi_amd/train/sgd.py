@@ -83,6 +83,19 @@ class BinarySGDTrainer:
 
     def step(self, X: torch.Tensor, y: torch.Tensor) -> None:
         B = X.shape[0]
+        if self.on_gpu and self.info.world == 1:
+            # one replica: gradient + reduce + update fused into 2 launches (no all-reduce between)
+            from mlapi_amd.ops.linear import _DT, _check, _stream
+
+            _check(X, y)
+            ws = self._workspace(B)
+            self._C.train_binary_step(_DT[X.dtype], X.data_ptr(), y.data_ptr(), self.params.data_ptr(),
+                                      0 if self.mom is None else self.mom.data_ptr(), B, self.F,
+                                      self.grad.data_ptr(), ws.data_ptr(), ws.numel(), float(self.lr), 1.0 / B,
+                                      float(self.l2), float(self.momentum), _stream())
+            self.steps += 1
+            self._n_seen = B
+            return
         if self.on_gpu:
             from mlapi_amd.ops.linear import sgd_update, train_binary_grad
 

@@ -193,3 +193,24 @@ def test_ops_reject_cpu_tensors():
     with pytest.raises(ValueError):
         ops.linear_small(torch.zeros(2, 4, dtype=torch.float64), torch.zeros(3, 4, dtype=torch.float64),
                          torch.zeros(3, dtype=torch.float64), Kind.MULTINOMIAL)
+
+
+def test_train_binary_step_fused_equals_unfused():
+    from mlapi_amd._native import C
+
+    B, F = 50000, 256
+    X = _rand((B, F), torch.bfloat16, 30)
+    y = (torch.rand(B, device=DEV) > 0.5).float()
+    p1 = _rand((F + 1,), torch.float32, 31, scale=0.01)
+    p2 = p1.clone()
+    m1 = torch.zeros_like(p1)
+    m2 = torch.zeros_like(p2)
+    ws = torch.empty(C().train_binary_workspace(B, F), dtype=torch.uint8, device=DEV)
+    g1 = torch.empty(F + 3, device=DEV)
+    for _ in range(3):
+        C().train_binary_step(2, X.data_ptr(), y.data_ptr(), p1.data_ptr(), m1.data_ptr(), B, F, g1.data_ptr(),
+                              ws.data_ptr(), ws.numel(), 0.3, 1.0 / B, 1e-3, 0.9, torch.cuda.current_stream().cuda_stream)
+        g2 = ops.train_binary_grad(X, y, p2[:F], p2[F:])
+        ops.sgd_update(p2, g2, F, 0.3, 1.0 / B, 1e-3, 0.9, m2)
+    torch.cuda.synchronize()
+    assert torch.equal(p1, p2) and torch.equal(g1, g2)
