@@ -79,28 +79,31 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
                                                            int32_t* __restrict__ out_idx, float* __restrict__ out_p,
                                                            unsigned int* __restrict__ counters,
                                                            float4* __restrict__ partials, float* __restrict__ Z) {
+  // Everything below is compile-time shaped: F == KS * 32 exactly (the wrapper pads other F).
+  // No runtime guard may sit on a load: hipcc then branches around each load and waits vmcnt(0)
+  // per element, serializing the W stream (seen in the v2 ISA; cdna_hip_programming.md S5 trap c).
   constexpr int ROWS_PER_WAVE = 16 * NT;
   constexpr int ROWS_PER_BLOCK = 4 * ROWS_PER_WAVE;
-  constexpr int MAX_ROW_BYTES = KS * 64;              // F * 2 bytes
-  constexpr int BUF_BYTES = CLASS_CHUNK * MAX_ROW_BYTES;
-  constexpr int PIECES = BUF_BYTES / 16 / 256;         // 16-byte pieces per thread per chunk (upper bound)
+  constexpr int F_ = KS * 32;
+  constexpr int ROW_BYTES = F_ * 2;
+  constexpr int NCH = F_ / 8;                          // 16-byte chunks per W row
+  constexpr int SWZ = NCH >= 16 ? 15 : NCH - 1;
+  constexpr int BUF_BYTES = CLASS_CHUNK * ROW_BYTES;
+  constexpr int PIECES = CLASS_CHUNK * NCH / 256;      // 16-byte pieces per thread per chunk (== KS)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF_BYTES + 16];
   int* const flag = reinterpret_cast<int*>(smem + 2 * BUF_BYTES);
+  (void)F;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int q = lane >> 4;
   const int col = lane & 15;
-  const int ksr = F / 32;
-  const int row_bytes = F * 2;
-  const int nch = F / 8;                               // 16-byte chunks per W row
-  const int swz_mask = (nch & -nch) >= 16 ? 15 : (nch & -nch) - 1;
   const bool ovr = kind == KIND_OVR;
   const int64_t row0 = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wave * ROWS_PER_WAVE;
   const int c_begin = blockIdx.y * classes_per_split;
   const int c_end = min(K, c_begin + classes_per_split);
-  const int pieces = CLASS_CHUNK * nch;                // actual pieces per chunk
+  const int c_last = c_begin + ((c_end - 1 - c_begin) / CLASS_CHUNK) * CLASS_CHUNK;  // last chunk start
 
   // ---- X fragments for the whole feature range, straight to registers (issued first)
   bf16x8_t xf[NT][KS];
@@ -108,32 +111,26 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
   for (int t = 0; t < NT; ++t) {
     int64_t r = row0 + t * 16 + col;
     r = r < B ? r : B - 1;
-    const uint16_t* xr = X + r * F + 8 * q;
+    const uint16_t* xr = X + r * F_ + 8 * q;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      xf[t][ks] = ks < ksr ? *reinterpret_cast<const bf16x8_t*>(xr + ks * 32) : bf16x8_t{};
+    for (int ks = 0; ks < KS; ++ks) xf[t][ks] = *reinterpret_cast<const bf16x8_t*>(xr + ks * 32);
   }
 
   // ---- W chunk staging: global -> registers (issue early) -> LDS (write late). Plain unrolled
-  // code, not lambdas: a lambda capturing `stage` by reference forces it into scratch memory.
+  // code with ext_vector registers: a lambda capture or HIP_vector_type array goes to scratch.
   u32x4_t stage[PIECES];
-#define MLAPI_LOAD_CHUNK(C0)                                                         \
-  _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                               \
-    const int p = tid + i * 256;                                                     \
-    if (p < pieces) {                                                                \
-      const int r = p / nch, ch = p % nch;                                           \
-      int cls = (C0) + r;                                                            \
-      cls = cls < K ? cls : K - 1;                                                   \
-      stage[i] = *reinterpret_cast<const u32x4_t*>(W + (int64_t)cls * F + ch * 8);  \
-    }                                                                                \
+#define MLAPI_LOAD_CHUNK(C0)                                                             \
+  _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                                   \
+    const int p = tid + i * 256;                                                         \
+    const int r = p / NCH, ch = p % NCH;                                                 \
+    const int cls = min((C0) + r, K - 1);                                                \
+    stage[i] = *reinterpret_cast<const u32x4_t*>(W + (int64_t)cls * F_ + ch * 8);        \
   }
-#define MLAPI_WRITE_CHUNK(BUF)                                                                         \
-  _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                                                 \
-    const int p = tid + i * 256;                                                                       \
-    if (p < pieces) {                                                                                  \
-      const int r = p / nch, ch = p % nch;                                                             \
-      *reinterpret_cast<u32x4_t*>(smem + (BUF) * BUF_BYTES + lds_off(r, ch, row_bytes, swz_mask)) = stage[i]; \
-    }                                                                                                  \
+#define MLAPI_WRITE_CHUNK(BUF)                                                                   \
+  _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                                           \
+    const int p = tid + i * 256;                                                                 \
+    const int r = p / NCH, ch = p % NCH;                                                         \
+    *reinterpret_cast<u32x4_t*>(smem + (BUF) * BUF_BYTES + lds_off(r, ch, ROW_BYTES, SWZ)) = stage[i]; \
   }
 
   RowState st[NT];
@@ -146,10 +143,16 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
 
   int buf = 0;
   for (int c0 = c_begin; c0 < c_end; c0 += CLASS_CHUNK) {
-    const bool has_next = c0 + CLASS_CHUNK < c_end;
-    if (has_next) {
-      MLAPI_LOAD_CHUNK(c0 + CLASS_CHUNK)
-    }
+    // Next chunk's loads go out before this chunk's MFMAs. On the last chunk the (valid) last
+    // chunk address is re-loaded into the idle buffer instead of branching around the loads.
+    const int c_next = min(c0 + CLASS_CHUNK, c_last);
+    MLAPI_LOAD_CHUNK(c_next)
+    // bias for this chunk's classes, also loaded unconditionally (clamped index, masked value)
+    float bv[4][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[mt][r] = bias[min(c0 + mt * 16 + q * 4 + r, K - 1)];
 
     f32x4_t acc[NT][4];
 #pragma unroll
@@ -159,28 +162,18 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
     const unsigned char* wb = smem + buf * BUF_BYTES;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      if (ks < ksr) {
-        bf16x8_t wf[4];
+      bf16x8_t wf[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        wf[mt] = *reinterpret_cast<const bf16x8_t*>(wb + lds_off(mt * 16 + col, ks * 4 + q, ROW_BYTES, SWZ));
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
-          wf[mt] = *reinterpret_cast<const bf16x8_t*>(wb + lds_off(mt * 16 + col, ks * 4 + q, row_bytes, swz_mask));
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt)
-            acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt], xf[t][ks], acc[t][mt], 0, 0, 0);
-      }
+          acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt], xf[t][ks], acc[t][mt], 0, 0, 0);
     }
 
     // epilogue for this chunk: lane owns classes c0 + mt*16 + q*4 + r of batch row (t, col)
-    float bv[4][4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int cls = c0 + mt * 16 + q * 4 + r;
-        bv[mt][r] = cls < c_end ? bias[cls] : 0.f;
-      }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       if constexpr (MODE == 1) {
@@ -223,9 +216,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
         S.s += add;
       }
     }
-    if (has_next) {
-      MLAPI_WRITE_CHUNK(buf ^ 1)
-    }
+    MLAPI_WRITE_CHUNK(buf ^ 1)
     __syncthreads();
     buf ^= 1;
   }
@@ -333,7 +324,8 @@ Plan make_plan(int64_t B, int K) {
 template <int MODE>
 void launch_mode(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind, int32_t* out_idx,
                  float* out_p, void* ws, float* Z, const Plan& plan, hipStream_t stream) {
-  if (F % 32 != 0 || F > 512) throw std::invalid_argument("gemm_softmax: F must be a multiple of 32 and <= 512");
+  if (F != 32 && F != 64 && F != 128 && F != 256 && F != 512)
+    throw std::invalid_argument("gemm_softmax: F must be 32, 64, 128, 256 or 512 (pad other widths)");
   const dim3 grid((unsigned)plan.row_blocks, (unsigned)plan.splits);
   auto x = static_cast<const uint16_t*>(X);
   auto w = static_cast<const uint16_t*>(W);
@@ -348,11 +340,13 @@ void launch_mode(const void* X, const void* W, const float* b, int64_t B, int F,
   else                               \
     MLAPI_GEMM_LAUNCH(KSV, 1);
   const int ks = F / 32;
-  if (ks <= 2) {
+  if (ks == 1) {
+    MLAPI_GEMM_NT(1)
+  } else if (ks == 2) {
     MLAPI_GEMM_NT(2)
-  } else if (ks <= 4) {
+  } else if (ks == 4) {
     MLAPI_GEMM_NT(4)
-  } else if (ks <= 8) {
+  } else if (ks == 8) {
     MLAPI_GEMM_NT(8)
   } else {
     MLAPI_GEMM_NT(16)

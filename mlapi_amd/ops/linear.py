@@ -65,6 +65,15 @@ def gemv_binary(X: torch.Tensor, w: torch.Tensor, bias: float, kind: int = Kind.
     return idx, p
 
 
+_GEMM_F = (32, 64, 128, 256, 512)
+
+
+def _pad_cols(t: torch.Tensor) -> torch.Tensor:
+    F = t.shape[1]
+    Fp = next(f for f in _GEMM_F if f >= F)
+    return torch.nn.functional.pad(t, (0, Fp - F)).contiguous()
+
+
 class GemmSoftmax:
     """Multiclass predict with a cached workspace (capture-safe launches after construction)."""
 
@@ -81,8 +90,11 @@ class GemmSoftmax:
             raise TypeError("gemm_softmax: X, W bf16 and b f32")
         B, F = X.shape
         K = W.shape[0]
-        if F % 32 or F > 512 or W.shape[1] != F or b.numel() != K:
-            raise ValueError("gemm_softmax: need F % 32 == 0, F <= 512 and matching W/b")
+        if F > 512 or W.shape[1] != F or b.numel() != K:
+            raise ValueError("gemm_softmax: need F <= 512 and matching W/b")
+        if F not in _GEMM_F:  # kernels are instantiated for exact widths: zero-pad the rest
+            X, W = _pad_cols(X), _pad_cols(W)
+            F = X.shape[1]
         need = C().gemm_softmax_workspace(B, K, F)
         if need > self.ws.numel():
             self.ws = torch.zeros(need, dtype=torch.uint8, device=X.device)
@@ -100,6 +112,8 @@ def gemm_softmax(X, W, b, kind: int = Kind.MULTINOMIAL):
 
 def gemm_logits(X, W, b) -> torch.Tensor:
     _check(X, W, b)
+    if X.shape[1] not in _GEMM_F:
+        X, W = _pad_cols(X), _pad_cols(W)
     B, F = X.shape
     K = W.shape[0]
     Z = torch.empty(B, K, dtype=torch.float32, device=X.device)
