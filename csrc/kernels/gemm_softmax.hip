@@ -113,7 +113,8 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
     r = r < B ? r : B - 1;
     const uint16_t* xr = X + r * F_ + 8 * q;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) xf[t][ks] = *reinterpret_cast<const bf16x8_t*>(xr + ks * 32);
+    for (int ks = 0; ks < KS; ++ks)  // X is streamed once: non-temporal, keep the L2 for W
+      xf[t][ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + ks * 32));
   }
 
   // ---- W chunk staging: global -> registers (issue early) -> LDS (write late). Plain unrolled
@@ -295,7 +296,8 @@ int g_force_nt = 0, g_force_splits = 0;
 Plan make_plan(int64_t B, int K) {
   Plan p;
   const int64_t rb2 = (B + 127) / 128;
-  p.nt = rb2 >= 512 ? 2 : 1;  // large batches: 32 rows/wave (W re-read from L2 half as often)
+  p.nt = 1;  // measured (tools/gemm_plan_sweep.py): NT=2 hits 256 VGPRs -> 1 wave/SIMD and loses at every B
+  (void)rb2;
   if (g_force_nt == 1 || g_force_nt == 2) p.nt = g_force_nt;
   if (g_force_splits > 0) {
     const int rows_per_block = 64 * p.nt;
@@ -309,7 +311,10 @@ Plan make_plan(int64_t B, int K) {
   const int rows_per_block = 64 * p.nt;
   p.row_blocks = (B + rows_per_block - 1) / rows_per_block;
   const int chunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
-  int64_t want = (256 + p.row_blocks - 1) / p.row_blocks;  // aim for >= 256 blocks (1 per CU)
+  // measured best: B=1024 -> 8 splits (128 blocks), B=8192 -> 4 (512 blocks): fill the chip, but
+  // keep >= 2 chunks per block so the LDS double buffer overlaps (the split merge is not free).
+  int64_t want = (512 + p.row_blocks - 1) / p.row_blocks;
+  if (want > chunks / 2) want = chunks / 2;
   int splits = (int)(want < 1 ? 1 : (want > chunks ? chunks : want));
   const int chunks_per_split = (chunks + splits - 1) / splits;
   p.classes_per_split = chunks_per_split * CLASS_CHUNK;
