@@ -1,0 +1,115 @@
+"""Training: L-BFGS parity with sklearn, estimator API, notebook CLI, SGD checkpoint/resume."""
+import json
+import os
+import pickle
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+ENV = {**os.environ, "PYTHONPATH": str(ROOT)}
+
+
+def test_lbfgs_binary_matches_sklearn(iris_data):
+    from sklearn.linear_model import LogisticRegression as SK
+
+    from mlapi_amd.train.lbfgs import fit_logistic_lbfgs
+
+    Xtr, _, ytr, _ = iris_data
+    yb = (ytr == "Iris-versicolor")
+    sk = SK().fit(Xtr, yb)
+    m = fit_logistic_lbfgs(Xtr, yb)
+    np.testing.assert_allclose(m.W, sk.coef_, atol=1e-6)
+    np.testing.assert_allclose(m.b, sk.intercept_, atol=1e-6)
+
+
+def test_lbfgs_multinomial_reproduces_notebook(iris_data):
+    """`Logistic Regression.ipynb:13`: hold-out accuracy 0.9666666666666667."""
+    from sklearn.linear_model import LogisticRegression as SK
+
+    from mlapi_amd.models.estimator import LogisticRegression
+
+    Xtr, Xte, ytr, yte = iris_data
+    ours = LogisticRegression(device="cpu").fit(Xtr, ytr)
+    sk = SK().fit(Xtr, ytr)
+    assert ours.score(Xte, yte) == 0.9666666666666667
+    np.testing.assert_array_equal(ours.predict(Xte), sk.predict(Xte))
+    np.testing.assert_allclose(ours.predict_proba(Xte), sk.predict_proba(Xte), atol=2e-3)
+    assert list(ours.classes_) == ["Iris-setosa", "Iris-versicolor", "Iris-virginica"]
+
+
+def test_lbfgs_ovr(iris_data):
+    from sklearn.linear_model import LogisticRegression as SK
+    from sklearn.multiclass import OneVsRestClassifier
+
+    from mlapi_amd.train.lbfgs import fit_logistic_lbfgs
+
+    Xtr, Xte, ytr, _ = iris_data
+    m = fit_logistic_lbfgs(Xtr, ytr, multi_class="ovr")
+    sk = OneVsRestClassifier(SK()).fit(Xtr, ytr)
+    np.testing.assert_array_equal(m.predict(Xte), sk.predict(Xte))
+
+
+def test_estimator_save_formats(tmp_path, iris_data):
+    from mlapi_amd.models.estimator import LogisticRegression
+
+    Xtr, Xte, ytr, yte = iris_data
+    clf = LogisticRegression(device="cpu").fit(Xtr, ytr)
+    clf.save(str(tmp_path / "a.pkl"))
+    clf.save(str(tmp_path / "a.safetensors"), format="native")
+    for p in ("a.pkl", "a.safetensors"):
+        assert LogisticRegression.load(str(tmp_path / p), device="cpu").score(Xte, yte) == clf.score(Xte, yte)
+    sk = pickle.loads((tmp_path / "a.pkl").read_bytes())  # our own file, readable by real sklearn
+    np.testing.assert_array_equal(sk.predict(Xte), clf.predict(Xte))
+
+
+def test_cli_iris_prints_reference_score(tmp_path):
+    out = subprocess.run([sys.executable, "-m", "mlapi_amd.train", "iris", "--device", "cpu"], cwd=tmp_path, env=ENV,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().splitlines()[-1] == "0.9666666666666667"
+    assert (tmp_path / "LRClassifier.pkl").exists()
+
+
+def test_cli_sgd_checkpoint_resume(tmp_path):
+    ck = str(tmp_path / "s.safetensors")
+    base = [sys.executable, "-m", "mlapi_amd.train", "sgd", "--features", "16", "--rows-per-rank", "8000",
+            "--batch", "1000", "--log-every", "1000", "--ckpt", ck, "--ckpt-every", "20"]
+    env = {**ENV, "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""}
+    full = subprocess.run(base + ["--steps", "40"], env=env, capture_output=True, text=True, timeout=300)
+    assert full.returncode == 0, full.stderr
+    final_full = json.loads(full.stdout.strip().splitlines()[-1])
+    os.remove(ck)
+    a = subprocess.run(base + ["--steps", "20"], env=env, capture_output=True, text=True, timeout=300)
+    assert a.returncode == 0, a.stderr
+    b = subprocess.run(base + ["--steps", "40", "--resume"], env=env, capture_output=True, text=True, timeout=300)
+    assert b.returncode == 0 and "resumed" in b.stdout, b.stdout + b.stderr
+    final_resumed = json.loads(b.stdout.strip().splitlines()[-1])
+    assert final_resumed["final_loss"] == pytest.approx(final_full["final_loss"], rel=1e-6)
+
+
+@pytest.mark.gpu
+def test_lbfgs_gpu_kernel_path_matches_cpu(iris_data):
+    import torch
+
+    from mlapi_amd.train.lbfgs import fit_logistic_lbfgs
+
+    Xtr, Xte, ytr, yte = iris_data
+    cpu = fit_logistic_lbfgs(Xtr, ytr)
+    gpu = fit_logistic_lbfgs(Xtr, ytr, device=torch.device("cuda", 0))
+    np.testing.assert_allclose(gpu.W, cpu.W, atol=1e-6)
+    assert gpu.score(Xte, yte) == 0.9666666666666667
+
+
+@pytest.mark.gpu
+def test_estimator_gpu_predict_and_sgd(iris_data):
+    from mlapi_amd.models.estimator import LogisticRegression
+
+    Xtr, Xte, ytr, yte = iris_data
+    clf = LogisticRegression(device="cuda").fit(Xtr, ytr)
+    assert clf.score(Xte, yte) == 0.9666666666666667
+    sgd = LogisticRegression(device="cuda", solver="sgd").fit(Xtr, ytr == "Iris-setosa")
+    assert sgd.score(Xte, yte == "Iris-setosa") == 1.0
