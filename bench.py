@@ -83,8 +83,12 @@ def bench_serve(args, info):
             w = lg.run(args.warmup * args.reqs_per_conn, False)
             if w["failed"]:
                 raise RuntimeError(f"warmup failed: {w}")
+        from mlapi_amd.utils.threads import cpu_by_group, utilization
+
         s0 = srv.runtime.handle.stats()
+        c0 = cpu_by_group()
         elapsed, res = _timed(info, lambda: lg.run(args.steps * args.reqs_per_conn, True))
+        cpu_util = utilization(c0, cpu_by_group(), elapsed)
         s1 = srv.runtime.handle.stats()
         lg.close()
         if res["failed"] or res["status_counts"].get(200, 0) != args.steps * args.reqs_per_conn * args.conns:
@@ -113,6 +117,8 @@ def bench_serve(args, info):
         "req_per_s_batch1_per_rank": float(np.min(per_rank[:, 4])),
         "mean_gpu_batch_rows": float(np.mean(per_rank[:, 5])),
         "backend": srv.runtime.handle.backend,
+        "cpu_cores_busy_rank0": cpu_util,
+        "threads": {"io": args.io_threads, "loadgen": args.client_threads},
         "requests_per_step": args.reqs_per_conn * args.conns * info.world,
         "baseline_note": "reference uvicorn+sklearn, 1 worker, c=64: 1494 req/s, p50 41.8 ms; c=1 p50 0.881 ms",
     }

@@ -21,6 +21,8 @@
 #include <stdexcept>
 #include <thread>
 
+#include <pthread.h>
+
 namespace mlapi {
 
 namespace {
@@ -105,6 +107,7 @@ LoadgenResult Loadgen::run(int64_t requests_per_conn, bool record) {
   std::atomic<int> failed{0};
   const int64_t t0 = mono_ns();
   auto worker = [&](int ti) {
+    pthread_setname_np(pthread_self(), "mlapi-loadgen");
     const int ep = epoll_create1(EPOLL_CLOEXEC);
     std::vector<LgConn*> mine;
     for (int i = ti; i < nc; i += threads_) mine.push_back(conns_[i].get());

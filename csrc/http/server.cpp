@@ -369,9 +369,29 @@ class IoThread : public Sink {
     }
   }
 
+  void flush_submits() {
+    if (pend_tags_.empty()) return;
+    const int n = (int)pend_tags_.size();
+    if (srv_->engine()->submit_many(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), this) != n) {
+      for (uint64_t id : pend_tags_) {  // engine stopping: answer 500 now
+        auto it = conns_.find(id);
+        if (it == conns_.end()) continue;
+        it->second->waiting = false;
+        internal_error(it->second.get());
+        flush(it->second.get());
+      }
+    }
+    pend_x_.clear();
+    pend_tags_.clear();
+  }
+
   void loop() {
+    char name[16];
+    snprintf(name, sizeof name, "mlapi-io-%d", index_);
+    pthread_setname_np(pthread_self(), name);
     epoll_event evs[256];
     while (!stop_.load()) {
+      flush_submits();
       const int n = epoll_wait(epfd_, evs, 256, 200);
       for (int i = 0; i < n; ++i) {
         const uint64_t id = evs[i].data.u64;
@@ -727,12 +747,10 @@ class IoThread : public Sink {
       if (path == cfg.predict_path && json_ctype(ctype) && nfeat_ > 0) {
         double x[256];
         if (nfeat_ <= 256 && parse_predict_body(body.data(), body.size(), cfg.feature_names, x)) {
-          Engine* eng = srv_->engine();
+          // queued locally; the whole epoll round goes to the engine in one submit_many()
           c->waiting = true;
-          if (!eng->submit(x, (int)nfeat_, c->id, this)) {
-            c->waiting = false;
-            internal_error(c);
-          }
+          pend_x_.insert(pend_x_.end(), x, x + nfeat_);
+          pend_tags_.push_back(c->id);
           n_fast.fetch_add(1, std::memory_order_relaxed);
           return 1;
         }
@@ -784,6 +802,8 @@ class IoThread : public Sink {
   std::mutex mu_;
   std::vector<FastBatch> fast_;
   std::vector<SlowResp> slow_;
+  std::vector<double> pend_x_;      // fast-path rows parsed in this epoll round (IO thread only)
+  std::vector<uint64_t> pend_tags_;
   std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns_;
   uint64_t next_id_ = 16;
 };

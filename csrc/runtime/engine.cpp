@@ -190,17 +190,26 @@ std::shared_ptr<const Model> Engine::model() const {
 }
 
 bool Engine::submit(const double* x, int nf, uint64_t tag, Sink* sink) {
-  if (nf < 0 || nf > cfg_.max_features) return false;
+  return submit_many(x, 1, nf, &tag, sink) == 1;
+}
+
+// One lock acquisition for a whole group of requests (an IO thread submits everything it parsed
+// in one epoll round), and a futex wake only when the batcher is actually asleep: at high load
+// the batcher is busy launching and the notify would be a wasted syscall per request.
+int Engine::submit_many(const double* X, int n, int nf, const uint64_t* tags, Sink* sink) {
+  if (nf < 0 || nf > cfg_.max_features || n <= 0) return 0;
   const int64_t t = now_ns();
+  bool wake;
   {
     std::lock_guard<std::mutex> lk(q_mu_);
-    if (stopping_) return false;
-    const int32_t off = (int32_t)q_x_.size();
-    q_x_.insert(q_x_.end(), x, x + nf);
-    q_meta_.push_back(Meta{tag, sink, t, nf, off});
+    if (stopping_) return 0;
+    int32_t off = (int32_t)q_x_.size();
+    q_x_.insert(q_x_.end(), X, X + (size_t)n * nf);
+    for (int i = 0; i < n; ++i, off += nf) q_meta_.push_back(Meta{tags[i], sink, t, nf, off});
+    wake = batcher_sleeping_;
   }
-  q_cv_.notify_one();
-  return true;
+  if (wake) q_cv_.notify_one();
+  return n;
 }
 
 namespace {
@@ -315,6 +324,7 @@ void Engine::run_cpu(std::vector<Meta>& metas, const std::vector<double>& xs, co
 }
 
 void Engine::batcher_loop() {
+  pthread_setname_np(pthread_self(), "mlapi-batch");
   if (cfg_.device >= 0) (void)hipSetDevice(cfg_.device);
   std::vector<Meta> metas;
   std::vector<double> xs;
@@ -323,12 +333,14 @@ void Engine::batcher_loop() {
   for (;;) {
     {
       std::unique_lock<std::mutex> lk(q_mu_);
+      batcher_sleeping_ = true;
       q_cv_.wait(lk, [&] { return stopping_ || !q_meta_.empty(); });
       if (q_meta_.empty() && stopping_) break;
       if (cfg_.max_wait_us > 0 && (int)q_meta_.size() < cfg_.max_batch && !stopping_) {
         q_cv_.wait_for(lk, std::chrono::microseconds(cfg_.max_wait_us),
                        [&] { return stopping_ || (int)q_meta_.size() >= cfg_.max_batch; });
       }
+      batcher_sleeping_ = false;
       metas.swap(q_meta_);
       xs.swap(q_x_);
       q_meta_.clear();
@@ -410,6 +422,7 @@ void Engine::batcher_loop() {
 }
 
 void Engine::completer_loop() {
+  pthread_setname_np(pthread_self(), "mlapi-compl");
   (void)hipSetDevice(cfg_.device);
   std::vector<int32_t> st;
   std::vector<double> pd;

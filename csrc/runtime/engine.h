@@ -108,6 +108,8 @@ class Engine {
 
   // Thread-safe. Returns false if the engine is stopping or nf exceeds max_features.
   bool submit(const double* x, int nf, uint64_t tag, Sink* sink);
+  // n rows (row-major, nf features each) under one lock; returns how many were accepted (0 or n).
+  int submit_many(const double* X, int n, int nf, const uint64_t* tags, Sink* sink);
   // Blocking convenience API (tests / bulk scoring through the batcher).
   void predict(const double* X, int64_t B, int F, int32_t* idx, double* p, int32_t* status);
 
@@ -160,6 +162,7 @@ class Engine {
   std::vector<Meta> q_meta_;
   std::vector<double> q_x_;
   bool stopping_ = false;
+  bool batcher_sleeping_ = false;  // guarded by q_mu_: submit wakes the batcher only if true
 
   // GPU slots
   hipStream_t stream_ = nullptr;
