@@ -162,6 +162,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("X"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"), py::arg("K"), py::arg("Z"),
       py::arg("stream") = 0);
   m.def("train_binary_workspace", &train_binary_workspace);
+  m.def("train_binary_set_max_blocks", &train_binary_set_max_blocks, py::arg("n") = 0);
   m.def(
       "train_binary_grad",
       [](int dt, uintptr_t X, uintptr_t y, uintptr_t w, uintptr_t b, int64_t B, int F, uintptr_t out, uintptr_t ws,

@@ -36,6 +36,7 @@ void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B,
 // [loss_sum, n_correct] into per-block slabs, then reduce_slabs() folds them into out[F + 3]:
 // out = [gW(F) | gb | loss_sum | n_correct]  (sums over the batch, not means).
 size_t train_binary_workspace(int64_t B, int F);
+void train_binary_set_max_blocks(int n);  // benchmark hook: grid cap of the gradient kernel (0 = default)
 void launch_train_binary_grad(int dt, const void* X, const float* y, const float* w, float bias_unused,
                               const float* bptr, int64_t B, int F, float* out, void* workspace, size_t ws_bytes,
                               hipStream_t stream);

@@ -297,9 +297,12 @@ BinPlan bin_plan(int chunks) {
   return {0, 0, 0, 0};
 }
 
+int g_train_max_blocks = 0;  // benchmark override (train_binary_set_max_blocks); 0 = default
+
 int64_t bin_blocks(int64_t B, const BinPlan& p) {
   int64_t blocks = (B + p.rows_per_block - 1) / p.rows_per_block;
-  const int64_t cap = 256;  // one fat block per CU: enough bytes in flight, few slabs to reduce
+  // Grid cap: more blocks = more bytes in flight (HBM-bound) but more slabs to reduce.
+  const int64_t cap = g_train_max_blocks > 0 ? g_train_max_blocks : 1024;
   return blocks < 1 ? 1 : (blocks > cap ? cap : blocks);
 }
 
@@ -473,8 +476,12 @@ __global__ __launch_bounds__(256) void sgd_update_kernel(float* __restrict__ p, 
 
 }  // namespace
 
+void train_binary_set_max_blocks(int n) { g_train_max_blocks = n; }
+
 size_t train_binary_workspace(int64_t B, int F) {
-  return (size_t)256 * 4 * (size_t)(F + 3) * sizeof(float);  // upper bound: cap blocks
+  (void)B;
+  const int64_t cap = g_train_max_blocks > 0 ? g_train_max_blocks : 1024;
+  return (size_t)(cap > 4096 ? cap : 4096) * (size_t)(F + 3) * sizeof(float);  // upper bound on slabs
 }
 
 namespace {
