@@ -18,6 +18,7 @@
 #include "mlapi/common.h"
 #include "mlapi/kernels.h"
 #include "mlapi/device.h"
+#include "mlapi/rowreduce.h"
 
 namespace mlapi {
 namespace {
@@ -29,18 +30,22 @@ struct Chunk;  // 16 bytes of one row
 template <>
 struct Chunk<uint16_t> {
   static constexpr int N = 8;
-  __device__ static __forceinline__ float dot(const uint4& x, const uint4& w, float acc) {
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x.x), __builtin_bit_cast(bf16x2_t, w.x), acc, false);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x.y), __builtin_bit_cast(bf16x2_t, w.y), acc, false);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x.z), __builtin_bit_cast(bf16x2_t, w.z), acc, false);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x.w), __builtin_bit_cast(bf16x2_t, w.w), acc, false);
+  // Elements are copied out by value before the bit_cast: __builtin_bit_cast of an ext-vector
+  // element lvalue (x.y) reads from the vector's base address in this clang (every component
+  // came out as x.x and the loads shrank to dwords).
+  __device__ static __forceinline__ bf16x2_t bf2(uint32_t u) { return __builtin_bit_cast(bf16x2_t, u); }
+  __device__ static __forceinline__ float dot(const u32x4_t& x, const u32x4_t& w, float acc) {
+    acc = __builtin_amdgcn_fdot2_f32_bf16(bf2(x.x), bf2(w.x), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(bf2(x.y), bf2(w.y), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(bf2(x.z), bf2(w.z), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(bf2(x.w), bf2(w.w), acc, false);
     return acc;
   }
 };
 template <>
 struct Chunk<float> {
   static constexpr int N = 4;
-  __device__ static __forceinline__ float dot(const uint4& x, const uint4& w, float acc) {
+  __device__ static __forceinline__ float dot(const u32x4_t& x, const u32x4_t& w, float acc) {
     acc = fmaf(__uint_as_float(x.x), __uint_as_float(w.x), acc);
     acc = fmaf(__uint_as_float(x.y), __uint_as_float(w.y), acc);
     acc = fmaf(__uint_as_float(x.z), __uint_as_float(w.z), acc);
@@ -49,59 +54,10 @@ struct Chunk<float> {
   }
 };
 
-// Butterfly reduce-scatter of U per-lane partials over groups of LPR lanes.
-// On return p[0] holds the full sum of row slot `slot` for this lane; see slot_of().
-template <int LPR, int U>
-__device__ __forceinline__ float reduce_scatter(float (&p)[U], int lane) {
-  int cnt = U;
-#pragma unroll
-  for (int off = LPR / 2; off >= 1; off >>= 1) {
-    if (cnt > 1) {
-      const int half = cnt / 2;
-      const bool upper = (lane & off) != 0;
-#pragma unroll
-      for (int j = 0; j < half; ++j) {
-        const float mine = upper ? p[j + half] : p[j];
-        const float other = upper ? p[j] : p[j + half];
-        p[j] = mine + __shfl_xor(other, off, 64);
-      }
-      cnt = half;
-    } else {
-      p[0] += __shfl_xor(p[0], off, 64);
-    }
-  }
-  return p[0];
-}
-
-template <int LPR, int U>
-__device__ __forceinline__ int slot_of(int lane) {
-  int slot = 0, cnt = U;
-#pragma unroll
-  for (int off = LPR / 2; off >= 1; off >>= 1) {
-    if (cnt > 1) {
-      const int half = cnt / 2;
-      if (lane & off) slot += half;
-      cnt = half;
-    }
-  }
-  return slot;
-}
-
-// Lowest lane offset used by the reduce-scatter phase; lanes whose bits below it are zero write.
-template <int LPR, int U>
-constexpr int writer_mask() {
-  int cnt = U, last = LPR;
-  for (int off = LPR / 2; off >= 1; off >>= 1) {
-    if (cnt > 1) { cnt /= 2; last = off; }
-  }
-  return last - 1;
-}
-
 template <typename T, int LPR, int CPL, int U>
 __global__ __launch_bounds__(256) void gemv_binary_kernel(const T* __restrict__ X, const T* __restrict__ w, float bias,
                                                           int64_t B, int F, int kind, int32_t* __restrict__ out_idx,
                                                           float* __restrict__ out_p) {
-  static_assert(U <= LPR, "reduce-scatter needs U <= LPR");
   constexpr int RPW = 64 / LPR;  // rows per wave-instruction
   constexpr int NE = Chunk<T>::N;
   const int lane = threadIdx.x & 63;
@@ -110,11 +66,11 @@ __global__ __launch_bounds__(256) void gemv_binary_kernel(const T* __restrict__ 
   const int chunks = F / NE;        // 16-byte chunks per row
   const int64_t ld16 = chunks;      // row stride in uint4
 
-  uint4 wv[CPL];
+  u32x4_t wv[CPL];
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int ch = cl + c * LPR;
-    wv[c] = ch < chunks ? reinterpret_cast<const uint4*>(w)[ch] : make_uint4(0, 0, 0, 0);
+    wv[c] = ch < chunks ? reinterpret_cast<const u32x4_t*>(w)[ch] : u32x4_t{0u, 0u, 0u, 0u};
   }
   const float scale = kind == KIND_BINARY_SOFTMAX ? 2.f : 1.f;
   const int slot = slot_of<LPR, U>(lane % LPR);
@@ -122,21 +78,31 @@ __global__ __launch_bounds__(256) void gemv_binary_kernel(const T* __restrict__ 
 
   const int64_t rows_per_wave_iter = (int64_t)U * RPW;
   const int64_t waves_total = (int64_t)gridDim.x * (blockDim.x / 64);
-  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  const uint4* X16 = reinterpret_cast<const uint4*>(X);
+  const int64_t wave_id =
+      (int64_t)blockIdx.x * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // SGPR
+  const u32x4_t* X16 = reinterpret_cast<const u32x4_t*>(X);
+  // Chunk column per c, clamped into the row (lanes past the last chunk have zero weights).
+  int coff[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) coff[c] = min(cl + c * LPR, chunks - 1);
+  const int64_t stride_u = (int64_t)RPW * ld16;
 
   for (int64_t base = wave_id * rows_per_wave_iter; base < B; base += waves_total * rows_per_wave_iter) {
-    uint4 xv[U][CPL];
+    // Unconditional loads: full iterations (wave-uniform test) use one base pointer + constant
+    // strides, only the final partial one clamps its rows.
+    u32x4_t xv[U][CPL];
+    if (base + rows_per_wave_iter <= B) {
+      const u32x4_t* p = X16 + (base + sub) * ld16;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      int64_t row = base + (int64_t)u * RPW + sub;
-      row = row < B ? row : B - 1;
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        const int ch = cl + c * LPR;
-        xv[u][c] = (CPL == 1 || ch < chunks) ? load_nt16(X16 + row * ld16 + (ch < chunks ? ch : 0))
-                                              : make_uint4(0, 0, 0, 0);
-        if (CPL == 1 && ch >= chunks) xv[u][c] = make_uint4(0, 0, 0, 0);
+        for (int c = 0; c < CPL; ++c) xv[u][c] = __builtin_nontemporal_load(p + u * stride_u + coff[c]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = min(base + (int64_t)u * RPW + sub, B - 1);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) xv[u][c] = __builtin_nontemporal_load(X16 + row * ld16 + coff[c]);
       }
     }
     float part[U];

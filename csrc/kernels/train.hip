@@ -21,6 +21,7 @@
 #include "mlapi/common.h"
 #include "mlapi/kernels.h"
 #include "mlapi/device.h"
+#include "mlapi/rowreduce.h"
 
 namespace mlapi {
 namespace {
@@ -35,7 +36,7 @@ struct TChunk;
 template <>
 struct TChunk<uint16_t> {
   static constexpr int N = 8;
-  __device__ static __forceinline__ void unpack(const uint4& v, float (&o)[8]) {
+  __device__ static __forceinline__ void unpack(const u32x4_t& v, float (&o)[8]) {
     const uint32_t u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -47,50 +48,13 @@ struct TChunk<uint16_t> {
 template <>
 struct TChunk<float> {
   static constexpr int N = 4;
-  __device__ static __forceinline__ void unpack(const uint4& v, float (&o)[4]) {
+  __device__ static __forceinline__ void unpack(const u32x4_t& v, float (&o)[4]) {
     o[0] = __uint_as_float(v.x);
     o[1] = __uint_as_float(v.y);
     o[2] = __uint_as_float(v.z);
     o[3] = __uint_as_float(v.w);
   }
 };
-
-template <int LPR, int U>
-__device__ __forceinline__ float reduce_scatter(float (&p)[U], int lane) {
-  int cnt = U;
-#pragma unroll
-  for (int off = LPR / 2; off >= 1; off >>= 1) {
-    if (cnt > 1) {
-      const int half = cnt / 2;
-      const bool upper = (lane & off) != 0;
-#pragma unroll
-      for (int j = 0; j < half; ++j) {
-        const float mine = upper ? p[j + half] : p[j];
-        const float other = upper ? p[j] : p[j + half];
-        p[j] = mine + __shfl_xor(other, off, 64);
-      }
-      cnt = half;
-    } else {
-      p[0] += __shfl_xor(p[0], off, 64);
-    }
-  }
-  return p[0];
-}
-
-// Lane (within an LPR group) that owns row slot u after reduce_scatter (its low bits are zero).
-template <int LPR, int U>
-__device__ __forceinline__ int owner_of(int u) {
-  int lane = 0, cnt = U;
-#pragma unroll
-  for (int off = LPR / 2; off >= 1; off >>= 1) {
-    if (cnt > 1) {
-      const int half = cnt / 2;
-      if (u >= half) { lane += off; u -= half; }
-      cnt = half;
-    }
-  }
-  return lane;
-}
 
 template <typename T, int LPR, int CPL, int U>
 __global__ __launch_bounds__(256) void train_binary_grad_kernel(const T* __restrict__ X, const float* __restrict__ y,
@@ -101,7 +65,7 @@ __global__ __launch_bounds__(256) void train_binary_grad_kernel(const T* __restr
   constexpr int NE = TChunk<T>::N;
   __shared__ float red[4 * RPW * CPL * LPR * NE + 4 * 3];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform -> SGPR loop control
   const int sub = lane / LPR;
   const int cl = lane % LPR;
   const int chunks = F / NE;
@@ -125,18 +89,44 @@ __global__ __launch_bounds__(256) void train_binary_grad_kernel(const T* __restr
   const int64_t rows_per_wave_iter = (int64_t)U * RPW;
   const int64_t waves_total = (int64_t)gridDim.x * 4;
   const int64_t wave_id = (int64_t)blockIdx.x * 4 + wave;
-  const uint4* X16 = reinterpret_cast<const uint4*>(X);
+
+  // After reduce_scatter every lane of an LPR group holds the complete dot product of ONE row slot
+  // (my_u); the sigmoid / loss / correct epilogue is evaluated once per lane for that slot and only
+  // the scalar gradient g is broadcast back for the dW accumulation (evaluating the epilogue for all
+  // U slots on every lane made the transcendentals, not HBM, the bottleneck).
+  const int my_u = slot_of<LPR, U>(cl);
+  const bool my_owner = cl == owner_of<LPR, U>(my_u);  // one lane per row counts the stats
+  const int group_base = lane - cl;
+
+  // Chunk column of this lane for each c, clamped into the row: lanes past the last chunk re-read a
+  // valid chunk; their forward weights are zero and their dW partials are never written out, so
+  // no per-value masking is needed (a select on the loaded data made hipcc wait for each load
+  // right after issuing it).
+  int coff[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) coff[c] = min(cl + c * LPR, chunks - 1);
+  const u32x4_t* X16 = reinterpret_cast<const u32x4_t*>(X);
+  const int64_t stride_u = (int64_t)RPW * ld16;  // elements of u32x4 between row slots u and u+1
 
   for (int64_t base = wave_id * rows_per_wave_iter; base < B; base += waves_total * rows_per_wave_iter) {
-    uint4 xv[U][CPL];
+    // Loads are unconditional (no per-load guard: a guarded load makes hipcc branch around it and
+    // wait vmcnt(0) per load, which serializes the stream). Full iterations (wave-uniform test)
+    // use one base pointer + constant strides; only the last, partial iteration clamps rows.
+    const int64_t my_row = base + (int64_t)my_u * RPW + sub;
+    const float my_y = y[min(my_row, B - 1)];
+    u32x4_t xv[U][CPL];
+    if (base + rows_per_wave_iter <= B) {
+      const u32x4_t* p = X16 + (base + sub) * ld16;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      int64_t row = base + (int64_t)u * RPW + sub;
-      row = row < B ? row : B - 1;
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        const int ch = cl + c * LPR;
-        xv[u][c] = ch < chunks ? load_nt16(X16 + row * ld16 + ch) : make_uint4(0, 0, 0, 0);
+        for (int c = 0; c < CPL; ++c) xv[u][c] = __builtin_nontemporal_load(p + u * stride_u + coff[c]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = min(base + (int64_t)u * RPW + sub, B - 1);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) xv[u][c] = __builtin_nontemporal_load(X16 + row * ld16 + coff[c]);
       }
     }
     float part[U];
@@ -152,26 +142,30 @@ __global__ __launch_bounds__(256) void train_binary_grad_kernel(const T* __restr
       }
       part[u] = acc;
     }
-    const float zown = reduce_scatter<LPR, U>(part, cl) + bias;
-    const int group_base = lane - cl;
+    // Register barrier: make the packed rows opaque here so the compiler re-unpacks them for the
+    // backward pass instead of keeping U x NE unpacked floats live across the reduction (that
+    // held the kernel at ~200 VGPRs / 2 waves per SIMD).
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < CPL; ++c) asm volatile("" : "+v"(xv[u][c]));
+    const float z = reduce_scatter<LPR, U>(part, cl) + bias;
+    const bool valid = my_row < B;
+    const float yy = valid ? my_y : 0.f;
+    const float g_mine = valid ? __builtin_amdgcn_rcpf(1.f + __expf(-z)) - yy : 0.f;
+    const bool own = valid && my_owner;
+    gb += own ? g_mine : 0.f;
+    loss += own ? fmaxf(z, 0.f) - z * yy + log1pf(__expf(-fabsf(z))) : 0.f;
+    correct += (own && ((z > 0.f) == (yy > 0.5f))) ? 1.f : 0.f;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float z = __shfl(zown, group_base + owner_of<LPR, U>(u), 64);
-      const int64_t row = base + (int64_t)u * RPW + sub;
-      const bool valid = row < B;
-      const float yy = valid ? y[row] : 0.f;
-      const float g = valid ? (1.f / (1.f + __expf(-z)) - yy) : 0.f;
+      const float g = __shfl(g_mine, group_base + owner_of<LPR, U>(u), 64);
 #pragma unroll
       for (int c = 0; c < CPL; ++c) {
         float xe[NE];
         TChunk<T>::unpack(xv[u][c], xe);
 #pragma unroll
         for (int e = 0; e < NE; ++e) gw[c][e] = fmaf(g, xe[e], gw[c][e]);
-      }
-      if (valid && cl == owner_of<LPR, U>(u)) {
-        gb += g;
-        loss += fmaxf(z, 0.f) - z * yy + log1pf(__expf(-fabsf(z)));
-        correct += ((z > 0.f) == (yy > 0.5f)) ? 1.f : 0.f;
       }
     }
   }
@@ -301,8 +295,9 @@ int g_train_max_blocks = 0;  // benchmark override (train_binary_set_max_blocks)
 
 int64_t bin_blocks(int64_t B, const BinPlan& p) {
   int64_t blocks = (B + p.rows_per_block - 1) / p.rows_per_block;
-  // Grid cap: more blocks = more bytes in flight (HBM-bound) but more slabs to reduce.
-  const int64_t cap = g_train_max_blocks > 0 ? g_train_max_blocks : 1024;
+  // Grid cap: more blocks = more bytes in flight (HBM-bound) but more slabs to reduce;
+  // 512 was fastest for 64K..1M rows x 256 bf16 (profiles/r1_train_v2/train_sweep.log).
+  const int64_t cap = g_train_max_blocks > 0 ? g_train_max_blocks : 512;
   return blocks < 1 ? 1 : (blocks > cap ? cap : blocks);
 }
 
@@ -480,7 +475,7 @@ void train_binary_set_max_blocks(int n) { g_train_max_blocks = n; }
 
 size_t train_binary_workspace(int64_t B, int F) {
   (void)B;
-  const int64_t cap = g_train_max_blocks > 0 ? g_train_max_blocks : 1024;
+  const int64_t cap = g_train_max_blocks > 0 ? g_train_max_blocks : 512;
   return (size_t)(cap > 4096 ? cap : 4096) * (size_t)(F + 3) * sizeof(float);  // upper bound on slabs
 }
 

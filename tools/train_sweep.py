@@ -37,6 +37,6 @@ for B in (65536, 262144, 1 << 20):
     for cap in caps:
         t = sorted(times[cap])[2]
         res[f"B{B}_cap{cap}"] = t
-        print(f"B={B:8d} cap={cap:5d}: {t:8.2f} us/step  {B * F * 2 / t / 1e6:7.1f} GB/s  {B / t:8.1f} M samples/s",
+        print(f"B={B:8d} cap={cap:5d}: {t:8.2f} us/step  {B * F * 2 / t / 1e6:7.2f} TB/s  {B / t:8.1f} M samples/s",
               flush=True)
 json.dump(res, open("gpurun_out/train_sweep.json", "w"), indent=1)
