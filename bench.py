@@ -33,6 +33,7 @@ BASELINES = {
     "gemv": 1.00e6,        # rows/s, sklearn binary 1M x 256 predict+proba
     "gemm": 87075.0,       # rows/s, sklearn 1000-class B=1024 F=256
     "train": 3.73e6,       # sample-gradients/s, sklearn lbfgs binary 100k x 256
+    "train_softmax": None,  # no reference number for 1000-class training
 }
 IRIS_LABELS = ["Iris-setosa", "Iris-versicolor", "Iris-virginica"]
 
@@ -191,12 +192,38 @@ def bench_train(args, info):
              "seq_len": 1, "features": F, "parallelism": f"dp{info.world}"})
 
 
+def bench_train_softmax(args, info):
+    """Multiclass (1000-class, F=256) DP SGD: MFMA fwd/grad + hipBLASLt dW + RCCL all-reduce."""
+    from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer, synthetic_multiclass
+
+    F, K, B = 256, 1000, args.softmax_batch
+    nb = max(1, args.shards // 2)
+    X, y = synthetic_multiclass(B * nb, F, K, seed=99 + info.rank, device=info.device)
+    tr = SoftmaxSGDTrainer(F, K, info=info, lr=0.5, l2=1e-5, device=info.device)
+    Xa = tr.prepare(X)
+    del X
+    shards = [(Xa[j * B:(j + 1) * B], y[j * B:(j + 1) * B]) for j in range(nb)]
+
+    def run(n):
+        for s in range(n):
+            tr.step(*shards[s % nb])
+
+    run(args.warmup)
+    elapsed, _ = _timed(info, lambda: run(args.steps))
+    value = info.world * B * args.steps / elapsed
+    flops = 3 * 2 * B * K * tr.F_aug * info.world * args.steps / elapsed  # 2 fwd passes + dW GEMM
+    return ("train_softmax_samples_per_sec", value, "samples/s", elapsed,
+            {"final_loss": tr.last_loss(), "tflops_incl_recompute": flops / 1e12},
+            {"model": f"{K}-class softmax LogisticRegression F={F} (mini-batch SGD)", "global_batch": B * info.world,
+             "seq_len": 1, "features": F, "classes": K, "parallelism": f"dp{info.world}"})
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--mode", default="serve", choices=["serve", "gemv", "gemm", "train"])
+    ap.add_argument("--mode", default="serve", choices=["serve", "gemv", "gemm", "train", "train_softmax"])
     ap.add_argument("--conns", type=int, default=64)
     ap.add_argument("--reqs-per-conn", type=int, default=16)
     ap.add_argument("--client-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
@@ -207,6 +234,7 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--train-batch", type=int, default=1 << 18)
     ap.add_argument("--shards", type=int, default=8)
+    ap.add_argument("--softmax-batch", type=int, default=1 << 16)
     ap.add_argument("--cpu", action="store_true", help="force the CPU backend (testing without a GPU)")
     args = ap.parse_args(argv)
 
@@ -230,13 +258,14 @@ def main(argv=None) -> int:
     if args.mode != "serve" and info.device is None:
         print(f"mode {args.mode} needs a GPU", file=sys.stderr)
         return 2
-    fn = {"serve": bench_serve, "gemv": bench_gemv, "gemm": bench_gemm, "train": bench_train}[args.mode]
+    fn = {"serve": bench_serve, "gemv": bench_gemv, "gemm": bench_gemm, "train": bench_train,
+          "train_softmax": bench_train_softmax}[args.mode]
     metric, value, unit, elapsed, extra, config = fn(args, info)
     if info.is_main:
         line = {
             "metric": metric, "value": value, "unit": unit, "n_gpus": info.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": value / BASELINES[args.mode],
+            "scaling": "weak", "vs_baseline": None if BASELINES[args.mode] is None else value / BASELINES[args.mode],
             "dtype": "fp64" if args.mode == "serve" else "bf16",
             "data": "synthetic (random-init weights, fixed synthetic inputs)", "config": config,
         }

@@ -64,21 +64,64 @@ __device__ __forceinline__ RowState shfl_state(RowState a, int off) {
   return RowState{__shfl_xor(a.m, off, 64), __shfl_xor(a.s, off, 64), __shfl_xor(a.bi, off, 64)};
 }
 
-// LDS byte offset of 16-byte chunk `ch` of class row `r` in a [64][F] bf16 image.
-__device__ __forceinline__ int lds_off(int r, int ch, int row_bytes, int swz_mask) {
-  return r * row_bytes + ((ch ^ (r & swz_mask)) << 4);
+// LDS byte offset of 16-byte chunk `ch` of class row `r` in a [64][NCH * 8] bf16 image. Chunks are
+// XOR-swizzled with the class row inside aligned groups of 16 (conflict-free ds_read_b128 of 16
+// classes at one k-offset); a trailing partial group (F_aug = F + 32 in training: 36, 68, ... chunks)
+// is swizzled within its own power-of-two width so no chunk leaves its row.
+template <int NCH>
+__device__ __forceinline__ int lds_off(int r, int ch, int row_bytes) {
+  constexpr int FULL = NCH & ~15;
+  constexpr int TAIL = NCH - FULL;
+  static_assert((TAIL & (TAIL - 1)) == 0, "chunk tail must be a power of two");
+  const int mask = ch < FULL ? 15 : (TAIL > 0 ? TAIL - 1 : 0);
+  return r * row_bytes + ((ch ^ (r & mask)) << 4);
+}
+// Same, for the fragment reads: chunk = 4 * ks + q with ks compile-time, so the mask folds.
+template <int NCH>
+__device__ __forceinline__ int lds_off_k(int r, int ks, int q, int row_bytes) {
+  constexpr int FULL = NCH & ~15;
+  constexpr int TAIL = NCH - FULL;
+  const int mask = 4 * ks < FULL ? 15 : (TAIL > 0 ? TAIL - 1 : 0);
+  return r * row_bytes + (((4 * ks + q) ^ (r & mask)) << 4);
 }
 
-// KS = F/32 upper bound (registers), NT = 16-row N-tiles per wave, MODE 0 = fused epilogue,
-// MODE 1 = write logits.
+struct GemmArgs {
+  const uint16_t* X;
+  const uint16_t* W;
+  const float* bias;       // MODE 0/1 only (MODE 2/3: intercept folded into W)
+  int64_t B;
+  int K;
+  int kind;
+  int classes_per_split;
+  int32_t* out_idx;        // MODE 0
+  float* out_p;            // MODE 0
+  unsigned int* counters;  // split merge (MODE 0/2)
+  float4* partials;        // split merge (MODE 0/2)
+  float* Z;                // MODE 1
+  const int32_t* y;        // MODE 3: class index per row
+  uint16_t* G;             // MODE 3: bf16 [B, ldg]
+  int64_t ldg;
+  float2* rowstat;         // MODE 2 output / MODE 3 input: {lse, argmax bits}
+  float* stat_slabs;       // MODE 3: [gridDim.y * gridDim.x][2] = {loss_sum, n_correct}
+};
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  const uint32_t lo = __builtin_bit_cast(uint16_t, (__bf16)a);
+  const uint32_t hi = __builtin_bit_cast(uint16_t, (__bf16)b);
+  return lo | (hi << 16);
+}
+
+// KS = F/32 (exact), NT = 16-row N-tiles per wave, MODE: 0 = fused predict epilogue,
+// 1 = write logits, 2 = training row stats, 3 = training gradient (see header).
 template <int KS, int NT, int MODE>
-__global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __restrict__ X,
-                                                           const uint16_t* __restrict__ W,
-                                                           const float* __restrict__ bias, int64_t B, int F, int K,
-                                                           int kind, int classes_per_split,
-                                                           int32_t* __restrict__ out_idx, float* __restrict__ out_p,
-                                                           unsigned int* __restrict__ counters,
-                                                           float4* __restrict__ partials, float* __restrict__ Z) {
+__global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
+  const uint16_t* __restrict__ X = a.X;
+  const uint16_t* __restrict__ W = a.W;
+  const float* __restrict__ bias = a.bias;
+  const int64_t B = a.B;
+  const int K = a.K;
+  const int kind = a.kind;
+  const int classes_per_split = a.classes_per_split;
   // Everything below is compile-time shaped: F == KS * 32 exactly (the wrapper pads other F).
   // No runtime guard may sit on a load: hipcc then branches around each load and waits vmcnt(0)
   // per element, serializing the W stream (seen in the v2 ISA; cdna_hip_programming.md S5 trap c).
@@ -87,12 +130,11 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
   constexpr int F_ = KS * 32;
   constexpr int ROW_BYTES = F_ * 2;
   constexpr int NCH = F_ / 8;                          // 16-byte chunks per W row
-  constexpr int SWZ = NCH >= 16 ? 15 : NCH - 1;
   constexpr int BUF_BYTES = CLASS_CHUNK * ROW_BYTES;
   constexpr int PIECES = CLASS_CHUNK * NCH / 256;      // 16-byte pieces per thread per chunk (== KS)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF_BYTES + 16];
   int* const flag = reinterpret_cast<int*>(smem + 2 * BUF_BYTES);
-  (void)F;
+  float* const red = reinterpret_cast<float*>(smem);  // MODE 3 stats reduction (after the last chunk)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -116,6 +158,21 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
     for (int ks = 0; ks < KS; ++ks)  // X is streamed once: non-temporal, keep the L2 for W
       xf[t][ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + ks * 32));
   }
+  // MODE 3: this lane's rows' label and {lse, argmax} (clamped loads, masked by row < B later)
+  int yl[NT];
+  float lse[NT];
+  int amax[NT];
+  if constexpr (MODE == 3) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int64_t r = min(row0 + t * 16 + col, B - 1);
+      yl[t] = a.y[r];
+      const float2 rs = a.rowstat[r];
+      lse[t] = rs.x;
+      amax[t] = __float_as_int(rs.y);
+    }
+  }
+  float loss_acc = 0.f, correct_acc = 0.f;
 
   // ---- W chunk staging: global -> registers (issue early) -> LDS (write late). Plain unrolled
   // code with ext_vector registers: a lambda capture or HIP_vector_type array goes to scratch.
@@ -127,11 +184,11 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
     const int cls = min((C0) + r, K - 1);                                                \
     stage[i] = *reinterpret_cast<const u32x4_t*>(W + (int64_t)cls * F_ + ch * 8);        \
   }
-#define MLAPI_WRITE_CHUNK(BUF)                                                                   \
-  _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                                           \
-    const int p = tid + i * 256;                                                                 \
-    const int r = p / NCH, ch = p % NCH;                                                         \
-    *reinterpret_cast<u32x4_t*>(smem + (BUF) * BUF_BYTES + lds_off(r, ch, ROW_BYTES, SWZ)) = stage[i]; \
+#define MLAPI_WRITE_CHUNK(BUF)                                                                          \
+  _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                                                  \
+    const int p = tid + i * 256;                                                                        \
+    const int r = p / NCH, ch = p % NCH;                                                                \
+    *reinterpret_cast<u32x4_t*>(smem + (BUF) * BUF_BYTES + lds_off<NCH>(r, ch, ROW_BYTES)) = stage[i]; \
   }
 
   RowState st[NT];
@@ -148,12 +205,13 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
     // chunk address is re-loaded into the idle buffer instead of branching around the loads.
     const int c_next = min(c0 + CLASS_CHUNK, c_last);
     MLAPI_LOAD_CHUNK(c_next)
-    // bias for this chunk's classes, also loaded unconditionally (clamped index, masked value)
+    // bias for this chunk's classes, also loaded unconditionally (clamped index, masked value);
+    // the training modes carry the intercept inside W.
     float bv[4][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bv[mt][r] = bias[min(c0 + mt * 16 + q * 4 + r, K - 1)];
+      for (int r = 0; r < 4; ++r) bv[mt][r] = MODE >= 2 ? 0.f : bias[min(c0 + mt * 16 + q * 4 + r, K - 1)];
 
     f32x4_t acc[NT][4];
 #pragma unroll
@@ -166,7 +224,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
       bf16x8_t wf[4];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
-        wf[mt] = *reinterpret_cast<const bf16x8_t*>(wb + lds_off(mt * 16 + col, ks * 4 + q, ROW_BYTES, SWZ));
+        wf[mt] = *reinterpret_cast<const bf16x8_t*>(wb + lds_off_k<NCH>(mt * 16 + col, ks, q, ROW_BYTES));
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -185,8 +243,30 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int cls = c0 + mt * 16 + q * 4 + r;
-              if (cls < c_end) Z[row * K + cls] = acc[t][mt][r] + bv[mt][r];
+              if (cls < c_end) a.Z[row * K + cls] = acc[t][mt][r] + bv[mt][r];
             }
+        }
+      } else if constexpr (MODE == 3) {
+        const int64_t row = row0 + t * 16 + col;
+        const bool row_ok = row < B;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const int cls0 = c0 + mt * 16 + q * 4;  // 4 consecutive classes -> one 8-byte store
+          float g[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int cls = cls0 + r;
+            const float z = acc[t][mt][r];
+            const bool hot = cls == yl[t];
+            const bool live = row_ok && cls < c_end;
+            const float pr = ovr ? sigmoidf_(z) : __expf(z - lse[t]);
+            g[r] = live ? pr - (hot ? 1.f : 0.f) : 0.f;
+            // softmax CE: lse - z_y (owned by the lane holding class y); OvR: sum of BCE terms
+            const float l = ovr ? fmaxf(z, 0.f) - (hot ? z : 0.f) + log1pf(__expf(-fabsf(z))) : lse[t] - z;
+            loss_acc += (live && (ovr || hot)) ? l : 0.f;
+          }
+          if (row_ok && cls0 < c_end)
+            *reinterpret_cast<uint2*>(a.G + row * a.ldg + cls0) = make_uint2(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]));
         }
       } else {
         float cm = -INFINITY;
@@ -224,7 +304,28 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
 
 #undef MLAPI_LOAD_CHUNK
 #undef MLAPI_WRITE_CHUNK
-  if constexpr (MODE == 0) {
+  if constexpr (MODE == 3) {
+    // correct count: split 0, one lane (q == 0) per row
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      correct_acc += (blockIdx.y == 0 && q == 0 && row0 + t * 16 + col < B && amax[t] == yl[t]) ? 1.f : 0.f;
+    // deterministic block reduction -> slab [split][row block][2]
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      loss_acc += __shfl_xor(loss_acc, off, 64);
+      correct_acc += __shfl_xor(correct_acc, off, 64);
+    }
+    if (lane == 0) {
+      red[wave * 2] = loss_acc;
+      red[wave * 2 + 1] = correct_acc;
+    }
+    __syncthreads();
+    if (tid < 2) {
+      const float v = red[tid] + red[2 + tid] + red[4 + tid] + red[6 + tid];
+      a.stat_slabs[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2 + tid] = v;
+    }
+  }
+  if constexpr (MODE == 0 || MODE == 2) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       RowState S = st[t];
@@ -237,8 +338,12 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
       for (int t = 0; t < NT; ++t) {
         const int64_t row = row0 + t * 16 + col;
         if (q == 0 && row < B) {
-          out_idx[row] = st[t].bi;
-          out_p[row] = ovr ? sigmoidf_(st[t].m) / st[t].s : 1.f / st[t].s;
+          if constexpr (MODE == 0) {
+            a.out_idx[row] = st[t].bi;
+            a.out_p[row] = ovr ? sigmoidf_(st[t].m) / st[t].s : 1.f / st[t].s;
+          } else {
+            a.rowstat[row] = make_float2(st[t].m + __logf(st[t].s), __int_as_float(st[t].bi));
+          }
         }
       }
       return;
@@ -248,7 +353,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
     for (int t = 0; t < NT; ++t) {
       const int64_t row = row0 + t * 16 + col;
       if (q == 0 && row < B)
-        partials[(int64_t)blockIdx.y * B + row] = make_float4(st[t].m, st[t].s, __int_as_float(st[t].bi), 0.f);
+        a.partials[(int64_t)blockIdx.y * B + row] = make_float4(st[t].m, st[t].s, __int_as_float(st[t].bi), 0.f);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
     __syncthreads();
@@ -256,7 +361,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: ROCm 7.2 may drop the fence's own wait
       const unsigned ticket =
-          __hip_atomic_fetch_add(&counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(&a.counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = ticket == gridDim.y - 1;
     }
     __syncthreads();
@@ -264,20 +369,24 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(const uint16_t* __res
     if (tid == 0) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+      __hip_atomic_store(&a.counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
     }
     __syncthreads();
     if (tid < ROWS_PER_BLOCK) {
       const int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + tid;
       if (row < B) {
-        float4 p0 = partials[row];
+        float4 p0 = a.partials[row];
         RowState S{p0.x, p0.y, __float_as_int(p0.z)};
         for (unsigned sp = 1; sp < gridDim.y; ++sp) {  // fixed split order: deterministic
-          const float4 p = partials[(int64_t)sp * B + row];
+          const float4 p = a.partials[(int64_t)sp * B + row];
           S = merge_state(S, RowState{p.x, p.y, __float_as_int(p.z)}, ovr);
         }
-        out_idx[row] = S.bi;
-        out_p[row] = ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s;
+        if constexpr (MODE == 0) {
+          a.out_idx[row] = S.bi;
+          a.out_p[row] = ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s;
+        } else {
+          a.rowstat[row] = make_float2(S.m + __logf(S.s), __int_as_float(S.bi));
+        }
       }
     }
   }
@@ -327,38 +436,76 @@ Plan make_plan(int64_t B, int K) {
 }
 
 template <int MODE>
-void launch_mode(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind, int32_t* out_idx,
-                 float* out_p, void* ws, float* Z, const Plan& plan, hipStream_t stream) {
-  if (F != 32 && F != 64 && F != 128 && F != 256 && F != 512)
-    throw std::invalid_argument("gemm_softmax: F must be 32, 64, 128, 256 or 512 (pad other widths)");
+void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
   const dim3 grid((unsigned)plan.row_blocks, (unsigned)plan.splits);
-  auto x = static_cast<const uint16_t*>(X);
-  auto w = static_cast<const uint16_t*>(W);
-  auto counters = static_cast<unsigned int*>(ws);
-  auto partials = ws ? reinterpret_cast<float4*>(static_cast<unsigned char*>(ws) + COUNTER_BYTES) : nullptr;
-#define MLAPI_GEMM_LAUNCH(KSV, NTV)                                                                              \
-  hipLaunchKernelGGL((gemm_softmax_kernel<KSV, NTV, MODE>), grid, dim3(256), 0, stream, x, w, b, B, F, K, kind, \
-                     plan.classes_per_split, out_idx, out_p, counters, partials, Z)
-#define MLAPI_GEMM_NT(KSV)           \
-  if (plan.nt == 2)                  \
-    MLAPI_GEMM_LAUNCH(KSV, 2);       \
-  else                               \
-    MLAPI_GEMM_LAUNCH(KSV, 1);
+  args.classes_per_split = plan.classes_per_split;
+#define MLAPI_GEMM_LAUNCH(KSV, NTV) \
+  hipLaunchKernelGGL((gemm_softmax_kernel<KSV, NTV, MODE>), grid, dim3(256), 0, stream, args)
   const int ks = F / 32;
-  if (ks == 1) {
-    MLAPI_GEMM_NT(1)
-  } else if (ks == 2) {
-    MLAPI_GEMM_NT(2)
-  } else if (ks == 4) {
-    MLAPI_GEMM_NT(4)
-  } else if (ks == 8) {
-    MLAPI_GEMM_NT(8)
-  } else {
-    MLAPI_GEMM_NT(16)
-  }
+  if constexpr (MODE <= 1) {  // predict / logits: F in {32, 64, 128, 256, 512}
+    if (F != 32 && F != 64 && F != 128 && F != 256 && F != 512)
+      throw std::invalid_argument("gemm_softmax: F must be 32, 64, 128, 256 or 512 (pad other widths)");
+#define MLAPI_GEMM_NT(KSV)       \
+  if (plan.nt == 2)              \
+    MLAPI_GEMM_LAUNCH(KSV, 2);   \
+  else                           \
+    MLAPI_GEMM_LAUNCH(KSV, 1);
+    if (ks == 1) {
+      MLAPI_GEMM_NT(1)
+    } else if (ks == 2) {
+      MLAPI_GEMM_NT(2)
+    } else if (ks == 4) {
+      MLAPI_GEMM_NT(4)
+    } else if (ks == 8) {
+      MLAPI_GEMM_NT(8)
+    } else {
+      MLAPI_GEMM_NT(16)
+    }
 #undef MLAPI_GEMM_NT
+  } else {  // training: F_aug = softmax_train_faug(F) in {64, 128, 160, 288, 544}, NT = 1
+    if (ks == 2) {
+      MLAPI_GEMM_LAUNCH(2, 1);
+    } else if (ks == 4) {
+      MLAPI_GEMM_LAUNCH(4, 1);
+    } else if (ks == 5) {
+      MLAPI_GEMM_LAUNCH(5, 1);
+    } else if (ks == 9) {
+      MLAPI_GEMM_LAUNCH(9, 1);
+    } else if (ks == 17) {
+      MLAPI_GEMM_LAUNCH(17, 1);
+    } else {
+      throw std::invalid_argument("softmax_train: F_aug must be 64, 128, 160, 288 or 544");
+    }
+  }
 #undef MLAPI_GEMM_LAUNCH
   MLAPI_HIP_CHECK(hipGetLastError());
+}
+
+GemmArgs base_args(const void* X, const void* W, int64_t B, int K, int kind) {
+  GemmArgs a{};
+  a.X = static_cast<const uint16_t*>(X);
+  a.W = static_cast<const uint16_t*>(W);
+  a.B = B;
+  a.K = K;
+  a.kind = kind;
+  return a;
+}
+
+struct TrainLayout {
+  Plan plan;
+  size_t partials_off, rowstat_off, slabs_off, total;
+};
+
+TrainLayout train_layout(int64_t B, int K) {
+  TrainLayout L;
+  L.plan = make_plan(B, K);
+  L.plan.nt = 1;
+  auto align = [](size_t v) { return (v + 255) & ~size_t(255); };
+  L.partials_off = COUNTER_BYTES;
+  L.rowstat_off = align(L.partials_off + (L.plan.splits > 1 ? (size_t)L.plan.splits * B * sizeof(float4) : 0));
+  L.slabs_off = align(L.rowstat_off + (size_t)B * sizeof(float2));
+  L.total = align(L.slabs_off + (size_t)L.plan.row_blocks * L.plan.splits * 2 * sizeof(float));
+  return L;
 }
 
 }  // namespace
@@ -366,6 +513,42 @@ void launch_mode(const void* X, const void* W, const float* b, int64_t B, int F,
 void gemm_softmax_force_plan(int nt, int splits) {
   g_force_nt = nt;
   g_force_splits = splits;
+}
+
+int softmax_train_faug(int F) {
+  switch (F) {
+    case 32: return 64;
+    case 64: return 128;  // 96 would leave a 12-chunk LDS tail that cannot be swizzled in place
+    case 128: return 160;
+    case 256: return 288;
+    case 512: return 544;
+    default: return -1;
+  }
+}
+
+size_t softmax_train_workspace(int64_t B, int K) { return train_layout(B, K).total; }
+
+void launch_softmax_train_grad(const void* X_aug, const void* W_aug, const int32_t* y, int64_t B, int F_aug, int K,
+                               int kind, void* G, int64_t ldg, float* stats_out, void* workspace, size_t ws_bytes,
+                               hipStream_t stream) {
+  if (B <= 0) return;
+  if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
+    throw std::invalid_argument("softmax_train: multiclass kinds only (binary models use train_binary)");
+  if (ldg < K || ldg % 8 != 0) throw std::invalid_argument("softmax_train: ldg must be >= K and a multiple of 8");
+  const TrainLayout L = train_layout(B, K);
+  if (ws_bytes < L.total) throw std::invalid_argument("softmax_train: workspace too small (zero it once)");
+  unsigned char* ws = static_cast<unsigned char*>(workspace);
+  GemmArgs args = base_args(X_aug, W_aug, B, K, kind);
+  args.counters = reinterpret_cast<unsigned int*>(ws);
+  args.partials = reinterpret_cast<float4*>(ws + L.partials_off);
+  args.rowstat = reinterpret_cast<float2*>(ws + L.rowstat_off);
+  args.stat_slabs = reinterpret_cast<float*>(ws + L.slabs_off);
+  args.y = y;
+  args.G = static_cast<uint16_t*>(G);
+  args.ldg = ldg;
+  launch_mode<2>(args, F_aug, L.plan, stream);  // {lse, argmax} per row (split merge in-launch)
+  launch_mode<3>(args, F_aug, L.plan, stream);  // G = P - Y (bf16) + [loss, correct] slabs
+  launch_reduce_slabs_f32(args.stat_slabs, (int)(L.plan.row_blocks * L.plan.splits), 2, stats_out, stream);
 }
 
 size_t gemm_softmax_workspace(int64_t B, int K, int F) {
@@ -382,8 +565,15 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
   const Plan plan = make_plan(B, K);
   if (plan.splits > 1 && ws_bytes < gemm_softmax_workspace(B, K, F))
     throw std::invalid_argument("gemm_softmax: workspace too small (must be zero-initialised once)");
-  launch_mode<0>(X, W, b, B, F, K, kind, out_idx, out_p, plan.splits > 1 ? workspace : nullptr, nullptr, plan,
-                 stream);
+  GemmArgs args = base_args(X, W, B, K, kind);
+  args.bias = b;
+  args.out_idx = out_idx;
+  args.out_p = out_p;
+  if (plan.splits > 1) {
+    args.counters = static_cast<unsigned int*>(workspace);
+    args.partials = reinterpret_cast<float4*>(static_cast<unsigned char*>(workspace) + COUNTER_BYTES);
+  }
+  launch_mode<0>(args, F, plan, stream);
 }
 
 void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B, int F, int K, float* Z,
@@ -391,7 +581,10 @@ void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B,
   if (B <= 0) return;
   Plan plan = make_plan(B, K);
   plan.splits = (K + plan.classes_per_split - 1) / plan.classes_per_split;  // no merge needed for logits
-  launch_mode<1>(X, W, b, B, F, K, KIND_MULTINOMIAL, nullptr, nullptr, nullptr, Z, plan, stream);
+  GemmArgs args = base_args(X, W, B, K, KIND_MULTINOMIAL);
+  args.bias = b;
+  args.Z = Z;
+  launch_mode<1>(args, F, plan, stream);
 }
 
 }  // namespace mlapi

@@ -469,6 +469,26 @@ __global__ __launch_bounds__(256) void sgd_update_kernel(float* __restrict__ p, 
   p[i] -= lr * d;
 }
 
+// 2-D variant for W_aug = [W | b | 0 pad] (multiclass training): L2 only on the first pen_cols
+// columns; writes the bf16 copy the next forward pass reads (saves a separate cast launch).
+__global__ __launch_bounds__(256) void sgd_update_2d_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                            float* __restrict__ mom, int64_t n, int cols,
+                                                            int pen_cols, float lr, float inv_n, float l2,
+                                                            float momentum, uint16_t* __restrict__ shadow) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % cols);
+  float d = g[i] * inv_n + (c < pen_cols ? l2 * p[i] : 0.f);
+  if (mom != nullptr) {
+    const float v = momentum * mom[i] + d;
+    mom[i] = v;
+    d = v;
+  }
+  const float np = p[i] - lr * d;
+  p[i] = np;
+  if (shadow != nullptr) shadow[i] = __builtin_bit_cast(uint16_t, (__bf16)np);
+}
+
 }  // namespace
 
 void train_binary_set_max_blocks(int n) { g_train_max_blocks = n; }
@@ -574,6 +594,20 @@ void launch_sgd_update(float* params, const float* grad, float* momentum_buf, in
   hipLaunchKernelGGL(sgd_update_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, params, grad,
                      momentum_buf, n, n_penalized, lr, inv_n, l2, momentum);
   MLAPI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_sgd_update_2d(float* params, const float* grad, float* momentum_buf, int64_t rows, int cols,
+                          int pen_cols, float lr, float inv_n, float l2, float momentum, uint16_t* shadow_bf16,
+                          hipStream_t stream) {
+  const int64_t n = rows * cols;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(sgd_update_2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, params, grad,
+                     momentum_buf, n, cols, pen_cols, lr, inv_n, l2, momentum, shadow_bf16);
+  MLAPI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_reduce_slabs_f32(const float* slabs, int nslabs, int width, float* out, hipStream_t stream) {
+  launch_reduce_slabs<float>(slabs, nslabs, width, out, stream);
 }
 
 }  // namespace mlapi

@@ -10,7 +10,8 @@ Drop-in for the reference notebook (`Logistic Regression.ipynb:33-42`)::
 Fitting evaluates the loss/gradient with the fp64 ``train_small_grad`` HIP kernel when a GPU is
 selected (``device='cuda'`` / ``'auto'`` with a GPU visible) and with float64 numpy otherwise.
 Prediction uses the fused ``linear_small`` (fp64) kernel on the GPU, or the float64 oracle.
-``solver='sgd'`` trains binary models with the fused mini-batch SGD kernels instead.
+``solver='sgd'`` trains with the mini-batch SGD kernels instead: the fused binary step for two
+classes, the MFMA softmax / one-vs-rest gradient + hipBLASLt dW GEMM for more.
 """
 from __future__ import annotations
 
@@ -100,10 +101,12 @@ class LogisticRegression:
         X = np.asarray(X, dtype=np.float64)
         y = np.asarray(y)
         classes = np.unique(y)
-        if len(classes) != 2:
-            raise ValueError("solver='sgd' supports binary problems (use lbfgs for multiclass)")
-        yb = (y == classes[1]).astype(np.float32)
+        if len(classes) < 2:
+            raise ValueError("need at least 2 classes")
         n, F = X.shape
+        if len(classes) > 2:
+            return self._fit_sgd_multiclass(X, y, classes, dev)
+        yb = (y == classes[1]).astype(np.float32)
         Xt = torch.as_tensor(X, dtype=torch.float32, device=dev)
         yt = torch.as_tensor(yb, device=dev)
         tr = BinarySGDTrainer(F, lr=self.lr, l2=1.0 / (self.C * n), momentum=0.9, device=dev)
@@ -115,6 +118,33 @@ class LogisticRegression:
                 tr.step(Xt[idx].contiguous(), yt[idx].contiguous())
         m = tr.to_model(classes=classes)
         m.meta["n_iter_"] = [tr.steps]
+        return m
+
+    def _fit_sgd_multiclass(self, X: np.ndarray, y: np.ndarray, classes: np.ndarray, dev) -> LinearModel:
+        import torch
+
+        from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer
+
+        n, F = X.shape
+        widths = [w for w in (32, 64, 128, 256, 512) if w >= F]
+        if not widths:
+            raise ValueError("solver='sgd' multiclass supports up to 512 features")
+        Fp = widths[0]  # zero feature columns get zero gradient: their weights stay 0 and are dropped
+        Xp = np.zeros((n, Fp), dtype=np.float32)
+        Xp[:, :F] = X
+        yi = torch.as_tensor(np.searchsorted(classes, y).astype(np.int32), device=dev)
+        kind = Kind.OVR if self.multi_class == "ovr" else Kind.MULTINOMIAL
+        tr = SoftmaxSGDTrainer(Fp, len(classes), kind=kind, lr=self.lr, l2=1.0 / (self.C * n), momentum=0.9,
+                               device=dev)
+        Xa = tr.prepare(torch.as_tensor(Xp, device=dev))
+        rng = np.random.default_rng(self.random_state)
+        for _ in range(self.epochs):
+            perm = torch.as_tensor(rng.permutation(n), device=dev)
+            for s in range(0, n, self.batch_size):
+                idx = perm[s:s + self.batch_size]
+                tr.step(Xa[idx].contiguous(), yi[idx].contiguous())
+        m = tr.to_model(classes=classes)
+        m = LinearModel(m.W[:, :F].copy(), m.b, classes, kind, meta={"solver": "sgd", "n_iter_": [tr.steps]})
         return m
 
     # ------------------------------------------------------------------ predict

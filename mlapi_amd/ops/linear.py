@@ -174,3 +174,79 @@ def cast(src: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     dst = torch.empty(src.shape, dtype=dtype, device=src.device)
     C().cast(_DT[src.dtype], src.data_ptr(), _DT[dtype], dst.data_ptr(), src.numel(), _stream())
     return dst
+
+
+# ------------------------------------------------------------------- multiclass training (MFMA)
+def softmax_train_faug(F: int) -> int:
+    """Augmented width F_aug (ones / intercept column + MFMA padding) for an F-feature model."""
+    fa = {32: 64, 64: 128, 128: 160, 256: 288, 512: 544}.get(int(F), -1)
+    if fa < 0:
+        raise ValueError("softmax training kernels need F in {32, 64, 128, 256, 512} (pad the features)")
+    return fa
+
+
+def augment_features(X: torch.Tensor, F_aug: int) -> torch.Tensor:
+    """[X | 1 | 0...] in bf16, shape [B, F_aug] (done once per dataset, not per step)."""
+    B, F = X.shape
+    out = torch.zeros(B, F_aug, dtype=torch.bfloat16, device=X.device)
+    out[:, :F] = X
+    out[:, F] = 1.0
+    return out
+
+
+def augment_weights(W: torch.Tensor, b: torch.Tensor, F_aug: int) -> torch.Tensor:
+    """[W | b | 0...] in f32, shape [K, F_aug]."""
+    K, F = W.shape
+    out = torch.zeros(K, F_aug, dtype=torch.float32, device=W.device)
+    out[:, :F] = W
+    out[:, F] = b.reshape(-1)
+    return out
+
+
+class SoftmaxTrainBuffers:
+    """Persistent per-batch-size buffers of the multiclass gradient (G, workspace, stats)."""
+
+    def __init__(self, B: int, K: int, device):
+        self.B, self.K = B, K
+        self.ldg = (K + 7) // 8 * 8
+        self.G = torch.empty(B, self.ldg, dtype=torch.bfloat16, device=device)
+        self.ws = torch.zeros(C().softmax_train_workspace(B, K), dtype=torch.uint8, device=device)
+        self.stats = torch.zeros(2, dtype=torch.float32, device=device)
+
+
+def softmax_train_grad(X_aug: torch.Tensor, W_aug_bf16: torch.Tensor, y: torch.Tensor, kind: int,
+                       bufs: SoftmaxTrainBuffers = None, dW_out: torch.Tensor = None,
+                       stats_out: torch.Tensor = None):
+    """Sums over the batch of the multiclass objective's gradient, intercept folded in.
+
+    Returns (dW_aug f32 [K, F_aug], stats f32 [loss_sum, n_correct]). Two MFMA launches produce
+    G = P - Y in bf16 (plus loss/correct); dW_aug = G^T X_aug is one hipBLASLt GEMM with f32 output.
+    """
+    _check(X_aug, W_aug_bf16, y)
+    if X_aug.dtype != torch.bfloat16 or W_aug_bf16.dtype != torch.bfloat16 or y.dtype != torch.int32:
+        raise TypeError("softmax_train_grad: X_aug, W_aug bf16 and y int32")
+    B, F_aug = X_aug.shape
+    K = W_aug_bf16.shape[0]
+    if W_aug_bf16.shape[1] != F_aug or y.numel() != B:
+        raise ValueError("softmax_train_grad: shape mismatch")
+    if bufs is None or bufs.B != B or bufs.K != K:
+        bufs = SoftmaxTrainBuffers(B, K, X_aug.device)
+    stats = bufs.stats if stats_out is None else stats_out
+    C().softmax_train_grad(X_aug.data_ptr(), W_aug_bf16.data_ptr(), y.data_ptr(), B, F_aug, K, int(kind),
+                           bufs.G.data_ptr(), bufs.ldg, stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(),
+                           _stream())
+    G = bufs.G[:, :K]
+    if dW_out is None:
+        dW_out = torch.empty(K, F_aug, dtype=torch.float32, device=X_aug.device)
+    torch.mm(G.t(), X_aug, out_dtype=torch.float32, out=dW_out)
+    return dW_out, stats
+
+
+def sgd_update_2d(params: torch.Tensor, grad: torch.Tensor, pen_cols: int, lr: float, inv_n: float, l2: float,
+                  momentum: float = 0.0, mom_buf: torch.Tensor = None, shadow: torch.Tensor = None) -> None:
+    """params [rows, cols] f32 -= lr * (grad / N + l2 * params[:, :pen_cols]); refreshes a bf16 shadow."""
+    _check(params, grad)
+    rows, cols = params.shape
+    C().sgd_update_2d(params.data_ptr(), grad.data_ptr(), 0 if mom_buf is None else mom_buf.data_ptr(), rows, cols,
+                      int(pen_cols), float(lr), float(inv_n), float(l2), float(momentum),
+                      0 if shadow is None else shadow.data_ptr(), _stream())

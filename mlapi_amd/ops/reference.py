@@ -58,3 +58,22 @@ def train_small_ref(X, y, W, b, kind: int):
         loss = (torch.clamp(z, min=0) - z * Y + torch.log1p(torch.exp(-z.abs()))).sum()
         correct = (torch.argmax(z, dim=1) == y).sum()
     return torch.cat([(g.T @ X).reshape(-1), g.sum(0), loss.reshape(1), correct.to(torch.float64).reshape(1)])
+
+
+def softmax_train_ref(X_aug, y, W_aug, kind: int, dtype=torch.float32):
+    """Oracle of ops.linear.softmax_train_grad: (G [B, K], dW_aug [K, F_aug], loss_sum, n_correct).
+
+    Also the CPU path of the multiclass SGD trainer (dtype float32)."""
+    X, W = X_aug.to(dtype), W_aug.to(dtype)
+    y = y.long()
+    z = X @ W.T
+    K = W.shape[0]
+    Y = torch.nn.functional.one_hot(y, K).to(dtype)
+    if kind == Kind.MULTINOMIAL:
+        G = torch.softmax(z, dim=1) - Y
+        loss = (torch.logsumexp(z, dim=1) - z.gather(1, y[:, None])[:, 0]).sum()
+    else:
+        G = torch.sigmoid(z) - Y
+        loss = (torch.clamp(z, min=0) - z * Y + torch.log1p(torch.exp(-z.abs()))).sum()
+    correct = (torch.argmax(z, dim=1) == y).sum().to(dtype)
+    return G, G.T @ X, loss, correct

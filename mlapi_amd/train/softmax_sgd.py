@@ -1,0 +1,198 @@
+"""Data-parallel mini-batch SGD for multiclass (softmax / one-vs-rest) logistic regression.
+
+The reference fits its 3-class Iris model once with sklearn's full-batch L-BFGS
+(`Logistic Regression.ipynb:33-34`); :mod:`mlapi_amd.train.lbfgs` reproduces that fit.
+This module is the scale-out counterpart (BASELINE config 5 with K classes): per step and rank
+
+  1. ``softmax_train_grad``: two MFMA launches over the rank's shard -> G = P - Y (bf16) with the
+     loss / correct sums, then dW_aug = G^T X_aug as one hipBLASLt GEMM (f32 out). The intercept
+     rides inside the GEMMs (X_aug = [X | 1], W_aug = [W | b]), so there is no separate bias pass;
+  2. one RCCL all-reduce of the fused buffer [dW_aug | loss_sum | n_correct] (C2 + C3);
+  3. ``sgd_update_2d``: W_aug -= lr * (g / N_global + l2 * W) with the intercept column
+     unpenalized, writing the bf16 copy the next forward reads in the same pass.
+
+fp32 master weights; every rank applies the identical update, so replicas stay bitwise equal.
+One replica (world == 1) can capture the whole step in a HIP graph (:meth:`capture`).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from mlapi_amd.models.linear import Kind
+from mlapi_amd.parallel.comm import DistInfo, all_reduce_sum_
+
+
+def synthetic_multiclass(n: int, F: int, K: int, *, seed: int = 0, device=None, noise: float = 1.0):
+    """Gaussian features, labels = argmax of a planted linear model + Gumbel-ish noise."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    W_true = torch.randn(K, F, generator=torch.Generator().manual_seed(43)) * (2.0 / F ** 0.5)
+    X = torch.randn(n, F, generator=g)
+    z = X @ W_true.T + noise * torch.randn(n, K, generator=g)
+    y = torch.argmax(z, dim=1).to(torch.int32)
+    return X.to(device), y.to(device)
+
+
+def _faug(F: int) -> int:
+    from mlapi_amd.ops.linear import softmax_train_faug
+
+    return softmax_train_faug(F)
+
+
+class SoftmaxSGDTrainer:
+    """Multiclass LR trainer, one GPU per rank (or the explicit CPU path used by gloo tests)."""
+
+    def __init__(self, n_features: int, n_classes: int, *, kind: int = Kind.MULTINOMIAL,
+                 info: Optional[DistInfo] = None, lr: float = 0.1, l2: float = 0.0, momentum: float = 0.0,
+                 device=None):
+        if kind not in (Kind.MULTINOMIAL, Kind.OVR):
+            raise ValueError("SoftmaxSGDTrainer: kind must be MULTINOMIAL or OVR (binary: BinarySGDTrainer)")
+        if n_classes < 2:
+            raise ValueError("need at least 2 classes")
+        self.F, self.K, self.kind = int(n_features), int(n_classes), int(kind)
+        self.F_aug = _faug(self.F)
+        self.info = info or DistInfo(device=device)
+        self.device = device if device is not None else self.info.device
+        if self.device is None:
+            self.device = torch.device("cpu")
+        self.on_gpu = torch.device(self.device).type == "cuda"
+        self.lr, self.l2, self.momentum = lr, l2, momentum
+        self.params = torch.zeros(self.K, self.F_aug, dtype=torch.float32, device=self.device)
+        self.shadow = torch.zeros(self.K, self.F_aug, dtype=torch.bfloat16, device=self.device) if self.on_gpu else None
+        n = self.K * self.F_aug
+        self.grad = torch.zeros(n + 2, dtype=torch.float32, device=self.device)  # [dW_aug | loss | correct]
+        self.mom = torch.zeros_like(self.params) if momentum else None
+        self._bufs = {}  # batch size -> SoftmaxTrainBuffers (a ragged last batch keeps its own)
+        self._graph = None
+        self.steps = 0
+        self._n_seen = 0
+
+    # ---------------------------------------------------------------------------------- data
+    def prepare(self, X: torch.Tensor) -> torch.Tensor:
+        """Augmented features [X | 1 | 0...] (bf16 on GPU, f32 on CPU); build once per dataset."""
+        from mlapi_amd.ops.linear import augment_features
+
+        Xa = augment_features(X.to(self.device), self.F_aug)
+        return Xa if self.on_gpu else Xa.float()
+
+    @property
+    def W(self) -> torch.Tensor:
+        return self.params[:, : self.F]
+
+    @property
+    def b(self) -> torch.Tensor:
+        return self.params[:, self.F]
+
+    def _dW(self) -> torch.Tensor:
+        return self.grad[: self.K * self.F_aug].view(self.K, self.F_aug)
+
+    def set_params(self, W: torch.Tensor, b: torch.Tensor) -> None:
+        self.params.zero_()
+        self.params[:, : self.F] = W.to(self.params)
+        self.params[:, self.F] = b.reshape(-1).to(self.params)
+        if self.shadow is not None:
+            self.shadow.copy_(self.params)
+
+    # ---------------------------------------------------------------------------------- step
+    def _local_grad(self, Xa: torch.Tensor, y: torch.Tensor) -> None:
+        if self.on_gpu:
+            from mlapi_amd.ops.linear import SoftmaxTrainBuffers, softmax_train_grad
+
+            B = Xa.shape[0]
+            if B not in self._bufs:
+                self._bufs[B] = SoftmaxTrainBuffers(B, self.K, Xa.device)
+            softmax_train_grad(Xa, self.shadow, y, self.kind, bufs=self._bufs[B], dW_out=self._dW(),
+                               stats_out=self.grad[self.K * self.F_aug:])
+        else:
+            from mlapi_amd.ops.reference import softmax_train_ref
+
+            _, dW, loss, correct = softmax_train_ref(Xa, y, self.params, self.kind)
+            self._dW().copy_(dW)
+            self.grad[-2] = loss
+            self.grad[-1] = correct
+
+    def _update(self, n_global: int) -> None:
+        if self.on_gpu:
+            from mlapi_amd.ops.linear import sgd_update_2d
+
+            sgd_update_2d(self.params, self.grad, self.F, self.lr, 1.0 / n_global, self.l2, self.momentum, self.mom,
+                          self.shadow)
+        else:
+            d = self._dW() / n_global
+            d[:, : self.F] += self.l2 * self.params[:, : self.F]
+            if self.mom is not None:
+                self.mom.mul_(self.momentum).add_(d)
+                d = self.mom
+            self.params.sub_(self.lr * d)
+
+    def step(self, Xa: torch.Tensor, y: torch.Tensor) -> None:
+        """One SGD step on this rank's shard (Xa from :meth:`prepare`, y int32 class indices)."""
+        if self._graph is not None and self._graph[1] is Xa and self._graph[2] is y:
+            self._graph[0].replay()
+        else:
+            self._local_grad(Xa, y)
+            all_reduce_sum_(self.grad, self.info)
+            self._update(Xa.shape[0] * self.info.world)
+        self.steps += 1
+        self._n_seen = Xa.shape[0] * self.info.world
+
+    def capture(self, Xa: torch.Tensor, y: torch.Tensor) -> None:
+        """Capture one whole step (2 MFMA launches + reduce + GEMM + update) in a HIP graph.
+
+        Later ``step(Xa, y)`` calls with these exact tensors replay it: one launch from the host.
+        Single replica only (the all-reduce stays outside graphs)."""
+        if not self.on_gpu or self.info.world != 1:
+            raise RuntimeError("graph capture: single-GPU replica only")
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        saved = (self.params.clone(), self.shadow.clone(), None if self.mom is None else self.mom.clone())
+        with torch.cuda.stream(s):  # warm-up: allocates the buffers and hipBLASLt's workspace
+            for _ in range(2):
+                self._local_grad(Xa, y)
+                self._update(Xa.shape[0])
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._local_grad(Xa, y)
+            self._update(Xa.shape[0])
+        self.params.copy_(saved[0])
+        self.shadow.copy_(saved[1])
+        if self.mom is not None:
+            self.mom.copy_(saved[2])
+        self._graph = (g, Xa, y)
+
+    # ---------------------------------------------------------------------------------- stats
+    def last_loss(self) -> float:
+        return float(self.grad[-2].item()) / max(1, self._n_seen)
+
+    def last_accuracy(self) -> float:
+        return float(self.grad[-1].item()) / max(1, self._n_seen)
+
+    def evaluate(self, Xa: torch.Tensor, y: torch.Tensor) -> Tuple[float, float]:
+        saved = self.grad.clone()
+        self._local_grad(Xa, y)
+        o = self.grad[-2:].cpu().clone()
+        self.grad.copy_(saved)
+        return float(o[0]) / Xa.shape[0], float(o[1]) / Xa.shape[0]
+
+    def state_dict(self) -> dict:
+        return {"params": self.params.detach().cpu(), "mom": None if self.mom is None else self.mom.detach().cpu(),
+                "steps": self.steps}
+
+    def load_state_dict(self, sd: dict) -> None:
+        self.params.copy_(sd["params"].to(self.device))
+        if self.shadow is not None:
+            self.shadow.copy_(self.params)
+        if self.mom is not None and sd.get("mom") is not None:
+            self.mom.copy_(sd["mom"].to(self.device))
+        self.steps = int(sd["steps"])
+
+    def to_model(self, classes=None):
+        from mlapi_amd.models.linear import LinearModel
+
+        p = self.params.detach().cpu().double().numpy()
+        classes = np.arange(self.K) if classes is None else np.asarray(classes)
+        return LinearModel(p[:, : self.F].copy(), p[:, self.F].copy(), classes, Kind(self.kind),
+                           meta={"solver": "sgd", "n_iter_": [self.steps]})

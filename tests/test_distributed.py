@@ -55,6 +55,9 @@ def test_broadcast_and_dp_sgd_determinism(tmp_path):
     single = np.load(tmp_path / "params_1_0.npy")
     np.testing.assert_allclose(p0, single, rtol=1e-4, atol=1e-5)  # DP == single-process on the global batch
     assert b0["acc"] > 0.8
+    m0, m1 = np.load(tmp_path / "mc_params_2_0.npy"), np.load(tmp_path / "mc_params_2_1.npy")
+    assert np.array_equal(m0, m1), "multiclass DP replicas must stay bitwise identical"
+    np.testing.assert_allclose(m0, np.load(tmp_path / "mc_params_1_0.npy"), rtol=1e-4, atol=1e-5)
 
 
 def test_dp_serving_reload(tmp_path, iris_pickle_bytes):

@@ -119,3 +119,59 @@ def test_estimator_gpu_predict_and_sgd(iris_data):
     assert clf.score(Xte, yte) == 0.9666666666666667
     sgd = LogisticRegression(device="cuda", solver="sgd").fit(Xtr, ytr == "Iris-setosa")
     assert sgd.score(Xte, yte == "Iris-setosa") == 1.0
+    mc = LogisticRegression(device="cuda", solver="sgd", lr=0.05, batch_size=20, epochs=200).fit(Xtr, ytr)
+    assert mc.score(Xte, yte) >= 0.9
+
+
+def test_softmax_ref_gradient_matches_autograd():
+    """The multiclass oracle (also the trainer's CPU path) is the true gradient of the objective."""
+    import torch
+
+    from mlapi_amd.models.linear import Kind
+    from mlapi_amd.ops.reference import softmax_train_ref
+
+    torch.manual_seed(0)
+    X, y = torch.randn(64, 10, dtype=torch.float64), torch.randint(0, 5, (64,), dtype=torch.int32)
+    for kind in (Kind.MULTINOMIAL, Kind.OVR):
+        W = torch.randn(5, 10, dtype=torch.float64, requires_grad=True)
+        z = X @ W.T
+        Y = torch.nn.functional.one_hot(y.long(), 5).double()
+        if kind == Kind.MULTINOMIAL:
+            loss = (torch.logsumexp(z, 1) - (z * Y).sum(1)).sum()
+        else:
+            loss = torch.nn.functional.binary_cross_entropy_with_logits(z, Y, reduction="sum")
+        loss.backward()
+        _, dW, lref, _ = softmax_train_ref(X, y, W.detach(), kind, dtype=torch.float64)
+        torch.testing.assert_close(dW, W.grad)
+        assert float(lref) == pytest.approx(float(loss.detach()), rel=1e-12)
+
+
+@pytest.mark.parametrize("kind_name", ["MULTINOMIAL", "OVR"])
+def test_softmax_sgd_cpu_learns(kind_name):
+    import torch
+
+    from mlapi_amd.models.linear import Kind
+    from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer, synthetic_multiclass
+
+    X, y = synthetic_multiclass(6000, 32, 7, seed=1, noise=0.3)
+    tr = SoftmaxSGDTrainer(32, 7, kind=Kind[kind_name], lr=0.5, momentum=0.9, device=torch.device("cpu"))
+    Xa = tr.prepare(X)
+    assert Xa.shape == (6000, 64) and torch.all(Xa[:, 32] == 1)
+    for s in range(60):
+        lo = (s * 500) % 5000
+        tr.step(Xa[lo:lo + 500], y[lo:lo + 500])
+    loss, acc = tr.evaluate(Xa[5000:], y[5000:])
+    assert acc > 0.8, (loss, acc)
+    m = tr.to_model()
+    pred = m.predict(X[5000:].double().numpy())
+    assert np.mean(pred == y[5000:].numpy()) == pytest.approx(acc, abs=0.01)  # f64 model vs f32 training math
+
+
+def test_estimator_sgd_multiclass_cpu(iris_data):
+    from mlapi_amd.models.estimator import LogisticRegression
+
+    Xtr, Xte, ytr, yte = iris_data
+    clf = LogisticRegression(solver="sgd", device="cpu", lr=0.05, batch_size=20, epochs=200).fit(Xtr, ytr)
+    assert list(clf.classes_) == ["Iris-setosa", "Iris-versicolor", "Iris-virginica"]
+    assert clf.coef_.shape == (3, 4)
+    assert clf.score(Xte, yte) >= 0.9
