@@ -470,7 +470,10 @@ void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
     } else if (ks == 5) {
       MLAPI_GEMM_LAUNCH(5, 1);
     } else if (ks == 9) {
-      MLAPI_GEMM_LAUNCH(9, 1);
+      if (plan.nt == 2)
+        MLAPI_GEMM_LAUNCH(9, 2);
+      else
+        MLAPI_GEMM_LAUNCH(9, 1);
     } else if (ks == 17) {
       MLAPI_GEMM_LAUNCH(17, 1);
     } else {
@@ -498,8 +501,7 @@ struct TrainLayout {
 
 TrainLayout train_layout(int64_t B, int K) {
   TrainLayout L;
-  L.plan = make_plan(B, K);
-  L.plan.nt = 1;
+  L.plan = make_plan(B, K);  // nt = 1 unless forced (gemm_softmax_force_plan; NT = 2 only built for F_aug 288)
   auto align = [](size_t v) { return (v + 255) & ~size_t(255); };
   L.partials_off = COUNTER_BYTES;
   L.rowstat_off = align(L.partials_off + (L.plan.splits > 1 ? (size_t)L.plan.splits * B * sizeof(float4) : 0));

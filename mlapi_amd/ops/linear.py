@@ -212,6 +212,14 @@ class SoftmaxTrainBuffers:
         self.G = torch.empty(B, self.ldg, dtype=torch.bfloat16, device=device)
         self.ws = torch.zeros(C().softmax_train_workspace(B, K), dtype=torch.uint8, device=device)
         self.stats = torch.zeros(2, dtype=torch.float32, device=device)
+        # dW split over the batch: hipBLASLt tiles only the small [K, F_aug] output, so one mm runs
+        # ~48 workgroups for K=1000 (245 us at B=65536); S batched slices of ~2048 rows + a sum
+        # fill the chip (72 us at S=32: tools/softmax_train_sweep.py, profiles/r1_softmax_train).
+        S = 1
+        while S < 64 and B % (2 * S) == 0 and B // (2 * S) >= 2048:
+            S *= 2
+        self.splits = S
+        self.part = None
 
 
 def softmax_train_grad(X_aug: torch.Tensor, W_aug_bf16: torch.Tensor, y: torch.Tensor, kind: int,
@@ -235,10 +243,17 @@ def softmax_train_grad(X_aug: torch.Tensor, W_aug_bf16: torch.Tensor, y: torch.T
     C().softmax_train_grad(X_aug.data_ptr(), W_aug_bf16.data_ptr(), y.data_ptr(), B, F_aug, K, int(kind),
                            bufs.G.data_ptr(), bufs.ldg, stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(),
                            _stream())
-    G = bufs.G[:, :K]
     if dW_out is None:
         dW_out = torch.empty(K, F_aug, dtype=torch.float32, device=X_aug.device)
-    torch.mm(G.t(), X_aug, out_dtype=torch.float32, out=dW_out)
+    S = bufs.splits
+    if S == 1:
+        torch.mm(bufs.G[:, :K].t(), X_aug, out_dtype=torch.float32, out=dW_out)
+    else:
+        if bufs.part is None:
+            bufs.part = torch.empty(S, K, F_aug, dtype=torch.float32, device=X_aug.device)
+        Gs = bufs.G.view(S, B // S, bufs.ldg)[:, :, :K]
+        torch.bmm(Gs.transpose(1, 2), X_aug.view(S, B // S, F_aug), out_dtype=torch.float32, out=bufs.part)
+        torch.sum(bufs.part, dim=0, out=dW_out)
     return dW_out, stats
 
 
