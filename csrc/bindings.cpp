@@ -12,6 +12,7 @@
 #include <cmath>
 #include <mutex>
 
+#include "dist/comm.h"
 #include "http/loadgen.h"
 #include "http/server.h"
 #include "mlapi/common.h"
@@ -326,6 +327,53 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("fast_path", &ServerConfig::fast_path)
       .def_readwrite("max_body", &ServerConfig::max_body)
       .def_readwrite("backlog", &ServerConfig::backlog);
+
+  // ---- native RCCL communicator (csrc/dist/comm.h)
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init([](py::bytes id, int rank, int world, int device) {
+             return new RcclComm(std::string(id), rank, world, device);
+           }),
+           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
+      .def_static("version", &RcclComm::version)
+      .def_static("library_path", &RcclComm::library_path)
+      .def("all_reduce",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op, uintptr_t stream) {
+             c.all_reduce(ptr<void>(send), ptr<void>(recv), count, dtype, op, stream_of(stream));
+           },
+           py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"), py::arg("op"), py::arg("stream"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("broadcast",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int root, uintptr_t stream) {
+             c.broadcast(ptr<void>(send), ptr<void>(recv), count, dtype, root, stream_of(stream));
+           },
+           py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"), py::arg("root"),
+           py::arg("stream"), py::call_guard<py::gil_scoped_release>())
+      .def("all_gather",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, uintptr_t stream) {
+             c.all_gather(ptr<void>(send), ptr<void>(recv), count, dtype, stream_of(stream));
+           },
+           py::arg("send"), py::arg("recv"), py::arg("count_per_rank"), py::arg("dtype"), py::arg("stream"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("reduce_scatter",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op, uintptr_t stream) {
+             c.reduce_scatter(ptr<void>(send), ptr<void>(recv), count, dtype, op, stream_of(stream));
+           },
+           py::arg("send"), py::arg("recv"), py::arg("recv_count"), py::arg("dtype"), py::arg("op"),
+           py::arg("stream"), py::call_guard<py::gil_scoped_release>())
+      .def("group_start", &RcclComm::group_start)
+      .def("group_end", &RcclComm::group_end)
+      .def("wait", [](RcclComm& c, uintptr_t stream, int timeout_ms) { return c.wait(stream_of(stream), timeout_ms); },
+           py::arg("stream"), py::arg("timeout_ms") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("barrier",
+           [](RcclComm& c, uintptr_t stream, int timeout_ms) { return c.barrier(stream_of(stream), timeout_ms); },
+           py::arg("stream"), py::arg("timeout_ms") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &RcclComm::abort)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world", &RcclComm::world)
+      .def_property_readonly("device", &RcclComm::device)
+      .def_property_readonly("aborted", &RcclComm::aborted);
 
   py::class_<HttpServer>(m, "HttpServer")
       .def(py::init<Engine*, const ServerConfig&>(), py::keep_alive<1, 2>())

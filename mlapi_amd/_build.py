@@ -32,6 +32,7 @@ SOURCES = [
     "runtime/engine.cpp",
     "http/server.cpp",
     "http/loadgen.cpp",
+    "dist/comm.cpp",
     "bindings.cpp",
 ]
 
@@ -91,7 +92,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     newest = max(o.stat().st_mtime for o in objs)
     if force or not out.exists() or out.stat().st_mtime < newest:
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out) + ".tmp"] + \
-              [str(o) for o in objs] + ["-lpthread"]
+              [str(o) for o in objs] + ["-lpthread", "-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")

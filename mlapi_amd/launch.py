@@ -1,0 +1,133 @@
+"""``python -m mlapi_amd.launch --nproc 8 [-m module | script.py] [args...]`` - one process per GPU.
+
+The framework's own launcher ("spawns N rank processes, each pinned to a GPU"), an
+alternative to ``torchrun`` with what a serving node needs:
+
+* hosts the job's TCP key-value store (the host channel over which rank 0 publishes the RCCL
+  unique id, :func:`mlapi_amd.parallel.rccl.exchange_unique_id`; torch.distributed's ``env://``
+  init joins it as a client via ``TORCHELASTIC_USE_AGENT_STORE``);
+* exports RANK / WORLD_SIZE / LOCAL_RANK / LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT, so every
+  entry point (``bench.py``, ``mlapi_amd.serve``, ``mlapi_amd.train``) runs unchanged;
+* pins each rank to a contiguous, disjoint slice of the CPUs it may use (the serving path is CPU
+  bound: HTTP parsing and JSON rendering run on these cores) and sizes OMP_NUM_THREADS to it; GPU
+  ``local_rank`` is selected by the rank itself (all devices stay visible so RCCL can map peers);
+* supervises: the first rank that exits non-zero brings the others down (SIGTERM, then SIGKILL
+  after ``--grace``) and its exit code becomes the launcher's.
+
+The launcher never touches the GPU itself, so starting the ranks with fork+exec is safe.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import List, Optional
+
+
+def _free_port(host: str) -> int:
+    s = socket.socket()
+    s.bind((host, 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def cpu_slices(nproc: int, cpus: Optional[List[int]] = None) -> List[List[int]]:
+    """Split the usable CPUs into ``nproc`` contiguous, disjoint, near-equal slices."""
+    cpus = sorted(cpus if cpus is not None else os.sched_getaffinity(0))
+    if nproc > len(cpus):  # oversubscribed: share round-robin
+        return [[cpus[i % len(cpus)]] for i in range(nproc)]
+    base, extra = divmod(len(cpus), nproc)
+    out, i = [], 0
+    for r in range(nproc):
+        n = base + (1 if r < extra else 0)
+        out.append(cpus[i:i + n])
+        i += n
+    return out
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m mlapi_amd.launch", description=__doc__.split("\n\n")[0])
+    ap.add_argument("--nproc", type=int, default=0, help="ranks (default: visible GPU count, at least 1)")
+    ap.add_argument("--master-addr", default="127.0.0.1")
+    ap.add_argument("--master-port", type=int, default=0, help="0 = pick a free port")
+    ap.add_argument("--no-pin", action="store_true", help="do not pin ranks to CPU slices")
+    ap.add_argument("--grace", type=float, default=10.0, help="seconds between SIGTERM and SIGKILL on failure")
+    ap.add_argument("-m", dest="module", default=None, help="run a module (like python -m)")
+    ap.add_argument("target", nargs=argparse.REMAINDER, help="script.py args... (or module args with -m)")
+    args = ap.parse_args(argv)
+
+    nproc = args.nproc
+    if nproc <= 0:
+        try:  # counting devices does not initialise the GPU on this image
+            import torch
+
+            nproc = max(1, torch.cuda.device_count())
+        except Exception:  # pragma: no cover
+            nproc = 1
+    if args.module is None and not args.target:
+        ap.error("nothing to run: give a script or -m module")
+    cmd = [sys.executable] + (["-m", args.module] if args.module else []) + args.target
+
+    import torch.distributed as dist
+
+    port = args.master_port or _free_port(args.master_addr)
+    store = dist.TCPStore(args.master_addr, port, nproc, is_master=True, wait_for_workers=False,
+                          use_libuv=True)
+    slices = cpu_slices(nproc)
+    procs: List[subprocess.Popen] = []
+    for r in range(nproc):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nproc), "LOCAL_WORLD_SIZE": str(nproc),
+                    "GROUP_RANK": "0", "MASTER_ADDR": args.master_addr, "MASTER_PORT": str(port),
+                    "TORCHELASTIC_USE_AGENT_STORE": "True", "MLAPI_LAUNCHER": "1"})
+        cpus = slices[r]
+        if not args.no_pin:
+            env["OMP_NUM_THREADS"] = str(max(1, len(cpus)))
+        pre = (lambda c=cpus: os.sched_setaffinity(0, c)) if not args.no_pin else None
+        procs.append(subprocess.Popen(cmd, env=env, preexec_fn=pre))
+
+    def _terminate(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except ProcessLookupError:  # pragma: no cover
+                    pass
+
+    signal.signal(signal.SIGTERM, lambda *_: _terminate())
+    code = 0
+    try:
+        while True:
+            alive = 0
+            for p in procs:
+                rc = p.poll()
+                if rc is None:
+                    alive += 1
+                elif rc != 0 and code == 0:
+                    code = rc if rc > 0 else 128 - rc
+                    print(f"[mlapi_amd.launch] rank {procs.index(p)} exited with {rc}; stopping the job",
+                          file=sys.stderr, flush=True)
+                    _terminate()
+                    deadline = time.monotonic() + args.grace
+                    while time.monotonic() < deadline and any(q.poll() is None for q in procs):
+                        time.sleep(0.05)
+                    _terminate(signal.SIGKILL)
+            if alive == 0:
+                break
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        _terminate(signal.SIGINT)
+        for p in procs:
+            p.wait()
+        code = 130
+    del store
+    return code
+
+
+if __name__ == "__main__":
+    sys.exit(main())

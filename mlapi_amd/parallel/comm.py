@@ -12,6 +12,12 @@ One process per GPU. On ROCm the ``"nccl"`` backend of torch.distributed IS RCCL
 
 All messages are <= ~1 MiB, i.e. latency-bound on xGMI: one fused buffer per step, never one
 collective per tensor.
+
+Data plane selection (``MLAPI_COMM``): ``torch`` (default) uses torch.distributed's ``nccl``
+backend (RCCL); ``native`` uses the framework's own C++ RCCL communicator
+(:class:`mlapi_amd.parallel.rccl.NativeComm`, csrc/dist/comm.cpp) with a gloo process group kept
+only as the host control plane; ``fake`` runs the same code paths on CPU through
+:class:`~mlapi_amd.parallel.rccl.FakeComm` (tests).
 """
 from __future__ import annotations
 
@@ -34,14 +40,19 @@ class DistInfo:
     local_rank: int = 0
     device: Optional[torch.device] = None  # None -> CPU
     backend: str = "none"
+    comm: Optional[object] = None  # NativeComm / FakeComm when MLAPI_COMM selects one
 
     @property
     def is_main(self) -> bool:
         return self.rank == 0
 
 
-def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None) -> DistInfo:
+def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None,
+                     comm: Optional[str] = None) -> DistInfo:
     """Initialise from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); no-op for 1 process."""
+    comm = (comm or os.environ.get("MLAPI_COMM", "torch")).lower()
+    if comm not in ("torch", "native", "fake"):
+        raise ValueError(f"MLAPI_COMM must be torch, native or fake (got {comm!r})")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -52,20 +63,39 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
         device = torch.device("cuda", local_rank % torch.cuda.device_count())
         torch.cuda.set_device(device)
     info = DistInfo(rank, world, local_rank, device, "none")
+    if comm == "native" and device is None:
+        raise RuntimeError("MLAPI_COMM=native needs a GPU (use fake for CPU runs)")
     if world > 1:
         if not dist.is_initialized():
+            if comm != "torch":
+                backend = "gloo"  # host control plane only; the data plane is info.comm
             backend = backend or ("nccl" if use_gpu else "gloo")
             kw = {"device_id": device} if backend == "nccl" else {}
             dist.init_process_group(backend=backend, **kw)
         info.backend = dist.get_backend()
+    if comm == "native":
+        from mlapi_amd.parallel.rccl import NativeComm
+
+        info.comm = NativeComm(rank, world, device)
+        info.backend = NativeComm.kind
+    elif comm == "fake":
+        from mlapi_amd.parallel.rccl import FakeComm
+
+        info.comm = FakeComm(rank, world)
+        info.backend = FakeComm.kind
     return info
 
 
 def _coll_device(info: DistInfo) -> torch.device:
+    if info.comm is not None:
+        return info.comm.device
     return info.device if (info.backend == "nccl" and info.device is not None) else torch.device("cpu")
 
 
 def barrier(info: DistInfo) -> None:
+    if info.comm is not None:
+        info.comm.barrier()
+        return
     if info.world > 1:
         if info.backend == "nccl":
             dist.barrier(device_ids=[info.device.index])
@@ -77,7 +107,10 @@ def all_reduce_max(value: float, info: DistInfo) -> float:
     if info.world == 1:
         return value
     t = torch.tensor([value], dtype=torch.float64, device=_coll_device(info))
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if info.comm is not None:
+        info.comm.all_reduce_(t, "max")
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
@@ -85,6 +118,8 @@ def all_gather_floats(values, info: DistInfo) -> np.ndarray:
     t = torch.tensor(list(values), dtype=torch.float64, device=_coll_device(info))
     if info.world == 1:
         return t.cpu().numpy()[None, :]
+    if info.comm is not None:
+        return info.comm.all_gather(t).cpu().numpy()
     out = [torch.empty_like(t) for _ in range(info.world)]
     dist.all_gather(out, t)
     return torch.stack(out).cpu().numpy()
@@ -93,18 +128,28 @@ def all_gather_floats(values, info: DistInfo) -> np.ndarray:
 def all_reduce_sum_(t: torch.Tensor, info: DistInfo) -> torch.Tensor:
     """In-place sum over ranks (C2). ``t`` must live on the collective's device."""
     if info.world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        if info.comm is not None:
+            info.comm.all_reduce_(t)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
+
+
+def _bcast(t: torch.Tensor, info: DistInfo, src: int) -> None:
+    if info.comm is not None:
+        info.comm.broadcast_(t, src)
+    else:
+        dist.broadcast(t, src)
 
 
 def _broadcast_bytes(payload: Optional[bytes], info: DistInfo, src: int = 0) -> bytes:
     dev = _coll_device(info)
     n = torch.tensor([len(payload) if payload is not None else 0], dtype=torch.int64, device=dev)
-    dist.broadcast(n, src)
+    _bcast(n, info, src)
     buf = torch.empty(int(n.item()), dtype=torch.uint8, device=dev)
     if info.rank == src:
         buf.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
-    dist.broadcast(buf, src)
+    _bcast(buf, info, src)
     return bytes(buf.cpu().numpy().tobytes())
 
 
@@ -126,12 +171,13 @@ def broadcast_model(model: Optional[LinearModel], info: DistInfo, src: int = 0) 
     flat = torch.empty(K * F + K, dtype=torch.float64, device=dev)
     if info.rank == src:
         flat.copy_(torch.from_numpy(np.concatenate([model.W.reshape(-1), model.b])))
-    dist.broadcast(flat, src)  # the one weight collective
+    _bcast(flat, info, src)  # the one weight collective
     arr = flat.cpu().numpy()
     classes = np.array(h["classes"], dtype=object if h["classes_dtype"] == "object" else np.dtype(h["classes_dtype"]))
     return LinearModel(arr[:K * F].reshape(K, F), arr[K * F:], classes, Kind(h["kind"]))
 
 
 def shutdown(info: DistInfo) -> None:
+    info.comm = None  # drops the RCCL communicator (ncclCommDestroy) before the process group
     if info.world > 1 and dist.is_initialized():
         dist.destroy_process_group()

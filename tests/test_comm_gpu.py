@@ -1,0 +1,50 @@
+"""Native RCCL communicator (csrc/dist/comm.cpp) on the GPU box (one GPU: world_size 1).
+
+Multi-rank RCCL runs need one GPU per rank (RCCL rejects two ranks on one device); the same
+collective code paths are covered at world_size 2 on CPU through FakeComm
+(tests/test_distributed.py::test_fake_comm_collectives)."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+ENV = {**os.environ, "PYTHONPATH": str(ROOT)}
+
+
+def test_native_comm_semantics_world1(tmp_path):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", "--master-port=29731", str(ROOT / "tests" / "dist" / "comm_semantics.py")]
+    out = subprocess.run(cmd, env={**ENV, "OUT": str(tmp_path), "MLAPI_COMM": "native"}, capture_output=True,
+                         text=True, timeout=240)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    assert (tmp_path / "OK_0").read_text() == "native-rccl"
+
+
+def test_native_comm_uses_torch_rccl_and_aborts():
+    from mlapi_amd._native import C
+    from mlapi_amd.parallel.rccl import NativeComm, measure_all_reduce
+
+    c = NativeComm(0, 1, torch.device("cuda", 0))
+    assert C().RcclComm.version() > 20000
+    assert "rccl" in C().RcclComm.library_path()
+    t = torch.arange(1 << 20, dtype=torch.float32, device="cuda:0")
+    c.all_reduce_(t)
+    c.wait(10_000)
+    assert torch.equal(t, torch.arange(1 << 20, dtype=torch.float32, device="cuda:0"))
+    assert measure_all_reduce(c, 1 << 20, iters=5) < 0.05
+    c.abort()
+    assert c.aborted
+    with pytest.raises(RuntimeError, match="aborted"):
+        c.all_reduce_(t)
+
+
+def test_bench_train_over_native_comm():
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--mode", "train", "--steps", "20", "--warmup", "2"],
+                         env={**ENV, "MLAPI_COMM": "native"}, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert '"train_samples_per_sec"' in out.stdout.strip().splitlines()[-1]

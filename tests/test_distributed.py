@@ -60,6 +60,54 @@ def test_broadcast_and_dp_sgd_determinism(tmp_path):
     np.testing.assert_allclose(m0, np.load(tmp_path / "mc_params_1_0.npy"), rtol=1e-4, atol=1e-5)
 
 
+def test_fake_comm_collectives(tmp_path):
+    """The framework communicator API (NativeComm's twin) over gloo, world_size 2 and 1."""
+    script = str(ROOT / "tests" / "dist" / "comm_semantics.py")
+    for n in (2, 1):
+        run(n, script, {"OUT": str(tmp_path), "MLAPI_COMM": "fake"})
+        for r in range(n):
+            assert (tmp_path / f"OK_{r}").read_text() == "fake-gloo"
+            (tmp_path / f"OK_{r}").unlink()
+
+
+def test_dp_sgd_through_fake_comm(tmp_path):
+    script = str(ROOT / "tests" / "dist" / "bcast_train.py")
+    run(2, script, {"OUT": str(tmp_path), "MLAPI_COMM": "fake"})
+    p0, p1 = np.load(tmp_path / "mc_params_2_0.npy"), np.load(tmp_path / "mc_params_2_1.npy")
+    assert np.array_equal(p0, p1)
+
+
+def test_launcher_pins_and_runs_collectives(tmp_path):
+    """python -m mlapi_amd.launch: rank env, disjoint CPU slices, store bootstrap, collectives."""
+    from mlapi_amd.launch import cpu_slices
+
+    assert cpu_slices(3, list(range(8))) == [[0, 1, 2], [3, 4, 5], [6, 7]]
+    launch = [sys.executable, "-m", "mlapi_amd.launch", "--nproc", "2"]
+    out = subprocess.run(launch + [str(ROOT / "tests" / "dist" / "affinity.py")], env={**ENV, "OUT": str(tmp_path)},
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    a = [json.loads((tmp_path / f"aff_{r}.json").read_text()) for r in range(2)]
+    assert [x["rank"] for x in a] == [0, 1] and all(x["world"] == 2 for x in a)
+    assert not set(a[0]["cpus"]) & set(a[1]["cpus"])
+    assert a[0]["omp"] == str(len(a[0]["cpus"]))
+    out = subprocess.run(launch + [str(ROOT / "tests" / "dist" / "comm_semantics.py")],
+                         env={**ENV, "OUT": str(tmp_path), "MLAPI_COMM": "fake"}, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert (tmp_path / "OK_1").read_text() == "fake-gloo"
+
+
+def test_launcher_propagates_failure(tmp_path):
+    t0 = time.monotonic()
+    out = subprocess.run([sys.executable, "-m", "mlapi_amd.launch", "--nproc", "2", "--grace", "2",
+                          str(ROOT / "tests" / "dist" / "affinity.py")],
+                         env={**ENV, "OUT": str(tmp_path), "FAIL_RANK": "1"}, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 7, out.stderr
+    assert time.monotonic() - t0 < 30  # the sleeping rank was stopped, not waited for
+    assert "rank 1 exited with 7" in out.stderr
+
+
 def test_dp_serving_reload(tmp_path, iris_pickle_bytes):
     import httpx
 
