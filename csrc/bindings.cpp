@@ -331,10 +331,11 @@ PYBIND11_MODULE(_C, m) {
   // ---- native RCCL communicator (csrc/dist/comm.h)
   py::class_<RcclComm>(m, "RcclComm")
       .def(py::init([](py::bytes id, int rank, int world, int device) {
-             return new RcclComm(std::string(id), rank, world, device);
+             std::string uid = id;  // copy while holding the GIL, then release it for ncclCommInitRank
+             py::gil_scoped_release nogil;
+             return new RcclComm(uid, rank, world, device);
            }),
-           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"),
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
       .def_static("version", &RcclComm::version)
       .def_static("library_path", &RcclComm::library_path)
