@@ -24,12 +24,12 @@ for s in $steps; do
       timeout -k 10 300 python bench.py --steps 200 --warmup 20 > gpurun_out/bench_serve.log 2>&1
       rc=$?; tail -3 gpurun_out/bench_serve.log; ok_or_stop $rc ;;
     kbench)
-      for m in gemv gemm train; do
+      for m in gemv gemm train train_softmax; do
         timeout -k 10 300 python bench.py --mode $m --steps 100 --warmup 10 > gpurun_out/bench_$m.log 2>&1
         rc=$?; tail -2 gpurun_out/bench_$m.log; ok_or_stop $rc
       done ;;
     prof)
-      for m in gemv gemm train; do
+      for m in gemv gemm train train_softmax; do
         timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$m -o $m -- \
           python3 bench.py --mode $m --steps 20 --warmup 2 > gpurun_out/prof_$m.log 2>&1
         rc=$?; tail -2 gpurun_out/prof_$m.log; ok_or_stop $rc
