@@ -64,25 +64,19 @@ __device__ __forceinline__ RowState shfl_state(RowState a, int off) {
   return RowState{__shfl_xor(a.m, off, 64), __shfl_xor(a.s, off, 64), __shfl_xor(a.bi, off, 64)};
 }
 
-// LDS byte offset of 16-byte chunk `ch` of class row `r` in a [64][NCH * 8] bf16 image. Chunks are
-// XOR-swizzled with the class row inside aligned groups of 16 (conflict-free ds_read_b128 of 16
-// classes at one k-offset); a trailing partial group (F_aug = F + 32 in training: 36, 68, ... chunks)
-// is swizzled within its own power-of-two width so no chunk leaves its row.
-template <int NCH>
-__device__ __forceinline__ int lds_off(int r, int ch, int row_bytes) {
-  constexpr int FULL = NCH & ~15;
-  constexpr int TAIL = NCH - FULL;
-  static_assert((TAIL & (TAIL - 1)) == 0, "chunk tail must be a power of two");
-  const int mask = ch < FULL ? 15 : (TAIL > 0 ? TAIL - 1 : 0);
-  return r * row_bytes + ((ch ^ (r & mask)) << 4);
+// LDS image of a 64-class W chunk: [64 rows][KS * 64 B], row stride padded by 32 B. With the
+// fragment reads (16 classes x one 16-B chunk per lane group, ds_read_b128 lane groups of
+// MI355X_MICROARCH.md "LDS") the padded stride is conflict-free for every KS >= 2 and the staging
+// writes stay within 8.9 of 8 cycles; the former XOR swizzle on unpadded rows was 2-way conflicted
+// at the training widths (F_aug = 288: SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS = 3.3 cycles per
+// instruction, profiles/r1_pmc). KS = 1 (F = 32) keeps unpadded rows with an (r >> 1) swizzle.
+template <int KS>
+__host__ __device__ constexpr int lds_row_stride() {
+  return KS == 1 ? 64 : KS * 64 + 32;
 }
-// Same, for the fragment reads: chunk = 4 * ks + q with ks compile-time, so the mask folds.
-template <int NCH>
-__device__ __forceinline__ int lds_off_k(int r, int ks, int q, int row_bytes) {
-  constexpr int FULL = NCH & ~15;
-  constexpr int TAIL = NCH - FULL;
-  const int mask = 4 * ks < FULL ? 15 : (TAIL > 0 ? TAIL - 1 : 0);
-  return r * row_bytes + (((4 * ks + q) ^ (r & mask)) << 4);
+template <int KS>
+__device__ __forceinline__ int lds_off(int r, int ch) {
+  return r * lds_row_stride<KS>() + ((KS == 1 ? (ch ^ ((r >> 1) & 3)) : ch) << 4);
 }
 
 struct GemmArgs {
@@ -130,7 +124,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   constexpr int F_ = KS * 32;
   constexpr int ROW_BYTES = F_ * 2;
   constexpr int NCH = F_ / 8;                          // 16-byte chunks per W row
-  constexpr int BUF_BYTES = CLASS_CHUNK * ROW_BYTES;
+  constexpr int BUF_BYTES = CLASS_CHUNK * lds_row_stride<KS>();
   constexpr int PIECES = CLASS_CHUNK * NCH / 256;      // 16-byte pieces per thread per chunk (== KS)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF_BYTES + 16];
   int* const flag = reinterpret_cast<int*>(smem + 2 * BUF_BYTES);
@@ -188,7 +182,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                                                  \
     const int p = tid + i * 256;                                                                        \
     const int r = p / NCH, ch = p % NCH;                                                                \
-    *reinterpret_cast<u32x4_t*>(smem + (BUF) * BUF_BYTES + lds_off<NCH>(r, ch, ROW_BYTES)) = stage[i]; \
+    *reinterpret_cast<u32x4_t*>(smem + (BUF) * BUF_BYTES + lds_off<KS>(r, ch)) = stage[i];            \
   }
 
   RowState st[NT];
@@ -224,7 +218,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
       bf16x8_t wf[4];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
-        wf[mt] = *reinterpret_cast<const bf16x8_t*>(wb + lds_off_k<NCH>(mt * 16 + col, ks, q, ROW_BYTES));
+        wf[mt] = *reinterpret_cast<const bf16x8_t*>(wb + lds_off<KS>(mt * 16 + col, 4 * ks + q));
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll

@@ -1,0 +1,55 @@
+"""Summarise tools/pmc_profile.sh output: per bench and kernel, mean counter values per dispatch
+plus derived rates (HBM bytes and GB/s, MFMA busy %, LDS bank-conflict cycles per LDS instruction)."""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+# (bench, kernel) -> counter -> [values per dispatch]; plus kernel durations
+vals = defaultdict(lambda: defaultdict(list))
+dur = defaultdict(list)
+for d in sorted(glob.glob(os.path.join(root, "*_*"))):
+    if not os.path.isdir(d):
+        continue
+    bench = os.path.basename(d).rsplit("_", 1)[0]
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        per = defaultdict(float)  # (dispatch, kernel, counter) summed over dimensions
+        for r in csv.DictReader(open(f)):
+            k = r.get("Kernel_Name", "?")
+            per[(r.get("Dispatch_Id"), k, r["Counter_Name"])] += float(r["Counter_Value"])
+        for (disp, k, c), v in per.items():
+            vals[(bench, k)][c].append(v)
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            dur[(bench, r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+
+
+def mean(x):
+    return sum(x) / len(x) if x else float("nan")
+
+
+print("| bench | kernel | µs | FETCH MB | WRITE MB | HBM GB/s* | MFMA busy % | bf16 MFMA MOPs | LDS confl/instr | VALU instr | waves |")
+print("|---|---|---|---|---|---|---|---|---|---|---|")
+for (bench, k), cs in sorted(vals.items()):
+    if not k.startswith("void mlapi") and "mlapi" not in k and not k.startswith("Cijk"):
+        continue
+    us = mean(dur.get((bench, k), []))
+    fetch = mean(cs.get("FETCH_SIZE", [])) / 1024  # KB -> MB
+    write = mean(cs.get("WRITE_SIZE", [])) / 1024
+    busy = mean(cs.get("SQ_VALU_MFMA_BUSY_CYCLES", []))
+    sqb = mean(cs.get("SQ_BUSY_CYCLES", []))
+    mfma_pct = 100 * busy / sqb if sqb == sqb and sqb else float("nan")
+    lds_c = mean(cs.get("SQ_LDS_BANK_CONFLICT", []))
+    lds_i = mean(cs.get("SQ_INSTS_LDS", []))
+    name = k.replace("void mlapi::(anonymous namespace)::", "")[:60]
+    gbs = (fetch + write) * 1e3 / us if us == us and us else float("nan")  # MB / us -> GB/s
+    print(f"| {bench} | `{name}` | {us:.1f} | {fetch:.1f} | {write:.1f} | {gbs:.0f} | {mfma_pct:.1f} | "
+          f"{mean(cs.get('SQ_INSTS_VALU_MFMA_MOPS_BF16', [])):.3g} | "
+          f"{(lds_c / lds_i if lds_i else float('nan')):.3f} | {mean(cs.get('SQ_INSTS_VALU', [])):.3g} | "
+          f"{mean(cs.get('SQ_WAVES', [])):.0f} |")
+print()
+print("*HBM GB/s = (FETCH_SIZE + WRITE_SIZE) / kernel time; on gfx950 FETCH_SIZE reads about half of")
+print(" the streamed bytes (MI355X_MICROARCH.md), so the true read rate is up to 2x this column.")
+print(" Kernel time here is measured under counter collection (serialised dispatches).")
