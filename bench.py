@@ -98,12 +98,16 @@ def bench_serve(args, info):
         # batch=1: one connection, closed loop
         lg1 = C().Loadgen("127.0.0.1", srv.port, req, 1, 1, 60.0)
         lg1.run(200, False)
+        s2 = srv.runtime.handle.stats()
         r1 = lg1.run(args.c1_requests, True)
+        s3 = srv.runtime.handle.stats()
         lg1.close()
         lat1 = r1["latencies_ns"] / 1e6
         per_rank = all_gather_floats([np.percentile(lat, 50), np.percentile(lat, 99), np.percentile(lat1, 50),
                                       np.percentile(lat1, 99), r1["completed"] / r1["elapsed_s"],
-                                      (s1["requests"] - s0["requests"]) / max(1, s1["batches"] - s0["batches"])],
+                                      (s1["requests"] - s0["requests"]) / max(1, s1["batches"] - s0["batches"]),
+                                      (s1["device_us_sum"] - s0["device_us_sum"]) / max(1, s1["batches"] - s0["batches"]),
+                                      (s3["device_us_sum"] - s2["device_us_sum"]) / max(1, s3["batches"] - s2["batches"])],
                                      info)
         barrier(info)
     finally:
@@ -117,6 +121,9 @@ def bench_serve(args, info):
         "p99_latency_ms_batch1": float(np.max(per_rank[:, 3])),
         "req_per_s_batch1_per_rank": float(np.min(per_rank[:, 4])),
         "mean_gpu_batch_rows": float(np.mean(per_rank[:, 5])),
+        # launch -> completion seen by the completer thread, per batch (the GPU leg of a request)
+        "gpu_leg_us_c64": float(np.mean(per_rank[:, 6])),
+        "gpu_leg_us_batch1": float(np.mean(per_rank[:, 7])),
         "backend": srv.runtime.handle.backend,
         "cpu_cores_busy_rank0": cpu_util,
         "threads": {"io": args.io_threads, "loadgen": args.client_threads},

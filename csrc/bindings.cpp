@@ -244,7 +244,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("max_features", &EngineConfig::max_features)
       .def_readwrite("watchdog_ms", &EngineConfig::watchdog_ms)
       .def_readwrite("fail_every", &EngineConfig::fail_every)
-      .def_readwrite("delay_us", &EngineConfig::delay_us);
+      .def_readwrite("delay_us", &EngineConfig::delay_us)
+      .def_readwrite("spin_us", &EngineConfig::spin_us);
 
   py::class_<PySink>(m, "PySink").def(py::init<>()).def("fd", &PySink::fd).def("drain", &PySink::drain);
 

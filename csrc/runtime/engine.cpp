@@ -206,6 +206,7 @@ int Engine::submit_many(const double* X, int n, int nf, const uint64_t* tags, Si
     int32_t off = (int32_t)q_x_.size();
     q_x_.insert(q_x_.end(), X, X + (size_t)n * nf);
     for (int i = 0; i < n; ++i, off += nf) q_meta_.push_back(Meta{tags[i], sink, t, nf, off});
+    q_count_.store((int)q_meta_.size(), std::memory_order_release);
     wake = batcher_sleeping_;
   }
   if (wake) q_cv_.notify_one();
@@ -331,9 +332,15 @@ void Engine::batcher_loop() {
   metas.reserve(4096);
   xs.reserve(4096 * 8);
   for (;;) {
+    if (cfg_.spin_us > 0 && q_count_.load(std::memory_order_acquire) == 0) {
+      // Adaptive spin: under load the next request arrives within microseconds; polling the
+      // queue counter avoids the submitter's futex wake (several us on the request path).
+      const int64_t until = now_ns() + (int64_t)cfg_.spin_us * 1000;
+      while (q_count_.load(std::memory_order_acquire) == 0 && now_ns() < until) _mm_pause();
+    }
     {
       std::unique_lock<std::mutex> lk(q_mu_);
-      batcher_sleeping_ = true;
+      if (q_meta_.empty()) batcher_sleeping_ = true;
       q_cv_.wait(lk, [&] { return stopping_ || !q_meta_.empty(); });
       if (q_meta_.empty() && stopping_) break;
       if (cfg_.max_wait_us > 0 && (int)q_meta_.size() < cfg_.max_batch && !stopping_) {
@@ -345,6 +352,7 @@ void Engine::batcher_loop() {
       xs.swap(q_x_);
       q_meta_.clear();
       q_x_.clear();
+      q_count_.store(0, std::memory_order_release);
     }
     const std::shared_ptr<const Model> m = model();
     size_t pos = 0;

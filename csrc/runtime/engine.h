@@ -80,6 +80,8 @@ struct EngineConfig {
   int watchdog_ms = 2000; // batch not complete after this -> engine marked unhealthy
   int fail_every = 0;     // fault injection: fail every N-th batch with ST_DEVICE_ERROR
   int delay_us = 0;       // fault injection: extra per-batch delay
+  int spin_us = 0;        // batcher polls the queue this long before sleeping on the condvar
+                          // (saves the futex wake-up on the request path under load)
 };
 
 struct EngineStats {
@@ -163,6 +165,7 @@ class Engine {
   std::vector<double> q_x_;
   bool stopping_ = false;
   bool batcher_sleeping_ = false;  // guarded by q_mu_: submit wakes the batcher only if true
+  std::atomic<int> q_count_{0};    // rows queued (lock-free hint for the batcher's spin phase)
 
   // GPU slots
   hipStream_t stream_ = nullptr;

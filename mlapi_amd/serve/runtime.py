@@ -52,6 +52,7 @@ class EngineHandle:
         ec.watchdog_ms = config.watchdog_ms
         ec.fail_every = config.fail_every
         ec.delay_us = config.delay_us
+        ec.spin_us = config.spin_us
         self.engine = c.Engine(ec)
         self._models: Dict[int, LinearModel] = {}
         self._lock = threading.Lock()

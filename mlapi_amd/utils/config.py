@@ -37,6 +37,7 @@ class Config:
     watchdog_ms: int = 2000
     fail_every: int = 0                       # fault injection (tests): fail every N-th batch
     delay_us: int = 0                         # fault injection: delay every batch
+    spin_us: int = 0                          # batcher spin before sleeping (0 = always sleep)
     # HTTP
     host: str = "127.0.0.1"
     port: int = 8000
