@@ -35,6 +35,8 @@ typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 
 constexpr int CLASS_CHUNK = 64;
+constexpr float LOG2E_F = 1.4426950408889634f;
+constexpr float LN2_F = 0.6931471805599453f;
 constexpr int COUNTER_BYTES = 4096;  // per-row-block arrival counters live at the start of the workspace
 
 struct RowState {
@@ -107,7 +109,7 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 
 // KS = F/32 (exact), NT = 16-row N-tiles per wave, MODE: 0 = fused predict epilogue,
 // 1 = write logits, 2 = training row stats, 3 = training gradient (see header).
-template <int KS, int NT, int MODE>
+template <int KS, int NT, int MODE, bool OVR>
 __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   const uint16_t* __restrict__ X = a.X;
   const uint16_t* __restrict__ W = a.W;
@@ -135,7 +137,8 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   const int wave = tid >> 6;
   const int q = lane >> 4;
   const int col = lane & 15;
-  const bool ovr = kind == KIND_OVR;
+  constexpr bool ovr = OVR;
+  (void)kind;
   const int64_t row0 = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wave * ROWS_PER_WAVE;
   const int c_begin = blockIdx.y * classes_per_split;
   const int c_end = min(K, c_begin + classes_per_split);
@@ -199,19 +202,20 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
     // chunk address is re-loaded into the idle buffer instead of branching around the loads.
     const int c_next = min(c0 + CLASS_CHUNK, c_last);
     MLAPI_LOAD_CHUNK(c_next)
-    // bias for this chunk's classes, also loaded unconditionally (clamped index, masked value);
-    // the training modes carry the intercept inside W.
-    float bv[4][4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bv[mt][r] = MODE >= 2 ? 0.f : bias[min(c0 + mt * 16 + q * 4 + r, K - 1)];
-
+    // The accumulators start at the bias (clamped index; classes past the split are masked
+    // later), so the epilogue needs no per-element add; the training modes carry the intercept
+    // inside W and start at zero.
     f32x4_t acc[NT][4];
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int mt = 0; mt < 4; ++mt) {
+      f32x4_t b0 = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      if constexpr (MODE <= 1) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[t][mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < 4; ++r) b0[r] = bias[min(c0 + mt * 16 + q * 4 + r, K - 1)];
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t][mt] = b0;
+    }
     const unsigned char* wb = smem + buf * BUF_BYTES;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -226,69 +230,90 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
           acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt], xf[t][ks], acc[t][mt], 0, 0, 0);
     }
 
-    // epilogue for this chunk: lane owns classes c0 + mt*16 + q*4 + r of batch row (t, col)
+    // Epilogue: lane owns classes c0 + mt*16 + q*4 + r (i = mt*4 + r, increasing class order) of
+    // batch row (t, col). Only a split's last chunk can hold classes >= c_end (wave-uniform test);
+    // they are masked to -inf, which every reduction below maps to "absent" (exp2 -> 0,
+    // sigmoid -> 0, never the max). No per-element branches: a runtime kind or bound check here
+    // made hipcc emit exec-mask branches around every element (SQ_INSTS_VALU 5.4k per wave).
+    const bool partial = c0 + CLASS_CHUNK > c_end;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = acc[t][i >> 2][i & 3];
+      if (partial) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = c0 + (i >> 2) * 16 + q * 4 + (i & 3) < c_end ? v[i] : -INFINITY;
+      }
       if constexpr (MODE == 1) {
         const int64_t row = row0 + t * 16 + col;
         if (row < B) {
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int cls = c0 + mt * 16 + q * 4 + r;
-              if (cls < c_end) a.Z[row * K + cls] = acc[t][mt][r] + bv[mt][r];
-            }
+          for (int i = 0; i < 16; ++i) {
+            const int cls = c0 + (i >> 2) * 16 + q * 4 + (i & 3);
+            if (cls < c_end) a.Z[row * K + cls] = v[i];
+          }
         }
       } else if constexpr (MODE == 3) {
         const int64_t row = row0 + t * 16 + col;
         const bool row_ok = row < B;
+        const float lse2 = lse[t] * LOG2E_F;
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
           const int cls0 = c0 + mt * 16 + q * 4;  // 4 consecutive classes -> one 8-byte store
           float g[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int cls = cls0 + r;
-            const float z = acc[t][mt][r];
-            const bool hot = cls == yl[t];
-            const bool live = row_ok && cls < c_end;
-            const float pr = ovr ? sigmoidf_(z) : __expf(z - lse[t]);
-            g[r] = live ? pr - (hot ? 1.f : 0.f) : 0.f;
-            // softmax CE: lse - z_y (owned by the lane holding class y); OvR: sum of BCE terms
-            const float l = ovr ? fmaxf(z, 0.f) - (hot ? z : 0.f) + log1pf(__expf(-fabsf(z))) : lse[t] - z;
-            loss_acc += (live && (ovr || hot)) ? l : 0.f;
+            const float z = v[mt * 4 + r];
+            const bool hot = cls0 + r == yl[t];
+            float pr, l;
+            if constexpr (OVR) {
+              const float e = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E_F);  // exp(-|z|) in (0, 1]
+              pr = z >= 0.f ? __builtin_amdgcn_rcpf(1.f + e) : e * __builtin_amdgcn_rcpf(1.f + e);
+              // BCE: softplus(z) - z*[hot]; softplus(z) = max(z, 0) + log(1 + exp(-|z|))
+              l = fmaxf(z, 0.f) - (hot ? z : 0.f) + __builtin_amdgcn_logf(1.f + e) * LN2_F;
+              l = z == -INFINITY ? 0.f : l;
+            } else {
+              pr = __builtin_amdgcn_exp2f(fmaf(z, LOG2E_F, -lse2));
+              l = hot ? lse[t] - z : 0.f;
+            }
+            g[r] = row_ok && z != -INFINITY ? pr - (hot ? 1.f : 0.f) : 0.f;
+            loss_acc += row_ok ? l : 0.f;
           }
           if (row_ok && cls0 < c_end)
             *reinterpret_cast<uint2*>(a.G + row * a.ldg + cls0) = make_uint2(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]));
         }
-      } else {
-        float cm = -INFINITY;
-        int ci = 0x7fffffff;
+      } else {  // MODE 0 / 2: online (max, sum, first argmax)
+        float cm = v[0];
+        int ci = 0;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int cls = c0 + mt * 16 + q * 4 + r;
-            const float v = acc[t][mt][r] + bv[mt][r];
-            if (cls < c_end && v > cm) { cm = v; ci = cls; }
-          }
-        RowState& S = st[t];
-        if (cm > S.m) {
-          if (!ovr) S.s = S.m == -INFINITY ? 0.f : S.s * __expf(S.m - cm);
-          S.m = cm;
-          S.bi = ci;
+        for (int i = 1; i < 16; ++i) {
+          const bool gt = v[i] > cm;  // strict: the first (lowest class) maximum wins
+          cm = gt ? v[i] : cm;
+          ci = gt ? i : ci;
         }
-        float add = 0.f;
+        RowState& S = st[t];
+        const bool take = cm > S.m;
+        const float m_new = take ? cm : S.m;
+        if constexpr (OVR) {
+          float add = 0.f;
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int cls = c0 + mt * 16 + q * 4 + r;
-            const float v = acc[t][mt][r] + bv[mt][r];
-            if (cls < c_end) add += ovr ? sigmoidf_(v) : __expf(v - S.m);
+          for (int i = 0; i < 16; ++i) {
+            const float e = __builtin_amdgcn_exp2f(-v[i] * LOG2E_F);  // -inf -> +inf -> sigmoid 0
+            add += __builtin_amdgcn_rcpf(1.f + e);
           }
-        S.s += add;
+          S.s += add;
+        } else {
+          const float m2 = m_new * LOG2E_F;
+          float add = 0.f;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) add += __builtin_amdgcn_exp2f(fmaf(v[i], LOG2E_F, -m2));
+          // rescale the running sum to the new max (S.m = -inf: nothing accumulated yet)
+          const float scale = S.m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(fmaf(S.m, LOG2E_F, -m2));
+          S.s = fmaf(S.s, scale, add);
+        }
+        S.bi = take ? c0 + (ci >> 2) * 16 + q * 4 + (ci & 3) : S.bi;
+        S.m = m_new;
       }
     }
     MLAPI_WRITE_CHUNK(buf ^ 1)
@@ -433,8 +458,13 @@ template <int MODE>
 void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
   const dim3 grid((unsigned)plan.row_blocks, (unsigned)plan.splits);
   args.classes_per_split = plan.classes_per_split;
-#define MLAPI_GEMM_LAUNCH(KSV, NTV) \
-  hipLaunchKernelGGL((gemm_softmax_kernel<KSV, NTV, MODE>), grid, dim3(256), 0, stream, args)
+#define MLAPI_GEMM_LAUNCH(KSV, NTV)                                                                      \
+  do {                                                                                                   \
+    if (args.kind == KIND_OVR)                                                                           \
+      hipLaunchKernelGGL((gemm_softmax_kernel<KSV, NTV, MODE, true>), grid, dim3(256), 0, stream, args); \
+    else                                                                                                 \
+      hipLaunchKernelGGL((gemm_softmax_kernel<KSV, NTV, MODE, false>), grid, dim3(256), 0, stream, args); \
+  } while (0)
   const int ks = F / 32;
   if constexpr (MODE <= 1) {  // predict / logits: F in {32, 64, 128, 256, 512}
     if (F != 32 && F != 64 && F != 128 && F != 256 && F != 512)
