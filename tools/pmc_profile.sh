@@ -14,8 +14,10 @@ declare -A GROUPS_=(
   [mfma]="SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES"
   [lds]="SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAVES"
   [valu]="SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES"
+  [stall]="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY"
+  [active]="SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM"
 )
-GROUP_ORDER="${PMC_GROUPS:-fetch write mfma lds valu}"
+GROUP_ORDER="${PMC_GROUPS:-fetch write mfma lds valu stall active}"
 BENCHES="${PMC_BENCHES:-gemv:--mode gemv --steps 5 --warmup 1|gemm:--mode gemm --steps 5 --warmup 1|gemm_big:--mode gemm --batch 262144 --steps 5 --warmup 1|train:--mode train --steps 5 --warmup 1|train_softmax:--mode train_softmax --steps 5 --warmup 1}"
 IFS='|' read -ra BL <<< "$BENCHES"
 for entry in "${BL[@]}"; do

@@ -30,26 +30,34 @@ def mean(x):
     return sum(x) / len(x) if x else float("nan")
 
 
-print("| bench | kernel | µs | FETCH MB | WRITE MB | HBM GB/s* | MFMA busy % | bf16 MFMA MOPs | LDS confl/instr | VALU instr | waves |")
-print("|---|---|---|---|---|---|---|---|---|---|---|")
+print("| bench | kernel | µs | FETCH MB | WRITE MB | HBM GB/s* | bf16 TFLOP/s | LDS confl/instr | VALU instr/wave | "
+      "wait % | wait-issue % | VALU-active % | LDS-active % | VMEM-active % | waves |")
+print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
 for (bench, k), cs in sorted(vals.items()):
     if not k.startswith("void mlapi") and "mlapi" not in k and not k.startswith("Cijk"):
         continue
     us = mean(dur.get((bench, k), []))
     fetch = mean(cs.get("FETCH_SIZE", [])) / 1024  # KB -> MB
     write = mean(cs.get("WRITE_SIZE", [])) / 1024
-    busy = mean(cs.get("SQ_VALU_MFMA_BUSY_CYCLES", []))
-    sqb = mean(cs.get("SQ_BUSY_CYCLES", []))
-    mfma_pct = 100 * busy / sqb if sqb == sqb and sqb else float("nan")
     lds_c = mean(cs.get("SQ_LDS_BANK_CONFLICT", []))
     lds_i = mean(cs.get("SQ_INSTS_LDS", []))
     name = k.replace("void mlapi::(anonymous namespace)::", "")[:60]
     gbs = (fetch + write) * 1e3 / us if us == us and us else float("nan")  # MB / us -> GB/s
-    print(f"| {bench} | `{name}` | {us:.1f} | {fetch:.1f} | {write:.1f} | {gbs:.0f} | {mfma_pct:.1f} | "
-          f"{mean(cs.get('SQ_INSTS_VALU_MFMA_MOPS_BF16', [])):.3g} | "
-          f"{(lds_c / lds_i if lds_i else float('nan')):.3f} | {mean(cs.get('SQ_INSTS_VALU', [])):.3g} | "
-          f"{mean(cs.get('SQ_WAVES', [])):.0f} |")
+    waves = mean(cs.get("SQ_WAVES", []))
+    wcyc = mean(cs.get("SQ_WAVE_CYCLES", []))
+
+    def pct(c):
+        return 100 * mean(cs.get(c, [])) / wcyc if wcyc == wcyc and wcyc else float("nan")
+
+    tflops = mean(cs.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", [])) * 512 / (us * 1e-6) / 1e12 if us == us and us else 0
+    print(f"| {bench} | `{name}` | {us:.1f} | {fetch:.1f} | {write:.1f} | {gbs:.0f} | {tflops:.0f} | "
+          f"{(lds_c / lds_i if lds_i else float('nan')):.3f} | {mean(cs.get('SQ_INSTS_VALU', [])) / waves:.0f} | "
+          f"{pct('SQ_WAIT_ANY'):.0f} | {pct('SQ_WAIT_INST_ANY'):.0f} | {pct('SQ_ACTIVE_INST_VALU'):.0f} | "
+          f"{pct('SQ_ACTIVE_INST_LDS'):.0f} | {pct('SQ_ACTIVE_INST_VMEM'):.0f} | {waves:.0f} |")
 print()
 print("*HBM GB/s = (FETCH_SIZE + WRITE_SIZE) / kernel time; on gfx950 FETCH_SIZE reads about half of")
 print(" the streamed bytes (MI355X_MICROARCH.md), so the true read rate is up to 2x this column.")
 print(" Kernel time here is measured under counter collection (serialised dispatches).")
+print(" bf16 TFLOP/s = SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512 / kernel time (dense peak ~2500).")
+print(" wait / active % = share of SQ_WAVE_CYCLES (summed over waves) spent waiting on anything /")
+print(" on instruction issue, or with a VALU / LDS / VMEM instruction in flight.")
