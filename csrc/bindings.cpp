@@ -203,29 +203,29 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("params"), py::arg("grad"), py::arg("mom"), py::arg("n"), py::arg("n_pen"), py::arg("lr"),
       py::arg("inv_n"), py::arg("l2"), py::arg("momentum"), py::arg("stream") = 0);
-  m.def("softmax_train_faug", &softmax_train_faug);
+  m.def("softmax_train_ldx", &softmax_train_ldx);
   m.def("softmax_train_workspace", &softmax_train_workspace);
   m.def(
       "softmax_train_grad",
-      [](uintptr_t X_aug, uintptr_t W_aug, uintptr_t y, int64_t B, int F_aug, int K, int kind, uintptr_t G,
-         int64_t ldg, uintptr_t stats_out, uintptr_t ws, size_t ws_bytes, uintptr_t stream) {
-        launch_softmax_train_grad(ptr<void>(X_aug), ptr<void>(W_aug), ptr<int32_t>(y), B, F_aug, K, kind,
+      [](uintptr_t X_aug, int64_t ldx, uintptr_t W, uintptr_t b, uintptr_t y, int64_t B, int F, int K, int kind,
+         uintptr_t G, int64_t ldg, uintptr_t stats_out, uintptr_t ws, size_t ws_bytes, uintptr_t stream) {
+        launch_softmax_train_grad(ptr<void>(X_aug), ldx, ptr<void>(W), ptr<float>(b), ptr<int32_t>(y), B, F, K, kind,
                                   ptr<void>(G), ldg, ptr<float>(stats_out), ptr<void>(ws), ws_bytes,
                                   stream_of(stream));
       },
-      py::arg("X_aug"), py::arg("W_aug"), py::arg("y"), py::arg("B"), py::arg("F_aug"), py::arg("K"),
-      py::arg("kind"), py::arg("G"), py::arg("ldg"), py::arg("stats_out"), py::arg("ws"), py::arg("ws_bytes"),
-      py::arg("stream") = 0);
+      py::arg("X_aug"), py::arg("ldx"), py::arg("W"), py::arg("b"), py::arg("y"), py::arg("B"), py::arg("F"),
+      py::arg("K"), py::arg("kind"), py::arg("G"), py::arg("ldg"), py::arg("stats_out"), py::arg("ws"),
+      py::arg("ws_bytes"), py::arg("stream") = 0);
   m.def(
       "sgd_update_2d",
       [](uintptr_t params, uintptr_t grad, uintptr_t mom, int64_t rows, int cols, int pen_cols, float lr,
-         float inv_n, float l2, float momentum, uintptr_t shadow, uintptr_t stream) {
+         float inv_n, float l2, float momentum, uintptr_t shadow_w, uintptr_t shadow_b, uintptr_t stream) {
         launch_sgd_update_2d(ptr<float>(params), ptr<float>(grad), ptr<float>(mom), rows, cols, pen_cols, lr, inv_n,
-                             l2, momentum, ptr<uint16_t>(shadow), stream_of(stream));
+                             l2, momentum, ptr<uint16_t>(shadow_w), ptr<float>(shadow_b), stream_of(stream));
       },
       py::arg("params"), py::arg("grad"), py::arg("mom"), py::arg("rows"), py::arg("cols"), py::arg("pen_cols"),
-      py::arg("lr"), py::arg("inv_n"), py::arg("l2"), py::arg("momentum"), py::arg("shadow"),
-      py::arg("stream") = 0);
+      py::arg("lr"), py::arg("inv_n"), py::arg("l2"), py::arg("momentum"), py::arg("shadow_w"),
+      py::arg("shadow_b"), py::arg("stream") = 0);
   m.def(
       "cast",
       [](int src_dt, uintptr_t src, int dst_dt, uintptr_t dst, int64_t n, uintptr_t stream) {

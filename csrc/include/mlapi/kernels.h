@@ -31,16 +31,18 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
 void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B, int F, int K, float* Z,
                         hipStream_t stream);
 
-// Multiclass training (gemm_softmax.hip, MODE 2 + 3): the intercept is folded into the GEMM, i.e.
-// X_aug = [X | 1 | 0...] and W_aug = [W | b | 0...] with F_aug = softmax_train_faug(F) columns.
-// Writes G = softmax(Z) - onehot(y) (OvR: sigmoid(Z) - onehot) as bf16 [B, ldg] and
-// stats_out = [loss_sum, n_correct]; dW_aug = G^T X_aug is then one library GEMM (hipBLASLt).
-// Workspace: softmax_train_workspace(B, K) bytes, zeroed once (split-merge counters re-arm).
-int softmax_train_faug(int F);  // -1 if F is not 32/64/128/256/512
-size_t softmax_train_workspace(int64_t B, int K);
-void launch_softmax_train_grad(const void* X_aug, const void* W_aug, const int32_t* y, int64_t B, int F_aug, int K,
-                               int kind, void* G, int64_t ldg, float* stats_out, void* workspace, size_t ws_bytes,
-                               hipStream_t stream);
+// Multiclass training (gemm_softmax.hip, MODE 2 + 3). X_aug = [X | 1 | 0 x 7] bf16 with row
+// stride ldx = softmax_train_ldx(F) = F + 8 (the forward reads the first F columns; the ones
+// column makes the backward GEMM produce the intercept gradient); W: [K, F] bf16; b: [K] f32.
+// Writes G = softmax(Z) - onehot(y) (OvR: sigmoid(Z) - onehot) as bf16 [B, ldg] (rows padded to a
+// multiple of 128: stores are unguarded) and stats_out = [loss_sum, n_correct];
+// dW_aug = G^T X_aug is then one library GEMM (hipBLASLt).
+// Workspace: softmax_train_workspace(B, K, F) bytes, zeroed once (split-merge counters re-arm).
+int softmax_train_ldx(int F);  // -1 unless F is 32/64/128/256/512
+size_t softmax_train_workspace(int64_t B, int K, int F);
+void launch_softmax_train_grad(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
+                               int64_t B, int F, int K, int kind, void* G, int64_t ldg, float* stats_out,
+                               void* workspace, size_t ws_bytes, hipStream_t stream);
 
 // ---- train kernels (train.hip) -----------------------------------------------------------------
 // Binary logistic regression, one pass over X: accumulates grad (F w-entries, 1 bias) and stats
@@ -70,11 +72,12 @@ void launch_sgd_update(float* params, const float* grad, float* momentum_buf, in
 
 // Deterministic column sums of [nslabs][width] f32 partial slabs -> out[width].
 void launch_reduce_slabs_f32(const float* slabs, int nslabs, int width, float* out, hipStream_t stream);
-// SGD step on a row-major [rows, cols] f32 matrix whose first pen_cols columns are L2-penalized
-// (the intercept column of W_aug is not); optionally refreshes a bf16 shadow copy in the same pass.
+// SGD step on a row-major [rows, cols] f32 matrix W_aug = [W | b | pad] whose first pen_cols
+// columns are L2-penalized (the intercept column is not); optionally refreshes in the same pass the
+// copies the next forward reads: shadow_w = bf16 W [rows, pen_cols], shadow_b = f32 column pen_cols.
 void launch_sgd_update_2d(float* params, const float* grad, float* momentum_buf, int64_t rows, int cols,
-                          int pen_cols, float lr, float inv_n, float l2, float momentum, uint16_t* shadow_bf16,
-                          hipStream_t stream);
+                          int pen_cols, float lr, float inv_n, float l2, float momentum, uint16_t* shadow_w,
+                          float* shadow_b, hipStream_t stream);
 
 // ---- pack.hip ----------------------------------------------------------------------------------
 void launch_cast(int src_dt, const void* src, int dst_dt, void* dst, int64_t n, hipStream_t stream);

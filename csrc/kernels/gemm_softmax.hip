@@ -8,18 +8,30 @@
 // an online (max, sum-exp, argmax) state over the classes it owns; the 4 lanes sharing a batch
 // row merge once at the end (2 xor-shuffles). No LDS is needed for the epilogue.
 //
-// Data movement (v2, after profiles/r1_first/gemm_kernel_stats.csv showed the v1 kernel exposing
-// one L2/HBM latency per k-step by loading W fragments straight to registers):
+// Data movement (v3):
 //  * X: each wave loads its NT x 16 batch rows for the whole F once, straight to registers;
-//  * W: 64-class chunks are staged cooperatively by all 4 waves into a double-buffered LDS image
-//    [64 classes][F] with a 16-byte-chunk XOR swizzle (chunk ^ (class & 15)), which makes the
-//    ds_read_b128 fragment reads (16 classes x 16 B at one k-offset per lane group) conflict-free;
-//    the global loads for chunk c+1 are issued before the MFMAs of chunk c and written to LDS
-//    after them (T14 issue-early / write-late), one barrier per chunk;
+//  * W: 64-class chunks are DMA'd by all 4 waves (global_load_lds_dwordx4) into a double-buffered
+//    LDS image [64 classes][F] whose 16-byte chunks are XOR-swizzled by class (chunk ^ (class & 15))
+//    on the source side, so the ds_read_b128 fragment reads (16 classes x 16 B at one k-offset per
+//    lane group) are conflict-free; chunk c+1 streams in while chunk c computes, one barrier per
+//    chunk. Without staging registers a wave can hold 32 rows (NT = 2), halving the LDS fragment
+//    reads per MFMA (B=262144: 230 -> 172 us);
 //  * small batches (B=1024 -> 16 row blocks) split the class range over gridDim.y so the launch
 //    fills the chip; the splits are merged IN THE SAME LAUNCH by the last-arriving block of each
 //    row block (agent-scope release fence + relaxed ticket, acquire fence in the reducer:
-//    Guideline 16), replacing v1's separate merge kernel (7.3 us of a 18.6 us total).
+//    Guideline 16), replacing v1's separate merge kernel (7.3 us of a 18.6 us total);
+//  * the epilogue is branch-free per element (kind is a template parameter; a split's partial
+//    last chunk is masked to -inf) and uses exp2/rcp; accumulators start at the bias.
+//
+// Training (multinomial / OvR mini-batch SGD, SURVEY 2.3 K6 at BASELINE config 5 scale) reuses the
+// same tiles with two more epilogues. X carries a ones column for the backward GEMM
+// (X_aug = [X | 1 | 0 x 7], row stride F + 8; the forward reads only its first F columns), so
+// dW_aug = G^T X_aug (one library GEMM) also yields the intercept gradient:
+//  * MODE 2 (row stats): the online (max, sum-exp, argmax) state, merged across class splits like
+//    MODE 0, is published as {lse = m + log s, argmax} per row;
+//  * MODE 3 (gradient): recomputes the logits tile by tile (cheaper than a B x K f32 round trip
+//    through HBM) and writes G = softmax(z) - onehot(y) (OvR: sigmoid(z) - onehot) in bf16, plus
+//    per-block [loss_sum, n_correct] slabs.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -66,25 +78,35 @@ __device__ __forceinline__ RowState shfl_state(RowState a, int off) {
   return RowState{__shfl_xor(a.m, off, 64), __shfl_xor(a.s, off, 64), __shfl_xor(a.bi, off, 64)};
 }
 
-// LDS image of a 64-class W chunk: [64 rows][KS * 64 B], row stride padded by 32 B. With the
-// fragment reads (16 classes x one 16-B chunk per lane group, ds_read_b128 lane groups of
-// MI355X_MICROARCH.md "LDS") the padded stride is conflict-free for every KS >= 2 and the staging
-// writes stay within 8.9 of 8 cycles; the former XOR swizzle on unpadded rows was 2-way conflicted
-// at the training widths (F_aug = 288: SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS = 3.3 cycles per
-// instruction, profiles/r1_pmc). KS = 1 (F = 32) keeps unpadded rows with an (r >> 1) swizzle.
+// LDS image of a 64-class W chunk: [64 rows][KS * 64 B], filled by LDS-DMA, whose destination is
+// lane-linear per wave-instruction: rows are unpadded and the fragment reads' conflict-free
+// swizzle (16-B chunk ^ (row & 15); KS = 1: ^ ((row >> 1) & 3)) is applied on the SOURCE address.
+// Every width is a power of two (the host pads F; the training X_aug is read with its own row
+// stride), for which this layout is conflict-free on the ds_read_b128 lane groups.
 template <int KS>
 __host__ __device__ constexpr int lds_row_stride() {
-  return KS == 1 ? 64 : KS * 64 + 32;
+  return KS * 64;
+}
+// Position of 16-byte chunk `ch` of row `r` inside its row (an involution: also maps a row
+// position back to the chunk that belongs there).
+template <int KS>
+__device__ __forceinline__ int lds_pos(int r, int ch) {
+  if constexpr (KS == 1) return ch ^ ((r >> 1) & 3);
+  return ch ^ (r & (KS * 4 >= 16 ? 15 : KS * 4 - 1));
 }
 template <int KS>
 __device__ __forceinline__ int lds_off(int r, int ch) {
-  return r * lds_row_stride<KS>() + ((KS == 1 ? (ch ^ ((r >> 1) & 3)) : ch) << 4);
+  return r * lds_row_stride<KS>() + (lds_pos<KS>(r, ch) << 4);
 }
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void glob_void_t;
 
 struct GemmArgs {
   const uint16_t* X;
   const uint16_t* W;
-  const float* bias;       // MODE 0/1 only (MODE 2/3: intercept folded into W)
+  const float* bias;       // [K] f32 (every mode)
+  int64_t ldx;             // X row stride in elements (F, or F + 8 for the training X_aug)
   int64_t B;
   int K;
   int kind;
@@ -107,6 +129,126 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return lo | (hi << 16);
 }
 
+// One 64-class chunk against the LDS image `wb`: MFMAs into bias-initialised accumulators, then the
+// mode's epilogue. Inlined into the kernel (reference parameters stay in registers).
+template <int KS, int NT, int MODE, bool OVR>
+__device__ __forceinline__ void compute_chunk(const unsigned char* wb, const bf16x8_t (&xf)[NT][KS], int c0, int c_end,
+                                              int q, int col, int64_t row0, int64_t B, int K, const float* bias,
+                                              const GemmArgs& a, RowState (&st)[NT], const int (&yl)[NT],
+                                              const float (&lse)[NT], float& loss_acc) {
+  constexpr bool ovr = OVR;
+  // The accumulators start at the bias (clamped index; classes past the split are masked
+  // later), so the epilogue needs no per-element add.
+  f32x4_t acc[NT][4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    f32x4_t b0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b0[r] = bias[min(c0 + mt * 16 + q * 4 + r, K - 1)];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t][mt] = b0;
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    bf16x8_t wf[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+      wf[mt] = *reinterpret_cast<const bf16x8_t*>(wb + lds_off<KS>(mt * 16 + col, 4 * ks + q));
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt], xf[t][ks], acc[t][mt], 0, 0, 0);
+  }
+
+  // Epilogue: lane owns classes c0 + mt*16 + q*4 + r (i = mt*4 + r, increasing class order) of
+  // batch row (t, col). Only a split's last chunk can hold classes >= c_end (wave-uniform test);
+  // they are masked to -inf, which every reduction below maps to "absent" (exp2 -> 0,
+  // sigmoid -> 0, never the max). No per-element branches: a runtime kind or bound check here
+  // made hipcc emit exec-mask branches around every element (SQ_INSTS_VALU 5.4k per wave).
+  const bool partial = c0 + CLASS_CHUNK > c_end;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = acc[t][i >> 2][i & 3];
+    if (partial) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = c0 + (i >> 2) * 16 + q * 4 + (i & 3) < c_end ? v[i] : -INFINITY;
+    }
+    if constexpr (MODE == 1) {
+      const int64_t row = row0 + t * 16 + col;
+      if (row < B) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int cls = c0 + (i >> 2) * 16 + q * 4 + (i & 3);
+          if (cls < c_end) a.Z[row * K + cls] = v[i];
+        }
+      }
+    } else if constexpr (MODE == 3) {
+      const int64_t row = row0 + t * 16 + col;
+      const bool row_ok = row < B;
+      const float lse2 = lse[t] * LOG2E_F;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int cls0 = c0 + mt * 16 + q * 4;  // 4 consecutive classes -> one 8-byte store
+        float g[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float z = v[mt * 4 + r];
+          const bool hot = cls0 + r == yl[t];
+          float pr, l;
+          if constexpr (OVR) {
+            const float e = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E_F);  // exp(-|z|) in (0, 1]
+            pr = z >= 0.f ? __builtin_amdgcn_rcpf(1.f + e) : e * __builtin_amdgcn_rcpf(1.f + e);
+            // BCE: softplus(z) - z*[hot]; softplus(z) = max(z, 0) + log(1 + exp(-|z|))
+            l = fmaxf(z, 0.f) - (hot ? z : 0.f) + __builtin_amdgcn_logf(1.f + e) * LN2_F;
+            l = z == -INFINITY ? 0.f : l;
+          } else {
+            pr = __builtin_amdgcn_exp2f(fmaf(z, LOG2E_F, -lse2));
+            l = hot ? lse[t] - z : 0.f;
+          }
+          g[r] = row_ok && z != -INFINITY ? pr - (hot ? 1.f : 0.f) : 0.f;
+          loss_acc += row_ok ? l : 0.f;
+        }
+        if (row_ok && cls0 < c_end)
+          *reinterpret_cast<uint2*>(a.G + row * a.ldg + cls0) = make_uint2(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]));
+      }
+    } else {  // MODE 0 / 2: online (max, sum, first argmax)
+      float cm = v[0];
+      int ci = 0;
+#pragma unroll
+      for (int i = 1; i < 16; ++i) {
+        const bool gt = v[i] > cm;  // strict: the first (lowest class) maximum wins
+        cm = gt ? v[i] : cm;
+        ci = gt ? i : ci;
+      }
+      RowState& S = st[t];
+      const bool take = cm > S.m;
+      const float m_new = take ? cm : S.m;
+      if constexpr (OVR) {
+        float add = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float e = __builtin_amdgcn_exp2f(-v[i] * LOG2E_F);  // -inf -> +inf -> sigmoid 0
+          add += __builtin_amdgcn_rcpf(1.f + e);
+        }
+        S.s += add;
+      } else {
+        const float m2 = m_new * LOG2E_F;
+        float add = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) add += __builtin_amdgcn_exp2f(fmaf(v[i], LOG2E_F, -m2));
+        // rescale the running sum to the new max (S.m = -inf: nothing accumulated yet)
+        const float scale = S.m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(fmaf(S.m, LOG2E_F, -m2));
+        S.s = fmaf(S.s, scale, add);
+      }
+      S.bi = take ? c0 + (ci >> 2) * 16 + q * 4 + (ci & 3) : S.bi;
+      S.m = m_new;
+    }
+  }
+}
+
 // KS = F/32 (exact), NT = 16-row N-tiles per wave, MODE: 0 = fused predict epilogue,
 // 1 = write logits, 2 = training row stats, 3 = training gradient (see header).
 template <int KS, int NT, int MODE, bool OVR>
@@ -124,7 +266,6 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   constexpr int ROWS_PER_WAVE = 16 * NT;
   constexpr int ROWS_PER_BLOCK = 4 * ROWS_PER_WAVE;
   constexpr int F_ = KS * 32;
-  constexpr int ROW_BYTES = F_ * 2;
   constexpr int NCH = F_ / 8;                          // 16-byte chunks per W row
   constexpr int BUF_BYTES = CLASS_CHUNK * lds_row_stride<KS>();
   constexpr int PIECES = CLASS_CHUNK * NCH / 256;      // 16-byte pieces per thread per chunk (== KS)
@@ -150,7 +291,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   for (int t = 0; t < NT; ++t) {
     int64_t r = row0 + t * 16 + col;
     r = r < B ? r : B - 1;
-    const uint16_t* xr = X + r * F_ + 8 * q;
+    const uint16_t* xr = X + r * a.ldx + 8 * q;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)  // X is streamed once: non-temporal, keep the L2 for W
       xf[t][ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + ks * 32));
@@ -173,156 +314,38 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
 
   // ---- W chunk staging: global -> registers (issue early) -> LDS (write late). Plain unrolled
   // code with ext_vector registers: a lambda capture or HIP_vector_type array goes to scratch.
-  u32x4_t stage[PIECES];
-#define MLAPI_LOAD_CHUNK(C0)                                                             \
-  _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                                   \
-    const int p = tid + i * 256;                                                         \
-    const int r = p / NCH, ch = p % NCH;                                                 \
-    const int cls = min((C0) + r, K - 1);                                                \
-    stage[i] = *reinterpret_cast<const u32x4_t*>(W + (int64_t)cls * F_ + ch * 8);        \
-  }
-#define MLAPI_WRITE_CHUNK(BUF)                                                                          \
+  // W staging: chunk c + 1 is DMA'd into the idle buffer while chunk c computes (no staging
+  // VGPRs, no ds_write pass); the barrier's vmcnt(0) retires it. On the last chunk the (valid)
+  // last chunk address is re-loaded instead of branching around the loads.
+  // Lane-linear destination: 16-B position P = i*256 + wave*64 + lane holds row P / NCH, in-row
+  // position P % NCH, i.e. source chunk lds_pos(row, P % NCH).
+#define MLAPI_DMA_CHUNK(C0, BUF)                                                                        \
   _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                                                  \
     const int p = tid + i * 256;                                                                        \
-    const int r = p / NCH, ch = p % NCH;                                                                \
-    *reinterpret_cast<u32x4_t*>(smem + (BUF) * BUF_BYTES + lds_off<KS>(r, ch)) = stage[i];            \
+    const int r = p / NCH;                                                                              \
+    const int cls = min((C0) + r, K - 1);                                                               \
+    const uint16_t* src = W + (int64_t)cls * F_ + lds_pos<KS>(r, p % NCH) * 8;                          \
+    __builtin_amdgcn_global_load_lds((glob_void_t*)src,                                                 \
+                                     (lds_void_t*)(smem + (BUF) * BUF_BYTES + (i * 256 + wave * 64) * 16), \
+                                     16, 0, 0);                                                         \
   }
 
   RowState st[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) st[t] = RowState{-INFINITY, 0.f, 0x7fffffff};
 
-  MLAPI_LOAD_CHUNK(c_begin)
-  MLAPI_WRITE_CHUNK(0)
-  __syncthreads();
-
   int buf = 0;
+  MLAPI_DMA_CHUNK(c_begin, 0)
+  __syncthreads();
   for (int c0 = c_begin; c0 < c_end; c0 += CLASS_CHUNK) {
-    // Next chunk's loads go out before this chunk's MFMAs. On the last chunk the (valid) last
-    // chunk address is re-loaded into the idle buffer instead of branching around the loads.
-    const int c_next = min(c0 + CLASS_CHUNK, c_last);
-    MLAPI_LOAD_CHUNK(c_next)
-    // The accumulators start at the bias (clamped index; classes past the split are masked
-    // later), so the epilogue needs no per-element add; the training modes carry the intercept
-    // inside W and start at zero.
-    f32x4_t acc[NT][4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      f32x4_t b0 = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      if constexpr (MODE <= 1) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) b0[r] = bias[min(c0 + mt * 16 + q * 4 + r, K - 1)];
-      }
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t][mt] = b0;
-    }
-    const unsigned char* wb = smem + buf * BUF_BYTES;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      bf16x8_t wf[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        wf[mt] = *reinterpret_cast<const bf16x8_t*>(wb + lds_off<KS>(mt * 16 + col, 4 * ks + q));
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-          acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt], xf[t][ks], acc[t][mt], 0, 0, 0);
-    }
-
-    // Epilogue: lane owns classes c0 + mt*16 + q*4 + r (i = mt*4 + r, increasing class order) of
-    // batch row (t, col). Only a split's last chunk can hold classes >= c_end (wave-uniform test);
-    // they are masked to -inf, which every reduction below maps to "absent" (exp2 -> 0,
-    // sigmoid -> 0, never the max). No per-element branches: a runtime kind or bound check here
-    // made hipcc emit exec-mask branches around every element (SQ_INSTS_VALU 5.4k per wave).
-    const bool partial = c0 + CLASS_CHUNK > c_end;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      float v[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = acc[t][i >> 2][i & 3];
-      if (partial) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = c0 + (i >> 2) * 16 + q * 4 + (i & 3) < c_end ? v[i] : -INFINITY;
-      }
-      if constexpr (MODE == 1) {
-        const int64_t row = row0 + t * 16 + col;
-        if (row < B) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int cls = c0 + (i >> 2) * 16 + q * 4 + (i & 3);
-            if (cls < c_end) a.Z[row * K + cls] = v[i];
-          }
-        }
-      } else if constexpr (MODE == 3) {
-        const int64_t row = row0 + t * 16 + col;
-        const bool row_ok = row < B;
-        const float lse2 = lse[t] * LOG2E_F;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const int cls0 = c0 + mt * 16 + q * 4;  // 4 consecutive classes -> one 8-byte store
-          float g[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float z = v[mt * 4 + r];
-            const bool hot = cls0 + r == yl[t];
-            float pr, l;
-            if constexpr (OVR) {
-              const float e = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E_F);  // exp(-|z|) in (0, 1]
-              pr = z >= 0.f ? __builtin_amdgcn_rcpf(1.f + e) : e * __builtin_amdgcn_rcpf(1.f + e);
-              // BCE: softplus(z) - z*[hot]; softplus(z) = max(z, 0) + log(1 + exp(-|z|))
-              l = fmaxf(z, 0.f) - (hot ? z : 0.f) + __builtin_amdgcn_logf(1.f + e) * LN2_F;
-              l = z == -INFINITY ? 0.f : l;
-            } else {
-              pr = __builtin_amdgcn_exp2f(fmaf(z, LOG2E_F, -lse2));
-              l = hot ? lse[t] - z : 0.f;
-            }
-            g[r] = row_ok && z != -INFINITY ? pr - (hot ? 1.f : 0.f) : 0.f;
-            loss_acc += row_ok ? l : 0.f;
-          }
-          if (row_ok && cls0 < c_end)
-            *reinterpret_cast<uint2*>(a.G + row * a.ldg + cls0) = make_uint2(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]));
-        }
-      } else {  // MODE 0 / 2: online (max, sum, first argmax)
-        float cm = v[0];
-        int ci = 0;
-#pragma unroll
-        for (int i = 1; i < 16; ++i) {
-          const bool gt = v[i] > cm;  // strict: the first (lowest class) maximum wins
-          cm = gt ? v[i] : cm;
-          ci = gt ? i : ci;
-        }
-        RowState& S = st[t];
-        const bool take = cm > S.m;
-        const float m_new = take ? cm : S.m;
-        if constexpr (OVR) {
-          float add = 0.f;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float e = __builtin_amdgcn_exp2f(-v[i] * LOG2E_F);  // -inf -> +inf -> sigmoid 0
-            add += __builtin_amdgcn_rcpf(1.f + e);
-          }
-          S.s += add;
-        } else {
-          const float m2 = m_new * LOG2E_F;
-          float add = 0.f;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) add += __builtin_amdgcn_exp2f(fmaf(v[i], LOG2E_F, -m2));
-          // rescale the running sum to the new max (S.m = -inf: nothing accumulated yet)
-          const float scale = S.m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(fmaf(S.m, LOG2E_F, -m2));
-          S.s = fmaf(S.s, scale, add);
-        }
-        S.bi = take ? c0 + (ci >> 2) * 16 + q * 4 + (ci & 3) : S.bi;
-        S.m = m_new;
-      }
-    }
-    MLAPI_WRITE_CHUNK(buf ^ 1)
-    __syncthreads();
+    MLAPI_DMA_CHUNK(min(c0 + CLASS_CHUNK, c_last), buf ^ 1)
+    compute_chunk<KS, NT, MODE, OVR>(smem + buf * BUF_BYTES, xf, c0, c_end, q, col, row0, B, K, bias, a, st, yl, lse,
+                                     loss_acc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA landed ...
+    __syncthreads();                                   // ... and every other wave's
     buf ^= 1;
   }
-
-#undef MLAPI_LOAD_CHUNK
-#undef MLAPI_WRITE_CHUNK
+#undef MLAPI_DMA_CHUNK
   if constexpr (MODE == 3) {
     // correct count: split 0, one lane (q == 0) per row
 #pragma unroll
@@ -421,11 +444,14 @@ struct Plan {
 // Benchmark hook (tools/gemm_plan_sweep.py): force (nt, splits); 0 = automatic.
 int g_force_nt = 0, g_force_splits = 0;
 
-Plan make_plan(int64_t B, int K) {
+Plan make_plan(int64_t B, int K, int F, bool training) {
   Plan p;
-  const int64_t rb2 = (B + 127) / 128;
-  p.nt = 1;  // measured (tools/gemm_plan_sweep.py): NT=2 hits 256 VGPRs -> 1 wave/SIMD and loses at every B
-  (void)rb2;
+  // 32 rows per wave (NT = 2) halve the LDS fragment reads per MFMA. It pays once the register
+  // staging is gone (LDS-DMA): B=262144 230 -> 172 us, B=8192 about even, B=1024 worse
+  // (tools/gemm_plan_sweep.py, profiles/r1_pmc/gemm_plan_sweep_dma.log). KS = 16 at NT = 2 needs
+  // all 256 VGPRs.
+  (void)training;
+  p.nt = (F <= 256 && B >= 16384) ? 2 : 1;
   if (g_force_nt == 1 || g_force_nt == 2) p.nt = g_force_nt;
   if (g_force_splits > 0) {
     const int rows_per_block = 64 * p.nt;
@@ -466,51 +492,33 @@ void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
       hipLaunchKernelGGL((gemm_softmax_kernel<KSV, NTV, MODE, false>), grid, dim3(256), 0, stream, args); \
   } while (0)
   const int ks = F / 32;
-  if constexpr (MODE <= 1) {  // predict / logits: F in {32, 64, 128, 256, 512}
-    if (F != 32 && F != 64 && F != 128 && F != 256 && F != 512)
-      throw std::invalid_argument("gemm_softmax: F must be 32, 64, 128, 256 or 512 (pad other widths)");
+  if (F != 32 && F != 64 && F != 128 && F != 256 && F != 512)
+    throw std::invalid_argument("gemm_softmax: F must be 32, 64, 128, 256 or 512 (pad other widths)");
 #define MLAPI_GEMM_NT(KSV)       \
   if (plan.nt == 2)              \
     MLAPI_GEMM_LAUNCH(KSV, 2);   \
   else                           \
     MLAPI_GEMM_LAUNCH(KSV, 1);
-    if (ks == 1) {
-      MLAPI_GEMM_NT(1)
-    } else if (ks == 2) {
-      MLAPI_GEMM_NT(2)
-    } else if (ks == 4) {
-      MLAPI_GEMM_NT(4)
-    } else if (ks == 8) {
-      MLAPI_GEMM_NT(8)
-    } else {
-      MLAPI_GEMM_NT(16)
-    }
-#undef MLAPI_GEMM_NT
-  } else {  // training: F_aug = softmax_train_faug(F) in {64, 128, 160, 288, 544}, NT = 1
-    if (ks == 2) {
-      MLAPI_GEMM_LAUNCH(2, 1);
-    } else if (ks == 4) {
-      MLAPI_GEMM_LAUNCH(4, 1);
-    } else if (ks == 5) {
-      MLAPI_GEMM_LAUNCH(5, 1);
-    } else if (ks == 9) {
-      if (plan.nt == 2)
-        MLAPI_GEMM_LAUNCH(9, 2);
-      else
-        MLAPI_GEMM_LAUNCH(9, 1);
-    } else if (ks == 17) {
-      MLAPI_GEMM_LAUNCH(17, 1);
-    } else {
-      throw std::invalid_argument("softmax_train: F_aug must be 64, 128, 160, 288 or 544");
-    }
+  if (ks == 1) {
+    MLAPI_GEMM_NT(1)
+  } else if (ks == 2) {
+    MLAPI_GEMM_NT(2)
+  } else if (ks == 4) {
+    MLAPI_GEMM_NT(4)
+  } else if (ks == 8) {
+    MLAPI_GEMM_NT(8)
+  } else {
+    MLAPI_GEMM_NT(16)
   }
+#undef MLAPI_GEMM_NT
 #undef MLAPI_GEMM_LAUNCH
   MLAPI_HIP_CHECK(hipGetLastError());
 }
 
-GemmArgs base_args(const void* X, const void* W, int64_t B, int K, int kind) {
+GemmArgs base_args(const void* X, const void* W, int64_t B, int F, int K, int kind) {
   GemmArgs a{};
   a.X = static_cast<const uint16_t*>(X);
+  a.ldx = F;
   a.W = static_cast<const uint16_t*>(W);
   a.B = B;
   a.K = K;
@@ -523,9 +531,9 @@ struct TrainLayout {
   size_t partials_off, rowstat_off, slabs_off, total;
 };
 
-TrainLayout train_layout(int64_t B, int K) {
+TrainLayout train_layout(int64_t B, int K, int F) {
   TrainLayout L;
-  L.plan = make_plan(B, K);  // nt = 1 unless forced (gemm_softmax_force_plan; NT = 2 only built for F_aug 288)
+  L.plan = make_plan(B, K, F, true);
   auto align = [](size_t v) { return (v + 255) & ~size_t(255); };
   L.partials_off = COUNTER_BYTES;
   L.rowstat_off = align(L.partials_off + (L.plan.splits > 1 ? (size_t)L.plan.splits * B * sizeof(float4) : 0));
@@ -541,30 +549,28 @@ void gemm_softmax_force_plan(int nt, int splits) {
   g_force_splits = splits;
 }
 
-int softmax_train_faug(int F) {
-  switch (F) {
-    case 32: return 64;
-    case 64: return 128;  // 96 would leave a 12-chunk LDS tail that cannot be swizzled in place
-    case 128: return 160;
-    case 256: return 288;
-    case 512: return 544;
-    default: return -1;
-  }
+int softmax_train_ldx(int F) {
+  return (F == 32 || F == 64 || F == 128 || F == 256 || F == 512) ? F + 8 : -1;
 }
 
-size_t softmax_train_workspace(int64_t B, int K) { return train_layout(B, K).total; }
+size_t softmax_train_workspace(int64_t B, int K, int F) { return train_layout(B, K, F).total; }
 
-void launch_softmax_train_grad(const void* X_aug, const void* W_aug, const int32_t* y, int64_t B, int F_aug, int K,
-                               int kind, void* G, int64_t ldg, float* stats_out, void* workspace, size_t ws_bytes,
-                               hipStream_t stream) {
+void launch_softmax_train_grad(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
+                               int64_t B, int F, int K, int kind, void* G, int64_t ldg, float* stats_out,
+                               void* workspace, size_t ws_bytes, hipStream_t stream) {
   if (B <= 0) return;
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("softmax_train: multiclass kinds only (binary models use train_binary)");
   if (ldg < K || ldg % 8 != 0) throw std::invalid_argument("softmax_train: ldg must be >= K and a multiple of 8");
-  const TrainLayout L = train_layout(B, K);
+  if (ldx < F || ldx % 8 != 0) throw std::invalid_argument("softmax_train: ldx must be >= F and a multiple of 8");
+  if (reinterpret_cast<uintptr_t>(X_aug) % 16 != 0 || reinterpret_cast<uintptr_t>(W) % 16 != 0)
+    throw std::invalid_argument("softmax_train: X_aug and W must be 16-byte aligned");
+  const TrainLayout L = train_layout(B, K, F);
   if (ws_bytes < L.total) throw std::invalid_argument("softmax_train: workspace too small (zero it once)");
   unsigned char* ws = static_cast<unsigned char*>(workspace);
-  GemmArgs args = base_args(X_aug, W_aug, B, K, kind);
+  GemmArgs args = base_args(X_aug, W, B, F, K, kind);
+  args.ldx = ldx;
+  args.bias = b;
   args.counters = reinterpret_cast<unsigned int*>(ws);
   args.partials = reinterpret_cast<float4*>(ws + L.partials_off);
   args.rowstat = reinterpret_cast<float2*>(ws + L.rowstat_off);
@@ -572,14 +578,14 @@ void launch_softmax_train_grad(const void* X_aug, const void* W_aug, const int32
   args.y = y;
   args.G = static_cast<uint16_t*>(G);
   args.ldg = ldg;
-  launch_mode<2>(args, F_aug, L.plan, stream);  // {lse, argmax} per row (split merge in-launch)
-  launch_mode<3>(args, F_aug, L.plan, stream);  // G = P - Y (bf16) + [loss, correct] slabs
+  launch_mode<2>(args, F, L.plan, stream);  // {lse, argmax} per row (split merge in-launch)
+  launch_mode<3>(args, F, L.plan, stream);  // G = P - Y (bf16) + [loss, correct] slabs
   launch_reduce_slabs_f32(args.stat_slabs, (int)(L.plan.row_blocks * L.plan.splits), 2, stats_out, stream);
 }
 
 size_t gemm_softmax_workspace(int64_t B, int K, int F) {
   (void)F;
-  const Plan p = make_plan(B, K);
+  const Plan p = make_plan(B, K, F, false);
   return p.splits > 1 ? (size_t)COUNTER_BYTES + (size_t)p.splits * (size_t)B * sizeof(float4) : 0;
 }
 
@@ -588,10 +594,10 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
   if (B <= 0) return;
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("gemm_softmax: multiclass kinds only (binary models use gemv_binary)");
-  const Plan plan = make_plan(B, K);
+  const Plan plan = make_plan(B, K, F, false);
   if (plan.splits > 1 && ws_bytes < gemm_softmax_workspace(B, K, F))
     throw std::invalid_argument("gemm_softmax: workspace too small (must be zero-initialised once)");
-  GemmArgs args = base_args(X, W, B, K, kind);
+  GemmArgs args = base_args(X, W, B, F, K, kind);
   args.bias = b;
   args.out_idx = out_idx;
   args.out_p = out_p;
@@ -605,9 +611,9 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
 void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B, int F, int K, float* Z,
                         hipStream_t stream) {
   if (B <= 0) return;
-  Plan plan = make_plan(B, K);
+  Plan plan = make_plan(B, K, F, false);
   plan.splits = (K + plan.classes_per_split - 1) / plan.classes_per_split;  // no merge needed for logits
-  GemmArgs args = base_args(X, W, B, K, KIND_MULTINOMIAL);
+  GemmArgs args = base_args(X, W, B, F, K, KIND_MULTINOMIAL);
   args.bias = b;
   args.Z = Z;
   launch_mode<1>(args, F, plan, stream);

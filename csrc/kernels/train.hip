@@ -470,14 +470,16 @@ __global__ __launch_bounds__(256) void sgd_update_kernel(float* __restrict__ p, 
 }
 
 // 2-D variant for W_aug = [W | b | 0 pad] (multiclass training): L2 only on the first pen_cols
-// columns; writes the bf16 copy the next forward pass reads (saves a separate cast launch).
+// columns; writes the bf16 W and the f32 bias the next forward reads (saves a cast launch).
 __global__ __launch_bounds__(256) void sgd_update_2d_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                             float* __restrict__ mom, int64_t n, int cols,
                                                             int pen_cols, float lr, float inv_n, float l2,
-                                                            float momentum, uint16_t* __restrict__ shadow) {
+                                                            float momentum, uint16_t* __restrict__ shadow_w,
+                                                            float* __restrict__ shadow_b) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int c = (int)(i % cols);
+  const int64_t row = i / cols;
+  const int c = (int)(i - row * cols);
   float d = g[i] * inv_n + (c < pen_cols ? l2 * p[i] : 0.f);
   if (mom != nullptr) {
     const float v = momentum * mom[i] + d;
@@ -486,7 +488,8 @@ __global__ __launch_bounds__(256) void sgd_update_2d_kernel(float* __restrict__ 
   }
   const float np = p[i] - lr * d;
   p[i] = np;
-  if (shadow != nullptr) shadow[i] = __builtin_bit_cast(uint16_t, (__bf16)np);
+  if (shadow_w != nullptr && c < pen_cols) shadow_w[row * pen_cols + c] = __builtin_bit_cast(uint16_t, (__bf16)np);
+  if (shadow_b != nullptr && c == pen_cols) shadow_b[row] = np;
 }
 
 }  // namespace
@@ -597,12 +600,12 @@ void launch_sgd_update(float* params, const float* grad, float* momentum_buf, in
 }
 
 void launch_sgd_update_2d(float* params, const float* grad, float* momentum_buf, int64_t rows, int cols,
-                          int pen_cols, float lr, float inv_n, float l2, float momentum, uint16_t* shadow_bf16,
-                          hipStream_t stream) {
+                          int pen_cols, float lr, float inv_n, float l2, float momentum, uint16_t* shadow_w,
+                          float* shadow_b, hipStream_t stream) {
   const int64_t n = rows * cols;
   if (n <= 0) return;
   hipLaunchKernelGGL(sgd_update_2d_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, params, grad,
-                     momentum_buf, n, cols, pen_cols, lr, inv_n, l2, momentum, shadow_bf16);
+                     momentum_buf, n, cols, pen_cols, lr, inv_n, l2, momentum, shadow_w, shadow_b);
   MLAPI_HIP_CHECK(hipGetLastError());
 }
 

@@ -178,11 +178,10 @@ def cast(src: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
 
 # ------------------------------------------------------------------- multiclass training (MFMA)
 def softmax_train_faug(F: int) -> int:
-    """Augmented width F_aug (ones / intercept column + MFMA padding) for an F-feature model."""
-    fa = {32: 64, 64: 128, 128: 160, 256: 288, 512: 544}.get(int(F), -1)
-    if fa < 0:
+    """Width F_aug = F + 8 of the augmented features [X | 1 | 0 x 7] (and of W_aug = [W | b | 0])."""
+    if int(F) not in (32, 64, 128, 256, 512):
         raise ValueError("softmax training kernels need F in {32, 64, 128, 256, 512} (pad the features)")
-    return fa
+    return int(F) + 8
 
 
 def augment_features(X: torch.Tensor, F_aug: int) -> torch.Tensor:
@@ -206,11 +205,12 @@ def augment_weights(W: torch.Tensor, b: torch.Tensor, F_aug: int) -> torch.Tenso
 class SoftmaxTrainBuffers:
     """Persistent per-batch-size buffers of the multiclass gradient (G, workspace, stats)."""
 
-    def __init__(self, B: int, K: int, device):
-        self.B, self.K = B, K
+    def __init__(self, B: int, K: int, F: int, device):
+        self.B, self.K, self.F = B, K, F
         self.ldg = (K + 7) // 8 * 8
-        self.G = torch.empty(B, self.ldg, dtype=torch.bfloat16, device=device)
-        self.ws = torch.zeros(C().softmax_train_workspace(B, K), dtype=torch.uint8, device=device)
+        # rows padded to whole 128-row blocks: the gradient kernel stores without a row guard
+        self.G = torch.empty((B + 127) // 128 * 128, self.ldg, dtype=torch.bfloat16, device=device)
+        self.ws = torch.zeros(C().softmax_train_workspace(B, K, F), dtype=torch.uint8, device=device)
         self.stats = torch.zeros(2, dtype=torch.float32, device=device)
         # dW split over the batch: hipBLASLt tiles only the small [K, F_aug] output, so one mm runs
         # ~48 workgroups for K=1000 (245 us at B=65536); S batched slices of ~2048 rows + a sum
@@ -222,46 +222,52 @@ class SoftmaxTrainBuffers:
         self.part = None
 
 
-def softmax_train_grad(X_aug: torch.Tensor, W_aug_bf16: torch.Tensor, y: torch.Tensor, kind: int,
+def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y: torch.Tensor, kind: int,
                        bufs: SoftmaxTrainBuffers = None, dW_out: torch.Tensor = None,
                        stats_out: torch.Tensor = None):
-    """Sums over the batch of the multiclass objective's gradient, intercept folded in.
+    """Sums over the batch of the multiclass objective's gradient, intercept included.
 
-    Returns (dW_aug f32 [K, F_aug], stats f32 [loss_sum, n_correct]). Two MFMA launches produce
-    G = P - Y in bf16 (plus loss/correct); dW_aug = G^T X_aug is one hipBLASLt GEMM with f32 output.
+    X_aug: [B, F + 8] bf16 from :func:`augment_features`; W: [K, F] bf16; b: [K] f32; y: int32.
+    Returns (dW_aug f32 [K, F + 8] with the intercept gradient in column F, stats f32
+    [loss_sum, n_correct]). Two MFMA launches produce G = P - Y in bf16 (plus loss/correct);
+    dW_aug = G^T X_aug is one hipBLASLt GEMM (batched over B slices) with f32 output.
     """
-    _check(X_aug, W_aug_bf16, y)
-    if X_aug.dtype != torch.bfloat16 or W_aug_bf16.dtype != torch.bfloat16 or y.dtype != torch.int32:
-        raise TypeError("softmax_train_grad: X_aug, W_aug bf16 and y int32")
+    _check(X_aug, W, b, y)
+    if X_aug.dtype != torch.bfloat16 or W.dtype != torch.bfloat16 or b.dtype != torch.float32 \
+            or y.dtype != torch.int32:
+        raise TypeError("softmax_train_grad: X_aug, W bf16, b f32 and y int32")
     B, F_aug = X_aug.shape
-    K = W_aug_bf16.shape[0]
-    if W_aug_bf16.shape[1] != F_aug or y.numel() != B:
+    K, F = W.shape
+    if F_aug != softmax_train_faug(F) or b.numel() != K or y.numel() != B:
         raise ValueError("softmax_train_grad: shape mismatch")
-    if bufs is None or bufs.B != B or bufs.K != K:
-        bufs = SoftmaxTrainBuffers(B, K, X_aug.device)
+    if bufs is None or bufs.B != B or bufs.K != K or bufs.F != F:
+        bufs = SoftmaxTrainBuffers(B, K, F, X_aug.device)
     stats = bufs.stats if stats_out is None else stats_out
-    C().softmax_train_grad(X_aug.data_ptr(), W_aug_bf16.data_ptr(), y.data_ptr(), B, F_aug, K, int(kind),
+    C().softmax_train_grad(X_aug.data_ptr(), F_aug, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
                            bufs.G.data_ptr(), bufs.ldg, stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(),
                            _stream())
     if dW_out is None:
         dW_out = torch.empty(K, F_aug, dtype=torch.float32, device=X_aug.device)
     S = bufs.splits
     if S == 1:
-        torch.mm(bufs.G[:, :K].t(), X_aug, out_dtype=torch.float32, out=dW_out)
+        torch.mm(bufs.G[:B, :K].t(), X_aug, out_dtype=torch.float32, out=dW_out)
     else:
         if bufs.part is None:
             bufs.part = torch.empty(S, K, F_aug, dtype=torch.float32, device=X_aug.device)
-        Gs = bufs.G.view(S, B // S, bufs.ldg)[:, :, :K]
+        Gs = bufs.G[:B].view(S, B // S, bufs.ldg)[:, :, :K]
         torch.bmm(Gs.transpose(1, 2), X_aug.view(S, B // S, F_aug), out_dtype=torch.float32, out=bufs.part)
         torch.sum(bufs.part, dim=0, out=dW_out)
     return dW_out, stats
 
 
 def sgd_update_2d(params: torch.Tensor, grad: torch.Tensor, pen_cols: int, lr: float, inv_n: float, l2: float,
-                  momentum: float = 0.0, mom_buf: torch.Tensor = None, shadow: torch.Tensor = None) -> None:
-    """params [rows, cols] f32 -= lr * (grad / N + l2 * params[:, :pen_cols]); refreshes a bf16 shadow."""
+                  momentum: float = 0.0, mom_buf: torch.Tensor = None, shadow_w: torch.Tensor = None,
+                  shadow_b: torch.Tensor = None) -> None:
+    """params [rows, cols] f32 -= lr * (grad / N + l2 * params[:, :pen_cols]); refreshes the bf16
+    weight copy shadow_w [rows, pen_cols] and the f32 bias copy shadow_b (column pen_cols)."""
     _check(params, grad)
     rows, cols = params.shape
     C().sgd_update_2d(params.data_ptr(), grad.data_ptr(), 0 if mom_buf is None else mom_buf.data_ptr(), rows, cols,
                       int(pen_cols), float(lr), float(inv_n), float(l2), float(momentum),
-                      0 if shadow is None else shadow.data_ptr(), _stream())
+                      0 if shadow_w is None else shadow_w.data_ptr(), 0 if shadow_b is None else shadow_b.data_ptr(),
+                      _stream())

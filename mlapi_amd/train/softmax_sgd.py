@@ -5,11 +5,11 @@ The reference fits its 3-class Iris model once with sklearn's full-batch L-BFGS
 This module is the scale-out counterpart (BASELINE config 5 with K classes): per step and rank
 
   1. ``softmax_train_grad``: two MFMA launches over the rank's shard -> G = P - Y (bf16) with the
-     loss / correct sums, then dW_aug = G^T X_aug as one hipBLASLt GEMM (f32 out). The intercept
-     rides inside the GEMMs (X_aug = [X | 1], W_aug = [W | b]), so there is no separate bias pass;
+     loss / correct sums, then dW_aug = G^T X_aug as one hipBLASLt GEMM (f32 out). X_aug carries a
+     ones column (X_aug = [X | 1 | 0 x 7]), so that GEMM also yields the intercept gradient;
   2. one RCCL all-reduce of the fused buffer [dW_aug | loss_sum | n_correct] (C2 + C3);
-  3. ``sgd_update_2d``: W_aug -= lr * (g / N_global + l2 * W) with the intercept column
-     unpenalized, writing the bf16 copy the next forward reads in the same pass.
+  3. ``sgd_update_2d``: W_aug = [W | b] -= lr * (g / N_global + l2 * W) with the intercept
+     unpenalized, writing the bf16 W and f32 b the next forward reads in the same pass.
 
 fp32 master weights; every rank applies the identical update, so replicas stay bitwise equal.
 One replica (world == 1) can capture the whole step in a HIP graph (:meth:`capture`).
@@ -60,7 +60,9 @@ class SoftmaxSGDTrainer:
         self.on_gpu = torch.device(self.device).type == "cuda"
         self.lr, self.l2, self.momentum = lr, l2, momentum
         self.params = torch.zeros(self.K, self.F_aug, dtype=torch.float32, device=self.device)
-        self.shadow = torch.zeros(self.K, self.F_aug, dtype=torch.bfloat16, device=self.device) if self.on_gpu else None
+        # what the MFMA forward reads: bf16 W [K, F] and f32 intercepts (refreshed by every update)
+        self.shadow_w = torch.zeros(self.K, self.F, dtype=torch.bfloat16, device=self.device) if self.on_gpu else None
+        self.shadow_b = torch.zeros(self.K, dtype=torch.float32, device=self.device) if self.on_gpu else None
         n = self.K * self.F_aug
         self.grad = torch.zeros(n + 2, dtype=torch.float32, device=self.device)  # [dW_aug | loss | correct]
         self.mom = torch.zeros_like(self.params) if momentum else None
@@ -92,8 +94,12 @@ class SoftmaxSGDTrainer:
         self.params.zero_()
         self.params[:, : self.F] = W.to(self.params)
         self.params[:, self.F] = b.reshape(-1).to(self.params)
-        if self.shadow is not None:
-            self.shadow.copy_(self.params)
+        self._refresh_shadow()
+
+    def _refresh_shadow(self) -> None:
+        if self.shadow_w is not None:
+            self.shadow_w.copy_(self.params[:, : self.F])
+            self.shadow_b.copy_(self.params[:, self.F])
 
     # ---------------------------------------------------------------------------------- step
     def _local_grad(self, Xa: torch.Tensor, y: torch.Tensor) -> None:
@@ -102,8 +108,8 @@ class SoftmaxSGDTrainer:
 
             B = Xa.shape[0]
             if B not in self._bufs:
-                self._bufs[B] = SoftmaxTrainBuffers(B, self.K, Xa.device)
-            softmax_train_grad(Xa, self.shadow, y, self.kind, bufs=self._bufs[B], dW_out=self._dW(),
+                self._bufs[B] = SoftmaxTrainBuffers(B, self.K, self.F, Xa.device)
+            softmax_train_grad(Xa, self.shadow_w, self.shadow_b, y, self.kind, bufs=self._bufs[B], dW_out=self._dW(),
                                stats_out=self.grad[self.K * self.F_aug:])
         else:
             from mlapi_amd.ops.reference import softmax_train_ref
@@ -118,7 +124,7 @@ class SoftmaxSGDTrainer:
             from mlapi_amd.ops.linear import sgd_update_2d
 
             sgd_update_2d(self.params, self.grad, self.F, self.lr, 1.0 / n_global, self.l2, self.momentum, self.mom,
-                          self.shadow)
+                          self.shadow_w, self.shadow_b)
         else:
             d = self._dW() / n_global
             d[:, : self.F] += self.l2 * self.params[:, : self.F]
@@ -147,7 +153,7 @@ class SoftmaxSGDTrainer:
             raise RuntimeError("graph capture: single-GPU replica only")
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        saved = (self.params.clone(), self.shadow.clone(), None if self.mom is None else self.mom.clone())
+        saved = (self.params.clone(), None if self.mom is None else self.mom.clone())
         with torch.cuda.stream(s):  # warm-up: allocates the buffers and hipBLASLt's workspace
             for _ in range(2):
                 self._local_grad(Xa, y)
@@ -158,9 +164,9 @@ class SoftmaxSGDTrainer:
             self._local_grad(Xa, y)
             self._update(Xa.shape[0])
         self.params.copy_(saved[0])
-        self.shadow.copy_(saved[1])
+        self._refresh_shadow()
         if self.mom is not None:
-            self.mom.copy_(saved[2])
+            self.mom.copy_(saved[1])
         self._graph = (g, Xa, y)
 
     # ---------------------------------------------------------------------------------- stats
@@ -183,8 +189,7 @@ class SoftmaxSGDTrainer:
 
     def load_state_dict(self, sd: dict) -> None:
         self.params.copy_(sd["params"].to(self.device))
-        if self.shadow is not None:
-            self.shadow.copy_(self.params)
+        self._refresh_shadow()
         if self.mom is not None and sd.get("mom") is not None:
             self.mom.copy_(sd["mom"].to(self.device))
         self.steps = int(sd["steps"])

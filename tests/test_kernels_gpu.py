@@ -226,13 +226,13 @@ def test_softmax_train_grad(B, F, K, kind):
     W, b = _rand((K, F), torch.float32, 12, scale=1 / np.sqrt(F)), _rand((K,), torch.float32, 13)
     y = torch.randint(0, K, (B,), generator=torch.Generator().manual_seed(14), dtype=torch.int32).to(DEV)
     Xa = ops.augment_features(X, Fa)
-    Wa = ops.augment_weights(W, b, Fa).to(torch.bfloat16)
-    bufs = ops.SoftmaxTrainBuffers(B, K, X.device)
+    Wb = W.to(torch.bfloat16)
+    bufs = ops.SoftmaxTrainBuffers(B, K, F, X.device)
     for _ in range(2):  # second call checks the split-merge counters re-armed
-        dW, stats = ops.softmax_train_grad(Xa, Wa, y, kind, bufs=bufs)
+        dW, stats = ops.softmax_train_grad(Xa, Wb, b, y, kind, bufs=bufs)
     torch.cuda.synchronize()
-    G_ref, dW_ref, loss_ref, corr_ref = ref.softmax_train_ref(Xa, y, Wa, kind)
-    G = bufs.G[:, :K].float()
+    G_ref, dW_ref, loss_ref, corr_ref = ref.softmax_train_ref(Xa, y, ops.augment_weights(Wb.float(), b, Fa), kind)
+    G = bufs.G[:B, :K].float()
     torch.testing.assert_close(G, G_ref, atol=8e-3, rtol=1e-2)  # bf16 storage of G
     scale = dW_ref.abs().max().item() + 1e-6
     assert (dW - dW_ref).abs().max().item() < 1e-2 * scale + 1e-2 * np.sqrt(B / 1000)
@@ -243,18 +243,20 @@ def test_softmax_train_grad(B, F, K, kind):
 
 
 def test_sgd_update_2d():
-    K, Fa, F = 9, 64, 32
+    K, Fa, F = 9, 40, 32
     p = _rand((K, Fa), torch.float32, 20)
     g = _rand((K * Fa + 2,), torch.float32, 21)
     mom = torch.zeros(K, Fa, device=DEV)
-    shadow = torch.empty(K, Fa, dtype=torch.bfloat16, device=DEV)
+    shadow_w = torch.empty(K, F, dtype=torch.bfloat16, device=DEV)
+    shadow_b = torch.empty(K, dtype=torch.float32, device=DEV)
     p0 = p.clone()
-    ops.sgd_update_2d(p, g, F, 0.1, 0.5, 0.01, 0.9, mom, shadow)
+    ops.sgd_update_2d(p, g, F, 0.1, 0.5, 0.01, 0.9, mom, shadow_w, shadow_b)
     d = g[: K * Fa].view(K, Fa) * 0.5
     d[:, :F] += 0.01 * p0[:, :F]
     torch.testing.assert_close(p, p0 - 0.1 * d)
     torch.testing.assert_close(mom, d)
-    assert torch.equal(shadow, p.to(torch.bfloat16))
+    assert torch.equal(shadow_w, p[:, :F].to(torch.bfloat16))
+    assert torch.equal(shadow_b, p[:, F])
 
 
 def test_softmax_sgd_gpu_trains_and_graph_replay_is_exact():

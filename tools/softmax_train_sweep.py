@@ -26,24 +26,25 @@ dev = torch.device("cuda", 0)
 B, F, K = 65536, 256, 1000
 Fa = ops.softmax_train_faug(F)
 X = ops.augment_features(torch.randn(B, F, device=dev), Fa)
-W = (torch.randn(K, Fa, device=dev) / 16).to(torch.bfloat16)
+W = (torch.randn(K, F, device=dev) / 16).to(torch.bfloat16)
+bias = torch.zeros(K, device=dev)
 y = torch.randint(0, K, (B,), device=dev, dtype=torch.int32)
 res = {}
 for nt in (1, 2):
     C().gemm_softmax_force_plan(nt, 0)
-    bufs = ops.SoftmaxTrainBuffers(B, K, dev)
+    bufs = ops.SoftmaxTrainBuffers(B, K, F, dev)
     st = torch.zeros(2, device=dev)
-    t = timeit(lambda: C().softmax_train_grad(X.data_ptr(), W.data_ptr(), y.data_ptr(), B, Fa, K, 2, bufs.G.data_ptr(),
-                                              bufs.ldg, st.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(),
-                                              torch.cuda.current_stream().cuda_stream))
+    t = timeit(lambda: C().softmax_train_grad(X.data_ptr(), Fa, W.data_ptr(), bias.data_ptr(), y.data_ptr(), B, F, K, 2,
+                                              bufs.G.data_ptr(), bufs.ldg, st.data_ptr(), bufs.ws.data_ptr(),
+                                              bufs.ws.numel(), torch.cuda.current_stream().cuda_stream))
     res[f"grad_launches_nt{nt}_us"] = t
 C().gemm_softmax_force_plan(0, 0)
-G = bufs.G[:, :K]
+G = bufs.G[:B, :K]
 out = torch.empty(K, Fa, device=dev)
 res["dW_mm_us"] = timeit(lambda: torch.mm(G.t(), X, out_dtype=torch.float32, out=out))
 ref = out.clone()
 for S in (2, 4, 8, 16, 32, 64):
-    Gs = bufs.G.view(S, B // S, bufs.ldg)[:, :, :K]
+    Gs = bufs.G[:B].view(S, B // S, bufs.ldg)[:, :, :K]
     Xs = X.view(S, B // S, Fa)
     part = torch.empty(S, K, Fa, device=dev)
 
