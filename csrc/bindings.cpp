@@ -93,6 +93,7 @@ py::dict stats_dict(const EngineStats& s) {
   d["queue_depth"] = s.queue_depth;
   d["model_version"] = s.model_version;
   d["healthy"] = s.healthy;
+  d["kernel_launches"] = s.kernel_launches;
   return d;
 }
 
@@ -245,7 +246,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("watchdog_ms", &EngineConfig::watchdog_ms)
       .def_readwrite("fail_every", &EngineConfig::fail_every)
       .def_readwrite("delay_us", &EngineConfig::delay_us)
-      .def_readwrite("spin_us", &EngineConfig::spin_us);
+      .def_readwrite("spin_us", &EngineConfig::spin_us)
+      .def_readwrite("persistent", &EngineConfig::persistent)
+      .def_readwrite("persistent_idle_ms", &EngineConfig::persistent_idle_ms);
 
   py::class_<PySink>(m, "PySink").def(py::init<>()).def("fd", &PySink::fd).def("drain", &PySink::drain);
 

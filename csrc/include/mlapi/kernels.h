@@ -14,6 +14,21 @@ namespace mlapi {
 void launch_linear_small(int dt, const void* X, int64_t ldx, const void* W, const void* b, int64_t B, int F,
                          int K, int kind, int32_t* out_idx, void* out_p, hipStream_t stream);
 
+// Persistent serving kernel (linear_small.hip): one resident workgroup consumes batches from a
+// host-pinned mailbox (see csrc/runtime/engine.cpp). All pointers are device-visible addresses.
+struct alignas(64) ServeMailSlot {
+  uint32_t seq;    // host -> device: batch index + 1, published last (release)
+  uint32_t n;      // rows in the batch
+  int32_t F, K, kind, pad;
+  uint64_t x;      // const T* rows [n, F]
+  uint64_t W, b;   // model (device memory, dtype of the engine)
+  uint64_t idx;    // int32_t* out
+  uint64_t p;      // T* out
+};
+constexpr int SERVE_DONE_STRIDE = 16;  // done words are 64 bytes apart (one cache line per slot)
+void launch_serve_persistent(int dt, ServeMailSlot* mail, uint32_t* done, const uint32_t* stop, int nslots,
+                             uint64_t start_seq, uint64_t idle_ticks, hipStream_t stream);
+
 // ---- gemv_binary.hip: binary LR predict, HBM-streaming GEMV + sigmoid epilogue ----------------
 // X: [B, F] bf16 or f32 row-major; w: [F] same dtype; bias: scalar f32.
 // out_idx: int32[B] (z > 0), out_p: f32[B] = sigmoid(|z|) (kind BINARY) or sigmoid(2|z|).

@@ -93,13 +93,31 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     MLAPI_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
     slots_.resize(cfg_.slots);
     const size_t xb = (size_t)cfg_.max_batch * cfg_.max_features * sizeof(double);
+    // fine-grained (coherent) host memory: the persistent kernel polls and writes it while the
+    // host does the same, with system-scope acquire/release on the sequence words
+    const unsigned hf = hipHostMallocMapped | (cfg_.persistent ? hipHostMallocCoherent : 0u);
+    if (cfg_.persistent) {
+      MLAPI_HIP_CHECK(hipHostMalloc((void**)&mail_h_, sizeof(ServeMailSlot) * cfg_.slots, hf));
+      std::memset(mail_h_, 0, sizeof(ServeMailSlot) * cfg_.slots);
+      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&mail_d_, mail_h_, 0));
+      const size_t done_bytes = sizeof(uint32_t) * SERVE_DONE_STRIDE * (cfg_.slots + 1);
+      MLAPI_HIP_CHECK(hipHostMalloc((void**)&done_h_, done_bytes, hf));
+      std::memset(done_h_, 0, done_bytes);
+      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&done_d_, done_h_, 0));
+      stop_h_ = done_h_ + SERVE_DONE_STRIDE * cfg_.slots;  // own 64-byte line after the done words
+      stop_d_ = done_d_ + SERVE_DONE_STRIDE * cfg_.slots;
+      MLAPI_HIP_CHECK(hipStreamCreateWithPriority(&pstream_, hipStreamNonBlocking, hi));
+      int rate_khz = 0;
+      MLAPI_HIP_CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, cfg_.device));
+      idle_ticks_ = (uint64_t)(rate_khz > 0 ? rate_khz : 100000) * (uint64_t)std::max(1, cfg_.persistent_idle_ms);
+    }
     for (int i = 0; i < cfg_.slots; ++i) {
       Slot& s = slots_[i];
-      MLAPI_HIP_CHECK(hipHostMalloc(&s.hx, xb, hipHostMallocMapped));
+      MLAPI_HIP_CHECK(hipHostMalloc(&s.hx, xb, hf));
       MLAPI_HIP_CHECK(hipHostGetDevicePointer(&s.dx, s.hx, 0));
-      MLAPI_HIP_CHECK(hipHostMalloc((void**)&s.hidx, (size_t)cfg_.max_batch * sizeof(int32_t), hipHostMallocMapped));
+      MLAPI_HIP_CHECK(hipHostMalloc((void**)&s.hidx, (size_t)cfg_.max_batch * sizeof(int32_t), hf));
       MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.didx, s.hidx, 0));
-      MLAPI_HIP_CHECK(hipHostMalloc(&s.hp, (size_t)cfg_.max_batch * sizeof(double), hipHostMallocMapped));
+      MLAPI_HIP_CHECK(hipHostMalloc(&s.hp, (size_t)cfg_.max_batch * sizeof(double), hf));
       MLAPI_HIP_CHECK(hipHostGetDevicePointer(&s.dp, s.hp, 0));
       MLAPI_HIP_CHECK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
       s.metas.reserve(cfg_.max_batch);
@@ -114,6 +132,13 @@ Engine::~Engine() {
   stop();
   if (cfg_.device >= 0) {
     (void)hipSetDevice(cfg_.device);
+    if (pstream_ != nullptr) {  // the resident kernel leaves on the stop word (or its idle timeout)
+      __atomic_store_n(stop_h_, 1u, __ATOMIC_RELEASE);
+      (void)hipStreamSynchronize(pstream_);
+      (void)hipStreamDestroy(pstream_);
+      (void)hipHostFree(mail_h_);
+      (void)hipHostFree(done_h_);
+    }
     for (Slot& s : slots_) {
       if (s.ev) (void)hipEventDestroy(s.ev);
       if (s.hx) (void)hipHostFree(s.hx);
@@ -399,7 +424,26 @@ void Engine::batcher_loop() {
           for (int f = 0; f < F; ++f) hx[i * F + f] = ok ? (float)xs[s.metas[i].off + f] : 0.f;
         }
       }
-      if (cfg_.fail_every > 0 && (++batch_counter_ % (uint64_t)cfg_.fail_every) == 0) {
+      if (cfg_.persistent) {
+        // Mailbox post: rows are in the slot already; publish the header, then the sequence word
+        // (release) that the resident kernel polls. An injected fault still posts an empty batch
+        // so the kernel's strict sequence order is kept.
+        s.batch = next_batch_++;
+        const bool inject = cfg_.fail_every > 0 && (++batch_counter_ % (uint64_t)cfg_.fail_every) == 0;
+        ServeMailSlot& mb = mail_h_[si];
+        mb.n = inject ? 0u : (uint32_t)n;
+        mb.F = F;
+        mb.K = m->K;
+        mb.kind = m->kind;
+        mb.x = (uint64_t)(uintptr_t)s.dx;
+        mb.W = (uint64_t)(uintptr_t)m->dW;
+        mb.b = (uint64_t)(uintptr_t)m->db;
+        mb.idx = (uint64_t)(uintptr_t)s.didx;
+        mb.p = (uint64_t)(uintptr_t)s.dp;
+        __atomic_store_n(&mb.seq, (uint32_t)(s.batch + 1), __ATOMIC_RELEASE);
+        s.failed = inject;
+        s.launched = !inject;
+      } else if (cfg_.fail_every > 0 && (++batch_counter_ % (uint64_t)cfg_.fail_every) == 0) {
         s.failed = true;
       } else {
         try {
@@ -429,6 +473,56 @@ void Engine::batcher_loop() {
   s_cv_.notify_all();
 }
 
+// Persistent mode: wait for the slot's `done` word. The completer owns the resident kernel's
+// lifecycle: it launches one when none is running (first batch, or after the kernel idled out),
+// starting at the oldest outstanding batch, and notices an exited kernel through its stream.
+bool Engine::wait_persistent(Slot& s, int si) {
+  const uint32_t want = (uint32_t)(s.batch + 1);
+  volatile uint32_t* dw = done_h_ + SERVE_DONE_STRIDE * si;
+  const int64_t t0 = now_ns();
+  // after a pause longer than the kernel's idle timeout it has most likely left already
+  if (kernel_running_ && t0 - last_done_ns_ > ((int64_t)cfg_.persistent_idle_ms - 1) * 1000000 &&
+      hipStreamQuery(pstream_) == hipSuccess)
+    kernel_running_ = false;
+  int spins = 0;
+  while (__atomic_load_n(dw, __ATOMIC_ACQUIRE) != want) {
+    if (!kernel_running_) {
+      try {
+        launch_serve_persistent(cfg_.dtype, mail_d_, done_d_, stop_d_, cfg_.slots, s.batch, idle_ticks_, pstream_);
+      } catch (const std::exception&) {
+        return false;
+      }
+      kernel_running_ = true;
+      std::lock_guard<std::mutex> lk(st_mu_);
+      ++stats_.kernel_launches;
+    }
+    ++spins;
+    if (spins < 20000) {
+      _mm_pause();
+    } else {
+      std::this_thread::sleep_for(std::chrono::microseconds(2));
+    }
+    if ((spins & 255) == 0) {
+      // the kernel may have idled out just before this batch was posted: relaunch at this batch
+      const hipError_t q = hipStreamQuery(pstream_);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(dw, __ATOMIC_ACQUIRE) == want) break;
+        kernel_running_ = false;
+      } else if (q != hipErrorNotReady) {
+        return false;
+      }
+      if (cfg_.watchdog_ms > 0) {
+        const int64_t waited = now_ns() - t0;
+        if (waited > (int64_t)cfg_.watchdog_ms * 1000000) healthy_.store(false);
+        // never block the completer forever: fail the batch (ST_DEVICE_ERROR) after 10x the watchdog
+        if (waited > (int64_t)cfg_.watchdog_ms * 10000000) return false;
+      }
+    }
+  }
+  last_done_ns_ = now_ns();
+  return true;
+}
+
 void Engine::completer_loop() {
   pthread_setname_np(pthread_self(), "mlapi-compl");
   (void)hipSetDevice(cfg_.device);
@@ -444,7 +538,12 @@ void Engine::completer_loop() {
       inflight_.pop_front();
     }
     Slot& s = slots_[si];
-    if (s.launched) {
+    if (cfg_.persistent) {
+      if (!wait_persistent(s, si)) {
+        s.failed = true;
+        healthy_.store(false);
+      }
+    } else if (s.launched) {
       // Poll the event: spin briefly (sub-10us kernels), then back off.
       const int64_t t0 = now_ns();
       int spins = 0;

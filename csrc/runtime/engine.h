@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "mlapi/common.h"
+#include "mlapi/kernels.h"
 
 namespace mlapi {
 
@@ -82,10 +83,14 @@ struct EngineConfig {
   int delay_us = 0;       // fault injection: extra per-batch delay
   int spin_us = 0;        // batcher polls the queue this long before sleeping on the condvar
                           // (saves the futex wake-up on the request path under load)
+  bool persistent = false;  // GPU: one resident kernel fed through a host mailbox instead of a
+                            // launch per batch (serve_persistent_kernel, linear_small.hip)
+  int persistent_idle_ms = 5;  // the resident kernel exits after this long without work
 };
 
 struct EngineStats {
   uint64_t requests = 0, batches = 0, errors = 0;
+  uint64_t kernel_launches = 0;     // persistent mode: (re)launches of the resident kernel
   uint64_t batch_hist[12] = {0};    // batch size buckets: 1,2,4,...,2048+
   uint64_t latency_hist[24] = {0};  // latency buckets in powers of two of 1us: <1us .. >=2^23us
   double latency_sum_us = 0;
@@ -140,6 +145,7 @@ class Engine {
     std::vector<int32_t> pre_status;  // per-row status decided before launch
     std::shared_ptr<const Model> model;
     int64_t t_launch = 0;
+    uint64_t batch = 0;  // persistent mode: global batch index (mailbox sequence - 1)
     int n = 0;
     bool launched = false;
     bool failed = false;
@@ -147,6 +153,7 @@ class Engine {
 
   void batcher_loop();
   void completer_loop();
+  bool wait_persistent(Slot& s, int si);
   void run_cpu(std::vector<Meta>& metas, const std::vector<double>& xs, const std::shared_ptr<const Model>& m);
   void finish(Slot& s, const int32_t* idx, const double* p, const int32_t* status);
   void deliver(std::vector<Meta>& metas, const int32_t* idx, const double* p, const int32_t* st,
@@ -175,6 +182,20 @@ class Engine {
   std::deque<int> free_slots_;
   std::deque<int> inflight_;
   bool batcher_done_ = false;
+
+  // persistent mode: host-pinned mailbox (device-visible), its stop word, the resident kernel's
+  // stream; kernel_running_ / relaunch bookkeeping are owned by the completer thread
+  ServeMailSlot* mail_h_ = nullptr;
+  ServeMailSlot* mail_d_ = nullptr;
+  uint32_t* done_h_ = nullptr;  // one word per slot, 64 B apart
+  uint32_t* done_d_ = nullptr;
+  uint32_t* stop_h_ = nullptr;
+  uint32_t* stop_d_ = nullptr;
+  hipStream_t pstream_ = nullptr;
+  bool kernel_running_ = false;
+  uint64_t idle_ticks_ = 0;
+  uint64_t next_batch_ = 0;     // batcher thread only
+  int64_t last_done_ns_ = 0;   // completer thread only
 
   std::thread batcher_, completer_;
   std::atomic<bool> healthy_{true};

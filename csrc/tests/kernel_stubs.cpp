@@ -9,4 +9,7 @@ void launch_linear_small(int, const void*, int64_t, const void*, const void*, in
                          hipStream_t) {
   throw std::logic_error("host-only test binary: launch_linear_small must not be reached");
 }
+void launch_serve_persistent(int, ServeMailSlot*, uint32_t*, const uint32_t*, int, uint64_t, uint64_t, hipStream_t) {
+  throw std::logic_error("host-only test binary: launch_serve_persistent must not be reached");
+}
 }  // namespace mlapi

@@ -53,6 +53,8 @@ class EngineHandle:
         ec.fail_every = config.fail_every
         ec.delay_us = config.delay_us
         ec.spin_us = config.spin_us
+        ec.persistent = bool(config.persistent)
+        ec.persistent_idle_ms = config.persistent_idle_ms
         self.engine = c.Engine(ec)
         self._models: Dict[int, LinearModel] = {}
         self._lock = threading.Lock()

@@ -38,6 +38,8 @@ class Config:
     fail_every: int = 0                       # fault injection (tests): fail every N-th batch
     delay_us: int = 0                         # fault injection: delay every batch
     spin_us: int = 0                          # batcher spin before sleeping (0 = always sleep)
+    persistent: bool = False                  # GPU: resident serving kernel fed by a host mailbox
+    persistent_idle_ms: int = 5               # ... which exits after this long without work
     # HTTP
     host: str = "127.0.0.1"
     port: int = 8000
