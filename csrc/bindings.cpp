@@ -94,6 +94,7 @@ py::dict stats_dict(const EngineStats& s) {
   d["model_version"] = s.model_version;
   d["healthy"] = s.healthy;
   d["kernel_launches"] = s.kernel_launches;
+  d["rejected"] = s.rejected;
   return d;
 }
 
@@ -248,6 +249,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("delay_us", &EngineConfig::delay_us)
       .def_readwrite("spin_us", &EngineConfig::spin_us)
       .def_readwrite("persistent", &EngineConfig::persistent)
+      .def_readwrite("max_queue", &EngineConfig::max_queue)
       .def_readwrite("persistent_idle_ms", &EngineConfig::persistent_idle_ms);
 
   py::class_<PySink>(m, "PySink").def(py::init<>()).def("fd", &PySink::fd).def("drain", &PySink::drain);
@@ -281,7 +283,9 @@ PYBIND11_MODULE(_C, m) {
       .def(
           "submit",
           [](Engine& e, py::array_t<double, py::array::c_style | py::array::forcecast> x, uint64_t tag, PySink& sink) {
-            return e.submit(x.data(), (int)x.size(), tag, &sink);
+            // 1 accepted, 0 engine stopping / malformed, -1 (Engine::SUBMIT_BUSY) queue full
+            const uint64_t t = tag;
+            return e.submit_many(x.data(), 1, (int)x.size(), &t, &sink);
           },
           py::arg("x"), py::arg("tag"), py::arg("sink"))
       .def(

@@ -372,12 +372,16 @@ class IoThread : public Sink {
   void flush_submits() {
     if (pend_tags_.empty()) return;
     const int n = (int)pend_tags_.size();
-    if (srv_->engine()->submit_many(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), this) != n) {
-      for (uint64_t id : pend_tags_) {  // engine stopping: answer 500 now
+    const int r = srv_->engine()->submit_many(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), this);
+    if (r != n) {
+      for (uint64_t id : pend_tags_) {  // overloaded: 503 + Retry-After; engine stopping: 500
         auto it = conns_.find(id);
         if (it == conns_.end()) continue;
         it->second->waiting = false;
-        internal_error(it->second.get());
+        if (r == Engine::SUBMIT_BUSY)
+          service_unavailable(it->second.get());
+        else
+          internal_error(it->second.get());
         flush(it->second.get());
       }
     }
@@ -509,7 +513,8 @@ class IoThread : public Sink {
     return true;
   }
 
-  void append_response(Conn* c, int status, const char* reason, const char* ctype, const std::string& body) {
+  void append_response(Conn* c, int status, const char* reason, const char* ctype, const std::string& body,
+                       const char* extra_headers = "") {
     std::string& o = c->out;
     o.reserve(o.size() + 160 + body.size());
     o += "HTTP/1.1 ";
@@ -525,13 +530,22 @@ class IoThread : public Sink {
     o += "\r\ncontent-type: ";
     o += ctype;
     if (c->close_after) o += "\r\nconnection: close";
-    o += "\r\n\r\n";
+    o += "\r\n";
+    o += extra_headers;  // each "name: value\r\n"
+    o += "\r\n";
     o += body;
     n_resp.fetch_add(1, std::memory_order_relaxed);
   }
 
   void internal_error(Conn* c) {
     append_response(c, 500, "Internal Server Error", "text/plain; charset=utf-8", "Internal Server Error");
+    n_err.fetch_add(1, std::memory_order_relaxed);
+  }
+
+  // Backpressure (engine queue over max_queue): the request was not queued; the client may retry.
+  void service_unavailable(Conn* c) {
+    append_response(c, 503, "Service Unavailable", "application/json",
+                     "{\"detail\":\"server overloaded, retry later\"}", "retry-after: 1\r\n");
     n_err.fetch_add(1, std::memory_order_relaxed);
   }
 

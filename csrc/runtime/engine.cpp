@@ -228,6 +228,11 @@ int Engine::submit_many(const double* X, int n, int nf, const uint64_t* tags, Si
   {
     std::lock_guard<std::mutex> lk(q_mu_);
     if (stopping_) return 0;
+    if ((int64_t)q_meta_.size() + n > (int64_t)cfg_.max_queue) {
+      std::lock_guard<std::mutex> sl(st_mu_);
+      stats_.rejected += (uint64_t)n;
+      return SUBMIT_BUSY;
+    }
     int32_t off = (int32_t)q_x_.size();
     q_x_.insert(q_x_.end(), X, X + (size_t)n * nf);
     for (int i = 0; i < n; ++i, off += nf) q_meta_.push_back(Meta{tags[i], sink, t, nf, off});

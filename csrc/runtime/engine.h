@@ -83,6 +83,7 @@ struct EngineConfig {
   int delay_us = 0;       // fault injection: extra per-batch delay
   int spin_us = 0;        // batcher polls the queue this long before sleeping on the condvar
                           // (saves the futex wake-up on the request path under load)
+  int max_queue = 1 << 20;  // backpressure: rows waiting for the batcher; beyond it submit is refused
   bool persistent = false;  // GPU: one resident kernel fed through a host mailbox instead of a
                             // launch per batch (serve_persistent_kernel, linear_small.hip)
   int persistent_idle_ms = 5;  // the resident kernel exits after this long without work
@@ -91,6 +92,7 @@ struct EngineConfig {
 struct EngineStats {
   uint64_t requests = 0, batches = 0, errors = 0;
   uint64_t kernel_launches = 0;     // persistent mode: (re)launches of the resident kernel
+  uint64_t rejected = 0;            // rows refused by backpressure (max_queue)
   uint64_t batch_hist[12] = {0};    // batch size buckets: 1,2,4,...,2048+
   uint64_t latency_hist[24] = {0};  // latency buckets in powers of two of 1us: <1us .. >=2^23us
   double latency_sum_us = 0;
@@ -115,7 +117,9 @@ class Engine {
 
   // Thread-safe. Returns false if the engine is stopping or nf exceeds max_features.
   bool submit(const double* x, int nf, uint64_t tag, Sink* sink);
-  // n rows (row-major, nf features each) under one lock; returns how many were accepted (0 or n).
+  // n rows (row-major, nf features each) under one lock; returns n if accepted, 0 if the engine
+  // is stopping (or the request is malformed), SUBMIT_BUSY if the queue is over max_queue.
+  static constexpr int SUBMIT_BUSY = -1;
   int submit_many(const double* X, int n, int nf, const uint64_t* tags, Sink* sink);
   // Blocking convenience API (tests / bulk scoring through the batcher).
   void predict(const double* X, int64_t B, int F, int32_t* idx, double* p, int32_t* status);

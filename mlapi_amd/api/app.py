@@ -132,6 +132,12 @@ def create_app(config: Optional[Config] = None, *, runtime=None) -> FastAPI:
             app.state.runtime = ServingRuntime(config)
         return app.state.runtime
 
+    from mlapi_amd.serve.runtime import EngineBusy
+
+    @app.exception_handler(EngineBusy)
+    async def _busy(request, exc):  # backpressure (not in the reference, which has no queue)
+        return JSONResponse({"detail": str(exc)}, status_code=503, headers={"retry-after": "1"})
+
     @app.post("/predict")
     async def predict_species(iris: Record):  # type: ignore[valid-type]
         data = iris.model_dump()

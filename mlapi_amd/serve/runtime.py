@@ -37,6 +37,10 @@ class PredictionError(RuntimeError):
     """Maps to HTTP 500 Internal Server Error (the reference's behaviour for every failure)."""
 
 
+class EngineBusy(PredictionError):
+    """Backpressure: the engine queue is over ``max_queue`` -> HTTP 503 with Retry-After."""
+
+
 class EngineHandle:
     def __init__(self, config: Config, device: Optional[int] = "config"):
         c = C()
@@ -54,6 +58,7 @@ class EngineHandle:
         ec.delay_us = config.delay_us
         ec.spin_us = config.spin_us
         ec.persistent = bool(config.persistent)
+        ec.max_queue = config.max_queue
         ec.persistent_idle_ms = config.persistent_idle_ms
         self.engine = c.Engine(ec)
         self._models: Dict[int, LinearModel] = {}
@@ -209,8 +214,11 @@ class AsyncEngine:
             tag = self._tag
         fut = loop.create_future()
         futures[tag] = fut
-        if not self.handle.engine.submit(np.asarray(row, dtype=np.float64), tag, sink):
+        r = self.handle.engine.submit(np.asarray(row, dtype=np.float64), tag, sink)
+        if r != 1:
             futures.pop(tag, None)
+            if r < 0:
+                raise EngineBusy("server overloaded, retry later")
             raise PredictionError("engine is not accepting requests")
         return await fut
 

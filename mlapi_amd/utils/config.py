@@ -38,6 +38,7 @@ class Config:
     fail_every: int = 0                       # fault injection (tests): fail every N-th batch
     delay_us: int = 0                         # fault injection: delay every batch
     spin_us: int = 0                          # batcher spin before sleeping (0 = always sleep)
+    max_queue: int = 1 << 20                  # backpressure: queued rows beyond this -> HTTP 503
     persistent: bool = False                  # GPU: resident serving kernel fed by a host mailbox
     persistent_idle_ms: int = 5               # ... which exits after this long without work
     # HTTP

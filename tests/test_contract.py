@@ -103,6 +103,14 @@ def test_hot_swap_by_replacing_the_file(iris_cwd):
     assert c.post("/predict", json=A1).status_code == 500
 
 
+def test_backpressure_is_503_with_retry_after(iris_cwd):
+    """Not in the reference (no queue): a full engine queue answers 503 instead of queueing forever."""
+    c = _client(max_queue=0)
+    r = c.post("/predict", json=A1)
+    assert r.status_code == 503 and r.headers["retry-after"] == "1"
+    assert r.json() == {"detail": "server overloaded, retry later"}
+
+
 def test_unsafe_checkpoint_is_refused(tmp_path, monkeypatch):
     class Evil:
         def __reduce__(self):

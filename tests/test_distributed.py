@@ -60,6 +60,18 @@ def test_broadcast_and_dp_sgd_determinism(tmp_path):
     np.testing.assert_allclose(m0, np.load(tmp_path / "mc_params_1_0.npy"), rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("world", [4, 8])
+def test_dp_sgd_determinism_more_ranks(tmp_path, world):
+    """N ranks == 1 rank on the same global batch (binary and multiclass), N = 4, 8."""
+    script = str(ROOT / "tests" / "dist" / "bcast_train.py")
+    run(1, script, {"OUT": str(tmp_path)})
+    run(world, script, {"OUT": str(tmp_path)}, timeout=300)
+    for name in ("params", "mc_params"):
+        ranks = [np.load(tmp_path / f"{name}_{world}_{r}.npy") for r in range(world)]
+        assert all(np.array_equal(ranks[0], x) for x in ranks[1:]), "replicas must stay bitwise identical"
+        np.testing.assert_allclose(ranks[0], np.load(tmp_path / f"{name}_1_0.npy"), rtol=1e-4, atol=1e-5)
+
+
 def test_fake_comm_collectives(tmp_path):
     """The framework communicator API (NativeComm's twin) over gloo, world_size 2 and 1."""
     script = str(ROOT / "tests" / "dist" / "comm_semantics.py")

@@ -103,7 +103,7 @@ def test_stop_is_idempotent_and_rejects(native, model):
     e.load_model(int(model.kind), model.W, model.b, model.label_json())
     e.stop()
     e.stop()
-    assert e.submit(np.zeros(4), 1, native.PySink()) is False
+    assert e.submit(np.zeros(4), 1, native.PySink()) == 0  # stopping (-1 would mean backpressure)
 
 
 def test_async_engine(model):
@@ -146,3 +146,66 @@ def test_model_store_watch(tmp_path, iris_pickle_bytes):
     assert h.version == 0 and store.last_error
     store.stop()
     h.close()
+
+
+def test_max_wait_fills_batches(native, model):
+    """max_wait_us > 0: the batcher waits (bounded) for more rows instead of launching at once."""
+    e = make_engine(native, max_wait_us=20000, max_batch=64)
+    e.load_model(int(model.kind), model.W, model.b, model.label_json())
+    sink = native.PySink()
+    X = np.random.default_rng(1).normal(size=(64, 4))
+    t0 = time.time()
+    for i in range(64):  # trickle in: without the wait these would be many small batches
+        e.submit(X[i], i, sink)
+        time.sleep(0.0001)
+    got = 0
+    while got < 64 and time.time() - t0 < 10:
+        got += len(sink.drain())
+        time.sleep(0.001)
+    s = e.stats()
+    e.stop()
+    assert got == 64 and s["batches"] <= 4
+
+
+def test_backpressure_refuses_beyond_max_queue(native, model):
+    e = make_engine(native, max_queue=100, delay_us=50000, max_batch=10)
+    e.load_model(int(model.kind), model.W, model.b, model.label_json())
+    sink = native.PySink()
+    results = [e.submit(np.ones(4), i, sink) for i in range(400)]
+    assert results.count(-1) > 0 and results.count(1) >= 100  # queue full -> refused, not dropped
+    assert e.stats()["rejected"] == results.count(-1)
+    e.stop()
+
+
+def test_backpressure_http_503(native, model, tmp_path):
+    """Native server: a refused submit answers 503 + Retry-After (the request was not queued)."""
+    import socket
+
+    e = make_engine(native, max_queue=1, delay_us=200000, max_batch=1)
+    e.load_model(int(model.kind), model.W, model.b, model.label_json())
+    sc = native.ServerConfig()
+    sc.port = 0
+    sc.io_threads = 1
+    sc.feature_names = ["sepal_length", "sepal_width", "petal_length", "petal_width"]
+    srv = native.HttpServer(e, sc)
+    srv.start()
+    body = b'{"sepal_length":1,"sepal_width":2,"petal_length":3,"petal_width":4}'
+    req = (b"POST /predict HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n%s"
+           % (len(body), body))
+    socks = []
+    try:
+        for _ in range(6):
+            s = socket.create_connection(("127.0.0.1", srv.port()))
+            s.sendall(req)
+            socks.append(s)
+        codes = []
+        for s in socks:
+            s.settimeout(10)
+            codes.append(s.recv(65536).split(b" ")[1])
+        assert b"503" in codes and b"200" in codes
+        assert srv.stats()["errors"] >= 1
+    finally:
+        for s in socks:
+            s.close()
+        srv.stop()
+        e.stop()
