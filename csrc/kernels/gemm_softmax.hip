@@ -133,18 +133,17 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 // mode's epilogue. Inlined into the kernel (reference parameters stay in registers).
 template <int KS, int NT, int MODE, bool OVR>
 __device__ __forceinline__ void compute_chunk(const unsigned char* wb, const bf16x8_t (&xf)[NT][KS], int c0, int c_end,
-                                              int q, int col, int64_t row0, int64_t B, int K, const float* bias,
+                                              int q, int col, int64_t row0, int64_t B, int K, const float* bias_lds,
                                               const GemmArgs& a, RowState (&st)[NT], const int (&yl)[NT],
                                               const float (&lse)[NT], float& loss_acc) {
   constexpr bool ovr = OVR;
-  // The accumulators start at the bias (clamped index; classes past the split are masked
-  // later), so the epilogue needs no per-element add.
+  // The accumulators start at the bias, which was DMA'd into LDS next to the W chunk (clamped
+  // index; classes past the split are masked later), so the epilogue needs no per-element add and
+  // no global load sits between the counted waits of the staging pipeline.
   f32x4_t acc[NT][4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
-    f32x4_t b0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) b0[r] = bias[min(c0 + mt * 16 + q * 4 + r, K - 1)];
+    const f32x4_t b0 = *reinterpret_cast<const f32x4_t*>(bias_lds + mt * 16 + q * 4);
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t][mt] = b0;
   }
@@ -267,7 +266,8 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   constexpr int ROWS_PER_BLOCK = 4 * ROWS_PER_WAVE;
   constexpr int F_ = KS * 32;
   constexpr int NCH = F_ / 8;                          // 16-byte chunks per W row
-  constexpr int BUF_BYTES = CLASS_CHUNK * lds_row_stride<KS>();
+  constexpr int W_BYTES = CLASS_CHUNK * lds_row_stride<KS>();
+  constexpr int BUF_BYTES = W_BYTES + CLASS_CHUNK * 4;  // [W chunk][64 f32 bias]
   constexpr int PIECES = CLASS_CHUNK * NCH / 256;      // 16-byte pieces per thread per chunk (== KS)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF_BYTES + 16];
   int* const flag = reinterpret_cast<int*>(smem + 2 * BUF_BYTES);
@@ -285,17 +285,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   const int c_end = min(K, c_begin + classes_per_split);
   const int c_last = c_begin + ((c_end - 1 - c_begin) / CLASS_CHUNK) * CLASS_CHUNK;  // last chunk start
 
-  // ---- X fragments for the whole feature range, straight to registers (issued first)
   bf16x8_t xf[NT][KS];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    int64_t r = row0 + t * 16 + col;
-    r = r < B ? r : B - 1;
-    const uint16_t* xr = X + r * a.ldx + 8 * q;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)  // X is streamed once: non-temporal, keep the L2 for W
-      xf[t][ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + ks * 32));
-  }
   // MODE 3: this lane's rows' label and {lse, argmax} (clamped loads, masked by row < B later)
   int yl[NT];
   float lse[NT];
@@ -328,23 +318,66 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
     __builtin_amdgcn_global_load_lds((glob_void_t*)src,                                                 \
                                      (lds_void_t*)(smem + (BUF) * BUF_BYTES + (i * 256 + wave * 64) * 16), \
                                      16, 0, 0);                                                         \
-  }
+  }                                                                                                     \
+  /* bias: each wave DMAs 16 floats (lanes 0-15), one more VM op per wave (uniform count) */            \
+  if (lane < 16)                                                                                        \
+    __builtin_amdgcn_global_load_lds((glob_void_t*)(bias + min((C0) + wave * 16 + lane, K - 1)),       \
+                                     (lds_void_t*)(smem + (BUF) * BUF_BYTES + W_BYTES + wave * 64), 4, 0, 0);
 
   RowState st[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) st[t] = RowState{-INFINITY, 0.f, 0x7fffffff};
 
+  // Two chunks in flight: the prologue DMAs chunks 0 and 1 together (a split of B=1024 has only
+  // two, so their latencies overlap instead of adding up); in the loop the DMA of chunk c+2 goes
+  // into the buffer chunk c was just read from (after a barrier: WAR), and a COUNTED wait retires
+  // chunk c+1 while c+2 stays in flight. Raw s_barrier, not __syncthreads(): the latter's fence
+  // waits vmcnt(0) and would drain the in-flight DMA (cdna_hip_programming.md "Pipelining across
+  // barriers"); the empty asm statements keep the compiler from moving LDS accesses across it.
+#define MLAPI_RAW_BARRIER()          \
+  asm volatile("" ::: "memory");     \
+  __builtin_amdgcn_s_barrier();      \
+  asm volatile("" ::: "memory");
   int buf = 0;
   MLAPI_DMA_CHUNK(c_begin, 0)
-  __syncthreads();
+  // X fragments for the whole feature range, straight to registers, issued between the DMAs of
+  // chunks 0 and 1 so that ONE counted wait retires chunk 0 + X while chunk 1 stays in flight
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    int64_t r = row0 + t * 16 + col;
+    r = r < B ? r : B - 1;
+    const uint16_t* xr = X + r * a.ldx + 8 * q;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)  // X is streamed once: non-temporal, keep the L2 for W
+      xf[t][ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + ks * 32));
+  }
+  // (the builtin form of s_waitcnt is visible to the compiler's wait insertion, so it does not
+  // add a vmcnt(0) for the X registers before the loop; encoding: vmcnt[3:0,15:14], expcnt[6:4],
+  // lgkmcnt[11:8] with the other two counters left at "no wait")
+  constexpr int kWaitChunk = ((PIECES + 1) & 15) | (7 << 4) | (15 << 8) | (((PIECES + 1) >> 4) << 14);
+  constexpr int kWaitAll = (7 << 4) | (15 << 8);
+  if (c_begin + CLASS_CHUNK < c_end) {
+    MLAPI_DMA_CHUNK(c_begin + CLASS_CHUNK, 1)
+    __builtin_amdgcn_s_waitcnt(kWaitChunk);  // chunk 0 + X landed, chunk 1 may still fly
+  } else {
+    __builtin_amdgcn_s_waitcnt(kWaitAll);
+  }
+  MLAPI_RAW_BARRIER()
   for (int c0 = c_begin; c0 < c_end; c0 += CLASS_CHUNK) {
-    MLAPI_DMA_CHUNK(min(c0 + CLASS_CHUNK, c_last), buf ^ 1)
-    compute_chunk<KS, NT, MODE, OVR>(smem + buf * BUF_BYTES, xf, c0, c_end, q, col, row0, B, K, bias, a, st, yl, lse,
+    compute_chunk<KS, NT, MODE, OVR>(smem + buf * BUF_BYTES, xf, c0, c_end, q, col, row0, B, K,
+                                     reinterpret_cast<const float*>(smem + buf * BUF_BYTES + W_BYTES), a, st, yl, lse,
                                      loss_acc);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA landed ...
-    __syncthreads();                                   // ... and every other wave's
+    if (c0 + 2 * CLASS_CHUNK < c_end) {
+      MLAPI_RAW_BARRIER()  // every wave is done reading `buf`
+      MLAPI_DMA_CHUNK(c0 + 2 * CLASS_CHUNK, buf)
+      __builtin_amdgcn_s_waitcnt(kWaitChunk);  // chunk c+1 landed, c+2 flies
+    } else {
+      __builtin_amdgcn_s_waitcnt(kWaitAll);
+    }
+    MLAPI_RAW_BARRIER()
     buf ^= 1;
   }
+#undef MLAPI_RAW_BARRIER
 #undef MLAPI_DMA_CHUNK
   if constexpr (MODE == 3) {
     // correct count: split 0, one lane (q == 0) per row
