@@ -10,7 +10,9 @@ LogisticRegression() (L-BFGS, C=1), pickle it to LRClassifier.pkl, reload it, pr
 
 ``torchrun --nproc-per-node N -m mlapi_amd.train sgd --features 256 --rows-per-rank 1048576 ...``
 runs data-parallel mini-batch SGD on synthetic data (BASELINE config 5) with checkpoint/resume
-in the native format (``--ckpt``; ``--resume``).
+in the native format (``--ckpt``; ``--resume``). ``--classes K`` (K > 2) trains a softmax
+(``--kind multinomial``) or one-vs-rest model with the MFMA gradient kernels; ``--graph``
+captures a single-GPU step in a HIP graph.
 """
 from __future__ import annotations
 
@@ -51,6 +53,9 @@ def cmd_fit(X, y, args) -> int:
 
 def cmd_sgd(args) -> int:
     import torch
+
+    if args.classes > 2:
+        return cmd_sgd_multiclass(args)
 
     from mlapi_amd.ckpt.native import TrainState, load_native, save_native
     from mlapi_amd.parallel.comm import barrier, init_distributed, shutdown
@@ -99,6 +104,63 @@ def cmd_sgd(args) -> int:
     return 0
 
 
+def cmd_sgd_multiclass(args) -> int:
+    import torch
+
+    from mlapi_amd.ckpt.native import TrainState, load_native, save_native
+    from mlapi_amd.models.linear import Kind
+    from mlapi_amd.parallel.comm import barrier, init_distributed, shutdown
+    from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer, synthetic_multiclass
+
+    info = init_distributed()
+    dev = info.device
+    kind = Kind.OVR if args.kind == "ovr" else Kind.MULTINOMIAL
+    X, y = synthetic_multiclass(args.rows_per_rank, args.features, args.classes, seed=1000 + info.rank,
+                                device=dev, noise=args.noise)
+    tr = SoftmaxSGDTrainer(args.features, args.classes, kind=kind, info=info, lr=args.lr, l2=args.l2,
+                           momentum=args.momentum, device=dev)
+    Xa = tr.prepare(X)
+    del X
+    start = 0
+    if args.resume and os.path.exists(args.ckpt):
+        model, st = load_native(args.ckpt)
+        tr.set_params(torch.as_tensor(model.W, dtype=torch.float32), torch.as_tensor(model.b, dtype=torch.float32))
+        if tr.mom is not None and "mom" in st.opt:
+            tr.mom.copy_(torch.as_tensor(st.opt["mom"], dtype=torch.float32))
+        start = tr.steps = st.step
+        if info.is_main:
+            print(f"resumed from {args.ckpt} at step {start}", flush=True)
+    nb = max(1, args.rows_per_rank // args.batch)
+    shards = [(Xa[j * args.batch:(j + 1) * args.batch], y[j * args.batch:(j + 1) * args.batch]) for j in range(nb)]
+    if args.graph and dev is not None and info.world == 1 and nb == 1:
+        tr.capture(*shards[0])  # one HIP graph launch per step
+    t0 = time.perf_counter()
+    for step in range(start, args.steps):
+        tr.step(*shards[step % nb])
+        if info.is_main and (step + 1) % args.log_every == 0:
+            print(json.dumps({"step": step + 1, "loss": tr.last_loss(), "acc": tr.last_accuracy()}), flush=True)
+        if args.ckpt and (step + 1) % args.ckpt_every == 0:
+            barrier(info)
+            if info.is_main:
+                st = TrainState(step=step + 1, opt={} if tr.mom is None else {"mom": tr.mom.cpu().numpy()},
+                                config=vars(args))
+                save_native(args.ckpt, tr.to_model(), st)
+    if dev is not None:
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if info.is_main:
+        n = (args.steps - start) * args.batch * info.world
+        print(json.dumps({"samples_per_s": n / max(dt, 1e-9), "final_loss": tr.last_loss(),
+                          "final_acc": tr.last_accuracy(), "world": info.world, "classes": args.classes}),
+              flush=True)
+        if args.out:
+            from mlapi_amd.ckpt.sklearn_pickle import export_sklearn_pickle
+
+            export_sklearn_pickle(tr.to_model(), args.out)
+    shutdown(info)
+    return 0
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="python -m mlapi_amd.train")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -125,6 +187,10 @@ def main(argv=None) -> int:
     p.add_argument("--ckpt-every", type=int, default=100)
     p.add_argument("--resume", action="store_true")
     p.add_argument("--out", default="")
+    p.add_argument("--classes", type=int, default=2, help="> 2: multiclass (softmax / one-vs-rest) SGD")
+    p.add_argument("--kind", default="multinomial", choices=["multinomial", "ovr"])
+    p.add_argument("--noise", type=float, default=1.0, help="multiclass synthetic label noise")
+    p.add_argument("--graph", action="store_true", help="capture the single-GPU step in a HIP graph")
     args = ap.parse_args(argv)
     if args.cmd == "iris":
         X, y = iris_dataset()

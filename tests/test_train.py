@@ -175,3 +175,25 @@ def test_estimator_sgd_multiclass_cpu(iris_data):
     assert list(clf.classes_) == ["Iris-setosa", "Iris-versicolor", "Iris-virginica"]
     assert clf.coef_.shape == (3, 4)
     assert clf.score(Xte, yte) >= 0.9
+
+
+def test_cli_sgd_multiclass_checkpoint_resume(tmp_path):
+    ck = str(tmp_path / "m.safetensors")
+    base = [sys.executable, "-m", "mlapi_amd.train", "sgd", "--features", "32", "--classes", "5",
+            "--rows-per-rank", "4000", "--batch", "500", "--log-every", "1000", "--ckpt", ck, "--ckpt-every", "10",
+            "--noise", "0.3"]
+    env = {**ENV, "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""}
+    full = subprocess.run(base + ["--steps", "20"], env=env, capture_output=True, text=True, timeout=300)
+    assert full.returncode == 0, full.stderr
+    final_full = json.loads(full.stdout.strip().splitlines()[-1])
+    assert final_full["classes"] == 5 and final_full["final_acc"] > 0.5
+    os.remove(ck)
+    a = subprocess.run(base + ["--steps", "10"], env=env, capture_output=True, text=True, timeout=300)
+    assert a.returncode == 0, a.stderr
+    b = subprocess.run(base + ["--steps", "20", "--resume", "--out", str(tmp_path / "m.pkl")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert b.returncode == 0 and "resumed" in b.stdout, b.stdout + b.stderr
+    final_resumed = json.loads(b.stdout.strip().splitlines()[-1])
+    assert final_resumed["final_loss"] == pytest.approx(final_full["final_loss"], rel=1e-6)
+    sk = pickle.loads((tmp_path / "m.pkl").read_bytes())  # our own export, readable by sklearn
+    assert sk.coef_.shape == (5, 32)
