@@ -126,7 +126,7 @@ def bench_serve(args, info):
         "gpu_leg_us_batch1": float(np.mean(per_rank[:, 7])),
         "backend": srv.runtime.handle.backend,
         "cpu_cores_busy_rank0": cpu_util,
-        "threads": {"io": args.io_threads, "loadgen": args.client_threads},
+        "threads": {"io": args.io_threads, "loadgen": args.client_threads, "pinned_cpus": args.pinned_cpus},
         "requests_per_step": args.reqs_per_conn * args.conns * info.world,
         "baseline_note": "reference uvicorn+sklearn, 1 worker, c=64: 1494 req/s, p50 41.8 ms; c=1 p50 0.881 ms",
     }
@@ -243,20 +243,30 @@ def main(argv=None) -> int:
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--softmax-batch", type=int, default=1 << 16)
     ap.add_argument("--cpu", action="store_true", help="force the CPU backend (testing without a GPU)")
+    ap.add_argument("--pin", default="auto", choices=["auto", "on", "off"],
+                    help="pin this rank to its share of physical cores on its GPU's NUMA node "
+                         "(auto: when several ranks share the node and no launcher pinned them)")
     args = ap.parse_args(argv)
 
     from mlapi_amd.parallel.comm import init_distributed, shutdown
 
     info = init_distributed(use_gpu=False if args.cpu else None)
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", info.world))
+    pinned = []
+    if args.pin == "on" or (args.pin == "auto" and local > 1 and not os.environ.get("MLAPI_LAUNCHER")):
+        # before any native thread starts: the server / batcher / load-generator threads inherit it
+        from mlapi_amd.utils.affinity import pin_this_rank
+
+        pinned = pin_this_rank(info.local_rank, local, None if info.device is None else info.device.index)
+    args.pinned_cpus = len(pinned)
     if args.io_threads <= 0 or args.client_threads <= 0:
         # Server IO threads and load-generator threads share this rank's CPUs (sweep on a 16-CPU
         # MI355X box share: 6 + 6 threads -> 519k req/s vs 3 + 3 -> 270k; tools/serve_sweep.sh).
-        try:
-            cpus = len(os.sched_getaffinity(0))
-        except AttributeError:  # pragma: no cover
-            cpus = os.cpu_count() or 8
-        local = int(os.environ.get("LOCAL_WORLD_SIZE", info.world))
-        per_rank = max(4, cpus // max(1, local))
+        # The CPU budget is the cgroup quota, not the affinity mask (a 1-GPU box: 256 CPUs in the
+        # mask, cpu.max = 16 cores), shared by the ranks of this node.
+        from mlapi_amd.utils.threads import effective_cpus
+
+        per_rank = max(4, len(pinned) if pinned else effective_cpus() // max(1, local))
         # measured on a 16-CPU share: io=8/client=6 -> 971k req/s; 6/6 -> 549k; 4/4 -> 282k
         io = max(2, min(8, (per_rank - 2) // 2 + 1))
         cl = max(2, min(6, per_rank - io - 2))

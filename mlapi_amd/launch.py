@@ -27,6 +27,8 @@ import sys
 import time
 from typing import List, Optional
 
+from mlapi_amd.utils.affinity import core_order, cpu_slices  # noqa: F401 (re-exported)
+
 
 def _free_port(host: str) -> int:
     s = socket.socket()
@@ -34,20 +36,6 @@ def _free_port(host: str) -> int:
     port = s.getsockname()[1]
     s.close()
     return port
-
-
-def cpu_slices(nproc: int, cpus: Optional[List[int]] = None) -> List[List[int]]:
-    """Split the usable CPUs into ``nproc`` contiguous, disjoint, near-equal slices."""
-    cpus = sorted(cpus if cpus is not None else os.sched_getaffinity(0))
-    if nproc > len(cpus):  # oversubscribed: share round-robin
-        return [[cpus[i % len(cpus)]] for i in range(nproc)]
-    base, extra = divmod(len(cpus), nproc)
-    out, i = [], 0
-    for r in range(nproc):
-        n = base + (1 if r < extra else 0)
-        out.append(cpus[i:i + n])
-        i += n
-    return out
 
 
 def main(argv=None) -> int:

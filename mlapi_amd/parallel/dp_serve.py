@@ -118,6 +118,13 @@ def start_dp_runtime(cfg: Config, info: Optional[DistInfo] = None):
     from mlapi_amd.serve.service import ServingRuntime
 
     info = info or init_distributed()
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", info.world))
+    if cfg.pin == "on" or (cfg.pin == "auto" and local > 1 and not os.environ.get("MLAPI_LAUNCHER")):
+        # before the engine / server threads exist: they inherit this rank's CPU slice
+        from mlapi_amd.utils.affinity import pin_this_rank
+
+        cpus = pin_this_rank(info.local_rank, local, None if info.device is None else info.device.index)
+        log.info("rank %d pinned to %d CPUs", info.rank, len(cpus))
     model = None
     if info.is_main:
         from mlapi_amd.ckpt.native import load_model

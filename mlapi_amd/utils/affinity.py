@@ -1,0 +1,185 @@
+"""CPU placement for one-process-per-GPU serving: physical cores, the GPU's NUMA node, the quota.
+
+The serving path is CPU bound (HTTP parse, batching, JSON render run on host threads; the GPU leg
+of a request is ~10 us), so where a rank's threads run decides whole-node req/s. Facts measured on
+the MI355X hosts (``tools/probe_box.sh``, ``profiles/r1_session5/probe.txt``):
+
+* 2 sockets x 64 cores x 2 SMT threads; logical CPUs N and N+128 are siblings; NUMA node 0 holds
+  CPUs 0-63 and 128-191, node 1 holds 64-127 and 192-255; four GPUs hang off each node.
+* The affinity mask shows all 256 CPUs, while the container's ``cpu.max`` allows 16 cores per GPU.
+
+So a rank is placed on ``quota / ranks`` distinct physical cores of its own GPU's NUMA node (the
+zero-copy request slots the kernel reads live in host memory of that node). Used by
+``mlapi_amd.launch`` and by ``bench.py`` / ``mlapi_amd.serve`` under ``torchrun``.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional
+
+SYS_CPU = "/sys/devices/system/cpu"
+SYS_NODE = "/sys/devices/system/node"
+
+
+def _read(path: str) -> Optional[str]:
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def parse_cpulist(s: str) -> List[int]:
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11]."""
+    out: List[int] = []
+    for part in s.split(","):
+        part = part.strip()
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            out.extend(range(int(a), int(b) + 1))
+        else:
+            out.append(int(part))
+    return out
+
+
+def _core_key(cpu: int, sysfs: str) -> tuple:
+    """(package, core) of a logical CPU; CPUs without topology info sort by their number."""
+    pkg = _read(f"{sysfs}/cpu{cpu}/topology/physical_package_id")
+    core = _read(f"{sysfs}/cpu{cpu}/topology/core_id")
+    try:
+        return (int(pkg), int(core))
+    except (TypeError, ValueError):
+        return (0, cpu)
+
+
+def _cores(cpus: List[int], sysfs: str) -> List[List[int]]:
+    """Physical cores (package-major) as lists of their logical CPUs among ``cpus``."""
+    by_core: Dict[tuple, List[int]] = {}
+    for c in sorted(cpus):
+        by_core.setdefault(_core_key(c, sysfs), []).append(c)
+    return [by_core[k] for k in sorted(by_core)]
+
+
+def _threads_first(cores: List[List[int]]) -> List[int]:
+    depth = max((len(c) for c in cores), default=0)
+    return [core[t] for t in range(depth) for core in cores if t < len(core)]
+
+
+def core_order(cpus: List[int], sysfs: str = SYS_CPU) -> List[int]:
+    """Logical CPUs ordered one hardware thread per physical core first (package-major), then the
+    SMT siblings in the same core order (numeric order would pair CPU N with its sibling N+128)."""
+    return _threads_first(_cores(cpus, sysfs))
+
+
+def _split_cores(cores: List[List[int]], nslices: int, per_slice: int) -> List[List[int]]:
+    """``nslices`` disjoint slices of at most ``per_slice`` CPUs that never share a physical core:
+    each slice owns whole cores, first threads first, and uses SMT siblings only of its own cores
+    when its budget exceeds the cores it owns."""
+    base, extra = divmod(len(cores), nslices)
+    out, i = [], 0
+    for j in range(nslices):
+        n = base + (1 if j < extra else 0)
+        out.append(_threads_first(cores[i:i + n])[:per_slice])
+        i += n
+    return out
+
+
+def cpu_slices(nproc: int, cpus: Optional[List[int]] = None, budget: Optional[int] = None,
+               sysfs: str = SYS_CPU) -> List[List[int]]:
+    """Split the usable CPUs into ``nproc`` disjoint, near-equal slices of whole physical cores.
+
+    ``budget`` caps the CPUs handed out (default when ``cpus`` is not given: the cgroup quota,
+    :func:`mlapi_amd.utils.threads.effective_cpus`)."""
+    from mlapi_amd.utils.threads import effective_cpus
+
+    if cpus is None:
+        cpus = sorted(os.sched_getaffinity(0))
+        if budget is None:
+            budget = effective_cpus()
+    cpus = list(cpus)
+    if nproc > len(cpus):  # oversubscribed: share round-robin
+        order = core_order(cpus, sysfs)
+        return [[order[i % len(order)]] for i in range(nproc)]
+    budget = len(cpus) if budget is None else max(nproc, min(budget, len(cpus)))
+    cores = _cores(cpus, sysfs)
+    if len(cores) >= nproc:
+        per, extra = divmod(budget, nproc)
+        return [s[:per + (1 if r < extra else 0)] for r, s in enumerate(_split_cores(cores, nproc, budget))]
+    order = core_order(cpus, sysfs)[:budget]  # fewer cores than ranks: slices share cores
+    base, extra = divmod(len(order), nproc)
+    out, i = [], 0
+    for r in range(nproc):
+        n = base + (1 if r < extra else 0)
+        out.append(order[i:i + n])
+        i += n
+    return out
+
+
+def node_cpus(node: int, sysnode: str = SYS_NODE) -> List[int]:
+    s = _read(f"{sysnode}/node{node}/cpulist")
+    return parse_cpulist(s) if s else []
+
+
+def gpu_numa_node(device_index: int) -> Optional[int]:
+    """NUMA node of a visible GPU (PCI location from the HIP device properties -> sysfs)."""
+    try:
+        import torch
+
+        p = torch.cuda.get_device_properties(device_index)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    except Exception:
+        return None
+    s = _read(f"/sys/bus/pci/devices/{bdf}/numa_node")
+    try:
+        n = int(s)
+    except (TypeError, ValueError):
+        return None
+    return n if n >= 0 else None
+
+
+def rank_cpus(local_rank: int, local_world: int, gpu_nodes: Optional[List[Optional[int]]] = None,
+              cpus: Optional[List[int]] = None, budget: Optional[int] = None, sysfs: str = SYS_CPU,
+              sysnode: str = SYS_NODE) -> List[int]:
+    """CPUs for ``local_rank``: its share of the budget, on its GPU's NUMA node when that node has
+    room for every rank attached to it, else a plain physical-core slice."""
+    from mlapi_amd.utils.threads import effective_cpus
+
+    if cpus is None:
+        cpus = sorted(os.sched_getaffinity(0))
+        if budget is None:
+            budget = effective_cpus()
+    budget = len(cpus) if budget is None else min(budget, len(cpus))
+    per_rank = max(1, budget // max(1, local_world))
+    node = gpu_nodes[local_rank] if gpu_nodes and local_rank < len(gpu_nodes) else None
+    if node is not None:
+        peers = [r for r in range(local_world) if gpu_nodes[r] == node]
+        allowed = set(cpus)
+        cores = _cores([c for c in node_cpus(node, sysnode) if c in allowed], sysfs)
+        if len(cores) >= len(peers) and sum(map(len, cores)) >= per_rank * len(peers):
+            return _split_cores(cores, len(peers), per_rank)[peers.index(local_rank)]
+    return cpu_slices(local_world, cpus, budget, sysfs)[local_rank]
+
+
+def pin_this_rank(local_rank: int, local_world: int, device_index: Optional[int] = None) -> List[int]:
+    """Pin the calling process (threads created afterwards inherit it) to :func:`rank_cpus`.
+
+    GPU ``i`` of this node is assumed to be the device of local rank ``i`` (torchrun /
+    ``mlapi_amd.launch`` convention). Returns the CPUs, or [] when pinning is not possible."""
+    nodes: List[Optional[int]] = []
+    try:
+        import torch
+
+        n = torch.cuda.device_count()
+        nodes = [gpu_numa_node(i) if i < n else None for i in range(local_world)]
+        if device_index is not None and local_rank < len(nodes):
+            nodes[local_rank] = gpu_numa_node(device_index)
+    except Exception:
+        nodes = []
+    try:
+        cpus = rank_cpus(local_rank, local_world, nodes or None)
+        os.sched_setaffinity(0, cpus)
+        return cpus
+    except (OSError, ValueError, IndexError):
+        return []

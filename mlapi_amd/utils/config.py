@@ -41,6 +41,7 @@ class Config:
     max_queue: int = 1 << 20                  # backpressure: queued rows beyond this -> HTTP 503
     persistent: bool = False                  # GPU: resident serving kernel fed by a host mailbox
     persistent_idle_ms: int = 5               # ... which exits after this long without work
+    pin: str = "auto"                         # CPU pinning per rank: auto (DP without launcher) | on | off
     # HTTP
     host: str = "127.0.0.1"
     port: int = 8000

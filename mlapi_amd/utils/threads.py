@@ -51,6 +51,45 @@ def cpu_by_group(pid: int | None = None) -> Dict[str, float]:
     return out
 
 
+def cgroup_cpu_quota(root: str = "/sys/fs/cgroup") -> float | None:
+    """CPU bandwidth limit of this container in cores (cgroup v2 ``cpu.max`` or v1 CFS), or None.
+
+    On the MI355X pool a 1-GPU box shows 256 CPUs in the affinity mask but ``cpu.max`` allows 16
+    cores: sizing thread pools from the mask alone oversubscribes the quota and the kernel
+    throttles the whole process for the rest of each 100 ms period.
+    """
+    try:
+        with open(os.path.join(root, "cpu.max")) as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max" and int(period) > 0:
+            return int(quota) / int(period)
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open(os.path.join(root, "cpu", "cpu.cfs_quota_us")) as f:
+            quota_us = int(f.read().strip())
+        with open(os.path.join(root, "cpu", "cpu.cfs_period_us")) as f:
+            period_us = int(f.read().strip())
+        if quota_us > 0 and period_us > 0:
+            return quota_us / period_us
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def effective_cpus(root: str = "/sys/fs/cgroup") -> int:
+    """CPUs this process can actually keep busy: min(affinity mask, cgroup quota)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    q = cgroup_cpu_quota(root)
+    if q is not None:
+        n = min(n, max(1, int(q)))
+    return max(1, n)
+
+
 def utilization(before: Dict[str, float], after: Dict[str, float], seconds: float) -> Dict[str, float]:
     """Cores busy per group over an interval."""
     keys = set(before) | set(after)
