@@ -50,6 +50,7 @@ constexpr int CLASS_CHUNK = 64;
 constexpr float LOG2E_F = 1.4426950408889634f;
 constexpr float LN2_F = 0.6931471805599453f;
 constexpr int COUNTER_BYTES = 4096;  // per-row-block arrival counters live at the start of the workspace
+constexpr int MERGE_MAX = 8;         // split partials the merging block loads at once (automatic plans: <= 8)
 
 struct RowState {
   float m;  // running max logit (-inf if nothing seen yet)
@@ -423,18 +424,28 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
       }
       return;
     }
-    // ---- split classes: publish partials, last-arriving block of this row block merges them
+    // ---- split classes: publish partials, last-arriving block of this row block merges them.
+    // Partials are stored write-through (sc1: agent-scope atomic stores into global memory), so
+    // no release fence (buffer_wbl2, ~1.7 us per block on the critical path) is needed before the
+    // ticket: every storing wave drains (vmcnt(0)), the workgroup barrier orders the waves, then one
+    // lane takes the ticket; the merging block keeps its agent acquire (cdna_hip_programming.md
+    // Guideline 16, R1).
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int64_t row = row0 + t * 16 + col;
-      if (q == 0 && row < B)
-        a.partials[(int64_t)blockIdx.y * B + row] = make_float4(st[t].m, st[t].s, __int_as_float(st[t].bi), 0.f);
+      if (q == 0 && row < B) {
+        typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+        typedef __attribute__((address_space(1))) unsigned int gu32_t;
+        float4* dst = a.partials + (int64_t)blockIdx.y * B + row;
+        const unsigned long long ms =
+            (unsigned long long)__float_as_uint(st[t].m) | ((unsigned long long)__float_as_uint(st[t].s) << 32);
+        __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu32_t*)dst + 2, (unsigned)st[t].bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
     __syncthreads();
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep: ROCm 7.2 may drop the fence's own wait
       const unsigned ticket =
           __hip_atomic_fetch_add(&a.counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = ticket == gridDim.y - 1;
@@ -450,11 +461,21 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
     if (tid < ROWS_PER_BLOCK) {
       const int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + tid;
       if (row < B) {
-        float4 p0 = a.partials[row];
-        RowState S{p0.x, p0.y, __float_as_int(p0.z)};
-        for (unsigned sp = 1; sp < gridDim.y; ++sp) {  // fixed split order: deterministic
-          const float4 p = a.partials[(int64_t)sp * B + row];
-          S = merge_state(S, RowState{p.x, p.y, __float_as_int(p.z)}, ovr);
+        // All splits' partials are issued before the first merge: a load-merge-load chain made each
+        // split one more dependent round trip to the memory-side cache (the partials were written
+        // by CUs of other XCDs), ~7 of them at B=1024.
+        const unsigned ns = gridDim.y;
+        float4 p[MERGE_MAX];
+#pragma unroll
+        for (int sp = 0; sp < MERGE_MAX; ++sp)
+          p[sp] = a.partials[(int64_t)min((unsigned)sp, ns - 1) * B + row];  // clamped: unconditional
+        RowState S{p[0].x, p[0].y, __float_as_int(p[0].z)};
+#pragma unroll
+        for (int sp = 1; sp < MERGE_MAX; ++sp)  // fixed split order: deterministic
+          if ((unsigned)sp < ns) S = merge_state(S, RowState{p[sp].x, p[sp].y, __float_as_int(p[sp].z)}, ovr);
+        for (unsigned sp = MERGE_MAX; sp < ns; ++sp) {  // plans with more splits (forced sweeps)
+          const float4 q = a.partials[(int64_t)sp * B + row];
+          S = merge_state(S, RowState{q.x, q.y, __float_as_int(q.z)}, ovr);
         }
         if constexpr (MODE == 0) {
           a.out_idx[row] = S.bi;
