@@ -374,11 +374,13 @@ class IoThread : public Sink {
     const int n = (int)pend_tags_.size();
     const int r = srv_->engine()->submit_many(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), this);
     if (r != n) {
-      for (uint64_t id : pend_tags_) {  // overloaded: 503 + Retry-After; engine stopping: 500
+      // rows [0, r) were queued; the rest: overloaded -> 503 + Retry-After, engine stopping -> 500
+      for (int i = r > 0 ? r : 0; i < n; ++i) {
+        const uint64_t id = pend_tags_[i];
         auto it = conns_.find(id);
         if (it == conns_.end()) continue;
         it->second->waiting = false;
-        if (r == Engine::SUBMIT_BUSY)
+        if (r != 0)  // SUBMIT_BUSY, or a partial accept
           service_unavailable(it->second.get());
         else
           internal_error(it->second.get());

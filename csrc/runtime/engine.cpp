@@ -228,10 +228,15 @@ int Engine::submit_many(const double* X, int n, int nf, const uint64_t* tags, Si
   {
     std::lock_guard<std::mutex> lk(q_mu_);
     if (stopping_) return 0;
-    if ((int64_t)q_meta_.size() + n > (int64_t)cfg_.max_queue) {
+    // Backpressure: accept the prefix that still fits under max_queue, refuse the rest (the caller
+    // answers those 503). All-or-nothing would refuse a whole epoll round's worth of requests
+    // because of the last one.
+    const int64_t room = (int64_t)cfg_.max_queue - (int64_t)q_meta_.size();
+    if (room < n) {
       std::lock_guard<std::mutex> sl(st_mu_);
-      stats_.rejected += (uint64_t)n;
-      return SUBMIT_BUSY;
+      stats_.rejected += (uint64_t)(n - std::max<int64_t>(room, 0));
+      if (room <= 0) return SUBMIT_BUSY;
+      n = (int)room;
     }
     int32_t off = (int32_t)q_x_.size();
     q_x_.insert(q_x_.end(), X, X + (size_t)n * nf);

@@ -117,8 +117,10 @@ class Engine {
 
   // Thread-safe. Returns false if the engine is stopping or nf exceeds max_features.
   bool submit(const double* x, int nf, uint64_t tag, Sink* sink);
-  // n rows (row-major, nf features each) under one lock; returns n if accepted, 0 if the engine
-  // is stopping (or the request is malformed), SUBMIT_BUSY if the queue is over max_queue.
+  // n rows (row-major, nf features each) under one lock. Returns the number k of rows accepted:
+  // rows [0, k) are queued, rows [k, n) were refused because the queue reached max_queue
+  // (k < n only under backpressure); SUBMIT_BUSY if none fits, 0 if the engine is stopping (or
+  // the request is malformed).
   static constexpr int SUBMIT_BUSY = -1;
   int submit_many(const double* X, int n, int nf, const uint64_t* tags, Sink* sink);
   // Blocking convenience API (tests / bulk scoring through the batcher).
