@@ -164,6 +164,36 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("X"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"), py::arg("K"), py::arg("Z"),
       py::arg("stream") = 0);
+  m.def(
+      "gemm_rowstate",
+      [](uintptr_t X, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind, uintptr_t out, uintptr_t ws,
+         size_t ws_bytes, uintptr_t stream) {
+        launch_gemm_rowstate(ptr<void>(X), ptr<void>(W), ptr<float>(b), B, F, K, kind, ptr<void>(out), ptr<void>(ws),
+                             ws_bytes, stream_of(stream));
+      },
+      py::arg("X"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"), py::arg("K"), py::arg("kind"),
+      py::arg("out"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream") = 0);
+  m.def(
+      "merge_rowstates",
+      [](uintptr_t parts, int nparts, int64_t B, std::vector<int> offsets, int kind, uintptr_t out_idx,
+         uintptr_t out_p, uintptr_t stream) {
+        if ((int)offsets.size() != nparts) throw std::invalid_argument("merge_rowstates: one offset per shard");
+        if (nparts < 1 || nparts > ShardOffsets::MAX) throw std::invalid_argument("merge_rowstates: 1..64 shards");
+        ShardOffsets o{};
+        for (int i = 0; i < nparts; ++i) o.off[i] = offsets[i];
+        launch_merge_rowstates(ptr<void>(parts), nparts, B, o, kind, ptr<int32_t>(out_idx), ptr<float>(out_p),
+                               stream_of(stream));
+      },
+      py::arg("parts"), py::arg("nparts"), py::arg("B"), py::arg("offsets"), py::arg("kind"), py::arg("out_idx"),
+      py::arg("out_p"), py::arg("stream") = 0);
+  m.def(
+      "logits_epilogue",
+      [](uintptr_t Z, uintptr_t b, int64_t B, int K, int kind, uintptr_t out_idx, uintptr_t out_p, uintptr_t stream) {
+        launch_logits_epilogue(ptr<float>(Z), ptr<float>(b), B, K, kind, ptr<int32_t>(out_idx), ptr<float>(out_p),
+                               stream_of(stream));
+      },
+      py::arg("Z"), py::arg("b"), py::arg("B"), py::arg("K"), py::arg("kind"), py::arg("out_idx"), py::arg("out_p"),
+      py::arg("stream") = 0);
   m.def("train_binary_workspace", &train_binary_workspace);
   m.def("train_binary_set_max_blocks", &train_binary_set_max_blocks, py::arg("n") = 0);
   m.def(

@@ -46,6 +46,24 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
 void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B, int F, int K, float* Z,
                         hipStream_t stream);
 
+// Online softmax state per row for a class shard (gemm_softmax.hip MODE 4): out[B] float4 =
+// {max logit, sum exp(z - max) (OvR: sum sigmoid(z)), argmax (int bits, shard-local), 0}.
+// Workspace as gemm_softmax_workspace(B, K, F).
+void launch_gemm_rowstate(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind,
+                          void* out_state, void* workspace, size_t ws_bytes, hipStream_t stream);
+
+// ---- shard.hip: epilogues of sharded models ------------------------------------------------------
+struct ShardOffsets {
+  static constexpr int MAX = 64;
+  int off[MAX];  // first class index of each shard (rank order)
+};
+// parts: [nparts][B] float4 row states (MODE 4), merged in shard order -> (label, p_max).
+void launch_merge_rowstates(const void* parts, int nparts, int64_t B, const ShardOffsets& offs, int kind,
+                            int32_t* out_idx, float* out_p, hipStream_t stream);
+// Full logits Z[B, K] f32 (+ bias b[K]) -> (label, p_max) with the sklearn epilogue of `kind`.
+void launch_logits_epilogue(const float* Z, const float* b, int64_t B, int K, int kind, int32_t* out_idx, float* out_p,
+                            hipStream_t stream);
+
 // Multiclass training (gemm_softmax.hip, MODE 2 + 3). X_aug = [X | 1 | 0 x 7] bf16 with row
 // stride ldx = softmax_train_ldx(F) = F + 8 (the forward reads the first F columns; the ones
 // column makes the backward GEMM produce the intercept gradient); W: [K, F] bf16; b: [K] f32.

@@ -18,8 +18,8 @@
 //    reads per MFMA (B=262144: 230 -> 172 us);
 //  * small batches (B=1024 -> 16 row blocks) split the class range over gridDim.y so the launch
 //    fills the chip; the splits are merged IN THE SAME LAUNCH by the last-arriving block of each
-//    row block (agent-scope release fence + relaxed ticket, acquire fence in the reducer:
-//    Guideline 16), replacing v1's separate merge kernel (7.3 us of a 18.6 us total);
+//    row block (partials stored write-through (sc1) + relaxed ticket, acquire fence in the reducer:
+//    Guideline 16 R1), replacing v1's separate merge kernel (7.3 us of a 18.6 us total);
 //  * the epilogue is branch-free per element (kind is a template parameter; a split's partial
 //    last chunk is masked to -inf) and uses exp2/rcp; accumulators start at the bias.
 //
@@ -121,6 +121,7 @@ struct GemmArgs {
   uint16_t* G;             // MODE 3: bf16 [B, ldg]
   int64_t ldg;
   float2* rowstat;         // MODE 2 output / MODE 3 input: {lse, argmax bits}
+  float4* rowstate;        // MODE 4 output: {max, sum, argmax bits, 0} (class-sharded TP)
   float* stat_slabs;       // MODE 3: [gridDim.y * gridDim.x][2] = {loss_sum, n_correct}
 };
 
@@ -250,7 +251,8 @@ __device__ __forceinline__ void compute_chunk(const unsigned char* wb, const bf1
 }
 
 // KS = F/32 (exact), NT = 16-row N-tiles per wave, MODE: 0 = fused predict epilogue,
-// 1 = write logits, 2 = training row stats, 3 = training gradient (see header).
+// 1 = write logits, 2 = training row stats, 3 = training gradient (see header), 4 = raw online
+// softmax state per row (class-sharded TP, merged across ranks by shard.hip).
 template <int KS, int NT, int MODE, bool OVR>
 __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   const uint16_t* __restrict__ X = a.X;
@@ -401,7 +403,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
       a.stat_slabs[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2 + tid] = v;
     }
   }
-  if constexpr (MODE == 0 || MODE == 2) {
+  if constexpr (MODE == 0 || MODE == 2 || MODE == 4) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       RowState S = st[t];
@@ -417,6 +419,8 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
           if constexpr (MODE == 0) {
             a.out_idx[row] = st[t].bi;
             a.out_p[row] = ovr ? sigmoidf_(st[t].m) / st[t].s : 1.f / st[t].s;
+          } else if constexpr (MODE == 4) {
+            a.rowstate[row] = make_float4(st[t].m, st[t].s, __int_as_float(st[t].bi), 0.f);
           } else {
             a.rowstat[row] = make_float2(st[t].m + __logf(st[t].s), __int_as_float(st[t].bi));
           }
@@ -480,6 +484,8 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
         if constexpr (MODE == 0) {
           a.out_idx[row] = S.bi;
           a.out_p[row] = ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s;
+        } else if constexpr (MODE == 4) {
+          a.rowstate[row] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
         } else {
           a.rowstat[row] = make_float2(S.m + __logf(S.s), __int_as_float(S.bi));
         }
@@ -660,6 +666,24 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
     args.partials = reinterpret_cast<float4*>(static_cast<unsigned char*>(workspace) + COUNTER_BYTES);
   }
   launch_mode<0>(args, F, plan, stream);
+}
+
+void launch_gemm_rowstate(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind,
+                          void* out_state, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  if (B <= 0) return;
+  if (K < 1 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
+    throw std::invalid_argument("gemm_rowstate: multiclass kinds only");
+  const Plan plan = make_plan(B, K, F, false);
+  if (plan.splits > 1 && ws_bytes < gemm_softmax_workspace(B, K, F))
+    throw std::invalid_argument("gemm_rowstate: workspace too small (must be zero-initialised once)");
+  GemmArgs args = base_args(X, W, B, F, K, kind);
+  args.bias = b;
+  args.rowstate = static_cast<float4*>(out_state);
+  if (plan.splits > 1) {
+    args.counters = static_cast<unsigned int*>(workspace);
+    args.partials = reinterpret_cast<float4*>(static_cast<unsigned char*>(workspace) + COUNTER_BYTES);
+  }
+  launch_mode<4>(args, F, plan, stream);
 }
 
 void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B, int F, int K, float* Z,

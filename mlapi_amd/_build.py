@@ -29,6 +29,7 @@ SOURCES = [
     "kernels/gemm_softmax.hip",
     "kernels/train.hip",
     "kernels/pack.hip",
+    "kernels/shard.hip",
     "runtime/engine.cpp",
     "http/server.cpp",
     "http/loadgen.cpp",

@@ -82,6 +82,22 @@ def test_fake_comm_collectives(tmp_path):
             (tmp_path / f"OK_{r}").unlink()
 
 
+@pytest.mark.parametrize("world,comm", [(1, "torch"), (2, "torch"), (3, "fake")])
+def test_tensor_parallel_matches_oracle(tmp_path, world, comm):
+    """Class-sharded (TP over K) and feature-sharded (split-F) predict == the unsharded oracle."""
+    run(world, str(ROOT / "tests" / "dist" / "tensor_parallel.py"), {"OUT": str(tmp_path), "MLAPI_COMM": comm})
+    for r in range(world):
+        assert (tmp_path / f"TP_OK_{r}").read_text() == str(world)
+
+
+def test_shard_bounds():
+    from mlapi_amd.parallel.tensor_parallel import shard_bounds
+
+    assert shard_bounds(10, 3) == [(0, 4), (4, 7), (7, 10)]
+    assert shard_bounds(4, 4) == [(0, 1), (1, 2), (2, 3), (3, 4)]
+    assert shard_bounds(2, 3)[-1] == (2, 2)
+
+
 def test_dp_sgd_through_fake_comm(tmp_path):
     script = str(ROOT / "tests" / "dist" / "bcast_train.py")
     run(2, script, {"OUT": str(tmp_path), "MLAPI_COMM": "fake"})
