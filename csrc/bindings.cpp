@@ -248,6 +248,19 @@ PYBIND11_MODULE(_C, m) {
       py::arg("X_aug"), py::arg("ldx"), py::arg("W"), py::arg("b"), py::arg("y"), py::arg("B"), py::arg("F"),
       py::arg("K"), py::arg("kind"), py::arg("G"), py::arg("ldg"), py::arg("stats_out"), py::arg("ws"),
       py::arg("ws_bytes"), py::arg("stream") = 0);
+  m.def("softmax_grad_dw_supported", &softmax_grad_dw_supported);
+  m.def("softmax_grad_dw_force_row_groups", &softmax_grad_dw_force_row_groups, py::arg("n") = 0);
+  m.def("softmax_grad_dw_workspace", &softmax_grad_dw_workspace);
+  m.def(
+      "softmax_grad_dw",
+      [](uintptr_t X_aug, int64_t ldx, uintptr_t W, uintptr_t b, uintptr_t y, int64_t B, int F, int K, int kind,
+         uintptr_t dW_out, uintptr_t stats_out, uintptr_t ws, size_t ws_bytes, uintptr_t stream) {
+        launch_softmax_grad_dw(ptr<void>(X_aug), ldx, ptr<void>(W), ptr<float>(b), ptr<int32_t>(y), B, F, K, kind,
+                               ptr<float>(dW_out), ptr<float>(stats_out), ptr<void>(ws), ws_bytes, stream_of(stream));
+      },
+      py::arg("X_aug"), py::arg("ldx"), py::arg("W"), py::arg("b"), py::arg("y"), py::arg("B"), py::arg("F"),
+      py::arg("K"), py::arg("kind"), py::arg("dW_out"), py::arg("stats_out"), py::arg("ws"), py::arg("ws_bytes"),
+      py::arg("stream") = 0);
   m.def(
       "sgd_update_2d",
       [](uintptr_t params, uintptr_t grad, uintptr_t mom, int64_t rows, int cols, int pen_cols, float lr,

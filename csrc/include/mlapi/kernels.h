@@ -76,6 +76,20 @@ size_t softmax_train_workspace(int64_t B, int K, int F);
 void launch_softmax_train_grad(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
                                int64_t B, int F, int K, int kind, void* G, int64_t ldg, float* stats_out,
                                void* workspace, size_t ws_bytes, hipStream_t stream);
+// MODE 2 alone: rowstat_out[B] = {logsumexp (OvR: max + log sum sigmoid), argmax bits} per row.
+size_t softmax_rowstats_workspace(int64_t B, int K, int F);
+void launch_softmax_rowstats(const void* X_aug, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K,
+                             int kind, void* rowstat_out, void* workspace, size_t ws_bytes, hipStream_t stream);
+// Fused gradient (softmax_grad_dw.hip): row stats, then G and dW_aug = G^T X_aug in one MFMA kernel
+// (G never touches HBM), then the deterministic slab reductions. dW_out: [K, F + 8] f32 (column F
+// = intercept gradient, F+1.. = 0); stats_out = [loss_sum, n_correct]. F in {128, 256},
+// ldx = F + 8. Workspace: softmax_grad_dw_workspace(B, K, F) bytes, zeroed once.
+bool softmax_grad_dw_supported(int F);
+void softmax_grad_dw_force_row_groups(int n);  // benchmark hook (0 = automatic)
+size_t softmax_grad_dw_workspace(int64_t B, int K, int F);
+void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
+                            int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,
+                            size_t ws_bytes, hipStream_t stream);
 
 // ---- train kernels (train.hip) -----------------------------------------------------------------
 // Binary logistic regression, one pass over X: accumulates grad (F w-entries, 1 bias) and stats

@@ -643,6 +643,29 @@ void launch_softmax_train_grad(const void* X_aug, int64_t ldx, const void* W, co
   launch_reduce_slabs_f32(args.stat_slabs, (int)(L.plan.row_blocks * L.plan.splits), 2, stats_out, stream);
 }
 
+size_t softmax_rowstats_workspace(int64_t B, int K, int F) {
+  const Plan p = make_plan(B, K, F, true);
+  return (size_t)COUNTER_BYTES + (p.splits > 1 ? (size_t)p.splits * (size_t)B * sizeof(float4) : 0);
+}
+
+void launch_softmax_rowstats(const void* X_aug, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K,
+                             int kind, void* rowstat_out, void* workspace, size_t ws_bytes, hipStream_t stream) {
+  if (B <= 0) return;
+  if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
+    throw std::invalid_argument("softmax_rowstats: multiclass kinds only");
+  if (ldx < F || ldx % 8 != 0) throw std::invalid_argument("softmax_rowstats: ldx must be >= F and a multiple of 8");
+  const Plan plan = make_plan(B, K, F, true);
+  if (ws_bytes < softmax_rowstats_workspace(B, K, F))
+    throw std::invalid_argument("softmax_rowstats: workspace too small (zero it once)");
+  GemmArgs args = base_args(X_aug, W, B, F, K, kind);
+  args.ldx = ldx;
+  args.bias = b;
+  args.counters = static_cast<unsigned int*>(workspace);
+  args.partials = reinterpret_cast<float4*>(static_cast<unsigned char*>(workspace) + COUNTER_BYTES);
+  args.rowstat = static_cast<float2*>(rowstat_out);
+  launch_mode<2>(args, F, plan, stream);
+}
+
 size_t gemm_softmax_workspace(int64_t B, int K, int F) {
   (void)F;
   const Plan p = make_plan(B, K, F, false);

@@ -1,0 +1,454 @@
+// Fused multiclass training gradient: G = softmax(z) - onehot(y) (OvR: sigmoid(z) - onehot) and
+// dW_aug = G^T X_aug in ONE kernel, so the B x K gradient never goes through HBM (SURVEY 2.3 K6 at
+// BASELINE config 5 scale; reference: LogisticRegression.fit, `Logistic Regression.ipynb:34`).
+//
+// v1 of the training step wrote G (bf16, 131 MB at B=65536, K=1000) from the gemm_softmax MODE 3
+// tiles and ran dW = G^T X as a split-B hipBLASLt GEMM + a sum over the splits: 72 + 68 + 10 us of
+// a 213 us step (profiles/r1_session6/train_softmax_kernel_stats.csv). Here each block owns 64
+// classes (16 per wave) and a contiguous range of 64-row tiles:
+//
+//  1. logits, transposed: Z^T tile = X_tile W_c^T with X as the MFMA A operand (M = rows) and the
+//     wave's 16 W rows as B (N = classes; held in VGPRs for the whole kernel), accumulators
+//     initialised to the bias. The C layout leaves one CLASS per lane (col = lane & 15) and 4 rows
+//     per M-tile in its registers;
+//  2. epilogue in registers: with lse per row from the row-stats pass (gemm_softmax MODE 2),
+//     g = exp(z - lse) - [y == class], loss and the intercept gradient sum(g) accumulate per lane;
+//  3. dW_c += G X_tile: the 4 rows a lane holds in each of two M-tiles ARE the 8 k-values of a
+//     16x16x32 A operand (the order of k inside one MFMA is free as long as A and B agree), so G
+//     feeds the next MFMA straight from registers; the matching B operand (8 rows of one feature
+//     column) comes from the SAME LDS image of the X tile through ds_read_b64_tr_b16
+//     (cdna_hip_programming.md T10). 16 N-tiles of f32 accumulators = 64 VGPRs per lane.
+//
+// X tiles are double-buffered in LDS by global_load_lds DMA (lane-linear destination, swizzle
+// applied on the source address: image (b) of T10 - 256-byte rows, 16-byte chunk ch of row r at
+// ch ^ (((r & 3) << 2) | ((r >> 2) & 3)) - in 128-column sub-images). The M index -> row map of
+// the A operand (grp_row) makes both the row reads and the transposed reads conflict-free. Per-block dW partials go to
+// [row group][K][F_aug] slabs folded by the deterministic slab reduction (no atomics: DP replicas
+// and reruns stay bitwise identical); XCD-aware block order keeps the class groups that share a
+// row range on one XCD's L2.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <type_traits>
+#include <utility>
+
+#include "mlapi/common.h"
+#include "mlapi/kernels.h"
+
+namespace mlapi {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+typedef __attribute__((ext_vector_type(4))) short i16x4_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void glob_void_t;
+
+constexpr int ROWS = 64;                // rows per tile (4 M-tiles of 16)
+constexpr int CLASSES = 64;             // classes per block (16 per wave)
+constexpr int SUB_BYTES = ROWS * 256;   // one [64 rows][128 bf16] sub-image
+constexpr int META_BYTES = 1024;        // [64 lse] [64 argmax bits] [64 y] [256 B DMA pad]
+constexpr float LOG2E_F = 1.4426950408889634f;
+constexpr float LN2_F = 0.6931471805599453f;
+
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// ds_read_b64_tr_b16 at an immediate offset, invisible to hipcc's wait insertion (see step 3)
+template <int OFF>
+__device__ __forceinline__ i16x4_t tr_read(uint32_t addr) {
+  i16x4_t v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+// s_waitcnt lgkmcnt(N) that orders every later use of a and b after it
+template <int N, typename A, typename B>
+__device__ __forceinline__ void lgkm_wait(A& a, B& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
+}
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+__device__ __forceinline__ int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+// byte offset of element column c (a multiple of 4) of tile row r
+__device__ __forceinline__ int img_off(int r, int c) {
+  return (c >> 7) * SUB_BYTES + r * 256 + ((((c >> 3) & 15) ^ swz(r)) << 4) + ((c & 7) << 1);
+}
+// First tile row of lane group g's 4 C-layout rows inside a 16-row M-tile. Quad q of M indices (i >> 2) maps to tile rows 4 * QROW[q] .. +3 with QROW = {0, 2, 3, 1}: the
+// 16-lane groups of the ds_read_b128 A-operand read ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...)
+// then hit four different swizzle classes (conflict-free), and each 32-lane half of the transposed
+// B-operand read takes two blocks 8 rows apart (conflict-free per T10).
+__device__ __forceinline__ int grp_row(int g) { return ((0x1320 >> (4 * g)) & 3) << 2; }
+// A-operand M index -> tile row (the same map)
+__device__ __forceinline__ int m_row(int i) { return (i & 3) | grp_row(i >> 2); }
+
+struct GradDwArgs {
+  const uint16_t* X;  // X_aug [B, ldx] bf16 (first F columns read; column F is the ones column)
+  int64_t ldx;
+  const uint16_t* W;  // [K, F] bf16
+  const float* bias;  // [K]
+  const int32_t* y;   // [B]
+  const float2* rowstat;  // [B] {lse, argmax bits} from the row-stats pass
+  int64_t B;
+  int K;
+  int tiles;            // ceil(B / 64)
+  int tiles_per_group;  // row-group length in tiles
+  int row_groups;
+  int class_groups;
+  int ldw;              // F_aug: slab row stride
+  float* dw_slabs;      // [row_groups][K][ldw]
+  float* stat_slabs;    // [row_groups * class_groups][2] = {loss_sum, n_correct}
+};
+
+template <int KS, bool OVR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void softmax_grad_dw_kernel(GradDwArgs a) {
+  constexpr int F_ = KS * 32;
+  constexpr int X_BYTES = (F_ / 128) * SUB_BYTES;
+  constexpr int BUF_BYTES = X_BYTES + META_BYTES;
+  constexpr int NT = F_ / 16;  // dW N-tiles (features)
+  static_assert(F_ % 128 == 0, "sub-images are 128 columns wide");
+  // ALL LDS in one __shared__ object: a second one (even a small reduction array) makes hipcc wait
+  // vmcnt(0) before the first ds_read of every tile, draining the in-flight DMA (guide 4(a)).
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF_BYTES];
+  float* const red = reinterpret_cast<float*>(smem);  // stats reduction, after the last tile
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: scalar descriptors
+  const int col = lane & 15;
+  const int g = lane >> 4;
+  const int64_t B = a.B;
+  const int K = a.K;
+
+  // XCD-aware block order: hardware block id b runs on XCD b % 8; logical id L puts the class
+  // groups of one row range on one XCD (its L2 then serves the 16x reuse of every X tile).
+  const int nblk = a.row_groups * a.class_groups;
+  int L = blockIdx.x;
+  if (nblk % 8 == 0) L = (blockIdx.x & 7) * (nblk >> 3) + (blockIdx.x >> 3);
+  const int rg = L / a.class_groups;
+  const int cg = L % a.class_groups;
+  const int t_begin = rg * a.tiles_per_group;
+  const int t_end = min(a.tiles, t_begin + a.tiles_per_group);
+
+  const int cls = cg * CLASSES + wave * 16 + col;  // this lane's class in steps 1-2
+  const bool cls_ok = cls < K;
+  const int cls_c = min(cls, K - 1);
+
+  // W rows of the wave's 16 classes: the B operand of every logits MFMA, resident in VGPRs.
+  bf16x8_t wf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    wf[ks] = *reinterpret_cast<const bf16x8_t*>(a.W + (int64_t)cls_c * F_ + ks * 32 + g * 8);
+  // padded classes: logits -1e30 (finite: 0 * z stays 0), so p = 0, g = 0 and loss = 0 with no
+  // per-element class check
+  const float bv = cls_ok ? a.bias[cls_c] : -1e30f;
+
+  f32x4_t acc[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) acc[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // intercept gradient sum_rows g = G^T (ones column of X_aug): one more MFMA per 32 rows with a
+  // constant B operand (column 0 = 1, the rest 0) instead of a VALU add per element
+  f32x4_t acc_db = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const bf16x8_t ones_b = col == 0 ? bf16x8_t{1, 1, 1, 1, 1, 1, 1, 1} : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  float loss = 0.f, lz = 0.f, correct = 0.f;
+  const bool row_wave = cg == 0 && wave == 0;  // one wave per row range: correct count (+ sum lse)
+
+  // ---- tile DMA: KS 16-byte pieces per thread + one dword of row metadata per lane, through
+  // buffer_load ... lds with per-tile scalar descriptors (base = the tile's first row, range = its
+  // valid rows): rows past B fail the range check instead of being clamped per lane, and the
+  // per-lane offsets are tile-invariant (piece i: row (tid >> 4) + 16 (i & 3), sub-image i >> 2).
+  uint32_t vo[4];
+  {
+    const int r = tid >> 4;
+    const int c = ((tid & 15) ^ swz(r)) << 3;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) vo[k] = (uint32_t)(((r + 16 * k) * a.ldx + c) * 2);
+  }
+  const uint32_t mvo = wave < 2 ? (uint32_t)(lane * 8 + wave * 4) : (uint32_t)(lane * 4);
+#define MLAPI_DMA_TILE(T, BUF)                                                                          \
+  {                                                                                                     \
+    const int64_t row0 = (int64_t)(T) * ROWS;                                                           \
+    const int nrows = (int)min<int64_t>(ROWS, B - row0);                                                \
+    unsigned char* dst = smem + (BUF) * BUF_BYTES;                                                      \
+    const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)(a.X + row0 * a.ldx), 0,                 \
+                                                       nrows * (int)a.ldx * 2, 0x00020000);             \
+    _Pragma("unroll") for (int i = 0; i < KS; ++i)                                                      \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsx, (lds_void_t*)(dst + (i * 256 + wave * 64) * 16), 16, \
+                                               vo[i & 3], (i >> 2) * 256, 0, 0);                        \
+    const auto rsm = wave < 2 ? __builtin_amdgcn_make_buffer_rsrc((void*)(a.rowstat + row0), 0, nrows * 8, \
+                                                                  0x00020000)                           \
+                              : __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + row0), 0, nrows * 4,    \
+                                                                  0x00020000);                          \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsm, (lds_void_t*)(dst + X_BYTES + wave * 256), 4, mvo, 0, 0, 0); \
+  }
+#define MLAPI_RAW_BARRIER()      \
+  asm volatile("" ::: "memory"); \
+  __builtin_amdgcn_s_barrier();  \
+  asm volatile("" ::: "memory");
+  constexpr int kWaitTile = ((KS + 1) & 15) | (7 << 4) | (15 << 8) | (((KS + 1) >> 4) << 14);
+  constexpr int kWaitAll = (7 << 4) | (15 << 8);
+
+  // Rows past B are never DMA'd; if this block owns the batch's ragged last tile, zero the LDS once
+  // so those rows hold zeros (not stale non-finite bits) where 0-gradients multiply them.
+  if ((int64_t)t_end * ROWS > B) {
+    for (int o = tid * 16; o < 2 * BUF_BYTES; o += 256 * 16) *reinterpret_cast<int4*>(smem + o) = int4{0, 0, 0, 0};
+    __syncthreads();
+  }
+  int buf = 0;
+  MLAPI_DMA_TILE(t_begin, 0)
+  if (t_begin + 1 < t_end) {
+    MLAPI_DMA_TILE(t_begin + 1, 1)
+    __builtin_amdgcn_s_waitcnt(kWaitTile);  // W, bias and tile 0 landed; tile 1 may still fly
+  } else {
+    __builtin_amdgcn_s_waitcnt(kWaitAll);
+  }
+  MLAPI_RAW_BARRIER()
+  for (int t = t_begin; t < t_end; ++t) {
+    const unsigned char* xb = smem + buf * BUF_BYTES;
+    const int64_t row0 = (int64_t)t * ROWS;
+
+    // 1. Z^T tile (rows x the wave's 16 classes), bias-initialised
+    f32x4_t z[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) z[mt] = f32x4_t{bv, bv, bv, bv};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const bf16x8_t xa = *reinterpret_cast<const bf16x8_t*>(xb + img_off(mt * 16 + m_row(col), ks * 32 + g * 8));
+        z[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wf[ks], z[mt], 0, 0, 0);
+      }
+    }
+
+    // 2. gradient in registers: lane holds rows mt*16 + grp_row(g) + r of class `cls`. Only the
+    //    last tile of the batch has padded rows (uniform branch); padded classes are -inf logits.
+    const int rows_left = (int)min<int64_t>(ROWS, B - row0);
+    // Row metadata (LDS after the X image: [64 lse][64 argmax bits][64 y]) through inline-asm
+    // ds_reads: hipcc cannot disambiguate an ordinary LDS read of this region from the DMA of tile
+    // t+2 still in flight and would wait vmcnt(0) before it, draining the pipeline every tile. Each
+    // counted wait takes the results as in-out operands, so every use is ordered after the data.
+    const uint32_t mb = lds_off(xb + X_BYTES);
+    bf16x8_t ga[2];
+    auto epilogue = [&](auto partial) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const uint32_t rb = mt * 16 + grp_row(g);
+        i32x4_t y4, l4;
+        asm volatile("ds_read_b128 %0, %1 offset:512" : "=v"(y4) : "v"(mb + rb * 4));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(l4) : "v"(mb + rb * 4));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(y4), "+v"(l4));
+        const int yv[4] = {y4[0], y4[1], y4[2], y4[3]};
+        const float lse[4] = {__int_as_float(l4[0]), __int_as_float(l4[1]), __int_as_float(l4[2]),
+                              __int_as_float(l4[3])};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool hot = cls == yv[r];
+          const float zz = z[mt][r];
+          float pr;
+          if constexpr (OVR) {
+            const float e = __builtin_amdgcn_exp2f(-fabsf(zz) * LOG2E_F);  // exp(-|z|)
+            const float re = __builtin_amdgcn_rcpf(1.f + e);
+            pr = zz >= 0.f ? re : e * re;
+            const float l = fmaxf(zz, 0.f) + __builtin_amdgcn_logf(1.f + e) * LN2_F;
+            loss += decltype(partial)::value ? (rb + r < rows_left ? l : 0.f) : l;
+          } else {
+            pr = __builtin_amdgcn_exp2f((zz - lse[r]) * LOG2E_F);
+          }
+          // loss = sum(lse) - sum(z_y) (multinomial); OvR: sum(softplus terms) - sum(z_y)
+          float msk = hot ? 1.f : 0.f;
+          float gv = pr - msk;
+          if constexpr (decltype(partial)::value) {
+            const bool ok = rb + r < (uint32_t)rows_left;
+            gv = ok ? gv : 0.f;
+            msk = ok ? msk : 0.f;
+          }
+          lz = fmaf(msk, zz, lz);
+          ga[mt >> 1][(mt & 1) * 4 + r] = (__bf16)gv;
+        }
+      }
+    };
+    if (rows_left == ROWS)
+      epilogue(std::false_type{});
+    else
+      epilogue(std::true_type{});
+    if (row_wave) {  // one row per lane: argmax == y, and sum lse
+      int yl, al, ll;
+      asm volatile("ds_read_b32 %0, %1 offset:512" : "=v"(yl) : "v"(mb + lane * 4));
+      asm volatile("ds_read_b32 %0, %1 offset:256" : "=v"(al) : "v"(mb + lane * 4));
+      asm volatile("ds_read_b32 %0, %1" : "=v"(ll) : "v"(mb + lane * 4));
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(yl), "+v"(al), "+v"(ll));
+      if (lane < rows_left) {
+        correct += al == yl ? 1.f : 0.f;
+        if constexpr (!OVR) loss += __int_as_float(ll);
+      }
+    }
+
+    // 3. dW_c += G X_tile: B operand = 8 rows of one feature column via two transposed reads
+    //    (lane 4q+p of group g addresses row base + q, columns n*16 + 4p .. +3). Inline asm with
+    //    counted waits (two (j, n) steps in flight): hipcc treats the ds_read_tr builtin as
+    //    aliasing the tile DMA in flight and would wait vmcnt(0) before the first one. Row base
+    //    + 16 (hi), + 32 (j) and the second 128-column sub-image (n >= 8) keep the swizzle, so they
+    //    are immediate offsets from 8 per-lane bases (one per n & 7).
+    {
+      uint32_t trb[8];
+      const uint32_t xo = lds_off(xb);
+#pragma unroll
+      for (int n = 0; n < 8; ++n) trb[n] = xo + img_off(grp_row(g) + (col >> 2), n * 16 + 4 * (col & 3));
+      i16x4_t tl[2 * NT], th[2 * NT];
+      auto issue = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        constexpr int off = (i / NT) * 32 * 256 + ((i % NT) >> 3) * SUB_BYTES;
+        tl[i] = tr_read<off>(trb[i & 7]);
+        th[i] = tr_read<off + 16 * 256>(trb[i & 7]);
+      };
+      issue(std::integral_constant<int, 0>{});
+      issue(std::integral_constant<int, 1>{});
+      static_for<2 * NT>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i + 2 < 2 * NT) issue(std::integral_constant<int, i + 2>{});
+        constexpr int pending = i + 2 < 2 * NT ? 4 : (i + 1 < 2 * NT ? 2 : 0);
+        lgkm_wait<pending>(tl[i], th[i]);
+        const bf16x8_t xbf = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, tl[i]),
+                                                     __builtin_bit_cast(bf16x4_t, th[i]), 0, 1, 2, 3, 4, 5, 6, 7);
+        acc[i % NT] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[i / NT], xbf, acc[i % NT], 0, 0, 0);
+        if constexpr (i % NT == NT - 1)
+          acc_db = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[i / NT], ones_b, acc_db, 0, 0, 0);
+      });
+    }
+
+    if (t + 2 < t_end) {
+      MLAPI_RAW_BARRIER()  // every wave is done reading `buf`
+      MLAPI_DMA_TILE(t + 2, buf)
+      __builtin_amdgcn_s_waitcnt(kWaitTile);  // tile t+1 landed, t+2 flies
+    } else {
+      __builtin_amdgcn_s_waitcnt(kWaitAll);
+    }
+    MLAPI_RAW_BARRIER()
+    buf ^= 1;
+  }
+#undef MLAPI_RAW_BARRIER
+#undef MLAPI_DMA_TILE
+
+  // ---- dW partial of this row group: lane holds dW[class base + 4g + r][n*16 + col]
+  float* slab = a.dw_slabs + (int64_t)rg * K * a.ldw;
+  const int cbase = cg * CLASSES + wave * 16 + 4 * g;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (cbase + r < K) {
+      float* dst = slab + (int64_t)(cbase + r) * a.ldw + col;
+#pragma unroll
+      for (int n = 0; n < NT; ++n) dst[n * 16] = acc[n][r];
+    }
+  }
+  // intercept gradient (column F) and the zero pad columns F+1 .. ldw-1: lane col of acc_db holds
+  // G^T e_col, i.e. sum(g) for col 0 and 0 otherwise
+  if (col < a.ldw - F_) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (cbase + r < K) slab[(int64_t)(cbase + r) * a.ldw + F_ + col] = acc_db[r];
+  }
+  // ---- [loss, correct] of the block (deterministic tree); padded rows/classes have z_y terms of 0
+  loss -= lz;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    loss += __shfl_xor(loss, off, 64);
+    correct += __shfl_xor(correct, off, 64);
+  }
+  __syncthreads();  // every wave is done reading the last tile before `red` overwrites it
+  if (lane == 0) {
+    red[wave * 2] = loss;
+    red[wave * 2 + 1] = correct;
+  }
+  __syncthreads();
+  if (tid < 2) a.stat_slabs[(int64_t)L * 2 + tid] = red[tid] + red[2 + tid] + red[4 + tid] + red[6 + tid];
+}
+
+struct GdwLayout {
+  int tiles, row_groups, tiles_per_group, class_groups;
+  size_t rowstat_off, dw_off, stat_off, total;
+};
+
+int g_force_row_groups = 0;  // benchmark hook (softmax_grad_dw_force_row_groups)
+
+GdwLayout gdw_layout(int64_t B, int K, int F) {
+  GdwLayout L;
+  L.tiles = (int)((B + ROWS - 1) / ROWS);
+  L.class_groups = (K + CLASSES - 1) / CLASSES;
+  // ~2 blocks per CU (512) unless the rows run out; every row group gets >= 1 tile
+  int want = g_force_row_groups > 0 ? g_force_row_groups : (512 + L.class_groups - 1) / L.class_groups;
+  want = want < 1 ? 1 : (want > L.tiles ? L.tiles : want);
+  L.tiles_per_group = (L.tiles + want - 1) / want;
+  L.row_groups = (L.tiles + L.tiles_per_group - 1) / L.tiles_per_group;
+  auto align = [](size_t v) { return (v + 255) & ~size_t(255); };
+  L.rowstat_off = align(softmax_rowstats_workspace(B, K, F));
+  L.dw_off = align(L.rowstat_off + (size_t)B * sizeof(float2));
+  L.stat_off = align(L.dw_off + (size_t)L.row_groups * K * (F + 8) * sizeof(float));
+  L.total = align(L.stat_off + (size_t)L.row_groups * L.class_groups * 2 * sizeof(float));
+  return L;
+}
+
+}  // namespace
+
+bool softmax_grad_dw_supported(int F) { return F == 128 || F == 256; }
+
+void softmax_grad_dw_force_row_groups(int n) { g_force_row_groups = n; }
+
+size_t softmax_grad_dw_workspace(int64_t B, int K, int F) { return gdw_layout(B, K, F).total; }
+
+void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
+                            int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,
+                            size_t ws_bytes, hipStream_t stream) {
+  if (B <= 0) return;
+  if (!softmax_grad_dw_supported(F)) throw std::invalid_argument("softmax_grad_dw: F must be 128 or 256");
+  if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
+    throw std::invalid_argument("softmax_grad_dw: multiclass kinds only");
+  if (ldx != F + 8) throw std::invalid_argument("softmax_grad_dw: X_aug row stride must be F + 8");
+  if (reinterpret_cast<uintptr_t>(X_aug) % 16 != 0 || reinterpret_cast<uintptr_t>(W) % 16 != 0)
+    throw std::invalid_argument("softmax_grad_dw: X_aug and W must be 16-byte aligned");
+  const GdwLayout L = gdw_layout(B, K, F);
+  if (ws_bytes < L.total) throw std::invalid_argument("softmax_grad_dw: workspace too small (zero it once)");
+  unsigned char* ws = static_cast<unsigned char*>(workspace);
+  float2* rowstat = reinterpret_cast<float2*>(ws + L.rowstat_off);
+  launch_softmax_rowstats(X_aug, ldx, W, b, B, F, K, kind, rowstat, ws, L.rowstat_off, stream);
+  GradDwArgs args{};
+  args.X = static_cast<const uint16_t*>(X_aug);
+  args.ldx = ldx;
+  args.W = static_cast<const uint16_t*>(W);
+  args.bias = b;
+  args.y = y;
+  args.rowstat = rowstat;
+  args.B = B;
+  args.K = K;
+  args.tiles = L.tiles;
+  args.tiles_per_group = L.tiles_per_group;
+  args.row_groups = L.row_groups;
+  args.class_groups = L.class_groups;
+  args.ldw = F + 8;
+  args.dw_slabs = reinterpret_cast<float*>(ws + L.dw_off);
+  args.stat_slabs = reinterpret_cast<float*>(ws + L.stat_off);
+  const dim3 grid((unsigned)(L.row_groups * L.class_groups));
+  const bool ovr = kind == KIND_OVR;
+  if (F == 128) {
+    if (ovr)
+      hipLaunchKernelGGL((softmax_grad_dw_kernel<4, true>), grid, dim3(256), 0, stream, args);
+    else
+      hipLaunchKernelGGL((softmax_grad_dw_kernel<4, false>), grid, dim3(256), 0, stream, args);
+  } else {
+    if (ovr)
+      hipLaunchKernelGGL((softmax_grad_dw_kernel<8, true>), grid, dim3(256), 0, stream, args);
+    else
+      hipLaunchKernelGGL((softmax_grad_dw_kernel<8, false>), grid, dim3(256), 0, stream, args);
+  }
+  MLAPI_HIP_CHECK(hipGetLastError());
+  launch_reduce_slabs_f32(args.dw_slabs, L.row_groups, K * (F + 8), dW_out, stream);
+  launch_reduce_slabs_f32(args.stat_slabs, L.row_groups * L.class_groups, 2, stats_out, stream);
+}
+
+}  // namespace mlapi

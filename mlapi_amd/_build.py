@@ -30,6 +30,7 @@ SOURCES = [
     "kernels/train.hip",
     "kernels/pack.hip",
     "kernels/shard.hip",
+    "kernels/softmax_grad_dw.hip",
     "runtime/engine.cpp",
     "http/server.cpp",
     "http/loadgen.cpp",

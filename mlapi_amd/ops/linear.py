@@ -12,6 +12,7 @@ Dispatch for ``predict`` (the reference's ``predict`` + ``predict_proba().max()`
 """
 from __future__ import annotations
 
+import os
 from typing import Tuple
 
 import torch
@@ -205,13 +206,26 @@ def augment_weights(W: torch.Tensor, b: torch.Tensor, F_aug: int) -> torch.Tenso
 class SoftmaxTrainBuffers:
     """Persistent per-batch-size buffers of the multiclass gradient (G, workspace, stats)."""
 
-    def __init__(self, B: int, K: int, F: int, device):
+    def __init__(self, B: int, K: int, F: int, device, dw_path: str = None):
         self.B, self.K, self.F = B, K, F
+        self.stats = torch.zeros(2, dtype=torch.float32, device=device)
+        self.part = None
+        # "fused": row stats + one kernel that forms G in registers and accumulates G^T X_aug
+        # (softmax_grad_dw.hip; G never reaches HBM). "gemm": G (bf16) + hipBLASLt dW GEMM.
+        path = dw_path or os.environ.get("MLAPI_SOFTMAX_DW", "fused")
+        if path not in ("fused", "gemm"):
+            raise ValueError(f"MLAPI_SOFTMAX_DW / dw_path must be 'fused' or 'gemm', got {path!r}")
+        self.fused = path == "fused" and bool(C().softmax_grad_dw_supported(F))
+        if self.fused:
+            self.G = None
+            self.ldg = 0
+            self.splits = 1
+            self.ws = torch.zeros(C().softmax_grad_dw_workspace(B, K, F), dtype=torch.uint8, device=device)
+            return
         self.ldg = (K + 7) // 8 * 8
         # rows padded to whole 128-row blocks: the gradient kernel stores without a row guard
         self.G = torch.empty((B + 127) // 128 * 128, self.ldg, dtype=torch.bfloat16, device=device)
         self.ws = torch.zeros(C().softmax_train_workspace(B, K, F), dtype=torch.uint8, device=device)
-        self.stats = torch.zeros(2, dtype=torch.float32, device=device)
         # dW split over the batch: hipBLASLt tiles only the small [K, F_aug] output, so one mm runs
         # ~48 workgroups for K=1000 (245 us at B=65536); S batched slices of ~2048 rows + a sum
         # fill the chip (72 us at S=32: tools/softmax_train_sweep.py, profiles/r1_softmax_train).
@@ -219,7 +233,6 @@ class SoftmaxTrainBuffers:
         while S < 64 and B % (2 * S) == 0 and B // (2 * S) >= 2048:
             S *= 2
         self.splits = S
-        self.part = None
 
 
 def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y: torch.Tensor, kind: int,
@@ -229,8 +242,11 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
 
     X_aug: [B, F + 8] bf16 from :func:`augment_features`; W: [K, F] bf16; b: [K] f32; y: int32.
     Returns (dW_aug f32 [K, F + 8] with the intercept gradient in column F, stats f32
-    [loss_sum, n_correct]). Two MFMA launches produce G = P - Y in bf16 (plus loss/correct);
-    dW_aug = G^T X_aug is one hipBLASLt GEMM (batched over B slices) with f32 output.
+    [loss_sum, n_correct]). Fused path (F in {128, 256}, the default): a row-stats launch, then one
+    MFMA kernel that forms G = P - Y in registers and accumulates dW_aug = G^T X_aug from the same
+    LDS tile, plus the deterministic slab sums. GEMM path (other widths, or MLAPI_SOFTMAX_DW=gemm):
+    two MFMA launches write G in bf16, and dW_aug = G^T X_aug is one hipBLASLt GEMM (batched over B
+    slices) with f32 output.
     """
     _check(X_aug, W, b, y)
     if X_aug.dtype != torch.bfloat16 or W.dtype != torch.bfloat16 or b.dtype != torch.float32 \
@@ -243,11 +259,17 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
     if bufs is None or bufs.B != B or bufs.K != K or bufs.F != F:
         bufs = SoftmaxTrainBuffers(B, K, F, X_aug.device)
     stats = bufs.stats if stats_out is None else stats_out
+    if dW_out is None:
+        dW_out = torch.empty(K, F_aug, dtype=torch.float32, device=X_aug.device)
+    if bufs.fused:
+        if not dW_out.is_contiguous() or dW_out.shape != (K, F_aug) or dW_out.dtype != torch.float32:
+            raise ValueError("softmax_train_grad: dW_out must be a contiguous f32 [K, F + 8] tensor")
+        C().softmax_grad_dw(X_aug.data_ptr(), F_aug, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
+                            dW_out.data_ptr(), stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(), _stream())
+        return dW_out, stats
     C().softmax_train_grad(X_aug.data_ptr(), F_aug, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
                            bufs.G.data_ptr(), bufs.ldg, stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(),
                            _stream())
-    if dW_out is None:
-        dW_out = torch.empty(K, F_aug, dtype=torch.float32, device=X_aug.device)
     S = bufs.splits
     if S == 1:
         torch.mm(bufs.G[:B, :K].t(), X_aug, out_dtype=torch.float32, out=dW_out)

@@ -4,9 +4,11 @@ The reference fits its 3-class Iris model once with sklearn's full-batch L-BFGS
 (`Logistic Regression.ipynb:33-34`); :mod:`mlapi_amd.train.lbfgs` reproduces that fit.
 This module is the scale-out counterpart (BASELINE config 5 with K classes): per step and rank
 
-  1. ``softmax_train_grad``: two MFMA launches over the rank's shard -> G = P - Y (bf16) with the
-     loss / correct sums, then dW_aug = G^T X_aug as one hipBLASLt GEMM (f32 out). X_aug carries a
-     ones column (X_aug = [X | 1 | 0 x 7]), so that GEMM also yields the intercept gradient;
+  1. ``softmax_train_grad``: a row-stats MFMA launch (logsumexp / argmax per row), then one fused
+     MFMA kernel that forms G = P - Y in registers and accumulates dW_aug = G^T X_aug from the same
+     LDS tile of X (G never reaches HBM), with the loss / correct sums. X_aug carries a ones column
+     (X_aug = [X | 1 | 0 x 7]), so dW_aug also holds the intercept gradient. Widths other than
+     F = 128/256 write G (bf16) and run dW as a hipBLASLt GEMM;
   2. one RCCL all-reduce of the fused buffer [dW_aug | loss_sum | n_correct] (C2 + C3);
   3. ``sgd_update_2d``: W_aug = [W | b] -= lr * (g / N_global + l2 * W) with the intercept
      unpenalized, writing the bf16 W and f32 b the next forward reads in the same pass.

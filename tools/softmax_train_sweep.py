@@ -1,5 +1,6 @@
 """Time the multiclass training step's pieces (K=1000, F=256, B=65536): MFMA row-stat/grad
-launches at NT 1/2 and the dW GEMM as one hipBLASLt mm vs a batched split-B bmm + sum."""
+launches at NT 1/2 and the dW GEMM as one hipBLASLt mm vs a batched split-B bmm + sum (the
+"gemm" dW path), and the fused G + dW kernel (softmax_grad_dw.hip) over forced row-group counts."""
 import json
 import sys
 
@@ -32,7 +33,7 @@ y = torch.randint(0, K, (B,), device=dev, dtype=torch.int32)
 res = {}
 for nt in (1, 2):
     C().gemm_softmax_force_plan(nt, 0)
-    bufs = ops.SoftmaxTrainBuffers(B, K, F, dev)
+    bufs = ops.SoftmaxTrainBuffers(B, K, F, dev, dw_path="gemm")
     st = torch.zeros(2, device=dev)
     t = timeit(lambda: C().softmax_train_grad(X.data_ptr(), Fa, W.data_ptr(), bias.data_ptr(), y.data_ptr(), B, F, K, 2,
                                               bufs.G.data_ptr(), bufs.ldg, st.data_ptr(), bufs.ws.data_ptr(),
@@ -54,6 +55,18 @@ for S in (2, 4, 8, 16, 32, 64):
 
     res[f"dW_bmm_S{S}_us"] = timeit(f)
     res[f"dW_bmm_S{S}_maxdiff"] = (out - ref).abs().max().item()
+# fused path: rowstats + G/dW kernel + slab sums, whole call
+stf = torch.zeros(2, device=dev)
+for groups in (0, 8, 16, 32, 64, 128):
+    C().softmax_grad_dw_force_row_groups(groups)
+    fb = ops.SoftmaxTrainBuffers(B, K, F, dev, dw_path="fused")
+    res[f"fused_groups{groups}_us"] = timeit(lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=fb, dW_out=out,
+                                                                            stats_out=stf))
+    res[f"fused_groups{groups}_maxdiff"] = (out - ref).abs().max().item()
+C().softmax_grad_dw_force_row_groups(0)
+gb = ops.SoftmaxTrainBuffers(B, K, F, dev, dw_path="gemm")
+res["gemm_path_total_us"] = timeit(lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=gb, dW_out=out, stats_out=stf))
+res["dW_ref_absmax"] = ref.abs().max().item()
 for k, v in res.items():
     print(f"{k:28s} {v:10.3f}")
 json.dump(res, open("gpurun_out/softmax_train_sweep.json", "w"), indent=1)
