@@ -370,6 +370,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (tid < 2) a.stat_slabs[(int64_t)L * 2 + tid] = red[tid] + red[2 + tid] + red[4 + tid] + red[6 + tid];
 }
 
+// Slab sums in one launch: blocks 0 .. nb-1 fold the [row group][K * F_aug] dW slabs, one float4
+// column per thread over all slabs in a fixed order (coalesced 16-B loads, 4 in flight); the last
+// block folds the per-block [loss, correct] pairs with a fixed tree. Deterministic: no atomics.
+__global__ __launch_bounds__(256) void gdw_reduce_kernel(const f32x4_t* __restrict__ slabs, int nslabs, int width4,
+                                                         f32x4_t* __restrict__ out, const float* __restrict__ stat_slabs,
+                                                         int nstat, float* __restrict__ stats_out) {
+  if (blockIdx.x == gridDim.x - 1) {
+    float l = 0.f, c = 0.f;
+    for (int i = threadIdx.x; i < nstat; i += 256) {
+      l += stat_slabs[2 * i];
+      c += stat_slabs[2 * i + 1];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      l += __shfl_xor(l, off, 64);
+      c += __shfl_xor(c, off, 64);
+    }
+    __shared__ float red[8];
+    if ((threadIdx.x & 63) == 0) {
+      red[(threadIdx.x >> 6) * 2] = l;
+      red[(threadIdx.x >> 6) * 2 + 1] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2)
+      stats_out[threadIdx.x] = (red[threadIdx.x] + red[2 + threadIdx.x]) + (red[4 + threadIdx.x] + red[6 + threadIdx.x]);
+    return;
+  }
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= width4) return;
+  f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+  int i = 0;
+  for (; i + 4 <= nslabs; i += 4) {
+    f32x4_t v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(slabs + (int64_t)(i + u) * width4 + j);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += v[u];
+  }
+  for (; i < nslabs; ++i) {
+    s += __builtin_nontemporal_load(slabs + (int64_t)i * width4 + j);
+  }
+  out[j] = s;
+}
+
 struct GdwLayout {
   int tiles, row_groups, tiles_per_group, class_groups;
   size_t rowstat_off, dw_off, stat_off, total;
@@ -447,8 +491,16 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
       hipLaunchKernelGGL((softmax_grad_dw_kernel<8, false>), grid, dim3(256), 0, stream, args);
   }
   MLAPI_HIP_CHECK(hipGetLastError());
-  launch_reduce_slabs_f32(args.dw_slabs, L.row_groups, K * (F + 8), dW_out, stream);
-  launch_reduce_slabs_f32(args.stat_slabs, L.row_groups * L.class_groups, 2, stats_out, stream);
+  if (reinterpret_cast<uintptr_t>(dW_out) % 16 == 0) {
+    const int width4 = K * (F + 8) / 4;
+    hipLaunchKernelGGL(gdw_reduce_kernel, dim3((unsigned)((width4 + 255) / 256 + 1)), dim3(256), 0, stream,
+                       reinterpret_cast<const f32x4_t*>(args.dw_slabs), L.row_groups, width4,
+                       reinterpret_cast<f32x4_t*>(dW_out), args.stat_slabs, L.row_groups * L.class_groups, stats_out);
+    MLAPI_HIP_CHECK(hipGetLastError());
+  } else {
+    launch_reduce_slabs_f32(args.dw_slabs, L.row_groups, K * (F + 8), dW_out, stream);
+    launch_reduce_slabs_f32(args.stat_slabs, L.row_groups * L.class_groups, 2, stats_out, stream);
+  }
 }
 
 }  // namespace mlapi
