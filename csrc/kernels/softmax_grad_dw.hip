@@ -46,8 +46,11 @@ typedef __attribute__((ext_vector_type(4))) int i32x4_t;
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void glob_void_t;
 
+#ifndef MLAPI_GDW_EXP
+#define MLAPI_GDW_EXP 0  // experiment mask for tools/gdw_bench.hip (1 no epilogue math, 2 no dW MFMA,
+#endif                   // 4 no logits MFMA, 8 no dW phase, 16 no per-tile DMA/barriers, 64 no dW reads)
 constexpr int ROWS = 64;                // rows per tile (4 M-tiles of 16)
-constexpr int CLASSES = 64;             // classes per block (16 per wave)
+constexpr int WAVE_CLASSES = 16;        // classes per MFMA N-tile; a wave owns NC of them
 constexpr int SUB_BYTES = ROWS * 256;   // one [64 rows][128 bf16] sub-image
 constexpr int META_BYTES = 1024;        // [64 lse] [64 argmax bits] [64 y] [256 B DMA pad]
 constexpr float LOG2E_F = 1.4426950408889634f;
@@ -62,6 +65,17 @@ __device__ __forceinline__ i16x4_t tr_read(uint32_t addr) {
   i16x4_t v;
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
   return v;
+}
+// ds_read_b128 at an immediate offset, invisible to hipcc's wait insertion
+template <int OFF, typename T>
+__device__ __forceinline__ T lds_read_b128(uint32_t addr) {
+  T v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+template <int N, typename A>
+__device__ __forceinline__ void lgkm_wait(A& a) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "i"(N));
 }
 // s_waitcnt lgkmcnt(N) that orders every later use of a and b after it
 template <int N, typename A, typename B>
@@ -107,8 +121,14 @@ struct GradDwArgs {
   float* stat_slabs;    // [row_groups * class_groups][2] = {loss_sum, n_correct}
 };
 
-template <int KS, bool OVR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void softmax_grad_dw_kernel(GradDwArgs a) {
+// NC = class tiles of 16 per wave. NC = 1: 64 classes per block, <= 256 VGPRs, 2 waves/SIMD (the
+// other wave hides the epilogue and the barriers). NC = 2: 128 classes per block, 1 wave/SIMD; every
+// X fragment read from LDS feeds two MFMAs, halving the LDS bytes per MFMA (at NC = 1 both phases
+// need 256 B/clk/CU, the LDS array's peak).
+template <int KS, bool OVR, int NC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3 - NC, 3 - NC))) void softmax_grad_dw_kernel(
+    GradDwArgs a) {
+  constexpr int CLASSES = 4 * WAVE_CLASSES * NC;
   constexpr int F_ = KS * 32;
   constexpr int X_BYTES = (F_ / 128) * SUB_BYTES;
   constexpr int BUF_BYTES = X_BYTES + META_BYTES;
@@ -137,25 +157,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int t_begin = rg * a.tiles_per_group;
   const int t_end = min(a.tiles, t_begin + a.tiles_per_group);
 
-  const int cls = cg * CLASSES + wave * 16 + col;  // this lane's class in steps 1-2
-  const bool cls_ok = cls < K;
-  const int cls_c = min(cls, K - 1);
+  const int cls0 = cg * CLASSES + wave * WAVE_CLASSES * NC + col;  // this lane's class, tile h: + 16 h
 
-  // W rows of the wave's 16 classes: the B operand of every logits MFMA, resident in VGPRs.
-  bf16x8_t wf[KS];
+  // W rows of the wave's classes: the B operands of every logits MFMA, resident in VGPRs.
+  // Padded classes: logits -1e30 (finite: 0 * z stays 0), so p = 0, g = 0 and loss = 0 with no
+  // per-element class check.
+  bf16x8_t wf[NC][KS];
+  float bv[NC];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-    wf[ks] = *reinterpret_cast<const bf16x8_t*>(a.W + (int64_t)cls_c * F_ + ks * 32 + g * 8);
-  // padded classes: logits -1e30 (finite: 0 * z stays 0), so p = 0, g = 0 and loss = 0 with no
-  // per-element class check
-  const float bv = cls_ok ? a.bias[cls_c] : -1e30f;
+  for (int h = 0; h < NC; ++h) {
+    const int cls = cls0 + h * WAVE_CLASSES;
+    const int cls_c = min(cls, K - 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      wf[h][ks] = *reinterpret_cast<const bf16x8_t*>(a.W + (int64_t)cls_c * F_ + ks * 32 + g * 8);
+    bv[h] = cls < K ? a.bias[cls_c] : -1e30f;
+  }
 
-  f32x4_t acc[NT];
-#pragma unroll
-  for (int n = 0; n < NT; ++n) acc[n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  f32x4_t acc[NC][NT];
   // intercept gradient sum_rows g = G^T (ones column of X_aug): one more MFMA per 32 rows with a
   // constant B operand (column 0 = 1, the rest 0) instead of a VALU add per element
-  f32x4_t acc_db = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  f32x4_t acc_db[NC];
+#pragma unroll
+  for (int h = 0; h < NC; ++h) {
+    acc_db[h] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[h][n] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
   const bf16x8_t ones_b = col == 0 ? bf16x8_t{1, 1, 1, 1, 1, 1, 1, 1} : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
   float loss = 0.f, lz = 0.f, correct = 0.f;
   const bool row_wave = cg == 0 && wave == 0;  // one wave per row range: correct count (+ sum lse)
@@ -214,43 +242,75 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const unsigned char* xb = smem + buf * BUF_BYTES;
     const int64_t row0 = (int64_t)t * ROWS;
 
-    // 1. Z^T tile (rows x the wave's 16 classes), bias-initialised
-    f32x4_t z[4];
+    // 1. Z^T tile (rows x the wave's 16 classes), bias-initialised. A fragments through inline-asm
+    //    ds_read_b128 with PF reads in flight (counted lgkmcnt waits; 4 per-lane bases, one per
+    //    ks & 3, the rest immediate offsets). Once the last A read is issued, the row metadata of
+    //    the epilogue (LDS after the X image: [64 lse][64 argmax bits][64 y]) is read behind it.
+    constexpr int PF = 6;
+    constexpr int NA = 4 * KS;
+    const uint32_t xo = lds_off(xb);
+    const uint32_t mb = xo + X_BYTES;
+    uint32_t ab[4];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) z[mt] = f32x4_t{bv, bv, bv, bv};
+    for (int k = 0; k < 4; ++k) ab[k] = xo + img_off(m_row(col), k * 32 + g * 8);
+    f32x4_t z[NC][4];
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+    for (int h = 0; h < NC; ++h)
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const bf16x8_t xa = *reinterpret_cast<const bf16x8_t*>(xb + img_off(mt * 16 + m_row(col), ks * 32 + g * 8));
-        z[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa, wf[ks], z[mt], 0, 0, 0);
+      for (int mt = 0; mt < 4; ++mt) z[h][mt] = f32x4_t{bv[h], bv[h], bv[h], bv[h]};
+    bf16x8_t xa[NA];
+    i32x4_t y4[4], l4[4];
+    auto issue_a = [&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int ks = i / 4, mt = i % 4;
+      xa[i] = lds_read_b128<(ks >> 2) * SUB_BYTES + mt * 16 * 256, bf16x8_t>(ab[ks & 3]);
+    };
+    static_for<PF>(issue_a);
+    static_for<NA>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if constexpr (i + PF < NA) issue_a(std::integral_constant<int, i + PF>{});
+      if constexpr (i + PF == NA) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const uint32_t rb = mt * 16 + grp_row(g);
+          y4[mt] = lds_read_b128<512, i32x4_t>(mb + rb * 4);
+          l4[mt] = lds_read_b128<0, i32x4_t>(mb + rb * 4);
+        }
       }
-    }
+      constexpr int after = (NA - 1 - i < PF ? NA - 1 - i : PF) + (i + PF >= NA ? 8 : 0);
+      lgkm_wait<after>(xa[i]);
+#pragma unroll
+      for (int h = 0; h < NC; ++h) {
+        if constexpr (!(MLAPI_GDW_EXP & 4))
+          z[h][i % 4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[i], wf[h][i / 4], z[h][i % 4], 0, 0, 0);
+        else
+          z[h][i % 4] += __builtin_bit_cast(f32x4_t, xa[i]);
+      }
+    });
 
     // 2. gradient in registers: lane holds rows mt*16 + grp_row(g) + r of class `cls`. Only the
-    //    last tile of the batch has padded rows (uniform branch); padded classes are -inf logits.
+    //    last tile of the batch has padded rows (uniform branch); padded classes are -1e30 logits.
     const int rows_left = (int)min<int64_t>(ROWS, B - row0);
-    // Row metadata (LDS after the X image: [64 lse][64 argmax bits][64 y]) through inline-asm
-    // ds_reads: hipcc cannot disambiguate an ordinary LDS read of this region from the DMA of tile
-    // t+2 still in flight and would wait vmcnt(0) before it, draining the pipeline every tile. Each
-    // counted wait takes the results as in-out operands, so every use is ordered after the data.
-    const uint32_t mb = lds_off(xb + X_BYTES);
-    bf16x8_t ga[2];
+    bf16x8_t ga[NC][2];
     auto epilogue = [&](auto partial) {
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const uint32_t rb = mt * 16 + grp_row(g);
-        i32x4_t y4, l4;
-        asm volatile("ds_read_b128 %0, %1 offset:512" : "=v"(y4) : "v"(mb + rb * 4));
-        asm volatile("ds_read_b128 %0, %1" : "=v"(l4) : "v"(mb + rb * 4));
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(y4), "+v"(l4));
-        const int yv[4] = {y4[0], y4[1], y4[2], y4[3]};
-        const float lse[4] = {__int_as_float(l4[0]), __int_as_float(l4[1]), __int_as_float(l4[2]),
-                              __int_as_float(l4[3])};
+        switch (mt) {  // meta of M-tile mt landed (reads of mt+1.. may still fly)
+          case 0: lgkm_wait<6>(y4[0], l4[0]); break;
+          case 1: lgkm_wait<4>(y4[1], l4[1]); break;
+          case 2: lgkm_wait<2>(y4[2], l4[2]); break;
+          default: lgkm_wait<0>(y4[3], l4[3]); break;
+        }
+        const int yv[4] = {y4[mt][0], y4[mt][1], y4[mt][2], y4[mt][3]};
+        const float lse[4] = {__int_as_float(l4[mt][0]), __int_as_float(l4[mt][1]), __int_as_float(l4[mt][2]),
+                              __int_as_float(l4[mt][3])};
+#pragma unroll
+        for (int h = 0; h < NC; ++h)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool hot = cls == yv[r];
-          const float zz = z[mt][r];
+          const bool hot = cls0 + h * WAVE_CLASSES == yv[r];
+          const float zz = z[h][mt][r];
           float pr;
           if constexpr (OVR) {
             const float e = __builtin_amdgcn_exp2f(-fabsf(zz) * LOG2E_F);  // exp(-|z|)
@@ -270,14 +330,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             msk = ok ? msk : 0.f;
           }
           lz = fmaf(msk, zz, lz);
-          ga[mt >> 1][(mt & 1) * 4 + r] = (__bf16)gv;
+          ga[h][mt >> 1][(mt & 1) * 4 + r] = (__bf16)gv;
         }
       }
     };
-    if (rows_left == ROWS)
+    if constexpr (MLAPI_GDW_EXP & 1) {
+      lgkm_wait<0>(y4[3], l4[3]);
+#pragma unroll
+      for (int h = 0; h < NC; ++h)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ga[h][mt >> 1][(mt & 1) * 4 + r] = (__bf16)z[h][mt][r];
+    } else if (rows_left == ROWS) {
       epilogue(std::false_type{});
-    else
+    } else {
       epilogue(std::true_type{});
+    }
     if (row_wave) {  // one row per lane: argmax == y, and sum lse
       int yl, al, ll;
       asm volatile("ds_read_b32 %0, %1 offset:512" : "=v"(yl) : "v"(mb + lane * 4));
@@ -292,7 +361,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
     // 3. dW_c += G X_tile: B operand = 8 rows of one feature column via two transposed reads
     //    (lane 4q+p of group g addresses row base + q, columns n*16 + 4p .. +3). Inline asm with
-    //    counted waits (two (j, n) steps in flight): hipcc treats the ds_read_tr builtin as
+    //    counted waits (DW_PF (j, n) steps in flight): hipcc treats the ds_read_tr builtin as
     //    aliasing the tile DMA in flight and would wait vmcnt(0) before the first one. Row base
     //    + 16 (hi), + 32 (j) and the second 128-column sub-image (n >= 8) keep the swizzle, so they
     //    are immediate offsets from 8 per-lane bases (one per n & 7).
@@ -308,29 +377,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         tl[i] = tr_read<off>(trb[i & 7]);
         th[i] = tr_read<off + 16 * 256>(trb[i & 7]);
       };
-      issue(std::integral_constant<int, 0>{});
-      issue(std::integral_constant<int, 1>{});
-      static_for<2 * NT>([&](auto ic) {
+      constexpr int DW_PF = 6;  // (j, n) steps in flight: 2 * DW_PF reads <= 15 (lgkmcnt field)
+      if constexpr (!(MLAPI_GDW_EXP & (8 | 64))) static_for<DW_PF>(issue);
+      if constexpr (!(MLAPI_GDW_EXP & 8)) static_for<2 * NT>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        if constexpr (i + 2 < 2 * NT) issue(std::integral_constant<int, i + 2>{});
-        constexpr int pending = i + 2 < 2 * NT ? 4 : (i + 1 < 2 * NT ? 2 : 0);
-        lgkm_wait<pending>(tl[i], th[i]);
-        const bf16x8_t xbf = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, tl[i]),
-                                                     __builtin_bit_cast(bf16x4_t, th[i]), 0, 1, 2, 3, 4, 5, 6, 7);
-        acc[i % NT] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[i / NT], xbf, acc[i % NT], 0, 0, 0);
-        if constexpr (i % NT == NT - 1)
-          acc_db = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[i / NT], ones_b, acc_db, 0, 0, 0);
+        bf16x8_t xbf;
+        if constexpr (MLAPI_GDW_EXP & 64) {  // experiment: MFMAs only, constant B operand
+          xbf = ones_b;
+        } else {
+          if constexpr (i + DW_PF < 2 * NT) issue(std::integral_constant<int, i + DW_PF>{});
+          constexpr int pending = 2 * (2 * NT - 1 - i < DW_PF ? 2 * NT - 1 - i : DW_PF);
+          lgkm_wait<pending>(tl[i], th[i]);
+          xbf = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, tl[i]), __builtin_bit_cast(bf16x4_t, th[i]), 0,
+                                        1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int h = 0; h < NC; ++h) {
+          if constexpr (!(MLAPI_GDW_EXP & 2))
+            acc[h][i % NT] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[h][i / NT], xbf, acc[h][i % NT], 0, 0, 0);
+          else
+            acc[h][i % NT] += __builtin_bit_cast(f32x4_t, xbf);
+          if constexpr (i % NT == NT - 1)
+            acc_db[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[h][i / NT], ones_b, acc_db[h], 0, 0, 0);
+        }
       });
     }
 
-    if (t + 2 < t_end) {
+    if (MLAPI_GDW_EXP & 16) {
+    } else if (t + 2 < t_end) {
       MLAPI_RAW_BARRIER()  // every wave is done reading `buf`
       MLAPI_DMA_TILE(t + 2, buf)
       __builtin_amdgcn_s_waitcnt(kWaitTile);  // tile t+1 landed, t+2 flies
     } else {
       __builtin_amdgcn_s_waitcnt(kWaitAll);
     }
-    MLAPI_RAW_BARRIER()
+    if (!(MLAPI_GDW_EXP & 16)) {
+      MLAPI_RAW_BARRIER()
+    }
     buf ^= 1;
   }
 #undef MLAPI_RAW_BARRIER
@@ -338,21 +421,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
   // ---- dW partial of this row group: lane holds dW[class base + 4g + r][n*16 + col]
   float* slab = a.dw_slabs + (int64_t)rg * K * a.ldw;
-  const int cbase = cg * CLASSES + wave * 16 + 4 * g;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    if (cbase + r < K) {
-      float* dst = slab + (int64_t)(cbase + r) * a.ldw + col;
+  for (int h = 0; h < NC; ++h) {
+    const int cbase = cg * CLASSES + wave * WAVE_CLASSES * NC + h * WAVE_CLASSES + 4 * g;
 #pragma unroll
-      for (int n = 0; n < NT; ++n) dst[n * 16] = acc[n][r];
+    for (int r = 0; r < 4; ++r) {
+      if (cbase + r < K) {
+        float* dst = slab + (int64_t)(cbase + r) * a.ldw + col;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) dst[n * 16] = acc[h][n][r];
+      }
     }
-  }
-  // intercept gradient (column F) and the zero pad columns F+1 .. ldw-1: lane col of acc_db holds
-  // G^T e_col, i.e. sum(g) for col 0 and 0 otherwise
-  if (col < a.ldw - F_) {
+    // intercept gradient (column F) and the zero pad columns F+1 .. ldw-1: lane col of acc_db
+    // holds G^T e_col, i.e. sum(g) for col 0 and 0 otherwise
+    if (col < a.ldw - F_) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (cbase + r < K) slab[(int64_t)(cbase + r) * a.ldw + F_ + col] = acc_db[r];
+      for (int r = 0; r < 4; ++r)
+        if (cbase + r < K) slab[(int64_t)(cbase + r) * a.ldw + F_ + col] = acc_db[h][r];
+    }
   }
   // ---- [loss, correct] of the block (deterministic tree); padded rows/classes have z_y terms of 0
   loss -= lz;
@@ -415,18 +501,25 @@ __global__ __launch_bounds__(256) void gdw_reduce_kernel(const f32x4_t* __restri
 }
 
 struct GdwLayout {
-  int tiles, row_groups, tiles_per_group, class_groups;
+  int nc, tiles, row_groups, tiles_per_group, class_groups;
   size_t rowstat_off, dw_off, stat_off, total;
 };
 
-int g_force_row_groups = 0;  // benchmark hook (softmax_grad_dw_force_row_groups)
+int g_force_row_groups = 0;  // benchmark hooks (softmax_grad_dw_force_plan)
+int g_force_nc = 0;
 
-GdwLayout gdw_layout(int64_t B, int K, int F) {
+int auto_nc(int K) { return g_force_nc > 0 ? g_force_nc : (K >= 256 ? 2 : 1); }
+
+GdwLayout gdw_layout(int64_t B, int K, int F, int nc) {
   GdwLayout L;
+  L.nc = nc;
   L.tiles = (int)((B + ROWS - 1) / ROWS);
-  L.class_groups = (K + CLASSES - 1) / CLASSES;
-  // ~2 blocks per CU (512) unless the rows run out; every row group gets >= 1 tile
-  int want = g_force_row_groups > 0 ? g_force_row_groups : (512 + L.class_groups - 1) / L.class_groups;
+  const int classes = 4 * WAVE_CLASSES * nc;
+  L.class_groups = (K + classes - 1) / classes;
+  // resident blocks: 2 per CU at NC = 1, 1 at NC = 2 (unless the rows run out); every row group
+  // gets >= 1 tile
+  const int target = nc == 1 ? 512 : 256;
+  int want = g_force_row_groups > 0 ? g_force_row_groups : (target + L.class_groups - 1) / L.class_groups;
   want = want < 1 ? 1 : (want > L.tiles ? L.tiles : want);
   L.tiles_per_group = (L.tiles + want - 1) / want;
   L.row_groups = (L.tiles + L.tiles_per_group - 1) / L.tiles_per_group;
@@ -442,9 +535,15 @@ GdwLayout gdw_layout(int64_t B, int K, int F) {
 
 bool softmax_grad_dw_supported(int F) { return F == 128 || F == 256; }
 
-void softmax_grad_dw_force_row_groups(int n) { g_force_row_groups = n; }
+void softmax_grad_dw_force_plan(int row_groups, int nc) {
+  g_force_row_groups = row_groups;
+  g_force_nc = nc;
+}
 
-size_t softmax_grad_dw_workspace(int64_t B, int K, int F) { return gdw_layout(B, K, F).total; }
+size_t softmax_grad_dw_workspace(int64_t B, int K, int F) {  // enough for either class-tile plan
+  const size_t a = gdw_layout(B, K, F, 1).total, b = gdw_layout(B, K, F, 2).total;
+  return a > b ? a : b;
+}
 
 void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
                             int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,
@@ -456,7 +555,7 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
   if (ldx != F + 8) throw std::invalid_argument("softmax_grad_dw: X_aug row stride must be F + 8");
   if (reinterpret_cast<uintptr_t>(X_aug) % 16 != 0 || reinterpret_cast<uintptr_t>(W) % 16 != 0)
     throw std::invalid_argument("softmax_grad_dw: X_aug and W must be 16-byte aligned");
-  const GdwLayout L = gdw_layout(B, K, F);
+  const GdwLayout L = gdw_layout(B, K, F, auto_nc(K));
   if (ws_bytes < L.total) throw std::invalid_argument("softmax_grad_dw: workspace too small (zero it once)");
   unsigned char* ws = static_cast<unsigned char*>(workspace);
   float2* rowstat = reinterpret_cast<float2*>(ws + L.rowstat_off);
@@ -479,17 +578,21 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
   args.stat_slabs = reinterpret_cast<float*>(ws + L.stat_off);
   const dim3 grid((unsigned)(L.row_groups * L.class_groups));
   const bool ovr = kind == KIND_OVR;
-  if (F == 128) {
+  auto launch = [&](auto ks, auto nc) {
+    constexpr int KS_ = decltype(ks)::value, NC_ = decltype(nc)::value;
     if (ovr)
-      hipLaunchKernelGGL((softmax_grad_dw_kernel<4, true>), grid, dim3(256), 0, stream, args);
+      hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, true, NC_>), grid, dim3(256), 0, stream, args);
     else
-      hipLaunchKernelGGL((softmax_grad_dw_kernel<4, false>), grid, dim3(256), 0, stream, args);
-  } else {
-    if (ovr)
-      hipLaunchKernelGGL((softmax_grad_dw_kernel<8, true>), grid, dim3(256), 0, stream, args);
-    else
-      hipLaunchKernelGGL((softmax_grad_dw_kernel<8, false>), grid, dim3(256), 0, stream, args);
-  }
+      hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, false, NC_>), grid, dim3(256), 0, stream, args);
+  };
+  using I4 = std::integral_constant<int, 4>;
+  using I8 = std::integral_constant<int, 8>;
+  using N1 = std::integral_constant<int, 1>;
+  using N2 = std::integral_constant<int, 2>;
+  if (F == 128)
+    L.nc == 1 ? launch(I4{}, N1{}) : launch(I4{}, N2{});
+  else
+    L.nc == 1 ? launch(I8{}, N1{}) : launch(I8{}, N2{});
   MLAPI_HIP_CHECK(hipGetLastError());
   if (reinterpret_cast<uintptr_t>(dW_out) % 16 == 0) {
     const int width4 = K * (F + 8) / 4;

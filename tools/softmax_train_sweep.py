@@ -57,13 +57,14 @@ for S in (2, 4, 8, 16, 32, 64):
     res[f"dW_bmm_S{S}_maxdiff"] = (out - ref).abs().max().item()
 # fused path: rowstats + G/dW kernel + slab sums, whole call
 stf = torch.zeros(2, device=dev)
-for groups in (0, 8, 16, 32, 64, 128):
-    C().softmax_grad_dw_force_row_groups(groups)
-    fb = ops.SoftmaxTrainBuffers(B, K, F, dev, dw_path="fused")
-    res[f"fused_groups{groups}_us"] = timeit(lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=fb, dW_out=out,
-                                                                            stats_out=stf))
-    res[f"fused_groups{groups}_maxdiff"] = (out - ref).abs().max().item()
-C().softmax_grad_dw_force_row_groups(0)
+for nc in (1, 2):
+    for groups in (0, 16, 32, 64, 128):
+        C().softmax_grad_dw_force_plan(groups, nc)
+        fb = ops.SoftmaxTrainBuffers(B, K, F, dev, dw_path="fused")
+        res[f"fused_nc{nc}_groups{groups}_us"] = timeit(
+            lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=fb, dW_out=out, stats_out=stf))
+        res[f"fused_nc{nc}_groups{groups}_maxdiff"] = (out - ref).abs().max().item()
+C().softmax_grad_dw_force_plan(0, 0)
 gb = ops.SoftmaxTrainBuffers(B, K, F, dev, dw_path="gemm")
 res["gemm_path_total_us"] = timeit(lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=gb, dW_out=out, stats_out=stf))
 res["dW_ref_absmax"] = ref.abs().max().item()
