@@ -291,17 +291,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3 - NC, 3 -
     // 2. gradient in registers: lane holds rows mt*16 + grp_row(g) + r of class `cls`. Only the
     //    last tile of the batch has padded rows (uniform branch); padded classes are -1e30 logits.
     const int rows_left = (int)min<int64_t>(ROWS, B - row0);
+    // every metadata read landed before the epilogue variants branch apart (one wait on all paths)
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(y4[0]), "+v"(y4[1]), "+v"(y4[2]), "+v"(y4[3]), "+v"(l4[0]), "+v"(l4[1]), "+v"(l4[2]),
+                   "+v"(l4[3]));
     bf16x8_t ga[NC][2];
     auto epilogue = [&](auto partial) {
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const uint32_t rb = mt * 16 + grp_row(g);
-        switch (mt) {  // meta of M-tile mt landed (reads of mt+1.. may still fly)
-          case 0: lgkm_wait<6>(y4[0], l4[0]); break;
-          case 1: lgkm_wait<4>(y4[1], l4[1]); break;
-          case 2: lgkm_wait<2>(y4[2], l4[2]); break;
-          default: lgkm_wait<0>(y4[3], l4[3]); break;
-        }
         const int yv[4] = {y4[mt][0], y4[mt][1], y4[mt][2], y4[mt][3]};
         const float lse[4] = {__int_as_float(l4[mt][0]), __int_as_float(l4[mt][1]), __int_as_float(l4[mt][2]),
                               __int_as_float(l4[mt][3])};
@@ -335,7 +333,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3 - NC, 3 -
       }
     };
     if constexpr (MLAPI_GDW_EXP & 1) {
-      lgkm_wait<0>(y4[3], l4[3]);
 #pragma unroll
       for (int h = 0; h < NC; ++h)
 #pragma unroll
