@@ -249,7 +249,8 @@ PYBIND11_MODULE(_C, m) {
       py::arg("K"), py::arg("kind"), py::arg("G"), py::arg("ldg"), py::arg("stats_out"), py::arg("ws"),
       py::arg("ws_bytes"), py::arg("stream") = 0);
   m.def("softmax_grad_dw_supported", &softmax_grad_dw_supported);
-  m.def("softmax_grad_dw_force_plan", &softmax_grad_dw_force_plan, py::arg("row_groups") = 0, py::arg("nc") = 0);
+  m.def("softmax_grad_dw_force_plan", &softmax_grad_dw_force_plan, py::arg("row_groups") = 0, py::arg("nc") = 0,
+        py::arg("pipe") = 0);
   m.def("softmax_grad_dw_workspace", &softmax_grad_dw_workspace);
   m.def(
       "softmax_grad_dw",

@@ -85,7 +85,7 @@ void launch_softmax_rowstats(const void* X_aug, int64_t ldx, const void* W, cons
 // = intercept gradient, F+1.. = 0); stats_out = [loss_sum, n_correct]. F in {128, 256},
 // ldx = F + 8. Workspace: softmax_grad_dw_workspace(B, K, F) bytes, zeroed once.
 bool softmax_grad_dw_supported(int F);
-void softmax_grad_dw_force_plan(int row_groups, int nc);  // benchmark hook (0 = automatic)
+void softmax_grad_dw_force_plan(int row_groups, int nc, int pipe);  // benchmark hook (0 = automatic)
 size_t softmax_grad_dw_workspace(int64_t B, int K, int F);
 void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
                             int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,

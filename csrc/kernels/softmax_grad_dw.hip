@@ -125,9 +125,15 @@ struct GradDwArgs {
 // other wave hides the epilogue and the barriers). NC = 2: 128 classes per block, 1 wave/SIMD; every
 // X fragment read from LDS feeds two MFMAs, halving the LDS bytes per MFMA (at NC = 1 both phases
 // need 256 B/clk/CU, the LDS array's peak).
-template <int KS, bool OVR, int NC>
+//
+// PIPE (NC = 2 only): a software pipeline across tiles with 3 LDS buffers. Iteration t computes the
+// logits of tile t+1 and the epilogue of tile t in one basic block, so the epilogue's VALU work
+// fills the MFMA issue gaps of the next tile's logits instead of running exposed at 1 wave/SIMD.
+template <int KS, bool OVR, int NC, bool PIPE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3 - NC, 3 - NC))) void softmax_grad_dw_kernel(
     GradDwArgs a) {
+  static_assert(!PIPE || NC == 2, "the pipelined variant runs at 1 wave/SIMD (NC = 2)");
+  constexpr int NBUF = PIPE ? 3 : 2;
   constexpr int CLASSES = 4 * WAVE_CLASSES * NC;
   constexpr int F_ = KS * 32;
   constexpr int X_BYTES = (F_ / 128) * SUB_BYTES;
@@ -136,7 +142,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3 - NC, 3 -
   static_assert(F_ % 128 == 0, "sub-images are 128 columns wide");
   // ALL LDS in one __shared__ object: a second one (even a small reduction array) makes hipcc wait
   // vmcnt(0) before the first ds_read of every tile, draining the in-flight DMA (guide 4(a)).
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF_BYTES];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * BUF_BYTES];
   float* const red = reinterpret_cast<float*>(smem);  // stats reduction, after the last tile
 
   const int tid = threadIdx.x;
@@ -226,40 +232,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3 - NC, 3 -
   // Rows past B are never DMA'd; if this block owns the batch's ragged last tile, zero the LDS once
   // so those rows hold zeros (not stale non-finite bits) where 0-gradients multiply them.
   if ((int64_t)t_end * ROWS > B) {
-    for (int o = tid * 16; o < 2 * BUF_BYTES; o += 256 * 16) *reinterpret_cast<int4*>(smem + o) = int4{0, 0, 0, 0};
+    for (int o = tid * 16; o < NBUF * BUF_BYTES; o += 256 * 16) *reinterpret_cast<int4*>(smem + o) = int4{0, 0, 0, 0};
     __syncthreads();
   }
-  int buf = 0;
-  MLAPI_DMA_TILE(t_begin, 0)
-  if (t_begin + 1 < t_end) {
-    MLAPI_DMA_TILE(t_begin + 1, 1)
-    __builtin_amdgcn_s_waitcnt(kWaitTile);  // W, bias and tile 0 landed; tile 1 may still fly
-  } else {
-    __builtin_amdgcn_s_waitcnt(kWaitAll);
-  }
-  MLAPI_RAW_BARRIER()
-  for (int t = t_begin; t < t_end; ++t) {
-    const unsigned char* xb = smem + buf * BUF_BYTES;
-    const int64_t row0 = (int64_t)t * ROWS;
-
-    // 1. Z^T tile (rows x the wave's 16 classes), bias-initialised. A fragments through inline-asm
-    //    ds_read_b128 with PF reads in flight (counted lgkmcnt waits; 4 per-lane bases, one per
-    //    ks & 3, the rest immediate offsets). Once the last A read is issued, the row metadata of
-    //    the epilogue (LDS after the X image: [64 lse][64 argmax bits][64 y]) is read behind it.
-    constexpr int PF = 6;
-    constexpr int NA = 4 * KS;
-    const uint32_t xo = lds_off(xb);
-    const uint32_t mb = xo + X_BYTES;
-    uint32_t ab[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ab[k] = xo + img_off(m_row(col), k * 32 + g * 8);
-    f32x4_t z[NC][4];
+  // ---- per-tile pieces (one LDS image at byte offset xo; its row metadata at xo + X_BYTES)
+  constexpr int PF = 6;  // A-fragment reads in flight
+  constexpr int NA = 4 * KS;
+  i32x4_t y4[4], l4[4];  // row metadata of the tile in the epilogue: y and lse of 4 rows per M-tile
+  bf16x8_t ga[NC][2];    // G of the tile as the dW A operand
+  auto init_z = [&](f32x4_t(&zz)[NC][4]) {
 #pragma unroll
     for (int h = 0; h < NC; ++h)
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) z[h][mt] = f32x4_t{bv[h], bv[h], bv[h], bv[h]};
+      for (int mt = 0; mt < 4; ++mt) zz[h][mt] = f32x4_t{bv[h], bv[h], bv[h], bv[h]};
+  };
+  auto read_meta = [&](uint32_t mb) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const uint32_t rb = mt * 16 + grp_row(g);
+      y4[mt] = lds_read_b128<512, i32x4_t>(mb + rb * 4);
+      l4[mt] = lds_read_b128<0, i32x4_t>(mb + rb * 4);
+    }
+  };
+  auto wait_meta = [&]() {  // every metadata read landed; one wait on all CFG paths
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(y4[0]), "+v"(y4[1]), "+v"(y4[2]), "+v"(y4[3]), "+v"(l4[0]), "+v"(l4[1]), "+v"(l4[2]),
+                   "+v"(l4[3]));
+  };
+  // 1. Z^T tile (rows x the wave's classes) into zz (bias-initialised by the caller). A fragments
+  //    through inline-asm ds_read_b128 with PF reads in flight (counted lgkmcnt waits; 4 per-lane
+  //    bases, one per ks & 3, the rest immediate offsets); with_meta: the tile's row metadata
+  //    (LDS after the X image: [64 lse][64 argmax bits][64 y]) is read behind the last A read.
+  auto logits = [&](uint32_t xo, f32x4_t(&zz)[NC][4], auto with_meta) {
+    uint32_t ab[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ab[k] = xo + img_off(m_row(col), k * 32 + g * 8);
     bf16x8_t xa[NA];
-    i32x4_t y4[4], l4[4];
     auto issue_a = [&](auto ic) {
       constexpr int i = decltype(ic)::value;
       constexpr int ks = i / 4, mt = i % 4;
@@ -268,56 +276,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3 - NC, 3 -
     static_for<PF>(issue_a);
     static_for<NA>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
+      constexpr bool meta = decltype(with_meta)::value;
       if constexpr (i + PF < NA) issue_a(std::integral_constant<int, i + PF>{});
-      if constexpr (i + PF == NA) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const uint32_t rb = mt * 16 + grp_row(g);
-          y4[mt] = lds_read_b128<512, i32x4_t>(mb + rb * 4);
-          l4[mt] = lds_read_b128<0, i32x4_t>(mb + rb * 4);
-        }
-      }
-      constexpr int after = (NA - 1 - i < PF ? NA - 1 - i : PF) + (i + PF >= NA ? 8 : 0);
+      if constexpr (meta && i + PF == NA) read_meta(xo + X_BYTES);
+      constexpr int after = (NA - 1 - i < PF ? NA - 1 - i : PF) + (meta && i + PF >= NA ? 8 : 0);
       lgkm_wait<after>(xa[i]);
 #pragma unroll
       for (int h = 0; h < NC; ++h) {
         if constexpr (!(MLAPI_GDW_EXP & 4))
-          z[h][i % 4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[i], wf[h][i / 4], z[h][i % 4], 0, 0, 0);
+          zz[h][i % 4] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa[i], wf[h][i / 4], zz[h][i % 4], 0, 0, 0);
         else
-          z[h][i % 4] += __builtin_bit_cast(f32x4_t, xa[i]);
+          zz[h][i % 4] += __builtin_bit_cast(f32x4_t, xa[i]);
       }
     });
-
-    // 2. gradient in registers: lane holds rows mt*16 + grp_row(g) + r of class `cls`. Only the
-    //    last tile of the batch has padded rows (uniform branch); padded classes are -1e30 logits.
-    const int rows_left = (int)min<int64_t>(ROWS, B - row0);
-    // every metadata read landed before the epilogue variants branch apart (one wait on all paths)
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(y4[0]), "+v"(y4[1]), "+v"(y4[2]), "+v"(y4[3]), "+v"(l4[0]), "+v"(l4[1]), "+v"(l4[2]),
-                   "+v"(l4[3]));
-    bf16x8_t ga[NC][2];
-    auto epilogue = [&](auto partial) {
+  };
+  // 2. gradient in registers: lane holds rows mt*16 + grp_row(g) + r of class cls0 + 16 h. Only
+  //    the last tile of the batch has padded rows (`partial`); padded classes are -1e30 logits.
+  auto epilogue = [&](auto partial, const f32x4_t(&zz)[NC][4], int rows_left) {
+    if constexpr (MLAPI_GDW_EXP & 1) {
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const uint32_t rb = mt * 16 + grp_row(g);
-        const int yv[4] = {y4[mt][0], y4[mt][1], y4[mt][2], y4[mt][3]};
-        const float lse[4] = {__int_as_float(l4[mt][0]), __int_as_float(l4[mt][1]), __int_as_float(l4[mt][2]),
-                              __int_as_float(l4[mt][3])};
+      for (int h = 0; h < NC; ++h)
 #pragma unroll
-        for (int h = 0; h < NC; ++h)
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ga[h][mt >> 1][(mt & 1) * 4 + r] = (__bf16)zz[h][mt][r];
+      return;
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const uint32_t rb = mt * 16 + grp_row(g);
+      const int yv[4] = {y4[mt][0], y4[mt][1], y4[mt][2], y4[mt][3]};
+      const float lse[4] = {__int_as_float(l4[mt][0]), __int_as_float(l4[mt][1]), __int_as_float(l4[mt][2]),
+                            __int_as_float(l4[mt][3])};
+#pragma unroll
+      for (int h = 0; h < NC; ++h)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const bool hot = cls0 + h * WAVE_CLASSES == yv[r];
-          const float zz = z[h][mt][r];
+          const float zv = zz[h][mt][r];
           float pr;
           if constexpr (OVR) {
-            const float e = __builtin_amdgcn_exp2f(-fabsf(zz) * LOG2E_F);  // exp(-|z|)
+            const float e = __builtin_amdgcn_exp2f(-fabsf(zv) * LOG2E_F);  // exp(-|z|)
             const float re = __builtin_amdgcn_rcpf(1.f + e);
-            pr = zz >= 0.f ? re : e * re;
-            const float l = fmaxf(zz, 0.f) + __builtin_amdgcn_logf(1.f + e) * LN2_F;
-            loss += decltype(partial)::value ? (rb + r < rows_left ? l : 0.f) : l;
+            pr = zv >= 0.f ? re : e * re;
+            const float l = fmaxf(zv, 0.f) + __builtin_amdgcn_logf(1.f + e) * LN2_F;
+            loss += decltype(partial)::value ? (rb + r < (uint32_t)rows_left ? l : 0.f) : l;
           } else {
-            pr = __builtin_amdgcn_exp2f((zz - lse[r]) * LOG2E_F);
+            pr = __builtin_amdgcn_exp2f((zv - lse[r]) * LOG2E_F);
           }
           // loss = sum(lse) - sum(z_y) (multinomial); OvR: sum(softplus terms) - sum(z_y)
           float msk = hot ? 1.f : 0.f;
@@ -327,23 +332,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3 - NC, 3 -
             gv = ok ? gv : 0.f;
             msk = ok ? msk : 0.f;
           }
-          lz = fmaf(msk, zz, lz);
+          lz = fmaf(msk, zv, lz);
           ga[h][mt >> 1][(mt & 1) * 4 + r] = (__bf16)gv;
         }
-      }
-    };
-    if constexpr (MLAPI_GDW_EXP & 1) {
-#pragma unroll
-      for (int h = 0; h < NC; ++h)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) ga[h][mt >> 1][(mt & 1) * 4 + r] = (__bf16)z[h][mt][r];
-    } else if (rows_left == ROWS) {
-      epilogue(std::false_type{});
-    } else {
-      epilogue(std::true_type{});
     }
+  };
+  auto row_stats = [&](uint32_t mb, int rows_left) {
     if (row_wave) {  // one row per lane: argmax == y, and sum lse
       int yl, al, ll;
       asm volatile("ds_read_b32 %0, %1 offset:512" : "=v"(yl) : "v"(mb + lane * 4));
@@ -355,63 +349,136 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3 - NC, 3 -
         if constexpr (!OVR) loss += __int_as_float(ll);
       }
     }
-
-    // 3. dW_c += G X_tile: B operand = 8 rows of one feature column via two transposed reads
-    //    (lane 4q+p of group g addresses row base + q, columns n*16 + 4p .. +3). Inline asm with
-    //    counted waits (DW_PF (j, n) steps in flight): hipcc treats the ds_read_tr builtin as
-    //    aliasing the tile DMA in flight and would wait vmcnt(0) before the first one. Row base
-    //    + 16 (hi), + 32 (j) and the second 128-column sub-image (n >= 8) keep the swizzle, so they
-    //    are immediate offsets from 8 per-lane bases (one per n & 7).
-    {
-      uint32_t trb[8];
-      const uint32_t xo = lds_off(xb);
+  };
+  // 3. dW_c += G X_tile: B operand = 8 rows of one feature column via two transposed reads
+  //    (lane 4q+p of group g addresses row base + q, columns n*16 + 4p .. +3). Inline asm with
+  //    counted waits (DW_PF (j, n) steps in flight): hipcc treats the ds_read_tr builtin as
+  //    aliasing the tile DMA in flight and would wait vmcnt(0) before the first one. Row base
+  //    + 16 (hi), + 32 (j) and the second 128-column sub-image (n >= 8) keep the swizzle, so they
+  //    are immediate offsets from 8 per-lane bases (one per n & 7).
+  auto dw = [&](uint32_t xo) {
+    uint32_t trb[8];
 #pragma unroll
-      for (int n = 0; n < 8; ++n) trb[n] = xo + img_off(grp_row(g) + (col >> 2), n * 16 + 4 * (col & 3));
-      i16x4_t tl[2 * NT], th[2 * NT];
-      auto issue = [&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        constexpr int off = (i / NT) * 32 * 256 + ((i % NT) >> 3) * SUB_BYTES;
-        tl[i] = tr_read<off>(trb[i & 7]);
-        th[i] = tr_read<off + 16 * 256>(trb[i & 7]);
-      };
-      constexpr int DW_PF = 6;  // (j, n) steps in flight: 2 * DW_PF reads <= 15 (lgkmcnt field)
-      if constexpr (!(MLAPI_GDW_EXP & (8 | 64))) static_for<DW_PF>(issue);
-      if constexpr (!(MLAPI_GDW_EXP & 8)) static_for<2 * NT>([&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        bf16x8_t xbf;
-        if constexpr (MLAPI_GDW_EXP & 64) {  // experiment: MFMAs only, constant B operand
-          xbf = ones_b;
-        } else {
-          if constexpr (i + DW_PF < 2 * NT) issue(std::integral_constant<int, i + DW_PF>{});
-          constexpr int pending = 2 * (2 * NT - 1 - i < DW_PF ? 2 * NT - 1 - i : DW_PF);
-          lgkm_wait<pending>(tl[i], th[i]);
-          xbf = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, tl[i]), __builtin_bit_cast(bf16x4_t, th[i]), 0,
-                                        1, 2, 3, 4, 5, 6, 7);
-        }
+    for (int n = 0; n < 8; ++n) trb[n] = xo + img_off(grp_row(g) + (col >> 2), n * 16 + 4 * (col & 3));
+    i16x4_t tl[2 * NT], th[2 * NT];
+    auto issue = [&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      constexpr int off = (i / NT) * 32 * 256 + ((i % NT) >> 3) * SUB_BYTES;
+      tl[i] = tr_read<off>(trb[i & 7]);
+      th[i] = tr_read<off + 16 * 256>(trb[i & 7]);
+    };
+    constexpr int DW_PF = 6;  // (j, n) steps in flight: 2 * DW_PF reads <= 15 (lgkmcnt field)
+    if constexpr (!(MLAPI_GDW_EXP & (8 | 64))) static_for<DW_PF>(issue);
+    if constexpr (!(MLAPI_GDW_EXP & 8)) static_for<2 * NT>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      bf16x8_t xbf;
+      if constexpr (MLAPI_GDW_EXP & 64) {  // experiment: MFMAs only, constant B operand
+        xbf = ones_b;
+      } else {
+        if constexpr (i + DW_PF < 2 * NT) issue(std::integral_constant<int, i + DW_PF>{});
+        constexpr int pending = 2 * (2 * NT - 1 - i < DW_PF ? 2 * NT - 1 - i : DW_PF);
+        lgkm_wait<pending>(tl[i], th[i]);
+        xbf = __builtin_shufflevector(__builtin_bit_cast(bf16x4_t, tl[i]), __builtin_bit_cast(bf16x4_t, th[i]), 0,
+                                      1, 2, 3, 4, 5, 6, 7);
+      }
 #pragma unroll
-        for (int h = 0; h < NC; ++h) {
-          if constexpr (!(MLAPI_GDW_EXP & 2))
-            acc[h][i % NT] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[h][i / NT], xbf, acc[h][i % NT], 0, 0, 0);
-          else
-            acc[h][i % NT] += __builtin_bit_cast(f32x4_t, xbf);
-          if constexpr (i % NT == NT - 1)
-            acc_db[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[h][i / NT], ones_b, acc_db[h], 0, 0, 0);
-        }
-      });
-    }
+      for (int h = 0; h < NC; ++h) {
+        if constexpr (!(MLAPI_GDW_EXP & 2))
+          acc[h][i % NT] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[h][i / NT], xbf, acc[h][i % NT], 0, 0, 0);
+        else
+          acc[h][i % NT] += __builtin_bit_cast(f32x4_t, xbf);
+        if constexpr (i % NT == NT - 1)
+          acc_db[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[h][i / NT], ones_b, acc_db[h], 0, 0, 0);
+      }
+    });
+  };
+  const uint32_t smem_off = lds_off(smem);
 
-    if (MLAPI_GDW_EXP & 16) {
-    } else if (t + 2 < t_end) {
-      MLAPI_RAW_BARRIER()  // every wave is done reading `buf`
-      MLAPI_DMA_TILE(t + 2, buf)
-      __builtin_amdgcn_s_waitcnt(kWaitTile);  // tile t+1 landed, t+2 flies
+  if constexpr (!PIPE) {
+    int buf = 0;
+    MLAPI_DMA_TILE(t_begin, 0)
+    if (t_begin + 1 < t_end) {
+      MLAPI_DMA_TILE(t_begin + 1, 1)
+      __builtin_amdgcn_s_waitcnt(kWaitTile);  // W, bias and tile 0 landed; tile 1 may still fly
     } else {
       __builtin_amdgcn_s_waitcnt(kWaitAll);
     }
-    if (!(MLAPI_GDW_EXP & 16)) {
-      MLAPI_RAW_BARRIER()
+    MLAPI_RAW_BARRIER()
+    for (int t = t_begin; t < t_end; ++t) {
+      const uint32_t xo = smem_off + buf * BUF_BYTES;
+      const int rows_left = (int)min<int64_t>(ROWS, B - (int64_t)t * ROWS);
+      f32x4_t z[NC][4];
+      init_z(z);
+      logits(xo, z, std::true_type{});
+      wait_meta();
+      if (rows_left == ROWS)
+        epilogue(std::false_type{}, z, rows_left);
+      else
+        epilogue(std::true_type{}, z, rows_left);
+      row_stats(xo + X_BYTES, rows_left);
+      dw(xo);
+      if (MLAPI_GDW_EXP & 16) {
+      } else if (t + 2 < t_end) {
+        MLAPI_RAW_BARRIER()  // every wave is done reading `buf`
+        MLAPI_DMA_TILE(t + 2, buf)
+        __builtin_amdgcn_s_waitcnt(kWaitTile);  // tile t+1 landed, t+2 flies
+      } else {
+        __builtin_amdgcn_s_waitcnt(kWaitAll);
+      }
+      if (!(MLAPI_GDW_EXP & 16)) {
+        MLAPI_RAW_BARRIER()
+      }
+      buf ^= 1;
     }
-    buf ^= 1;
+  } else {
+    // prologue: tiles 0, 1, 2 in flight; 0 and 1 landed before the first logits
+    MLAPI_DMA_TILE(t_begin, 0)
+    if (t_begin + 1 < t_end) MLAPI_DMA_TILE(t_begin + 1, 1)
+    if (t_begin + 2 < t_end) {
+      MLAPI_DMA_TILE(t_begin + 2, 2)
+      __builtin_amdgcn_s_waitcnt(kWaitTile);
+    } else {
+      __builtin_amdgcn_s_waitcnt(kWaitAll);
+    }
+    MLAPI_RAW_BARRIER()
+    f32x4_t zc[NC][4];
+    init_z(zc);
+    logits(smem_off, zc, std::false_type{});
+    int bcur = 0;
+    for (int t = t_begin; t < t_end; ++t) {
+      const int bnext = bcur == NBUF - 1 ? 0 : bcur + 1;
+      const uint32_t xo = smem_off + bcur * BUF_BYTES;
+      const uint32_t xn = smem_off + bnext * BUF_BYTES;  // tile t+1 (stale data on the last tile: unused)
+      const int rows_left = (int)min<int64_t>(ROWS, B - (int64_t)t * ROWS);
+      read_meta(xo + X_BYTES);
+      wait_meta();
+      // logits of tile t+1 and the epilogue of tile t: one basic block per epilogue variant, so the
+      // scheduler can interleave the epilogue's VALU with the independent MFMAs
+      f32x4_t zn[NC][4];
+      init_z(zn);
+      if (rows_left == ROWS) {
+        logits(xn, zn, std::false_type{});
+        epilogue(std::false_type{}, zc, rows_left);
+      } else {
+        logits(xn, zn, std::false_type{});
+        epilogue(std::true_type{}, zc, rows_left);
+      }
+      row_stats(xo + X_BYTES, rows_left);
+      dw(xo);
+      if (t + 3 < t_end) {
+        MLAPI_RAW_BARRIER()  // every wave is done reading buffer bcur (tile t)
+        MLAPI_DMA_TILE(t + 3, bcur)
+        __builtin_amdgcn_s_waitcnt(kWaitTile);  // tile t+2 landed, t+3 flies
+      } else {
+        __builtin_amdgcn_s_waitcnt(kWaitAll);
+      }
+      MLAPI_RAW_BARRIER()
+#pragma unroll
+      for (int h = 0; h < NC; ++h)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) zc[h][mt] = zn[h][mt];
+      bcur = bnext;
+    }
   }
 #undef MLAPI_RAW_BARRIER
 #undef MLAPI_DMA_TILE
@@ -504,6 +571,7 @@ struct GdwLayout {
 
 int g_force_row_groups = 0;  // benchmark hooks (softmax_grad_dw_force_plan)
 int g_force_nc = 0;
+int g_force_pipe = 0;  // 0 auto (off), 1 off, 2 on (NC = 2 only)
 
 int auto_nc(int K) { return g_force_nc > 0 ? g_force_nc : (K >= 256 ? 2 : 1); }
 
@@ -532,9 +600,10 @@ GdwLayout gdw_layout(int64_t B, int K, int F, int nc) {
 
 bool softmax_grad_dw_supported(int F) { return F == 128 || F == 256; }
 
-void softmax_grad_dw_force_plan(int row_groups, int nc) {
+void softmax_grad_dw_force_plan(int row_groups, int nc, int pipe) {
   g_force_row_groups = row_groups;
   g_force_nc = nc;
+  g_force_pipe = pipe;
 }
 
 size_t softmax_grad_dw_workspace(int64_t B, int K, int F) {  // enough for either class-tile plan
@@ -577,10 +646,22 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
   const bool ovr = kind == KIND_OVR;
   auto launch = [&](auto ks, auto nc) {
     constexpr int KS_ = decltype(ks)::value, NC_ = decltype(nc)::value;
+    // measured equal to the plain NC = 2 loop (127-130 us either way at B=65536, K=1000; the
+    // scheduler interleaves only part of the epilogue), so the simpler loop stays the default
+    const bool pipe = NC_ == 2 && g_force_pipe == 2;
+    if constexpr (NC_ == 2) {
+      if (pipe) {
+        if (ovr)
+          hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, true, 2, true>), grid, dim3(256), 0, stream, args);
+        else
+          hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, false, 2, true>), grid, dim3(256), 0, stream, args);
+        return;
+      }
+    }
     if (ovr)
-      hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, true, NC_>), grid, dim3(256), 0, stream, args);
+      hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, true, NC_, false>), grid, dim3(256), 0, stream, args);
     else
-      hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, false, NC_>), grid, dim3(256), 0, stream, args);
+      hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, false, NC_, false>), grid, dim3(256), 0, stream, args);
   };
   using I4 = std::integral_constant<int, 4>;
   using I8 = std::integral_constant<int, 8>;

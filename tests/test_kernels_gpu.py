@@ -243,14 +243,15 @@ def test_softmax_train_grad(B, F, K, kind):
     assert torch.all(dW[:, F + 1:] == 0)  # padding columns of X_aug are zero
 
 
-@pytest.mark.parametrize("nc", [1, 2])
+@pytest.mark.parametrize("nc,pipe", [(1, 0), (2, 1), (2, 2)])
 @pytest.mark.parametrize("B,F,K,kind,groups", [
     (1000, 256, 1000, Kind.MULTINOMIAL, 0), (8192, 256, 1000, Kind.MULTINOMIAL, 0),
     (4099, 128, 37, Kind.MULTINOMIAL, 0), (77, 128, 10, Kind.OVR, 0), (300, 256, 130, Kind.OVR, 0),
     (64, 256, 3, Kind.MULTINOMIAL, 0), (20000, 128, 200, Kind.OVR, 3), (65, 256, 64, Kind.MULTINOMIAL, 1),
     (9000, 256, 300, Kind.OVR, 0)])
-def test_softmax_grad_dw_fused(B, F, K, kind, groups, nc):
-    """Fused G + dW kernel (softmax_grad_dw.hip) vs the fp32 oracle at 16 and 32 classes per wave:
+def test_softmax_grad_dw_fused(B, F, K, kind, groups, nc, pipe):
+    """Fused G + dW kernel (softmax_grad_dw.hip) vs the fp32 oracle at 16 and 32 classes per wave
+    (the latter with and without the cross-tile pipeline):
     ragged row tiles, partial class groups, both kinds, forced row-group counts; reruns are bitwise
     identical (slab sums, no atomics)."""
     from mlapi_amd._native import C
@@ -261,7 +262,7 @@ def test_softmax_grad_dw_fused(B, F, K, kind, groups, nc):
     y = torch.randint(0, K, (B,), generator=torch.Generator().manual_seed(44), dtype=torch.int32).to(DEV)
     Xa = ops.augment_features(X, Fa)
     Wb = W.to(torch.bfloat16)
-    C().softmax_grad_dw_force_plan(groups, nc)
+    C().softmax_grad_dw_force_plan(groups, nc, pipe)
     try:
         bufs = ops.SoftmaxTrainBuffers(B, K, F, X.device, dw_path="fused")
         assert bufs.fused and bufs.G is None
@@ -270,7 +271,7 @@ def test_softmax_grad_dw_fused(B, F, K, kind, groups, nc):
         dW2, st2 = ops.softmax_train_grad(Xa, Wb, b, y, kind, bufs=bufs)
         torch.cuda.synchronize()
     finally:
-        C().softmax_grad_dw_force_plan(0, 0)
+        C().softmax_grad_dw_force_plan(0, 0, 0)
     assert torch.equal(dW1, dW2) and torch.equal(st1, st2)
     _, dW_ref, loss_ref, corr_ref = ref.softmax_train_ref(Xa, y, ops.augment_weights(Wb.float(), b, Fa), kind)
     scale = dW_ref.abs().max().item() + 1e-6

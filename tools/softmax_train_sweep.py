@@ -57,14 +57,14 @@ for S in (2, 4, 8, 16, 32, 64):
     res[f"dW_bmm_S{S}_maxdiff"] = (out - ref).abs().max().item()
 # fused path: rowstats + G/dW kernel + slab sums, whole call
 stf = torch.zeros(2, device=dev)
-for nc in (1, 2):
-    for groups in (0, 16, 32, 64, 128):
-        C().softmax_grad_dw_force_plan(groups, nc)
+for nc, pipe in ((1, 0), (2, 1), (2, 2)):
+    for groups in (0, 16, 32, 64):
+        C().softmax_grad_dw_force_plan(groups, nc, pipe)
         fb = ops.SoftmaxTrainBuffers(B, K, F, dev, dw_path="fused")
-        res[f"fused_nc{nc}_groups{groups}_us"] = timeit(
+        res[f"fused_nc{nc}_pipe{pipe}_groups{groups}_us"] = timeit(
             lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=fb, dW_out=out, stats_out=stf))
-        res[f"fused_nc{nc}_groups{groups}_maxdiff"] = (out - ref).abs().max().item()
-C().softmax_grad_dw_force_plan(0, 0)
+        res[f"fused_nc{nc}_pipe{pipe}_groups{groups}_maxdiff"] = (out - ref).abs().max().item()
+C().softmax_grad_dw_force_plan(0, 0, 0)
 gb = ops.SoftmaxTrainBuffers(B, K, F, dev, dw_path="gemm")
 res["gemm_path_total_us"] = timeit(lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=gb, dW_out=out, stats_out=stf))
 res["dW_ref_absmax"] = ref.abs().max().item()
