@@ -206,15 +206,15 @@ __global__ __launch_bounds__(256) void train_binary_grad_kernel(const T* __restr
   }
 }
 
-// Deterministic slab reduction: 16 columns x 16 partitions per 256-thread block. Partition p sums
-// slabs p, p+16, p+32, ... in increasing order (each partition row reads 16 consecutive columns =
-// one coalesced 64-B segment per slab), then the 16 partials are added in fixed order through LDS.
+// Deterministic slab reduction: COLS columns x PARTS partitions per 256-thread block. Partition p
+// sums slabs p, p+PARTS, ... in increasing order (each partition row reads COLS consecutive
+// columns of a slab), then the PARTS partials are added in fixed order through LDS.
 // A single thread per column walking all slabs serially was the bottleneck of the training step
 // (232 us vs 22 us for the fused gradient kernel: profiles/r1_first/train_kernel_stats.csv).
 // FUSE_SGD: when no all-reduce separates them (one replica), the SGD update of the parameter
 // vector is applied by the same thread that produced the column's gradient sum (saves a launch).
-constexpr int RED_COLS = 16;
-constexpr int RED_PARTS = 16;
+// Narrow parameter vectors (binary logistic on a handful of features: width ~5) use 4-column
+// groups so 64 partitions share the slab walk instead of 16 (11 of 16 columns would idle).
 struct SgdArgs {
   float* params = nullptr;
   float* mom = nullptr;
@@ -222,9 +222,10 @@ struct SgdArgs {
   float lr = 0.f, inv_n = 0.f, l2 = 0.f, momentum = 0.f;
 };
 
-template <typename T, bool FUSE_SGD>
+template <typename T, bool FUSE_SGD, int RED_COLS>
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(const T* __restrict__ slabs, int nslabs, int width,
                                                            T* __restrict__ out, SgdArgs sgd) {
+  constexpr int RED_PARTS = 256 / RED_COLS;
   __shared__ T part[RED_PARTS][RED_COLS];
   const int c = threadIdx.x % RED_COLS;
   const int p = threadIdx.x / RED_COLS;
@@ -265,16 +266,26 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const T* __restrict__
   }
 }
 
+template <typename T, int COLS>
+void launch_reduce_slabs_cols(const T* slabs, int nslabs, int width, T* out, hipStream_t stream,
+                              const SgdArgs* sgd) {
+  const dim3 grid((unsigned)((width + COLS - 1) / COLS));
+  if (sgd != nullptr)
+    hipLaunchKernelGGL((reduce_slabs_kernel<T, true, COLS>), grid, dim3(256), 0, stream, slabs, nslabs, width, out,
+                       *sgd);
+  else
+    hipLaunchKernelGGL((reduce_slabs_kernel<T, false, COLS>), grid, dim3(256), 0, stream, slabs, nslabs, width,
+                       out, SgdArgs{});
+  MLAPI_HIP_CHECK(hipGetLastError());
+}
+
 template <typename T>
 void launch_reduce_slabs(const T* slabs, int nslabs, int width, T* out, hipStream_t stream,
                          const SgdArgs* sgd = nullptr) {
-  const dim3 grid((unsigned)((width + RED_COLS - 1) / RED_COLS));
-  if (sgd != nullptr)
-    hipLaunchKernelGGL((reduce_slabs_kernel<T, true>), grid, dim3(256), 0, stream, slabs, nslabs, width, out, *sgd);
+  if (width <= 8)
+    launch_reduce_slabs_cols<T, 4>(slabs, nslabs, width, out, stream, sgd);
   else
-    hipLaunchKernelGGL((reduce_slabs_kernel<T, false>), grid, dim3(256), 0, stream, slabs, nslabs, width, out,
-                       SgdArgs{});
-  MLAPI_HIP_CHECK(hipGetLastError());
+    launch_reduce_slabs_cols<T, 16>(slabs, nslabs, width, out, stream, sgd);
 }
 
 struct BinPlan {
