@@ -93,8 +93,13 @@ py::dict stats_dict(const EngineStats& s) {
   d["queue_depth"] = s.queue_depth;
   d["model_version"] = s.model_version;
   d["healthy"] = s.healthy;
-  d["kernel_launches"] = s.kernel_launches;
+  d["dropped"] = s.dropped;
   d["rejected"] = s.rejected;
+  py::dict paths;
+  static const char* names[PATH_COUNT] = {"small", "gemv", "gemm", "generic"};
+  for (int i = 0; i < PATH_COUNT; ++i) paths[names[i]] = s.path_batches[i];
+  d["path_batches"] = paths;
+  d["inline_batches"] = s.inline_batches;
   return d;
 }
 
@@ -292,9 +297,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("fail_every", &EngineConfig::fail_every)
       .def_readwrite("delay_us", &EngineConfig::delay_us)
       .def_readwrite("spin_us", &EngineConfig::spin_us)
-      .def_readwrite("persistent", &EngineConfig::persistent)
-      .def_readwrite("max_queue", &EngineConfig::max_queue)
-      .def_readwrite("persistent_idle_ms", &EngineConfig::persistent_idle_ms);
+      .def_readwrite("wide_dtype", &EngineConfig::wide_dtype)
+      .def_readwrite("inline_args", &EngineConfig::inline_args)
+      .def_readwrite("max_queue", &EngineConfig::max_queue);
 
   py::class_<PySink>(m, "PySink").def(py::init<>()).def("fd", &PySink::fd).def("drain", &PySink::drain);
 
@@ -324,6 +329,14 @@ PYBIND11_MODULE(_C, m) {
              auto mm = e.model();
              return mm ? mm->F : 0;
            })
+      .def("model_path",
+           [](Engine& e) -> std::string {
+             static const char* names[PATH_COUNT] = {"small", "gemv", "gemm", "generic"};
+             auto mm = e.model();
+             return mm ? names[mm->path] : "";
+           })
+      .def("inject_drop", &Engine::inject_drop, py::arg("on"))
+      .def("mark_healthy", &Engine::mark_healthy)
       .def(
           "submit",
           [](Engine& e, py::array_t<double, py::array::c_style | py::array::forcecast> x, uint64_t tag, PySink& sink) {
@@ -378,6 +391,11 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("server_header", &ServerConfig::server_header)
       .def_readwrite("fast_path", &ServerConfig::fast_path)
       .def_readwrite("max_body", &ServerConfig::max_body)
+      .def_readwrite("pipeline_cap", &ServerConfig::pipeline_cap)
+      .def_readwrite("access_log", &ServerConfig::access_log)
+      .def_readwrite("access_log_fd", &ServerConfig::access_log_fd)
+      .def_readwrite("health_dispatch", &ServerConfig::health_dispatch)
+      .def_readwrite("health_probe_ms", &ServerConfig::health_probe_ms)
       .def_readwrite("backlog", &ServerConfig::backlog);
 
   // ---- native RCCL communicator (csrc/dist/comm.h)
@@ -481,6 +499,9 @@ PYBIND11_MODULE(_C, m) {
         d["connections"] = st.connections;
         d["errors"] = st.errors;
         d["bad_requests"] = st.bad_requests;
+        d["listen_closes"] = st.listen_closes;
+        d["accepting"] = st.accepting;
+        d["listeners"] = s.listeners();
         return d;
       });
 

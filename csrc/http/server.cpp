@@ -14,6 +14,8 @@
 #include <cerrno>
 #include <cmath>
 #include <cstdlib>
+#include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <ctime>
 #include <stdexcept>
@@ -57,7 +59,36 @@ static inline std::string trim(const std::string& s) {
 
 namespace {
 
-// Skip one JSON value starting at p[i]; returns false on malformed input.
+inline bool is_hex(char c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); }
+
+// RFC 8259 number grammar (no value conversion): -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
+bool scan_number(const char* p, size_t n, size_t& i) {
+  if (i < n && p[i] == '-') ++i;
+  if (i >= n) return false;
+  if (p[i] == '0') {
+    ++i;
+  } else if (p[i] >= '1' && p[i] <= '9') {
+    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
+  } else {
+    return false;
+  }
+  if (i < n && p[i] == '.') {
+    ++i;
+    if (i >= n || !(p[i] >= '0' && p[i] <= '9')) return false;
+    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
+  }
+  if (i < n && (p[i] == 'e' || p[i] == 'E')) {
+    ++i;
+    if (i < n && (p[i] == '+' || p[i] == '-')) ++i;
+    if (i >= n || !(p[i] >= '0' && p[i] <= '9')) return false;
+    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
+  }
+  return true;
+}
+
+// Skip one JSON value starting at p[i]; returns false on malformed input, and also on anything
+// json.loads might judge differently from a strict scanner (non-ASCII bytes in strings, which
+// depend on the body's UTF-8 validity): those requests go to the Python slow path instead.
 bool skip_value(const char* p, size_t n, size_t& i, int depth) {
   if (depth > 64) return false;
   while (i < n && is_ws(p[i])) ++i;
@@ -68,10 +99,20 @@ bool skip_value(const char* p, size_t n, size_t& i, int depth) {
     while (i < n) {
       const unsigned char ch = (unsigned char)p[i];
       if (ch == '\\') {
-        i += 2;
+        if (i + 1 >= n) return false;
+        const char e = p[i + 1];
+        if (e == 'u') {
+          if (n - i < 6 || !is_hex(p[i + 2]) || !is_hex(p[i + 3]) || !is_hex(p[i + 4]) || !is_hex(p[i + 5]))
+            return false;
+          i += 6;
+        } else if (e == '"' || e == '\\' || e == '/' || e == 'b' || e == 'f' || e == 'n' || e == 'r' || e == 't') {
+          i += 2;
+        } else {
+          return false;
+        }
         continue;
       }
-      if (ch < 0x20) return false;
+      if (ch < 0x20 || ch >= 0x80) return false;
       if (ch == '"') {
         ++i;
         return true;
@@ -116,39 +157,14 @@ bool skip_value(const char* p, size_t n, size_t& i, int depth) {
   if (c == 't' && n - i >= 4 && memcmp(p + i, "true", 4) == 0) { i += 4; return true; }
   if (c == 'f' && n - i >= 5 && memcmp(p + i, "false", 5) == 0) { i += 5; return true; }
   if (c == 'n' && n - i >= 4 && memcmp(p + i, "null", 4) == 0) { i += 4; return true; }
-  if (c == '-' || (c >= '0' && c <= '9')) {
-    ++i;
-    while (i < n && ((p[i] >= '0' && p[i] <= '9') || p[i] == '.' || p[i] == 'e' || p[i] == 'E' || p[i] == '+' ||
-                     p[i] == '-'))
-      ++i;
-    return true;
-  }
+  if (c == '-' || (c >= '0' && c <= '9')) return scan_number(p, n, i);
   return false;  // NaN / Infinity / garbage -> slow path
 }
 
 // Strict JSON number (RFC 8259 grammar) -> finite double.
 bool parse_number(const char* p, size_t n, size_t& i, double* out) {
   const size_t s = i;
-  if (i < n && p[i] == '-') ++i;
-  if (i >= n) return false;
-  if (p[i] == '0') {
-    ++i;
-  } else if (p[i] >= '1' && p[i] <= '9') {
-    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
-  } else {
-    return false;
-  }
-  if (i < n && p[i] == '.') {
-    ++i;
-    if (i >= n || !(p[i] >= '0' && p[i] <= '9')) return false;
-    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
-  }
-  if (i < n && (p[i] == 'e' || p[i] == 'E')) {
-    ++i;
-    if (i < n && (p[i] == '+' || p[i] == '-')) ++i;
-    if (i >= n || !(p[i] >= '0' && p[i] <= '9')) return false;
-    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
-  }
+  if (!scan_number(p, n, i)) return false;
   const size_t len = i - s;
   if (len > 400) return false;  // absurd literals: let Python decide
   char buf[416];
@@ -167,7 +183,7 @@ bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>&
   const size_t nk = names.size();
   if (nk > 4096) return false;
   std::vector<char> seen(nk, 0);
-  size_t i = 0;
+  size_t i = 0, hint = 0;
   while (i < n && is_ws(p[i])) ++i;
   if (i >= n || p[i] != '{') return false;
   ++i;
@@ -181,7 +197,8 @@ bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>&
       ++i;
       const size_t ks = i;
       while (i < n && p[i] != '"') {
-        if (p[i] == '\\' || (unsigned char)p[i] < 0x20) return false;  // escaped keys -> slow path
+        // escaped or non-ASCII keys -> slow path
+        if (p[i] == '\\' || (unsigned char)p[i] < 0x20 || (unsigned char)p[i] >= 0x80) return false;
         ++i;
       }
       if (i >= n) return false;
@@ -191,13 +208,20 @@ bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>&
       if (i >= n || p[i] != ':') return false;
       ++i;
       while (i < n && is_ws(p[i])) ++i;
+      // keys usually arrive in schema order: try the one after the last match first, so a wide
+      // model's body parses in O(F) instead of O(F^2) comparisons
       int which = -1;
-      for (size_t k = 0; k < nk; ++k) {
-        if (names[k].size() == klen && memcmp(names[k].data(), p + ks, klen) == 0) {
-          which = (int)k;
-          break;
+      if (hint < nk && names[hint].size() == klen && memcmp(names[hint].data(), p + ks, klen) == 0) {
+        which = (int)hint;
+      } else {
+        for (size_t k = 0; k < nk; ++k) {
+          if (names[k].size() == klen && memcmp(names[k].data(), p + ks, klen) == 0) {
+            which = (int)k;
+            break;
+          }
         }
       }
+      if (which >= 0) hint = (size_t)which + 1;
       if (which >= 0) {
         double v;
         if (!parse_number(p, n, i, &v)) return false;
@@ -245,8 +269,10 @@ struct Conn {
   bool close_after = false;   // close once `out` is flushed
   bool sent_continue = false;
   bool epollout = false;
+  bool paused = false;        // EPOLLIN dropped: too many unparsed bytes behind an outstanding request
   std::string client_host, server_host;
   int client_port = 0, server_port = 0;
+  std::string req_line;       // access log: request line of the outstanding request
 };
 
 struct FastBatch {
@@ -358,7 +384,7 @@ class IoThread : public Sink {
     wake();
   }
 
-  std::atomic<uint64_t> n_fast{0}, n_slow{0}, n_resp{0}, n_conn{0}, n_err{0}, n_bad{0};
+  std::atomic<uint64_t> n_fast{0}, n_slow{0}, n_resp{0}, n_conn{0}, n_err{0}, n_bad{0}, n_listen_close{0};
 
  private:
   void wake() {
@@ -380,10 +406,13 @@ class IoThread : public Sink {
         auto it = conns_.find(id);
         if (it == conns_.end()) continue;
         it->second->waiting = false;
-        if (r != 0)  // SUBMIT_BUSY, or a partial accept
+        if (r != 0) {  // SUBMIT_BUSY, or a partial accept
           service_unavailable(it->second.get());
-        else
+          log_access(it->second.get(), 503, "Service Unavailable");
+        } else {
           internal_error(it->second.get());
+          log_access(it->second.get(), 500, "Internal Server Error");
+        }
         flush(it->second.get());
       }
     }
@@ -398,11 +427,12 @@ class IoThread : public Sink {
     epoll_event evs[256];
     while (!stop_.load()) {
       flush_submits();
+      flush_log();
       const int n = epoll_wait(epfd_, evs, 256, 200);
       for (int i = 0; i < n; ++i) {
         const uint64_t id = evs[i].data.u64;
         if (id == ID_LISTEN) {
-          accept_all();
+          if (lfd_ >= 0) accept_all();
         } else if (id == ID_EVENT) {
           uint64_t v;
           ssize_t r = read(evfd_, &v, sizeof v);
@@ -413,12 +443,90 @@ class IoThread : public Sink {
           auto it = conns_.find(id);
           if (it == conns_.end()) continue;
           Conn* c = it->second.get();
-          bool alive = true;
-          if (evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR | EPOLLRDHUP)) alive = on_readable(c);
-          if (alive && (evs[i].events & EPOLLOUT)) alive = flush(c);
+          // One misbehaving connection (e.g. an allocation failure while buffering its request)
+          // must never take the process down: drop that connection and keep serving.
+          try {
+            bool alive = true;
+            if (evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR | EPOLLRDHUP)) alive = on_readable(c);
+            if (alive && (evs[i].events & EPOLLOUT)) alive = flush(c);
+          } catch (const std::exception&) {
+            n_bad.fetch_add(1, std::memory_order_relaxed);
+            if (conns_.count(id)) close_conn(c);
+          }
         }
       }
+      apply_listen_state();
     }
+  }
+
+  // Health-aware dispatch (SO_REUSEPORT group membership): an IO thread whose engine is unhealthy
+  // closes its listening socket, so the kernel stops routing new connections of the shared port
+  // to this rank; it re-binds once the engine is healthy again. Connections already accepted keep
+  // being served (their requests complete with 500 while the engine is down).
+  void apply_listen_state() {
+    const bool want = srv_->accepting();
+    if (want == listening_.load(std::memory_order_relaxed)) return;
+    if (!want) {
+      epoll_ctl(epfd_, EPOLL_CTL_DEL, lfd_, nullptr);
+      close(lfd_);
+      lfd_ = -1;
+      listening_ = false;
+      n_listen_close.fetch_add(1, std::memory_order_relaxed);
+      return;
+    }
+    try {
+      int bp = 0;
+      const auto& cfg = srv_->config();
+      lfd_ = make_listener(cfg.host, srv_->port(), true, cfg.backlog, &bp);
+    } catch (const std::exception&) {
+      return;  // retried on the next loop iteration (<= 200 ms)
+    }
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = ID_LISTEN;
+    epoll_ctl(epfd_, EPOLL_CTL_ADD, lfd_, &ev);
+    listening_ = true;
+  }
+
+ public:
+  bool listening() const { return listening_.load(std::memory_order_relaxed); }
+
+ private:
+  // uvicorn-format access log ('INFO:     127.0.0.1:5000 - "POST /predict HTTP/1.1" 200 OK'),
+  // buffered per IO thread and written with one write(2) per epoll round.
+  void log_access(Conn* c, int status, const char* reason) {
+    if (!srv_->config().access_log || c->req_line.empty()) return;
+    log_ += "INFO:     ";
+    log_ += c->client_host;
+    log_ += ':';
+    log_ += std::to_string(c->client_port);
+    log_ += " - \"";
+    log_ += c->req_line;
+    log_ += "\" ";
+    log_ += std::to_string(status);
+    log_ += ' ';
+    log_ += reason;
+    log_ += '\n';
+    c->req_line.clear();
+  }
+  void flush_log() {
+    if (log_.empty()) return;
+    size_t off = 0;
+    while (off < log_.size()) {
+      const ssize_t w = write(srv_->config().access_log_fd, log_.data() + off, log_.size() - off);
+      if (w <= 0) break;
+      off += (size_t)w;
+    }
+    log_.clear();
+  }
+
+  // EPOLLIN is dropped while a request is outstanding and more than pipeline_cap bytes of later
+  // requests are already buffered (a client that keeps writing cannot grow server memory).
+  void update_events(Conn* c) {
+    epoll_event ev{};
+    ev.events = EPOLLRDHUP | (c->paused ? 0u : (uint32_t)EPOLLIN) | (c->epollout ? (uint32_t)EPOLLOUT : 0u);
+    ev.data.u64 = c->id;
+    epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev);
   }
 
   void accept_all() {
@@ -475,6 +583,10 @@ class IoThread : public Sink {
       close_conn(c);
       return false;
     }
+    if (c->waiting && !c->paused && c->in.size() - c->in_pos > srv_->config().pipeline_cap) {
+      c->paused = true;
+      update_events(c);
+    }
     return process(c);
   }
 
@@ -485,11 +597,8 @@ class IoThread : public Sink {
         c->out_pos += (size_t)w;
       } else if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
         if (!c->epollout) {
-          epoll_event ev{};
-          ev.events = EPOLLIN | EPOLLRDHUP | EPOLLOUT;
-          ev.data.u64 = c->id;
-          epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev);
           c->epollout = true;
+          update_events(c);
         }
         return true;
       } else if (w < 0 && errno == EINTR) {
@@ -502,11 +611,8 @@ class IoThread : public Sink {
     c->out.clear();
     c->out_pos = 0;
     if (c->epollout) {
-      epoll_event ev{};
-      ev.events = EPOLLIN | EPOLLRDHUP;
-      ev.data.u64 = c->id;
-      epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev);
       c->epollout = false;
+      update_events(c);
     }
     if (c->close_after && !c->waiting) {
       close_conn(c);
@@ -581,10 +687,13 @@ class IoThread : public Sink {
           ok = append_py_float(body, cp.p);
           body += '}';
         }
-        if (ok)
+        if (ok) {
           append_response(c, 200, "OK", "application/json", body);
-        else
+          log_access(c, 200, "OK");
+        } else {
           internal_error(c);
+          log_access(c, 500, "Internal Server Error");
+        }
         process(c);  // dispatches pipelined requests, then flushes (may close c)
       }
     }
@@ -593,6 +702,11 @@ class IoThread : public Sink {
       if (it == conns_.end()) continue;
       Conn* c = it->second.get();
       c->waiting = false;
+      if (!c->req_line.empty() && sr.bytes.size() > 12) {  // "HTTP/1.1 NNN reason\r\n..."
+        const size_t le = sr.bytes.find("\r\n");
+        const std::string st = sr.bytes.substr(13, le == std::string::npos ? 0 : le - 13);
+        log_access(c, atoi(sr.bytes.c_str() + 9), st.c_str());
+      }
       c->out += sr.bytes;
       if (sr.close) c->close_after = true;
       n_resp.fetch_add(1, std::memory_order_relaxed);
@@ -611,6 +725,10 @@ class IoThread : public Sink {
     if (c->in_pos > 0 && (c->in_pos == c->in.size() || c->in_pos > (1u << 16))) {
       c->in.erase(0, c->in_pos);
       c->in_pos = 0;
+    }
+    if (c->paused && (!c->waiting || c->in.size() - c->in_pos <= srv_->config().pipeline_cap)) {
+      c->paused = false;
+      update_events(c);
     }
     return flush(c);
   }
@@ -648,6 +766,7 @@ class IoThread : public Sink {
     }
     std::string method = line.substr(0, s1), target = line.substr(s1 + 1, s2 - s1 - 1),
                 version = line.substr(s2 + 1);
+    if (cfg.access_log) c->req_line = line;
     if (version != "HTTP/1.1" && version != "HTTP/1.0") {
       bad_request(c, 400, "Bad Request");
       return -1;
@@ -706,14 +825,21 @@ class IoThread : public Sink {
           if (expect100 && !c->sent_continue) send_continue(c);
           return 0;
         }
-        const std::string szs(base + pos, (size_t)(static_cast<const char*>(ce) - (base + pos)));
-        char* endp = nullptr;
-        const unsigned long long sz = strtoull(szs.c_str(), &endp, 16);
-        if (endp == szs.c_str()) {
+        // chunk-size = 1*HEXDIG [ ; ext ]: at most 15 hex digits (no sign, no 0x, no overflow)
+        const char* sp = base + pos;
+        const char* se = static_cast<const char*>(ce);
+        size_t sz = 0;
+        int ndig = 0;
+        while (sp < se && is_hex(*sp) && ndig < 16) {
+          const char h = *sp++;
+          sz = (sz << 4) | (size_t)(h <= '9' ? h - '0' : (h | 0x20) - 'a' + 10);
+          ++ndig;
+        }
+        if (ndig == 0 || ndig > 15 || (sp < se && *sp != ';' && *sp != ' ' && *sp != '\t')) {
           bad_request(c, 400, "Bad Request");
           return -1;
         }
-        pos = (size_t)(static_cast<const char*>(ce) - base) + 2;
+        pos = (size_t)(se - base) + 2;
         if (sz == 0) {
           // trailers until empty line
           const void* te = memmem(base + pos, avail - pos, "\r\n", 2);
@@ -726,13 +852,17 @@ class IoThread : public Sink {
           pos += 2;
           break;
         }
-        if (body.size() + sz > cfg.max_body) {
+        if (sz > cfg.max_body - std::min(body.size(), cfg.max_body)) {  // no overflow: sz < 2^60
           bad_request(c, 413, "Payload Too Large");
           return -1;
         }
         if (avail - pos < sz + 2) {
           if (expect100 && !c->sent_continue) send_continue(c);
           return 0;
+        }
+        if (base[pos + sz] != '\r' || base[pos + sz + 1] != '\n') {
+          bad_request(c, 400, "Bad Request");
+          return -1;
         }
         body.append(base + pos, sz);
         pos += sz + 2;
@@ -761,15 +891,17 @@ class IoThread : public Sink {
       const size_t q = target.find('?');
       const std::string path = q == std::string::npos ? target : target.substr(0, q);
       if (path == cfg.predict_path && json_ctype(ctype) && nfeat_ > 0) {
-        double x[256];
-        if (nfeat_ <= 256 && parse_predict_body(body.data(), body.size(), cfg.feature_names, x)) {
-          // queued locally; the whole epoll round goes to the engine in one submit_many()
+        // parsed straight into the pending arena; the whole epoll round goes to the engine in
+        // one submit_many()
+        const size_t at = pend_x_.size();
+        pend_x_.resize(at + nfeat_);
+        if (parse_predict_body(body.data(), body.size(), cfg.feature_names, pend_x_.data() + at)) {
           c->waiting = true;
-          pend_x_.insert(pend_x_.end(), x, x + nfeat_);
           pend_tags_.push_back(c->id);
           n_fast.fetch_add(1, std::memory_order_relaxed);
           return 1;
         }
+        pend_x_.resize(at);
       }
     }
     // ---- slow path: hand to the Python ASGI app
@@ -822,6 +954,8 @@ class IoThread : public Sink {
   std::vector<uint64_t> pend_tags_;
   std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns_;
   uint64_t next_id_ = 16;
+  std::atomic<bool> listening_{true};
+  std::string log_;  // access-log lines of this epoll round
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -831,6 +965,46 @@ HttpServer::HttpServer(Engine* engine, const ServerConfig& cfg) : engine_(engine
 }
 
 HttpServer::~HttpServer() { stop(); }
+
+namespace {
+// Completion of a health probe row: a successful batch re-admits the rank.
+struct ProbeSink : Sink {
+  Engine* eng;
+  std::atomic<int> state{0};  // 0 idle, 1 outstanding
+  explicit ProbeSink(Engine* e) : eng(e) {}
+  void on_complete(const Completion* c, size_t n, const std::shared_ptr<const Model>&) override {
+    if (n > 0 && c[0].status == ST_OK) eng->mark_healthy();
+    state.store(0);
+  }
+};
+}  // namespace
+
+void HttpServer::health_loop() {
+  pthread_setname_np(pthread_self(), "mlapi-health");
+  ProbeSink probe(engine_);
+  std::vector<double> row;
+  while (!health_stop_.load()) {
+    const bool ok = engine_->healthy();
+    if (accepting_.load() != ok) accepting_.store(ok);
+    if (!ok && probe.state.load() == 0) {
+      auto m = engine_->model();
+      if (m) {
+        row.assign((size_t)m->F, 0.0);
+        probe.state.store(1);
+        if (!engine_->submit(row.data(), m->F, 0, &probe)) probe.state.store(0);
+      }
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(std::max(5, cfg_.health_probe_ms)));
+  }
+  // the engine outlives the server: wait for an outstanding probe so its sink stays valid
+  for (int i = 0; i < 2000 && probe.state.load() != 0; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+}
+
+int HttpServer::listeners() const {
+  int n = 0;
+  for (const auto& t : threads_) n += t->listening() ? 1 : 0;
+  return n;
+}
 
 void HttpServer::start() {
   if (started_) return;
@@ -851,6 +1025,7 @@ void HttpServer::start() {
   }
   for (int i = 0; i < cfg_.io_threads; ++i) threads_.push_back(std::make_unique<IoThread>(this, i, fds[i]));
   for (auto& t : threads_) t->start();
+  if (cfg_.health_dispatch) health_ = std::thread([this] { health_loop(); });
   started_ = true;
 }
 
@@ -861,6 +1036,8 @@ void HttpServer::stop() {
     stopping_ = true;
   }
   slow_cv_.notify_all();
+  health_stop_.store(true);
+  if (health_.joinable()) health_.join();
   for (auto& t : threads_) t->stop();
   threads_.clear();
 }
@@ -926,7 +1103,9 @@ ServerStats HttpServer::stats() const {
     s.connections += t->n_conn.load();
     s.errors += t->n_err.load();
     s.bad_requests += t->n_bad.load();
+    s.listen_closes += t->n_listen_close.load();
   }
+  s.accepting = accepting_.load();
   return s;
 }
 

@@ -40,7 +40,15 @@ struct ServerConfig {
   bool fast_path = true;
   size_t max_body = 64u << 20;
   size_t max_header = 64u << 10;
+  size_t pipeline_cap = 1u << 20;  // unparsed bytes buffered behind an outstanding request (then EPOLLIN off)
   int backlog = 4096;
+  bool access_log = false;         // uvicorn-format access log lines
+  int access_log_fd = 2;
+  // DP serving: while the engine is unhealthy, close this rank's SO_REUSEPORT listeners so the
+  // kernel routes new connections to the healthy ranks; a probe row every health_probe_ms
+  // re-admits the rank once a batch succeeds again.
+  bool health_dispatch = false;
+  int health_probe_ms = 100;
 };
 
 struct SlowRequest {
@@ -54,6 +62,8 @@ struct SlowRequest {
 
 struct ServerStats {
   uint64_t fast = 0, slow = 0, responses = 0, connections = 0, errors = 0, bad_requests = 0;
+  uint64_t listen_closes = 0;  // health_dispatch: times this rank left its SO_REUSEPORT group
+  bool accepting = true;
 };
 
 class IoThread;
@@ -72,6 +82,9 @@ class HttpServer {
   ServerStats stats() const;
   const ServerConfig& config() const { return cfg_; }
   Engine* engine() const { return engine_; }
+  // false while health_dispatch has taken this rank out of its SO_REUSEPORT group
+  bool accepting() const { return accepting_.load(std::memory_order_relaxed); }
+  int listeners() const;  // IO threads currently holding a listening socket
 
   // internal, used by IoThread
   void push_slow(SlowRequest&& r);
@@ -86,6 +99,10 @@ class HttpServer {
   std::deque<SlowRequest> slow_q_;
   bool stopping_ = false;
   bool started_ = false;
+  std::atomic<bool> accepting_{true};
+  std::atomic<bool> health_stop_{false};
+  std::thread health_;
+  void health_loop();
 };
 
 // Strict parser for the fast path. Returns true only for a JSON object in which every name in

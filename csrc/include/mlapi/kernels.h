@@ -14,20 +14,22 @@ namespace mlapi {
 void launch_linear_small(int dt, const void* X, int64_t ldx, const void* W, const void* b, int64_t B, int F,
                          int K, int kind, int32_t* out_idx, void* out_p, hipStream_t stream);
 
-// Persistent serving kernel (linear_small.hip): one resident workgroup consumes batches from a
-// host-pinned mailbox (see csrc/runtime/engine.cpp). All pointers are device-visible addresses.
-struct alignas(64) ServeMailSlot {
-  uint32_t seq;    // host -> device: batch index + 1, published last (release)
-  uint32_t n;      // rows in the batch
-  int32_t F, K, kind, pad;
-  uint64_t x;      // const T* rows [n, F]
-  uint64_t W, b;   // model (device memory, dtype of the engine)
-  uint64_t idx;    // int32_t* out
-  uint64_t p;      // T* out
+// Kernel-argument batch (linear_small.hip): a tiny serving batch travels INSIDE the kernel's
+// argument block (rows + W + b), so the kernel reads nothing over the host link: the runtime
+// copies the argument block into device-visible kernarg memory together with the dispatch
+// packet. Only the (idx, p) results go back, written straight into host-mapped memory.
+constexpr int INLINE_X_BYTES = 3072;
+constexpr int INLINE_WB_BYTES = 512;
+struct InlineBatch {
+  int32_t n, F, K, kind;
+  int32_t* out_idx;
+  void* out_p;
+  alignas(16) unsigned char wb[INLINE_WB_BYTES];  // W [K][F] then b [K] (dtype of the launch)
+  alignas(16) unsigned char x[INLINE_X_BYTES];    // rows [n][F]
 };
-constexpr int SERVE_DONE_STRIDE = 16;  // done words are 64 bytes apart (one cache line per slot)
-void launch_serve_persistent(int dt, ServeMailSlot* mail, uint32_t* done, const uint32_t* stop, int nslots,
-                             uint64_t start_seq, uint64_t idle_ticks, hipStream_t stream);
+// true if n rows of F features (and the K x F model) fit the argument block in dtype `dt`
+bool linear_inline_fits(int dt, int64_t n, int F, int K);
+void launch_linear_inline(int dt, const InlineBatch& a, hipStream_t stream);
 
 // ---- gemv_binary.hip: binary LR predict, HBM-streaming GEMV + sigmoid epilogue ----------------
 // X: [B, F] bf16 or f32 row-major; w: [F] same dtype; bias: scalar f32.

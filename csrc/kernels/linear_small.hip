@@ -156,67 +156,37 @@ __global__ __launch_bounds__(256) void linear_generic_kernel(const T* __restrict
   row_predict_generic<T>(X + r * ldx, W, b, F, K, kind, out_idx[r], out_p[r]);
 }
 
-// ---- persistent serving kernel --------------------------------------------------------------
-// One resident workgroup that takes batches from a host-pinned mailbox instead of one kernel
-// launch per batch: the host batcher writes the rows and the header, then publishes the slot's
-// sequence number (release); thread 0 polls it (system-scope acquire over the host link, s_sleep
-// between polls), the block computes the rows straight from / to host memory (zero-copy), and
-// publishes `done` (system-scope release). Batches are consumed strictly in sequence order.
-// The kernel leaves when told to stop or after `idle_ticks` of the constant-rate wall clock
-// without work, so a device-wide synchronize in the process returns once traffic pauses; the
-// engine relaunches it on demand (csrc/runtime/engine.cpp).
+// ---- kernel-argument batch -------------------------------------------------------------------
+// The rows, W and b are fields of the (by-value) kernel argument, which lives in the dispatch's
+// kernarg segment: every load below hits device-visible memory the command processor already
+// staged, none crosses the host link. One lane per row, one or two waves.
+// The argument is read through the kernarg segment pointer (it is the only argument, at offset 0):
+// naming the by-value parameter's fields with dynamic indices made clang copy the whole 3.6 KB
+// block into scratch first.
+template <typename T, int FMAX, int KMAX>
+__global__ __launch_bounds__(128) void linear_inline_kernel(const InlineBatch arg) {
+  (void)arg;
+  const InlineBatch* a = (const InlineBatch*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int r = threadIdx.x;
+  const int n = a->n, F = a->F, K = a->K, kind = a->kind;
+  if (r >= n) return;
+  const T* W = reinterpret_cast<const T*>(a->wb);
+  const T* b = W + K * F;
+  int32_t idx;
+  T p;
+  row_predict<T, FMAX, KMAX>(reinterpret_cast<const T*>(a->x) + r * F, W, b, F, K, kind, idx, p);
+  a->out_idx[r] = idx;
+  static_cast<T*>(a->out_p)[r] = p;
+}
+
 template <typename T>
-__global__ __launch_bounds__(256) void serve_persistent_kernel(ServeMailSlot* mail, uint32_t* done,
-                                                               const uint32_t* stop, int nslots,
-                                                               uint64_t start_seq, uint64_t idle_ticks) {
-  __shared__ ServeMailSlot hdr;
-  __shared__ int go;
-  uint64_t seq = start_seq;  // batch index; slot = seq % nslots, published value = seq + 1
-  for (;;) {
-    const int slot = (int)(seq % (uint64_t)nslots);
-    if (threadIdx.x == 0) {
-      const uint64_t t0 = wall_clock64();
-      int g = 0;
-      for (;;) {
-        const uint32_t v = __hip_atomic_load(&mail[slot].seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (v == (uint32_t)(seq + 1)) {
-          g = 1;
-          break;
-        }
-        if (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
-        if (wall_clock64() - t0 > idle_ticks) break;
-        __builtin_amdgcn_s_sleep(8);
-      }
-      if (g) hdr = mail[slot];
-      go = g;
-    }
-    __syncthreads();
-    if (!go) return;  // every thread of the block leaves together
-    const int n = (int)hdr.n, F = hdr.F, K = hdr.K, kind = hdr.kind;
-    const T* X = reinterpret_cast<const T*>(hdr.x);
-    const T* W = reinterpret_cast<const T*>(hdr.W);
-    const T* b = reinterpret_cast<const T*>(hdr.b);
-    int32_t* oi = reinterpret_cast<int32_t*>(hdr.idx);
-    T* op = reinterpret_cast<T*>(hdr.p);
-    for (int r = threadIdx.x; r < n; r += blockDim.x) {
-      int32_t idx;
-      T p;
-      if (F <= 8 && K <= 4)
-        row_predict<T, 8, 4>(X + (int64_t)r * F, W, b, F, K, kind, idx, p);
-      else if (F <= 32 && K <= 16)
-        row_predict<T, 32, 16>(X + (int64_t)r * F, W, b, F, K, kind, idx, p);
-      else
-        row_predict_generic<T>(X + (int64_t)r * F, W, b, F, K, kind, idx, p);
-      oi[r] = idx;
-      op[r] = p;
-    }
-    __threadfence_system();  // results reach host memory before `done`
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store(&done[slot * SERVE_DONE_STRIDE], (uint32_t)(seq + 1), __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-    ++seq;
-  }
+void dispatch_inline(const InlineBatch& a, hipStream_t stream) {
+  const int threads = a.n <= 64 ? 64 : 128;
+  if (a.F <= 8 && a.K <= 4)
+    hipLaunchKernelGGL((linear_inline_kernel<T, 8, 4>), dim3(1), dim3(threads), 0, stream, a);
+  else
+    hipLaunchKernelGGL((linear_inline_kernel<T, 32, 16>), dim3(1), dim3(threads), 0, stream, a);
+  MLAPI_HIP_CHECK(hipGetLastError());
 }
 
 template <typename T>
@@ -243,17 +213,19 @@ void dispatch(const void* X, int64_t ldx, const void* W, const void* b, int64_t 
 
 }  // namespace
 
-void launch_serve_persistent(int dt, ServeMailSlot* mail, uint32_t* done, const uint32_t* stop, int nslots,
-                             uint64_t start_seq, uint64_t idle_ticks, hipStream_t stream) {
+bool linear_inline_fits(int dt, int64_t n, int F, int K) {
+  if (dt != DT_F64 && dt != DT_F32) return false;
+  const size_t es = dtype_size(dt);
+  return n >= 1 && n <= 128 && F >= 1 && F <= 32 && K >= 1 && K <= 16 && (size_t)n * F * es <= INLINE_X_BYTES &&
+         (size_t)K * (F + 1) * es <= INLINE_WB_BYTES;
+}
+
+void launch_linear_inline(int dt, const InlineBatch& a, hipStream_t stream) {
+  if (!linear_inline_fits(dt, a.n, a.F, a.K)) throw std::invalid_argument("linear_inline: batch does not fit");
   if (dt == DT_F64)
-    hipLaunchKernelGGL((serve_persistent_kernel<double>), dim3(1), dim3(256), 0, stream, mail, done, stop, nslots,
-                       start_seq, idle_ticks);
-  else if (dt == DT_F32)
-    hipLaunchKernelGGL((serve_persistent_kernel<float>), dim3(1), dim3(256), 0, stream, mail, done, stop, nslots,
-                       start_seq, idle_ticks);
+    dispatch_inline<double>(a, stream);
   else
-    throw std::invalid_argument("serve_persistent: dtype must be f64 or f32");
-  MLAPI_HIP_CHECK(hipGetLastError());
+    dispatch_inline<float>(a, stream);
 }
 
 void launch_linear_small(int dt, const void* X, int64_t ldx, const void* W, const void* b, int64_t B, int F, int K,

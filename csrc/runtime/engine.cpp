@@ -25,6 +25,7 @@ Model::~Model() {
     (void)hipSetDevice(device);
     if (dW) (void)hipFree(dW);
     if (db) (void)hipFree(db);
+    if (ws) (void)hipFree(ws);
     (void)hipSetDevice(prev);
   }
 }
@@ -80,10 +81,27 @@ void cpu_linear_predict(const Model& m, const double* X, int64_t B, int32_t* idx
   }
 }
 
+namespace {
+// rows of every path are padded to at most this multiple (GEMM: F -> 32..512 power of two)
+size_t padded_features(int F) {
+  const size_t f = (size_t)std::max(F, 1);
+  return f <= 512 ? std::max<size_t>(32, size_t(1) << (64 - __builtin_clzll(f - 1 | 1))) : (f + 511) / 512 * 512;
+}
+
+inline uint16_t f32_to_bf16(float f) {  // round to nearest even (inputs are finite)
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+}  // namespace
+
 Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   if (cfg_.max_batch < 1) cfg_.max_batch = 1;
   if (cfg_.slots < 1) cfg_.slots = 1;
   if (cfg_.dtype != DT_F64 && cfg_.dtype != DT_F32) throw std::invalid_argument("engine dtype must be f64 or f32");
+  if (cfg_.wide_dtype != DT_F64 && cfg_.wide_dtype != DT_F32 && cfg_.wide_dtype != DT_BF16)
+    throw std::invalid_argument("engine wide_dtype must be f64, f32 or bf16");
+  if (cfg_.max_features < 1) cfg_.max_features = 1;
   q_meta_.reserve(4096);
   q_x_.reserve(4096 * 8);
   if (cfg_.device >= 0) {
@@ -92,32 +110,16 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     MLAPI_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     MLAPI_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
     slots_.resize(cfg_.slots);
-    const size_t xb = (size_t)cfg_.max_batch * cfg_.max_features * sizeof(double);
-    // fine-grained (coherent) host memory: the persistent kernel polls and writes it while the
-    // host does the same, with system-scope acquire/release on the sequence words
-    const unsigned hf = hipHostMallocMapped | (cfg_.persistent ? hipHostMallocCoherent : 0u);
-    if (cfg_.persistent) {
-      MLAPI_HIP_CHECK(hipHostMalloc((void**)&mail_h_, sizeof(ServeMailSlot) * cfg_.slots, hf));
-      std::memset(mail_h_, 0, sizeof(ServeMailSlot) * cfg_.slots);
-      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&mail_d_, mail_h_, 0));
-      const size_t done_bytes = sizeof(uint32_t) * SERVE_DONE_STRIDE * (cfg_.slots + 1);
-      MLAPI_HIP_CHECK(hipHostMalloc((void**)&done_h_, done_bytes, hf));
-      std::memset(done_h_, 0, done_bytes);
-      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&done_d_, done_h_, 0));
-      stop_h_ = done_h_ + SERVE_DONE_STRIDE * cfg_.slots;  // own 64-byte line after the done words
-      stop_d_ = done_d_ + SERVE_DONE_STRIDE * cfg_.slots;
-      MLAPI_HIP_CHECK(hipStreamCreateWithPriority(&pstream_, hipStreamNonBlocking, hi));
-      int rate_khz = 0;
-      MLAPI_HIP_CHECK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, cfg_.device));
-      idle_ticks_ = (uint64_t)(rate_khz > 0 ? rate_khz : 100000) * (uint64_t)std::max(1, cfg_.persistent_idle_ms);
-    }
+    slot_row_bytes_ = padded_features(cfg_.max_features) * sizeof(double);
+    const size_t xb = (size_t)cfg_.max_batch * slot_row_bytes_;
     for (int i = 0; i < cfg_.slots; ++i) {
       Slot& s = slots_[i];
-      MLAPI_HIP_CHECK(hipHostMalloc(&s.hx, xb, hf));
+      MLAPI_HIP_CHECK(hipHostMalloc(&s.hx, xb, hipHostMallocMapped));
       MLAPI_HIP_CHECK(hipHostGetDevicePointer(&s.dx, s.hx, 0));
-      MLAPI_HIP_CHECK(hipHostMalloc((void**)&s.hidx, (size_t)cfg_.max_batch * sizeof(int32_t), hf));
+      MLAPI_HIP_CHECK(hipMalloc(&s.dstage, xb));
+      MLAPI_HIP_CHECK(hipHostMalloc((void**)&s.hidx, (size_t)cfg_.max_batch * sizeof(int32_t), hipHostMallocMapped));
       MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.didx, s.hidx, 0));
-      MLAPI_HIP_CHECK(hipHostMalloc(&s.hp, (size_t)cfg_.max_batch * sizeof(double), hf));
+      MLAPI_HIP_CHECK(hipHostMalloc(&s.hp, (size_t)cfg_.max_batch * sizeof(double), hipHostMallocMapped));
       MLAPI_HIP_CHECK(hipHostGetDevicePointer(&s.dp, s.hp, 0));
       MLAPI_HIP_CHECK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
       s.metas.reserve(cfg_.max_batch);
@@ -132,16 +134,11 @@ Engine::~Engine() {
   stop();
   if (cfg_.device >= 0) {
     (void)hipSetDevice(cfg_.device);
-    if (pstream_ != nullptr) {  // the resident kernel leaves on the stop word (or its idle timeout)
-      __atomic_store_n(stop_h_, 1u, __ATOMIC_RELEASE);
-      (void)hipStreamSynchronize(pstream_);
-      (void)hipStreamDestroy(pstream_);
-      (void)hipHostFree(mail_h_);
-      (void)hipHostFree(done_h_);
-    }
+    if (stream_) (void)hipStreamSynchronize(stream_);
     for (Slot& s : slots_) {
       if (s.ev) (void)hipEventDestroy(s.ev);
       if (s.hx) (void)hipHostFree(s.hx);
+      if (s.dstage) (void)hipFree(s.dstage);
       if (s.hidx) (void)hipHostFree(s.hidx);
       if (s.hp) (void)hipHostFree(s.hp);
     }
@@ -176,21 +173,68 @@ uint64_t Engine::load_model(int kind, int F, int K, const double* W, const doubl
   m->W.assign(W, W + (size_t)K * F);
   m->b.assign(b, b + K);
   m->label_json = label_json;
+  // ---- kernel path (see engine.h); the CPU backend ignores it
+  const bool binary = kind == KIND_BINARY || kind == KIND_BINARY_SOFTMAX;
+  if (F <= 32 && K <= 16) {
+    m->path = PATH_SMALL;
+    m->xdt = cfg_.dtype;
+    m->ldx = F;
+  } else if (binary && K == 1 && cfg_.wide_dtype != DT_F64 &&
+             F <= (cfg_.wide_dtype == DT_BF16 ? 4096 : 2048)) {
+    m->path = PATH_GEMV;
+    m->xdt = cfg_.wide_dtype;
+    const int ne = cfg_.wide_dtype == DT_BF16 ? 8 : 4;  // elements per 16-byte chunk
+    m->ldx = (F + ne - 1) / ne * ne;
+  } else if (!binary && K >= 2 && cfg_.wide_dtype == DT_BF16 && F <= 512) {
+    m->path = PATH_GEMM;
+    m->xdt = DT_BF16;
+    m->ldx = (int)padded_features(F);
+  } else {
+    m->path = PATH_GENERIC;
+    m->xdt = cfg_.wide_dtype == DT_F64 ? DT_F64 : DT_F32;
+    m->ldx = F;
+  }
+  m->pdt = (m->path == PATH_GEMV || m->path == PATH_GEMM) ? DT_F32 : m->xdt;
+  m->bias0 = (float)b[0];
   m->version = next_version_.fetch_add(1);
   if (cfg_.device >= 0) {
     MLAPI_HIP_CHECK(hipSetDevice(cfg_.device));
     m->device = cfg_.device;
-    const size_t es = dtype_size(cfg_.dtype);
-    MLAPI_HIP_CHECK(hipMalloc(&m->dW, (size_t)K * F * es));
-    MLAPI_HIP_CHECK(hipMalloc(&m->db, (size_t)K * es));
-    if (cfg_.dtype == DT_F64) {
-      MLAPI_HIP_CHECK(hipMemcpy(m->dW, m->W.data(), (size_t)K * F * 8, hipMemcpyHostToDevice));
-      MLAPI_HIP_CHECK(hipMemcpy(m->db, m->b.data(), (size_t)K * 8, hipMemcpyHostToDevice));
+    // W as the kernel reads it: [K][ldx] in xdt, zero-padded columns
+    const size_t wn = (size_t)K * m->ldx;
+    std::vector<unsigned char> wbuf(wn * dtype_size(m->xdt), 0);
+    for (int k = 0; k < K; ++k)
+      for (int f = 0; f < F; ++f) {
+        const double v = W[(size_t)k * F + f];
+        const size_t i = (size_t)k * m->ldx + f;
+        if (m->xdt == DT_F64)
+          reinterpret_cast<double*>(wbuf.data())[i] = v;
+        else if (m->xdt == DT_F32)
+          reinterpret_cast<float*>(wbuf.data())[i] = (float)v;
+        else
+          reinterpret_cast<uint16_t*>(wbuf.data())[i] = f32_to_bf16((float)v);
+      }
+    MLAPI_HIP_CHECK(hipMalloc(&m->dW, wbuf.size()));
+    MLAPI_HIP_CHECK(hipMemcpy(m->dW, wbuf.data(), wbuf.size(), hipMemcpyHostToDevice));
+    // bias: xdt for SMALL / GENERIC (the kernels' T), f32 for GEMM (GEMV takes a scalar)
+    const int bdt = m->path == PATH_SMALL || m->path == PATH_GENERIC ? m->xdt : DT_F32;
+    MLAPI_HIP_CHECK(hipMalloc(&m->db, (size_t)K * dtype_size(bdt)));
+    if (bdt == DT_F64) {
+      MLAPI_HIP_CHECK(hipMemcpy(m->db, b, (size_t)K * 8, hipMemcpyHostToDevice));
     } else {
-      std::vector<float> wf(m->W.begin(), m->W.end()), bf(m->b.begin(), m->b.end());
-      MLAPI_HIP_CHECK(hipMemcpy(m->dW, wf.data(), wf.size() * 4, hipMemcpyHostToDevice));
+      std::vector<float> bf(b, b + K);
       MLAPI_HIP_CHECK(hipMemcpy(m->db, bf.data(), bf.size() * 4, hipMemcpyHostToDevice));
     }
+    if (m->path == PATH_GEMM) {
+      // the split plan depends on the batch size: size for the largest any batch can need
+      for (int64_t B = 1; B <= cfg_.max_batch; ++B)
+        m->ws_bytes = std::max(m->ws_bytes, gemm_softmax_workspace(B, K, m->ldx));
+      if (m->ws_bytes) {
+        MLAPI_HIP_CHECK(hipMalloc(&m->ws, m->ws_bytes));
+        MLAPI_HIP_CHECK(hipMemset(m->ws, 0, m->ws_bytes));
+      }
+    }
+    MLAPI_HIP_CHECK(hipDeviceSynchronize());
   }
   std::shared_ptr<const Model> cm = m;
   {
@@ -351,12 +395,104 @@ void Engine::run_cpu(std::vector<Meta>& metas, const std::vector<double>& xs, co
       std::memcpy(&X[i * m->F], &xs[metas[i].off], sizeof(double) * m->F);
     }
     cpu_linear_predict(*m, X.data(), (int64_t)n, idx.data(), p.data());
-    if (cfg_.fail_every > 0 && (++batch_counter_ % (uint64_t)cfg_.fail_every) == 0)
+    if (drop_.load(std::memory_order_relaxed)) {
       std::fill(st.begin(), st.end(), (int32_t)ST_DEVICE_ERROR);
+      healthy_.store(false);
+    } else if (cfg_.fail_every > 0 && (++batch_counter_ % (uint64_t)cfg_.fail_every) == 0) {
+      std::fill(st.begin(), st.end(), (int32_t)ST_DEVICE_ERROR);
+    }
   }
   if (cfg_.delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(cfg_.delay_us));
   record_batch(n);
   deliver(metas, idx.data(), p.data(), st.data(), m, now_ns());
+}
+
+// Rows of the batch -> the slot's pinned buffer in the model's row layout (xdt, stride ldx,
+// zero padding). A row whose feature count does not match the model is zeroed and answered
+// ST_SHAPE.
+void Engine::pack_rows(Slot& s, const std::vector<double>& xs, const Model& m) {
+  const int F = m.F, ld = m.ldx;
+  const size_t n = (size_t)s.n;
+  for (size_t i = 0; i < n; ++i) {
+    const bool ok = s.metas[i].nf == F;
+    if (!ok) s.pre_status[i] = ST_SHAPE;
+    const double* src = &xs[s.metas[i].off];
+    if (m.xdt == DT_F64) {
+      double* d = static_cast<double*>(s.hx) + i * ld;
+      if (ok)
+        std::memcpy(d, src, sizeof(double) * F);
+      else
+        std::memset(d, 0, sizeof(double) * F);
+      for (int f = F; f < ld; ++f) d[f] = 0.0;
+    } else if (m.xdt == DT_F32) {
+      float* d = static_cast<float*>(s.hx) + i * ld;
+      for (int f = 0; f < F; ++f) d[f] = ok ? (float)src[f] : 0.f;
+      for (int f = F; f < ld; ++f) d[f] = 0.f;
+    } else {
+      uint16_t* d = static_cast<uint16_t*>(s.hx) + i * ld;
+      for (int f = 0; f < F; ++f) d[f] = ok ? f32_to_bf16((float)src[f]) : 0;
+      for (int f = F; f < ld; ++f) d[f] = 0;
+    }
+  }
+}
+
+// One launch for the whole batch on the model's kernel path (engine.h).
+void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs) {
+  const int64_t n = s.n;
+  if (m.path == PATH_SMALL && cfg_.inline_args && linear_inline_fits(m.xdt, n, m.F, m.K)) {
+    // rows, W and b ride in the kernel-argument block
+    InlineBatch& a = inline_;
+    a.n = (int32_t)n;
+    a.F = m.F;
+    a.K = m.K;
+    a.kind = m.kind;
+    a.out_idx = s.didx;
+    a.out_p = s.dp;
+    const size_t es = dtype_size(m.xdt);
+    const size_t kf = (size_t)m.K * m.F;
+    if (m.xdt == DT_F64) {
+      double* wb = reinterpret_cast<double*>(a.wb);
+      std::memcpy(wb, m.W.data(), kf * es);
+      std::memcpy(wb + kf, m.b.data(), (size_t)m.K * es);
+      double* x = reinterpret_cast<double*>(a.x);
+      for (int64_t i = 0; i < n; ++i) {
+        const bool ok = s.metas[i].nf == m.F;
+        if (!ok) s.pre_status[i] = ST_SHAPE;
+        for (int f = 0; f < m.F; ++f) x[i * m.F + f] = ok ? xs[s.metas[i].off + f] : 0.0;
+      }
+    } else {
+      float* wb = reinterpret_cast<float*>(a.wb);
+      for (size_t i = 0; i < kf; ++i) wb[i] = (float)m.W[i];
+      for (int k = 0; k < m.K; ++k) wb[kf + k] = (float)m.b[k];
+      float* x = reinterpret_cast<float*>(a.x);
+      for (int64_t i = 0; i < n; ++i) {
+        const bool ok = s.metas[i].nf == m.F;
+        if (!ok) s.pre_status[i] = ST_SHAPE;
+        for (int f = 0; f < m.F; ++f) x[i * m.F + f] = ok ? (float)xs[s.metas[i].off + f] : 0.f;
+      }
+    }
+    launch_linear_inline(m.xdt, a, stream_);
+    std::lock_guard<std::mutex> lk(st_mu_);
+    stats_.path_batches[PATH_SMALL]++;
+    stats_.inline_batches++;
+    return;
+  }
+  pack_rows(s, xs, m);
+  const size_t bytes = (size_t)n * m.ldx * dtype_size(m.xdt);
+  if (m.path == PATH_SMALL) {  // zero-copy: the kernel reads the pinned rows over the host link
+    launch_linear_small(m.xdt, s.dx, m.ldx, m.dW, m.db, n, m.F, m.K, m.kind, s.didx, s.dp, stream_);
+  } else {
+    MLAPI_HIP_CHECK(hipMemcpyAsync(s.dstage, s.hx, bytes, hipMemcpyHostToDevice, stream_));
+    if (m.path == PATH_GEMV)
+      launch_gemv_binary(m.xdt, s.dstage, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_);
+    else if (m.path == PATH_GEMM)
+      launch_gemm_softmax(s.dstage, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
+                          static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_);
+    else
+      launch_linear_small(m.xdt, s.dstage, m.ldx, m.dW, m.db, n, m.F, m.K, m.kind, s.didx, s.dp, stream_);
+  }
+  std::lock_guard<std::mutex> lk(st_mu_);
+  stats_.path_batches[m.path]++;
 }
 
 void Engine::batcher_loop() {
@@ -415,50 +551,14 @@ void Engine::batcher_loop() {
       s.failed = false;
       s.launched = false;
       s.pre_status.assign(n, ST_OK);
-      const int F = m->F;
-      if (m->dtype == DT_F64) {
-        double* hx = static_cast<double*>(s.hx);
-        for (size_t i = 0; i < n; ++i) {
-          if (s.metas[i].nf != F) {
-            s.pre_status[i] = ST_SHAPE;
-            std::memset(hx + i * F, 0, sizeof(double) * F);
-          } else {
-            std::memcpy(hx + i * F, &xs[s.metas[i].off], sizeof(double) * F);
-          }
-        }
-      } else {
-        float* hx = static_cast<float*>(s.hx);
-        for (size_t i = 0; i < n; ++i) {
-          const bool ok = s.metas[i].nf == F;
-          if (!ok) s.pre_status[i] = ST_SHAPE;
-          for (int f = 0; f < F; ++f) hx[i * F + f] = ok ? (float)xs[s.metas[i].off + f] : 0.f;
-        }
-      }
-      if (cfg_.persistent) {
-        // Mailbox post: rows are in the slot already; publish the header, then the sequence word
-        // (release) that the resident kernel polls. An injected fault still posts an empty batch
-        // so the kernel's strict sequence order is kept.
-        s.batch = next_batch_++;
-        const bool inject = cfg_.fail_every > 0 && (++batch_counter_ % (uint64_t)cfg_.fail_every) == 0;
-        ServeMailSlot& mb = mail_h_[si];
-        mb.n = inject ? 0u : (uint32_t)n;
-        mb.F = F;
-        mb.K = m->K;
-        mb.kind = m->kind;
-        mb.x = (uint64_t)(uintptr_t)s.dx;
-        mb.W = (uint64_t)(uintptr_t)m->dW;
-        mb.b = (uint64_t)(uintptr_t)m->db;
-        mb.idx = (uint64_t)(uintptr_t)s.didx;
-        mb.p = (uint64_t)(uintptr_t)s.dp;
-        __atomic_store_n(&mb.seq, (uint32_t)(s.batch + 1), __ATOMIC_RELEASE);
-        s.failed = inject;
-        s.launched = !inject;
+      if (drop_.load(std::memory_order_relaxed)) {
+        s.failed = true;
+        healthy_.store(false);
       } else if (cfg_.fail_every > 0 && (++batch_counter_ % (uint64_t)cfg_.fail_every) == 0) {
         s.failed = true;
       } else {
         try {
-          launch_linear_small(m->dtype, s.dx, F, m->dW, m->db, (int64_t)n, F, m->K, m->kind, s.didx, s.dp,
-                              stream_);
+          launch_batch(s, *m, xs);
           MLAPI_HIP_CHECK(hipEventRecord(s.ev, stream_));
           s.launched = true;
         } catch (const std::exception&) {
@@ -483,56 +583,6 @@ void Engine::batcher_loop() {
   s_cv_.notify_all();
 }
 
-// Persistent mode: wait for the slot's `done` word. The completer owns the resident kernel's
-// lifecycle: it launches one when none is running (first batch, or after the kernel idled out),
-// starting at the oldest outstanding batch, and notices an exited kernel through its stream.
-bool Engine::wait_persistent(Slot& s, int si) {
-  const uint32_t want = (uint32_t)(s.batch + 1);
-  volatile uint32_t* dw = done_h_ + SERVE_DONE_STRIDE * si;
-  const int64_t t0 = now_ns();
-  // after a pause longer than the kernel's idle timeout it has most likely left already
-  if (kernel_running_ && t0 - last_done_ns_ > ((int64_t)cfg_.persistent_idle_ms - 1) * 1000000 &&
-      hipStreamQuery(pstream_) == hipSuccess)
-    kernel_running_ = false;
-  int spins = 0;
-  while (__atomic_load_n(dw, __ATOMIC_ACQUIRE) != want) {
-    if (!kernel_running_) {
-      try {
-        launch_serve_persistent(cfg_.dtype, mail_d_, done_d_, stop_d_, cfg_.slots, s.batch, idle_ticks_, pstream_);
-      } catch (const std::exception&) {
-        return false;
-      }
-      kernel_running_ = true;
-      std::lock_guard<std::mutex> lk(st_mu_);
-      ++stats_.kernel_launches;
-    }
-    ++spins;
-    if (spins < 20000) {
-      _mm_pause();
-    } else {
-      std::this_thread::sleep_for(std::chrono::microseconds(2));
-    }
-    if ((spins & 255) == 0) {
-      // the kernel may have idled out just before this batch was posted: relaunch at this batch
-      const hipError_t q = hipStreamQuery(pstream_);
-      if (q == hipSuccess) {
-        if (__atomic_load_n(dw, __ATOMIC_ACQUIRE) == want) break;
-        kernel_running_ = false;
-      } else if (q != hipErrorNotReady) {
-        return false;
-      }
-      if (cfg_.watchdog_ms > 0) {
-        const int64_t waited = now_ns() - t0;
-        if (waited > (int64_t)cfg_.watchdog_ms * 1000000) healthy_.store(false);
-        // never block the completer forever: fail the batch (ST_DEVICE_ERROR) after 10x the watchdog
-        if (waited > (int64_t)cfg_.watchdog_ms * 10000000) return false;
-      }
-    }
-  }
-  last_done_ns_ = now_ns();
-  return true;
-}
-
 void Engine::completer_loop() {
   pthread_setname_np(pthread_self(), "mlapi-compl");
   (void)hipSetDevice(cfg_.device);
@@ -548,12 +598,7 @@ void Engine::completer_loop() {
       inflight_.pop_front();
     }
     Slot& s = slots_[si];
-    if (cfg_.persistent) {
-      if (!wait_persistent(s, si)) {
-        s.failed = true;
-        healthy_.store(false);
-      }
-    } else if (s.launched) {
+    if (s.launched) {
       // Poll the event: spin briefly (sub-10us kernels), then back off.
       const int64_t t0 = now_ns();
       int spins = 0;
@@ -581,7 +626,7 @@ void Engine::completer_loop() {
     if (s.failed) {
       std::fill(st.begin(), st.end(), (int32_t)ST_DEVICE_ERROR);
       std::fill(pd.begin(), pd.end(), 0.0);
-    } else if (s.model->dtype == DT_F64) {
+    } else if (s.model->pdt == DT_F64) {
       std::memcpy(pd.data(), s.hp, n * sizeof(double));
     } else {
       const float* pf = static_cast<const float*>(s.hp);
@@ -614,6 +659,7 @@ EngineStats Engine::stats() const {
     s.queue_depth = q_meta_.size();
   }
   s.healthy = healthy_.load();
+  s.dropped = drop_.load();
   return s;
 }
 

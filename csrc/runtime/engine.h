@@ -4,11 +4,21 @@
 // calls, serialized on the event loop) with a server-side batcher (BASELINE north star): every
 // request submitted while the previous batch is on the GPU is coalesced into the next launch.
 //
-//   submit() (any thread, lock-free fast append under a short mutex)
-//     -> batcher thread: drains up to max_batch rows, packs them into a host-pinned,
-//        device-mapped slot (zero-copy: the kernel reads x and writes (idx, p) over the host
-//        link directly, no hipMemcpy), launches launch_linear_small on a high-priority stream,
-//        records an event; up to `slots` batches are in flight;
+//   submit() (any thread, short mutex, one lock per epoll round of an IO thread)
+//     -> batcher thread: drains up to max_batch rows and launches ONE kernel for them on a
+//        high-priority stream; the kernel is picked per model at load time (Model::path):
+//          SMALL   (F <= 32, K <= 16; the Iris shape): linear_small, fp64 (sklearn bit parity) or
+//                  fp32. Batches that fit 3 KB travel inside the kernel-argument block
+//                  (launch_linear_inline: no host-link read at all); larger ones are read
+//                  zero-copy from the pinned slot;
+//          GEMV    (binary, wide F): rows packed as bf16 (or fp32), one hipMemcpyAsync H2D into
+//                  the slot's device buffer, then the HBM-streaming gemv_binary kernel;
+//          GEMM    (multiclass, wide F / many classes): bf16 rows (F zero-padded to the MFMA
+//                  width) H2D, then the MFMA gemm_softmax kernel with its online softmax/argmax
+//                  epilogue (workspace per model, zeroed once);
+//          GENERIC (wide models served in fp32/fp64): H2D + one-row-per-lane scalar kernel;
+//        the (idx, p) results are written by the kernel straight into host-mapped memory;
+//        up to `slots` batches are in flight;
 //     -> completer thread: polls the oldest slot's event, groups results by Sink and hands them
 //        over (HTTP IO threads, Python futures, blocking callers).
 //
@@ -42,17 +52,26 @@ enum Status : int32_t {
   ST_SHUTDOWN = 5,
 };
 
+enum ServePath : int32_t { PATH_SMALL = 0, PATH_GEMV = 1, PATH_GEMM = 2, PATH_GENERIC = 3, PATH_COUNT = 4 };
+
 struct Model {
   int kind = KIND_MULTINOMIAL;
   int F = 0;          // features
   int K = 0;          // rows of W (1 for binary kinds)
-  int dtype = DT_F64; // device compute dtype (f64 / f32)
+  int dtype = DT_F64; // small-path compute dtype (f64 / f32)
+  int path = PATH_SMALL;
+  int xdt = DT_F64;   // dtype of the rows as the kernel reads them (f64 / f32 / bf16)
+  int ldx = 0;        // row stride of the packed rows (F, or F zero-padded for GEMV / GEMM)
+  int pdt = DT_F64;   // dtype of the kernel's p output (f32 on the GEMV / GEMM paths)
+  float bias0 = 0.f;  // GEMV: scalar intercept
   uint64_t version = 0;
   std::vector<double> W, b;             // host float64 copies (CPU backend + reload)
   std::vector<std::string> label_json;  // pre-rendered JSON per class index
   int device = -1;
   void* dW = nullptr;
   void* db = nullptr;
+  void* ws = nullptr;  // GEMM: gemm_softmax workspace (zeroed once; split-merge counters re-arm)
+  size_t ws_bytes = 0;
   ~Model();
 };
 
@@ -76,30 +95,32 @@ struct EngineConfig {
   int max_batch = 256;    // rows per launch
   int max_wait_us = 0;    // 0 = continuous batching; >0 = also wait up to this long to fill a batch
   int slots = 4;          // batches in flight
-  int dtype = DT_F64;     // device compute dtype for served models (f64 = bit parity with sklearn)
-  int max_features = 256; // per-request feature cap
+  int dtype = DT_F64;     // SMALL-path compute dtype (f64 = bit parity with sklearn, or f32)
+  int wide_dtype = DT_BF16;  // dtype of models too wide for the SMALL path: bf16 -> GEMV / MFMA
+                             // GEMM kernels; f32 -> GEMV (binary) / GENERIC; f64 -> GENERIC
+  int max_features = 256; // per-request feature cap (sizes the slot buffers)
+  bool inline_args = true;  // SMALL path: batches that fit travel in the kernel-argument block
   int watchdog_ms = 2000; // batch not complete after this -> engine marked unhealthy
   int fail_every = 0;     // fault injection: fail every N-th batch with ST_DEVICE_ERROR
   int delay_us = 0;       // fault injection: extra per-batch delay
   int spin_us = 0;        // batcher polls the queue this long before sleeping on the condvar
                           // (saves the futex wake-up on the request path under load)
   int max_queue = 1 << 20;  // backpressure: rows waiting for the batcher; beyond it submit is refused
-  bool persistent = false;  // GPU: one resident kernel fed through a host mailbox instead of a
-                            // launch per batch (serve_persistent_kernel, linear_small.hip)
-  int persistent_idle_ms = 5;  // the resident kernel exits after this long without work
 };
 
 struct EngineStats {
   uint64_t requests = 0, batches = 0, errors = 0;
-  uint64_t kernel_launches = 0;     // persistent mode: (re)launches of the resident kernel
   uint64_t rejected = 0;            // rows refused by backpressure (max_queue)
   uint64_t batch_hist[12] = {0};    // batch size buckets: 1,2,4,...,2048+
   uint64_t latency_hist[24] = {0};  // latency buckets in powers of two of 1us: <1us .. >=2^23us
+  uint64_t path_batches[PATH_COUNT] = {0};  // GPU batches per kernel path
+  uint64_t inline_batches = 0;      // SMALL batches launched through the kernel-argument block
   double latency_sum_us = 0;
   double device_us_sum = 0;         // launch -> completion observed by the completer
   uint64_t queue_depth = 0;
   uint64_t model_version = 0;
   bool healthy = true;
+  bool dropped = false;             // fault injection: every batch fails (drop-a-rank)
 };
 
 class Engine {
@@ -129,6 +150,14 @@ class Engine {
   EngineStats stats() const;
   const EngineConfig& config() const { return cfg_; }
   bool healthy() const { return healthy_.load(std::memory_order_relaxed); }
+  // Health probe succeeded (HttpServer's health thread): the engine serves again.
+  void mark_healthy() { healthy_.store(!drop_.load()); }
+  // Fault injection "drop this rank": while on, every batch fails with ST_DEVICE_ERROR and the
+  // engine reports unhealthy (DP dispatch takes the rank out of its SO_REUSEPORT group).
+  void inject_drop(bool on) {
+    drop_.store(on);
+    if (on) healthy_.store(false);
+  }
   void stop();
 
  private:
@@ -140,9 +169,10 @@ class Engine {
     int32_t off;  // offset into the feature arena
   };
   struct Slot {
-    void* hx = nullptr;       // host pinned, device mapped (inputs, model dtype)
-    void* dx = nullptr;
-    int32_t* hidx = nullptr;  // host pinned outputs
+    void* hx = nullptr;       // host pinned, device mapped: packed rows (model xdt)
+    void* dx = nullptr;       // device address of hx (zero-copy reads)
+    void* dstage = nullptr;   // device buffer: H2D destination of the GEMV / GEMM / GENERIC paths
+    int32_t* hidx = nullptr;  // host pinned outputs, written by the kernel over the host link
     int32_t* didx = nullptr;
     void* hp = nullptr;
     void* dp = nullptr;
@@ -151,7 +181,6 @@ class Engine {
     std::vector<int32_t> pre_status;  // per-row status decided before launch
     std::shared_ptr<const Model> model;
     int64_t t_launch = 0;
-    uint64_t batch = 0;  // persistent mode: global batch index (mailbox sequence - 1)
     int n = 0;
     bool launched = false;
     bool failed = false;
@@ -159,7 +188,8 @@ class Engine {
 
   void batcher_loop();
   void completer_loop();
-  bool wait_persistent(Slot& s, int si);
+  void pack_rows(Slot& s, const std::vector<double>& xs, const Model& m);
+  void launch_batch(Slot& s, const Model& m, const std::vector<double>& xs);
   void run_cpu(std::vector<Meta>& metas, const std::vector<double>& xs, const std::shared_ptr<const Model>& m);
   void finish(Slot& s, const int32_t* idx, const double* p, const int32_t* status);
   void deliver(std::vector<Meta>& metas, const int32_t* idx, const double* p, const int32_t* st,
@@ -189,22 +219,12 @@ class Engine {
   std::deque<int> inflight_;
   bool batcher_done_ = false;
 
-  // persistent mode: host-pinned mailbox (device-visible), its stop word, the resident kernel's
-  // stream; kernel_running_ / relaunch bookkeeping are owned by the completer thread
-  ServeMailSlot* mail_h_ = nullptr;
-  ServeMailSlot* mail_d_ = nullptr;
-  uint32_t* done_h_ = nullptr;  // one word per slot, 64 B apart
-  uint32_t* done_d_ = nullptr;
-  uint32_t* stop_h_ = nullptr;
-  uint32_t* stop_d_ = nullptr;
-  hipStream_t pstream_ = nullptr;
-  bool kernel_running_ = false;
-  uint64_t idle_ticks_ = 0;
-  uint64_t next_batch_ = 0;     // batcher thread only
-  int64_t last_done_ns_ = 0;   // completer thread only
+  size_t slot_row_bytes_ = 0;  // capacity of one packed row in a slot (any path)
+  InlineBatch inline_{};        // batcher thread only
 
   std::thread batcher_, completer_;
   std::atomic<bool> healthy_{true};
+  std::atomic<bool> drop_{false};
 
   mutable std::mutex st_mu_;
   EngineStats stats_;

@@ -191,10 +191,21 @@ def create_app(config: Optional[Config] = None, *, runtime=None) -> FastAPI:
     async def metrics():
         return PlainTextResponse(rt().metrics_text(), media_type="text/plain; version=0.0.4")
 
+    def admin_allowed(request: Request) -> bool:
+        mode = str(config.admin).lower()
+        if mode == "on":
+            return True
+        if mode == "off":
+            return False
+        host = request.client.host if request.client else ""
+        return host in ("127.0.0.1", "::1", "localhost", "testclient")  # loopback (default)
+
     @app.post("/admin/reload", include_in_schema=False)
-    async def admin_reload():
+    async def admin_reload(request: Request):
+        if not admin_allowed(request):
+            return JSONResponse({"detail": "Not Found"}, status_code=404)
         r = rt()
-        r.store._key = ("force",)  # next check() re-reads the file
+        r.store.invalidate()  # next check() re-reads the file
         ok = r.store.check()
         r.on_admin_reload()
         return JSONResponse({"reloaded": ok, "model_version": r.handle.version, "error": r.store.last_error},

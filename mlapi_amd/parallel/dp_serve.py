@@ -135,6 +135,9 @@ def start_dp_runtime(cfg: Config, info: Optional[DistInfo] = None):
     rcfg = Config.from_env(**{**cfg.__dict__, "device": device})
     rt = ServingRuntime(rcfg, load=False)
     rt.handle.load(model)
+    if cfg.fault_drop_rank == info.rank:  # fault injection: this replica fails every batch
+        log.warning("rank %d: fault injection, dropping this replica", info.rank)
+        rt.handle.engine.inject_drop(True)
     rt.store.reload = "off"  # the controller owns reloads in DP mode
     ctl = DPReloadController(rt, info, cfg.reload_interval_ms)
     rt.on_admin_reload = ctl.request.set  # POST /admin/reload on any rank

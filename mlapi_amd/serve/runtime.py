@@ -30,7 +30,7 @@ from mlapi_amd.utils.config import Config
 
 log = logging.getLogger("mlapi_amd.serve")
 
-DTYPES = {"f64": 0, "float64": 0, "f32": 1, "float32": 1}
+DTYPES = {"f64": 0, "float64": 0, "f32": 1, "float32": 1, "bf16": 2, "bfloat16": 2}
 
 
 class PredictionError(RuntimeError):
@@ -52,14 +52,14 @@ class EngineHandle:
         ec.max_wait_us = config.max_wait_us
         ec.slots = config.slots
         ec.dtype = DTYPES[config.dtype]
+        ec.wide_dtype = DTYPES[config.wide_dtype]
         ec.max_features = max(64, len(config.feature_names))
         ec.watchdog_ms = config.watchdog_ms
         ec.fail_every = config.fail_every
         ec.delay_us = config.delay_us
         ec.spin_us = config.spin_us
-        ec.persistent = bool(config.persistent)
+        ec.inline_args = bool(config.inline_args)
         ec.max_queue = config.max_queue
-        ec.persistent_idle_ms = config.persistent_idle_ms
         self.engine = c.Engine(ec)
         self._models: Dict[int, LinearModel] = {}
         self._lock = threading.Lock()
@@ -115,6 +115,11 @@ class ModelStore:
         self._stop = threading.Event()
         self.last_error: Optional[str] = None
         self.loads = 0
+
+    def invalidate(self) -> None:
+        """Forget the file's identity: the next :meth:`check` re-reads the checkpoint."""
+        with self._lock:
+            self._key = ("unchecked",)
 
     def _stat_key(self):
         try:

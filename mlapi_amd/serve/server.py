@@ -10,6 +10,7 @@ to FastAPI; the model runs in the same batching engine either way.
 from __future__ import annotations
 
 import logging
+import os
 import signal
 import threading
 from typing import Optional
@@ -24,7 +25,8 @@ log = logging.getLogger("mlapi_amd.serve")
 
 
 class NativeServer:
-    def __init__(self, config: Config, runtime: Optional[ServingRuntime] = None, app=None):
+    def __init__(self, config: Config, runtime: Optional[ServingRuntime] = None, app=None,
+                 access_log_fd: int = 2):
         self.config = config
         self.runtime = runtime or ServingRuntime(config)
         self.runtime.owned_by_app = False
@@ -38,6 +40,10 @@ class NativeServer:
         sc.feature_names = list(config.feature_names)
         sc.server_header = config.server_header
         sc.fast_path = bool(config.fast_path)
+        sc.access_log = bool(config.access_log)
+        sc.access_log_fd = int(access_log_fd)
+        hd = str(config.health_dispatch).lower()
+        sc.health_dispatch = hd == "on" or (hd == "auto" and int(os.environ.get("WORLD_SIZE", "1")) > 1)
         self.http = c.HttpServer(self.runtime.handle.engine, sc)
         self.runtime.http = self.http
         self.bridge = AsgiBridge(self.app, self.http, workers=config.slow_workers)

@@ -30,7 +30,8 @@ class Config:
     files_strict_parity: bool = True          # /files/: 500 on int/bool/NaN cells like the reference (R4d)
     # device / engine
     device: str = "auto"                      # "auto" | "cpu" | "cuda" | "cuda:N" | "N"
-    dtype: str = "f64"                        # serving compute dtype: f64 (sklearn parity) | f32
+    dtype: str = "f64"                        # small-model (F<=32, K<=16) compute dtype: f64 (sklearn parity) | f32
+    wide_dtype: str = "bf16"                  # wider models: bf16 (GEMV / MFMA GEMM kernels) | f32 | f64
     max_batch: int = 256
     max_wait_us: int = 0                      # 0 = continuous batching
     slots: int = 4
@@ -39,8 +40,8 @@ class Config:
     delay_us: int = 0                         # fault injection: delay every batch
     spin_us: int = 0                          # batcher spin before sleeping (0 = always sleep)
     max_queue: int = 1 << 20                  # backpressure: queued rows beyond this -> HTTP 503
-    persistent: bool = False                  # GPU: resident serving kernel fed by a host mailbox
-    persistent_idle_ms: int = 5               # ... which exits after this long without work
+    inline_args: bool = True                  # GPU: tiny batches travel in the kernel-argument block
+    fault_drop_rank: int = -1                 # fault injection: this DP rank's engine fails every batch
     pin: str = "auto"                         # CPU pinning per rank: auto (DP without launcher) | on | off
     # HTTP
     host: str = "127.0.0.1"
@@ -51,7 +52,9 @@ class Config:
     server_header: str = "uvicorn"
     slow_workers: int = 1
     log_level: str = "warning"
-    access_log: bool = False
+    access_log: bool = False                  # uvicorn-format access log lines on stderr
+    health_dispatch: str = "auto"             # auto (DP, world > 1) | on | off: unhealthy ranks leave the port
+    admin: str = "loopback"                   # POST /admin/*: loopback (local clients only) | on | off
     # observability
     metrics: bool = True
 

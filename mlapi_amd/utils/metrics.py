@@ -54,8 +54,15 @@ def render(engine_stats: Optional[dict] = None, server_stats: Optional[dict] = N
         _line(out, "mlapi_queue_depth", es["queue_depth"], labels)
         out += ["# TYPE mlapi_model_version gauge"]
         _line(out, "mlapi_model_version", es["model_version"], labels)
-        out += ["# TYPE mlapi_engine_healthy gauge"]
+        out += ["# HELP mlapi_engine_healthy 1 while this rank's engine completes batches (per rank).",
+                "# TYPE mlapi_engine_healthy gauge"]
         _line(out, "mlapi_engine_healthy", 1 if es["healthy"] else 0, labels)
+        if "path_batches" in es:
+            out += ["# HELP mlapi_kernel_batches_total GPU batches per kernel path.",
+                    "# TYPE mlapi_kernel_batches_total counter"]
+            for path, n in es["path_batches"].items():
+                _line(out, "mlapi_kernel_batches_total", n, {**labels, "kernel": path})
+            _line(out, "mlapi_kernel_batches_total", es.get("inline_batches", 0), {**labels, "kernel": "small_inline"})
     if server_stats:
         out += ["# HELP mlapi_http_requests_total HTTP requests by path taken.",
                 "# TYPE mlapi_http_requests_total counter"]
@@ -65,6 +72,12 @@ def render(engine_stats: Optional[dict] = None, server_stats: Optional[dict] = N
         _line(out, "mlapi_http_connections_total", server_stats["connections"], labels)
         out += ["# TYPE mlapi_http_internal_errors_total counter"]
         _line(out, "mlapi_http_internal_errors_total", server_stats["errors"], labels)
+        if "accepting" in server_stats:
+            out += ["# HELP mlapi_rank_accepting 1 while this rank is in its SO_REUSEPORT group (health dispatch).",
+                    "# TYPE mlapi_rank_accepting gauge"]
+            _line(out, "mlapi_rank_accepting", 1 if server_stats["accepting"] else 0, labels)
+            out += ["# TYPE mlapi_rank_listen_closes_total counter"]
+            _line(out, "mlapi_rank_listen_closes_total", server_stats["listen_closes"], labels)
     for name, value, lab in extra:
         _line(out, name, value, {**labels, **(lab or {})})
     return "\n".join(out) + "\n"

@@ -195,3 +195,71 @@ def test_bench_contract_two_ranks():
               "vs_baseline", "dtype", "data", "config"):
         assert k in d
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["value"] > 0
+
+
+def _post_new_conn(port, body):
+    """One request on a NEW connection (SO_REUSEPORT balances connections, not requests)."""
+    s = socket.create_connection(("127.0.0.1", port), timeout=10)
+    try:
+        s.sendall(b"POST /predict HTTP/1.1\r\nHost: t\r\nContent-Type: application/json\r\nConnection: close\r\n"
+                  b"Content-Length: %d\r\n\r\n%s" % (len(body), body))
+        data = b""
+        while True:
+            c = s.recv(65536)
+            if not c:
+                break
+            data += c
+        return int(data.split()[1])
+    except (ConnectionError, IndexError):
+        return 0
+    finally:
+        s.close()
+
+
+def test_dp_health_dispatch_drops_and_readmits_rank(tmp_path, iris_pickle_bytes):
+    """3 CPU ranks share one port; rank 1 is fault-injected ("drop a rank"). Once it has left the
+    SO_REUSEPORT group, clients see 100% 200s; after recovery the probe re-admits it."""
+    (tmp_path / "LRClassifier.pkl").write_bytes(iris_pickle_bytes)
+    port = free_port()
+    p = torchrun(3, str(ROOT / "tests" / "dist" / "dp_health.py"),
+                 {"OUT": str(tmp_path), "PORT": str(port), "MLAPI_FAULT_DROP_RANK": "1"}, cwd=str(tmp_path))
+    body = b'{"sepal_length":5.1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}'
+
+    def state(r):
+        try:
+            return json.loads((tmp_path / f"state_{r}").read_text())
+        except (OSError, ValueError):
+            return None
+
+    try:
+        t0 = time.time()
+        while not (all(state(r) for r in range(3)) and state(1)["listen_closes"] >= 1):
+            assert p.poll() is None, p.stdout.read()
+            assert time.time() - t0 < 90, [state(r) for r in range(3)]
+            time.sleep(0.1)
+        s1 = state(1)
+        assert not s1["accepting"] and s1["listeners"] == 0 and not s1["healthy"]
+        assert 'mlapi_engine_healthy{rank="1",backend="cpu"} 0' in s1["metrics"]
+        assert 'mlapi_rank_accepting{rank="1",backend="cpu"} 0' in s1["metrics"]
+        codes = [_post_new_conn(port, body) for _ in range(300)]
+        assert codes == [200] * 300, {c: codes.count(c) for c in set(codes)}
+        (tmp_path / "recover").touch()
+        t0 = time.time()
+        while not (state(1)["accepting"] and state(1)["listeners"] == 2):
+            assert time.time() - t0 < 30, state(1)
+            time.sleep(0.05)
+        time.sleep(0.2)
+        served = [state(r)["requests"] for r in range(3)]
+        codes = [_post_new_conn(port, body) for _ in range(300)]
+        assert codes == [200] * 300, {c: codes.count(c) for c in set(codes)}
+        time.sleep(0.2)
+        assert state(1)["requests"] > served[1], "re-admitted rank must receive connections again"
+        assert state(0)["requests"] > served[0] and state(2)["requests"] > served[2]
+    finally:
+        (tmp_path / "stop").touch()
+        try:
+            out, _ = p.communicate(timeout=60)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+    assert p.returncode == 0, out[-3000:]

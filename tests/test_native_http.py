@@ -1,5 +1,7 @@
 """Native HTTP front end (CPU backend): wire-level parity with FastAPI, HTTP/1.1 edge cases, load."""
 import json
+import os
+import re
 import socket
 import threading
 import time
@@ -177,9 +179,90 @@ def test_parser_accepts_plain_numbers(native):
     '{"sepal\\u005flength":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
     '[1,2,3,4]', 'hello', '', '{"sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2} x',
     '{"sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2,}',
+    # extra values json.loads rejects: the fast path must not answer 200 for them
+    '{"x":1..2e-,"sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"x":-,"sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"x":"\\q","sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"x":"\\u12","sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"x":1.5e,"sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"x":--1,"sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"x":01,"sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"x":"\u00e9","sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
 ])
 def test_parser_delegates_everything_else(native, body):
     assert _parse(native, body) is None
+
+
+@pytest.mark.parametrize("body", [
+    '{"x":"a\\"b\\\\c\\/\\b\\f\\n\\r\\t\\u00e9","sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+    '{"x":[1e400,-0.5E-3,0,{"y":[]}],"sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',
+])
+def test_parser_accepts_valid_extras(native, body):
+    json.loads(body)  # the reference accepts these bodies too
+    assert _parse(native, body) == [1, 3.5, 1.4, 0.2]
+
+
+def test_invalid_extra_value_gets_fastapi_422(server):
+    body = b'{"x":1..2e-,"sepal_length":1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}'
+    (status, _, b), = raw(server.port, post(body))
+    assert status == 422 and json.loads(b)["detail"][0]["type"] == "json_invalid"
+
+
+@pytest.mark.parametrize("size", [b"ffffffffffffffff", b"-1", b"10000000000000000", b"0x10", b"zz"])
+def test_chunked_size_overflow_is_rejected(server, size):
+    """a huge / negative / malformed chunk size once aborted the process."""
+    data = (b"POST /predict HTTP/1.1\r\nHost: t\r\nContent-Type: application/json\r\n"
+            b"Transfer-Encoding: chunked\r\n\r\n1\r\n{\r\n" + size + b"\r\nxxxx")
+    res = raw(server.port, data)
+    assert res and res[0][0] in (400, 413)
+    (status, _, _), = raw(server.port, post(A1))  # the server is still alive
+    assert status == 200
+
+
+def test_chunk_without_crlf_terminator_is_rejected(server):
+    data = (b"POST /predict HTTP/1.1\r\nHost: t\r\nContent-Type: application/json\r\n"
+            b"Transfer-Encoding: chunked\r\n\r\n2\r\n{}XX0\r\n\r\n")
+    (status, _, _), = raw(server.port, data)
+    assert status == 400
+
+
+def test_pipelined_flood_while_waiting_is_served_in_order(iris_cwd):
+    """A client that keeps writing while its first request is in the engine: the server stops
+    reading past pipeline_cap (bounded memory) and resumes once the response is out."""
+    from mlapi_amd.serve.server import NativeServer
+    from mlapi_amd.utils.config import Config
+
+    srv = NativeServer(Config.from_env(port=0, device="cpu", io_threads=1, delay_us=5000)).start()
+    try:
+        n = 200  # 200 x 8 KB = 1.6 MB pipelined behind a 5 ms batch: > the 1 MiB pipeline cap
+        body = A1[:-1] + b',"pad":"' + b"a" * 8192 + b'"}'
+        res = raw(srv.port, post(body) * n, n_responses=n, timeout=60)
+        assert len(res) == n and all(r[0] == 200 for r in res)
+        assert srv.http.stats()["fast"] >= n
+    finally:
+        srv.stop()
+
+
+def test_access_log_uvicorn_format(iris_cwd, tmp_path):
+    from mlapi_amd.serve.server import NativeServer
+    from mlapi_amd.utils.config import Config
+
+    r, w = os.pipe()
+    srv = NativeServer(Config.from_env(port=0, device="cpu", io_threads=1, access_log=True), access_log_fd=w)
+    srv.start()
+    try:
+        raw(srv.port, post(A1))
+        raw(srv.port, b"GET /nope HTTP/1.1\r\nHost: t\r\n\r\n")
+        time.sleep(0.5)
+        os.set_blocking(r, False)
+        text = os.read(r, 65536).decode()
+    finally:
+        srv.stop()
+        os.close(r)
+        os.close(w)
+    lines = text.strip().splitlines()
+    assert re.match(r'^INFO:     127\.0\.0\.1:\d+ - "POST /predict HTTP/1\.1" 200 OK$', lines[0]), lines
+    assert re.match(r'^INFO:     127\.0\.0\.1:\d+ - "GET /nope HTTP/1\.1" 404 Not Found$', lines[1]), lines
 
 
 @settings(max_examples=300, deadline=None)

@@ -89,59 +89,42 @@ def test_native_server_gpu_end_to_end(iris_cwd, native):
         assert stats["batches"] < stats["requests"], "concurrent requests must be coalesced into batches"
 
 
-# ---- persistent (resident-kernel) serving mode -------------------------------------------------
-@pytest.mark.parametrize("dtype", [0, 1])
-@pytest.mark.parametrize("kind,K", [(Kind.MULTINOMIAL, 3), (Kind.BINARY, 1), (Kind.OVR, 5), (Kind.MULTINOMIAL, 40)])
-def test_engine_persistent_matches_oracle(native, dtype, kind, K):
-    F = 4 if K < 40 else 48  # K=40/F=48 exercises the generic row path inside the resident kernel
-    m = LinearModel.random(F, 2 if K == 1 else K, seed=K, kind=kind)
-    e = _engine(native, dtype=dtype, max_batch=64, persistent=True)
+# ---- small-model launch modes: kernel-argument batches vs zero-copy pinned rows ------------------
+@pytest.mark.parametrize("inline", [True, False])
+@pytest.mark.parametrize("max_batch", [16, 256])
+def test_engine_small_inline_and_zero_copy(native, inline, max_batch):
+    m = LinearModel.random(4, 3, seed=7)
+    e = _engine(native, max_batch=max_batch, inline_args=inline)
     try:
         e.load_model(int(m.kind), m.W, m.b, m.label_json())
-        X = np.random.default_rng(2).standard_normal((3000, F))
+        assert e.model_path() == "small"
+        X = np.random.default_rng(8).standard_normal((4000, 4))
         idx, p, st = e.predict(X)
         ridx, rp = m.predict_max(X)
         assert (st == 0).all()
         np.testing.assert_array_equal(idx, ridx)
-        np.testing.assert_allclose(p, rp, rtol=1e-12 if dtype == 0 else 1e-5, atol=0 if dtype == 0 else 1e-6)
+        np.testing.assert_allclose(p, rp, rtol=1e-12, atol=0)
         s = e.stats()
-        assert s["requests"] == 3000 and s["kernel_launches"] >= 1
+        assert s["path_batches"]["small"] == s["batches"]
+        if not inline:
+            assert s["inline_batches"] == 0
+        elif max_batch == 16:
+            assert s["inline_batches"] == s["batches"]  # 16 rows x 4 x f64 always fit
     finally:
         e.stop()
 
 
-def test_engine_persistent_idle_exit_relaunch_reload_and_sync(native):
-    import time
-
-    import torch
-
-    m1, m2 = LinearModel.random(4, 3, seed=1), LinearModel.random(4, 3, seed=2)
-    e = _engine(native, persistent=True, persistent_idle_ms=3, max_batch=16)
-    try:
-        e.load_model(int(m1.kind), m1.W, m1.b, m1.label_json())
-        X = np.random.default_rng(3).standard_normal((200, 4))
-        np.testing.assert_array_equal(e.predict(X)[0], m1.predict_max(X)[0])
-        time.sleep(0.05)  # > idle timeout: the resident kernel leaves ...
-        t0 = time.perf_counter()
-        torch.cuda.synchronize()  # ... so a device-wide synchronize returns
-        assert time.perf_counter() - t0 < 1.0
-        e.load_model(int(m2.kind), m2.W, m2.b, m2.label_json())  # hot reload between batches
-        idx, p, st = e.predict(X)  # relaunched on demand
-        np.testing.assert_array_equal(idx, m2.predict_max(X)[0])
-        assert (st == 0).all() and e.stats()["kernel_launches"] >= 2
-    finally:
-        e.stop()
-
-
-def test_engine_persistent_fault_injection_keeps_order(native):
+def test_engine_drop_injection_and_recovery(native):
     m = LinearModel.random(4, 3, seed=0)
-    e = _engine(native, persistent=True, fail_every=3, max_batch=1)
+    e = _engine(native, max_batch=8)
     try:
         e.load_model(int(m.kind), m.W, m.b, m.label_json())
-        X = np.random.default_rng(4).standard_normal((12, 4))
-        idx, p, st = e.predict(X)
-        assert (st == 4).sum() == 4 and (st == 0).sum() == 8  # every 3rd single-row batch fails
-        ok = st == 0
-        np.testing.assert_array_equal(idx[ok], m.predict_max(X)[0][ok])
+        e.inject_drop(True)
+        _, _, st = e.predict(np.ones((5, 4)))
+        assert (st == 4).all() and not e.healthy() and e.stats()["dropped"]
+        e.inject_drop(False)
+        e.mark_healthy()
+        idx, _, st = e.predict(np.ones((5, 4)))
+        assert (st == 0).all() and e.healthy()
     finally:
         e.stop()

@@ -1,0 +1,142 @@
+"""Wide models on the /predict hot path: the engine routes binary models to the bf16 GEMV kernel
+and multiclass models to the MFMA gemm_softmax kernel (reference call sites
+/root/reference/main.py:21-22). Every result is compared with the float64 oracle evaluated on the
+bf16-rounded inputs the kernel actually sees (tolerance table: labels exact unless the top-2
+logit margin is < 1e-3, p_max rel 1e-4)."""
+import json
+import socket
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from mlapi_amd.models.linear import Kind, LinearModel
+
+pytestmark = pytest.mark.gpu
+
+DT = {"f64": 0, "f32": 1, "bf16": 2}
+
+
+def bf16_round(a):
+    u = np.ascontiguousarray(np.asarray(a, dtype=np.float32)).view(np.uint32).astype(np.uint64)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return u.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+def rounded_oracle(m: LinearModel, X, xdt):
+    """The model and rows as the kernel reads them."""
+    if xdt == "bf16":
+        Wr, Xr, br = bf16_round(m.W), bf16_round(X), m.b.astype(np.float32).astype(np.float64)
+    elif xdt == "f32":
+        Wr, Xr, br = (a.astype(np.float32).astype(np.float64) for a in (m.W, X, m.b))
+    else:
+        Wr, Xr, br = m.W, np.asarray(X, dtype=np.float64), m.b
+    return LinearModel(Wr, br, m.classes, m.kind), Xr
+
+
+def check(m: LinearModel, X, idx, p, xdt, rtol=1e-4):
+    om, Xr = rounded_oracle(m, X, xdt)
+    ridx, rp = om.predict_max(Xr)
+    z = om.decision_function(Xr)
+    if z.ndim == 1:
+        margin = np.abs(z)
+    else:
+        zs = np.sort(z, axis=1)
+        margin = zs[:, -1] - zs[:, -2]
+    bad = (idx != ridx) & (margin > 1e-3)
+    assert not bad.any(), f"{bad.sum()} label mismatches away from ties"
+    np.testing.assert_allclose(p, rp, rtol=rtol, atol=1e-6)
+
+
+def _engine(native, **kw):
+    cfg = native.EngineConfig()
+    cfg.device = 0
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return native.Engine(cfg)
+
+
+@pytest.mark.parametrize("F,K,kind,wide,path", [
+    (256, 2, Kind.BINARY, "bf16", "gemv"),
+    (256, 2, Kind.BINARY_SOFTMAX, "bf16", "gemv"),
+    (100, 2, Kind.BINARY, "bf16", "gemv"),        # F padded to 104
+    (256, 2, Kind.BINARY, "f32", "gemv"),
+    (256, 1000, Kind.MULTINOMIAL, "bf16", "gemm"),
+    (256, 50, Kind.OVR, "bf16", "gemm"),
+    (100, 10, Kind.MULTINOMIAL, "bf16", "gemm"),  # F padded to 128
+    (512, 300, Kind.MULTINOMIAL, "bf16", "gemm"),
+    (48, 40, Kind.MULTINOMIAL, "f32", "generic"),
+    (48, 40, Kind.OVR, "f64", "generic"),
+])
+def test_engine_wide_paths_match_oracle(native, F, K, kind, wide, path):
+    m = LinearModel.random(F, K, seed=F + K, kind=kind)
+    e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide])
+    try:
+        e.load_model(int(m.kind), m.W, m.b, m.label_json())
+        assert e.model_path() == path
+        X = np.random.default_rng(F * K).standard_normal((3000, F))
+        idx, p, st = e.predict(X)
+        assert (st == 0).all()
+        check(m, X, idx, p, "f64" if path == "generic" and wide == "f64" else wide,
+              rtol=1e-12 if wide == "f64" else 1e-4)
+        s = e.stats()
+        assert s["path_batches"][path] == s["batches"] and s["requests"] == 3000
+    finally:
+        e.stop()
+
+
+def _post(port, bodies):
+    out = []
+    s = socket.create_connection(("127.0.0.1", port), timeout=30)
+    try:
+        for body in bodies:
+            s.sendall(b"POST /predict HTTP/1.1\r\nHost: t\r\nContent-Type: application/json\r\n"
+                      b"Content-Length: %d\r\n\r\n%s" % (len(body), body))
+            buf = b""
+            while b"\r\n\r\n" not in buf:
+                buf += s.recv(65536)
+            head, rest = buf.split(b"\r\n\r\n", 1)
+            n = int([l.split(b":")[1] for l in head.split(b"\r\n") if l.lower().startswith(b"content-length")][0])
+            while len(rest) < n:
+                rest += s.recv(65536)
+            out.append((int(head.split()[1]), rest[:n]))
+    finally:
+        s.close()
+    return out
+
+
+@pytest.mark.parametrize("K,kind", [(2, Kind.BINARY), (1000, Kind.MULTINOMIAL)])
+def test_native_server_wide_model_every_response(native, K, kind):
+    from mlapi_amd.serve.server import NativeServer
+    from mlapi_amd.utils.config import Config
+
+    F = 256
+    names = [f"f{i}" for i in range(F)]
+    m = LinearModel.random(F, K, seed=K, kind=kind, labels=[f"c{i}" for i in range(K)])
+    cfg = Config.from_env(port=0, device="cuda:0", feature_names=names, reload="off", missing_model="keep",
+                          model_path="/nonexistent/wide.pkl", io_threads=4)
+    srv = NativeServer(cfg)
+    srv.runtime.handle.load(m)
+    srv.start()
+    try:
+        rng = np.random.default_rng(5)
+        X = rng.standard_normal((1024, F))
+        bodies = [json.dumps(dict(zip(names, map(float, row))), separators=(",", ":")).encode() for row in X]
+        with ThreadPoolExecutor(16) as ex:  # 16 concurrent connections -> coalesced batches
+            parts = list(ex.map(lambda j: _post(srv.port, bodies[j::16]), range(16)))
+        res = [None] * len(bodies)
+        for j, part in enumerate(parts):
+            for i, r in enumerate(part):
+                res[j + 16 * i] = r
+        assert all(st == 200 for st, _ in res)
+        got = [json.loads(b) for _, b in res]
+        idx = np.array([int(g["prediction"][1:]) for g in got])
+        p = np.array([g["probability"] for g in got])
+        check(m, X, idx, p, "bf16")
+        st = srv.runtime.handle.stats()
+        path = "gemv" if K == 2 else "gemm"
+        assert st["path_batches"][path] >= 1 and st["path_batches"]["generic"] == 0
+        assert st["batches"] < st["requests"]
+        assert srv.http.stats()["fast"] >= 1024  # no request fell back to the Python slow path
+    finally:
+        srv.stop()
