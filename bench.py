@@ -7,12 +7,18 @@
 serve (flagship, BASELINE config 1/4): every rank runs the full production stack on its GPU -
 native HTTP server -> batching engine -> fused fp64 HIP kernel -> JSON response - with the Iris
 LogisticRegression architecture (F=4 features, K=3 classes; random-init weights, seeded,
-broadcast from rank 0 over RCCL = collective C1), and a native closed-loop load generator with
-64 keep-alive connections ("batch=64": 64 concurrent single-row POST /predict requests).
-  step  = each of the 64 connections completes --reqs-per-conn (16) requests = 1024 requests/rank
-  value = whole-node requests/s = N * K * 1024 / max-over-ranks elapsed
+broadcast from rank 0 over RCCL = collective C1). All ranks' servers share ONE SO_REUSEPORT port
+(the dp_serve topology, health-aware dispatch at N > 1); each rank drives it with its own
+out-of-process native load generator (mlapi-loadgen, pinned apart from the server threads when
+the rank is pinned): 64 keep-alive connections ("batch=64": 64 concurrent single-row POST
+/predict requests) cycling through 1024 distinct Iris-like requests, every response body checked
+byte for byte against the engine's answer (itself checked against the fp64 oracle).
+  step  = each of the 64 connections completes --reqs-per-conn (2048) requests = 131,072 requests
+          per rank (~0.1-0.2 s, so the driver's --steps 20 times >= 2 s)
+  value = whole-node requests/s = requests completed by all ranks / max-over-ranks elapsed
   p50/p99 at concurrency 64 come from the timed run; batch=1 latency (concurrency 1) is measured
-  afterwards on every rank and reported as extra fields.
+  afterwards by rank 0 alone and reported as extra fields.
+serve_wide: the same with an F=256 model (--wide-classes 1000: MFMA gemm_softmax; 2: bf16 GEMV).
 Other modes (extra evidence, not the headline): gemv (config 2: 1M x 256 bf16 binary predict),
 gemm (config 3: B=1024, F=256, K=1000 bf16 multiclass predict), train (config 5: binary LR
 mini-batch SGD, F=256 bf16, DP gradient all-reduce).
@@ -30,6 +36,7 @@ import numpy as np
 # Reference numbers (measured on the reference itself, CPU, no published numbers):
 BASELINES = {
     "serve": 1494.0,       # req/s, 1 uvicorn worker, concurrency 64
+    "serve_wide": None,    # the reference serves Iris only
     "gemv": 1.00e6,        # rows/s, sklearn binary 1M x 256 predict+proba
     "gemm": 87075.0,       # rows/s, sklearn 1000-class B=1024 F=256
     "train": 3.73e6,       # sample-gradients/s, sklearn lbfgs binary 100k x 256
@@ -59,80 +66,146 @@ def _timed(info, fn):
     return all_reduce_max(t1 - t0, info), out
 
 
-def bench_serve(args, info):
-    from mlapi_amd._native import C
-    from mlapi_amd.models.linear import LinearModel
-    from mlapi_amd.parallel.comm import all_gather_floats, barrier, broadcast_model
+def _share_port(port: int, info) -> int:
+    """Rank 0's bound port, known to every rank (the shared SO_REUSEPORT port of the DP group)."""
+    from mlapi_amd.parallel.comm import all_gather_floats
+
+    return int(all_gather_floats([float(port)], info)[0, 0])
+
+
+def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_kw, model_desc, features):
+    """Production topology on every rank: native HTTP server + batching engine + HIP kernel, all
+    ranks in ONE SO_REUSEPORT group on a shared port (health-aware dispatch on at N > 1), driven by
+    an out-of-process native load generator per rank (pinned apart from the server when the rank
+    is pinned) whose every response body is validated."""
+    from mlapi_amd.parallel.comm import all_gather_floats, barrier
+    from mlapi_amd.serve.loadgen import make_workload
     from mlapi_amd.serve.server import NativeServer
     from mlapi_amd.utils.config import Config
+    from mlapi_amd.utils.threads import cpu_by_group, utilization
 
-    model = LinearModel.random(4, 3, seed=0, labels=IRIS_LABELS) if info.is_main else None
-    model = broadcast_model(model, info)  # C1 over RCCL
+    lg = args.lg_proc
     device = "cpu" if info.device is None else f"cuda:{info.device.index}"
-    cfg = Config.from_env(port=0, device=device, reload="off", missing_model="keep", io_threads=args.io_threads,
-                          max_batch=args.max_batch, model_path="/nonexistent/bench.pkl")
-    srv = NativeServer(cfg)
-    srv.runtime.handle.load(model)
-    srv.start()
-    body = json.dumps({"sepal_length": 5.1, "sepal_width": 3.5, "petal_length": 1.4, "petal_width": 0.2},
-                      separators=(",", ":")).encode()
-    req = (b"POST /predict HTTP/1.1\r\nHost: 127.0.0.1\r\nContent-Type: application/json\r\n"
-           b"Content-Length: %d\r\n\r\n%s" % (len(body), body)).decode()
+    mk = lambda port: Config.from_env(port=port, device=device, reload="off", missing_model="keep",  # noqa: E731
+                                      io_threads=args.io_threads, max_batch=args.max_batch, reuseport=True,
+                                      model_path="/nonexistent/bench.pkl", feature_names=list(names), **dtype_cfg)
+    srv = None
+    if info.is_main:  # rank 0 binds an ephemeral port, the other ranks join its SO_REUSEPORT group
+        srv = NativeServer(mk(0))
+        srv.runtime.handle.load(model)
+        srv.start()
+    port = _share_port(srv.port if srv is not None else 0, info)
+    if srv is None:
+        srv = NativeServer(mk(port))
+        srv.runtime.handle.load(model)
+        srv.start()
+    reqs, exp = make_workload(srv.runtime.handle.engine, model, names, rows, **oracle_kw)
+    lg.workload(reqs, exp, rel_tol)
+    barrier(info)  # every rank's listeners are in the group before any client connects
     try:
-        lg = C().Loadgen("127.0.0.1", srv.port, req, args.conns, args.client_threads, 60.0)
+        lg.connect("127.0.0.1", port, args.conns, args.client_threads)
         if args.warmup:
             w = lg.run(args.warmup * args.reqs_per_conn, False)
-            if w["failed"]:
+            if w["failed"] or w["errors"]:
                 raise RuntimeError(f"warmup failed: {w}")
-        from mlapi_amd.utils.threads import cpu_by_group, utilization
-
         s0 = srv.runtime.handle.stats()
-        c0 = cpu_by_group()
+        c0, l0 = cpu_by_group(), cpu_by_group(lg.pid)
         elapsed, res = _timed(info, lambda: lg.run(args.steps * args.reqs_per_conn, True))
         cpu_util = utilization(c0, cpu_by_group(), elapsed)
+        cpu_util["loadgen_process"] = utilization(l0, cpu_by_group(lg.pid), elapsed).get("process_total", 0.0)
         s1 = srv.runtime.handle.stats()
-        lg.close()
-        if res["failed"] or res["status_counts"].get(200, 0) != args.steps * args.reqs_per_conn * args.conns:
-            raise RuntimeError(f"load generator saw errors: {res['status_counts']} failed={res['failed']}")
-        lat = res["latencies_ns"] / 1e6
-        # batch=1: one connection, closed loop
-        lg1 = C().Loadgen("127.0.0.1", srv.port, req, 1, 1, 60.0)
-        lg1.run(200, False)
-        s2 = srv.runtime.handle.stats()
-        r1 = lg1.run(args.c1_requests, True)
-        s3 = srv.runtime.handle.stats()
-        lg1.close()
-        lat1 = r1["latencies_ns"] / 1e6
-        per_rank = all_gather_floats([np.percentile(lat, 50), np.percentile(lat, 99), np.percentile(lat1, 50),
-                                      np.percentile(lat1, 99), r1["completed"] / r1["elapsed_s"],
-                                      (s1["requests"] - s0["requests"]) / max(1, s1["batches"] - s0["batches"]),
-                                      (s1["device_us_sum"] - s0["device_us_sum"]) / max(1, s1["batches"] - s0["batches"]),
-                                      (s3["device_us_sum"] - s2["device_us_sum"]) / max(1, s3["batches"] - s2["batches"])],
-                                     info)
+        lg.cmd("close")
+        want = args.steps * args.reqs_per_conn * args.conns
+        if res["failed"] or res["errors"] or res["body_mismatches"] or res["ok200"] != want:
+            raise RuntimeError(f"load generator saw errors: {res}")
+        # batch = 1: one client, closed loop, measured by rank 0 alone (the other ranks idle)
+        r1 = {"p50_ns": 0, "p99_ns": 0, "completed": 0, "elapsed_s": 1.0}
         barrier(info)
+        s2 = srv.runtime.handle.stats()
+        if info.is_main:
+            lg.connect("127.0.0.1", port, 1, 1)
+            lg.run(200, False)
+            s2 = srv.runtime.handle.stats()
+            r1 = lg.run(args.c1_requests, True)
+            lg.cmd("close")
+            if r1["errors"] or r1["body_mismatches"]:
+                raise RuntimeError(f"batch=1 run saw errors: {r1}")
+        s3 = srv.runtime.handle.stats()
+        barrier(info)
+        nb = max(1, s1["batches"] - s0["batches"])
+        per_rank = all_gather_floats([res["p50_ns"] / 1e6, res["p99_ns"] / 1e6, res["completed"],
+                                      (s1["requests"] - s0["requests"]) / nb,
+                                      (s1["device_us_sum"] - s0["device_us_sum"]) / nb,
+                                      (s3["device_us_sum"] - s2["device_us_sum"]) / max(1, s3["batches"] - s2["batches"]),
+                                      s1["requests"] - s0["requests"]], info)
+        barrier(info)
+        paths = {k: s1["path_batches"][k] - s0["path_batches"][k] for k in s1["path_batches"]}
     finally:
         srv.stop()
-    total = info.world * args.steps * args.reqs_per_conn * args.conns
+    total = float(np.sum(per_rank[:, 2]))
     value = total / elapsed
     extra = {
         "p50_latency_ms_c64": float(np.max(per_rank[:, 0])),
         "p99_latency_ms_c64": float(np.max(per_rank[:, 1])),
-        "p50_latency_ms_batch1": float(np.max(per_rank[:, 2])),
-        "p99_latency_ms_batch1": float(np.max(per_rank[:, 3])),
-        "req_per_s_batch1_per_rank": float(np.min(per_rank[:, 4])),
-        "mean_gpu_batch_rows": float(np.mean(per_rank[:, 5])),
+        "p50_latency_ms_batch1": r1["p50_ns"] / 1e6,
+        "p99_latency_ms_batch1": r1["p99_ns"] / 1e6,
+        "req_per_s_batch1": r1["completed"] / r1["elapsed_s"],
+        "timed_region_s": elapsed,
+        "body_mismatches": 0,
+        "validated_responses": int(total),
+        "served_per_rank": [int(v) for v in per_rank[:, 6]],
+        "mean_gpu_batch_rows": float(np.mean(per_rank[:, 3])),
         # launch -> completion seen by the completer thread, per batch (the GPU leg of a request)
-        "gpu_leg_us_c64": float(np.mean(per_rank[:, 6])),
-        "gpu_leg_us_batch1": float(np.mean(per_rank[:, 7])),
+        "gpu_leg_us_c64": float(np.mean(per_rank[:, 4])),
+        "gpu_leg_us_batch1": float(per_rank[0, 5]),
+        "kernel_batches": paths,
         "backend": srv.runtime.handle.backend,
         "cpu_cores_busy_rank0": cpu_util,
         "threads": {"io": args.io_threads, "loadgen": args.client_threads, "pinned_cpus": args.pinned_cpus},
         "requests_per_step": args.reqs_per_conn * args.conns * info.world,
-        "baseline_note": "reference uvicorn+sklearn, 1 worker, c=64: 1494 req/s, p50 41.8 ms; c=1 p50 0.881 ms",
+        "topology": "one SO_REUSEPORT port shared by all ranks; one out-of-process load generator per rank",
     }
     return ("requests_per_sec_whole_node", value, "req/s", elapsed, extra,
-            {"model": "sklearn LogisticRegression (Iris: F=4, K=3) via POST /predict", "global_batch": args.conns * info.world,
-             "seq_len": 1, "features": 4, "parallelism": f"dp{info.world}", "concurrency_per_gpu": args.conns})
+            {"model": model_desc, "global_batch": args.conns * info.world, "seq_len": 1, "features": features,
+             "parallelism": f"dp{info.world}", "concurrency_per_gpu": args.conns})
+
+
+def bench_serve(args, info):
+    """Headline: the reference's Iris /predict (F=4, K=3, fp64 = sklearn parity)."""
+    from mlapi_amd.models.linear import LinearModel
+    from mlapi_amd.parallel.comm import broadcast_model
+    from mlapi_amd.utils.config import IRIS_FEATURES
+
+    model = LinearModel.random(4, 3, seed=0, labels=IRIS_LABELS) if info.is_main else None
+    model = broadcast_model(model, info)  # C1 over RCCL
+    rng = np.random.default_rng(7)
+    rows = np.round(np.array([5.84, 3.05, 3.76, 1.2]) + rng.standard_normal((args.workload_rows, 4))
+                    * np.array([0.83, 0.43, 1.76, 0.76]), 1)  # Iris-like requests, 1 decimal like the dataset
+    extra_note = {"baseline_note": "reference uvicorn+sklearn, 1 worker, c=64: 1494 req/s, p50 41.8 ms; "
+                                   "c=1 p50 0.881 ms"}
+    out = _serve_bench(args, info, model, IRIS_FEATURES, rows, dtype_cfg={"dtype": "f64"}, rel_tol=0.0,
+                       oracle_kw={"rtol_oracle": 1e-12}, features=4,
+                       model_desc="sklearn LogisticRegression (Iris: F=4, K=3) via POST /predict")
+    out[4].update(extra_note)
+    return out
+
+
+def bench_serve_wide(args, info):
+    """Wide model on the /predict hot path: F=256, K classes (2 -> bf16 GEMV kernel, else the
+    MFMA gemm_softmax kernel), bodies validated against the engine within rel 1e-5."""
+    from mlapi_amd.models.linear import LinearModel
+    from mlapi_amd.parallel.comm import broadcast_model
+    from mlapi_amd.serve.loadgen import bf16_oracle
+
+    F, K = 256, args.wide_classes
+    names = [f"f{i}" for i in range(F)]
+    model = LinearModel.random(F, K, seed=0, labels=[f"class_{i}" for i in range(K)]) if info.is_main else None
+    model = broadcast_model(model, info)
+    rows = np.round(np.random.default_rng(7).standard_normal((args.workload_rows, F)), 3)
+    return _serve_bench(args, info, model, names, rows, dtype_cfg={"wide_dtype": "bf16"}, rel_tol=1e-5,
+                        oracle_kw={"rtol_oracle": 1e-4, "label_margin": 1e-3, "oracle": bf16_oracle(model, rows)},
+                        features=F, model_desc=f"LogisticRegression F={F} K={K} ({'binary' if K == 2 else 'softmax'}) "
+                                               "via POST /predict, bf16 kernels")
 
 
 def bench_gemv(args, info):
@@ -230,9 +303,13 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--mode", default="serve", choices=["serve", "gemv", "gemm", "train", "train_softmax"])
+    ap.add_argument("--mode", default="serve",
+                    choices=["serve", "serve_wide", "gemv", "gemm", "train", "train_softmax"])
     ap.add_argument("--conns", type=int, default=64)
-    ap.add_argument("--reqs-per-conn", type=int, default=16)
+    ap.add_argument("--reqs-per-conn", type=int, default=2048,
+                    help="serve: one step = conns x this many requests per rank (~0.1-0.2 s)")
+    ap.add_argument("--workload-rows", type=int, default=1024, help="serve: distinct validated requests")
+    ap.add_argument("--wide-classes", type=int, default=1000, help="serve_wide: 2 = binary GEMV, else softmax GEMM")
     ap.add_argument("--client-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--io-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--max-batch", type=int, default=256)
@@ -247,6 +324,11 @@ def main(argv=None) -> int:
                     help="pin this rank to its share of physical cores on its GPU's NUMA node "
                          "(auto: when several ranks share the node and no launcher pinned them)")
     args = ap.parse_args(argv)
+    if args.mode in ("serve", "serve_wide"):
+        # the load generator is its own process, started before anything touches the GPU
+        from mlapi_amd.serve.loadgen import LoadgenProcess
+
+        args.lg_proc = LoadgenProcess()
 
     from mlapi_amd.parallel.comm import init_distributed, shutdown
 
@@ -272,12 +354,23 @@ def main(argv=None) -> int:
         cl = max(2, min(6, per_rank - io - 2))
         args.io_threads = args.io_threads if args.io_threads > 0 else io
         args.client_threads = args.client_threads if args.client_threads > 0 else cl
+    if pinned and getattr(args, "lg_proc", None) is not None and len(pinned) > args.io_threads + 3:
+        # server threads (IO + batcher + completer) and the load generator on disjoint CPUs
+        import os as _os
+
+        n_srv = args.io_threads + 2
+        _os.sched_setaffinity(0, pinned[:n_srv])
+        args.lg_proc.pin(pinned[n_srv:])
     if args.mode != "serve" and info.device is None:
         print(f"mode {args.mode} needs a GPU", file=sys.stderr)
         return 2
-    fn = {"serve": bench_serve, "gemv": bench_gemv, "gemm": bench_gemm, "train": bench_train,
-          "train_softmax": bench_train_softmax}[args.mode]
-    metric, value, unit, elapsed, extra, config = fn(args, info)
+    fn = {"serve": bench_serve, "serve_wide": bench_serve_wide, "gemv": bench_gemv, "gemm": bench_gemm,
+          "train": bench_train, "train_softmax": bench_train_softmax}[args.mode]
+    try:
+        metric, value, unit, elapsed, extra, config = fn(args, info)
+    finally:
+        if getattr(args, "lg_proc", None) is not None:
+            args.lg_proc.close()
     if info.is_main:
         line = {
             "metric": metric, "value": value, "unit": unit, "n_gpus": info.world, "steps": args.steps,
@@ -285,6 +378,7 @@ def main(argv=None) -> int:
             "scaling": "weak", "vs_baseline": None if BASELINES[args.mode] is None else value / BASELINES[args.mode],
             "dtype": "fp64" if args.mode == "serve" else "bf16",
             "data": "synthetic (random-init weights, fixed synthetic inputs)", "config": config,
+            "comm_backend": info.backend,
         }
         line.update(extra)
         print(json.dumps(line), flush=True)

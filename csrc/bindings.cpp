@@ -522,6 +522,7 @@ PYBIND11_MODULE(_C, m) {
             d["completed"] = r.completed;
             d["errors"] = r.errors;
             d["failed"] = r.failed;
+            d["body_mismatches"] = r.body_mismatches;
             py::array_t<int64_t> lat((py::ssize_t)r.latencies_ns.size());
             if (!r.latencies_ns.empty())
               std::memcpy(lat.mutable_data(), r.latencies_ns.data(), r.latencies_ns.size() * sizeof(int64_t));
@@ -533,5 +534,7 @@ PYBIND11_MODULE(_C, m) {
             return d;
           },
           py::arg("requests_per_conn"), py::arg("record") = true)
+      .def("set_workload", &Loadgen::set_workload, py::arg("requests"), py::arg("expected"),
+           py::arg("rel_tol") = 0.0)
       .def("close", &Loadgen::close_all);
 }

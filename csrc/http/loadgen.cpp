@@ -1,10 +1,12 @@
 // Closed-loop HTTP/1.1 load generator (no wrk/ab/hey in the image; a single aiohttp
 // client caps at ~7.4k req/s, far below what the native server sustains).
 //
-// `threads` epoll loops share `conns` keep-alive connections; every connection sends the same
-// request, waits for the complete response (status line + content-length body), records the
-// latency, and immediately sends the next one until it has completed `n` requests. One send() per
-// request, TCP_NODELAY, so the client itself never introduces Nagle stalls.
+// `threads` epoll loops share `conns` keep-alive connections; every connection cycles through the
+// workload's requests, waits for the complete response (status line + content-length body),
+// checks the body byte for byte against the expected one (a wrong label or probability at HTTP
+// 200 is a failure, not throughput), records the latency, and immediately sends the next one
+// until it has completed `n` requests. One send() per request, TCP_NODELAY, so the client itself
+// never introduces Nagle stalls.
 #include "loadgen.h"
 
 #include <arpa/inet.h>
@@ -16,6 +18,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cmath>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -36,6 +39,7 @@ struct LgConn {
   int fd = -1;
   std::string in;
   size_t sent = 0;
+  size_t next = 0;  // workload entry of the outstanding request
   int64_t t_send = 0;
   int64_t remaining = 0;
   bool active = false;
@@ -43,7 +47,7 @@ struct LgConn {
 
 Loadgen::Loadgen(const std::string& host, int port, const std::string& request, int conns, int threads,
                  double timeout_s)
-    : host_(host), port_(port), request_(request), timeout_s_(timeout_s) {
+    : host_(host), port_(port), requests_{request}, timeout_s_(timeout_s) {
   if (conns < 1) conns = 1;
   if (threads < 1) threads = 1;
   if (threads > conns) threads = conns;
@@ -71,6 +75,16 @@ Loadgen::Loadgen(const std::string& host, int port, const std::string& request, 
 
 Loadgen::~Loadgen() { close_all(); }
 
+void Loadgen::set_workload(const std::vector<std::string>& requests, const std::vector<std::string>& expected,
+                           double rel_tol) {
+  rel_tol_ = rel_tol;
+  if (requests.empty()) throw std::invalid_argument("loadgen: empty workload");
+  if (!expected.empty() && expected.size() != requests.size())
+    throw std::invalid_argument("loadgen: one expected body per request");
+  requests_ = requests;
+  expected_ = expected;
+}
+
 void Loadgen::close_all() {
   for (auto& c : conns_)
     if (c && c->fd >= 0) {
@@ -81,7 +95,21 @@ void Loadgen::close_all() {
 
 // Parses one complete response at the front of `in`. Returns bytes consumed (0 if incomplete),
 // -1 on protocol error. *status receives the HTTP status code.
-static int64_t parse_response(const std::string& in, int* status) {
+// Body check: exact bytes, or (rel_tol > 0) exact up to the last ':' and the trailing number
+// (up to the closing brace) within rel_tol.
+static bool body_matches(const char* b, size_t n, const std::string& ex, double rel_tol) {
+  if (rel_tol <= 0) return n == ex.size() && memcmp(b, ex.data(), n) == 0;
+  const size_t ce = ex.rfind(':');
+  if (ce == std::string::npos || n <= ce || memcmp(b, ex.data(), ce + 1) != 0) return false;
+  const std::string got(b + ce + 1, n - ce - 1), want = ex.substr(ce + 1);
+  char* e1 = nullptr;
+  char* e2 = nullptr;
+  const double x = strtod(got.c_str(), &e1), y = strtod(want.c_str(), &e2);
+  if (e1 == got.c_str() || e2 == want.c_str() || std::strcmp(e1, e2) != 0) return false;
+  return std::fabs(x - y) <= rel_tol * std::fabs(y);
+}
+
+static int64_t parse_response(const std::string& in, int* status, size_t* body_off) {
   const size_t he = in.find("\r\n\r\n");
   if (he == std::string::npos) return 0;
   if (in.size() < 12 || in.compare(0, 5, "HTTP/") != 0) return -1;
@@ -95,6 +123,7 @@ static int64_t parse_response(const std::string& in, int* status) {
   }
   const int64_t total = (int64_t)he + 4 + clen;
   if ((int64_t)in.size() < total) return 0;
+  *body_off = he + 4;
   return total;
 }
 
@@ -103,7 +132,7 @@ LoadgenResult Loadgen::run(int64_t requests_per_conn, bool record) {
   const int nc = (int)conns_.size();
   std::vector<std::vector<int64_t>> lats(threads_);
   std::vector<std::vector<uint64_t>> statuses(threads_, std::vector<uint64_t>(600, 0));
-  std::vector<uint64_t> errs(threads_, 0);
+  std::vector<uint64_t> errs(threads_, 0), mism(threads_, 0);
   std::atomic<int> failed{0};
   const int64_t t0 = mono_ns();
   auto worker = [&](int ti) {
@@ -113,11 +142,13 @@ LoadgenResult Loadgen::run(int64_t requests_per_conn, bool record) {
     for (int i = ti; i < nc; i += threads_) mine.push_back(conns_[i].get());
     if (record) lats[ti].reserve((size_t)(requests_per_conn * (int64_t)mine.size()));
     int live = 0;
+    const size_t nw = requests_.size();
     auto send_req = [&](LgConn* c) -> bool {
       c->t_send = mono_ns();
+      const std::string& rq = requests_[c->next];
       size_t off = 0;
-      while (off < request_.size()) {
-        const ssize_t w = send(c->fd, request_.data() + off, request_.size() - off, MSG_NOSIGNAL);
+      while (off < rq.size()) {
+        const ssize_t w = send(c->fd, rq.data() + off, rq.size() - off, MSG_NOSIGNAL);
         if (w <= 0) {
           if (w < 0 && errno == EINTR) continue;
           return false;
@@ -130,6 +161,7 @@ LoadgenResult Loadgen::run(int64_t requests_per_conn, bool record) {
       LgConn* c = mine[k];
       c->remaining = requests_per_conn;
       c->in.clear();
+      c->next = (size_t)(ti + k * threads_) % nw;  // = connection index mod workload size
       if (c->remaining <= 0) continue;
       epoll_event ev{};
       ev.events = EPOLLIN;
@@ -164,14 +196,23 @@ LoadgenResult Loadgen::run(int64_t requests_per_conn, bool record) {
         c->in.append(buf, (size_t)r);
         for (;;) {
           int st = 0;
-          const int64_t used = parse_response(c->in, &st);
+          size_t boff = 0;
+          const int64_t used = parse_response(c->in, &st, &boff);
           if (used == 0) break;
           if (used < 0) {
             failed.store(4);
             break;
           }
           const int64_t now = mono_ns();
+          if (st == 200 && !expected_.empty()) {
+            const std::string& ex = expected_[c->next];
+            if (!body_matches(c->in.data() + boff, (size_t)used - boff, ex, rel_tol_)) {
+              mism[ti]++;
+              errs[ti]++;
+            }
+          }
           c->in.erase(0, (size_t)used);
+          c->next = c->next + 1 == nw ? 0 : c->next + 1;
           if (st >= 0 && st < 600) statuses[ti][st]++;
           if (st != 200) errs[ti]++;
           if (record) lats[ti].push_back(now - c->t_send);
@@ -197,6 +238,7 @@ LoadgenResult Loadgen::run(int64_t requests_per_conn, bool record) {
   R.failed = failed.load();
   for (int t = 0; t < threads_; ++t) {
     R.errors += errs[t];
+    R.body_mismatches += mism[t];
     R.latencies_ns.insert(R.latencies_ns.end(), lats[t].begin(), lats[t].end());
     for (int s = 0; s < 600; ++s) R.status_counts[s] += statuses[t][s];
   }

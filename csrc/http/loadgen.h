@@ -10,6 +10,7 @@ namespace mlapi {
 struct LoadgenResult {
   double elapsed_s = 0;
   uint64_t completed = 0, errors = 0;
+  uint64_t body_mismatches = 0;  // 200 responses whose body differs from the expected bytes
   int failed = 0;  // nonzero: connection error / timeout code
   std::vector<int64_t> latencies_ns;
   uint64_t status_counts[600] = {0};
@@ -23,6 +24,13 @@ class Loadgen {
   Loadgen(const std::string& host, int port, const std::string& request, int conns, int threads,
           double timeout_s = 30.0);
   ~Loadgen();
+  // Distinct requests cycled per connection (connection c starts at entry c % n), each with the
+  // exact response body it must produce; empty `expected` = status-only checking.
+  // `rel_tol` > 0: the text after the body's last ':' (the probability) is compared as a number
+  // within rel_tol, the bytes before it exactly (batch-size-dependent reduction orders of the
+  // bf16 GEMM path change the last bits); 0 = the whole body byte for byte.
+  void set_workload(const std::vector<std::string>& requests, const std::vector<std::string>& expected,
+                    double rel_tol = 0.0);
   // Every connection completes `requests_per_conn` closed-loop requests.
   LoadgenResult run(int64_t requests_per_conn, bool record = true);
   void close_all();
@@ -30,7 +38,9 @@ class Loadgen {
  private:
   std::string host_;
   int port_;
-  std::string request_;
+  std::vector<std::string> requests_;
+  std::vector<std::string> expected_;
+  double rel_tol_ = 0.0;
   double timeout_s_ = 30.0;
   int threads_;
   std::vector<std::unique_ptr<LgConn>> conns_;

@@ -5,11 +5,21 @@
 #include "mlapi/kernels.h"
 
 namespace mlapi {
+[[noreturn]] static void unreachable(const char* what) {
+  throw std::logic_error(std::string("host-only test binary: ") + what + " must not be reached");
+}
 void launch_linear_small(int, const void*, int64_t, const void*, const void*, int64_t, int, int, int, int32_t*, void*,
                          hipStream_t) {
-  throw std::logic_error("host-only test binary: launch_linear_small must not be reached");
+  unreachable("launch_linear_small");
 }
-void launch_serve_persistent(int, ServeMailSlot*, uint32_t*, const uint32_t*, int, uint64_t, uint64_t, hipStream_t) {
-  throw std::logic_error("host-only test binary: launch_serve_persistent must not be reached");
+bool linear_inline_fits(int, int64_t, int, int) { return false; }
+void launch_linear_inline(int, const InlineBatch&, hipStream_t) { unreachable("launch_linear_inline"); }
+void launch_gemv_binary(int, const void*, const void*, float, int64_t, int, int, int32_t*, float*, hipStream_t) {
+  unreachable("launch_gemv_binary");
+}
+size_t gemm_softmax_workspace(int64_t, int, int) { return 0; }
+void launch_gemm_softmax(const void*, const void*, const float*, int64_t, int, int, int, int32_t*, float*, void*, size_t,
+                         hipStream_t) {
+  unreachable("launch_gemm_softmax");
 }
 }  // namespace mlapi

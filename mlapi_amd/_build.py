@@ -84,6 +84,30 @@ def _compile(src: str, force: bool, hmt: float) -> Path:
     return obj
 
 
+def loadgen_path() -> Path:
+    return ROOT / "mlapi_amd" / "bin" / "mlapi-loadgen"
+
+
+def _build_loadgen(force: bool, verbose: bool) -> Path:
+    """The standalone load-generator process (csrc/http/loadgen_main.cpp + loadgen.cpp): host-only
+    C++, no HIP, so benchmarks can run it on CPUs apart from the server."""
+    out = loadgen_path()
+    srcs = [CSRC / "http" / "loadgen_main.cpp", CSRC / "http" / "loadgen.cpp"]
+    newest = max(max(p.stat().st_mtime for p in srcs), _headers_mtime())
+    if not force and out.exists() and out.stat().st_mtime >= newest:
+        return out
+    out.parent.mkdir(parents=True, exist_ok=True)
+    cxx = shutil.which("g++") or shutil.which("c++") or hipcc()
+    cmd = [cxx, "-O2", "-std=c++17", f"-I{CSRC}", "-o", str(out) + ".tmp"] + [str(p) for p in srcs] + ["-lpthread"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"loadgen build failed:\n{r.stderr[-4000:]}")
+    os.replace(str(out) + ".tmp", out)
+    if verbose:
+        print(f"[mlapi_amd] built {out.relative_to(ROOT)}", file=sys.stderr)
+    return out
+
+
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> Path:
     BUILD.mkdir(parents=True, exist_ok=True)
     hmt = _headers_mtime()
@@ -101,6 +125,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
         os.replace(str(out) + ".tmp", out)
         if verbose:
             print(f"[mlapi_amd] built {out.relative_to(ROOT)}", file=sys.stderr)
+    _build_loadgen(force, verbose)
     return out
 
 

@@ -13,10 +13,12 @@ One process per GPU. On ROCm the ``"nccl"`` backend of torch.distributed IS RCCL
 All messages are <= ~1 MiB, i.e. latency-bound on xGMI: one fused buffer per step, never one
 collective per tensor.
 
-Data plane selection (``MLAPI_COMM``): ``torch`` (default) uses torch.distributed's ``nccl``
-backend (RCCL); ``native`` uses the framework's own C++ RCCL communicator
-(:class:`mlapi_amd.parallel.rccl.NativeComm`, csrc/dist/comm.cpp) with a gloo process group kept
-only as the host control plane; ``fake`` runs the same code paths on CPU through
+Data plane selection (``MLAPI_COMM``): ``auto`` (default) = ``native`` when the rank has a GPU,
+``torch`` otherwise. ``native`` is the framework's own C++ RCCL communicator
+(:class:`mlapi_amd.parallel.rccl.NativeComm`, csrc/dist/comm.cpp: RCCL called directly, on the
+stream PyTorch hands over, with deadline/abort) with a gloo process group kept only as the host
+control plane (rendezvous, unique-id exchange, reload control); ``torch`` uses torch.distributed
+(``nccl`` = RCCL on GPUs, ``gloo`` on CPUs); ``fake`` runs the native code paths on CPU through
 :class:`~mlapi_amd.parallel.rccl.FakeComm` (tests).
 """
 from __future__ import annotations
@@ -50,9 +52,9 @@ class DistInfo:
 def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None,
                      comm: Optional[str] = None) -> DistInfo:
     """Initialise from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); no-op for 1 process."""
-    comm = (comm or os.environ.get("MLAPI_COMM", "torch")).lower()
-    if comm not in ("torch", "native", "fake"):
-        raise ValueError(f"MLAPI_COMM must be torch, native or fake (got {comm!r})")
+    comm = (comm or os.environ.get("MLAPI_COMM", "auto")).lower()
+    if comm not in ("auto", "torch", "native", "fake"):
+        raise ValueError(f"MLAPI_COMM must be auto, torch, native or fake (got {comm!r})")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -62,6 +64,8 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
     if use_gpu:
         device = torch.device("cuda", local_rank % torch.cuda.device_count())
         torch.cuda.set_device(device)
+    if comm == "auto":
+        comm = "native" if device is not None else "torch"
     info = DistInfo(rank, world, local_rank, device, "none")
     if comm == "native" and device is None:
         raise RuntimeError("MLAPI_COMM=native needs a GPU (use fake for CPU runs)")

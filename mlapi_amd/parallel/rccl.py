@@ -10,9 +10,9 @@ channel, plus a ``FakeComm`` with identical semantics for CPU-only multi-rank te
   hanging on a dead peer.
 * :class:`FakeComm` implements the same methods with torch.distributed (gloo) on CPU tensors.
 
-Both speak in torch tensors and are selected with ``MLAPI_COMM=native`` (see
-:func:`mlapi_amd.parallel.comm.init_distributed`); the default data plane stays torch's own
-``nccl`` backend (which is also RCCL).
+Both speak in torch tensors. NativeComm is the default data plane of every GPU rank
+(``MLAPI_COMM=auto``, see :func:`mlapi_amd.parallel.comm.init_distributed`); ``MLAPI_COMM=torch``
+selects torch.distributed's own ``nccl`` backend (also RCCL) instead.
 """
 from __future__ import annotations
 

@@ -59,6 +59,7 @@ def cmd_sgd(args) -> int:
 
     from mlapi_amd.ckpt.native import TrainState, load_native, save_native
     from mlapi_amd.parallel.comm import barrier, init_distributed, shutdown
+    from mlapi_amd.train.schedule import BatchSchedule
     from mlapi_amd.train.sgd import BinarySGDTrainer, synthetic_binary
 
     info = init_distributed()
@@ -66,6 +67,8 @@ def cmd_sgd(args) -> int:
     X, y = synthetic_binary(args.rows_per_rank, args.features, seed=1000 + info.rank, device=dev,
                             dtype=torch.bfloat16 if dev is not None else torch.float32)
     tr = BinarySGDTrainer(args.features, info=info, lr=args.lr, l2=args.l2, momentum=args.momentum, device=dev)
+    nb = max(1, args.rows_per_rank // args.batch)
+    sched = BatchSchedule(nb, seed=args.seed, shuffle=not args.no_shuffle)
     start = 0
     if args.resume and os.path.exists(args.ckpt):
         model, st = load_native(args.ckpt)
@@ -74,20 +77,21 @@ def cmd_sgd(args) -> int:
             tr.mom.copy_(torch.as_tensor(st.opt["mom"], dtype=torch.float32))
         start = st.step
         tr.steps = start
+        sched.restore(st.epoch, st.data_cursor, st.rng_state)
         if info.is_main:
-            print(f"resumed from {args.ckpt} at step {start}", flush=True)
-    nb = max(1, args.rows_per_rank // args.batch)
+            print(f"resumed from {args.ckpt} at step {start} (epoch {st.epoch}, batch {st.data_cursor})", flush=True)
     t0 = time.perf_counter()
     for step in range(start, args.steps):
-        j = step % nb
+        j = sched.next()
         tr.step(X[j * args.batch:(j + 1) * args.batch], y[j * args.batch:(j + 1) * args.batch])
         if info.is_main and (step + 1) % args.log_every == 0:
             print(json.dumps({"step": step + 1, "loss": tr.last_loss(), "acc": tr.last_accuracy()}), flush=True)
         if args.ckpt and (step + 1) % args.ckpt_every == 0:
             barrier(info)
             if info.is_main:
-                st = TrainState(step=step + 1, opt={} if tr.mom is None else {"mom": tr.mom.cpu().numpy()},
-                                config=vars(args))
+                st = TrainState(step=step + 1, epoch=sched.epoch, data_cursor=sched.cursor,
+                                rng_state=sched.rng_state(),
+                                opt={} if tr.mom is None else {"mom": tr.mom.cpu().numpy()}, config=vars(args))
                 save_native(args.ckpt, tr.to_model(), st)
     if dev is not None:
         torch.cuda.synchronize()
@@ -110,6 +114,7 @@ def cmd_sgd_multiclass(args) -> int:
     from mlapi_amd.ckpt.native import TrainState, load_native, save_native
     from mlapi_amd.models.linear import Kind
     from mlapi_amd.parallel.comm import barrier, init_distributed, shutdown
+    from mlapi_amd.train.schedule import BatchSchedule
     from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer, synthetic_multiclass
 
     info = init_distributed()
@@ -121,6 +126,8 @@ def cmd_sgd_multiclass(args) -> int:
                            momentum=args.momentum, device=dev)
     Xa = tr.prepare(X)
     del X
+    nb = max(1, args.rows_per_rank // args.batch)
+    sched = BatchSchedule(nb, seed=args.seed, shuffle=not args.no_shuffle)
     start = 0
     if args.resume and os.path.exists(args.ckpt):
         model, st = load_native(args.ckpt)
@@ -128,22 +135,23 @@ def cmd_sgd_multiclass(args) -> int:
         if tr.mom is not None and "mom" in st.opt:
             tr.mom.copy_(torch.as_tensor(st.opt["mom"], dtype=torch.float32))
         start = tr.steps = st.step
+        sched.restore(st.epoch, st.data_cursor, st.rng_state)
         if info.is_main:
-            print(f"resumed from {args.ckpt} at step {start}", flush=True)
-    nb = max(1, args.rows_per_rank // args.batch)
+            print(f"resumed from {args.ckpt} at step {start} (epoch {st.epoch}, batch {st.data_cursor})", flush=True)
     shards = [(Xa[j * args.batch:(j + 1) * args.batch], y[j * args.batch:(j + 1) * args.batch]) for j in range(nb)]
-    if args.graph and dev is not None and info.world == 1 and nb == 1:
+    if args.graph and dev is not None and info.world == 1 and nb == 1:  # one batch: order is moot
         tr.capture(*shards[0])  # one HIP graph launch per step
     t0 = time.perf_counter()
     for step in range(start, args.steps):
-        tr.step(*shards[step % nb])
+        tr.step(*shards[sched.next()])
         if info.is_main and (step + 1) % args.log_every == 0:
             print(json.dumps({"step": step + 1, "loss": tr.last_loss(), "acc": tr.last_accuracy()}), flush=True)
         if args.ckpt and (step + 1) % args.ckpt_every == 0:
             barrier(info)
             if info.is_main:
-                st = TrainState(step=step + 1, opt={} if tr.mom is None else {"mom": tr.mom.cpu().numpy()},
-                                config=vars(args))
+                st = TrainState(step=step + 1, epoch=sched.epoch, data_cursor=sched.cursor,
+                                rng_state=sched.rng_state(),
+                                opt={} if tr.mom is None else {"mom": tr.mom.cpu().numpy()}, config=vars(args))
                 save_native(args.ckpt, tr.to_model(), st)
     if dev is not None:
         torch.cuda.synchronize()
@@ -191,6 +199,8 @@ def main(argv=None) -> int:
     p.add_argument("--kind", default="multinomial", choices=["multinomial", "ovr"])
     p.add_argument("--noise", type=float, default=1.0, help="multiclass synthetic label noise")
     p.add_argument("--graph", action="store_true", help="capture the single-GPU step in a HIP graph")
+    p.add_argument("--seed", type=int, default=0, help="mini-batch order (epoch shuffles; same on every rank)")
+    p.add_argument("--no-shuffle", action="store_true", help="visit the batches in order every epoch")
     args = ap.parse_args(argv)
     if args.cmd == "iris":
         X, y = iris_dataset()

@@ -31,10 +31,12 @@ setup(
     version="0.1.0",
     description=("MI355X-native ML-inference microservice: FastAPI-compatible /predict over sklearn "
                  "LogisticRegression checkpoints, batched gfx950 HIP kernels, RCCL data parallelism"),
+    license="MIT",
+    license_files=["LICENSE"],
     python_requires=">=3.10",
     packages=find_packages(include=["mlapi_amd", "mlapi_amd.*"]),
     py_modules=["main"],
-    package_data={"mlapi_amd": ["_C*.so"]},
+    package_data={"mlapi_amd": ["_C*.so", "bin/mlapi-loadgen"]},
     # torch must be a ROCm build (the extension binds to the HIP runtime torch loads);
     # python-multipart is not needed (mlapi_amd.api.multipart replaces it).
     install_requires=["torch>=2.4", "numpy>=1.20", "fastapi>=0.63", "pydantic>=1.7", "uvicorn>=0.13",

@@ -3,6 +3,7 @@
 Multi-rank RCCL runs need one GPU per rank (RCCL rejects two ranks on one device); the same
 collective code paths are covered at world_size 2 on CPU through FakeComm
 (tests/test_distributed.py::test_fake_comm_collectives)."""
+import json
 import os
 import subprocess
 import sys
@@ -43,8 +44,13 @@ def test_native_comm_uses_torch_rccl_and_aborts():
         c.all_reduce_(t)
 
 
-def test_bench_train_over_native_comm():
-    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--mode", "train", "--steps", "20", "--warmup", "2"],
-                         env={**ENV, "MLAPI_COMM": "native"}, capture_output=True, text=True, timeout=300, cwd=ROOT)
+@pytest.mark.parametrize("mode", ["train", "serve"])
+def test_bench_defaults_to_native_comm(mode):
+    """MLAPI_COMM unset on a GPU rank -> the framework's C++ RCCL communicator is the data plane."""
+    env = {k: v for k, v in ENV.items() if k != "MLAPI_COMM"}
+    args = ["--steps", "5", "--warmup", "1"] + (["--reqs-per-conn", "64"] if mode == "serve" else [])
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--mode", mode, *args], env=env,
+                         capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
-    assert '"train_samples_per_sec"' in out.stdout.strip().splitlines()[-1]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["comm_backend"] == "native-rccl"

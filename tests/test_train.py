@@ -197,3 +197,30 @@ def test_cli_sgd_multiclass_checkpoint_resume(tmp_path):
     assert final_resumed["final_loss"] == pytest.approx(final_full["final_loss"], rel=1e-6)
     sk = pickle.loads((tmp_path / "m.pkl").read_bytes())  # our own export, readable by sklearn
     assert sk.coef_.shape == (5, 32)
+
+
+def test_batch_schedule_resume_visits_the_same_batches():
+    from mlapi_amd.train.schedule import BatchSchedule
+
+    full = BatchSchedule(7, seed=3)
+    seq = [full.next() for _ in range(30)]
+    assert sorted(seq[:7]) == list(range(7)) and seq[:7] != list(range(7))  # a permutation per epoch
+    a = BatchSchedule(7, seed=3)
+    head = [a.next() for _ in range(17)]
+    b = BatchSchedule(7, seed=99)  # a fresh process with the checkpointed state
+    b.restore(a.epoch, a.cursor, a.rng_state())
+    assert head + [b.next() for _ in range(13)] == seq
+
+
+def test_cli_sgd_checkpoint_holds_rng_and_cursor(tmp_path):
+    from mlapi_amd.ckpt.native import load_native
+
+    ck = str(tmp_path / "s.safetensors")
+    env = {**ENV, "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""}
+    out = subprocess.run([sys.executable, "-m", "mlapi_amd.train", "sgd", "--features", "8", "--rows-per-rank", "3000",
+                          "--batch", "1000", "--steps", "7", "--ckpt", ck, "--ckpt-every", "7", "--log-every", "100"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    _, st = load_native(ck)
+    assert (st.step, st.epoch, st.data_cursor) == (7, 2, 1)  # 3 batches per epoch
+    assert st.rng_state is not None and st.rng_state.dtype == np.uint8 and st.rng_state.size > 0

@@ -1,42 +1,64 @@
 #!/bin/bash
-# One GPU session: tests, smoke, benches, profiles. Stops at the first GPU fault / timeout.
-# Usage (on the GPU box): bash tools/gpu_session.sh [steps...]   steps: test smoke serve kbench prof
+# One GPU session on the MI355X box: tests, smoke, benches, A/B runs and rocprofv3 profiles.
+# Every GPU step has its own time limit; the session stops at the first failing step
+# (fault / abort / timeout), so nothing runs on a GPU in a bad state.
+#
+#   bash tools/gpu_session.sh [OUT=dir] step...       (default steps: test smoke serve kbench prof)
+#
+# steps:
+#   test          pytest -m gpu (whole GPU tier)          smoke      __graft_entry__.smoke()
+#   serve         headline bench (Iris /predict)           serve_wide F=256 /predict, K=1000 and K=2
+#   serve_ab      serve with kernel-argument batches on/off, interleaved x2 (box variance is large)
+#   kbench        gemv / gemm / train / train_softmax benches
+#   prof          rocprofv3 --kernel-trace --stats of every bench mode (incl. serve and serve_wide)
+#   pmc_gemm      hardware counters of the gemm bench (tools/pmc_profile.sh)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-ok_or_stop() {  # $1 = rc, $2 = allow test failures (1)
-  local rc=$1
-  if [ "$rc" -eq 0 ]; then return 0; fi
-  if [ "${2:-0}" = "1" ] && [ "$rc" -eq 1 ]; then return 0; fi
-  echo "STOP: step failed with rc=$rc"; exit "$rc"
+O=gpurun_out
+if [[ "${1:-}" == OUT=* ]]; then O="${1#OUT=}"; shift; fi
+mkdir -p "$O"
+O=$(cd "$O" && pwd)
+stop() { echo "STOP: $1 failed with rc=$2"; tail -20 "$3"; exit "$2"; }
+run() {  # run <name> <limit_s> <cmd...>: output to $O/<name>.log
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  [ $rc -eq 0 ] || stop "$name" $rc "$O/$name.log"
+  tail -2 "$O/$name.log" | cut -c1-600
+}
+prof() {  # prof <name> <limit_s> <bench args...>
+  local name=$1 lim=$2; shift 2
+  (cd /tmp && timeout -k 10 "$lim" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$name" -o "$name" \
+     -- python3 "$R/bench.py" "$@" > "$O/prof_$name.log" 2>&1)
+  local rc=$?
+  [ $rc -eq 0 ] || stop "prof_$name" $rc "$O/prof_$name.log"
+  tail -1 "$O/prof_$name.log" | cut -c1-300
 }
 steps="${*:-test smoke serve kbench prof}"
 for s in $steps; do
   case $s in
-    test)
-      timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
-      rc=$?; tail -40 gpurun_out/pytest_gpu.log; ok_or_stop $rc 1 ;;
-    smoke)
-      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-      rc=$?; tail -5 gpurun_out/smoke.log; ok_or_stop $rc ;;
-    serve)
-      timeout -k 10 300 python bench.py --steps 200 --warmup 20 > gpurun_out/bench_serve.log 2>&1
-      rc=$?; tail -3 gpurun_out/bench_serve.log; ok_or_stop $rc ;;
-    kbench)
-      for m in gemv gemm train train_softmax; do
-        timeout -k 10 300 python bench.py --mode $m --steps 100 --warmup 10 > gpurun_out/bench_$m.log 2>&1
-        rc=$?; tail -2 gpurun_out/bench_$m.log; ok_or_stop $rc
+    test) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    serve) run bench_serve 300 python -u bench.py --steps 200 --warmup 20 ;;
+    serve_wide)
+      run bench_serve_wide_k1000 300 python -u bench.py --mode serve_wide --wide-classes 1000 --steps 40 --warmup 5
+      run bench_serve_wide_k2 300 python -u bench.py --mode serve_wide --wide-classes 2 --steps 40 --warmup 5 ;;
+    serve_ab)
+      for r in 1 2; do
+        for m in 1 0; do
+          MLAPI_INLINE_ARGS=$m run "serve_inline${m}_r$r" 300 python -u bench.py --steps 100 --warmup 10
+        done
       done ;;
+    kbench)
+      for m in gemv gemm train train_softmax; do run "bench_$m" 300 python -u bench.py --mode $m --steps 100 --warmup 10; done ;;
     prof)
-      for m in gemv gemm train train_softmax; do
-        timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$m -o $m -- \
-          python3 bench.py --mode $m --steps 20 --warmup 2 > gpurun_out/prof_$m.log 2>&1
-        rc=$?; tail -2 gpurun_out/prof_$m.log; ok_or_stop $rc
-      done
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_serve -o serve -- \
-        python3 bench.py --steps 50 --warmup 5 > gpurun_out/prof_serve.log 2>&1
-      rc=$?; tail -2 gpurun_out/prof_serve.log; ok_or_stop $rc ;;
+      for m in gemv gemm train train_softmax; do prof "$m" 300 --mode $m --steps 20 --warmup 2; done
+      prof serve 300 --steps 20 --warmup 2 --reqs-per-conn 512
+      prof serve_wide 300 --mode serve_wide --steps 10 --warmup 2 --reqs-per-conn 256 ;;
+    pmc_gemm) PMC_BENCHES="gemm:--mode gemm --steps 5 --warmup 1|gemm_big:--mode gemm --batch 262144 --steps 5 --warmup 1" run pmc_gemm 600 bash tools/pmc_profile.sh ;;
+    *) echo "unknown step $s"; exit 2 ;;
   esac
 done
 echo "SESSION DONE"
