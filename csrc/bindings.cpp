@@ -299,6 +299,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("spin_us", &EngineConfig::spin_us)
       .def_readwrite("wide_dtype", &EngineConfig::wide_dtype)
       .def_readwrite("inline_args", &EngineConfig::inline_args)
+      .def_readwrite("stage_wide", &EngineConfig::stage_wide)
       .def_readwrite("max_queue", &EngineConfig::max_queue);
 
   py::class_<PySink>(m, "PySink").def(py::init<>()).def("fd", &PySink::fd).def("drain", &PySink::drain);

@@ -8,11 +8,26 @@
 
 namespace mlapi {
 
+// Serving completion signal: instead of an event per batch (hipEventRecord + polling costs
+// ~12 us launch-to-observed on MI355X, tools/launch_probe.hip), the serving kernel itself
+// publishes `seq` into a host-coherent word once every block's results are out (system-scope
+// release; multi-block launches elect the last block through `counter`, a device word that is
+// zero between launches). The engine's completer spins on the word (~7 us). done == nullptr:
+// no signal (library / test callers).
+struct ServeSignal {
+  uint32_t* done = nullptr;     // host-coherent, device-mapped
+  uint32_t seq = 0;
+  uint32_t* counter = nullptr;  // device memory, zero-initialised (multi-block kernels)
+};
+// Standalone signal (one wave) for kernels without a built-in one; stream order puts it after them.
+void launch_serve_signal(const ServeSignal& sig, hipStream_t stream);
+
 // ---- linear_small.hip: fused  z = x W^T + b  -> (argmax label, p_max)  for small F, K ----------
 // X: [B, F] (ld = ldx elements) in dtype `dt` (F64 or F32); W: [K, F]; b: [K] (same dtype).
 // out_idx: int32[B]; out_p: dtype[B]. K = rows of W (1 for binary kinds).
 void launch_linear_small(int dt, const void* X, int64_t ldx, const void* W, const void* b, int64_t B, int F,
-                         int K, int kind, int32_t* out_idx, void* out_p, hipStream_t stream);
+                         int K, int kind, int32_t* out_idx, void* out_p, hipStream_t stream,
+                         const ServeSignal& sig = ServeSignal());
 
 // Kernel-argument batch (linear_small.hip): a tiny serving batch travels INSIDE the kernel's
 // argument block (rows + W + b), so the kernel reads nothing over the host link: the runtime
@@ -24,6 +39,8 @@ struct InlineBatch {
   int32_t n, F, K, kind;
   int32_t* out_idx;
   void* out_p;
+  uint32_t* done;  // ServeSignal of the batch (one block: no counter)
+  uint32_t seq;
   alignas(16) unsigned char wb[INLINE_WB_BYTES];  // W [K][F] then b [K] (dtype of the launch)
   alignas(16) unsigned char x[INLINE_X_BYTES];    // rows [n][F]
 };

@@ -101,14 +101,35 @@ __device__ __forceinline__ void row_predict(const T* __restrict__ xr, const T* _
 }
 
 
+// End of a serving launch: every wave makes its stores visible at system scope, the block meets,
+// and the last block to arrive (one block: itself) publishes the batch's sequence number.
+__device__ __forceinline__ void serve_signal(uint32_t* done, uint32_t seq, uint32_t* counter) {
+  if (done == nullptr) return;  // uniform
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bool last = true;
+    if (gridDim.x > 1) {
+      last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) == gridDim.x - 1;
+      if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    if (last) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ __launch_bounds__(64) void serve_signal_kernel(uint32_t* done, uint32_t seq) {
+  serve_signal(done, seq, nullptr);
+}
+
 template <typename T, int FMAX, int KMAX>
 __global__ __launch_bounds__(256) void linear_small_kernel(const T* __restrict__ X, int64_t ldx,
                                                            const T* __restrict__ W, const T* __restrict__ b,
                                                            int64_t B, int F, int K, int kind,
-                                                           int32_t* __restrict__ out_idx, T* __restrict__ out_p) {
+                                                           int32_t* __restrict__ out_idx, T* __restrict__ out_p,
+                                                           ServeSignal sig) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= B) return;
-  row_predict<T, FMAX, KMAX>(X + r * ldx, W, b, F, K, kind, out_idx[r], out_p[r]);
+  if (r < B) row_predict<T, FMAX, KMAX>(X + r * ldx, W, b, F, K, kind, out_idx[r], out_p[r]);
+  serve_signal(sig.done, sig.seq, sig.counter);
 }
 
 // Generic fallback for wider models (F > 32 or K > 16): one pass, online (max, sum-exp).
@@ -150,10 +171,11 @@ template <typename T>
 __global__ __launch_bounds__(256) void linear_generic_kernel(const T* __restrict__ X, int64_t ldx,
                                                              const T* __restrict__ W, const T* __restrict__ b,
                                                              int64_t B, int F, int K, int kind,
-                                                             int32_t* __restrict__ out_idx, T* __restrict__ out_p) {
+                                                             int32_t* __restrict__ out_idx, T* __restrict__ out_p,
+                                                             ServeSignal sig) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= B) return;
-  row_predict_generic<T>(X + r * ldx, W, b, F, K, kind, out_idx[r], out_p[r]);
+  if (r < B) row_predict_generic<T>(X + r * ldx, W, b, F, K, kind, out_idx[r], out_p[r]);
+  serve_signal(sig.done, sig.seq, sig.counter);
 }
 
 // ---- kernel-argument batch -------------------------------------------------------------------
@@ -169,14 +191,16 @@ __global__ __launch_bounds__(128) void linear_inline_kernel(const InlineBatch ar
   const InlineBatch* a = (const InlineBatch*)__builtin_amdgcn_kernarg_segment_ptr();
   const int r = threadIdx.x;
   const int n = a->n, F = a->F, K = a->K, kind = a->kind;
-  if (r >= n) return;
-  const T* W = reinterpret_cast<const T*>(a->wb);
-  const T* b = W + K * F;
-  int32_t idx;
-  T p;
-  row_predict<T, FMAX, KMAX>(reinterpret_cast<const T*>(a->x) + r * F, W, b, F, K, kind, idx, p);
-  a->out_idx[r] = idx;
-  static_cast<T*>(a->out_p)[r] = p;
+  if (r < n) {
+    const T* W = reinterpret_cast<const T*>(a->wb);
+    const T* b = W + K * F;
+    int32_t idx;
+    T p;
+    row_predict<T, FMAX, KMAX>(reinterpret_cast<const T*>(a->x) + r * F, W, b, F, K, kind, idx, p);
+    a->out_idx[r] = idx;
+    static_cast<T*>(a->out_p)[r] = p;
+  }
+  serve_signal(a->done, a->seq, nullptr);
 }
 
 template <typename T>
@@ -191,7 +215,7 @@ void dispatch_inline(const InlineBatch& a, hipStream_t stream) {
 
 template <typename T>
 void dispatch(const void* X, int64_t ldx, const void* W, const void* b, int64_t B, int F, int K, int kind,
-              int32_t* out_idx, void* out_p, hipStream_t stream) {
+              int32_t* out_idx, void* out_p, hipStream_t stream, const ServeSignal& sig) {
   if (B <= 0) return;
   const int threads = B <= 64 ? 64 : 256;  // tiny serving batches: one wave, no idle waves
   const dim3 grid((unsigned)((B + threads - 1) / threads));
@@ -201,13 +225,13 @@ void dispatch(const void* X, int64_t ldx, const void* W, const void* b, int64_t 
   auto p = static_cast<T*>(out_p);
   if (F <= 8 && K <= 4)
     hipLaunchKernelGGL((linear_small_kernel<T, 8, 4>), grid, dim3(threads), 0, stream, x, ldx, w, bb, B, F, K, kind,
-                       out_idx, p);
+                       out_idx, p, sig);
   else if (F <= 32 && K <= 16)
     hipLaunchKernelGGL((linear_small_kernel<T, 32, 16>), grid, dim3(threads), 0, stream, x, ldx, w, bb, B, F, K,
-                       kind, out_idx, p);
+                       kind, out_idx, p, sig);
   else
     hipLaunchKernelGGL((linear_generic_kernel<T>), grid, dim3(threads), 0, stream, x, ldx, w, bb, B, F, K, kind,
-                       out_idx, p);
+                       out_idx, p, sig);
   MLAPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -228,12 +252,20 @@ void launch_linear_inline(int dt, const InlineBatch& a, hipStream_t stream) {
     dispatch_inline<float>(a, stream);
 }
 
+void launch_serve_signal(const ServeSignal& sig, hipStream_t stream) {
+  if (sig.done == nullptr) return;
+  hipLaunchKernelGGL(serve_signal_kernel, dim3(1), dim3(64), 0, stream, sig.done, sig.seq);
+  MLAPI_HIP_CHECK(hipGetLastError());
+}
+
 void launch_linear_small(int dt, const void* X, int64_t ldx, const void* W, const void* b, int64_t B, int F, int K,
-                         int kind, int32_t* out_idx, void* out_p, hipStream_t stream) {
+                         int kind, int32_t* out_idx, void* out_p, hipStream_t stream, const ServeSignal& sig) {
+  if (sig.done != nullptr && B > 256 && sig.counter == nullptr)
+    throw std::invalid_argument("linear_small: a multi-block signalled launch needs a counter");
   if (dt == DT_F64)
-    dispatch<double>(X, ldx, W, b, B, F, K, kind, out_idx, out_p, stream);
+    dispatch<double>(X, ldx, W, b, B, F, K, kind, out_idx, out_p, stream, sig);
   else if (dt == DT_F32)
-    dispatch<float>(X, ldx, W, b, B, F, K, kind, out_idx, out_p, stream);
+    dispatch<float>(X, ldx, W, b, B, F, K, kind, out_idx, out_p, stream, sig);
   else
     throw std::invalid_argument("linear_small: dtype must be f64 or f32");
 }

@@ -112,6 +112,13 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     slots_.resize(cfg_.slots);
     slot_row_bytes_ = padded_features(cfg_.max_features) * sizeof(double);
     const size_t xb = (size_t)cfg_.max_batch * slot_row_bytes_;
+    const size_t done_bytes = sizeof(uint32_t) * SIGNAL_STRIDE * cfg_.slots;
+    MLAPI_HIP_CHECK(hipHostMalloc((void**)&done_h_, done_bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(done_h_, 0, done_bytes);
+    MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&done_d_, done_h_, 0));
+    MLAPI_HIP_CHECK(hipMalloc((void**)&sig_counter_, sizeof(uint32_t)));
+    MLAPI_HIP_CHECK(hipMemset(sig_counter_, 0, sizeof(uint32_t)));
+    MLAPI_HIP_CHECK(hipDeviceSynchronize());
     for (int i = 0; i < cfg_.slots; ++i) {
       Slot& s = slots_[i];
       MLAPI_HIP_CHECK(hipHostMalloc(&s.hx, xb, hipHostMallocMapped));
@@ -121,7 +128,6 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.didx, s.hidx, 0));
       MLAPI_HIP_CHECK(hipHostMalloc(&s.hp, (size_t)cfg_.max_batch * sizeof(double), hipHostMallocMapped));
       MLAPI_HIP_CHECK(hipHostGetDevicePointer(&s.dp, s.hp, 0));
-      MLAPI_HIP_CHECK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
       s.metas.reserve(cfg_.max_batch);
       free_slots_.push_back(i);
     }
@@ -135,8 +141,9 @@ Engine::~Engine() {
   if (cfg_.device >= 0) {
     (void)hipSetDevice(cfg_.device);
     if (stream_) (void)hipStreamSynchronize(stream_);
+    if (done_h_) (void)hipHostFree(done_h_);
+    if (sig_counter_) (void)hipFree(sig_counter_);
     for (Slot& s : slots_) {
-      if (s.ev) (void)hipEventDestroy(s.ev);
       if (s.hx) (void)hipHostFree(s.hx);
       if (s.dstage) (void)hipFree(s.dstage);
       if (s.hidx) (void)hipHostFree(s.hidx);
@@ -439,6 +446,11 @@ void Engine::pack_rows(Slot& s, const std::vector<double>& xs, const Model& m) {
 // One launch for the whole batch on the model's kernel path (engine.h).
 void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs) {
   const int64_t n = s.n;
+  const int si = (int)(&s - slots_.data());
+  ServeSignal sig;
+  sig.done = done_d_ + (size_t)si * SIGNAL_STRIDE;
+  sig.seq = ++s.seq;
+  sig.counter = sig_counter_;
   if (m.path == PATH_SMALL && cfg_.inline_args && linear_inline_fits(m.xdt, n, m.F, m.K)) {
     // rows, W and b ride in the kernel-argument block
     InlineBatch& a = inline_;
@@ -448,6 +460,8 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     a.kind = m.kind;
     a.out_idx = s.didx;
     a.out_p = s.dp;
+    a.done = sig.done;
+    a.seq = sig.seq;
     const size_t es = dtype_size(m.xdt);
     const size_t kf = (size_t)m.K * m.F;
     if (m.xdt == DT_F64) {
@@ -479,17 +493,22 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
   }
   pack_rows(s, xs, m);
   const size_t bytes = (size_t)n * m.ldx * dtype_size(m.xdt);
-  if (m.path == PATH_SMALL) {  // zero-copy: the kernel reads the pinned rows over the host link
-    launch_linear_small(m.xdt, s.dx, m.ldx, m.dW, m.db, n, m.F, m.K, m.kind, s.didx, s.dp, stream_);
-  } else {
+  // rows: zero-copy from the pinned slot (one host-link round trip inside the kernel), or staged
+  // by a copy first (a blit kernel of its own: ~4 us at serving sizes)
+  const void* X = s.dx;
+  if (m.path != PATH_SMALL && cfg_.stage_wide) {
     MLAPI_HIP_CHECK(hipMemcpyAsync(s.dstage, s.hx, bytes, hipMemcpyHostToDevice, stream_));
+    X = s.dstage;
+  }
+  if (m.path == PATH_SMALL || m.path == PATH_GENERIC) {
+    launch_linear_small(m.xdt, X, m.ldx, m.dW, m.db, n, m.F, m.K, m.kind, s.didx, s.dp, stream_, sig);
+  } else {
     if (m.path == PATH_GEMV)
-      launch_gemv_binary(m.xdt, s.dstage, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_);
-    else if (m.path == PATH_GEMM)
-      launch_gemm_softmax(s.dstage, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
-                          static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_);
+      launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_);
     else
-      launch_linear_small(m.xdt, s.dstage, m.ldx, m.dW, m.db, n, m.F, m.K, m.kind, s.didx, s.dp, stream_);
+      launch_gemm_softmax(X, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
+                          static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_);
+    launch_serve_signal(sig, stream_);
   }
   std::lock_guard<std::mutex> lk(st_mu_);
   stats_.path_batches[m.path]++;
@@ -559,7 +578,6 @@ void Engine::batcher_loop() {
       } else {
         try {
           launch_batch(s, *m, xs);
-          MLAPI_HIP_CHECK(hipEventRecord(s.ev, stream_));
           s.launched = true;
         } catch (const std::exception&) {
           s.failed = true;
@@ -599,22 +617,32 @@ void Engine::completer_loop() {
     }
     Slot& s = slots_[si];
     if (s.launched) {
-      // Poll the event: spin briefly (sub-10us kernels), then back off.
+      // Spin on the slot's done word (the kernel publishes s.seq with a system-scope release);
+      // back off after ~50 us, check the stream for a fault now and then, and give up on the
+      // batch (ST_DEVICE_ERROR) after 10x the watchdog.
+      volatile uint32_t* dw = done_h_ + (size_t)si * SIGNAL_STRIDE;
       const int64_t t0 = now_ns();
-      int spins = 0;
-      for (;;) {
-        const hipError_t e = hipEventQuery(s.ev);
-        if (e == hipSuccess) break;
-        if (e != hipErrorNotReady) {
-          s.failed = true;
-          healthy_.store(false);
-          break;
-        }
-        if (++spins < 2000) {
+      uint32_t spins = 0;
+      while (__atomic_load_n(dw, __ATOMIC_ACQUIRE) != s.seq) {
+        ++spins;
+        if (spins < 20000) {
           _mm_pause();
-        } else {
-          std::this_thread::sleep_for(std::chrono::microseconds(20));
-          if (cfg_.watchdog_ms > 0 && now_ns() - t0 > (int64_t)cfg_.watchdog_ms * 1000000) healthy_.store(false);
+          continue;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(spins < 40000 ? 2 : 50));
+        if ((spins & 63) == 0) {
+          const hipError_t q = hipStreamQuery(stream_);
+          if (q != hipSuccess && q != hipErrorNotReady) {
+            s.failed = true;
+            healthy_.store(false);
+            break;
+          }
+          const int64_t waited = now_ns() - t0;
+          if (cfg_.watchdog_ms > 0 && waited > (int64_t)cfg_.watchdog_ms * 1000000) healthy_.store(false);
+          if (cfg_.watchdog_ms > 0 && waited > (int64_t)cfg_.watchdog_ms * 10000000) {
+            s.failed = true;
+            break;
+          }
         }
       }
     }

@@ -11,16 +11,20 @@
 //                  fp32. Batches that fit 3 KB travel inside the kernel-argument block
 //                  (launch_linear_inline: no host-link read at all); larger ones are read
 //                  zero-copy from the pinned slot;
-//          GEMV    (binary, wide F): rows packed as bf16 (or fp32), one hipMemcpyAsync H2D into
-//                  the slot's device buffer, then the HBM-streaming gemv_binary kernel;
+//          GEMV    (binary, wide F): rows packed as bf16 (or fp32) into the pinned slot, read
+//                  zero-copy by the gemv_binary kernel (stage_wide: one hipMemcpyAsync H2D
+//                  into a device buffer first);
 //          GEMM    (multiclass, wide F / many classes): bf16 rows (F zero-padded to the MFMA
-//                  width) H2D, then the MFMA gemm_softmax kernel with its online softmax/argmax
-//                  epilogue (workspace per model, zeroed once);
-//          GENERIC (wide models served in fp32/fp64): H2D + one-row-per-lane scalar kernel;
-//        the (idx, p) results are written by the kernel straight into host-mapped memory;
+//                  width), the MFMA gemm_softmax kernel with its online softmax/argmax epilogue
+//                  (workspace per model, zeroed once);
+//          GENERIC (wide models served in fp32/fp64): one-row-per-lane scalar kernel;
+//        the (idx, p) results are written by the kernel straight into host-mapped memory, and
+//        the kernel (or, on the GEMV / GEMM paths, a one-wave signal kernel behind it) publishes
+//        the batch's sequence number into the slot's host-coherent done word (ServeSignal);
 //        up to `slots` batches are in flight;
-//     -> completer thread: polls the oldest slot's event, groups results by Sink and hands them
-//        over (HTTP IO threads, Python futures, blocking callers).
+//     -> completer thread: spins on the oldest slot's done word (no HIP event: launch-to-
+//        observed drops from ~12 to ~7 us, tools/launch_probe.hip), groups results by Sink and
+//        hands them over (HTTP IO threads, Python futures, blocking callers).
 //
 // The CPU backend (device = -1) runs the same math in C++ float64 (a "FakeDevice" for tests and
 // GPU-less hosts). Models are immutable and swapped atomically (hot reload): an in-flight batch
@@ -100,6 +104,7 @@ struct EngineConfig {
                              // GEMM kernels; f32 -> GEMV (binary) / GENERIC; f64 -> GENERIC
   int max_features = 256; // per-request feature cap (sizes the slot buffers)
   bool inline_args = true;  // SMALL path: batches that fit travel in the kernel-argument block
+  bool stage_wide = false;  // GEMV / GEMM / GENERIC: H2D-copy the rows first (default: zero-copy reads)
   int watchdog_ms = 2000; // batch not complete after this -> engine marked unhealthy
   int fail_every = 0;     // fault injection: fail every N-th batch with ST_DEVICE_ERROR
   int delay_us = 0;       // fault injection: extra per-batch delay
@@ -176,7 +181,7 @@ class Engine {
     int32_t* didx = nullptr;
     void* hp = nullptr;
     void* dp = nullptr;
-    hipEvent_t ev = nullptr;
+    uint32_t seq = 0;         // sequence number the launch publishes into the done word
     std::vector<Meta> metas;
     std::vector<int32_t> pre_status;  // per-row status decided before launch
     std::shared_ptr<const Model> model;
@@ -220,6 +225,10 @@ class Engine {
   bool batcher_done_ = false;
 
   size_t slot_row_bytes_ = 0;  // capacity of one packed row in a slot (any path)
+  uint32_t* done_h_ = nullptr;  // per-slot done words (host-coherent, SIGNAL_STRIDE apart)
+  uint32_t* done_d_ = nullptr;
+  uint32_t* sig_counter_ = nullptr;  // device word for multi-block signalled launches
+  static constexpr int SIGNAL_STRIDE = 16;  // 64 bytes: one cache line per slot
   InlineBatch inline_{};        // batcher thread only
 
   std::thread batcher_, completer_;

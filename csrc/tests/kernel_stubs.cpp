@@ -9,9 +9,10 @@ namespace mlapi {
   throw std::logic_error(std::string("host-only test binary: ") + what + " must not be reached");
 }
 void launch_linear_small(int, const void*, int64_t, const void*, const void*, int64_t, int, int, int, int32_t*, void*,
-                         hipStream_t) {
+                         hipStream_t, const ServeSignal&) {
   unreachable("launch_linear_small");
 }
+void launch_serve_signal(const ServeSignal&, hipStream_t) { unreachable("launch_serve_signal"); }
 bool linear_inline_fits(int, int64_t, int, int) { return false; }
 void launch_linear_inline(int, const InlineBatch&, hipStream_t) { unreachable("launch_linear_inline"); }
 void launch_gemv_binary(int, const void*, const void*, float, int64_t, int, int, int32_t*, float*, hipStream_t) {

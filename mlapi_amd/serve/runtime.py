@@ -59,6 +59,7 @@ class EngineHandle:
         ec.delay_us = config.delay_us
         ec.spin_us = config.spin_us
         ec.inline_args = bool(config.inline_args)
+        ec.stage_wide = bool(config.stage_wide)
         ec.max_queue = config.max_queue
         self.engine = c.Engine(ec)
         self._models: Dict[int, LinearModel] = {}

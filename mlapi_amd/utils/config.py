@@ -41,6 +41,7 @@ class Config:
     spin_us: int = 0                          # batcher spin before sleeping (0 = always sleep)
     max_queue: int = 1 << 20                  # backpressure: queued rows beyond this -> HTTP 503
     inline_args: bool = True                  # GPU: tiny batches travel in the kernel-argument block
+    stage_wide: bool = False                  # GPU: copy wide models' rows H2D first (default: zero-copy reads)
     fault_drop_rank: int = -1                 # fault injection: this DP rank's engine fails every batch
     pin: str = "auto"                         # CPU pinning per rank: auto (DP without launcher) | on | off
     # HTTP

@@ -91,7 +91,7 @@ def test_native_server_gpu_end_to_end(iris_cwd, native):
 
 # ---- small-model launch modes: kernel-argument batches vs zero-copy pinned rows ------------------
 @pytest.mark.parametrize("inline", [True, False])
-@pytest.mark.parametrize("max_batch", [16, 256])
+@pytest.mark.parametrize("max_batch", [16, 256, 1024])
 def test_engine_small_inline_and_zero_copy(native, inline, max_batch):
     m = LinearModel.random(4, 3, seed=7)
     e = _engine(native, max_batch=max_batch, inline_args=inline)

@@ -56,6 +56,7 @@ def _engine(native, **kw):
     return native.Engine(cfg)
 
 
+@pytest.mark.parametrize("stage", [False, True])
 @pytest.mark.parametrize("F,K,kind,wide,path", [
     (256, 2, Kind.BINARY, "bf16", "gemv"),
     (256, 2, Kind.BINARY_SOFTMAX, "bf16", "gemv"),
@@ -68,9 +69,9 @@ def _engine(native, **kw):
     (48, 40, Kind.MULTINOMIAL, "f32", "generic"),
     (48, 40, Kind.OVR, "f64", "generic"),
 ])
-def test_engine_wide_paths_match_oracle(native, F, K, kind, wide, path):
+def test_engine_wide_paths_match_oracle(native, F, K, kind, wide, path, stage):
     m = LinearModel.random(F, K, seed=F + K, kind=kind)
-    e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide])
+    e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide], stage_wide=stage)
     try:
         e.load_model(int(m.kind), m.W, m.b, m.label_json())
         assert e.model_path() == path

@@ -1,0 +1,136 @@
+// Launch / completion latency probe for the batch=1 serving leg.
+//
+// Measures, host-side, launch-call -> completion-observed for a one-wave kernel in several
+// variants (what the engine's completer sees), and lets rocprofv3 report the kernels' own
+// durations:
+//   empty      : no memory traffic
+//   dev_write  : 64 lanes write int+double to device memory
+//   host_write : same, to host-mapped pinned memory (the engine's (idx, p) outputs)
+//   host_read  : 64 lanes read 32 B each from host-mapped memory (zero-copy rows)
+//   kernarg    : 64 lanes read 32 B each from a 3.5 KB by-value argument (inline batches)
+//   flag       : host_write + a system-scope release of a done word the host spins on
+// Completion is observed either by hipEventQuery polling or (flag) by spinning on the word.
+//
+//   hipcc -O3 --offload-arch=gfx950 tools/launch_probe.hip -o build/launch_probe && build/launch_probe
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#define CHECK(x)                                                                  \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) {                                                       \
+      std::fprintf(stderr, "%s failed: %s\n", #x, hipGetErrorString(e_));        \
+      std::exit(1);                                                               \
+    }                                                                             \
+  } while (0)
+
+struct Big {
+  int n;
+  int pad[3];
+  unsigned char x[3520];
+};
+
+__global__ void k_empty(int* out) {
+  if (threadIdx.x == 1000) out[0] = 1;
+}
+__global__ void k_write(int* idx, double* p) {
+  idx[threadIdx.x] = threadIdx.x;
+  p[threadIdx.x] = 0.5 * threadIdx.x;
+}
+__global__ void k_read(const double* x, int* idx, double* p) {
+  const double* r = x + threadIdx.x * 4;
+  const double s = r[0] + r[1] + r[2] + r[3];
+  idx[threadIdx.x] = s > 0;
+  p[threadIdx.x] = s;
+}
+__global__ void k_kernarg(const Big a, int* idx, double* p) {
+  (void)a;
+  const Big* b = (const Big*)__builtin_amdgcn_kernarg_segment_ptr();
+  const double* r = reinterpret_cast<const double*>(b->x) + threadIdx.x * 4;
+  const double s = r[0] + r[1] + r[2] + r[3];
+  idx[threadIdx.x] = s > 0;
+  p[threadIdx.x] = s;
+}
+__global__ void k_flag(int* idx, double* p, unsigned* done, unsigned seq) {
+  idx[threadIdx.x] = threadIdx.x;
+  p[threadIdx.x] = 0.5 * threadIdx.x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
+  CHECK(hipSetDevice(0));
+  int lo, hi;
+  CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  hipStream_t s;
+  CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
+  hipEvent_t ev;
+  CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  int *d_idx, *h_idx, *hd_idx;
+  double *d_p, *h_p, *hd_p, *h_x, *hd_x;
+  unsigned *h_done, *hd_done;
+  CHECK(hipMalloc(&d_idx, 256));
+  CHECK(hipMalloc(&d_p, 512));
+  CHECK(hipHostMalloc((void**)&h_idx, 256, hipHostMallocMapped));
+  CHECK(hipHostGetDevicePointer((void**)&hd_idx, h_idx, 0));
+  CHECK(hipHostMalloc((void**)&h_p, 512, hipHostMallocMapped));
+  CHECK(hipHostGetDevicePointer((void**)&hd_p, h_p, 0));
+  CHECK(hipHostMalloc((void**)&h_x, 64 * 32, hipHostMallocMapped));
+  CHECK(hipHostGetDevicePointer((void**)&hd_x, h_x, 0));
+  CHECK(hipHostMalloc((void**)&h_done, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  CHECK(hipHostGetDevicePointer((void**)&hd_done, h_done, 0));
+  std::memset(h_x, 0, 64 * 32);
+  *h_done = 0;
+  Big big{};
+  big.n = 64;
+
+  const char* names[] = {"empty", "dev_write", "host_write", "host_read", "kernarg", "flag_event", "flag_spin"};
+  unsigned seq = 0;
+  for (int v = 0; v < 7; ++v) {
+    std::vector<double> lat, api;
+    for (int i = 0; i < iters + 50; ++i) {
+      const double t0 = now_us();
+      switch (v) {
+        case 0: hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s, d_idx); break;
+        case 1: hipLaunchKernelGGL(k_write, dim3(1), dim3(64), 0, s, d_idx, d_p); break;
+        case 2: hipLaunchKernelGGL(k_write, dim3(1), dim3(64), 0, s, hd_idx, hd_p); break;
+        case 3: hipLaunchKernelGGL(k_read, dim3(1), dim3(64), 0, s, hd_x, hd_idx, hd_p); break;
+        case 4: hipLaunchKernelGGL(k_kernarg, dim3(1), dim3(64), 0, s, big, hd_idx, hd_p); break;
+        default: hipLaunchKernelGGL(k_flag, dim3(1), dim3(64), 0, s, hd_idx, hd_p, hd_done, ++seq); break;
+      }
+      if (v != 6) CHECK(hipEventRecord(ev, s));
+      const double t1 = now_us();
+      if (v == 6) {
+        while (__atomic_load_n(h_done, __ATOMIC_ACQUIRE) != seq) {
+        }
+      } else {
+        while (hipEventQuery(ev) == hipErrorNotReady) {
+        }
+      }
+      const double t2 = now_us();
+      if (i >= 50) {
+        lat.push_back(t2 - t0);
+        api.push_back(t1 - t0);
+      }
+    }
+    if (v == 6) CHECK(hipStreamSynchronize(s));
+    std::sort(lat.begin(), lat.end());
+    std::sort(api.begin(), api.end());
+    std::printf("%-11s launch+record %6.2f us   launch->done p50 %6.2f us  p10 %6.2f  p90 %6.2f\n", names[v],
+                api[api.size() / 2], lat[lat.size() / 2], lat[lat.size() / 10], lat[lat.size() * 9 / 10]);
+  }
+  return 0;
+}
