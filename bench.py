@@ -273,10 +273,10 @@ def bench_train(args, info):
 
 
 def bench_train_softmax(args, info):
-    """Multiclass (1000-class, F=256) DP SGD: MFMA fwd/grad + hipBLASLt dW + RCCL all-reduce."""
+    """Multiclass (1000-class, F=256) DP SGD: MFMA row stats + fused G/dW kernel + RCCL all-reduce."""
     from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer, synthetic_multiclass
 
-    F, K, B = 256, 1000, args.softmax_batch
+    F, K, B = args.softmax_features, 1000, args.softmax_batch
     nb = max(1, args.shards // 2)
     X, y = synthetic_multiclass(B * nb, F, K, seed=99 + info.rank, device=info.device)
     tr = SoftmaxSGDTrainer(F, K, info=info, lr=0.5, l2=1e-5, device=info.device)
@@ -291,7 +291,7 @@ def bench_train_softmax(args, info):
     run(args.warmup)
     elapsed, _ = _timed(info, lambda: run(args.steps))
     value = info.world * B * args.steps / elapsed
-    flops = 3 * 2 * B * K * tr.F_aug * info.world * args.steps / elapsed  # 2 fwd passes + dW GEMM
+    flops = 3 * 2 * B * K * tr.F_aug * info.world * args.steps / elapsed  # 2 logits passes + dW
     return ("train_softmax_samples_per_sec", value, "samples/s", elapsed,
             {"final_loss": tr.last_loss(), "tflops_incl_recompute": flops / 1e12},
             {"model": f"{K}-class softmax LogisticRegression F={F} (mini-batch SGD)", "global_batch": B * info.world,
@@ -319,6 +319,7 @@ def main(argv=None) -> int:
     ap.add_argument("--train-batch", type=int, default=1 << 18)
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--softmax-batch", type=int, default=1 << 16)
+    ap.add_argument("--softmax-features", type=int, default=256, help="train_softmax: F (<= 512)")
     ap.add_argument("--cpu", action="store_true", help="force the CPU backend (testing without a GPU)")
     ap.add_argument("--pin", default="auto", choices=["auto", "on", "off"],
                     help="pin this rank to its share of physical cores on its GPU's NUMA node "

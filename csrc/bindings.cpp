@@ -240,19 +240,6 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("params"), py::arg("grad"), py::arg("mom"), py::arg("n"), py::arg("n_pen"), py::arg("lr"),
       py::arg("inv_n"), py::arg("l2"), py::arg("momentum"), py::arg("stream") = 0);
-  m.def("softmax_train_ldx", &softmax_train_ldx);
-  m.def("softmax_train_workspace", &softmax_train_workspace);
-  m.def(
-      "softmax_train_grad",
-      [](uintptr_t X_aug, int64_t ldx, uintptr_t W, uintptr_t b, uintptr_t y, int64_t B, int F, int K, int kind,
-         uintptr_t G, int64_t ldg, uintptr_t stats_out, uintptr_t ws, size_t ws_bytes, uintptr_t stream) {
-        launch_softmax_train_grad(ptr<void>(X_aug), ldx, ptr<void>(W), ptr<float>(b), ptr<int32_t>(y), B, F, K, kind,
-                                  ptr<void>(G), ldg, ptr<float>(stats_out), ptr<void>(ws), ws_bytes,
-                                  stream_of(stream));
-      },
-      py::arg("X_aug"), py::arg("ldx"), py::arg("W"), py::arg("b"), py::arg("y"), py::arg("B"), py::arg("F"),
-      py::arg("K"), py::arg("kind"), py::arg("G"), py::arg("ldg"), py::arg("stats_out"), py::arg("ws"),
-      py::arg("ws_bytes"), py::arg("stream") = 0);
   m.def("softmax_grad_dw_supported", &softmax_grad_dw_supported);
   m.def("softmax_grad_dw_force_plan", &softmax_grad_dw_force_plan, py::arg("row_groups") = 0, py::arg("nc") = 0,
         py::arg("pipe") = 0);

@@ -83,26 +83,17 @@ void launch_merge_rowstates(const void* parts, int nparts, int64_t B, const Shar
 void launch_logits_epilogue(const float* Z, const float* b, int64_t B, int K, int kind, int32_t* out_idx, float* out_p,
                             hipStream_t stream);
 
-// Multiclass training (gemm_softmax.hip, MODE 2 + 3). X_aug = [X | 1 | 0 x 7] bf16 with row
-// stride ldx = softmax_train_ldx(F) = F + 8 (the forward reads the first F columns; the ones
-// column makes the backward GEMM produce the intercept gradient); W: [K, F] bf16; b: [K] f32.
-// Writes G = softmax(Z) - onehot(y) (OvR: sigmoid(Z) - onehot) as bf16 [B, ldg] (rows padded to a
-// multiple of 128: stores are unguarded) and stats_out = [loss_sum, n_correct];
-// dW_aug = G^T X_aug is then one library GEMM (hipBLASLt).
-// Workspace: softmax_train_workspace(B, K, F) bytes, zeroed once (split-merge counters re-arm).
-int softmax_train_ldx(int F);  // -1 unless F is 32/64/128/256/512
-size_t softmax_train_workspace(int64_t B, int K, int F);
-void launch_softmax_train_grad(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
-                               int64_t B, int F, int K, int kind, void* G, int64_t ldg, float* stats_out,
-                               void* workspace, size_t ws_bytes, hipStream_t stream);
+// Multiclass training row stats (gemm_softmax.hip MODE 2), X_aug = [X | 0.. | 1 | 0 x 7] bf16
+// read through its row stride ldx (the first F columns); W: [K, F] bf16; b: [K] f32.
 // MODE 2 alone: rowstat_out[B] = {logsumexp (OvR: max + log sum sigmoid), argmax bits} per row.
 size_t softmax_rowstats_workspace(int64_t B, int K, int F);
 void launch_softmax_rowstats(const void* X_aug, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K,
                              int kind, void* rowstat_out, void* workspace, size_t ws_bytes, hipStream_t stream);
 // Fused gradient (softmax_grad_dw.hip): row stats, then G and dW_aug = G^T X_aug in one MFMA kernel
 // (G never touches HBM), then the deterministic slab reductions. dW_out: [K, F + 8] f32 (column F
-// = intercept gradient, F+1.. = 0); stats_out = [loss_sum, n_correct]. F in {128, 256},
-// ldx = F + 8. Workspace: softmax_grad_dw_workspace(B, K, F) bytes, zeroed once.
+// = intercept gradient, F+1.. = 0); stats_out = [loss_sum, n_correct]. F in {128, 256, 512}
+// (narrower models are zero-padded by the caller), ldx = F + 8. Workspace:
+// softmax_grad_dw_workspace(B, K, F) bytes, zeroed once.
 bool softmax_grad_dw_supported(int F);
 void softmax_grad_dw_force_plan(int row_groups, int nc, int pipe);  // benchmark hook (0 = automatic)
 size_t softmax_grad_dw_workspace(int64_t B, int K, int F);

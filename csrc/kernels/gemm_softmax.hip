@@ -24,14 +24,10 @@
 //    last chunk is masked to -inf) and uses exp2/rcp; accumulators start at the bias.
 //
 // Training (multinomial / OvR mini-batch SGD, SURVEY 2.3 K6 at BASELINE config 5 scale) reuses the
-// same tiles with two more epilogues. X carries a ones column for the backward GEMM
-// (X_aug = [X | 1 | 0 x 7], row stride F + 8; the forward reads only its first F columns), so
-// dW_aug = G^T X_aug (one library GEMM) also yields the intercept gradient:
-//  * MODE 2 (row stats): the online (max, sum-exp, argmax) state, merged across class splits like
-//    MODE 0, is published as {lse = m + log s, argmax} per row;
-//  * MODE 3 (gradient): recomputes the logits tile by tile (cheaper than a B x K f32 round trip
-//    through HBM) and writes G = softmax(z) - onehot(y) (OvR: sigmoid(z) - onehot) in bf16, plus
-//    per-block [loss_sum, n_correct] slabs.
+// same tiles for its row-stats pass (MODE 2): the online (max, sum-exp, argmax) state, merged
+// across class splits like MODE 0, is published as {lse = m + log s, argmax} per row; the fused
+// gradient kernel (softmax_grad_dw.hip) consumes it. X_aug may carry extra columns (row stride
+// ldx >= F; the forward reads only its first F columns).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -117,27 +113,16 @@ struct GemmArgs {
   unsigned int* counters;  // split merge (MODE 0/2)
   float4* partials;        // split merge (MODE 0/2)
   float* Z;                // MODE 1
-  const int32_t* y;        // MODE 3: class index per row
-  uint16_t* G;             // MODE 3: bf16 [B, ldg]
-  int64_t ldg;
-  float2* rowstat;         // MODE 2 output / MODE 3 input: {lse, argmax bits}
+  float2* rowstat;         // MODE 2 output: {lse, argmax bits}
   float4* rowstate;        // MODE 4 output: {max, sum, argmax bits, 0} (class-sharded TP)
-  float* stat_slabs;       // MODE 3: [gridDim.y * gridDim.x][2] = {loss_sum, n_correct}
 };
-
-__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  const uint32_t lo = __builtin_bit_cast(uint16_t, (__bf16)a);
-  const uint32_t hi = __builtin_bit_cast(uint16_t, (__bf16)b);
-  return lo | (hi << 16);
-}
 
 // One 64-class chunk against the LDS image `wb`: MFMAs into bias-initialised accumulators, then the
 // mode's epilogue. Inlined into the kernel (reference parameters stay in registers).
 template <int KS, int NT, int MODE, bool OVR>
 __device__ __forceinline__ void compute_chunk(const unsigned char* wb, const bf16x8_t (&xf)[NT][KS], int c0, int c_end,
                                               int q, int col, int64_t row0, int64_t B, int K, const float* bias_lds,
-                                              const GemmArgs& a, RowState (&st)[NT], const int (&yl)[NT],
-                                              const float (&lse)[NT], float& loss_acc) {
+                                              const GemmArgs& a, RowState (&st)[NT]) {
   constexpr bool ovr = OVR;
   // The accumulators start at the bias, which was DMA'd into LDS next to the W chunk (clamped
   // index; classes past the split are masked later), so the epilogue needs no per-element add and
@@ -186,35 +171,6 @@ __device__ __forceinline__ void compute_chunk(const unsigned char* wb, const bf1
           if (cls < c_end) a.Z[row * K + cls] = v[i];
         }
       }
-    } else if constexpr (MODE == 3) {
-      const int64_t row = row0 + t * 16 + col;
-      const bool row_ok = row < B;
-      const float lse2 = lse[t] * LOG2E_F;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int cls0 = c0 + mt * 16 + q * 4;  // 4 consecutive classes -> one 8-byte store
-        float g[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float z = v[mt * 4 + r];
-          const bool hot = cls0 + r == yl[t];
-          float pr, l;
-          if constexpr (OVR) {
-            const float e = __builtin_amdgcn_exp2f(-fabsf(z) * LOG2E_F);  // exp(-|z|) in (0, 1]
-            pr = z >= 0.f ? __builtin_amdgcn_rcpf(1.f + e) : e * __builtin_amdgcn_rcpf(1.f + e);
-            // BCE: softplus(z) - z*[hot]; softplus(z) = max(z, 0) + log(1 + exp(-|z|))
-            l = fmaxf(z, 0.f) - (hot ? z : 0.f) + __builtin_amdgcn_logf(1.f + e) * LN2_F;
-            l = z == -INFINITY ? 0.f : l;
-          } else {
-            pr = __builtin_amdgcn_exp2f(fmaf(z, LOG2E_F, -lse2));
-            l = hot ? lse[t] - z : 0.f;
-          }
-          g[r] = row_ok && z != -INFINITY ? pr - (hot ? 1.f : 0.f) : 0.f;
-          loss_acc += row_ok ? l : 0.f;
-        }
-        if (row_ok && cls0 < c_end)
-          *reinterpret_cast<uint2*>(a.G + row * a.ldg + cls0) = make_uint2(pack_bf16x2(g[0], g[1]), pack_bf16x2(g[2], g[3]));
-      }
     } else {  // MODE 0 / 2: online (max, sum, first argmax)
       float cm = v[0];
       int ci = 0;
@@ -251,8 +207,8 @@ __device__ __forceinline__ void compute_chunk(const unsigned char* wb, const bf1
 }
 
 // KS = F/32 (exact), NT = 16-row N-tiles per wave, MODE: 0 = fused predict epilogue,
-// 1 = write logits, 2 = training row stats, 3 = training gradient (see header), 4 = raw online
-// softmax state per row (class-sharded TP, merged across ranks by shard.hip).
+// 1 = write logits, 2 = training row stats (see header), 4 = raw online softmax state per row
+// (class-sharded TP, merged across ranks by shard.hip).
 template <int KS, int NT, int MODE, bool OVR>
 __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   const uint16_t* __restrict__ X = a.X;
@@ -274,7 +230,6 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   constexpr int PIECES = CLASS_CHUNK * NCH / 256;      // 16-byte pieces per thread per chunk (== KS)
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF_BYTES + 16];
   int* const flag = reinterpret_cast<int*>(smem + 2 * BUF_BYTES);
-  float* const red = reinterpret_cast<float*>(smem);  // MODE 3 stats reduction (after the last chunk)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -289,21 +244,6 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   const int c_last = c_begin + ((c_end - 1 - c_begin) / CLASS_CHUNK) * CLASS_CHUNK;  // last chunk start
 
   bf16x8_t xf[NT][KS];
-  // MODE 3: this lane's rows' label and {lse, argmax} (clamped loads, masked by row < B later)
-  int yl[NT];
-  float lse[NT];
-  int amax[NT];
-  if constexpr (MODE == 3) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int64_t r = min(row0 + t * 16 + col, B - 1);
-      yl[t] = a.y[r];
-      const float2 rs = a.rowstat[r];
-      lse[t] = rs.x;
-      amax[t] = __float_as_int(rs.y);
-    }
-  }
-  float loss_acc = 0.f, correct_acc = 0.f;
 
   // ---- W chunk staging: global -> registers (issue early) -> LDS (write late). Plain unrolled
   // code with ext_vector registers: a lambda capture or HIP_vector_type array goes to scratch.
@@ -368,8 +308,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   MLAPI_RAW_BARRIER()
   for (int c0 = c_begin; c0 < c_end; c0 += CLASS_CHUNK) {
     compute_chunk<KS, NT, MODE, OVR>(smem + buf * BUF_BYTES, xf, c0, c_end, q, col, row0, B, K,
-                                     reinterpret_cast<const float*>(smem + buf * BUF_BYTES + W_BYTES), a, st, yl, lse,
-                                     loss_acc);
+                                     reinterpret_cast<const float*>(smem + buf * BUF_BYTES + W_BYTES), a, st);
     if (c0 + 2 * CLASS_CHUNK < c_end) {
       MLAPI_RAW_BARRIER()  // every wave is done reading `buf`
       MLAPI_DMA_CHUNK(c0 + 2 * CLASS_CHUNK, buf)
@@ -382,27 +321,6 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   }
 #undef MLAPI_RAW_BARRIER
 #undef MLAPI_DMA_CHUNK
-  if constexpr (MODE == 3) {
-    // correct count: split 0, one lane (q == 0) per row
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-      correct_acc += (blockIdx.y == 0 && q == 0 && row0 + t * 16 + col < B && amax[t] == yl[t]) ? 1.f : 0.f;
-    // deterministic block reduction -> slab [split][row block][2]
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      loss_acc += __shfl_xor(loss_acc, off, 64);
-      correct_acc += __shfl_xor(correct_acc, off, 64);
-    }
-    if (lane == 0) {
-      red[wave * 2] = loss_acc;
-      red[wave * 2 + 1] = correct_acc;
-    }
-    __syncthreads();
-    if (tid < 2) {
-      const float v = red[tid] + red[2 + tid] + red[4 + tid] + red[6 + tid];
-      a.stat_slabs[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 2 + tid] = v;
-    }
-  }
   if constexpr (MODE == 0 || MODE == 2 || MODE == 4) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -586,61 +504,11 @@ GemmArgs base_args(const void* X, const void* W, int64_t B, int F, int K, int ki
   return a;
 }
 
-struct TrainLayout {
-  Plan plan;
-  size_t partials_off, rowstat_off, slabs_off, total;
-};
-
-TrainLayout train_layout(int64_t B, int K, int F) {
-  TrainLayout L;
-  L.plan = make_plan(B, K, F, true);
-  auto align = [](size_t v) { return (v + 255) & ~size_t(255); };
-  L.partials_off = COUNTER_BYTES;
-  L.rowstat_off = align(L.partials_off + (L.plan.splits > 1 ? (size_t)L.plan.splits * B * sizeof(float4) : 0));
-  L.slabs_off = align(L.rowstat_off + (size_t)B * sizeof(float2));
-  L.total = align(L.slabs_off + (size_t)L.plan.row_blocks * L.plan.splits * 2 * sizeof(float));
-  return L;
-}
-
 }  // namespace
 
 void gemm_softmax_force_plan(int nt, int splits) {
   g_force_nt = nt;
   g_force_splits = splits;
-}
-
-int softmax_train_ldx(int F) {
-  return (F == 32 || F == 64 || F == 128 || F == 256 || F == 512) ? F + 8 : -1;
-}
-
-size_t softmax_train_workspace(int64_t B, int K, int F) { return train_layout(B, K, F).total; }
-
-void launch_softmax_train_grad(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
-                               int64_t B, int F, int K, int kind, void* G, int64_t ldg, float* stats_out,
-                               void* workspace, size_t ws_bytes, hipStream_t stream) {
-  if (B <= 0) return;
-  if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
-    throw std::invalid_argument("softmax_train: multiclass kinds only (binary models use train_binary)");
-  if (ldg < K || ldg % 8 != 0) throw std::invalid_argument("softmax_train: ldg must be >= K and a multiple of 8");
-  if (ldx < F || ldx % 8 != 0) throw std::invalid_argument("softmax_train: ldx must be >= F and a multiple of 8");
-  if (reinterpret_cast<uintptr_t>(X_aug) % 16 != 0 || reinterpret_cast<uintptr_t>(W) % 16 != 0)
-    throw std::invalid_argument("softmax_train: X_aug and W must be 16-byte aligned");
-  const TrainLayout L = train_layout(B, K, F);
-  if (ws_bytes < L.total) throw std::invalid_argument("softmax_train: workspace too small (zero it once)");
-  unsigned char* ws = static_cast<unsigned char*>(workspace);
-  GemmArgs args = base_args(X_aug, W, B, F, K, kind);
-  args.ldx = ldx;
-  args.bias = b;
-  args.counters = reinterpret_cast<unsigned int*>(ws);
-  args.partials = reinterpret_cast<float4*>(ws + L.partials_off);
-  args.rowstat = reinterpret_cast<float2*>(ws + L.rowstat_off);
-  args.stat_slabs = reinterpret_cast<float*>(ws + L.slabs_off);
-  args.y = y;
-  args.G = static_cast<uint16_t*>(G);
-  args.ldg = ldg;
-  launch_mode<2>(args, F, L.plan, stream);  // {lse, argmax} per row (split merge in-launch)
-  launch_mode<3>(args, F, L.plan, stream);  // G = P - Y (bf16) + [loss, correct] slabs
-  launch_reduce_slabs_f32(args.stat_slabs, (int)(L.plan.row_blocks * L.plan.splits), 2, stats_out, stream);
 }
 
 size_t softmax_rowstats_workspace(int64_t B, int K, int F) {

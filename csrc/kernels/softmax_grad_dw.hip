@@ -129,9 +129,20 @@ struct GradDwArgs {
 // PIPE (NC = 2 only): a software pipeline across tiles with 3 LDS buffers. Iteration t computes the
 // logits of tile t+1 and the epilogue of tile t in one basic block, so the epilogue's VALU work
 // fills the MFMA issue gaps of the next tile's logits instead of running exposed at 1 wave/SIMD.
+//
+// F = 512 (KS = 16): the double-buffered tile is 2 x 65 KB of LDS (one block per CU) and the 32
+// dW N-tiles alone take 128 accumulator registers, so it runs NC = 1 at one wave per SIMD
+// (512 VGPRs: the accumulators spill into the AGPR half instead of scratch).
+template <int KS, int NC>
+constexpr int gdw_waves_per_eu() {
+  return KS >= 16 ? 1 : 3 - NC;
+}
+
 template <int KS, bool OVR, int NC, bool PIPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3 - NC, 3 - NC))) void softmax_grad_dw_kernel(
-    GradDwArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gdw_waves_per_eu<KS, NC>(),
+                                                                     gdw_waves_per_eu<KS, NC>()))) void
+softmax_grad_dw_kernel(GradDwArgs a) {
+  static_assert(KS < 16 || NC == 1, "F = 512 runs 16 classes per wave");
   static_assert(!PIPE || NC == 2, "the pipelined variant runs at 1 wave/SIMD (NC = 2)");
   constexpr int NBUF = PIPE ? 3 : 2;
   constexpr int CLASSES = 4 * WAVE_CLASSES * NC;
@@ -573,7 +584,10 @@ int g_force_row_groups = 0;  // benchmark hooks (softmax_grad_dw_force_plan)
 int g_force_nc = 0;
 int g_force_pipe = 0;  // 0 auto (off), 1 off, 2 on (NC = 2 only)
 
-int auto_nc(int K) { return g_force_nc > 0 ? g_force_nc : (K >= 256 ? 2 : 1); }
+int auto_nc(int K, int F) {
+  if (F >= 512) return 1;
+  return g_force_nc > 0 ? g_force_nc : (K >= 256 ? 2 : 1);
+}
 
 GdwLayout gdw_layout(int64_t B, int K, int F, int nc) {
   GdwLayout L;
@@ -581,9 +595,9 @@ GdwLayout gdw_layout(int64_t B, int K, int F, int nc) {
   L.tiles = (int)((B + ROWS - 1) / ROWS);
   const int classes = 4 * WAVE_CLASSES * nc;
   L.class_groups = (K + classes - 1) / classes;
-  // resident blocks: 2 per CU at NC = 1, 1 at NC = 2 (unless the rows run out); every row group
-  // gets >= 1 tile
-  const int target = nc == 1 ? 512 : 256;
+  // resident blocks: 2 per CU at NC = 1, 1 at NC = 2 or F = 512 (unless the rows run out); every
+  // row group gets >= 1 tile
+  const int target = nc == 1 && F < 512 ? 512 : 256;
   int want = g_force_row_groups > 0 ? g_force_row_groups : (target + L.class_groups - 1) / L.class_groups;
   want = want < 1 ? 1 : (want > L.tiles ? L.tiles : want);
   L.tiles_per_group = (L.tiles + want - 1) / want;
@@ -598,7 +612,7 @@ GdwLayout gdw_layout(int64_t B, int K, int F, int nc) {
 
 }  // namespace
 
-bool softmax_grad_dw_supported(int F) { return F == 128 || F == 256; }
+bool softmax_grad_dw_supported(int F) { return F == 128 || F == 256 || F == 512; }
 
 void softmax_grad_dw_force_plan(int row_groups, int nc, int pipe) {
   g_force_row_groups = row_groups;
@@ -615,13 +629,14 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
                             int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,
                             size_t ws_bytes, hipStream_t stream) {
   if (B <= 0) return;
-  if (!softmax_grad_dw_supported(F)) throw std::invalid_argument("softmax_grad_dw: F must be 128 or 256");
+  if (!softmax_grad_dw_supported(F))
+    throw std::invalid_argument("softmax_grad_dw: F must be 128, 256 or 512 (pad narrower features)");
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("softmax_grad_dw: multiclass kinds only");
   if (ldx != F + 8) throw std::invalid_argument("softmax_grad_dw: X_aug row stride must be F + 8");
   if (reinterpret_cast<uintptr_t>(X_aug) % 16 != 0 || reinterpret_cast<uintptr_t>(W) % 16 != 0)
     throw std::invalid_argument("softmax_grad_dw: X_aug and W must be 16-byte aligned");
-  const GdwLayout L = gdw_layout(B, K, F, auto_nc(K));
+  const GdwLayout L = gdw_layout(B, K, F, auto_nc(K, F));
   if (ws_bytes < L.total) throw std::invalid_argument("softmax_grad_dw: workspace too small (zero it once)");
   unsigned char* ws = static_cast<unsigned char*>(workspace);
   float2* rowstat = reinterpret_cast<float2*>(ws + L.rowstat_off);
@@ -665,12 +680,15 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
   };
   using I4 = std::integral_constant<int, 4>;
   using I8 = std::integral_constant<int, 8>;
+  using I16 = std::integral_constant<int, 16>;
   using N1 = std::integral_constant<int, 1>;
   using N2 = std::integral_constant<int, 2>;
   if (F == 128)
     L.nc == 1 ? launch(I4{}, N1{}) : launch(I4{}, N2{});
-  else
+  else if (F == 256)
     L.nc == 1 ? launch(I8{}, N1{}) : launch(I8{}, N2{});
+  else
+    launch(I16{}, N1{});
   MLAPI_HIP_CHECK(hipGetLastError());
   if (reinterpret_cast<uintptr_t>(dW_out) % 16 == 0) {
     const int width4 = K * (F + 8) / 4;

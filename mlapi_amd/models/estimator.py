@@ -11,7 +11,8 @@ Fitting evaluates the loss/gradient with the fp64 ``train_small_grad`` HIP kerne
 selected (``device='cuda'`` / ``'auto'`` with a GPU visible) and with float64 numpy otherwise.
 Prediction uses the fused ``linear_small`` (fp64) kernel on the GPU, or the float64 oracle.
 ``solver='sgd'`` trains with the mini-batch SGD kernels instead: the fused binary step for two
-classes, the MFMA softmax / one-vs-rest gradient + hipBLASLt dW GEMM for more.
+classes, the fused MFMA softmax / one-vs-rest gradient kernel (G and dW = G^T X in one kernel, no
+vendor GEMM) for more.
 """
 from __future__ import annotations
 
@@ -126,17 +127,14 @@ class LogisticRegression:
         from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer
 
         n, F = X.shape
-        widths = [w for w in (32, 64, 128, 256, 512) if w >= F]
-        if not widths:
+        if F > 512:
             raise ValueError("solver='sgd' multiclass supports up to 512 features")
-        Fp = widths[0]  # zero feature columns get zero gradient: their weights stay 0 and are dropped
-        Xp = np.zeros((n, Fp), dtype=np.float32)
-        Xp[:, :F] = X
         yi = torch.as_tensor(np.searchsorted(classes, y).astype(np.int32), device=dev)
         kind = Kind.OVR if self.multi_class == "ovr" else Kind.MULTINOMIAL
-        tr = SoftmaxSGDTrainer(Fp, len(classes), kind=kind, lr=self.lr, l2=1.0 / (self.C * n), momentum=0.9,
+        # the trainer zero-pads F to its kernel width; padded weights get zero gradients and stay 0
+        tr = SoftmaxSGDTrainer(F, len(classes), kind=kind, lr=self.lr, l2=1.0 / (self.C * n), momentum=0.9,
                                device=dev)
-        Xa = tr.prepare(torch.as_tensor(Xp, device=dev))
+        Xa = tr.prepare(torch.as_tensor(np.asarray(X, dtype=np.float32), device=dev))
         rng = np.random.default_rng(self.random_state)
         for _ in range(self.epochs):
             perm = torch.as_tensor(rng.permutation(n), device=dev)
@@ -144,7 +142,7 @@ class LogisticRegression:
                 idx = perm[s:s + self.batch_size]
                 tr.step(Xa[idx].contiguous(), yi[idx].contiguous())
         m = tr.to_model(classes=classes)
-        m = LinearModel(m.W[:, :F].copy(), m.b, classes, kind, meta={"solver": "sgd", "n_iter_": [tr.steps]})
+        m.meta.update(solver="sgd", n_iter_=[tr.steps])
         return m
 
     # ------------------------------------------------------------------ predict

@@ -178,61 +178,55 @@ def cast(src: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------- multiclass training (MFMA)
+SOFTMAX_TRAIN_WIDTHS = (128, 256, 512)
+
+
+def softmax_kernel_width(F: int) -> int:
+    """Feature width the fused gradient kernel trains at: F rounded up to 128 / 256 / 512.
+
+    Narrower models are zero-padded: padded columns of X are 0, so their weights get a zero
+    gradient (and a zero L2 / momentum term) and stay exactly 0 - the trained model is the same."""
+    for w in SOFTMAX_TRAIN_WIDTHS:
+        if int(F) <= w:
+            return w
+    raise ValueError(f"softmax training kernels support up to F = 512 features (got {F}); shard wider models "
+                     "over GPUs (parallel.tensor_parallel.FeatureShardedLinear)")
+
+
 def softmax_train_faug(F: int) -> int:
-    """Width F_aug = F + 8 of the augmented features [X | 1 | 0 x 7] (and of W_aug = [W | b | 0])."""
-    if int(F) not in (32, 64, 128, 256, 512):
-        raise ValueError("softmax training kernels need F in {32, 64, 128, 256, 512} (pad the features)")
-    return int(F) + 8
+    """Width F_aug = Fk + 8 of the augmented features [X | 0.. | 1 | 0 x 7] (and of W_aug = [W | 0.. | b | 0]),
+    with Fk = :func:`softmax_kernel_width` (F)."""
+    return softmax_kernel_width(F) + 8
 
 
 def augment_features(X: torch.Tensor, F_aug: int) -> torch.Tensor:
-    """[X | 1 | 0...] in bf16, shape [B, F_aug] (done once per dataset, not per step)."""
+    """[X | 0.. | 1 | 0...] in bf16, shape [B, F_aug], the ones column at F_aug - 8 (done once per
+    dataset, not per step)."""
     B, F = X.shape
     out = torch.zeros(B, F_aug, dtype=torch.bfloat16, device=X.device)
     out[:, :F] = X
-    out[:, F] = 1.0
+    out[:, F_aug - 8] = 1.0
     return out
 
 
 def augment_weights(W: torch.Tensor, b: torch.Tensor, F_aug: int) -> torch.Tensor:
-    """[W | b | 0...] in f32, shape [K, F_aug]."""
+    """[W | 0.. | b | 0...] in f32, shape [K, F_aug], the intercept at column F_aug - 8."""
     K, F = W.shape
     out = torch.zeros(K, F_aug, dtype=torch.float32, device=W.device)
     out[:, :F] = W
-    out[:, F] = b.reshape(-1)
+    out[:, F_aug - 8] = b.reshape(-1)
     return out
 
 
 class SoftmaxTrainBuffers:
-    """Persistent per-batch-size buffers of the multiclass gradient (G, workspace, stats)."""
+    """Persistent per-batch-size workspace of the fused multiclass gradient."""
 
-    def __init__(self, B: int, K: int, F: int, device, dw_path: str = None):
+    def __init__(self, B: int, K: int, F: int, device):
         self.B, self.K, self.F = B, K, F
+        if not C().softmax_grad_dw_supported(F):
+            raise ValueError(f"fused gradient kernel width must be one of {SOFTMAX_TRAIN_WIDTHS} (got {F})")
         self.stats = torch.zeros(2, dtype=torch.float32, device=device)
-        self.part = None
-        # "fused": row stats + one kernel that forms G in registers and accumulates G^T X_aug
-        # (softmax_grad_dw.hip; G never reaches HBM). "gemm": G (bf16) + hipBLASLt dW GEMM.
-        path = dw_path or os.environ.get("MLAPI_SOFTMAX_DW", "fused")
-        if path not in ("fused", "gemm"):
-            raise ValueError(f"MLAPI_SOFTMAX_DW / dw_path must be 'fused' or 'gemm', got {path!r}")
-        self.fused = path == "fused" and bool(C().softmax_grad_dw_supported(F))
-        if self.fused:
-            self.G = None
-            self.ldg = 0
-            self.splits = 1
-            self.ws = torch.zeros(C().softmax_grad_dw_workspace(B, K, F), dtype=torch.uint8, device=device)
-            return
-        self.ldg = (K + 7) // 8 * 8
-        # rows padded to whole 128-row blocks: the gradient kernel stores without a row guard
-        self.G = torch.empty((B + 127) // 128 * 128, self.ldg, dtype=torch.bfloat16, device=device)
-        self.ws = torch.zeros(C().softmax_train_workspace(B, K, F), dtype=torch.uint8, device=device)
-        # dW split over the batch: hipBLASLt tiles only the small [K, F_aug] output, so one mm runs
-        # ~48 workgroups for K=1000 (245 us at B=65536); S batched slices of ~2048 rows + a sum
-        # fill the chip (72 us at S=32: tools/softmax_train_sweep.py, profiles/r1_softmax_train).
-        S = 1
-        while S < 64 and B % (2 * S) == 0 and B // (2 * S) >= 2048:
-            S *= 2
-        self.splits = S
+        self.ws = torch.zeros(C().softmax_grad_dw_workspace(B, K, F), dtype=torch.uint8, device=device)
 
 
 def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y: torch.Tensor, kind: int,
@@ -240,13 +234,12 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
                        stats_out: torch.Tensor = None):
     """Sums over the batch of the multiclass objective's gradient, intercept included.
 
-    X_aug: [B, F + 8] bf16 from :func:`augment_features`; W: [K, F] bf16; b: [K] f32; y: int32.
-    Returns (dW_aug f32 [K, F + 8] with the intercept gradient in column F, stats f32
-    [loss_sum, n_correct]). Fused path (F in {128, 256}, the default): a row-stats launch, then one
-    MFMA kernel that forms G = P - Y in registers and accumulates dW_aug = G^T X_aug from the same
-    LDS tile, plus the deterministic slab sums. GEMM path (other widths, or MLAPI_SOFTMAX_DW=gemm):
-    two MFMA launches write G in bf16, and dW_aug = G^T X_aug is one hipBLASLt GEMM (batched over B
-    slices) with f32 output.
+    X_aug: [B, Fk + 8] bf16 from :func:`augment_features`; W: [K, Fk] bf16 (Fk in 128/256/512;
+    zero-pad narrower models); b: [K] f32; y: int32. Returns (dW_aug f32 [K, Fk + 8] with the
+    intercept gradient in column Fk, stats f32 [loss_sum, n_correct]). Two HIP launches and no
+    vendor GEMM: a row-stats pass (logsumexp / argmax per row, gemm_softmax.hip MODE 2), then
+    softmax_grad_dw.hip, which forms G = P - Y in registers and accumulates dW_aug = G^T X_aug from
+    the same LDS tile (G never reaches HBM), followed by its deterministic slab sums.
     """
     _check(X_aug, W, b, y)
     if X_aug.dtype != torch.bfloat16 or W.dtype != torch.bfloat16 or b.dtype != torch.float32 \
@@ -254,31 +247,17 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
         raise TypeError("softmax_train_grad: X_aug, W bf16, b f32 and y int32")
     B, F_aug = X_aug.shape
     K, F = W.shape
-    if F_aug != softmax_train_faug(F) or b.numel() != K or y.numel() != B:
-        raise ValueError("softmax_train_grad: shape mismatch")
+    if F not in SOFTMAX_TRAIN_WIDTHS or F_aug != F + 8 or b.numel() != K or y.numel() != B:
+        raise ValueError("softmax_train_grad: shape mismatch (W must be [K, Fk], Fk in 128/256/512, X_aug [B, Fk + 8])")
     if bufs is None or bufs.B != B or bufs.K != K or bufs.F != F:
         bufs = SoftmaxTrainBuffers(B, K, F, X_aug.device)
     stats = bufs.stats if stats_out is None else stats_out
     if dW_out is None:
         dW_out = torch.empty(K, F_aug, dtype=torch.float32, device=X_aug.device)
-    if bufs.fused:
-        if not dW_out.is_contiguous() or dW_out.shape != (K, F_aug) or dW_out.dtype != torch.float32:
-            raise ValueError("softmax_train_grad: dW_out must be a contiguous f32 [K, F + 8] tensor")
-        C().softmax_grad_dw(X_aug.data_ptr(), F_aug, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
-                            dW_out.data_ptr(), stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(), _stream())
-        return dW_out, stats
-    C().softmax_train_grad(X_aug.data_ptr(), F_aug, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
-                           bufs.G.data_ptr(), bufs.ldg, stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(),
-                           _stream())
-    S = bufs.splits
-    if S == 1:
-        torch.mm(bufs.G[:B, :K].t(), X_aug, out_dtype=torch.float32, out=dW_out)
-    else:
-        if bufs.part is None:
-            bufs.part = torch.empty(S, K, F_aug, dtype=torch.float32, device=X_aug.device)
-        Gs = bufs.G[:B].view(S, B // S, bufs.ldg)[:, :, :K]
-        torch.bmm(Gs.transpose(1, 2), X_aug.view(S, B // S, F_aug), out_dtype=torch.float32, out=bufs.part)
-        torch.sum(bufs.part, dim=0, out=dW_out)
+    if not dW_out.is_contiguous() or dW_out.shape != (K, F_aug) or dW_out.dtype != torch.float32:
+        raise ValueError("softmax_train_grad: dW_out must be a contiguous f32 [K, Fk + 8] tensor")
+    C().softmax_grad_dw(X_aug.data_ptr(), F_aug, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
+                        dW_out.data_ptr(), stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(), _stream())
     return dW_out, stats
 
 

@@ -7,8 +7,9 @@ This module is the scale-out counterpart (BASELINE config 5 with K classes): per
   1. ``softmax_train_grad``: a row-stats MFMA launch (logsumexp / argmax per row), then one fused
      MFMA kernel that forms G = P - Y in registers and accumulates dW_aug = G^T X_aug from the same
      LDS tile of X (G never reaches HBM), with the loss / correct sums. X_aug carries a ones column
-     (X_aug = [X | 1 | 0 x 7]), so dW_aug also holds the intercept gradient. Widths other than
-     F = 128/256 write G (bf16) and run dW as a hipBLASLt GEMM;
+     (X_aug = [X | 0.. | 1 | 0 x 7]), so dW_aug also holds the intercept gradient. The kernel
+     trains at Fk = 128 / 256 / 512 features; narrower models are zero-padded to Fk (padded
+     weights get zero gradients and stay 0), so no width needs a vendor GEMM;
   2. one RCCL all-reduce of the fused buffer [dW_aug | loss_sum | n_correct] (C2 + C3);
   3. ``sgd_update_2d``: W_aug = [W | b] -= lr * (g / N_global + l2 * W) with the intercept
      unpenalized, writing the bf16 W and f32 b the next forward reads in the same pass.
@@ -37,10 +38,10 @@ def synthetic_multiclass(n: int, F: int, K: int, *, seed: int = 0, device=None, 
     return X.to(device), y.to(device)
 
 
-def _faug(F: int) -> int:
-    from mlapi_amd.ops.linear import softmax_train_faug
+def _kernel_width(F: int) -> int:
+    from mlapi_amd.ops.linear import softmax_kernel_width
 
-    return softmax_train_faug(F)
+    return softmax_kernel_width(F)
 
 
 class SoftmaxSGDTrainer:
@@ -54,7 +55,8 @@ class SoftmaxSGDTrainer:
         if n_classes < 2:
             raise ValueError("need at least 2 classes")
         self.F, self.K, self.kind = int(n_features), int(n_classes), int(kind)
-        self.F_aug = _faug(self.F)
+        self.Fk = _kernel_width(self.F)  # trained width (zero-padded features beyond F)
+        self.F_aug = self.Fk + 8
         self.info = info or DistInfo(device=device)
         self.device = device if device is not None else self.info.device
         if self.device is None:
@@ -62,8 +64,8 @@ class SoftmaxSGDTrainer:
         self.on_gpu = torch.device(self.device).type == "cuda"
         self.lr, self.l2, self.momentum = lr, l2, momentum
         self.params = torch.zeros(self.K, self.F_aug, dtype=torch.float32, device=self.device)
-        # what the MFMA forward reads: bf16 W [K, F] and f32 intercepts (refreshed by every update)
-        self.shadow_w = torch.zeros(self.K, self.F, dtype=torch.bfloat16, device=self.device) if self.on_gpu else None
+        # what the MFMA forward reads: bf16 W [K, Fk] and f32 intercepts (refreshed by every update)
+        self.shadow_w = torch.zeros(self.K, self.Fk, dtype=torch.bfloat16, device=self.device) if self.on_gpu else None
         self.shadow_b = torch.zeros(self.K, dtype=torch.float32, device=self.device) if self.on_gpu else None
         n = self.K * self.F_aug
         self.grad = torch.zeros(n + 2, dtype=torch.float32, device=self.device)  # [dW_aug | loss | correct]
@@ -87,7 +89,7 @@ class SoftmaxSGDTrainer:
 
     @property
     def b(self) -> torch.Tensor:
-        return self.params[:, self.F]
+        return self.params[:, self.Fk]
 
     def _dW(self) -> torch.Tensor:
         return self.grad[: self.K * self.F_aug].view(self.K, self.F_aug)
@@ -95,13 +97,13 @@ class SoftmaxSGDTrainer:
     def set_params(self, W: torch.Tensor, b: torch.Tensor) -> None:
         self.params.zero_()
         self.params[:, : self.F] = W.to(self.params)
-        self.params[:, self.F] = b.reshape(-1).to(self.params)
+        self.params[:, self.Fk] = b.reshape(-1).to(self.params)
         self._refresh_shadow()
 
     def _refresh_shadow(self) -> None:
         if self.shadow_w is not None:
-            self.shadow_w.copy_(self.params[:, : self.F])
-            self.shadow_b.copy_(self.params[:, self.F])
+            self.shadow_w.copy_(self.params[:, : self.Fk])
+            self.shadow_b.copy_(self.params[:, self.Fk])
 
     # ---------------------------------------------------------------------------------- step
     def _local_grad(self, Xa: torch.Tensor, y: torch.Tensor) -> None:
@@ -110,7 +112,7 @@ class SoftmaxSGDTrainer:
 
             B = Xa.shape[0]
             if B not in self._bufs:
-                self._bufs[B] = SoftmaxTrainBuffers(B, self.K, self.F, Xa.device)
+                self._bufs[B] = SoftmaxTrainBuffers(B, self.K, self.Fk, Xa.device)
             softmax_train_grad(Xa, self.shadow_w, self.shadow_b, y, self.kind, bufs=self._bufs[B], dW_out=self._dW(),
                                stats_out=self.grad[self.K * self.F_aug:])
         else:
@@ -125,11 +127,11 @@ class SoftmaxSGDTrainer:
         if self.on_gpu:
             from mlapi_amd.ops.linear import sgd_update_2d
 
-            sgd_update_2d(self.params, self.grad, self.F, self.lr, 1.0 / n_global, self.l2, self.momentum, self.mom,
+            sgd_update_2d(self.params, self.grad, self.Fk, self.lr, 1.0 / n_global, self.l2, self.momentum, self.mom,
                           self.shadow_w, self.shadow_b)
         else:
             d = self._dW() / n_global
-            d[:, : self.F] += self.l2 * self.params[:, : self.F]
+            d[:, : self.Fk] += self.l2 * self.params[:, : self.Fk]
             if self.mom is not None:
                 self.mom.mul_(self.momentum).add_(d)
                 d = self.mom
@@ -147,7 +149,7 @@ class SoftmaxSGDTrainer:
         self._n_seen = Xa.shape[0] * self.info.world
 
     def capture(self, Xa: torch.Tensor, y: torch.Tensor) -> None:
-        """Capture one whole step (2 MFMA launches + reduce + GEMM + update) in a HIP graph.
+        """Capture one whole step (row stats + fused gradient + slab sums + update) in a HIP graph.
 
         Later ``step(Xa, y)`` calls with these exact tensors replay it: one launch from the host.
         Single replica only (the all-reduce stays outside graphs)."""
@@ -156,7 +158,7 @@ class SoftmaxSGDTrainer:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         saved = (self.params.clone(), None if self.mom is None else self.mom.clone())
-        with torch.cuda.stream(s):  # warm-up: allocates the buffers and hipBLASLt's workspace
+        with torch.cuda.stream(s):  # warm-up: allocates the buffers
             for _ in range(2):
                 self._local_grad(Xa, y)
                 self._update(Xa.shape[0])
@@ -201,5 +203,5 @@ class SoftmaxSGDTrainer:
 
         p = self.params.detach().cpu().double().numpy()
         classes = np.arange(self.K) if classes is None else np.asarray(classes)
-        return LinearModel(p[:, : self.F].copy(), p[:, self.F].copy(), classes, Kind(self.kind),
+        return LinearModel(p[:, : self.F].copy(), p[:, self.Fk].copy(), classes, Kind(self.kind),
                            meta={"solver": "sgd", "n_iter_": [self.steps]})

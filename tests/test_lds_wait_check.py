@@ -58,4 +58,5 @@ def test_fused_gradient_kernels_have_no_in_flight_reads(tmp_path):
     for name, body in chk.kernels(str(out), "softmax_grad_dw_kernel"):
         names.append(name)
         assert chk.check(body, name) == [], name
-    assert len(names) == 12  # F 128/256 x multinomial/OvR x {16, 32, 32 pipelined} classes per wave
+    # F 128/256 x multinomial/OvR x {16, 32, 32 pipelined} classes per wave + F 512 x 2 kinds x 16
+    assert len(names) == 14

@@ -156,7 +156,7 @@ def test_softmax_sgd_cpu_learns(kind_name):
     X, y = synthetic_multiclass(6000, 32, 7, seed=1, noise=0.3)
     tr = SoftmaxSGDTrainer(32, 7, kind=Kind[kind_name], lr=0.5, momentum=0.9, device=torch.device("cpu"))
     Xa = tr.prepare(X)
-    assert Xa.shape == (6000, 40) and torch.all(Xa[:, 32] == 1)
+    assert Xa.shape == (6000, 136) and torch.all(Xa[:, 128] == 1)  # F=32 trains zero-padded to 128
     for s in range(60):
         lo = (s * 500) % 5000
         tr.step(Xa[lo:lo + 500], y[lo:lo + 500])

@@ -1,6 +1,6 @@
-"""Time the multiclass training step's pieces (K=1000, F=256, B=65536): MFMA row-stat/grad
-launches at NT 1/2 and the dW GEMM as one hipBLASLt mm vs a batched split-B bmm + sum (the
-"gemm" dW path), and the fused G + dW kernel (softmax_grad_dw.hip) over forced row-group counts."""
+"""Time the fused multiclass gradient (row stats + softmax_grad_dw.hip + slab sums) over forced
+plans (class tiles per wave, cross-tile pipeline, row-group counts) and feature widths; every
+plan's dW is checked against the automatic plan's."""
 import json
 import sys
 
@@ -24,50 +24,29 @@ def timeit(fn, n=20):
 
 
 dev = torch.device("cuda", 0)
-B, F, K = 65536, 256, 1000
-Fa = ops.softmax_train_faug(F)
-X = ops.augment_features(torch.randn(B, F, device=dev), Fa)
-W = (torch.randn(K, F, device=dev) / 16).to(torch.bfloat16)
-bias = torch.zeros(K, device=dev)
-y = torch.randint(0, K, (B,), device=dev, dtype=torch.int32)
+B, K = 65536, 1000
 res = {}
-for nt in (1, 2):
-    C().gemm_softmax_force_plan(nt, 0)
-    bufs = ops.SoftmaxTrainBuffers(B, K, F, dev, dw_path="gemm")
-    st = torch.zeros(2, device=dev)
-    t = timeit(lambda: C().softmax_train_grad(X.data_ptr(), Fa, W.data_ptr(), bias.data_ptr(), y.data_ptr(), B, F, K, 2,
-                                              bufs.G.data_ptr(), bufs.ldg, st.data_ptr(), bufs.ws.data_ptr(),
-                                              bufs.ws.numel(), torch.cuda.current_stream().cuda_stream))
-    res[f"grad_launches_nt{nt}_us"] = t
-C().gemm_softmax_force_plan(0, 0)
-G = bufs.G[:B, :K]
-out = torch.empty(K, Fa, device=dev)
-res["dW_mm_us"] = timeit(lambda: torch.mm(G.t(), X, out_dtype=torch.float32, out=out))
-ref = out.clone()
-for S in (2, 4, 8, 16, 32, 64):
-    Gs = bufs.G[:B].view(S, B // S, bufs.ldg)[:, :, :K]
-    Xs = X.view(S, B // S, Fa)
-    part = torch.empty(S, K, Fa, device=dev)
-
-    def f():
-        torch.bmm(Gs.transpose(1, 2), Xs, out_dtype=torch.float32, out=part)
-        torch.sum(part, dim=0, out=out)
-
-    res[f"dW_bmm_S{S}_us"] = timeit(f)
-    res[f"dW_bmm_S{S}_maxdiff"] = (out - ref).abs().max().item()
-# fused path: rowstats + G/dW kernel + slab sums, whole call
 stf = torch.zeros(2, device=dev)
-for nc, pipe in ((1, 0), (2, 1), (2, 2)):
-    for groups in (0, 16, 32, 64):
-        C().softmax_grad_dw_force_plan(groups, nc, pipe)
-        fb = ops.SoftmaxTrainBuffers(B, K, F, dev, dw_path="fused")
-        res[f"fused_nc{nc}_pipe{pipe}_groups{groups}_us"] = timeit(
-            lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=fb, dW_out=out, stats_out=stf))
-        res[f"fused_nc{nc}_pipe{pipe}_groups{groups}_maxdiff"] = (out - ref).abs().max().item()
-C().softmax_grad_dw_force_plan(0, 0, 0)
-gb = ops.SoftmaxTrainBuffers(B, K, F, dev, dw_path="gemm")
-res["gemm_path_total_us"] = timeit(lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=gb, dW_out=out, stats_out=stf))
-res["dW_ref_absmax"] = ref.abs().max().item()
+for F in (128, 256, 512):
+    Fa = ops.softmax_train_faug(F)
+    X = ops.augment_features(torch.randn(B, F, device=dev), Fa)
+    W = (torch.randn(K, F, device=dev) / 16).to(torch.bfloat16)
+    bias = torch.zeros(K, device=dev)
+    y = torch.randint(0, K, (B,), device=dev, dtype=torch.int32)
+    out = torch.empty(K, Fa, device=dev)
+    fb = ops.SoftmaxTrainBuffers(B, K, F, dev)
+    res[f"F{F}_auto_us"] = timeit(lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=fb, dW_out=out, stats_out=stf))
+    ref = out.clone()
+    plans = ((1, 0), (2, 1), (2, 2)) if F < 512 else ((1, 0),)
+    for nc, pipe in plans:
+        for groups in (0, 16, 32, 64):
+            C().softmax_grad_dw_force_plan(groups, nc, pipe)
+            pb = ops.SoftmaxTrainBuffers(B, K, F, dev)  # the workspace layout depends on the forced plan
+            res[f"F{F}_nc{nc}_pipe{pipe}_groups{groups}_us"] = timeit(
+                lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=pb, dW_out=out, stats_out=stf))
+            res[f"F{F}_nc{nc}_pipe{pipe}_groups{groups}_maxdiff"] = (out - ref).abs().max().item()
+    C().softmax_grad_dw_force_plan(0, 0, 0)
+    res[f"F{F}_tflops_auto"] = 4 * B * K * Fa / res[f"F{F}_auto_us"] / 1e6  # rowstats + logits + dW
 for k, v in res.items():
-    print(f"{k:28s} {v:10.3f}")
+    print(f"{k:36s} {v:10.3f}")
 json.dump(res, open("gpurun_out/softmax_train_sweep.json", "w"), indent=1)
