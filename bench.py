@@ -208,6 +208,27 @@ def bench_serve_wide(args, info):
                                                "via POST /predict, bf16 kernels")
 
 
+def _launcher(args, call):
+    """The timed region of the kernel benches: args.steps calls of ``call``, either eager or
+    captured once into a HIP graph (outside the timed region) and replayed in it."""
+    import torch
+
+    if args.launch == "eager" or not torch.cuda.is_available():
+        return lambda: [call() for _ in range(args.steps)]
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        call()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(args.steps):
+            call()
+    g.replay()  # first replay uploads the graph: untimed
+    torch.cuda.synchronize()
+    return g.replay
+
+
 def bench_gemv(args, info):
     import torch
 
@@ -220,8 +241,8 @@ def bench_gemv(args, info):
     idx = torch.empty(B, dtype=torch.int32, device=info.device)
     p = torch.empty(B, dtype=torch.float32, device=info.device)
     for _ in range(args.warmup):
-        ops.gemv_binary(X, w, 0.1)
-    elapsed, _ = _timed(info, lambda: [ops.gemv_binary(X, w, 0.1) for _ in range(args.steps)])
+        ops.gemv_binary(X, w, 0.1, out=(idx, p))
+    elapsed, _ = _timed(info, _launcher(args, lambda: ops.gemv_binary(X, w, 0.1, out=(idx, p))))
     value = info.world * B * args.steps / elapsed
     gbps = B * F * 2 * args.steps / (elapsed) / 1e9
     return ("rows_per_sec_binary_predict", value, "rows/s", elapsed, {"hbm_GBps_per_gpu": gbps},
@@ -243,10 +264,12 @@ def bench_gemm(args, info):
     out = (torch.empty(B, dtype=torch.int32, device=info.device), torch.empty(B, device=info.device))
     for _ in range(args.warmup):
         op(X, W, b, out=out)
-    elapsed, _ = _timed(info, lambda: [op(X, W, b, out=out) for _ in range(args.steps)])
+    run = _launcher(args, lambda: op(X, W, b, out=out))
+    elapsed, _ = _timed(info, run)
     value = info.world * B * args.steps / elapsed
     tflops = 2 * B * F * K * args.steps / elapsed / 1e12
-    return ("rows_per_sec_softmax_predict", value, "rows/s", elapsed, {"tflops_per_gpu": tflops},
+    return ("rows_per_sec_softmax_predict", value, "rows/s", elapsed,
+            {"tflops_per_gpu": tflops, "us_per_call": elapsed / args.steps * 1e6, "launch": args.launch},
             {"model": "softmax regression F=256 K=1000", "global_batch": B * info.world, "seq_len": 1,
              "features": F, "parallelism": f"dp{info.world}"})
 
@@ -316,6 +339,9 @@ def main(argv=None) -> int:
     ap.add_argument("--c1-requests", type=int, default=3000)
     ap.add_argument("--rows", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--launch", default="graph", choices=["graph", "eager"],
+                    help="gemv/gemm: the timed K calls replayed from one captured HIP graph (GPU time) or "
+                         "dispatched one by one from Python (adds host overhead per call)")
     ap.add_argument("--train-batch", type=int, default=1 << 18)
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--softmax-batch", type=int, default=1 << 16)

@@ -152,7 +152,8 @@ PYBIND11_MODULE(_C, m) {
       py::arg("dt"), py::arg("X"), py::arg("w"), py::arg("bias"), py::arg("B"), py::arg("F"), py::arg("kind"),
       py::arg("out_idx"), py::arg("out_p"), py::arg("stream") = 0);
   m.def("gemm_softmax_workspace", &gemm_softmax_workspace);
-  m.def("gemm_softmax_force_plan", &gemm_softmax_force_plan, py::arg("nt") = 0, py::arg("splits") = 0);
+  m.def("gemm_softmax_force_plan", &gemm_softmax_force_plan, py::arg("nt") = 0, py::arg("splits") = 0,
+        py::arg("kernel") = 0);
   m.def(
       "gemm_softmax",
       [](uintptr_t X, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind, uintptr_t out_idx,

@@ -55,10 +55,13 @@ void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_
                         int32_t* out_idx, float* out_p, hipStream_t stream);
 
 // ---- gemm_softmax.hip: multiclass predict, bf16 MFMA GEMM + online softmax/argmax epilogue ----
-// X: [B, F] bf16; W: [K, F] bf16; b: [K] f32. F % 32 == 0. Workspace: gemm_softmax_workspace().
+// X: [B, F] bf16; W: [K, F] bf16; b: [K] f32. F in {32, 64, 128, 256} or a multiple of 256 (any
+// width: the row-group kernel loops F in 256-feature slices). Workspace: gemm_softmax_workspace()
+// (0 when the row-group kernel serves the shape).
 size_t gemm_softmax_workspace(int64_t B, int K, int F);
-// Benchmark hook: force the (rows-per-wave tiles, class splits) plan; (0, 0) = automatic.
-void gemm_softmax_force_plan(int nt, int splits);
+// Benchmark hook: force the tiles kernel's (rows-per-wave tiles, class splits) plan and the
+// kernel (0 automatic, 1 tiles, 2 row-group); all 0 = automatic.
+void gemm_softmax_force_plan(int nt, int splits, int kernel = 0);
 void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind,
                          int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream);
 // Full logits (for tests / decision_function): Z[B, K] f32.

@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
+#include <utility>
 
 #include "mlapi/common.h"
 #include "mlapi/kernels.h"
@@ -117,23 +119,110 @@ struct GemmArgs {
   float4* rowstate;        // MODE 4 output: {max, sum, argmax bits, 0} (class-sharded TP)
 };
 
-// One 64-class chunk against the LDS image `wb`: MFMAs into bias-initialised accumulators, then the
-// mode's epilogue. Inlined into the kernel (reference parameters stay in registers).
-template <int KS, int NT, int MODE, bool OVR>
-__device__ __forceinline__ void compute_chunk(const unsigned char* wb, const bf16x8_t (&xf)[NT][KS], int c0, int c_end,
-                                              int q, int col, int64_t row0, int64_t B, int K, const float* bias_lds,
-                                              const GemmArgs& a, RowState (&st)[NT]) {
-  constexpr bool ovr = OVR;
-  // The accumulators start at the bias, which was DMA'd into LDS next to the W chunk (clamped
-  // index; classes past the split are masked later), so the epilogue needs no per-element add and
-  // no global load sits between the counted waits of the staging pipeline.
-  f32x4_t acc[NT][4];
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Online (max, sum, first argmax) update of a row state with the 16 logits a lane holds for one
+// chunk (class of v[i] = c0 + (i >> 2) * 16 + q * 4 + (i & 3), increasing with i), in three
+// stages so the pipelined loop can spread them between MFMA groups. Tree-shaped for
+// instruction-level parallelism (v3 issued one 16-step cmp -> s_nop -> cndmask chain): chunk max
+// by max3, first index holding it by a min tree over (v == max ? i : 16).
+struct OnlineTmp {
+  float m_new, part;
+  int bi;
+};
+
+template <bool OVR>
+__device__ __forceinline__ void online_stage(int stage, const float (&v)[16], int c0, int q, const RowState& S,
+                                             OnlineTmp& T) {
+  if (stage == 0) {  // chunk max, its first index, the new running max / argmax
+    float m4[4];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const f32x4_t b0 = *reinterpret_cast<const f32x4_t*>(bias_lds + mt * 16 + q * 4);
+    for (int j = 0; j < 4; ++j) m4[j] = fmaxf(fmaxf(v[4 * j], v[4 * j + 1]), fmaxf(v[4 * j + 2], v[4 * j + 3]));
+    const float cm = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+    unsigned id[16];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t][mt] = b0;
+    for (int i = 0; i < 16; ++i) id[i] = v[i] == cm ? (unsigned)i : 16u;
+    unsigned i4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) i4[j] = min(min(id[4 * j], id[4 * j + 1]), min(id[4 * j + 2], id[4 * j + 3]));
+    const unsigned ci = min(min(i4[0], i4[1]), min(i4[2], i4[3]));
+    const bool take = cm > S.m;  // strict: an earlier class (chunk) keeps a tie
+    T.m_new = take ? cm : S.m;
+    // A bit blend through an opaque mask, not a select: as a select hipcc sank the whole index
+    // computation under `take` (an exec branch splitting the pipelined MFMA / epilogue block)
+    // and rebuilt the min tree as a serial compare/select chain.
+    const int cls = c0 + (int)((ci >> 2) * 16 + q * 4 + (ci & 3));
+    int mask = -(int)take;
+    asm("" : "+v"(mask));
+    T.bi = S.bi ^ ((S.bi ^ cls) & mask);
+  } else {  // stage 1 / 2: exp (or sigmoid) terms of elements 0-7 / 8-15
+    const int i0 = stage == 1 ? 0 : 8;
+    float e[8];
+    if constexpr (OVR) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e[i] = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-v[i0 + i] * LOG2E_F));
+    } else {
+      const float m2 = T.m_new * LOG2E_F;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e[i] = __builtin_amdgcn_exp2f(fmaf(v[i0 + i], LOG2E_F, -m2));
+    }
+    const float sum = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
+    T.part = stage == 1 ? sum : T.part + sum;
   }
+}
+
+template <bool OVR>
+__device__ __forceinline__ void online_finish(const OnlineTmp& T, RowState& S) {
+  if constexpr (OVR) {
+    S.s += T.part;
+  } else {
+    // rescale the running sum to the new max; S.m = -inf (nothing accumulated yet) gives
+    // exp2(-inf) = 0. Unconditional: a select here became a branch around the exp2. (A lane that
+    // has seen only padded classes carries m = -inf with a NaN sum; merge_state drops it.)
+    const float scale = __builtin_amdgcn_exp2f(fmaf(S.m, LOG2E_F, -T.m_new * LOG2E_F));
+    S.s = fmaf(S.s, scale, T.part);
+  }
+  S.bi = T.bi;
+  S.m = T.m_new;
+}
+
+template <bool OVR>
+__device__ __forceinline__ void online_update(const float (&v)[16], int c0, int q, RowState& S) {
+  OnlineTmp T;
+  online_stage<OVR>(0, v, c0, q, S, T);
+  online_stage<OVR>(1, v, c0, q, S, T);
+  online_stage<OVR>(2, v, c0, q, S, T);
+  online_finish<OVR>(T, S);
+}
+
+// Logits of one 64-class chunk against the LDS image `wb`: MFMAs into bias-initialised
+// accumulators (the bias was DMA'd into LDS next to the W chunk, so no global load sits between
+// the staging pipeline's counted waits). Classes >= c_end (only the very last chunk of the
+// problem) get a -inf bias, which every reduction of the epilogue maps to "absent" (exp2 -> 0,
+// sigmoid -> 0, never the max): the epilogue then needs no per-element class check.
+template <int KS, int NT>
+__device__ __forceinline__ void mfma_chunk(const unsigned char* wb, const bf16x8_t (&xf)[NT][KS], int c0, int c_end,
+                                           int q, int col, const float* bias_lds, f32x4_t (&acc)[NT][4]) {
+  f32x4_t b4[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) b4[mt] = *reinterpret_cast<const f32x4_t*>(bias_lds + mt * 16 + q * 4);
+  if (c0 + CLASS_CHUNK > c_end) {  // wave-uniform: the last chunk only
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) b4[mt][r] = c0 + mt * 16 + q * 4 + r < c_end ? b4[mt][r] : -INFINITY;
+  }
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t][mt] = b4[mt];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     bf16x8_t wf[4];
@@ -146,22 +235,75 @@ __device__ __forceinline__ void compute_chunk(const unsigned char* wb, const bf1
       for (int mt = 0; mt < 4; ++mt)
         acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt], xf[t][ks], acc[t][mt], 0, 0, 0);
   }
+}
 
-  // Epilogue: lane owns classes c0 + mt*16 + q*4 + r (i = mt*4 + r, increasing class order) of
-  // batch row (t, col). Only a split's last chunk can hold classes >= c_end (wave-uniform test);
-  // they are masked to -inf, which every reduction below maps to "absent" (exp2 -> 0,
-  // sigmoid -> 0, never the max). No per-element branches: a runtime kind or bound check here
-  // made hipcc emit exec-mask branches around every element (SQ_INSTS_VALU 5.4k per wave).
-  const bool partial = c0 + CLASS_CHUNK > c_end;
+// One pipelined step (MODE 0 / 2 / 4): the MFMAs of the next chunk (nb -> nxt) with the epilogue
+// of the current one (acc -> st) spread over its k-steps: after the MFMAs of k-step k come the
+// epilogue stages scheduled there, and a sched_barrier that lets only LDS reads cross keeps the
+// interleave (the scheduler otherwise hoists all 64 MFMAs and leaves the VALU work exposed).
+template <int KS, int NT, bool OVR>
+__device__ __forceinline__ void fused_step(const unsigned char* nb, const bf16x8_t (&xf)[NT][KS], int cn, int c_end,
+                                           int q, int col, f32x4_t (&nxt)[NT][4], const f32x4_t (&acc)[NT][4], int c0,
+                                           RowState (&st)[NT]) {
+  const float* bias_lds = reinterpret_cast<const float*>(nb + CLASS_CHUNK * lds_row_stride<KS>());
+  f32x4_t b4[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) b4[mt] = *reinterpret_cast<const f32x4_t*>(bias_lds + mt * 16 + q * 4);
+  if (cn + CLASS_CHUNK > c_end) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) b4[mt][r] = cn + mt * 16 + q * 4 + r < c_end ? b4[mt][r] : -INFINITY;
+  }
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) nxt[t][mt] = b4[mt];
+  float v[NT][16];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[t][i] = acc[t][i >> 2][i & 3];
+  OnlineTmp T[NT];
+  constexpr int NSTAGE = 3 * NT + NT;  // 3 stages + finish per row tile
+  static_for<KS>([&](auto kc) {
+    constexpr int ks = decltype(kc)::value;
+    bf16x8_t wf[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+      wf[mt] = *reinterpret_cast<const bf16x8_t*>(nb + lds_off<KS>(mt * 16 + col, 4 * ks + q));
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        nxt[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt], xf[t][ks], nxt[t][mt], 0, 0, 0);
+    // epilogue stages j with slot(j) == ks, slot(j) = j * KS / NSTAGE (every stage placed once)
+    static_for<NSTAGE>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      if constexpr ((j * KS) / NSTAGE == ks) {
+        constexpr int t = j / 4, stg = j % 4;
+        if constexpr (stg < 3)
+          online_stage<OVR>(stg, v[t], c0, q, st[t], T[t]);
+        else
+          online_finish<OVR>(T[t], st[t]);
+      }
+    });
+    if constexpr (KS >= 4) __builtin_amdgcn_sched_barrier(0x100);  // only LDS reads may cross
+  });
+}
+
+// Epilogue of one chunk's logits: lane owns classes c0 + mt*16 + q*4 + r (i = mt*4 + r, increasing
+// class order) of batch row (t, col). Branch-free per element (a runtime kind or bound check here
+// made hipcc emit exec-mask branches around every element: SQ_INSTS_VALU 5.4k per wave).
+template <int NT, int MODE, bool OVR>
+__device__ __forceinline__ void epilogue_chunk(const f32x4_t (&acc)[NT][4], int c0, int c_end, int q, int col,
+                                               int64_t row0, int64_t B, int K, const GemmArgs& a,
+                                               RowState (&st)[NT]) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = acc[t][i >> 2][i & 3];
-    if (partial) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = c0 + (i >> 2) * 16 + q * 4 + (i & 3) < c_end ? v[i] : -INFINITY;
-    }
     if constexpr (MODE == 1) {
       const int64_t row = row0 + t * 16 + col;
       if (row < B) {
@@ -171,37 +313,8 @@ __device__ __forceinline__ void compute_chunk(const unsigned char* wb, const bf1
           if (cls < c_end) a.Z[row * K + cls] = v[i];
         }
       }
-    } else {  // MODE 0 / 2: online (max, sum, first argmax)
-      float cm = v[0];
-      int ci = 0;
-#pragma unroll
-      for (int i = 1; i < 16; ++i) {
-        const bool gt = v[i] > cm;  // strict: the first (lowest class) maximum wins
-        cm = gt ? v[i] : cm;
-        ci = gt ? i : ci;
-      }
-      RowState& S = st[t];
-      const bool take = cm > S.m;
-      const float m_new = take ? cm : S.m;
-      if constexpr (OVR) {
-        float add = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float e = __builtin_amdgcn_exp2f(-v[i] * LOG2E_F);  // -inf -> +inf -> sigmoid 0
-          add += __builtin_amdgcn_rcpf(1.f + e);
-        }
-        S.s += add;
-      } else {
-        const float m2 = m_new * LOG2E_F;
-        float add = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) add += __builtin_amdgcn_exp2f(fmaf(v[i], LOG2E_F, -m2));
-        // rescale the running sum to the new max (S.m = -inf: nothing accumulated yet)
-        const float scale = S.m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(fmaf(S.m, LOG2E_F, -m2));
-        S.s = fmaf(S.s, scale, add);
-      }
-      S.bi = take ? c0 + (ci >> 2) * 16 + q * 4 + (ci & 3) : S.bi;
-      S.m = m_new;
+    } else {  // MODE 0 / 2 / 4: online (max, sum, first argmax)
+      online_update<OVR>(v, c0, q, st[t]);
     }
   }
 }
@@ -252,39 +365,36 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   // last chunk address is re-loaded instead of branching around the loads.
   // Lane-linear destination: 16-B position P = i*256 + wave*64 + lane holds row P / NCH, in-row
   // position P % NCH, i.e. source chunk lds_pos(row, P % NCH).
-#define MLAPI_DMA_CHUNK(C0, BUF)                                                                        \
-  _Pragma("unroll") for (int i = 0; i < PIECES; ++i) {                                                  \
-    const int p = tid + i * 256;                                                                        \
-    const int r = p / NCH;                                                                              \
-    const int cls = min((C0) + r, K - 1);                                                               \
-    const uint16_t* src = W + (int64_t)cls * F_ + lds_pos<KS>(r, p % NCH) * 8;                          \
-    __builtin_amdgcn_global_load_lds((glob_void_t*)src,                                                 \
-                                     (lds_void_t*)(smem + (BUF) * BUF_BYTES + (i * 256 + wave * 64) * 16), \
-                                     16, 0, 0);                                                         \
-  }                                                                                                     \
-  /* bias: each wave DMAs 16 floats (lanes 0-15), one more VM op per wave (uniform count) */            \
-  if (lane < 16)                                                                                        \
-    __builtin_amdgcn_global_load_lds((glob_void_t*)(bias + min((C0) + wave * 16 + lane, K - 1)),       \
-                                     (lds_void_t*)(smem + (BUF) * BUF_BYTES + W_BYTES + wave * 64), 4, 0, 0);
+  // buffer_load ... lds through range-checked descriptors: the per-thread source offsets are
+  // chunk-invariant (hoisted out of the loop by the compiler; a local offset array here made
+  // hipcc's host pass drop every device stub of this kernel), the chunk base is a scalar offset, and classes past K read
+  // as zeros (masked in the epilogue) instead of being clamped per piece - v3 recomputed a clamped
+  // 64-bit address per piece and chunk (~90 VALU per chunk).
+  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, K * F_ * 2, 0x00020000);
+  const auto brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)bias, 0, K * 4, 0x00020000);
+#define MLAPI_DMA_CHUNK(C0, BUF)                                                                          \
+  _Pragma("unroll") for (int i = 0; i < PIECES; ++i)                                                       \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                              \
+        wrsrc, (lds_void_t*)(smem + (BUF) * BUF_BYTES + (i * 256 + wave * 64) * 16), 16, (uint32_t)((((tid + i * 256) / NCH) * F_ + lds_pos<KS>((tid + i * 256) / NCH, (tid + i * 256) % NCH) * 8) * 2),         \
+        (C0) * F_ * 2, 0, 0);                                                                              \
+  /* bias: 64 floats per chunk, every wave DMAs the same 256 B (one more VM op per wave: uniform count) */ \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void_t*)(smem + (BUF) * BUF_BYTES + W_BYTES), 4,   \
+                                           (uint32_t)lane * 4, (C0) * 4, 0, 0);
 
   RowState st[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) st[t] = RowState{-INFINITY, 0.f, 0x7fffffff};
 
-  // Two chunks in flight: the prologue DMAs chunks 0 and 1 together (a split of B=1024 has only
-  // two, so their latencies overlap instead of adding up); in the loop the DMA of chunk c+2 goes
-  // into the buffer chunk c was just read from (after a barrier: WAR), and a COUNTED wait retires
-  // chunk c+1 while c+2 stays in flight. Raw s_barrier, not __syncthreads(): the latter's fence
-  // waits vmcnt(0) and would drain the in-flight DMA (cdna_hip_programming.md "Pipelining across
-  // barriers"); the empty asm statements keep the compiler from moving LDS accesses across it.
+  // Raw s_barrier, not __syncthreads(): the latter's fence waits vmcnt(0) and would drain the
+  // in-flight DMA (cdna_hip_programming.md "Pipelining across barriers"); the empty asm statements
+  // keep the compiler from moving LDS accesses across it.
 #define MLAPI_RAW_BARRIER()          \
   asm volatile("" ::: "memory");     \
   __builtin_amdgcn_s_barrier();      \
   asm volatile("" ::: "memory");
   int buf = 0;
   MLAPI_DMA_CHUNK(c_begin, 0)
-  // X fragments for the whole feature range, straight to registers, issued between the DMAs of
-  // chunks 0 and 1 so that ONE counted wait retires chunk 0 + X while chunk 1 stays in flight
+  // X fragments for the whole feature range, straight to registers, in flight with chunk 0
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     int64_t r = row0 + t * 16 + col;
@@ -294,29 +404,40 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
     for (int ks = 0; ks < KS; ++ks)  // X is streamed once: non-temporal, keep the L2 for W
       xf[t][ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + ks * 32));
   }
-  // (the builtin form of s_waitcnt is visible to the compiler's wait insertion, so it does not
-  // add a vmcnt(0) for the X registers before the loop; encoding: vmcnt[3:0,15:14], expcnt[6:4],
-  // lgkmcnt[11:8] with the other two counters left at "no wait")
-  constexpr int kWaitChunk = ((PIECES + 1) & 15) | (7 << 4) | (15 << 8) | (((PIECES + 1) >> 4) << 14);
+  // (the builtin form of s_waitcnt is visible to the compiler's wait insertion; encoding:
+  // vmcnt[3:0,15:14], expcnt[6:4], lgkmcnt[11:8] with the other two counters left at "no wait")
   constexpr int kWaitAll = (7 << 4) | (15 << 8);
-  if (c_begin + CLASS_CHUNK < c_end) {
-    MLAPI_DMA_CHUNK(c_begin + CLASS_CHUNK, 1)
-    __builtin_amdgcn_s_waitcnt(kWaitChunk);  // chunk 0 + X landed, chunk 1 may still fly
-  } else {
-    __builtin_amdgcn_s_waitcnt(kWaitAll);
-  }
+  // Software pipeline over class chunks (v4): iteration c issues the MFMAs of chunk c+1 and the
+  // epilogue of chunk c in ONE basic block, so the epilogue's VALU work (max / exp2 / sums, ~250
+  // instructions a chunk) issues in the MFMA shadow instead of after it, and no VALU reads an
+  // accumulator right behind its MFMA (v3: 50 s_nop hazard pads per chunk). One barrier per chunk:
+  // at the top of iteration c every wave has finished reading the buffer of chunk c (last
+  // iteration's MFMAs), so the DMA of chunk c+2 goes there and has a whole iteration to land.
+  __builtin_amdgcn_s_waitcnt(kWaitAll);  // chunk 0 + X
   MLAPI_RAW_BARRIER()
-  for (int c0 = c_begin; c0 < c_end; c0 += CLASS_CHUNK) {
-    compute_chunk<KS, NT, MODE, OVR>(smem + buf * BUF_BYTES, xf, c0, c_end, q, col, row0, B, K,
-                                     reinterpret_cast<const float*>(smem + buf * BUF_BYTES + W_BYTES), a, st);
-    if (c0 + 2 * CLASS_CHUNK < c_end) {
-      MLAPI_RAW_BARRIER()  // every wave is done reading `buf`
-      MLAPI_DMA_CHUNK(c0 + 2 * CLASS_CHUNK, buf)
-      __builtin_amdgcn_s_waitcnt(kWaitChunk);  // chunk c+1 landed, c+2 flies
-    } else {
-      __builtin_amdgcn_s_waitcnt(kWaitAll);
+  if (c_begin + CLASS_CHUNK < c_end) MLAPI_DMA_CHUNK(c_begin + CLASS_CHUNK, 1)
+  f32x4_t acc[NT][4];
+  mfma_chunk<KS, NT>(smem, xf, c_begin, c_end, q, col, reinterpret_cast<const float*>(smem + W_BYTES), acc);
+  for (int c0 = c_begin;; c0 += CLASS_CHUNK) {
+    if (c0 + CLASS_CHUNK >= c_end) {
+      epilogue_chunk<NT, MODE, OVR>(acc, c0, c_end, q, col, row0, B, K, a, st);
+      break;
     }
-    MLAPI_RAW_BARRIER()
+    __builtin_amdgcn_s_waitcnt(kWaitAll);  // chunk c+1 landed (the only DMA in flight)
+    MLAPI_RAW_BARRIER()                     // ... for every wave; and everyone is done with chunk c
+    if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA_CHUNK(c0 + 2 * CLASS_CHUNK, buf)
+    const unsigned char* nb = smem + (buf ^ 1) * BUF_BYTES;
+    f32x4_t nxt[NT][4];
+    if constexpr (MODE == 1) {
+      mfma_chunk<KS, NT>(nb, xf, c0 + CLASS_CHUNK, c_end, q, col, reinterpret_cast<const float*>(nb + W_BYTES), nxt);
+      epilogue_chunk<NT, MODE, OVR>(acc, c0, c_end, q, col, row0, B, K, a, st);
+    } else {
+      fused_step<KS, NT, OVR>(nb, xf, c0 + CLASS_CHUNK, c_end, q, col, nxt, acc, c0, st);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[t][mt] = nxt[t][mt];
     buf ^= 1;
   }
 #undef MLAPI_RAW_BARRIER
@@ -410,6 +531,217 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
       }
     }
   }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Row-group kernel (small / medium batches, and any F): one block owns 16 * NT batch rows and
+// ALL classes. Its nw waves split the 64-class chunks round-robin; every wave streams its W
+// fragments straight from L2 into VGPRs (no LDS staging, no barrier per chunk: for a small batch
+// the tiles kernel above spends its time in DMA latency and the cross-block split merge), keeps
+// the online (max, sum, argmax) state per row in registers, and the waves merge through LDS once
+// at the end, in wave order (deterministic). The feature dimension is looped in slices of KS * 32
+// (F <= 256: one slice, X kept in registers; wider F: 256-feature slices with X reloaded per slice
+// from L2), so any F that is a multiple of 256 (or a power of two <= 256) runs in ONE launch with
+// no split-K partials and no extra merge pass. MODE: 0 predict, 1 logits, 2 row stats, 4 row state.
+constexpr int ROWS_MAX_WAVES = 8;
+
+struct RowsArgs {
+  const uint16_t* X;
+  int64_t ldx;
+  const uint16_t* W;  // [K, F] bf16, row stride F
+  const float* bias;
+  int64_t B;
+  int K;
+  int F;
+  int32_t* out_idx;
+  float* out_p;
+  float* Z;
+  float2* rowstat;
+  float4* rowstate;
+};
+
+template <int KS, int NT, int MODE, bool OVR>
+__global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
+  constexpr int ROWS = 16 * NT;
+  constexpr int SLICE = KS * 32;
+  __shared__ float4 part[ROWS_MAX_WAVES][ROWS];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = blockDim.x >> 6;
+  const int q = lane >> 4;
+  const int col = lane & 15;
+  const int64_t B = a.B;
+  const int K = a.K;
+  const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+  const int nslices = a.F / SLICE;
+  const int nchunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
+
+  bf16x8_t xf[NT][KS];
+  auto load_x = [&](int slice) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int64_t r = min(row0 + t * 16 + col, B - 1);
+      const uint16_t* xr = a.X + r * a.ldx + slice * SLICE + 8 * q;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) xf[t][ks] = *reinterpret_cast<const bf16x8_t*>(xr + ks * 32);
+    }
+  };
+  if (nslices == 1) load_x(0);
+
+  RowState st[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) st[t] = RowState{-INFINITY, 0.f, 0x7fffffff};
+
+  for (int c = wave; c < nchunks; c += nw) {
+    const int c0 = c * CLASS_CHUNK;
+    f32x4_t acc[NT][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int cb = c0 + mt * 16 + q * 4;
+      const f32x4_t b0 = {a.bias[min(cb, K - 1)], a.bias[min(cb + 1, K - 1)], a.bias[min(cb + 2, K - 1)],
+                          a.bias[min(cb + 3, K - 1)]};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t][mt] = b0;
+    }
+    for (int sl = 0; sl < nslices; ++sl) {
+      if (nslices > 1) load_x(sl);
+      bf16x8_t wf[4][KS];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int cls = min(c0 + mt * 16 + col, K - 1);  // classes past K: masked below
+        const uint16_t* wr = a.W + (int64_t)cls * a.F + sl * SLICE + 8 * q;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) wf[mt][ks] = *reinterpret_cast<const bf16x8_t*>(wr + ks * 32);
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+            acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt][ks], xf[t][ks], acc[t][mt], 0, 0, 0);
+    }
+    // epilogue: lane owns classes c0 + mt*16 + q*4 + r of batch row (t, col)
+    const bool partial = c0 + CLASS_CHUNK > K;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = acc[t][i >> 2][i & 3];
+      if (partial) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = c0 + (i >> 2) * 16 + q * 4 + (i & 3) < K ? v[i] : -INFINITY;
+      }
+      if constexpr (MODE == 1) {
+        const int64_t row = row0 + t * 16 + col;
+        if (row < B) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int cls = c0 + (i >> 2) * 16 + q * 4 + (i & 3);
+            if (cls < K) a.Z[row * K + cls] = v[i];
+          }
+        }
+      } else {
+        online_update<OVR>(v, c0, q, st[t]);
+      }
+    }
+  }
+  if constexpr (MODE != 1) {
+    // the 4 lanes of a row (q = 0..3) hold disjoint class subsets: merge them, then the waves
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      RowState S = st[t];
+      S = merge_state(S, shfl_state(S, 16), OVR);
+      S = merge_state(S, shfl_state(S, 32), OVR);
+      if (q == 0) part[wave][t * 16 + col] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < ROWS) {
+      const int r = threadIdx.x;
+      const float4 p0 = part[0][r];
+      RowState S{p0.x, p0.y, __float_as_int(p0.z)};
+      for (int w = 1; w < nw; ++w) {
+        const float4 pw = part[w][r];
+        S = merge_state(S, RowState{pw.x, pw.y, __float_as_int(pw.z)}, OVR);
+      }
+      const int64_t row = row0 + r;
+      if (row < B) {
+        if constexpr (MODE == 0) {
+          a.out_idx[row] = S.bi;
+          a.out_p[row] = OVR ? sigmoidf_(S.m) / S.s : 1.f / S.s;
+        } else if constexpr (MODE == 4) {
+          a.rowstate[row] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
+        } else {
+          a.rowstat[row] = make_float2(S.m + __logf(S.s), __int_as_float(S.bi));
+        }
+      }
+    }
+  }
+}
+
+// Which kernel serves (B, K, F): the row-group kernel only where the tiles kernel has no
+// instantiation (F > 512, the only kernel that loops F). At F <= 512 the tiles kernel with class
+// splits is faster at every B (profiles/r2_gemm/sweep.log: B <= 4096 rows 17-19 us vs tiles 7-10).
+int g_force_kernel = 0;  // benchmark hook: 0 automatic, 1 tiles, 2 row-group
+
+bool rows_supported(int F) { return F == 32 || F == 64 || F == 128 || F == 256 || (F > 256 && F % 256 == 0); }
+bool tiles_supported(int F) { return F == 32 || F == 64 || F == 128 || F == 256 || F == 512; }
+
+bool use_rows(int64_t B, int F) {
+  if (!tiles_supported(F)) return true;
+  if (g_force_kernel == 1) return false;
+  (void)B;
+  return g_force_kernel == 2 && rows_supported(F);
+}
+
+template <int MODE>
+void launch_rows(RowsArgs a, int kind, hipStream_t stream) {
+  if (!rows_supported(a.F))
+    throw std::invalid_argument("gemm_softmax: F must be 32/64/128/256 or a multiple of 256 (pad other widths)");
+  if (a.ldx % 8 != 0 || reinterpret_cast<uintptr_t>(a.X) % 16 || reinterpret_cast<uintptr_t>(a.W) % 16)
+    throw std::invalid_argument("gemm_softmax: X rows and W must be 16-byte aligned");
+  const int nchunks = (a.K + CLASS_CHUNK - 1) / CLASS_CHUNK;
+  const int nw = nchunks < ROWS_MAX_WAVES ? nchunks : ROWS_MAX_WAVES;
+  const int nt = a.B >= 16384 ? 2 : 1;
+  const dim3 grid((unsigned)((a.B + 16 * nt - 1) / (16 * nt))), block(64 * nw);
+  const bool ovr = kind == KIND_OVR;
+#define MLAPI_ROWS_LAUNCH(KSV, NTV)                                                                \
+  do {                                                                                             \
+    if (ovr)                                                                                       \
+      hipLaunchKernelGGL((softmax_rows_kernel<KSV, NTV, MODE, true>), grid, block, 0, stream, a);  \
+    else                                                                                           \
+      hipLaunchKernelGGL((softmax_rows_kernel<KSV, NTV, MODE, false>), grid, block, 0, stream, a); \
+  } while (0)
+#define MLAPI_ROWS_NT(KSV)     \
+  if (nt == 2)                 \
+    MLAPI_ROWS_LAUNCH(KSV, 2); \
+  else                         \
+    MLAPI_ROWS_LAUNCH(KSV, 1);
+  if (a.F == 32) {
+    MLAPI_ROWS_NT(1)
+  } else if (a.F == 64) {
+    MLAPI_ROWS_NT(2)
+  } else if (a.F == 128) {
+    MLAPI_ROWS_NT(4)
+  } else {
+    MLAPI_ROWS_NT(8)
+  }
+#undef MLAPI_ROWS_NT
+#undef MLAPI_ROWS_LAUNCH
+  MLAPI_HIP_CHECK(hipGetLastError());
+}
+
+RowsArgs rows_args(const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K) {
+  RowsArgs a{};
+  a.X = static_cast<const uint16_t*>(X);
+  a.ldx = ldx;
+  a.W = static_cast<const uint16_t*>(W);
+  a.bias = b;
+  a.B = B;
+  a.K = K;
+  a.F = F;
+  return a;
 }
 
 struct Plan {
@@ -506,9 +838,10 @@ GemmArgs base_args(const void* X, const void* W, int64_t B, int F, int K, int ki
 
 }  // namespace
 
-void gemm_softmax_force_plan(int nt, int splits) {
+void gemm_softmax_force_plan(int nt, int splits, int kernel) {
   g_force_nt = nt;
   g_force_splits = splits;
+  g_force_kernel = kernel;
 }
 
 size_t softmax_rowstats_workspace(int64_t B, int K, int F) {
@@ -535,7 +868,7 @@ void launch_softmax_rowstats(const void* X_aug, int64_t ldx, const void* W, cons
 }
 
 size_t gemm_softmax_workspace(int64_t B, int K, int F) {
-  (void)F;
+  if (use_rows(B, F)) return 0;
   const Plan p = make_plan(B, K, F, false);
   return p.splits > 1 ? (size_t)COUNTER_BYTES + (size_t)p.splits * (size_t)B * sizeof(float4) : 0;
 }
@@ -545,6 +878,13 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
   if (B <= 0) return;
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("gemm_softmax: multiclass kinds only (binary models use gemv_binary)");
+  if (use_rows(B, F)) {
+    RowsArgs ra = rows_args(X, F, W, b, B, F, K);
+    ra.out_idx = out_idx;
+    ra.out_p = out_p;
+    launch_rows<0>(ra, kind, stream);
+    return;
+  }
   const Plan plan = make_plan(B, K, F, false);
   if (plan.splits > 1 && ws_bytes < gemm_softmax_workspace(B, K, F))
     throw std::invalid_argument("gemm_softmax: workspace too small (must be zero-initialised once)");
@@ -564,6 +904,12 @@ void launch_gemm_rowstate(const void* X, const void* W, const float* b, int64_t 
   if (B <= 0) return;
   if (K < 1 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("gemm_rowstate: multiclass kinds only");
+  if (use_rows(B, F)) {
+    RowsArgs ra = rows_args(X, F, W, b, B, F, K);
+    ra.rowstate = static_cast<float4*>(out_state);
+    launch_rows<4>(ra, kind, stream);
+    return;
+  }
   const Plan plan = make_plan(B, K, F, false);
   if (plan.splits > 1 && ws_bytes < gemm_softmax_workspace(B, K, F))
     throw std::invalid_argument("gemm_rowstate: workspace too small (must be zero-initialised once)");
@@ -580,6 +926,12 @@ void launch_gemm_rowstate(const void* X, const void* W, const float* b, int64_t 
 void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B, int F, int K, float* Z,
                         hipStream_t stream) {
   if (B <= 0) return;
+  if (use_rows(B, F)) {
+    RowsArgs ra = rows_args(X, F, W, b, B, F, K);
+    ra.Z = Z;
+    launch_rows<1>(ra, KIND_MULTINOMIAL, stream);
+    return;
+  }
   Plan plan = make_plan(B, K, F, false);
   plan.splits = (K + plan.classes_per_split - 1) / plan.classes_per_split;  // no merge needed for logits
   GemmArgs args = base_args(X, W, B, F, K, KIND_MULTINOMIAL);

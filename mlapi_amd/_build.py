@@ -39,6 +39,14 @@ SOURCES = [
 ]
 
 
+# Per-source extra flags. gemm_softmax.hip: MFMA results in VGPRs (on gfx950 the register file is
+# unified; hipcc's default put the accumulators in AGPRs and paid a v_accvgpr_read per element in
+# the softmax epilogue - 96 extra moves per class chunk).
+FILE_FLAGS = {
+    "kernels/gemm_softmax.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+}
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and Path(cand).exists():
@@ -74,7 +82,7 @@ def _compile(src: str, force: bool, hmt: float) -> Path:
     obj = BUILD / (src.replace("/", "__") + ".o")
     if not force and obj.exists() and obj.stat().st_mtime >= max(s.stat().st_mtime, hmt):
         return obj
-    cmd = [hipcc()] + _flags() + _includes()
+    cmd = [hipcc()] + _flags() + FILE_FLAGS.get(src, []) + _includes()
     if s.suffix == ".cpp":
         cmd += ["-x", "hip"] if src == "bindings.cpp" else []
     cmd += ["-c", str(s), "-o", str(obj)]

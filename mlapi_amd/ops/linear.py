@@ -8,7 +8,8 @@ Dispatch for ``predict`` (the reference's ``predict`` + ``predict_proba().max()`
 `main.py:21-22`):
   * f64 / f32 inputs with small F, K  -> ``linear_small`` (fused, one row per lane);
   * binary (K == 1) bf16 / f32        -> ``gemv_binary`` (HBM-streaming GEMV + sigmoid);
-  * multiclass bf16                   -> ``gemm_softmax`` (MFMA + online softmax/argmax).
+  * multiclass bf16                   -> ``gemm_softmax`` (MFMA + online softmax/argmax; any F:
+                                         the row-group kernel loops wide F in 256-feature slices).
 """
 from __future__ import annotations
 
@@ -51,28 +52,36 @@ def linear_small(X: torch.Tensor, W: torch.Tensor, b: torch.Tensor, kind: int) -
     return idx, p
 
 
-def gemv_binary(X: torch.Tensor, w: torch.Tensor, bias: float, kind: int = Kind.BINARY):
-    """Binary LR over a large batch: (int32 z>0, f32 sigmoid(|z|)). X: [B, F] bf16/f32."""
+def gemv_binary(X: torch.Tensor, w: torch.Tensor, bias: float, kind: int = Kind.BINARY, out=None):
+    """Binary LR over a large batch: (int32 z>0, f32 sigmoid(|z|)). X: [B, F] bf16/f32.
+    ``out=(idx, p)`` writes into preallocated outputs (graph-capture safe)."""
     _check(X, w)
     if X.dtype not in (torch.bfloat16, torch.float32) or w.dtype != X.dtype:
         raise TypeError("gemv_binary: X and w must share dtype bf16 or f32")
     B, F = X.shape
     if w.numel() != F:
         raise ValueError("gemv_binary: w must have F entries")
-    idx = torch.empty(B, dtype=torch.int32, device=X.device)
-    p = torch.empty(B, dtype=torch.float32, device=X.device)
+    if out is None:
+        out = (torch.empty(B, dtype=torch.int32, device=X.device), torch.empty(B, dtype=torch.float32, device=X.device))
+    idx, p = out
     C().gemv_binary(_DT[X.dtype], X.data_ptr(), w.data_ptr(), float(bias), B, F, int(kind), idx.data_ptr(),
                     p.data_ptr(), _stream())
     return idx, p
 
 
-_GEMM_F = (32, 64, 128, 256, 512)
+def gemm_width(F: int) -> int:
+    """Feature width the multiclass kernels run at: a power of two >= 32 up to 256, else a multiple
+    of 256 (wider models loop F in 256-feature slices inside one launch; zero columns add nothing)."""
+    F = int(F)
+    if F <= 256:
+        return max(32, 1 << (F - 1).bit_length())
+    return (F + 255) // 256 * 256
 
 
 def _pad_cols(t: torch.Tensor) -> torch.Tensor:
     F = t.shape[1]
-    Fp = next(f for f in _GEMM_F if f >= F)
-    return torch.nn.functional.pad(t, (0, Fp - F)).contiguous()
+    Fp = gemm_width(F)
+    return t.contiguous() if Fp == F else torch.nn.functional.pad(t, (0, Fp - F)).contiguous()
 
 
 class GemmSoftmax:
@@ -91,9 +100,9 @@ class GemmSoftmax:
             raise TypeError("gemm_softmax: X, W bf16 and b f32")
         B, F = X.shape
         K = W.shape[0]
-        if F > 512 or W.shape[1] != F or b.numel() != K:
-            raise ValueError("gemm_softmax: need F <= 512 and matching W/b")
-        if F not in _GEMM_F:  # kernels are instantiated for exact widths: zero-pad the rest
+        if W.shape[1] != F or b.numel() != K:
+            raise ValueError("gemm_softmax: W must be [K, F] and b [K]")
+        if gemm_width(F) != F:  # kernels are instantiated for exact widths: zero-pad the rest
             X, W = _pad_cols(X), _pad_cols(W)
             F = X.shape[1]
         need = C().gemm_softmax_workspace(B, K, F)
@@ -113,7 +122,7 @@ def gemm_softmax(X, W, b, kind: int = Kind.MULTINOMIAL):
 
 def gemm_logits(X, W, b) -> torch.Tensor:
     _check(X, W, b)
-    if X.shape[1] not in _GEMM_F:
+    if gemm_width(X.shape[1]) != X.shape[1]:
         X, W = _pad_cols(X), _pad_cols(W)
     B, F = X.shape
     K = W.shape[0]

@@ -121,8 +121,6 @@ class ClassShardedLinear:
         if _on_gpu(self.device):
             from mlapi_amd.ops.linear import _pad_cols
 
-            if self.F > 512:
-                raise ValueError("class sharding on the GPU: F <= 512 (shard the features instead)")
             self.W = _pad_cols(W.to(self.device).to(torch.bfloat16))  # exact-width MFMA instantiations
             self.b = b.to(self.device).contiguous()
             self._ws = None

@@ -82,10 +82,24 @@ def test_gemv_binary_large_stream():
     torch.testing.assert_close(p, torch.sigmoid(z.abs()), rtol=1e-4, atol=1e-4)
 
 
+@pytest.fixture(params=[0, 1, 2], ids=["auto", "tiles", "rows"])
+def gemm_kernel(request):
+    """Run a multiclass test under the automatic plan and with each kernel forced (tiles: the
+    LDS-staged, chunk-pipelined kernel; rows: the row-group kernel)."""
+    from mlapi_amd._native import C
+
+    C().gemm_softmax_force_plan(0, 0, request.param)
+    yield request.param
+    C().gemm_softmax_force_plan(0, 0, 0)
+
+
 @pytest.mark.parametrize("B,F,K", [(1024, 256, 1000), (1, 256, 1000), (130, 64, 10), (2048, 128, 37),
-                                   (4096, 256, 3), (100, 512, 200), (37, 32, 65)])
+                                   (4096, 256, 3), (100, 512, 200), (37, 32, 65), (20000, 256, 130),
+                                   (300, 1024, 100), (65, 4096, 1000), (5, 700, 12)])
 @pytest.mark.parametrize("kind", [Kind.MULTINOMIAL, Kind.OVR])
-def test_gemm_softmax(B, F, K, kind):
+def test_gemm_softmax(B, F, K, kind, gemm_kernel):
+    """Both multiclass kernels vs the fp64 oracle on bf16 operands; F > 512 (row-group kernel, F
+    looped in 256-feature slices inside one launch) and F not a kernel width (zero-padded)."""
     X = _rand((B, F), torch.bfloat16, 9)
     W = _rand((K, F), torch.bfloat16, 10, scale=1 / np.sqrt(F))
     b = _rand((K,), torch.float32, 11, scale=0.1)
@@ -97,6 +111,25 @@ def test_gemm_softmax(B, F, K, kind):
     torch.cuda.synchronize()
     assert torch.equal(idx[clear].cpu(), ridx[clear].cpu())
     torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=2e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("F", [1024, 4096])
+def test_predict_wide_multiclass_matches_fp64_oracle(F):
+    """ops.predict on F = 1024 / 4096 multiclass models against the float64
+    oracle of the same bf16-rounded operands."""
+    from mlapi_amd.models.linear import LinearModel
+    from mlapi_amd.serve.loadgen import bf16_oracle
+
+    m = LinearModel.random(F, 300, seed=F, kind=Kind.MULTINOMIAL)
+    Xn = np.random.default_rng(F).standard_normal((777, F))
+    idx, p = ops.predict(torch.tensor(Xn, device=DEV, dtype=torch.bfloat16), torch.tensor(m.W, device=DEV),
+                         torch.tensor(m.b, device=DEV), Kind.MULTINOMIAL)
+    om, Xr = bf16_oracle(m, Xn)
+    ridx, rp = om.predict_max(Xr)
+    zs = np.sort(om.decision_function(Xr), axis=1)
+    clear = zs[:, -1] - zs[:, -2] > 1e-3
+    np.testing.assert_array_equal(idx.cpu().numpy()[clear], ridx[clear])
+    np.testing.assert_allclose(p.cpu().numpy(), rp, rtol=2e-4, atol=2e-5)
 
 
 def test_gemm_softmax_large_batch_and_rearm():
@@ -118,18 +151,25 @@ def test_gemm_softmax_large_batch_and_rearm():
             torch.testing.assert_close(p.double(), rp, rtol=2e-4, atol=2e-5)
 
 
-def test_gemm_logits_asymmetric():
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_gemm_logits_asymmetric(kernel):
     """A = I-style check with an asymmetric operand: catches a transposed C write (guide S3)."""
     B, F, K = 64, 64, 48
     X = torch.zeros(B, F, device=DEV, dtype=torch.bfloat16)
     X[torch.arange(B), torch.arange(B) % F] = 1
     W = (torch.arange(K * F, device=DEV, dtype=torch.float32).reshape(K, F) % 13 - 6).to(torch.bfloat16)
     b = torch.arange(K, device=DEV, dtype=torch.float32) * 0.5
-    Z = ops.gemm_logits(X, W, b)
+    from mlapi_amd._native import C
+
+    C().gemm_softmax_force_plan(0, 0, kernel)
+    try:
+        Z = ops.gemm_logits(X, W, b)
+    finally:
+        C().gemm_softmax_force_plan(0, 0, 0)
     torch.testing.assert_close(Z, ref.logits_ref(X, W, b), rtol=0, atol=0)
 
 
-def test_gemm_ties_first_max():
+def test_gemm_ties_first_max(gemm_kernel):
     B, F, K = 256, 32, 130
     X = torch.ones(B, F, device=DEV, dtype=torch.bfloat16)
     W = torch.zeros(K, F, device=DEV, dtype=torch.bfloat16)
