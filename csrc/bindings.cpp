@@ -154,6 +154,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_softmax_workspace", &gemm_softmax_workspace);
   m.def("gemm_softmax_force_plan", &gemm_softmax_force_plan, py::arg("nt") = 0, py::arg("splits") = 0,
         py::arg("kernel") = 0);
+  m.def("gemm_softmax_set_stamps", [](uintptr_t p) { gemm_softmax_set_stamps(reinterpret_cast<void*>(p)); });
   m.def(
       "gemm_softmax",
       [](uintptr_t X, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind, uintptr_t out_idx,

@@ -117,7 +117,18 @@ struct GemmArgs {
   float* Z;                // MODE 1
   float2* rowstat;         // MODE 2 output: {lse, argmax bits}
   float4* rowstate;        // MODE 4 output: {max, sum, argmax bits, 0} (class-sharded TP)
+  unsigned long long* stamps;  // profiling (tools/gemm_phase_probe.py): 4 s_memtime stamps per wave
 };
+
+// Phase stamps of one wave (profiling builds of a launch only: a.stamps is null otherwise):
+// 0 entry, 1 first W chunk + X landed, 2 class loop done, 3 row state reduced.
+__device__ __forceinline__ void phase_stamp(const GemmArgs& a, int waves_per_block, int wave, int lane, int j) {
+  if (a.stamps != nullptr && lane == 0) {
+    const unsigned long long gid =
+        ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) * (unsigned)waves_per_block + (unsigned)wave;
+    a.stamps[gid * 4 + j] = __builtin_amdgcn_s_memtime();
+  }
+}
 
 template <typename F, int... I>
 __device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
@@ -202,6 +213,94 @@ __device__ __forceinline__ void online_update(const float (&v)[16], int c0, int 
   online_finish<OVR>(T, S);
 }
 
+// Lane state of the tiles kernel (v5): running max / sum and, instead of a running argmax, the 16
+// logits of the chunk that last raised the max plus that chunk's first class. The first index
+// holding the max is resolved ONCE, after the class loop (tile_result). Per chunk that costs 16
+// bit-blends (one v_bitop3 each, no VCC) where v4's in-loop argmax paid 16 compare/select pairs,
+// each pair separated by a VCC hazard pad (hipcc rebuilt the min tree as a serial chain).
+struct TileState {
+  float m, s;
+  int bc;         // first class of the chunk held in bv (0x7fffffff: none yet)
+  unsigned bv[16];  // that chunk's logits (float bits), element i = class bc + (i>>2)*16 + q*4 + (i&3)
+};
+
+__device__ __forceinline__ float vmax(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+
+struct TileTmp {
+  float m_new, part;
+};
+
+__device__ __forceinline__ void tile_init(TileState& S) {
+  S.m = -INFINITY;
+  S.s = 0.f;
+  S.bc = 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) S.bv[i] = __float_as_uint(-INFINITY);
+}
+
+template <bool OVR>
+__device__ __forceinline__ void tile_stage(int stage, const float (&v)[16], int c0, TileState& S, TileTmp& T) {
+  if (stage == 0) {  // chunk max, new running max, keep this chunk's logits if it raised the max
+    // IEEE-2019 maximum (NaN-propagating) maps to v_maximum3_f32 with no operand quieting; fmaxf
+    // (maxnum) made hipcc canonicalize every MFMA result first (one extra v_max per element).
+    float cm = vmax(v[0], v[1]);
+#pragma unroll
+    for (int i = 2; i < 16; ++i) cm = vmax(cm, v[i]);
+    // strict: an earlier chunk keeps a tie (first max wins). The blend goes through an opaque
+    // mask: as selects, hipcc sank them under an exec branch splitting the pipelined block.
+    unsigned mask = -(unsigned)(cm > S.m);
+    asm("" : "+v"(mask));
+    T.m_new = vmax(cm, S.m);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) S.bv[i] = S.bv[i] ^ ((S.bv[i] ^ __float_as_uint(v[i])) & mask);
+    S.bc = (int)((unsigned)S.bc ^ (((unsigned)S.bc ^ (unsigned)c0) & mask));
+  } else {  // stage 1 / 2: exp (or sigmoid) terms of elements 0-7 / 8-15
+    const int i0 = stage == 1 ? 0 : 8;
+    float e[8];
+    if constexpr (OVR) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e[i] = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-v[i0 + i] * LOG2E_F));
+    } else {
+      const float m2 = T.m_new * LOG2E_F;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e[i] = __builtin_amdgcn_exp2f(fmaf(v[i0 + i], LOG2E_F, -m2));
+    }
+    const float sum = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
+    T.part = stage == 1 ? sum : T.part + sum;
+  }
+}
+
+template <bool OVR>
+__device__ __forceinline__ void tile_finish(const TileTmp& T, TileState& S) {
+  if constexpr (OVR) {
+    S.s += T.part;
+  } else {
+    // rescale the running sum to the new max (S.m = -inf: exp2(-inf) = 0); unconditional, a
+    // select here became a branch around the exp2
+    const float scale = __builtin_amdgcn_exp2f(fmaf(S.m, LOG2E_F, -T.m_new * LOG2E_F));
+    S.s = fmaf(S.s, scale, T.part);
+  }
+  S.m = T.m_new;
+}
+
+template <bool OVR>
+__device__ __forceinline__ void tile_update(const float (&v)[16], int c0, TileState& S) {
+  TileTmp T;
+  tile_stage<OVR>(0, v, c0, S, T);
+  tile_stage<OVR>(1, v, c0, S, T);
+  tile_stage<OVR>(2, v, c0, S, T);
+  tile_finish<OVR>(T, S);
+}
+
+// (max, sum, first argmax) of a lane: the first element of the kept chunk equal to the max
+__device__ __forceinline__ RowState tile_result(const TileState& S, int q) {
+  int ci = 16;
+#pragma unroll
+  for (int i = 15; i >= 0; --i) ci = __uint_as_float(S.bv[i]) == S.m ? i : ci;
+  const int bi = (S.m == -INFINITY || ci == 16) ? 0x7fffffff : S.bc + (ci >> 2) * 16 + q * 4 + (ci & 3);
+  return RowState{S.m, S.s, bi};
+}
+
 // Logits of one 64-class chunk against the LDS image `wb`: MFMAs into bias-initialised
 // accumulators (the bias was DMA'd into LDS next to the W chunk, so no global load sits between
 // the staging pipeline's counted waits). Classes >= c_end (only the very last chunk of the
@@ -244,7 +343,7 @@ __device__ __forceinline__ void mfma_chunk(const unsigned char* wb, const bf16x8
 template <int KS, int NT, bool OVR>
 __device__ __forceinline__ void fused_step(const unsigned char* nb, const bf16x8_t (&xf)[NT][KS], int cn, int c_end,
                                            int q, int col, f32x4_t (&nxt)[NT][4], const f32x4_t (&acc)[NT][4], int c0,
-                                           RowState (&st)[NT]) {
+                                           TileState (&st)[NT]) {
   const float* bias_lds = reinterpret_cast<const float*>(nb + CLASS_CHUNK * lds_row_stride<KS>());
   f32x4_t b4[4];
 #pragma unroll
@@ -264,7 +363,7 @@ __device__ __forceinline__ void fused_step(const unsigned char* nb, const bf16x8
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[t][i] = acc[t][i >> 2][i & 3];
-  OnlineTmp T[NT];
+  TileTmp T[NT];
   constexpr int NSTAGE = 3 * NT + NT;  // 3 stages + finish per row tile
   static_for<KS>([&](auto kc) {
     constexpr int ks = decltype(kc)::value;
@@ -283,9 +382,9 @@ __device__ __forceinline__ void fused_step(const unsigned char* nb, const bf16x8
       if constexpr ((j * KS) / NSTAGE == ks) {
         constexpr int t = j / 4, stg = j % 4;
         if constexpr (stg < 3)
-          online_stage<OVR>(stg, v[t], c0, q, st[t], T[t]);
+          tile_stage<OVR>(stg, v[t], c0, st[t], T[t]);
         else
-          online_finish<OVR>(T[t], st[t]);
+          tile_finish<OVR>(T[t], st[t]);
       }
     });
     if constexpr (KS >= 4) __builtin_amdgcn_sched_barrier(0x100);  // only LDS reads may cross
@@ -298,7 +397,7 @@ __device__ __forceinline__ void fused_step(const unsigned char* nb, const bf16x8
 template <int NT, int MODE, bool OVR>
 __device__ __forceinline__ void epilogue_chunk(const f32x4_t (&acc)[NT][4], int c0, int c_end, int q, int col,
                                                int64_t row0, int64_t B, int K, const GemmArgs& a,
-                                               RowState (&st)[NT]) {
+                                               TileState (&st)[NT]) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     float v[16];
@@ -314,7 +413,7 @@ __device__ __forceinline__ void epilogue_chunk(const f32x4_t (&acc)[NT][4], int 
         }
       }
     } else {  // MODE 0 / 2 / 4: online (max, sum, first argmax)
-      online_update<OVR>(v, c0, q, st[t]);
+      tile_update<OVR>(v, c0, st[t]);
     }
   }
 }
@@ -322,8 +421,26 @@ __device__ __forceinline__ void epilogue_chunk(const f32x4_t (&acc)[NT][4], int 
 // KS = F/32 (exact), NT = 16-row N-tiles per wave, MODE: 0 = fused predict epilogue,
 // 1 = write logits, 2 = training row stats (see header), 4 = raw online softmax state per row
 // (class-sharded TP, merged across ranks by shard.hip).
+// Two waves per SIMD (2 blocks of 4 waves per CU, LDS 2 x 66 KB): the register budget is 256.
+// v5's kept-chunk logits (16 VGPRs per row tile) put NT = 2 at 261 without the cap; with it
+// 4 VGPRs spill around (not inside) the class loop. F = 512 runs one block per CU anyway (its
+// double-buffered W chunks take 2 x 66 KB of LDS), so it keeps the whole register file.
+template <int KS, int MODE>
+constexpr int tiles_waves_per_eu() {
+  return KS == 16 ? 1 : 2;
+}
+// Waves per block. The large-batch plan (NT = 2) runs 8 waves = 256 rows per block, one block
+// per CU: every block streams ALL of W through LDS, so W's L2 -> CU traffic is (B / rows per
+// block) x |W| (v4, 128-row blocks: 1 GB at B = 262144, ~12 B/clk/CU for the whole kernel).
+template <int KS, int NT>
+constexpr int tiles_block_waves() {
+  return (NT == 2 && KS >= 2 && KS <= 8) ? 8 : 4;
+}
+
 template <int KS, int NT, int MODE, bool OVR>
-__global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
+__global__ __launch_bounds__((64 * tiles_block_waves<KS, NT>())) __attribute__((amdgpu_waves_per_eu(tiles_waves_per_eu<KS, MODE>(),
+                                                                     tiles_waves_per_eu<KS, MODE>()))) void
+gemm_softmax_kernel(GemmArgs a) {
   const uint16_t* __restrict__ X = a.X;
   const uint16_t* __restrict__ W = a.W;
   const float* __restrict__ bias = a.bias;
@@ -335,14 +452,19 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   // No runtime guard may sit on a load: hipcc then branches around each load and waits vmcnt(0)
   // per element, serializing the W stream (seen in the v2 ISA; cdna_hip_programming.md S5 trap c).
   constexpr int ROWS_PER_WAVE = 16 * NT;
-  constexpr int ROWS_PER_BLOCK = 4 * ROWS_PER_WAVE;
+  constexpr int WV = tiles_block_waves<KS, NT>();
+  constexpr int NTHR = 64 * WV;
+  constexpr int ROWS_PER_BLOCK = WV * ROWS_PER_WAVE;
   constexpr int F_ = KS * 32;
   constexpr int NCH = F_ / 8;                          // 16-byte chunks per W row
   constexpr int W_BYTES = CLASS_CHUNK * lds_row_stride<KS>();
   constexpr int BUF_BYTES = W_BYTES + CLASS_CHUNK * 4;  // [W chunk][64 f32 bias]
-  constexpr int PIECES = CLASS_CHUNK * NCH / 256;      // 16-byte pieces per thread per chunk (== KS)
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF_BYTES + 16];
-  int* const flag = reinterpret_cast<int*>(smem + 2 * BUF_BYTES);
+  constexpr int PIECES = CLASS_CHUNK * NCH / NTHR;     // 16-byte pieces per thread per chunk
+  // W chunk buffers: 8-wave blocks (one per CU) have the LDS for a third, which gives every DMA
+  // two iterations to land instead of one; logits mode (stores in the loop) keeps two.
+  constexpr int NBUF = (WV == 8 && MODE != 1) ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * BUF_BYTES + 16];
+  int* const flag = reinterpret_cast<int*>(smem + NBUF * BUF_BYTES);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -352,6 +474,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   constexpr bool ovr = OVR;
   (void)kind;
   const int64_t row0 = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wave * ROWS_PER_WAVE;
+  phase_stamp(a, WV, wave, lane, 0);
   const int c_begin = blockIdx.y * classes_per_split;
   const int c_end = min(K, c_begin + classes_per_split);
   const int c_last = c_begin + ((c_end - 1 - c_begin) / CLASS_CHUNK) * CLASS_CHUNK;  // last chunk start
@@ -363,7 +486,7 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   // W staging: chunk c + 1 is DMA'd into the idle buffer while chunk c computes (no staging
   // VGPRs, no ds_write pass); the barrier's vmcnt(0) retires it. On the last chunk the (valid)
   // last chunk address is re-loaded instead of branching around the loads.
-  // Lane-linear destination: 16-B position P = i*256 + wave*64 + lane holds row P / NCH, in-row
+  // Lane-linear destination: 16-B position P = i*NTHR + wave*64 + lane holds row P / NCH, in-row
   // position P % NCH, i.e. source chunk lds_pos(row, P % NCH).
   // buffer_load ... lds through range-checked descriptors: the per-thread source offsets are
   // chunk-invariant (hoisted out of the loop by the compiler; a local offset array here made
@@ -373,17 +496,19 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, K * F_ * 2, 0x00020000);
   const auto brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)bias, 0, K * 4, 0x00020000);
 #define MLAPI_DMA_CHUNK(C0, BUF)                                                                          \
+  {                                                                                                        \
   _Pragma("unroll") for (int i = 0; i < PIECES; ++i)                                                       \
     __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                              \
-        wrsrc, (lds_void_t*)(smem + (BUF) * BUF_BYTES + (i * 256 + wave * 64) * 16), 16, (uint32_t)((((tid + i * 256) / NCH) * F_ + lds_pos<KS>((tid + i * 256) / NCH, (tid + i * 256) % NCH) * 8) * 2),         \
+        wrsrc, (lds_void_t*)(smem + (BUF) * BUF_BYTES + (i * NTHR + wave * 64) * 16), 16, (uint32_t)((((tid + i * NTHR) / NCH) * F_ + lds_pos<KS>((tid + i * NTHR) / NCH, (tid + i * NTHR) % NCH) * 8) * 2),         \
         (C0) * F_ * 2, 0, 0);                                                                              \
   /* bias: 64 floats per chunk, every wave DMAs the same 256 B (one more VM op per wave: uniform count) */ \
   __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void_t*)(smem + (BUF) * BUF_BYTES + W_BYTES), 4,   \
-                                           (uint32_t)lane * 4, (C0) * 4, 0, 0);
+                                           (uint32_t)lane * 4, (C0) * 4, 0, 0);                           \
+  }
 
-  RowState st[NT];
+  TileState ts[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) st[t] = RowState{-INFINITY, 0.f, 0x7fffffff};
+  for (int t = 0; t < NT; ++t) tile_init(ts[t]);
 
   // Raw s_barrier, not __syncthreads(): the latter's fence waits vmcnt(0) and would drain the
   // in-flight DMA (cdna_hip_programming.md "Pipelining across barriers"); the empty asm statements
@@ -392,7 +517,6 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   asm volatile("" ::: "memory");     \
   __builtin_amdgcn_s_barrier();      \
   asm volatile("" ::: "memory");
-  int buf = 0;
   MLAPI_DMA_CHUNK(c_begin, 0)
   // X fragments for the whole feature range, straight to registers, in flight with chunk 0
 #pragma unroll
@@ -407,49 +531,69 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   // (the builtin form of s_waitcnt is visible to the compiler's wait insertion; encoding:
   // vmcnt[3:0,15:14], expcnt[6:4], lgkmcnt[11:8] with the other two counters left at "no wait")
   constexpr int kWaitAll = (7 << 4) | (15 << 8);
+  constexpr int kWaitChunk = kWaitAll | ((PIECES + 1) & 15) | (((PIECES + 1) >> 4) << 14);  // one chunk may fly
   // Software pipeline over class chunks (v4): iteration c issues the MFMAs of chunk c+1 and the
   // epilogue of chunk c in ONE basic block, so the epilogue's VALU work (max / exp2 / sums, ~250
   // instructions a chunk) issues in the MFMA shadow instead of after it, and no VALU reads an
   // accumulator right behind its MFMA (v3: 50 s_nop hazard pads per chunk). One barrier per chunk:
   // at the top of iteration c every wave has finished reading the buffer of chunk c (last
   // iteration's MFMAs), so the DMA of chunk c+2 goes there and has a whole iteration to land.
-  __builtin_amdgcn_s_waitcnt(kWaitAll);  // chunk 0 + X
+  if constexpr (NBUF == 3) {
+    if (c_begin + CLASS_CHUNK < c_end) {  // chunk 1 flies on while chunk 0 computes
+      MLAPI_DMA_CHUNK(c_begin + CLASS_CHUNK, 1)
+      __builtin_amdgcn_s_waitcnt(kWaitChunk);  // chunk 0 + X
+    } else {
+      __builtin_amdgcn_s_waitcnt(kWaitAll);
+    }
+  } else {
+    __builtin_amdgcn_s_waitcnt(kWaitAll);  // chunk 0 + X
+  }
   MLAPI_RAW_BARRIER()
-  if (c_begin + CLASS_CHUNK < c_end) MLAPI_DMA_CHUNK(c_begin + CLASS_CHUNK, 1)
+  phase_stamp(a, WV, wave, lane, 1);
+  if (c_begin + (NBUF - 1) * CLASS_CHUNK < c_end) MLAPI_DMA_CHUNK(c_begin + (NBUF - 1) * CLASS_CHUNK, NBUF - 1)
   f32x4_t acc[NT][4];
   mfma_chunk<KS, NT>(smem, xf, c_begin, c_end, q, col, reinterpret_cast<const float*>(smem + W_BYTES), acc);
+  int buf = 0;  // buffer of chunk c0
   for (int c0 = c_begin;; c0 += CLASS_CHUNK) {
     if (c0 + CLASS_CHUNK >= c_end) {
-      epilogue_chunk<NT, MODE, OVR>(acc, c0, c_end, q, col, row0, B, K, a, st);
+      epilogue_chunk<NT, MODE, OVR>(acc, c0, c_end, q, col, row0, B, K, a, ts);
       break;
     }
-    __builtin_amdgcn_s_waitcnt(kWaitAll);  // chunk c+1 landed (the only DMA in flight)
-    MLAPI_RAW_BARRIER()                     // ... for every wave; and everyone is done with chunk c
-    if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA_CHUNK(c0 + 2 * CLASS_CHUNK, buf)
-    const unsigned char* nb = smem + (buf ^ 1) * BUF_BYTES;
+    // chunk c+1 landed: with 3 buffers chunk c+2 (if issued) may stay in flight
+    if (NBUF == 3 && c0 + 2 * CLASS_CHUNK < c_end)
+      __builtin_amdgcn_s_waitcnt(kWaitChunk);
+    else
+      __builtin_amdgcn_s_waitcnt(kWaitAll);
+    MLAPI_RAW_BARRIER()  // ... for every wave; and everyone is done with chunk c's buffer
+    if (c0 + NBUF * CLASS_CHUNK < c_end) MLAPI_DMA_CHUNK(c0 + NBUF * CLASS_CHUNK, buf)
+    const int nbuf = buf + 1 == NBUF ? 0 : buf + 1;
+    const unsigned char* nb = smem + nbuf * BUF_BYTES;
     f32x4_t nxt[NT][4];
     if constexpr (MODE == 1) {
       mfma_chunk<KS, NT>(nb, xf, c0 + CLASS_CHUNK, c_end, q, col, reinterpret_cast<const float*>(nb + W_BYTES), nxt);
-      epilogue_chunk<NT, MODE, OVR>(acc, c0, c_end, q, col, row0, B, K, a, st);
+      epilogue_chunk<NT, MODE, OVR>(acc, c0, c_end, q, col, row0, B, K, a, ts);
     } else {
-      fused_step<KS, NT, OVR>(nb, xf, c0 + CLASS_CHUNK, c_end, q, col, nxt, acc, c0, st);
+      fused_step<KS, NT, OVR>(nb, xf, c0 + CLASS_CHUNK, c_end, q, col, nxt, acc, c0, ts);
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) acc[t][mt] = nxt[t][mt];
-    buf ^= 1;
+    buf = nbuf;
   }
 #undef MLAPI_RAW_BARRIER
 #undef MLAPI_DMA_CHUNK
+  phase_stamp(a, WV, wave, lane, 2);
   if constexpr (MODE == 0 || MODE == 2 || MODE == 4) {
+    RowState st[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      RowState S = st[t];
+      RowState S = tile_result(ts[t], q);
       S = merge_state(S, shfl_state(S, 16), ovr);
       S = merge_state(S, shfl_state(S, 32), ovr);
       st[t] = S;
     }
+    phase_stamp(a, WV, wave, lane, 3);
     if (gridDim.y == 1) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -533,6 +677,336 @@ __global__ __launch_bounds__(256) void gemm_softmax_kernel(GemmArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Large-batch tiles kernel (v6): v_mfma_f32_32x32x16_bf16. One 32-row N tile per wave; a 64-class
+// chunk is two 32-class M tiles x F/16 k-steps = 2F/16 MFMAs of 32 cycles (the 16x16x32 NT=2
+// kernel issues twice as many of half the length for the same work). Each 32-cycle MFMA gap
+// hides ~5 VALU fillers where a 16-cycle gap hides ~2 (MI355X_MICROARCH.md constants table), so
+// the softmax epilogue of the previous chunk fits the MFMA shadow; a lane's 16 accumulators of a
+// tile all belong to ONE batch row (col = lane & 31; class 8*(i>>2) + 4*(lane>>5) + (i&3)), so the
+// row state is one TileState per lane (v5's NT = 2 kept two) and the 2 lanes of a row merge with
+// one shuffle. Same LDS image, DMA and split merge as the 16x16 kernel; F in {64, 128, 256}.
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+__device__ __forceinline__ RowState tile_result32(const TileState& S, int h) {
+  int ci = 16;
+#pragma unroll
+  for (int i = 15; i >= 0; --i) ci = __uint_as_float(S.bv[i]) == S.m ? i : ci;
+  const int bi = (S.m == -INFINITY || ci == 16) ? 0x7fffffff : S.bc + (ci >> 2) * 8 + h * 4 + (ci & 3);
+  return RowState{S.m, S.s, bi};
+}
+
+// Finer epilogue stages for the 32x32 kernel (7 per tile, ~10-16 VALU each) so the scheduler can
+// spread a tile's update across the MFMA gaps of many k-steps:
+//   0: chunk max + new running max + take mask   1/2: keep-chunk blends of elements 0-7 / 8-15
+//   3..6: exp (sigmoid) terms of elements 4(s-3)..+3; stage 6 also rescales the sum and commits m
+struct TileTmp7 {
+  float m_new, m2, part;
+  unsigned mask;
+};
+
+template <bool OVR>
+__device__ __forceinline__ void tile_stage7(int stage, const float (&v)[16], int c0, TileState& S, TileTmp7& T) {
+  if (stage == 0) {
+    float cm = vmax(v[0], v[1]);
+#pragma unroll
+    for (int i = 2; i < 16; ++i) cm = vmax(cm, v[i]);
+    unsigned mask = -(unsigned)(cm > S.m);  // strict: an earlier chunk keeps a tie
+    asm("" : "+v"(mask));
+    T.mask = mask;
+    T.m_new = vmax(cm, S.m);
+    T.m2 = T.m_new * LOG2E_F;
+    T.part = 0.f;
+  } else if (stage <= 2) {
+    const int i0 = stage == 1 ? 0 : 8;
+#pragma unroll
+    for (int i = i0; i < i0 + 8; ++i) S.bv[i] = S.bv[i] ^ ((S.bv[i] ^ __float_as_uint(v[i])) & T.mask);
+    if (stage == 2) S.bc = (int)((unsigned)S.bc ^ (((unsigned)S.bc ^ (unsigned)c0) & T.mask));
+  } else {
+    const int i0 = (stage - 3) * 4;
+    float e[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (OVR)
+        e[i] = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-v[i0 + i] * LOG2E_F));
+      else
+        e[i] = __builtin_amdgcn_exp2f(fmaf(v[i0 + i], LOG2E_F, -T.m2));
+    }
+    T.part += (e[0] + e[1]) + (e[2] + e[3]);
+    if (stage == 6) {
+      if constexpr (OVR) {
+        S.s += T.part;
+      } else {
+        const float scale = __builtin_amdgcn_exp2f(fmaf(S.m, LOG2E_F, -T.m2));
+        S.s = fmaf(S.s, scale, T.part);
+      }
+      S.m = T.m_new;
+    }
+  }
+}
+
+// bias of the two 32-class tiles of chunk c0 in accumulator layout; classes >= c_end -> -inf
+__device__ __forceinline__ void bias32(const float* bias_lds, int c0, int c_end, int h, f32x16_t (&bt)[2]) {
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4_t v = *reinterpret_cast<const f32x4_t*>(bias_lds + ct * 32 + 8 * j + 4 * h);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bt[ct][4 * j + r] = v[r];
+    }
+  if (c0 + CLASS_CHUNK > c_end) {  // wave-uniform: the last chunk only
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        bt[ct][i] = c0 + ct * 32 + 8 * (i >> 2) + 4 * h + (i & 3) < c_end ? bt[ct][i] : -INFINITY;
+  }
+}
+
+template <int KS>
+__device__ __forceinline__ void mfma32_chunk(const unsigned char* wb, const bf16x8_t (&xf)[2 * KS], int c0, int c_end,
+                                             int h, int col, f32x16_t (&acc)[2]) {
+  f32x16_t bt[2];
+  bias32(reinterpret_cast<const float*>(wb + CLASS_CHUNK * lds_row_stride<KS>()), c0, c_end, h, bt);
+  acc[0] = bt[0];
+  acc[1] = bt[1];
+#pragma unroll
+  for (int k = 0; k < 2 * KS; ++k) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const bf16x8_t wf = *reinterpret_cast<const bf16x8_t*>(wb + lds_off<KS>(ct * 32 + col, 2 * k + h));
+      acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xf[k], acc[ct], 0, 0, 0);
+    }
+  }
+}
+
+// MFMAs of chunk cn (nb -> nxt) with the epilogue of chunk c0 (acc -> S) spread over the k-steps
+template <int KS, bool OVR>
+__device__ __forceinline__ void fused32_step(const unsigned char* nb, const bf16x8_t (&xf)[2 * KS], int cn, int c_end,
+                                             int h, int col, f32x16_t (&nxt)[2], const f32x16_t (&acc)[2], int c0,
+                                             TileState& S) {
+  f32x16_t bt[2];
+  bias32(reinterpret_cast<const float*>(nb + CLASS_CHUNK * lds_row_stride<KS>()), cn, c_end, h, bt);
+  nxt[0] = bt[0];
+  nxt[1] = bt[1];
+  float v[2][16];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[ct][i] = acc[ct][i];
+  TileTmp7 T[2];
+  constexpr int K2 = 2 * KS;
+  constexpr int NSTAGE = 14;  // 7 per tile; tile 1 follows tile 0 (same row state)
+  // W fragments one k-step ahead in registers: the reads of step k+1 issue before the MFMAs of
+  // step k (a full 64-cycle MFMA pair of cover for the LDS latency); the scheduling barriers pin
+  // them there (left free, hipcc sank every read next to its MFMA).
+  bf16x8_t wf[2][2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) wf[0][ct] = *reinterpret_cast<const bf16x8_t*>(nb + lds_off<KS>(ct * 32 + col, h));
+  static_for<K2>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    if constexpr (k + 1 < K2) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+        wf[(k + 1) & 1][ct] = *reinterpret_cast<const bf16x8_t*>(nb + lds_off<KS>(ct * 32 + col, 2 * (k + 1) + h));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+      nxt[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k & 1][ct], xf[k], nxt[ct], 0, 0, 0);
+    static_for<NSTAGE>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      if constexpr ((j * K2) / NSTAGE == k) {
+        constexpr int t = j / 7, stg = j % 7;
+        tile_stage7<OVR>(stg, v[t], c0 + 32 * t, S, T[t]);
+      }
+    });
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
+template <int WV>
+constexpr int t32_nbuf() {
+  return WV == 8 ? 3 : 2;
+}
+
+template <int KS, int WV, int MODE, bool OVR>
+__global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_softmax32_kernel(
+    GemmArgs a) {
+  static_assert(MODE == 0 || MODE == 2 || MODE == 4, "logits mode runs the 16x16 kernel");
+  const uint16_t* __restrict__ X = a.X;
+  const uint16_t* __restrict__ W = a.W;
+  const float* __restrict__ bias = a.bias;
+  const int64_t B = a.B;
+  const int K = a.K;
+  const int classes_per_split = a.classes_per_split;
+  constexpr int K2 = 2 * KS;
+  constexpr int NTHR = 64 * WV;
+  constexpr int ROWS_PER_BLOCK = 32 * WV;
+  constexpr int F_ = KS * 32;
+  constexpr int NCH = F_ / 8;
+  constexpr int W_BYTES = CLASS_CHUNK * lds_row_stride<KS>();
+  constexpr int BUF_BYTES = W_BYTES + CLASS_CHUNK * 4;
+  constexpr int PIECES = CLASS_CHUNK * NCH / NTHR;
+  constexpr int NBUF = t32_nbuf<WV>();
+  static_assert(PIECES >= 1 && CLASS_CHUNK * NCH % NTHR == 0, "W chunk must split evenly over the block");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * BUF_BYTES + 16];
+  int* const flag = reinterpret_cast<int*>(smem + NBUF * BUF_BYTES);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int h = lane >> 5;
+  const int col = lane & 31;
+  constexpr bool ovr = OVR;
+  const int64_t row0 = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wave * 32;
+  const int c_begin = blockIdx.y * classes_per_split;
+  const int c_end = min(K, c_begin + classes_per_split);
+  phase_stamp(a, WV, wave, lane, 0);
+
+  const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)W, 0, K * F_ * 2, 0x00020000);
+  const auto brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)bias, 0, K * 4, 0x00020000);
+#define MLAPI_DMA32(C0, BUF)                                                                                    \
+  {                                                                                                              \
+    _Pragma("unroll") for (int i = 0; i < PIECES; ++i) __builtin_amdgcn_raw_ptr_buffer_load_lds(                \
+        wrsrc, (lds_void_t*)(smem + (BUF) * BUF_BYTES + (i * NTHR + wave * 64) * 16), 16,                        \
+        (uint32_t)((((tid + i * NTHR) / NCH) * F_ + lds_pos<KS>((tid + i * NTHR) / NCH, (tid + i * NTHR) % NCH) * 8) * \
+                   2),                                                                                           \
+        (C0) * F_ * 2, 0, 0);                                                                                    \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void_t*)(smem + (BUF) * BUF_BYTES + W_BYTES), 4,       \
+                                             (uint32_t)lane * 4, (C0) * 4, 0, 0);                                \
+  }
+#define MLAPI_RAW_BARRIER32()    \
+  asm volatile("" ::: "memory"); \
+  __builtin_amdgcn_s_barrier();  \
+  asm volatile("" ::: "memory");
+
+  TileState ts;
+  tile_init(ts);
+  bf16x8_t xf[K2];
+  MLAPI_DMA32(c_begin, 0)
+  {
+    int64_t r = row0 + col;
+    r = r < B ? r : B - 1;
+    const uint16_t* xr = X + r * a.ldx + 8 * h;
+#pragma unroll
+    for (int k = 0; k < K2; ++k) xf[k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + k * 16));
+  }
+  constexpr int kWaitAll = (7 << 4) | (15 << 8);
+  constexpr int kWaitChunk = kWaitAll | ((PIECES + 1) & 15) | (((PIECES + 1) >> 4) << 14);
+  if constexpr (NBUF == 3) {
+    if (c_begin + CLASS_CHUNK < c_end) {
+      MLAPI_DMA32(c_begin + CLASS_CHUNK, 1)
+      __builtin_amdgcn_s_waitcnt(kWaitChunk);  // chunk 0 + X; chunk 1 flies on
+    } else {
+      __builtin_amdgcn_s_waitcnt(kWaitAll);
+    }
+  } else {
+    __builtin_amdgcn_s_waitcnt(kWaitAll);
+  }
+  MLAPI_RAW_BARRIER32()
+  phase_stamp(a, WV, wave, lane, 1);
+  if (c_begin + (NBUF - 1) * CLASS_CHUNK < c_end) MLAPI_DMA32(c_begin + (NBUF - 1) * CLASS_CHUNK, NBUF - 1)
+  f32x16_t acc[2];
+  mfma32_chunk<KS>(smem, xf, c_begin, c_end, h, col, acc);
+  int buf = 0;
+  for (int c0 = c_begin;; c0 += CLASS_CHUNK) {
+    if (c0 + CLASS_CHUNK >= c_end) {
+      float v[16];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = acc[ct][i];
+        tile_update<OVR>(v, c0 + 32 * ct, ts);
+      }
+      break;
+    }
+    if (NBUF == 3 && c0 + 2 * CLASS_CHUNK < c_end)
+      __builtin_amdgcn_s_waitcnt(kWaitChunk);
+    else
+      __builtin_amdgcn_s_waitcnt(kWaitAll);
+    MLAPI_RAW_BARRIER32()
+    if (c0 + NBUF * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + NBUF * CLASS_CHUNK, buf)
+    const int nbuf = buf + 1 == NBUF ? 0 : buf + 1;
+    f32x16_t nxt[2];
+    fused32_step<KS, OVR>(smem + nbuf * BUF_BYTES, xf, c0 + CLASS_CHUNK, c_end, h, col, nxt, acc, c0, ts);
+    acc[0] = nxt[0];
+    acc[1] = nxt[1];
+    buf = nbuf;
+  }
+#undef MLAPI_RAW_BARRIER32
+#undef MLAPI_DMA32
+  phase_stamp(a, WV, wave, lane, 2);
+  RowState S = tile_result32(ts, h);
+  S = merge_state(S, shfl_state(S, 32), ovr);
+  phase_stamp(a, WV, wave, lane, 3);
+  const int64_t row = row0 + col;
+  if (gridDim.y == 1) {
+    if (h == 0 && row < B) {
+      if constexpr (MODE == 0) {
+        a.out_idx[row] = S.bi;
+        a.out_p[row] = ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s;
+      } else if constexpr (MODE == 4) {
+        a.rowstate[row] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
+      } else {
+        a.rowstat[row] = make_float2(S.m + __logf(S.s), __int_as_float(S.bi));
+      }
+    }
+    return;
+  }
+  // split classes: the 16x16 kernel's publish / last-arriver merge (see there)
+  if (h == 0 && row < B) {
+    typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+    typedef __attribute__((address_space(1))) unsigned int gu32_t;
+    float4* dst = a.partials + (int64_t)blockIdx.y * B + row;
+    const unsigned long long ms =
+        (unsigned long long)__float_as_uint(S.m) | ((unsigned long long)__float_as_uint(S.s) << 32);
+    __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S.bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned ticket =
+        __hip_atomic_fetch_add(&a.counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = ticket == gridDim.y - 1;
+  }
+  __syncthreads();
+  if (*flag == 0) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&a.counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (tid < ROWS_PER_BLOCK) {
+    const int64_t mrow = (int64_t)blockIdx.x * ROWS_PER_BLOCK + tid;
+    if (mrow < B) {
+      const unsigned ns = gridDim.y;
+      float4 p[MERGE_MAX];
+#pragma unroll
+      for (int sp = 0; sp < MERGE_MAX; ++sp) p[sp] = a.partials[(int64_t)min((unsigned)sp, ns - 1) * B + mrow];
+      RowState R{p[0].x, p[0].y, __float_as_int(p[0].z)};
+#pragma unroll
+      for (int sp = 1; sp < MERGE_MAX; ++sp)
+        if ((unsigned)sp < ns) R = merge_state(R, RowState{p[sp].x, p[sp].y, __float_as_int(p[sp].z)}, ovr);
+      for (unsigned sp = MERGE_MAX; sp < ns; ++sp) {
+        const float4 pq = a.partials[(int64_t)sp * B + mrow];
+        R = merge_state(R, RowState{pq.x, pq.y, __float_as_int(pq.z)}, ovr);
+      }
+      if constexpr (MODE == 0) {
+        a.out_idx[mrow] = R.bi;
+        a.out_p[mrow] = ovr ? sigmoidf_(R.m) / R.s : 1.f / R.s;
+      } else if constexpr (MODE == 4) {
+        a.rowstate[mrow] = make_float4(R.m, R.s, __int_as_float(R.bi), 0.f);
+      } else {
+        a.rowstat[mrow] = make_float2(R.m + __logf(R.s), __int_as_float(R.bi));
+      }
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------------------------
 // Row-group kernel (small / medium batches, and any F): one block owns 16 * NT batch rows and
@@ -683,7 +1157,7 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
 // Which kernel serves (B, K, F): the row-group kernel only where the tiles kernel has no
 // instantiation (F > 512, the only kernel that loops F). At F <= 512 the tiles kernel with class
 // splits is faster at every B (profiles/r2_gemm/sweep.log: B <= 4096 rows 17-19 us vs tiles 7-10).
-int g_force_kernel = 0;  // benchmark hook: 0 automatic, 1 tiles, 2 row-group
+int g_force_kernel = 0;  // benchmark hook: 0 automatic, 1 tiles 16x16, 2 row-group, 3/4 tiles 32x32 (4/8 waves)
 
 bool rows_supported(int F) { return F == 32 || F == 64 || F == 128 || F == 256 || (F > 256 && F % 256 == 0); }
 bool tiles_supported(int F) { return F == 32 || F == 64 || F == 128 || F == 256 || F == 512; }
@@ -745,7 +1219,8 @@ RowsArgs rows_args(const void* X, int64_t ldx, const void* W, const float* b, in
 }
 
 struct Plan {
-  int nt;                 // 16-row tiles per wave
+  int k32 = 0;            // > 0: the 32x32x16 kernel with this many waves per block
+  int nt;                 // 16-row tiles per wave (16x16x32 kernel)
   int splits;
   int classes_per_split;
   int64_t row_blocks;
@@ -754,8 +1229,22 @@ struct Plan {
 // Benchmark hook (tools/gemm_plan_sweep.py): force (nt, splits); 0 = automatic.
 int g_force_nt = 0, g_force_splits = 0;
 
-Plan make_plan(int64_t B, int K, int F, bool training) {
+// rows per block of the tiles kernel (host mirror of tiles_block_waves)
+int block_rows(int F, int nt) {
+  const int ks = F / 32;
+  return 16 * nt * ((nt == 2 && ks >= 2 && ks <= 8) ? 8 : 4);
+}
+
+bool t32_supported(int F) { return F == 64 || F == 128 || F == 256; }
+
+// allow32 = false for the logits mode (only the 16x16 kernel writes Z)
+Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   Plan p;
+  if (allow32 && t32_supported(F)) {
+    if (g_force_kernel == 3) p.k32 = 4;
+    else if (g_force_kernel == 4) p.k32 = 8;
+    else if (g_force_kernel == 0 && B >= 16384) p.k32 = 4;
+  }
   // 32 rows per wave (NT = 2) halve the LDS fragment reads per MFMA. It pays once the register
   // staging is gone (LDS-DMA): B=262144 230 -> 172 us, B=8192 about even, B=1024 worse
   // (tools/gemm_plan_sweep.py, profiles/r1_pmc/gemm_plan_sweep_dma.log). KS = 16 at NT = 2 needs
@@ -764,7 +1253,7 @@ Plan make_plan(int64_t B, int K, int F, bool training) {
   p.nt = (F <= 256 && B >= 16384) ? 2 : 1;
   if (g_force_nt == 1 || g_force_nt == 2) p.nt = g_force_nt;
   if (g_force_splits > 0) {
-    const int rows_per_block = 64 * p.nt;
+    const int rows_per_block = p.k32 ? 32 * p.k32 : block_rows(F, p.nt);
     p.row_blocks = (B + rows_per_block - 1) / rows_per_block;
     const int chunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
     const int sp = g_force_splits > chunks ? chunks : g_force_splits;
@@ -772,7 +1261,7 @@ Plan make_plan(int64_t B, int K, int F, bool training) {
     p.splits = (K + p.classes_per_split - 1) / p.classes_per_split;
     if (!(p.splits > 1 && p.row_blocks * 4 > COUNTER_BYTES)) return p;
   }
-  const int rows_per_block = 64 * p.nt;
+  const int rows_per_block = p.k32 ? 32 * p.k32 : block_rows(F, p.nt);
   p.row_blocks = (B + rows_per_block - 1) / rows_per_block;
   const int chunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
   // measured best: B=1024 -> 8 splits (128 blocks), B=8192 -> 4 (512 blocks): fill the chip, but
@@ -790,16 +1279,42 @@ Plan make_plan(int64_t B, int K, int F, bool training) {
   return p;
 }
 
+template <int MODE, int KS>
+void launch32(const GemmArgs& args, const dim3& grid, int wv, hipStream_t stream) {
+  if constexpr (MODE != 1) {
+    const bool o = args.kind == KIND_OVR;
+    if (wv == 8) {
+      if (o) hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 8, MODE, true>), grid, dim3(512), 0, stream, args);
+      else hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 8, MODE, false>), grid, dim3(512), 0, stream, args);
+    } else {
+      if (o) hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, MODE, true>), grid, dim3(256), 0, stream, args);
+      else hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, MODE, false>), grid, dim3(256), 0, stream, args);
+    }
+  }
+}
+
+void* g_stamps = nullptr;  // profiling hook (gemm_softmax_set_stamps)
+
 template <int MODE>
 void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
   const dim3 grid((unsigned)plan.row_blocks, (unsigned)plan.splits);
   args.classes_per_split = plan.classes_per_split;
+  args.stamps = static_cast<unsigned long long*>(g_stamps);
+  if (MODE != 1 && plan.k32) {
+    if (F == 64) launch32<MODE, 2>(args, grid, plan.k32, stream);
+    else if (F == 128) launch32<MODE, 4>(args, grid, plan.k32, stream);
+    else launch32<MODE, 8>(args, grid, plan.k32, stream);
+    MLAPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
 #define MLAPI_GEMM_LAUNCH(KSV, NTV)                                                                      \
   do {                                                                                                   \
     if (args.kind == KIND_OVR)                                                                           \
-      hipLaunchKernelGGL((gemm_softmax_kernel<KSV, NTV, MODE, true>), grid, dim3(256), 0, stream, args); \
+      hipLaunchKernelGGL((gemm_softmax_kernel<KSV, NTV, MODE, true>), grid,                             \
+                         dim3(64 * tiles_block_waves<KSV, NTV>()), 0, stream, args);                     \
     else                                                                                                 \
-      hipLaunchKernelGGL((gemm_softmax_kernel<KSV, NTV, MODE, false>), grid, dim3(256), 0, stream, args); \
+      hipLaunchKernelGGL((gemm_softmax_kernel<KSV, NTV, MODE, false>), grid,                            \
+                         dim3(64 * tiles_block_waves<KSV, NTV>()), 0, stream, args);                     \
   } while (0)
   const int ks = F / 32;
   if (F != 32 && F != 64 && F != 128 && F != 256 && F != 512)
@@ -837,6 +1352,8 @@ GemmArgs base_args(const void* X, const void* W, int64_t B, int F, int K, int ki
 }
 
 }  // namespace
+
+void gemm_softmax_set_stamps(void* stamps) { g_stamps = stamps; }
 
 void gemm_softmax_force_plan(int nt, int splits, int kernel) {
   g_force_nt = nt;
@@ -932,7 +1449,7 @@ void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B,
     launch_rows<1>(ra, KIND_MULTINOMIAL, stream);
     return;
   }
-  Plan plan = make_plan(B, K, F, false);
+  Plan plan = make_plan(B, K, F, false, false);
   plan.splits = (K + plan.classes_per_split - 1) / plan.classes_per_split;  // no merge needed for logits
   GemmArgs args = base_args(X, W, B, F, K, KIND_MULTINOMIAL);
   args.bias = b;

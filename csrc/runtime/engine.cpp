@@ -192,7 +192,9 @@ uint64_t Engine::load_model(int kind, int F, int K, const double* W, const doubl
     m->xdt = cfg_.wide_dtype;
     const int ne = cfg_.wide_dtype == DT_BF16 ? 8 : 4;  // elements per 16-byte chunk
     m->ldx = (F + ne - 1) / ne * ne;
-  } else if (!binary && K >= 2 && cfg_.wide_dtype == DT_BF16 && F <= 512) {
+  } else if (!binary && K >= 2 && cfg_.wide_dtype == DT_BF16 && F <= 4096) {
+    // F <= 512: the tiles kernels at a power-of-two width; wider: the row-group kernel at a
+    // multiple of 512 (it loops F in 256-feature slices inside one launch)
     m->path = PATH_GEMM;
     m->xdt = DT_BF16;
     m->ldx = (int)padded_features(F);

@@ -82,10 +82,11 @@ def test_gemv_binary_large_stream():
     torch.testing.assert_close(p, torch.sigmoid(z.abs()), rtol=1e-4, atol=1e-4)
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["auto", "tiles", "rows"])
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["auto", "tiles", "rows", "t32w4", "t32w8"])
 def gemm_kernel(request):
     """Run a multiclass test under the automatic plan and with each kernel forced (tiles: the
-    LDS-staged, chunk-pipelined kernel; rows: the row-group kernel)."""
+    LDS-staged, chunk-pipelined 16x16x32 kernel; rows: the row-group kernel; t32w4 / t32w8: the
+    32x32x16 large-batch kernel with 4 / 8 waves per block, F in {64, 128, 256}, else tiles)."""
     from mlapi_amd._native import C
 
     C().gemm_softmax_force_plan(0, 0, request.param)
@@ -169,8 +170,9 @@ def test_gemm_logits_asymmetric(kernel):
     torch.testing.assert_close(Z, ref.logits_ref(X, W, b), rtol=0, atol=0)
 
 
-def test_gemm_ties_first_max(gemm_kernel):
-    B, F, K = 256, 32, 130
+@pytest.mark.parametrize("F", [32, 64, 256])
+def test_gemm_ties_first_max(gemm_kernel, F):
+    B, K = 256, 130
     X = torch.ones(B, F, device=DEV, dtype=torch.bfloat16)
     W = torch.zeros(K, F, device=DEV, dtype=torch.bfloat16)
     b = torch.zeros(K, device=DEV)

@@ -66,6 +66,8 @@ def _engine(native, **kw):
     (256, 50, Kind.OVR, "bf16", "gemm"),
     (100, 10, Kind.MULTINOMIAL, "bf16", "gemm"),  # F padded to 128
     (512, 300, Kind.MULTINOMIAL, "bf16", "gemm"),
+    (1024, 200, Kind.MULTINOMIAL, "bf16", "gemm"),  # row-group kernel (F looped in slices)
+    (700, 30, Kind.OVR, "bf16", "gemm"),            # F padded to 1024
     (48, 40, Kind.MULTINOMIAL, "f32", "generic"),
     (48, 40, Kind.OVR, "f64", "generic"),
 ])

@@ -30,7 +30,7 @@ def _clear_rows(m: LinearModel, X: np.ndarray) -> np.ndarray:
 
 
 @pytest.mark.parametrize("world", [1, 3, 8])
-@pytest.mark.parametrize("B,F,K", [(1024, 256, 1000), (77, 64, 37), (5000, 128, 200)])
+@pytest.mark.parametrize("B,F,K", [(1024, 256, 1000), (77, 64, 37), (5000, 128, 200), (20000, 256, 1000)])
 @pytest.mark.parametrize("kind", [Kind.MULTINOMIAL, Kind.OVR])
 def test_class_sharded_merge(world, B, F, K, kind):
     m, X = _bf16_exact(LinearModel.random(F, K, seed=K + world, kind=kind), np.random.default_rng(3).standard_normal((B, F)))

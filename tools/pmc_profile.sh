@@ -16,6 +16,8 @@ declare -A GROUPS_=(
   [valu]="SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES"
   [stall]="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY"
   [active]="SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM"
+  [l2]="TCC_HIT_sum TCC_MISS_sum"
+  [ldswait]="SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_SALU"
 )
 GROUP_ORDER="${PMC_GROUPS:-fetch write mfma lds valu stall active}"
 BENCHES="${PMC_BENCHES:-gemv:--mode gemv --steps 5 --warmup 1|gemm:--mode gemm --steps 5 --warmup 1|gemm_big:--mode gemm --batch 262144 --steps 5 --warmup 1|train:--mode train --steps 5 --warmup 1|train_softmax:--mode train_softmax --steps 5 --warmup 1}"

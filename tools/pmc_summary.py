@@ -55,6 +55,24 @@ for (bench, k), cs in sorted(vals.items()):
           f"{pct('SQ_WAIT_ANY'):.0f} | {pct('SQ_WAIT_INST_ANY'):.0f} | {pct('SQ_ACTIVE_INST_VALU'):.0f} | "
           f"{pct('SQ_ACTIVE_INST_LDS'):.0f} | {pct('SQ_ACTIVE_INST_VMEM'):.0f} | {waves:.0f} |")
 print()
+print("| bench | kernel | L2 hit % | LDS-wait % | MFMA busy % | MISC-active % | SALU instr/wave |")
+print("|---|---|---|---|---|---|---|")
+for (bench, k), cs in sorted(vals.items()):
+    if "mlapi" not in k and not k.startswith("Cijk"):
+        continue
+    name = k.replace("void mlapi::(anonymous namespace)::", "")[:60]
+    hit, miss = mean(cs.get("TCC_HIT_sum", [])), mean(cs.get("TCC_MISS_sum", []))
+    wcyc = mean(cs.get("SQ_WAVE_CYCLES", []))
+    waves = mean(cs.get("SQ_WAVES", []))
+    busy, sqb = mean(cs.get("SQ_VALU_MFMA_BUSY_CYCLES", [])), mean(cs.get("SQ_BUSY_CYCLES", []))
+
+    def pc(c):
+        return 100 * mean(cs.get(c, [])) / wcyc if wcyc == wcyc and wcyc else float("nan")
+
+    print(f"| {bench} | `{name}` | {100 * hit / (hit + miss) if hit + miss else float('nan'):.1f} | "
+          f"{pc('SQ_WAIT_INST_LDS'):.0f} | {100 * busy / sqb / 4 if sqb == sqb and sqb else float('nan'):.0f} | "
+          f"{pc('SQ_ACTIVE_INST_MISC'):.0f} | {mean(cs.get('SQ_INSTS_SALU', [])) / waves if waves else float('nan'):.0f} |")
+print()
 print("*HBM GB/s = (FETCH_SIZE + WRITE_SIZE) / kernel time; on gfx950 FETCH_SIZE reads about half of")
 print(" the streamed bytes (MI355X_MICROARCH.md), so the true read rate is up to 2x this column.")
 print(" Kernel time here is measured under counter collection (serialised dispatches).")
