@@ -48,7 +48,7 @@ constexpr int CLASS_CHUNK = 64;
 constexpr float LOG2E_F = 1.4426950408889634f;
 constexpr float LN2_F = 0.6931471805599453f;
 constexpr int COUNTER_BYTES = 4096;  // per-row-block arrival counters live at the start of the workspace
-constexpr int MERGE_MAX = 8;         // split partials the merging block loads at once (automatic plans: <= 8)
+constexpr int MERGE_MAX = 16;        // split partials the merging block loads at once (automatic plans: <= 16)
 
 struct RowState {
   float m;  // running max logit (-inf if nothing seen yet)
@@ -117,17 +117,22 @@ struct GemmArgs {
   float* Z;                // MODE 1
   float2* rowstat;         // MODE 2 output: {lse, argmax bits}
   float4* rowstate;        // MODE 4 output: {max, sum, argmax bits, 0} (class-sharded TP)
-  unsigned long long* stamps;  // profiling (tools/gemm_phase_probe.py): 4 s_memtime stamps per wave
+  unsigned long long* stamps;  // profiling (tools/gemm_phase_probe.py): 8 s_memtime slots per wave
 };
 
-// Phase stamps of one wave (profiling builds of a launch only: a.stamps is null otherwise):
-// 0 entry, 1 first W chunk + X landed, 2 class loop done, 3 row state reduced.
-__device__ __forceinline__ void phase_stamp(const GemmArgs& a, int waves_per_block, int wave, int lane, int j) {
+// Phase stamps of one wave (profiled launches only: a.stamps is null otherwise): 0 entry, 1 first
+// W chunk + X landed, 2 class loop done, 3 row state reduced; slot 4: cycles the class loop spent
+// in its per-chunk wait + barrier (32x32 kernel).
+__device__ __forceinline__ void phase_put(const GemmArgs& a, int waves_per_block, int wave, int lane, int j,
+                                          unsigned long long v) {
   if (a.stamps != nullptr && lane == 0) {
     const unsigned long long gid =
         ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) * (unsigned)waves_per_block + (unsigned)wave;
-    a.stamps[gid * 4 + j] = __builtin_amdgcn_s_memtime();
+    a.stamps[gid * 8 + j] = v;
   }
+}
+__device__ __forceinline__ void phase_stamp(const GemmArgs& a, int waves_per_block, int wave, int lane, int j) {
+  if (a.stamps != nullptr) phase_put(a, waves_per_block, wave, lane, j, __builtin_amdgcn_s_memtime());
 }
 
 template <typename F, int... I>
@@ -429,12 +434,12 @@ template <int KS, int MODE>
 constexpr int tiles_waves_per_eu() {
   return KS == 16 ? 1 : 2;
 }
-// Waves per block. The large-batch plan (NT = 2) runs 8 waves = 256 rows per block, one block
-// per CU: every block streams ALL of W through LDS, so W's L2 -> CU traffic is (B / rows per
-// block) x |W| (v4, 128-row blocks: 1 GB at B = 262144, ~12 B/clk/CU for the whole kernel).
+// Waves per block: 4 (two blocks per CU). 8-wave blocks (256 rows, one block per CU, a third W
+// buffer) halve W's L2 -> CU traffic but measured slower at B = 262144 (170 vs 145 us,
+// profiles/r2_gemm/phase_probe.log): one barrier then stalls all 8 waves of the CU.
 template <int KS, int NT>
 constexpr int tiles_block_waves() {
-  return (NT == 2 && KS >= 2 && KS <= 8) ? 8 : 4;
+  return 4;
 }
 
 template <int KS, int NT, int MODE, bool OVR>
@@ -782,13 +787,41 @@ __device__ __forceinline__ void mfma32_chunk(const unsigned char* wb, const bf16
   }
 }
 
-// MFMAs of chunk cn (nb -> nxt) with the epilogue of chunk c0 (acc -> S) spread over the k-steps
-template <int KS, bool OVR>
-__device__ __forceinline__ void fused32_step(const unsigned char* nb, const bf16x8_t (&xf)[2 * KS], int cn, int c_end,
-                                             int h, int col, f32x16_t (&nxt)[2], const f32x16_t (&acc)[2], int c0,
-                                             TileState& S) {
+// Per-lane LDS byte offsets of the W fragments of one k-step period: the XOR swizzle repeats every
+// P = (mask + 1) / 2 k-steps (8 at F >= 128), so fragment (ct, k) sits at off[k % P] + ct * 32 rows
+// + (k / P) * 256 B, and with the buffer index a template constant every read is
+// `ds_read_b128 v, off offset:IMM` (v5 recomputed ~30 address VALU per chunk).
+template <int KS>
+constexpr int t32_period() {
+  return KS * 4 >= 16 ? 8 : KS * 2;
+}
+template <int KS>
+struct FragOff {
+  uint32_t o[t32_period<KS>()];
+};
+template <int KS>
+__device__ __forceinline__ FragOff<KS> frag_offsets(int h, int col) {
+  FragOff<KS> f;
+#pragma unroll
+  for (int j = 0; j < t32_period<KS>(); ++j) f.o[j] = (uint32_t)lds_off<KS>(col, 2 * j + h);
+  return f;
+}
+template <int KS, int BUF, int BUF_BYTES>
+__device__ __forceinline__ bf16x8_t frag32(const unsigned char* smem, const FragOff<KS>& f, int ct, int k) {
+  constexpr int P = t32_period<KS>();
+  return *reinterpret_cast<const bf16x8_t*>(smem + BUF * BUF_BYTES + f.o[k % P] + ct * 32 * lds_row_stride<KS>() +
+                                            (k / P) * (P * 2 * 16));
+}
+
+// MFMAs of chunk cn (LDS buffer BUF -> nxt) with the epilogue of chunk c0 (acc -> S) spread over
+// the k-steps
+template <int KS, bool OVR, int BUF, int BUF_BYTES>
+__device__ __forceinline__ void fused32_step(const unsigned char* smem, const FragOff<KS>& fo,
+                                             const bf16x8_t (&xf)[2 * KS], int cn, int c_end, int h,
+                                             f32x16_t (&nxt)[2], const f32x16_t (&acc)[2], int c0, TileState& S) {
   f32x16_t bt[2];
-  bias32(reinterpret_cast<const float*>(nb + CLASS_CHUNK * lds_row_stride<KS>()), cn, c_end, h, bt);
+  bias32(reinterpret_cast<const float*>(smem + BUF * BUF_BYTES + CLASS_CHUNK * lds_row_stride<KS>()), cn, c_end, h,
+         bt);
   nxt[0] = bt[0];
   nxt[1] = bt[1];
   float v[2][16];
@@ -800,17 +833,16 @@ __device__ __forceinline__ void fused32_step(const unsigned char* nb, const bf16
   constexpr int K2 = 2 * KS;
   constexpr int NSTAGE = 14;  // 7 per tile; tile 1 follows tile 0 (same row state)
   // W fragments one k-step ahead in registers: the reads of step k+1 issue before the MFMAs of
-  // step k (a full 64-cycle MFMA pair of cover for the LDS latency); the scheduling barriers pin
-  // them there (left free, hipcc sank every read next to its MFMA).
+  // step k (a 64-cycle MFMA pair of cover for the LDS latency); the scheduling barriers pin them
+  // there (left free, hipcc sank every read next to its MFMA).
   bf16x8_t wf[2][2];
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct) wf[0][ct] = *reinterpret_cast<const bf16x8_t*>(nb + lds_off<KS>(ct * 32 + col, h));
+  for (int ct = 0; ct < 2; ++ct) wf[0][ct] = frag32<KS, BUF, BUF_BYTES>(smem, fo, ct, 0);
   static_for<K2>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     if constexpr (k + 1 < K2) {
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-        wf[(k + 1) & 1][ct] = *reinterpret_cast<const bf16x8_t*>(nb + lds_off<KS>(ct * 32 + col, 2 * (k + 1) + h));
+      for (int ct = 0; ct < 2; ++ct) wf[(k + 1) & 1][ct] = frag32<KS, BUF, BUF_BYTES>(smem, fo, ct, k + 1);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -827,9 +859,15 @@ __device__ __forceinline__ void fused32_step(const unsigned char* nb, const bf16
   });
 }
 
-template <int WV>
-constexpr int t32_nbuf() {
-  return WV == 8 ? 3 : 2;
+template <bool OVR>
+__device__ __forceinline__ void epilogue32(const f32x16_t (&acc)[2], int c0, TileState& ts) {
+  float v[16];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = acc[ct][i];
+    tile_update<OVR>(v, c0 + 32 * ct, ts);
+  }
 }
 
 template <int KS, int WV, int MODE, bool OVR>
@@ -850,7 +888,7 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(2, 2)))
   constexpr int W_BYTES = CLASS_CHUNK * lds_row_stride<KS>();
   constexpr int BUF_BYTES = W_BYTES + CLASS_CHUNK * 4;
   constexpr int PIECES = CLASS_CHUNK * NCH / NTHR;
-  constexpr int NBUF = t32_nbuf<WV>();
+  constexpr int NBUF = 2;
   static_assert(PIECES >= 1 && CLASS_CHUNK * NCH % NTHR == 0, "W chunk must split evenly over the block");
   __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * BUF_BYTES + 16];
   int* const flag = reinterpret_cast<int*>(smem + NBUF * BUF_BYTES);
@@ -895,50 +933,47 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(2, 2)))
     for (int k = 0; k < K2; ++k) xf[k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + k * 16));
   }
   constexpr int kWaitAll = (7 << 4) | (15 << 8);
-  constexpr int kWaitChunk = kWaitAll | ((PIECES + 1) & 15) | (((PIECES + 1) >> 4) << 14);
-  if constexpr (NBUF == 3) {
-    if (c_begin + CLASS_CHUNK < c_end) {
-      MLAPI_DMA32(c_begin + CLASS_CHUNK, 1)
-      __builtin_amdgcn_s_waitcnt(kWaitChunk);  // chunk 0 + X; chunk 1 flies on
-    } else {
-      __builtin_amdgcn_s_waitcnt(kWaitAll);
-    }
-  } else {
-    __builtin_amdgcn_s_waitcnt(kWaitAll);
-  }
+  __builtin_amdgcn_s_waitcnt(kWaitAll);  // chunk 0 + X
   MLAPI_RAW_BARRIER32()
   phase_stamp(a, WV, wave, lane, 1);
-  if (c_begin + (NBUF - 1) * CLASS_CHUNK < c_end) MLAPI_DMA32(c_begin + (NBUF - 1) * CLASS_CHUNK, NBUF - 1)
-  f32x16_t acc[2];
-  mfma32_chunk<KS>(smem, xf, c_begin, c_end, h, col, acc);
-  int buf = 0;
-  for (int c0 = c_begin;; c0 += CLASS_CHUNK) {
+  if (c_begin + CLASS_CHUNK < c_end) MLAPI_DMA32(c_begin + CLASS_CHUNK, 1)
+  const FragOff<KS> fo = frag_offsets<KS>(h, col);
+  f32x16_t accA[2], accB[2];
+  mfma32_chunk<KS>(smem, xf, c_begin, c_end, h, col, accA);
+  // Unrolled by the two LDS buffers: chunk c (in accA, buffer 0) / c+1 (accB, buffer 1) swap roles
+  // each half, so the buffer offsets are immediates and no accumulator is copied.
+  unsigned long long waited = 0;  // profiling only (a.stamps)
+  const bool prof = a.stamps != nullptr;
+#define MLAPI_WAIT_BARRIER32()                                    \
+  {                                                               \
+    const unsigned long long w0 = prof ? __builtin_amdgcn_s_memtime() : 0; \
+    __builtin_amdgcn_s_waitcnt(kWaitAll);                         \
+    MLAPI_RAW_BARRIER32()                                         \
+    if (prof) waited += __builtin_amdgcn_s_memtime() - w0;        \
+  }
+  for (int c0 = c_begin;;) {
     if (c0 + CLASS_CHUNK >= c_end) {
-      float v[16];
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = acc[ct][i];
-        tile_update<OVR>(v, c0 + 32 * ct, ts);
-      }
+      epilogue32<OVR>(accA, c0, ts);
       break;
     }
-    if (NBUF == 3 && c0 + 2 * CLASS_CHUNK < c_end)
-      __builtin_amdgcn_s_waitcnt(kWaitChunk);
-    else
-      __builtin_amdgcn_s_waitcnt(kWaitAll);
-    MLAPI_RAW_BARRIER32()
-    if (c0 + NBUF * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + NBUF * CLASS_CHUNK, buf)
-    const int nbuf = buf + 1 == NBUF ? 0 : buf + 1;
-    f32x16_t nxt[2];
-    fused32_step<KS, OVR>(smem + nbuf * BUF_BYTES, xf, c0 + CLASS_CHUNK, c_end, h, col, nxt, acc, c0, ts);
-    acc[0] = nxt[0];
-    acc[1] = nxt[1];
-    buf = nbuf;
+    MLAPI_WAIT_BARRIER32()
+    if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 0)
+    fused32_step<KS, OVR, 1, BUF_BYTES>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0, ts);
+    c0 += CLASS_CHUNK;
+    if (c0 + CLASS_CHUNK >= c_end) {
+      epilogue32<OVR>(accB, c0, ts);
+      break;
+    }
+    MLAPI_WAIT_BARRIER32()
+    if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 1)
+    fused32_step<KS, OVR, 0, BUF_BYTES>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0, ts);
+    c0 += CLASS_CHUNK;
   }
+#undef MLAPI_WAIT_BARRIER32
 #undef MLAPI_RAW_BARRIER32
 #undef MLAPI_DMA32
   phase_stamp(a, WV, wave, lane, 2);
+  if (prof) phase_put(a, WV, wave, lane, 4, waited);
   RowState S = tile_result32(ts, h);
   S = merge_state(S, shfl_state(S, 32), ovr);
   phase_stamp(a, WV, wave, lane, 3);
@@ -1231,8 +1266,8 @@ int g_force_nt = 0, g_force_splits = 0;
 
 // rows per block of the tiles kernel (host mirror of tiles_block_waves)
 int block_rows(int F, int nt) {
-  const int ks = F / 32;
-  return 16 * nt * ((nt == 2 && ks >= 2 && ks <= 8) ? 8 : 4);
+  (void)F;
+  return 16 * nt * 4;
 }
 
 bool t32_supported(int F) { return F == 64 || F == 128 || F == 256; }
@@ -1241,8 +1276,7 @@ bool t32_supported(int F) { return F == 64 || F == 128 || F == 256; }
 Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   Plan p;
   if (allow32 && t32_supported(F)) {
-    if (g_force_kernel == 3) p.k32 = 4;
-    else if (g_force_kernel == 4) p.k32 = 8;
+    if (g_force_kernel == 3 || g_force_kernel == 4) p.k32 = 4;
     else if (g_force_kernel == 0 && B >= 16384) p.k32 = 4;
   }
   // 32 rows per wave (NT = 2) halve the LDS fragment reads per MFMA. It pays once the register
@@ -1283,13 +1317,9 @@ template <int MODE, int KS>
 void launch32(const GemmArgs& args, const dim3& grid, int wv, hipStream_t stream) {
   if constexpr (MODE != 1) {
     const bool o = args.kind == KIND_OVR;
-    if (wv == 8) {
-      if (o) hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 8, MODE, true>), grid, dim3(512), 0, stream, args);
-      else hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 8, MODE, false>), grid, dim3(512), 0, stream, args);
-    } else {
-      if (o) hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, MODE, true>), grid, dim3(256), 0, stream, args);
-      else hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, MODE, false>), grid, dim3(256), 0, stream, args);
-    }
+    (void)wv;  // 4 waves per block (2 blocks per CU); the 8-wave variant measured slower
+    if (o) hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, MODE, true>), grid, dim3(256), 0, stream, args);
+    else hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, MODE, false>), grid, dim3(256), 0, stream, args);
   }
 }
 

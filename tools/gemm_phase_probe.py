@@ -1,5 +1,6 @@
 """Where a gemm_softmax wave spends its time: every wave of one launch writes 4 s_memtime stamps
-(entry, first W chunk + X landed, class loop done, row state reduced); this prints per-phase
+(entry, first W chunk + X landed, class loop done, row state reduced) and, in the 32x32 kernel, the
+cycles its class loop waited at the per-chunk DMA wait + barrier; this prints per-phase
 cycle statistics per kernel plan. Run on the GPU box:
 
     python tools/gemm_phase_probe.py [B ...]          (default 1024 262144)
@@ -15,12 +16,12 @@ from mlapi_amd.ops import linear as ops  # noqa: E402
 
 dev = torch.device("cuda", 0)
 F, K = 256, 1000
-PLANS = {"auto": (0, 0, 0), "t16_nt2": (2, 0, 1), "t16_nt1": (1, 0, 1), "t32w4": (0, 0, 3), "t32w8": (0, 0, 4)}
+PLANS = {"auto": (0, 0, 0), "t16_nt2": (2, 0, 1), "t16_nt1": (1, 0, 1), "t32": (0, 0, 3)}
 for B in tuple(int(a) for a in sys.argv[1:]) or (1024, 262144):
     X = torch.randn(B, F, device=dev).to(torch.bfloat16)
     W = (torch.randn(K, F, device=dev) / 16).to(torch.bfloat16)
     b = torch.randn(K, device=dev) * 0.1
-    stamps = torch.zeros(4 * (B // 16 + 64) * 16, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(8 * (B // 16 + 64) * 16, dtype=torch.int64, device=dev)
     for name, plan in PLANS.items():
         C().gemm_softmax_force_plan(*plan)
         op = ops.GemmSoftmax(B, K, F, dev)
@@ -39,11 +40,13 @@ for B in tuple(int(a) for a in sys.argv[1:]) or (1024, 262144):
         op(X, W, b, out=out)
         torch.cuda.synchronize()
         C().gemm_softmax_set_stamps(0)
-        t = stamps.view(-1, 4).cpu().numpy()
-        t = t[t[:, 0] != 0].astype(np.float64)
+        t8 = stamps.view(-1, 8).cpu().numpy()
+        t8 = t8[t8[:, 0] != 0].astype(np.float64)
+        t, wait = t8[:, :4], t8[:, 4]
         d = np.diff(t, axis=1)
         life = t[:, 3] - t[:, 0]
         q = lambda a: f"{np.median(a):9.0f} {np.percentile(a, 90):9.0f}"  # noqa: E731
         print(f"B={B:7d} {name:8s} {us:8.2f} us/launch  waves {len(t):6d} | median/p90 cycles: "
-              f"prologue {q(d[:, 0])} | loop {q(d[:, 1])} | reduce {q(d[:, 2])} | life {q(life)}", flush=True)
+              f"prologue {q(d[:, 0])} | loop {q(d[:, 1])} (wait+barrier {q(wait)}) | reduce {q(d[:, 2])} | "
+              f"life {q(life)}", flush=True)
     C().gemm_softmax_force_plan(0, 0, 0)
