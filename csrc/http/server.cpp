@@ -254,6 +254,14 @@ bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>&
 // IO thread
 // ------------------------------------------------------------------------------------------------
 namespace {
+inline int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+}
+}  // namespace
+
+namespace {
 
 constexpr uint64_t ID_LISTEN = 0;
 constexpr uint64_t ID_EVENT = 1;
@@ -387,7 +395,12 @@ class IoThread : public Sink {
   std::atomic<uint64_t> n_fast{0}, n_slow{0}, n_resp{0}, n_conn{0}, n_err{0}, n_bad{0}, n_listen_close{0};
 
  private:
+  // Hand-off from other threads: a spinning IO thread sees `pending_` on its next poll; a blocked
+  // one needs the eventfd. Both flags are seq_cst so the spin -> block transition cannot lose a
+  // wake (the IO thread clears spinning_ and then re-reads pending_ before it blocks).
   void wake() {
+    pending_.store(true);
+    if (spinning_.load()) return;
     if (!signaled_.exchange(true)) {
       const uint64_t one = 1;
       ssize_t r = write(evfd_, &one, sizeof one);
@@ -425,10 +438,31 @@ class IoThread : public Sink {
     snprintf(name, sizeof name, "mlapi-io-%d", index_);
     pthread_setname_np(pthread_self(), name);
     epoll_event evs[256];
+    const int64_t spin_ns = (int64_t)srv_->config().io_spin_us * 1000;
+    int64_t last_active = 0;
     while (!stop_.load()) {
       flush_submits();
       flush_log();
-      const int n = epoll_wait(epfd_, evs, 256, 200);
+      int timeout = 200;
+      if (spin_ns > 0) {
+        const int64_t now = mono_ns();
+        if (now - last_active < spin_ns) {
+          spinning_.store(true);
+          timeout = 0;
+        } else {
+          spinning_.store(false);
+          if (pending_.load()) timeout = 0;  // a hand-off raced with the transition
+        }
+      }
+      const int n = epoll_wait(epfd_, evs, 256, timeout);
+      if (spin_ns > 0) {
+        if (n > 0) last_active = mono_ns();
+        if (pending_.load()) {
+          pending_.store(false);
+          drain_pending();
+          last_active = mono_ns();
+        }
+      }
       for (int i = 0; i < n; ++i) {
         const uint64_t id = evs[i].data.u64;
         if (id == ID_LISTEN) {
@@ -438,6 +472,7 @@ class IoThread : public Sink {
           ssize_t r = read(evfd_, &v, sizeof v);
           (void)r;
           signaled_.store(false);
+          pending_.store(false);
           drain_pending();
         } else {
           auto it = conns_.find(id);
@@ -947,6 +982,8 @@ class IoThread : public Sink {
   std::thread th_;
   std::atomic<bool> stop_{false};
   std::atomic<bool> signaled_{false};
+  std::atomic<bool> pending_{false};   // completions / slow responses queued for this thread
+  std::atomic<bool> spinning_{false};  // inside the busy-poll window (no eventfd needed)
   std::mutex mu_;
   std::vector<FastBatch> fast_;
   std::vector<SlowResp> slow_;

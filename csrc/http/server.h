@@ -49,6 +49,10 @@ struct ServerConfig {
   // re-admits the rank once a batch succeeds again.
   bool health_dispatch = false;
   int health_probe_ms = 100;
+  // Busy-poll window: after activity an IO thread polls epoll (timeout 0) and its completion
+  // queue for this long before blocking, and the engine's completer then hands it batches
+  // without an eventfd write (no wake-up on the request path). 0 = always block.
+  int io_spin_us = 0;
 };
 
 struct SlowRequest {

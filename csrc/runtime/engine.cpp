@@ -590,6 +590,7 @@ void Engine::batcher_loop() {
       {
         std::lock_guard<std::mutex> lk(s_mu_);
         inflight_.push_back(si);
+        inflight_n_.fetch_add(1, std::memory_order_release);
       }
       s_cv_.notify_all();
     }
@@ -610,12 +611,18 @@ void Engine::completer_loop() {
   std::vector<double> pd;
   for (;;) {
     int si;
+    if (cfg_.spin_us > 0 && inflight_n_.load(std::memory_order_acquire) == 0) {
+      // as the batcher: poll for the next launched batch before paying a futex wake
+      const int64_t until = now_ns() + (int64_t)cfg_.spin_us * 1000;
+      while (inflight_n_.load(std::memory_order_acquire) == 0 && now_ns() < until) _mm_pause();
+    }
     {
       std::unique_lock<std::mutex> lk(s_mu_);
       s_cv_.wait(lk, [&] { return !inflight_.empty() || batcher_done_; });
       if (inflight_.empty()) break;  // batcher has exited and nothing is in flight
       si = inflight_.front();
       inflight_.pop_front();
+      inflight_n_.fetch_sub(1, std::memory_order_relaxed);
     }
     Slot& s = slots_[si];
     if (s.launched) {

@@ -108,7 +108,7 @@ struct EngineConfig {
   int watchdog_ms = 2000; // batch not complete after this -> engine marked unhealthy
   int fail_every = 0;     // fault injection: fail every N-th batch with ST_DEVICE_ERROR
   int delay_us = 0;       // fault injection: extra per-batch delay
-  int spin_us = 0;        // batcher polls the queue this long before sleeping on the condvar
+  int spin_us = 0;        // batcher / completer poll their queues this long before sleeping on a condvar
                           // (saves the futex wake-up on the request path under load)
   int max_queue = 1 << 20;  // backpressure: rows waiting for the batcher; beyond it submit is refused
 };
@@ -222,6 +222,7 @@ class Engine {
   std::condition_variable s_cv_;
   std::deque<int> free_slots_;
   std::deque<int> inflight_;
+  std::atomic<int> inflight_n_{0};  // inflight_.size(), readable without s_mu_ (completer spin)
   bool batcher_done_ = false;
 
   size_t slot_row_bytes_ = 0;  // capacity of one packed row in a slot (any path)

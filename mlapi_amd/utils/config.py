@@ -38,7 +38,8 @@ class Config:
     watchdog_ms: int = 2000
     fail_every: int = 0                       # fault injection (tests): fail every N-th batch
     delay_us: int = 0                         # fault injection: delay every batch
-    spin_us: int = 0                          # batcher spin before sleeping (0 = always sleep)
+    spin_us: int = 0                          # batcher / completer spin before sleeping (0 = always sleep)
+    io_spin_us: int = 0                       # IO threads busy-poll this long after activity (0 = block)
     max_queue: int = 1 << 20                  # backpressure: queued rows beyond this -> HTTP 503
     inline_args: bool = True                  # GPU: tiny batches travel in the kernel-argument block
     stage_wide: bool = False                  # GPU: copy wide models' rows H2D first (default: zero-copy reads)

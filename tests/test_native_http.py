@@ -19,12 +19,15 @@ NAMES = ["sepal_length", "sepal_width", "petal_length", "petal_width"]
 A1 = b'{"sepal_length":5.1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}'
 
 
-@pytest.fixture
-def server(iris_cwd):
+@pytest.fixture(params=[0, 200], ids=["block", "spin"])
+def server(iris_cwd, request):
+    """Blocking IO threads, and busy-polling IO threads + spinning batcher / completer (the
+    completion hand-off then skips the eventfd)."""
     from mlapi_amd.serve.server import NativeServer
     from mlapi_amd.utils.config import Config
 
-    srv = NativeServer(Config.from_env(port=0, device="cpu", io_threads=2)).start()
+    srv = NativeServer(Config.from_env(port=0, device="cpu", io_threads=2, io_spin_us=request.param,
+                                       spin_us=request.param)).start()
     yield srv
     srv.stop()
 
