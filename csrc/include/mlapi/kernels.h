@@ -60,8 +60,7 @@ void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_
 // (0 when the row-group kernel serves the shape).
 size_t gemm_softmax_workspace(int64_t B, int K, int F);
 // Benchmark hook: force the tiles kernel's (rows-per-wave tiles, class splits) plan and the
-// kernel (0 automatic, 1 tiles 16x16x32, 2 row-group, 3 / 4 tiles 32x32x16 with 4 / 8 waves per
-// block); all 0 = automatic.
+// kernel (0 automatic, 1 tiles 16x16x32, 2 row-group, 3 tiles 32x32x16); all 0 = automatic.
 void gemm_softmax_force_plan(int nt, int splits, int kernel = 0);
 // Profiling hook: tiles launches write 4 s_memtime stamps per wave to this device buffer
 // (tools/gemm_phase_probe.py); nullptr = off (default).

@@ -770,19 +770,24 @@ __device__ __forceinline__ void bias32(const float* bias_lds, int c0, int c_end,
   }
 }
 
-template <int KS>
-__device__ __forceinline__ void mfma32_chunk(const unsigned char* wb, const bf16x8_t (&xf)[2 * KS], int c0, int c_end,
-                                             int h, int col, f32x16_t (&acc)[2]) {
+template <int KS, int RT>
+__device__ __forceinline__ void mfma32_chunk(const unsigned char* wb, const bf16x8_t (&xf)[RT][2 * KS], int c0,
+                                             int c_end, int h, int col, f32x16_t (&acc)[RT][2]) {
   f32x16_t bt[2];
   bias32(reinterpret_cast<const float*>(wb + CLASS_CHUNK * lds_row_stride<KS>()), c0, c_end, h, bt);
-  acc[0] = bt[0];
-  acc[1] = bt[1];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    acc[rt][0] = bt[0];
+    acc[rt][1] = bt[1];
+  }
 #pragma unroll
   for (int k = 0; k < 2 * KS; ++k) {
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) {
       const bf16x8_t wf = *reinterpret_cast<const bf16x8_t*>(wb + lds_off<KS>(ct * 32 + col, 2 * k + h));
-      acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xf[k], acc[ct], 0, 0, 0);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+        acc[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf, xf[rt][k], acc[rt][ct], 0, 0, 0);
     }
   }
 }
@@ -815,23 +820,29 @@ __device__ __forceinline__ bf16x8_t frag32(const unsigned char* smem, const Frag
 
 // MFMAs of chunk cn (LDS buffer BUF -> nxt) with the epilogue of chunk c0 (acc -> S) spread over
 // the k-steps
-template <int KS, bool OVR, int BUF, int BUF_BYTES>
+template <int KS, int RT, bool OVR, int BUF, int BUF_BYTES>
 __device__ __forceinline__ void fused32_step(const unsigned char* smem, const FragOff<KS>& fo,
-                                             const bf16x8_t (&xf)[2 * KS], int cn, int c_end, int h,
-                                             f32x16_t (&nxt)[2], const f32x16_t (&acc)[2], int c0, TileState& S) {
+                                             const bf16x8_t (&xf)[RT][2 * KS], int cn, int c_end, int h,
+                                             f32x16_t (&nxt)[RT][2], const f32x16_t (&acc)[RT][2], int c0,
+                                             TileState (&S)[RT]) {
   f32x16_t bt[2];
   bias32(reinterpret_cast<const float*>(smem + BUF * BUF_BYTES + CLASS_CHUNK * lds_row_stride<KS>()), cn, c_end, h,
          bt);
-  nxt[0] = bt[0];
-  nxt[1] = bt[1];
-  float v[2][16];
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct)
+  for (int rt = 0; rt < RT; ++rt) {
+    nxt[rt][0] = bt[0];
+    nxt[rt][1] = bt[1];
+  }
+  float v[RT][2][16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[ct][i] = acc[ct][i];
-  TileTmp7 T[2];
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[rt][ct][i] = acc[rt][ct][i];
+  TileTmp7 T[RT][2];
   constexpr int K2 = 2 * KS;
-  constexpr int NSTAGE = 14;  // 7 per tile; tile 1 follows tile 0 (same row state)
+  constexpr int NSTAGE = 14 * RT;  // 7 per class tile; class tile 1 follows tile 0 (same row state)
   // W fragments one k-step ahead in registers: the reads of step k+1 issue before the MFMAs of
   // step k (a 64-cycle MFMA pair of cover for the LDS latency); the scheduling barriers pin them
   // there (left free, hipcc sank every read next to its MFMA).
@@ -847,32 +858,40 @@ __device__ __forceinline__ void fused32_step(const unsigned char* smem, const Fr
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
-      nxt[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k & 1][ct], xf[k], nxt[ct], 0, 0, 0);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+        nxt[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k & 1][ct], xf[rt][k], nxt[rt][ct], 0, 0, 0);
     static_for<NSTAGE>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       if constexpr ((j * K2) / NSTAGE == k) {
-        constexpr int t = j / 7, stg = j % 7;
-        tile_stage7<OVR>(stg, v[t], c0 + 32 * t, S, T[t]);
+        constexpr int rt = j / 14, t = (j % 14) / 7, stg = j % 7;
+        tile_stage7<OVR>(stg, v[rt][t], c0 + 32 * t, S[rt], T[rt][t]);
       }
     });
     __builtin_amdgcn_sched_barrier(0);
   });
 }
 
-template <bool OVR>
-__device__ __forceinline__ void epilogue32(const f32x16_t (&acc)[2], int c0, TileState& ts) {
+template <bool OVR, int RT>
+__device__ __forceinline__ void epilogue32(const f32x16_t (&acc)[RT][2], int c0, TileState (&ts)[RT]) {
   float v[16];
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = acc[ct][i];
-    tile_update<OVR>(v, c0 + 32 * ct, ts);
-  }
+    for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = acc[rt][ct][i];
+      tile_update<OVR>(v, c0 + 32 * ct, ts[rt]);
+    }
 }
 
-template <int KS, int WV, int MODE, bool OVR>
-__global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_softmax32_kernel(
-    GemmArgs a) {
+// RT = 32-row tiles per wave. RT = 1 (two waves per SIMD) is the one launched: RT = 2 (one wave per
+// SIMD, 64 rows, each W fragment feeding 4 MFMAs) needs 412 registers, pays ~90 AGPR reads per
+// chunk and measured 26% slower at B = 262144 (loop 69.5k cycles per 64 rows vs 52.7k for two
+// 32-row waves; profiles/r2_gemm/phase_probe_rt2.log).
+template <int KS, int WV, int RT, int MODE, bool OVR>
+__global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(RT == 2 ? 1 : 2, RT == 2 ? 1 : 2))) void
+gemm_softmax32_kernel(GemmArgs a) {
   static_assert(MODE == 0 || MODE == 2 || MODE == 4, "logits mode runs the 16x16 kernel");
   const uint16_t* __restrict__ X = a.X;
   const uint16_t* __restrict__ W = a.W;
@@ -882,7 +901,7 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int classes_per_split = a.classes_per_split;
   constexpr int K2 = 2 * KS;
   constexpr int NTHR = 64 * WV;
-  constexpr int ROWS_PER_BLOCK = 32 * WV;
+  constexpr int ROWS_PER_BLOCK = 32 * RT * WV;
   constexpr int F_ = KS * 32;
   constexpr int NCH = F_ / 8;
   constexpr int W_BYTES = CLASS_CHUNK * lds_row_stride<KS>();
@@ -899,7 +918,7 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const int h = lane >> 5;
   const int col = lane & 31;
   constexpr bool ovr = OVR;
-  const int64_t row0 = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wave * 32;
+  const int64_t row0 = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wave * 32 * RT;
   const int c_begin = blockIdx.y * classes_per_split;
   const int c_end = min(K, c_begin + classes_per_split);
   phase_stamp(a, WV, wave, lane, 0);
@@ -921,16 +940,19 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(2, 2)))
   __builtin_amdgcn_s_barrier();  \
   asm volatile("" ::: "memory");
 
-  TileState ts;
-  tile_init(ts);
-  bf16x8_t xf[K2];
+  TileState ts[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) tile_init(ts[rt]);
+  bf16x8_t xf[RT][K2];
   MLAPI_DMA32(c_begin, 0)
-  {
-    int64_t r = row0 + col;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    int64_t r = row0 + rt * 32 + col;
     r = r < B ? r : B - 1;
     const uint16_t* xr = X + r * a.ldx + 8 * h;
 #pragma unroll
-    for (int k = 0; k < K2; ++k) xf[k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + k * 16));
+    for (int k = 0; k < K2; ++k)
+      xf[rt][k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + k * 16));
   }
   constexpr int kWaitAll = (7 << 4) | (15 << 8);
   __builtin_amdgcn_s_waitcnt(kWaitAll);  // chunk 0 + X
@@ -938,8 +960,8 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(2, 2)))
   phase_stamp(a, WV, wave, lane, 1);
   if (c_begin + CLASS_CHUNK < c_end) MLAPI_DMA32(c_begin + CLASS_CHUNK, 1)
   const FragOff<KS> fo = frag_offsets<KS>(h, col);
-  f32x16_t accA[2], accB[2];
-  mfma32_chunk<KS>(smem, xf, c_begin, c_end, h, col, accA);
+  f32x16_t accA[RT][2], accB[RT][2];
+  mfma32_chunk<KS, RT>(smem, xf, c_begin, c_end, h, col, accA);
   // Unrolled by the two LDS buffers: chunk c (in accA, buffer 0) / c+1 (accB, buffer 1) swap roles
   // each half, so the buffer offsets are immediates and no accumulator is copied.
   unsigned long long waited = 0;  // profiling only (a.stamps)
@@ -953,20 +975,20 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(2, 2)))
   }
   for (int c0 = c_begin;;) {
     if (c0 + CLASS_CHUNK >= c_end) {
-      epilogue32<OVR>(accA, c0, ts);
+      epilogue32<OVR, RT>(accA, c0, ts);
       break;
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 0)
-    fused32_step<KS, OVR, 1, BUF_BYTES>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0, ts);
+    fused32_step<KS, RT, OVR, 1, BUF_BYTES>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0, ts);
     c0 += CLASS_CHUNK;
     if (c0 + CLASS_CHUNK >= c_end) {
-      epilogue32<OVR>(accB, c0, ts);
+      epilogue32<OVR, RT>(accB, c0, ts);
       break;
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 1)
-    fused32_step<KS, OVR, 0, BUF_BYTES>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0, ts);
+    fused32_step<KS, RT, OVR, 0, BUF_BYTES>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0, ts);
     c0 += CLASS_CHUNK;
   }
 #undef MLAPI_WAIT_BARRIER32
@@ -974,32 +996,43 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #undef MLAPI_DMA32
   phase_stamp(a, WV, wave, lane, 2);
   if (prof) phase_put(a, WV, wave, lane, 4, waited);
-  RowState S = tile_result32(ts, h);
-  S = merge_state(S, shfl_state(S, 32), ovr);
+  RowState S[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    S[rt] = tile_result32(ts[rt], h);
+    S[rt] = merge_state(S[rt], shfl_state(S[rt], 32), ovr);
+  }
   phase_stamp(a, WV, wave, lane, 3);
-  const int64_t row = row0 + col;
   if (gridDim.y == 1) {
-    if (h == 0 && row < B) {
-      if constexpr (MODE == 0) {
-        a.out_idx[row] = S.bi;
-        a.out_p[row] = ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s;
-      } else if constexpr (MODE == 4) {
-        a.rowstate[row] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
-      } else {
-        a.rowstat[row] = make_float2(S.m + __logf(S.s), __int_as_float(S.bi));
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int64_t row = row0 + rt * 32 + col;
+      if (h == 0 && row < B) {
+        if constexpr (MODE == 0) {
+          a.out_idx[row] = S[rt].bi;
+          a.out_p[row] = ovr ? sigmoidf_(S[rt].m) / S[rt].s : 1.f / S[rt].s;
+        } else if constexpr (MODE == 4) {
+          a.rowstate[row] = make_float4(S[rt].m, S[rt].s, __int_as_float(S[rt].bi), 0.f);
+        } else {
+          a.rowstat[row] = make_float2(S[rt].m + __logf(S[rt].s), __int_as_float(S[rt].bi));
+        }
       }
     }
     return;
   }
   // split classes: the 16x16 kernel's publish / last-arriver merge (see there)
-  if (h == 0 && row < B) {
-    typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-    typedef __attribute__((address_space(1))) unsigned int gu32_t;
-    float4* dst = a.partials + (int64_t)blockIdx.y * B + row;
-    const unsigned long long ms =
-        (unsigned long long)__float_as_uint(S.m) | ((unsigned long long)__float_as_uint(S.s) << 32);
-    __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S.bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int64_t row = row0 + rt * 32 + col;
+    if (h == 0 && row < B) {
+      typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+      typedef __attribute__((address_space(1))) unsigned int gu32_t;
+      float4* dst = a.partials + (int64_t)blockIdx.y * B + row;
+      const unsigned long long ms =
+          (unsigned long long)__float_as_uint(S[rt].m) | ((unsigned long long)__float_as_uint(S[rt].s) << 32);
+      __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S[rt].bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1016,8 +1049,8 @@ __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(2, 2)))
     __hip_atomic_store(&a.counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  if (tid < ROWS_PER_BLOCK) {
-    const int64_t mrow = (int64_t)blockIdx.x * ROWS_PER_BLOCK + tid;
+  for (int mr = tid; mr < ROWS_PER_BLOCK; mr += NTHR) {
+    const int64_t mrow = (int64_t)blockIdx.x * ROWS_PER_BLOCK + mr;
     if (mrow < B) {
       const unsigned ns = gridDim.y;
       float4 p[MERGE_MAX];
@@ -1192,7 +1225,7 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
 // Which kernel serves (B, K, F): the row-group kernel only where the tiles kernel has no
 // instantiation (F > 512, the only kernel that loops F). At F <= 512 the tiles kernel with class
 // splits is faster at every B (profiles/r2_gemm/sweep.log: B <= 4096 rows 17-19 us vs tiles 7-10).
-int g_force_kernel = 0;  // benchmark hook: 0 automatic, 1 tiles 16x16, 2 row-group, 3/4 tiles 32x32 (4/8 waves)
+int g_force_kernel = 0;  // benchmark hook: 0 automatic, 1 tiles 16x16, 2 row-group, 3 tiles 32x32
 
 bool rows_supported(int F) { return F == 32 || F == 64 || F == 128 || F == 256 || (F > 256 && F % 256 == 0); }
 bool tiles_supported(int F) { return F == 32 || F == 64 || F == 128 || F == 256 || F == 512; }
@@ -1255,6 +1288,7 @@ RowsArgs rows_args(const void* X, int64_t ldx, const void* W, const float* b, in
 
 struct Plan {
   int k32 = 0;            // > 0: the 32x32x16 kernel with this many waves per block
+  int rt32 = 1;           // its 32-row tiles per wave
   int nt;                 // 16-row tiles per wave (16x16x32 kernel)
   int splits;
   int classes_per_split;
@@ -1276,7 +1310,7 @@ bool t32_supported(int F) { return F == 64 || F == 128 || F == 256; }
 Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   Plan p;
   if (allow32 && t32_supported(F)) {
-    if (g_force_kernel == 3 || g_force_kernel == 4) p.k32 = 4;
+    if (g_force_kernel == 3) p.k32 = 4;
     else if (g_force_kernel == 0 && B >= 16384) p.k32 = 4;
   }
   // 32 rows per wave (NT = 2) halve the LDS fragment reads per MFMA. It pays once the register
@@ -1287,7 +1321,7 @@ Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   p.nt = (F <= 256 && B >= 16384) ? 2 : 1;
   if (g_force_nt == 1 || g_force_nt == 2) p.nt = g_force_nt;
   if (g_force_splits > 0) {
-    const int rows_per_block = p.k32 ? 32 * p.k32 : block_rows(F, p.nt);
+    const int rows_per_block = p.k32 ? 32 * p.rt32 * p.k32 : block_rows(F, p.nt);
     p.row_blocks = (B + rows_per_block - 1) / rows_per_block;
     const int chunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
     const int sp = g_force_splits > chunks ? chunks : g_force_splits;
@@ -1295,7 +1329,7 @@ Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
     p.splits = (K + p.classes_per_split - 1) / p.classes_per_split;
     if (!(p.splits > 1 && p.row_blocks * 4 > COUNTER_BYTES)) return p;
   }
-  const int rows_per_block = p.k32 ? 32 * p.k32 : block_rows(F, p.nt);
+  const int rows_per_block = p.k32 ? 32 * p.rt32 * p.k32 : block_rows(F, p.nt);
   p.row_blocks = (B + rows_per_block - 1) / rows_per_block;
   const int chunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
   // measured best: B=1024 -> 8 splits (128 blocks), B=8192 -> 4 (512 blocks): fill the chip, but
@@ -1314,12 +1348,14 @@ Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
 }
 
 template <int MODE, int KS>
-void launch32(const GemmArgs& args, const dim3& grid, int wv, hipStream_t stream) {
+void launch32(const GemmArgs& args, const dim3& grid, int rt, hipStream_t stream) {
   if constexpr (MODE != 1) {
+    // 4 waves per block, 1 row tile per wave (8-wave blocks and RT = 2 measured slower:
+    // profiles/r2_gemm/phase_probe_rt2.log)
+    (void)rt;
     const bool o = args.kind == KIND_OVR;
-    (void)wv;  // 4 waves per block (2 blocks per CU); the 8-wave variant measured slower
-    if (o) hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, MODE, true>), grid, dim3(256), 0, stream, args);
-    else hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, MODE, false>), grid, dim3(256), 0, stream, args);
+    if (o) hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, true>), grid, dim3(256), 0, stream, args);
+    else hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false>), grid, dim3(256), 0, stream, args);
   }
 }
 
@@ -1331,9 +1367,9 @@ void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
   args.classes_per_split = plan.classes_per_split;
   args.stamps = static_cast<unsigned long long*>(g_stamps);
   if (MODE != 1 && plan.k32) {
-    if (F == 64) launch32<MODE, 2>(args, grid, plan.k32, stream);
-    else if (F == 128) launch32<MODE, 4>(args, grid, plan.k32, stream);
-    else launch32<MODE, 8>(args, grid, plan.k32, stream);
+    if (F == 64) launch32<MODE, 2>(args, grid, plan.rt32, stream);
+    else if (F == 128) launch32<MODE, 4>(args, grid, plan.rt32, stream);
+    else launch32<MODE, 8>(args, grid, plan.rt32, stream);
     MLAPI_HIP_CHECK(hipGetLastError());
     return;
   }

@@ -82,11 +82,11 @@ def test_gemv_binary_large_stream():
     torch.testing.assert_close(p, torch.sigmoid(z.abs()), rtol=1e-4, atol=1e-4)
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["auto", "tiles", "rows", "t32w4", "t32w8"])
+@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "tiles", "rows", "t32"])
 def gemm_kernel(request):
     """Run a multiclass test under the automatic plan and with each kernel forced (tiles: the
-    LDS-staged, chunk-pipelined 16x16x32 kernel; rows: the row-group kernel; t32w4 / t32w8: the
-    32x32x16 large-batch kernel with 4 / 8 waves per block, F in {64, 128, 256}, else tiles)."""
+    LDS-staged, chunk-pipelined 16x16x32 kernel; rows: the row-group kernel; t32: the 32x32x16
+    large-batch kernel, F in {64, 128, 256}, else tiles)."""
     from mlapi_amd._native import C
 
     C().gemm_softmax_force_plan(0, 0, request.param)
