@@ -530,8 +530,15 @@ gemm_softmax_kernel(GemmArgs a) {
     r = r < B ? r : B - 1;
     const uint16_t* xr = X + r * a.ldx + 8 * q;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)  // X is streamed once: non-temporal, keep the L2 for W
-      xf[t][ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + ks * 32));
+    for (int ks = 0; ks < KS; ++ks) {
+      // Large batches (NT = 2) stream X once: non-temporal, keep the L2 for W. Small batches split
+      // the classes, and every split block of a row block (same XCD: blockIdx.x + 16y = x mod 8)
+      // re-reads the same X rows, so those loads stay cacheable.
+      if constexpr (NT == 2)
+        xf[t][ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + ks * 32));
+      else
+        xf[t][ks] = *reinterpret_cast<const bf16x8_t*>(xr + ks * 32);
+    }
   }
   // (the builtin form of s_waitcnt is visible to the compiler's wait insertion; encoding:
   // vmcnt[3:0,15:14], expcnt[6:4], lgkmcnt[11:8] with the other two counters left at "no wait")

@@ -55,6 +55,9 @@ for (bench, k), cs in sorted(vals.items()):
           f"{pct('SQ_WAIT_ANY'):.0f} | {pct('SQ_WAIT_INST_ANY'):.0f} | {pct('SQ_ACTIVE_INST_VALU'):.0f} | "
           f"{pct('SQ_ACTIVE_INST_LDS'):.0f} | {pct('SQ_ACTIVE_INST_VMEM'):.0f} | {waves:.0f} |")
 print()
+# MFMA busy %: SQ_VALU_MFMA_BUSY_CYCLES is summed over all 1024 SIMDs, SQ_BUSY_CYCLES over the 32
+# shader engines (8 XCDs x 4), so busy / (1024 x SQ_BUSY / 32) = busy / (32 x SQ_BUSY).
+SE_COUNT = 32
 print("| bench | kernel | L2 hit % | LDS-wait % | MFMA busy % | MISC-active % | SALU instr/wave |")
 print("|---|---|---|---|---|---|---|")
 for (bench, k), cs in sorted(vals.items()):
@@ -70,7 +73,7 @@ for (bench, k), cs in sorted(vals.items()):
         return 100 * mean(cs.get(c, [])) / wcyc if wcyc == wcyc and wcyc else float("nan")
 
     print(f"| {bench} | `{name}` | {100 * hit / (hit + miss) if hit + miss else float('nan'):.1f} | "
-          f"{pc('SQ_WAIT_INST_LDS'):.0f} | {100 * busy / sqb / 4 if sqb == sqb and sqb else float('nan'):.0f} | "
+          f"{pc('SQ_WAIT_INST_LDS'):.0f} | {100 * busy / sqb / SE_COUNT if sqb == sqb and sqb else float('nan'):.0f} | "
           f"{pc('SQ_ACTIVE_INST_MISC'):.0f} | {mean(cs.get('SQ_INSTS_SALU', [])) / waves if waves else float('nan'):.0f} |")
 print()
 print("*HBM GB/s = (FETCH_SIZE + WRITE_SIZE) / kernel time; on gfx950 FETCH_SIZE reads about half of")
