@@ -12,7 +12,10 @@ alternative to ``torchrun`` with what a serving node needs:
   bound: HTTP parsing and JSON rendering run on these cores) and sizes OMP_NUM_THREADS to it; GPU
   ``local_rank`` is selected by the rank itself (all devices stay visible so RCCL can map peers);
 * supervises: the first rank that exits non-zero brings the others down (SIGTERM, then SIGKILL
-  after ``--grace``) and its exit code becomes the launcher's.
+  after ``--grace``) and its exit code becomes the launcher's; with ``--restart N`` a failed rank
+  is instead started again (at most N times per rank) while the others keep running, with
+  ``MLAPI_REPLICA_RESTART=<n>`` in its environment (serving: it comes back as a standalone replica
+  on the shared port, :func:`mlapi_amd.parallel.dp_serve.serve_replica`).
 
 The launcher never touches the GPU itself, so starting the ranks with fork+exec is safe.
 """
@@ -45,9 +48,21 @@ def main(argv=None) -> int:
     ap.add_argument("--master-port", type=int, default=0, help="0 = pick a free port")
     ap.add_argument("--no-pin", action="store_true", help="do not pin ranks to CPU slices")
     ap.add_argument("--grace", type=float, default=10.0, help="seconds between SIGTERM and SIGKILL on failure")
+    ap.add_argument("--restart", type=int, default=0,
+                    help="restart a rank that exits non-zero up to N times instead of stopping the job "
+                         "(serving replicas; training jobs should keep 0)")
     ap.add_argument("-m", dest="module", default=None, help="run a module (like python -m)")
     ap.add_argument("target", nargs=argparse.REMAINDER, help="script.py args... (or module args with -m)")
+    argv = list(sys.argv[1:] if argv is None else argv)
+    module, mod_args = None, []
+    if "-m" in argv:  # everything after `-m MODULE` belongs to the module, like `python -m`
+        i = argv.index("-m")
+        if i + 1 >= len(argv):
+            ap.error("-m needs a module name")
+        module, mod_args, argv = argv[i + 1], argv[i + 2:], argv[:i]
     args = ap.parse_args(argv)
+    if module is not None:
+        args.module, args.target = module, mod_args
 
     nproc = args.nproc
     if nproc <= 0:
@@ -67,17 +82,22 @@ def main(argv=None) -> int:
     store = dist.TCPStore(args.master_addr, port, nproc, is_master=True, wait_for_workers=False,
                           use_libuv=True)
     slices = cpu_slices(nproc)
-    procs: List[subprocess.Popen] = []
-    for r in range(nproc):
+
+    def _spawn(r: int, restart: int = 0) -> subprocess.Popen:
         env = dict(os.environ)
         env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(nproc), "LOCAL_WORLD_SIZE": str(nproc),
                     "GROUP_RANK": "0", "MASTER_ADDR": args.master_addr, "MASTER_PORT": str(port),
                     "TORCHELASTIC_USE_AGENT_STORE": "True", "MLAPI_LAUNCHER": "1"})
+        if restart:
+            env["MLAPI_REPLICA_RESTART"] = str(restart)
         cpus = slices[r]
         if not args.no_pin:
             env["OMP_NUM_THREADS"] = str(max(1, len(cpus)))
         pre = (lambda c=cpus: os.sched_setaffinity(0, c)) if not args.no_pin else None
-        procs.append(subprocess.Popen(cmd, env=env, preexec_fn=pre))
+        return subprocess.Popen(cmd, env=env, preexec_fn=pre)
+
+    procs: List[subprocess.Popen] = [_spawn(r) for r in range(nproc)]
+    restarts = [0] * nproc
 
     def _terminate(sig=signal.SIGTERM):
         for p in procs:
@@ -92,13 +112,19 @@ def main(argv=None) -> int:
     try:
         while True:
             alive = 0
-            for p in procs:
+            for i, p in enumerate(procs):
                 rc = p.poll()
                 if rc is None:
                     alive += 1
+                elif rc != 0 and code == 0 and restarts[i] < args.restart:
+                    restarts[i] += 1
+                    print(f"[mlapi_amd.launch] rank {i} exited with {rc}; restart {restarts[i]}/{args.restart}",
+                          file=sys.stderr, flush=True)
+                    procs[i] = _spawn(i, restarts[i])
+                    alive += 1
                 elif rc != 0 and code == 0:
                     code = rc if rc > 0 else 128 - rc
-                    print(f"[mlapi_amd.launch] rank {procs.index(p)} exited with {rc}; stopping the job",
+                    print(f"[mlapi_amd.launch] rank {i} exited with {rc}; stopping the job",
                           file=sys.stderr, flush=True)
                     _terminate()
                     deadline = time.monotonic() + args.grace

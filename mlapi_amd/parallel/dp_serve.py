@@ -13,6 +13,12 @@
   host side) every ``reload_interval_ms``; when rank 0 has seen the file change (or any rank got
   ``POST /admin/reload``), all ranks enter the same RCCL broadcast and swap models atomically.
   A deleted checkpoint is broadcast as "no model" and every replica answers 500 (A16).
+* Replica restart (``python -m mlapi_amd.launch --restart N``): a replica that dies is started
+  again by the launcher with ``MLAPI_REPLICA_RESTART`` set. It cannot rejoin the survivors' RCCL /
+  gloo groups, so it comes back as a standalone replica (:func:`serve_replica`): it reads the
+  checkpoint itself, joins the same SO_REUSEPORT port and watches the file on its own. The
+  survivors' reload controller sees its control group break at the next tick and falls back to
+  per-rank file watching, so "replace the file, the served model changes" keeps holding.
 """
 from __future__ import annotations
 
@@ -46,6 +52,7 @@ class DPReloadController:
         self.request = threading.Event()
         self._stop = threading.Event()
         self._key = None
+        self.degraded = False
         self._thread: Optional[threading.Thread] = None
 
     def _file_key(self):
@@ -69,8 +76,19 @@ class DPReloadController:
         while not self._stop.wait(self.interval):
             try:
                 self.tick()
-            except Exception:  # pragma: no cover - never kill the control thread
-                log.exception("dp reload tick")
+            except Exception as e:  # a peer left the control group (crashed / restarted replica)
+                self.degrade(e)
+                return
+
+    def degrade(self, err: Exception) -> None:
+        """The control group is broken: keep serving and reload from the file locally instead."""
+        log.warning("rank %d: DP reload group failed (%s); falling back to per-rank file watching",
+                    self.info.rank, err)
+        self.degraded = True
+        st = self.rt.store
+        st.reload = self.rt.config.reload
+        st._key = self._key if self._key is not None else ("unchecked",)
+        st.start_watcher(self.rt.config.reload_interval_ms)
 
     def tick(self) -> None:
         req = 1 if self.request.is_set() else 0
@@ -149,6 +167,21 @@ def start_dp_runtime(cfg: Config, info: Optional[DistInfo] = None):
     return rt, ctl, key, info
 
 
+def serve_replica(cfg: Config, port_stride: int = 0) -> int:
+    """A restarted replica (``MLAPI_REPLICA_RESTART``): standalone on this rank's GPU and port."""
+    from mlapi_amd.serve.server import NativeServer
+    from mlapi_amd.serve.service import ServingRuntime
+
+    rank = int(os.environ.get("RANK", "0"))
+    # device "auto" resolves to this rank's GPU through LOCAL_RANK (Config.device_index)
+    rcfg = Config.from_env(**{**cfg.__dict__, "port": cfg.port + port_stride * rank, "reuseport": True})
+    srv = NativeServer(rcfg, runtime=ServingRuntime(rcfg))
+    log.warning("rank %d restarted (%s): standalone replica on port %d", rank,
+                os.environ.get("MLAPI_REPLICA_RESTART"), srv.port)
+    srv.serve_forever()
+    return 0
+
+
 def serve_dp(cfg: Config, port_stride: int = 0) -> int:
     from mlapi_amd.serve.server import NativeServer
 
@@ -156,6 +189,9 @@ def serve_dp(cfg: Config, port_stride: int = 0) -> int:
     cfg_r = Config.from_env(**{**cfg.__dict__, "port": cfg.port + port_stride * info.rank, "reuseport": True})
     srv = NativeServer(cfg_r, runtime=rt)
     ctl.start(key)
+    if cfg.fault_exit_rank == info.rank:  # fault injection: a replica process dies while serving
+        log.warning("rank %d: fault injection, exiting in %d ms", info.rank, cfg.fault_exit_after_ms)
+        threading.Timer(cfg.fault_exit_after_ms / 1000.0, lambda: os._exit(3)).start()
     log.info("rank %d/%d serving on port %d (%s)", info.rank, info.world, srv.port, rt.handle.backend)
     try:
         srv.serve_forever()

@@ -22,8 +22,10 @@ def main(argv=None) -> int:
     logging.basicConfig(level=getattr(logging, cfg.log_level.upper(), logging.WARNING),
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        from mlapi_amd.parallel.dp_serve import serve_dp
+        from mlapi_amd.parallel.dp_serve import serve_dp, serve_replica
 
+        if os.environ.get("MLAPI_REPLICA_RESTART"):  # relaunched by `mlapi_amd.launch --restart`
+            return serve_replica(cfg)
         return serve_dp(cfg)
     if a.uvicorn:
         import uvicorn

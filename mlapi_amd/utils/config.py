@@ -44,6 +44,8 @@ class Config:
     inline_args: bool = True                  # GPU: tiny batches travel in the kernel-argument block
     stage_wide: bool = False                  # GPU: copy wide models' rows H2D first (default: zero-copy reads)
     fault_drop_rank: int = -1                 # fault injection: this DP rank's engine fails every batch
+    fault_exit_rank: int = -1                 # fault injection: this DP rank's process dies (exit 3) ...
+    fault_exit_after_ms: int = 2000           # ... this long after it starts serving (not after a restart)
     pin: str = "auto"                         # CPU pinning per rank: auto (DP without launcher) | on | off
     # HTTP
     host: str = "127.0.0.1"

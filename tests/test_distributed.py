@@ -1,5 +1,6 @@
 """T5: multi-process semantics on CPU with gloo (world_size 2), via torchrun."""
 import json
+import signal
 import os
 import socket
 import subprocess
@@ -263,3 +264,78 @@ def test_dp_health_dispatch_drops_and_readmits_rank(tmp_path, iris_pickle_bytes)
             p.kill()
             out, _ = p.communicate()
     assert p.returncode == 0, out[-3000:]
+
+
+def test_launcher_restarts_a_crashed_replica(tmp_path, iris_pickle_bytes):
+    """`mlapi_amd.launch --restart 1`, 3 CPU serving ranks on one port: rank 1 dies while serving
+    (fault injection). Clients keep getting 200s from the survivors, the launcher brings rank 1 back
+    as a standalone replica, and a replaced checkpoint is then picked up by every replica (the
+    survivors' broken reload group falls back to per-rank file watching)."""
+    from mlapi_amd.models.linear import LinearModel
+
+    (tmp_path / "LRClassifier.pkl").write_bytes(iris_pickle_bytes)
+    port = free_port()
+    cmd = [sys.executable, "-m", "mlapi_amd.launch", "--nproc", "3", "--no-pin", "--restart", "1", "-m",
+           "mlapi_amd.serve", "--device", "cpu", "--port", str(port), "--io-threads", "1",
+           "--reload-interval-ms", "50"]
+    env = {**ENV, "MLAPI_FAULT_EXIT_RANK": "1", "MLAPI_FAULT_EXIT_AFTER_MS": "1500",
+           "PYTHONPATH": str(ROOT)}
+    p = subprocess.Popen(cmd, env=env, cwd=str(tmp_path), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    body = b'{"sepal_length":5.1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}'
+    try:
+        t0 = time.time()
+        while True:  # up
+            assert p.poll() is None, p.stdout.read()
+            assert time.time() - t0 < 90
+            try:
+                if _post_new_conn(port, body) == 200:
+                    break
+            except OSError:
+                time.sleep(0.2)
+        codes = []
+        t0 = time.time()
+        while time.time() - t0 < 8:  # across the crash and the restart
+            try:
+                codes.append(_post_new_conn(port, body))
+            except OSError:
+                codes.append(-1)  # a connection the dying rank had accepted
+            time.sleep(0.01)
+        assert p.poll() is None, "the launcher must keep the job alive"
+        ok = codes.count(200)
+        assert ok >= 0.97 * len(codes), {c: codes.count(c) for c in set(codes)}
+        # hot reload after the restart: a model that always answers class 2 ("Iris-virginica")
+        W = np.zeros((3, 4))
+        b = np.array([0.0, 0.0, 5.0])
+        m = LinearModel(W=W, b=b, classes=np.array(["Iris-setosa", "Iris-versicolor", "Iris-virginica"]),
+                        kind=2)
+        from mlapi_amd.ckpt.sklearn_pickle import export_sklearn_pickle
+
+        export_sklearn_pickle(m, str(tmp_path / "new.pkl"))
+        os.replace(tmp_path / "new.pkl", tmp_path / "LRClassifier.pkl")
+        t0 = time.time()
+        while True:
+            labels = []
+            for _ in range(60):
+                s = socket.create_connection(("127.0.0.1", port), timeout=10)
+                s.sendall(b"POST /predict HTTP/1.1\r\nHost: t\r\nContent-Type: application/json\r\n"
+                          b"Connection: close\r\nContent-Length: %d\r\n\r\n%s" % (len(body), body))
+                data = b""
+                while True:
+                    c = s.recv(65536)
+                    if not c:
+                        break
+                    data += c
+                s.close()
+                labels.append(json.loads(data.split(b"\r\n\r\n", 1)[1])["prediction"])
+            if labels == ["Iris-virginica"] * 60:
+                break
+            assert time.time() - t0 < 20, labels
+            time.sleep(0.2)
+    finally:
+        p.send_signal(signal.SIGTERM)
+        try:
+            out, _ = p.communicate(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+    assert "restart 1/1" in out, out[-3000:]
