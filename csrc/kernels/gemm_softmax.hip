@@ -827,7 +827,7 @@ __device__ __forceinline__ bf16x8_t frag32(const unsigned char* smem, const Frag
 
 // MFMAs of chunk cn (LDS buffer BUF -> nxt) with the epilogue of chunk c0 (acc -> S) spread over
 // the k-steps
-template <int KS, int RT, bool OVR, int BUF, int BUF_BYTES>
+template <int KS, int RT, bool OVR, int BUF, int BUF_BYTES, bool EPI = true>
 __device__ __forceinline__ void fused32_step(const unsigned char* smem, const FragOff<KS>& fo,
                                              const bf16x8_t (&xf)[RT][2 * KS], int cn, int c_end, int h,
                                              f32x16_t (&nxt)[RT][2], const f32x16_t (&acc)[RT][2], int c0,
@@ -872,7 +872,7 @@ __device__ __forceinline__ void fused32_step(const unsigned char* smem, const Fr
       constexpr int j = decltype(jc)::value;
       if constexpr ((j * K2) / NSTAGE == k) {
         constexpr int rt = j / 14, t = (j % 14) / 7, stg = j % 7;
-        tile_stage7<OVR>(stg, v[rt][t], c0 + 32 * t, S[rt], T[rt][t]);
+        if constexpr (EPI) tile_stage7<OVR>(stg, v[rt][t], c0 + 32 * t, S[rt], T[rt][t]);
       }
     });
     __builtin_amdgcn_sched_barrier(0);
@@ -896,7 +896,11 @@ __device__ __forceinline__ void epilogue32(const f32x16_t (&acc)[RT][2], int c0,
 // SIMD, 64 rows, each W fragment feeding 4 MFMAs) needs 412 registers, pays ~90 AGPR reads per
 // chunk and measured 26% slower at B = 262144 (loop 69.5k cycles per 64 rows vs 52.7k for two
 // 32-row waves; profiles/r2_gemm/phase_probe_rt2.log).
-template <int KS, int WV, int RT, int MODE, bool OVR>
+// EPI = false: the softmax epilogue compiled out (measurement only: forced kernel 5 in
+// tools/gemm_phase_probe.py; its outputs are meaningless). It splits the class loop's time into the
+// MFMA / LDS feed and the epilogue: 44.4k of 52.2k cycles per wave are the feed
+// (profiles/r2_gemm/phase_probe_noepi.log).
+template <int KS, int WV, int RT, int MODE, bool OVR, bool EPI = true>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(RT == 2 ? 1 : 2, RT == 2 ? 1 : 2))) void
 gemm_softmax32_kernel(GemmArgs a) {
   static_assert(MODE == 0 || MODE == 2 || MODE == 4, "logits mode runs the 16x16 kernel");
@@ -987,7 +991,7 @@ gemm_softmax32_kernel(GemmArgs a) {
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 0)
-    fused32_step<KS, RT, OVR, 1, BUF_BYTES>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0, ts);
+    fused32_step<KS, RT, OVR, 1, BUF_BYTES, EPI>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0, ts);
     c0 += CLASS_CHUNK;
     if (c0 + CLASS_CHUNK >= c_end) {
       epilogue32<OVR, RT>(accB, c0, ts);
@@ -995,7 +999,7 @@ gemm_softmax32_kernel(GemmArgs a) {
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 1)
-    fused32_step<KS, RT, OVR, 0, BUF_BYTES>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0, ts);
+    fused32_step<KS, RT, OVR, 0, BUF_BYTES, EPI>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0, ts);
     c0 += CLASS_CHUNK;
   }
 #undef MLAPI_WAIT_BARRIER32
@@ -1233,6 +1237,7 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
 // instantiation (F > 512, the only kernel that loops F). At F <= 512 the tiles kernel with class
 // splits is faster at every B (profiles/r2_gemm/sweep.log: B <= 4096 rows 17-19 us vs tiles 7-10).
 int g_force_kernel = 0;  // benchmark hook: 0 automatic, 1 tiles 16x16, 2 row-group, 3 tiles 32x32
+                         // (5: 32x32 with the epilogue compiled out, measurement only)
 
 bool rows_supported(int F) { return F == 32 || F == 64 || F == 128 || F == 256 || (F > 256 && F % 256 == 0); }
 bool tiles_supported(int F) { return F == 32 || F == 64 || F == 128 || F == 256 || F == 512; }
@@ -1317,7 +1322,7 @@ bool t32_supported(int F) { return F == 64 || F == 128 || F == 256; }
 Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   Plan p;
   if (allow32 && t32_supported(F)) {
-    if (g_force_kernel == 3) p.k32 = 4;
+    if (g_force_kernel == 3 || g_force_kernel == 5) p.k32 = 4;
     else if (g_force_kernel == 0 && B >= 16384) p.k32 = 4;
   }
   // 32 rows per wave (NT = 2) halve the LDS fragment reads per MFMA. It pays once the register
@@ -1361,6 +1366,12 @@ void launch32(const GemmArgs& args, const dim3& grid, int rt, hipStream_t stream
     // profiles/r2_gemm/phase_probe_rt2.log)
     (void)rt;
     const bool o = args.kind == KIND_OVR;
+    if constexpr (MODE == 0 && KS == 8) {
+      if (!o && g_force_kernel == 5) {  // measurement: epilogue compiled out
+        hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, false>), grid, dim3(256), 0, stream, args);
+        return;
+      }
+    }
     if (o) hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, true>), grid, dim3(256), 0, stream, args);
     else hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false>), grid, dim3(256), 0, stream, args);
   }
