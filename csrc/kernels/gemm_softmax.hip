@@ -827,7 +827,7 @@ __device__ __forceinline__ bf16x8_t frag32(const unsigned char* smem, const Frag
 
 // MFMAs of chunk cn (LDS buffer BUF -> nxt) with the epilogue of chunk c0 (acc -> S) spread over
 // the k-steps
-template <int KS, int RT, bool OVR, int BUF, int BUF_BYTES, bool EPI = true>
+template <int KS, int RT, bool OVR, int BUF, int BUF_BYTES, bool EPI = true, int AHEAD = 2>
 __device__ __forceinline__ void fused32_step(const unsigned char* smem, const FragOff<KS>& fo,
                                              const bf16x8_t (&xf)[RT][2 * KS], int cn, int c_end, int h,
                                              f32x16_t (&nxt)[RT][2], const f32x16_t (&acc)[RT][2], int c0,
@@ -853,21 +853,27 @@ __device__ __forceinline__ void fused32_step(const unsigned char* smem, const Fr
   // W fragments one k-step ahead in registers: the reads of step k+1 issue before the MFMAs of
   // step k (a 64-cycle MFMA pair of cover for the LDS latency); the scheduling barriers pin them
   // there (left free, hipcc sank every read next to its MFMA).
-  bf16x8_t wf[2][2];
+  // W fragments AHEAD k-steps in flight ahead of their MFMAs
+  bf16x8_t wf[AHEAD + 1][2];
+  static_for<AHEAD>([&](auto pc) {
+    constexpr int k0 = decltype(pc)::value;
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct) wf[0][ct] = frag32<KS, BUF, BUF_BYTES>(smem, fo, ct, 0);
+    for (int ct = 0; ct < 2; ++ct) wf[k0][ct] = frag32<KS, BUF, BUF_BYTES>(smem, fo, ct, k0);
+  });
   static_for<K2>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
-    if constexpr (k + 1 < K2) {
+    if constexpr (k + AHEAD < K2) {
 #pragma unroll
-      for (int ct = 0; ct < 2; ++ct) wf[(k + 1) & 1][ct] = frag32<KS, BUF, BUF_BYTES>(smem, fo, ct, k + 1);
+      for (int ct = 0; ct < 2; ++ct)
+        wf[(k + AHEAD) % (AHEAD + 1)][ct] = frag32<KS, BUF, BUF_BYTES>(smem, fo, ct, k + AHEAD);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
-        nxt[rt][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k & 1][ct], xf[rt][k], nxt[rt][ct], 0, 0, 0);
+        nxt[rt][ct] =
+            __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k % (AHEAD + 1)][ct], xf[rt][k], nxt[rt][ct], 0, 0, 0);
     static_for<NSTAGE>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       if constexpr ((j * K2) / NSTAGE == k) {
@@ -900,7 +906,7 @@ __device__ __forceinline__ void epilogue32(const f32x16_t (&acc)[RT][2], int c0,
 // tools/gemm_phase_probe.py; its outputs are meaningless). It splits the class loop's time into the
 // MFMA / LDS feed and the epilogue: 44.4k of 52.2k cycles per wave are the feed
 // (profiles/r2_gemm/phase_probe_noepi.log).
-template <int KS, int WV, int RT, int MODE, bool OVR, bool EPI = true>
+template <int KS, int WV, int RT, int MODE, bool OVR, bool EPI = true, int AHEAD = 2>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(RT == 2 ? 1 : 2, RT == 2 ? 1 : 2))) void
 gemm_softmax32_kernel(GemmArgs a) {
   static_assert(MODE == 0 || MODE == 2 || MODE == 4, "logits mode runs the 16x16 kernel");
@@ -991,7 +997,8 @@ gemm_softmax32_kernel(GemmArgs a) {
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 0)
-    fused32_step<KS, RT, OVR, 1, BUF_BYTES, EPI>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0, ts);
+    fused32_step<KS, RT, OVR, 1, BUF_BYTES, EPI, AHEAD>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0,
+                                                        ts);
     c0 += CLASS_CHUNK;
     if (c0 + CLASS_CHUNK >= c_end) {
       epilogue32<OVR, RT>(accB, c0, ts);
@@ -999,7 +1006,8 @@ gemm_softmax32_kernel(GemmArgs a) {
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 1)
-    fused32_step<KS, RT, OVR, 0, BUF_BYTES, EPI>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0, ts);
+    fused32_step<KS, RT, OVR, 0, BUF_BYTES, EPI, AHEAD>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0,
+                                                        ts);
     c0 += CLASS_CHUNK;
   }
 #undef MLAPI_WAIT_BARRIER32
@@ -1237,7 +1245,8 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
 // instantiation (F > 512, the only kernel that loops F). At F <= 512 the tiles kernel with class
 // splits is faster at every B (profiles/r2_gemm/sweep.log: B <= 4096 rows 17-19 us vs tiles 7-10).
 int g_force_kernel = 0;  // benchmark hook: 0 automatic, 1 tiles 16x16, 2 row-group, 3 tiles 32x32
-                         // (5: 32x32 with the epilogue compiled out, measurement only)
+                         // (measurement only: 5 32x32 with the epilogue compiled out, 6 / 7 with
+                         // W fragments 1 / 3 k-steps ahead instead of 2)
 
 bool rows_supported(int F) { return F == 32 || F == 64 || F == 128 || F == 256 || (F > 256 && F % 256 == 0); }
 bool tiles_supported(int F) { return F == 32 || F == 64 || F == 128 || F == 256 || F == 512; }
@@ -1322,7 +1331,7 @@ bool t32_supported(int F) { return F == 64 || F == 128 || F == 256; }
 Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   Plan p;
   if (allow32 && t32_supported(F)) {
-    if (g_force_kernel == 3 || g_force_kernel == 5) p.k32 = 4;
+    if (g_force_kernel == 3 || g_force_kernel >= 5) p.k32 = 4;
     else if (g_force_kernel == 0 && B >= 16384) p.k32 = 4;
   }
   // 32 rows per wave (NT = 2) halve the LDS fragment reads per MFMA. It pays once the register
@@ -1369,6 +1378,13 @@ void launch32(const GemmArgs& args, const dim3& grid, int rt, hipStream_t stream
     if constexpr (MODE == 0 && KS == 8) {
       if (!o && g_force_kernel == 5) {  // measurement: epilogue compiled out
         hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, false>), grid, dim3(256), 0, stream, args);
+        return;
+      }
+      if (!o && (g_force_kernel == 6 || g_force_kernel == 7)) {  // measurement: fragment prefetch depth 1 / 3
+        if (g_force_kernel == 6)
+          hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, true, 1>), grid, dim3(256), 0, stream, args);
+        else
+          hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, true, 3>), grid, dim3(256), 0, stream, args);
         return;
       }
     }
