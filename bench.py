@@ -376,9 +376,11 @@ def main(argv=None) -> int:
         from mlapi_amd.utils.threads import effective_cpus
 
         per_rank = max(4, len(pinned) if pinned else effective_cpus() // max(1, local))
-        # measured on a 16-CPU share: io=8/client=6 -> 971k req/s; 6/6 -> 549k; 4/4 -> 282k
-        io = max(2, min(8, (per_rank - 2) // 2 + 1))
-        cl = max(2, min(6, per_rank - io - 2))
+        # measured on a 16-CPU share with the out-of-process load generator (profiles/r2_serve_threads/
+        # sweep_io*): io=10/client=4 -> 0.99-1.11 M req/s; 9/5 0.89-0.93 M; 8/6 0.75-0.94 M;
+        # 7/6 0.52-0.79 M; 11/3 0.66-0.83 M (two interleaved rounds)
+        cl = max(2, min(6, per_rank // 4))
+        io = max(2, min(12, per_rank - cl - 2))
         args.io_threads = args.io_threads if args.io_threads > 0 else io
         args.client_threads = args.client_threads if args.client_threads > 0 else cl
     if pinned and getattr(args, "lg_proc", None) is not None and len(pinned) > args.io_threads + 3:
