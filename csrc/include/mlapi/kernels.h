@@ -51,9 +51,8 @@ void launch_linear_inline(int dt, const InlineBatch& a, hipStream_t stream);
 // ---- gemv_binary.hip: binary LR predict, HBM-streaming GEMV + sigmoid epilogue ----------------
 // X: [B, F] bf16 or f32 row-major; w: [F] same dtype; bias: scalar f32.
 // out_idx: int32[B] (z > 0), out_p: f32[B] = sigmoid(|z|) (kind BINARY) or sigmoid(2|z|).
-// sig: serving launches publish their own done word (no trailing serve_signal kernel).
 void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_t B, int F, int kind,
-                        int32_t* out_idx, float* out_p, hipStream_t stream, const ServeSignal& sig = ServeSignal());
+                        int32_t* out_idx, float* out_p, hipStream_t stream);
 
 // ---- gemm_softmax.hip: multiclass predict, bf16 MFMA GEMM + online softmax/argmax epilogue ----
 // X: [B, F] bf16; W: [K, F] bf16; b: [K] f32. F in {32, 64, 128, 256} or a multiple of 256 (any
@@ -67,8 +66,7 @@ void gemm_softmax_force_plan(int nt, int splits, int kernel = 0);
 // (tools/gemm_phase_probe.py); nullptr = off (default).
 void gemm_softmax_set_stamps(void* stamps);
 void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind,
-                         int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream,
-                         const ServeSignal& sig = ServeSignal());
+                         int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream);
 // Full logits (for tests / decision_function): Z[B, K] f32.
 void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B, int F, int K, float* Z,
                         hipStream_t stream);

@@ -36,7 +36,6 @@
 
 #include "mlapi/common.h"
 #include "mlapi/kernels.h"
-#include "mlapi/serve_signal.h"
 
 namespace mlapi {
 namespace {
@@ -119,7 +118,6 @@ struct GemmArgs {
   float2* rowstat;         // MODE 2 output: {lse, argmax bits}
   float4* rowstate;        // MODE 4 output: {max, sum, argmax bits, 0} (class-sharded TP)
   unsigned long long* stamps;  // profiling (tools/gemm_phase_probe.py): 8 s_memtime slots per wave
-  ServeSignal sig;             // MODE 0 serving launches: done word published by the kernel itself
 };
 
 // Phase stamps of one wave (profiled launches only: a.stamps is null otherwise): 0 entry, 1 first
@@ -623,7 +621,6 @@ gemm_softmax_kernel(GemmArgs a) {
           }
         }
       }
-      if constexpr (MODE == 0) serve_signal(a.sig.done, a.sig.seq, a.sig.counter);
       return;
     }
     // ---- split classes: publish partials, last-arriving block of this row block merges them.
@@ -689,8 +686,6 @@ gemm_softmax_kernel(GemmArgs a) {
         }
       }
     }
-    // the merging block of every row block (gridDim.x of them) takes part in the serving signal
-    if constexpr (MODE == 0) serve_signal(a.sig.done, a.sig.seq, a.sig.counter);
   }
 }
 
@@ -1042,7 +1037,6 @@ gemm_softmax32_kernel(GemmArgs a) {
         }
       }
     }
-    if constexpr (MODE == 0) serve_signal(a.sig.done, a.sig.seq, a.sig.counter);
     return;
   }
   // split classes: the 16x16 kernel's publish / last-arriver merge (see there)
@@ -1099,7 +1093,6 @@ gemm_softmax32_kernel(GemmArgs a) {
       }
     }
   }
-  if constexpr (MODE == 0) serve_signal(a.sig.done, a.sig.seq, a.sig.counter);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1115,7 +1108,6 @@ gemm_softmax32_kernel(GemmArgs a) {
 constexpr int ROWS_MAX_WAVES = 8;
 
 struct RowsArgs {
-  ServeSignal sig;  // MODE 0 serving launches
   const uint16_t* X;
   int64_t ldx;
   const uint16_t* W;  // [K, F] bf16, row stride F
@@ -1247,7 +1239,6 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
       }
     }
   }
-  if constexpr (MODE == 0) serve_signal(a.sig.done, a.sig.seq, a.sig.counter);
 }
 
 // Which kernel serves (B, K, F): the row-group kernel only where the tiles kernel has no
@@ -1500,8 +1491,7 @@ size_t gemm_softmax_workspace(int64_t B, int K, int F) {
 }
 
 void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind,
-                         int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream,
-                         const ServeSignal& sig) {
+                         int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream) {
   if (B <= 0) return;
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("gemm_softmax: multiclass kinds only (binary models use gemv_binary)");
@@ -1509,7 +1499,6 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
     RowsArgs ra = rows_args(X, F, W, b, B, F, K);
     ra.out_idx = out_idx;
     ra.out_p = out_p;
-    ra.sig = sig;
     launch_rows<0>(ra, kind, stream);
     return;
   }
@@ -1520,7 +1509,6 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
   args.bias = b;
   args.out_idx = out_idx;
   args.out_p = out_p;
-  args.sig = sig;
   if (plan.splits > 1) {
     args.counters = static_cast<unsigned int*>(workspace);
     args.partials = reinterpret_cast<float4*>(static_cast<unsigned char*>(workspace) + COUNTER_BYTES);

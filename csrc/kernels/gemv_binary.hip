@@ -17,7 +17,6 @@
 
 #include "mlapi/common.h"
 #include "mlapi/kernels.h"
-#include "mlapi/serve_signal.h"
 #include "mlapi/device.h"
 #include "mlapi/rowreduce.h"
 
@@ -58,7 +57,7 @@ struct Chunk<float> {
 template <typename T, int LPR, int CPL, int U>
 __global__ __launch_bounds__(256) void gemv_binary_kernel(const T* __restrict__ X, const T* __restrict__ w, float bias,
                                                           int64_t B, int F, int kind, int32_t* __restrict__ out_idx,
-                                                          float* __restrict__ out_p, ServeSignal sig) {
+                                                          float* __restrict__ out_p) {
   constexpr int RPW = 64 / LPR;  // rows per wave-instruction
   constexpr int NE = Chunk<T>::N;
   const int lane = threadIdx.x & 63;
@@ -123,44 +122,43 @@ __global__ __launch_bounds__(256) void gemv_binary_kernel(const T* __restrict__ 
       out_p[row] = 1.f / (1.f + __expf(-a));
     }
   }
-  serve_signal(sig.done, sig.seq, sig.counter);  // serving launches: publish the batch (no extra kernel)
 }
 
 template <typename T, int LPR, int CPL, int U>
 void launch(const void* X, const void* w, float bias, int64_t B, int F, int kind, int32_t* out_idx, float* out_p,
-            hipStream_t stream, const ServeSignal& sig) {
+            hipStream_t stream) {
   constexpr int rows_per_block_iter = 4 * U * (64 / LPR);
   int64_t blocks = (B + rows_per_block_iter - 1) / rows_per_block_iter;
   const int64_t cap = 256 * 8;  // 256 CUs x 8 resident blocks: grid-stride beyond that
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL((gemv_binary_kernel<T, LPR, CPL, U>), dim3((unsigned)blocks), dim3(256), 0, stream,
-                     static_cast<const T*>(X), static_cast<const T*>(w), bias, B, F, kind, out_idx, out_p, sig);
+                     static_cast<const T*>(X), static_cast<const T*>(w), bias, B, F, kind, out_idx, out_p);
   MLAPI_HIP_CHECK(hipGetLastError());
 }
 
 template <typename T>
 void dispatch(const void* X, const void* w, float bias, int64_t B, int F, int kind, int32_t* out_idx, float* out_p,
-              hipStream_t stream, const ServeSignal& sig) {
+              hipStream_t stream) {
   constexpr int NE = Chunk<T>::N;
   if (F % NE != 0) throw std::invalid_argument("gemv_binary: F must be a multiple of 16 bytes of elements");
   const int chunks = F / NE;
   if (chunks <= 4)
-    launch<T, 4, 1, 4>(X, w, bias, B, F, kind, out_idx, out_p, stream, sig);
+    launch<T, 4, 1, 4>(X, w, bias, B, F, kind, out_idx, out_p, stream);
   else if (chunks <= 8)
-    launch<T, 8, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream, sig);
+    launch<T, 8, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
   else if (chunks <= 16)
-    launch<T, 16, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream, sig);
+    launch<T, 16, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
   else if (chunks <= 32)
-    launch<T, 32, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream, sig);
+    launch<T, 32, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
   else if (chunks <= 64)
-    launch<T, 64, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream, sig);
+    launch<T, 64, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
   else if (chunks <= 128)
-    launch<T, 64, 2, 4>(X, w, bias, B, F, kind, out_idx, out_p, stream, sig);
+    launch<T, 64, 2, 4>(X, w, bias, B, F, kind, out_idx, out_p, stream);
   else if (chunks <= 256)
-    launch<T, 64, 4, 2>(X, w, bias, B, F, kind, out_idx, out_p, stream, sig);
+    launch<T, 64, 4, 2>(X, w, bias, B, F, kind, out_idx, out_p, stream);
   else if (chunks <= 512)
-    launch<T, 64, 8, 1>(X, w, bias, B, F, kind, out_idx, out_p, stream, sig);
+    launch<T, 64, 8, 1>(X, w, bias, B, F, kind, out_idx, out_p, stream);
   else
     throw std::invalid_argument("gemv_binary: F too large (max 4096 bf16 / 2048 f32)");
 }
@@ -168,14 +166,14 @@ void dispatch(const void* X, const void* w, float bias, int64_t B, int F, int ki
 }  // namespace
 
 void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_t B, int F, int kind,
-                        int32_t* out_idx, float* out_p, hipStream_t stream, const ServeSignal& sig) {
+                        int32_t* out_idx, float* out_p, hipStream_t stream) {
   if (B <= 0) return;
   if (reinterpret_cast<uintptr_t>(X) % 16 || reinterpret_cast<uintptr_t>(w) % 16)
     throw std::invalid_argument("gemv_binary: X and w must be 16-byte aligned");
   if (dt == DT_BF16)
-    dispatch<uint16_t>(X, w, bias, B, F, kind, out_idx, out_p, stream, sig);
+    dispatch<uint16_t>(X, w, bias, B, F, kind, out_idx, out_p, stream);
   else if (dt == DT_F32)
-    dispatch<float>(X, w, bias, B, F, kind, out_idx, out_p, stream, sig);
+    dispatch<float>(X, w, bias, B, F, kind, out_idx, out_p, stream);
   else
     throw std::invalid_argument("gemv_binary: dtype must be bf16 or f32");
 }

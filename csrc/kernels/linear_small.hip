@@ -14,7 +14,6 @@
 
 #include "mlapi/common.h"
 #include "mlapi/kernels.h"
-#include "mlapi/serve_signal.h"
 
 namespace mlapi {
 namespace {
@@ -101,6 +100,22 @@ __device__ __forceinline__ void row_predict(const T* __restrict__ xr, const T* _
   out_p = p;
 }
 
+
+// End of a serving launch: every wave makes its stores visible at system scope, the block meets,
+// and the last block to arrive (one block: itself) publishes the batch's sequence number.
+__device__ __forceinline__ void serve_signal(uint32_t* done, uint32_t seq, uint32_t* counter) {
+  if (done == nullptr) return;  // uniform
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bool last = true;
+    if (gridDim.x > 1) {
+      last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM) == gridDim.x - 1;
+      if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    if (last) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 
 __global__ __launch_bounds__(64) void serve_signal_kernel(uint32_t* done, uint32_t seq) {
   serve_signal(done, seq, nullptr);

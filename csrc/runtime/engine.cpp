@@ -505,12 +505,12 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
   if (m.path == PATH_SMALL || m.path == PATH_GENERIC) {
     launch_linear_small(m.xdt, X, m.ldx, m.dW, m.db, n, m.F, m.K, m.kind, s.didx, s.dp, stream_, sig);
   } else {
-    // both kernels publish the batch's done word themselves (one launch per batch)
     if (m.path == PATH_GEMV)
-      launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_, sig);
+      launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_);
     else
       launch_gemm_softmax(X, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
-                          static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_, sig);
+                          static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_);
+    launch_serve_signal(sig, stream_);
   }
   std::lock_guard<std::mutex> lk(st_mu_);
   stats_.path_batches[m.path]++;
