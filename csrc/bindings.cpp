@@ -100,6 +100,8 @@ py::dict stats_dict(const EngineStats& s) {
   for (int i = 0; i < PATH_COUNT; ++i) paths[names[i]] = s.path_batches[i];
   d["path_batches"] = paths;
   d["inline_batches"] = s.inline_batches;
+  d["direct_batches"] = s.direct_batches;
+  d["direct_dispatch"] = s.direct_dispatch;
   return d;
 }
 
@@ -289,6 +291,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("wide_dtype", &EngineConfig::wide_dtype)
       .def_readwrite("inline_args", &EngineConfig::inline_args)
       .def_readwrite("stage_wide", &EngineConfig::stage_wide)
+      .def_readwrite("direct_dispatch", &EngineConfig::direct_dispatch)
+      .def_readwrite("hsaco_path", &EngineConfig::hsaco_path)
       .def_readwrite("max_queue", &EngineConfig::max_queue);
 
   py::class_<PySink>(m, "PySink").def(py::init<>()).def("fd", &PySink::fd).def("drain", &PySink::drain);

@@ -1,0 +1,191 @@
+// HSA side of the engine's direct dispatch (see direct_dispatch.h).
+#include "direct_dispatch.h"
+
+#include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+
+#include <atomic>
+#include <cstring>
+#include <fstream>
+#include <iterator>
+#include <stdexcept>
+#include <vector>
+
+namespace mlapi {
+namespace {
+
+struct Kernel {
+  uint64_t object = 0;
+  uint32_t group = 0, priv = 0, kernarg = 0;
+};
+
+struct AgentSearch {
+  uint32_t bdf = 0, domain = 0;
+  hsa_agent_t gpu{}, cpu{};
+  bool have_gpu = false, have_cpu = false;
+};
+
+hsa_status_t pick_agents(hsa_agent_t a, void* data) {
+  auto* s = static_cast<AgentSearch*>(data);
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
+  if (t == HSA_DEVICE_TYPE_CPU && !s->have_cpu) {
+    s->cpu = a;
+    s->have_cpu = true;
+  } else if (t == HSA_DEVICE_TYPE_GPU && !s->have_gpu) {
+    uint32_t bdf = 0, dom = 0;
+    hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+    hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+    if (bdf == s->bdf && dom == s->domain) {
+      s->gpu = a;
+      s->have_gpu = true;
+    }
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t pick_kernarg_pool(hsa_amd_memory_pool_t p, void* data) {
+  hsa_amd_segment_t seg;
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+  uint32_t flags = 0;
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  if (seg == HSA_AMD_SEGMENT_GLOBAL && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT)) {
+    *static_cast<hsa_amd_memory_pool_t*>(data) = p;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+void queue_error(hsa_status_t, hsa_queue_t*, void* data);
+
+class HsaInlineDispatcher final : public InlineDispatcher {
+ public:
+  ~HsaInlineDispatcher() override {
+    if (queue_) hsa_queue_destroy(queue_);
+    if (kernargs_) hsa_amd_memory_pool_free(kernargs_);
+    if (exe_.handle) hsa_executable_destroy(exe_);
+    if (reader_.handle) hsa_code_object_reader_destroy(reader_);
+    if (inited_) hsa_shut_down();
+  }
+
+  bool init(int device, const std::string& path, std::string* why) {
+    auto fail = [&](const std::string& m) {
+      if (why) *why = m;
+      return false;
+    };
+    int bus = 0, dev = 0, dom = 0;
+    if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+        hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess)
+      return fail("no PCI id for the HIP device");
+    (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device);
+    if (hsa_init() != HSA_STATUS_SUCCESS) return fail("hsa_init failed");
+    inited_ = true;
+    AgentSearch s;
+    s.bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3);
+    s.domain = (uint32_t)dom;
+    hsa_iterate_agents(pick_agents, &s);
+    if (!s.have_gpu || !s.have_cpu) return fail("HSA agent of the HIP device not found");
+    gpu_ = s.gpu;
+    hsa_amd_memory_pool_t pool{};
+    if (hsa_amd_agent_iterate_memory_pools(s.cpu, pick_kernarg_pool, &pool) != HSA_STATUS_INFO_BREAK)
+      return fail("no kernarg memory pool");
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return fail("code object " + path + " not found");
+    blob_.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    if (hsa_code_object_reader_create_from_memory(blob_.data(), blob_.size(), &reader_) != HSA_STATUS_SUCCESS)
+      return fail("unreadable code object");
+    if (hsa_executable_create_alt(HSA_PROFILE_FULL, HSA_DEFAULT_FLOAT_ROUNDING_MODE_DEFAULT, nullptr, &exe_) !=
+            HSA_STATUS_SUCCESS ||
+        hsa_executable_load_agent_code_object(exe_, gpu_, reader_, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
+        hsa_executable_freeze(exe_, nullptr) != HSA_STATUS_SUCCESS)
+      return fail("code object does not load for this GPU");
+    const char* names[4] = {"mlapi_inline_f64_s.kd", "mlapi_inline_f64_w.kd", "mlapi_inline_f32_s.kd",
+                            "mlapi_inline_f32_w.kd"};
+    for (int i = 0; i < 4; ++i) {
+      hsa_executable_symbol_t sym;
+      if (hsa_executable_get_symbol_by_name(exe_, names[i], &gpu_, &sym) != HSA_STATUS_SUCCESS)
+        return fail(std::string("kernel ") + names[i] + " missing");
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k_[i].object);
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k_[i].group);
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k_[i].priv);
+      hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k_[i].kernarg);
+      if (k_[i].kernarg < sizeof(InlineBatch) || k_[i].kernarg > stride_) return fail("unexpected kernarg layout");
+    }
+    if (hsa_queue_create(gpu_, QUEUE_SIZE, HSA_QUEUE_TYPE_SINGLE, queue_error, this, UINT32_MAX, UINT32_MAX,
+                         &queue_) != HSA_STATUS_SUCCESS)
+      return fail("hsa_queue_create failed");
+    // Kernarg ring: a buffer is rewritten KA_SLOTS launches later; the engine keeps at most
+    // `slots` (a handful) batches in flight, so its previous kernel has long finished reading it.
+    if (hsa_amd_memory_pool_allocate(pool, (size_t)stride_ * KA_SLOTS, 0, (void**)&kernargs_) != HSA_STATUS_SUCCESS ||
+        hsa_amd_agents_allow_access(1, &gpu_, nullptr, kernargs_) != HSA_STATUS_SUCCESS)
+      return fail("kernarg allocation failed");
+    std::memset(kernargs_, 0, (size_t)stride_ * KA_SLOTS);
+    return true;
+  }
+
+  void launch(int dt, const InlineBatch& a) override {
+    if (dt != DT_F64 && dt != DT_F32) throw std::invalid_argument("direct dispatch: f64 / f32 batches only");
+    if (faulted()) throw std::runtime_error("direct dispatch: queue error");
+    const Kernel& k = k_[(dt == DT_F64 ? 0 : 2) + (a.F <= 8 && a.K <= 4 ? 0 : 1)];
+    char* ka = kernargs_ + (size_t)(launches_++ % KA_SLOTS) * stride_;
+    std::memcpy(ka, &a, sizeof(InlineBatch));
+    const uint64_t wi = hsa_queue_add_write_index_relaxed(queue_, 1);
+    while (wi - hsa_queue_load_read_index_scacquire(queue_) >= queue_->size) {
+      // full (cannot happen with a few batches in flight): wait for the packet processor
+    }
+    auto* pkt = reinterpret_cast<hsa_kernel_dispatch_packet_t*>(queue_->base_address) + (wi & (queue_->size - 1));
+    const uint16_t threads = a.n <= 64 ? 64 : 128;
+    pkt->workgroup_size_x = threads;
+    pkt->workgroup_size_y = 1;
+    pkt->workgroup_size_z = 1;
+    pkt->reserved0 = 0;
+    pkt->grid_size_x = threads;
+    pkt->grid_size_y = 1;
+    pkt->grid_size_z = 1;
+    pkt->private_segment_size = k.priv;
+    pkt->group_segment_size = k.group;
+    pkt->kernel_object = k.object;
+    pkt->kernarg_address = ka;
+    pkt->reserved2 = 0;
+    pkt->completion_signal.handle = 0;  // completion: the kernel's own done word
+    // Acquire at agent scope invalidates the caches the kernel reads its (host-written) kernarg
+    // block through; no release fence: the kernel publishes its outputs at system scope itself.
+    const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                            (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                            (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+    const uint32_t setup = 1;  // one grid dimension
+    __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), (uint32_t)header | (setup << 16), __ATOMIC_RELEASE);
+    hsa_signal_store_relaxed(queue_->doorbell_signal, (hsa_signal_value_t)wi);
+  }
+
+  bool faulted() const override { return fault_.load(std::memory_order_relaxed); }
+  void set_fault() { fault_.store(true); }
+
+ private:
+  static constexpr uint32_t QUEUE_SIZE = 256;
+  static constexpr int KA_SLOTS = 64;
+  const uint32_t stride_ = (uint32_t)((sizeof(InlineBatch) + 255) / 256 * 256);
+  bool inited_ = false;
+  hsa_agent_t gpu_{};
+  std::vector<char> blob_;
+  hsa_code_object_reader_t reader_{};
+  hsa_executable_t exe_{};
+  Kernel k_[4];
+  hsa_queue_t* queue_ = nullptr;
+  char* kernargs_ = nullptr;
+  uint64_t launches_ = 0;
+  std::atomic<bool> fault_{false};
+};
+
+void queue_error(hsa_status_t, hsa_queue_t*, void* data) { static_cast<HsaInlineDispatcher*>(data)->set_fault(); }
+
+}  // namespace
+
+std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int device, const std::string& hsaco_path, std::string* why) {
+  auto d = std::make_unique<HsaInlineDispatcher>();
+  if (!d->init(device, hsaco_path, why)) return nullptr;
+  return d;
+}
+
+}  // namespace mlapi

@@ -1,0 +1,33 @@
+// Direct AQL dispatch of the serving kernels ("hsaco loader, direct-launch wrappers").
+//
+// hipLaunchKernel spends ~2.5 us of the calling thread per launch and its path from launch to a
+// kernel-written done word is ~7.5 us for a one-wave kernel on MI355X; writing the AQL packet into
+// an HSA queue of our own costs ~0.03 us and that path ~5.3 us (tools/hsa_dispatch_probe.cpp,
+// profiles/r2_signal/hsa_probe.txt). The engine uses it for kernel-argument batches (InlineBatch:
+// the whole batch travels in the kernarg segment, so a dispatch is one memcpy + one packet).
+#pragma once
+
+#include <memory>
+#include <string>
+
+#include "mlapi/common.h"
+#include "mlapi/kernels.h"
+
+namespace mlapi {
+
+class InlineDispatcher {
+ public:
+  virtual ~InlineDispatcher() = default;
+  // Enqueue one kernel-argument batch (dt: DT_F64 / DT_F32); completion is the batch's done word.
+  // Single producer (the engine's batcher thread). Throws on failure.
+  virtual void launch(int dt, const InlineBatch& a) = 0;
+  // true once the queue reported an error (the engine then fails the batches instead of waiting)
+  virtual bool faulted() const = 0;
+};
+
+// Loads `hsaco_path` (csrc/kernels/serve_direct.hip) for the GPU behind HIP device `device` and
+// creates the queue; nullptr with the reason in *why if anything is missing (the engine then keeps
+// using hipLaunchKernel).
+std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int device, const std::string& hsaco_path, std::string* why);
+
+}  // namespace mlapi

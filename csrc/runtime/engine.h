@@ -44,6 +44,7 @@
 
 #include "mlapi/common.h"
 #include "mlapi/kernels.h"
+#include "direct_dispatch.h"
 
 namespace mlapi {
 
@@ -111,6 +112,10 @@ struct EngineConfig {
   int spin_us = 0;        // batcher / completer poll their queues this long before sleeping on a condvar
                           // (saves the futex wake-up on the request path under load)
   int max_queue = 1 << 20;  // backpressure: rows waiting for the batcher; beyond it submit is refused
+  // Kernel-argument batches go through the engine's own HSA queue (direct_dispatch.h) when the
+  // serving code object loads; empty path or failure -> hipLaunchKernel.
+  bool direct_dispatch = true;
+  std::string hsaco_path;
 };
 
 struct EngineStats {
@@ -120,6 +125,8 @@ struct EngineStats {
   uint64_t latency_hist[24] = {0};  // latency buckets in powers of two of 1us: <1us .. >=2^23us
   uint64_t path_batches[PATH_COUNT] = {0};  // GPU batches per kernel path
   uint64_t inline_batches = 0;      // SMALL batches launched through the kernel-argument block
+  uint64_t direct_batches = 0;      // ... of which written straight into the HSA queue
+  bool direct_dispatch = false;     // the direct queue is up
   double latency_sum_us = 0;
   double device_us_sum = 0;         // launch -> completion observed by the completer
   uint64_t queue_depth = 0;
@@ -217,6 +224,7 @@ class Engine {
 
   // GPU slots
   hipStream_t stream_ = nullptr;
+  std::unique_ptr<InlineDispatcher> direct_;  // direct AQL dispatch of kernel-argument batches
   std::vector<Slot> slots_;
   std::mutex s_mu_;
   std::condition_variable s_cv_;

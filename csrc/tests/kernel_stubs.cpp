@@ -3,6 +3,7 @@
 #include <stdexcept>
 
 #include "mlapi/kernels.h"
+#include "../runtime/direct_dispatch.h"
 
 namespace mlapi {
 [[noreturn]] static void unreachable(const char* what) {
@@ -22,5 +23,9 @@ size_t gemm_softmax_workspace(int64_t, int, int) { return 0; }
 void launch_gemm_softmax(const void*, const void*, const float*, int64_t, int, int, int, int32_t*, float*, void*, size_t,
                          hipStream_t) {
   unreachable("launch_gemm_softmax");
+}
+std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int, const std::string&, std::string* why) {
+  if (why) *why = "host-only build";
+  return nullptr;
 }
 }  // namespace mlapi

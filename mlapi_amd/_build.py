@@ -22,6 +22,7 @@ ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "csrc"
 BUILD = ROOT / "build" / "native"
 ARCH = os.environ.get("MLAPI_OFFLOAD_ARCH", "gfx950")
+ROCM_LIB = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / "lib"
 
 SOURCES = [
     "kernels/linear_small.hip",
@@ -32,6 +33,7 @@ SOURCES = [
     "kernels/shard.hip",
     "kernels/softmax_grad_dw.hip",
     "runtime/engine.cpp",
+    "runtime/direct_dispatch.cpp",
     "http/server.cpp",
     "http/loadgen.cpp",
     "dist/comm.cpp",
@@ -116,6 +118,29 @@ def _build_loadgen(force: bool, verbose: bool) -> Path:
     return out
 
 
+def hsaco_path() -> Path:
+    return ROOT / "mlapi_amd" / "serve_kernels.hsaco"
+
+
+def _build_hsaco(force: bool, verbose: bool) -> Path:
+    """The engine's directly dispatched serving kernels (csrc/kernels/serve_direct.hip) as a plain
+    gfx950 code object the HSA loader reads (csrc/runtime/direct_dispatch.cpp); not part of _C."""
+    out = hsaco_path()
+    src = CSRC / "kernels" / "serve_direct.hip"
+    newest = max(src.stat().st_mtime, _headers_mtime(), (CSRC / "kernels" / "linear_rows.h").stat().st_mtime)
+    if not force and out.exists() and out.stat().st_mtime >= newest:
+        return out
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "--cuda-device-only", "--no-gpu-bundle-output", "-O3", "-std=c++17"] + \
+        _includes() + [str(src), "-o", str(out) + ".tmp"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for serve_direct.hip:\n{r.stderr[-4000:]}")
+    os.replace(str(out) + ".tmp", out)
+    if verbose:
+        print(f"[mlapi_amd] built {out.relative_to(ROOT)}", file=sys.stderr)
+    return out
+
+
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> Path:
     BUILD.mkdir(parents=True, exist_ok=True)
     hmt = _headers_mtime()
@@ -126,7 +151,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     newest = max(o.stat().st_mtime for o in objs)
     if force or not out.exists() or out.stat().st_mtime < newest:
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out) + ".tmp"] + \
-              [str(o) for o in objs] + ["-lpthread", "-ldl"]
+              [str(o) for o in objs] + [f"-L{ROCM_LIB}", "-lhsa-runtime64", "-lpthread", "-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
@@ -134,6 +159,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
         if verbose:
             print(f"[mlapi_amd] built {out.relative_to(ROOT)}", file=sys.stderr)
     _build_loadgen(force, verbose)
+    _build_hsaco(force, verbose)
     return out
 
 

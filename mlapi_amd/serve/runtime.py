@@ -61,6 +61,12 @@ class EngineHandle:
         ec.inline_args = bool(config.inline_args)
         ec.stage_wide = bool(config.stage_wide)
         ec.max_queue = config.max_queue
+        ec.direct_dispatch = bool(config.direct_dispatch)
+        if ec.direct_dispatch:
+            from mlapi_amd._build import hsaco_path
+
+            hp = hsaco_path()
+            ec.hsaco_path = str(hp) if hp.exists() else ""
         self.engine = c.Engine(ec)
         self._models: Dict[int, LinearModel] = {}
         self._lock = threading.Lock()

@@ -114,6 +114,37 @@ def test_engine_small_inline_and_zero_copy(native, inline, max_batch):
         e.stop()
 
 
+@pytest.mark.parametrize("dtype", [0, 1])
+@pytest.mark.parametrize("F,K,kind", [(4, 3, Kind.MULTINOMIAL), (4, 1, Kind.BINARY), (8, 4, Kind.OVR), (10, 5, Kind.MULTINOMIAL)])
+def test_engine_direct_dispatch_matches_hip_launch(native, dtype, F, K, kind):
+    """Kernel-argument batches written as AQL packets into the engine's own HSA queue (code object
+    mlapi_amd/serve_kernels.hsaco) give bit-identical results to the hipLaunchKernel path."""
+    from mlapi_amd._build import hsaco_path
+
+    m = LinearModel.random(F, 2 if K == 1 else K, seed=F + K, kind=kind)
+    X = np.random.default_rng(F * K).standard_normal((3000, F))
+    out = {}
+    for mode in ("hip", "direct"):
+        e = _engine(native, dtype=dtype, max_batch=32, max_features=F,
+                    hsaco_path=str(hsaco_path()) if mode == "direct" else "")
+        try:
+            e.load_model(int(m.kind), m.W, m.b, m.label_json())
+            idx, p, st = e.predict(X)
+            assert (st == 0).all()
+            s = e.stats()
+            assert s["direct_dispatch"] == (mode == "direct")
+            assert s["inline_batches"] == s["batches"]
+            assert s["direct_batches"] == (s["batches"] if mode == "direct" else 0)
+            out[mode] = (idx, p)
+        finally:
+            e.stop()
+    np.testing.assert_array_equal(out["hip"][0], out["direct"][0])
+    np.testing.assert_array_equal(out["hip"][1], out["direct"][1])
+    ridx, rp = m.predict_max(X)
+    np.testing.assert_array_equal(out["direct"][0], ridx)
+    np.testing.assert_allclose(out["direct"][1], rp, rtol=1e-12 if dtype == 0 else 1e-5, atol=0 if dtype == 0 else 1e-6)
+
+
 def test_engine_drop_injection_and_recovery(native):
     m = LinearModel.random(4, 3, seed=0)
     e = _engine(native, max_batch=8)
