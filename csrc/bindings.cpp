@@ -102,6 +102,7 @@ py::dict stats_dict(const EngineStats& s) {
   d["inline_batches"] = s.inline_batches;
   d["direct_batches"] = s.direct_batches;
   d["direct_dispatch"] = s.direct_dispatch;
+  d["direct_device_kernargs"] = s.direct_device_kernargs;
   return d;
 }
 

@@ -5,6 +5,9 @@
 // an HSA queue of our own costs ~0.03 us and that path ~5.3 us (tools/hsa_dispatch_probe.cpp,
 // profiles/r2_signal/hsa_probe.txt). The engine uses it for kernel-argument batches (InlineBatch:
 // the whole batch travels in the kernarg segment, so a dispatch is one memcpy + one packet).
+// Where that segment lives decides the latency: with a 3.5 KB block, a kernarg ring in host memory
+// made the path 14.0 us (the kernel's scalar loads cross the host link), one in device HBM written
+// through the BAR + HDP flush 6.9 us, hipLaunchKernel 9.5 us (profiles/r2_signal/hsa_probe_kernarg.txt).
 #pragma once
 
 #include <memory>
@@ -23,6 +26,8 @@ class InlineDispatcher {
   virtual void launch(int dt, const InlineBatch& a) = 0;
   // true once the queue reported an error (the engine then fails the batches instead of waiting)
   virtual bool faulted() const = 0;
+  // true if the kernarg ring is in device memory (else the host kernarg pool)
+  virtual bool device_kernargs() const = 0;
 };
 
 // Loads `hsaco_path` (csrc/kernels/serve_direct.hip) for the GPU behind HIP device `device` and

@@ -708,6 +708,7 @@ EngineStats Engine::stats() const {
   s.healthy = healthy_.load();
   s.dropped = drop_.load();
   s.direct_dispatch = direct_ != nullptr;
+  s.direct_device_kernargs = direct_ != nullptr && direct_->device_kernargs();
   return s;
 }
 

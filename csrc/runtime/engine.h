@@ -127,6 +127,7 @@ struct EngineStats {
   uint64_t inline_batches = 0;      // SMALL batches launched through the kernel-argument block
   uint64_t direct_batches = 0;      // ... of which written straight into the HSA queue
   bool direct_dispatch = false;     // the direct queue is up
+  bool direct_device_kernargs = false;  // ... and its kernarg ring is in device memory
   double latency_sum_us = 0;
   double device_us_sum = 0;         // launch -> completion observed by the completer
   uint64_t queue_depth = 0;

@@ -133,6 +133,7 @@ def test_engine_direct_dispatch_matches_hip_launch(native, dtype, F, K, kind):
             assert (st == 0).all()
             s = e.stats()
             assert s["direct_dispatch"] == (mode == "direct")
+            assert s["direct_device_kernargs"] == (mode == "direct")  # ring in HBM, not host memory
             assert s["inline_batches"] == s["batches"]
             assert s["direct_batches"] == (s["batches"] if mode == "direct" else 0)
             out[mode] = (idx, p)

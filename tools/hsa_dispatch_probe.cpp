@@ -61,6 +61,25 @@ static hsa_status_t find_pools(hsa_amd_memory_pool_t p, void* data) {
   return HSA_STATUS_SUCCESS;
 }
 
+struct BigArgsH {
+  unsigned long long* out;
+  unsigned* done;
+  unsigned seq;
+  unsigned pad;
+  unsigned long long payload[440];
+};
+__global__ void big_hip(const BigArgsH) {
+  const BigArgsH* a = (const BigArgsH*)__builtin_amdgcn_kernarg_segment_ptr();
+  unsigned long long s = 0;
+  for (int i = threadIdx.x; i < 440; i += 64) s += a->payload[i];
+  a->out[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(a->done, a->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __global__ void hip_flag(int* idx, double* p, unsigned* done, unsigned seq) {
   idx[threadIdx.x] = (int)(threadIdx.x + seq);
   p[threadIdx.x] = 0.5 * threadIdx.x + seq;
@@ -204,6 +223,134 @@ int main(int argc, char** argv) {
     else
       std::printf("%-26s: every launch timed out (%ld)\n", names[m], timeouts[m]);
   std::printf("outputs not visible at done: %ld\n", bad);
+
+  // ---- serving-sized kernel argument (3.5 KB): where the kernarg block lives matters -------------
+  struct BigArgs {
+    unsigned long long* out;
+    unsigned* done;
+    unsigned seq;
+    unsigned pad;
+    unsigned long long payload[440];
+  };
+  hsa_executable_symbol_t bsym;
+  HC(hsa_executable_get_symbol_by_name(ex, "probe_big.kd", &ag.gpu, &bsym));
+  uint64_t bobj = 0;
+  uint32_t bka = 0;
+  HC(hsa_executable_symbol_get_info(bsym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &bobj));
+  HC(hsa_executable_symbol_get_info(bsym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &bka));
+  const uint32_t bstride = (bka + 255) / 256 * 256;
+  char* ka_host = nullptr;
+  HC(hsa_amd_memory_pool_allocate(pl.kernarg, (size_t)bstride * NKA, 0, (void**)&ka_host));
+  HC(hsa_amd_agents_allow_access(1, &ag.gpu, nullptr, ka_host));
+  // device-local kernarg ring the CPU writes through the BAR
+  struct GpuPool {
+    hsa_amd_memory_pool_t pool{};
+    bool have = false;
+  } gp;
+  HC(hsa_amd_agent_iterate_memory_pools(
+      ag.gpu,
+      [](hsa_amd_memory_pool_t p, void* d) -> hsa_status_t {
+        auto* g = static_cast<GpuPool*>(d);
+        hsa_amd_segment_t seg;
+        hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+        uint32_t flags = 0;
+        hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+        if (seg == HSA_AMD_SEGMENT_GLOBAL && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) && !g->have) {
+          g->pool = p;
+          g->have = true;
+        }
+        return HSA_STATUS_SUCCESS;
+      },
+      &gp));
+  char* ka_dev = nullptr;
+  bool dev_ok = gp.have && hsa_amd_memory_pool_allocate(gp.pool, (size_t)bstride * NKA, 0, (void**)&ka_dev) ==
+                               HSA_STATUS_SUCCESS;
+  if (dev_ok) dev_ok = hsa_amd_agents_allow_access(1, &ag.cpu, nullptr, ka_dev) == HSA_STATUS_SUCCESS;
+  hsa_amd_hdp_flush_t hdp{};
+  hsa_agent_get_info(ag.gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp);
+  std::printf("device kernarg ring: %s, HDP flush register: %s\n", dev_ok ? "yes" : "no",
+              hdp.HDP_MEM_FLUSH_CNTL ? "yes" : "no");
+  unsigned long long* out = nullptr;
+  HC(hsa_amd_memory_pool_allocate(pl.fine, 4096, 0, (void**)&out));
+  HC(hsa_amd_agents_allow_access(1, &ag.gpu, nullptr, out));
+  const char* bnames[] = {"hipLaunch 3.5KB", "AQL 3.5KB host kernarg", "AQL 3.5KB dev kernarg+hdp",
+                          "AQL 3.5KB dev kernarg+hdp+rb"};
+  for (int mode = 0; mode < 4; ++mode) {
+    if (mode >= 2 && !dev_ok) continue;
+    std::vector<double> L, A;
+    long wrong = 0, tos = 0;
+    for (int i = 0; i < iters + 50; ++i) {
+      ++seq;
+      BigArgs b{};
+      b.out = out;
+      b.done = done;
+      b.seq = seq;
+      unsigned long long expect[64] = {0};
+      for (int j = 0; j < 440; ++j) {
+        b.payload[j] = (unsigned long long)seq * 1000003ull + (unsigned long long)j * 7919ull;
+        expect[j % 64] += b.payload[j];
+      }
+      const double t0 = now_us();
+      if (mode == 0) {
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(big_hip), dim3(1), dim3(64), 0, s, *reinterpret_cast<BigArgsH*>(&b));
+      } else {
+        char* base = mode == 1 ? ka_host : ka_dev;
+        char* k = base + (size_t)(seq % NKA) * bstride;
+        std::memcpy(k, &b, sizeof b);
+        if (mode >= 2) {
+          __builtin_ia32_sfence();
+          if (hdp.HDP_MEM_FLUSH_CNTL) {
+            *(volatile uint32_t*)hdp.HDP_MEM_FLUSH_CNTL = 1u;
+            if (mode == 3) (void)*(volatile uint32_t*)hdp.HDP_MEM_FLUSH_CNTL;
+          }
+        }
+        const uint64_t wi = hsa_queue_add_write_index_relaxed(q, 1);
+        auto* pkt = reinterpret_cast<hsa_kernel_dispatch_packet_t*>(q->base_address) + (wi & (q->size - 1));
+        pkt->workgroup_size_x = 64;
+        pkt->workgroup_size_y = 1;
+        pkt->workgroup_size_z = 1;
+        pkt->reserved0 = 0;
+        pkt->grid_size_x = 64;
+        pkt->grid_size_y = 1;
+        pkt->grid_size_z = 1;
+        pkt->private_segment_size = 0;
+        pkt->group_segment_size = 0;
+        pkt->kernel_object = bobj;
+        pkt->kernarg_address = k;
+        pkt->reserved2 = 0;
+        pkt->completion_signal.handle = 0;
+        const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                                (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                                (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+        __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), (uint32_t)header | (1u << 16), __ATOMIC_RELEASE);
+        hsa_signal_store_relaxed(q->doorbell_signal, (hsa_signal_value_t)wi);
+      }
+      const double t1 = now_us();
+      bool to = false;
+      while (__atomic_load_n(done, __ATOMIC_ACQUIRE) != seq) {
+        if (now_us() - t1 > 200000) {
+          to = true;
+          break;
+        }
+      }
+      const double t2 = now_us();
+      if (to) {
+        ++tos;
+        continue;
+      }
+      for (int l = 0; l < 64; ++l) wrong += out[l] != expect[l];
+      if (i >= 50) {
+        L.push_back(t2 - t0);
+        A.push_back(t1 - t0);
+      }
+    }
+    if (mode == 0) hipStreamSynchronize(s);
+    if (L.empty())
+      std::printf("%-30s: all timed out\n", bnames[mode]);
+    else
+      std::printf("%-30s: submit %.2f us  launch->done p50 %.2f us  p90 %.2f  wrong %ld  timeouts %ld\n", bnames[mode],
+                  med(A, 0.5), med(L, 0.5), med(L, 0.9), wrong, tos);
+  }
   hsa_queue_destroy(q);
   hsa_executable_destroy(ex);
   hsa_code_object_reader_destroy(rd);
