@@ -140,6 +140,7 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
                                       s1["requests"] - s0["requests"]], info)
         barrier(info)
         paths = {k: s1["path_batches"][k] - s0["path_batches"][k] for k in s1["path_batches"]}
+        idle = {"c64": s1["idle_batches"] - s0["idle_batches"], "batch1": s3["idle_batches"] - s2["idle_batches"]}
     finally:
         srv.stop()
     total = float(np.sum(per_rank[:, 2]))
@@ -159,6 +160,8 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         "gpu_leg_us_c64": float(np.mean(per_rank[:, 4])),
         "gpu_leg_us_batch1": float(per_rank[0, 5]),
         "kernel_batches": paths,
+        # batches the IO thread launched itself on an idle engine (Engine::run_idle)
+        "idle_path_batches": idle,
         "backend": srv.runtime.handle.backend,
         "cpu_cores_busy_rank0": cpu_util,
         "threads": {"io": args.io_threads, "loadgen": args.client_threads, "pinned_cpus": args.pinned_cpus},

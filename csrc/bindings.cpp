@@ -101,6 +101,7 @@ py::dict stats_dict(const EngineStats& s) {
   d["path_batches"] = paths;
   d["inline_batches"] = s.inline_batches;
   d["direct_batches"] = s.direct_batches;
+  d["idle_batches"] = s.idle_batches;
   d["direct_dispatch"] = s.direct_dispatch;
   d["direct_device_kernargs"] = s.direct_device_kernargs;
   return d;
@@ -291,6 +292,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("spin_us", &EngineConfig::spin_us)
       .def_readwrite("wide_dtype", &EngineConfig::wide_dtype)
       .def_readwrite("inline_args", &EngineConfig::inline_args)
+      .def_readwrite("idle_inline_rows", &EngineConfig::idle_inline_rows)
       .def_readwrite("stage_wide", &EngineConfig::stage_wide)
       .def_readwrite("direct_dispatch", &EngineConfig::direct_dispatch)
       .def_readwrite("hsaco_path", &EngineConfig::hsaco_path)

@@ -411,6 +411,20 @@ class IoThread : public Sink {
   void flush_submits() {
     if (pend_tags_.empty()) return;
     const int n = (int)pend_tags_.size();
+    {
+      // idle engine: this thread launches the rows itself and renders the responses right away
+      // (no batcher / completer hand-off, no eventfd round trip)
+      idle_done_.clear();
+      std::shared_ptr<const Model> m;
+      if (srv_->engine()->run_idle(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), idle_done_, m)) {
+        pend_x_.clear();
+        pend_tags_.clear();
+        FastBatch fb{std::move(m), std::move(idle_done_)};
+        idle_done_ = std::vector<Completion>();
+        render_fast(fb);  // may parse pipelined requests into pend_*: flushed on the next round
+        return;
+      }
+    }
     const int r = srv_->engine()->submit_many(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), this);
     if (r != n) {
       // rows [0, r) were queued; the rest: overloaded -> 503 + Retry-After, engine stopping -> 500
@@ -698,6 +712,35 @@ class IoThread : public Sink {
     n_bad.fetch_add(1, std::memory_order_relaxed);
   }
 
+  // Responses of one batch of fast-path completions (each one then dispatches its connection's
+  // pipelined requests and flushes).
+  void render_fast(const FastBatch& fb) {
+    std::string& body = body_;
+    for (const Completion& cp : fb.c) {
+      auto it = conns_.find(cp.tag);
+      if (it == conns_.end()) continue;  // client went away
+      Conn* c = it->second.get();
+      c->waiting = false;
+      bool ok = cp.status == ST_OK && fb.model && cp.idx >= 0 && (size_t)cp.idx < fb.model->label_json.size();
+      if (ok) {
+        body.clear();
+        body += "{\"prediction\":";
+        body += fb.model->label_json[cp.idx];
+        body += ",\"probability\":";
+        ok = append_py_float(body, cp.p);
+        body += '}';
+      }
+      if (ok) {
+        append_response(c, 200, "OK", "application/json", body);
+        log_access(c, 200, "OK");
+      } else {
+        internal_error(c);
+        log_access(c, 500, "Internal Server Error");
+      }
+      process(c);  // dispatches pipelined requests, then flushes (may close c)
+    }
+  }
+
   void drain_pending() {
     std::vector<FastBatch> fast;
     std::vector<SlowResp> slow;
@@ -706,32 +749,7 @@ class IoThread : public Sink {
       fast.swap(fast_);
       slow.swap(slow_);
     }
-    std::string body;
-    for (FastBatch& fb : fast) {
-      for (const Completion& cp : fb.c) {
-        auto it = conns_.find(cp.tag);
-        if (it == conns_.end()) continue;  // client went away
-        Conn* c = it->second.get();
-        c->waiting = false;
-        bool ok = cp.status == ST_OK && fb.model && cp.idx >= 0 && (size_t)cp.idx < fb.model->label_json.size();
-        if (ok) {
-          body.clear();
-          body += "{\"prediction\":";
-          body += fb.model->label_json[cp.idx];
-          body += ",\"probability\":";
-          ok = append_py_float(body, cp.p);
-          body += '}';
-        }
-        if (ok) {
-          append_response(c, 200, "OK", "application/json", body);
-          log_access(c, 200, "OK");
-        } else {
-          internal_error(c);
-          log_access(c, 500, "Internal Server Error");
-        }
-        process(c);  // dispatches pipelined requests, then flushes (may close c)
-      }
-    }
+    for (FastBatch& fb : fast) render_fast(fb);
     for (SlowResp& sr : slow) {
       auto it = conns_.find(sr.conn_id);
       if (it == conns_.end()) continue;
@@ -986,6 +1004,8 @@ class IoThread : public Sink {
   std::atomic<bool> spinning_{false};  // inside the busy-poll window (no eventfd needed)
   std::mutex mu_;
   std::vector<FastBatch> fast_;
+  std::vector<Completion> idle_done_;  // run_idle completions (this thread only)
+  std::string body_;                   // response body scratch (this thread only)
   std::vector<SlowResp> slow_;
   std::vector<double> pend_x_;      // fast-path rows parsed in this epoll round (IO thread only)
   std::vector<uint64_t> pend_tags_;

@@ -589,6 +589,7 @@ void Engine::batcher_loop() {
         s.failed = true;
       } else {
         try {
+          std::lock_guard<std::mutex> lk(launch_mu_);
           launch_batch(s, *m, xs);
           s.launched = true;
         } catch (const std::exception&) {
@@ -614,6 +615,130 @@ void Engine::batcher_loop() {
   s_cv_.notify_all();
 }
 
+// Spin on the slot's done word (the kernel publishes s.seq with a system-scope release); back off
+// after ~50 us, check the stream / direct queue for a fault now and then, and give up on the batch
+// (ST_DEVICE_ERROR) after 10x the watchdog.
+void Engine::wait_done(Slot& s) {
+  const int si = (int)(&s - slots_.data());
+  volatile uint32_t* dw = done_h_ + (size_t)si * SIGNAL_STRIDE;
+  const int64_t t0 = now_ns();
+  uint32_t spins = 0;
+  while (__atomic_load_n(dw, __ATOMIC_ACQUIRE) != s.seq) {
+    ++spins;
+    if (spins < 20000) {
+      _mm_pause();
+      continue;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(spins < 40000 ? 2 : 50));
+    if ((spins & 63) == 0) {
+      const hipError_t q = hipStreamQuery(stream_);
+      if ((q != hipSuccess && q != hipErrorNotReady) || (direct_ && direct_->faulted())) {
+        s.failed = true;
+        healthy_.store(false);
+        return;
+      }
+      const int64_t waited = now_ns() - t0;
+      if (cfg_.watchdog_ms > 0 && waited > (int64_t)cfg_.watchdog_ms * 1000000) healthy_.store(false);
+      if (cfg_.watchdog_ms > 0 && waited > (int64_t)cfg_.watchdog_ms * 10000000) {
+        s.failed = true;
+        return;
+      }
+    }
+  }
+}
+
+namespace {
+struct CollectSink : Sink {
+  std::vector<Completion>* out;
+  void on_complete(const Completion* c, size_t n, const std::shared_ptr<const Model>&) override {
+    out->insert(out->end(), c, c + n);
+  }
+};
+}  // namespace
+
+// Idle-engine fast path. At batch = 1 the queued path costs two thread hand-offs before the
+// response can be written (submitter -> batcher futex wake, completer -> submitter eventfd wake),
+// several us each; with nothing queued or in flight there is no batch to join, so the submitting
+// thread launches and waits itself. The check is a heuristic (a request submitted by another
+// thread right after it simply takes the queued path and runs concurrently in another slot).
+bool Engine::run_idle(const double* X, int n, int nf, const uint64_t* tags, std::vector<Completion>& out,
+                      std::shared_ptr<const Model>& m_out) {
+  if (cfg_.idle_inline_rows <= 0 || n <= 0 || n > cfg_.idle_inline_rows || cfg_.device < 0) return false;
+  if (nf < 0 || nf > cfg_.max_features) return false;
+  if (drop_.load(std::memory_order_relaxed) || cfg_.fail_every > 0 || cfg_.delay_us > 0) return false;
+  if (inflight_n_.load(std::memory_order_acquire) != 0) return false;
+  std::shared_ptr<const Model> m = model();
+  // SMALL models only: their batches are kernel-argument packets (~0.03 us to dispatch) with a
+  // ~6 us GPU leg. Wide models are bound by the IO threads' JSON parsing; blocking one on a GEMV /
+  // GEMM launch + leg cost c=64 throughput (F=256 binary: 265k vs 306-310k req/s).
+  if (!m || m->path != PATH_SMALL) return false;
+  const int64_t t = now_ns();
+  {
+    std::lock_guard<std::mutex> lk(q_mu_);
+    if (stopping_ || !q_meta_.empty() || !batcher_sleeping_) return false;
+  }
+  int si;
+  {
+    std::lock_guard<std::mutex> lk(s_mu_);
+    if (free_slots_.empty() || !inflight_.empty()) return false;
+    si = free_slots_.front();
+    free_slots_.pop_front();
+  }
+  Slot& s = slots_[si];
+  thread_local std::vector<double> xs;
+  xs.assign(X, X + (size_t)n * nf);
+  s.metas.clear();
+  for (int i = 0; i < n; ++i) s.metas.push_back(Meta{tags[i], nullptr, t, nf, i * nf});
+  s.model = m;
+  s.n = n;
+  s.failed = false;
+  s.launched = false;
+  s.pre_status.assign((size_t)n, ST_OK);
+  try {
+    std::lock_guard<std::mutex> lk(launch_mu_);
+    launch_batch(s, *m, xs);
+    s.launched = true;
+  } catch (const std::exception&) {
+    s.failed = true;
+    healthy_.store(false);
+  }
+  s.t_launch = now_ns();
+  if (s.launched) wait_done(s);
+  const int64_t now = now_ns();
+  thread_local std::vector<int32_t> st;
+  thread_local std::vector<double> pd;
+  st.assign(s.pre_status.begin(), s.pre_status.end());
+  pd.resize((size_t)n);
+  if (s.failed) {
+    std::fill(st.begin(), st.end(), (int32_t)ST_DEVICE_ERROR);
+    std::fill(pd.begin(), pd.end(), 0.0);
+  } else if (m->pdt == DT_F64) {
+    std::memcpy(pd.data(), s.hp, (size_t)n * sizeof(double));
+  } else {
+    const float* pf = static_cast<const float*>(s.hp);
+    for (int i = 0; i < n; ++i) pd[i] = pf[i];
+  }
+  {
+    std::lock_guard<std::mutex> lk(st_mu_);
+    stats_.device_us_sum += (double)(now - s.t_launch) * 1e-3;
+    stats_.idle_batches++;
+  }
+  record_batch((size_t)n);
+  CollectSink sink;
+  sink.out = &out;
+  for (Meta& mt : s.metas) mt.sink = &sink;
+  deliver(s.metas, s.hidx, pd.data(), st.data(), m, now);
+  s.metas.clear();
+  s.model.reset();
+  m_out = std::move(m);
+  {
+    std::lock_guard<std::mutex> lk(s_mu_);
+    free_slots_.push_back(si);
+  }
+  s_cv_.notify_all();
+  return true;
+}
+
 void Engine::completer_loop() {
   pthread_setname_np(pthread_self(), "mlapi-compl");
   (void)hipSetDevice(cfg_.device);
@@ -635,36 +760,7 @@ void Engine::completer_loop() {
       inflight_n_.fetch_sub(1, std::memory_order_relaxed);
     }
     Slot& s = slots_[si];
-    if (s.launched) {
-      // Spin on the slot's done word (the kernel publishes s.seq with a system-scope release);
-      // back off after ~50 us, check the stream for a fault now and then, and give up on the
-      // batch (ST_DEVICE_ERROR) after 10x the watchdog.
-      volatile uint32_t* dw = done_h_ + (size_t)si * SIGNAL_STRIDE;
-      const int64_t t0 = now_ns();
-      uint32_t spins = 0;
-      while (__atomic_load_n(dw, __ATOMIC_ACQUIRE) != s.seq) {
-        ++spins;
-        if (spins < 20000) {
-          _mm_pause();
-          continue;
-        }
-        std::this_thread::sleep_for(std::chrono::microseconds(spins < 40000 ? 2 : 50));
-        if ((spins & 63) == 0) {
-          const hipError_t q = hipStreamQuery(stream_);
-          if ((q != hipSuccess && q != hipErrorNotReady) || (direct_ && direct_->faulted())) {
-            s.failed = true;
-            healthy_.store(false);
-            break;
-          }
-          const int64_t waited = now_ns() - t0;
-          if (cfg_.watchdog_ms > 0 && waited > (int64_t)cfg_.watchdog_ms * 1000000) healthy_.store(false);
-          if (cfg_.watchdog_ms > 0 && waited > (int64_t)cfg_.watchdog_ms * 10000000) {
-            s.failed = true;
-            break;
-          }
-        }
-      }
-    }
+    if (s.launched) wait_done(s);
     if (cfg_.delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(cfg_.delay_us));
     const int64_t now = now_ns();
     const size_t n = (size_t)s.n;

@@ -116,6 +116,11 @@ struct EngineConfig {
   // serving code object loads; empty path or failure -> hipLaunchKernel.
   bool direct_dispatch = true;
   std::string hsaco_path;
+  // Idle-engine fast path (run_idle): when nothing is queued or in flight, the submitting thread
+  // launches its rows itself and waits for the done word, skipping the batcher and completer
+  // wake-ups (two futex hand-offs on a batch=1 request). SMALL-path models, batches of at most
+  // this many rows; 0 = off.
+  int idle_inline_rows = 8;
 };
 
 struct EngineStats {
@@ -126,6 +131,7 @@ struct EngineStats {
   uint64_t path_batches[PATH_COUNT] = {0};  // GPU batches per kernel path
   uint64_t inline_batches = 0;      // SMALL batches launched through the kernel-argument block
   uint64_t direct_batches = 0;      // ... of which written straight into the HSA queue
+  uint64_t idle_batches = 0;        // batches run by the submitting thread (run_idle)
   bool direct_dispatch = false;     // the direct queue is up
   bool direct_device_kernargs = false;  // ... and its kernarg ring is in device memory
   double latency_sum_us = 0;
@@ -157,6 +163,12 @@ class Engine {
   // the request is malformed).
   static constexpr int SUBMIT_BUSY = -1;
   int submit_many(const double* X, int n, int nf, const uint64_t* tags, Sink* sink);
+  // Idle-engine fast path: if the engine has nothing queued or in flight (and the rows fit
+  // cfg.idle_inline_rows), launch the rows from the calling thread, wait for their done word and
+  // append their completions to `out` (model in `m_out`); true = done, the caller must not submit
+  // them. false = not eligible (busy, CPU backend, fault injection on, no model): submit normally.
+  bool run_idle(const double* X, int n, int nf, const uint64_t* tags, std::vector<Completion>& out,
+                std::shared_ptr<const Model>& m_out);
   // Blocking convenience API (tests / bulk scoring through the batcher).
   void predict(const double* X, int64_t B, int F, int32_t* idx, double* p, int32_t* status);
 
@@ -208,6 +220,8 @@ class Engine {
   void deliver(std::vector<Meta>& metas, const int32_t* idx, const double* p, const int32_t* st,
                const std::shared_ptr<const Model>& m, int64_t now);
   void record_batch(size_t n);
+  // Wait for a launched slot's done word (spin, then back off; fault and watchdog checks).
+  void wait_done(Slot& s);
 
   EngineConfig cfg_;
   std::shared_ptr<const Model> model_;
@@ -239,7 +253,8 @@ class Engine {
   uint32_t* done_d_ = nullptr;
   uint32_t* sig_counter_ = nullptr;  // device word for multi-block signalled launches
   static constexpr int SIGNAL_STRIDE = 16;  // 64 bytes: one cache line per slot
-  InlineBatch inline_{};        // batcher thread only
+  InlineBatch inline_{};        // guarded by launch_mu_
+  std::mutex launch_mu_;        // launch_batch: batcher thread and run_idle callers
 
   std::thread batcher_, completer_;
   std::atomic<bool> healthy_{true};

@@ -143,3 +143,47 @@ def test_native_server_wide_model_every_response(native, K, kind):
         assert srv.http.stats()["fast"] >= 1024  # no request fell back to the Python slow path
     finally:
         srv.stop()
+
+
+@pytest.mark.parametrize("F,K,kind", [(4, 3, Kind.MULTINOMIAL), (256, 2, Kind.BINARY), (256, 1000, Kind.MULTINOMIAL)])
+def test_idle_engine_fast_path(native, F, K, kind):
+    """One client, one request at a time: the engine is idle at every submit, so for a SMALL-path
+    model the IO thread launches the row itself (Engine::run_idle); wide models always take the
+    queued path. Bodies are identical to the queued path's (idle_inline_rows=0) and match the
+    oracle."""
+    from mlapi_amd.serve.server import NativeServer
+    from mlapi_amd.utils.config import Config
+
+    names = [f"f{i}" for i in range(F)]
+    m = LinearModel.random(F, K, seed=F + K, kind=kind, labels=[f"c{i}" for i in range(K)])
+    X = np.round(np.random.default_rng(11).standard_normal((200, F)), 3)
+    bodies = [json.dumps(dict(zip(names, map(float, row))), separators=(",", ":")).encode() for row in X]
+    out = {}
+    for rows in (8, 0):
+        cfg = Config.from_env(port=0, device="cuda:0", feature_names=names, reload="off", missing_model="keep",
+                              model_path="/nonexistent/idle.pkl", io_threads=2, idle_inline_rows=rows)
+        srv = NativeServer(cfg)
+        srv.runtime.handle.load(m)
+        srv.start()
+        try:
+            res = _post(srv.port, bodies)
+            assert all(st == 200 for st, _ in res)
+            out[rows] = [b for _, b in res]
+            st = srv.runtime.handle.stats()
+            if rows and F <= 32:
+                assert st["idle_batches"] >= 150, st  # nearly every request took the idle path
+            else:
+                assert st["idle_batches"] == 0
+            assert st["requests"] == len(bodies)
+        finally:
+            srv.stop()
+    assert out[8] == out[0]
+    got = [json.loads(b) for b in out[8]]
+    idx = np.array([int(g["prediction"][1:]) for g in got])
+    p = np.array([g["probability"] for g in got])
+    if F == 4:  # fp64 small path: exact sklearn parity
+        ridx, rp = m.predict_max(X)
+        np.testing.assert_array_equal(idx, ridx)
+        np.testing.assert_allclose(p, rp, rtol=1e-12, atol=0)
+    else:
+        check(m, X, idx, p, "bf16")
