@@ -13,6 +13,7 @@
 #include <mutex>
 
 #include "dist/comm.h"
+#include "dist/p2p.h"
 #include "http/loadgen.h"
 #include "http/server.h"
 #include "mlapi/common.h"
@@ -443,6 +444,31 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("world", &RcclComm::world)
       .def_property_readonly("device", &RcclComm::device)
       .def_property_readonly("aborted", &RcclComm::aborted);
+
+  // ---- one-shot P2P all-reduce over IPC-mapped peer buffers (csrc/dist/p2p.h)
+  py::class_<P2PAllReduce>(m, "P2PAllReduce")
+      .def(py::init<int, int, int, size_t>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("max_bytes"))
+      .def("data_handle", [](const P2PAllReduce& p) { return py::bytes(p.data_handle()); })
+      .def("flag_handle", [](const P2PAllReduce& p) { return py::bytes(p.flag_handle()); })
+      .def("open_peers",
+           [](P2PAllReduce& p, const std::vector<py::bytes>& d, const std::vector<py::bytes>& f) {
+             std::vector<std::string> ds, fs;
+             for (const auto& x : d) ds.emplace_back(x);
+             for (const auto& x : f) fs.emplace_back(x);
+             py::gil_scoped_release nogil;
+             p.open_peers(ds, fs);
+           },
+           py::arg("data_handles"), py::arg("flag_handles"))
+      .def("all_reduce",
+           [](P2PAllReduce& p, uintptr_t buf, size_t count, int dtype, uintptr_t stream, int timeout_ms) {
+             p.all_reduce(ptr<void>(buf), count, dtype, stream_of(stream), timeout_ms);
+           },
+           py::arg("buf"), py::arg("count"), py::arg("dtype"), py::arg("stream"), py::arg("timeout_ms") = 60000,
+           py::call_guard<py::gil_scoped_release>())
+      .def("status", &P2PAllReduce::status, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("epoch", &P2PAllReduce::epoch)
+      .def_property_readonly("max_bytes", &P2PAllReduce::max_bytes);
 
   py::class_<HttpServer>(m, "HttpServer")
       .def(py::init<Engine*, const ServerConfig&>(), py::keep_alive<1, 2>())

@@ -1,0 +1,69 @@
+// One-shot peer-to-peer all-reduce over IPC-mapped device memory ("a custom
+// one-shot P2P all-reduce over IPC peer pointers for the <= 1 MiB training gradients").
+//
+// Why: every DP collective of this framework is small (the fused [dW | b | loss | correct] buffer
+// is <= ~1 MiB), so it is latency bound. RCCL's ring pays 2(N-1) = 14 sequential hops
+// on 8 GPUs; on MI355X's full xGMI mesh each rank can instead read all N peers' buffers directly
+// (7 links in parallel) and reduce them itself: one hop, one launch.
+//
+// Protocol (per call, epoch e = 1, 2, ...):
+//   1. the caller's tensor is copied into this rank's IPC-exported buffer half (e & 1)
+//      (uncached memory: the stores reach HBM, so a peer reading over xGMI sees them);
+//   2. one kernel: block 0 publishes e into every peer's flag array (slot = this rank, system-scope
+//      release), every block waits until all N flags of its own array reached e (bounded spin:
+//      after timeout_ms it records a timeout in the status word and exits - never a hang), then
+//      sums the N peers' halves IN RANK ORDER (bitwise-identical results on every rank) into the
+//      caller's tensor.
+//   Double buffering makes a second barrier unnecessary: a rank overwrites half (e & 1) at epoch
+//   e + 2 only after its kernel for e + 1 saw every peer's flag e + 1, which each peer published
+//   after its kernel for e (the reads of half (e & 1)) had completed.
+//
+// Handles (hipIpcMemHandle_t, 64 bytes) are exchanged by the caller over the job's TCP store
+// (mlapi_amd/parallel/p2p.py). Peers on the SAME device (several ranks sharing one GPU, as in the
+// 1-GPU test box) work through the same code path.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mlapi {
+
+class P2PAllReduce {
+ public:
+  static constexpr int MAX_RANKS = 16;
+  P2PAllReduce(int rank, int world, int device, size_t max_bytes);
+  ~P2PAllReduce();
+  P2PAllReduce(const P2PAllReduce&) = delete;
+  P2PAllReduce& operator=(const P2PAllReduce&) = delete;
+
+  // This rank's exported handles: data buffer, flag array (64 bytes each).
+  std::string data_handle() const;
+  std::string flag_handle() const;
+  // Map every peer's buffers (handles indexed by rank; this rank's own entry is ignored).
+  void open_peers(const std::vector<std::string>& data_handles, const std::vector<std::string>& flag_handles);
+
+  // In-place sum of `count` elements (dtype: 7 = float32, 9 = bfloat16; RCCL enum values) on
+  // `stream`. count * elem_size <= max_bytes.
+  void all_reduce(void* buf, size_t count, int dtype, hipStream_t stream, int timeout_ms);
+  // 0 = every call so far completed; 1 = a call timed out waiting for a peer (sticky). Syncs.
+  int status();
+  uint32_t epoch() const { return epoch_; }
+  size_t max_bytes() const { return max_bytes_; }
+
+ private:
+  int rank_, world_, device_;
+  size_t max_bytes_;
+  void* data_ = nullptr;        // 2 halves of max_bytes (uncached, IPC-exported)
+  uint32_t* flags_ = nullptr;   // MAX_RANKS epoch words (uncached, IPC-exported)
+  uint32_t* status_ = nullptr;  // device word
+  void* peer_data_[MAX_RANKS] = {};
+  uint32_t* peer_flags_[MAX_RANKS] = {};
+  bool opened_[MAX_RANKS] = {};
+  uint32_t epoch_ = 0;
+  bool ready_ = false;
+};
+
+}  // namespace mlapi

@@ -37,6 +37,7 @@ SOURCES = [
     "http/server.cpp",
     "http/loadgen.cpp",
     "dist/comm.cpp",
+    "dist/p2p_allreduce.hip",
     "bindings.cpp",
 ]
 

@@ -1,0 +1,80 @@
+"""One-shot P2P all-reduce over IPC-mapped peer buffers (kernel and protocol:
+``csrc/dist/p2p.h``).
+
+Every DP collective of this framework is small (the fused ``[dW | b | loss | correct]`` gradient
+buffer), so it is latency bound: RCCL's ring pays 2(N-1) sequential hops, while on
+MI355X's full xGMI mesh each rank can read all N peers' buffers in one hop and reduce them itself.
+The reduction order is the rank order on every rank, so DP replicas stay bitwise identical.
+
+Handles are exchanged over the job's TCP store (the same host channel as RCCL's unique id). Ranks
+sharing one GPU (the 1-GPU test box) use the same code path. :class:`NativeComm` routes sum
+all-reduces of float32/bfloat16 tensors up to ``MLAPI_P2P_BYTES`` bytes here (0 = off).
+"""
+from __future__ import annotations
+
+import datetime
+from typing import Optional
+
+import torch
+
+_KEY = "mlapi/p2p/{gen}/{rank}/{what}"
+_DT = {torch.float32: 7, torch.bfloat16: 9}
+
+
+class P2PAllReduce:
+    """In-place sum all-reduce of float32 / bfloat16 GPU tensors across ``world`` ranks."""
+
+    def __init__(self, rank: int, world: int, device: torch.device, store=None, max_bytes: int = 4 << 20,
+                 generation: int = 0, timeout_s: float = 300.0):
+        from mlapi_amd._native import C
+
+        if device is None or device.type != "cuda":
+            raise ValueError("P2PAllReduce needs a GPU device")
+        self.rank, self.world, self.device = rank, world, device
+        self._p = C().P2PAllReduce(rank, world, device.index, int(max_bytes))
+        if world > 1:
+            if store is None:
+                from mlapi_amd.parallel.rccl import default_store
+
+                store = default_store()
+            for what, h in (("data", self._p.data_handle()), ("flag", self._p.flag_handle())):
+                store.set(_KEY.format(gen=generation, rank=rank, what=what), h)
+            keys = [_KEY.format(gen=generation, rank=r, what=w) for r in range(world) for w in ("data", "flag")]
+            store.wait(keys, datetime.timedelta(seconds=timeout_s))
+            data = [bytes(store.get(_KEY.format(gen=generation, rank=r, what="data"))) for r in range(world)]
+            flag = [bytes(store.get(_KEY.format(gen=generation, rank=r, what="flag"))) for r in range(world)]
+            self._p.open_peers(data, flag)
+
+    @property
+    def max_bytes(self) -> int:
+        return self._p.max_bytes
+
+    def supports(self, t: torch.Tensor, op: str = "sum") -> bool:
+        return (op == "sum" and t.dtype in _DT and t.is_cuda and t.is_contiguous()
+                and t.numel() * t.element_size() <= self.max_bytes and t.data_ptr() % 16 == 0)
+
+    def all_reduce_(self, t: torch.Tensor, timeout_ms: int = 60_000) -> torch.Tensor:
+        if not self.supports(t):
+            raise ValueError("P2PAllReduce: contiguous, 16-byte aligned float32/bfloat16 GPU tensor "
+                             f"of at most {self.max_bytes} bytes expected")
+        self._p.all_reduce(t.data_ptr(), t.numel(), _DT[t.dtype], torch.cuda.current_stream(t.device).cuda_stream,
+                           int(timeout_ms))
+        return t
+
+    def status(self) -> int:
+        """0 = every call completed; 1 = a call timed out waiting for a peer (sticky). Synchronises."""
+        return int(self._p.status())
+
+    def check(self) -> None:
+        if self.status() != 0:
+            raise RuntimeError("P2PAllReduce: a peer did not arrive within the timeout")
+
+
+def from_env(rank: int, world: int, device: torch.device, store=None) -> Optional[P2PAllReduce]:
+    """The P2P accelerator NativeComm uses when ``MLAPI_P2P_BYTES`` > 0 (and world > 1)."""
+    import os
+
+    n = int(os.environ.get("MLAPI_P2P_BYTES", "0"))
+    if n <= 0 or world <= 1:
+        return None
+    return P2PAllReduce(rank, world, device, store=store, max_bytes=n)

@@ -12,7 +12,8 @@ channel, plus a ``FakeComm`` with identical semantics for CPU-only multi-rank te
 
 Both speak in torch tensors. NativeComm is the default data plane of every GPU rank
 (``MLAPI_COMM=auto``, see :func:`mlapi_amd.parallel.comm.init_distributed`); ``MLAPI_COMM=torch``
-selects torch.distributed's own ``nccl`` backend (also RCCL) instead.
+selects torch.distributed's own ``nccl`` backend (also RCCL) instead. With ``MLAPI_P2P_BYTES`` > 0,
+small float32/bfloat16 sum all-reduces go through the one-shot P2P kernel (``parallel/p2p.py``).
 """
 from __future__ import annotations
 
@@ -70,6 +71,10 @@ class NativeComm:
         uid = (exchange_unique_id(store, rank, self._C.RcclComm.unique_id, generation) if world > 1
                else self._C.RcclComm.unique_id())
         self.comm = self._C.RcclComm(uid, rank, world, device.index)
+        # small sum all-reduces through the one-shot P2P kernel when MLAPI_P2P_BYTES > 0 (parallel/p2p.py)
+        from mlapi_amd.parallel.p2p import from_env
+
+        self.p2p = from_env(rank, world, device, store=store)
 
     @staticmethod
     def _stream() -> int:
@@ -81,6 +86,8 @@ class NativeComm:
 
     def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         self._check(t)
+        if self.p2p is not None and self.p2p.supports(t, op):
+            return self.p2p.all_reduce_(t, self.timeout_ms)
         self.comm.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPE[t.dtype], _OPS[op], self._stream())
         return t
 

@@ -2,7 +2,8 @@
 
 Multi-rank RCCL runs need one GPU per rank (RCCL rejects two ranks on one device); the same
 collective code paths are covered at world_size 2 on CPU through FakeComm
-(tests/test_distributed.py::test_fake_comm_collectives)."""
+(tests/test_distributed.py::test_fake_comm_collectives). The one-shot P2P all-reduce runs with
+2 and 4 processes sharing the GPU."""
 import json
 import os
 import subprocess
@@ -54,3 +55,26 @@ def test_bench_defaults_to_native_comm(mode):
     assert out.returncode == 0, out.stderr[-3000:]
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["comm_backend"] == "native-rccl"
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_p2p_allreduce_multiprocess(tmp_path, world):
+    """One-shot P2P all-reduce (csrc/dist/p2p_allreduce.hip) across `world` processes: IPC handles
+    exchanged over the TCP store, peers' buffers mapped, bitwise rank-order sums, double-buffered
+    epochs, and a bounded wait (status 1, no hang) when a peer never arrives. On the 1-GPU box all
+    ranks share the GPU (RCCL itself refuses that), which exercises the same code path."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(ROOT / "tests" / "dist" / "p2p_allreduce.py")]
+    out = subprocess.run(cmd, env={**ENV, "OUT": str(tmp_path), "OMP_NUM_THREADS": "1"}, capture_output=True,
+                         text=True, timeout=240, cwd=ROOT)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
+    res = [json.loads((tmp_path / f"P2P_{r}.json").read_text()) for r in range(world)]
+    assert all(x["checks"] == 7 for x in res)
+    assert res[0]["timed_out"] == 1
+    print({"world": world, "us_per_call_256k": [round(x["us_per_call_256k"], 1) for x in res]})
