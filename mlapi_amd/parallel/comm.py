@@ -19,7 +19,10 @@ Data plane selection (``MLAPI_COMM``): ``auto`` (default) = ``native`` when the 
 stream PyTorch hands over, with deadline/abort) with a gloo process group kept only as the host
 control plane (rendezvous, unique-id exchange, reload control); ``torch`` uses torch.distributed
 (``nccl`` = RCCL on GPUs, ``gloo`` on CPUs); ``fake`` runs the native code paths on CPU through
-:class:`~mlapi_amd.parallel.rccl.FakeComm` (tests).
+:class:`~mlapi_amd.parallel.rccl.FakeComm` (tests); ``p2p`` keeps float32/bfloat16 sum
+all-reduces on the GPU through the one-shot P2P kernel (:class:`mlapi_amd.parallel.p2p.P2PComm`,
+csrc/dist/p2p_allreduce.hip) and sends the rest through gloo - it also runs with several ranks on
+one device, which RCCL refuses.
 """
 from __future__ import annotations
 
@@ -53,8 +56,8 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
                      comm: Optional[str] = None) -> DistInfo:
     """Initialise from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); no-op for 1 process."""
     comm = (comm or os.environ.get("MLAPI_COMM", "auto")).lower()
-    if comm not in ("auto", "torch", "native", "fake"):
-        raise ValueError(f"MLAPI_COMM must be auto, torch, native or fake (got {comm!r})")
+    if comm not in ("auto", "torch", "native", "fake", "p2p"):
+        raise ValueError(f"MLAPI_COMM must be auto, torch, native, fake or p2p (got {comm!r})")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -67,8 +70,8 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
     if comm == "auto":
         comm = "native" if device is not None else "torch"
     info = DistInfo(rank, world, local_rank, device, "none")
-    if comm == "native" and device is None:
-        raise RuntimeError("MLAPI_COMM=native needs a GPU (use fake for CPU runs)")
+    if comm in ("native", "p2p") and device is None:
+        raise RuntimeError(f"MLAPI_COMM={comm} needs a GPU (use fake for CPU runs)")
     if world > 1:
         if not dist.is_initialized():
             if comm != "torch":
@@ -82,6 +85,11 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
 
         info.comm = NativeComm(rank, world, device)
         info.backend = NativeComm.kind
+    elif comm == "p2p":
+        from mlapi_amd.parallel.p2p import P2PComm
+
+        info.comm = P2PComm(rank, world, device)
+        info.backend = P2PComm.kind
     elif comm == "fake":
         from mlapi_amd.parallel.rccl import FakeComm
 

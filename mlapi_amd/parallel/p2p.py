@@ -78,3 +78,53 @@ def from_env(rank: int, world: int, device: torch.device, store=None) -> Optiona
     if n <= 0 or world <= 1:
         return None
     return P2PAllReduce(rank, world, device, store=store, max_bytes=n)
+
+
+class P2PComm:
+    """Communicator (NativeComm's API) whose data plane is the one-shot P2P kernel: float32 /
+    bfloat16 sum all-reduces stay on the GPU; the rare control-plane collectives (broadcast,
+    gather, max) go through the host gloo group. Selected with ``MLAPI_COMM=p2p``; it is the GPU
+    data plane that also works with several ranks on ONE device (RCCL refuses that), which is how
+    multi-rank DP training is exercised on the 1-GPU test box."""
+
+    kind = "p2p+gloo"
+
+    def __init__(self, rank: int, world: int, device: torch.device, max_bytes: int = 4 << 20):
+        from mlapi_amd.parallel.rccl import FakeComm
+
+        self.rank, self.world, self.device = rank, world, device
+        self.p2p = P2PAllReduce(rank, world, device, max_bytes=max_bytes) if world > 1 else None
+        self._host = FakeComm(rank, world)
+        self.aborted = False
+
+    def _via_host(self, t: torch.Tensor, fn) -> torch.Tensor:
+        h = t.detach().cpu()
+        out = fn(h)
+        return out.to(t.device) if out is not h else t.copy_(h)
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.world == 1:
+            return t
+        if self.p2p is not None and self.p2p.supports(t, op):
+            return self.p2p.all_reduce_(t)
+        return self._via_host(t, lambda h: self._host.all_reduce_(h, op))
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        return self._via_host(t, lambda h: self._host.broadcast_(h, src))
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        return self._host.all_gather(t.detach().cpu()).to(t.device)
+
+    def reduce_scatter(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        return self._host.reduce_scatter(t.detach().cpu(), op).to(t.device)
+
+    def barrier(self) -> None:
+        torch.cuda.synchronize(self.device)
+        self._host.barrier()
+
+    def wait(self, timeout_ms: Optional[int] = None) -> None:
+        if self.p2p is not None:
+            self.p2p.check()
+
+    def abort(self) -> None:
+        self.aborted = True

@@ -78,3 +78,34 @@ def test_p2p_allreduce_multiprocess(tmp_path, world):
     assert all(x["checks"] == 7 for x in res)
     assert res[0]["timed_out"] == 1
     print({"world": world, "us_per_call_256k": [round(x["us_per_call_256k"], 1) for x in res]})
+
+
+def _torchrun(world, script, out_dir):
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(ROOT / "tests" / "dist" / script)]
+    out = subprocess.run(cmd, env={**ENV, "OUT": str(out_dir), "OMP_NUM_THREADS": "1"}, capture_output=True,
+                         text=True, timeout=240, cwd=ROOT)
+    assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
+
+
+def test_dp_sgd_on_gpu_with_p2p_allreduce(tmp_path):
+    """Two GPU ranks (sharing the box's GPU) train with HIP gradient kernels and the P2P all-reduce
+    as the data plane: replicas stay bitwise identical, match one rank on the global batch, and the
+    model broadcast (C1) arrives intact."""
+    import numpy as np
+
+    _torchrun(1, "dp_train_gpu.py", tmp_path)
+    _torchrun(2, "dp_train_gpu.py", tmp_path)
+    for name in ("params", "mc_params"):
+        a, b = np.load(tmp_path / f"{name}_2_0.npy"), np.load(tmp_path / f"{name}_2_1.npy")
+        assert np.array_equal(a, b), f"{name}: DP replicas must stay bitwise identical"
+        np.testing.assert_allclose(a, np.load(tmp_path / f"{name}_1_0.npy"), rtol=2e-3, atol=2e-4)
+    j0, j1 = (json.loads((tmp_path / f"bcast_2_{r}.json").read_text()) for r in range(2))
+    assert j0["W"] == j1["W"] and j0["classes"] == list("abcde")
+    assert j0["p2p_calls"] >= 35 and j0["acc"] > 0.8
