@@ -351,8 +351,10 @@ def main(argv=None) -> int:
     ap.add_argument("--softmax-features", type=int, default=256, help="train_softmax: F (<= 512)")
     ap.add_argument("--cpu", action="store_true", help="force the CPU backend (testing without a GPU)")
     ap.add_argument("--pin", default="auto", choices=["auto", "on", "off"],
-                    help="pin this rank to its share of physical cores on its GPU's NUMA node "
-                         "(auto: when several ranks share the node and no launcher pinned them)")
+                    help="pin this rank to its share of physical cores on its GPU's NUMA node, server "
+                         "and load generator on disjoint cores (auto = off: measured interleaved on "
+                         "one box, pinning cost c=64 throughput at N=1 (0.65-0.80 M vs 0.98-1.06 M "
+                         "req/s) and N=2 (0.83-0.85 M vs 0.92-1.02 M), profiles/r2_pin/)")
     args = ap.parse_args(argv)
     if args.mode in ("serve", "serve_wide"):
         # the load generator is its own process, started before anything touches the GPU
@@ -365,7 +367,7 @@ def main(argv=None) -> int:
     info = init_distributed(use_gpu=False if args.cpu else None)
     local = int(os.environ.get("LOCAL_WORLD_SIZE", info.world))
     pinned = []
-    if args.pin == "on" or (args.pin == "auto" and local > 1 and not os.environ.get("MLAPI_LAUNCHER")):
+    if args.pin == "on":
         # before any native thread starts: the server / batcher / load-generator threads inherit it
         from mlapi_amd.utils.affinity import pin_this_rank
 

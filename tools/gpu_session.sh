@@ -10,6 +10,7 @@
 #   serve         headline bench (Iris /predict)           serve_wide F=256 /predict, K=1000 and K=2
 #   serve_ab      serve with kernel-argument batches on/off, interleaved x2 (box variance is large)
 #   serve_idle    serve with the idle-engine fast path on (8 rows) / off, interleaved x2
+#   serve_pin     serve with the rank pinned to physical cores (server / load generator apart) vs unpinned, x2
 #   serve_spin    serve with busy-polling IO threads / spinning batcher+completer (SPINS="0 50"), interleaved x2
 #   kbench        gemv / gemm / train / train_softmax benches
 #   prof          rocprofv3 --kernel-trace --stats of every bench mode (incl. serve and serve_wide)
@@ -57,6 +58,12 @@ for s in $steps; do
       for r in 1 2; do
         for m in 8 0; do
           MLAPI_IDLE_INLINE_ROWS=$m run "serve_idle${m}_r$r" 300 python -u bench.py --steps 60 --warmup 5
+        done
+      done ;;
+    serve_pin)
+      for r in 1 2; do
+        for p in on off; do
+          run "serve_pin${p}_r$r" 300 python -u bench.py --steps 60 --warmup 5 --pin $p
         done
       done ;;
     serve_spin)
