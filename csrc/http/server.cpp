@@ -161,11 +161,63 @@ bool skip_value(const char* p, size_t n, size_t& i, int depth) {
   return false;  // NaN / Infinity / garbage -> slow path
 }
 
+// Clinger's fast path for a token scan_number() accepted: when the decimal significand has at most
+// 15 significant digits (< 2^53, exact in a double) and the power of ten is exact too (|e| <= 22),
+// ONE correctly rounded IEEE multiply or divide gives the correctly rounded value, i.e. exactly
+// what strtod / Python's float() return. Everything else falls back to strtod. A wide model's
+// body is 256+ numbers; strtod's ~100 ns each made the IO threads' parsing the bottleneck.
+bool fast_decimal(const char* p, size_t len, double* out) {
+  static const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                    1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  size_t i = 0;
+  const bool neg = p[0] == '-';
+  if (neg) ++i;
+  uint64_t m = 0;
+  int sig = 0, e10 = 0;
+  for (; i < len && p[i] >= '0' && p[i] <= '9'; ++i) {
+    if (m == 0 && p[i] == '0') continue;  // leading zeros are not significant
+    if (++sig > 15) return false;
+    m = m * 10 + (uint64_t)(p[i] - '0');
+  }
+  if (i < len && p[i] == '.') {
+    for (++i; i < len && p[i] >= '0' && p[i] <= '9'; ++i) {
+      --e10;
+      if (m == 0 && p[i] == '0') continue;
+      if (++sig > 15) return false;
+      m = m * 10 + (uint64_t)(p[i] - '0');
+    }
+  }
+  if (i < len && (p[i] == 'e' || p[i] == 'E')) {
+    ++i;
+    bool eneg = false;
+    if (p[i] == '+' || p[i] == '-') eneg = p[i++] == '-';
+    int x = 0;
+    for (; i < len; ++i) {
+      if (x > 1000) return false;
+      x = x * 10 + (p[i] - '0');
+    }
+    e10 += eneg ? -x : x;
+  }
+  double v;
+  if (m == 0) {
+    v = 0.0;
+  } else if (e10 >= 0 && e10 <= 22) {
+    v = (double)m * kPow10[e10];
+  } else if (e10 < 0 && e10 >= -22) {
+    v = (double)m / kPow10[-e10];
+  } else {
+    return false;
+  }
+  *out = neg ? -v : v;
+  return true;
+}
+
 // Strict JSON number (RFC 8259 grammar) -> finite double.
 bool parse_number(const char* p, size_t n, size_t& i, double* out) {
   const size_t s = i;
   if (!scan_number(p, n, i)) return false;
   const size_t len = i - s;
+  if (fast_decimal(p + s, len, out) && std::isfinite(*out)) return true;
   if (len > 400) return false;  // absurd literals: let Python decide
   char buf[416];
   memcpy(buf, p + s, len);

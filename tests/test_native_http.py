@@ -286,3 +286,33 @@ def test_parser_matches_json_loads(native, vals, extra):
 @given(st.floats(allow_nan=False, allow_infinity=False))
 def test_float_repr_matches_python(native, v):
     assert native.py_float_repr(v) == repr(v) == json.dumps(v)
+
+
+def test_fast_number_path_matches_python_float(native):
+    """The parser's Clinger fast path (<= 15 significant digits, |10^e| <= 22) and its strtod
+    fallback both give Python's float() bit for bit, over tokens of every shape the wide-model
+    bodies and the reference's clients send."""
+    import random
+    import struct
+
+    rng = random.Random(12)
+    toks = ["0", "-0", "0.0", "-0.0", "1", "-1", "5.1", "3.5", "1e22", "1e23", "1e-22", "1e-23", "9007199254740993",
+            "123456789012345", "1234567890123456", "0.1", "0.30000000000000004", "1.7976931348623157e308",
+            "2.2250738585072014e-308", "4.9e-324", "1E+2", "1e-0", "0.000000000000000000001", "100000000000000000000000",
+            "123.456e-5", "-9.87654321012345e10"]
+    for _ in range(3000):
+        kind = rng.randrange(4)
+        if kind == 0:
+            toks.append(repr(rng.gauss(0, 1)))
+        elif kind == 1:
+            toks.append(f"{rng.uniform(-1e4, 1e4):.{rng.randrange(0, 8)}f}")
+        elif kind == 2:
+            toks.append(f"{rng.randrange(1, 10**rng.randrange(1, 18))}e{rng.randrange(-30, 30)}")
+        else:
+            toks.append(f"{rng.choice(['', '-'])}{rng.randrange(0, 10**6)}.{rng.randrange(0, 10**rng.randrange(1, 12))}")
+    names = [f"f{i}" for i in range(len(toks))]
+    body = "{" + ",".join(f'"{n}":{t}' for n, t in zip(names, toks)) + "}"
+    got = native.parse_predict_body(body, names)
+    assert got is not None
+    for t, g in zip(toks, got):
+        assert struct.pack("<d", g) == struct.pack("<d", float(t)), t
