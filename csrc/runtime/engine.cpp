@@ -663,7 +663,7 @@ struct CollectSink : Sink {
 // thread right after it simply takes the queued path and runs concurrently in another slot).
 bool Engine::run_idle(const double* X, int n, int nf, const uint64_t* tags, std::vector<Completion>& out,
                       std::shared_ptr<const Model>& m_out) {
-  if (cfg_.idle_inline_rows <= 0 || n <= 0 || n > cfg_.idle_inline_rows || cfg_.device < 0) return false;
+  if (cfg_.idle_inline_rows <= 0 || n <= 0 || n > cfg_.idle_inline_rows) return false;
   if (nf < 0 || nf > cfg_.max_features) return false;
   if (drop_.load(std::memory_order_relaxed) || cfg_.fail_every > 0 || cfg_.delay_us > 0) return false;
   if (inflight_n_.load(std::memory_order_acquire) != 0) return false;
@@ -676,6 +676,22 @@ bool Engine::run_idle(const double* X, int n, int nf, const uint64_t* tags, std:
   {
     std::lock_guard<std::mutex> lk(q_mu_);
     if (stopping_ || !q_meta_.empty() || !batcher_sleeping_) return false;
+  }
+  CollectSink sink;
+  sink.out = &out;
+  if (cfg_.device < 0) {  // CPU backend: the float64 oracle, in this thread
+    thread_local std::vector<Meta> metas;
+    thread_local std::vector<double> xs;
+    xs.assign(X, X + (size_t)n * nf);
+    metas.clear();
+    for (int i = 0; i < n; ++i) metas.push_back(Meta{tags[i], &sink, t, nf, i * nf});
+    run_cpu(metas, xs, m);
+    {
+      std::lock_guard<std::mutex> lk(st_mu_);
+      stats_.idle_batches++;
+    }
+    m_out = std::move(m);
+    return true;
   }
   int si;
   {
@@ -724,8 +740,6 @@ bool Engine::run_idle(const double* X, int n, int nf, const uint64_t* tags, std:
     stats_.idle_batches++;
   }
   record_batch((size_t)n);
-  CollectSink sink;
-  sink.out = &out;
   for (Meta& mt : s.metas) mt.sink = &sink;
   deliver(s.metas, s.hidx, pd.data(), st.data(), m, now);
   s.metas.clear();

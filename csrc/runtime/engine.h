@@ -119,7 +119,7 @@ struct EngineConfig {
   // Idle-engine fast path (run_idle): when nothing is queued or in flight, the submitting thread
   // launches its rows itself and waits for the done word, skipping the batcher and completer
   // wake-ups (two futex hand-offs on a batch=1 request). SMALL-path models, batches of at most
-  // this many rows; 0 = off.
+  // this many rows; 0 = off. On the CPU backend the calling thread runs the float64 oracle.
   int idle_inline_rows = 8;
 };
 

@@ -316,3 +316,34 @@ def test_fast_number_path_matches_python_float(native):
     assert got is not None
     for t, g in zip(toks, got):
         assert struct.pack("<d", g) == struct.pack("<d", float(t)), t
+
+
+def test_idle_engine_fast_path_cpu_backend(iris_cwd):
+    """One client at a time: the IO thread runs the row itself (Engine::run_idle, here the float64
+    oracle of the CPU backend), bodies identical to the queued path; under concurrency the batcher
+    still coalesces."""
+    from mlapi_amd.serve.server import NativeServer
+    from mlapi_amd.utils.config import Config
+
+    rng = np.random.default_rng(3)
+    bodies = [json.dumps(dict(zip(NAMES, map(float, np.round(r, 1))))).encode() for r in
+              rng.normal([5.8, 3.0, 3.8, 1.2], [0.8, 0.4, 1.8, 0.8], (60, 4))]
+    out = {}
+    for rows in (8, 0):
+        srv = NativeServer(Config.from_env(port=0, device="cpu", io_threads=2, idle_inline_rows=rows)).start()
+        try:
+            s = socket.create_connection(("127.0.0.1", srv.port), timeout=5)
+            got = []
+            for b in bodies:
+                s.sendall(post(b))
+                buf = b""
+                while not buf.endswith(b"}"):
+                    buf += s.recv(4096)
+                got.append(buf.split(b"\r\n\r\n", 1)[1])
+            s.close()
+            st = srv.runtime.handle.stats()
+            assert (st["idle_batches"] >= 50) if rows else st["idle_batches"] == 0, st
+            out[rows] = got
+        finally:
+            srv.stop()
+    assert out[8] == out[0]
