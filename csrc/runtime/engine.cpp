@@ -139,7 +139,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     }
   }
   batcher_ = std::thread([this] { batcher_loop(); });
-  if (cfg_.device >= 0) completer_ = std::thread([this] { completer_loop(); });
+  if (cfg_.device >= 0)
+    for (int i = 0; i < std::max(1, cfg_.completers); ++i) completers_.emplace_back([this] { completer_loop(); });
 }
 
 Engine::~Engine() {
@@ -171,7 +172,8 @@ void Engine::stop() {
   q_cv_.notify_all();
   if (batcher_.joinable()) batcher_.join();
   s_cv_.notify_all();
-  if (completer_.joinable()) completer_.join();
+  for (std::thread& t : completers_)
+    if (t.joinable()) t.join();
 }
 
 uint64_t Engine::load_model(int kind, int F, int K, const double* W, const double* b,

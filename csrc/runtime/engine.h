@@ -111,6 +111,11 @@ struct EngineConfig {
   int delay_us = 0;       // fault injection: extra per-batch delay
   int spin_us = 0;        // batcher / completer poll their queues this long before sleeping on a condvar
                           // (saves the futex wake-up on the request path under load)
+  // Completer threads: each takes the oldest in-flight slot, waits for its done word and delivers
+  // it (grouping by sink, one eventfd wake per IO thread); with several, the delivery of batch k
+  // overlaps the wait for batch k+1. Per-connection order is safe: a connection has at most one
+  // request outstanding.
+  int completers = 1;
   int max_queue = 1 << 20;  // backpressure: rows waiting for the batcher; beyond it submit is refused
   // Kernel-argument batches go through the engine's own HSA queue (direct_dispatch.h) when the
   // serving code object loads; empty path or failure -> hipLaunchKernel.
@@ -256,7 +261,8 @@ class Engine {
   InlineBatch inline_{};        // guarded by launch_mu_
   std::mutex launch_mu_;        // launch_batch: batcher thread and run_idle callers
 
-  std::thread batcher_, completer_;
+  std::thread batcher_;
+  std::vector<std::thread> completers_;
   std::atomic<bool> healthy_{true};
   std::atomic<bool> drop_{false};
 
