@@ -39,10 +39,19 @@ struct InlineBatch {
   int32_t n, F, K, kind;
   int32_t* out_idx;
   void* out_p;
-  uint32_t* done;  // ServeSignal of the batch (one block: no counter)
+  uint32_t* done;  // ServeSignal of the batch (one block: no counter); null with `rec`
   uint32_t seq;
+  // Per-row completion records (host-mapped, ServeRecord[n]); when set, each row's result AND the
+  // batch's sequence number go out in ONE 16-byte store, with no fence and no done word.
+  void* rec;
   alignas(16) unsigned char wb[INLINE_WB_BYTES];  // W [K][F] then b [K] (dtype of the launch)
   alignas(16) unsigned char x[INLINE_X_BYTES];    // rows [n][F]
+};
+// One row's result as the host polls it: seq last written by the batch that produced it.
+struct alignas(16) ServeRecord {
+  uint32_t seq;
+  int32_t idx;
+  double p;
 };
 // true if n rows of F features (and the K x F model) fit the argument block in dtype `dt`
 bool linear_inline_fits(int dt, int64_t n, int F, int K);

@@ -124,6 +124,46 @@ __device__ __forceinline__ void inline_batch_rows(const InlineBatch* a) {
     int32_t idx;
     T p;
     row_predict<T, FMAX, KMAX>(reinterpret_cast<const T*>(a->x) + r * F, W, b, F, K, kind, idx, p);
+    if (a->rec != nullptr) {  // uniform: one 16-byte store carries the result and the batch's seq
+      const uint64_t pb = __builtin_bit_cast(uint64_t, (double)p);
+      typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
+      const u32x4_t v = {a->seq, (uint32_t)idx, (uint32_t)pb, (uint32_t)(pb >> 32)};
+      // System-scope (sc0 sc1) write-through vector store: the record reaches host memory without
+      // a release fence or an end-of-kernel cache flush (a plain store sat in the GPU's caches
+      // until something else flushed them: ~1 s with the fence-free direct-dispatch packet). The
+      // compiler emits the same bits for a 4/8-byte system-scope atomic store; there is no 16-byte
+      // atomic, hence the asm.
+      ServeRecord* dst = static_cast<ServeRecord*>(a->rec) + r;
+      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
+    } else {
+      a->out_idx[r] = idx;
+      static_cast<T*>(a->out_p)[r] = p;
+    }
+  }
+}
+
+// Exact-shape variant (compile-time F, K: the headline Iris model is F=4, K=3). Every address is
+// a constant offset from the kernarg base or the lane's row, so all loads issue at once: the
+// runtime-shape kernel first waits for the header (n, F, K), then issues guarded loads, then walks
+// W with a scalar load and a wait per element (5+ dependent round trips to the freshly written
+// kernarg memory). Lanes past n read a clamped in-bounds row and do not store.
+template <typename T, int F, int K>
+__device__ __forceinline__ void inline_batch_rows_exact(const InlineBatch* a) {
+  constexpr int XCAP = INLINE_X_BYTES / (F * (int)sizeof(T));
+  const int r = threadIdx.x;
+  const int rr = r < XCAP ? r : XCAP - 1;
+  const T* W = reinterpret_cast<const T*>(a->wb);
+  int32_t idx;
+  T p;
+  row_predict<T, F, K>(reinterpret_cast<const T*>(a->x) + rr * F, W, W + K * F, F, K, a->kind, idx, p);
+  if (r >= a->n) return;
+  if (a->rec != nullptr) {
+    const uint64_t pb = __builtin_bit_cast(uint64_t, (double)p);
+    typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
+    const u32x4_t v = {a->seq, (uint32_t)idx, (uint32_t)pb, (uint32_t)(pb >> 32)};
+    ServeRecord* dst = static_cast<ServeRecord*>(a->rec) + r;
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
+  } else {
     a->out_idx[r] = idx;
     static_cast<T*>(a->out_p)[r] = p;
   }

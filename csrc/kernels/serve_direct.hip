@@ -13,10 +13,13 @@
 
 namespace {
 
-template <typename T, int FMAX, int KMAX>
+template <typename T, int FMAX, int KMAX, bool EXACT = false>
 __device__ __forceinline__ void direct_inline() {
   const mlapi::InlineBatch* a = (const mlapi::InlineBatch*)__builtin_amdgcn_kernarg_segment_ptr();
-  mlapi::rows::inline_batch_rows<T, FMAX, KMAX>(a);
+  if constexpr (EXACT)
+    mlapi::rows::inline_batch_rows_exact<T, FMAX, KMAX>(a);
+  else
+    mlapi::rows::inline_batch_rows<T, FMAX, KMAX>(a);
   if (a->done == nullptr) return;  // uniform
   __threadfence_system();
   __syncthreads();
@@ -37,4 +40,11 @@ extern "C" __global__ __launch_bounds__(128) void mlapi_inline_f32_s(const mlapi
 }
 extern "C" __global__ __launch_bounds__(128) void mlapi_inline_f32_w(const mlapi::InlineBatch) {
   direct_inline<float, 32, 16>();
+}
+// exact F=4, K=3 (the headline Iris shape): all loads in one batch
+extern "C" __global__ __launch_bounds__(128) void mlapi_inline_f64_4x3(const mlapi::InlineBatch) {
+  direct_inline<double, 4, 3, true>();
+}
+extern "C" __global__ __launch_bounds__(128) void mlapi_inline_f32_4x3(const mlapi::InlineBatch) {
+  direct_inline<float, 4, 3, true>();
 }

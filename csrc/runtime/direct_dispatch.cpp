@@ -117,9 +117,9 @@ class HsaInlineDispatcher final : public InlineDispatcher {
         hsa_executable_load_agent_code_object(exe_, gpu_, reader_, nullptr, nullptr) != HSA_STATUS_SUCCESS ||
         hsa_executable_freeze(exe_, nullptr) != HSA_STATUS_SUCCESS)
       return fail("code object does not load for this GPU");
-    const char* names[4] = {"mlapi_inline_f64_s.kd", "mlapi_inline_f64_w.kd", "mlapi_inline_f32_s.kd",
-                            "mlapi_inline_f32_w.kd"};
-    for (int i = 0; i < 4; ++i) {
+    const char* names[6] = {"mlapi_inline_f64_s.kd", "mlapi_inline_f64_w.kd", "mlapi_inline_f32_s.kd",
+                            "mlapi_inline_f32_w.kd", "mlapi_inline_f64_4x3.kd", "mlapi_inline_f32_4x3.kd"};
+    for (int i = 0; i < 6; ++i) {
       hsa_executable_symbol_t sym;
       if (hsa_executable_get_symbol_by_name(exe_, names[i], &gpu_, &sym) != HSA_STATUS_SUCCESS)
         return fail(std::string("kernel ") + names[i] + " missing");
@@ -162,7 +162,8 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   void launch(int dt, const InlineBatch& a) override {
     if (dt != DT_F64 && dt != DT_F32) throw std::invalid_argument("direct dispatch: f64 / f32 batches only");
     if (faulted()) throw std::runtime_error("direct dispatch: queue error");
-    const Kernel& k = k_[(dt == DT_F64 ? 0 : 2) + (a.F <= 8 && a.K <= 4 ? 0 : 1)];
+    const Kernel& k = (a.F == 4 && a.K == 3) ? k_[dt == DT_F64 ? 4 : 5]  // exact shape: one load batch
+                                              : k_[(dt == DT_F64 ? 0 : 2) + (a.F <= 8 && a.K <= 4 ? 0 : 1)];
     char* ka = kernargs_ + (size_t)(launches_++ % KA_SLOTS) * stride_;
     // Only the bytes the kernel reads: header + W/b of this model + n rows.
     const size_t es = dt == DT_F64 ? 8 : 4;
@@ -215,7 +216,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   std::vector<char> blob_;
   hsa_code_object_reader_t reader_{};
   hsa_executable_t exe_{};
-  Kernel k_[4];
+  Kernel k_[6];
   hsa_queue_t* queue_ = nullptr;
   char* kernargs_ = nullptr;
   uint32_t* hdp_flush_ = nullptr;  // non-null: the ring is in device memory

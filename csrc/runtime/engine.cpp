@@ -134,6 +134,10 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.didx, s.hidx, 0));
       MLAPI_HIP_CHECK(hipHostMalloc(&s.hp, (size_t)cfg_.max_batch * sizeof(double), hipHostMallocMapped));
       MLAPI_HIP_CHECK(hipHostGetDevicePointer(&s.dp, s.hp, 0));
+      const size_t rb = (size_t)cfg_.max_batch * sizeof(ServeRecord);
+      MLAPI_HIP_CHECK(hipHostMalloc((void**)&s.hrec, rb, hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(s.hrec, 0, rb);  // seq 0 is never launched
+      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.drec, s.hrec, 0));
       s.metas.reserve(cfg_.max_batch);
       free_slots_.push_back(i);
     }
@@ -155,6 +159,7 @@ Engine::~Engine() {
       if (s.dstage) (void)hipFree(s.dstage);
       if (s.hidx) (void)hipHostFree(s.hidx);
       if (s.hp) (void)hipHostFree(s.hp);
+      if (s.hrec) (void)hipHostFree(s.hrec);
     }
     {
       std::lock_guard<std::mutex> lk(model_mu_);
@@ -470,7 +475,9 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     a.kind = m.kind;
     a.out_idx = s.didx;
     a.out_p = s.dp;
-    a.done = sig.done;
+    s.rec_mode = cfg_.record_completion;
+    a.done = s.rec_mode ? nullptr : sig.done;
+    a.rec = s.rec_mode ? s.drec : nullptr;
     a.seq = sig.seq;
     const size_t es = dtype_size(m.xdt);
     const size_t kf = (size_t)m.K * m.F;
@@ -505,6 +512,7 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     if (direct_) stats_.direct_batches++;
     return;
   }
+  s.rec_mode = false;
   pack_rows(s, xs, m);
   const size_t bytes = (size_t)n * m.ldx * dtype_size(m.xdt);
   // rows: zero-copy from the pinned slot (one host-link round trip inside the kernel), or staged
@@ -620,12 +628,26 @@ void Engine::batcher_loop() {
 // Spin on the slot's done word (the kernel publishes s.seq with a system-scope release); back off
 // after ~50 us, check the stream / direct queue for a fault now and then, and give up on the batch
 // (ST_DEVICE_ERROR) after 10x the watchdog.
+namespace {
+// One 16-byte load (atomic on x86-64 with AVX): seq, idx and p of a record from the same store.
+inline __m128i load_record(const ServeRecord* r) {
+  asm volatile("" ::: "memory");  // re-read every poll
+  return _mm_load_si128(reinterpret_cast<const __m128i*>(r));
+}
+}  // namespace
+
 void Engine::wait_done(Slot& s) {
   const int si = (int)(&s - slots_.data());
   volatile uint32_t* dw = done_h_ + (size_t)si * SIGNAL_STRIDE;
   const int64_t t0 = now_ns();
   uint32_t spins = 0;
-  while (__atomic_load_n(dw, __ATOMIC_ACQUIRE) != s.seq) {
+  int next_row = 0;  // record mode: rows [0, next_row) seen complete
+  auto done = [&]() -> bool {
+    if (!s.rec_mode) return __atomic_load_n(dw, __ATOMIC_ACQUIRE) == s.seq;
+    while (next_row < s.n && (uint32_t)_mm_cvtsi128_si32(load_record(s.hrec + next_row)) == s.seq) ++next_row;
+    return next_row == s.n;
+  };
+  while (!done()) {
     ++spins;
     if (spins < 20000) {
       _mm_pause();
@@ -647,6 +669,35 @@ void Engine::wait_done(Slot& s) {
       }
     }
   }
+}
+
+const int32_t* Engine::collect(Slot& s, std::vector<int32_t>& st, std::vector<double>& pd, std::vector<int32_t>& idx) {
+  const size_t n = (size_t)s.n;
+  st.assign(s.pre_status.begin(), s.pre_status.end());
+  pd.resize(n);
+  if (s.failed) {
+    std::fill(st.begin(), st.end(), (int32_t)ST_DEVICE_ERROR);
+    std::fill(pd.begin(), pd.end(), 0.0);
+    idx.assign(n, 0);
+    return idx.data();
+  }
+  if (s.rec_mode) {
+    idx.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      alignas(16) ServeRecord r;
+      _mm_store_si128(reinterpret_cast<__m128i*>(&r), load_record(s.hrec + i));
+      idx[i] = r.idx;
+      pd[i] = r.p;
+    }
+    return idx.data();
+  }
+  if (s.model->pdt == DT_F64) {
+    std::memcpy(pd.data(), s.hp, n * sizeof(double));
+  } else {
+    const float* pf = static_cast<const float*>(s.hp);
+    for (size_t i = 0; i < n; ++i) pd[i] = pf[i];
+  }
+  return s.hidx;
 }
 
 namespace {
@@ -723,19 +774,9 @@ bool Engine::run_idle(const double* X, int n, int nf, const uint64_t* tags, std:
   s.t_launch = now_ns();
   if (s.launched) wait_done(s);
   const int64_t now = now_ns();
-  thread_local std::vector<int32_t> st;
+  thread_local std::vector<int32_t> st, ix;
   thread_local std::vector<double> pd;
-  st.assign(s.pre_status.begin(), s.pre_status.end());
-  pd.resize((size_t)n);
-  if (s.failed) {
-    std::fill(st.begin(), st.end(), (int32_t)ST_DEVICE_ERROR);
-    std::fill(pd.begin(), pd.end(), 0.0);
-  } else if (m->pdt == DT_F64) {
-    std::memcpy(pd.data(), s.hp, (size_t)n * sizeof(double));
-  } else {
-    const float* pf = static_cast<const float*>(s.hp);
-    for (int i = 0; i < n; ++i) pd[i] = pf[i];
-  }
+  const int32_t* idx = collect(s, st, pd, ix);
   {
     std::lock_guard<std::mutex> lk(st_mu_);
     stats_.device_us_sum += (double)(now - s.t_launch) * 1e-3;
@@ -743,7 +784,7 @@ bool Engine::run_idle(const double* X, int n, int nf, const uint64_t* tags, std:
   }
   record_batch((size_t)n);
   for (Meta& mt : s.metas) mt.sink = &sink;
-  deliver(s.metas, s.hidx, pd.data(), st.data(), m, now);
+  deliver(s.metas, idx, pd.data(), st.data(), m, now);
   s.metas.clear();
   s.model.reset();
   m_out = std::move(m);
@@ -758,7 +799,7 @@ bool Engine::run_idle(const double* X, int n, int nf, const uint64_t* tags, std:
 void Engine::completer_loop() {
   pthread_setname_np(pthread_self(), "mlapi-compl");
   (void)hipSetDevice(cfg_.device);
-  std::vector<int32_t> st;
+  std::vector<int32_t> st, ix;
   std::vector<double> pd;
   for (;;) {
     int si;
@@ -780,24 +821,14 @@ void Engine::completer_loop() {
     if (cfg_.delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(cfg_.delay_us));
     const int64_t now = now_ns();
     const size_t n = (size_t)s.n;
-    st.assign(s.pre_status.begin(), s.pre_status.end());
-    pd.resize(n);
-    if (s.failed) {
-      std::fill(st.begin(), st.end(), (int32_t)ST_DEVICE_ERROR);
-      std::fill(pd.begin(), pd.end(), 0.0);
-    } else if (s.model->pdt == DT_F64) {
-      std::memcpy(pd.data(), s.hp, n * sizeof(double));
-    } else {
-      const float* pf = static_cast<const float*>(s.hp);
-      for (size_t i = 0; i < n; ++i) pd[i] = pf[i];
-    }
+    const int32_t* idx = collect(s, st, pd, ix);
     {
       std::lock_guard<std::mutex> lk(st_mu_);
       stats_.device_us_sum += (double)(now - s.t_launch) * 1e-3;
     }
     record_batch(n);
     std::shared_ptr<const Model> m = std::move(s.model);
-    deliver(s.metas, s.hidx, pd.data(), st.data(), m, now);
+    deliver(s.metas, idx, pd.data(), st.data(), m, now);
     s.metas.clear();
     {
       std::lock_guard<std::mutex> lk(s_mu_);

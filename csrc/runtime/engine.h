@@ -105,6 +105,9 @@ struct EngineConfig {
                              // GEMM kernels; f32 -> GEMV (binary) / GENERIC; f64 -> GENERIC
   int max_features = 256; // per-request feature cap (sizes the slot buffers)
   bool inline_args = true;  // SMALL path: batches that fit travel in the kernel-argument block
+  // ... and complete through per-row 16-byte records {seq, idx, p} (one store per row, no fence,
+  // no done word) instead of outputs + a fenced done word
+  bool record_completion = true;
   bool stage_wide = false;  // GEMV / GEMM / GENERIC: H2D-copy the rows first (default: zero-copy reads)
   int watchdog_ms = 2000; // batch not complete after this -> engine marked unhealthy
   int fail_every = 0;     // fault injection: fail every N-th batch with ST_DEVICE_ERROR
@@ -206,6 +209,9 @@ class Engine {
     int32_t* didx = nullptr;
     void* hp = nullptr;
     void* dp = nullptr;
+    ServeRecord* hrec = nullptr;  // host pinned per-row completion records (kernel-argument batches)
+    ServeRecord* drec = nullptr;
+    bool rec_mode = false;    // this launch completes through hrec (no done word)
     uint32_t seq = 0;         // sequence number the launch publishes into the done word
     std::vector<Meta> metas;
     std::vector<int32_t> pre_status;  // per-row status decided before launch
@@ -227,6 +233,8 @@ class Engine {
   void record_batch(size_t n);
   // Wait for a launched slot's done word (spin, then back off; fault and watchdog checks).
   void wait_done(Slot& s);
+  // The launched slot's results -> idx / p (from the records or the output arrays).
+  const int32_t* collect(Slot& s, std::vector<int32_t>& st, std::vector<double>& pd, std::vector<int32_t>& idx);
 
   EngineConfig cfg_;
   std::shared_ptr<const Model> model_;

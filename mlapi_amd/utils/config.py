@@ -42,6 +42,7 @@ class Config:
     io_spin_us: int = 0                       # IO threads busy-poll this long after activity (0 = block)
     max_queue: int = 1 << 20                  # backpressure: queued rows beyond this -> HTTP 503
     inline_args: bool = True                  # GPU: tiny batches travel in the kernel-argument block
+    record_completion: bool = True            # GPU: kernel-argument batches complete through 16-B per-row records
     completers: int = 1                       # GPU: completer threads (done-word wait + delivery)
     idle_inline_rows: int = 8                 # GPU: idle engine -> the IO thread launches <= this many rows itself (0 = off)
     direct_dispatch: bool = True              # GPU: ... written as AQL packets into the engine's own HSA queue

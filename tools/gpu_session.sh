@@ -10,6 +10,7 @@
 #   serve         headline bench (Iris /predict)           serve_wide F=256 /predict, K=1000 and K=2
 #   serve_ab      serve with kernel-argument batches on/off, interleaved x2 (box variance is large)
 #   serve_idle    serve with the idle-engine fast path on (8 rows) / off, interleaved x2
+#   serve_abenv   serve with AB_VAR set to each of AB_VALS, interleaved x2
 #   serve_compl   serve with COMPLS completer threads (default "1 2"), interleaved x2
 #   serve_pin     serve with the rank pinned to physical cores (server / load generator apart) vs unpinned, x2
 #   serve_spin    serve with busy-polling IO threads / spinning batcher+completer (SPINS="0 50"), interleaved x2
@@ -59,6 +60,14 @@ for s in $steps; do
       for r in 1 2; do
         for m in 8 0; do
           MLAPI_IDLE_INLINE_ROWS=$m run "serve_idle${m}_r$r" 300 python -u bench.py --steps 60 --warmup 5
+        done
+      done ;;
+    serve_abenv)  # generic interleaved A/B: AB_VAR=<env var> AB_VALS="<v1> <v2> ..."
+      for r in 1 2; do
+        for v in $AB_VALS; do
+          env "$AB_VAR=$v" timeout -k 10 300 python -u bench.py --steps 60 --warmup 5 > "$O/serve_${AB_VAR}_${v}_r$r.log" 2>&1 \
+            || stop "serve_${AB_VAR}_${v}_r$r" $? "$O/serve_${AB_VAR}_${v}_r$r.log"
+          tail -1 "$O/serve_${AB_VAR}_${v}_r$r.log" | cut -c1-300
         done
       done ;;
     serve_compl)
