@@ -67,6 +67,7 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
     if use_gpu:
         device = torch.device("cuda", local_rank % torch.cuda.device_count())
         torch.cuda.set_device(device)
+    auto = comm == "auto"
     if comm == "auto":
         comm = "native" if device is not None else "torch"
     info = DistInfo(rank, world, local_rank, device, "none")
@@ -81,10 +82,23 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
             dist.init_process_group(backend=backend, **kw)
         info.backend = dist.get_backend()
     if comm == "native":
-        from mlapi_amd.parallel.rccl import NativeComm
+        from mlapi_amd.parallel.rccl import FakeComm, NativeComm
 
-        info.comm = NativeComm(rank, world, device)
-        info.backend = NativeComm.kind
+        try:
+            info.comm = NativeComm(rank, world, device)
+            info.backend = NativeComm.kind
+        except Exception as e:  # noqa: BLE001
+            if not auto or world == 1:
+                raise
+            # auto mode: a rank set whose RCCL communicator cannot initialise (e.g. a node whose
+            # topology RCCL rejects) still runs, with the collectives on the host gloo group; the
+            # backend name says so in every bench line / log.
+            import sys
+
+            print(f"[mlapi] rank {rank}: RCCL communicator init failed ({e}); collectives fall back to gloo",
+                  file=sys.stderr, flush=True)
+            info.comm = FakeComm(rank, world)
+            info.backend = "gloo-fallback"
     elif comm == "p2p":
         from mlapi_amd.parallel.p2p import P2PComm
 
