@@ -827,7 +827,7 @@ __device__ __forceinline__ bf16x8_t frag32(const unsigned char* smem, const Frag
 
 // MFMAs of chunk cn (LDS buffer BUF -> nxt) with the epilogue of chunk c0 (acc -> S) spread over
 // the k-steps
-template <int KS, int RT, bool OVR, int BUF, int BUF_BYTES, bool EPI = true, int AHEAD = 2>
+template <int KS, int RT, bool OVR, int BUF, int BUF_BYTES, bool EPI = true, int AHEAD = 2, bool PRIO = false>
 __device__ __forceinline__ void fused32_step(const unsigned char* smem, const FragOff<KS>& fo,
                                              const bf16x8_t (&xf)[RT][2 * KS], int cn, int c_end, int h,
                                              f32x16_t (&nxt)[RT][2], const f32x16_t (&acc)[RT][2], int c0,
@@ -868,12 +868,16 @@ __device__ __forceinline__ void fused32_step(const unsigned char* smem, const Fr
         wf[(k + AHEAD) % (AHEAD + 1)][ct] = frag32<KS, BUF, BUF_BYTES>(smem, fo, ct, k + AHEAD);
     }
     __builtin_amdgcn_sched_barrier(0);
+    // PRIO (measurement variant): the wave issuing its MFMAs outranks the SIMD's other wave, whose
+    // epilogue VALU then fills the gaps instead of delaying the next MFMA issue
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
         nxt[rt][ct] =
             __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[k % (AHEAD + 1)][ct], xf[rt][k], nxt[rt][ct], 0, 0, 0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     static_for<NSTAGE>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       if constexpr ((j * K2) / NSTAGE == k) {
@@ -906,7 +910,7 @@ __device__ __forceinline__ void epilogue32(const f32x16_t (&acc)[RT][2], int c0,
 // tools/gemm_phase_probe.py; its outputs are meaningless). It splits the class loop's time into the
 // MFMA / LDS feed and the epilogue: 44.4k of 52.2k cycles per wave are the feed
 // (profiles/r2_gemm/phase_probe_noepi.log).
-template <int KS, int WV, int RT, int MODE, bool OVR, bool EPI = true, int AHEAD = 2>
+template <int KS, int WV, int RT, int MODE, bool OVR, bool EPI = true, int AHEAD = 2, bool PRIO = false>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(RT == 2 ? 1 : 2, RT == 2 ? 1 : 2))) void
 gemm_softmax32_kernel(GemmArgs a) {
   static_assert(MODE == 0 || MODE == 2 || MODE == 4, "logits mode runs the 16x16 kernel");
@@ -997,7 +1001,7 @@ gemm_softmax32_kernel(GemmArgs a) {
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 0)
-    fused32_step<KS, RT, OVR, 1, BUF_BYTES, EPI, AHEAD>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0,
+    fused32_step<KS, RT, OVR, 1, BUF_BYTES, EPI, AHEAD, PRIO>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0,
                                                         ts);
     c0 += CLASS_CHUNK;
     if (c0 + CLASS_CHUNK >= c_end) {
@@ -1006,7 +1010,7 @@ gemm_softmax32_kernel(GemmArgs a) {
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 1)
-    fused32_step<KS, RT, OVR, 0, BUF_BYTES, EPI, AHEAD>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0,
+    fused32_step<KS, RT, OVR, 0, BUF_BYTES, EPI, AHEAD, PRIO>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0,
                                                         ts);
     c0 += CLASS_CHUNK;
   }
@@ -1331,7 +1335,7 @@ bool t32_supported(int F) { return F == 64 || F == 128 || F == 256; }
 Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   Plan p;
   if (allow32 && t32_supported(F)) {
-    if (g_force_kernel == 3 || g_force_kernel >= 5) p.k32 = 4;
+    if (g_force_kernel == 3 || g_force_kernel >= 5) p.k32 = 4;  // 5-8: 32x32 measurement variants
     else if (g_force_kernel == 0 && B >= 16384) p.k32 = 4;
   }
   // 32 rows per wave (NT = 2) halve the LDS fragment reads per MFMA. It pays once the register
@@ -1378,6 +1382,11 @@ void launch32(const GemmArgs& args, const dim3& grid, int rt, hipStream_t stream
     if constexpr (MODE == 0 && KS == 8) {
       if (!o && g_force_kernel == 5) {  // measurement: epilogue compiled out
         hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, false>), grid, dim3(256), 0, stream, args);
+        return;
+      }
+      if (!o && g_force_kernel == 8) {  // measurement: s_setprio around each k-step's MFMAs
+        hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, true, 2, true>), grid, dim3(256), 0, stream,
+                           args);
         return;
       }
       if (!o && (g_force_kernel == 6 || g_force_kernel == 7)) {  // measurement: fragment prefetch depth 1 / 3

@@ -27,6 +27,8 @@ for B in tuple(int(a) for a in sys.argv[1:]) or (1, 64, 256, 1024, 2048, 4096, 8
         plans += [(nt, sp, 1) for nt, sp in itertools.product((1, 2), (2, 4, 8, 16, 32))]
     if F in (64, 128, 256):
         plans += [(0, sp, 3) for sp in (0, 2, 4, 8)]
+    if os.environ.get("SWEEP_PLANS"):  # e.g. "0,0,3 0,0,8": (nt, splits, kernel) triples only
+        plans = [tuple(int(v) for v in t.split(",")) for t in os.environ["SWEEP_PLANS"].split()]
     times = {p: [] for p in plans}
     ops_ = {}
     for p in plans:
@@ -80,6 +82,6 @@ for B in tuple(int(a) for a in sys.argv[1:]) or (1, 64, 256, 1024, 2048, 4096, 8
         te = sorted(eager[p])[len(eager[p]) // 2]
         res[f"B{B}_nt{p[0]}_s{p[1]}_k{p[2]}"] = {"graph_us": t, "eager_us": te}
         tf = 2 * B * F * K / t / 1e6
-        name = {0: "auto", 1: "tiles", 2: "rows", 3: "t32"}[p[2]]
+        name = {0: "auto", 1: "tiles", 2: "rows", 3: "t32"}.get(p[2], f"k{p[2]}")
         print(f"B={B:7d} {name:5s} nt={p[0]} splits={p[1]:2d}: {t:9.2f} us graph {te:9.2f} us eager  {tf:7.1f} TF/s", flush=True)
 json.dump(res, open("gpurun_out/gemm_plan_sweep.json", "w"), indent=1)
