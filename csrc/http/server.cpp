@@ -504,12 +504,20 @@ class IoThread : public Sink {
     snprintf(name, sizeof name, "mlapi-io-%d", index_);
     pthread_setname_np(pthread_self(), name);
     epoll_event evs[256];
-    const int64_t spin_ns = (int64_t)srv_->config().io_spin_us * 1000;
+    const int64_t always_spin_ns = (int64_t)srv_->config().io_spin_us * 1000;
+    const int64_t lowload_spin_ns = (int64_t)srv_->config().io_spin_lowload_us * 1000;
+    const int lowload_conns = srv_->config().io_spin_max_conns;
     int64_t last_active = 0;
     while (!stop_.load()) {
       flush_submits();
       flush_log();
       int timeout = 200;
+      // busy-poll window: always (io_spin_us), or at low load only (a batch=1 client)
+      const int64_t spin_ns =
+          always_spin_ns > 0 ? always_spin_ns
+                             : (lowload_spin_ns > 0 && srv_->open_conns.load(std::memory_order_relaxed) <= lowload_conns
+                                    ? lowload_spin_ns
+                                    : 0);
       if (spin_ns > 0) {
         const int64_t now = mono_ns();
         if (now - last_active < spin_ns) {
@@ -519,15 +527,19 @@ class IoThread : public Sink {
           spinning_.store(false);
           if (pending_.load()) timeout = 0;  // a hand-off raced with the transition
         }
+      } else if (spinning_.load(std::memory_order_relaxed)) {
+        spinning_.store(false);  // left the low-load regime: hand-offs need the eventfd again
+        if (pending_.load()) timeout = 0;
       }
       const int n = epoll_wait(epfd_, evs, 256, timeout);
-      if (spin_ns > 0) {
-        if (n > 0) last_active = mono_ns();
-        if (pending_.load()) {
-          pending_.store(false);
-          drain_pending();
-          last_active = mono_ns();
-        }
+      const bool spin_enabled = always_spin_ns > 0 || lowload_spin_ns > 0;
+      if (n > 0 && spin_enabled) last_active = mono_ns();
+      // hand-offs posted while spinning come without an eventfd write (also the ones that raced
+      // with leaving the spin regime); with an eventfd pending too, its later drain finds nothing
+      if (pending_.load()) {
+        pending_.store(false);
+        drain_pending();
+        if (spin_enabled) last_active = mono_ns();
       }
       for (int i = 0; i < n; ++i) {
         const uint64_t id = evs[i].data.u64;
@@ -652,6 +664,7 @@ class IoThread : public Sink {
       epoll_ctl(epfd_, EPOLL_CTL_ADD, fd, &ev);
       conns_.emplace(c->id, std::move(c));
       n_conn.fetch_add(1, std::memory_order_relaxed);
+      srv_->open_conns.fetch_add(1, std::memory_order_relaxed);
     }
   }
 
@@ -659,6 +672,7 @@ class IoThread : public Sink {
     epoll_ctl(epfd_, EPOLL_CTL_DEL, c->fd, nullptr);
     close(c->fd);
     conns_.erase(c->id);  // destroys c
+    srv_->open_conns.fetch_sub(1, std::memory_order_relaxed);
   }
 
   // returns false if the connection was closed

@@ -53,6 +53,12 @@ struct ServerConfig {
   // queue for this long before blocking, and the engine's completer then hands it batches
   // without an eventfd write (no wake-up on the request path). 0 = always block.
   int io_spin_us = 0;
+  // Low-load busy-poll: while the whole server holds at most io_spin_max_conns open connections
+  // (a batch=1 client), an IO thread that just had activity polls for this long before blocking,
+  // so the client's next request does not pay an idle-thread wake-up. Under concurrency (more
+  // connections) the threads block as usual and no CPU is spent spinning. 0 = off.
+  int io_spin_lowload_us = 50;
+  int io_spin_max_conns = 2;
 };
 
 struct SlowRequest {
@@ -85,6 +91,7 @@ class HttpServer {
                bool close);
   ServerStats stats() const;
   const ServerConfig& config() const { return cfg_; }
+  std::atomic<int> open_conns{0};  // keep-alive connections open across all IO threads
   Engine* engine() const { return engine_; }
   // false while health_dispatch has taken this rank out of its SO_REUSEPORT group
   bool accepting() const { return accepting_.load(std::memory_order_relaxed); }
