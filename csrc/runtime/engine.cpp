@@ -722,7 +722,7 @@ bool Engine::run_idle(const double* X, int n, int nf, const uint64_t* tags, std:
   if (inflight_n_.load(std::memory_order_acquire) != 0) return false;
   std::shared_ptr<const Model> m = model();
   // SMALL models only: their batches are kernel-argument packets (~0.03 us to dispatch) with a
-  // ~6 us GPU leg. Wide models are bound by the IO threads' JSON parsing; blocking one on a GEMV /
+  // ~4 us GPU leg. Wide models are bound by the IO threads' JSON parsing; blocking one on a GEMV /
   // GEMM launch + leg cost c=64 throughput (F=256 binary: 265k vs 306-310k req/s).
   if (!m || m->path != PATH_SMALL) return false;
   const int64_t t = now_ns();
