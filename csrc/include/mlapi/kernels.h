@@ -112,9 +112,20 @@ void launch_softmax_rowstats(const void* X_aug, int64_t ldx, const void* W, cons
 bool softmax_grad_dw_supported(int F);
 void softmax_grad_dw_force_plan(int row_groups, int nc, int pipe);  // benchmark hook (0 = automatic)
 size_t softmax_grad_dw_workspace(int64_t B, int K, int F);
+// Optional SGD update fused into the final slab sum (one replica: no all-reduce between them):
+// params [K, cols] -= lr * (dW / N + l2 * params[:, :pen_cols]) with momentum, refreshing the bf16 /
+// f32 shadow copies the forward reads - sgd_update_2d's arithmetic, one launch fewer.
+struct Sgd2D {
+  float* params = nullptr;
+  float* mom = nullptr;
+  uint16_t* shadow_w = nullptr;
+  float* shadow_b = nullptr;
+  int cols = 0, pen_cols = 0;
+  float lr = 0.f, inv_n = 0.f, l2 = 0.f, momentum = 0.f;
+};
 void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
                             int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,
-                            size_t ws_bytes, hipStream_t stream);
+                            size_t ws_bytes, hipStream_t stream, const Sgd2D* update = nullptr);
 
 // ---- train kernels (train.hip) -----------------------------------------------------------------
 // Binary logistic regression, one pass over X: accumulates grad (F w-entries, 1 bias) and stats

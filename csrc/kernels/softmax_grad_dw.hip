@@ -536,7 +536,7 @@ softmax_grad_dw_kernel(GradDwArgs a) {
 // block folds the per-block [loss, correct] pairs with a fixed tree. Deterministic: no atomics.
 __global__ __launch_bounds__(256) void gdw_reduce_kernel(const f32x4_t* __restrict__ slabs, int nslabs, int width4,
                                                          f32x4_t* __restrict__ out, const float* __restrict__ stat_slabs,
-                                                         int nstat, float* __restrict__ stats_out) {
+                                                         int nstat, float* __restrict__ stats_out, Sgd2D upd) {
   if (blockIdx.x == gridDim.x - 1) {
     float l = 0.f, c = 0.f;
     for (int i = threadIdx.x; i < nstat; i += 256) {
@@ -573,6 +573,25 @@ __global__ __launch_bounds__(256) void gdw_reduce_kernel(const f32x4_t* __restri
     s += __builtin_nontemporal_load(slabs + (int64_t)i * width4 + j);
   }
   out[j] = s;
+  if (upd.params != nullptr) {  // uniform: the fused SGD update of these 4 parameters
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t e = 4 * (int64_t)j + q;
+      const int64_t row = e / upd.cols;
+      const int c = (int)(e - row * upd.cols);
+      float d = s[q] * upd.inv_n + (c < upd.pen_cols ? upd.l2 * upd.params[e] : 0.f);
+      if (upd.mom != nullptr) {
+        const float v = upd.momentum * upd.mom[e] + d;
+        upd.mom[e] = v;
+        d = v;
+      }
+      const float np = upd.params[e] - upd.lr * d;
+      upd.params[e] = np;
+      if (upd.shadow_w != nullptr && c < upd.pen_cols)
+        upd.shadow_w[row * upd.pen_cols + c] = __builtin_bit_cast(uint16_t, (__bf16)np);
+      if (upd.shadow_b != nullptr && c == upd.pen_cols) upd.shadow_b[row] = np;
+    }
+  }
 }
 
 struct GdwLayout {
@@ -627,8 +646,10 @@ size_t softmax_grad_dw_workspace(int64_t B, int K, int F) {  // enough for eithe
 
 void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
                             int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,
-                            size_t ws_bytes, hipStream_t stream) {
+                            size_t ws_bytes, hipStream_t stream, const Sgd2D* update) {
   if (B <= 0) return;
+  if (update != nullptr && (update->params == nullptr || update->cols != F + 8 || update->pen_cols > F))
+    throw std::invalid_argument("softmax_grad_dw: fused update needs params [K, F + 8]");
   if (!softmax_grad_dw_supported(F))
     throw std::invalid_argument("softmax_grad_dw: F must be 128, 256 or 512 (pad narrower features)");
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
@@ -694,11 +715,15 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
     const int width4 = K * (F + 8) / 4;
     hipLaunchKernelGGL(gdw_reduce_kernel, dim3((unsigned)((width4 + 255) / 256 + 1)), dim3(256), 0, stream,
                        reinterpret_cast<const f32x4_t*>(args.dw_slabs), L.row_groups, width4,
-                       reinterpret_cast<f32x4_t*>(dW_out), args.stat_slabs, L.row_groups * L.class_groups, stats_out);
+                       reinterpret_cast<f32x4_t*>(dW_out), args.stat_slabs, L.row_groups * L.class_groups, stats_out,
+                       update != nullptr ? *update : Sgd2D{});
     MLAPI_HIP_CHECK(hipGetLastError());
   } else {
     launch_reduce_slabs_f32(args.dw_slabs, L.row_groups, K * (F + 8), dW_out, stream);
     launch_reduce_slabs_f32(args.stat_slabs, L.row_groups * L.class_groups, 2, stats_out, stream);
+    if (update != nullptr)
+      launch_sgd_update_2d(update->params, dW_out, update->mom, K, update->cols, update->pen_cols, update->lr,
+                           update->inv_n, update->l2, update->momentum, update->shadow_w, update->shadow_b, stream);
   }
 }
 

@@ -240,7 +240,7 @@ class SoftmaxTrainBuffers:
 
 def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y: torch.Tensor, kind: int,
                        bufs: SoftmaxTrainBuffers = None, dW_out: torch.Tensor = None,
-                       stats_out: torch.Tensor = None):
+                       stats_out: torch.Tensor = None, update: dict = None):
     """Sums over the batch of the multiclass objective's gradient, intercept included.
 
     X_aug: [B, Fk + 8] bf16 from :func:`augment_features`; W: [K, Fk] bf16 (Fk in 128/256/512;
@@ -249,6 +249,10 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
     vendor GEMM: a row-stats pass (logsumexp / argmax per row, gemm_softmax.hip MODE 2), then
     softmax_grad_dw.hip, which forms G = P - Y in registers and accumulates dW_aug = G^T X_aug from
     the same LDS tile (G never reaches HBM), followed by its deterministic slab sums.
+
+    ``update`` (one replica only): the SGD step :func:`sgd_update_2d` would apply next, fused into
+    the final slab sum - keys params [K, Fk + 8] f32, lr, inv_n, l2, and optionally momentum,
+    mom_buf, shadow_w, shadow_b.
     """
     _check(X_aug, W, b, y)
     if X_aug.dtype != torch.bfloat16 or W.dtype != torch.bfloat16 or b.dtype != torch.float32 \
@@ -265,8 +269,18 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
         dW_out = torch.empty(K, F_aug, dtype=torch.float32, device=X_aug.device)
     if not dW_out.is_contiguous() or dW_out.shape != (K, F_aug) or dW_out.dtype != torch.float32:
         raise ValueError("softmax_train_grad: dW_out must be a contiguous f32 [K, Fk + 8] tensor")
+    upd = {}
+    if update is not None:
+        p = update["params"]
+        if not p.is_contiguous() or p.shape != (K, F_aug) or p.dtype != torch.float32:
+            raise ValueError("softmax_train_grad: update params must be a contiguous f32 [K, Fk + 8] tensor")
+        ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+        upd = dict(params=p.data_ptr(), mom=ptr(update.get("mom_buf")), shadow_w=ptr(update.get("shadow_w")),
+                   shadow_b=ptr(update.get("shadow_b")), pen_cols=F, lr=float(update["lr"]),
+                   inv_n=float(update["inv_n"]), l2=float(update.get("l2", 0.0)),
+                   momentum=float(update.get("momentum", 0.0)))
     C().softmax_grad_dw(X_aug.data_ptr(), F_aug, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
-                        dW_out.data_ptr(), stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(), _stream())
+                        dW_out.data_ptr(), stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(), _stream(), **upd)
     return dW_out, stats
 
 

@@ -12,7 +12,8 @@ This module is the scale-out counterpart (BASELINE config 5 with K classes): per
      weights get zero gradients and stay 0), so no width needs a vendor GEMM;
   2. one RCCL all-reduce of the fused buffer [dW_aug | loss_sum | n_correct] (C2 + C3);
   3. ``sgd_update_2d``: W_aug = [W | b] -= lr * (g / N_global + l2 * W) with the intercept
-     unpenalized, writing the bf16 W and f32 b the next forward reads in the same pass.
+     unpenalized, writing the bf16 W and f32 b the next forward reads in the same pass. With one
+     replica (no all-reduce in between) the same arithmetic runs inside step 1's final slab sum.
 
 fp32 master weights; every rank applies the identical update, so replicas stay bitwise equal.
 One replica (world == 1) can capture the whole step in a HIP graph (:meth:`capture`).
@@ -106,15 +107,21 @@ class SoftmaxSGDTrainer:
             self.shadow_b.copy_(self.params[:, self.Fk])
 
     # ---------------------------------------------------------------------------------- step
-    def _local_grad(self, Xa: torch.Tensor, y: torch.Tensor) -> None:
+    def _local_grad(self, Xa: torch.Tensor, y: torch.Tensor, fused_update_n: int = 0) -> None:
+        """Gradient sums into self.grad; with ``fused_update_n`` (one replica) the SGD update for
+        that global batch size runs inside the gradient's final slab sum (one launch fewer)."""
         if self.on_gpu:
             from mlapi_amd.ops.linear import SoftmaxTrainBuffers, softmax_train_grad
 
             B = Xa.shape[0]
             if B not in self._bufs:
                 self._bufs[B] = SoftmaxTrainBuffers(B, self.K, self.Fk, Xa.device)
+            upd = None
+            if fused_update_n:
+                upd = dict(params=self.params, lr=self.lr, inv_n=1.0 / fused_update_n, l2=self.l2,
+                           momentum=self.momentum, mom_buf=self.mom, shadow_w=self.shadow_w, shadow_b=self.shadow_b)
             softmax_train_grad(Xa, self.shadow_w, self.shadow_b, y, self.kind, bufs=self._bufs[B], dW_out=self._dW(),
-                               stats_out=self.grad[self.K * self.F_aug:])
+                               stats_out=self.grad[self.K * self.F_aug:], update=upd)
         else:
             from mlapi_amd.ops.reference import softmax_train_ref
 
@@ -141,6 +148,8 @@ class SoftmaxSGDTrainer:
         """One SGD step on this rank's shard (Xa from :meth:`prepare`, y int32 class indices)."""
         if self._graph is not None and self._graph[1] is Xa and self._graph[2] is y:
             self._graph[0].replay()
+        elif self.on_gpu and self.info.world == 1:
+            self._local_grad(Xa, y, fused_update_n=Xa.shape[0])
         else:
             self._local_grad(Xa, y)
             all_reduce_sum_(self.grad, self.info)
@@ -160,13 +169,11 @@ class SoftmaxSGDTrainer:
         saved = (self.params.clone(), None if self.mom is None else self.mom.clone())
         with torch.cuda.stream(s):  # warm-up: allocates the buffers
             for _ in range(2):
-                self._local_grad(Xa, y)
-                self._update(Xa.shape[0])
+                self._local_grad(Xa, y, fused_update_n=Xa.shape[0])
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._local_grad(Xa, y)
-            self._update(Xa.shape[0])
+            self._local_grad(Xa, y, fused_update_n=Xa.shape[0])
         self.params.copy_(saved[0])
         self._refresh_shadow()
         if self.mom is not None:

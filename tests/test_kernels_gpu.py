@@ -321,6 +321,27 @@ def test_sgd_update_2d():
     assert torch.equal(shadow_b, p[:, F])
 
 
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+def test_softmax_fused_update_equals_separate_update(momentum):
+    """The SGD update fused into the gradient's final slab sum (one replica) is bit-identical to
+    softmax_train_grad followed by sgd_update_2d, including the bf16 / f32 shadow copies."""
+    from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer, synthetic_multiclass
+
+    X, y = synthetic_multiclass(4096, 256, 300, seed=4, noise=0.3, device=DEV)
+    a = SoftmaxSGDTrainer(256, 300, lr=0.3, l2=1e-3, momentum=momentum, device=torch.device(DEV))
+    b = SoftmaxSGDTrainer(256, 300, lr=0.3, l2=1e-3, momentum=momentum, device=torch.device(DEV))
+    Xa = a.prepare(X)
+    for _ in range(4):
+        a.step(Xa, y)  # fused
+        b._local_grad(Xa, y)
+        b._update(Xa.shape[0])
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params) and torch.equal(a.shadow_w, b.shadow_w) and torch.equal(a.shadow_b, b.shadow_b)
+    assert torch.equal(a.grad, b.grad)
+    if momentum:
+        assert torch.equal(a.mom, b.mom)
+
+
 def test_softmax_sgd_gpu_trains_and_graph_replay_is_exact():
     from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer, synthetic_multiclass
 
