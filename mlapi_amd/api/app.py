@@ -132,6 +132,11 @@ def create_app(config: Optional[Config] = None, *, runtime=None) -> FastAPI:
             app.state.runtime = ServingRuntime(config)
         return app.state.runtime
 
+    if config.asgi_fast_path and names:
+        from mlapi_amd.api.fastpath import PredictFastPath
+
+        app.add_middleware(PredictFastPath, names=names, runtime=rt)
+
     from mlapi_amd.serve.runtime import EngineBusy
 
     @app.exception_handler(EngineBusy)

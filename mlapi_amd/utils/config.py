@@ -59,6 +59,7 @@ class Config:
     io_threads: int = 2
     reuseport: bool = True
     fast_path: bool = True
+    asgi_fast_path: bool = True               # uvicorn main:app: POST /predict answered by an ASGI middleware
     server_header: str = "uvicorn"
     slow_workers: int = 1
     log_level: str = "warning"

@@ -208,3 +208,30 @@ def test_operational_endpoints(iris_cwd):
     m = c.get("/metrics").text
     assert "mlapi_requests_total" in m and "mlapi_batch_size_bucket" in m
     assert c.post("/admin/reload").json()["reloaded"] is True
+
+
+def test_asgi_fast_path_is_byte_identical_to_the_route(iris_cwd):
+    """`uvicorn main:app`'s POST /predict middleware (api/fastpath.py) answers with exactly the
+    bytes and headers the FastAPI route sends, and hands every unusual body to the route."""
+    import numpy as np
+
+    from mlapi_amd.api.fastpath import PredictFastPath
+
+    fast, route = _client(), _client(asgi_fast_path=False)
+    served0 = PredictFastPath.served
+    rng = np.random.default_rng(9)
+    bodies = [json.dumps(dict(zip(A1, map(float, np.round(r, 2))))) for r in
+              rng.normal([5.8, 3.0, 3.8, 1.2], [0.8, 0.4, 1.8, 0.8], (40, 4))]
+    bodies += ['{"sepal_length":5,"sepal_width":3,"petal_length":1,"petal_width":0,"extra":[1,{"a":null}]}',
+               '{"sepal_length":"5.1","sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',  # string: route
+               '{"sepal_length":5.1,"sepal_width":3.5,"petal_length":1.4}',                       # missing: 422
+               '{"sepal_length":NaN,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',     # NaN: route
+               '{"sepal_length":1e400,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',   # inf: route
+               '[1,2,3]', '', '{"sepal_length":5.1']
+    for b in bodies:
+        for ctype in ("application/json", "application/vnd.api+json; charset=utf-8", "text/plain"):
+            r1 = fast.post("/predict", content=b.encode(), headers={"content-type": ctype})
+            r2 = route.post("/predict", content=b.encode(), headers={"content-type": ctype})
+            assert (r1.status_code, r1.content, r1.headers.get("content-type"), r1.headers.get("content-length")) == \
+                (r2.status_code, r2.content, r2.headers.get("content-type"), r2.headers.get("content-length")), b
+    assert PredictFastPath.served - served0 == 2 * 41  # 40 random + the extra-member body, two JSON types
