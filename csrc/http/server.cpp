@@ -468,7 +468,9 @@ class IoThread : public Sink {
       // (no batcher / completer hand-off, no eventfd round trip)
       idle_done_.clear();
       std::shared_ptr<const Model> m;
-      if (srv_->engine()->run_idle(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), idle_done_, m)) {
+      // wide models too while the server is at low load (a batch=1 client)
+      const bool low = srv_->open_conns.load(std::memory_order_relaxed) <= srv_->config().io_spin_max_conns;
+      if (srv_->engine()->run_idle(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), idle_done_, m, low)) {
         pend_x_.clear();
         pend_tags_.clear();
         FastBatch fb{std::move(m), std::move(idle_done_)};

@@ -715,7 +715,7 @@ struct CollectSink : Sink {
 // thread launches and waits itself. The check is a heuristic (a request submitted by another
 // thread right after it simply takes the queued path and runs concurrently in another slot).
 bool Engine::run_idle(const double* X, int n, int nf, const uint64_t* tags, std::vector<Completion>& out,
-                      std::shared_ptr<const Model>& m_out) {
+                      std::shared_ptr<const Model>& m_out, bool allow_wide) {
   if (cfg_.idle_inline_rows <= 0 || n <= 0 || n > cfg_.idle_inline_rows) return false;
   if (nf < 0 || nf > cfg_.max_features) return false;
   if (drop_.load(std::memory_order_relaxed) || cfg_.fail_every > 0 || cfg_.delay_us > 0) return false;
@@ -723,8 +723,9 @@ bool Engine::run_idle(const double* X, int n, int nf, const uint64_t* tags, std:
   std::shared_ptr<const Model> m = model();
   // SMALL models only: their batches are kernel-argument packets (~0.03 us to dispatch) with a
   // ~4 us GPU leg. Wide models are bound by the IO threads' JSON parsing; blocking one on a GEMV /
-  // GEMM launch + leg cost c=64 throughput (F=256 binary: 265k vs 306-310k req/s).
-  if (!m || m->path != PATH_SMALL) return false;
+  // GEMM launch + leg cost c=64 throughput (F=256 binary: 265k vs 306-310k req/s) - unless the
+  // caller vouches for low load (allow_wide).
+  if (!m || (m->path != PATH_SMALL && !allow_wide)) return false;
   const int64_t t = now_ns();
   {
     std::lock_guard<std::mutex> lk(q_mu_);

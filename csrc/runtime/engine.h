@@ -175,8 +175,10 @@ class Engine {
   // cfg.idle_inline_rows), launch the rows from the calling thread, wait for their done word and
   // append their completions to `out` (model in `m_out`); true = done, the caller must not submit
   // them. false = not eligible (busy, CPU backend, fault injection on, no model): submit normally.
+  // allow_wide: also for GEMV / GEMM / GENERIC models (the caller knows the load is low, e.g. one
+  // open connection; under concurrency their IO threads are better spent parsing).
   bool run_idle(const double* X, int n, int nf, const uint64_t* tags, std::vector<Completion>& out,
-                std::shared_ptr<const Model>& m_out);
+                std::shared_ptr<const Model>& m_out, bool allow_wide = false);
   // Blocking convenience API (tests / bulk scoring through the batcher).
   void predict(const double* X, int64_t B, int F, int32_t* idx, double* p, int32_t* status);
 
