@@ -17,6 +17,9 @@ import json
 from typing import Callable, List
 
 
+MAX_FAST_BODY = 1 << 20  # bytes buffered here before the request is handed to the route as is
+
+
 def _json_ctype(ct: str) -> bool:
     """FastAPI's rule (routing.py): maintype 'application', subtype 'json' or '*+json'."""
     v = ct.split(";", 1)[0].strip().lower()
@@ -50,17 +53,22 @@ class PredictFastPath:
         if not _json_ctype(ctype):
             return await self.app(scope, receive, send)
         messages = []
-        body = b""
+        size = 0
+        complete = False
         while True:
             msg = await receive()
             messages.append(msg)
             if msg["type"] != "http.request":
                 break  # client went away: let the app see the same messages
-            body += msg.get("body", b"")
+            size += len(msg.get("body", b""))
             if not msg.get("more_body", False):
+                complete = True
                 break
+            if size > MAX_FAST_BODY:
+                break  # not a plausible feature record: the route reads (and judges) the rest
         result = None
-        if messages[-1]["type"] == "http.request":
+        if complete:
+            body = b"".join(m.get("body", b"") for m in messages)
             x = self._parse(body, self.names) if body else None
             if x is not None:
                 result = await self._predict(x)
