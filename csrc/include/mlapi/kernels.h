@@ -53,6 +53,30 @@ struct alignas(16) ServeRecord {
   int32_t idx;
   double p;
 };
+// Completion-record output of a serving launch: when `rec` is set, each row's (idx, p) and `seq`
+// leave the kernel in one 16-byte system-scope store into rec[row] instead of out_idx / out_p.
+struct RecOut {
+  ServeRecord* rec = nullptr;
+  uint32_t seq = 0;
+};
+#if defined(__HIP__)  // HIP sources (both compilation passes); plain C++ includers skip it
+__device__ __forceinline__ void put_record(ServeRecord* dst, uint32_t seq, int32_t idx, double p) {
+  const uint64_t pb = __builtin_bit_cast(uint64_t, p);
+  typedef __attribute__((ext_vector_type(4))) uint32_t rec_u32x4_t;
+  const rec_u32x4_t v = {seq, (uint32_t)idx, (uint32_t)pb, (uint32_t)(pb >> 32)};
+  // write-through vector store (sc0 sc1): visible to the host without a fence or a flush
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
+}
+__device__ __forceinline__ void put_result(int32_t* out_idx, float* out_p, const RecOut& ro, int64_t row,
+                                           int32_t idx, float p) {
+  if (ro.rec != nullptr) {
+    put_record(ro.rec + row, ro.seq, idx, (double)p);
+  } else {
+    out_idx[row] = idx;
+    out_p[row] = p;
+  }
+}
+#endif
 // true if n rows of F features (and the K x F model) fit the argument block in dtype `dt`
 bool linear_inline_fits(int dt, int64_t n, int F, int K);
 void launch_linear_inline(int dt, const InlineBatch& a, hipStream_t stream);
@@ -61,7 +85,7 @@ void launch_linear_inline(int dt, const InlineBatch& a, hipStream_t stream);
 // X: [B, F] bf16 or f32 row-major; w: [F] same dtype; bias: scalar f32.
 // out_idx: int32[B] (z > 0), out_p: f32[B] = sigmoid(|z|) (kind BINARY) or sigmoid(2|z|).
 void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_t B, int F, int kind,
-                        int32_t* out_idx, float* out_p, hipStream_t stream);
+                        int32_t* out_idx, float* out_p, hipStream_t stream, RecOut ro = RecOut{});
 
 // ---- gemm_softmax.hip: multiclass predict, bf16 MFMA GEMM + online softmax/argmax epilogue ----
 // X: [B, F] bf16; W: [K, F] bf16; b: [K] f32. F in {32, 64, 128, 256} or a multiple of 256 (any
@@ -75,7 +99,8 @@ void gemm_softmax_force_plan(int nt, int splits, int kernel = 0);
 // (tools/gemm_phase_probe.py); nullptr = off (default).
 void gemm_softmax_set_stamps(void* stamps);
 void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind,
-                         int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream);
+                         int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream,
+                         RecOut ro = RecOut{});
 // Full logits (for tests / decision_function): Z[B, K] f32.
 void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B, int F, int K, float* Z,
                         hipStream_t stream);

@@ -112,6 +112,7 @@ struct GemmArgs {
   int classes_per_split;
   int32_t* out_idx;        // MODE 0
   float* out_p;            // MODE 0
+  RecOut ro;               // MODE 0 serving: per-row completion records instead of out_idx / out_p
   unsigned int* counters;  // split merge (MODE 0/2)
   float4* partials;        // split merge (MODE 0/2)
   float* Z;                // MODE 1
@@ -612,8 +613,7 @@ gemm_softmax_kernel(GemmArgs a) {
         const int64_t row = row0 + t * 16 + col;
         if (q == 0 && row < B) {
           if constexpr (MODE == 0) {
-            a.out_idx[row] = st[t].bi;
-            a.out_p[row] = ovr ? sigmoidf_(st[t].m) / st[t].s : 1.f / st[t].s;
+            put_result(a.out_idx, a.out_p, a.ro, row, st[t].bi, ovr ? sigmoidf_(st[t].m) / st[t].s : 1.f / st[t].s);
           } else if constexpr (MODE == 4) {
             a.rowstate[row] = make_float4(st[t].m, st[t].s, __int_as_float(st[t].bi), 0.f);
           } else {
@@ -677,8 +677,7 @@ gemm_softmax_kernel(GemmArgs a) {
           S = merge_state(S, RowState{q.x, q.y, __float_as_int(q.z)}, ovr);
         }
         if constexpr (MODE == 0) {
-          a.out_idx[row] = S.bi;
-          a.out_p[row] = ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s;
+          put_result(a.out_idx, a.out_p, a.ro, row, S.bi, ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s);
         } else if constexpr (MODE == 4) {
           a.rowstate[row] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
         } else {
@@ -1032,8 +1031,7 @@ gemm_softmax32_kernel(GemmArgs a) {
       const int64_t row = row0 + rt * 32 + col;
       if (h == 0 && row < B) {
         if constexpr (MODE == 0) {
-          a.out_idx[row] = S[rt].bi;
-          a.out_p[row] = ovr ? sigmoidf_(S[rt].m) / S[rt].s : 1.f / S[rt].s;
+          put_result(a.out_idx, a.out_p, a.ro, row, S[rt].bi, ovr ? sigmoidf_(S[rt].m) / S[rt].s : 1.f / S[rt].s);
         } else if constexpr (MODE == 4) {
           a.rowstate[row] = make_float4(S[rt].m, S[rt].s, __int_as_float(S[rt].bi), 0.f);
         } else {
@@ -1088,8 +1086,7 @@ gemm_softmax32_kernel(GemmArgs a) {
         R = merge_state(R, RowState{pq.x, pq.y, __float_as_int(pq.z)}, ovr);
       }
       if constexpr (MODE == 0) {
-        a.out_idx[mrow] = R.bi;
-        a.out_p[mrow] = ovr ? sigmoidf_(R.m) / R.s : 1.f / R.s;
+        put_result(a.out_idx, a.out_p, a.ro, mrow, R.bi, ovr ? sigmoidf_(R.m) / R.s : 1.f / R.s);
       } else if constexpr (MODE == 4) {
         a.rowstate[mrow] = make_float4(R.m, R.s, __int_as_float(R.bi), 0.f);
       } else {
@@ -1121,6 +1118,7 @@ struct RowsArgs {
   int F;
   int32_t* out_idx;
   float* out_p;
+  RecOut ro;  // serving: per-row completion records (MODE 0)
   float* Z;
   float2* rowstat;
   float4* rowstate;
@@ -1233,8 +1231,7 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
       const int64_t row = row0 + r;
       if (row < B) {
         if constexpr (MODE == 0) {
-          a.out_idx[row] = S.bi;
-          a.out_p[row] = OVR ? sigmoidf_(S.m) / S.s : 1.f / S.s;
+          put_result(a.out_idx, a.out_p, a.ro, row, S.bi, OVR ? sigmoidf_(S.m) / S.s : 1.f / S.s);
         } else if constexpr (MODE == 4) {
           a.rowstate[row] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
         } else {
@@ -1500,7 +1497,8 @@ size_t gemm_softmax_workspace(int64_t B, int K, int F) {
 }
 
 void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind,
-                         int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream) {
+                         int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream,
+                         RecOut ro) {
   if (B <= 0) return;
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("gemm_softmax: multiclass kinds only (binary models use gemv_binary)");
@@ -1508,6 +1506,7 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
     RowsArgs ra = rows_args(X, F, W, b, B, F, K);
     ra.out_idx = out_idx;
     ra.out_p = out_p;
+    ra.ro = ro;
     launch_rows<0>(ra, kind, stream);
     return;
   }
@@ -1518,6 +1517,7 @@ void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B
   args.bias = b;
   args.out_idx = out_idx;
   args.out_p = out_p;
+  args.ro = ro;
   if (plan.splits > 1) {
     args.counters = static_cast<unsigned int*>(workspace);
     args.partials = reinterpret_cast<float4*>(static_cast<unsigned char*>(workspace) + COUNTER_BYTES);

@@ -57,7 +57,7 @@ struct Chunk<float> {
 template <typename T, int LPR, int CPL, int U>
 __global__ __launch_bounds__(256) void gemv_binary_kernel(const T* __restrict__ X, const T* __restrict__ w, float bias,
                                                           int64_t B, int F, int kind, int32_t* __restrict__ out_idx,
-                                                          float* __restrict__ out_p) {
+                                                          float* __restrict__ out_p, RecOut ro) {
   constexpr int RPW = 64 / LPR;  // rows per wave-instruction
   constexpr int NE = Chunk<T>::N;
   const int lane = threadIdx.x & 63;
@@ -118,14 +118,14 @@ __global__ __launch_bounds__(256) void gemv_binary_kernel(const T* __restrict__ 
     if (writer && row < B) {
       const float z = z0 + bias;
       const float a = scale * fabsf(z);
-      out_idx[row] = z > 0.f;
-      out_p[row] = 1.f / (1.f + __expf(-a));
+      put_result(out_idx, out_p, ro, row, z > 0.f, 1.f / (1.f + __expf(-a)));
     }
   }
 }
 
 template <typename T, int LPR, int CPL, int U>
 void launch(const void* X, const void* w, float bias, int64_t B, int F, int kind, int32_t* out_idx, float* out_p,
+            const RecOut& ro,
             hipStream_t stream) {
   constexpr int rows_per_block_iter = 4 * U * (64 / LPR);
   int64_t blocks = (B + rows_per_block_iter - 1) / rows_per_block_iter;
@@ -133,32 +133,33 @@ void launch(const void* X, const void* w, float bias, int64_t B, int F, int kind
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL((gemv_binary_kernel<T, LPR, CPL, U>), dim3((unsigned)blocks), dim3(256), 0, stream,
-                     static_cast<const T*>(X), static_cast<const T*>(w), bias, B, F, kind, out_idx, out_p);
+                     static_cast<const T*>(X), static_cast<const T*>(w), bias, B, F, kind, out_idx, out_p, ro);
   MLAPI_HIP_CHECK(hipGetLastError());
 }
 
 template <typename T>
 void dispatch(const void* X, const void* w, float bias, int64_t B, int F, int kind, int32_t* out_idx, float* out_p,
+              const RecOut& ro,
               hipStream_t stream) {
   constexpr int NE = Chunk<T>::N;
   if (F % NE != 0) throw std::invalid_argument("gemv_binary: F must be a multiple of 16 bytes of elements");
   const int chunks = F / NE;
   if (chunks <= 4)
-    launch<T, 4, 1, 4>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+    launch<T, 4, 1, 4>(X, w, bias, B, F, kind, out_idx, out_p, ro, stream);
   else if (chunks <= 8)
-    launch<T, 8, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+    launch<T, 8, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, ro, stream);
   else if (chunks <= 16)
-    launch<T, 16, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+    launch<T, 16, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, ro, stream);
   else if (chunks <= 32)
-    launch<T, 32, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+    launch<T, 32, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, ro, stream);
   else if (chunks <= 64)
-    launch<T, 64, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+    launch<T, 64, 1, 8>(X, w, bias, B, F, kind, out_idx, out_p, ro, stream);
   else if (chunks <= 128)
-    launch<T, 64, 2, 4>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+    launch<T, 64, 2, 4>(X, w, bias, B, F, kind, out_idx, out_p, ro, stream);
   else if (chunks <= 256)
-    launch<T, 64, 4, 2>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+    launch<T, 64, 4, 2>(X, w, bias, B, F, kind, out_idx, out_p, ro, stream);
   else if (chunks <= 512)
-    launch<T, 64, 8, 1>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+    launch<T, 64, 8, 1>(X, w, bias, B, F, kind, out_idx, out_p, ro, stream);
   else
     throw std::invalid_argument("gemv_binary: F too large (max 4096 bf16 / 2048 f32)");
 }
@@ -166,14 +167,14 @@ void dispatch(const void* X, const void* w, float bias, int64_t B, int F, int ki
 }  // namespace
 
 void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_t B, int F, int kind,
-                        int32_t* out_idx, float* out_p, hipStream_t stream) {
+                        int32_t* out_idx, float* out_p, hipStream_t stream, RecOut ro) {
   if (B <= 0) return;
   if (reinterpret_cast<uintptr_t>(X) % 16 || reinterpret_cast<uintptr_t>(w) % 16)
     throw std::invalid_argument("gemv_binary: X and w must be 16-byte aligned");
   if (dt == DT_BF16)
-    dispatch<uint16_t>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+    dispatch<uint16_t>(X, w, bias, B, F, kind, out_idx, out_p, ro, stream);
   else if (dt == DT_F32)
-    dispatch<float>(X, w, bias, B, F, kind, out_idx, out_p, stream);
+    dispatch<float>(X, w, bias, B, F, kind, out_idx, out_p, ro, stream);
   else
     throw std::invalid_argument("gemv_binary: dtype must be bf16 or f32");
 }

@@ -525,12 +525,22 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
   if (m.path == PATH_SMALL || m.path == PATH_GENERIC) {
     launch_linear_small(m.xdt, X, m.ldx, m.dW, m.db, n, m.F, m.K, m.kind, s.didx, s.dp, stream_, sig);
   } else {
+    // GEMM: completion records written by the kernel's result stores (no trailing one-wave
+    // serve_signal launch: 3.9 us of GPU time and a hipLaunchKernel per batch). GEMV keeps the
+    // signal kernel: with records its batch-1 leg measured 6.3-6.9 us vs 5.6-6.0
+    // (profiles/r2_records/wide_ab/); the GEMM's was unchanged (10.2-10.6 vs 10.2-10.5).
+    RecOut ro;
+    if (cfg_.record_completion && m.path == PATH_GEMM) {
+      ro.rec = s.drec;
+      ro.seq = sig.seq;
+      s.rec_mode = true;
+    }
     if (m.path == PATH_GEMV)
-      launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_);
+      launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_, ro);
     else
       launch_gemm_softmax(X, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
-                          static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_);
-    launch_serve_signal(sig, stream_);
+                          static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_, ro);
+    if (!s.rec_mode) launch_serve_signal(sig, stream_);
   }
   std::lock_guard<std::mutex> lk(st_mu_);
   stats_.path_batches[m.path]++;

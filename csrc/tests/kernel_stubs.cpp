@@ -16,12 +16,12 @@ void launch_linear_small(int, const void*, int64_t, const void*, const void*, in
 void launch_serve_signal(const ServeSignal&, hipStream_t) { unreachable("launch_serve_signal"); }
 bool linear_inline_fits(int, int64_t, int, int) { return false; }
 void launch_linear_inline(int, const InlineBatch&, hipStream_t) { unreachable("launch_linear_inline"); }
-void launch_gemv_binary(int, const void*, const void*, float, int64_t, int, int, int32_t*, float*, hipStream_t) {
+void launch_gemv_binary(int, const void*, const void*, float, int64_t, int, int, int32_t*, float*, hipStream_t, RecOut) {
   unreachable("launch_gemv_binary");
 }
 size_t gemm_softmax_workspace(int64_t, int, int) { return 0; }
 void launch_gemm_softmax(const void*, const void*, const float*, int64_t, int, int, int, int32_t*, float*, void*, size_t,
-                         hipStream_t) {
+                         hipStream_t, RecOut) {
   unreachable("launch_gemm_softmax");
 }
 std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int, const std::string&, std::string* why) {
