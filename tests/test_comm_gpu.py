@@ -80,18 +80,20 @@ def test_p2p_allreduce_multiprocess(tmp_path, world):
     print({"world": world, "us_per_call_256k": [round(x["us_per_call_256k"], 1) for x in res]})
 
 
-def _torchrun(world, script, out_dir):
+def _torchrun(world, script, out_dir, args=(), env=None):
     import socket
 
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    path = script if script.endswith("bench.py") else str(ROOT / "tests" / "dist" / script)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", str(ROOT / "tests" / "dist" / script)]
-    out = subprocess.run(cmd, env={**ENV, "OUT": str(out_dir), "OMP_NUM_THREADS": "1"}, capture_output=True,
-                         text=True, timeout=240, cwd=ROOT)
+           "--master-addr=127.0.0.1", f"--master-port={port}", path, *args]
+    out = subprocess.run(cmd, env={**ENV, "OUT": str(out_dir), "OMP_NUM_THREADS": "1", **(env or {})},
+                         capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
+    return out.stdout
 
 
 def test_dp_sgd_on_gpu_with_p2p_allreduce(tmp_path):
@@ -109,3 +111,18 @@ def test_dp_sgd_on_gpu_with_p2p_allreduce(tmp_path):
     j0, j1 = (json.loads((tmp_path / f"bcast_2_{r}.json").read_text()) for r in range(2))
     assert j0["W"] == j1["W"] and j0["classes"] == list("abcde")
     assert j0["p2p_calls"] >= 35 and j0["acc"] > 0.8
+
+
+@pytest.mark.parametrize("mode", ["serve", "serve_wide"])
+def test_dp_serving_bench_two_gpu_ranks(tmp_path, mode):
+    """The driver's multi-GPU launch shape (torchrun, one rank per device) on the 1-GPU box: two
+    ranks share the GPU (MLAPI_COMM=p2p: RCCL refuses two ranks on one device), each with its own
+    engine and out-of-process load generator behind ONE SO_REUSEPORT port; every response body
+    is validated and both ranks serve."""
+    out = _torchrun(2, str(ROOT / "bench.py"), tmp_path,
+                    args=["--gpus", "2", "--mode", mode, "--steps", "3", "--warmup", "1", "--reqs-per-conn", "64",
+                          "--c1-requests", "200"], env={"MLAPI_COMM": "p2p"})
+    line = json.loads(out.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["comm_backend"] == "p2p+gloo" and line["body_mismatches"] == 0
+    assert line["config"]["parallelism"] == "dp2" and line["value"] > 0
+    assert len(line["served_per_rank"]) == 2 and min(line["served_per_rank"]) > 0, line["served_per_rank"]
