@@ -28,7 +28,7 @@ namespace mlapi {
 // ------------------------------------------------------------------------------------------------
 // helpers
 // ------------------------------------------------------------------------------------------------
-std::string http_date_now() {
+const std::string& http_date_now() {  // per-thread cache, re-rendered once a second
   thread_local time_t cached_t = 0;
   thread_local std::string cached;
   const time_t t = time(nullptr);

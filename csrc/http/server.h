@@ -122,6 +122,6 @@ class HttpServer {
 bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>& names, double* out);
 
 // HTTP date (RFC 7231 IMF-fixdate), cached per second.
-std::string http_date_now();
+const std::string& http_date_now();  // per-thread cache
 
 }  // namespace mlapi
