@@ -81,18 +81,46 @@ class BinarySGDTrainer:
         self.grad[self.F + 1] = (torch.clamp(z, min=0) - z * y + torch.log1p(torch.exp(-z.abs()))).sum()
         self.grad[self.F + 2] = ((z > 0) == (y > 0.5)).sum()
 
+    def _fused_step(self, X: torch.Tensor, y: torch.Tensor) -> None:
+        # one replica: gradient + reduce + update fused into 2 launches (no all-reduce between)
+        from mlapi_amd.ops.linear import _DT, _check, _stream
+
+        _check(X, y)
+        B = X.shape[0]
+        ws = self._workspace(B)
+        self._C.train_binary_step(_DT[X.dtype], X.data_ptr(), y.data_ptr(), self.params.data_ptr(),
+                                  0 if self.mom is None else self.mom.data_ptr(), B, self.F,
+                                  self.grad.data_ptr(), ws.data_ptr(), ws.numel(), float(self.lr), 1.0 / B,
+                                  float(self.l2), float(self.momentum), _stream())
+
+    def capture(self, X: torch.Tensor, y: torch.Tensor) -> None:
+        """Capture the one-replica step for (X, y) in a HIP graph; later ``step(X, y)`` calls with
+        these exact tensors replay it (one host call for the whole step - small batches are
+        launch-bound). Single replica only (the all-reduce stays outside graphs)."""
+        if not self.on_gpu or self.info.world != 1:
+            raise RuntimeError("graph capture: single-GPU replica only")
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        saved = (self.params.clone(), None if self.mom is None else self.mom.clone())
+        with torch.cuda.stream(s):  # warm-up: allocates the workspace outside the capture
+            self._fused_step(X, y)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._fused_step(X, y)
+        self.params.copy_(saved[0])
+        if self.mom is not None:
+            self.mom.copy_(saved[1])
+        self._graph = (g, X, y)
+
     def step(self, X: torch.Tensor, y: torch.Tensor) -> None:
         B = X.shape[0]
         if self.on_gpu and self.info.world == 1:
-            # one replica: gradient + reduce + update fused into 2 launches (no all-reduce between)
-            from mlapi_amd.ops.linear import _DT, _check, _stream
-
-            _check(X, y)
-            ws = self._workspace(B)
-            self._C.train_binary_step(_DT[X.dtype], X.data_ptr(), y.data_ptr(), self.params.data_ptr(),
-                                      0 if self.mom is None else self.mom.data_ptr(), B, self.F,
-                                      self.grad.data_ptr(), ws.data_ptr(), ws.numel(), float(self.lr), 1.0 / B,
-                                      float(self.l2), float(self.momentum), _stream())
+            g = getattr(self, "_graph", None)
+            if g is not None and g[1] is X and g[2] is y:
+                g[0].replay()
+            else:
+                self._fused_step(X, y)
             self.steps += 1
             self._n_seen = B
             return

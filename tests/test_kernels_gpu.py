@@ -342,6 +342,22 @@ def test_softmax_fused_update_equals_separate_update(momentum):
         assert torch.equal(a.mom, b.mom)
 
 
+def test_binary_sgd_graph_replay_is_exact():
+    """BinarySGDTrainer.capture: the replayed HIP graph runs the same two launches as eager steps."""
+    from mlapi_amd.train.sgd import BinarySGDTrainer, synthetic_binary
+
+    X, y = synthetic_binary(4096, 256, seed=3, dtype=torch.bfloat16, device=DEV)
+    eager = BinarySGDTrainer(256, lr=0.5, l2=1e-3, momentum=0.9, device=torch.device(DEV))
+    graphed = BinarySGDTrainer(256, lr=0.5, l2=1e-3, momentum=0.9, device=torch.device(DEV))
+    graphed.capture(X, y)
+    assert torch.equal(graphed.params, eager.params)  # capture leaves the parameters untouched
+    for _ in range(25):
+        eager.step(X, y)
+        graphed.step(X, y)
+    torch.cuda.synchronize()
+    assert torch.equal(eager.params, graphed.params) and eager.last_accuracy() > 0.8
+
+
 def test_softmax_sgd_gpu_trains_and_graph_replay_is_exact():
     from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer, synthetic_multiclass
 
