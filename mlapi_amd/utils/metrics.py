@@ -63,6 +63,11 @@ def render(engine_stats: Optional[dict] = None, server_stats: Optional[dict] = N
             for path, n in es["path_batches"].items():
                 _line(out, "mlapi_kernel_batches_total", n, {**labels, "kernel": path})
             _line(out, "mlapi_kernel_batches_total", es.get("inline_batches", 0), {**labels, "kernel": "small_inline"})
+            _line(out, "mlapi_kernel_batches_total", es.get("direct_batches", 0), {**labels, "kernel": "small_direct_aql"})
+        if "idle_batches" in es:
+            out += ["# HELP mlapi_idle_path_batches_total Batches the submitting IO thread ran itself on an idle engine.",
+                    "# TYPE mlapi_idle_path_batches_total counter"]
+            _line(out, "mlapi_idle_path_batches_total", es["idle_batches"], labels)
     if server_stats:
         out += ["# HELP mlapi_http_requests_total HTTP requests by path taken.",
                 "# TYPE mlapi_http_requests_total counter"]

@@ -207,6 +207,7 @@ def test_operational_endpoints(iris_cwd):
     c.post("/predict", json=A1)
     m = c.get("/metrics").text
     assert "mlapi_requests_total" in m and "mlapi_batch_size_bucket" in m
+    assert "mlapi_idle_path_batches_total" in m  # the engine's idle-path counter is exported
     assert c.post("/admin/reload").json()["reloaded"] is True
 
 
