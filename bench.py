@@ -332,8 +332,9 @@ def main(argv=None) -> int:
     ap.add_argument("--mode", default="serve",
                     choices=["serve", "serve_wide", "gemv", "gemm", "train", "train_softmax"])
     ap.add_argument("--conns", type=int, default=64)
-    ap.add_argument("--reqs-per-conn", type=int, default=2048,
-                    help="serve: one step = conns x this many requests per rank (~0.1-0.2 s)")
+    ap.add_argument("--reqs-per-conn", type=int, default=3072,
+                    help="serve: one step = conns x this many requests per rank (~0.15-0.25 s, so the "
+                         "driver's 20 steps time >= 2 s even at 1.3 M req/s)")
     ap.add_argument("--workload-rows", type=int, default=1024, help="serve: distinct validated requests")
     ap.add_argument("--wide-classes", type=int, default=1000, help="serve_wide: 2 = binary GEMV, else softmax GEMM")
     ap.add_argument("--client-threads", type=int, default=0, help="0 = auto from the CPUs per rank")

@@ -188,7 +188,7 @@ def test_dp_serving_reload(tmp_path, iris_pickle_bytes):
 
 def test_bench_contract_two_ranks():
     out = run(2, str(ROOT / "bench.py"), {}, args=["--cpu", "--gpus", "2", "--steps", "10", "--warmup", "2",
-                                                   "--c1-requests", "200"])
+                                                   "--c1-requests", "200", "--reqs-per-conn", "512"])
     lines = [l for l in out.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out
     d = json.loads(lines[0])
