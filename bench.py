@@ -66,6 +66,50 @@ def _timed(info, fn):
     return all_reduce_max(t1 - t0, info), out
 
 
+def _comm_probe(info, model=None) -> dict:
+    """Evidence of the job's communicator, measured before the timed region and reported in every
+    bench line: how many ranks RCCL itself counts (ncclCommCount), the C1 model broadcast latency,
+    and the C2 all-reduce latency at the two gradient sizes of SURVEY 2.4 (1 KiB binary, 1 MiB
+    1000-class). All max over ranks."""
+    import torch
+
+    from mlapi_amd.models.linear import LinearModel
+    from mlapi_amd.parallel.comm import _coll_device, all_reduce_max, all_reduce_sum_, barrier, broadcast_model
+
+    out = {"comm_nranks": info.comm_nranks()}
+    kind = getattr(info.comm, "kind", info.backend)
+    out["rccl_nranks"] = (info.comm_nranks() if kind == "native-rccl" or info.backend == "nccl" else None)
+    if model is None:
+        model = LinearModel.random(256, 1000, seed=3) if info.is_main else None
+    barrier(info)
+    t0 = time.perf_counter()
+    broadcast_model(model if info.is_main else None, info)
+    out["c1_bcast_us"] = all_reduce_max(time.perf_counter() - t0, info) * 1e6
+    out["c1_payload"] = "K=1000 x F=256 f64 W|b (2 MB) + label header"
+    dev = _coll_device(info)
+    ar = {}
+    for name, nbytes in (("1KiB", 1 << 10), ("1MiB", 1 << 20)):
+        t = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+        for _ in range(3):
+            all_reduce_sum_(t, info)
+        _sync(info)
+        barrier(info)
+        iters = 20
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            all_reduce_sum_(t, info)
+        _sync(info)
+        dt = (time.perf_counter() - t0) / iters
+        if info.comm is not None and hasattr(info.comm, "wait"):
+            info.comm.wait()
+        ar[name] = all_reduce_max(dt, info) * 1e6
+        want = float(info.world) ** (3 + iters)
+        if info.world > 1 and abs(float(t[0].item()) - want) > 1e-4 * want:
+            raise RuntimeError(f"all-reduce probe ({name}) returned {float(t[0].item())}")
+    out["allreduce_us"] = ar
+    return out
+
+
 def _share_port(port: int, info) -> int:
     """Rank 0's bound port, known to every rank (the shared SO_REUSEPORT port of the DP group)."""
     from mlapi_amd.parallel.comm import all_gather_floats
@@ -88,6 +132,7 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
     device = "cpu" if info.device is None else f"cuda:{info.device.index}"
     mk = lambda port: Config.from_env(port=port, device=device, reload="off", missing_model="keep",  # noqa: E731
                                       io_threads=args.io_threads, max_batch=args.max_batch, reuseport=True,
+                                      dispatch=args.dispatch,
                                       model_path="/nonexistent/bench.pkl", feature_names=list(names), **dtype_cfg)
     srv = None
     if info.is_main:  # rank 0 binds an ephemeral port, the other ranks join its SO_REUSEPORT group
@@ -133,14 +178,16 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         s3 = srv.runtime.handle.stats()
         barrier(info)
         nb = max(1, s1["batches"] - s0["batches"])
+        # the batch=1 connection lands on whichever replica the dispatcher picks: sum its deltas over ranks
         per_rank = all_gather_floats([res["p50_ns"] / 1e6, res["p99_ns"] / 1e6, res["completed"],
                                       (s1["requests"] - s0["requests"]) / nb,
                                       (s1["device_us_sum"] - s0["device_us_sum"]) / nb,
-                                      (s3["device_us_sum"] - s2["device_us_sum"]) / max(1, s3["batches"] - s2["batches"]),
-                                      s1["requests"] - s0["requests"]], info)
+                                      s3["device_us_sum"] - s2["device_us_sum"], s3["batches"] - s2["batches"],
+                                      s1["requests"] - s0["requests"], s1["idle_batches"] - s0["idle_batches"],
+                                      s3["idle_batches"] - s2["idle_batches"]], info)
         barrier(info)
         paths = {k: s1["path_batches"][k] - s0["path_batches"][k] for k in s1["path_batches"]}
-        idle = {"c64": s1["idle_batches"] - s0["idle_batches"], "batch1": s3["idle_batches"] - s2["idle_batches"]}
+        idle = {"c64": int(per_rank[:, 8].sum()), "batch1": int(per_rank[:, 9].sum())}
     finally:
         srv.stop()
     total = float(np.sum(per_rank[:, 2]))
@@ -154,11 +201,11 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         "timed_region_s": elapsed,
         "body_mismatches": 0,
         "validated_responses": int(total),
-        "served_per_rank": [int(v) for v in per_rank[:, 6]],
+        "served_per_rank": [int(v) for v in per_rank[:, 7]],
         "mean_gpu_batch_rows": float(np.mean(per_rank[:, 3])),
         # launch -> completion seen by the completer thread, per batch (the GPU leg of a request)
         "gpu_leg_us_c64": float(np.mean(per_rank[:, 4])),
-        "gpu_leg_us_batch1": float(per_rank[0, 5]),
+        "gpu_leg_us_batch1": float(per_rank[:, 5].sum() / max(1.0, per_rank[:, 6].sum())),
         "kernel_batches": paths,
         # batches the IO thread launched itself on an idle engine (Engine::run_idle)
         "idle_path_batches": idle,
@@ -166,7 +213,9 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         "cpu_cores_busy_rank0": cpu_util,
         "threads": {"io": args.io_threads, "loadgen": args.client_threads, "pinned_cpus": args.pinned_cpus},
         "requests_per_step": args.reqs_per_conn * args.conns * info.world,
-        "topology": "one SO_REUSEPORT port shared by all ranks; one out-of-process load generator per rank",
+        "topology": ("one port for all ranks, connections dealt round robin by the group's acceptor "
+                     "(csrc/http/dispatch.h); one out-of-process load generator per rank"),
+        "dispatch": srv.config.dispatch,
     }
     return ("requests_per_sec_whole_node", value, "req/s", elapsed, extra,
             {"model": model_desc, "global_batch": args.conns * info.world, "seq_len": 1, "features": features,
@@ -324,6 +373,27 @@ def bench_train_softmax(args, info):
              "seq_len": 1, "features": F, "classes": K, "parallelism": f"dp{info.world}"})
 
 
+def _self_launch(args, argv) -> int:
+    """Parent of a self-launched N-rank run. Refuses more ranks than GPUs unless the data plane is
+    the P2P kernel (``MLAPI_COMM=p2p``, several ranks per device) or the run is on CPUs."""
+    comm = os.environ.get("MLAPI_COMM", "auto").lower()
+    if not args.cpu:
+        import torch  # device_count() does not initialise the GPU on this image
+
+        ndev = torch.cuda.device_count()
+        if ndev == 0:
+            print("bench.py: --gpus > 1 but no GPU is visible (use --cpu for a CPU rehearsal)", file=sys.stderr)
+            return 2
+        if args.gpus > ndev and comm != "p2p":
+            print(f"bench.py: --gpus {args.gpus} but only {ndev} GPU(s) visible; RCCL needs one GPU per rank "
+                  "(MLAPI_COMM=p2p shares a device between ranks)", file=sys.stderr)
+            return 2
+    from mlapi_amd import launch
+
+    largv = ["--nproc", str(args.gpus)] + ([] if args.pin == "on" else ["--no-pin"])
+    return launch.main(largv + [os.path.abspath(__file__)] + list(argv))
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -340,6 +410,8 @@ def main(argv=None) -> int:
     ap.add_argument("--client-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--io-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--max-batch", type=int, default=256)
+    ap.add_argument("--dispatch", default="acceptor", choices=["acceptor", "reuseport"],
+                    help="serve: connections dealt round robin by one acceptor (default) or hashed by SO_REUSEPORT")
     ap.add_argument("--c1-requests", type=int, default=3000)
     ap.add_argument("--rows", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=1024)
@@ -357,6 +429,18 @@ def main(argv=None) -> int:
                          "one box, pinning cost c=64 throughput at N=1 (0.65-0.80 M vs 0.98-1.06 M "
                          "req/s) and N=2 (0.83-0.85 M vs 0.92-1.02 M), profiles/r2_pin/)")
     args = ap.parse_args(argv)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # `python bench.py --gpus N`: start the N rank processes ourselves (one per GPU) through the
+        # framework's launcher - fresh child processes, nothing re-exec'd, this parent never touches
+        # the GPU. Rank 0's JSON line reaches stdout through the inherited descriptor.
+        return _self_launch(args, sys.argv[1:] if argv is None else list(argv))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks",
+              file=sys.stderr)
+        return 2
     if args.mode in ("serve", "serve_wide"):
         # the load generator is its own process, started before anything touches the GPU
         from mlapi_amd.serve.loadgen import LoadgenProcess
@@ -366,6 +450,14 @@ def main(argv=None) -> int:
     from mlapi_amd.parallel.comm import init_distributed, shutdown
 
     info = init_distributed(use_gpu=False if args.cpu else None)
+    if info.backend == "gloo-fallback":
+        # the RCCL communicator failed to initialise: a number measured over the host gloo group
+        # would be mislabelled as a GPU-collective run
+        print(f"bench.py: rank {info.rank}: RCCL unavailable (gloo fallback); refusing to benchmark", file=sys.stderr)
+        return 3
+    if info.world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but {info.world} rank(s) initialised", file=sys.stderr)
+        return 2
     local = int(os.environ.get("LOCAL_WORLD_SIZE", info.world))
     pinned = []
     if args.pin == "on":
@@ -399,6 +491,10 @@ def main(argv=None) -> int:
     if args.mode != "serve" and info.device is None:
         print(f"mode {args.mode} needs a GPU", file=sys.stderr)
         return 2
+    probe = _comm_probe(info)
+    if info.world > 1 and probe["comm_nranks"] != info.world:
+        print(f"bench.py: communicator reports {probe['comm_nranks']} ranks, expected {info.world}", file=sys.stderr)
+        return 2
     fn = {"serve": bench_serve, "serve_wide": bench_serve_wide, "gemv": bench_gemv, "gemm": bench_gemm,
           "train": bench_train, "train_softmax": bench_train_softmax}[args.mode]
     try:
@@ -415,6 +511,7 @@ def main(argv=None) -> int:
             "data": "synthetic (random-init weights, fixed synthetic inputs)", "config": config,
             "comm_backend": info.backend,
         }
+        line.update(probe)
         line.update(extra)
         print(json.dumps(line), flush=True)
     shutdown(info)

@@ -16,6 +16,7 @@
 #include "dist/p2p.h"
 #include "http/loadgen.h"
 #include "http/server.h"
+#include "http/dispatch.h"
 #include "mlapi/common.h"
 #include "mlapi/kernels.h"
 #include "runtime/engine.h"
@@ -415,7 +416,10 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("access_log_fd", &ServerConfig::access_log_fd)
       .def_readwrite("health_dispatch", &ServerConfig::health_dispatch)
       .def_readwrite("health_probe_ms", &ServerConfig::health_probe_ms)
-      .def_readwrite("backlog", &ServerConfig::backlog);
+      .def_readwrite("backlog", &ServerConfig::backlog)
+      .def_readwrite("dispatch", &ServerConfig::dispatch)
+      .def_readwrite("dispatch_group", &ServerConfig::dispatch_group)
+      .def_readwrite("dispatch_rank", &ServerConfig::dispatch_rank);
 
   // ---- native RCCL communicator (csrc/dist/comm.h)
   py::class_<RcclComm>(m, "RcclComm")
@@ -463,7 +467,10 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("world", &RcclComm::world)
       .def_property_readonly("device", &RcclComm::device)
-      .def_property_readonly("aborted", &RcclComm::aborted);
+      .def_property_readonly("aborted", &RcclComm::aborted)
+      .def("comm_count", &RcclComm::comm_count)
+      .def("comm_device", &RcclComm::comm_device)
+      .def("comm_rank", &RcclComm::comm_rank);
 
   // ---- one-shot P2P all-reduce over IPC-mapped peer buffers (csrc/dist/p2p.h)
   py::class_<P2PAllReduce>(m, "P2PAllReduce")
@@ -546,6 +553,17 @@ PYBIND11_MODULE(_C, m) {
         d["listen_closes"] = st.listen_closes;
         d["accepting"] = st.accepting;
         d["listeners"] = s.listeners();
+        if (const ConnDispatcher* dp = s.dispatcher()) {
+          py::dict x;
+          x["leader"] = dp->leader();
+          x["group"] = dp->group();
+          x["received"] = dp->received();
+          x["elections"] = dp->elections();
+          py::list ts;
+          for (const auto& t : dp->targets()) ts.append(py::make_tuple(t.rank, t.conns, t.healthy));
+          x["targets"] = ts;
+          d["dispatch"] = x;
+        }
         return d;
       });
 

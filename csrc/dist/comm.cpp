@@ -30,6 +30,9 @@ struct RcclApi {
   decltype(&::ncclReduceScatter) ReduceScatter = nullptr;
   decltype(&::ncclGroupStart) GroupStart = nullptr;
   decltype(&::ncclGroupEnd) GroupEnd = nullptr;
+  decltype(&::ncclCommCount) CommCount = nullptr;
+  decltype(&::ncclCommCuDevice) CommCuDevice = nullptr;
+  decltype(&::ncclCommUserRank) CommUserRank = nullptr;
 };
 
 namespace {
@@ -71,6 +74,9 @@ const RcclApi& api() {
       bind(h, a.ReduceScatter, "ncclReduceScatter");
       bind(h, a.GroupStart, "ncclGroupStart");
       bind(h, a.GroupEnd, "ncclGroupEnd");
+      bind(h, a.CommCount, "ncclCommCount");
+      bind(h, a.CommCuDevice, "ncclCommCuDevice");
+      bind(h, a.CommUserRank, "ncclCommUserRank");
     } catch (const std::exception& e) {
       error = e.what();
       a.handle = nullptr;
@@ -148,6 +154,27 @@ void RcclComm::reduce_scatter(const void* send, void* recv, size_t recv_count, i
   check(api_->ReduceScatter(send, recv, recv_count, static_cast<ncclDataType_t>(dtype),
                             static_cast<ncclRedOp_t>(op), as_comm(comm_), stream),
         "ncclReduceScatter");
+}
+
+int RcclComm::comm_count() const {
+  int n = 0;
+  if (aborted_) throw std::runtime_error("RcclComm: communicator aborted");
+  const_cast<RcclComm*>(this)->check(api_->CommCount(as_comm(comm_), &n), "ncclCommCount");
+  return n;
+}
+
+int RcclComm::comm_device() const {
+  int d = -1;
+  if (aborted_) throw std::runtime_error("RcclComm: communicator aborted");
+  const_cast<RcclComm*>(this)->check(api_->CommCuDevice(as_comm(comm_), &d), "ncclCommCuDevice");
+  return d;
+}
+
+int RcclComm::comm_rank() const {
+  int r = -1;
+  if (aborted_) throw std::runtime_error("RcclComm: communicator aborted");
+  const_cast<RcclComm*>(this)->check(api_->CommUserRank(as_comm(comm_), &r), "ncclCommUserRank");
+  return r;
 }
 
 void RcclComm::group_start() { check(api_->GroupStart(), "ncclGroupStart"); }

@@ -48,6 +48,12 @@ class RcclComm {
   bool barrier(hipStream_t stream, int timeout_ms);
   void abort();
 
+  // What RCCL itself reports for this communicator (ncclCommCount / ncclCommCuDevice /
+  // ncclCommUserRank): the evidence that a job really runs `world` RCCL ranks.
+  int comm_count() const;
+  int comm_device() const;
+  int comm_rank() const;
+
   int rank() const { return rank_; }
   int world() const { return world_; }
   int device() const { return device_; }

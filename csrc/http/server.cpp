@@ -1,6 +1,8 @@
 // Native HTTP/1.1 server (see server.h).
 #include "server.h"
 
+#include "dispatch.h"
+
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netdb.h>
@@ -406,8 +408,11 @@ class IoThread : public Sink {
     if (epfd_ < 0 || evfd_ < 0) throw std::runtime_error("epoll/eventfd creation failed");
     epoll_event ev{};
     ev.events = EPOLLIN;
-    ev.data.u64 = ID_LISTEN;
-    epoll_ctl(epfd_, EPOLL_CTL_ADD, lfd_, &ev);
+    if (lfd_ >= 0) {  // reuseport mode: this thread's own listener; acceptor mode: adopt() hands connections
+      ev.data.u64 = ID_LISTEN;
+      epoll_ctl(epfd_, EPOLL_CTL_ADD, lfd_, &ev);
+    }
+    listening_.store(lfd_ >= 0);
     ev.data.u64 = ID_EVENT;
     epoll_ctl(epfd_, EPOLL_CTL_ADD, evfd_, &ev);
     const auto& cfg = srv_->config();
@@ -432,6 +437,15 @@ class IoThread : public Sink {
     {
       std::lock_guard<std::mutex> lk(mu_);
       fast_.push_back(FastBatch{model, std::vector<Completion>(c, c + n)});
+    }
+    wake();
+  }
+
+  // Acceptor mode: a connected socket from the group's dispatcher (any thread).
+  void adopt(int fd) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      adopted_.push_back(fd);
     }
     wake();
   }
@@ -579,6 +593,7 @@ class IoThread : public Sink {
   // to this rank; it re-binds once the engine is healthy again. Connections already accepted keep
   // being served (their requests complete with 500 while the engine is down).
   void apply_listen_state() {
+    if (srv_->acceptor_mode()) return;  // the group's dispatcher skips unhealthy replicas instead
     const bool want = srv_->accepting();
     if (want == listening_.load(std::memory_order_relaxed)) return;
     if (!want) {
@@ -650,6 +665,12 @@ class IoThread : public Sink {
       socklen_t sl = sizeof ss;
       const int fd = accept4(lfd_, reinterpret_cast<sockaddr*>(&ss), &sl, SOCK_NONBLOCK | SOCK_CLOEXEC);
       if (fd < 0) return;
+      register_conn(fd, ss);
+    }
+  }
+
+  void register_conn(int fd, const sockaddr_storage& ss) {
+    {
       int one = 1;
       setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);  // never Nagle
       auto c = std::make_unique<Conn>();
@@ -812,10 +833,18 @@ class IoThread : public Sink {
   void drain_pending() {
     std::vector<FastBatch> fast;
     std::vector<SlowResp> slow;
+    std::vector<int> adopted;
     {
       std::lock_guard<std::mutex> lk(mu_);
       fast.swap(fast_);
       slow.swap(slow_);
+      adopted.swap(adopted_);
+    }
+    for (int fd : adopted) {
+      sockaddr_storage ss{};
+      socklen_t sl = sizeof ss;
+      getpeername(fd, reinterpret_cast<sockaddr*>(&ss), &sl);
+      register_conn(fd, ss);
     }
     for (FastBatch& fb : fast) render_fast(fb);
     for (SlowResp& sr : slow) {
@@ -1071,6 +1100,7 @@ class IoThread : public Sink {
   std::atomic<bool> pending_{false};   // completions / slow responses queued for this thread
   std::atomic<bool> spinning_{false};  // inside the busy-poll window (no eventfd needed)
   std::mutex mu_;
+  std::vector<int> adopted_;  // acceptor mode: connections handed over by the dispatcher
   std::vector<FastBatch> fast_;
   std::vector<Completion> idle_done_;  // run_idle completions (this thread only)
   std::string body_;                   // response body scratch (this thread only)
@@ -1089,7 +1119,10 @@ HttpServer::HttpServer(Engine* engine, const ServerConfig& cfg) : engine_(engine
   if (cfg_.io_threads > 64) cfg_.io_threads = 64;
 }
 
-HttpServer::~HttpServer() { stop(); }
+HttpServer::~HttpServer() {
+  stop();
+  for (auto& t : threads_) (void)t;  // IO threads are joined by stop()
+}
 
 namespace {
 // Completion of a health probe row: a successful batch re-admits the rank.
@@ -1110,7 +1143,10 @@ void HttpServer::health_loop() {
   std::vector<double> row;
   while (!health_stop_.load()) {
     const bool ok = engine_->healthy();
-    if (accepting_.load() != ok) accepting_.store(ok);
+    if (accepting_.load() != ok) {
+      if (!ok) leaves_.fetch_add(1);
+      accepting_.store(ok);
+    }
     if (!ok && probe.state.load() == 0) {
       auto m = engine_->model();
       if (m) {
@@ -1126,6 +1162,7 @@ void HttpServer::health_loop() {
 }
 
 int HttpServer::listeners() const {
+  if (acceptor_) return accepting() ? (int)threads_.size() : 0;
   int n = 0;
   for (const auto& t : threads_) n += t->listening() ? 1 : 0;
   return n;
@@ -1133,6 +1170,28 @@ int HttpServer::listeners() const {
 
 void HttpServer::start() {
   if (started_) return;
+  if (cfg_.dispatch == "acceptor") {
+    acceptor_ = true;
+    for (int i = 0; i < cfg_.io_threads; ++i) threads_.push_back(std::make_unique<IoThread>(this, i, -1));
+    for (auto& t : threads_) t->start();
+    dispatcher_ = std::make_unique<ConnDispatcher>(
+        cfg_.dispatch_group, cfg_.host, cfg_.port, cfg_.backlog, cfg_.dispatch_rank,
+        [this](int fd) { threads_[adopt_rr_.fetch_add(1, std::memory_order_relaxed) % threads_.size()]->adopt(fd); },
+        [this] { return accepting(); });
+    try {
+      dispatcher_->start();
+    } catch (...) {
+      for (auto& t : threads_) t->stop();
+      threads_.clear();
+      dispatcher_.reset();
+      throw;
+    }
+    bound_port_ = dispatcher_->port();
+    if (cfg_.health_dispatch) health_ = std::thread([this] { health_loop(); });
+    started_ = true;
+    return;
+  }
+  if (cfg_.dispatch != "reuseport") throw std::invalid_argument("dispatch must be acceptor or reuseport");
   int port = cfg_.port;
   std::vector<int> fds;
   try {
@@ -1163,6 +1222,7 @@ void HttpServer::stop() {
   slow_cv_.notify_all();
   health_stop_.store(true);
   if (health_.joinable()) health_.join();
+  if (dispatcher_) dispatcher_->stop();  // no new connections while the IO threads wind down
   for (auto& t : threads_) t->stop();
   threads_.clear();
 }
@@ -1230,6 +1290,7 @@ ServerStats HttpServer::stats() const {
     s.bad_requests += t->n_bad.load();
     s.listen_closes += t->n_listen_close.load();
   }
+  s.listen_closes += leaves_.load();
   s.accepting = accepting_.load();
   return s;
 }

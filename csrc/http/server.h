@@ -59,6 +59,12 @@ struct ServerConfig {
   // connections) the threads block as usual and no CPU is spent spinning. 0 = off.
   int io_spin_lowload_us = 50;
   int io_spin_max_conns = 2;
+  // Connection dispatch (dispatch.h): "acceptor" (default) = one acceptor per serving group hands
+  // every new connection to the next healthy replica / IO thread, round robin; "reuseport" = every
+  // IO thread listens on the port itself and the kernel hashes connections over the listeners.
+  std::string dispatch = "acceptor";
+  std::string dispatch_group;  // "" = named after host:port
+  int dispatch_rank = 0;       // this replica's rank (reported to the group's leader)
 };
 
 struct SlowRequest {
@@ -72,9 +78,11 @@ struct SlowRequest {
 
 struct ServerStats {
   uint64_t fast = 0, slow = 0, responses = 0, connections = 0, errors = 0, bad_requests = 0;
-  uint64_t listen_closes = 0;  // health_dispatch: times this rank left its SO_REUSEPORT group
+  uint64_t listen_closes = 0;  // health_dispatch: times this rank left its dispatch group
   bool accepting = true;
 };
+
+class ConnDispatcher;
 
 class IoThread;
 
@@ -99,6 +107,8 @@ class HttpServer {
 
   // internal, used by IoThread
   void push_slow(SlowRequest&& r);
+  bool acceptor_mode() const { return acceptor_; }
+  ConnDispatcher* dispatcher() const { return dispatcher_.get(); }
 
  private:
   Engine* engine_;
@@ -114,6 +124,10 @@ class HttpServer {
   std::atomic<bool> health_stop_{false};
   std::thread health_;
   void health_loop();
+  bool acceptor_ = false;
+  std::unique_ptr<ConnDispatcher> dispatcher_;
+  std::atomic<uint64_t> adopt_rr_{0};
+  std::atomic<uint64_t> leaves_{0};  // acceptor mode: healthy -> unhealthy transitions
 };
 
 // Strict parser for the fast path. Returns true only for a JSON object in which every name in

@@ -7,7 +7,11 @@
 
 #include <immintrin.h>
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstddef>
 #include <cstring>
 #include <fstream>
@@ -24,9 +28,10 @@ struct Kernel {
 };
 
 struct AgentSearch {
-  uint32_t bdf = 0, domain = 0;
+  uint32_t bdf = 0, domain = 0;  // bdf = bus << 8 | device << 3 | function
   hsa_agent_t gpu{}, cpu{};
   bool have_gpu = false, have_cpu = false;
+  int matches = 0;  // GPU agents with this exact domain:bus:device.function (must be 1)
 };
 
 hsa_status_t pick_agents(hsa_agent_t a, void* data) {
@@ -36,13 +41,16 @@ hsa_status_t pick_agents(hsa_agent_t a, void* data) {
   if (t == HSA_DEVICE_TYPE_CPU && !s->have_cpu) {
     s->cpu = a;
     s->have_cpu = true;
-  } else if (t == HSA_DEVICE_TYPE_GPU && !s->have_gpu) {
+  } else if (t == HSA_DEVICE_TYPE_GPU) {
     uint32_t bdf = 0, dom = 0;
     hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
     hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
     if (bdf == s->bdf && dom == s->domain) {
-      s->gpu = a;
-      s->have_gpu = true;
+      ++s->matches;
+      if (!s->have_gpu) {
+        s->gpu = a;
+        s->have_gpu = true;
+      }
     }
   }
   return HSA_STATUS_SUCCESS;
@@ -86,7 +94,9 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     if (inited_) hsa_shut_down();
   }
 
-  bool init(int device, const std::string& path, std::string* why) {
+  bool init(int device, const std::string& path, int max_in_flight, std::string* why) {
+    ka_slots_ = std::max<uint32_t>(64u, 8u * (uint32_t)std::max(1, max_in_flight));
+    if (const char* e = getenv("MLAPI_HDP_READBACK")) hdp_readback_ = atoi(e) != 0;
     auto fail = [&](const std::string& m) {
       if (why) *why = m;
       return false;
@@ -96,13 +106,22 @@ class HsaInlineDispatcher final : public InlineDispatcher {
         hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess)
       return fail("no PCI id for the HIP device");
     (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device);
+    // The PCI function matters in partitioned modes (several agents behind one bus:device, each
+    // its own function): the full "dddd:bb:dd.f" id names exactly one agent.
+    int fn = 0;
+    char pci[64] = {0};
+    if (hipDeviceGetPCIBusId(pci, sizeof pci, device) == hipSuccess) {
+      unsigned d0 = 0, b0 = 0, v0 = 0, f0 = 0;
+      if (sscanf(pci, "%x:%x:%x.%x", &d0, &b0, &v0, &f0) == 4 && (int)b0 == bus && (int)v0 == dev) fn = (int)f0;
+    }
     if (hsa_init() != HSA_STATUS_SUCCESS) return fail("hsa_init failed");
     inited_ = true;
     AgentSearch s;
-    s.bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3);
+    s.bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3) | ((uint32_t)fn & 7u);
     s.domain = (uint32_t)dom;
     hsa_iterate_agents(pick_agents, &s);
     if (!s.have_gpu || !s.have_cpu) return fail("HSA agent of the HIP device not found");
+    if (s.matches != 1) return fail("HIP device matches " + std::to_string(s.matches) + " HSA agents");
     gpu_ = s.gpu;
     hsa_amd_memory_pool_t pool{};
     if (hsa_amd_agent_iterate_memory_pools(s.cpu, pick_kernarg_pool, &pool) != HSA_STATUS_INFO_BREAK)
@@ -143,7 +162,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     if (hsa_agent_get_info(gpu_, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp) == HSA_STATUS_SUCCESS &&
         hdp.HDP_MEM_FLUSH_CNTL != nullptr &&
         hsa_amd_agent_iterate_memory_pools(gpu_, pick_device_pool, &dpool) == HSA_STATUS_INFO_BREAK &&
-        hsa_amd_memory_pool_allocate(dpool, (size_t)stride_ * KA_SLOTS, 0, (void**)&kernargs_) == HSA_STATUS_SUCCESS) {
+        hsa_amd_memory_pool_allocate(dpool, (size_t)stride_ * ka_slots_, 0, (void**)&kernargs_) == HSA_STATUS_SUCCESS) {
       if (hsa_amd_agents_allow_access(1, &s.cpu, nullptr, kernargs_) == HSA_STATUS_SUCCESS) {
         hdp_flush_ = hdp.HDP_MEM_FLUSH_CNTL;
       } else {
@@ -152,10 +171,10 @@ class HsaInlineDispatcher final : public InlineDispatcher {
       }
     }
     if (kernargs_ == nullptr &&
-        (hsa_amd_memory_pool_allocate(pool, (size_t)stride_ * KA_SLOTS, 0, (void**)&kernargs_) != HSA_STATUS_SUCCESS ||
+        (hsa_amd_memory_pool_allocate(pool, (size_t)stride_ * ka_slots_, 0, (void**)&kernargs_) != HSA_STATUS_SUCCESS ||
          hsa_amd_agents_allow_access(1, &gpu_, nullptr, kernargs_) != HSA_STATUS_SUCCESS))
       return fail("kernarg allocation failed");
-    std::memset(kernargs_, 0, (size_t)stride_ * KA_SLOTS);
+    std::memset(kernargs_, 0, (size_t)stride_ * ka_slots_);
     return true;
   }
 
@@ -164,7 +183,20 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     if (faulted()) throw std::runtime_error("direct dispatch: queue error");
     const Kernel& k = (a.F == 4 && a.K == 3) ? k_[dt == DT_F64 ? 4 : 5]  // exact shape: one load batch
                                               : k_[(dt == DT_F64 ? 0 : 2) + (a.F <= 8 && a.K <= 4 ? 0 : 1)];
-    char* ka = kernargs_ + (size_t)(launches_++ % KA_SLOTS) * stride_;
+    // Ring entry reuse: the packet that last used this entry (ka_slots_ launches ago) must have been
+    // consumed by the packet processor. With at most `slots` batches in flight and the ring >= 8x
+    // deeper, its kernel has finished as well; after a watchdog failure (a batch given up while its
+    // packet may still be queued) this wait is what keeps live arguments from being overwritten.
+    if (launches_ >= ka_slots_) {
+      const uint64_t need = launches_ - ka_slots_ + 1;
+      const auto t0 = std::chrono::steady_clock::now();
+      while (hsa_queue_load_read_index_scacquire(queue_) < need) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200))
+          throw std::runtime_error("direct dispatch: kernarg ring entry still owned by a queued packet");
+        _mm_pause();
+      }
+    }
+    char* ka = kernargs_ + (size_t)(launches_++ % ka_slots_) * stride_;
     // Only the bytes the kernel reads: header + W/b of this model + n rows.
     const size_t es = dt == DT_F64 ? 8 : 4;
     const size_t wb_end = offsetof(InlineBatch, wb) + (size_t)a.K * (a.F + 1) * es;
@@ -173,6 +205,11 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     if (hdp_flush_ != nullptr) {
       _mm_sfence();  // drain the write-combined BAR writes, then flush the HDP ahead of the doorbell
       *reinterpret_cast<volatile uint32_t*>(hdp_flush_) = 1u;
+      // The flush register write is posted: read it back so the flush has completed before the
+      // packet (and so the kernel's kernarg loads) can be seen. MLAPI_HDP_READBACK=0 skips it
+      // (measured ~0.9 us per launch, tools/hsa_dispatch_probe.cpp mode 3) at the risk of stale
+      // kernargs.
+      if (hdp_readback_) (void)*reinterpret_cast<volatile uint32_t*>(hdp_flush_);
     }
     const uint64_t wi = hsa_queue_add_write_index_relaxed(queue_, 1);
     while (wi - hsa_queue_load_read_index_scacquire(queue_) >= queue_->size) {
@@ -209,7 +246,8 @@ class HsaInlineDispatcher final : public InlineDispatcher {
 
  private:
   static constexpr uint32_t QUEUE_SIZE = 256;
-  static constexpr int KA_SLOTS = 64;
+  uint32_t ka_slots_ = 64;
+  bool hdp_readback_ = true;
   const uint32_t stride_ = (uint32_t)((sizeof(InlineBatch) + 255) / 256 * 256);
   bool inited_ = false;
   hsa_agent_t gpu_{};
@@ -228,9 +266,10 @@ void queue_error(hsa_status_t, hsa_queue_t*, void* data) { static_cast<HsaInline
 
 }  // namespace
 
-std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int device, const std::string& hsaco_path, std::string* why) {
+std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int device, const std::string& hsaco_path, int max_in_flight,
+                                                         std::string* why) {
   auto d = std::make_unique<HsaInlineDispatcher>();
-  if (!d->init(device, hsaco_path, why)) return nullptr;
+  if (!d->init(device, hsaco_path, max_in_flight, why)) return nullptr;
   return d;
 }
 

@@ -33,6 +33,10 @@ class InlineDispatcher {
 // Loads `hsaco_path` (csrc/kernels/serve_direct.hip) for the GPU behind HIP device `device` and
 // creates the queue; nullptr with the reason in *why if anything is missing (the engine then keeps
 // using hipLaunchKernel).
-std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int device, const std::string& hsaco_path, std::string* why);
+// `max_in_flight`: the engine's slot count. The kernarg ring is sized to a multiple of it (at least
+// 64 entries), and an entry is rewritten only after the packet processor has consumed the packet
+// that last used it (bounded wait, then an error instead of overwriting live arguments).
+std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int device, const std::string& hsaco_path, int max_in_flight,
+                                                         std::string* why);
 
 }  // namespace mlapi

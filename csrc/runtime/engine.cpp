@@ -122,7 +122,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     MLAPI_HIP_CHECK(hipDeviceSynchronize());
     if (cfg_.direct_dispatch && !cfg_.hsaco_path.empty()) {
       std::string why;
-      direct_ = make_direct_dispatcher(cfg_.device, cfg_.hsaco_path, &why);
+      direct_ = make_direct_dispatcher(cfg_.device, cfg_.hsaco_path, cfg_.slots, &why);
       if (!direct_) std::fprintf(stderr, "[mlapi engine] direct dispatch off (%s): using hipLaunchKernel\n", why.c_str());
     }
     for (int i = 0; i < cfg_.slots; ++i) {

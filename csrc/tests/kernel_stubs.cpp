@@ -24,7 +24,7 @@ void launch_gemm_softmax(const void*, const void*, const float*, int64_t, int, i
                          hipStream_t, RecOut) {
   unreachable("launch_gemm_softmax");
 }
-std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int, const std::string&, std::string* why) {
+std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int, const std::string&, int, std::string* why) {
   if (why) *why = "host-only build";
   return nullptr;
 }

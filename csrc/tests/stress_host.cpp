@@ -30,6 +30,7 @@
 
 #include "http/loadgen.h"
 #include "http/server.h"
+#include "http/dispatch.h"
 #include "runtime/engine.h"
 
 using namespace mlapi;
@@ -213,15 +214,29 @@ void http_stress() {
   scfg.feature_names = {"sepal_length", "sepal_width", "petal_length", "petal_width"};
   HttpServer srv(&eng, scfg);
   srv.start();
+  // a second replica joins srv's dispatch group (same port): the leader deals connections to both
+  // over the SCM_RIGHTS channel while the load below runs
+  ServerConfig mcfg = scfg;
+  mcfg.port = srv.port();
+  mcfg.dispatch_rank = 1;
+  mcfg.io_threads = 2;
+  HttpServer member(&eng, mcfg);
+  member.start();
+  CHECK(srv.dispatcher() && srv.dispatcher()->leader() && member.dispatcher() && !member.dispatcher()->leader(),
+        "dispatch roles");
+  for (int i = 0; i < 500 && srv.dispatcher()->targets().size() < 2; ++i)
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
   std::atomic<bool> stop{false};
   std::atomic<int> slow_seen{0};
   std::thread slow([&] {  // stands in for the Python ASGI app
     SlowRequest r;
     while (!stop.load()) {
-      if (!srv.next_slow(&r, 50)) continue;
-      slow_seen.fetch_add(1);
-      srv.respond(r.token, 422, "Unprocessable Entity", {{"content-type", "application/json"}}, "{\"detail\":[]}",
-                  false);
+      for (HttpServer* h : {&srv, &member}) {  // each replica has its own slow-path queue
+        if (!h->next_slow(&r, 10)) continue;
+        slow_seen.fetch_add(1);
+        h->respond(r.token, 422, "Unprocessable Entity", {{"content-type", "application/json"}}, "{\"detail\":[]}",
+                   false);
+      }
     }
   });
   const std::string body = "{\"sepal_length\":5.1,\"sepal_width\":3.5,\"petal_length\":1.4,\"petal_width\":0.2}";
@@ -288,6 +303,12 @@ void http_stress() {
   stop = true;
   slow.join();
   CHECK(slow_seen.load() > 0, "slow path never used");
+  const auto tg = srv.dispatcher()->targets();
+  CHECK(tg.size() == 2 && tg[1].conns > 0 && (tg[0].conns > tg[1].conns ? tg[0].conns - tg[1].conns
+                                                                        : tg[1].conns - tg[0].conns) <= 1,
+        "round robin: %llu vs %llu", (unsigned long long)tg[0].conns,
+        (unsigned long long)(tg.size() > 1 ? tg[1].conns : 0));
+  member.stop();
   srv.stop();
   eng.stop();
 }

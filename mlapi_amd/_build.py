@@ -35,6 +35,7 @@ SOURCES = [
     "runtime/engine.cpp",
     "runtime/direct_dispatch.cpp",
     "http/server.cpp",
+    "http/dispatch.cpp",
     "http/loadgen.cpp",
     "dist/comm.cpp",
     "dist/p2p_allreduce.hip",

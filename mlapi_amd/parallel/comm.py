@@ -46,6 +46,16 @@ class DistInfo:
     device: Optional[torch.device] = None  # None -> CPU
     backend: str = "none"
     comm: Optional[object] = None  # NativeComm / FakeComm when MLAPI_COMM selects one
+    local_world: int = 1
+
+    def comm_nranks(self) -> int:
+        """Ranks of the data-plane communicator as the communicator itself reports them
+        (ncclCommCount for the native RCCL comm; the process group size otherwise)."""
+        if self.comm is not None and hasattr(self.comm, "nranks"):
+            return int(self.comm.nranks())
+        if self.world > 1 and dist.is_initialized():
+            return dist.get_world_size()
+        return self.world
 
     @property
     def is_main(self) -> bool:
@@ -61,16 +71,24 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if use_gpu is None:
         use_gpu = torch.cuda.is_available() and torch.cuda.device_count() > 0
-    device = None
-    if use_gpu:
-        device = torch.device("cuda", local_rank % torch.cuda.device_count())
-        torch.cuda.set_device(device)
     auto = comm == "auto"
     if comm == "auto":
-        comm = "native" if device is not None else "torch"
+        comm = "native" if use_gpu else "torch"
+    device = None
+    if use_gpu:
+        ndev = torch.cuda.device_count()
+        if local_world > ndev and comm in ("native", "torch"):
+            # RCCL needs one GPU per rank; wrapping local_rank onto a shared device would only fail
+            # later inside ncclCommInitRank (or, worse, run fewer GPUs than the job claims)
+            raise RuntimeError(f"{local_world} ranks on this node but only {ndev} visible GPU(s): RCCL needs one GPU "
+                               "per rank (MLAPI_COMM=p2p runs several ranks on one device)")
+        device = torch.device("cuda", local_rank % ndev)
+        torch.cuda.set_device(device)
     info = DistInfo(rank, world, local_rank, device, "none")
+    info.local_world = local_world
     if comm in ("native", "p2p") and device is None:
         raise RuntimeError(f"MLAPI_COMM={comm} needs a GPU (use fake for CPU runs)")
     if world > 1:

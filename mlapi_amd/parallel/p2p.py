@@ -70,14 +70,16 @@ class P2PAllReduce:
             raise RuntimeError("P2PAllReduce: a peer did not arrive within the timeout")
 
 
-def from_env(rank: int, world: int, device: torch.device, store=None) -> Optional[P2PAllReduce]:
-    """The P2P accelerator NativeComm uses when ``MLAPI_P2P_BYTES`` > 0 (and world > 1)."""
+def from_env(rank: int, world: int, device: torch.device, store=None, generation: int = 0) -> Optional[P2PAllReduce]:
+    """The P2P accelerator NativeComm uses when ``MLAPI_P2P_BYTES`` > 0 (and world > 1). The IPC
+    handles are published under ``generation`` (the communicator's), so a communicator rebuilt after
+    an abort never opens the previous generation's (freed) buffers."""
     import os
 
     n = int(os.environ.get("MLAPI_P2P_BYTES", "0"))
     if n <= 0 or world <= 1:
         return None
-    return P2PAllReduce(rank, world, device, store=store, max_bytes=n)
+    return P2PAllReduce(rank, world, device, store=store, max_bytes=n, generation=generation)
 
 
 class P2PComm:
@@ -125,6 +127,9 @@ class P2PComm:
     def wait(self, timeout_ms: Optional[int] = None) -> None:
         if self.p2p is not None:
             self.p2p.check()
+
+    def nranks(self) -> int:
+        return self.world
 
     def abort(self) -> None:
         self.aborted = True

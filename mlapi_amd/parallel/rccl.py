@@ -71,10 +71,19 @@ class NativeComm:
         uid = (exchange_unique_id(store, rank, self._C.RcclComm.unique_id, generation) if world > 1
                else self._C.RcclComm.unique_id())
         self.comm = self._C.RcclComm(uid, rank, world, device.index)
-        # small sum all-reduces through the one-shot P2P kernel when MLAPI_P2P_BYTES > 0 (parallel/p2p.py)
+        n = self.comm.comm_count()
+        if n != world:  # RCCL's own view of the job must match the launcher's
+            raise RuntimeError(f"rank {rank}: ncclCommCount reports {n} ranks, expected {world}")
+        # small sum all-reduces through the one-shot P2P kernel when MLAPI_P2P_BYTES > 0 (parallel/p2p.py);
+        # its IPC handles are versioned by the same generation as the RCCL unique id
         from mlapi_amd.parallel.p2p import from_env
 
-        self.p2p = from_env(rank, world, device, store=store)
+        self.generation = generation
+        self.p2p = from_env(rank, world, device, store=store, generation=generation)
+
+    def nranks(self) -> int:
+        """Ranks in the RCCL communicator as RCCL reports them (ncclCommCount)."""
+        return int(self.comm.comm_count())
 
     @staticmethod
     def _stream() -> int:
@@ -114,10 +123,20 @@ class NativeComm:
     def barrier(self) -> None:
         if not self.comm.barrier(self._stream(), self.timeout_ms):
             raise RuntimeError(f"rank {self.rank}: RCCL barrier timed out or failed; communicator aborted")
+        self.check_p2p()
 
     def wait(self, timeout_ms: Optional[int] = None) -> None:
         if not self.comm.wait(self._stream(), self.timeout_ms if timeout_ms is None else timeout_ms):
             raise RuntimeError(f"rank {self.rank}: RCCL collective timed out or failed; communicator aborted")
+        self.check_p2p()
+
+    def check_p2p(self) -> None:
+        """A P2P all-reduce whose peer never arrived leaves only the local gradient in the buffer
+        (the kernel records a sticky timeout and exits): surface it like an RCCL timeout, and abort
+        the communicator so no later collective runs on diverged replicas."""
+        if self.p2p is not None and self.p2p.status() != 0:
+            self.abort()
+            raise RuntimeError(f"rank {self.rank}: P2P all-reduce timed out waiting for a peer; communicator aborted")
 
     def abort(self) -> None:
         self.comm.abort()
@@ -174,6 +193,9 @@ class FakeComm:
 
     def wait(self, timeout_ms: Optional[int] = None) -> None:
         return None
+
+    def nranks(self) -> int:
+        return self.world if self.group is None else self._dist.get_world_size(self.group)
 
     def abort(self) -> None:
         self.aborted = True

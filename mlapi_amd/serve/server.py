@@ -45,6 +45,9 @@ class NativeServer:
         sc.io_spin_lowload_us = int(config.io_spin_lowload_us)
         sc.io_spin_max_conns = int(config.io_spin_max_conns)
         sc.access_log_fd = int(access_log_fd)
+        sc.dispatch = str(config.dispatch)
+        sc.dispatch_group = str(config.dispatch_group)
+        sc.dispatch_rank = int(os.environ.get("RANK", "0"))
         hd = str(config.health_dispatch).lower()
         sc.health_dispatch = hd == "on" or (hd == "auto" and int(os.environ.get("WORLD_SIZE", "1")) > 1)
         self.http = c.HttpServer(self.runtime.handle.engine, sc)

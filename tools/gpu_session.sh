@@ -14,6 +14,7 @@
 #   serve_compl   serve with COMPLS completer threads (default "1 2"), interleaved x2
 #   serve_pin     serve with the rank pinned to physical cores (server / load generator apart) vs unpinned, x2
 #   serve_spin    serve with busy-polling IO threads / spinning batcher+completer (SPINS="0 50"), interleaved x2
+#   selfl         bench.py --gpus 2 self-launched (p2p on one device) + the refusal without p2p
 #   kbench        gemv / gemm / train / train_softmax benches
 #   prof          rocprofv3 --kernel-trace --stats of every bench mode (incl. serve and serve_wide)
 #   pmc_gemm      hardware counters of the gemm bench (tools/pmc_profile.sh)
@@ -88,6 +89,11 @@ for s in $steps; do
           MLAPI_SPIN_US=$sp MLAPI_IO_SPIN_US=$sp run "serve_spin${sp}_r$r" 300 python -u bench.py --steps 60 --warmup 5
         done
       done ;;
+    selfl)  # bench.py --gpus N self-launch on the 1-GPU box: p2p shares the device; plain RCCL must refuse
+      MLAPI_COMM=p2p run bench_selflaunch_p2p_n2 300 python -u bench.py --gpus 2 --steps 20 --warmup 3
+      MLAPI_COMM=p2p run bench_selflaunch_p2p_train_n2 300 python -u bench.py --gpus 2 --mode train --steps 50 --warmup 5
+      timeout -k 10 120 python -u bench.py --gpus 2 --steps 3 --warmup 1 > "$O/bench_selflaunch_rccl_n2_refused.log" 2>&1
+      rc=$?; echo "rccl n2 on 1 GPU: rc=$rc (expected 2)"; [ $rc -eq 2 ] || stop selfl_refuse $rc "$O/bench_selflaunch_rccl_n2_refused.log" ;;
     kbench)
       for m in gemv gemm train train_softmax; do run "bench_$m" 300 python -u bench.py --mode $m --steps 100 --warmup 10; done ;;
     prof)
