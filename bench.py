@@ -342,7 +342,9 @@ def bench_train(args, info):
     run(args.warmup)
     elapsed, _ = _timed(info, lambda: run(args.steps))
     value = info.world * args.train_batch * args.steps / elapsed
-    return ("train_samples_per_sec", value, "samples/s", elapsed, {"final_loss": tr.last_loss()},
+    return ("train_samples_per_sec", value, "samples/s", elapsed,
+            {"final_loss": tr.last_loss(), "dp_exchange": tr.dp_exchange,
+             "launches_per_step": 2 if tr.dp_exchange in ("fused-p2p", "local") else 3},
             {"model": "binary LogisticRegression F=256 (mini-batch SGD)", "global_batch": args.train_batch * info.world,
              "seq_len": 1, "features": F, "parallelism": f"dp{info.world}"})
 
@@ -368,7 +370,8 @@ def bench_train_softmax(args, info):
     value = info.world * B * args.steps / elapsed
     flops = 3 * 2 * B * K * tr.F_aug * info.world * args.steps / elapsed  # 2 logits passes + dW
     return ("train_softmax_samples_per_sec", value, "samples/s", elapsed,
-            {"final_loss": tr.last_loss(), "tflops_incl_recompute": flops / 1e12},
+            {"final_loss": tr.last_loss(), "tflops_incl_recompute": flops / 1e12, "dp_exchange": tr.dp_exchange,
+             "launches_per_step": 3 if tr.dp_exchange in ("fused-p2p", "local") else 4},
             {"model": f"{K}-class softmax LogisticRegression F={F} (mini-batch SGD)", "global_batch": B * info.world,
              "seq_len": 1, "features": F, "classes": K, "parallelism": f"dp{info.world}"})
 

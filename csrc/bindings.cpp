@@ -221,14 +221,15 @@ PYBIND11_MODULE(_C, m) {
   m.def(
       "train_binary_step",
       [](int dt, uintptr_t X, uintptr_t y, uintptr_t params, uintptr_t mom, int64_t B, int F, uintptr_t grad_out,
-         uintptr_t ws, size_t ws_bytes, float lr, float inv_n, float l2, float momentum, uintptr_t stream) {
+         uintptr_t ws, size_t ws_bytes, float lr, float inv_n, float l2, float momentum, uintptr_t stream,
+         P2PAllReduce* p2p, int timeout_ms) {
         launch_train_binary_step(dt, ptr<void>(X), ptr<float>(y), ptr<float>(params), ptr<float>(mom), B, F,
                                  ptr<float>(grad_out), ptr<void>(ws), ws_bytes, lr, inv_n, l2, momentum,
-                                 stream_of(stream));
+                                 stream_of(stream), p2p, timeout_ms);
       },
       py::arg("dt"), py::arg("X"), py::arg("y"), py::arg("params"), py::arg("mom"), py::arg("B"), py::arg("F"),
       py::arg("grad_out"), py::arg("ws"), py::arg("ws_bytes"), py::arg("lr"), py::arg("inv_n"), py::arg("l2"),
-      py::arg("momentum"), py::arg("stream") = 0);
+      py::arg("momentum"), py::arg("stream") = 0, py::arg("p2p") = nullptr, py::arg("timeout_ms") = 60000);
   m.def("train_small_workspace", &train_small_workspace);
   m.def(
       "train_small_grad",
@@ -257,7 +258,7 @@ PYBIND11_MODULE(_C, m) {
       [](uintptr_t X_aug, int64_t ldx, uintptr_t W, uintptr_t b, uintptr_t y, int64_t B, int F, int K, int kind,
          uintptr_t dW_out, uintptr_t stats_out, uintptr_t ws, size_t ws_bytes, uintptr_t stream, uintptr_t params,
          uintptr_t mom, uintptr_t shadow_w, uintptr_t shadow_b, int pen_cols, float lr, float inv_n, float l2,
-         float momentum) {
+         float momentum, P2PAllReduce* p2p, int timeout_ms) {
         Sgd2D u;
         u.params = ptr<float>(params);
         u.mom = ptr<float>(mom);
@@ -271,13 +272,13 @@ PYBIND11_MODULE(_C, m) {
         u.momentum = momentum;
         launch_softmax_grad_dw(ptr<void>(X_aug), ldx, ptr<void>(W), ptr<float>(b), ptr<int32_t>(y), B, F, K, kind,
                                ptr<float>(dW_out), ptr<float>(stats_out), ptr<void>(ws), ws_bytes, stream_of(stream),
-                               params != 0 ? &u : nullptr);
+                               params != 0 ? &u : nullptr, p2p, timeout_ms);
       },
       py::arg("X_aug"), py::arg("ldx"), py::arg("W"), py::arg("b"), py::arg("y"), py::arg("B"), py::arg("F"),
       py::arg("K"), py::arg("kind"), py::arg("dW_out"), py::arg("stats_out"), py::arg("ws"), py::arg("ws_bytes"),
       py::arg("stream") = 0, py::arg("params") = 0, py::arg("mom") = 0, py::arg("shadow_w") = 0,
       py::arg("shadow_b") = 0, py::arg("pen_cols") = 0, py::arg("lr") = 0.f, py::arg("inv_n") = 0.f,
-      py::arg("l2") = 0.f, py::arg("momentum") = 0.f);
+      py::arg("l2") = 0.f, py::arg("momentum") = 0.f, py::arg("p2p") = nullptr, py::arg("timeout_ms") = 60000);
   m.def(
       "sgd_update_2d",
       [](uintptr_t params, uintptr_t grad, uintptr_t mom, int64_t rows, int cols, int pen_cols, float lr,

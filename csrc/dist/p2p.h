@@ -31,9 +31,28 @@
 
 namespace mlapi {
 
+// Kernel-side view of one fused exchange (p2p_device.h): gradient-reduction kernels store their
+// local slice into `mine`, publish it per BLOCK, wait for the same block of every rank and sum the
+// ranks' slices in rank order - the all-reduce happens inside the kernel that produced the
+// gradient, and the SGD update runs right after it in the same kernel (DP training, VERDICT r2
+// next 2). Block b's flag of rank r lives at bflags[b * MAX_RANKS + r] of the receiving rank.
+struct P2PBlockArgs {
+  static constexpr int MAX_RANKS = 16;
+  float* mine = nullptr;                          // this rank's data half of this epoch
+  const float* peer[MAX_RANKS] = {};              // every rank's same half (peer[rank] == mine)
+  uint32_t* peer_bflags[MAX_RANKS] = {};          // every rank's block-flag array
+  const uint32_t* my_bflags = nullptr;
+  uint32_t* status = nullptr;                     // sticky: 1 = a peer did not arrive in time
+  int rank = 0, world = 1;
+  uint32_t epoch = 0;
+  uint64_t timeout_ticks = 0;                     // wall_clock64() ticks (100 MHz)
+  uint32_t mode = 0;  // bit 0: release fence + release flag store; bit 1: acquire polling (A/B: MLAPI_P2P_MODE)
+};
+
 class P2PAllReduce {
  public:
   static constexpr int MAX_RANKS = 16;
+  static constexpr int MAX_FLAG_BLOCKS = 4096;  // blocks of a fused-exchange kernel
   P2PAllReduce(int rank, int world, int device, size_t max_bytes);
   ~P2PAllReduce();
   P2PAllReduce(const P2PAllReduce&) = delete;
@@ -50,6 +69,9 @@ class P2PAllReduce {
   void all_reduce(void* buf, size_t count, int dtype, hipStream_t stream, int timeout_ms);
   // 0 = every call so far completed; 1 = a call timed out waiting for a peer (sticky). Syncs.
   int status();
+  // One fused exchange for a kernel of `nblocks` blocks whose slices total `bytes` (advances the
+  // epoch; every rank must issue the same sequence of calls).
+  P2PBlockArgs block_exchange(size_t bytes, int nblocks, int timeout_ms);
   uint32_t epoch() const { return epoch_; }
   size_t max_bytes() const { return max_bytes_; }
 
@@ -57,13 +79,17 @@ class P2PAllReduce {
   int rank_, world_, device_;
   size_t max_bytes_;
   void* data_ = nullptr;        // 2 halves of max_bytes (uncached, IPC-exported)
-  uint32_t* flags_ = nullptr;   // MAX_RANKS epoch words (uncached, IPC-exported)
+  uint32_t* flags_ = nullptr;   // FLAG_WORDS_ALLREDUCE epoch words + block flags (uncached, IPC-exported)
   uint32_t* status_ = nullptr;  // device word
   void* peer_data_[MAX_RANKS] = {};
   uint32_t* peer_flags_[MAX_RANKS] = {};
   bool opened_[MAX_RANKS] = {};
   uint32_t epoch_ = 0;
   bool ready_ = false;
+
+ public:
+  static constexpr size_t FLAG_WORDS_ALLREDUCE = 64;  // all_reduce(): one word per source rank
+  static constexpr size_t FLAG_BYTES = (FLAG_WORDS_ALLREDUCE + (size_t)MAX_RANKS * MAX_FLAG_BLOCKS) * 4;
 };
 
 }  // namespace mlapi

@@ -1,6 +1,7 @@
 // One-shot P2P all-reduce over IPC-mapped peer buffers; protocol in p2p.h.
 #include "p2p.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -133,10 +134,10 @@ P2PAllReduce::P2PAllReduce(int rank, int world, int device, size_t max_bytes)
   MLAPI_HIP_CHECK(hipSetDevice(device));
   // Uncached: stores go to HBM, so a peer GPU reading over xGMI never sees a stale L2 line.
   MLAPI_HIP_CHECK(hipExtMallocWithFlags(&data_, 2 * max_bytes_, hipDeviceMallocUncached));
-  MLAPI_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), 256, hipDeviceMallocUncached));
+  MLAPI_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), FLAG_BYTES, hipDeviceMallocUncached));
   MLAPI_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&status_), sizeof(uint32_t)));
   MLAPI_HIP_CHECK(hipMemset(data_, 0, 2 * max_bytes_));
-  MLAPI_HIP_CHECK(hipMemset(flags_, 0, 256));
+  MLAPI_HIP_CHECK(hipMemset(flags_, 0, FLAG_BYTES));
   MLAPI_HIP_CHECK(hipMemset(status_, 0, sizeof(uint32_t)));
   MLAPI_HIP_CHECK(hipDeviceSynchronize());
   peer_data_[rank] = data_;
@@ -221,6 +222,32 @@ void P2PAllReduce::all_reduce(void* buf, size_t count, int dtype, hipStream_t st
   else
     hipLaunchKernelGGL(p2p_allreduce_bf16, dim3(blocks), dim3(THREADS), 0, stream, a);
   MLAPI_HIP_CHECK(hipGetLastError());
+}
+
+P2PBlockArgs P2PAllReduce::block_exchange(size_t bytes, int nblocks, int timeout_ms) {
+  if (!ready_) throw std::runtime_error("P2PAllReduce: open_peers() first");
+  if (bytes > max_bytes_) throw std::invalid_argument("P2PAllReduce::block_exchange: slice larger than max_bytes");
+  if (nblocks < 1 || nblocks > MAX_FLAG_BLOCKS) throw std::invalid_argument("P2PAllReduce::block_exchange: too many blocks");
+  ++epoch_;
+  const size_t half = (size_t)(epoch_ & 1u) * max_bytes_;
+  P2PBlockArgs a;
+  a.mine = reinterpret_cast<float*>(static_cast<unsigned char*>(data_) + half);
+  for (int j = 0; j < world_; ++j) {
+    a.peer[j] = reinterpret_cast<const float*>(static_cast<const unsigned char*>(peer_data_[j]) + half);
+    a.peer_bflags[j] = peer_flags_[j] + FLAG_WORDS_ALLREDUCE;
+  }
+  a.my_bflags = flags_ + FLAG_WORDS_ALLREDUCE;
+  a.status = status_;
+  a.rank = rank_;
+  a.world = world_;
+  a.epoch = epoch_;
+  a.timeout_ticks = (uint64_t)(timeout_ms > 0 ? timeout_ms : 60000) * 100000ull;
+  static const uint32_t mode = [] {
+    const char* e = getenv("MLAPI_P2P_MODE");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  a.mode = mode;
+  return a;
 }
 
 int P2PAllReduce::status() {

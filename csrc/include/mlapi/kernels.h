@@ -8,6 +8,8 @@
 
 namespace mlapi {
 
+class P2PAllReduce;  // csrc/dist/p2p.h: the rank's IPC exchange for fused DP all-reduces
+
 // Serving completion signal: instead of an event per batch (hipEventRecord + polling costs
 // ~12 us launch-to-observed on MI355X, tools/launch_probe.hip), the serving kernel itself
 // publishes `seq` into a host-coherent word once every block's results are out (system-scope
@@ -148,9 +150,12 @@ struct Sgd2D {
   int cols = 0, pen_cols = 0;
   float lr = 0.f, inv_n = 0.f, l2 = 0.f, momentum = 0.f;
 };
+// With `dp`, the final slab sum also performs the DP all-reduce in-kernel (p2p_device.h) before the
+// fused update: 3 launches per multiclass step at any world size.
 void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
                             int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,
-                            size_t ws_bytes, hipStream_t stream, const Sgd2D* update = nullptr);
+                            size_t ws_bytes, hipStream_t stream, const Sgd2D* update = nullptr,
+                            P2PAllReduce* dp = nullptr, int dp_timeout_ms = 0);
 
 // ---- train kernels (train.hip) -----------------------------------------------------------------
 // Binary logistic regression, one pass over X: accumulates grad (F w-entries, 1 bias) and stats
@@ -161,12 +166,13 @@ void train_binary_set_max_blocks(int n);  // benchmark hook: grid cap of the gra
 void launch_train_binary_grad(int dt, const void* X, const float* y, const float* w, float bias_unused,
                               const float* bptr, int64_t B, int F, float* out, void* workspace, size_t ws_bytes,
                               hipStream_t stream);
-// Single-replica fused step: gradient (as above, into grad_out) + deterministic reduce + SGD update
-// of params = [w (F) | b] in place (2 launches total). DP training uses launch_train_binary_grad,
-// an all-reduce, then launch_sgd_update.
+// Fused step: gradient (as above, into grad_out) + deterministic reduce + SGD update of params =
+// [w (F) | b] in place: 2 launches. With `dp` (the rank's P2P exchange, csrc/dist/p2p.h) the
+// data-parallel all-reduce runs inside the reduce launch (p2p_device.h): still 2 launches per step
+// at any world size, and world = 1 runs the same kernels. inv_n = 1 / global batch.
 void launch_train_binary_step(int dt, const void* X, const float* y, float* params, float* mom, int64_t B, int F,
                               float* grad_out, void* workspace, size_t ws_bytes, float lr, float inv_n, float l2,
-                              float momentum, hipStream_t stream);
+                              float momentum, hipStream_t stream, P2PAllReduce* dp = nullptr, int dp_timeout_ms = 0);
 // Small multiclass / binary (F*K <= 1024): fp64 or fp32, exact loss+grad of sklearn's objective
 // terms. out = [gW (K*F, row-major) | gb (K) | loss_sum | n_correct].
 size_t train_small_workspace(int64_t B, int F, int K);

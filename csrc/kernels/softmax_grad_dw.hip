@@ -34,6 +34,7 @@
 
 #include "mlapi/common.h"
 #include "mlapi/kernels.h"
+#include "dist/p2p_device.h"
 
 namespace mlapi {
 namespace {
@@ -534,9 +535,15 @@ softmax_grad_dw_kernel(GradDwArgs a) {
 // Slab sums in one launch: blocks 0 .. nb-1 fold the [row group][K * F_aug] dW slabs, one float4
 // column per thread over all slabs in a fixed order (coalesced 16-B loads, 4 in flight); the last
 // block folds the per-block [loss, correct] pairs with a fixed tree. Deterministic: no atomics.
+// Final slab sums (+ fused SGD update). DP: the ranks' sums are exchanged inside this kernel
+// (p2p_device.h): block b stores its local f32x4 column sums (the last block: the [loss, correct]
+// stats) into the exchange buffer, waits for block b of every rank and sums them in rank order
+// before the update. Exchange layout: [width4 f32x4 | loss | correct].
+template <bool DP>
 __global__ __launch_bounds__(256) void gdw_reduce_kernel(const f32x4_t* __restrict__ slabs, int nslabs, int width4,
                                                          f32x4_t* __restrict__ out, const float* __restrict__ stat_slabs,
-                                                         int nstat, float* __restrict__ stats_out, Sgd2D upd) {
+                                                         int nstat, float* __restrict__ stats_out, Sgd2D upd,
+                                                         P2PBlockArgs dp) {
   if (blockIdx.x == gridDim.x - 1) {
     float l = 0.f, c = 0.f;
     for (int i = threadIdx.x; i < nstat; i += 256) {
@@ -554,24 +561,45 @@ __global__ __launch_bounds__(256) void gdw_reduce_kernel(const f32x4_t* __restri
       red[(threadIdx.x >> 6) * 2 + 1] = c;
     }
     __syncthreads();
-    if (threadIdx.x < 2)
-      stats_out[threadIdx.x] = (red[threadIdx.x] + red[2 + threadIdx.x]) + (red[4 + threadIdx.x] + red[6 + threadIdx.x]);
+    float st = 0.f;
+    if (threadIdx.x < 2) st = (red[threadIdx.x] + red[2 + threadIdx.x]) + (red[4 + threadIdx.x] + red[6 + threadIdx.x]);
+    if constexpr (DP) {
+      float* xs = dp.mine + 4 * (int64_t)width4;
+      if (threadIdx.x < 2) xs[threadIdx.x] = st;
+      if (!p2p_block_sync(dp, blockIdx.x)) return;
+      if (threadIdx.x < 2) {
+        st = dp.peer[0][4 * (int64_t)width4 + threadIdx.x];
+        for (int r = 1; r < dp.world; ++r) st += dp.peer[r][4 * (int64_t)width4 + threadIdx.x];
+      }
+    }
+    if (threadIdx.x < 2) stats_out[threadIdx.x] = st;
     return;
   }
   const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= width4) return;
+  const bool active = j < width4;
   f32x4_t s = {0.f, 0.f, 0.f, 0.f};
-  int i = 0;
-  for (; i + 4 <= nslabs; i += 4) {
-    f32x4_t v[4];
+  if (active) {
+    int i = 0;
+    for (; i + 4 <= nslabs; i += 4) {
+      f32x4_t v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(slabs + (int64_t)(i + u) * width4 + j);
+      for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(slabs + (int64_t)(i + u) * width4 + j);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) s += v[u];
+      for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; i < nslabs; ++i) {
+      s += __builtin_nontemporal_load(slabs + (int64_t)i * width4 + j);
+    }
   }
-  for (; i < nslabs; ++i) {
-    s += __builtin_nontemporal_load(slabs + (int64_t)i * width4 + j);
+  if constexpr (DP) {
+    if (active) reinterpret_cast<f32x4_t*>(dp.mine)[j] = s;
+    if (!p2p_block_sync(dp, blockIdx.x)) return;  // peer missing: status recorded, no update
+    if (active) {
+      s = reinterpret_cast<const f32x4_t*>(dp.peer[0])[j];
+      for (int r = 1; r < dp.world; ++r) s += reinterpret_cast<const f32x4_t*>(dp.peer[r])[j];
+    }
   }
+  if (!active) return;
   out[j] = s;
   if (upd.params != nullptr) {  // uniform: the fused SGD update of these 4 parameters
 #pragma unroll
@@ -646,8 +674,11 @@ size_t softmax_grad_dw_workspace(int64_t B, int K, int F) {  // enough for eithe
 
 void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
                             int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,
-                            size_t ws_bytes, hipStream_t stream, const Sgd2D* update) {
+                            size_t ws_bytes, hipStream_t stream, const Sgd2D* update, P2PAllReduce* dp,
+                            int dp_timeout_ms) {
   if (B <= 0) return;
+  if (dp != nullptr && reinterpret_cast<uintptr_t>(dW_out) % 16 != 0)
+    throw std::invalid_argument("softmax_grad_dw: the fused DP exchange needs a 16-byte aligned dW_out");
   if (update != nullptr && (update->params == nullptr || update->cols != F + 8 || update->pen_cols > F))
     throw std::invalid_argument("softmax_grad_dw: fused update needs params [K, F + 8]");
   if (!softmax_grad_dw_supported(F))
@@ -713,10 +744,19 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
   MLAPI_HIP_CHECK(hipGetLastError());
   if (reinterpret_cast<uintptr_t>(dW_out) % 16 == 0) {
     const int width4 = K * (F + 8) / 4;
-    hipLaunchKernelGGL(gdw_reduce_kernel, dim3((unsigned)((width4 + 255) / 256 + 1)), dim3(256), 0, stream,
-                       reinterpret_cast<const f32x4_t*>(args.dw_slabs), L.row_groups, width4,
-                       reinterpret_cast<f32x4_t*>(dW_out), args.stat_slabs, L.row_groups * L.class_groups, stats_out,
-                       update != nullptr ? *update : Sgd2D{});
+    const int nblocks = (width4 + 255) / 256 + 1;
+    if (dp != nullptr) {
+      const P2PBlockArgs a = dp->block_exchange(((size_t)width4 * 4 + 4) * sizeof(float), nblocks, dp_timeout_ms);
+      hipLaunchKernelGGL(gdw_reduce_kernel<true>, dim3((unsigned)nblocks), dim3(256), 0, stream,
+                         reinterpret_cast<const f32x4_t*>(args.dw_slabs), L.row_groups, width4,
+                         reinterpret_cast<f32x4_t*>(dW_out), args.stat_slabs, L.row_groups * L.class_groups, stats_out,
+                         update != nullptr ? *update : Sgd2D{}, a);
+    } else {
+      hipLaunchKernelGGL(gdw_reduce_kernel<false>, dim3((unsigned)nblocks), dim3(256), 0, stream,
+                         reinterpret_cast<const f32x4_t*>(args.dw_slabs), L.row_groups, width4,
+                         reinterpret_cast<f32x4_t*>(dW_out), args.stat_slabs, L.row_groups * L.class_groups, stats_out,
+                         update != nullptr ? *update : Sgd2D{}, P2PBlockArgs{});
+    }
     MLAPI_HIP_CHECK(hipGetLastError());
   } else {
     launch_reduce_slabs_f32(args.dw_slabs, L.row_groups, K * (F + 8), dW_out, stream);

@@ -22,6 +22,7 @@
 #include "mlapi/kernels.h"
 #include "mlapi/device.h"
 #include "mlapi/rowreduce.h"
+#include "dist/p2p_device.h"
 
 namespace mlapi {
 namespace {
@@ -222,9 +223,13 @@ struct SgdArgs {
   float lr = 0.f, inv_n = 0.f, l2 = 0.f, momentum = 0.f;
 };
 
-template <typename T, bool FUSE_SGD, int RED_COLS>
+// DP: the data-parallel all-reduce happens here too (p2p_device.h): each block publishes its
+// columns' local sums to the IPC-mapped exchange buffer, waits for the same block of every rank,
+// and sums the ranks' values in rank order before the update - gradient kernel + this kernel are
+// the whole DP step (2 launches at any world size, bitwise-identical replicas).
+template <typename T, bool FUSE_SGD, int RED_COLS, bool DP>
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(const T* __restrict__ slabs, int nslabs, int width,
-                                                           T* __restrict__ out, SgdArgs sgd) {
+                                                           T* __restrict__ out, SgdArgs sgd, P2PBlockArgs dp) {
   constexpr int RED_PARTS = 256 / RED_COLS;
   __shared__ T part[RED_PARTS][RED_COLS];
   const int c = threadIdx.x % RED_COLS;
@@ -247,10 +252,23 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const T* __restrict__
   }
   part[p][c] = s;
   __syncthreads();
+  T t = T(0);
   if (p == 0 && j < width) {
-    T t = part[0][c];
+    t = part[0][c];
 #pragma unroll
     for (int q = 1; q < RED_PARTS; ++q) t += part[q][c];
+  }
+  if constexpr (DP) {
+    static_assert(sizeof(T) == sizeof(float), "fused DP exchange: f32 gradients");
+    if (p == 0 && j < width) dp.mine[j] = (float)t;
+    if (!p2p_block_sync(dp, blockIdx.x)) return;  // peer missing: status recorded, no update
+    if (p == 0 && j < width) {
+      float g = dp.peer[0][j];
+      for (int r = 1; r < dp.world; ++r) g += dp.peer[r][j];
+      t = (T)g;
+    }
+  }
+  if (p == 0 && j < width) {
     out[j] = t;
     if constexpr (FUSE_SGD) {
       if (j < sgd.n_params) {
@@ -268,24 +286,40 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const T* __restrict__
 
 template <typename T, int COLS>
 void launch_reduce_slabs_cols(const T* slabs, int nslabs, int width, T* out, hipStream_t stream,
-                              const SgdArgs* sgd) {
-  const dim3 grid((unsigned)((width + COLS - 1) / COLS));
+                              const SgdArgs* sgd, P2PAllReduce* dp, int dp_timeout_ms) {
+  const int nblocks = (width + COLS - 1) / COLS;
+  const dim3 grid((unsigned)nblocks);
+  if constexpr (sizeof(T) == sizeof(float)) {
+    if (dp != nullptr) {
+      const P2PBlockArgs a = dp->block_exchange((size_t)width * sizeof(float), nblocks, dp_timeout_ms);
+      if (sgd != nullptr)
+        hipLaunchKernelGGL((reduce_slabs_kernel<T, true, COLS, true>), grid, dim3(256), 0, stream, slabs, nslabs,
+                           width, out, *sgd, a);
+      else
+        hipLaunchKernelGGL((reduce_slabs_kernel<T, false, COLS, true>), grid, dim3(256), 0, stream, slabs, nslabs,
+                           width, out, SgdArgs{}, a);
+      MLAPI_HIP_CHECK(hipGetLastError());
+      return;
+    }
+  } else {
+    if (dp != nullptr) throw std::invalid_argument("fused DP exchange: f32 gradients only");
+  }
   if (sgd != nullptr)
-    hipLaunchKernelGGL((reduce_slabs_kernel<T, true, COLS>), grid, dim3(256), 0, stream, slabs, nslabs, width, out,
-                       *sgd);
+    hipLaunchKernelGGL((reduce_slabs_kernel<T, true, COLS, false>), grid, dim3(256), 0, stream, slabs, nslabs, width,
+                       out, *sgd, P2PBlockArgs{});
   else
-    hipLaunchKernelGGL((reduce_slabs_kernel<T, false, COLS>), grid, dim3(256), 0, stream, slabs, nslabs, width,
-                       out, SgdArgs{});
+    hipLaunchKernelGGL((reduce_slabs_kernel<T, false, COLS, false>), grid, dim3(256), 0, stream, slabs, nslabs,
+                       width, out, SgdArgs{}, P2PBlockArgs{});
   MLAPI_HIP_CHECK(hipGetLastError());
 }
 
 template <typename T>
 void launch_reduce_slabs(const T* slabs, int nslabs, int width, T* out, hipStream_t stream,
-                         const SgdArgs* sgd = nullptr) {
+                         const SgdArgs* sgd = nullptr, P2PAllReduce* dp = nullptr, int dp_timeout_ms = 0) {
   if (width <= 8)
-    launch_reduce_slabs_cols<T, 4>(slabs, nslabs, width, out, stream, sgd);
+    launch_reduce_slabs_cols<T, 4>(slabs, nslabs, width, out, stream, sgd, dp, dp_timeout_ms);
   else
-    launch_reduce_slabs_cols<T, 16>(slabs, nslabs, width, out, stream, sgd);
+    launch_reduce_slabs_cols<T, 16>(slabs, nslabs, width, out, stream, sgd, dp, dp_timeout_ms);
 }
 
 struct BinPlan {
@@ -515,7 +549,8 @@ size_t train_binary_workspace(int64_t B, int F) {
 
 namespace {
 void train_binary_impl(int dt, const void* X, const float* y, const float* w, const float* bptr, int64_t B, int F,
-                       float* out, void* workspace, size_t ws_bytes, hipStream_t stream, const SgdArgs* sgd) {
+                       float* out, void* workspace, size_t ws_bytes, hipStream_t stream, const SgdArgs* sgd,
+                       P2PAllReduce* dp = nullptr, int dp_timeout_ms = 0) {
   if (B <= 0) return;
   const int ne = dt == DT_BF16 ? 8 : 4;
   if (F % ne != 0) throw std::invalid_argument("train_binary: F must be a multiple of 16 bytes of elements");
@@ -544,7 +579,7 @@ void train_binary_impl(int dt, const void* X, const float* y, const float* w, co
 #undef MLAPI_TB_ALL
 #undef MLAPI_TB
   MLAPI_HIP_CHECK(hipGetLastError());
-  launch_reduce_slabs<float>(slabs, (int)blocks, F + 3, out, stream, sgd);
+  launch_reduce_slabs<float>(slabs, (int)blocks, F + 3, out, stream, sgd, dp, dp_timeout_ms);
 }
 }  // namespace
 
@@ -556,7 +591,7 @@ void launch_train_binary_grad(int dt, const void* X, const float* y, const float
 
 void launch_train_binary_step(int dt, const void* X, const float* y, float* params, float* mom, int64_t B, int F,
                               float* grad_out, void* workspace, size_t ws_bytes, float lr, float inv_n, float l2,
-                              float momentum, hipStream_t stream) {
+                              float momentum, hipStream_t stream, P2PAllReduce* dp, int dp_timeout_ms) {
   SgdArgs a;
   a.params = params;
   a.mom = mom;
@@ -566,7 +601,7 @@ void launch_train_binary_step(int dt, const void* X, const float* y, float* para
   a.inv_n = inv_n;
   a.l2 = l2;
   a.momentum = momentum;
-  train_binary_impl(dt, X, y, params, params + F, B, F, grad_out, workspace, ws_bytes, stream, &a);
+  train_binary_impl(dt, X, y, params, params + F, B, F, grad_out, workspace, ws_bytes, stream, &a, dp, dp_timeout_ms);
 }
 
 size_t train_small_workspace(int64_t B, int F, int K) {

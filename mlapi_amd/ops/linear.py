@@ -240,7 +240,7 @@ class SoftmaxTrainBuffers:
 
 def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y: torch.Tensor, kind: int,
                        bufs: SoftmaxTrainBuffers = None, dW_out: torch.Tensor = None,
-                       stats_out: torch.Tensor = None, update: dict = None):
+                       stats_out: torch.Tensor = None, update: dict = None, p2p=None, timeout_ms: int = 60000):
     """Sums over the batch of the multiclass objective's gradient, intercept included.
 
     X_aug: [B, Fk + 8] bf16 from :func:`augment_features`; W: [K, Fk] bf16 (Fk in 128/256/512;
@@ -250,9 +250,11 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
     softmax_grad_dw.hip, which forms G = P - Y in registers and accumulates dW_aug = G^T X_aug from
     the same LDS tile (G never reaches HBM), followed by its deterministic slab sums.
 
-    ``update`` (one replica only): the SGD step :func:`sgd_update_2d` would apply next, fused into
-    the final slab sum - keys params [K, Fk + 8] f32, lr, inv_n, l2, and optionally momentum,
-    mom_buf, shadow_w, shadow_b.
+    ``update``: the SGD step :func:`sgd_update_2d` would apply next, fused into the final slab sum -
+    keys params [K, Fk + 8] f32, lr, inv_n (1 / global batch), l2, and optionally momentum, mom_buf,
+    shadow_w, shadow_b. ``p2p`` (a :class:`mlapi_amd.parallel.p2p.P2PAllReduce`): the data-parallel
+    all-reduce of [dW_aug | loss | correct] runs inside that final slab sum too (p2p_device.h), so
+    a DP step stays 3 launches at any world size.
     """
     _check(X_aug, W, b, y)
     if X_aug.dtype != torch.bfloat16 or W.dtype != torch.bfloat16 or b.dtype != torch.float32 \
@@ -280,7 +282,8 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
                    inv_n=float(update["inv_n"]), l2=float(update.get("l2", 0.0)),
                    momentum=float(update.get("momentum", 0.0)))
     C().softmax_grad_dw(X_aug.data_ptr(), F_aug, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
-                        dW_out.data_ptr(), stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(), _stream(), **upd)
+                        dW_out.data_ptr(), stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(), _stream(), **upd,
+                        p2p=None if p2p is None else p2p.native, timeout_ms=int(timeout_ms))
     return dW_out, stats
 
 

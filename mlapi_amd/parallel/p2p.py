@@ -49,6 +49,11 @@ class P2PAllReduce:
     def max_bytes(self) -> int:
         return self._p.max_bytes
 
+    @property
+    def native(self):
+        """The C++ object the fused DP kernels take (``p2p=`` of the train launchers)."""
+        return self._p
+
     def supports(self, t: torch.Tensor, op: str = "sum") -> bool:
         return (op == "sum" and t.dtype in _DT and t.is_cuda and t.is_contiguous()
                 and t.numel() * t.element_size() <= self.max_bytes and t.data_ptr() % 16 == 0)
@@ -68,6 +73,38 @@ class P2PAllReduce:
     def check(self) -> None:
         if self.status() != 0:
             raise RuntimeError("P2PAllReduce: a peer did not arrive within the timeout")
+
+
+def dp_exchange(info, nbytes: int) -> Optional[P2PAllReduce]:
+    """The rank's exchange for fused DP training steps (gradient reduction + all-reduce + update in
+    one kernel, csrc/dist/p2p_device.h), or None when it does not apply: CPU ranks, ranks spread over
+    several hosts (IPC peers must share a host), or ``MLAPI_DP_FUSED=0``. One replica (world = 1)
+    gets one too, so the N = 1 step runs the same kernels as the N > 1 step. Collective: every rank
+    calls it with the same ``nbytes``. Reuses the communicator's P2P buffers when they are big
+    enough; otherwise a dedicated exchange is set up (its own store keys, ``dp<N>`` generation).
+    """
+    import os
+
+    if info.device is None or os.environ.get("MLAPI_DP_FUSED", "1") == "0":
+        return None
+    if info.world > 1 and getattr(info, "local_world", info.world) != info.world:
+        return None
+    comm_p2p = getattr(info.comm, "p2p", None)
+    if isinstance(comm_p2p, P2PAllReduce) and comm_p2p.max_bytes >= nbytes:
+        return comm_p2p
+    cache = info.__dict__.setdefault("_dp_exchanges", [])
+    for ex in cache:
+        if ex.max_bytes >= nbytes:
+            return ex
+    store = None
+    if info.world > 1:
+        from mlapi_amd.parallel.rccl import default_store
+
+        store = default_store()
+    ex = P2PAllReduce(info.rank, info.world, info.device, store=store, max_bytes=max(nbytes, 4096),
+                      generation=f"dp{len(cache)}")
+    cache.append(ex)
+    return ex
 
 
 def from_env(rank: int, world: int, device: torch.device, store=None, generation: int = 0) -> Optional[P2PAllReduce]:

@@ -1,13 +1,20 @@
 """Data-parallel mini-batch SGD for logistic regression (BASELINE config 5).
 
 Re-imagines the reference's offline ``LogisticRegression().fit`` (`Logistic Regression.ipynb:33-34`)
-as a DP training loop. Per step and rank:
+as a DP training loop. Per step and rank, TWO launches at any world size (one GPU per rank, ranks
+on one host - the MI355X node):
 
-  1. ``train_binary_grad`` (one HBM pass over the rank's shard: forward, sigmoid, BCE, and the
-     dW = sum g_i x_i reduction - all fused; deterministic slab reduction) writes the fused
-     buffer  [gW (F) | gb | loss_sum | n_correct];
-  2. one RCCL all-reduce of that buffer (C2; the loss/accuracy scalars C3 ride along);
-  3. ``sgd_update``: w -= lr * (g / N_global + l2 * w) (intercept unpenalized, like sklearn's L2).
+  1. the gradient kernel (one HBM pass over the rank's shard: forward, sigmoid, BCE, and the
+     dW = sum g_i x_i reduction - all fused) writes per-block slabs of
+     [gW (F) | gb | loss_sum | n_correct];
+  2. the slab-reduction kernel sums them, exchanges each block's column sums with the same block
+     of every rank through IPC-mapped buffers over xGMI (C2 + C3, csrc/dist/p2p_device.h: one
+     hop, peers summed in rank order) and applies w -= lr * (g / N_global + l2 * w) (intercept
+     unpenalized, like sklearn's L2) in the same kernel.
+
+World = 1 runs the same two kernels (the exchange with itself), so the N = 1 and N > 1 benches
+time the same code. Ranks on several hosts (or ``MLAPI_DP_FUSED=0``) use the unfused path: the
+gradient, an RCCL all-reduce of the fused buffer, then ``sgd_update``.
 
 Every rank applies the identical update to identical parameters, so replicas stay bitwise equal
 (checked by tests) without ever broadcasting parameters after initialisation.
@@ -53,6 +60,12 @@ class BinarySGDTrainer:
         self.mom = torch.zeros_like(self.params) if momentum else None
         self._ws = None
         self._C = C()
+        self._dp = None
+        if self.on_gpu:
+            from mlapi_amd.parallel.p2p import dp_exchange
+
+            self._dp = dp_exchange(self.info, (n_features + 3) * 4)
+        self.dp_timeout_ms = 60_000
         self.steps = 0
         self._stats = torch.zeros(2, dtype=torch.float64)
         self._n_seen = 0
@@ -81,8 +94,18 @@ class BinarySGDTrainer:
         self.grad[self.F + 1] = (torch.clamp(z, min=0) - z * y + torch.log1p(torch.exp(-z.abs()))).sum()
         self.grad[self.F + 2] = ((z > 0) == (y > 0.5)).sum()
 
+    @property
+    def dp_exchange(self) -> str:
+        """How this trainer's step reduces over ranks: ``fused-p2p`` (in-kernel, 2 launches),
+        ``local`` (one replica without an exchange), ``rccl`` (unfused), ``cpu``."""
+        if not self.on_gpu:
+            return "cpu"
+        if self._dp is not None:
+            return "fused-p2p"
+        return "local" if self.info.world == 1 else "rccl"
+
     def _fused_step(self, X: torch.Tensor, y: torch.Tensor) -> None:
-        # one replica: gradient + reduce + update fused into 2 launches (no all-reduce between)
+        # gradient + reduce (+ in-kernel DP exchange) + update: 2 launches at any world size
         from mlapi_amd.ops.linear import _DT, _check, _stream
 
         _check(X, y)
@@ -90,15 +113,21 @@ class BinarySGDTrainer:
         ws = self._workspace(B)
         self._C.train_binary_step(_DT[X.dtype], X.data_ptr(), y.data_ptr(), self.params.data_ptr(),
                                   0 if self.mom is None else self.mom.data_ptr(), B, self.F,
-                                  self.grad.data_ptr(), ws.data_ptr(), ws.numel(), float(self.lr), 1.0 / B,
-                                  float(self.l2), float(self.momentum), _stream())
+                                  self.grad.data_ptr(), ws.data_ptr(), ws.numel(), float(self.lr),
+                                  1.0 / (B * self.info.world), float(self.l2), float(self.momentum), _stream(),
+                                  p2p=None if self._dp is None else self._dp.native, timeout_ms=self.dp_timeout_ms)
+
+    def check(self) -> None:
+        """Raise if a fused DP exchange timed out waiting for a peer (synchronises the device)."""
+        if self._dp is not None:
+            self._dp.check()
 
     def capture(self, X: torch.Tensor, y: torch.Tensor) -> None:
         """Capture the one-replica step for (X, y) in a HIP graph; later ``step(X, y)`` calls with
         these exact tensors replay it (one host call for the whole step - small batches are
         launch-bound). Single replica only (the all-reduce stays outside graphs)."""
         if not self.on_gpu or self.info.world != 1:
-            raise RuntimeError("graph capture: single-GPU replica only")
+            raise RuntimeError("graph capture: single-GPU replica only (DP steps exchange per call)")
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         saved = (self.params.clone(), None if self.mom is None else self.mom.clone())
@@ -115,6 +144,11 @@ class BinarySGDTrainer:
 
     def step(self, X: torch.Tensor, y: torch.Tensor) -> None:
         B = X.shape[0]
+        if self.on_gpu and self._dp is not None and self.info.world > 1:
+            self._fused_step(X, y)
+            self.steps += 1
+            self._n_seen = B * self.info.world
+            return
         if self.on_gpu and self.info.world == 1:
             g = getattr(self, "_graph", None)
             if g is not None and g[1] is X and g[2] is y:
@@ -146,14 +180,17 @@ class BinarySGDTrainer:
 
     def last_loss(self) -> float:
         """Mean loss of the last step's global batch (reads back the fused buffer)."""
+        self.check()
         g = self.grad.detach().cpu()
         return float(g[self.F + 1]) / max(1, self._n_seen)
 
     def last_accuracy(self) -> float:
+        self.check()
         g = self.grad.detach().cpu()
         return float(g[self.F + 2]) / max(1, self._n_seen)
 
     def state_dict(self) -> dict:
+        self.check()
         return {"params": self.params.detach().cpu(), "mom": None if self.mom is None else self.mom.detach().cpu(),
                 "steps": self.steps}
 

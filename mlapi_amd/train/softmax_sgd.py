@@ -10,10 +10,14 @@ This module is the scale-out counterpart (BASELINE config 5 with K classes): per
      (X_aug = [X | 0.. | 1 | 0 x 7]), so dW_aug also holds the intercept gradient. The kernel
      trains at Fk = 128 / 256 / 512 features; narrower models are zero-padded to Fk (padded
      weights get zero gradients and stay 0), so no width needs a vendor GEMM;
-  2. one RCCL all-reduce of the fused buffer [dW_aug | loss_sum | n_correct] (C2 + C3);
-  3. ``sgd_update_2d``: W_aug = [W | b] -= lr * (g / N_global + l2 * W) with the intercept
-     unpenalized, writing the bf16 W and f32 b the next forward reads in the same pass. With one
-     replica (no all-reduce in between) the same arithmetic runs inside step 1's final slab sum.
+  2. the final slab sum of that kernel's partials exchanges [dW_aug | loss_sum | n_correct] with
+     every rank in-kernel (C2 + C3 over IPC-mapped buffers on xGMI, csrc/dist/p2p_device.h; each
+     block pairs with the same block of every rank, ranks summed in rank order) and applies
+     W_aug = [W | b] -= lr * (g / N_global + l2 * W) (intercept unpenalized), writing the bf16 W and
+     f32 b the next forward reads in the same pass.
+  That is 3 launches per step at any world size; world = 1 runs the same kernels. Ranks on several
+  hosts (or ``MLAPI_DP_FUSED=0``) fall back to an RCCL all-reduce of the fused buffer followed by
+  ``sgd_update_2d``.
 
 fp32 master weights; every rank applies the identical update, so replicas stay bitwise equal.
 One replica (world == 1) can capture the whole step in a HIP graph (:meth:`capture`).
@@ -73,6 +77,12 @@ class SoftmaxSGDTrainer:
         self.mom = torch.zeros_like(self.params) if momentum else None
         self._bufs = {}  # batch size -> SoftmaxTrainBuffers (a ragged last batch keeps its own)
         self._graph = None
+        self._dp = None
+        if self.on_gpu:
+            from mlapi_amd.parallel.p2p import dp_exchange
+
+            self._dp = dp_exchange(self.info, (n + 4) * 4)
+        self.dp_timeout_ms = 60_000
         self.steps = 0
         self._n_seen = 0
 
@@ -107,9 +117,23 @@ class SoftmaxSGDTrainer:
             self.shadow_b.copy_(self.params[:, self.Fk])
 
     # ---------------------------------------------------------------------------------- step
-    def _local_grad(self, Xa: torch.Tensor, y: torch.Tensor, fused_update_n: int = 0) -> None:
-        """Gradient sums into self.grad; with ``fused_update_n`` (one replica) the SGD update for
-        that global batch size runs inside the gradient's final slab sum (one launch fewer)."""
+    @property
+    def dp_exchange(self) -> str:
+        if not self.on_gpu:
+            return "cpu"
+        if self._dp is not None:
+            return "fused-p2p"
+        return "local" if self.info.world == 1 else "rccl"
+
+    def check(self) -> None:
+        """Raise if a fused DP exchange timed out waiting for a peer (synchronises the device)."""
+        if self._dp is not None:
+            self._dp.check()
+
+    def _local_grad(self, Xa: torch.Tensor, y: torch.Tensor, fused_update_n: int = 0, dp=None) -> None:
+        """Gradient sums into self.grad; with ``fused_update_n`` the SGD update for that global
+        batch size runs inside the gradient's final slab sum, after the in-kernel DP exchange when
+        ``dp`` is given (then self.grad holds the global sums)."""
         if self.on_gpu:
             from mlapi_amd.ops.linear import SoftmaxTrainBuffers, softmax_train_grad
 
@@ -121,7 +145,8 @@ class SoftmaxSGDTrainer:
                 upd = dict(params=self.params, lr=self.lr, inv_n=1.0 / fused_update_n, l2=self.l2,
                            momentum=self.momentum, mom_buf=self.mom, shadow_w=self.shadow_w, shadow_b=self.shadow_b)
             softmax_train_grad(Xa, self.shadow_w, self.shadow_b, y, self.kind, bufs=self._bufs[B], dW_out=self._dW(),
-                               stats_out=self.grad[self.K * self.F_aug:], update=upd)
+                               stats_out=self.grad[self.K * self.F_aug:], update=upd, p2p=dp,
+                               timeout_ms=self.dp_timeout_ms)
         else:
             from mlapi_amd.ops.reference import softmax_train_ref
 
@@ -148,8 +173,8 @@ class SoftmaxSGDTrainer:
         """One SGD step on this rank's shard (Xa from :meth:`prepare`, y int32 class indices)."""
         if self._graph is not None and self._graph[1] is Xa and self._graph[2] is y:
             self._graph[0].replay()
-        elif self.on_gpu and self.info.world == 1:
-            self._local_grad(Xa, y, fused_update_n=Xa.shape[0])
+        elif self.on_gpu and (self._dp is not None or self.info.world == 1):
+            self._local_grad(Xa, y, fused_update_n=Xa.shape[0] * self.info.world, dp=self._dp)
         else:
             self._local_grad(Xa, y)
             all_reduce_sum_(self.grad, self.info)
@@ -169,11 +194,11 @@ class SoftmaxSGDTrainer:
         saved = (self.params.clone(), None if self.mom is None else self.mom.clone())
         with torch.cuda.stream(s):  # warm-up: allocates the buffers
             for _ in range(2):
-                self._local_grad(Xa, y, fused_update_n=Xa.shape[0])
+                self._local_grad(Xa, y, fused_update_n=Xa.shape[0], dp=self._dp)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._local_grad(Xa, y, fused_update_n=Xa.shape[0])
+            self._local_grad(Xa, y, fused_update_n=Xa.shape[0], dp=self._dp)
         self.params.copy_(saved[0])
         self._refresh_shadow()
         if self.mom is not None:
@@ -182,9 +207,11 @@ class SoftmaxSGDTrainer:
 
     # ---------------------------------------------------------------------------------- stats
     def last_loss(self) -> float:
+        self.check()
         return float(self.grad[-2].item()) / max(1, self._n_seen)
 
     def last_accuracy(self) -> float:
+        self.check()
         return float(self.grad[-1].item()) / max(1, self._n_seen)
 
     def evaluate(self, Xa: torch.Tensor, y: torch.Tensor) -> Tuple[float, float]:
@@ -195,6 +222,7 @@ class SoftmaxSGDTrainer:
         return float(o[0]) / Xa.shape[0], float(o[1]) / Xa.shape[0]
 
     def state_dict(self) -> dict:
+        self.check()
         return {"params": self.params.detach().cpu(), "mom": None if self.mom is None else self.mom.detach().cpu(),
                 "steps": self.steps}
 

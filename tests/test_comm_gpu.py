@@ -104,13 +104,26 @@ def test_dp_sgd_on_gpu_with_p2p_allreduce(tmp_path):
 
     _torchrun(1, "dp_train_gpu.py", tmp_path)
     _torchrun(2, "dp_train_gpu.py", tmp_path)
+    _torchrun(2, "dp_train_gpu.py", tmp_path, env={"MLAPI_DP_FUSED": "0"})
     for name in ("params", "mc_params"):
         a, b = np.load(tmp_path / f"{name}_2_0.npy"), np.load(tmp_path / f"{name}_2_1.npy")
         assert np.array_equal(a, b), f"{name}: DP replicas must stay bitwise identical"
+        # the in-kernel exchange sums ranks in the same order as the all-reduce kernel: bitwise equal
+        u = np.load(tmp_path / f"{name}_2_0_unfused.npy")
+        assert np.array_equal(a, u), f"{name}: fused DP step must equal gradient + all-reduce + update bitwise"
+        assert np.array_equal(u, np.load(tmp_path / f"{name}_2_1_unfused.npy"))
         np.testing.assert_allclose(a, np.load(tmp_path / f"{name}_1_0.npy"), rtol=2e-3, atol=2e-4)
     j0, j1 = (json.loads((tmp_path / f"bcast_2_{r}.json").read_text()) for r in range(2))
     assert j0["W"] == j1["W"] and j0["classes"] == list("abcde")
     assert j0["p2p_calls"] >= 35 and j0["acc"] > 0.8
+
+
+def test_dp_fused_exchange_times_out_without_a_peer(tmp_path):
+    """Rank 1 never joins a fused DP step: rank 0's in-kernel wait gives up (status 1, no hang),
+    its update is skipped, and check() raises."""
+    _torchrun(2, "dp_fused_timeout.py", tmp_path)
+    res = json.loads((tmp_path / "timeout_0.json").read_text())
+    assert res["raised"] and res["params_unchanged"] and res["elapsed_s"] < 30
 
 
 @pytest.mark.parametrize("mode", ["serve", "serve_wide"])

@@ -12,9 +12,11 @@
 #   serve_idle    serve with the idle-engine fast path on (8 rows) / off, interleaved x2
 #   serve_abenv   serve with AB_VAR set to each of AB_VALS, interleaved x2
 #   serve_compl   serve with COMPLS completer threads (default "1 2"), interleaved x2
+#   dispatch_ab   serve with the round-robin acceptor vs SO_REUSEPORT dispatch, N=1 and N=2 (p2p), x2
 #   serve_pin     serve with the rank pinned to physical cores (server / load generator apart) vs unpinned, x2
 #   serve_spin    serve with busy-polling IO threads / spinning batcher+completer (SPINS="0 50"), interleaved x2
 #   selfl         bench.py --gpus 2 self-launched (p2p on one device) + the refusal without p2p
+#   dptrain       fused DP training: GPU comm tests, N=1 / N=2 (p2p) benches, fused vs unfused, kernel traces
 #   kbench        gemv / gemm / train / train_softmax benches
 #   prof          rocprofv3 --kernel-trace --stats of every bench mode (incl. serve and serve_wide)
 #   pmc_gemm      hardware counters of the gemm bench (tools/pmc_profile.sh)
@@ -77,6 +79,13 @@ for s in $steps; do
           MLAPI_COMPLETERS=$c run "serve_compl${c}_r$r" 300 python -u bench.py --steps 60 --warmup 5
         done
       done ;;
+    dispatch_ab)  # connection dispatch: round-robin acceptor vs SO_REUSEPORT hash, interleaved x2 (N=1 and p2p N=2)
+      for r in 1 2; do
+        for d in acceptor reuseport; do
+          run "serve_dispatch_${d}_r$r" 300 python -u bench.py --steps 60 --warmup 5 --dispatch $d
+          MLAPI_COMM=p2p run "serve_dispatch_${d}_n2_r$r" 300 python -u bench.py --gpus 2 --steps 30 --warmup 3 --dispatch $d
+        done
+      done ;;
     serve_pin)
       for r in 1 2; do
         for p in on off; do
@@ -94,6 +103,22 @@ for s in $steps; do
       MLAPI_COMM=p2p run bench_selflaunch_p2p_train_n2 300 python -u bench.py --gpus 2 --mode train --steps 50 --warmup 5
       timeout -k 10 120 python -u bench.py --gpus 2 --steps 3 --warmup 1 > "$O/bench_selflaunch_rccl_n2_refused.log" 2>&1
       rc=$?; echo "rccl n2 on 1 GPU: rc=$rc (expected 2)"; [ $rc -eq 2 ] || stop selfl_refuse $rc "$O/bench_selflaunch_rccl_n2_refused.log" ;;
+    dptrain)  # fused DP training step: GPU tests, benches at N=1 / N=2 (p2p on one device), kernel traces
+      run pytest_dp 600 python -u -m pytest tests/test_comm_gpu.py -x -v -p no:cacheprovider --timeout 240 --timeout-method thread
+      for m in train train_softmax; do
+        run "bench_${m}_n1" 300 python -u bench.py --mode $m --steps 100 --warmup 10
+        MLAPI_DP_FUSED=0 run "bench_${m}_n1_unfused" 300 python -u bench.py --mode $m --steps 100 --warmup 10
+        MLAPI_COMM=p2p run "bench_${m}_n2" 300 python -u bench.py --gpus 2 --mode $m --steps 100 --warmup 10
+        prof "${m}_n1" 300 --mode $m --steps 20 --warmup 2
+      done ;;
+    p2pmode)  # fused DP exchange protocol variants (MLAPI_P2P_MODE bits), interleaved x2, N=1 and N=2
+      for r in 1 2; do
+        for md in 0 1 2 3; do
+          MLAPI_P2P_MODE=$md run "tsm_mode${md}_r$r" 300 python -u bench.py --mode train_softmax --steps 100 --warmup 10
+          MLAPI_P2P_MODE=$md MLAPI_COMM=p2p run "tsm_mode${md}_n2_r$r" 300 python -u bench.py --gpus 2 --mode train_softmax --steps 100 --warmup 10
+        done
+        MLAPI_DP_FUSED=0 run "tsm_unfused_r$r" 300 python -u bench.py --mode train_softmax --steps 100 --warmup 10
+      done ;;
     kbench)
       for m in gemv gemm train train_softmax; do run "bench_$m" 300 python -u bench.py --mode $m --steps 100 --warmup 10; done ;;
     prof)
