@@ -312,7 +312,13 @@ def bench_gemm(args, info):
     X = torch.randn(B, F, device=info.device, generator=g).to(torch.bfloat16)
     W = (torch.randn(K, F, device=info.device, generator=g) / 16).to(torch.bfloat16)
     b = torch.randn(K, device=info.device, generator=g) * 0.1
-    op = ops.GemmSoftmax(B, K, F, info.device)
+    if args.gemm_kernel == "split" or args.gemm_dtype == "f32":
+        # class-split kernel (small serving batches; the f32 MFMA path)
+        if args.gemm_dtype == "f32":
+            X, W = X.float(), W.float()
+        op = ops.LinearSplit(B, K, info.device)
+    else:
+        op = ops.GemmSoftmax(B, K, F, info.device)
     out = (torch.empty(B, dtype=torch.int32, device=info.device), torch.empty(B, device=info.device))
     for _ in range(args.warmup):
         op(X, W, b, out=out)
@@ -321,7 +327,8 @@ def bench_gemm(args, info):
     value = info.world * B * args.steps / elapsed
     tflops = 2 * B * F * K * args.steps / elapsed / 1e12
     return ("rows_per_sec_softmax_predict", value, "rows/s", elapsed,
-            {"tflops_per_gpu": tflops, "us_per_call": elapsed / args.steps * 1e6, "launch": args.launch},
+            {"tflops_per_gpu": tflops, "us_per_call": elapsed / args.steps * 1e6, "launch": args.launch,
+             "kernel": "linear_split" if isinstance(op, ops.LinearSplit) else "gemm_softmax", "dtype": args.gemm_dtype},
             {"model": "softmax regression F=256 K=1000", "global_batch": B * info.world, "seq_len": 1,
              "features": F, "parallelism": f"dp{info.world}"})
 
@@ -418,6 +425,9 @@ def main(argv=None) -> int:
     ap.add_argument("--c1-requests", type=int, default=3000)
     ap.add_argument("--rows", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--gemm-kernel", default="auto", choices=["auto", "split"],
+                    help="gemm: auto = the tiles kernel; split = the class-split small-batch kernel")
+    ap.add_argument("--gemm-dtype", default="bf16", choices=["bf16", "f32"], help="gemm: f32 runs the split kernel")
     ap.add_argument("--launch", default="graph", choices=["graph", "eager"],
                     help="gemv/gemm: the timed K calls replayed from one captured HIP graph (GPU time) or "
                          "dispatched one by one from Python (adds host overhead per call)")

@@ -170,6 +170,18 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("X"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"), py::arg("K"), py::arg("kind"),
       py::arg("out_idx"), py::arg("out_p"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream") = 0);
+  m.def("linear_split_supported", &linear_split_supported);
+  m.def("linear_split_workspace", &linear_split_workspace);
+  m.def(
+      "linear_split",
+      [](int dt, uintptr_t X, int64_t ldx, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind,
+         uintptr_t out_idx, uintptr_t out_p, uintptr_t ws, size_t ws_bytes, uintptr_t stream) {
+        launch_linear_split(dt, ptr<void>(X), ldx, ptr<void>(W), ptr<float>(b), B, F, K, kind, ptr<int32_t>(out_idx),
+                            ptr<float>(out_p), ptr<void>(ws), ws_bytes, stream_of(stream));
+      },
+      py::arg("dt"), py::arg("X"), py::arg("ldx"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"),
+      py::arg("K"), py::arg("kind"), py::arg("out_idx"), py::arg("out_p"), py::arg("ws"), py::arg("ws_bytes"),
+      py::arg("stream") = 0);
   m.def(
       "gemm_logits",
       [](uintptr_t X, uintptr_t W, uintptr_t b, int64_t B, int F, int K, uintptr_t Z, uintptr_t stream) {

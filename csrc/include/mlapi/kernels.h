@@ -125,6 +125,16 @@ void launch_merge_rowstates(const void* parts, int nparts, int64_t B, const Shar
 void launch_logits_epilogue(const float* Z, const float* b, int64_t B, int K, int kind, int32_t* out_idx, float* out_p,
                             hipStream_t stream);
 
+// ---- linear_split.hip: class-split multiclass predict for small batches (serving: B <= 32 rows)
+// and for f32 models at any batch (v_mfma_f32_16x16x4_f32). X, W in dt (DT_BF16 or DT_F32), W row
+// stride F (a power of two: bf16 32..512, f32 16..512), b f32 [K]. Workspace:
+// linear_split_workspace(B, K) bytes, zeroed once (split-merge counters re-armed in-kernel).
+bool linear_split_supported(int dt, int F);
+size_t linear_split_workspace(int64_t B, int K);
+void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K,
+                         int kind, int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes,
+                         hipStream_t stream, RecOut ro = RecOut());
+
 // Multiclass training row stats (gemm_softmax.hip MODE 2), X_aug = [X | 0.. | 1 | 0 x 7] bf16
 // read through its row stride ldx (the first F columns); W: [K, F] bf16; b: [K] f32.
 // MODE 2 alone: rowstat_out[B] = {logsumexp (OvR: max + log sum sigmoid), argmax bits} per row.

@@ -1,0 +1,210 @@
+// Class-split multiclass predict for small serving batches and for f32 models (VERDICT r2 next 3
+// and 7): z = X W^T + b -> (first argmax, p_max) with the sklearn epilogue of `kind`.
+//
+// Why a separate kernel: served multiclass batches average a handful of rows, and the B = 1024
+// tiles kernel (gemm_softmax.hip) spends ~9.6 us on them - its 64-class LDS-DMA chunks, double
+// buffer and three dependent round trips of the split merge are built for throughput. Here:
+//  * grid = (ceil(K / 64) class blocks, ceil(B / 32) row groups); a block = 4 waves, a wave owns
+//    16 classes: its W fragments (16 classes x F) are loaded ONCE, straight to registers (no LDS
+//    staging: at <= 32 rows every W element is used by at most 2 MFMAs), together with the X
+//    fragments of its <= 32 rows - one round trip to L2 / MALL for everything;
+//  * MFMA: bf16 -> v_mfma_f32_16x16x32_bf16 (A = 16 classes, B = 16 rows, 8 k per lane);
+//    f32 -> v_mfma_f32_16x16x4_f32 with each lane's 16-byte load feeding 4 MFMAs (a consistent
+//    permutation of k for A and B: k = 16 j + 4 g + e, g = lane >> 4), accumulators start at the
+//    bias (-inf for padding classes, which every reduction maps to "absent");
+//  * epilogue in registers: a lane holds 4 classes of one row; 2 xor-shuffles merge the 4 lane
+//    groups, the 4 waves merge through 512 B of LDS in fixed order (first max wins: ties go to the
+//    lower class index, like numpy's argmax);
+//  * split merge with ONE cross-block round trip: wave 0 stores the block's row states
+//    write-through (sc1), drains them (vmcnt(0)), and takes a ticket on its row group's counter;
+//    the last arriver (agent-scope acquire) loads every split's state in fixed split order and
+//    writes (label, p_max) - or the serving completion record.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "mlapi/kernels.h"
+
+namespace mlapi {
+namespace split {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 sbf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float sf32x4_t;
+
+constexpr int CLASSES_PER_BLOCK = 64;
+constexpr int ROWS_PER_GROUP = 32;
+
+struct SplitArgs {
+  const void* X;
+  int64_t ldx;          // X row stride (elements)
+  const void* W;        // [K][F] row stride F, same dtype as X
+  const float* bias;    // [K]
+  int32_t B, K, kind, nsplit;
+  int32_t* out_idx;
+  float* out_p;
+  RecOut ro;            // serving: per-row completion records instead of out_idx / out_p
+  unsigned int* counters;  // [row groups], zero between launches (re-armed by the merging block)
+  float4* partials;        // [row groups][nsplit][32] {m, s, argmax bits, 0}
+};
+
+struct SState {
+  float m, s;
+  int bi;
+};
+
+__device__ __forceinline__ SState smerge(SState a, SState b, bool ovr) {
+  const bool take_b = (b.m > a.m) || (b.m == a.m && b.bi < a.bi);
+  SState r;
+  r.m = take_b ? b.m : a.m;
+  r.bi = take_b ? b.bi : a.bi;
+  if (ovr) {
+    r.s = a.s + b.s;
+  } else {
+    const float sa = a.m == -INFINITY ? 0.f : a.s * expf(a.m - r.m);
+    const float sb = b.m == -INFINITY ? 0.f : b.s * expf(b.m - r.m);
+    r.s = sa + sb;
+  }
+  return r;
+}
+
+__device__ __forceinline__ SState sshfl(SState a, int off) {
+  return SState{__shfl_xor(a.m, off, 64), __shfl_xor(a.s, off, 64), __shfl_xor(a.bi, off, 64)};
+}
+
+__device__ __forceinline__ float ssigmoid(float z) { return 1.f / (1.f + expf(-z)); }
+
+// T = uint16_t (bf16 bits) or float. KS: 16-byte units per lane per row (bf16: F / 32, f32: F / 16).
+// NB: 16-row tiles per wave (1 or 2).
+template <typename T, int KS, int NB, bool OVR>
+__device__ __forceinline__ void split_predict(const SplitArgs& a) {
+  constexpr bool BF = sizeof(T) == 2;
+  constexpr int F = BF ? KS * 32 : KS * 16;
+  __shared__ float4 red[4][NB * 16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int c0 = blockIdx.x * CLASSES_PER_BLOCK + wave * 16;
+  const int row0 = blockIdx.y * ROWS_PER_GROUP;
+  // ---- every load of the block up front: W fragments, X fragments, bias
+  const int ca = min(c0 + r16, a.K - 1);  // padding classes read a real row (masked by a -inf bias)
+  const uint4* wp = reinterpret_cast<const uint4*>(static_cast<const T*>(a.W) + (int64_t)ca * F) + g;
+  uint4 af[KS];
+#pragma unroll
+  for (int j = 0; j < KS; ++j) af[j] = wp[j * 4];
+  uint4 xf[NB][KS];
+#pragma unroll
+  for (int t = 0; t < NB; ++t) {
+    const int row = min(row0 + t * 16 + r16, a.B - 1);
+    const uint4* xp = reinterpret_cast<const uint4*>(static_cast<const T*>(a.X) + (int64_t)row * a.ldx) + g;
+#pragma unroll
+    for (int j = 0; j < KS; ++j) xf[t][j] = xp[j * 4];
+  }
+  sf32x4_t bias;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int c = c0 + g * 4 + r;
+    const float bv = a.bias[min(c, a.K - 1)];
+    bias[r] = c < a.K ? bv : -INFINITY;
+  }
+  // keep every load above in flight together: without this fence the scheduler sinks half of them
+  // below the first MFMAs to save registers (two dependent round trips instead of one)
+  __builtin_amdgcn_sched_barrier(0);
+  // ---- logits
+  sf32x4_t acc[NB];
+#pragma unroll
+  for (int t = 0; t < NB; ++t) acc[t] = bias;
+#pragma unroll
+  for (int j = 0; j < KS; ++j) {
+    if constexpr (BF) {
+      const sbf16x8_t av = __builtin_bit_cast(sbf16x8_t, af[j]);
+#pragma unroll
+      for (int t = 0; t < NB; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(sbf16x8_t, xf[t][j]), acc[t], 0, 0, 0);
+    } else {
+      const uint32_t aw[4] = {af[j].x, af[j].y, af[j].z, af[j].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+          const uint32_t xw[4] = {xf[t][j].x, xf[t][j].y, xf[t][j].z, xf[t][j].w};
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(aw[e]), __uint_as_float(xw[e]), acc[t], 0, 0,
+                                                        0);
+        }
+      }
+    }
+  }
+  // ---- row states: 4 classes per lane -> 16 per wave (2 shuffles) -> 64 per block (LDS)
+#pragma unroll
+  for (int t = 0; t < NB; ++t) {
+    float m = acc[t][0];
+    int br = 0;
+#pragma unroll
+    for (int r = 1; r < 4; ++r) {
+      if (acc[t][r] > m) {
+        m = acc[t][r];
+        br = r;
+      }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s += OVR ? ssigmoid(acc[t][r]) : (m == -INFINITY ? 0.f : expf(acc[t][r] - m));
+    SState S{m, s, m == -INFINITY ? 0x7fffffff : c0 + g * 4 + br};
+    S = smerge(S, sshfl(S, 16), OVR);
+    S = smerge(S, sshfl(S, 32), OVR);
+    if (g == 0) red[wave][t * 16 + r16] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  const int l = lane;  // row of the group this lane finishes
+  const int64_t row = row0 + l;
+  const bool live = l < NB * 16 && row < a.B;
+  SState S{-INFINITY, 0.f, 0x7fffffff};
+  if (l < NB * 16) {
+    const float4 v0 = red[0][l];
+    S = SState{v0.x, v0.y, __float_as_int(v0.z)};
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const float4 v = red[w][l];
+      S = smerge(S, SState{v.x, v.y, __float_as_int(v.z)}, OVR);
+    }
+  }
+  if (gridDim.x > 1) {
+    // one cross-block round trip: write-through partials, drained, then the row group's ticket
+    typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+    typedef __attribute__((address_space(1))) unsigned int gu32_t;
+    float4* part = a.partials + ((int64_t)blockIdx.y * a.nsplit) * ROWS_PER_GROUP;
+    if (live) {
+      float4* dst = part + (int64_t)blockIdx.x * ROWS_PER_GROUP + l;
+      const unsigned long long ms =
+          (unsigned long long)__float_as_uint(S.m) | ((unsigned long long)__float_as_uint(S.s) << 32);
+      __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S.bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned ticket = 0;
+    if (l == 0)
+      ticket = __hip_atomic_fetch_add(&a.counters[blockIdx.y], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __shfl(ticket, 0, 64);
+    if (ticket != gridDim.x - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (l == 0) __hip_atomic_store(&a.counters[blockIdx.y], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!live) return;
+    // fixed split order (deterministic); 16 states in flight per batch of loads
+    const float4* src = part + l;
+    float4 v[16];
+    S = SState{-INFINITY, 0.f, 0x7fffffff};
+    for (int sp0 = 0; sp0 < a.nsplit; sp0 += 16) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = src[(int64_t)min(sp0 + u, a.nsplit - 1) * ROWS_PER_GROUP];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (sp0 + u < a.nsplit) S = smerge(S, SState{v[u].x, v[u].y, __float_as_int(v[u].z)}, OVR);
+    }
+  }
+  if (!live) return;
+  const float p = OVR ? ssigmoid(S.m) / S.s : 1.f / S.s;
+  put_result(a.out_idx, a.out_p, a.ro, row, S.bi, p);
+}
+
+}  // namespace split
+}  // namespace mlapi

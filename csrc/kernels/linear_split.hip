@@ -1,0 +1,107 @@
+// Host launchers of the class-split multiclass predict (linear_split.h).
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+
+#include "linear_split.h"
+#include "mlapi/common.h"
+#include "mlapi/kernels.h"
+
+namespace mlapi {
+namespace {
+
+constexpr size_t COUNTER_REGION = 256;  // 64 row groups of counters (B <= 2048)
+
+template <typename T, int KS, int NB, bool OVR>
+__global__ __launch_bounds__(256) void linear_split_kernel(split::SplitArgs a) {
+  split::split_predict<T, KS, NB, OVR>(a);
+}
+
+template <typename T, int KS>
+void launch_ks(const split::SplitArgs& a, dim3 grid, bool nb2, bool ovr, hipStream_t stream) {
+  if (nb2) {
+    if (ovr)
+      hipLaunchKernelGGL((linear_split_kernel<T, KS, 2, true>), grid, dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((linear_split_kernel<T, KS, 2, false>), grid, dim3(256), 0, stream, a);
+  } else {
+    if (ovr)
+      hipLaunchKernelGGL((linear_split_kernel<T, KS, 1, true>), grid, dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((linear_split_kernel<T, KS, 1, false>), grid, dim3(256), 0, stream, a);
+  }
+}
+
+int row_groups(int64_t B) { return (int)((B + split::ROWS_PER_GROUP - 1) / split::ROWS_PER_GROUP); }
+int nsplits(int K) { return (K + split::CLASSES_PER_BLOCK - 1) / split::CLASSES_PER_BLOCK; }
+
+}  // namespace
+
+bool linear_split_supported(int dt, int F) {
+  const bool pow2 = F > 0 && (F & (F - 1)) == 0;
+  if (dt == DT_BF16) return pow2 && F >= 32 && F <= 512;
+  if (dt == DT_F32) return pow2 && F >= 16 && F <= 512;
+  return false;
+}
+
+size_t linear_split_workspace(int64_t B, int K) {
+  const int rg = row_groups(B);
+  return COUNTER_REGION + (size_t)rg * nsplits(K) * split::ROWS_PER_GROUP * sizeof(float4);
+}
+
+void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K,
+                         int kind, int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes,
+                         hipStream_t stream, RecOut ro) {
+  if (B <= 0) return;
+  if (!linear_split_supported(dt, F))
+    throw std::invalid_argument("linear_split: bf16 F in 32..512 or f32 F in 16..512, a power of two");
+  if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
+    throw std::invalid_argument("linear_split: multiclass kinds only");
+  if (ldx < F || (ldx * (dt == DT_BF16 ? 2 : 4)) % 16 != 0)
+    throw std::invalid_argument("linear_split: ldx must be >= F and rows 16-byte aligned");
+  if (reinterpret_cast<uintptr_t>(X) % 16 != 0 || reinterpret_cast<uintptr_t>(W) % 16 != 0)
+    throw std::invalid_argument("linear_split: X and W must be 16-byte aligned");
+  const int rg = row_groups(B), ns = nsplits(K);
+  if (rg > (int)(COUNTER_REGION / sizeof(unsigned int)))
+    throw std::invalid_argument("linear_split: B too large (<= 2048 rows per launch)");
+  if (ns > 1 && ws_bytes < linear_split_workspace(B, K))
+    throw std::invalid_argument("linear_split: workspace too small (zero it once)");
+  split::SplitArgs a{};
+  a.X = X;
+  a.ldx = ldx;
+  a.W = W;
+  a.bias = b;
+  a.B = (int32_t)B;
+  a.K = K;
+  a.kind = kind;
+  a.nsplit = ns;
+  a.out_idx = out_idx;
+  a.out_p = out_p;
+  a.ro = ro;
+  a.counters = static_cast<unsigned int*>(workspace);
+  a.partials = reinterpret_cast<float4*>(static_cast<unsigned char*>(workspace) + COUNTER_REGION);
+  const dim3 grid((unsigned)ns, (unsigned)rg);
+  const bool nb2 = B > 16;
+  const bool ovr = kind == KIND_OVR;
+  if (dt == DT_BF16) {
+    switch (F) {
+      case 32: launch_ks<uint16_t, 1>(a, grid, nb2, ovr, stream); break;
+      case 64: launch_ks<uint16_t, 2>(a, grid, nb2, ovr, stream); break;
+      case 128: launch_ks<uint16_t, 4>(a, grid, nb2, ovr, stream); break;
+      case 256: launch_ks<uint16_t, 8>(a, grid, nb2, ovr, stream); break;
+      default: launch_ks<uint16_t, 16>(a, grid, nb2, ovr, stream); break;
+    }
+  } else {
+    switch (F) {
+      case 16: launch_ks<float, 1>(a, grid, nb2, ovr, stream); break;
+      case 32: launch_ks<float, 2>(a, grid, nb2, ovr, stream); break;
+      case 64: launch_ks<float, 4>(a, grid, nb2, ovr, stream); break;
+      case 128: launch_ks<float, 8>(a, grid, nb2, ovr, stream); break;
+      case 256: launch_ks<float, 16>(a, grid, nb2, ovr, stream); break;
+      default: launch_ks<float, 32>(a, grid, nb2, ovr, stream); break;
+    }
+  }
+  MLAPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace mlapi

@@ -28,6 +28,7 @@ SOURCES = [
     "kernels/linear_small.hip",
     "kernels/gemv_binary.hip",
     "kernels/gemm_softmax.hip",
+    "kernels/linear_split.hip",
     "kernels/train.hip",
     "kernels/pack.hip",
     "kernels/shard.hip",

@@ -116,6 +116,43 @@ class GemmSoftmax:
         return idx, p
 
 
+class LinearSplit:
+    """Class-split multiclass predict (csrc/kernels/linear_split.h): small batches (one launch,
+    one cross-block merge round trip) and f32 models via v_mfma_f32_16x16x4_f32. X, W share dtype
+    bf16 or f32; F a power of two (bf16 32..512, f32 16..512; narrower models are zero-padded)."""
+
+    def __init__(self, max_batch: int, n_classes: int, device):
+        self.max_batch, self.K = max_batch, n_classes
+        self.ws = torch.zeros(C().linear_split_workspace(max_batch, n_classes), dtype=torch.uint8, device=device)
+
+    def __call__(self, X, W, b, kind: int = Kind.MULTINOMIAL, out=None):
+        _check(X, W, b)
+        if X.dtype not in (torch.bfloat16, torch.float32) or W.dtype != X.dtype or b.dtype != torch.float32:
+            raise TypeError("linear_split: X, W bf16 or f32 (same dtype), b f32")
+        B, F = X.shape
+        K = W.shape[0]
+        if W.shape[1] != F or b.numel() != K or K != self.K:
+            raise ValueError("linear_split: W must be [K, F] and b [K]")
+        if not C().linear_split_supported(_DT[X.dtype], F):
+            Fp = max(16 if X.dtype == torch.float32 else 32, 1 << (F - 1).bit_length())
+            X = torch.nn.functional.pad(X, (0, Fp - F)).contiguous()
+            W = torch.nn.functional.pad(W, (0, Fp - F)).contiguous()
+            F = Fp
+        need = C().linear_split_workspace(B, K)
+        if need > self.ws.numel():
+            self.ws = torch.zeros(need, dtype=torch.uint8, device=X.device)
+        if out is None:
+            out = (torch.empty(B, dtype=torch.int32, device=X.device), torch.empty(B, dtype=torch.float32, device=X.device))
+        idx, p = out
+        C().linear_split(_DT[X.dtype], X.data_ptr(), F, W.data_ptr(), b.data_ptr(), B, F, K, int(kind), idx.data_ptr(),
+                         p.data_ptr(), self.ws.data_ptr(), self.ws.numel(), _stream())
+        return idx, p
+
+
+def linear_split(X, W, b, kind: int = Kind.MULTINOMIAL):
+    return LinearSplit(X.shape[0], W.shape[0], X.device)(X, W, b, kind)
+
+
 def gemm_softmax(X, W, b, kind: int = Kind.MULTINOMIAL):
     return GemmSoftmax(X.shape[0], W.shape[0], X.shape[1], X.device)(X, W, b, kind)
 

@@ -379,3 +379,66 @@ def test_softmax_sgd_gpu_trains_and_graph_replay_is_exact():
     for _ in range(30):
         cpu.step(Xc[:8192], y[:8192].cpu())
     np.testing.assert_allclose(eager.params.cpu().numpy(), cpu.params.numpy(), atol=0.05, rtol=0.05)
+
+
+# ---- class-split multiclass predict (linear_split.h): small serving batches, f32 MFMA path
+@pytest.mark.parametrize("kind", [Kind.MULTINOMIAL, Kind.OVR])
+@pytest.mark.parametrize("K", [3, 17, 64, 65, 1000, 4100])
+@pytest.mark.parametrize("B", [1, 5, 8, 16, 17, 32, 33, 200])
+def test_linear_split_bf16(B, K, kind):
+    """bf16 operands vs the fp64 oracle of the same rounded values, B = 1..32 (one row group) and
+    beyond (several row groups, one merge counter each); labels compared where the top-2 gap is clear."""
+    F = 256
+    X = _rand((B, F), torch.bfloat16, 31)
+    W = _rand((K, F), torch.bfloat16, 32, scale=1 / np.sqrt(F))
+    b = _rand((K,), torch.float32, 33, scale=0.1)
+    op = ops.LinearSplit(B, K, DEV)
+    for _ in range(2):  # the second launch checks the in-kernel counter re-arm
+        idx, p = op(X, W, b, kind)
+        Z = ref.logits_ref(X, W, b, dtype=torch.float64)
+        ridx, rp = ref.predict_ref(X, W, b, kind)
+        top2 = torch.topk(Z, min(2, K), dim=1).values
+        clear = (top2[:, 0] - top2[:, -1]) > 1e-3
+        torch.cuda.synchronize()
+        assert torch.equal(idx[clear].cpu(), ridx[clear].cpu())
+        torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("kind", [Kind.MULTINOMIAL, Kind.OVR])
+@pytest.mark.parametrize("B,F,K", [(1, 256, 1000), (8, 256, 1000), (32, 256, 1000), (256, 256, 1000), (7, 16, 3),
+                                   (64, 100, 40), (19, 512, 129)])
+def test_linear_split_f32_matches_fp64(B, F, K, kind):
+    """f32 MFMA path (v_mfma_f32_16x16x4_f32) within rel 1e-6 of the fp64 oracle on the same f32
+    operands (F=256, K=1000 served in f32)."""
+    X = _rand((B, F), torch.float32, 41)
+    W = _rand((K, F), torch.float32, 42, scale=1 / np.sqrt(F))
+    b = _rand((K,), torch.float32, 43, scale=0.1)
+    idx, p = ops.linear_split(X, W, b, kind)
+    Z = ref.logits_ref(X, W, b, dtype=torch.float64)
+    ridx, rp = ref.predict_ref(X, W, b, kind)
+    top2 = torch.topk(Z, min(2, K), dim=1).values
+    clear = (top2[:, 0] - top2[:, -1]) > 1e-5
+    torch.cuda.synchronize()
+    assert torch.equal(idx[clear].cpu(), ridx[clear].cpu())
+    torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_linear_split_ties_and_asymmetric(dtype):
+    """Three-way tie -> the first max; an asymmetric operand catches a transposed C layout."""
+    B, F, K = 12, 64, 130
+    X = torch.ones(B, F, device=DEV, dtype=dtype)
+    W = torch.zeros(K, F, device=DEV, dtype=dtype)
+    b = torch.zeros(K, device=DEV)
+    b[[5, 77, 129]] = 1.0
+    idx, p = ops.linear_split(X, W, b)
+    assert (idx == 5).all()
+    torch.testing.assert_close(p, torch.full_like(p, float(torch.softmax(b.double(), 0).max())), rtol=1e-5, atol=1e-6)
+    # row i selects feature i: logits z[i, k] = W[k, i] + b[k] with W[k, i] distinct per (k, i)
+    X = torch.zeros(B, F, device=DEV, dtype=dtype)
+    X[torch.arange(B), torch.arange(B)] = 1
+    W = ((torch.arange(K * F, device=DEV, dtype=torch.float32).reshape(K, F) * 7) % 61 / 8.0).to(dtype)
+    idx, p = ops.linear_split(X, W, b)
+    ridx, rp = ref.predict_ref(X, W, b, Kind.MULTINOMIAL)
+    assert torch.equal(idx.cpu(), ridx.cpu())
+    torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=1e-5, atol=1e-6)

@@ -119,6 +119,16 @@ for s in $steps; do
         done
         MLAPI_DP_FUSED=0 run "tsm_unfused_r$r" 300 python -u bench.py --mode train_softmax --steps 100 --warmup 10
       done ;;
+    split)  # class-split multiclass kernel: GPU tests, graph-replay timings vs the tiles kernel, rocprofv3
+      run pytest_split 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "linear_split or gemm"
+      for B in 1 8 32; do
+        run "gemm_tiles_b$B" 120 python -u bench.py --mode gemm --batch $B --steps 2000 --warmup 50
+        run "gemm_split_b$B" 120 python -u bench.py --mode gemm --batch $B --steps 2000 --warmup 50 --gemm-kernel split
+      done
+      run gemm_split_f32_b256 120 python -u bench.py --mode gemm --batch 256 --steps 1000 --warmup 50 --gemm-dtype f32
+      run gemm_split_f32_b1024 120 python -u bench.py --mode gemm --batch 1024 --steps 1000 --warmup 50 --gemm-dtype f32
+      prof gemm_split_b8 120 --mode gemm --batch 8 --steps 200 --warmup 5 --gemm-kernel split --launch eager
+      prof gemm_tiles_b8 120 --mode gemm --batch 8 --steps 200 --warmup 5 --launch eager ;;
     kbench)
       for m in gemv gemm train train_softmax; do run "bench_$m" 300 python -u bench.py --mode $m --steps 100 --warmup 10; done ;;
     prof)
