@@ -322,6 +322,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("delay_us", &EngineConfig::delay_us)
       .def_readwrite("spin_us", &EngineConfig::spin_us)
       .def_readwrite("wide_dtype", &EngineConfig::wide_dtype)
+      .def_readwrite("split_max_rows", &EngineConfig::split_max_rows)
       .def_readwrite("inline_args", &EngineConfig::inline_args)
       .def_readwrite("idle_inline_rows", &EngineConfig::idle_inline_rows)
       .def_readwrite("completers", &EngineConfig::completers)

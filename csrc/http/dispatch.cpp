@@ -389,7 +389,7 @@ void ConnDispatcher::member_loop() {
       if (send(chan_fd_, &h, 1, MSG_NOSIGNAL | MSG_DONTWAIT) == 1) sent = h;
     }
     pollfd pf[2] = {{wake_fd_, POLLIN, 0}, {chan_fd_, POLLIN, 0}};
-    const int n = poll(pf, 2, 50);
+    const int n = poll(pf, 2, 20);  // health changes reach the leader within one period
     if (n < 0 && errno != EINTR) break;
     if (n <= 0) continue;
     if (pf[0].revents) return;

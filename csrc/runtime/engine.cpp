@@ -27,6 +27,7 @@ Model::~Model() {
     if (dW) (void)hipFree(dW);
     if (db) (void)hipFree(db);
     if (ws) (void)hipFree(ws);
+    if (ws_split) (void)hipFree(ws_split);
     (void)hipSetDevice(prev);
   }
 }
@@ -211,6 +212,11 @@ uint64_t Engine::load_model(int kind, int F, int K, const double* W, const doubl
     m->path = PATH_GEMM;
     m->xdt = DT_BF16;
     m->ldx = (int)padded_features(F);
+  } else if (!binary && K >= 2 && cfg_.wide_dtype == DT_F32 && F <= 512) {
+    // f32 MFMA class-split kernel at a power-of-two width (v_mfma_f32_16x16x4_f32)
+    m->path = PATH_GEMM;
+    m->xdt = DT_F32;
+    m->ldx = (int)padded_features(F);
   } else {
     m->path = PATH_GENERIC;
     m->xdt = cfg_.wide_dtype == DT_F64 ? DT_F64 : DT_F32;
@@ -249,11 +255,17 @@ uint64_t Engine::load_model(int kind, int F, int K, const double* W, const doubl
     }
     if (m->path == PATH_GEMM) {
       // the split plan depends on the batch size: size for the largest any batch can need
-      for (int64_t B = 1; B <= cfg_.max_batch; ++B)
-        m->ws_bytes = std::max(m->ws_bytes, gemm_softmax_workspace(B, K, m->ldx));
+      if (m->xdt == DT_BF16)
+        for (int64_t B = 1; B <= cfg_.max_batch; ++B)
+          m->ws_bytes = std::max(m->ws_bytes, gemm_softmax_workspace(B, K, m->ldx));
       if (m->ws_bytes) {
         MLAPI_HIP_CHECK(hipMalloc(&m->ws, m->ws_bytes));
         MLAPI_HIP_CHECK(hipMemset(m->ws, 0, m->ws_bytes));
+      }
+      if (linear_split_supported(m->xdt, m->ldx)) {
+        m->ws_split_bytes = linear_split_workspace(cfg_.max_batch, K);
+        MLAPI_HIP_CHECK(hipMalloc(&m->ws_split, m->ws_split_bytes));
+        MLAPI_HIP_CHECK(hipMemset(m->ws_split, 0, m->ws_split_bytes));
       }
     }
     MLAPI_HIP_CHECK(hipDeviceSynchronize());
@@ -537,6 +549,10 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     }
     if (m.path == PATH_GEMV)
       launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_, ro);
+    else if (m.ws_split != nullptr && (m.xdt == DT_F32 || n <= cfg_.split_max_rows))
+      // small batches (and every f32 batch): the class-split kernel, one cross-block merge round trip
+      launch_linear_split(m.xdt, X, m.ldx, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
+                          static_cast<float*>(s.dp), m.ws_split, m.ws_split_bytes, stream_, ro);
     else
       launch_gemm_softmax(X, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
                           static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_, ro);

@@ -77,6 +77,8 @@ struct Model {
   void* db = nullptr;
   void* ws = nullptr;  // GEMM: gemm_softmax workspace (zeroed once; split-merge counters re-arm)
   size_t ws_bytes = 0;
+  void* ws_split = nullptr;  // GEMM: linear_split workspace (small batches; every f32 batch)
+  size_t ws_split_bytes = 0;
   ~Model();
 };
 
@@ -101,8 +103,11 @@ struct EngineConfig {
   int max_wait_us = 0;    // 0 = continuous batching; >0 = also wait up to this long to fill a batch
   int slots = 4;          // batches in flight
   int dtype = DT_F64;     // SMALL-path compute dtype (f64 = bit parity with sklearn, or f32)
-  int wide_dtype = DT_BF16;  // dtype of models too wide for the SMALL path: bf16 -> GEMV / MFMA
-                             // GEMM kernels; f32 -> GEMV (binary) / GENERIC; f64 -> GENERIC
+  int wide_dtype = DT_F32;   // dtype of models too wide for the SMALL path: f32 -> GEMV (binary) /
+                             // f32 MFMA class-split kernel (multiclass, F <= 512); bf16 -> GEMV /
+                             // bf16 MFMA GEMM kernels; f64 (or f32 beyond F = 512) -> GENERIC
+  int split_max_rows = 32;   // bf16 GEMM path: batches of at most this many rows take the
+                             // class-split kernel (linear_split.h; 0 = always the tiles kernel)
   int max_features = 256; // per-request feature cap (sizes the slot buffers)
   bool inline_args = true;  // SMALL path: batches that fit travel in the kernel-argument block
   // ... and complete through per-row 16-byte records {seq, idx, p} (one store per row, no fence,

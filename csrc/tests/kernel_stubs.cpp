@@ -24,6 +24,12 @@ void launch_gemm_softmax(const void*, const void*, const float*, int64_t, int, i
                          hipStream_t, RecOut) {
   unreachable("launch_gemm_softmax");
 }
+bool linear_split_supported(int, int) { return false; }
+size_t linear_split_workspace(int64_t, int) { return 0; }
+void launch_linear_split(int, const void*, int64_t, const void*, const float*, int64_t, int, int, int, int32_t*, float*,
+                         void*, size_t, hipStream_t, RecOut) {
+  unreachable("launch_linear_split");
+}
 std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int, const std::string&, int, std::string* why) {
   if (why) *why = "host-only build";
   return nullptr;

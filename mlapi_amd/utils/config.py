@@ -31,7 +31,9 @@ class Config:
     # device / engine
     device: str = "auto"                      # "auto" | "cpu" | "cuda" | "cuda:N" | "N"
     dtype: str = "f64"                        # small-model (F<=32, K<=16) compute dtype: f64 (sklearn parity) | f32
-    wide_dtype: str = "bf16"                  # wider models: bf16 (GEMV / MFMA GEMM kernels) | f32 | f64
+    wide_dtype: str = "f32"                   # wider models: f32 (GEMV / f32-MFMA class-split kernel; F <= 512
+                                              # multiclass) | bf16 (opt-in: bf16 GEMV / MFMA GEMM) | f64 (GENERIC)
+    split_max_rows: int = 32                  # bf16 multiclass: batches <= this many rows take the class-split kernel
     max_batch: int = 256
     max_wait_us: int = 0                      # 0 = continuous batching
     slots: int = 4

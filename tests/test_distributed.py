@@ -238,6 +238,7 @@ def test_dp_health_dispatch_drops_and_readmits_rank(tmp_path, iris_pickle_bytes)
             assert p.poll() is None, p.stdout.read()
             assert time.time() - t0 < 90, [state(r) for r in range(3)]
             time.sleep(0.1)
+        time.sleep(0.25)  # the group's acceptor learns of it over the member channel (<= one poll period)
         s1 = state(1)
         assert not s1["accepting"] and s1["listeners"] == 0 and not s1["healthy"]
         assert 'mlapi_engine_healthy{rank="1",backend="cpu"} 0' in s1["metrics"]

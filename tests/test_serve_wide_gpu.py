@@ -68,7 +68,10 @@ def _engine(native, **kw):
     (512, 300, Kind.MULTINOMIAL, "bf16", "gemm"),
     (1024, 200, Kind.MULTINOMIAL, "bf16", "gemm"),  # row-group kernel (F looped in slices)
     (700, 30, Kind.OVR, "bf16", "gemm"),            # F padded to 1024
-    (48, 40, Kind.MULTINOMIAL, "f32", "generic"),
+    (48, 40, Kind.MULTINOMIAL, "f32", "gemm"),     # f32 MFMA class-split kernel, F padded to 64
+    (256, 1000, Kind.MULTINOMIAL, "f32", "gemm"),
+    (100, 10, Kind.OVR, "f32", "gemm"),
+    (700, 30, Kind.MULTINOMIAL, "f32", "generic"),  # f32 beyond F = 512
     (48, 40, Kind.OVR, "f64", "generic"),
 ])
 def test_engine_wide_paths_match_oracle(native, F, K, kind, wide, path, stage):
@@ -81,9 +84,28 @@ def test_engine_wide_paths_match_oracle(native, F, K, kind, wide, path, stage):
         idx, p, st = e.predict(X)
         assert (st == 0).all()
         check(m, X, idx, p, "f64" if path == "generic" and wide == "f64" else wide,
-              rtol=1e-12 if wide == "f64" else 1e-4)
+              rtol=1e-12 if wide == "f64" else (1e-6 if wide == "f32" and path == "gemm" else 1e-4))
         s = e.stats()
         assert s["path_batches"][path] == s["batches"] and s["requests"] == 3000
+    finally:
+        e.stop()
+
+
+@pytest.mark.parametrize("wide", ["bf16", "f32"])
+def test_engine_small_multiclass_batches_take_split_kernel(native, wide):
+    """Serving-sized multiclass batches (1..32 rows) run the class-split kernel (linear_split.h)
+    with completion records; results match the oracle batch by batch."""
+    F, K = 256, 1000
+    m = LinearModel.random(F, K, seed=5, kind=Kind.MULTINOMIAL)
+    e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide])
+    try:
+        e.load_model(int(m.kind), m.W, m.b, m.label_json())
+        rng = np.random.default_rng(9)
+        for n in (1, 2, 5, 8, 16, 31, 32, 33):
+            X = rng.standard_normal((n, F))
+            idx, p, st = e.predict(X)
+            assert (st == 0).all()
+            check(m, X, idx, p, wide, rtol=1e-6 if wide == "f32" else 1e-4)
     finally:
         e.stop()
 
