@@ -153,12 +153,23 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
             w = lg.run(args.warmup * args.reqs_per_conn, False)
             if w["failed"] or w["errors"]:
                 raise RuntimeError(f"warmup failed: {w}")
-        s0 = srv.runtime.handle.stats()
+        barrier(info)  # every rank's warmup traffic has drained before the counters are read
+        s0, h0 = srv.runtime.handle.stats(), srv.http.stats()
         c0, l0 = cpu_by_group(), cpu_by_group(lg.pid)
         elapsed, res = _timed(info, lambda: lg.run(args.steps * args.reqs_per_conn, True))
         cpu_util = utilization(c0, cpu_by_group(), elapsed)
         cpu_util["loadgen_process"] = utilization(l0, cpu_by_group(lg.pid), elapsed).get("process_total", 0.0)
-        s1 = srv.runtime.handle.stats()
+        s1, h1 = srv.runtime.handle.stats(), srv.http.stats()
+        nreq = max(1, s1["requests"] - s0["requests"])
+        # where this rank's server CPU goes, per request (IO-thread stage clock, exclusive; "poll"
+        # is epoll_wait + loop overhead, mostly idle blocking) and the server-side HTTP latency
+        cpu_breakdown = {
+            "server_cpu_us_per_req": cpu_util.get("process_total", 0.0) * elapsed / nreq * 1e6,
+            "io_stage_us_per_req": {k: (h1["stage_ns"][k] - h0["stage_ns"][k]) / nreq / 1e3 for k in h1["stage_ns"]},
+            "engine_queue_wait_us_per_req": (s1["queue_wait_us_sum"] - s0["queue_wait_us_sum"]) / nreq,
+            "server_http_latency_us_mean": (h1["http_latency_sum_ns"] - h0["http_latency_sum_ns"]) / 1e3
+            / max(1, h1["http_latency_count"] - h0["http_latency_count"]),
+        }
         lg.cmd("close")
         want = args.steps * args.reqs_per_conn * args.conns
         if res["failed"] or res["errors"] or res["body_mismatches"] or res["ok200"] != want:
@@ -211,6 +222,7 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         "idle_path_batches": idle,
         "backend": srv.runtime.handle.backend,
         "cpu_cores_busy_rank0": cpu_util,
+        "cpu_breakdown_rank0": cpu_breakdown,
         "threads": {"io": args.io_threads, "loadgen": args.client_threads, "pinned_cpus": args.pinned_cpus},
         "requests_per_step": args.reqs_per_conn * args.conns * info.world,
         "topology": ("one port for all ranks, connections dealt round robin by the group's acceptor "

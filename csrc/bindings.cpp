@@ -92,6 +92,7 @@ py::dict stats_dict(const EngineStats& s) {
   d["latency_hist_us_pow2"] = lh;
   d["latency_sum_us"] = s.latency_sum_us;
   d["device_us_sum"] = s.device_us_sum;
+  d["queue_wait_us_sum"] = s.queue_wait_us_sum;
   d["queue_depth"] = s.queue_depth;
   d["model_version"] = s.model_version;
   d["healthy"] = s.healthy;
@@ -432,6 +433,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("health_probe_ms", &ServerConfig::health_probe_ms)
       .def_readwrite("backlog", &ServerConfig::backlog)
       .def_readwrite("dispatch", &ServerConfig::dispatch)
+      .def_readwrite("stage_timing", &ServerConfig::stage_timing)
       .def_readwrite("dispatch_group", &ServerConfig::dispatch_group)
       .def_readwrite("dispatch_rank", &ServerConfig::dispatch_rank);
 
@@ -567,6 +569,14 @@ PYBIND11_MODULE(_C, m) {
         d["listen_closes"] = st.listen_closes;
         d["accepting"] = st.accepting;
         d["listeners"] = s.listeners();
+        py::dict stg;
+        for (int i = 0; i < SS_COUNT; ++i) stg[server_stage_name(i)] = st.stage_ns[i];
+        d["stage_ns"] = stg;
+        py::list lh;
+        for (int i = 0; i < HTTP_LAT_BUCKETS; ++i) lh.append(st.http_latency_hist[i]);
+        d["http_latency_hist_us_pow2"] = lh;
+        d["http_latency_sum_ns"] = st.http_latency_sum_ns;
+        d["http_latency_count"] = st.http_latency_count;
         if (const ConnDispatcher* dp = s.dispatcher()) {
           py::dict x;
           x["leader"] = dp->leader();

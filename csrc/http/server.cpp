@@ -12,6 +12,7 @@
 #include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <unistd.h>
+#include <x86intrin.h>
 
 #include <cerrno>
 #include <cmath>
@@ -24,6 +25,7 @@
 #include <unordered_map>
 
 #include "../runtime/float_repr.h"
+#include "../runtime/trace.h"
 
 namespace mlapi {
 
@@ -236,7 +238,8 @@ bool parse_number(const char* p, size_t n, size_t& i, double* out) {
 bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>& names, double* out) {
   const size_t nk = names.size();
   if (nk > 4096) return false;
-  std::vector<char> seen(nk, 0);
+  uint64_t seen_bits[64];  // no per-request allocation: one bit per feature name
+  std::memset(seen_bits, 0, ((nk + 63) / 64) * sizeof(uint64_t));
   size_t i = 0, hint = 0;
   while (i < n && is_ws(p[i])) ++i;
   if (i >= n || p[i] != '{') return false;
@@ -280,7 +283,7 @@ bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>&
         double v;
         if (!parse_number(p, n, i, &v)) return false;
         out[which] = v;
-        seen[which] = 1;
+        seen_bits[(size_t)which >> 6] |= uint64_t(1) << ((size_t)which & 63);
       } else {
         if (!skip_value(p, n, i, 0)) return false;
       }
@@ -300,7 +303,7 @@ bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>&
   while (i < n && is_ws(p[i])) ++i;
   if (i != n) return false;
   for (size_t k = 0; k < nk; ++k)
-    if (!seen[k]) return false;
+    if (!(seen_bits[k >> 6] >> (k & 63) & 1)) return false;
   return true;
 }
 
@@ -313,7 +316,30 @@ inline int64_t mono_ns() {
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
 }
+
+// rdtsc ticks -> ns, calibrated once (HttpServer::start, off the request path)
+double tsc_ns_per_tick() {
+  static const double r = [] {
+    const int64_t n0 = mono_ns();
+    const uint64_t t0 = __rdtsc();
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    const int64_t n1 = mono_ns();
+    const uint64_t t1 = __rdtsc();
+    return t1 > t0 ? (double)(n1 - n0) / (double)(t1 - t0) : 1.0;
+  }();
+  return r;
+}
+
+const char* const kStageRange[SS_COUNT] = {"mlapi.http.poll",   "mlapi.http.recv",   "mlapi.http.parse",
+                                           "mlapi.http.submit", "mlapi.http.idle_gpu", "mlapi.http.render",
+                                           "mlapi.http.send",   "mlapi.http.handoff"};
 }  // namespace
+
+const char* server_stage_name(int s) {
+  static const char* const names[SS_COUNT] = {"poll", "recv", "parse", "submit", "idle_gpu", "render", "send",
+                                              "handoff"};
+  return s >= 0 && s < SS_COUNT ? names[s] : "?";
+}
 
 namespace {
 
@@ -335,6 +361,7 @@ struct Conn {
   std::string client_host, server_host;
   int client_port = 0, server_port = 0;
   std::string req_line;       // access log: request line of the outstanding request
+  uint64_t t_req = 0;         // rdtsc when the outstanding request was fully parsed
 };
 
 struct FastBatch {
@@ -459,6 +486,10 @@ class IoThread : public Sink {
   }
 
   std::atomic<uint64_t> n_fast{0}, n_slow{0}, n_resp{0}, n_conn{0}, n_err{0}, n_bad{0}, n_listen_close{0};
+  // published copies of the stage clock / latency histogram (ticks; see ServerStats)
+  std::atomic<uint64_t> pub_stage[SS_COUNT] = {};
+  std::atomic<uint64_t> pub_lat[HTTP_LAT_BUCKETS] = {};
+  std::atomic<uint64_t> pub_lat_sum{0}, pub_lat_n{0};
 
  private:
   // Hand-off from other threads: a spinning IO thread sees `pending_` on its next poll; a blocked
@@ -474,8 +505,49 @@ class IoThread : public Sink {
     }
   }
 
+  // ---- stage clock: exclusive time per stage (ServerStage), rdtsc between transitions
+  void stage(int st) {
+    if (!timing_) return;
+    const uint64_t t = __rdtsc();
+    st_acc_[st_cur_] += t - st_last_;
+    st_last_ = t;
+    st_cur_ = st;
+  }
+  struct Stage {
+    IoThread* io;
+    int prev;
+    bool rtx;
+    Stage(IoThread* i, int st) : io(i), prev(i->st_cur_), rtx(Roctx::get().enabled) {
+      io->stage(st);
+      if (rtx) Roctx::get().push(kStageRange[st]);
+    }
+    ~Stage() {
+      if (rtx) Roctx::get().pop();
+      io->stage(prev);
+    }
+  };
+  void publish_clock() {
+    if (!timing_) return;
+    stage(st_cur_);
+    for (int i = 0; i < SS_COUNT; ++i) pub_stage[i].store(st_acc_[i], std::memory_order_relaxed);
+    for (int i = 0; i < HTTP_LAT_BUCKETS; ++i) pub_lat[i].store(lat_hist_[i], std::memory_order_relaxed);
+    pub_lat_sum.store(lat_sum_, std::memory_order_relaxed);
+    pub_lat_n.store(lat_n_, std::memory_order_relaxed);
+  }
+  // the response to c's outstanding request was just handed to send()
+  void note_latency(uint64_t t_req) {
+    if (!timing_ || t_req == 0) return;
+    const uint64_t d = __rdtsc() - t_req;
+    const uint64_t us = (uint64_t)((double)d * ns_per_tick_ * 1e-3);
+    const int b = us == 0 ? 0 : std::min(HTTP_LAT_BUCKETS - 1, 64 - __builtin_clzll(us));
+    ++lat_hist_[b];
+    lat_sum_ += d;
+    ++lat_n_;
+  }
+
   void flush_submits() {
     if (pend_tags_.empty()) return;
+    Stage sg(this, SS_SUBMIT);
     const int n = (int)pend_tags_.size();
     {
       // idle engine: this thread launches the rows itself and renders the responses right away
@@ -484,7 +556,12 @@ class IoThread : public Sink {
       std::shared_ptr<const Model> m;
       // wide models too while the server is at low load (a batch=1 client)
       const bool low = srv_->open_conns.load(std::memory_order_relaxed) <= srv_->config().io_spin_max_conns;
-      if (srv_->engine()->run_idle(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), idle_done_, m, low)) {
+      bool ran;
+      {
+        Stage sg2(this, SS_IDLE_GPU);
+        ran = srv_->engine()->run_idle(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), idle_done_, m, low);
+      }
+      if (ran) {
         pend_x_.clear();
         pend_tags_.clear();
         FastBatch fb{std::move(m), std::move(idle_done_)};
@@ -519,6 +596,10 @@ class IoThread : public Sink {
     char name[16];
     snprintf(name, sizeof name, "mlapi-io-%d", index_);
     pthread_setname_np(pthread_self(), name);
+    timing_ = srv_->config().stage_timing;
+    ns_per_tick_ = tsc_ns_per_tick();
+    st_last_ = __rdtsc();
+    st_cur_ = SS_POLL;
     epoll_event evs[256];
     const int64_t always_spin_ns = (int64_t)srv_->config().io_spin_us * 1000;
     const int64_t lowload_spin_ns = (int64_t)srv_->config().io_spin_lowload_us * 1000;
@@ -527,6 +608,7 @@ class IoThread : public Sink {
     while (!stop_.load()) {
       flush_submits();
       flush_log();
+      publish_clock();
       int timeout = 200;
       // busy-poll window: always (io_spin_us), or at low load only (a batch=1 client)
       const int64_t spin_ns =
@@ -547,6 +629,7 @@ class IoThread : public Sink {
         spinning_.store(false);  // left the low-load regime: hand-offs need the eventfd again
         if (pending_.load()) timeout = 0;
       }
+      stage(SS_POLL);
       const int n = epoll_wait(epfd_, evs, 256, timeout);
       const bool spin_enabled = always_spin_ns > 0 || lowload_spin_ns > 0;
       if (n > 0 && spin_enabled) last_active = mono_ns();
@@ -702,6 +785,7 @@ class IoThread : public Sink {
   bool on_readable(Conn* c) {
     char buf[65536];
     bool eof = false;
+    Stage sg(this, SS_RECV);
     for (;;) {
       const ssize_t r = recv(c->fd, buf, sizeof buf, 0);
       if (r > 0) {
@@ -725,10 +809,12 @@ class IoThread : public Sink {
       c->paused = true;
       update_events(c);
     }
+    stage(SS_PARSE);  // the rest of this call is parsing (process() switches to SEND itself)
     return process(c);
   }
 
   bool flush(Conn* c) {
+    Stage sg(this, SS_SEND);
     while (c->out_pos < c->out.size()) {
       const ssize_t w = send(c->fd, c->out.data() + c->out_pos, c->out.size() - c->out_pos, MSG_NOSIGNAL);
       if (w > 0) {
@@ -805,11 +891,13 @@ class IoThread : public Sink {
   // pipelined requests and flushes).
   void render_fast(const FastBatch& fb) {
     std::string& body = body_;
+    Stage sg(this, SS_RENDER);
     for (const Completion& cp : fb.c) {
       auto it = conns_.find(cp.tag);
       if (it == conns_.end()) continue;  // client went away
       Conn* c = it->second.get();
       c->waiting = false;
+      const uint64_t t_req = c->t_req;
       bool ok = cp.status == ST_OK && fb.model && cp.idx >= 0 && (size_t)cp.idx < fb.model->label_json.size();
       if (ok) {
         body.clear();
@@ -826,11 +914,16 @@ class IoThread : public Sink {
         internal_error(c);
         log_access(c, 500, "Internal Server Error");
       }
-      process(c);  // dispatches pipelined requests, then flushes (may close c)
+      {
+        Stage sp(this, SS_PARSE);  // pipelined requests behind this one, then the flush (SEND)
+        process(c);                // (may close c)
+      }
+      note_latency(t_req);
     }
   }
 
   void drain_pending() {
+    Stage sg(this, SS_HANDOFF);
     std::vector<FastBatch> fast;
     std::vector<SlowResp> slow;
     std::vector<int> adopted;
@@ -860,7 +953,9 @@ class IoThread : public Sink {
       c->out += sr.bytes;
       if (sr.close) c->close_after = true;
       n_resp.fetch_add(1, std::memory_order_relaxed);
+      const uint64_t t_req = c->t_req;
       process(c);  // dispatches pipelined requests, then flushes (may close c)
+      note_latency(t_req);
     }
   }
 
@@ -883,8 +978,111 @@ class IoThread : public Sink {
     return flush(c);
   }
 
+  static bool ieq(const char* a, size_t n, const char* lower_lit, size_t m) {
+    if (n != m) return false;
+    for (size_t i = 0; i < n; ++i) {
+      char ch = a[i];
+      if (ch >= 'A' && ch <= 'Z') ch = (char)(ch | 0x20);
+      if (ch != lower_lit[i]) return false;
+    }
+    return true;
+  }
+  static bool icontains(const char* a, size_t n, const char* lower_lit, size_t m) {
+    for (size_t i = 0; i + m <= n; ++i)
+      if (ieq(a + i, m, lower_lit, m)) return true;
+    return false;
+  }
+  // FastAPI's JSON content-type rule (json_ctype) on a view
+  static bool json_ctype_view(const char* p, size_t n) {
+    const char* semi = static_cast<const char*>(memchr(p, ';', n));
+    if (semi) n = (size_t)(semi - p);
+    while (n && (p[0] == ' ' || p[0] == '\t')) ++p, --n;
+    while (n && (p[n - 1] == ' ' || p[n - 1] == '\t')) --n;
+    if (n < 12 || !ieq(p, 12, "application/", 12)) return false;
+    p += 12;
+    n -= 12;
+    return ieq(p, n, "json", 4) || (n > 5 && ieq(p + n - 5, 5, "+json", 5));
+  }
+
+  // Zero-allocation parse of the common request: `POST <predict_path>[?q] HTTP/1.1` with a
+  // Content-Length, a JSON content type, no Expect / Transfer-Encoding, and a body the strict
+  // parser accepts - parsed straight into the pending arena. 1 = queued for the engine,
+  // 0 = incomplete (wait for bytes), -2 = anything else: the full parser below decides (and
+  // produces the exact same responses it always did).
+  int parse_fast(Conn* c) {
+    const auto& cfg = srv_->config();
+    if (!cfg.fast_path || cfg.access_log || nfeat_ == 0) return -2;
+    const char* base = c->in.data() + c->in_pos;
+    const size_t avail = c->in.size() - c->in_pos;
+    if (avail < 5 || memcmp(base, "POST ", 5) != 0) return -2;
+    const char* hend = static_cast<const char*>(memmem(base, avail, "\r\n\r\n", 4));
+    if (hend == nullptr) return avail > cfg.max_header ? -2 : 0;
+    const size_t hlen = (size_t)(hend - base) + 4;
+    const char* le = static_cast<const char*>(memmem(base, hlen, "\r\n", 2));
+    const char* t0 = base + 5;
+    const char* sp = static_cast<const char*>(memchr(t0, ' ', (size_t)(le - t0)));
+    if (sp == nullptr || (size_t)(le - sp - 1) != 8 || memcmp(sp + 1, "HTTP/1.1", 8) != 0) return -2;
+    const char* q = static_cast<const char*>(memchr(t0, '?', (size_t)(sp - t0)));
+    const char* pe = q ? q : sp;
+    if ((size_t)(pe - t0) != cfg.predict_path.size() || memcmp(t0, cfg.predict_path.data(), (size_t)(pe - t0)) != 0)
+      return -2;
+    int64_t clen = -1;
+    bool close = false, json = false, seen_ctype = false;
+    const char* hp = le + 2;
+    const char* hlim = base + hlen - 2;
+    while (hp < hlim) {
+      const char* e = static_cast<const char*>(memmem(hp, (size_t)(hlim - hp) + 2, "\r\n", 2));
+      if (e == nullptr) return -2;
+      const char* colon = static_cast<const char*>(memchr(hp, ':', (size_t)(e - hp)));
+      if (colon == nullptr) return -2;
+      const char* v = colon + 1;
+      const char* ve = e;
+      while (v < ve && (*v == ' ' || *v == '\t')) ++v;
+      while (ve > v && (ve[-1] == ' ' || ve[-1] == '\t')) --ve;
+      const size_t nl = (size_t)(colon - hp), vl = (size_t)(ve - v);
+      if (ieq(hp, nl, "content-length", 14)) {
+        if (vl == 0 || vl > 18) return -2;
+        int64_t x = 0;
+        for (size_t i = 0; i < vl; ++i) {
+          if (v[i] < '0' || v[i] > '9') return -2;
+          x = x * 10 + (v[i] - '0');
+        }
+        if (clen >= 0 && clen != x) return -2;
+        clen = x;
+      } else if (ieq(hp, nl, "transfer-encoding", 17) || ieq(hp, nl, "expect", 6)) {
+        return -2;
+      } else if (ieq(hp, nl, "connection", 10)) {
+        close = close || icontains(v, vl, "close", 5);  // any Connection header (h11 joins them)
+      } else if (ieq(hp, nl, "content-type", 12)) {
+        if (!seen_ctype) json = json_ctype_view(v, vl);  // the first one (Starlette's headers[...])
+        seen_ctype = true;
+      }
+      hp = e + 2;
+    }
+    if (clen < 0 || !json || (size_t)clen > cfg.max_body) return -2;
+    if (avail - hlen < (size_t)clen) return 0;
+    const size_t at = pend_x_.size();
+    pend_x_.resize(at + nfeat_);
+    if (!parse_predict_body(base + hlen, (size_t)clen, cfg.feature_names, pend_x_.data() + at)) {
+      pend_x_.resize(at);
+      return -2;
+    }
+    c->in_pos += hlen + (size_t)clen;
+    c->sent_continue = false;
+    if (close) c->close_after = true;
+    c->waiting = true;
+    c->t_req = timing_ ? __rdtsc() : 0;
+    pend_tags_.push_back(c->id);
+    n_fast.fetch_add(1, std::memory_order_relaxed);
+    return 1;
+  }
+
   // 1 = dispatched a request, 0 = incomplete, -1 = protocol error (response queued)
   int parse_one(Conn* c) {
+    {
+      const int f = parse_fast(c);
+      if (f != -2) return f;
+    }
     const auto& cfg = srv_->config();
     const char* base = c->in.data() + c->in_pos;
     const size_t avail = c->in.size() - c->in_pos;
@@ -924,7 +1122,7 @@ class IoThread : public Sink {
     // headers
     std::vector<std::pair<std::string, std::string>> headers;
     int64_t clen = -1;
-    bool chunked = false, expect100 = false;
+    bool chunked = false, expect100 = false, have_ctype = false;
     std::string conn_hdr, ctype;
     const char* hp = le + 2;
     const char* hlim = base + hlen - 2;
@@ -952,10 +1150,12 @@ class IoThread : public Sink {
         lower_inplace(v);
         if (v.find("chunked") != std::string::npos) chunked = true;
       } else if (name == "connection") {
-        conn_hdr = value;
-        lower_inplace(conn_hdr);
+        std::string v = value;  // every Connection header counts (h11 joins them)
+        lower_inplace(v);
+        conn_hdr += conn_hdr.empty() ? v : "," + v;
       } else if (name == "content-type") {
-        ctype = value;
+        if (!have_ctype) ctype = value;  // the first one: what FastAPI (Starlette headers[...]) reads
+        have_ctype = true;
       } else if (name == "expect") {
         std::string v = value;
         lower_inplace(v);
@@ -1047,6 +1247,7 @@ class IoThread : public Sink {
         pend_x_.resize(at + nfeat_);
         if (parse_predict_body(body.data(), body.size(), cfg.feature_names, pend_x_.data() + at)) {
           c->waiting = true;
+          c->t_req = timing_ ? __rdtsc() : 0;
           pend_tags_.push_back(c->id);
           n_fast.fetch_add(1, std::memory_order_relaxed);
           return 1;
@@ -1067,6 +1268,7 @@ class IoThread : public Sink {
     sr.server_host = c->server_host;
     sr.server_port = c->server_port;
     c->waiting = true;
+    c->t_req = timing_ ? __rdtsc() : 0;
     n_slow.fetch_add(1, std::memory_order_relaxed);
     srv_->push_slow(std::move(sr));
     return 1;
@@ -1101,6 +1303,13 @@ class IoThread : public Sink {
   std::atomic<bool> spinning_{false};  // inside the busy-poll window (no eventfd needed)
   std::mutex mu_;
   std::vector<int> adopted_;  // acceptor mode: connections handed over by the dispatcher
+  bool timing_ = false;
+  double ns_per_tick_ = 1.0;
+  uint64_t st_acc_[SS_COUNT] = {};
+  uint64_t st_last_ = 0;
+  int st_cur_ = SS_POLL;
+  uint64_t lat_hist_[HTTP_LAT_BUCKETS] = {};
+  uint64_t lat_sum_ = 0, lat_n_ = 0;
   std::vector<FastBatch> fast_;
   std::vector<Completion> idle_done_;  // run_idle completions (this thread only)
   std::string body_;                   // response body scratch (this thread only)
@@ -1170,6 +1379,7 @@ int HttpServer::listeners() const {
 
 void HttpServer::start() {
   if (started_) return;
+  (void)tsc_ns_per_tick();  // calibrate the stage clock before any IO thread needs it
   if (cfg_.dispatch == "acceptor") {
     acceptor_ = true;
     for (int i = 0; i < cfg_.io_threads; ++i) threads_.push_back(std::make_unique<IoThread>(this, i, -1));
@@ -1292,6 +1502,13 @@ ServerStats HttpServer::stats() const {
   }
   s.listen_closes += leaves_.load();
   s.accepting = accepting_.load();
+  const double k = tsc_ns_per_tick();
+  for (const auto& t : threads_) {
+    for (int i = 0; i < SS_COUNT; ++i) s.stage_ns[i] += (uint64_t)((double)t->pub_stage[i].load() * k);
+    for (int i = 0; i < HTTP_LAT_BUCKETS; ++i) s.http_latency_hist[i] += t->pub_lat[i].load();
+    s.http_latency_sum_ns += (uint64_t)((double)t->pub_lat_sum.load() * k);
+    s.http_latency_count += t->pub_lat_n.load();
+  }
   return s;
 }
 

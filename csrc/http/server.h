@@ -59,6 +59,7 @@ struct ServerConfig {
   // connections) the threads block as usual and no CPU is spent spinning. 0 = off.
   int io_spin_lowload_us = 50;
   int io_spin_max_conns = 2;
+  bool stage_timing = true;  // per-stage CPU accounting + HTTP latency histogram (a few rdtsc per request)
   // Connection dispatch (dispatch.h): "acceptor" (default) = one acceptor per serving group hands
   // every new connection to the next healthy replica / IO thread, round robin; "reuseport" = every
   // IO thread listens on the port itself and the kernel hashes connections over the listeners.
@@ -76,10 +77,31 @@ struct SlowRequest {
   int client_port = 0, server_port = 0;
 };
 
+// Where the IO threads spend their time (exclusive, per stage; rdtsc-clocked, summed over the
+// threads): the per-request CPU breakdown of the serving front end. Also the
+// names of the roctx ranges emitted under MLAPI_ROCTX=1 ("mlapi.http.<stage>").
+enum ServerStage : int {
+  SS_POLL = 0,   // epoll_wait (blocking: idle, not CPU) + loop overhead
+  SS_RECV,       // recv() syscalls
+  SS_PARSE,      // HTTP + JSON parse of requests
+  SS_SUBMIT,     // handing parsed rows to the engine (submit_many)
+  SS_IDLE_GPU,   // idle-engine path: launch + wait for the GPU in this thread (run_idle)
+  SS_RENDER,     // JSON response rendering
+  SS_SEND,       // send() syscalls
+  SS_HANDOFF,    // completion / slow-path hand-offs drained from other threads
+  SS_COUNT
+};
+const char* server_stage_name(int s);
+constexpr int HTTP_LAT_BUCKETS = 24;  // power-of-two microsecond buckets: <1us .. >=2^23us
+
 struct ServerStats {
   uint64_t fast = 0, slow = 0, responses = 0, connections = 0, errors = 0, bad_requests = 0;
   uint64_t listen_closes = 0;  // health_dispatch: times this rank left its dispatch group
   bool accepting = true;
+  uint64_t stage_ns[SS_COUNT] = {};
+  // end-to-end inside the server: request fully parsed -> its response handed to send()
+  uint64_t http_latency_hist[HTTP_LAT_BUCKETS] = {};
+  uint64_t http_latency_sum_ns = 0, http_latency_count = 0;
 };
 
 class ConnDispatcher;

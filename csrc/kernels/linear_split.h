@@ -46,6 +46,7 @@ struct SplitArgs {
   RecOut ro;            // serving: per-row completion records instead of out_idx / out_p
   unsigned int* counters;  // [row groups], zero between launches (re-armed by the merging block)
   float4* partials;        // [row groups][nsplit][32] {m, s, argmax bits, 0}
+  int32_t probe;           // measurement only (MLAPI_SPLIT_PROBE): 1 = stop after the block merge, 2 = after the partial stores
 };
 
 struct SState {
@@ -154,7 +155,7 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
     if (g == 0) red[wave][t * 16 + r16] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
   }
   __syncthreads();
-  if (wave != 0) return;
+  if (wave != 0 || a.probe == 1) return;
   const int l = lane;  // row of the group this lane finishes
   const int64_t row = row0 + l;
   const bool live = l < NB * 16 && row < a.B;
@@ -181,6 +182,7 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
       __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S.bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.probe == 2) return;
     unsigned ticket = 0;
     if (l == 0)
       ticket = __hip_atomic_fetch_add(&a.counters[blockIdx.y], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

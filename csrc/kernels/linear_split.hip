@@ -1,6 +1,7 @@
 // Host launchers of the class-split multiclass predict (linear_split.h).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <stdexcept>
 
 #include "linear_split.h"
@@ -80,6 +81,11 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
   a.ro = ro;
   a.counters = static_cast<unsigned int*>(workspace);
   a.partials = reinterpret_cast<float4*>(static_cast<unsigned char*>(workspace) + COUNTER_REGION);
+  static const int probe = [] {
+    const char* e = getenv("MLAPI_SPLIT_PROBE");
+    return e ? atoi(e) : 0;
+  }();
+  a.probe = probe;
   const dim3 grid((unsigned)ns, (unsigned)rg);
   const bool nb2 = B > 16;
   const bool ovr = kind == KIND_OVR;

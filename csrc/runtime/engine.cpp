@@ -635,6 +635,12 @@ void Engine::batcher_loop() {
       }
       s.t_launch = now_ns();
       {
+        double qw = 0;
+        for (const Meta& mt : s.metas) qw += (double)(s.t_launch - mt.t_enq);
+        std::lock_guard<std::mutex> lk(st_mu_);
+        stats_.queue_wait_us_sum += qw * 1e-3;
+      }
+      {
         std::lock_guard<std::mutex> lk(s_mu_);
         inflight_.push_back(si);
         inflight_n_.fetch_add(1, std::memory_order_release);
@@ -844,8 +850,12 @@ void Engine::completer_loop() {
       inflight_n_.fetch_sub(1, std::memory_order_relaxed);
     }
     Slot& s = slots_[si];
-    if (s.launched) wait_done(s);
+    if (s.launched) {
+      TraceRange tw("mlapi.batch.wait_gpu");
+      wait_done(s);
+    }
     if (cfg_.delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(cfg_.delay_us));
+    TraceRange td("mlapi.batch.deliver");
     const int64_t now = now_ns();
     const size_t n = (size_t)s.n;
     const int32_t* idx = collect(s, st, pd, ix);

@@ -149,6 +149,7 @@ struct EngineStats {
   bool direct_device_kernargs = false;  // ... and its kernarg ring is in device memory
   double latency_sum_us = 0;
   double device_us_sum = 0;         // launch -> completion observed by the completer
+  double queue_wait_us_sum = 0;     // per row: submit -> its batch's launch (batcher queue + packing)
   uint64_t queue_depth = 0;
   uint64_t model_version = 0;
   bool healthy = true;

@@ -48,8 +48,9 @@ class PredictFastPath:
             return await self.app(scope, receive, send)
         ctype = ""
         for k, v in scope.get("headers", ()):
-            if k == b"content-type":
+            if k == b"content-type":  # the first one, like Starlette's request.headers[...]
                 ctype = v.decode("latin-1")
+                break
         if not _json_ctype(ctype):
             return await self.app(scope, receive, send)
         messages = []

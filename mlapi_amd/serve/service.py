@@ -39,7 +39,9 @@ class ServingRuntime:
         srv = self.http.stats() if self.http is not None else None
         return metrics_mod.render(self.handle.stats(), srv,
                                   labels={"rank": str(self.rank), "backend": self.handle.backend},
-                                  extra=[("mlapi_model_loads_total", self.store.loads, None)])
+                                  extra=[("mlapi_model_loads_total", self.store.loads, None),
+                                         ("mlapi_serving_dtype_info", 1, {"small": str(self.config.dtype),
+                                                                          "wide": str(self.config.wide_dtype)})])
 
     def close(self) -> None:
         self.store.stop()

@@ -50,6 +50,13 @@ def render(engine_stats: Optional[dict] = None, server_stats: Optional[dict] = N
         _line(out, "mlapi_request_latency_seconds_count", es["requests"], labels)
         out += ["# TYPE mlapi_device_seconds_total counter"]
         _line(out, "mlapi_device_seconds_total", f"{es['device_us_sum'] * 1e-6:.9g}", labels)
+        if "queue_wait_us_sum" in es:
+            out += ["# HELP mlapi_queue_wait_seconds_total Sum over rows of submit -> batch launch.",
+                    "# TYPE mlapi_queue_wait_seconds_total counter"]
+            _line(out, "mlapi_queue_wait_seconds_total", f"{es['queue_wait_us_sum'] * 1e-6:.9g}", labels)
+        out += ["# HELP mlapi_requests_rejected_total Rows refused by backpressure (max_queue; HTTP 503).",
+                "# TYPE mlapi_requests_rejected_total counter"]
+        _line(out, "mlapi_requests_rejected_total", es.get("rejected", 0), labels)
         out += ["# TYPE mlapi_queue_depth gauge"]
         _line(out, "mlapi_queue_depth", es["queue_depth"], labels)
         out += ["# TYPE mlapi_model_version gauge"]
@@ -77,8 +84,24 @@ def render(engine_stats: Optional[dict] = None, server_stats: Optional[dict] = N
         _line(out, "mlapi_http_connections_total", server_stats["connections"], labels)
         out += ["# TYPE mlapi_http_internal_errors_total counter"]
         _line(out, "mlapi_http_internal_errors_total", server_stats["errors"], labels)
+        if "http_latency_hist_us_pow2" in server_stats:
+            out += ["# HELP mlapi_http_request_duration_seconds Native server: request parsed -> response sent.",
+                    "# TYPE mlapi_http_request_duration_seconds histogram"]
+            cum = 0
+            for i, c in enumerate(server_stats["http_latency_hist_us_pow2"]):
+                cum += c
+                _line(out, "mlapi_http_request_duration_seconds_bucket", cum, {**labels, "le": f"{(2 ** i) * 1e-6:.6g}"})
+            _line(out, "mlapi_http_request_duration_seconds_bucket", cum, {**labels, "le": "+Inf"})
+            _line(out, "mlapi_http_request_duration_seconds_sum", f"{server_stats['http_latency_sum_ns'] * 1e-9:.9g}",
+                  labels)
+            _line(out, "mlapi_http_request_duration_seconds_count", server_stats["http_latency_count"], labels)
+        if "stage_ns" in server_stats:
+            out += ["# HELP mlapi_server_stage_seconds_total IO-thread time per stage (exclusive; poll = epoll wait).",
+                    "# TYPE mlapi_server_stage_seconds_total counter"]
+            for stage, ns in server_stats["stage_ns"].items():
+                _line(out, "mlapi_server_stage_seconds_total", f"{ns * 1e-9:.9g}", {**labels, "stage": stage})
         if "accepting" in server_stats:
-            out += ["# HELP mlapi_rank_accepting 1 while this rank is in its SO_REUSEPORT group (health dispatch).",
+            out += ["# HELP mlapi_rank_accepting 1 while this rank receives new connections (health dispatch).",
                     "# TYPE mlapi_rank_accepting gauge"]
             _line(out, "mlapi_rank_accepting", 1 if server_stats["accepting"] else 0, labels)
             out += ["# TYPE mlapi_rank_listen_closes_total counter"]

@@ -347,3 +347,53 @@ def test_idle_engine_fast_path_cpu_backend(iris_cwd):
         finally:
             srv.stop()
     assert out[8] == out[0]
+
+
+def test_metrics_expose_http_latency_stages_and_rejections(iris_cwd):
+    """/metrics on the native server: the server-side HTTP latency histogram, the per-stage IO
+    thread clock, queue wait, backpressure rejections and the serving dtypes."""
+    from mlapi_amd.serve.server import NativeServer
+    from mlapi_amd.utils.config import Config
+
+    srv = NativeServer(Config.from_env(port=0, device="cpu", io_threads=2)).start()
+    try:
+        for _ in range(50):
+            assert raw(srv.port, b"POST /predict HTTP/1.1\r\nHost: t\r\nContent-Type: application/json\r\n"
+                                 b"Content-Length: %d\r\n\r\n%s" % (len(A1), A1))[0][0] == 200
+        time.sleep(0.3)  # IO threads publish their clocks once per loop
+        st = srv.http.stats()
+        assert st["http_latency_count"] >= 50 and sum(st["http_latency_hist_us_pow2"]) == st["http_latency_count"]
+        assert st["stage_ns"]["parse"] > 0 and st["stage_ns"]["send"] > 0 and st["stage_ns"]["recv"] > 0
+        (_, _, body), = raw(srv.port, b"GET /metrics HTTP/1.1\r\nHost: t\r\n\r\n")
+        m = body.decode()
+        for name in ('mlapi_http_request_duration_seconds_bucket{rank="0",backend="cpu",le="+Inf"}',
+                     "mlapi_http_request_duration_seconds_count", 'mlapi_server_stage_seconds_total{rank="0",'
+                     'backend="cpu",stage="parse"}', "mlapi_requests_rejected_total", "mlapi_queue_wait_seconds_total",
+                     'mlapi_serving_dtype_info{rank="0",backend="cpu",small="f64",wide="f32"} 1'):
+            assert name in m, name
+    finally:
+        srv.stop()
+
+
+def test_fast_parser_matches_full_parser_on_header_variants(server):
+    """The zero-allocation fast path and the full parser answer header variants identically:
+    case-insensitive names, duplicate content-type (last wins), query string, Connection: close,
+    and HTTP/1.0 / chunked / Expect requests (full parser) all give the same 200 body."""
+    pre = b"POST /predict?x=1 HTTP/1.1\r\nHOST: t\r\ncontent-TYPE:  application/json ; charset=utf-8 \r\nX-A: b\r\n"
+    r1 = raw(server.port, pre + b"CONTENT-LENGTH: %d\r\n\r\n%s" % (len(A1), A1))
+    r2 = raw(server.port, b"POST /predict HTTP/1.1\r\nHost: t\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked"
+                          b"\r\n\r\n%x\r\n%s\r\n0\r\n\r\n" % (len(A1), A1))
+    r3 = raw(server.port, b"POST /predict HTTP/1.0\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n%s"
+             % (len(A1), A1))
+    r4 = raw(server.port, b"POST /predict HTTP/1.1\r\nContent-Type: application/json\r\nConnection: Close\r\n"
+                          b"Content-Length: %d\r\n\r\n%s" % (len(A1), A1))
+    assert r1[0][0] == r2[0][0] == r3[0][0] == r4[0][0] == 200
+    assert r1[0][2] == r2[0][2] == r3[0][2] == r4[0][2]
+    assert r4[0][1].get("connection") == "close"
+    # duplicate Content-Type: FastAPI reads the FIRST one (Starlette headers[...]); text/plain first -> 422
+    r5 = raw(server.port, b"POST /predict HTTP/1.1\r\nContent-Type: text/plain\r\nContent-Type: application/json\r\n"
+                          b"Content-Length: %d\r\n\r\n%s" % (len(A1), A1))
+    assert r5[0][0] == 422
+    r6 = raw(server.port, b"POST /predict HTTP/1.1\r\nContent-Type: application/json\r\nContent-Type: text/plain\r\n"
+                          b"Content-Length: %d\r\n\r\n%s" % (len(A1), A1))
+    assert r6[0][0] == 200 and r6[0][2] == r1[0][2]

@@ -129,6 +129,12 @@ for s in $steps; do
       run gemm_split_f32_b1024 120 python -u bench.py --mode gemm --batch 1024 --steps 1000 --warmup 50 --gemm-dtype f32
       prof gemm_split_b8 120 --mode gemm --batch 8 --steps 200 --warmup 5 --gemm-kernel split --launch eager
       prof gemm_tiles_b8 120 --mode gemm --batch 8 --steps 200 --warmup 5 --launch eager ;;
+    splitprobe)  # phase cost of the class-split kernel: full / no merge / no ticket (kernel durations)
+      for pr in 0 1 2; do
+        MLAPI_SPLIT_PROBE=$pr prof "split_probe${pr}_b8" 120 --mode gemm --batch 8 --steps 300 --warmup 5 --gemm-kernel split --launch eager
+        MLAPI_SPLIT_PROBE=$pr prof "split_probe${pr}_b1" 120 --mode gemm --batch 1 --steps 300 --warmup 5 --gemm-kernel split --launch eager
+      done
+      prof "tiles_b1" 120 --mode gemm --batch 1 --steps 300 --warmup 5 --launch eager ;;
     kbench)
       for m in gemv gemm train train_softmax; do run "bench_$m" 300 python -u bench.py --mode $m --steps 100 --warmup 10; done ;;
     prof)
