@@ -255,8 +255,10 @@ def bench_serve(args, info):
 
 
 def bench_serve_wide(args, info):
-    """Wide model on the /predict hot path: F=256, K classes (2 -> bf16 GEMV kernel, else the
-    MFMA gemm_softmax kernel), bodies validated against the engine within rel 1e-5."""
+    """Wide model on the /predict hot path: F=256, K classes (2 -> GEMV kernel, else the class-split
+    MFMA kernel for serving-sized batches / the tiles kernel for large ones). --wide-dtype f32
+    (default, the engine default): f32 operands, every body within rel 1e-6 of the fp64 oracle of
+    the f32-rounded model; bf16: within rel 1e-4 of the bf16-rounded oracle."""
     from mlapi_amd.models.linear import LinearModel
     from mlapi_amd.parallel.comm import broadcast_model
     from mlapi_amd.serve.loadgen import bf16_oracle
@@ -266,10 +268,18 @@ def bench_serve_wide(args, info):
     model = LinearModel.random(F, K, seed=0, labels=[f"class_{i}" for i in range(K)]) if info.is_main else None
     model = broadcast_model(model, info)
     rows = np.round(np.random.default_rng(7).standard_normal((args.workload_rows, F)), 3)
-    return _serve_bench(args, info, model, names, rows, dtype_cfg={"wide_dtype": "bf16"}, rel_tol=1e-5,
-                        oracle_kw={"rtol_oracle": 1e-4, "label_margin": 1e-3, "oracle": bf16_oracle(model, rows)},
-                        features=F, model_desc=f"LogisticRegression F={F} K={K} ({'binary' if K == 2 else 'softmax'}) "
-                                               "via POST /predict, bf16 kernels")
+    if args.wide_dtype == "bf16":
+        okw = {"rtol_oracle": 1e-4, "label_margin": 1e-3, "oracle": bf16_oracle(model, rows)}
+        rel = 1e-5
+    else:
+        f32 = lambda a: np.asarray(a, dtype=np.float32).astype(np.float64)  # noqa: E731
+        okw = {"rtol_oracle": 1e-6, "label_margin": 1e-5,
+               "oracle": (LinearModel(f32(model.W), f32(model.b), model.classes, model.kind), f32(rows))}
+        rel = 1e-6
+    return _serve_bench(args, info, model, names, rows, dtype_cfg={"wide_dtype": args.wide_dtype}, rel_tol=rel,
+                        oracle_kw=okw, features=F,
+                        model_desc=f"LogisticRegression F={F} K={K} ({'binary' if K == 2 else 'softmax'}) "
+                                   f"via POST /predict, {args.wide_dtype} kernels")
 
 
 def _launcher(args, call):
@@ -429,6 +439,7 @@ def main(argv=None) -> int:
                          "driver's 20 steps time >= 2 s even at 1.3 M req/s)")
     ap.add_argument("--workload-rows", type=int, default=1024, help="serve: distinct validated requests")
     ap.add_argument("--wide-classes", type=int, default=1000, help="serve_wide: 2 = binary GEMV, else softmax GEMM")
+    ap.add_argument("--wide-dtype", default="f32", choices=["f32", "bf16"], help="serve_wide: kernel operand dtype")
     ap.add_argument("--client-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--io-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--max-batch", type=int, default=256)
@@ -532,7 +543,7 @@ def main(argv=None) -> int:
             "metric": metric, "value": value, "unit": unit, "n_gpus": info.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None if BASELINES[args.mode] is None else value / BASELINES[args.mode],
-            "dtype": "fp64" if args.mode == "serve" else "bf16",
+            "dtype": "fp64" if args.mode == "serve" else (args.wide_dtype if args.mode == "serve_wide" else "bf16"),
             "data": "synthetic (random-init weights, fixed synthetic inputs)", "config": config,
             "comm_backend": info.backend,
         }

@@ -105,6 +105,7 @@ py::dict stats_dict(const EngineStats& s) {
   d["inline_batches"] = s.inline_batches;
   d["direct_batches"] = s.direct_batches;
   d["idle_batches"] = s.idle_batches;
+  d["bar_batches"] = s.bar_batches;
   d["direct_dispatch"] = s.direct_dispatch;
   d["direct_device_kernargs"] = s.direct_device_kernargs;
   return d;
@@ -324,6 +325,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("spin_us", &EngineConfig::spin_us)
       .def_readwrite("wide_dtype", &EngineConfig::wide_dtype)
       .def_readwrite("split_max_rows", &EngineConfig::split_max_rows)
+      .def_readwrite("bar_rows", &EngineConfig::bar_rows)
       .def_readwrite("inline_args", &EngineConfig::inline_args)
       .def_readwrite("idle_inline_rows", &EngineConfig::idle_inline_rows)
       .def_readwrite("completers", &EngineConfig::completers)

@@ -89,6 +89,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   ~HsaInlineDispatcher() override {
     if (queue_) hsa_queue_destroy(queue_);
     if (kernargs_) hsa_amd_memory_pool_free(kernargs_);
+    for (void* p : bar_bufs_) hsa_amd_memory_pool_free(p);
     if (exe_.handle) hsa_executable_destroy(exe_);
     if (reader_.handle) hsa_code_object_reader_destroy(reader_);
     if (inited_) hsa_shut_down();
@@ -165,6 +166,8 @@ class HsaInlineDispatcher final : public InlineDispatcher {
         hsa_amd_memory_pool_allocate(dpool, (size_t)stride_ * ka_slots_, 0, (void**)&kernargs_) == HSA_STATUS_SUCCESS) {
       if (hsa_amd_agents_allow_access(1, &s.cpu, nullptr, kernargs_) == HSA_STATUS_SUCCESS) {
         hdp_flush_ = hdp.HDP_MEM_FLUSH_CNTL;
+        dpool_ = dpool;
+        cpu_ = s.cpu;
       } else {
         hsa_amd_memory_pool_free(kernargs_);
         kernargs_ = nullptr;
@@ -240,6 +243,28 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     hsa_signal_store_relaxed(queue_->doorbell_signal, (hsa_signal_value_t)wi);
   }
 
+  void* bar_alloc(size_t bytes) override {
+    if (hdp_flush_ == nullptr || bytes == 0) return nullptr;
+    void* p = nullptr;
+    // uncached (MTYPE UC): the GPU never keeps a line of it in L2, so a row the CPU rewrote through
+    // the BAR for the slot's next batch cannot be shadowed by a stale cached copy of the last one
+    if (hsa_amd_memory_pool_allocate(dpool_, (bytes + 255) & ~size_t(255), HSA_AMD_MEMORY_POOL_UNCACHED_FLAG, &p) !=
+        HSA_STATUS_SUCCESS)
+      return nullptr;
+    if (hsa_amd_agents_allow_access(1, &cpu_, nullptr, p) != HSA_STATUS_SUCCESS) {
+      hsa_amd_memory_pool_free(p);
+      return nullptr;
+    }
+    bar_bufs_.push_back(p);
+    return p;
+  }
+  void bar_flush() override {
+    if (hdp_flush_ == nullptr) return;
+    _mm_sfence();
+    *reinterpret_cast<volatile uint32_t*>(hdp_flush_) = 1u;
+    (void)*reinterpret_cast<volatile uint32_t*>(hdp_flush_);  // the flush is posted: wait for it
+  }
+
   bool faulted() const override { return fault_.load(std::memory_order_relaxed); }
   bool device_kernargs() const override { return hdp_flush_ != nullptr; }
   void set_fault() { fault_.store(true); }
@@ -258,6 +283,9 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   hsa_queue_t* queue_ = nullptr;
   char* kernargs_ = nullptr;
   uint32_t* hdp_flush_ = nullptr;  // non-null: the ring is in device memory
+  hsa_amd_memory_pool_t dpool_{};
+  hsa_agent_t cpu_{};
+  std::vector<void*> bar_bufs_;
   uint64_t launches_ = 0;
   std::atomic<bool> fault_{false};
 };

@@ -28,6 +28,13 @@ class InlineDispatcher {
   virtual bool faulted() const = 0;
   // true if the kernarg ring is in device memory (else the host kernarg pool)
   virtual bool device_kernargs() const = 0;
+  // Device HBM the CPU writes directly through the BAR (the kernarg ring's mechanism), for rows
+  // of small wide batches: the kernel then reads them from HBM / L2 instead of pulling them over
+  // the host link once per wave. nullptr if the device has no HDP flush (no BAR staging). Freed
+  // with the dispatcher.
+  virtual void* bar_alloc(size_t bytes) = 0;
+  // Make BAR writes visible to the device: sfence, HDP flush, read-back. Call before the launch.
+  virtual void bar_flush() = 0;
 };
 
 // Loads `hsaco_path` (csrc/kernels/serve_direct.hip) for the GPU behind HIP device `device` and

@@ -139,6 +139,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       MLAPI_HIP_CHECK(hipHostMalloc((void**)&s.hrec, rb, hipHostMallocMapped | hipHostMallocCoherent));
       std::memset(s.hrec, 0, rb);  // seq 0 is never launched
       MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.drec, s.hrec, 0));
+      if (direct_ && cfg_.bar_rows > 0) s.xbar = direct_->bar_alloc((size_t)cfg_.bar_rows * slot_row_bytes_);
       s.metas.reserve(cfg_.max_batch);
       free_slots_.push_back(i);
     }
@@ -444,7 +445,7 @@ void Engine::run_cpu(std::vector<Meta>& metas, const std::vector<double>& xs, co
 // Rows of the batch -> the slot's pinned buffer in the model's row layout (xdt, stride ldx,
 // zero padding). A row whose feature count does not match the model is zeroed and answered
 // ST_SHAPE.
-void Engine::pack_rows(Slot& s, const std::vector<double>& xs, const Model& m) {
+void Engine::pack_rows(Slot& s, const std::vector<double>& xs, const Model& m, void* dst) {
   const int F = m.F, ld = m.ldx;
   const size_t n = (size_t)s.n;
   for (size_t i = 0; i < n; ++i) {
@@ -452,18 +453,18 @@ void Engine::pack_rows(Slot& s, const std::vector<double>& xs, const Model& m) {
     if (!ok) s.pre_status[i] = ST_SHAPE;
     const double* src = &xs[s.metas[i].off];
     if (m.xdt == DT_F64) {
-      double* d = static_cast<double*>(s.hx) + i * ld;
+      double* d = static_cast<double*>(dst) + i * ld;
       if (ok)
         std::memcpy(d, src, sizeof(double) * F);
       else
         std::memset(d, 0, sizeof(double) * F);
       for (int f = F; f < ld; ++f) d[f] = 0.0;
     } else if (m.xdt == DT_F32) {
-      float* d = static_cast<float*>(s.hx) + i * ld;
+      float* d = static_cast<float*>(dst) + i * ld;
       for (int f = 0; f < F; ++f) d[f] = ok ? (float)src[f] : 0.f;
       for (int f = F; f < ld; ++f) d[f] = 0.f;
     } else {
-      uint16_t* d = static_cast<uint16_t*>(s.hx) + i * ld;
+      uint16_t* d = static_cast<uint16_t*>(dst) + i * ld;
       for (int f = 0; f < F; ++f) d[f] = ok ? f32_to_bf16((float)src[f]) : 0;
       for (int f = F; f < ld; ++f) d[f] = 0;
     }
@@ -525,12 +526,20 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     return;
   }
   s.rec_mode = false;
-  pack_rows(s, xs, m);
   const size_t bytes = (size_t)n * m.ldx * dtype_size(m.xdt);
-  // rows: zero-copy from the pinned slot (one host-link round trip inside the kernel), or staged
-  // by a copy first (a blit kernel of its own: ~4 us at serving sizes)
+  const bool bar = s.xbar != nullptr && m.path != PATH_SMALL && n <= cfg_.bar_rows &&
+                   bytes <= (size_t)cfg_.bar_rows * slot_row_bytes_;
+  pack_rows(s, xs, m, bar ? s.xbar : s.hx);
+  // rows: written into device HBM through the BAR (small wide batches: every wave then reads them
+  // from HBM / L2), zero-copy from the pinned slot (one host-link round trip per reading wave), or
+  // staged by a copy first (a blit kernel of its own: ~4 us at serving sizes)
   const void* X = s.dx;
-  if (m.path != PATH_SMALL && cfg_.stage_wide) {
+  if (bar) {
+    direct_->bar_flush();
+    X = s.xbar;
+    std::lock_guard<std::mutex> lk(st_mu_);
+    stats_.bar_batches++;
+  } else if (m.path != PATH_SMALL && cfg_.stage_wide) {
     MLAPI_HIP_CHECK(hipMemcpyAsync(s.dstage, s.hx, bytes, hipMemcpyHostToDevice, stream_));
     X = s.dstage;
   }

@@ -106,6 +106,9 @@ struct EngineConfig {
   int wide_dtype = DT_F32;   // dtype of models too wide for the SMALL path: f32 -> GEMV (binary) /
                              // f32 MFMA class-split kernel (multiclass, F <= 512); bf16 -> GEMV /
                              // bf16 MFMA GEMM kernels; f64 (or f32 beyond F = 512) -> GENERIC
+  int bar_rows = 32;         // wide paths: batches of at most this many rows are written straight into
+                             // device HBM through the BAR (direct dispatch's HDP-flushed mapping) instead
+                             // of being read by every wave over the host link (0 = off)
   int split_max_rows = 32;   // bf16 GEMM path: batches of at most this many rows take the
                              // class-split kernel (linear_split.h; 0 = always the tiles kernel)
   int max_features = 256; // per-request feature cap (sizes the slot buffers)
@@ -145,6 +148,7 @@ struct EngineStats {
   uint64_t inline_batches = 0;      // SMALL batches launched through the kernel-argument block
   uint64_t direct_batches = 0;      // ... of which written straight into the HSA queue
   uint64_t idle_batches = 0;        // batches run by the submitting thread (run_idle)
+  uint64_t bar_batches = 0;         // wide batches whose rows were written into HBM through the BAR
   bool direct_dispatch = false;     // the direct queue is up
   bool direct_device_kernargs = false;  // ... and its kernarg ring is in device memory
   double latency_sum_us = 0;
@@ -213,6 +217,7 @@ class Engine {
     void* hx = nullptr;       // host pinned, device mapped: packed rows (model xdt)
     void* dx = nullptr;       // device address of hx (zero-copy reads)
     void* dstage = nullptr;   // device buffer: H2D destination of the GEMV / GEMM / GENERIC paths
+    void* xbar = nullptr;     // device HBM written by the CPU through the BAR: rows of small wide batches
     int32_t* hidx = nullptr;  // host pinned outputs, written by the kernel over the host link
     int32_t* didx = nullptr;
     void* hp = nullptr;
@@ -232,7 +237,7 @@ class Engine {
 
   void batcher_loop();
   void completer_loop();
-  void pack_rows(Slot& s, const std::vector<double>& xs, const Model& m);
+  void pack_rows(Slot& s, const std::vector<double>& xs, const Model& m, void* dst);
   void launch_batch(Slot& s, const Model& m, const std::vector<double>& xs);
   void run_cpu(std::vector<Meta>& metas, const std::vector<double>& xs, const std::shared_ptr<const Model>& m);
   void finish(Slot& s, const int32_t* idx, const double* p, const int32_t* status);

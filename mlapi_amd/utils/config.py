@@ -34,6 +34,7 @@ class Config:
     wide_dtype: str = "f32"                   # wider models: f32 (GEMV / f32-MFMA class-split kernel; F <= 512
                                               # multiclass) | bf16 (opt-in: bf16 GEMV / MFMA GEMM) | f64 (GENERIC)
     split_max_rows: int = 32                  # bf16 multiclass: batches <= this many rows take the class-split kernel
+    bar_rows: int = 32                        # GPU wide paths: batches <= this many rows go to HBM through the BAR (0 = off)
     max_batch: int = 256
     max_wait_us: int = 0                      # 0 = continuous batching
     slots: int = 4

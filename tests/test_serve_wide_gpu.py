@@ -110,6 +110,33 @@ def test_engine_small_multiclass_batches_take_split_kernel(native, wide):
         e.stop()
 
 
+@pytest.mark.parametrize("wide", ["bf16", "f32"])
+@pytest.mark.parametrize("K", [2, 1000])
+def test_bar_staged_rows_match_zero_copy(native, wide, K):
+    """Small wide batches written into device HBM through the BAR (bar_rows) give the same results
+    as zero-copy host reads, across slot reuse (uncached BAR buffers: no stale L2 lines)."""
+    F = 256
+    m = LinearModel.random(F, K, seed=K + 1, kind=Kind.BINARY if K == 2 else Kind.MULTINOMIAL)
+    X = np.random.default_rng(3).standard_normal((400, F))
+    outs = {}
+    for bar in (32, 0):
+        e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide], bar_rows=bar)
+        try:
+            e.load_model(int(m.kind), m.W, m.b, m.label_json())
+            res = [e.predict(X[i:i + 7]) for i in range(0, 400, 7)]
+            idx = np.concatenate([r[0] for r in res])
+            p = np.concatenate([r[1] for r in res])
+            assert all((r[2] == 0).all() for r in res)
+            st = e.stats()
+            assert (st["bar_batches"] > 0) == (bar > 0 and st["direct_dispatch"] and st["direct_device_kernargs"])
+            outs[bar] = (idx, p)
+        finally:
+            e.stop()
+    np.testing.assert_array_equal(outs[32][0], outs[0][0])
+    np.testing.assert_array_equal(outs[32][1], outs[0][1])
+    check(m, X, outs[32][0], outs[32][1], wide, rtol=1e-6 if (wide == "f32" and K > 2) else 1e-4)
+
+
 def _post(port, bodies):
     out = []
     s = socket.create_connection(("127.0.0.1", port), timeout=30)

@@ -7,7 +7,8 @@
 #
 # steps:
 #   test          pytest -m gpu (whole GPU tier)          smoke      __graft_entry__.smoke()
-#   serve         headline bench (Iris /predict)           serve_wide F=256 /predict, K=1000 and K=2
+#   serve         headline bench (Iris /predict)           serve_wide F=256 /predict, K=1000 and K=2, f32 and bf16
+#   marker        rocprofv3 --marker-trace of serve / serve_wide with the roctx stage ranges on
 #   serve_ab      serve with kernel-argument batches on/off, interleaved x2 (box variance is large)
 #   serve_idle    serve with the idle-engine fast path on (8 rows) / off, interleaved x2
 #   serve_abenv   serve with AB_VAR set to each of AB_VALS, interleaved x2
@@ -51,8 +52,18 @@ for s in $steps; do
     smoke) run smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     serve) run bench_serve 300 python -u bench.py --steps 200 --warmup 20 ;;
     serve_wide)
-      run bench_serve_wide_k1000 300 python -u bench.py --mode serve_wide --wide-classes 1000 --steps 40 --warmup 5
-      run bench_serve_wide_k2 300 python -u bench.py --mode serve_wide --wide-classes 2 --steps 40 --warmup 5 ;;
+      for dt in f32 bf16; do
+        run bench_serve_wide_k1000_$dt 300 python -u bench.py --mode serve_wide --wide-classes 1000 --wide-dtype $dt --steps 40 --warmup 5
+        run bench_serve_wide_k2_$dt 300 python -u bench.py --mode serve_wide --wide-classes 2 --wide-dtype $dt --steps 40 --warmup 5
+      done ;;
+    marker)  # roctx ranges of every serving stage (MLAPI_ROCTX=1) + kernel trace: rocprofv3 --marker-trace
+      (cd /tmp && MLAPI_ROCTX=1 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv \
+         -d "$O/prof_marker_serve" -o serve -- python3 "$R/bench.py" --steps 5 --warmup 1 --reqs-per-conn 256 --c1-requests 500 \
+         > "$O/prof_marker_serve.log" 2>&1) || stop marker $? "$O/prof_marker_serve.log"
+      (cd /tmp && MLAPI_ROCTX=1 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv \
+         -d "$O/prof_marker_serve_wide" -o serve_wide -- python3 "$R/bench.py" --mode serve_wide --steps 3 --warmup 1 \
+         --reqs-per-conn 128 --c1-requests 300 > "$O/prof_marker_serve_wide.log" 2>&1) || stop marker_wide $? "$O/prof_marker_serve_wide.log"
+      tail -1 "$O/prof_marker_serve.log" | cut -c1-200 ;;
     serve_ab)
       for r in 1 2; do
         for m in 1 0; do
