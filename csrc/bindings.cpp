@@ -326,6 +326,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("wide_dtype", &EngineConfig::wide_dtype)
       .def_readwrite("split_max_rows", &EngineConfig::split_max_rows)
       .def_readwrite("bar_rows", &EngineConfig::bar_rows)
+      .def_readwrite("host_merge_rows", &EngineConfig::host_merge_rows)
       .def_readwrite("inline_args", &EngineConfig::inline_args)
       .def_readwrite("idle_inline_rows", &EngineConfig::idle_inline_rows)
       .def_readwrite("completers", &EngineConfig::completers)

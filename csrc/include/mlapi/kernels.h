@@ -129,11 +129,24 @@ void launch_logits_epilogue(const float* Z, const float* b, int64_t B, int K, in
 // and for f32 models at any batch (v_mfma_f32_16x16x4_f32). X, W in dt (DT_BF16 or DT_F32), W row
 // stride F (a power of two: bf16 32..512, f32 16..512), b f32 [K]. Workspace:
 // linear_split_workspace(B, K) bytes, zeroed once (split-merge counters re-armed in-kernel).
+// Host-merge output (serving, B <= 32): each 64-class block writes one 16-byte record per row
+// {seq, argmax, m, s} (m, s: f32 bits; s = sum exp(z - m), OvR: sum sigmoid(z)) at
+// rec[block * 32 + row]; the host merges the linear_split_nsplit(K) blocks in block order.
+struct alignas(16) SplitRecord {
+  uint32_t seq;
+  int32_t bi;
+  float m, s;
+};
+struct SplitRecOut {
+  SplitRecord* rec = nullptr;
+  uint32_t seq = 0;
+};
 bool linear_split_supported(int dt, int F);
 size_t linear_split_workspace(int64_t B, int K);
+int linear_split_nsplit(int K);
 void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K,
                          int kind, int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes,
-                         hipStream_t stream, RecOut ro = RecOut());
+                         hipStream_t stream, RecOut ro = RecOut(), SplitRecOut sro = SplitRecOut());
 
 // Multiclass training row stats (gemm_softmax.hip MODE 2), X_aug = [X | 0.. | 1 | 0 x 7] bf16
 // read through its row stride ldx (the first F columns); W: [K, F] bf16; b: [K] f32.

@@ -47,6 +47,12 @@ struct SplitArgs {
   unsigned int* counters;  // [row groups], zero between launches (re-armed by the merging block)
   float4* partials;        // [row groups][nsplit][32] {m, s, argmax bits, 0}
   int32_t probe;           // measurement only (MLAPI_SPLIT_PROBE): 1 = stop after the block merge, 2 = after the partial stores
+  // Host merge (serving, one row group): each block publishes its per-row states as 16-byte
+  // completion records {seq, argmax, m, s} into host-mapped memory at hrec[block * 32 + row] and
+  // is done - no ticket, no cross-block round trips; the engine's completer merges the splits in
+  // split order (csrc/runtime/engine.cpp, collect()).
+  uint4* hrec;
+  uint32_t rec_seq;
 };
 
 struct SState {
@@ -168,6 +174,16 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
       const float4 v = red[w][l];
       S = smerge(S, SState{v.x, v.y, __float_as_int(v.z)}, OVR);
     }
+  }
+  if (a.hrec != nullptr) {
+    if (live) {
+      typedef __attribute__((ext_vector_type(4))) uint32_t su32x4_t;
+      const su32x4_t r = {a.rec_seq, (uint32_t)S.bi, __float_as_uint(S.m), __float_as_uint(S.s)};
+      uint4* dst = a.hrec + (int64_t)blockIdx.x * ROWS_PER_GROUP + l;
+      // write-through (sc0 sc1): visible to the host poller without a fence, as one 16-byte unit
+      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(r) : "memory");
+    }
+    return;
   }
   if (gridDim.x > 1) {
     // one cross-block round trip: write-through partials, drained, then the row group's ticket

@@ -50,9 +50,11 @@ size_t linear_split_workspace(int64_t B, int K) {
   return COUNTER_REGION + (size_t)rg * nsplits(K) * split::ROWS_PER_GROUP * sizeof(float4);
 }
 
+int linear_split_nsplit(int K) { return nsplits(K); }
+
 void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K,
                          int kind, int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes,
-                         hipStream_t stream, RecOut ro) {
+                         hipStream_t stream, RecOut ro, SplitRecOut sro) {
   if (B <= 0) return;
   if (!linear_split_supported(dt, F))
     throw std::invalid_argument("linear_split: bf16 F in 32..512 or f32 F in 16..512, a power of two");
@@ -65,7 +67,8 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
   const int rg = row_groups(B), ns = nsplits(K);
   if (rg > (int)(COUNTER_REGION / sizeof(unsigned int)))
     throw std::invalid_argument("linear_split: B too large (<= 2048 rows per launch)");
-  if (ns > 1 && ws_bytes < linear_split_workspace(B, K))
+  if (sro.rec != nullptr && rg != 1) throw std::invalid_argument("linear_split: host merge needs B <= 32");
+  if (sro.rec == nullptr && ns > 1 && ws_bytes < linear_split_workspace(B, K))
     throw std::invalid_argument("linear_split: workspace too small (zero it once)");
   split::SplitArgs a{};
   a.X = X;
@@ -86,6 +89,8 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
     return e ? atoi(e) : 0;
   }();
   a.probe = probe;
+  a.hrec = reinterpret_cast<uint4*>(sro.rec);
+  a.rec_seq = sro.seq;
   const dim3 grid((unsigned)ns, (unsigned)rg);
   const bool nb2 = B > 16;
   const bool ovr = kind == KIND_OVR;

@@ -140,6 +140,12 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       std::memset(s.hrec, 0, rb);  // seq 0 is never launched
       MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.drec, s.hrec, 0));
       if (direct_ && cfg_.bar_rows > 0) s.xbar = direct_->bar_alloc((size_t)cfg_.bar_rows * slot_row_bytes_);
+      if (cfg_.host_merge_rows > 0) {
+        const size_t sb = (size_t)64 * 32 * sizeof(SplitRecord);
+        MLAPI_HIP_CHECK(hipHostMalloc((void**)&s.hsrec, sb, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(s.hsrec, 0, sb);
+        MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.dsrec, s.hsrec, 0));
+      }
       s.metas.reserve(cfg_.max_batch);
       free_slots_.push_back(i);
     }
@@ -162,6 +168,7 @@ Engine::~Engine() {
       if (s.hidx) (void)hipHostFree(s.hidx);
       if (s.hp) (void)hipHostFree(s.hp);
       if (s.hrec) (void)hipHostFree(s.hrec);
+      if (s.hsrec) (void)hipHostFree(s.hsrec);
     }
     {
       std::lock_guard<std::mutex> lk(model_mu_);
@@ -488,7 +495,7 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     a.kind = m.kind;
     a.out_idx = s.didx;
     a.out_p = s.dp;
-    s.rec_mode = cfg_.record_completion;
+    s.rec_mode = cfg_.record_completion ? REC_ROWS : 0;
     a.done = s.rec_mode ? nullptr : sig.done;
     a.rec = s.rec_mode ? s.drec : nullptr;
     a.seq = sig.seq;
@@ -525,7 +532,7 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     if (direct_) stats_.direct_batches++;
     return;
   }
-  s.rec_mode = false;
+  s.rec_mode = 0;
   const size_t bytes = (size_t)n * m.ldx * dtype_size(m.xdt);
   const bool bar = s.xbar != nullptr && m.path != PATH_SMALL && n <= cfg_.bar_rows &&
                    bytes <= (size_t)cfg_.bar_rows * slot_row_bytes_;
@@ -554,15 +561,25 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     if (cfg_.record_completion && m.path == PATH_GEMM) {
       ro.rec = s.drec;
       ro.seq = sig.seq;
-      s.rec_mode = true;
+      s.rec_mode = REC_ROWS;
     }
     if (m.path == PATH_GEMV)
       launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_, ro);
-    else if (m.ws_split != nullptr && (m.xdt == DT_F32 || n <= cfg_.split_max_rows))
-      // small batches (and every f32 batch): the class-split kernel, one cross-block merge round trip
+    else if (m.ws_split != nullptr && (m.xdt == DT_F32 || n <= cfg_.split_max_rows)) {
+      // small batches (and every f32 batch): the class-split kernel. Serving-sized batches end in
+      // per-block records the completer merges; larger ones merge in-kernel (one round trip).
+      SplitRecOut sro;
+      const int ns = linear_split_nsplit(m.K);
+      if (s.hsrec != nullptr && n <= cfg_.host_merge_rows && n <= 32 && ns <= 64) {
+        sro.rec = s.dsrec;
+        sro.seq = sig.seq;
+        ro = RecOut();
+        s.rec_mode = REC_SPLITS;
+        s.rec_nsplit = ns;
+      }
       launch_linear_split(m.xdt, X, m.ldx, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
-                          static_cast<float*>(s.dp), m.ws_split, m.ws_split_bytes, stream_, ro);
-    else
+                          static_cast<float*>(s.dp), m.ws_split, m.ws_split_bytes, stream_, ro, sro);
+    } else
       launch_gemm_softmax(X, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
                           static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_, ro);
     if (!s.rec_mode) launch_serve_signal(sig, stream_);
@@ -683,8 +700,18 @@ void Engine::wait_done(Slot& s) {
   const int64_t t0 = now_ns();
   uint32_t spins = 0;
   int next_row = 0;  // record mode: rows [0, next_row) seen complete
+  const int nrec = s.rec_mode == REC_SPLITS ? s.rec_nsplit * s.n : s.n;
   auto done = [&]() -> bool {
     if (!s.rec_mode) return __atomic_load_n(dw, __ATOMIC_ACQUIRE) == s.seq;
+    if (s.rec_mode == REC_SPLITS) {  // record k: split k / n, row k % n (at [split][32])
+      while (next_row < nrec) {
+        const int sp = next_row / s.n, row = next_row - sp * s.n;
+        const SplitRecord* r = s.hsrec + (size_t)sp * 32 + row;
+        if ((uint32_t)_mm_cvtsi128_si32(load_record(reinterpret_cast<const ServeRecord*>(r))) != s.seq) break;
+        ++next_row;
+      }
+      return next_row == nrec;
+    }
     while (next_row < s.n && (uint32_t)_mm_cvtsi128_si32(load_record(s.hrec + next_row)) == s.seq) ++next_row;
     return next_row == s.n;
   };
@@ -720,6 +747,37 @@ const int32_t* Engine::collect(Slot& s, std::vector<int32_t>& st, std::vector<do
     std::fill(st.begin(), st.end(), (int32_t)ST_DEVICE_ERROR);
     std::fill(pd.begin(), pd.end(), 0.0);
     idx.assign(n, 0);
+    return idx.data();
+  }
+  if (s.rec_mode == REC_SPLITS) {
+    // host merge of the class-split kernel's per-block states, in block order (deterministic), in
+    // double: max (first max wins on ties, like numpy's argmax), then the rescaled sums
+    idx.resize(n);
+    const bool ovr = s.model->kind == KIND_OVR;
+    const int ns = s.rec_nsplit;
+    for (size_t i = 0; i < n; ++i) {
+      double M = -INFINITY;
+      int bi = 0x7fffffff;
+      alignas(16) SplitRecord r[64];
+      for (int sp = 0; sp < ns; ++sp) {
+        _mm_store_si128(reinterpret_cast<__m128i*>(&r[sp]),
+                        load_record(reinterpret_cast<const ServeRecord*>(s.hsrec + (size_t)sp * 32 + i)));
+        const double m = r[sp].m;
+        if (m > M || (m == M && r[sp].bi < bi)) {
+          M = m;
+          bi = r[sp].bi;
+        }
+      }
+      double S = 0;
+      for (int sp = 0; sp < ns; ++sp) {
+        if (ovr)
+          S += r[sp].s;
+        else if (r[sp].m != -INFINITY)
+          S += (double)r[sp].s * std::exp((double)r[sp].m - M);
+      }
+      idx[i] = bi;
+      pd[i] = ovr ? (1.0 / (1.0 + std::exp(-M))) / S : 1.0 / S;
+    }
     return idx.data();
   }
   if (s.rec_mode) {

@@ -57,6 +57,8 @@ enum Status : int32_t {
   ST_SHUTDOWN = 5,
 };
 
+enum RecMode : int { REC_ROWS = 1, REC_SPLITS = 2 };  // how a launched batch completes (Slot::rec_mode)
+
 enum ServePath : int32_t { PATH_SMALL = 0, PATH_GEMV = 1, PATH_GEMM = 2, PATH_GENERIC = 3, PATH_COUNT = 4 };
 
 struct Model {
@@ -109,6 +111,8 @@ struct EngineConfig {
   int bar_rows = 32;         // wide paths: batches of at most this many rows are written straight into
                              // device HBM through the BAR (direct dispatch's HDP-flushed mapping) instead
                              // of being read by every wave over the host link (0 = off)
+  int host_merge_rows = 16;  // class-split launches of at most this many rows publish per-block states
+                             // and the completer merges them (no in-kernel merge round trips; 0 = off)
   int split_max_rows = 32;   // bf16 GEMM path: batches of at most this many rows take the
                              // class-split kernel (linear_split.h; 0 = always the tiles kernel)
   int max_features = 256; // per-request feature cap (sizes the slot buffers)
@@ -224,7 +228,10 @@ class Engine {
     void* dp = nullptr;
     ServeRecord* hrec = nullptr;  // host pinned per-row completion records (kernel-argument batches)
     ServeRecord* drec = nullptr;
-    bool rec_mode = false;    // this launch completes through hrec (no done word)
+    int rec_mode = 0;         // 0: done word; REC_ROWS: per-row records (hrec); REC_SPLITS: per-split records (hsrec)
+    SplitRecord* hsrec = nullptr;  // host-merge class-split launches: [64 splits][32 rows]
+    SplitRecord* dsrec = nullptr;
+    int rec_nsplit = 0;
     uint32_t seq = 0;         // sequence number the launch publishes into the done word
     std::vector<Meta> metas;
     std::vector<int32_t> pre_status;  // per-row status decided before launch

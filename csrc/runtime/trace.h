@@ -21,7 +21,11 @@ struct Roctx {
       Roctx x;
       const char* e = std::getenv("MLAPI_ROCTX");
       if (e && e[0] == '1') {
-        void* h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_GLOBAL);
+        // rocprofiler-sdk's roctx first: rocprofv3 --marker-trace intercepts that library (the
+        // legacy libroctx64 ranges are not recorded by rocprofv3)
+        void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("libroctx64.so.4", RTLD_NOW | RTLD_GLOBAL);
         if (!h) h = dlopen("/opt/rocm/lib/libroctx64.so.4", RTLD_NOW | RTLD_GLOBAL);
         if (h) {
           x.push = reinterpret_cast<push_fn>(dlsym(h, "roctxRangePushA"));

@@ -55,6 +55,7 @@ class EngineHandle:
         ec.wide_dtype = DTYPES[config.wide_dtype]
         ec.split_max_rows = int(config.split_max_rows)
         ec.bar_rows = int(config.bar_rows)
+        ec.host_merge_rows = int(config.host_merge_rows)
         ec.max_features = max(64, len(config.feature_names))
         ec.watchdog_ms = config.watchdog_ms
         ec.fail_every = config.fail_every

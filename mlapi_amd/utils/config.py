@@ -35,6 +35,7 @@ class Config:
                                               # multiclass) | bf16 (opt-in: bf16 GEMV / MFMA GEMM) | f64 (GENERIC)
     split_max_rows: int = 32                  # bf16 multiclass: batches <= this many rows take the class-split kernel
     bar_rows: int = 32                        # GPU wide paths: batches <= this many rows go to HBM through the BAR (0 = off)
+    host_merge_rows: int = 16                 # GPU multiclass: class-split batches <= this many rows merge on the host
     max_batch: int = 256
     max_wait_us: int = 0                      # 0 = continuous batching
     slots: int = 4
