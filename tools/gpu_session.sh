@@ -56,6 +56,10 @@ for s in $steps; do
         run bench_serve_wide_k1000_$dt 300 python -u bench.py --mode serve_wide --wide-classes 1000 --wide-dtype $dt --steps 40 --warmup 5
         run bench_serve_wide_k2_$dt 300 python -u bench.py --mode serve_wide --wide-classes 2 --wide-dtype $dt --steps 40 --warmup 5
       done ;;
+    prof_wide)  # kernel durations of the served wide batches (class-split + host merge, BAR-staged rows)
+      for dt in bf16 f32; do
+        prof "serve_wide_k1000_$dt" 300 --mode serve_wide --wide-dtype $dt --steps 10 --warmup 2 --reqs-per-conn 256
+      done ;;
     marker)  # roctx ranges of every serving stage (MLAPI_ROCTX=1) + kernel trace: rocprofv3 --marker-trace
       (cd /tmp && MLAPI_ROCTX=1 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv \
          -d "$O/prof_marker_serve" -o serve -- python3 "$R/bench.py" --steps 5 --warmup 1 --reqs-per-conn 256 --c1-requests 500 \
