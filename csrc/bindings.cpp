@@ -293,6 +293,34 @@ PYBIND11_MODULE(_C, m) {
       py::arg("stream") = 0, py::arg("params") = 0, py::arg("mom") = 0, py::arg("shadow_w") = 0,
       py::arg("shadow_b") = 0, py::arg("pen_cols") = 0, py::arg("lr") = 0.f, py::arg("inv_n") = 0.f,
       py::arg("l2") = 0.f, py::arg("momentum") = 0.f, py::arg("p2p") = nullptr, py::arg("timeout_ms") = 60000);
+  m.def("softmax_grad_wide_supported", &softmax_grad_wide_supported);
+  m.def("softmax_grad_wide_workspace", &softmax_grad_wide_workspace);
+  m.def(
+      "softmax_grad_wide",
+      [](uintptr_t X_aug, int64_t ldx, uintptr_t W, uintptr_t b, uintptr_t y, int64_t B, int F, int K, int kind,
+         uintptr_t dW_out, uintptr_t stats_out, uintptr_t ws, size_t ws_bytes, uintptr_t stream, uintptr_t params,
+         uintptr_t mom, uintptr_t shadow_w, uintptr_t shadow_b, int pen_cols, float lr, float inv_n, float l2,
+         float momentum, P2PAllReduce* p2p, int timeout_ms) {
+        Sgd2D u;
+        u.params = ptr<float>(params);
+        u.mom = ptr<float>(mom);
+        u.shadow_w = ptr<uint16_t>(shadow_w);
+        u.shadow_b = ptr<float>(shadow_b);
+        u.cols = F + 8;
+        u.pen_cols = pen_cols;
+        u.lr = lr;
+        u.inv_n = inv_n;
+        u.l2 = l2;
+        u.momentum = momentum;
+        launch_softmax_grad_wide(ptr<void>(X_aug), ldx, ptr<void>(W), ptr<float>(b), ptr<int32_t>(y), B, F, K, kind,
+                                 ptr<float>(dW_out), ptr<float>(stats_out), ptr<void>(ws), ws_bytes, stream_of(stream),
+                                 params != 0 ? &u : nullptr, p2p, timeout_ms);
+      },
+      py::arg("X_aug"), py::arg("ldx"), py::arg("W"), py::arg("b"), py::arg("y"), py::arg("B"), py::arg("F"),
+      py::arg("K"), py::arg("kind"), py::arg("dW_out"), py::arg("stats_out"), py::arg("ws"), py::arg("ws_bytes"),
+      py::arg("stream") = 0, py::arg("params") = 0, py::arg("mom") = 0, py::arg("shadow_w") = 0,
+      py::arg("shadow_b") = 0, py::arg("pen_cols") = 0, py::arg("lr") = 0.f, py::arg("inv_n") = 0.f,
+      py::arg("l2") = 0.f, py::arg("momentum") = 0.f, py::arg("p2p") = nullptr, py::arg("timeout_ms") = 60000);
   m.def(
       "sgd_update_2d",
       [](uintptr_t params, uintptr_t grad, uintptr_t mom, int64_t rows, int cols, int pen_cols, float lr,

@@ -180,6 +180,25 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
                             size_t ws_bytes, hipStream_t stream, const Sgd2D* update = nullptr,
                             P2PAllReduce* dp = nullptr, int dp_timeout_ms = 0);
 
+// The deterministic final sum of [nslabs][K][F_aug] dW slabs + [nstat][2] stat slabs, with the
+// optional fused SGD update and in-kernel DP exchange (softmax_grad_dw.hip's last launch).
+void launch_gdw_reduce(const float* slabs, int nslabs, int K, int F_aug, float* dW_out, const float* stat_slabs,
+                       int nstat, float* stats_out, const Sgd2D* update, P2PAllReduce* dp, int dp_timeout_ms,
+                       hipStream_t stream);
+// Full logits Z [B, K] f32 of X [B, F] (row stride ldx) through the row-group kernel.
+void launch_gemm_logits_ld(const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K, float* Z,
+                           hipStream_t stream);
+// Multiclass training gradient for wide models (softmax_grad_wide.hip): F a multiple of 256 above
+// 512 (X_aug row stride F + 8). Row stats and logits by the row-group kernel, G = P - Y (bf16) with
+// the loss / correct stats, dW slabs = G^T X_aug by an MFMA kernel (LDS tiles read through
+// ds_read_b64_tr_b16), then launch_gdw_reduce. Workspace: softmax_grad_wide_workspace bytes.
+bool softmax_grad_wide_supported(int F);
+size_t softmax_grad_wide_workspace(int64_t B, int K, int F);
+void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
+                              int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,
+                              size_t ws_bytes, hipStream_t stream, const Sgd2D* update = nullptr,
+                              P2PAllReduce* dp = nullptr, int dp_timeout_ms = 0);
+
 // ---- train kernels (train.hip) -----------------------------------------------------------------
 // Binary logistic regression, one pass over X: accumulates grad (F w-entries, 1 bias) and stats
 // [loss_sum, n_correct] into per-block slabs, then reduce_slabs() folds them into out[F + 3]:

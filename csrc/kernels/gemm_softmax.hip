@@ -1478,6 +1478,12 @@ void launch_softmax_rowstats(const void* X_aug, int64_t ldx, const void* W, cons
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("softmax_rowstats: multiclass kinds only");
   if (ldx < F || ldx % 8 != 0) throw std::invalid_argument("softmax_rowstats: ldx must be >= F and a multiple of 8");
+  if (!tiles_supported(F)) {  // wide models (F a multiple of 256 beyond 512): the row-group kernel
+    RowsArgs ra = rows_args(X_aug, ldx, W, b, B, F, K);
+    ra.rowstat = static_cast<float2*>(rowstat_out);
+    launch_rows<2>(ra, kind, stream);
+    return;
+  }
   const Plan plan = make_plan(B, K, F, true);
   if (ws_bytes < softmax_rowstats_workspace(B, K, F))
     throw std::invalid_argument("softmax_rowstats: workspace too small (zero it once)");
@@ -1547,6 +1553,14 @@ void launch_gemm_rowstate(const void* X, const void* W, const float* b, int64_t 
     args.partials = reinterpret_cast<float4*>(static_cast<unsigned char*>(workspace) + COUNTER_BYTES);
   }
   launch_mode<4>(args, F, plan, stream);
+}
+
+void launch_gemm_logits_ld(const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K, float* Z,
+                           hipStream_t stream) {
+  if (B <= 0) return;
+  RowsArgs ra = rows_args(X, ldx, W, b, B, F, K);
+  ra.Z = Z;
+  launch_rows<1>(ra, KIND_MULTINOMIAL, stream);
 }
 
 void launch_gemm_logits(const void* X, const void* W, const float* b, int64_t B, int F, int K, float* Z,

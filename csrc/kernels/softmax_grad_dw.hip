@@ -622,6 +622,31 @@ __global__ __launch_bounds__(256) void gdw_reduce_kernel(const f32x4_t* __restri
   }
 }
 
+}  // namespace
+
+void launch_gdw_reduce(const float* slabs, int nslabs, int K, int F_aug, float* dW_out, const float* stat_slabs,
+                       int nstat, float* stats_out, const Sgd2D* update, P2PAllReduce* dp, int dp_timeout_ms,
+                       hipStream_t stream) {
+  if ((K * F_aug) % 4 != 0 || reinterpret_cast<uintptr_t>(dW_out) % 16 != 0 ||
+      reinterpret_cast<uintptr_t>(slabs) % 16 != 0)
+    throw std::invalid_argument("gdw_reduce: K * F_aug must be a multiple of 4 and the buffers 16-byte aligned");
+  const int width4 = K * F_aug / 4;
+  const int nblocks = (width4 + 255) / 256 + 1;
+  if (dp != nullptr) {
+    const P2PBlockArgs a = dp->block_exchange(((size_t)width4 * 4 + 4) * sizeof(float), nblocks, dp_timeout_ms);
+    hipLaunchKernelGGL(gdw_reduce_kernel<true>, dim3((unsigned)nblocks), dim3(256), 0, stream,
+                       reinterpret_cast<const f32x4_t*>(slabs), nslabs, width4, reinterpret_cast<f32x4_t*>(dW_out),
+                       stat_slabs, nstat, stats_out, update != nullptr ? *update : Sgd2D{}, a);
+  } else {
+    hipLaunchKernelGGL(gdw_reduce_kernel<false>, dim3((unsigned)nblocks), dim3(256), 0, stream,
+                       reinterpret_cast<const f32x4_t*>(slabs), nslabs, width4, reinterpret_cast<f32x4_t*>(dW_out),
+                       stat_slabs, nstat, stats_out, update != nullptr ? *update : Sgd2D{}, P2PBlockArgs{});
+  }
+  MLAPI_HIP_CHECK(hipGetLastError());
+}
+
+namespace {
+
 struct GdwLayout {
   int nc, tiles, row_groups, tiles_per_group, class_groups;
   size_t rowstat_off, dw_off, stat_off, total;

@@ -1,0 +1,224 @@
+// Multiclass training gradient for wide models (F > 512) on ONE GPU (reference:
+// LogisticRegression.fit on any F, `Logistic Regression.ipynb:33-34`).
+//
+// The fused kernel (softmax_grad_dw.hip) keeps a 64-row X tile and a wave's 16 W rows in LDS /
+// registers for the whole F, which stops at F = 512. Beyond it the step is five launches, all
+// hand-written (no vendor GEMM):
+//   1. row stats {lse, argmax} (row-group kernel, gemm_softmax.hip MODE 2);
+//   2. logits Z = X W^T + b, f32 (row-group kernel MODE 1);
+//   3. softmax_g_kernel: one wave per row - G = softmax(z) - onehot(y) (OvR: sigmoid(z) - onehot)
+//      as bf16 [B][Kp] (Kp = K rounded up to 64, zero padded) plus per-block {loss, correct};
+//   4. gdw_gemm_kernel: dW slabs[row group][K][F_aug] = G^T X_aug over the group's rows -
+//      v_mfma_f32_16x16x32_bf16 with M = classes, N = features, K = rows: both operands are
+//      row-major [rows][*] tiles, so each is staged in LDS (32 rows x 64 columns, one 16-byte load
+//      per thread) and read transposed with ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane
+//      group, two reads = the 8 rows of a lane's k-slice);
+//   5. launch_gdw_reduce: deterministic slab sum + fused SGD update (+ in-kernel DP exchange).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <stdexcept>
+
+#include "mlapi/common.h"
+#include "mlapi/kernels.h"
+
+namespace mlapi {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 wbf16x8_t;
+typedef __attribute__((ext_vector_type(4))) short wi16x4_t;
+typedef __attribute__((ext_vector_type(4))) float wf32x4_t;
+typedef __attribute__((address_space(3))) wi16x4_t lds_i16x4_t;
+
+constexpr int G_ROWS_PER_BLOCK = 4;  // one wave per row
+constexpr int TILE_ROWS = 32;        // MFMA k-step (rows)
+constexpr int TILE_COLS = 64;        // classes / features per block tile
+
+__device__ __forceinline__ uint16_t to_bf16(float f) {  // round to nearest even
+  const uint32_t u = __float_as_uint(f);
+  return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+// ---- 3. G = P - Y (bf16) + loss / correct per block
+template <bool OVR>
+__global__ __launch_bounds__(64 * G_ROWS_PER_BLOCK) void softmax_g_kernel(const float* __restrict__ Z,
+                                                                          const float2* __restrict__ rowstat,
+                                                                          const int32_t* __restrict__ y, int64_t B,
+                                                                          int K, int Kp, uint16_t* __restrict__ G,
+                                                                          float* __restrict__ stat_slabs) {
+  __shared__ float red[G_ROWS_PER_BLOCK][2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t row = (int64_t)blockIdx.x * G_ROWS_PER_BLOCK + wave;
+  float loss = 0.f, correct = 0.f;
+  if (row < B) {
+    const float2 rs = rowstat[row];
+    const float lse = rs.x;
+    const int yr = y[row];
+    const float* zr = Z + row * K;
+    uint16_t* gr = G + row * Kp;
+    for (int k = lane; k < Kp; k += 64) {
+      float g = 0.f;
+      if (k < K) {
+        const float z = zr[k];
+        const float p = OVR ? 1.f / (1.f + expf(-z)) : expf(z - lse);
+        g = p - (k == yr ? 1.f : 0.f);
+        if (OVR) loss += fmaxf(z, 0.f) - (k == yr ? z : 0.f) + log1pf(expf(-fabsf(z)));
+        else if (k == yr) loss += lse - z;
+      }
+      gr[k] = to_bf16(g);
+    }
+    if (lane == 0) correct = __float_as_int(rs.y) == yr ? 1.f : 0.f;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) loss += __shfl_xor(loss, off, 64);
+  if (lane == 0) {
+    red[wave][0] = loss;
+    red[wave][1] = correct;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    float s = 0.f;
+    for (int w = 0; w < G_ROWS_PER_BLOCK; ++w) s += red[w][threadIdx.x];
+    stat_slabs[2 * (int64_t)blockIdx.x + threadIdx.x] = s;
+  }
+}
+
+// ---- 4. dW slabs = G^T X_aug per row group
+// grid (Kp / 64, ceil(F_aug / 64), row_groups); a wave owns 16 classes x 64 features (4 N-tiles).
+__global__ __launch_bounds__(256) void gdw_gemm_kernel(const uint16_t* __restrict__ G, int Kp, const uint16_t* __restrict__ X,
+                                                       int64_t ldx, int F_aug, int64_t B, int K, int64_t rows_per_group,
+                                                       float* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) uint16_t gt[TILE_ROWS][TILE_COLS];
+  __shared__ __attribute__((aligned(16))) uint16_t xt[TILE_ROWS][TILE_COLS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * TILE_COLS, f0 = blockIdx.y * TILE_COLS;
+  const int64_t r_begin = (int64_t)blockIdx.z * rows_per_group;
+  const int64_t r_end = min(B, r_begin + rows_per_group);
+  // staging: thread t loads 16 B = 8 columns of row t / 8, column chunk t % 8
+  const int sr = threadIdx.x >> 3, sc = (threadIdx.x & 7) * 8;
+  // transposed reads: lane 4q + p of group g supplies row 8g + q (+4), columns base + 4p
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  wf32x4_t acc[4] = {};
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += TILE_ROWS) {
+    const int64_t r = r0 + sr;
+    uint4 gv = {0, 0, 0, 0}, xv = {0, 0, 0, 0};
+    if (r < r_end) {
+      gv = *reinterpret_cast<const uint4*>(G + r * Kp + c0 + sc);  // Kp % 64 == 0: always in bounds
+      if (f0 + sc + 8 <= ldx) {
+        xv = *reinterpret_cast<const uint4*>(X + r * ldx + f0 + sc);
+      } else {
+        uint16_t tmp[8];
+        for (int e = 0; e < 8; ++e) tmp[e] = f0 + sc + e < ldx ? X[r * ldx + f0 + sc + e] : 0;
+        __builtin_memcpy(&xv, tmp, sizeof xv);
+      }
+    }
+    __syncthreads();  // the previous tile's reads are done
+    *reinterpret_cast<uint4*>(&gt[sr][sc]) = gv;
+    *reinterpret_cast<uint4*>(&xt[sr][sc]) = xv;
+    __syncthreads();
+    // A: 16 classes (wave * 16 + i) x 8 rows (8g + j)
+    const wi16x4_t a_lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&gt[8 * g + q][wave * 16 + 4 * p]);
+    const wi16x4_t a_hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&gt[8 * g + 4 + q][wave * 16 + 4 * p]);
+    const wi16x4_t av[2] = {a_lo, a_hi};
+    const wbf16x8_t a = __builtin_bit_cast(wbf16x8_t, av);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const wi16x4_t b_lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&xt[8 * g + q][n * 16 + 4 * p]);
+      const wi16x4_t b_hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&xt[8 * g + 4 + q][n * 16 + 4 * p]);
+      const wi16x4_t bv[2] = {b_lo, b_hi};
+      acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(wbf16x8_t, bv), acc[n], 0, 0, 0);
+    }
+  }
+  // C layout: class c0 + wave * 16 + 4g + i (register i), feature f0 + 16n + (lane & 15)
+  float* slab = slabs + (int64_t)blockIdx.z * K * F_aug;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int f = f0 + n * 16 + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + wave * 16 + 4 * g + i;
+      if (c < K && f < F_aug) slab[(int64_t)c * F_aug + f] = acc[n][i];
+    }
+  }
+}
+
+struct WideLayout {
+  size_t rowstat_off, z_off, g_off, dw_off, stat_off, total;
+  int Kp, row_groups, g_blocks;
+  int64_t rows_per_group;
+};
+
+WideLayout wide_layout(int64_t B, int K, int F) {
+  WideLayout L{};
+  const int F_aug = F + 8;
+  L.Kp = (K + TILE_COLS - 1) / TILE_COLS * TILE_COLS;
+  const int tiles = (L.Kp / TILE_COLS) * ((F_aug + TILE_COLS - 1) / TILE_COLS);
+  int64_t rg = (2048 + tiles - 1) / tiles;
+  const int64_t max_rg = (B + 255) / 256;
+  if (rg > max_rg) rg = max_rg;
+  if (rg < 1) rg = 1;
+  L.rows_per_group = ((B + rg - 1) / rg + TILE_ROWS - 1) / TILE_ROWS * TILE_ROWS;
+  L.row_groups = (int)((B + L.rows_per_group - 1) / L.rows_per_group);
+  L.g_blocks = (int)((B + G_ROWS_PER_BLOCK - 1) / G_ROWS_PER_BLOCK);
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  size_t o = 0;
+  L.rowstat_off = o;
+  o = al(o + (size_t)B * sizeof(float2));
+  L.z_off = o;
+  o = al(o + (size_t)B * K * sizeof(float));
+  L.g_off = o;
+  o = al(o + (size_t)B * L.Kp * sizeof(uint16_t));
+  L.dw_off = o;
+  o = al(o + (size_t)L.row_groups * K * F_aug * sizeof(float));
+  L.stat_off = o;
+  o = al(o + (size_t)L.g_blocks * 2 * sizeof(float));
+  L.total = o;
+  return L;
+}
+
+}  // namespace
+
+bool softmax_grad_wide_supported(int F) { return F > 512 && F % 256 == 0; }
+
+size_t softmax_grad_wide_workspace(int64_t B, int K, int F) { return wide_layout(B, K, F).total; }
+
+void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
+                              int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,
+                              size_t ws_bytes, hipStream_t stream, const Sgd2D* update, P2PAllReduce* dp,
+                              int dp_timeout_ms) {
+  if (B <= 0) return;
+  if (!softmax_grad_wide_supported(F)) throw std::invalid_argument("softmax_grad_wide: F must be a multiple of 256 above 512");
+  if (ldx != F + 8) throw std::invalid_argument("softmax_grad_wide: X_aug row stride must be F + 8");
+  if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
+    throw std::invalid_argument("softmax_grad_wide: multiclass kinds only");
+  if (update != nullptr && (update->params == nullptr || update->cols != F + 8 || update->pen_cols > F))
+    throw std::invalid_argument("softmax_grad_wide: fused update needs params [K, F + 8]");
+  if (reinterpret_cast<uintptr_t>(X_aug) % 16 != 0 || reinterpret_cast<uintptr_t>(W) % 16 != 0)
+    throw std::invalid_argument("softmax_grad_wide: X_aug and W must be 16-byte aligned");
+  const WideLayout L = wide_layout(B, K, F);
+  if (ws_bytes < L.total) throw std::invalid_argument("softmax_grad_wide: workspace too small");
+  unsigned char* ws = static_cast<unsigned char*>(workspace);
+  float2* rowstat = reinterpret_cast<float2*>(ws + L.rowstat_off);
+  float* Z = reinterpret_cast<float*>(ws + L.z_off);
+  uint16_t* G = reinterpret_cast<uint16_t*>(ws + L.g_off);
+  float* slabs = reinterpret_cast<float*>(ws + L.dw_off);
+  float* stat_slabs = reinterpret_cast<float*>(ws + L.stat_off);
+  launch_softmax_rowstats(X_aug, ldx, W, b, B, F, K, kind, rowstat, nullptr, 0, stream);
+  launch_gemm_logits_ld(X_aug, ldx, W, b, B, F, K, Z, stream);
+  if (kind == KIND_OVR)
+    hipLaunchKernelGGL(softmax_g_kernel<true>, dim3((unsigned)L.g_blocks), dim3(64 * G_ROWS_PER_BLOCK), 0, stream, Z,
+                       rowstat, y, B, K, L.Kp, G, stat_slabs);
+  else
+    hipLaunchKernelGGL(softmax_g_kernel<false>, dim3((unsigned)L.g_blocks), dim3(64 * G_ROWS_PER_BLOCK), 0, stream, Z,
+                       rowstat, y, B, K, L.Kp, G, stat_slabs);
+  MLAPI_HIP_CHECK(hipGetLastError());
+  const int F_aug = F + 8;
+  const dim3 grid((unsigned)(L.Kp / TILE_COLS), (unsigned)((F_aug + TILE_COLS - 1) / TILE_COLS), (unsigned)L.row_groups);
+  hipLaunchKernelGGL(gdw_gemm_kernel, grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug), ldx,
+                     F_aug, B, K, L.rows_per_group, slabs);
+  MLAPI_HIP_CHECK(hipGetLastError());
+  launch_gdw_reduce(slabs, L.row_groups, K, F_aug, dW_out, stat_slabs, L.g_blocks, stats_out, update, dp,
+                    dp_timeout_ms, stream);
+}
+
+}  // namespace mlapi

@@ -38,6 +38,7 @@ SOURCES = [
     "kernels/pack.hip",
     "kernels/shard.hip",
     "kernels/softmax_grad_dw.hip",
+    "kernels/softmax_grad_wide.hip",
     "runtime/engine.cpp",
     "runtime/direct_dispatch.cpp",
     "http/server.cpp",

@@ -127,8 +127,6 @@ class LogisticRegression:
         from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer
 
         n, F = X.shape
-        if F > 512:
-            raise ValueError("solver='sgd' multiclass supports up to 512 features")
         yi = torch.as_tensor(np.searchsorted(classes, y).astype(np.int32), device=dev)
         kind = Kind.OVR if self.multi_class == "ovr" else Kind.MULTINOMIAL
         # the trainer zero-pads F to its kernel width; padded weights get zero gradients and stay 0

@@ -228,15 +228,15 @@ SOFTMAX_TRAIN_WIDTHS = (128, 256, 512)
 
 
 def softmax_kernel_width(F: int) -> int:
-    """Feature width the fused gradient kernel trains at: F rounded up to 128 / 256 / 512.
+    """Feature width the multiclass training kernels run at: F rounded up to 128 / 256 / 512 (the
+    fused gradient kernel), or to a multiple of 256 above 512 (softmax_grad_wide.hip).
 
     Narrower models are zero-padded: padded columns of X are 0, so their weights get a zero
     gradient (and a zero L2 / momentum term) and stay exactly 0 - the trained model is the same."""
     for w in SOFTMAX_TRAIN_WIDTHS:
         if int(F) <= w:
             return w
-    raise ValueError(f"softmax training kernels support up to F = 512 features (got {F}); shard wider models "
-                     "over GPUs (parallel.tensor_parallel.FeatureShardedLinear)")
+    return (int(F) + 255) // 256 * 256
 
 
 def softmax_train_faug(F: int) -> int:
@@ -269,10 +269,13 @@ class SoftmaxTrainBuffers:
 
     def __init__(self, B: int, K: int, F: int, device):
         self.B, self.K, self.F = B, K, F
-        if not C().softmax_grad_dw_supported(F):
-            raise ValueError(f"fused gradient kernel width must be one of {SOFTMAX_TRAIN_WIDTHS} (got {F})")
+        self.wide = C().softmax_grad_wide_supported(F)
+        if not (self.wide or C().softmax_grad_dw_supported(F)):
+            raise ValueError(f"training kernel width must be one of {SOFTMAX_TRAIN_WIDTHS} or a multiple of 256 "
+                             f"above 512 (got {F})")
         self.stats = torch.zeros(2, dtype=torch.float32, device=device)
-        self.ws = torch.zeros(C().softmax_grad_dw_workspace(B, K, F), dtype=torch.uint8, device=device)
+        nbytes = (C().softmax_grad_wide_workspace(B, K, F) if self.wide else C().softmax_grad_dw_workspace(B, K, F))
+        self.ws = torch.zeros(nbytes, dtype=torch.uint8, device=device)
 
 
 def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y: torch.Tensor, kind: int,
@@ -299,8 +302,10 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
         raise TypeError("softmax_train_grad: X_aug, W bf16, b f32 and y int32")
     B, F_aug = X_aug.shape
     K, F = W.shape
-    if F not in SOFTMAX_TRAIN_WIDTHS or F_aug != F + 8 or b.numel() != K or y.numel() != B:
-        raise ValueError("softmax_train_grad: shape mismatch (W must be [K, Fk], Fk in 128/256/512, X_aug [B, Fk + 8])")
+    if (F not in SOFTMAX_TRAIN_WIDTHS and not C().softmax_grad_wide_supported(F)) or F_aug != F + 8 \
+            or b.numel() != K or y.numel() != B:
+        raise ValueError("softmax_train_grad: shape mismatch (W must be [K, Fk], Fk in 128/256/512 or a multiple "
+                         "of 256 above 512, X_aug [B, Fk + 8])")
     if bufs is None or bufs.B != B or bufs.K != K or bufs.F != F:
         bufs = SoftmaxTrainBuffers(B, K, F, X_aug.device)
     stats = bufs.stats if stats_out is None else stats_out
@@ -318,9 +323,10 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
                    shadow_b=ptr(update.get("shadow_b")), pen_cols=F, lr=float(update["lr"]),
                    inv_n=float(update["inv_n"]), l2=float(update.get("l2", 0.0)),
                    momentum=float(update.get("momentum", 0.0)))
-    C().softmax_grad_dw(X_aug.data_ptr(), F_aug, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
-                        dW_out.data_ptr(), stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(), _stream(), **upd,
-                        p2p=None if p2p is None else p2p.native, timeout_ms=int(timeout_ms))
+    launch = C().softmax_grad_wide if bufs.wide else C().softmax_grad_dw  # F > 512: softmax_grad_wide.hip
+    launch(X_aug.data_ptr(), F_aug, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
+           dW_out.data_ptr(), stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(), _stream(), **upd,
+           p2p=None if p2p is None else p2p.native, timeout_ms=int(timeout_ms))
     return dW_out, stats
 
 

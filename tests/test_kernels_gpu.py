@@ -304,6 +304,50 @@ def test_softmax_grad_dw_fused(B, F, K, kind, groups, nc, pipe):
     assert torch.all(dW2[:, F:Fk] == 0) and torch.all(dW2[:, Fk + 1:] == 0)  # padded features, pad columns
 
 
+@pytest.mark.parametrize("B,F,K,kind", [(2048, 1024, 100, Kind.MULTINOMIAL), (777, 700, 37, Kind.OVR),
+                                        (4099, 1024, 1000, Kind.MULTINOMIAL), (65, 2048, 3, Kind.MULTINOMIAL)])
+def test_softmax_grad_wide(B, F, K, kind):
+    """Wide multiclass gradient (F > 512, softmax_grad_wide.hip: row stats + logits by the row-group
+    kernel, G in bf16, G^T X_aug by the transposed-LDS MFMA kernel, slab sum) vs the fp32 oracle;
+    reruns bitwise identical; padded feature columns get exactly zero gradient."""
+    Fa = ops.softmax_train_faug(F)
+    Fk = Fa - 8
+    assert Fk % 256 == 0 and Fk > 512
+    X = _rand((B, F), torch.float32, 51)
+    W, b = _rand((K, F), torch.float32, 52, scale=2 / np.sqrt(F)), _rand((K,), torch.float32, 53)
+    y = torch.randint(0, K, (B,), generator=torch.Generator().manual_seed(54), dtype=torch.int32).to(DEV)
+    Xa = ops.augment_features(X, Fa)
+    Wb = torch.zeros(K, Fk, dtype=torch.bfloat16, device=DEV)
+    Wb[:, :F] = W.to(torch.bfloat16)
+    bufs = ops.SoftmaxTrainBuffers(B, K, Fk, X.device)
+    assert bufs.wide
+    dW1, st1 = ops.softmax_train_grad(Xa, Wb, b, y, kind, bufs=bufs)
+    dW1, st1 = dW1.clone(), st1.clone()
+    dW2, st2 = ops.softmax_train_grad(Xa, Wb, b, y, kind, bufs=bufs)
+    torch.cuda.synchronize()
+    assert torch.equal(dW1, dW2) and torch.equal(st1, st2)
+    _, dW_ref, loss_ref, corr_ref = ref.softmax_train_ref(Xa, y, ops.augment_weights(Wb.float(), b, Fa), kind)
+    scale = dW_ref.abs().max().item() + 1e-6
+    err = (dW2 - dW_ref).abs().max().item()
+    assert err < 1e-2 * scale + 1e-2 * np.sqrt(B / 1000), (err, scale)
+    torch.testing.assert_close(dW2[:, Fk], dW_ref[:, Fk], atol=2e-2 * np.sqrt(B / 100), rtol=1e-2)  # intercept
+    assert st2[0].item() == pytest.approx(loss_ref.item(), rel=1e-4)
+    assert abs(st2[1].item() - corr_ref.item()) <= max(2, B // 2000)
+    assert torch.all(dW2[:, F:Fk] == 0) and torch.all(dW2[:, Fk + 1:] == 0)
+
+
+def test_sgd_wide_multiclass_estimator_one_gpu():
+    """LogisticRegression(solver='sgd') on an F = 1024 multiclass problem trains on ONE GPU (no
+    sharding, no vendor GEMM) and learns it."""
+    from mlapi_amd.models.estimator import LogisticRegression
+    from mlapi_amd.train.softmax_sgd import synthetic_multiclass
+
+    X, y = synthetic_multiclass(6000, 1024, 5, seed=3, noise=0.1)
+    est = LogisticRegression(solver="sgd", epochs=8, device="cuda:0").fit(X.numpy(), y.numpy())
+    acc = (est.predict(X.numpy()) == y.numpy()).mean()
+    assert acc > 0.9, acc
+
+
 def test_sgd_update_2d():
     K, Fa, F = 9, 40, 32
     p = _rand((K, Fa), torch.float32, 20)
