@@ -340,6 +340,11 @@ def bench_gemm(args, info):
             X, W = X.float(), W.float()
         op = ops.LinearSplit(B, K, info.device)
     else:
+        forced = {"tiles": 1, "rows": 2, "t32": 3, "ws": 4}.get(args.gemm_kernel, 0)
+        if forced:
+            from mlapi_amd._native import C
+
+            C().gemm_softmax_force_plan(0, 0, forced)
         op = ops.GemmSoftmax(B, K, F, info.device)
     out = (torch.empty(B, dtype=torch.int32, device=info.device), torch.empty(B, device=info.device))
     for _ in range(args.warmup):
@@ -350,7 +355,8 @@ def bench_gemm(args, info):
     tflops = 2 * B * F * K * args.steps / elapsed / 1e12
     return ("rows_per_sec_softmax_predict", value, "rows/s", elapsed,
             {"tflops_per_gpu": tflops, "us_per_call": elapsed / args.steps * 1e6, "launch": args.launch,
-             "kernel": "linear_split" if isinstance(op, ops.LinearSplit) else "gemm_softmax", "dtype": args.gemm_dtype},
+             "kernel": "linear_split" if isinstance(op, ops.LinearSplit) else "gemm_softmax",
+             "gemm_kernel": args.gemm_kernel, "dtype": args.gemm_dtype},
             {"model": "softmax regression F=256 K=1000", "global_batch": B * info.world, "seq_len": 1,
              "features": F, "parallelism": f"dp{info.world}"})
 
@@ -448,8 +454,9 @@ def main(argv=None) -> int:
     ap.add_argument("--c1-requests", type=int, default=3000)
     ap.add_argument("--rows", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=1024)
-    ap.add_argument("--gemm-kernel", default="auto", choices=["auto", "split"],
-                    help="gemm: auto = the tiles kernel; split = the class-split small-batch kernel")
+    ap.add_argument("--gemm-kernel", default="auto", choices=["auto", "split", "tiles", "rows", "t32", "ws"],
+                    help="gemm: auto = the planner's choice; split = the class-split small-batch kernel; "
+                         "tiles / rows / t32 / ws = that gemm_softmax kernel forced (measurement)")
     ap.add_argument("--gemm-dtype", default="bf16", choices=["bf16", "f32"], help="gemm: f32 runs the split kernel")
     ap.add_argument("--launch", default="graph", choices=["graph", "eager"],
                     help="gemv/gemm: the timed K calls replayed from one captured HIP graph (GPU time) or "
@@ -504,7 +511,7 @@ def main(argv=None) -> int:
     args.pinned_cpus = len(pinned)
     if args.io_threads <= 0 or args.client_threads <= 0:
         # Server IO threads and load-generator threads share this rank's CPUs (sweep on a 16-CPU
-        # MI355X box share: 6 + 6 threads -> 519k req/s vs 3 + 3 -> 270k; tools/serve_sweep.sh).
+        # MI355X box share: 6 + 6 threads -> 519k req/s vs 3 + 3 -> 270k; tools/gpu_session.sh threads).
         # The CPU budget is the cgroup quota, not the affinity mask (a 1-GPU box: 256 CPUs in the
         # mask, cpu.max = 16 cores), shared by the ranks of this node.
         from mlapi_amd.utils.threads import effective_cpus

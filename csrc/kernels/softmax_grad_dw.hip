@@ -563,13 +563,14 @@ __global__ __launch_bounds__(256) void gdw_reduce_kernel(const f32x4_t* __restri
     __syncthreads();
     float st = 0.f;
     if (threadIdx.x < 2) st = (red[threadIdx.x] + red[2 + threadIdx.x]) + (red[4 + threadIdx.x] + red[6 + threadIdx.x]);
-    if constexpr (DP) {
+    if (DP && dp.world > 1) {  // one rank: nothing to exchange (the same kernel, no peers)
       float* xs = dp.mine + 4 * (int64_t)width4;
       if (threadIdx.x < 2) xs[threadIdx.x] = st;
       if (!p2p_block_sync(dp, blockIdx.x)) return;
       if (threadIdx.x < 2) {
-        st = dp.peer[0][4 * (int64_t)width4 + threadIdx.x];
-        for (int r = 1; r < dp.world; ++r) st += dp.peer[r][4 * (int64_t)width4 + threadIdx.x];
+        const float own = st;  // this rank's slice from registers, not re-read from the buffer
+        st = dp.rank == 0 ? own : dp.peer[0][4 * (int64_t)width4 + threadIdx.x];
+        for (int r = 1; r < dp.world; ++r) st += r == dp.rank ? own : dp.peer[r][4 * (int64_t)width4 + threadIdx.x];
       }
     }
     if (threadIdx.x < 2) stats_out[threadIdx.x] = st;
@@ -591,12 +592,13 @@ __global__ __launch_bounds__(256) void gdw_reduce_kernel(const f32x4_t* __restri
       s += __builtin_nontemporal_load(slabs + (int64_t)i * width4 + j);
     }
   }
-  if constexpr (DP) {
+  if (DP && dp.world > 1) {
     if (active) reinterpret_cast<f32x4_t*>(dp.mine)[j] = s;
     if (!p2p_block_sync(dp, blockIdx.x)) return;  // peer missing: status recorded, no update
-    if (active) {
-      s = reinterpret_cast<const f32x4_t*>(dp.peer[0])[j];
-      for (int r = 1; r < dp.world; ++r) s += reinterpret_cast<const f32x4_t*>(dp.peer[r])[j];
+    if (active) {  // rank order; the own slice from registers (same bits as the published copy)
+      const f32x4_t own = s;
+      s = dp.rank == 0 ? own : reinterpret_cast<const f32x4_t*>(dp.peer[0])[j];
+      for (int r = 1; r < dp.world; ++r) s += r == dp.rank ? own : reinterpret_cast<const f32x4_t*>(dp.peer[r])[j];
     }
   }
   if (!active) return;

@@ -258,13 +258,14 @@ __global__ __launch_bounds__(256) void reduce_slabs_kernel(const T* __restrict__
 #pragma unroll
     for (int q = 1; q < RED_PARTS; ++q) t += part[q][c];
   }
-  if constexpr (DP) {
-    static_assert(sizeof(T) == sizeof(float), "fused DP exchange: f32 gradients");
+  static_assert(!DP || sizeof(T) == sizeof(float), "fused DP exchange: f32 gradients");
+  if (DP && dp.world > 1) {  // one rank: nothing to exchange (the same kernel, no peers)
     if (p == 0 && j < width) dp.mine[j] = (float)t;
     if (!p2p_block_sync(dp, blockIdx.x)) return;  // peer missing: status recorded, no update
-    if (p == 0 && j < width) {
-      float g = dp.peer[0][j];
-      for (int r = 1; r < dp.world; ++r) g += dp.peer[r][j];
+    if (p == 0 && j < width) {  // rank order; the own slice from registers (same bits as the published copy)
+      const float own = (float)t;
+      float g = dp.rank == 0 ? own : dp.peer[0][j];
+      for (int r = 1; r < dp.world; ++r) g += r == dp.rank ? own : dp.peer[r][j];
       t = (T)g;
     }
   }

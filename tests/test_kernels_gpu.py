@@ -82,11 +82,12 @@ def test_gemv_binary_large_stream():
     torch.testing.assert_close(p, torch.sigmoid(z.abs()), rtol=1e-4, atol=1e-4)
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "tiles", "rows", "t32"])
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["auto", "tiles", "rows", "t32", "ws"])
 def gemm_kernel(request):
     """Run a multiclass test under the automatic plan and with each kernel forced (tiles: the
     LDS-staged, chunk-pipelined 16x16x32 kernel; rows: the row-group kernel; t32: the 32x32x16
-    large-batch kernel, F in {64, 128, 256}, else tiles)."""
+    large-batch kernel, F in {64, 128, 256}, else tiles; ws: the W-stationary persistent kernel,
+    F in {128, 256}, else tiles)."""
     from mlapi_amd._native import C
 
     C().gemm_softmax_force_plan(0, 0, request.param)
@@ -96,7 +97,8 @@ def gemm_kernel(request):
 
 @pytest.mark.parametrize("B,F,K", [(1024, 256, 1000), (1, 256, 1000), (130, 64, 10), (2048, 128, 37),
                                    (4096, 256, 3), (100, 512, 200), (37, 32, 65), (20000, 256, 130),
-                                   (300, 1024, 100), (65, 4096, 1000), (5, 700, 12)])
+                                   (300, 1024, 100), (65, 4096, 1000), (5, 700, 12), (5000, 256, 600),
+                                   (3000, 128, 1100)])
 @pytest.mark.parametrize("kind", [Kind.MULTINOMIAL, Kind.OVR])
 def test_gemm_softmax(B, F, K, kind, gemm_kernel):
     """Both multiclass kernels vs the fp64 oracle on bf16 operands; F > 512 (row-group kernel, F

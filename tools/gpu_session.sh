@@ -21,6 +21,10 @@
 #   kbench        gemv / gemm / train / train_softmax benches
 #   prof          rocprofv3 --kernel-trace --stats of every bench mode (incl. serve and serve_wide)
 #   pmc_gemm      hardware counters of the gemm bench (tools/pmc_profile.sh)
+#   gemm_ws       W-stationary persistent gemm_softmax kernel vs the 32x32 kernel (tests, A/B x2, kernel stats)
+#   threads       IO-thread / load-generator-thread split sweep, THREADS="io:cl ..." (default "10:4 8:6 6:6"), x2
+#   gdw           softmax G+dW kernel: its GPU tests + tools/softmax_train_sweep.py timings
+#   gemm_ab       interleaved x3 gemm bench: ab_old/mlapi_amd (stashed previous build) vs the working tree
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
@@ -43,7 +47,11 @@ prof() {  # prof <name> <limit_s> <bench args...>
      -- python3 "$R/bench.py" "$@" > "$O/prof_$name.log" 2>&1)
   local rc=$?
   [ $rc -eq 0 ] || stop "prof_$name" $rc "$O/prof_$name.log"
+  trim
   tail -1 "$O/prof_$name.log" | cut -c1-300
+}
+trim() {  # gpurun copies gpurun_out/ back only below 64 MiB: keep the --stats summaries, drop big traces
+  find "$O" -name '*_trace.csv' -size +6M -delete
 }
 steps="${*:-test smoke serve kbench prof}"
 for s in $steps; do
@@ -67,6 +75,7 @@ for s in $steps; do
       (cd /tmp && MLAPI_ROCTX=1 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv \
          -d "$O/prof_marker_serve_wide" -o serve_wide -- python3 "$R/bench.py" --mode serve_wide --steps 3 --warmup 1 \
          --reqs-per-conn 128 --c1-requests 300 > "$O/prof_marker_serve_wide.log" 2>&1) || stop marker_wide $? "$O/prof_marker_serve_wide.log"
+      trim
       tail -1 "$O/prof_marker_serve.log" | cut -c1-200 ;;
     serve_ab)
       for r in 1 2; do
@@ -157,6 +166,34 @@ for s in $steps; do
       prof serve 300 --steps 20 --warmup 2 --reqs-per-conn 512
       prof serve_wide 300 --mode serve_wide --steps 10 --warmup 2 --reqs-per-conn 256 ;;
     pmc_gemm) PMC_BENCHES="gemm:--mode gemm --steps 5 --warmup 1|gemm_big:--mode gemm --batch 262144 --steps 5 --warmup 1" run pmc_gemm 600 bash tools/pmc_profile.sh ;;
+    gemm_ws)  # W-stationary persistent kernel vs the 32x32 kernel: tests, interleaved benches, kernel stats
+      run pytest_gemm 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "gemm or softmax"
+      for r in 1 2; do
+        for kk in t32 ws; do
+          run "gemm_${kk}_b262144_r$r" 120 python -u bench.py --mode gemm --batch 262144 --steps 200 --warmup 10 --gemm-kernel $kk
+          run "gemm_${kk}_b65536_r$r" 120 python -u bench.py --mode gemm --batch 65536 --steps 500 --warmup 10 --gemm-kernel $kk
+        done
+      done
+      run bench_train_softmax 300 python -u bench.py --mode train_softmax --steps 100 --warmup 10
+      prof gemm_ws_b262144 120 --mode gemm --batch 262144 --steps 20 --warmup 2 --gemm-kernel ws
+      prof gemm_t32_b262144 120 --mode gemm --batch 262144 --steps 20 --warmup 2 --gemm-kernel t32
+      prof train_softmax_ws 300 --mode train_softmax --steps 20 --warmup 2 ;;
+    threads)
+      for r in 1 2; do
+        for tc in ${THREADS:-10:4 8:6 6:6}; do
+          run "sweep_io${tc%%:*}_cl${tc##*:}_r$r" 300 python -u bench.py --steps 60 --warmup 5 \
+            --io-threads "${tc%%:*}" --client-threads "${tc##*:}" --c1-requests 1000
+        done
+      done ;;
+    gdw)
+      run pytest_gdw 240 python -u -m pytest tests/test_kernels_gpu.py -k "softmax_grad" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+      run gdw_sweep 180 python -u tools/softmax_train_sweep.py ;;
+    gemm_ab)
+      for r in 1 2 3; do
+        run "gemm_old_r$r" 120 python -c "import sys, runpy; sys.path.insert(0, 'ab_old'); sys.argv = ['bench.py'] + sys.argv[1:]; runpy.run_path('bench.py', run_name='__main__')" \
+          --mode gemm --steps 2000 --warmup 100 ${EXTRA:-}
+        run "gemm_new_r$r" 120 python -u bench.py --mode gemm --steps 2000 --warmup 100 ${EXTRA:-}
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
