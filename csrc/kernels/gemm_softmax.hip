@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -1549,7 +1550,14 @@ bool ws_plan(int64_t B, int K, int F, Plan& p) {
 // allow32 = false for the logits mode (only the 16x16 kernel writes Z)
 Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   Plan p;
-  if (allow32 && (g_force_kernel == 4 || (g_force_kernel == 0 && B >= 16384)) && ws_plan(B, K, F, p)) return p;
+  // W-stationary kernel: forced (4), or automatic for large batches once enabled (MLAPI_GEMM_WS=1;
+  // off by default until its A/B against the 32x32 kernel is measured on the box)
+  static const bool ws_auto = [] {
+    const char* e = getenv("MLAPI_GEMM_WS");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  if (allow32 && (g_force_kernel == 4 || (g_force_kernel == 0 && ws_auto && B >= 16384)) && ws_plan(B, K, F, p))
+    return p;
   if (allow32 && t32_supported(F)) {
     if (g_force_kernel == 3 || g_force_kernel >= 5) p.k32 = 4;  // 5-8: 32x32 measurement variants
     else if (g_force_kernel == 0 && B >= 16384) p.k32 = 4;

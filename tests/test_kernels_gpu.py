@@ -1,4 +1,6 @@
 """T3: every HIP kernel vs a plain PyTorch fp64/fp32 reference of the same op."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -90,6 +92,8 @@ def gemm_kernel(request):
     F in {128, 256}, else tiles)."""
     from mlapi_amd._native import C
 
+    if request.param == 4 and os.environ.get("MLAPI_GEMM_WS", "0") == "0":
+        pytest.skip("W-stationary kernel is opt-in (MLAPI_GEMM_WS=1) until measured on the box")
     C().gemm_softmax_force_plan(0, 0, request.param)
     yield request.param
     C().gemm_softmax_force_plan(0, 0, 0)

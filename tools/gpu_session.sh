@@ -167,17 +167,20 @@ for s in $steps; do
       prof serve_wide 300 --mode serve_wide --steps 10 --warmup 2 --reqs-per-conn 256 ;;
     pmc_gemm) PMC_BENCHES="gemm:--mode gemm --steps 5 --warmup 1|gemm_big:--mode gemm --batch 262144 --steps 5 --warmup 1" run pmc_gemm 600 bash tools/pmc_profile.sh ;;
     gemm_ws)  # W-stationary persistent kernel vs the 32x32 kernel: tests, interleaved benches, kernel stats
-      run pytest_gemm 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "gemm or softmax"
+      MLAPI_GEMM_WS=1 run pytest_gemm 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "gemm or softmax"
       for r in 1 2; do
         for kk in t32 ws; do
           run "gemm_${kk}_b262144_r$r" 120 python -u bench.py --mode gemm --batch 262144 --steps 200 --warmup 10 --gemm-kernel $kk
           run "gemm_${kk}_b65536_r$r" 120 python -u bench.py --mode gemm --batch 65536 --steps 500 --warmup 10 --gemm-kernel $kk
         done
       done
-      run bench_train_softmax 300 python -u bench.py --mode train_softmax --steps 100 --warmup 10
+      for r in 1 2; do
+        run "bench_train_softmax_t32_r$r" 300 python -u bench.py --mode train_softmax --steps 100 --warmup 10
+        MLAPI_GEMM_WS=1 run "bench_train_softmax_ws_r$r" 300 python -u bench.py --mode train_softmax --steps 100 --warmup 10
+      done
       prof gemm_ws_b262144 120 --mode gemm --batch 262144 --steps 20 --warmup 2 --gemm-kernel ws
       prof gemm_t32_b262144 120 --mode gemm --batch 262144 --steps 20 --warmup 2 --gemm-kernel t32
-      prof train_softmax_ws 300 --mode train_softmax --steps 20 --warmup 2 ;;
+      MLAPI_GEMM_WS=1 prof train_softmax_ws 300 --mode train_softmax --steps 20 --warmup 2 ;;
     threads)
       for r in 1 2; do
         for tc in ${THREADS:-10:4 8:6 6:6}; do
