@@ -19,6 +19,9 @@
 //    re-admitted when its health probe succeeds (the round-2 leave/rejoin semantics).
 //  * failover: a member whose channel breaks (the leader died or stopped) runs the election again;
 //    the winner re-binds the TCP port and the others re-join it. A restarted replica simply joins.
+//  * trust: both ends check SO_PEERCRED - a member must run as the leader's user (the abstract
+//    name is visible to every process of the network namespace), and a member only accepts
+//    sockets from a leader of its own user.
 //  * port 0: the process binds an ephemeral TCP port first and names the group after it (it is
 //    the leader by construction; the others are given the bound port).
 #pragma once
