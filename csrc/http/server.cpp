@@ -364,9 +364,10 @@ struct Conn {
   uint64_t t_req = 0;         // rdtsc when the outstanding request was fully parsed
 };
 
-struct FastBatch {
+// A run of engine completions that share one model (render_fast's unit).
+struct FastSeg {
+  size_t begin;  // index of the run's first completion
   std::shared_ptr<const Model> model;
-  std::vector<Completion> c;
 };
 
 struct SlowResp {
@@ -463,7 +464,9 @@ class IoThread : public Sink {
   void on_complete(const Completion* c, size_t n, const std::shared_ptr<const Model>& model) override {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      fast_.push_back(FastBatch{model, std::vector<Completion>(c, c + n)});
+      // appended to reusable buffers (no allocation per hand-off once they have grown)
+      if (fast_seg_.empty() || fast_seg_.back().model != model) fast_seg_.push_back(FastSeg{fast_c_.size(), model});
+      fast_c_.insert(fast_c_.end(), c, c + n);
     }
     wake();
   }
@@ -564,9 +567,8 @@ class IoThread : public Sink {
       if (ran) {
         pend_x_.clear();
         pend_tags_.clear();
-        FastBatch fb{std::move(m), std::move(idle_done_)};
-        idle_done_ = std::vector<Completion>();
-        render_fast(fb);  // may parse pipelined requests into pend_*: flushed on the next round
+        render_fast(m, idle_done_.data(), idle_done_.size());  // may parse pipelined requests into
+                                                               // pend_*: flushed on the next round
         return;
       }
     }
@@ -889,20 +891,21 @@ class IoThread : public Sink {
 
   // Responses of one batch of fast-path completions (each one then dispatches its connection's
   // pipelined requests and flushes).
-  void render_fast(const FastBatch& fb) {
+  void render_fast(const std::shared_ptr<const Model>& model, const Completion* comps, size_t ncomp) {
     std::string& body = body_;
     Stage sg(this, SS_RENDER);
-    for (const Completion& cp : fb.c) {
+    for (size_t ci = 0; ci < ncomp; ++ci) {
+      const Completion& cp = comps[ci];
       auto it = conns_.find(cp.tag);
       if (it == conns_.end()) continue;  // client went away
       Conn* c = it->second.get();
       c->waiting = false;
       const uint64_t t_req = c->t_req;
-      bool ok = cp.status == ST_OK && fb.model && cp.idx >= 0 && (size_t)cp.idx < fb.model->label_json.size();
+      bool ok = cp.status == ST_OK && model && cp.idx >= 0 && (size_t)cp.idx < model->label_json.size();
       if (ok) {
         body.clear();
         body += "{\"prediction\":";
-        body += fb.model->label_json[cp.idx];
+        body += model->label_json[cp.idx];
         body += ",\"probability\":";
         ok = append_py_float(body, cp.p);
         body += '}';
@@ -924,14 +927,19 @@ class IoThread : public Sink {
 
   void drain_pending() {
     Stage sg(this, SS_HANDOFF);
-    std::vector<FastBatch> fast;
+    // double-buffered: the spare vectors keep their capacity, so a hand-off allocates nothing
+    std::vector<Completion>& fast_c = spare_c_;
+    std::vector<FastSeg>& fast_seg = spare_seg_;
+    fast_c.clear();
+    fast_seg.clear();
     std::vector<SlowResp> slow;
     std::vector<int> adopted;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      fast.swap(fast_);
-      slow.swap(slow_);
-      adopted.swap(adopted_);
+      fast_c.swap(fast_c_);
+      fast_seg.swap(fast_seg_);
+      if (!slow_.empty()) slow.swap(slow_);
+      if (!adopted_.empty()) adopted.swap(adopted_);
     }
     for (int fd : adopted) {
       sockaddr_storage ss{};
@@ -939,7 +947,10 @@ class IoThread : public Sink {
       getpeername(fd, reinterpret_cast<sockaddr*>(&ss), &sl);
       register_conn(fd, ss);
     }
-    for (FastBatch& fb : fast) render_fast(fb);
+    for (size_t k = 0; k < fast_seg.size(); ++k) {
+      const size_t b = fast_seg[k].begin, e = k + 1 < fast_seg.size() ? fast_seg[k + 1].begin : fast_c.size();
+      render_fast(fast_seg[k].model, fast_c.data() + b, e - b);
+    }
     for (SlowResp& sr : slow) {
       auto it = conns_.find(sr.conn_id);
       if (it == conns_.end()) continue;
@@ -1310,7 +1321,10 @@ class IoThread : public Sink {
   int st_cur_ = SS_POLL;
   uint64_t lat_hist_[HTTP_LAT_BUCKETS] = {};
   uint64_t lat_sum_ = 0, lat_n_ = 0;
-  std::vector<FastBatch> fast_;
+  std::vector<Completion> fast_c_;  // completions handed over by the engine (guarded by mu_) ...
+  std::vector<FastSeg> fast_seg_;   // ... in runs of one model each
+  std::vector<Completion> spare_c_;  // drain_pending's side of the double buffer (this thread only)
+  std::vector<FastSeg> spare_seg_;
   std::vector<Completion> idle_done_;  // run_idle completions (this thread only)
   std::string body_;                   // response body scratch (this thread only)
   std::vector<SlowResp> slow_;
