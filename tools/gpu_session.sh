@@ -22,6 +22,7 @@
 #   prof          rocprofv3 --kernel-trace --stats of every bench mode (incl. serve and serve_wide)
 #   pmc_gemm      hardware counters of the gemm bench (tools/pmc_profile.sh)
 #   gemm_ws       W-stationary persistent gemm_softmax kernel vs the 32x32 kernel (tests, A/B x2, kernel stats)
+#   split_big     class-split kernel vs tiles kernel at B = 256 / 1024 / 2048, interleaved x2
 #   threads       IO-thread / load-generator-thread split sweep, THREADS="io:cl ..." (default "10:4 8:6 6:6"), x2
 #   gdw           softmax G+dW kernel: its GPU tests + tools/softmax_train_sweep.py timings
 #   gemm_ab       interleaved x3 gemm bench: ab_old/mlapi_amd (stashed previous build) vs the working tree
@@ -181,6 +182,13 @@ for s in $steps; do
       prof gemm_ws_b262144 120 --mode gemm --batch 262144 --steps 20 --warmup 2 --gemm-kernel ws
       prof gemm_t32_b262144 120 --mode gemm --batch 262144 --steps 20 --warmup 2 --gemm-kernel t32
       MLAPI_GEMM_WS=1 prof train_softmax_ws 300 --mode train_softmax --steps 20 --warmup 2 ;;
+    split_big)  # class-split kernel vs the tiles kernel at medium batches (B=1024 is BASELINE config 3)
+      for r in 1 2; do
+        for B in 256 1024 2048; do
+          run "gemm_tiles_b${B}_r$r" 120 python -u bench.py --mode gemm --batch $B --steps 2000 --warmup 50
+          run "gemm_split_b${B}_r$r" 120 python -u bench.py --mode gemm --batch $B --steps 2000 --warmup 50 --gemm-kernel split
+        done
+      done ;;
     threads)
       for r in 1 2; do
         for tc in ${THREADS:-10:4 8:6 6:6}; do
