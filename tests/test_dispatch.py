@@ -204,6 +204,17 @@ def test_bench_self_launches_n_ranks():
     assert all(abs(v - mean) <= 0.02 * mean for v in d["served_per_rank"]), d["served_per_rank"]
     assert d["comm_nranks"] == 4 and d["rccl_nranks"] is None  # gloo on CPU: no RCCL claimed
     assert set(d["allreduce_us"]) == {"1KiB", "1MiB"} and d["c1_bcast_us"] > 0
+    # the driver's line contract (task spec) and the round-3 host-CPU evidence
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["steps"] == 3 and d["warmup"] == 1 and d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert {"model", "global_batch", "seq_len", "parallelism"} <= set(d["config"])
+    cb = d["cpu_breakdown_rank0"]
+    assert cb["server_cpu_us_per_req"] > 0
+    assert set(cb["io_stage_us_per_req"]) == {"poll", "recv", "parse", "submit", "idle_gpu", "render", "send",
+                                              "handoff"}
+    assert d["dispatch"] == "acceptor"
 
 
 def test_bench_refuses_world_size_mismatch():
