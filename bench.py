@@ -78,7 +78,8 @@ def _comm_probe(info, model=None) -> dict:
 
     out = {"comm_nranks": info.comm_nranks()}
     kind = getattr(info.comm, "kind", info.backend)
-    out["rccl_nranks"] = (info.comm_nranks() if kind == "native-rccl" or info.backend == "nccl" else None)
+    out["rccl_nranks"] = (info.comm_nranks() if kind in ("native-rccl", "torch-rccl") or info.backend == "nccl"
+                          else None)
     if model is None:
         model = LinearModel.random(256, 1000, seed=3) if info.is_main else None
     barrier(info)

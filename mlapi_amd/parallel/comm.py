@@ -100,7 +100,7 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
             dist.init_process_group(backend=backend, **kw)
         info.backend = dist.get_backend()
     if comm == "native":
-        from mlapi_amd.parallel.rccl import FakeComm, NativeComm
+        from mlapi_amd.parallel.rccl import FakeComm, NativeComm, TorchRcclComm
 
         try:
             info.comm = NativeComm(rank, world, device)
@@ -108,15 +108,21 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
         except Exception as e:  # noqa: BLE001
             if not auto or world == 1:
                 raise
-            # auto mode: a rank set whose RCCL communicator cannot initialise (e.g. a node whose
-            # topology RCCL rejects) still runs, with the collectives on the host gloo group; the
-            # backend name says so in every bench line / log.
+            # auto mode: a rank set whose native communicator cannot initialise first tries
+            # torch.distributed's RCCL (still RCCL over xGMI), then the host gloo group; the backend
+            # name says which in every bench line / log (bench.py refuses to report "gloo-fallback").
             import sys
 
-            print(f"[mlapi] rank {rank}: RCCL communicator init failed ({e}); collectives fall back to gloo",
+            print(f"[mlapi] rank {rank}: native RCCL communicator init failed ({e}); trying torch's RCCL",
                   file=sys.stderr, flush=True)
-            info.comm = FakeComm(rank, world)
-            info.backend = "gloo-fallback"
+            try:
+                info.comm = TorchRcclComm(rank, world, device)
+                info.backend = TorchRcclComm.kind
+            except Exception as e2:  # noqa: BLE001
+                print(f"[mlapi] rank {rank}: torch RCCL group failed too ({e2}); collectives fall back to gloo",
+                      file=sys.stderr, flush=True)
+                info.comm = FakeComm(rank, world)
+                info.backend = "gloo-fallback"
     elif comm == "p2p":
         from mlapi_amd.parallel.p2p import P2PComm
 

@@ -201,6 +201,31 @@ class FakeComm:
         self.aborted = True
 
 
+class TorchRcclComm(FakeComm):
+    """torch.distributed's RCCL (the ``nccl`` backend) on a subgroup of all ranks, with NativeComm's
+    API. Auto mode's second choice when the native communicator cannot initialise: the data plane
+    stays on RCCL over xGMI (device tensors) instead of dropping to the host gloo group."""
+
+    kind = "torch-rccl"
+
+    def __init__(self, rank: int, world: int, device: torch.device):
+        import torch.distributed as dist
+
+        super().__init__(rank, world, group=dist.new_group(ranks=list(range(world)), backend="nccl"))
+        self.device = device
+        if world > 1:  # fail here, not in the first real collective
+            self.all_reduce_(torch.zeros(1, device=device))
+            torch.cuda.synchronize(device)
+
+    def barrier(self) -> None:
+        if self.world > 1:
+            self.all_reduce_(torch.zeros(1, device=self.device))
+            torch.cuda.synchronize(self.device)
+
+    def wait(self, timeout_ms: Optional[int] = None) -> None:
+        torch.cuda.current_stream(self.device).synchronize()
+
+
 def measure_all_reduce(comm, nbytes: int, iters: int = 20) -> float:
     """Latency (seconds) of an in-place f32 sum all-reduce of ``nbytes`` (bus-bandwidth probes)."""
     t = torch.ones(max(1, nbytes // 4), dtype=torch.float32, device=comm.device)
