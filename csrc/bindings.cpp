@@ -21,6 +21,7 @@
 #include "mlapi/kernels.h"
 #include "runtime/engine.h"
 #include "runtime/float_repr.h"
+#include "runtime/split_merge.h"
 
 namespace py = pybind11;
 using namespace mlapi;
@@ -200,6 +201,20 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("X"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"), py::arg("K"), py::arg("kind"),
       py::arg("out"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream") = 0);
+  m.def(
+      "merge_split_records",
+      [](const std::vector<int32_t>& bi, const std::vector<float>& m, const std::vector<float>& sm, bool ovr) {
+        // one row's per-block states in block order -> (label, p): the completer's host merge
+        const size_t ns = bi.size();
+        if (ns == 0 || ns > 64 || m.size() != ns || sm.size() != ns)
+          throw std::invalid_argument("merge_split_records: 1..64 blocks, equal lengths");
+        SplitRecord r[64];
+        for (size_t k = 0; k < ns; ++k) r[k] = SplitRecord{0u, bi[k], m[k], sm[k]};
+        int32_t label = 0;
+        const double p = merge_split_records(r, (int)ns, ovr, &label);
+        return py::make_tuple(label, p);
+      },
+      py::arg("argmax"), py::arg("max"), py::arg("sum"), py::arg("ovr"));
   m.def(
       "merge_rowstates",
       [](uintptr_t parts, int nparts, int64_t B, std::vector<int> offsets, int kind, uintptr_t out_idx,

@@ -1,5 +1,6 @@
 // Serving engine implementation (see engine.h for the design).
 #include "engine.h"
+#include "split_merge.h"
 
 #include <immintrin.h>
 
@@ -756,27 +757,11 @@ const int32_t* Engine::collect(Slot& s, std::vector<int32_t>& st, std::vector<do
     const bool ovr = s.model->kind == KIND_OVR;
     const int ns = s.rec_nsplit;
     for (size_t i = 0; i < n; ++i) {
-      double M = -INFINITY;
-      int bi = 0x7fffffff;
       alignas(16) SplitRecord r[64];
-      for (int sp = 0; sp < ns; ++sp) {
+      for (int sp = 0; sp < ns; ++sp)
         _mm_store_si128(reinterpret_cast<__m128i*>(&r[sp]),
                         load_record(reinterpret_cast<const ServeRecord*>(s.hsrec + (size_t)sp * 32 + i)));
-        const double m = r[sp].m;
-        if (m > M || (m == M && r[sp].bi < bi)) {
-          M = m;
-          bi = r[sp].bi;
-        }
-      }
-      double S = 0;
-      for (int sp = 0; sp < ns; ++sp) {
-        if (ovr)
-          S += r[sp].s;
-        else if (r[sp].m != -INFINITY)
-          S += (double)r[sp].s * std::exp((double)r[sp].m - M);
-      }
-      idx[i] = bi;
-      pd[i] = ovr ? (1.0 / (1.0 + std::exp(-M))) / S : 1.0 / S;
+      pd[i] = merge_split_records(r, ns, ovr, &idx[i]);
     }
     return idx.data();
   }

@@ -1,0 +1,36 @@
+// Host merge of the class-split kernel's per-block row states (linear_split.hip host-record mode):
+// ns records {seq, argmax, m, s} of one row, one per 64-class block in block order, -> (label, p).
+// In double: the max (first max wins on ties - lower block, then the block's own first index -
+// like numpy's argmax), then the sums rescaled to it. Softmax: p = 1 / sum_b s_b exp(m_b - M);
+// OvR: p = sigmoid(M) / sum_b s_b. The engine's completer runs it (Engine::collect); pure so CPU
+// tests can check it against the float64 oracle.
+#pragma once
+#include <cmath>
+#include <cstdint>
+
+#include "mlapi/kernels.h"
+
+namespace mlapi {
+
+inline double merge_split_records(const SplitRecord* r, int ns, bool ovr, int32_t* label) {
+  double M = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int sp = 0; sp < ns; ++sp) {
+    const double m = r[sp].m;
+    if (m > M || (m == M && r[sp].bi < bi)) {
+      M = m;
+      bi = r[sp].bi;
+    }
+  }
+  double S = 0;
+  for (int sp = 0; sp < ns; ++sp) {
+    if (ovr)
+      S += r[sp].s;
+    else if (r[sp].m != -INFINITY)
+      S += (double)r[sp].s * std::exp((double)r[sp].m - M);
+  }
+  *label = bi;
+  return ovr ? (1.0 / (1.0 + std::exp(-M))) / S : 1.0 / S;
+}
+
+}  // namespace mlapi
