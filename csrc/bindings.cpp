@@ -161,6 +161,18 @@ PYBIND11_MODULE(_C, m) {
       py::arg("dt"), py::arg("X"), py::arg("w"), py::arg("bias"), py::arg("B"), py::arg("F"), py::arg("kind"),
       py::arg("out_idx"), py::arg("out_p"), py::arg("stream") = 0);
   m.def("gemm_softmax_workspace", &gemm_softmax_workspace);
+  m.def("gemm_softmax_ws_plan", [](int64_t B, int K, int F, int cus_per_xcd) -> py::object {
+    int ns = 0, sc = 0, gpx = 0;
+    int64_t tpg = 0, grid = 0;
+    if (!gemm_softmax_ws_plan(B, K, F, cus_per_xcd, &ns, &sc, &gpx, &tpg, &grid)) return py::none();
+    py::dict d;
+    d["slices"] = ns;
+    d["slice_classes"] = sc;
+    d["groups_per_xcd"] = gpx;
+    d["tiles_per_group"] = tpg;
+    d["grid"] = grid;
+    return d;
+  });
   m.def("gemm_softmax_force_plan", &gemm_softmax_force_plan, py::arg("nt") = 0, py::arg("splits") = 0,
         py::arg("kernel") = 0);
   m.def("gemm_softmax_set_stamps", [](uintptr_t p) { gemm_softmax_set_stamps(reinterpret_cast<void*>(p)); });

@@ -1529,11 +1529,11 @@ int cus_per_xcd() {  // CUs of the current device / 8 XCDs (the dispatcher round
 }
 
 // W-stationary plan: class slices of 128 KiB, as many row groups per XCD as whole slice sets fit
-bool ws_plan(int64_t B, int K, int F, Plan& p) {
+bool ws_plan_for(int64_t B, int K, int F, int cus_xcd, Plan& p) {
   if (F != 128 && F != 256) return false;  // F = 64 spills SGPRs at 16 chunks per slice: the 32x32 kernel
   const int slice = (WS_SLICE_BYTES / (F * 2) / CLASS_CHUNK) * CLASS_CHUNK;
   const int ns = (K + slice - 1) / slice;
-  const int gpx = cus_per_xcd() / ns;
+  const int gpx = cus_xcd / ns;
   const int64_t tiles = (B + 31) / 32;
   if (gpx < 1 || tiles * 4 > COUNTER_BYTES) return false;
   p.ws = 1;
@@ -1546,6 +1546,8 @@ bool ws_plan(int64_t B, int K, int F, Plan& p) {
   p.row_blocks = 8LL * gpx * ns;  // the grid
   return true;
 }
+
+bool ws_plan(int64_t B, int K, int F, Plan& p) { return ws_plan_for(B, K, F, cus_per_xcd(), p); }
 
 // allow32 = false for the logits mode (only the 16x16 kernel writes Z)
 Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
@@ -1707,6 +1709,18 @@ GemmArgs base_args(const void* X, const void* W, int64_t B, int F, int K, int ki
 }  // namespace
 
 void gemm_softmax_set_stamps(void* stamps) { g_stamps = stamps; }
+
+bool gemm_softmax_ws_plan(int64_t B, int K, int F, int cus_per_xcd, int* slices, int* slice_classes,
+                          int* groups_per_xcd, int64_t* tiles_per_group, int64_t* grid) {
+  Plan p;
+  if (!ws_plan_for(B, K, F, cus_per_xcd, p)) return false;
+  *slices = p.ws_slices;
+  *slice_classes = p.classes_per_split;
+  *groups_per_xcd = p.ws_groups_per_xcd;
+  *tiles_per_group = p.ws_tiles_per_group;
+  *grid = p.row_blocks;
+  return true;
+}
 
 void gemm_softmax_force_plan(int nt, int splits, int kernel) {
   g_force_nt = nt;
