@@ -15,6 +15,7 @@
 #include "dist/comm.h"
 #include "dist/p2p.h"
 #include "http/loadgen.h"
+#include "http/json_body.h"
 #include "http/server.h"
 #include "http/dispatch.h"
 #include "mlapi/common.h"

@@ -2,6 +2,7 @@
 #include "server.h"
 
 #include "dispatch.h"
+#include "json_body.h"
 
 #include <arpa/inet.h>
 #include <fcntl.h>
@@ -65,247 +66,7 @@ namespace {
 
 inline bool is_hex(char c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); }
 
-// RFC 8259 number grammar (no value conversion): -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
-bool scan_number(const char* p, size_t n, size_t& i) {
-  if (i < n && p[i] == '-') ++i;
-  if (i >= n) return false;
-  if (p[i] == '0') {
-    ++i;
-  } else if (p[i] >= '1' && p[i] <= '9') {
-    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
-  } else {
-    return false;
-  }
-  if (i < n && p[i] == '.') {
-    ++i;
-    if (i >= n || !(p[i] >= '0' && p[i] <= '9')) return false;
-    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
-  }
-  if (i < n && (p[i] == 'e' || p[i] == 'E')) {
-    ++i;
-    if (i < n && (p[i] == '+' || p[i] == '-')) ++i;
-    if (i >= n || !(p[i] >= '0' && p[i] <= '9')) return false;
-    while (i < n && p[i] >= '0' && p[i] <= '9') ++i;
-  }
-  return true;
-}
-
-// Skip one JSON value starting at p[i]; returns false on malformed input, and also on anything
-// json.loads might judge differently from a strict scanner (non-ASCII bytes in strings, which
-// depend on the body's UTF-8 validity): those requests go to the Python slow path instead.
-bool skip_value(const char* p, size_t n, size_t& i, int depth) {
-  if (depth > 64) return false;
-  while (i < n && is_ws(p[i])) ++i;
-  if (i >= n) return false;
-  const char c = p[i];
-  if (c == '"') {
-    ++i;
-    while (i < n) {
-      const unsigned char ch = (unsigned char)p[i];
-      if (ch == '\\') {
-        if (i + 1 >= n) return false;
-        const char e = p[i + 1];
-        if (e == 'u') {
-          if (n - i < 6 || !is_hex(p[i + 2]) || !is_hex(p[i + 3]) || !is_hex(p[i + 4]) || !is_hex(p[i + 5]))
-            return false;
-          i += 6;
-        } else if (e == '"' || e == '\\' || e == '/' || e == 'b' || e == 'f' || e == 'n' || e == 'r' || e == 't') {
-          i += 2;
-        } else {
-          return false;
-        }
-        continue;
-      }
-      if (ch < 0x20 || ch >= 0x80) return false;
-      if (ch == '"') {
-        ++i;
-        return true;
-      }
-      ++i;
-    }
-    return false;
-  }
-  if (c == '{' || c == '[') {
-    const char close = c == '{' ? '}' : ']';
-    ++i;
-    while (i < n && is_ws(p[i])) ++i;
-    if (i < n && p[i] == close) {
-      ++i;
-      return true;
-    }
-    for (;;) {
-      if (c == '{') {
-        while (i < n && is_ws(p[i])) ++i;
-        if (i >= n || p[i] != '"') return false;
-        if (!skip_value(p, n, i, depth + 1)) return false;
-        while (i < n && is_ws(p[i])) ++i;
-        if (i >= n || p[i] != ':') return false;
-        ++i;
-      }
-      if (!skip_value(p, n, i, depth + 1)) return false;
-      while (i < n && is_ws(p[i])) ++i;
-      if (i >= n) return false;
-      if (p[i] == ',') {
-        ++i;
-        continue;
-      }
-      if (p[i] == close) {
-        ++i;
-        return true;
-      }
-      return false;
-    }
-  }
-  // literals / numbers: consume a token of allowed characters; strictness only matters for the
-  // required keys (parsed separately), an odd extra value just needs to be skippable.
-  if (c == 't' && n - i >= 4 && memcmp(p + i, "true", 4) == 0) { i += 4; return true; }
-  if (c == 'f' && n - i >= 5 && memcmp(p + i, "false", 5) == 0) { i += 5; return true; }
-  if (c == 'n' && n - i >= 4 && memcmp(p + i, "null", 4) == 0) { i += 4; return true; }
-  if (c == '-' || (c >= '0' && c <= '9')) return scan_number(p, n, i);
-  return false;  // NaN / Infinity / garbage -> slow path
-}
-
-// Clinger's fast path for a token scan_number() accepted: when the decimal significand has at most
-// 15 significant digits (< 2^53, exact in a double) and the power of ten is exact too (|e| <= 22),
-// ONE correctly rounded IEEE multiply or divide gives the correctly rounded value, i.e. exactly
-// what strtod / Python's float() return. Everything else falls back to strtod. A wide model's
-// body is 256+ numbers; strtod's ~100 ns each made the IO threads' parsing the bottleneck.
-bool fast_decimal(const char* p, size_t len, double* out) {
-  static const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
-                                    1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
-  size_t i = 0;
-  const bool neg = p[0] == '-';
-  if (neg) ++i;
-  uint64_t m = 0;
-  int sig = 0, e10 = 0;
-  for (; i < len && p[i] >= '0' && p[i] <= '9'; ++i) {
-    if (m == 0 && p[i] == '0') continue;  // leading zeros are not significant
-    if (++sig > 15) return false;
-    m = m * 10 + (uint64_t)(p[i] - '0');
-  }
-  if (i < len && p[i] == '.') {
-    for (++i; i < len && p[i] >= '0' && p[i] <= '9'; ++i) {
-      --e10;
-      if (m == 0 && p[i] == '0') continue;
-      if (++sig > 15) return false;
-      m = m * 10 + (uint64_t)(p[i] - '0');
-    }
-  }
-  if (i < len && (p[i] == 'e' || p[i] == 'E')) {
-    ++i;
-    bool eneg = false;
-    if (p[i] == '+' || p[i] == '-') eneg = p[i++] == '-';
-    int x = 0;
-    for (; i < len; ++i) {
-      if (x > 1000) return false;
-      x = x * 10 + (p[i] - '0');
-    }
-    e10 += eneg ? -x : x;
-  }
-  double v;
-  if (m == 0) {
-    v = 0.0;
-  } else if (e10 >= 0 && e10 <= 22) {
-    v = (double)m * kPow10[e10];
-  } else if (e10 < 0 && e10 >= -22) {
-    v = (double)m / kPow10[-e10];
-  } else {
-    return false;
-  }
-  *out = neg ? -v : v;
-  return true;
-}
-
-// Strict JSON number (RFC 8259 grammar) -> finite double.
-bool parse_number(const char* p, size_t n, size_t& i, double* out) {
-  const size_t s = i;
-  if (!scan_number(p, n, i)) return false;
-  const size_t len = i - s;
-  if (fast_decimal(p + s, len, out) && std::isfinite(*out)) return true;
-  if (len > 400) return false;  // absurd literals: let Python decide
-  char buf[416];
-  memcpy(buf, p + s, len);
-  buf[len] = '\0';
-  char* end = nullptr;
-  const double v = strtod(buf, &end);
-  if (end != buf + len || !std::isfinite(v)) return false;
-  *out = v;
-  return true;
-}
-
 }  // namespace
-
-bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>& names, double* out) {
-  const size_t nk = names.size();
-  if (nk > 4096) return false;
-  uint64_t seen_bits[64];  // no per-request allocation: one bit per feature name
-  std::memset(seen_bits, 0, ((nk + 63) / 64) * sizeof(uint64_t));
-  size_t i = 0, hint = 0;
-  while (i < n && is_ws(p[i])) ++i;
-  if (i >= n || p[i] != '{') return false;
-  ++i;
-  while (i < n && is_ws(p[i])) ++i;
-  if (i < n && p[i] == '}') {
-    ++i;
-  } else {
-    for (;;) {
-      while (i < n && is_ws(p[i])) ++i;
-      if (i >= n || p[i] != '"') return false;
-      ++i;
-      const size_t ks = i;
-      while (i < n && p[i] != '"') {
-        // escaped or non-ASCII keys -> slow path
-        if (p[i] == '\\' || (unsigned char)p[i] < 0x20 || (unsigned char)p[i] >= 0x80) return false;
-        ++i;
-      }
-      if (i >= n) return false;
-      const size_t klen = i - ks;
-      ++i;
-      while (i < n && is_ws(p[i])) ++i;
-      if (i >= n || p[i] != ':') return false;
-      ++i;
-      while (i < n && is_ws(p[i])) ++i;
-      // keys usually arrive in schema order: try the one after the last match first, so a wide
-      // model's body parses in O(F) instead of O(F^2) comparisons
-      int which = -1;
-      if (hint < nk && names[hint].size() == klen && memcmp(names[hint].data(), p + ks, klen) == 0) {
-        which = (int)hint;
-      } else {
-        for (size_t k = 0; k < nk; ++k) {
-          if (names[k].size() == klen && memcmp(names[k].data(), p + ks, klen) == 0) {
-            which = (int)k;
-            break;
-          }
-        }
-      }
-      if (which >= 0) hint = (size_t)which + 1;
-      if (which >= 0) {
-        double v;
-        if (!parse_number(p, n, i, &v)) return false;
-        out[which] = v;
-        seen_bits[(size_t)which >> 6] |= uint64_t(1) << ((size_t)which & 63);
-      } else {
-        if (!skip_value(p, n, i, 0)) return false;
-      }
-      while (i < n && is_ws(p[i])) ++i;
-      if (i >= n) return false;
-      if (p[i] == ',') {
-        ++i;
-        continue;
-      }
-      if (p[i] == '}') {
-        ++i;
-        break;
-      }
-      return false;
-    }
-  }
-  while (i < n && is_ws(p[i])) ++i;
-  if (i != n) return false;
-  for (size_t k = 0; k < nk; ++k)
-    if (!(seen_bits[k >> 6] >> (k & 63) & 1)) return false;
-  return true;
-}
 
 // ------------------------------------------------------------------------------------------------
 // IO thread
@@ -445,6 +206,7 @@ class IoThread : public Sink {
     epoll_ctl(epfd_, EPOLL_CTL_ADD, evfd_, &ev);
     const auto& cfg = srv_->config();
     nfeat_ = cfg.feature_names.size();
+    body_parser_ = std::make_unique<PredictBodyParser>(cfg.feature_names);
   }
   ~IoThread() override {
     for (auto& kv : conns_) close(kv.second->fd);
@@ -1074,7 +836,7 @@ class IoThread : public Sink {
     if (avail - hlen < (size_t)clen) return 0;
     const size_t at = pend_x_.size();
     pend_x_.resize(at + nfeat_);
-    if (!parse_predict_body(base + hlen, (size_t)clen, cfg.feature_names, pend_x_.data() + at)) {
+    if (!body_parser_->parse(base + hlen, (size_t)clen, pend_x_.data() + at)) {
       pend_x_.resize(at);
       return -2;
     }
@@ -1256,7 +1018,7 @@ class IoThread : public Sink {
         // one submit_many()
         const size_t at = pend_x_.size();
         pend_x_.resize(at + nfeat_);
-        if (parse_predict_body(body.data(), body.size(), cfg.feature_names, pend_x_.data() + at)) {
+        if (body_parser_->parse(body.data(), body.size(), pend_x_.data() + at)) {
           c->waiting = true;
           c->t_req = timing_ ? __rdtsc() : 0;
           pend_tags_.push_back(c->id);
@@ -1307,6 +1069,7 @@ class IoThread : public Sink {
   int lfd_;
   int epfd_ = -1, evfd_ = -1;
   size_t nfeat_ = 0;
+  std::unique_ptr<PredictBodyParser> body_parser_;  // /predict JSON keys -> feature columns
   std::thread th_;
   std::atomic<bool> stop_{false};
   std::atomic<bool> signaled_{false};

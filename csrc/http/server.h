@@ -152,11 +152,6 @@ class HttpServer {
   std::atomic<uint64_t> leaves_{0};  // acceptor mode: healthy -> unhealthy transitions
 };
 
-// Strict parser for the fast path. Returns true only for a JSON object in which every name in
-// `names` appears with a finite JSON-number value (last duplicate wins, like json.loads); extra
-// keys may hold any JSON value. Anything else returns false (-> slow path decides).
-bool parse_predict_body(const char* p, size_t n, const std::vector<std::string>& names, double* out);
-
 // HTTP date (RFC 7231 IMF-fixdate), cached per second.
 const std::string& http_date_now();  // per-thread cache
 

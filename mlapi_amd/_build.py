@@ -42,6 +42,7 @@ SOURCES = [
     "runtime/engine.cpp",
     "runtime/direct_dispatch.cpp",
     "http/server.cpp",
+    "http/json_body.cpp",
     "http/dispatch.cpp",
     "http/loadgen.cpp",
     "dist/comm.cpp",

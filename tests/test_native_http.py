@@ -170,6 +170,16 @@ def test_parser_accepts_plain_numbers(native):
                           '"petal_width":4,"y":true}') == [1, 2, 3, 4]
 
 
+def test_parser_key_prefixes_and_unclean_names(native):
+    """The schema-order key match compares name + closing quote: a name that is a prefix of the
+    next key must not match it, and a name JSON can only spell escaped never matches (slow path)."""
+    assert native.parse_predict_body('{"f10":2,"f1":1}', ["f1", "f10"]) == [1.0, 2.0]
+    assert native.parse_predict_body('{"f1":1,"f10":2}', ["f1", "f10"]) == [1.0, 2.0]
+    assert native.parse_predict_body('{"f1" :1, "f10":2 ,"f1":3}', ["f1", "f10"]) == [3.0, 2.0]
+    assert native.parse_predict_body('{"f1":1,"a\\"b":3}', ["f1", 'a"b']) is None
+    assert native.parse_predict_body('{"f1":1,"a"b":3}', ["f1", 'a"b']) is None
+
+
 @pytest.mark.parametrize("body", [
     '{"sepal_length":"5.1","sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',  # string -> pydantic coerces
     '{"sepal_length":NaN,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}',

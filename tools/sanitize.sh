@@ -6,7 +6,7 @@ set -u
 cd "$(dirname "$0")/.."
 OUT=build/sanitize
 mkdir -p "$OUT"
-SRC="csrc/tests/stress_host.cpp csrc/tests/kernel_stubs.cpp csrc/runtime/engine.cpp csrc/http/server.cpp csrc/http/dispatch.cpp csrc/http/loadgen.cpp"
+SRC="csrc/tests/stress_host.cpp csrc/tests/kernel_stubs.cpp csrc/runtime/engine.cpp csrc/http/server.cpp csrc/http/json_body.cpp csrc/http/dispatch.cpp csrc/http/loadgen.cpp"
 COMMON="--offload-arch=gfx950 -std=c++17 -O1 -g -fno-omit-frame-pointer -Icsrc -Icsrc/include -lpthread -ldl"
 rc=0
 for kind in ${*:-asan tsan}; do
