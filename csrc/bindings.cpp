@@ -188,6 +188,8 @@ PYBIND11_MODULE(_C, m) {
       py::arg("out_idx"), py::arg("out_p"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream") = 0);
   m.def("linear_split_supported", &linear_split_supported);
   m.def("linear_split_workspace", &linear_split_workspace);
+  m.def("linear_split_xcd_err_offset", &linear_split_xcd_err_offset);
+  m.def("gemm_softmax_xcd_err_offset", &gemm_softmax_xcd_err_offset);
   m.def(
       "linear_split",
       [](int dt, uintptr_t X, int64_t ldx, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind,

@@ -147,6 +147,12 @@ struct SplitRecOut {
 };
 bool linear_split_supported(int dt, int F);
 size_t linear_split_workspace(int64_t B, int K);
+// byte offset of the XCD-placement error word in the workspace (non-zero: a block of the
+// XCD-local merge ran on another XCD than planned; bit x = planned XCD x)
+size_t linear_split_xcd_err_offset();
+// gemm_softmax / softmax_rowstats workspaces: byte offset of the XCD-placement error word of the
+// XCD-local split merge (bit x: a block planned for XCD x ran elsewhere)
+size_t gemm_softmax_xcd_err_offset();
 int linear_split_nsplit(int K);
 void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K,
                          int kind, int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes,

@@ -124,10 +124,81 @@ struct GemmArgs {
   float2* rowstat;         // MODE 2 output: {lse, argmax bits}
   float4* rowstate;        // MODE 4 output: {max, sum, argmax bits, 0} (class-sharded TP)
   unsigned long long* stamps;  // profiling (tools/gemm_phase_probe.py): 8 s_memtime slots per wave
+  int xcd_local;               // split merge meets in one XCD's L2 (grid.x % 8 == 0; see xcd_put_partial)
   int ws_slices;               // W-stationary kernel: class slices (NS), row groups per XCD, tiles per group
   int ws_groups_per_xcd;
   int64_t ws_tiles_per_group;
 };
+
+// ---- split-merge protocol (tiles kernels). Default (agent scope): partials stored write-through
+// (sc1), the ticket, and an agent-scope acquire (buffer_inv sc1) in the merging block. XCD-local
+// (a.xcd_local, chosen by the host when gridDim.x % 8 == 0): hardware block b = y * gridDim.x + x
+// runs on XCD b % 8 = x % 8, so every split of row block x runs on ONE XCD and the partials, the
+// ticket and the merging block's loads all meet in that XCD's L2 - plain stores, an L2 atomic and
+// L1-bypassing (sc0) loads, no write-through and no L2 invalidate. Each block compares the XCD it
+// really runs on (HW_REG_XCC_ID) with the plan and flags a mismatch in the last counter slot.
+constexpr int XCD_ERR_SLOT = COUNTER_BYTES / 4 - 1;
+
+__device__ __forceinline__ void xcd_check(const GemmArgs& a) {
+  unsigned hw;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
+  const unsigned planned = (blockIdx.y * gridDim.x + blockIdx.x) & 7;
+  if ((hw & 15) != planned && threadIdx.x == 0)
+    __hip_atomic_fetch_or(a.counters + XCD_ERR_SLOT, 1u << planned, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void put_partial(const GemmArgs& a, int64_t idx, const RowState& S) {
+  float4* dst = a.partials + idx;
+  if (a.xcd_local) {
+    *dst = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
+    return;
+  }
+  typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+  typedef __attribute__((address_space(1))) unsigned int gu32_t;
+  const unsigned long long ms = (unsigned long long)__float_as_uint(S.m) | ((unsigned long long)__float_as_uint(S.s) << 32);
+  __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S.bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned take_ticket(const GemmArgs& a, unsigned slot) {
+  return a.xcd_local ? __hip_atomic_fetch_add(a.counters + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                     : __hip_atomic_fetch_add(a.counters + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// merging block: acquire (agent protocol only) and re-arm the counter
+__device__ __forceinline__ void merge_begin(const GemmArgs& a, unsigned slot) {
+  if (a.xcd_local) {
+    __hip_atomic_store(a.counters + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(a.counters + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// partial idx (float4 units) as seen by the merging block
+__device__ __forceinline__ float4 get_partial(const GemmArgs& a, int64_t idx) {
+  if (a.xcd_local) {  // cache policy sc0: miss this CU's L1, read the XCD's L2 (host: < 2^31 bytes)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.partials, 0, 0x7fffffff, 0x00020000);
+    const f32x4_t t = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(idx * 16), 0, 1));
+    return make_float4(t[0], t[1], t[2], t[3]);
+  }
+  return a.partials[idx];
+}
+// the first MERGE_MAX splits' partials of `row`, every load issued before the first use (one
+// round trip; the protocol branch sits outside the loads so none of them waits on another)
+__device__ __forceinline__ void get_partials(const GemmArgs& a, int64_t row, unsigned ns, float4 (&p)[MERGE_MAX]) {
+  const int64_t B = a.B;
+  if (a.xcd_local) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.partials, 0, 0x7fffffff, 0x00020000);
+    f32x4_t t[MERGE_MAX];
+#pragma unroll
+    for (int sp = 0; sp < MERGE_MAX; ++sp)
+      t[sp] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rs, (uint32_t)(((int64_t)min((unsigned)sp, ns - 1) * B + row) * 16), 0, 1));
+#pragma unroll
+    for (int sp = 0; sp < MERGE_MAX; ++sp) p[sp] = make_float4(t[sp][0], t[sp][1], t[sp][2], t[sp][3]);
+  } else {
+#pragma unroll
+    for (int sp = 0; sp < MERGE_MAX; ++sp) p[sp] = a.partials[(int64_t)min((unsigned)sp, ns - 1) * B + row];
+  }
+}
 
 // Phase stamps of one wave (profiled launches only: a.stamps is null otherwise): 0 entry, 1 first
 // W chunk + X landed, 2 class loop done, 3 row state reduced; slot 4: cycles the class loop spent
@@ -469,6 +540,7 @@ gemm_softmax_kernel(GemmArgs a) {
   constexpr int WV = tiles_block_waves<KS, NT>();
   constexpr int NTHR = 64 * WV;
   constexpr int ROWS_PER_BLOCK = WV * ROWS_PER_WAVE;
+  if ((int64_t)blockIdx.x * ROWS_PER_BLOCK >= a.B) return;  // XCD-padded grid (uniform per block)
   constexpr int F_ = KS * 32;
   constexpr int NCH = F_ / 8;                          // 16-byte chunks per W row
   constexpr int W_BYTES = CLASS_CHUNK * lds_row_stride<KS>();
@@ -632,38 +704,23 @@ gemm_softmax_kernel(GemmArgs a) {
       return;
     }
     // ---- split classes: publish partials, last-arriving block of this row block merges them.
-    // Partials are stored write-through (sc1: agent-scope atomic stores into global memory), so
-    // no release fence (buffer_wbl2, ~1.7 us per block on the critical path) is needed before the
-    // ticket: every storing wave drains (vmcnt(0)), the workgroup barrier orders the waves, then one
-    // lane takes the ticket; the merging block keeps its agent acquire (cdna_hip_programming.md
-    // Guideline 16, R1).
+    // Agent protocol: partials stored write-through (sc1: agent-scope atomic stores into global
+    // memory), so no release fence (buffer_wbl2, ~1.7 us per block on the critical path) is needed
+    // before the ticket: every storing wave drains (vmcnt(0)), the workgroup barrier orders the
+    // waves, then one lane takes the ticket; the merging block keeps its agent acquire
+    // (cdna_hip_programming.md Guideline 16, R1). XCD-local protocol: see put_partial.
+    if (a.xcd_local) xcd_check(a);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int64_t row = row0 + t * 16 + col;
-      if (q == 0 && row < B) {
-        typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-        typedef __attribute__((address_space(1))) unsigned int gu32_t;
-        float4* dst = a.partials + (int64_t)blockIdx.y * B + row;
-        const unsigned long long ms =
-            (unsigned long long)__float_as_uint(st[t].m) | ((unsigned long long)__float_as_uint(st[t].s) << 32);
-        __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gu32_t*)dst + 2, (unsigned)st[t].bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (q == 0 && row < B) put_partial(a, (int64_t)blockIdx.y * B + row, st[t]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
     __syncthreads();
-    if (tid == 0) {
-      const unsigned ticket =
-          __hip_atomic_fetch_add(&a.counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = ticket == gridDim.y - 1;
-    }
+    if (tid == 0) *flag = take_ticket(a, blockIdx.x) == gridDim.y - 1;
     __syncthreads();
     if (*flag == 0) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&a.counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-    }
+    if (tid == 0) merge_begin(a, blockIdx.x);
     __syncthreads();
     if (tid < ROWS_PER_BLOCK) {
       const int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + tid;
@@ -673,15 +730,13 @@ gemm_softmax_kernel(GemmArgs a) {
         // by CUs of other XCDs), ~7 of them at B=1024.
         const unsigned ns = gridDim.y;
         float4 p[MERGE_MAX];
-#pragma unroll
-        for (int sp = 0; sp < MERGE_MAX; ++sp)
-          p[sp] = a.partials[(int64_t)min((unsigned)sp, ns - 1) * B + row];  // clamped: unconditional
+        get_partials(a, row, ns, p);  // clamped: unconditional
         RowState S{p[0].x, p[0].y, __float_as_int(p[0].z)};
 #pragma unroll
         for (int sp = 1; sp < MERGE_MAX; ++sp)  // fixed split order: deterministic
           if ((unsigned)sp < ns) S = merge_state(S, RowState{p[sp].x, p[sp].y, __float_as_int(p[sp].z)}, ovr);
         for (unsigned sp = MERGE_MAX; sp < ns; ++sp) {  // plans with more splits (forced sweeps)
-          const float4 q = a.partials[(int64_t)sp * B + row];
+          const float4 q = get_partial(a, (int64_t)sp * B + row);
           S = merge_state(S, RowState{q.x, q.y, __float_as_int(q.z)}, ovr);
         }
         if constexpr (MODE == 0) {
@@ -930,6 +985,7 @@ gemm_softmax32_kernel(GemmArgs a) {
   constexpr int K2 = 2 * KS;
   constexpr int NTHR = 64 * WV;
   constexpr int ROWS_PER_BLOCK = 32 * RT * WV;
+  if ((int64_t)blockIdx.x * ROWS_PER_BLOCK >= a.B) return;  // XCD-padded grid (uniform per block)
   constexpr int F_ = KS * 32;
   constexpr int NCH = F_ / 8;
   constexpr int W_BYTES = CLASS_CHUNK * lds_row_stride<KS>();
@@ -1050,47 +1106,31 @@ gemm_softmax32_kernel(GemmArgs a) {
     return;
   }
   // split classes: the 16x16 kernel's publish / last-arriver merge (see there)
+  if (a.xcd_local) xcd_check(a);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     const int64_t row = row0 + rt * 32 + col;
-    if (h == 0 && row < B) {
-      typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-      typedef __attribute__((address_space(1))) unsigned int gu32_t;
-      float4* dst = a.partials + (int64_t)blockIdx.y * B + row;
-      const unsigned long long ms =
-          (unsigned long long)__float_as_uint(S[rt].m) | ((unsigned long long)__float_as_uint(S[rt].s) << 32);
-      __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S[rt].bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (h == 0 && row < B) put_partial(a, (int64_t)blockIdx.y * B + row, S[rt]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) {
-    const unsigned ticket =
-        __hip_atomic_fetch_add(&a.counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = ticket == gridDim.y - 1;
-  }
+  if (tid == 0) *flag = take_ticket(a, blockIdx.x) == gridDim.y - 1;
   __syncthreads();
   if (*flag == 0) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(&a.counters[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (tid == 0) merge_begin(a, blockIdx.x);
   __syncthreads();
   for (int mr = tid; mr < ROWS_PER_BLOCK; mr += NTHR) {
     const int64_t mrow = (int64_t)blockIdx.x * ROWS_PER_BLOCK + mr;
     if (mrow < B) {
       const unsigned ns = gridDim.y;
       float4 p[MERGE_MAX];
-#pragma unroll
-      for (int sp = 0; sp < MERGE_MAX; ++sp) p[sp] = a.partials[(int64_t)min((unsigned)sp, ns - 1) * B + mrow];
+      get_partials(a, mrow, ns, p);
       RowState R{p[0].x, p[0].y, __float_as_int(p[0].z)};
 #pragma unroll
       for (int sp = 1; sp < MERGE_MAX; ++sp)
         if ((unsigned)sp < ns) R = merge_state(R, RowState{p[sp].x, p[sp].y, __float_as_int(p[sp].z)}, ovr);
       for (unsigned sp = MERGE_MAX; sp < ns; ++sp) {
-        const float4 pq = a.partials[(int64_t)sp * B + mrow];
+        const float4 pq = get_partial(a, (int64_t)sp * B + mrow);
         R = merge_state(R, RowState{pq.x, pq.y, __float_as_int(pq.z)}, ovr);
       }
       if constexpr (MODE == 0) {
@@ -1654,7 +1694,19 @@ void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
     MLAPI_HIP_CHECK(hipGetLastError());
     return;
   }
-  const dim3 grid((unsigned)plan.row_blocks, (unsigned)plan.splits);
+  // XCD-local split merge (xcd_check / put_partial): on by default, MLAPI_GEMM_XCD=0 selects the
+  // agent-scope protocol. The grid's x extent is padded to a multiple of 8 (blocks past the batch
+  // return at once) so that every split of a row block lands on the same XCD.
+  static const int xcd_env = [] {
+    const char* e = getenv("MLAPI_GEMM_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  const int rb_pad = (plan.row_blocks + 7) / 8 * 8;
+  args.xcd_local = (MODE != 1 && xcd_env != 0 && plan.splits > 1 && rb_pad < XCD_ERR_SLOT &&
+                    (uint64_t)plan.splits * (uint64_t)args.B * 16u < 0x7fffffffu)
+                       ? 1
+                       : 0;
+  const dim3 grid((unsigned)(args.xcd_local ? rb_pad : plan.row_blocks), (unsigned)plan.splits);
   if (MODE != 1 && plan.k32) {
     if (F == 64) launch32<MODE, 2>(args, grid, plan.rt32, stream);
     else if (F == 128) launch32<MODE, 4>(args, grid, plan.rt32, stream);
@@ -1709,6 +1761,8 @@ GemmArgs base_args(const void* X, const void* W, int64_t B, int F, int K, int ki
 }  // namespace
 
 void gemm_softmax_set_stamps(void* stamps) { g_stamps = stamps; }
+
+size_t gemm_softmax_xcd_err_offset() { return (size_t)XCD_ERR_SLOT * 4; }
 
 bool gemm_softmax_ws_plan(int64_t B, int K, int F, int cus_per_xcd, int* slices, int* slice_classes,
                           int* groups_per_xcd, int64_t* tiles_per_group, int64_t* grid) {

@@ -19,6 +19,12 @@
 //    write-through (sc1), drains them (vmcnt(0)), and takes a ticket on its row group's counter;
 //    the last arriver (agent-scope acquire) loads every split's state in fixed split order and
 //    writes (label, p_max) - or the serving completion record.
+//  * XCD-local merge (xcd_local): the grid is 1-D and ordered so that every split of a row group
+//    runs on ONE XCD (hardware block b runs on XCD b % 8: row group r -> XCD r % 8). All of the
+//    protocol's traffic - partial stores, the ticket, the last arriver's loads - then meets in that
+//    XCD's L2: plain stores, an L2 atomic and L1-bypassing (sc0) loads, with no write-through to
+//    HBM and no agent-scope L2 invalidate (buffer_inv sc1) on the merge path. Every block checks
+//    the XCD it really runs on (HW_REG_XCC_ID) and flags a mismatch in the workspace's error word.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -46,6 +52,9 @@ struct SplitArgs {
   RecOut ro;            // serving: per-row completion records instead of out_idx / out_p
   unsigned int* counters;  // [row groups], zero between launches (re-armed by the merging block)
   float4* partials;        // [row groups][nsplit][32] {m, s, argmax bits, 0}
+  unsigned int* xcd_err;   // xcd_local: set non-zero by a block that runs on another XCD than planned
+  int32_t xcd_local;        // 1-D XCD-ordered grid + L2-local merge protocol (see the header)
+  int32_t row_groups;
   int32_t probe;           // measurement only (MLAPI_SPLIT_PROBE): 1 = stop after the block merge, 2 = after the partial stores
   // Host merge (serving, one row group): each block publishes its per-row states as 16-byte
   // completion records {seq, argmax, m, s} into host-mapped memory at hrec[block * 32 + row] and
@@ -90,8 +99,19 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
   __shared__ float4 red[4][NB * 16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int c0 = blockIdx.x * CLASSES_PER_BLOCK + wave * 16;
-  const int row0 = blockIdx.y * ROWS_PER_GROUP;
+  int split = blockIdx.x, rgi = blockIdx.y;
+  if (a.xcd_local) {  // b -> XCD b & 7; its j-th block: row group xcd + 8 (j / nsplit), split j % nsplit
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    rgi = xcd + 8 * (j / a.nsplit);
+    split = j % a.nsplit;
+    if (rgi >= a.row_groups) return;  // uniform per block
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
+    if ((int)(hw & 15) != xcd && threadIdx.x == 0)
+      __hip_atomic_fetch_or(a.xcd_err, 1u << xcd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const int c0 = split * CLASSES_PER_BLOCK + wave * 16;
+  const int row0 = rgi * ROWS_PER_GROUP;
   // ---- every load of the block up front: W fragments, X fragments, bias
   const int ca = min(c0 + r16, a.K - 1);  // padding classes read a real row (masked by a -inf bias)
   const uint4* wp = reinterpret_cast<const uint4*>(static_cast<const T*>(a.W) + (int64_t)ca * F) + g;
@@ -179,41 +199,62 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
     if (live) {
       typedef __attribute__((ext_vector_type(4))) uint32_t su32x4_t;
       const su32x4_t r = {a.rec_seq, (uint32_t)S.bi, __float_as_uint(S.m), __float_as_uint(S.s)};
-      uint4* dst = a.hrec + (int64_t)blockIdx.x * ROWS_PER_GROUP + l;
+      uint4* dst = a.hrec + (int64_t)split * ROWS_PER_GROUP + l;
       // write-through (sc0 sc1): visible to the host poller without a fence, as one 16-byte unit
       asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(r) : "memory");
     }
     return;
   }
-  if (gridDim.x > 1) {
-    // one cross-block round trip: write-through partials, drained, then the row group's ticket
+  if (a.nsplit > 1) {
+    // one cross-block round trip: partials, drained, then the row group's ticket
     typedef __attribute__((address_space(1))) unsigned long long gu64_t;
     typedef __attribute__((address_space(1))) unsigned int gu32_t;
-    float4* part = a.partials + ((int64_t)blockIdx.y * a.nsplit) * ROWS_PER_GROUP;
+    float4* part = a.partials + ((int64_t)rgi * a.nsplit) * ROWS_PER_GROUP;
+    unsigned int* ctr = a.counters + rgi;
     if (live) {
-      float4* dst = part + (int64_t)blockIdx.x * ROWS_PER_GROUP + l;
-      const unsigned long long ms =
-          (unsigned long long)__float_as_uint(S.m) | ((unsigned long long)__float_as_uint(S.s) << 32);
-      __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S.bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      float4* dst = part + (int64_t)split * ROWS_PER_GROUP + l;
+      if (a.xcd_local) {  // plain store: L1 is write-through, the row group's L2 is the meeting point
+        *dst = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
+      } else {  // write-through past this XCD's L2
+        const unsigned long long ms =
+            (unsigned long long)__float_as_uint(S.m) | ((unsigned long long)__float_as_uint(S.s) << 32);
+        __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S.bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stores are acknowledged before the ticket
     if (a.probe == 2) return;
     unsigned ticket = 0;
     if (l == 0)
-      ticket = __hip_atomic_fetch_add(&a.counters[blockIdx.y], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ticket = a.xcd_local ? __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                           : __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ticket = __shfl(ticket, 0, 64);
-    if (ticket != gridDim.x - 1) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (l == 0) __hip_atomic_store(&a.counters[blockIdx.y], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ticket != (unsigned)a.nsplit - 1) return;
+    if (a.xcd_local) {
+      if (l == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (l == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (!live) return;
     // fixed split order (deterministic); 16 states in flight per batch of loads
     const float4* src = part + l;
     float4 v[16];
     S = SState{-INFINITY, 0.f, 0x7fffffff};
     for (int sp0 = 0; sp0 < a.nsplit; sp0 += 16) {
+      if (a.xcd_local) {  // cache policy sc0: miss this CU's L1, read the row group's L2
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, a.nsplit * ROWS_PER_GROUP * 16, 0x00020000);
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = src[(int64_t)min(sp0 + u, a.nsplit - 1) * ROWS_PER_GROUP];
+        for (int u = 0; u < 16; ++u) {
+          const sf32x4_t t = __builtin_bit_cast(
+              sf32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                            rs, (uint32_t)((min(sp0 + u, a.nsplit - 1) * ROWS_PER_GROUP + l) * 16), 0, 1));
+          v[u] = make_float4(t[0], t[1], t[2], t[3]);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = src[(int64_t)min(sp0 + u, a.nsplit - 1) * ROWS_PER_GROUP];
+      }
 #pragma unroll
       for (int u = 0; u < 16; ++u)
         if (sp0 + u < a.nsplit) S = smerge(S, SState{v[u].x, v[u].y, __float_as_int(v[u].z)}, OVR);

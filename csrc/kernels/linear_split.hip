@@ -11,7 +11,10 @@
 namespace mlapi {
 namespace {
 
-constexpr size_t COUNTER_REGION = 256;  // 64 row groups of counters (B <= 2048)
+// workspace: [64 row-group counters (B <= 2048)] [xcd error word at byte 256] [pad] [partials]
+constexpr size_t COUNTER_REGION = 512;
+constexpr size_t MAX_ROW_GROUPS = 64;
+constexpr size_t XCD_ERR_OFFSET = 256;
 
 template <typename T, int KS, int NB, bool OVR>
 __global__ __launch_bounds__(256) void linear_split_kernel(split::SplitArgs a) {
@@ -45,6 +48,8 @@ bool linear_split_supported(int dt, int F) {
   return false;
 }
 
+size_t linear_split_xcd_err_offset() { return XCD_ERR_OFFSET; }
+
 size_t linear_split_workspace(int64_t B, int K) {
   const int rg = row_groups(B);
   return COUNTER_REGION + (size_t)rg * nsplits(K) * split::ROWS_PER_GROUP * sizeof(float4);
@@ -65,7 +70,7 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
   if (reinterpret_cast<uintptr_t>(X) % 16 != 0 || reinterpret_cast<uintptr_t>(W) % 16 != 0)
     throw std::invalid_argument("linear_split: X and W must be 16-byte aligned");
   const int rg = row_groups(B), ns = nsplits(K);
-  if (rg > (int)(COUNTER_REGION / sizeof(unsigned int)))
+  if (rg > (int)MAX_ROW_GROUPS)
     throw std::invalid_argument("linear_split: B too large (<= 2048 rows per launch)");
   if (sro.rec != nullptr && rg != 1) throw std::invalid_argument("linear_split: host merge needs B <= 32");
   if (sro.rec == nullptr && ns > 1 && ws_bytes < linear_split_workspace(B, K))
@@ -91,7 +96,16 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
   a.probe = probe;
   a.hrec = reinterpret_cast<uint4*>(sro.rec);
   a.rec_seq = sro.seq;
-  const dim3 grid((unsigned)ns, (unsigned)rg);
+  // XCD-local merge (linear_split.h): default on; MLAPI_SPLIT_XCD=0 selects the agent-scope protocol
+  static const int xcd_env = [] {
+    const char* e = getenv("MLAPI_SPLIT_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  a.xcd_local = (xcd_env != 0 && ns > 1 && sro.rec == nullptr) ? 1 : 0;
+  a.row_groups = rg;
+  a.xcd_err = reinterpret_cast<unsigned int*>(static_cast<unsigned char*>(workspace) + XCD_ERR_OFFSET);
+  // XCD-ordered 1-D grid: 8 XCDs x ceil(rg / 8) row groups x ns splits (blocks past rg exit at once)
+  const dim3 grid = a.xcd_local ? dim3((unsigned)(8 * ((rg + 7) / 8) * ns), 1u) : dim3((unsigned)ns, (unsigned)rg);
   const bool nb2 = B > 16;
   const bool ovr = kind == KIND_OVR;
   if (dt == DT_BF16) {

@@ -115,6 +115,14 @@ class GemmSoftmax:
                          self.ws.data_ptr(), self.ws.numel(), _stream())
         return idx, p
 
+    def xcd_errors(self) -> int:
+        """Bit mask of planned XCDs whose blocks ran elsewhere during an XCD-local split merge
+        (gemm_softmax.hip, put_partial); 0 while the block -> XCD placement held."""
+        o = C().gemm_softmax_xcd_err_offset()
+        if self.ws.numel() < o + 4:
+            return 0  # no split plan has run: nothing was checked
+        return int(self.ws[o:o + 4].view(torch.int32).item())
+
 
 class LinearSplit:
     """Class-split multiclass predict (csrc/kernels/linear_split.h): small batches (one launch,
@@ -147,6 +155,12 @@ class LinearSplit:
         C().linear_split(_DT[X.dtype], X.data_ptr(), F, W.data_ptr(), b.data_ptr(), B, F, K, int(kind), idx.data_ptr(),
                          p.data_ptr(), self.ws.data_ptr(), self.ws.numel(), _stream())
         return idx, p
+
+    def xcd_errors(self) -> int:
+        """Bit mask of planned XCDs whose blocks ran elsewhere (XCD-local merge); 0 when the
+        hardware's round-robin block -> XCD placement held for every launch so far."""
+        o = C().linear_split_xcd_err_offset()
+        return int(self.ws[o:o + 4].view(torch.int32).item())
 
 
 def linear_split(X, W, b, kind: int = Kind.MULTINOMIAL):

@@ -93,7 +93,7 @@ def gemm_kernel(request):
     from mlapi_amd._native import C
 
     if request.param == 4 and os.environ.get("MLAPI_GEMM_WS", "0") == "0":
-        pytest.skip("W-stationary kernel is opt-in (MLAPI_GEMM_WS=1) until measured on the box")
+        pytest.skip("W-stationary kernel is opt-in (MLAPI_GEMM_WS=1): measured slower than the tiles kernel, profiles/r3_ws")
     C().gemm_softmax_force_plan(0, 0, request.param)
     yield request.param
     C().gemm_softmax_force_plan(0, 0, 0)
@@ -156,6 +156,30 @@ def test_gemm_softmax_large_batch_and_rearm():
             idx, p = op(X, W, b)
             assert torch.equal(idx[clear], torch.argmax(Z, dim=1).to(torch.int32)[clear])
             torch.testing.assert_close(p.double(), rp, rtol=2e-4, atol=2e-5)
+        assert op.xcd_errors() == 0
+
+
+@pytest.mark.parametrize("kind", [Kind.MULTINOMIAL, Kind.OVR])
+@pytest.mark.parametrize("B", [1024, 8192])
+def test_gemm_softmax_xcd_local_merge_repeated(B, kind):
+    """BASELINE config 3 (B = 1024, K = 1000, F = 256) and a 4-split plan: the row blocks' splits meet
+    in one XCD's L2 (gemm_softmax.hip, put_partial). Twenty back-to-back launches on fresh inputs all
+    match the oracle, and no block ran on another XCD than planned."""
+    F, K = 256, 1000
+    W = _rand((K, F), torch.bfloat16, 61, scale=1 / 16)
+    b = _rand((K,), torch.float32, 62, scale=0.1)
+    op = ops.GemmSoftmax(B, K, F, DEV)
+    Xs = [_rand((B, F), torch.bfloat16, 200 + i) for i in range(20)]
+    outs = [tuple(t.clone() for t in op(X, W, b, kind)) for X in Xs]
+    torch.cuda.synchronize()
+    for X, (idx, p) in zip(Xs, outs):
+        Z = ref.logits_ref(X, W, b, dtype=torch.float64)
+        ridx, rp = ref.predict_ref(X, W, b, kind)
+        top2 = torch.topk(Z, 2, dim=1).values
+        clear = (top2[:, 0] - top2[:, 1]) > 1e-3
+        assert torch.equal(idx[clear].cpu(), ridx[clear].cpu())
+        torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=2e-4, atol=2e-5)
+    assert op.xcd_errors() == 0
 
 
 @pytest.mark.parametrize("kernel", [1, 2])
@@ -452,6 +476,34 @@ def test_linear_split_bf16(B, K, kind):
         torch.cuda.synchronize()
         assert torch.equal(idx[clear].cpu(), ridx[clear].cpu())
         torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=2e-5, atol=2e-6)
+    assert op.xcd_errors() == 0
+
+
+@pytest.mark.parametrize("kind", [Kind.MULTINOMIAL, Kind.OVR])
+@pytest.mark.parametrize("B", [1024, 2048])
+def test_linear_split_xcd_local_merge_repeated(B, kind):
+    """BASELINE config 3 shape (K = 1000, F = 256): 32 / 64 row groups whose 16 splits meet in one
+    XCD's L2 (linear_split.h, XCD-local merge). Twenty back-to-back launches on fresh inputs: every
+    one matches the oracle (a counter not re-armed or a stale L2 read would show up as a wrong row),
+    and no block ran on another XCD than the plan."""
+    F, K = 256, 1000
+    W = _rand((K, F), torch.bfloat16, 52, scale=1 / np.sqrt(F))
+    b = _rand((K,), torch.float32, 53, scale=0.1)
+    op = ops.LinearSplit(B, K, DEV)
+    outs = []
+    Xs = [_rand((B, F), torch.bfloat16, 100 + i) for i in range(20)]
+    for X in Xs:
+        idx, p = op(X, W, b, kind)
+        outs.append((idx.clone(), p.clone()))
+    torch.cuda.synchronize()
+    for X, (idx, p) in zip(Xs, outs):
+        Z = ref.logits_ref(X, W, b, dtype=torch.float64)
+        ridx, rp = ref.predict_ref(X, W, b, kind)
+        top2 = torch.topk(Z, 2, dim=1).values
+        clear = (top2[:, 0] - top2[:, 1]) > 1e-3
+        assert torch.equal(idx[clear].cpu(), ridx[clear].cpu())
+        torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=2e-5, atol=2e-6)
+    assert op.xcd_errors() == 0
 
 
 @pytest.mark.parametrize("kind", [Kind.MULTINOMIAL, Kind.OVR])

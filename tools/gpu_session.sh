@@ -23,6 +23,8 @@
 #   pmc_gemm      hardware counters of the gemm bench (tools/pmc_profile.sh)
 #   gemm_ws       W-stationary persistent gemm_softmax kernel vs the 32x32 kernel (tests, A/B x2, kernel stats)
 #   split_big     class-split kernel vs tiles kernel at B = 256 / 1024 / 2048, interleaved x2
+#   gemm_xcd      XCD-local vs agent-scope split merge in the tiles kernels (MLAPI_GEMM_XCD=1/0), B = 1024 / 8192
+#   split_xcd     XCD-local vs agent-scope split merge (MLAPI_SPLIT_XCD=1/0), B = 32..2048, x2 + kernel stats
 #   threads       IO-thread / load-generator-thread split sweep, THREADS="io:cl ..." (default "10:4 8:6 6:6"), x2
 #   gdw           softmax G+dW kernel: its GPU tests + tools/softmax_train_sweep.py timings
 #   gemm_ab       interleaved x3 gemm bench: ab_old/mlapi_amd (stashed previous build) vs the working tree
@@ -182,6 +184,32 @@ for s in $steps; do
       prof gemm_ws_b262144 120 --mode gemm --batch 262144 --steps 20 --warmup 2 --gemm-kernel ws
       prof gemm_t32_b262144 120 --mode gemm --batch 262144 --steps 20 --warmup 2 --gemm-kernel t32
       MLAPI_GEMM_WS=1 prof train_softmax_ws 300 --mode train_softmax --steps 20 --warmup 2 ;;
+    split_xcd)  # XCD-local vs agent-scope split merge (linear_split.h): tests, interleaved benches, kernel stats
+      run pytest_split_xcd 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "linear_split"
+      for r in 1 2; do
+        for x in 1 0; do
+          for B in 32 256 1024 2048; do
+            MLAPI_SPLIT_XCD=$x run "gemm_split_xcd${x}_b${B}_r$r" 120 python -u bench.py --mode gemm --batch $B --steps 2000 --warmup 50 --gemm-kernel split
+          done
+        done
+        run "gemm_tiles_b1024_r$r" 120 python -u bench.py --mode gemm --batch 1024 --steps 2000 --warmup 50
+      done
+      for x in 1 0; do
+        MLAPI_SPLIT_XCD=$x prof "split_xcd${x}_b1024" 120 --mode gemm --batch 1024 --steps 300 --warmup 5 --gemm-kernel split --launch eager
+        MLAPI_SPLIT_XCD=$x prof "split_xcd${x}_b32" 120 --mode gemm --batch 32 --steps 300 --warmup 5 --gemm-kernel split --launch eager
+      done ;;
+    gemm_xcd)  # XCD-local vs agent-scope split merge in the tiles kernels (MLAPI_GEMM_XCD=1/0), x2 + kernel stats
+      run pytest_gemm_xcd 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "gemm or softmax or rowstat or train"
+      for r in 1 2; do
+        for x in 1 0; do
+          for B in 1024 8192; do
+            MLAPI_GEMM_XCD=$x run "gemm_xcd${x}_b${B}_r$r" 120 python -u bench.py --mode gemm --batch $B --steps 2000 --warmup 50
+          done
+        done
+      done
+      for x in 1 0; do
+        MLAPI_GEMM_XCD=$x prof "gemm_xcd${x}_b1024" 120 --mode gemm --batch 1024 --steps 300 --warmup 5 --launch eager
+      done ;;
     split_big)  # class-split kernel vs the tiles kernel at medium batches (B=1024 is BASELINE config 3)
       for r in 1 2; do
         for B in 256 1024 2048; do
