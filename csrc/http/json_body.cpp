@@ -149,6 +149,33 @@ bool parse_number_strtod(const char* p, size_t n, size_t& i, double* out) {
   return true;
 }
 
+// ---- SWAR digit runs (8 bytes at a time, little-endian): the digit loops of a short decimal
+// ("-0.891") are data-dependent branches that mispredict once or twice per number; counting a
+// run with one mask and converting it with three multiplies has none.
+inline uint64_t load8(const char* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+}
+// leading ASCII digits among the 8 bytes (a +6 carry out of a byte >= 0xFA only reaches bytes
+// after that non-digit, so the leading run is exact)
+inline int digit_run8(uint64_t v) {
+  const uint64_t hi = v & 0xF0F0F0F0F0F0F0F0ull;
+  const uint64_t hi6 = (v + 0x0606060606060606ull) & 0xF0F0F0F0F0F0F0F0ull;
+  const uint64_t x = (hi ^ 0x3030303030303030ull) | (hi6 ^ 0x3030303030303030ull);  // byte != 0: not a digit
+  const uint64_t y = (((x & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | x) & 0x8080808080808080ull;
+  return y == 0 ? 8 : __builtin_ctzll(y) >> 3;
+}
+// value of the first c (1..8) digits: bytes past the run may borrow upward only, and the shift
+// drops them; the zero bytes shifted in are leading zeros
+inline uint64_t digits_value(uint64_t v, int c) {
+  uint64_t t = (v - 0x3030303030303030ull) << (8 * (8 - c));
+  t = (t * 10 + (t >> 8)) & 0x00FF00FF00FF00FFull;
+  t = (t * 100 + (t >> 16)) & 0x0000FFFF0000FFFFull;
+  return (t * 10000 + (t >> 32)) & 0xFFFFFFFFull;
+}
+const uint64_t kPow10u[9] = {1, 10, 100, 1000, 10000, 100000, 1000000, 10000000, 100000000};
+
 // Strict JSON number -> finite double, scanned and converted in one pass. Significand digits
 // accumulate into m (leading zeros skipped); e10 is the decimal exponent of m's last digit.
 // Exact (Clinger) when m has <= 15 significant digits and |e10| <= 22; otherwise strtod.
@@ -157,6 +184,33 @@ inline bool parse_number(const char* p, size_t n, size_t& i, double* out) {
   const bool neg = j < n && p[j] == '-';
   j += neg;
   if (j >= n) return false;
+  if (n - j >= 24) {  // SWAR fast path: int part and fraction of <= 7 digits each, no exponent
+    const uint64_t v = load8(p + j);
+    const int c1 = digit_run8(v);
+    if (c1 == 0) return false;
+    if (c1 > 1 && p[j] == '0') return false;  // leading zero: not JSON
+    if (c1 < 8) {
+      size_t k = j + (size_t)c1;
+      uint64_t m = digits_value(v, c1);
+      int c2 = 0;
+      if (p[k] == '.') {
+        const uint64_t w = load8(p + k + 1);
+        c2 = digit_run8(w);
+        if (c2 == 0) return false;
+        if (c2 < 8) {
+          m = m * kPow10u[c2] + digits_value(w, c2);
+          k += 1 + (size_t)c2;
+        }
+      }
+      if (c2 < 8 && (p[k] | 0x20) != 'e') {  // c1 + c2 <= 14 digits: m < 2^53, Clinger exact
+        const double d = m == 0 ? 0.0 : (c2 == 0 ? (double)m : (double)m / kPow10[c2]);
+        // an integer literal is a Python int: "-0" is 0, not -0.0
+        *out = neg && (m != 0 || c2 != 0) ? -d : d;
+        i = k;
+        return true;
+      }
+    }
+  }
   uint64_t m = 0;
   int sig = 0, e10 = 0;
   unsigned d = digit(p[j]);
@@ -171,7 +225,9 @@ inline bool parse_number(const char* p, size_t n, size_t& i, double* out) {
   } else {
     return false;
   }
+  bool is_int = true;  // no fraction, no exponent
   if (j < n && p[j] == '.') {
+    is_int = false;
     ++j;
     if (j >= n || digit(p[j]) > 9) return false;
     while (j < n && (d = digit(p[j])) <= 9) {
@@ -182,6 +238,7 @@ inline bool parse_number(const char* p, size_t n, size_t& i, double* out) {
     }
   }
   if (j < n && (p[j] | 0x20) == 'e') {
+    is_int = false;
     ++j;
     bool eneg = false;
     if (j < n && (p[j] == '+' || p[j] == '-')) eneg = p[j++] == '-';
@@ -195,7 +252,7 @@ inline bool parse_number(const char* p, size_t n, size_t& i, double* out) {
   }
   if (sig > 15 || e10 > 22 || e10 < -22) return parse_number_strtod(p, n, i, out);  // i: token start
   const double v = m == 0 ? 0.0 : (e10 >= 0 ? (double)m * kPow10[e10] : (double)m / kPow10[-e10]);
-  *out = neg ? -v : v;
+  *out = neg && !(m == 0 && is_int) ? -v : v;  // "-0" is the Python int 0
   i = j;
   return true;
 }

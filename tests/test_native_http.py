@@ -3,6 +3,7 @@ import json
 import os
 import re
 import socket
+import struct
 import threading
 import time
 
@@ -168,6 +169,31 @@ def test_parser_accepts_plain_numbers(native):
         == [100.0, 0.0, 12345678901234567890.0, -0.0]
     assert _parse(native, '{"x":{"a":[1,"}",{"b":null}]},"sepal_length":1,"sepal_width":2,"petal_length":3,'
                           '"petal_width":4,"y":true}') == [1, 2, 3, 4]
+
+
+@pytest.mark.parametrize("tok", [
+    "0", "-0", "0.0", "-0.0", "7", "1234567", "12345678", "123456789", "0.1234567", "0.12345678",
+    "1234567.1234567", "1234567.12345678", "9999999.9999999", "5.", "-", "-a", "01", "-01", "00.5", "1.e5",
+    "1.5e3", "1.5E-3", "2e0", "0e5", "1234567e-7", ".5", "+1", "1.2.3", "1..2", "3.14159", "-2.5", "100",
+])
+def test_parser_swar_numbers_match_json(native, tok):
+    """Numbers followed by >= 24 more bytes take the 8-byte-at-a-time (SWAR) path of
+    csrc/http/json_body.cpp: every token parses to exactly float(tok) when json.loads accepts it,
+    and is refused (slow path) when it does not - including runs of exactly 7 / 8 digits."""
+    names = ["a", "b"]
+    body = '{"a":' + tok + ', "b": 1, "padding_padding_padding": 0}'
+    try:
+        want = json.loads(body)["a"]
+        ok = isinstance(want, (int, float)) and not isinstance(want, bool)
+    except ValueError:
+        ok = False
+    got = native.parse_predict_body(body, names)
+    if not ok:
+        assert got is None, tok
+    else:
+        assert got is not None, tok
+        assert struct.pack("<d", got[0]) == struct.pack("<d", float(want)), tok
+        assert got[1] == 1.0
 
 
 def test_parser_key_prefixes_and_unclean_names(native):
