@@ -350,8 +350,8 @@ def test_fast_number_path_matches_python_float(native):
     body = "{" + ",".join(f'"{n}":{t}' for n, t in zip(names, toks)) + "}"
     got = native.parse_predict_body(body, names)
     assert got is not None
-    for t, g in zip(toks, got):
-        assert struct.pack("<d", g) == struct.pack("<d", float(t)), t
+    for t, g in zip(toks, got):  # the FastAPI oracle: json.loads (an integer literal is an int), then float
+        assert struct.pack("<d", g) == struct.pack("<d", float(json.loads(t))), t
 
 
 def test_idle_engine_fast_path_cpu_backend(iris_cwd):
