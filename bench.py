@@ -325,6 +325,15 @@ def bench_gemv(args, info):
              "features": F, "parallelism": f"dp{info.world}"})
 
 
+def _xcd_placement(info):
+    """Block -> XCD placement probe result of this device (csrc/kernels/xcd.hip): 'round-robin'
+    when the XCD-local split merges are on, 'off' when the probe found another order."""
+    from mlapi_amd._native import C
+
+    st = C().xcd_placement_state(info.device.index if info.device is not None else 0)
+    return {0: "not probed", 1: "round-robin", 2: "off"}.get(st, str(st))
+
+
 def bench_gemm(args, info):
     import torch
 
@@ -357,7 +366,8 @@ def bench_gemm(args, info):
     return ("rows_per_sec_softmax_predict", value, "rows/s", elapsed,
             {"tflops_per_gpu": tflops, "us_per_call": elapsed / args.steps * 1e6, "launch": args.launch,
              "kernel": "linear_split" if isinstance(op, ops.LinearSplit) else "gemm_softmax",
-             "gemm_kernel": args.gemm_kernel, "dtype": args.gemm_dtype},
+             "gemm_kernel": args.gemm_kernel, "dtype": args.gemm_dtype,
+             "xcd_placement": _xcd_placement(info)},
             {"model": "softmax regression F=256 K=1000", "global_batch": B * info.world, "seq_len": 1,
              "features": F, "parallelism": f"dp{info.world}"})
 

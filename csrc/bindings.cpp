@@ -190,6 +190,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_split_workspace", &linear_split_workspace);
   m.def("linear_split_xcd_err_offset", &linear_split_xcd_err_offset);
   m.def("gemm_softmax_xcd_err_offset", &gemm_softmax_xcd_err_offset);
+  m.def("xcd_placement_state", &xcd_placement_state, py::arg("device") = 0);
+  m.def("xcd_placement_mismatches", &xcd_placement_mismatches, py::arg("device") = 0);
   m.def(
       "linear_split",
       [](int dt, uintptr_t X, int64_t ldx, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind,

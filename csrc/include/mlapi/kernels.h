@@ -153,6 +153,13 @@ size_t linear_split_xcd_err_offset();
 // gemm_softmax / softmax_rowstats workspaces: byte offset of the XCD-placement error word of the
 // XCD-local split merge (bit x: a block planned for XCD x ran elsewhere)
 size_t gemm_softmax_xcd_err_offset();
+// xcd.hip: may the XCD-local split merges run on the current device? The first eager call probes
+// the block -> XCD placement (1024 blocks read HW_REG_XCC_ID); inside a stream capture it answers
+// the plan's default (true) without probing. xcd_placement_state: 0 not probed, 1 as planned,
+// 2 off (mismatches: blocks off the plan in the probe, -1 if the probe itself failed).
+bool xcd_local_allowed(hipStream_t stream);
+int xcd_placement_state(int device);
+int xcd_placement_mismatches(int device);
 int linear_split_nsplit(int K);
 void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K,
                          int kind, int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes,

@@ -1703,7 +1703,7 @@ void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
   }();
   const int rb_pad = (plan.row_blocks + 7) / 8 * 8;
   args.xcd_local = (MODE != 1 && xcd_env != 0 && plan.splits > 1 && rb_pad < XCD_ERR_SLOT &&
-                    (uint64_t)plan.splits * (uint64_t)args.B * 16u < 0x7fffffffu)
+                    (uint64_t)plan.splits * (uint64_t)args.B * 16u < 0x7fffffffu && xcd_local_allowed(stream))
                        ? 1
                        : 0;
   const dim3 grid((unsigned)(args.xcd_local ? rb_pad : plan.row_blocks), (unsigned)plan.splits);

@@ -101,7 +101,7 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
     const char* e = getenv("MLAPI_SPLIT_XCD");
     return e ? atoi(e) : 1;
   }();
-  a.xcd_local = (xcd_env != 0 && ns > 1 && sro.rec == nullptr) ? 1 : 0;
+  a.xcd_local = (xcd_env != 0 && ns > 1 && sro.rec == nullptr && xcd_local_allowed(stream)) ? 1 : 0;
   a.row_groups = rg;
   a.xcd_err = reinterpret_cast<unsigned int*>(static_cast<unsigned char*>(workspace) + XCD_ERR_OFFSET);
   // XCD-ordered 1-D grid: 8 XCDs x ceil(rg / 8) row groups x ns splits (blocks past rg exit at once)

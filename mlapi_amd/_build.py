@@ -39,6 +39,7 @@ SOURCES = [
     "kernels/shard.hip",
     "kernels/softmax_grad_dw.hip",
     "kernels/softmax_grad_wide.hip",
+    "kernels/xcd.hip",
     "runtime/engine.cpp",
     "runtime/direct_dispatch.cpp",
     "http/server.cpp",

@@ -172,6 +172,11 @@ def test_gemm_softmax_xcd_local_merge_repeated(B, kind):
     Xs = [_rand((B, F), torch.bfloat16, 200 + i) for i in range(20)]
     outs = [tuple(t.clone() for t in op(X, W, b, kind)) for X in Xs]
     torch.cuda.synchronize()
+    from mlapi_amd._native import C
+
+    # the placement probe ran before the first XCD-local launch and found the round-robin order
+    assert C().xcd_placement_state(torch.cuda.current_device()) == 1
+    assert C().xcd_placement_mismatches(torch.cuda.current_device()) == 0
     for X, (idx, p) in zip(Xs, outs):
         Z = ref.logits_ref(X, W, b, dtype=torch.float64)
         ridx, rp = ref.predict_ref(X, W, b, kind)
