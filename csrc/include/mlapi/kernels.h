@@ -148,14 +148,14 @@ struct SplitRecOut {
 bool linear_split_supported(int dt, int F);
 size_t linear_split_workspace(int64_t B, int K);
 // byte offset of the XCD-placement error word in the workspace (non-zero: a block of the
-// XCD-local merge ran on another XCD than planned; bit x = planned XCD x)
+// XCD-local merge read a partial written on another XCD; bit x = the merging block's XCD)
 size_t linear_split_xcd_err_offset();
 // gemm_softmax / softmax_rowstats workspaces: byte offset of the XCD-placement error word of the
-// XCD-local split merge (bit x: a block planned for XCD x ran elsewhere)
+// XCD-local split merge (bit x: a merging block on XCD x read a partial written elsewhere)
 size_t gemm_softmax_xcd_err_offset();
 // xcd.hip: may the XCD-local split merges run on the current device? The first eager call probes
 // the block -> XCD placement (1024 blocks read HW_REG_XCC_ID); inside a stream capture it answers
-// the plan's default (true) without probing. xcd_placement_state: 0 not probed, 1 as planned,
+// the plan's default (true) without probing. xcd_placement_state: 0 not probed, 1 blocks b and b + 8k share an XCD,
 // 2 off (mismatches: blocks off the plan in the probe, -1 if the probe itself failed).
 bool xcd_local_allowed(hipStream_t stream);
 int xcd_placement_state(int device);

@@ -132,24 +132,24 @@ struct GemmArgs {
 
 // ---- split-merge protocol (tiles kernels). Default (agent scope): partials stored write-through
 // (sc1), the ticket, and an agent-scope acquire (buffer_inv sc1) in the merging block. XCD-local
-// (a.xcd_local, chosen by the host when gridDim.x % 8 == 0): hardware block b = y * gridDim.x + x
-// runs on XCD b % 8 = x % 8, so every split of row block x runs on ONE XCD and the partials, the
-// ticket and the merging block's loads all meet in that XCD's L2 - plain stores, an L2 atomic and
-// L1-bypassing (sc0) loads, no write-through and no L2 invalidate. Each block compares the XCD it
-// really runs on (HW_REG_XCC_ID) with the plan and flags a mismatch in the last counter slot.
+// (a.xcd_local, chosen by the host when gridDim.x % 8 == 0): hardware blocks are dealt round-robin
+// over the 8 XCDs, so block b = y * gridDim.x + x runs on XCD (c + b) % 8 = (c + x) % 8 - c is
+// wherever the dispatcher's rotation stood when the launch began - and every split of row block
+// x runs on ONE XCD: the partials, the ticket and the merging block's loads all meet in that
+// XCD's L2 (plain stores, an L2 atomic and L1-bypassing sc0 loads; no write-through, no L2
+// invalidate). Each partial carries the XCD that wrote it (HW_REG_XCC_ID, 4th word); the merging
+// block checks them against its own and flags a mismatch in the last counter slot (bit = XCD).
 constexpr int XCD_ERR_SLOT = COUNTER_BYTES / 4 - 1;
 
-__device__ __forceinline__ void xcd_check(const GemmArgs& a) {
+__device__ __forceinline__ unsigned my_xcc() {
   unsigned hw;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
-  const unsigned planned = (blockIdx.y * gridDim.x + blockIdx.x) & 7;
-  if ((hw & 15) != planned && threadIdx.x == 0)
-    __hip_atomic_fetch_or(a.counters + XCD_ERR_SLOT, 1u << planned, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return hw & 15;
 }
 __device__ __forceinline__ void put_partial(const GemmArgs& a, int64_t idx, const RowState& S) {
   float4* dst = a.partials + idx;
   if (a.xcd_local) {
-    *dst = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
+    *dst = make_float4(S.m, S.s, __int_as_float(S.bi), __uint_as_float(my_xcc()));
     return;
   }
   typedef __attribute__((address_space(1))) unsigned long long gu64_t;
@@ -180,6 +180,15 @@ __device__ __forceinline__ float4 get_partial(const GemmArgs& a, int64_t idx) {
     return make_float4(t[0], t[1], t[2], t[3]);
   }
   return a.partials[idx];
+}
+// merging block, XCD-local protocol: every partial it merges came from its own XCD's L2
+__device__ __forceinline__ void xcd_verify(const GemmArgs& a, const float4 (&p)[MERGE_MAX], unsigned ns) {
+  if (!a.xcd_local) return;
+  const unsigned me = my_xcc();
+  bool bad = false;
+#pragma unroll
+  for (int sp = 0; sp < MERGE_MAX; ++sp) bad |= (unsigned)sp < ns && __float_as_uint(p[sp].w) != me;
+  if (bad) __hip_atomic_fetch_or(a.counters + XCD_ERR_SLOT, 1u << me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // the first MERGE_MAX splits' partials of `row`, every load issued before the first use (one
 // round trip; the protocol branch sits outside the loads so none of them waits on another)
@@ -709,7 +718,6 @@ gemm_softmax_kernel(GemmArgs a) {
     // before the ticket: every storing wave drains (vmcnt(0)), the workgroup barrier orders the
     // waves, then one lane takes the ticket; the merging block keeps its agent acquire
     // (cdna_hip_programming.md Guideline 16, R1). XCD-local protocol: see put_partial.
-    if (a.xcd_local) xcd_check(a);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int64_t row = row0 + t * 16 + col;
@@ -731,6 +739,7 @@ gemm_softmax_kernel(GemmArgs a) {
         const unsigned ns = gridDim.y;
         float4 p[MERGE_MAX];
         get_partials(a, row, ns, p);  // clamped: unconditional
+        xcd_verify(a, p, ns);
         RowState S{p[0].x, p[0].y, __float_as_int(p[0].z)};
 #pragma unroll
         for (int sp = 1; sp < MERGE_MAX; ++sp)  // fixed split order: deterministic
@@ -1106,7 +1115,6 @@ gemm_softmax32_kernel(GemmArgs a) {
     return;
   }
   // split classes: the 16x16 kernel's publish / last-arriver merge (see there)
-  if (a.xcd_local) xcd_check(a);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     const int64_t row = row0 + rt * 32 + col;
@@ -1125,6 +1133,7 @@ gemm_softmax32_kernel(GemmArgs a) {
       const unsigned ns = gridDim.y;
       float4 p[MERGE_MAX];
       get_partials(a, mrow, ns, p);
+      xcd_verify(a, p, ns);
       RowState R{p[0].x, p[0].y, __float_as_int(p[0].z)};
 #pragma unroll
       for (int sp = 1; sp < MERGE_MAX; ++sp)
@@ -1694,7 +1703,7 @@ void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
     MLAPI_HIP_CHECK(hipGetLastError());
     return;
   }
-  // XCD-local split merge (xcd_check / put_partial): on by default, MLAPI_GEMM_XCD=0 selects the
+  // XCD-local split merge (put_partial / xcd_verify): on by default, MLAPI_GEMM_XCD=0 selects the
   // agent-scope protocol. The grid's x extent is padded to a multiple of 8 (blocks past the batch
   // return at once) so that every split of a row block lands on the same XCD.
   static const int xcd_env = [] {

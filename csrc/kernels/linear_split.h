@@ -20,11 +20,13 @@
 //    the last arriver (agent-scope acquire) loads every split's state in fixed split order and
 //    writes (label, p_max) - or the serving completion record.
 //  * XCD-local merge (xcd_local): the grid is 1-D and ordered so that every split of a row group
-//    runs on ONE XCD (hardware block b runs on XCD b % 8: row group r -> XCD r % 8). All of the
-//    protocol's traffic - partial stores, the ticket, the last arriver's loads - then meets in that
-//    XCD's L2: plain stores, an L2 atomic and L1-bypassing (sc0) loads, with no write-through to
-//    HBM and no agent-scope L2 invalidate (buffer_inv sc1) on the merge path. Every block checks
-//    the XCD it really runs on (HW_REG_XCC_ID) and flags a mismatch in the workspace's error word.
+//    runs on ONE XCD (blocks are dealt round-robin over the 8 XCDs, starting wherever the
+//    dispatcher's rotation stood: block b runs on XCD (c + b) % 8, and the splits of row group r
+//    are the blocks with b % 8 == r % 8). All of the protocol's traffic - partial stores, the
+//    ticket, the last arriver's loads - then meets in that XCD's L2: plain stores, an L2 atomic and
+//    L1-bypassing (sc0) loads, with no write-through to HBM and no agent-scope L2 invalidate
+//    (buffer_inv sc1) on the merge path. Each partial carries the XCD that wrote it
+//    (HW_REG_XCC_ID); the merging block checks them and flags a mismatch in the error word.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -52,7 +54,7 @@ struct SplitArgs {
   RecOut ro;            // serving: per-row completion records instead of out_idx / out_p
   unsigned int* counters;  // [row groups], zero between launches (re-armed by the merging block)
   float4* partials;        // [row groups][nsplit][32] {m, s, argmax bits, 0}
-  unsigned int* xcd_err;   // xcd_local: set non-zero by a block that runs on another XCD than planned
+  unsigned int* xcd_err;   // xcd_local: bit x set when a merging block on XCD x read a partial written elsewhere
   int32_t xcd_local;        // 1-D XCD-ordered grid + L2-local merge protocol (see the header)
   int32_t row_groups;
   int32_t probe;           // measurement only (MLAPI_SPLIT_PROBE): 1 = stop after the block merge, 2 = after the partial stores
@@ -105,10 +107,6 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
     rgi = xcd + 8 * (j / a.nsplit);
     split = j % a.nsplit;
     if (rgi >= a.row_groups) return;  // uniform per block
-    unsigned hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
-    if ((int)(hw & 15) != xcd && threadIdx.x == 0)
-      __hip_atomic_fetch_or(a.xcd_err, 1u << xcd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const int c0 = split * CLASSES_PER_BLOCK + wave * 16;
   const int row0 = rgi * ROWS_PER_GROUP;
@@ -214,7 +212,9 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
     if (live) {
       float4* dst = part + (int64_t)split * ROWS_PER_GROUP + l;
       if (a.xcd_local) {  // plain store: L1 is write-through, the row group's L2 is the meeting point
-        *dst = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
+        unsigned hw;      // 4th word: the XCD that wrote it (checked by the merging block)
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
+        *dst = make_float4(S.m, S.s, __int_as_float(S.bi), __uint_as_float(hw & 15));
       } else {  // write-through past this XCD's L2
         const unsigned long long ms =
             (unsigned long long)__float_as_uint(S.m) | ((unsigned long long)__float_as_uint(S.s) << 32);
@@ -258,6 +258,15 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
 #pragma unroll
       for (int u = 0; u < 16; ++u)
         if (sp0 + u < a.nsplit) S = smerge(S, SState{v[u].x, v[u].y, __float_as_int(v[u].z)}, OVR);
+      if (a.xcd_local) {  // every merged state came from this XCD's L2
+        unsigned me;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(me));
+        me &= 15;
+        bool bad = false;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) bad |= sp0 + u < a.nsplit && __float_as_uint(v[u].w) != me;
+        if (bad) __hip_atomic_fetch_or(a.xcd_err, 1u << me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   if (!live) return;

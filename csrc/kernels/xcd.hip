@@ -1,9 +1,10 @@
 // Block -> XCD placement probe for the XCD-local split merges (gemm_softmax.hip put_partial,
-// linear_split.h). Those protocols rely on hardware block b running on XCD b % 8 (round-robin
-// dispatch over the 8 XCDs of an SPX-mode MI355X): every split of a row block then meets in one
-// XCD's L2. Before the first XCD-local launch on a device, 1024 blocks record the XCD they run on
-// (HW_REG_XCC_ID); any block off the plan (another partition mode, another dispatch order)
-// switches the XCD-local protocol off for that device, and the agent-scope protocol is used.
+// linear_split.h). Those protocols rely on blocks b and b + 8k running on one XCD (round-robin
+// dispatch over the 8 XCDs of an SPX-mode MI355X; the rotation's start varies from launch to
+// launch): every split of a row block then meets in one XCD's L2. Before the first XCD-local launch
+// on a device, 1024 blocks record the XCD they run on (HW_REG_XCC_ID); any block whose XCD differs
+// from that of block b % 8 (another partition mode, another dispatch order) switches the XCD-local
+// protocol off for that device, and the agent-scope protocol is used.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -41,7 +42,9 @@ int run_probe(int dev) {
   if (s != nullptr) (void)hipStreamDestroy(s);
   if (d != nullptr) (void)hipFree(d);
   int bad = 0;
-  for (int b = 0; b < PROBE_BLOCKS; ++b) bad += h[b] != (unsigned)(b & 7);
+  // the merges need blocks b and b + 8k on one XCD; the first XCD of a launch follows the
+  // dispatcher's rotation (block 0 need not run on XCD 0)
+  for (int b = 0; b < PROBE_BLOCKS; ++b) bad += h[b] != h[b & 7] || h[b] > 15;
   g_mismatch[dev].store(ok ? bad : -1);
   return ok && bad == 0 ? 1 : 2;
 }

@@ -116,8 +116,8 @@ class GemmSoftmax:
         return idx, p
 
     def xcd_errors(self) -> int:
-        """Bit mask of planned XCDs whose blocks ran elsewhere during an XCD-local split merge
-        (gemm_softmax.hip, put_partial); 0 while the block -> XCD placement held."""
+        """Bit mask of XCDs whose merging block read a partial written on another XCD during an
+        XCD-local split merge (gemm_softmax.hip, xcd_verify); 0 while every merge stayed in one L2."""
         o = C().gemm_softmax_xcd_err_offset()
         if self.ws.numel() < o + 4:
             return 0  # no split plan has run: nothing was checked
@@ -157,8 +157,8 @@ class LinearSplit:
         return idx, p
 
     def xcd_errors(self) -> int:
-        """Bit mask of planned XCDs whose blocks ran elsewhere (XCD-local merge); 0 when the
-        hardware's round-robin block -> XCD placement held for every launch so far."""
+        """Bit mask of XCDs whose merging block read a partial written on another XCD (XCD-local
+        merge); 0 while the splits of every row group met in one XCD's L2."""
         o = C().linear_split_xcd_err_offset()
         return int(self.ws[o:o + 4].view(torch.int32).item())
 

@@ -164,7 +164,7 @@ def test_gemm_softmax_large_batch_and_rearm():
 def test_gemm_softmax_xcd_local_merge_repeated(B, kind):
     """BASELINE config 3 (B = 1024, K = 1000, F = 256) and a 4-split plan: the row blocks' splits meet
     in one XCD's L2 (gemm_softmax.hip, put_partial). Twenty back-to-back launches on fresh inputs all
-    match the oracle, and no block ran on another XCD than planned."""
+    match the oracle, and every merged partial came from the merging block's XCD."""
     F, K = 256, 1000
     W = _rand((K, F), torch.bfloat16, 61, scale=1 / 16)
     b = _rand((K,), torch.float32, 62, scale=0.1)
@@ -490,7 +490,7 @@ def test_linear_split_xcd_local_merge_repeated(B, kind):
     """BASELINE config 3 shape (K = 1000, F = 256): 32 / 64 row groups whose 16 splits meet in one
     XCD's L2 (linear_split.h, XCD-local merge). Twenty back-to-back launches on fresh inputs: every
     one matches the oracle (a counter not re-armed or a stale L2 read would show up as a wrong row),
-    and no block ran on another XCD than the plan."""
+    and every merged partial came from the merging block's XCD."""
     F, K = 256, 1000
     W = _rand((K, F), torch.bfloat16, 52, scale=1 / np.sqrt(F))
     b = _rand((K,), torch.float32, 53, scale=0.1)
