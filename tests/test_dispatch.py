@@ -217,6 +217,23 @@ def test_bench_self_launches_n_ranks():
     assert d["dispatch"] == "acceptor"
 
 
+def test_bench_self_launches_eight_ranks():
+    """The driver's whole-node shape, rehearsed on the CPU: `bench.py --cpu --gpus 8` starts 8
+    ranks (gloo), the acceptor deals connections round robin to all of them, and the line reports
+    dp8 with 8 balanced per-rank counts."""
+    r = _bench(["--cpu", "--gpus", "8", "--steps", "2", "--warmup", "1", "--reqs-per-conn", "16",
+                "--c1-requests", "50"], timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "dp8" and d["comm_nranks"] == 8
+    assert len(d["served_per_rank"]) == 8
+    mean = sum(d["served_per_rank"]) / 8
+    assert all(abs(v - mean) <= 0.02 * mean for v in d["served_per_rank"]), d["served_per_rank"]
+    assert d["body_mismatches"] == 0
+
+
 def test_bench_refuses_world_size_mismatch():
     r = _bench(["--cpu", "--gpus", "2", "--steps", "1", "--warmup", "0"], env={"WORLD_SIZE": "1"})
     assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
