@@ -162,12 +162,18 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         cpu_util["loadgen_process"] = utilization(l0, cpu_by_group(lg.pid), elapsed).get("process_total", 0.0)
         s1, h1 = srv.runtime.handle.stats(), srv.http.stats()
         nreq = max(1, s1["requests"] - s0["requests"])
+        nbat = max(1, (s1["batches"] - s0["batches"]) - (s1["idle_batches"] - s0["idle_batches"]))
         # where this rank's server CPU goes, per request (IO-thread stage clock, exclusive; "poll"
         # is epoll_wait + loop overhead, mostly idle blocking) and the server-side HTTP latency
         cpu_breakdown = {
             "server_cpu_us_per_req": cpu_util.get("process_total", 0.0) * elapsed / nreq * 1e6,
             "io_stage_us_per_req": {k: (h1["stage_ns"][k] - h0["stage_ns"][k]) / nreq / 1e3 for k in h1["stage_ns"]},
             "engine_queue_wait_us_per_req": (s1["queue_wait_us_sum"] - s0["queue_wait_us_sum"]) / nreq,
+            # engine threads, per GPU batch (launched by the batcher): where a batch's time goes
+            "batcher_us_per_batch": {k: (s1["batcher_ns"][k] - s0["batcher_ns"][k]) / nbat / 1e3
+                                     for k in s1["batcher_ns"]},
+            "completer_us_per_batch": {k: (s1["completer_ns"][k] - s0["completer_ns"][k]) / nbat / 1e3
+                                       for k in s1["completer_ns"]},
             "server_http_latency_us_mean": (h1["http_latency_sum_ns"] - h0["http_latency_sum_ns"]) / 1e3
             / max(1, h1["http_latency_count"] - h0["http_latency_count"]),
         }

@@ -95,6 +95,15 @@ py::dict stats_dict(const EngineStats& s) {
   d["latency_sum_us"] = s.latency_sum_us;
   d["device_us_sum"] = s.device_us_sum;
   d["queue_wait_us_sum"] = s.queue_wait_us_sum;
+  {
+    py::dict bn, cn;
+    const char* bs[4] = {"take", "slot", "launch", "book"};
+    for (int i = 0; i < 4; ++i) bn[bs[i]] = s.batcher_ns[i];
+    cn["wait_gpu"] = s.completer_ns[0];
+    cn["deliver"] = s.completer_ns[1];
+    d["batcher_ns"] = bn;
+    d["completer_ns"] = cn;
+  }
   d["queue_depth"] = s.queue_depth;
   d["model_version"] = s.model_version;
   d["healthy"] = s.healthy;

@@ -596,6 +596,7 @@ void Engine::batcher_loop() {
   std::vector<double> xs;
   metas.reserve(4096);
   xs.reserve(4096 * 8);
+  int64_t t_take = 0;
   for (;;) {
     if (cfg_.spin_us > 0 && q_count_.load(std::memory_order_acquire) == 0) {
       // Adaptive spin: under load the next request arrives within microseconds; polling the
@@ -612,6 +613,7 @@ void Engine::batcher_loop() {
         q_cv_.wait_for(lk, std::chrono::microseconds(cfg_.max_wait_us),
                        [&] { return stopping_ || (int)q_meta_.size() >= cfg_.max_batch; });
       }
+      t_take = now_ns();
       batcher_sleeping_ = false;
       metas.swap(q_meta_);
       xs.swap(q_x_);
@@ -620,6 +622,8 @@ void Engine::batcher_loop() {
       q_count_.store(0, std::memory_order_release);
     }
     const std::shared_ptr<const Model> m = model();
+    int64_t t_prev = now_ns();
+    double take_ns = (double)(t_prev - t_take);  // charged to the first batch of this take
     size_t pos = 0;
     while (pos < metas.size()) {
       const size_t n = std::min(metas.size() - pos, (size_t)cfg_.max_batch);
@@ -637,6 +641,7 @@ void Engine::batcher_loop() {
         si = free_slots_.front();
         free_slots_.pop_front();
       }
+      const int64_t t_slot = now_ns();
       Slot& s = slots_[si];
       TraceRange tr("mlapi.batch.launch");
       s.metas.swap(chunk);
@@ -666,13 +671,23 @@ void Engine::batcher_loop() {
         for (const Meta& mt : s.metas) qw += (double)(s.t_launch - mt.t_enq);
         std::lock_guard<std::mutex> lk(st_mu_);
         stats_.queue_wait_us_sum += qw * 1e-3;
+        stats_.batcher_ns[0] += take_ns;
+        stats_.batcher_ns[1] += (double)(t_slot - t_prev);
+        stats_.batcher_ns[2] += (double)(s.t_launch - t_slot);
       }
+      take_ns = 0;
       {
         std::lock_guard<std::mutex> lk(s_mu_);
         inflight_.push_back(si);
         inflight_n_.fetch_add(1, std::memory_order_release);
       }
       s_cv_.notify_all();
+      const int64_t t_end = now_ns();
+      {
+        std::lock_guard<std::mutex> lk(st_mu_);
+        stats_.batcher_ns[3] += (double)(t_end - s.t_launch);
+      }
+      t_prev = t_end;
     }
     metas.clear();
     xs.clear();
@@ -902,6 +917,7 @@ void Engine::completer_loop() {
       inflight_n_.fetch_sub(1, std::memory_order_relaxed);
     }
     Slot& s = slots_[si];
+    const int64_t t_w0 = now_ns();
     if (s.launched) {
       TraceRange tw("mlapi.batch.wait_gpu");
       wait_done(s);
@@ -924,6 +940,12 @@ void Engine::completer_loop() {
       free_slots_.push_back(si);
     }
     s_cv_.notify_all();
+    {
+      const int64_t t_d1 = now_ns();
+      std::lock_guard<std::mutex> lk(st_mu_);
+      stats_.completer_ns[0] += (double)(now - t_w0);
+      stats_.completer_ns[1] += (double)(t_d1 - now);
+    }
   }
 }
 

@@ -158,6 +158,12 @@ struct EngineStats {
   double latency_sum_us = 0;
   double device_us_sum = 0;         // launch -> completion observed by the completer
   double queue_wait_us_sum = 0;     // per row: submit -> its batch's launch (batcher queue + packing)
+  // Engine-thread stage clocks (ns, summed over GPU batches): batcher - take (queue swap + model
+  // ref), slot (wait for a free slot), launch (pack + dispatch), book (stats, in-flight hand-off,
+  // wake); completer - wait_gpu (launch -> records seen), deliver (collect + per-sink delivery +
+  // slot return). Sleeping on an empty queue is in neither.
+  double batcher_ns[4] = {0, 0, 0, 0};
+  double completer_ns[2] = {0, 0};
   uint64_t queue_depth = 0;
   uint64_t model_version = 0;
   bool healthy = true;
