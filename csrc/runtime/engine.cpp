@@ -592,9 +592,10 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
 void Engine::batcher_loop() {
   pthread_setname_np(pthread_self(), "mlapi-batch");
   if (cfg_.device >= 0) (void)hipSetDevice(cfg_.device);
-  std::vector<Meta> metas;
+  std::vector<Meta> metas, chunk;
   std::vector<double> xs;
   metas.reserve(4096);
+  chunk.reserve(4096);
   xs.reserve(4096 * 8);
   int64_t t_take = 0;
   for (;;) {
@@ -627,7 +628,9 @@ void Engine::batcher_loop() {
     size_t pos = 0;
     while (pos < metas.size()) {
       const size_t n = std::min(metas.size() - pos, (size_t)cfg_.max_batch);
-      std::vector<Meta> chunk(metas.begin() + pos, metas.begin() + pos + n);
+      // no allocation per batch: chunk and the slots' meta vectors trade buffers (s.metas.swap
+      // below hands this one to the slot and takes back the slot's cleared one)
+      chunk.assign(metas.begin() + pos, metas.begin() + pos + n);
       pos += n;
       if (cfg_.device < 0 || !m) {
         run_cpu(chunk, xs, m);
