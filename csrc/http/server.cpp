@@ -263,6 +263,12 @@ class IoThread : public Sink {
   void wake() {
     pending_.store(true);
     if (spinning_.load()) return;
+    // Only a thread blocked (or about to block) in epoll_wait needs the eventfd: a running one
+    // sees `pending_` before it blocks again. Dekker pair with loop(): it stores blocked_ and then
+    // loads pending_, this stores pending_ and then loads blocked_ (all seq_cst), so at least one
+    // side sees the other and no hand-off is lost. Under load most IO threads are running, and
+    // each eventfd write that wakes a sleeping reader costs the completer ~1 us.
+    if (!blocked_.load()) return;
     if (!signaled_.exchange(true)) {
       const uint64_t one = 1;
       ssize_t r = write(evfd_, &one, sizeof one);
@@ -394,7 +400,12 @@ class IoThread : public Sink {
         if (pending_.load()) timeout = 0;
       }
       stage(SS_POLL);
+      if (timeout != 0) {
+        blocked_.store(true);
+        if (pending_.load()) timeout = 0;  // a hand-off that did not write the eventfd
+      }
       const int n = epoll_wait(epfd_, evs, 256, timeout);
+      blocked_.store(false);
       const bool spin_enabled = always_spin_ns > 0 || lowload_spin_ns > 0;
       if (n > 0 && spin_enabled) last_active = mono_ns();
       // hand-offs posted while spinning come without an eventfd write (also the ones that raced
@@ -1075,6 +1086,7 @@ class IoThread : public Sink {
   std::atomic<bool> signaled_{false};
   std::atomic<bool> pending_{false};   // completions / slow responses queued for this thread
   std::atomic<bool> spinning_{false};  // inside the busy-poll window (no eventfd needed)
+  std::atomic<bool> blocked_{true};    // in (or about to enter) a blocking epoll_wait: hand-offs need the eventfd
   std::mutex mu_;
   std::vector<int> adopted_;  // acceptor mode: connections handed over by the dispatcher
   bool timing_ = false;
