@@ -158,9 +158,14 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     // host data path with an HDP flush before the doorbell). Measured on MI355X
     // (profiles/r2_signal/hsa_probe_kernarg.txt), batch-1 launch -> done with a 3.5 KB argument:
     // device ring 6.9 us, hipLaunchKernel 9.5 us, host kernarg pool 14.0 us.
+    // MLAPI_KERNARG_HOST=1: the ring in host memory instead - no HDP flush + read-back on the
+    // launching (batcher) thread, at the price of the packet processor reading the block over the
+    // host link.
+    const char* kh = getenv("MLAPI_KERNARG_HOST");
+    const bool host_ring = kh != nullptr && atoi(kh) != 0;
     hsa_amd_hdp_flush_t hdp{};
     hsa_amd_memory_pool_t dpool{};
-    if (hsa_agent_get_info(gpu_, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp) == HSA_STATUS_SUCCESS &&
+    if (!host_ring && hsa_agent_get_info(gpu_, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp) == HSA_STATUS_SUCCESS &&
         hdp.HDP_MEM_FLUSH_CNTL != nullptr &&
         hsa_amd_agent_iterate_memory_pools(gpu_, pick_device_pool, &dpool) == HSA_STATUS_INFO_BREAK &&
         hsa_amd_memory_pool_allocate(dpool, (size_t)stride_ * ka_slots_, 0, (void**)&kernargs_) == HSA_STATUS_SUCCESS) {

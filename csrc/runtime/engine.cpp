@@ -151,7 +151,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       free_slots_.push_back(i);
     }
   }
-  batcher_ = std::thread([this] { batcher_loop(); });
+  for (int i = 0; i < std::max(1, cfg_.batchers); ++i) batchers_.emplace_back([this] { batcher_loop(); });
   if (cfg_.device >= 0)
     for (int i = 0; i < std::max(1, cfg_.completers); ++i) completers_.emplace_back([this] { completer_loop(); });
 }
@@ -185,7 +185,8 @@ void Engine::stop() {
     stopping_ = true;
   }
   q_cv_.notify_all();
-  if (batcher_.joinable()) batcher_.join();
+  for (std::thread& t : batchers_)
+    if (t.joinable()) t.join();
   s_cv_.notify_all();
   for (std::thread& t : completers_)
     if (t.joinable()) t.join();
@@ -329,7 +330,7 @@ int Engine::submit_many(const double* X, int n, int nf, const uint64_t* tags, Si
     q_x_.insert(q_x_.end(), X, X + (size_t)n * nf);
     for (int i = 0; i < n; ++i, off += nf) q_meta_.push_back(Meta{tags[i], sink, t, nf, off});
     q_count_.store((int)q_meta_.size(), std::memory_order_release);
-    wake = batcher_sleeping_;
+    wake = batchers_sleeping_ > 0;
   }
   if (wake) q_cv_.notify_one();
   return n;
@@ -607,15 +608,16 @@ void Engine::batcher_loop() {
     }
     {
       std::unique_lock<std::mutex> lk(q_mu_);
-      if (q_meta_.empty()) batcher_sleeping_ = true;
+      const bool slept = q_meta_.empty();
+      if (slept) ++batchers_sleeping_;
       q_cv_.wait(lk, [&] { return stopping_ || !q_meta_.empty(); });
-      if (q_meta_.empty() && stopping_) break;
+      if (slept) --batchers_sleeping_;
+      if (q_meta_.empty() && stopping_) break;  // (another batcher may have taken the last rows)
       if (cfg_.max_wait_us > 0 && (int)q_meta_.size() < cfg_.max_batch && !stopping_) {
         q_cv_.wait_for(lk, std::chrono::microseconds(cfg_.max_wait_us),
                        [&] { return stopping_ || (int)q_meta_.size() >= cfg_.max_batch; });
       }
       t_take = now_ns();
-      batcher_sleeping_ = false;
       metas.swap(q_meta_);
       xs.swap(q_x_);
       q_meta_.clear();
@@ -697,7 +699,7 @@ void Engine::batcher_loop() {
   }
   {
     std::lock_guard<std::mutex> lk(s_mu_);
-    batcher_done_ = true;
+    ++batchers_done_;
   }
   s_cv_.notify_all();
 }
@@ -831,7 +833,7 @@ bool Engine::run_idle(const double* X, int n, int nf, const uint64_t* tags, std:
   const int64_t t = now_ns();
   {
     std::lock_guard<std::mutex> lk(q_mu_);
-    if (stopping_ || !q_meta_.empty() || !batcher_sleeping_) return false;
+    if (stopping_ || !q_meta_.empty() || batchers_sleeping_ < (int)batchers_.size()) return false;
   }
   CollectSink sink;
   sink.out = &out;
@@ -915,7 +917,7 @@ void Engine::completer_loop() {
     }
     {
       std::unique_lock<std::mutex> lk(s_mu_);
-      s_cv_.wait(lk, [&] { return !inflight_.empty() || batcher_done_; });
+      s_cv_.wait(lk, [&] { return !inflight_.empty() || batchers_done_ >= (int)batchers_.size(); });
       if (inflight_.empty()) break;  // batcher has exited and nothing is in flight
       si = inflight_.front();
       inflight_.pop_front();

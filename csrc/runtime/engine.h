@@ -131,6 +131,11 @@ struct EngineConfig {
   // overlaps the wait for batch k+1. Per-connection order is safe: a connection has at most one
   // request outstanding.
   int completers = 1;
+  // Batcher threads: each drains the queue and launches (packing + dispatch serialised on the
+  // launch lock); with two, one batch's queue take / slot wait / bookkeeping overlaps the other's
+  // launch. The batcher is a single-server queue at ~80 % utilisation under the c=64 load, which
+  // is what the rows' queue wait is made of (engine stage clocks).
+  int batchers = 1;
   int max_queue = 1 << 20;  // backpressure: rows waiting for the batcher; beyond it submit is refused
   // Kernel-argument batches go through the engine's own HSA queue (direct_dispatch.h) when the
   // serving code object loads; empty path or failure -> hipLaunchKernel.
@@ -273,7 +278,7 @@ class Engine {
   std::vector<Meta> q_meta_;
   std::vector<double> q_x_;
   bool stopping_ = false;
-  bool batcher_sleeping_ = false;  // guarded by q_mu_: submit wakes the batcher only if true
+  int batchers_sleeping_ = 0;  // guarded by q_mu_: submit wakes a batcher only if one sleeps
   std::atomic<int> q_count_{0};    // rows queued (lock-free hint for the batcher's spin phase)
 
   // GPU slots
@@ -285,7 +290,7 @@ class Engine {
   std::deque<int> free_slots_;
   std::deque<int> inflight_;
   std::atomic<int> inflight_n_{0};  // inflight_.size(), readable without s_mu_ (completer spin)
-  bool batcher_done_ = false;
+  int batchers_done_ = 0;  // guarded by s_mu_: the completers exit once every batcher has
 
   size_t slot_row_bytes_ = 0;  // capacity of one packed row in a slot (any path)
   uint32_t* done_h_ = nullptr;  // per-slot done words (host-coherent, SIGNAL_STRIDE apart)
@@ -295,14 +300,14 @@ class Engine {
   InlineBatch inline_{};        // guarded by launch_mu_
   std::mutex launch_mu_;        // launch_batch: batcher thread and run_idle callers
 
-  std::thread batcher_;
+  std::vector<std::thread> batchers_;
   std::vector<std::thread> completers_;
   std::atomic<bool> healthy_{true};
   std::atomic<bool> drop_{false};
 
   mutable std::mutex st_mu_;
   EngineStats stats_;
-  uint64_t batch_counter_ = 0;
+  std::atomic<uint64_t> batch_counter_{0};  // fault injection (fail_every), any batcher
 };
 
 // Reference float64 implementation of the fused epilogue (CPU backend + host-side oracle).

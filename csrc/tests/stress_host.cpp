@@ -99,6 +99,7 @@ void engine_stress() {
   EngineConfig cfg;
   cfg.device = -1;
   cfg.max_batch = 64;
+  cfg.batchers = 2;  // two batcher threads draining one queue
   Engine eng(cfg);
   auto m0 = make_model(1, KIND_MULTINOMIAL);
   eng.load_model(m0.kind, m0.F, m0.K, m0.W.data(), m0.b.data(), {"\"a\"", "\"b\"", "\"c\""});

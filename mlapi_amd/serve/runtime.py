@@ -64,6 +64,7 @@ class EngineHandle:
         ec.inline_args = bool(config.inline_args)
         ec.idle_inline_rows = int(config.idle_inline_rows)
         ec.completers = int(config.completers)
+        ec.batchers = int(config.batchers)
         ec.record_completion = bool(config.record_completion)
         ec.stage_wide = bool(config.stage_wide)
         ec.max_queue = config.max_queue

@@ -27,6 +27,8 @@
 #   split_xcd     XCD-local vs agent-scope split merge (MLAPI_SPLIT_XCD=1/0), B = 32..2048, x2 + kernel stats
 #   threads       IO-thread / load-generator-thread split sweep, THREADS="io:cl ..." (default "10:4 8:6 6:6"), x2
 #   gdw           softmax G+dW kernel: its GPU tests + tools/softmax_train_sweep.py timings
+#   serve_ab_old  interleaved x3 serve bench: ab_old/ (previous build) vs the working tree
+#   serve_ab3     interleaved x2: ab_old/ vs the working tree vs the working tree with AB_ENV (e.g. MLAPI_KERNARG_HOST=1)
 #   gemm_ab       interleaved x3 gemm bench: ab_old/mlapi_amd (stashed previous build) vs the working tree
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -227,6 +229,21 @@ for s in $steps; do
     gdw)
       run pytest_gdw 240 python -u -m pytest tests/test_kernels_gpu.py -k "softmax_grad" -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
       run gdw_sweep 180 python -u tools/softmax_train_sweep.py ;;
+    serve_ab_old)  # interleaved x3 serve bench: ab_old/ (previous build + its bench.py) vs the working tree
+      for r in 1 2 3; do
+        run "serve_old_r$r" 300 python -c "import sys, runpy; sys.path.insert(0, 'ab_old'); sys.argv = ['bench.py'] + sys.argv[1:]; runpy.run_path('ab_old/bench.py', run_name='__main__')" \
+          --steps 100 --warmup 10 ${EXTRA:-}
+        run "serve_new_r$r" 300 python -u bench.py --steps 100 --warmup 10 ${EXTRA:-}
+      done ;;
+    serve_ab3)  # interleaved x2: ab_old/ (previous build) vs the working tree vs the working tree with AB_ENV set
+      for r in 1 2; do
+        run "serve_old_r$r" 300 python -c "import sys, runpy; sys.path.insert(0, 'ab_old'); sys.argv = ['bench.py'] + sys.argv[1:]; runpy.run_path('ab_old/bench.py', run_name='__main__')" \
+          --steps 100 --warmup 10
+        run "serve_new_r$r" 300 python -u bench.py --steps 100 --warmup 10
+        env ${AB_ENV:-MLAPI_NOTHING=1} timeout -k 10 300 python -u bench.py --steps 100 --warmup 10 > "$O/serve_newenv_r$r.log" 2>&1 \
+          || stop "serve_newenv_r$r" $? "$O/serve_newenv_r$r.log"
+        tail -1 "$O/serve_newenv_r$r.log" | cut -c1-200
+      done ;;
     gemm_ab)
       for r in 1 2 3; do
         run "gemm_old_r$r" 120 python -c "import sys, runpy; sys.path.insert(0, 'ab_old'); sys.argv = ['bench.py'] + sys.argv[1:]; runpy.run_path('bench.py', run_name='__main__')" \
