@@ -214,6 +214,9 @@ def test_bench_self_launches_n_ranks():
     assert cb["server_cpu_us_per_req"] > 0
     assert set(cb["io_stage_us_per_req"]) == {"poll", "recv", "parse", "submit", "idle_gpu", "render", "send",
                                               "handoff"}
+    # engine-thread stage clocks per GPU batch (zero on the CPU backend, which has no GPU batches)
+    assert set(cb["batcher_us_per_batch"]) == {"take", "slot", "launch", "book"}
+    assert set(cb["completer_us_per_batch"]) == {"wait_gpu", "deliver"}
     assert d["dispatch"] == "acceptor"
 
 
