@@ -400,6 +400,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("idle_inline_rows", &EngineConfig::idle_inline_rows)
       .def_readwrite("completers", &EngineConfig::completers)
       .def_readwrite("batchers", &EngineConfig::batchers)
+      .def_readwrite("gemv_record_rows", &EngineConfig::gemv_record_rows)
       .def_readwrite("record_completion", &EngineConfig::record_completion)
       .def_readwrite("stage_wide", &EngineConfig::stage_wide)
       .def_readwrite("direct_dispatch", &EngineConfig::direct_dispatch)

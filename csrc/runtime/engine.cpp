@@ -556,11 +556,14 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     launch_linear_small(m.xdt, X, m.ldx, m.dW, m.db, n, m.F, m.K, m.kind, s.didx, s.dp, stream_, sig);
   } else {
     // GEMM: completion records written by the kernel's result stores (no trailing one-wave
-    // serve_signal launch: 3.9 us of GPU time and a hipLaunchKernel per batch). GEMV keeps the
-    // signal kernel: with records its batch-1 leg measured 6.3-6.9 us vs 5.6-6.0
-    // (profiles/r2_records/wide_ab/); the GEMM's was unchanged (10.2-10.6 vs 10.2-10.5).
+    // serve_signal launch: 3.9 us of GPU time and a hipLaunchKernel per batch). GEMV: records from
+    // gemv_record_rows rows up - a batch-1 leg measured 6.3-6.9 us with records vs 5.6-6.0 with the
+    // signal kernel (profiles/r2_records/wide_ab/), but under load the signal kernel's second
+    // hipLaunchKernel is batcher time, and the batcher is what queues the rows (engine stage
+    // clocks: launch ~10 us per GEMV batch at c=64, profiles/r3_s19/).
     RecOut ro;
-    if (cfg_.record_completion && m.path == PATH_GEMM) {
+    const bool gemv_rec = m.path == PATH_GEMV && cfg_.gemv_record_rows > 0 && n >= cfg_.gemv_record_rows;
+    if (cfg_.record_completion && (m.path == PATH_GEMM || gemv_rec)) {
       ro.rec = s.drec;
       ro.seq = sig.seq;
       s.rec_mode = REC_ROWS;

@@ -120,6 +120,7 @@ struct EngineConfig {
   // ... and complete through per-row 16-byte records {seq, idx, p} (one store per row, no fence,
   // no done word) instead of outputs + a fenced done word
   bool record_completion = true;
+  int gemv_record_rows = 2;  // GEMV batches of at least this many rows complete through records (0 = never)
   bool stage_wide = false;  // GEMV / GEMM / GENERIC: H2D-copy the rows first (default: zero-copy reads)
   int watchdog_ms = 2000; // batch not complete after this -> engine marked unhealthy
   int fail_every = 0;     // fault injection: fail every N-th batch with ST_DEVICE_ERROR

@@ -65,6 +65,7 @@ class EngineHandle:
         ec.idle_inline_rows = int(config.idle_inline_rows)
         ec.completers = int(config.completers)
         ec.batchers = int(config.batchers)
+        ec.gemv_record_rows = int(config.gemv_record_rows)
         ec.record_completion = bool(config.record_completion)
         ec.stage_wide = bool(config.stage_wide)
         ec.max_queue = config.max_queue

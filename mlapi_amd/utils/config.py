@@ -51,6 +51,7 @@ class Config:
     record_completion: bool = True            # GPU: kernel-argument batches complete through 16-B per-row records
     completers: int = 1                       # GPU: completer threads (done-word wait + delivery)
     batchers: int = 1                         # batcher threads (queue take + launch; launches serialised)
+    gemv_record_rows: int = 2                 # GEMV batches >= this many rows complete via records (0 = never)
     idle_inline_rows: int = 8                 # GPU: idle engine -> the IO thread launches <= this many rows itself (0 = off)
     direct_dispatch: bool = True              # GPU: ... written as AQL packets into the engine's own HSA queue
     stage_wide: bool = False                  # GPU: copy wide models' rows H2D first (default: zero-copy reads)
