@@ -174,6 +174,9 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
                                      for k in s1["batcher_ns"]},
             "completer_us_per_batch": {k: (s1["completer_ns"][k] - s0["completer_ns"][k]) / nbat / 1e3
                                        for k in s1["completer_ns"]},
+            # inside `launch`, zero-copy / BAR batches only (the wide models' paths), per such batch
+            "wide_launch_us_per_batch": {k: (s1["launch_ns"][k] - s0["launch_ns"][k]) / nbat / 1e3
+                                         for k in s1["launch_ns"]},
             "server_http_latency_us_mean": (h1["http_latency_sum_ns"] - h0["http_latency_sum_ns"]) / 1e3
             / max(1, h1["http_latency_count"] - h0["http_latency_count"]),
         }

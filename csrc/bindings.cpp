@@ -102,6 +102,10 @@ py::dict stats_dict(const EngineStats& s) {
     cn["wait_gpu"] = s.completer_ns[0];
     cn["deliver"] = s.completer_ns[1];
     d["batcher_ns"] = bn;
+    py::dict ln;
+    const char* ls[3] = {"pack", "flush", "kernel"};
+    for (int i = 0; i < 3; ++i) ln[ls[i]] = s.launch_ns[i];
+    d["launch_ns"] = ln;
     d["completer_ns"] = cn;
   }
   d["queue_depth"] = s.queue_depth;

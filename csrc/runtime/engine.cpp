@@ -457,25 +457,59 @@ void Engine::run_cpu(std::vector<Meta>& metas, const std::vector<double>& xs, co
 void Engine::pack_rows(Slot& s, const std::vector<double>& xs, const Model& m, void* dst) {
   const int F = m.F, ld = m.ldx;
   const size_t n = (size_t)s.n;
+  static const bool staged = [] {  // MLAPI_PACK_STAGED=0: convert straight into dst (the old loop)
+    const char* e = getenv("MLAPI_PACK_STAGED");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  const size_t es = dtype_size(m.xdt);
+  // staged: each row is converted in a cached scratch row (branch-free loops the compiler
+  // vectorises) and then copied out in one memcpy - dst is often the BAR (write-combined,
+  // uncached device memory), where element-by-element stores with a per-element select were
+  // the batcher's largest cost on wide models
+  thread_local std::vector<unsigned char> row;
+  if (staged && row.size() < (size_t)ld * es) row.resize((size_t)ld * es);
   for (size_t i = 0; i < n; ++i) {
     const bool ok = s.metas[i].nf == F;
     if (!ok) s.pre_status[i] = ST_SHAPE;
     const double* src = &xs[s.metas[i].off];
-    if (m.xdt == DT_F64) {
-      double* d = static_cast<double*>(dst) + i * ld;
-      if (ok)
+    unsigned char* d = static_cast<unsigned char*>(dst) + i * ld * es;
+    if (staged) {
+      if (!ok) {
+        std::memset(d, 0, (size_t)ld * es);
+        continue;
+      }
+      if (m.xdt == DT_F64) {
         std::memcpy(d, src, sizeof(double) * F);
+        if (ld > F) std::memset(d + sizeof(double) * F, 0, sizeof(double) * (ld - F));
+        continue;
+      }
+      if (m.xdt == DT_F32) {
+        float* t = reinterpret_cast<float*>(row.data());
+        for (int f = 0; f < F; ++f) t[f] = (float)src[f];
+        for (int f = F; f < ld; ++f) t[f] = 0.f;
+      } else {
+        uint16_t* t = reinterpret_cast<uint16_t*>(row.data());
+        for (int f = 0; f < F; ++f) t[f] = f32_to_bf16((float)src[f]);
+        for (int f = F; f < ld; ++f) t[f] = 0;
+      }
+      std::memcpy(d, row.data(), (size_t)ld * es);
+      continue;
+    }
+    if (m.xdt == DT_F64) {
+      double* dd = reinterpret_cast<double*>(d);
+      if (ok)
+        std::memcpy(dd, src, sizeof(double) * F);
       else
-        std::memset(d, 0, sizeof(double) * F);
-      for (int f = F; f < ld; ++f) d[f] = 0.0;
+        std::memset(dd, 0, sizeof(double) * F);
+      for (int f = F; f < ld; ++f) dd[f] = 0.0;
     } else if (m.xdt == DT_F32) {
-      float* d = static_cast<float*>(dst) + i * ld;
-      for (int f = 0; f < F; ++f) d[f] = ok ? (float)src[f] : 0.f;
-      for (int f = F; f < ld; ++f) d[f] = 0.f;
+      float* df = reinterpret_cast<float*>(d);
+      for (int f = 0; f < F; ++f) df[f] = ok ? (float)src[f] : 0.f;
+      for (int f = F; f < ld; ++f) df[f] = 0.f;
     } else {
-      uint16_t* d = static_cast<uint16_t*>(dst) + i * ld;
-      for (int f = 0; f < F; ++f) d[f] = ok ? f32_to_bf16((float)src[f]) : 0;
-      for (int f = F; f < ld; ++f) d[f] = 0;
+      uint16_t* dh = reinterpret_cast<uint16_t*>(d);
+      for (int f = 0; f < F; ++f) dh[f] = ok ? f32_to_bf16((float)src[f]) : 0;
+      for (int f = F; f < ld; ++f) dh[f] = 0;
     }
   }
 }
@@ -538,7 +572,9 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
   const size_t bytes = (size_t)n * m.ldx * dtype_size(m.xdt);
   const bool bar = s.xbar != nullptr && m.path != PATH_SMALL && n <= cfg_.bar_rows &&
                    bytes <= (size_t)cfg_.bar_rows * slot_row_bytes_;
+  const int64_t t_p0 = now_ns();
   pack_rows(s, xs, m, bar ? s.xbar : s.hx);
+  const int64_t t_p1 = now_ns();
   // rows: written into device HBM through the BAR (small wide batches: every wave then reads them
   // from HBM / L2), zero-copy from the pinned slot (one host-link round trip per reading wave), or
   // staged by a copy first (a blit kernel of its own: ~4 us at serving sizes)
@@ -546,12 +582,11 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
   if (bar) {
     direct_->bar_flush();
     X = s.xbar;
-    std::lock_guard<std::mutex> lk(st_mu_);
-    stats_.bar_batches++;
   } else if (m.path != PATH_SMALL && cfg_.stage_wide) {
     MLAPI_HIP_CHECK(hipMemcpyAsync(s.dstage, s.hx, bytes, hipMemcpyHostToDevice, stream_));
     X = s.dstage;
   }
+  const int64_t t_p2 = now_ns();
   if (m.path == PATH_SMALL || m.path == PATH_GENERIC) {
     launch_linear_small(m.xdt, X, m.ldx, m.dW, m.db, n, m.F, m.K, m.kind, s.didx, s.dp, stream_, sig);
   } else {
@@ -589,8 +624,13 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
                           static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_, ro);
     if (!s.rec_mode) launch_serve_signal(sig, stream_);
   }
+  const int64_t t_p3 = now_ns();
   std::lock_guard<std::mutex> lk(st_mu_);
   stats_.path_batches[m.path]++;
+  if (bar) stats_.bar_batches++;
+  stats_.launch_ns[0] += (double)(t_p1 - t_p0);
+  stats_.launch_ns[1] += (double)(t_p2 - t_p1);
+  stats_.launch_ns[2] += (double)(t_p3 - t_p2);
 }
 
 void Engine::batcher_loop() {

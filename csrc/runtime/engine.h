@@ -169,6 +169,10 @@ struct EngineStats {
   // wake); completer - wait_gpu (launch -> records seen), deliver (collect + per-sink delivery +
   // slot return). Sleeping on an empty queue is in neither.
   double batcher_ns[4] = {0, 0, 0, 0};
+  // inside `launch` for zero-copy / BAR batches (not kernel-argument ones): pack (rows -> the
+  // model dtype, into the slot or through the BAR), flush (HDP flush + read-back of BAR rows),
+  // kernel (the launch call(s))
+  double launch_ns[3] = {0, 0, 0};
   double completer_ns[2] = {0, 0};
   uint64_t queue_depth = 0;
   uint64_t model_version = 0;
