@@ -457,9 +457,12 @@ void Engine::run_cpu(std::vector<Meta>& metas, const std::vector<double>& xs, co
 void Engine::pack_rows(Slot& s, const std::vector<double>& xs, const Model& m, void* dst) {
   const int F = m.F, ld = m.ldx;
   const size_t n = (size_t)s.n;
-  static const bool staged = [] {  // MLAPI_PACK_STAGED=0: convert straight into dst (the old loop)
+  // MLAPI_PACK_STAGED=1: stage each row in a scratch row (below). Off by default: interleaved x2 on
+  // one box it was 0-7 % slower end to end than converting straight into dst
+  // (profiles/r3_pack_staged/), though its own pack stage was shorter at K = 1000.
+  static const bool staged = [] {
     const char* e = getenv("MLAPI_PACK_STAGED");
-    return e == nullptr || atoi(e) != 0;
+    return e != nullptr && atoi(e) != 0;
   }();
   const size_t es = dtype_size(m.xdt);
   // staged: each row is converted in a cached scratch row (branch-free loops the compiler
