@@ -119,6 +119,7 @@ py::dict stats_dict(const EngineStats& s) {
   d["path_batches"] = paths;
   d["inline_batches"] = s.inline_batches;
   d["direct_batches"] = s.direct_batches;
+  d["direct_wide_batches"] = s.direct_wide_batches;
   d["idle_batches"] = s.idle_batches;
   d["bar_batches"] = s.bar_batches;
   d["direct_dispatch"] = s.direct_dispatch;
@@ -405,6 +406,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("completers", &EngineConfig::completers)
       .def_readwrite("batchers", &EngineConfig::batchers)
       .def_readwrite("gemv_record_rows", &EngineConfig::gemv_record_rows)
+      .def_readwrite("direct_wide", &EngineConfig::direct_wide)
+      .def_readwrite("direct_wide_max_weight_bytes", &EngineConfig::direct_wide_max_weight_bytes)
       .def_readwrite("record_completion", &EngineConfig::record_completion)
       .def_readwrite("stage_wide", &EngineConfig::stage_wide)
       .def_readwrite("direct_dispatch", &EngineConfig::direct_dispatch)

@@ -61,6 +61,20 @@ struct RecOut {
   ServeRecord* rec = nullptr;
   uint32_t seq = 0;
 };
+
+// A queue of the caller's own that launches kernels of the serving code object by name
+// (csrc/runtime/direct_dispatch.cpp: AQL packets into an HSA queue, ~0.1 us of CPU instead of
+// hipLaunchKernel's ~3 us). `args`: the kernel's by-value argument block; grid in blocks.
+// ordered: the kernel starts after every earlier packet of that queue has finished and its writes
+// are released at kernel end (a stream's order: launches that share a workspace); unordered: it
+// may overlap earlier kernels and must publish what it writes itself (write-through completion
+// records). false: the kernel is not in the code object (the caller then uses hipLaunchKernel).
+class KernelLauncher {
+ public:
+  virtual ~KernelLauncher() = default;
+  virtual bool launch_kernel(const char* name, const void* args, size_t bytes, unsigned grid_x, unsigned grid_y,
+                             unsigned block, bool ordered) = 0;
+};
 #if defined(__HIP__)  // HIP sources (both compilation passes); plain C++ includers skip it
 __device__ __forceinline__ void put_record(ServeRecord* dst, uint32_t seq, int32_t idx, double p) {
   const uint64_t pb = __builtin_bit_cast(uint64_t, p);
@@ -87,7 +101,8 @@ void launch_linear_inline(int dt, const InlineBatch& a, hipStream_t stream);
 // X: [B, F] bf16 or f32 row-major; w: [F] same dtype; bias: scalar f32.
 // out_idx: int32[B] (z > 0), out_p: f32[B] = sigmoid(|z|) (kind BINARY) or sigmoid(2|z|).
 void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_t B, int F, int kind,
-                        int32_t* out_idx, float* out_p, hipStream_t stream, RecOut ro = RecOut{});
+                        int32_t* out_idx, float* out_p, hipStream_t stream, RecOut ro = RecOut{},
+                        KernelLauncher* direct = nullptr);
 
 // ---- gemm_softmax.hip: multiclass predict, bf16 MFMA GEMM + online softmax/argmax epilogue ----
 // X: [B, F] bf16; W: [K, F] bf16; b: [K] f32. F in {32, 64, 128, 256} or a multiple of 256 (any
@@ -161,9 +176,13 @@ bool xcd_local_allowed(hipStream_t stream);
 int xcd_placement_state(int device);
 int xcd_placement_mismatches(int device);
 int linear_split_nsplit(int K);
+// direct: launch through that queue instead of `stream` (the caller keeps every launch that shares
+// the workspace on one of the two; serving completes through records, so nothing else needs the
+// stream's order)
 void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K,
                          int kind, int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes,
-                         hipStream_t stream, RecOut ro = RecOut(), SplitRecOut sro = SplitRecOut());
+                         hipStream_t stream, RecOut ro = RecOut(), SplitRecOut sro = SplitRecOut(),
+                         KernelLauncher* direct = nullptr);
 
 // Multiclass training row stats (gemm_softmax.hip MODE 2), X_aug = [X | 0.. | 1 | 0 x 7] bf16
 // read through its row stride ldx (the first F columns); W: [K, F] bf16; b: [K] f32.

@@ -1,6 +1,7 @@
 // Host launchers of the class-split multiclass predict (linear_split.h).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 
@@ -22,7 +23,16 @@ __global__ __launch_bounds__(256) void linear_split_kernel(split::SplitArgs a) {
 }
 
 template <typename T, int KS>
-void launch_ks(const split::SplitArgs& a, dim3 grid, bool nb2, bool ovr, hipStream_t stream) {
+void launch_ks(const split::SplitArgs& a, dim3 grid, bool nb2, bool ovr, hipStream_t stream, KernelLauncher* direct) {
+  if (direct != nullptr) {
+    // the same kernel, unmangled, in the serving code object (serve_direct.hip)
+    char name[64];
+    std::snprintf(name, sizeof name, "mlapi_split_%s_ks%d_nb%d_%s", sizeof(T) == 2 ? "bf16" : "f32", KS, nb2 ? 2 : 1,
+                  ovr ? "ovr" : "mn");
+    // host merge (hrec): write-through records and no workspace - unordered; the in-kernel merge
+    // re-arms the workspace counters for the next launch - ordered
+    if (direct->launch_kernel(name, &a, sizeof a, grid.x, grid.y, 256, a.hrec == nullptr)) return;
+  }
   if (nb2) {
     if (ovr)
       hipLaunchKernelGGL((linear_split_kernel<T, KS, 2, true>), grid, dim3(256), 0, stream, a);
@@ -59,7 +69,7 @@ int linear_split_nsplit(int K) { return nsplits(K); }
 
 void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K,
                          int kind, int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes,
-                         hipStream_t stream, RecOut ro, SplitRecOut sro) {
+                         hipStream_t stream, RecOut ro, SplitRecOut sro, KernelLauncher* direct) {
   if (B <= 0) return;
   if (!linear_split_supported(dt, F))
     throw std::invalid_argument("linear_split: bf16 F in 32..512 or f32 F in 16..512, a power of two");
@@ -110,20 +120,20 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
   const bool ovr = kind == KIND_OVR;
   if (dt == DT_BF16) {
     switch (F) {
-      case 32: launch_ks<uint16_t, 1>(a, grid, nb2, ovr, stream); break;
-      case 64: launch_ks<uint16_t, 2>(a, grid, nb2, ovr, stream); break;
-      case 128: launch_ks<uint16_t, 4>(a, grid, nb2, ovr, stream); break;
-      case 256: launch_ks<uint16_t, 8>(a, grid, nb2, ovr, stream); break;
-      default: launch_ks<uint16_t, 16>(a, grid, nb2, ovr, stream); break;
+      case 32: launch_ks<uint16_t, 1>(a, grid, nb2, ovr, stream, direct); break;
+      case 64: launch_ks<uint16_t, 2>(a, grid, nb2, ovr, stream, direct); break;
+      case 128: launch_ks<uint16_t, 4>(a, grid, nb2, ovr, stream, direct); break;
+      case 256: launch_ks<uint16_t, 8>(a, grid, nb2, ovr, stream, direct); break;
+      default: launch_ks<uint16_t, 16>(a, grid, nb2, ovr, stream, direct); break;
     }
   } else {
     switch (F) {
-      case 16: launch_ks<float, 1>(a, grid, nb2, ovr, stream); break;
-      case 32: launch_ks<float, 2>(a, grid, nb2, ovr, stream); break;
-      case 64: launch_ks<float, 4>(a, grid, nb2, ovr, stream); break;
-      case 128: launch_ks<float, 8>(a, grid, nb2, ovr, stream); break;
-      case 256: launch_ks<float, 16>(a, grid, nb2, ovr, stream); break;
-      default: launch_ks<float, 32>(a, grid, nb2, ovr, stream); break;
+      case 16: launch_ks<float, 1>(a, grid, nb2, ovr, stream, direct); break;
+      case 32: launch_ks<float, 2>(a, grid, nb2, ovr, stream, direct); break;
+      case 64: launch_ks<float, 4>(a, grid, nb2, ovr, stream, direct); break;
+      case 128: launch_ks<float, 8>(a, grid, nb2, ovr, stream, direct); break;
+      case 256: launch_ks<float, 16>(a, grid, nb2, ovr, stream, direct); break;
+      default: launch_ks<float, 32>(a, grid, nb2, ovr, stream, direct); break;
     }
   }
   MLAPI_HIP_CHECK(hipGetLastError());

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 
 #include "linear_rows.h"
+#include "gemv_binary.h"
+#include "linear_split.h"
 
 namespace {
 
@@ -48,3 +50,48 @@ extern "C" __global__ __launch_bounds__(128) void mlapi_inline_f64_4x3(const mla
 extern "C" __global__ __launch_bounds__(128) void mlapi_inline_f32_4x3(const mlapi::InlineBatch) {
   direct_inline<float, 4, 3, true>();
 }
+
+// The class-split multiclass predict (linear_split.h) for the engine's wide serving batches: the
+// same device code as linear_split.hip's linear_split_kernel<T, KS, NB, OVR>, one unmangled entry
+// per instantiation (launch_linear_split formats the name). It reads no implicit kernel argument
+// (no gridDim / blockDim), so the kernarg block is the SplitArgs alone.
+#define MLAPI_SPLIT_ENTRY(TN, T, KS, NB, OVR, SUF)                                                        \
+  extern "C" __global__ __launch_bounds__(256) void mlapi_split_##TN##_ks##KS##_nb##NB##_##SUF(          \
+      const mlapi::split::SplitArgs a) {                                                                \
+    mlapi::split::split_predict<T, KS, NB, OVR>(a);                                                     \
+  }
+#define MLAPI_SPLIT_ENTRIES(TN, T, KS)           \
+  MLAPI_SPLIT_ENTRY(TN, T, KS, 1, false, mn)     \
+  MLAPI_SPLIT_ENTRY(TN, T, KS, 1, true, ovr)     \
+  MLAPI_SPLIT_ENTRY(TN, T, KS, 2, false, mn)     \
+  MLAPI_SPLIT_ENTRY(TN, T, KS, 2, true, ovr)
+MLAPI_SPLIT_ENTRIES(bf16, uint16_t, 1)
+MLAPI_SPLIT_ENTRIES(bf16, uint16_t, 2)
+MLAPI_SPLIT_ENTRIES(bf16, uint16_t, 4)
+MLAPI_SPLIT_ENTRIES(bf16, uint16_t, 8)
+MLAPI_SPLIT_ENTRIES(bf16, uint16_t, 16)
+MLAPI_SPLIT_ENTRIES(f32, float, 1)
+MLAPI_SPLIT_ENTRIES(f32, float, 2)
+MLAPI_SPLIT_ENTRIES(f32, float, 4)
+MLAPI_SPLIT_ENTRIES(f32, float, 8)
+MLAPI_SPLIT_ENTRIES(f32, float, 16)
+MLAPI_SPLIT_ENTRIES(f32, float, 32)
+
+// The binary GEMV (gemv_binary.h) for record-completing wide binary batches: the entries of
+// gemv_binary.hip's dispatch table, named mlapi_gemv_<dtype>_l<LPR>_c<CPL>_u<U>.
+#define MLAPI_GEMV_ENTRY(TN, T, LPR, CPL, U)                                                                    \
+  extern "C" __global__ __launch_bounds__(256) void mlapi_gemv_##TN##_l##LPR##_c##CPL##_u##U(                   \
+      const mlapi::gemv::GemvArgs a) {                                                                          \
+    mlapi::gemv::gemv_rows<T, LPR, CPL, U>(a);                                                                  \
+  }
+#define MLAPI_GEMV_ENTRIES(TN, T) \
+  MLAPI_GEMV_ENTRY(TN, T, 4, 1, 4)   \
+  MLAPI_GEMV_ENTRY(TN, T, 8, 1, 8)   \
+  MLAPI_GEMV_ENTRY(TN, T, 16, 1, 8)  \
+  MLAPI_GEMV_ENTRY(TN, T, 32, 1, 8)  \
+  MLAPI_GEMV_ENTRY(TN, T, 64, 1, 8)  \
+  MLAPI_GEMV_ENTRY(TN, T, 64, 2, 4)  \
+  MLAPI_GEMV_ENTRY(TN, T, 64, 4, 2)  \
+  MLAPI_GEMV_ENTRY(TN, T, 64, 8, 1)
+MLAPI_GEMV_ENTRIES(bf16, uint16_t)
+MLAPI_GEMV_ENTRIES(f32, float)

@@ -17,6 +17,8 @@
 #include <fstream>
 #include <iterator>
 #include <stdexcept>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 namespace mlapi {
@@ -53,6 +55,27 @@ hsa_status_t pick_agents(hsa_agent_t a, void* data) {
       }
     }
   }
+  return HSA_STATUS_SUCCESS;
+}
+
+// the code object's "mlapi_split_*" / "mlapi_gemv_*" kernels (serve_direct.hip), by name without ".kd"
+hsa_status_t collect_split_kernels(hsa_executable_t, hsa_agent_t, hsa_executable_symbol_t sym, void* data) {
+  hsa_symbol_kind_t kind;
+  if (hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_TYPE, &kind) != HSA_STATUS_SUCCESS ||
+      kind != HSA_SYMBOL_KIND_KERNEL)
+    return HSA_STATUS_SUCCESS;
+  uint32_t len = 0;
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_NAME_LENGTH, &len);
+  std::string name(len, '\0');
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_NAME, &name[0]);
+  if (name.size() > 3 && name.compare(name.size() - 3, 3, ".kd") == 0) name.resize(name.size() - 3);
+  if (name.rfind("mlapi_split_", 0) != 0 && name.rfind("mlapi_gemv_", 0) != 0) return HSA_STATUS_SUCCESS;
+  Kernel k;
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.object);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.group);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.priv);
+  hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k.kernarg);
+  (*static_cast<std::unordered_map<std::string, Kernel>*>(data))[name] = k;
   return HSA_STATUS_SUCCESS;
 }
 
@@ -149,6 +172,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
       hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k_[i].kernarg);
       if (k_[i].kernarg < sizeof(InlineBatch) || k_[i].kernarg > stride_) return fail("unexpected kernarg layout");
     }
+    hsa_executable_iterate_agent_symbols(exe_, gpu_, collect_split_kernels, &named_);
     if (hsa_queue_create(gpu_, QUEUE_SIZE, HSA_QUEUE_TYPE_SINGLE, queue_error, this, UINT32_MAX, UINT32_MAX,
                          &queue_) != HSA_STATUS_SUCCESS)
       return fail("hsa_queue_create failed");
@@ -191,61 +215,41 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     if (faulted()) throw std::runtime_error("direct dispatch: queue error");
     const Kernel& k = (a.F == 4 && a.K == 3) ? k_[dt == DT_F64 ? 4 : 5]  // exact shape: one load batch
                                               : k_[(dt == DT_F64 ? 0 : 2) + (a.F <= 8 && a.K <= 4 ? 0 : 1)];
-    // Ring entry reuse: the packet that last used this entry (ka_slots_ launches ago) must have been
-    // consumed by the packet processor. With at most `slots` batches in flight and the ring >= 8x
-    // deeper, its kernel has finished as well; after a watchdog failure (a batch given up while its
-    // packet may still be queued) this wait is what keeps live arguments from being overwritten.
-    if (launches_ >= ka_slots_) {
-      const uint64_t need = launches_ - ka_slots_ + 1;
-      const auto t0 = std::chrono::steady_clock::now();
-      while (hsa_queue_load_read_index_scacquire(queue_) < need) {
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200))
-          throw std::runtime_error("direct dispatch: kernarg ring entry still owned by a queued packet");
-        _mm_pause();
-      }
-    }
-    char* ka = kernargs_ + (size_t)(launches_++ % ka_slots_) * stride_;
+    char* ka = next_kernarg();
     // Only the bytes the kernel reads: header + W/b of this model + n rows.
     const size_t es = dt == DT_F64 ? 8 : 4;
     const size_t wb_end = offsetof(InlineBatch, wb) + (size_t)a.K * (a.F + 1) * es;
     std::memcpy(ka, &a, wb_end);
     std::memcpy(ka + offsetof(InlineBatch, x), a.x, (size_t)a.n * a.F * es);
-    if (hdp_flush_ != nullptr) {
-      _mm_sfence();  // drain the write-combined BAR writes, then flush the HDP ahead of the doorbell
-      *reinterpret_cast<volatile uint32_t*>(hdp_flush_) = 1u;
-      // The flush register write is posted: read it back so the flush has completed before the
-      // packet (and so the kernel's kernarg loads) can be seen. MLAPI_HDP_READBACK=0 skips it
-      // (measured ~0.9 us per launch, tools/hsa_dispatch_probe.cpp mode 3) at the risk of stale
-      // kernargs.
-      if (hdp_readback_) (void)*reinterpret_cast<volatile uint32_t*>(hdp_flush_);
-    }
-    const uint64_t wi = hsa_queue_add_write_index_relaxed(queue_, 1);
-    while (wi - hsa_queue_load_read_index_scacquire(queue_) >= queue_->size) {
-      // full (cannot happen with a few batches in flight): wait for the packet processor
-    }
-    auto* pkt = reinterpret_cast<hsa_kernel_dispatch_packet_t*>(queue_->base_address) + (wi & (queue_->size - 1));
+    flush_kernargs();
     const uint16_t threads = a.n <= 64 ? 64 : 128;
-    pkt->workgroup_size_x = threads;
-    pkt->workgroup_size_y = 1;
-    pkt->workgroup_size_z = 1;
-    pkt->reserved0 = 0;
-    pkt->grid_size_x = threads;
-    pkt->grid_size_y = 1;
-    pkt->grid_size_z = 1;
-    pkt->private_segment_size = k.priv;
-    pkt->group_segment_size = k.group;
-    pkt->kernel_object = k.object;
-    pkt->kernarg_address = ka;
-    pkt->reserved2 = 0;
-    pkt->completion_signal.handle = 0;  // completion: the kernel's own done word
     // Acquire at agent scope invalidates the caches the kernel reads its (host-written) kernarg
     // block through; no release fence: the kernel publishes its outputs at system scope itself.
-    const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                            (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                            (HSA_FENCE_SCOPE_NONE << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
-    const uint32_t setup = 1;  // one grid dimension
-    __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), (uint32_t)header | (setup << 16), __ATOMIC_RELEASE);
-    hsa_signal_store_relaxed(queue_->doorbell_signal, (hsa_signal_value_t)wi);
+    submit(k, ka, threads, 1, threads, false, HSA_FENCE_SCOPE_NONE);
+  }
+
+  bool launch_kernel(const char* name, const void* args, size_t bytes, unsigned grid_x, unsigned grid_y,
+                     unsigned block, bool ordered) override {
+    if (named_.empty()) return false;
+    const auto it = named_.find(name);
+    if (it == named_.end()) return false;
+    const Kernel& k = it->second;
+    // the entries read no implicit argument: their kernarg segment is exactly the argument block
+    if (bytes != k.kernarg || bytes > stride_ || block == 0 || block > 1024 || grid_x == 0 || grid_y == 0 ||
+        (uint64_t)grid_x * block > UINT32_MAX)
+      throw std::invalid_argument(std::string("direct dispatch: bad launch of ") + name);
+    if (faulted()) throw std::runtime_error("direct dispatch: queue error");
+    char* ka = next_kernarg();
+    std::memcpy(ka, args, bytes);
+    flush_kernargs();
+    // ordered: barrier bit (the kernel starts after every earlier packet of this queue has
+    // finished: the order of hipLaunchKernel's stream, for launches that share a workspace) and a
+    // system-scope release at kernel end, as a HIP stream's; unordered: neither - the kernel's
+    // results are write-through records and it may overlap the batch before it
+    submit(k, ka, grid_x * block, grid_y, (uint16_t)block, ordered,
+           ordered ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_NONE);
+    ++named_launches_;
+    return true;
   }
 
   void* bar_alloc(size_t bytes) override {
@@ -271,10 +275,69 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   }
 
   bool faulted() const override { return fault_.load(std::memory_order_relaxed); }
+  uint64_t named_launches() const override { return named_launches_; }
   bool device_kernargs() const override { return hdp_flush_ != nullptr; }
   void set_fault() { fault_.store(true); }
 
  private:
+  // Ring entry reuse: the packet that last used this entry (ka_slots_ launches ago) must have been
+  // consumed by the packet processor. With at most `slots` batches in flight and the ring >= 8x
+  // deeper, its kernel has finished as well; after a watchdog failure (a batch given up while its
+  // packet may still be queued) this wait is what keeps live arguments from being overwritten.
+  char* next_kernarg() {
+    if (launches_ >= ka_slots_) {
+      const uint64_t need = launches_ - ka_slots_ + 1;
+      const auto t0 = std::chrono::steady_clock::now();
+      while (hsa_queue_load_read_index_scacquire(queue_) < need) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200))
+          throw std::runtime_error("direct dispatch: kernarg ring entry still owned by a queued packet");
+        _mm_pause();
+      }
+    }
+    return kernargs_ + (size_t)(launches_++ % ka_slots_) * stride_;
+  }
+
+  void flush_kernargs() {
+    if (hdp_flush_ == nullptr) return;
+    _mm_sfence();  // drain the write-combined BAR writes, then flush the HDP ahead of the doorbell
+    *reinterpret_cast<volatile uint32_t*>(hdp_flush_) = 1u;
+    // The flush register write is posted: read it back so the flush has completed before the
+    // packet (and so the kernel's kernarg loads) can be seen. MLAPI_HDP_READBACK=0 skips it
+    // (measured ~0.9 us per launch, tools/hsa_dispatch_probe.cpp mode 3) at the risk of stale
+    // kernargs.
+    if (hdp_readback_) (void)*reinterpret_cast<volatile uint32_t*>(hdp_flush_);
+  }
+
+  // grid_x in work-items (AQL), grid_y in blocks of height 1
+  void submit(const Kernel& k, const char* ka, uint32_t grid_x, uint32_t grid_y, uint16_t block, bool barrier,
+              int release_scope) {
+    const uint64_t wi = hsa_queue_add_write_index_relaxed(queue_, 1);
+    while (wi - hsa_queue_load_read_index_scacquire(queue_) >= queue_->size) {
+      // full (cannot happen with a few batches in flight): wait for the packet processor
+    }
+    auto* pkt = reinterpret_cast<hsa_kernel_dispatch_packet_t*>(queue_->base_address) + (wi & (queue_->size - 1));
+    pkt->workgroup_size_x = block;
+    pkt->workgroup_size_y = 1;
+    pkt->workgroup_size_z = 1;
+    pkt->reserved0 = 0;
+    pkt->grid_size_x = grid_x;
+    pkt->grid_size_y = grid_y;
+    pkt->grid_size_z = 1;
+    pkt->private_segment_size = k.priv;
+    pkt->group_segment_size = k.group;
+    pkt->kernel_object = k.object;
+    pkt->kernarg_address = const_cast<char*>(ka);
+    pkt->reserved2 = 0;
+    pkt->completion_signal.handle = 0;  // completion: the kernel's own done word / records
+    const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                            ((barrier ? 1 : 0) << HSA_PACKET_HEADER_BARRIER) |
+                            (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                            (release_scope << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+    const uint32_t setup = grid_y > 1 ? 2 : 1;  // grid dimensions
+    __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), (uint32_t)header | (setup << 16), __ATOMIC_RELEASE);
+    hsa_signal_store_relaxed(queue_->doorbell_signal, (hsa_signal_value_t)wi);
+  }
+
   static constexpr uint32_t QUEUE_SIZE = 256;
   uint32_t ka_slots_ = 64;
   bool hdp_readback_ = true;
@@ -285,6 +348,8 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   hsa_code_object_reader_t reader_{};
   hsa_executable_t exe_{};
   Kernel k_[6];
+  std::unordered_map<std::string, Kernel> named_;  // launch_kernel's kernels
+  uint64_t named_launches_ = 0;
   hsa_queue_t* queue_ = nullptr;
   char* kernargs_ = nullptr;
   uint32_t* hdp_flush_ = nullptr;  // non-null: the ring is in device memory

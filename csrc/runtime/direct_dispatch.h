@@ -18,14 +18,19 @@
 
 namespace mlapi {
 
-class InlineDispatcher {
+// KernelLauncher: the wide serving kernels of the same code object (linear_split's class-split
+// predict, the binary GEMV) by name, through the same queue and kernarg ring; the ring entry is written through the
+// BAR and one HDP flush covers it and any BAR-staged rows written before it.
+class InlineDispatcher : public KernelLauncher {
  public:
-  virtual ~InlineDispatcher() = default;
+  ~InlineDispatcher() override = default;
   // Enqueue one kernel-argument batch (dt: DT_F64 / DT_F32); completion is the batch's done word.
   // Single producer (the engine's batcher thread). Throws on failure.
   virtual void launch(int dt, const InlineBatch& a) = 0;
   // true once the queue reported an error (the engine then fails the batches instead of waiting)
   virtual bool faulted() const = 0;
+  // launches made through launch_kernel (wide serving batches dispatched without hipLaunchKernel)
+  virtual uint64_t named_launches() const = 0;
   // true if the kernarg ring is in device memory (else the host kernarg pool)
   virtual bool device_kernargs() const = 0;
   // Device HBM the CPU writes directly through the BAR (the kernarg ring's mechanism), for rows

@@ -575,6 +575,18 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
   const size_t bytes = (size_t)n * m.ldx * dtype_size(m.xdt);
   const bool bar = s.xbar != nullptr && m.path != PATH_SMALL && n <= cfg_.bar_rows &&
                    bytes <= (size_t)cfg_.bar_rows * slot_row_bytes_;
+  // class-split and record-completing GEMV batches go into the direct dispatcher's own queue: ~0.1 us of batcher time instead of hipLaunchKernel's ~3 us, and that launch's HDP flush
+  // also covers the BAR rows (no flush of their own)
+  const bool split_path = m.path != PATH_SMALL && m.path != PATH_GENERIC && m.path != PATH_GEMV &&
+                          m.ws_split != nullptr && (m.xdt == DT_F32 || n <= cfg_.split_max_rows);
+  const bool gemv_rec = m.path == PATH_GEMV && cfg_.gemv_record_rows > 0 && n >= cfg_.gemv_record_rows;
+  // ... for models whose weights stay small: the packet's agent-scope acquire (it covers the
+  // kernarg block written through the BAR) invalidates L2, so every batch re-reads W - measured
+  // +4 us on the GPU leg for a 1 MB f32 K = 1000 model, which outweighs the ~2 us of batcher time
+  // saved (profiles/r3_direct_wide/)
+  const size_t w_bytes = (size_t)(m.path == PATH_GEMV ? 1 : m.K) * m.ldx * dtype_size(m.xdt);
+  const bool direct_wide = direct_ && cfg_.direct_wide && cfg_.record_completion && (split_path || gemv_rec) &&
+                           w_bytes <= (size_t)cfg_.direct_wide_max_weight_bytes;
   const int64_t t_p0 = now_ns();
   pack_rows(s, xs, m, bar ? s.xbar : s.hx);
   const int64_t t_p1 = now_ns();
@@ -583,13 +595,14 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
   // staged by a copy first (a blit kernel of its own: ~4 us at serving sizes)
   const void* X = s.dx;
   if (bar) {
-    direct_->bar_flush();
+    if (!direct_wide) direct_->bar_flush();
     X = s.xbar;
   } else if (m.path != PATH_SMALL && cfg_.stage_wide) {
     MLAPI_HIP_CHECK(hipMemcpyAsync(s.dstage, s.hx, bytes, hipMemcpyHostToDevice, stream_));
     X = s.dstage;
   }
   const int64_t t_p2 = now_ns();
+  bool direct_wide_used = false;
   if (m.path == PATH_SMALL || m.path == PATH_GENERIC) {
     launch_linear_small(m.xdt, X, m.ldx, m.dW, m.db, n, m.F, m.K, m.kind, s.didx, s.dp, stream_, sig);
   } else {
@@ -600,14 +613,27 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     // hipLaunchKernel is batcher time, and the batcher is what queues the rows (engine stage
     // clocks: launch ~10 us per GEMV batch at c=64, profiles/r3_s19/).
     RecOut ro;
-    const bool gemv_rec = m.path == PATH_GEMV && cfg_.gemv_record_rows > 0 && n >= cfg_.gemv_record_rows;
     if (cfg_.record_completion && (m.path == PATH_GEMM || gemv_rec)) {
       ro.rec = s.drec;
       ro.seq = sig.seq;
       s.rec_mode = REC_ROWS;
     }
+    // a kernel the code object lacks falls back to hipLaunchKernel: flush the BAR rows first
+    struct Direct final : KernelLauncher {
+      InlineDispatcher* d;
+      bool flush_on_miss, used = false;
+      bool launch_kernel(const char* name, const void* args, size_t bytes, unsigned gx, unsigned gy, unsigned block,
+                         bool ordered) override {
+        if (d->launch_kernel(name, args, bytes, gx, gy, block, ordered)) return used = true;
+        if (flush_on_miss) d->bar_flush();
+        return false;
+      }
+    } dl;
+    dl.d = direct_.get();
+    dl.flush_on_miss = bar;
     if (m.path == PATH_GEMV)
-      launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_, ro);
+      launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_, ro,
+                         direct_wide && ro.rec != nullptr ? &dl : nullptr);
     else if (m.ws_split != nullptr && (m.xdt == DT_F32 || n <= cfg_.split_max_rows)) {
       // small batches (and every f32 batch): the class-split kernel. Serving-sized batches end in
       // per-block records the completer merges; larger ones merge in-kernel (one round trip).
@@ -621,16 +647,19 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
         s.rec_nsplit = ns;
       }
       launch_linear_split(m.xdt, X, m.ldx, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
-                          static_cast<float*>(s.dp), m.ws_split, m.ws_split_bytes, stream_, ro, sro);
+                          static_cast<float*>(s.dp), m.ws_split, m.ws_split_bytes, stream_, ro, sro,
+                          direct_wide ? &dl : nullptr);
     } else
       launch_gemm_softmax(X, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
                           static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_, ro);
     if (!s.rec_mode) launch_serve_signal(sig, stream_);
+    direct_wide_used = dl.used;
   }
   const int64_t t_p3 = now_ns();
   std::lock_guard<std::mutex> lk(st_mu_);
   stats_.path_batches[m.path]++;
   if (bar) stats_.bar_batches++;
+  if (direct_wide_used) stats_.direct_wide_batches++;
   stats_.launch_ns[0] += (double)(t_p1 - t_p0);
   stats_.launch_ns[1] += (double)(t_p2 - t_p1);
   stats_.launch_ns[2] += (double)(t_p3 - t_p2);

@@ -120,6 +120,8 @@ struct EngineConfig {
   // ... and complete through per-row 16-byte records {seq, idx, p} (one store per row, no fence,
   // no done word) instead of outputs + a fenced done word
   bool record_completion = true;
+  bool direct_wide = true;   // class-split / record GEMV batches dispatched into the direct queue (needs record_completion)
+  int64_t direct_wide_max_weight_bytes = 256 << 10;  // ... for models with at most this many bytes of W
   int gemv_record_rows = 2;  // GEMV batches of at least this many rows complete through records (0 = never)
   bool stage_wide = false;  // GEMV / GEMM / GENERIC: H2D-copy the rows first (default: zero-copy reads)
   int watchdog_ms = 2000; // batch not complete after this -> engine marked unhealthy
@@ -157,6 +159,7 @@ struct EngineStats {
   uint64_t path_batches[PATH_COUNT] = {0};  // GPU batches per kernel path
   uint64_t inline_batches = 0;      // SMALL batches launched through the kernel-argument block
   uint64_t direct_batches = 0;      // ... of which written straight into the HSA queue
+  uint64_t direct_wide_batches = 0; // class-split (wide multiclass) batches dispatched into that queue
   uint64_t idle_batches = 0;        // batches run by the submitting thread (run_idle)
   uint64_t bar_batches = 0;         // wide batches whose rows were written into HBM through the BAR
   bool direct_dispatch = false;     // the direct queue is up

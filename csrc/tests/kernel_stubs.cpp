@@ -16,7 +16,8 @@ void launch_linear_small(int, const void*, int64_t, const void*, const void*, in
 void launch_serve_signal(const ServeSignal&, hipStream_t) { unreachable("launch_serve_signal"); }
 bool linear_inline_fits(int, int64_t, int, int) { return false; }
 void launch_linear_inline(int, const InlineBatch&, hipStream_t) { unreachable("launch_linear_inline"); }
-void launch_gemv_binary(int, const void*, const void*, float, int64_t, int, int, int32_t*, float*, hipStream_t, RecOut) {
+void launch_gemv_binary(int, const void*, const void*, float, int64_t, int, int, int32_t*, float*, hipStream_t, RecOut,
+                        KernelLauncher*) {
   unreachable("launch_gemv_binary");
 }
 size_t gemm_softmax_workspace(int64_t, int, int) { return 0; }
@@ -28,7 +29,7 @@ bool linear_split_supported(int, int) { return false; }
 size_t linear_split_workspace(int64_t, int) { return 0; }
 int linear_split_nsplit(int K) { return (K + 63) / 64; }
 void launch_linear_split(int, const void*, int64_t, const void*, const float*, int64_t, int, int, int, int32_t*, float*,
-                         void*, size_t, hipStream_t, RecOut, SplitRecOut) {
+                         void*, size_t, hipStream_t, RecOut, SplitRecOut, KernelLauncher*) {
   unreachable("launch_linear_split");
 }
 std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int, const std::string&, int, std::string* why) {

@@ -66,6 +66,8 @@ class EngineHandle:
         ec.completers = int(config.completers)
         ec.batchers = int(config.batchers)
         ec.gemv_record_rows = int(config.gemv_record_rows)
+        ec.direct_wide = bool(config.direct_wide)
+        ec.direct_wide_max_weight_bytes = int(config.direct_wide_max_weight_bytes)
         ec.record_completion = bool(config.record_completion)
         ec.stage_wide = bool(config.stage_wide)
         ec.max_queue = config.max_queue

@@ -54,6 +54,8 @@ class Config:
     gemv_record_rows: int = 2                 # GEMV batches >= this many rows complete via records (0 = never)
     idle_inline_rows: int = 8                 # GPU: idle engine -> the IO thread launches <= this many rows itself (0 = off)
     direct_dispatch: bool = True              # GPU: ... written as AQL packets into the engine's own HSA queue
+    direct_wide: bool = True                  # GPU: class-split / record GEMV batches into that queue too ...
+    direct_wide_max_weight_bytes: int = 256 << 10  # ... for models with at most this many bytes of W
     stage_wide: bool = False                  # GPU: copy wide models' rows H2D first (default: zero-copy reads)
     fault_drop_rank: int = -1                 # fault injection: this DP rank's engine fails every batch
     fault_exit_rank: int = -1                 # fault injection: this DP rank's process dies (exit 3) ...

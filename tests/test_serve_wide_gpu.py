@@ -136,6 +136,82 @@ def test_bar_staged_rows_match_zero_copy(native, wide, K):
     np.testing.assert_array_equal(outs[32][1], outs[0][1])
     check(m, X, outs[32][0], outs[32][1], wide, rtol=1e-6 if (wide == "f32" and K > 2) else 1e-4)
 
+@pytest.mark.parametrize("wide", ["bf16", "f32"])
+@pytest.mark.parametrize("F,kind", [(256, Kind.BINARY), (64, Kind.BINARY_SOFTMAX), (1024, Kind.BINARY)])
+def test_direct_dispatched_gemv_batches_match_hip_launch(native, wide, F, kind):
+    """Record-completing binary GEMV batches (>= gemv_record_rows rows) dispatched into the engine's
+    HSA queue (mlapi_gemv_* entries, unordered packets) match hipLaunchKernel of the same kernel;
+    batch-1 keeps the signal-kernel path on the HIP stream alongside."""
+    from mlapi_amd._build import hsaco_path
+
+    m = LinearModel.random(F, 2, seed=F, kind=kind)
+    rng = np.random.default_rng(F)
+    Xs = [rng.standard_normal((n, F)) for n in (1, 2, 3, 8, 1, 64, 250, 5)]
+    outs = {}
+    for mode in ("direct", "direct_nobar", "hip"):
+        e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide],
+                    hsaco_path=str(hsaco_path()), direct_wide=(mode != "hip"),
+                    direct_wide_max_weight_bytes=1 << 30, bar_rows=0 if mode == "direct_nobar" else 32)
+        try:
+            e.load_model(int(m.kind), m.W, m.b, m.label_json())
+            assert e.model_path() == "gemv"
+            res = [e.predict(X) for X in Xs]
+            assert all((r[2] == 0).all() for r in res)
+            st = e.stats()
+            assert st["direct_dispatch"], "the serving code object did not load"
+            assert (st["direct_wide_batches"] > 0) == (mode != "hip")
+            outs[mode] = (np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res]))
+        finally:
+            e.stop()
+    for mode in ("direct", "direct_nobar"):
+        np.testing.assert_array_equal(outs[mode][0], outs["hip"][0])
+        np.testing.assert_allclose(outs[mode][1], outs["hip"][1], rtol=1e-6, atol=0)
+    check(m, np.concatenate(Xs), outs["direct"][0], outs["direct"][1], wide)
+
+
+@pytest.mark.parametrize("wide", ["bf16", "f32"])
+@pytest.mark.parametrize("F,K,kind", [(256, 1000, Kind.MULTINOMIAL), (64, 40, Kind.OVR), (512, 130, Kind.MULTINOMIAL)])
+def test_direct_dispatched_split_batches_match_hip_launch(native, wide, F, K, kind):
+    """Class-split batches written as AQL packets into the engine's own HSA queue (the serving code
+    object's mlapi_split_* entries, barrier-ordered, kernarg + BAR rows under one HDP flush) give
+    the results of hipLaunchKernel of the same kernel (labels exactly), for host-merged (<= 32 rows)
+    and in-kernel-merged batches, with and without BAR-staged rows."""
+    from mlapi_amd._build import hsaco_path
+
+    m = LinearModel.random(F, K, seed=F + K, kind=kind)
+    rng = np.random.default_rng(K)
+    sizes = [1, 2, 7, 16, 31, 32, 33, 64, 200, 5, 1]
+    Xs = [rng.standard_normal((n, F)) for n in sizes]
+    outs = {}
+    for mode in ("direct", "direct_nobar", "hip"):
+        e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide],
+                    hsaco_path=str(hsaco_path()), direct_wide=(mode != "hip"),
+                    direct_wide_max_weight_bytes=1 << 30, bar_rows=0 if mode == "direct_nobar" else 32)
+        try:
+            e.load_model(int(m.kind), m.W, m.b, m.label_json())
+            res = [e.predict(X) for X in Xs]
+            assert all((r[2] == 0).all() for r in res)
+            st = e.stats()
+            assert st["direct_dispatch"], "the serving code object did not load"
+            if mode == "hip":
+                assert st["direct_wide_batches"] == 0
+            else:  # f32: every batch is class-split; bf16: beyond split_max_rows the tiles kernel
+                assert st["direct_wide_batches"] > 0
+                assert wide != "f32" or st["direct_wide_batches"] == st["batches"]
+            outs[mode] = (np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res]))
+        finally:
+            e.stop()
+    # labels identical; p_max to the last bits only: the engine's batches are whatever rows were
+    # queued when the batcher looked, and a row's splits merge on the host (<= 32-row batches) or
+    # in the kernel (larger ones), whose float orders differ by an ulp or two
+    for mode in ("direct", "direct_nobar"):
+        np.testing.assert_array_equal(outs[mode][0], outs["hip"][0])
+        np.testing.assert_allclose(outs[mode][1], outs["hip"][1], rtol=1e-6, atol=0)
+    check(m, np.concatenate(Xs), outs["direct"][0], outs["direct"][1], wide,
+          rtol=1e-6 if wide == "f32" else 1e-4)
+
+
+
 
 def _post(port, bodies):
     out = []

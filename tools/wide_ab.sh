@@ -2,6 +2,7 @@
 # Wide-model serving A/B on the box: the serving GPU tests, then serve_wide (K = 1000 f32 and K = 2
 # bf16) with AB_VAR set to each of AB_VALS, interleaved x2; prints value and the engine's launch
 # breakdown per batch. Usage: AB_VAR=MLAPI_PACK_STAGED AB_VALS="1 0" bash tools/wide_ab.sh
+# (CFGS="1000 f32,1000 bf16": the "classes dtype" pairs, comma-separated; OUT: the output dir)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${OUT:-wide_ab}; mkdir -p $O
@@ -10,7 +11,8 @@ timeout -k 10 600 python -u -m pytest tests/test_serve_wide_gpu.py tests/test_se
 tail -1 $O/pytest.log
 for r in 1 2; do
   for v in $AB_VALS; do
-    for cfg in "1000 f32" "2 bf16"; do
+    IFS=, read -ra cfgs <<< "${CFGS:-1000 f32,2 bf16}"
+    for cfg in "${cfgs[@]}"; do
       set -- $cfg
       f=$O/k$1_$2_${AB_VAR}_${v}_r$r.log
       env "$AB_VAR=$v" timeout -k 10 300 python -u bench.py --mode serve_wide --wide-classes $1 --wide-dtype $2 \
