@@ -73,6 +73,14 @@ for s in $steps; do
       for dt in bf16 f32; do
         prof "serve_wide_k1000_$dt" 300 --mode serve_wide --wide-dtype $dt --steps 10 --warmup 2 --reqs-per-conn 256
       done ;;
+    prof_direct)  # wide batches dispatched into the engine's HSA queue: mlapi_gemv_* / mlapi_split_* in the trace
+      prof serve_wide_k2_bf16_direct 300 --mode serve_wide --wide-classes 2 --wide-dtype bf16 --steps 10 --warmup 2 --reqs-per-conn 256
+      prof serve_wide_k40_f32_direct 300 --mode serve_wide --wide-classes 40 --wide-dtype f32 --steps 10 --warmup 2 --reqs-per-conn 256
+      run bench_serve_wide_k40_f32 300 python -u bench.py --mode serve_wide --wide-classes 40 --wide-dtype f32 --steps 40 --warmup 5
+      MLAPI_DIRECT_WIDE=0 run bench_serve_wide_k40_f32_hip 300 python -u bench.py --mode serve_wide --wide-classes 40 --wide-dtype f32 --steps 40 --warmup 5
+      run bench_serve_wide_k40_f32_r2 300 python -u bench.py --mode serve_wide --wide-classes 40 --wide-dtype f32 --steps 40 --warmup 5
+      MLAPI_DIRECT_WIDE=0 run bench_serve_wide_k40_f32_hip_r2 300 python -u bench.py --mode serve_wide --wide-classes 40 --wide-dtype f32 --steps 40 --warmup 5
+      ;;
     marker)  # roctx ranges of every serving stage (MLAPI_ROCTX=1) + kernel trace: rocprofv3 --marker-trace
       (cd /tmp && MLAPI_ROCTX=1 timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv \
          -d "$O/prof_marker_serve" -o serve -- python3 "$R/bench.py" --steps 5 --warmup 1 --reqs-per-conn 256 --c1-requests 500 \
