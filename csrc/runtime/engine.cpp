@@ -389,9 +389,30 @@ void Engine::record_batch(size_t n) {
 void Engine::deliver(std::vector<Meta>& metas, const int32_t* idx, const double* p, const int32_t* st,
                      const std::shared_ptr<const Model>& m, int64_t now) {
   const size_t n = metas.size();
-  uint64_t errors = 0;
-  uint64_t lat_hist[24] = {0};
-  double lat_sum = 0;
+  auto status = [&](size_t j) {
+    const int32_t s = st[j];
+    return s == ST_OK && !std::isfinite(p[j]) ? (int32_t)ST_NONFINITE : s;
+  };
+  // stats first: a sink's waiter may read them as soon as its on_complete has run (counted after
+  // the hand-off, a predict() could return before its own requests were in `requests`)
+  {
+    uint64_t errors = 0;
+    uint64_t lat_hist[24] = {0};
+    double lat_sum = 0;
+    for (size_t j = 0; j < n; ++j) {
+      if (status(j) != ST_OK) ++errors;
+      const double us = (double)(now - metas[j].t_enq) * 1e-3;
+      lat_sum += us;
+      int bkt = 0;
+      while (bkt < 23 && (double)(int64_t(1) << bkt) <= us) ++bkt;
+      lat_hist[bkt]++;
+    }
+    std::lock_guard<std::mutex> lk(st_mu_);
+    stats_.requests += n;
+    stats_.errors += errors;
+    stats_.latency_sum_us += lat_sum;
+    for (int b = 0; b < 24; ++b) stats_.latency_hist[b] += lat_hist[b];
+  }
   // group by sink, preserving submission order inside each sink
   std::vector<Completion> buf;
   buf.reserve(n);
@@ -403,24 +424,10 @@ void Engine::deliver(std::vector<Meta>& metas, const int32_t* idx, const double*
     for (size_t j = i; j < n; ++j) {
       if (done[j] || metas[j].sink != sk) continue;
       done[j] = 1;
-      const int64_t lat = now - metas[j].t_enq;
-      int32_t s = st[j];
-      if (s == ST_OK && !std::isfinite(p[j])) s = ST_NONFINITE;
-      if (s != ST_OK) ++errors;
-      buf.push_back(Completion{metas[j].tag, idx[j], s, p[j], lat});
-      const double us = (double)lat * 1e-3;
-      lat_sum += us;
-      int bkt = 0;
-      while (bkt < 23 && (double)(int64_t(1) << bkt) <= us) ++bkt;
-      lat_hist[bkt]++;
+      buf.push_back(Completion{metas[j].tag, idx[j], status(j), p[j], now - metas[j].t_enq});
     }
     if (sk) sk->on_complete(buf.data(), buf.size(), m);
   }
-  std::lock_guard<std::mutex> lk(st_mu_);
-  stats_.requests += n;
-  stats_.errors += errors;
-  stats_.latency_sum_us += lat_sum;
-  for (int b = 0; b < 24; ++b) stats_.latency_hist[b] += lat_hist[b];
 }
 
 void Engine::run_cpu(std::vector<Meta>& metas, const std::vector<double>& xs, const std::shared_ptr<const Model>& m) {

@@ -209,3 +209,23 @@ def test_backpressure_http_503(native, model, tmp_path):
             s.close()
         srv.stop()
         e.stop()
+
+
+def test_direct_wide_knobs_reach_the_engine_config(native, monkeypatch):
+    """MLAPI_DIRECT_WIDE / MLAPI_DIRECT_WIDE_MAX_WEIGHT_BYTES (wide batches as AQL packets into the
+    engine's HSA queue, csrc/runtime/engine.cpp launch_batch) parse from the environment and the
+    native EngineConfig carries them; defaults: on, for W <= 256 KiB."""
+    from mlapi_amd.utils.config import Config
+
+    ec = native.EngineConfig()
+    assert ec.direct_wide is True and ec.direct_wide_max_weight_bytes == 256 << 10
+    cfg = Config.from_env(device="cpu")
+    assert cfg.direct_wide is True and cfg.direct_wide_max_weight_bytes == 256 << 10
+    monkeypatch.setenv("MLAPI_DIRECT_WIDE", "0")
+    monkeypatch.setenv("MLAPI_DIRECT_WIDE_MAX_WEIGHT_BYTES", "1024")
+    cfg = Config.from_env(device="cpu")
+    assert cfg.direct_wide is False and cfg.direct_wide_max_weight_bytes == 1024
+    ec.direct_wide = cfg.direct_wide
+    ec.direct_wide_max_weight_bytes = cfg.direct_wide_max_weight_bytes
+    e = native.Engine(ec)  # the CPU backend ignores both
+    e.stop()
