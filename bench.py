@@ -136,19 +136,22 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
                                       dispatch=args.dispatch,
                                       model_path="/nonexistent/bench.pkl", feature_names=list(names), **dtype_cfg)
     srv = None
-    if info.is_main:  # rank 0 binds an ephemeral port, the other ranks join its SO_REUSEPORT group
-        srv = NativeServer(mk(0))
-        srv.runtime.handle.load(model)
-        srv.start()
-    port = _share_port(srv.port if srv is not None else 0, info)
-    if srv is None:
-        srv = NativeServer(mk(port))
-        srv.runtime.handle.load(model)
-        srv.start()
-    reqs, exp = make_workload(srv.runtime.handle.engine, model, names, rows, **oracle_kw)
-    lg.workload(reqs, exp, rel_tol)
-    barrier(info)  # every rank's listeners are in the group before any client connects
+    # everything from the server start on is inside the try: a failed workload pre-check (or any
+    # error) stops the server and its threads before the exception leaves, so the process exits
+    # non-zero through the normal path (tests/test_bench_cli.py)
     try:
+        if info.is_main:  # rank 0 binds an ephemeral port, the other ranks join its SO_REUSEPORT group
+            srv = NativeServer(mk(0))
+            srv.runtime.handle.load(model)
+            srv.start()
+        port = _share_port(srv.port if srv is not None else 0, info)
+        if srv is None:
+            srv = NativeServer(mk(port))
+            srv.runtime.handle.load(model)
+            srv.start()
+        reqs, exp = make_workload(srv.runtime.handle.engine, model, names, rows, **oracle_kw)
+        lg.workload(reqs, exp, rel_tol)
+        barrier(info)  # every rank's listeners are in the group before any client connects
         lg.connect("127.0.0.1", port, args.conns, args.client_threads)
         if args.warmup:
             w = lg.run(args.warmup * args.reqs_per_conn, False)
@@ -210,7 +213,8 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         paths = {k: s1["path_batches"][k] - s0["path_batches"][k] for k in s1["path_batches"]}
         idle = {"c64": int(per_rank[:, 8].sum()), "batch1": int(per_rank[:, 9].sum())}
     finally:
-        srv.stop()
+        if srv is not None:
+            srv.stop()
     total = float(np.sum(per_rank[:, 2]))
     value = total / elapsed
     extra = {

@@ -9,10 +9,12 @@ to FastAPI; the model runs in the same batching engine either way.
 """
 from __future__ import annotations
 
+import atexit
 import logging
 import os
 import signal
 import threading
+import weakref
 from typing import Optional
 
 from mlapi_amd._native import C
@@ -22,6 +24,23 @@ from mlapi_amd.serve.service import ServingRuntime
 from mlapi_amd.utils.config import Config
 
 log = logging.getLogger("mlapi_amd.serve")
+
+# Servers still running when the interpreter exits (e.g. an exception escaped between start() and
+# stop()): their ASGI pump threads are daemon threads parked inside HttpServer.next_slow with the
+# GIL released. During finalization such a thread is torn down by a forced unwind when it tries to
+# take the GIL back, and that unwind through pybind11's noexcept gil_scoped_release ends the
+# process in std::terminate ("terminate called without an active exception", rc 134). atexit
+# handlers run before finalization, so stopping the servers there joins those threads cleanly.
+_RUNNING: "weakref.WeakSet[NativeServer]" = weakref.WeakSet()
+
+
+@atexit.register
+def _stop_running_servers() -> None:
+    for srv in list(_RUNNING):
+        try:
+            srv.stop()
+        except Exception:  # pragma: no cover - best effort at exit
+            log.exception("stopping server at exit")
 
 
 class NativeServer:
@@ -64,6 +83,7 @@ class NativeServer:
         self.http.start()
         self.bridge.start()
         self._started = True
+        _RUNNING.add(self)
         log.info("serving on %s:%d (backend %s)", self.config.host, self.port, self.runtime.handle.backend)
         return self
 
@@ -71,6 +91,7 @@ class NativeServer:
         if not self._started:
             return
         self._started = False
+        _RUNNING.discard(self)
         self.http.stop()
         self.bridge.stop()
         self.runtime.close()

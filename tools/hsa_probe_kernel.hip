@@ -12,6 +12,12 @@ extern "C" __global__ __launch_bounds__(64) void probe_flag(int* idx, double* p,
   }
 }
 
+// tools/dispatch_rate_probe.cpp: one write-through record store per launch (the serving kernels'
+// completion shape), no fence, no done word
+extern "C" __global__ __launch_bounds__(64) void probe_rec(unsigned* rec, unsigned seq) {
+  if (threadIdx.x == 0) __hip_atomic_store(rec, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // A serving-sized (3.5 KB) kernel argument: every lane sums its share of the payload, so a stale
 // or partly written argument block shows up as a wrong checksum on the host.
 struct BigArgs {
