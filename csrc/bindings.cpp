@@ -121,6 +121,7 @@ py::dict stats_dict(const EngineStats& s) {
   d["direct_batches"] = s.direct_batches;
   d["direct_wide_batches"] = s.direct_wide_batches;
   d["idle_batches"] = s.idle_batches;
+  d["lane_batches"] = s.lane_batches;
   d["bar_batches"] = s.bar_batches;
   d["direct_dispatch"] = s.direct_dispatch;
   d["direct_device_kernargs"] = s.direct_device_kernargs;
@@ -403,6 +404,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("host_merge_rows", &EngineConfig::host_merge_rows)
       .def_readwrite("inline_args", &EngineConfig::inline_args)
       .def_readwrite("idle_inline_rows", &EngineConfig::idle_inline_rows)
+      .def_readwrite("lanes", &EngineConfig::lanes)
       .def_readwrite("completers", &EngineConfig::completers)
       .def_readwrite("batchers", &EngineConfig::batchers)
       .def_readwrite("gemv_record_rows", &EngineConfig::gemv_record_rows)

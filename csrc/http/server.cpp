@@ -316,10 +316,29 @@ class IoThread : public Sink {
     ++lat_n_;
   }
 
+  // Lane batches (rows this thread dispatched itself) whose records have landed: render them.
+  void harvest_lane() {
+    if (lane_ == nullptr || lane_->inflight() == 0) return;
+    lane_c_.clear();
+    lane_seg_.clear();
+    lane_->poll(lane_c_, lane_seg_);
+    for (size_t k = 0; k < lane_seg_.size(); ++k) {
+      const size_t b = lane_seg_[k].begin, e = k + 1 < lane_seg_.size() ? lane_seg_[k + 1].begin : lane_c_.size();
+      render_fast(lane_seg_[k].model, lane_c_.data() + b, e - b);
+    }
+  }
+
   void flush_submits() {
     if (pend_tags_.empty()) return;
     Stage sg(this, SS_SUBMIT);
     const int n = (int)pend_tags_.size();
+    // this thread dispatches the round's rows itself (engine lane: no batcher / completer hop);
+    // not eligible (wide model, lane slots busy, ...) -> the idle path or the engine queue
+    if (lane_ != nullptr && lane_->submit(pend_x_.data(), n, (int)nfeat_, pend_tags_.data())) {
+      pend_x_.clear();
+      pend_tags_.clear();
+      return;
+    }
     {
       // idle engine: this thread launches the rows itself and renders the responses right away
       // (no batcher / completer hand-off, no eventfd round trip)
@@ -375,7 +394,9 @@ class IoThread : public Sink {
     const int64_t lowload_spin_ns = (int64_t)srv_->config().io_spin_lowload_us * 1000;
     const int lowload_conns = srv_->config().io_spin_max_conns;
     int64_t last_active = 0;
+    lane_ = srv_->engine() != nullptr ? srv_->engine()->open_lane() : nullptr;
     while (!stop_.load()) {
+      harvest_lane();
       flush_submits();
       flush_log();
       publish_clock();
@@ -399,6 +420,7 @@ class IoThread : public Sink {
         spinning_.store(false);  // left the low-load regime: hand-offs need the eventfd again
         if (pending_.load()) timeout = 0;
       }
+      if (lane_ != nullptr && lane_->inflight() > 0) timeout = 0;  // poll the lane's records
       stage(SS_POLL);
       if (timeout != 0) {
         blocked_.store(true);
@@ -444,6 +466,8 @@ class IoThread : public Sink {
       }
       apply_listen_state();
     }
+    if (lane_ != nullptr) srv_->engine()->close_lane(lane_);
+    lane_ = nullptr;
   }
 
   // Health-aware dispatch (SO_REUSEPORT group membership): an IO thread whose engine is unhealthy
@@ -1101,6 +1125,9 @@ class IoThread : public Sink {
   std::vector<Completion> spare_c_;  // drain_pending's side of the double buffer (this thread only)
   std::vector<FastSeg> spare_seg_;
   std::vector<Completion> idle_done_;  // run_idle completions (this thread only)
+  Lane* lane_ = nullptr;               // this thread's dispatch lane (engine-owned), or none
+  std::vector<Completion> lane_c_;     // harvest_lane scratch (this thread only)
+  std::vector<Lane::Seg> lane_seg_;
   std::string body_;                   // response body scratch (this thread only)
   std::vector<SlowResp> slow_;
   std::vector<double> pend_x_;      // fast-path rows parsed in this epoll round (IO thread only)

@@ -18,6 +18,7 @@
 #include <iterator>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -118,8 +119,10 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     if (inited_) hsa_shut_down();
   }
 
-  bool init(int device, const std::string& path, int max_in_flight, std::string* why) {
+  bool init(int device, const std::string& path, int max_in_flight, std::string* why, int max_producers) {
     ka_slots_ = std::max<uint32_t>(64u, 8u * (uint32_t)std::max(1, max_in_flight));
+    max_lanes_ = std::max(0, std::min(max_producers, MAX_LANES));
+    const uint32_t ka_total = ka_slots_ + (uint32_t)max_lanes_ * LANE_KERNARGS;
     if (const char* e = getenv("MLAPI_HDP_READBACK")) hdp_readback_ = atoi(e) != 0;
     auto fail = [&](const std::string& m) {
       if (why) *why = m;
@@ -173,8 +176,8 @@ class HsaInlineDispatcher final : public InlineDispatcher {
       if (k_[i].kernarg < sizeof(InlineBatch) || k_[i].kernarg > stride_) return fail("unexpected kernarg layout");
     }
     hsa_executable_iterate_agent_symbols(exe_, gpu_, collect_split_kernels, &named_);
-    if (hsa_queue_create(gpu_, QUEUE_SIZE, HSA_QUEUE_TYPE_SINGLE, queue_error, this, UINT32_MAX, UINT32_MAX,
-                         &queue_) != HSA_STATUS_SUCCESS)
+    if (hsa_queue_create(gpu_, QUEUE_SIZE, max_lanes_ > 0 ? HSA_QUEUE_TYPE_MULTI : HSA_QUEUE_TYPE_SINGLE, queue_error,
+                         this, UINT32_MAX, UINT32_MAX, &queue_) != HSA_STATUS_SUCCESS)
       return fail("hsa_queue_create failed");
     // Kernarg ring: a buffer is rewritten KA_SLOTS launches later; the engine keeps at most
     // `slots` (a handful) batches in flight, so its previous kernel has long finished reading it.
@@ -192,7 +195,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     if (!host_ring && hsa_agent_get_info(gpu_, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &hdp) == HSA_STATUS_SUCCESS &&
         hdp.HDP_MEM_FLUSH_CNTL != nullptr &&
         hsa_amd_agent_iterate_memory_pools(gpu_, pick_device_pool, &dpool) == HSA_STATUS_INFO_BREAK &&
-        hsa_amd_memory_pool_allocate(dpool, (size_t)stride_ * ka_slots_, 0, (void**)&kernargs_) == HSA_STATUS_SUCCESS) {
+        hsa_amd_memory_pool_allocate(dpool, (size_t)stride_ * ka_total, 0, (void**)&kernargs_) == HSA_STATUS_SUCCESS) {
       if (hsa_amd_agents_allow_access(1, &s.cpu, nullptr, kernargs_) == HSA_STATUS_SUCCESS) {
         hdp_flush_ = hdp.HDP_MEM_FLUSH_CNTL;
         dpool_ = dpool;
@@ -203,19 +206,36 @@ class HsaInlineDispatcher final : public InlineDispatcher {
       }
     }
     if (kernargs_ == nullptr &&
-        (hsa_amd_memory_pool_allocate(pool, (size_t)stride_ * ka_slots_, 0, (void**)&kernargs_) != HSA_STATUS_SUCCESS ||
+        (hsa_amd_memory_pool_allocate(pool, (size_t)stride_ * ka_total, 0, (void**)&kernargs_) != HSA_STATUS_SUCCESS ||
          hsa_amd_agents_allow_access(1, &gpu_, nullptr, kernargs_) != HSA_STATUS_SUCCESS))
       return fail("kernarg allocation failed");
-    std::memset(kernargs_, 0, (size_t)stride_ * ka_slots_);
+    std::memset(kernargs_, 0, (size_t)stride_ * ka_total);
+    prod_[0].base = kernargs_;
+    prod_[0].entries = ka_slots_;
+    prod_[0].wi.assign(ka_slots_, ~uint64_t(0));
+    for (int p = 1; p <= max_lanes_; ++p) {
+      prod_[p].base = kernargs_ + (size_t)stride_ * (ka_slots_ + (uint32_t)(p - 1) * LANE_KERNARGS);
+      prod_[p].entries = LANE_KERNARGS;
+      prod_[p].wi.assign(LANE_KERNARGS, ~uint64_t(0));
+    }
+    published_.store(hsa_queue_load_write_index_scacquire(queue_), std::memory_order_relaxed);
     return true;
   }
 
-  void launch(int dt, const InlineBatch& a) override {
+  int add_producer() override {
+    const int p = next_producer_.fetch_add(1) + 1;
+    return p <= max_lanes_ ? p : -1;
+  }
+
+  void launch(int dt, const InlineBatch& a, int producer) override {
     if (dt != DT_F64 && dt != DT_F32) throw std::invalid_argument("direct dispatch: f64 / f32 batches only");
+    if (producer < 0 || producer > max_lanes_) throw std::invalid_argument("direct dispatch: unknown producer");
     if (faulted()) throw std::runtime_error("direct dispatch: queue error");
     const Kernel& k = (a.F == 4 && a.K == 3) ? k_[dt == DT_F64 ? 4 : 5]  // exact shape: one load batch
                                               : k_[(dt == DT_F64 ? 0 : 2) + (a.F <= 8 && a.K <= 4 ? 0 : 1)];
-    char* ka = next_kernarg();
+    Producer& pr = prod_[producer];
+    uint64_t* wi_slot = nullptr;
+    char* ka = next_kernarg(pr, &wi_slot);
     // Only the bytes the kernel reads: header + W/b of this model + n rows.
     const size_t es = dt == DT_F64 ? 8 : 4;
     const size_t wb_end = offsetof(InlineBatch, wb) + (size_t)a.K * (a.F + 1) * es;
@@ -225,7 +245,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     const uint16_t threads = a.n <= 64 ? 64 : 128;
     // Acquire at agent scope invalidates the caches the kernel reads its (host-written) kernarg
     // block through; no release fence: the kernel publishes its outputs at system scope itself.
-    submit(k, ka, threads, 1, threads, false, HSA_FENCE_SCOPE_NONE);
+    submit(k, ka, threads, 1, threads, false, HSA_FENCE_SCOPE_NONE, wi_slot);
   }
 
   bool launch_kernel(const char* name, const void* args, size_t bytes, unsigned grid_x, unsigned grid_y,
@@ -239,7 +259,8 @@ class HsaInlineDispatcher final : public InlineDispatcher {
         (uint64_t)grid_x * block > UINT32_MAX)
       throw std::invalid_argument(std::string("direct dispatch: bad launch of ") + name);
     if (faulted()) throw std::runtime_error("direct dispatch: queue error");
-    char* ka = next_kernarg();
+    uint64_t* wi_slot = nullptr;
+    char* ka = next_kernarg(prod_[0], &wi_slot);
     std::memcpy(ka, args, bytes);
     flush_kernargs();
     // ordered: barrier bit (the kernel starts after every earlier packet of this queue has
@@ -247,7 +268,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     // system-scope release at kernel end, as a HIP stream's; unordered: neither - the kernel's
     // results are write-through records and it may overlap the batch before it
     submit(k, ka, grid_x * block, grid_y, (uint16_t)block, ordered,
-           ordered ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_NONE);
+           ordered ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_NONE, wi_slot);
     ++named_launches_;
     return true;
   }
@@ -280,21 +301,33 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   void set_fault() { fault_.store(true); }
 
  private:
-  // Ring entry reuse: the packet that last used this entry (ka_slots_ launches ago) must have been
-  // consumed by the packet processor. With at most `slots` batches in flight and the ring >= 8x
-  // deeper, its kernel has finished as well; after a watchdog failure (a batch given up while its
-  // packet may still be queued) this wait is what keeps live arguments from being overwritten.
-  char* next_kernarg() {
-    if (launches_ >= ka_slots_) {
-      const uint64_t need = launches_ - ka_slots_ + 1;
+  // One producer's part of the kernarg ring: `entries` argument blocks used round robin; wi[e] is
+  // the packet id that last used entry e (~0: never).
+  struct alignas(64) Producer {
+    char* base = nullptr;
+    uint32_t entries = 0;
+    uint64_t launches = 0;
+    std::vector<uint64_t> wi;
+  };
+
+  // Ring entry reuse: the packet that last used this entry must have been consumed by the packet
+  // processor (its read index passed it). With at most a few batches in flight per producer and
+  // the region several times deeper, its kernel has finished as well; after a watchdog failure (a
+  // batch given up while its packet may still be queued) this wait is what keeps live arguments
+  // from being overwritten.
+  char* next_kernarg(Producer& p, uint64_t** slot) {
+    const uint32_t e = (uint32_t)(p.launches++ % p.entries);
+    const uint64_t last = p.wi[e];
+    if (last != ~uint64_t(0)) {
       const auto t0 = std::chrono::steady_clock::now();
-      while (hsa_queue_load_read_index_scacquire(queue_) < need) {
+      while (hsa_queue_load_read_index_scacquire(queue_) <= last) {
         if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200))
           throw std::runtime_error("direct dispatch: kernarg ring entry still owned by a queued packet");
         _mm_pause();
       }
     }
-    return kernargs_ + (size_t)(launches_++ % ka_slots_) * stride_;
+    *slot = &p.wi[e];  // submit() records the packet id here
+    return p.base + (size_t)e * stride_;
   }
 
   void flush_kernargs() {
@@ -308,12 +341,17 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     if (hdp_readback_) (void)*reinterpret_cast<volatile uint32_t*>(hdp_flush_);
   }
 
-  // grid_x in work-items (AQL), grid_y in blocks of height 1
+  // grid_x in work-items (AQL), grid_y in blocks of height 1. Multi-producer: the packet slot is
+  // reserved by an atomic add on the write index; the header store and the doorbell go out in
+  // reservation order (published_), so the packet processor never sees a valid header behind an
+  // unpublished one and the doorbell value never decreases.
   void submit(const Kernel& k, const char* ka, uint32_t grid_x, uint32_t grid_y, uint16_t block, bool barrier,
-              int release_scope) {
-    const uint64_t wi = hsa_queue_add_write_index_relaxed(queue_, 1);
+              int release_scope, uint64_t* wi_slot) {
+    const uint64_t wi = hsa_queue_add_write_index_scacq_screl(queue_, 1);
+    *wi_slot = wi;
     while (wi - hsa_queue_load_read_index_scacquire(queue_) >= queue_->size) {
-      // full (cannot happen with a few batches in flight): wait for the packet processor
+      // full (cannot happen with a few batches in flight per producer): wait for the packet processor
+      _mm_pause();
     }
     auto* pkt = reinterpret_cast<hsa_kernel_dispatch_packet_t*>(queue_->base_address) + (wi & (queue_->size - 1));
     pkt->workgroup_size_x = block;
@@ -334,8 +372,16 @@ class HsaInlineDispatcher final : public InlineDispatcher {
                             (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                             (release_scope << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
     const uint32_t setup = grid_y > 1 ? 2 : 1;  // grid dimensions
+    if (max_lanes_ > 0) {
+      // earlier reservations publish first (their owners are between the add and the header store:
+      // a few stores); yield if one was descheduled in that window
+      uint32_t spins = 0;
+      while (published_.load(std::memory_order_acquire) != wi)
+        if (++spins > 4096) std::this_thread::yield(); else _mm_pause();
+    }
     __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), (uint32_t)header | (setup << 16), __ATOMIC_RELEASE);
     hsa_signal_store_relaxed(queue_->doorbell_signal, (hsa_signal_value_t)wi);
+    if (max_lanes_ > 0) published_.store(wi + 1, std::memory_order_release);
   }
 
   static constexpr uint32_t QUEUE_SIZE = 256;
@@ -356,7 +402,11 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   hsa_amd_memory_pool_t dpool_{};
   hsa_agent_t cpu_{};
   std::vector<void*> bar_bufs_;
-  uint64_t launches_ = 0;
+  static constexpr int MAX_LANES = 64;
+  int max_lanes_ = 0;
+  Producer prod_[MAX_LANES + 1];
+  std::atomic<int> next_producer_{0};
+  alignas(64) std::atomic<uint64_t> published_{0};  // next packet id allowed to publish (lanes on)
   std::atomic<bool> fault_{false};
 };
 
@@ -365,9 +415,9 @@ void queue_error(hsa_status_t, hsa_queue_t*, void* data) { static_cast<HsaInline
 }  // namespace
 
 std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int device, const std::string& hsaco_path, int max_in_flight,
-                                                         std::string* why) {
+                                                         std::string* why, int max_producers) {
   auto d = std::make_unique<HsaInlineDispatcher>();
-  if (!d->init(device, hsaco_path, max_in_flight, why)) return nullptr;
+  if (!d->init(device, hsaco_path, max_in_flight, why, max_producers)) return nullptr;
   return d;
 }
 

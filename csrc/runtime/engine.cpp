@@ -96,6 +96,42 @@ inline uint16_t f32_to_bf16(float f) {  // round to nearest even (inputs are fin
   std::memcpy(&u, &f, 4);
   return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
+
+// Kernel-argument batch: W + b of the model and n rows (row(i): the row's features, nullptr if its
+// feature count does not match the model -> zeroed, ST_SHAPE in pre[i]) into `a`, in the model's
+// small-path dtype.
+template <class RowFn>
+void fill_inline(InlineBatch& a, const Model& m, int64_t n, RowFn row, int32_t* pre) {
+  a.n = (int32_t)n;
+  a.F = m.F;
+  a.K = m.K;
+  a.kind = m.kind;
+  const size_t kf = (size_t)m.K * m.F;
+  if (m.xdt == DT_F64) {
+    double* wb = reinterpret_cast<double*>(a.wb);
+    std::memcpy(wb, m.W.data(), kf * sizeof(double));
+    std::memcpy(wb + kf, m.b.data(), (size_t)m.K * sizeof(double));
+    double* x = reinterpret_cast<double*>(a.x);
+    for (int64_t i = 0; i < n; ++i) {
+      const double* r = row(i);
+      if (r == nullptr) pre[i] = ST_SHAPE;
+      if (r != nullptr)
+        std::memcpy(x + i * m.F, r, sizeof(double) * m.F);
+      else
+        std::memset(x + i * m.F, 0, sizeof(double) * m.F);
+    }
+  } else {
+    float* wb = reinterpret_cast<float*>(a.wb);
+    for (size_t i = 0; i < kf; ++i) wb[i] = (float)m.W[i];
+    for (int k = 0; k < m.K; ++k) wb[kf + k] = (float)m.b[k];
+    float* x = reinterpret_cast<float*>(a.x);
+    for (int64_t i = 0; i < n; ++i) {
+      const double* r = row(i);
+      if (r == nullptr) pre[i] = ST_SHAPE;
+      for (int f = 0; f < m.F; ++f) x[i * m.F + f] = r != nullptr ? (float)r[f] : 0.f;
+    }
+  }
+}
 }  // namespace
 
 Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
@@ -124,7 +160,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     MLAPI_HIP_CHECK(hipDeviceSynchronize());
     if (cfg_.direct_dispatch && !cfg_.hsaco_path.empty()) {
       std::string why;
-      direct_ = make_direct_dispatcher(cfg_.device, cfg_.hsaco_path, cfg_.slots, &why);
+      direct_ = make_direct_dispatcher(cfg_.device, cfg_.hsaco_path, cfg_.slots, &why, cfg_.lanes > 0 ? 64 : 0);
       if (!direct_) std::fprintf(stderr, "[mlapi engine] direct dispatch off (%s): using hipLaunchKernel\n", why.c_str());
     }
     for (int i = 0; i < cfg_.slots; ++i) {
@@ -535,39 +571,16 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
   if (m.path == PATH_SMALL && cfg_.inline_args && linear_inline_fits(m.xdt, n, m.F, m.K)) {
     // rows, W and b ride in the kernel-argument block
     InlineBatch& a = inline_;
-    a.n = (int32_t)n;
-    a.F = m.F;
-    a.K = m.K;
-    a.kind = m.kind;
     a.out_idx = s.didx;
     a.out_p = s.dp;
     s.rec_mode = cfg_.record_completion ? REC_ROWS : 0;
     a.done = s.rec_mode ? nullptr : sig.done;
     a.rec = s.rec_mode ? s.drec : nullptr;
     a.seq = sig.seq;
-    const size_t es = dtype_size(m.xdt);
-    const size_t kf = (size_t)m.K * m.F;
-    if (m.xdt == DT_F64) {
-      double* wb = reinterpret_cast<double*>(a.wb);
-      std::memcpy(wb, m.W.data(), kf * es);
-      std::memcpy(wb + kf, m.b.data(), (size_t)m.K * es);
-      double* x = reinterpret_cast<double*>(a.x);
-      for (int64_t i = 0; i < n; ++i) {
-        const bool ok = s.metas[i].nf == m.F;
-        if (!ok) s.pre_status[i] = ST_SHAPE;
-        for (int f = 0; f < m.F; ++f) x[i * m.F + f] = ok ? xs[s.metas[i].off + f] : 0.0;
-      }
-    } else {
-      float* wb = reinterpret_cast<float*>(a.wb);
-      for (size_t i = 0; i < kf; ++i) wb[i] = (float)m.W[i];
-      for (int k = 0; k < m.K; ++k) wb[kf + k] = (float)m.b[k];
-      float* x = reinterpret_cast<float*>(a.x);
-      for (int64_t i = 0; i < n; ++i) {
-        const bool ok = s.metas[i].nf == m.F;
-        if (!ok) s.pre_status[i] = ST_SHAPE;
-        for (int f = 0; f < m.F; ++f) x[i * m.F + f] = ok ? (float)xs[s.metas[i].off + f] : 0.f;
-      }
-    }
+    fill_inline(
+        a, m, n,
+        [&](int64_t i) -> const double* { return s.metas[i].nf == m.F ? &xs[s.metas[i].off] : nullptr; },
+        s.pre_status.data());
     if (direct_)
       direct_->launch(m.xdt, a);  // ~0.03 us: one packet into the engine's own HSA queue
     else
@@ -1045,6 +1058,179 @@ void Engine::completer_loop() {
       stats_.completer_ns[1] += (double)(t_d1 - now);
     }
   }
+}
+
+// ---- per-IO-thread dispatch lanes ---------------------------------------------------------------
+Lane* Engine::open_lane() {
+  if (cfg_.device < 0 || cfg_.lanes <= 0 || !direct_ || !cfg_.record_completion || !cfg_.inline_args) return nullptr;
+  {
+    std::lock_guard<std::mutex> lk(lanes_mu_);
+    if (!free_lanes_.empty()) {
+      Lane* l = free_lanes_.back();
+      free_lanes_.pop_back();
+      return l;
+    }
+  }
+  const int p = direct_->add_producer();
+  if (p < 0) return nullptr;
+  std::unique_ptr<Lane> l(new Lane(this, p));
+  std::lock_guard<std::mutex> lk(lanes_mu_);
+  lanes_.push_back(std::move(l));
+  return lanes_.back().get();
+}
+
+void Engine::close_lane(Lane* lane) {
+  if (lane == nullptr) return;
+  std::vector<Completion> c;
+  std::vector<Lane::Seg> segs;
+  const int64_t until = now_ns() + 2000000000LL;
+  while (lane->poll(c, segs) > 0 && now_ns() < until) _mm_pause();
+  if (lane->inflight() > 0) return;  // still running after 2 s: never reuse it (its records may be written)
+  std::lock_guard<std::mutex> lk(lanes_mu_);
+  free_lanes_.push_back(lane);
+}
+
+namespace {
+constexpr int LANE_MAX_ROWS = 128;  // the inline kernels run one block of <= 128 threads
+}
+
+Lane::Lane(Engine* e, int producer) : eng_(e), producer_(producer) {
+  // distinct sequence numbers per lane (a slot's records never carry a stale match)
+  seq_base_ = (uint32_t)producer << 24;
+  MLAPI_HIP_CHECK(hipSetDevice(e->cfg_.device));
+  for (LSlot& s : slots_) {
+    const size_t rb = (size_t)LANE_MAX_ROWS * sizeof(ServeRecord);
+    MLAPI_HIP_CHECK(hipHostMalloc((void**)&s.hrec, rb, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(s.hrec, 0, rb);
+    MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.drec, s.hrec, 0));
+    s.tags.reserve(LANE_MAX_ROWS);
+    s.pre.reserve(LANE_MAX_ROWS);
+  }
+}
+
+Lane::~Lane() {
+  // a kernel still in flight writes into these records: wait for it (bounded) before freeing
+  const int64_t until = now_ns() + 2000000000LL;
+  for (int k = 0; k < SLOTS; ++k) {
+    LSlot& s = slots_[k];
+    if (!s.busy || s.failed) continue;
+    for (int i = 0; i < s.n && now_ns() < until; ++i)
+      while (__atomic_load_n(&s.hrec[i].seq, __ATOMIC_ACQUIRE) != s.seq && now_ns() < until) _mm_pause();
+  }
+  (void)hipSetDevice(eng_->cfg_.device);
+  for (LSlot& s : slots_)
+    if (s.hrec) (void)hipHostFree(s.hrec);
+}
+
+bool Lane::submit(const double* X, int n, int nf, const uint64_t* tags) {
+  Engine& e = *eng_;
+  if (n <= 0 || n > LANE_MAX_ROWS || inflight_ == SLOTS) return false;
+  if (nf < 0 || nf > e.cfg_.max_features) return false;
+  if (e.drop_.load(std::memory_order_relaxed) || e.cfg_.fail_every > 0 || e.cfg_.delay_us > 0) return false;
+  if (e.direct_->faulted()) return false;
+  std::shared_ptr<const Model> m = e.model();
+  if (!m || m->path != PATH_SMALL || !linear_inline_fits(m->xdt, n, m->F, m->K)) return false;
+  const int64_t t = now_ns();
+  LSlot& s = slots_[(next_ + inflight_) % SLOTS];
+  s.n = n;
+  s.tags.assign(tags, tags + n);
+  s.pre.assign((size_t)n, ST_OK);
+  s.seen = 0;
+  s.failed = false;
+  uint32_t sq = ++seq_base_;
+  if (sq == 0) sq = ++seq_base_;  // 0 is the records' initial value
+  s.seq = sq;
+  InlineBatch& a = batch_;
+  a.out_idx = nullptr;
+  a.out_p = nullptr;
+  a.done = nullptr;
+  a.rec = s.drec;
+  a.seq = s.seq;
+  fill_inline(
+      a, *m, n, [&](int64_t i) -> const double* { return nf == m->F ? X + i * nf : nullptr; }, s.pre.data());
+  try {
+    TraceRange tr("mlapi.lane.launch");
+    e.direct_->launch(m->xdt, a, producer_);
+  } catch (const std::exception&) {
+    e.healthy_.store(false);
+    return false;  // nothing was published: the caller's queued submit answers the rows
+  }
+  s.t_enq = t;
+  s.t_launch = now_ns();
+  s.model = std::move(m);
+  s.busy = true;
+  ++inflight_;
+  return true;
+}
+
+int Lane::poll(std::vector<Completion>& out, std::vector<Seg>& segs) {
+  Engine& e = *eng_;
+  while (inflight_ > 0) {
+    LSlot& s = slots_[next_];
+    if (!s.failed) {
+      while (s.seen < s.n && (uint32_t)_mm_cvtsi128_si32(load_record(s.hrec + s.seen)) == s.seq) ++s.seen;
+      if (s.seen < s.n) {
+        const int64_t waited = now_ns() - s.t_launch;
+        const int64_t wd = (int64_t)e.cfg_.watchdog_ms * 1000000;
+        if (e.direct_->faulted()) {
+          s.failed = true;
+          e.healthy_.store(false);
+        } else if (wd > 0 && waited > wd) {
+          e.healthy_.store(false);
+          if (waited > 10 * wd) s.failed = true;
+        }
+        if (!s.failed) return inflight_;
+      }
+    }
+    const int64_t now = now_ns();
+    const size_t base = out.size();
+    segs.push_back(Seg{base, s.model});
+    int errors = 0;
+    for (int i = 0; i < s.n; ++i) {
+      int32_t st = s.pre[i], idx = 0;
+      double p = 0.0;
+      if (s.failed) {
+        st = ST_DEVICE_ERROR;
+      } else {
+        alignas(16) ServeRecord r;
+        _mm_store_si128(reinterpret_cast<__m128i*>(&r), load_record(s.hrec + i));
+        idx = r.idx;
+        p = r.p;
+        if (st == ST_OK && !std::isfinite(p)) st = ST_NONFINITE;
+      }
+      errors += st != ST_OK;
+      out.push_back(Completion{s.tags[i], idx, st, p, now - s.t_enq});
+    }
+    e.record_lane(s, errors, now);
+    s.busy = false;
+    s.model.reset();
+    next_ = (next_ + 1) % SLOTS;
+    --inflight_;
+  }
+  return 0;
+}
+
+void Engine::record_lane(const Lane::LSlot& s, int errors, int64_t now) {
+  const double lat_us = (double)(now - s.t_enq) * 1e-3;
+  int lb = 0;
+  while (lb < 23 && (double)(int64_t(1) << lb) <= lat_us) ++lb;
+  int bb = 0;
+  while ((1 << (bb + 1)) <= s.n && bb < 11) ++bb;
+  std::lock_guard<std::mutex> lk(st_mu_);
+  stats_.requests += (uint64_t)s.n;
+  stats_.errors += (uint64_t)errors;
+  stats_.latency_sum_us += lat_us * s.n;
+  stats_.latency_hist[lb] += (uint64_t)s.n;
+  stats_.batches++;
+  stats_.batch_hist[bb]++;
+  stats_.lane_batches++;
+  if (!s.failed) {
+    stats_.path_batches[PATH_SMALL]++;
+    stats_.inline_batches++;
+    stats_.direct_batches++;
+  }
+  stats_.device_us_sum += (double)(now - s.t_launch) * 1e-3;
+  stats_.queue_wait_us_sum += (double)(s.t_launch - s.t_enq) * 1e-3 * s.n;
 }
 
 EngineStats Engine::stats() const {

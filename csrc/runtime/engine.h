@@ -92,6 +92,58 @@ struct Completion {
   int64_t latency_ns;  // submit -> completion
 };
 
+class Engine;
+
+// Per-IO-thread dispatch lane (take the engine hop out of the request path).
+// An HTTP IO thread that parsed an epoll round's rows dispatches them itself - one AQL packet into
+// the engine's HSA queue (multi-producer: InlineDispatcher::launch's producer id), rows + W + b in
+// the kernel-argument block - and polls the batch's per-row completion records in its own event
+// loop, so a request never waits for the batcher thread (queue + futex wake) or the completer
+// thread (delivery + eventfd wake). SMALL-path models whose batch fits the argument block; the
+// engine queue remains the path for everything else (wide models, lane slots all busy, fault
+// injection, no direct dispatcher). One thread per lane.
+class Lane {
+ public:
+  ~Lane();
+  Lane(const Lane&) = delete;
+  Lane& operator=(const Lane&) = delete;
+  // Launch n rows (nf features each) from the calling thread. true = dispatched, completions come
+  // from poll(); false = not eligible now (the caller submits the rows to the engine queue).
+  bool submit(const double* X, int n, int nf, const uint64_t* tags);
+  struct Seg {
+    size_t begin;  // first completion of the batch in poll()'s output
+    std::shared_ptr<const Model> model;
+  };
+  // Appends the completions of finished batches (oldest first) to `out`, one Seg per batch, and
+  // returns the number of batches still in flight. Checks the watchdog and queue faults.
+  int poll(std::vector<Completion>& out, std::vector<Seg>& segs);
+  int inflight() const { return inflight_; }
+
+ private:
+  friend class Engine;
+  explicit Lane(Engine* e, int producer);
+  struct LSlot {
+    ServeRecord* hrec = nullptr;
+    ServeRecord* drec = nullptr;
+    uint32_t seq = 0;
+    int n = 0;
+    int seen = 0;  // rows [0, seen) have their record
+    bool busy = false, failed = false;
+    int64_t t_enq = 0, t_launch = 0;
+    std::vector<uint64_t> tags;
+    std::vector<int32_t> pre;
+    std::shared_ptr<const Model> model;
+  };
+  static constexpr int SLOTS = 4;
+  Engine* eng_;
+  int producer_;
+  int inflight_ = 0;
+  int next_ = 0;         // oldest busy slot (completion order = launch order)
+  uint32_t seq_base_;    // lane-distinct sequence numbers
+  LSlot slots_[SLOTS];
+  InlineBatch batch_;    // argument block under construction
+};
+
 class Sink {
  public:
   virtual ~Sink() = default;
@@ -149,6 +201,8 @@ struct EngineConfig {
   // wake-ups (two futex hand-offs on a batch=1 request). SMALL-path models, batches of at most
   // this many rows; 0 = off. On the CPU backend the calling thread runs the float64 oracle.
   int idle_inline_rows = 8;
+  // IO threads dispatch SMALL-path batches themselves through lanes (open_lane); 0 = off
+  int lanes = 1;
 };
 
 struct EngineStats {
@@ -161,6 +215,7 @@ struct EngineStats {
   uint64_t direct_batches = 0;      // ... of which written straight into the HSA queue
   uint64_t direct_wide_batches = 0; // class-split (wide multiclass) batches dispatched into that queue
   uint64_t idle_batches = 0;        // batches run by the submitting thread (run_idle)
+  uint64_t lane_batches = 0;        // batches dispatched by IO threads through lanes (Lane::submit)
   uint64_t bar_batches = 0;         // wide batches whose rows were written into HBM through the BAR
   bool direct_dispatch = false;     // the direct queue is up
   bool direct_device_kernargs = false;  // ... and its kernarg ring is in device memory
@@ -214,6 +269,13 @@ class Engine {
                 std::shared_ptr<const Model>& m_out, bool allow_wide = false);
   // Blocking convenience API (tests / bulk scoring through the batcher).
   void predict(const double* X, int64_t B, int F, int32_t* idx, double* p, int32_t* status);
+
+  // A dispatch lane for the calling IO thread (owned by the engine, valid until it is destroyed),
+  // or nullptr: CPU backend, lanes off, no direct dispatcher or no producer id left.
+  Lane* open_lane();
+  // The thread is done with the lane: its in-flight batches are waited for (bounded) and dropped,
+  // and the lane goes back to the engine's pool for the next open_lane().
+  void close_lane(Lane* lane);
 
   EngineStats stats() const;
   const EngineConfig& config() const { return cfg_; }
@@ -270,6 +332,9 @@ class Engine {
   void deliver(std::vector<Meta>& metas, const int32_t* idx, const double* p, const int32_t* st,
                const std::shared_ptr<const Model>& m, int64_t now);
   void record_batch(size_t n);
+  friend class Lane;
+  // Lane batch bookkeeping (stats under st_mu_)
+  void record_lane(const Lane::LSlot& s, int errors, int64_t now);
   // Wait for a launched slot's done word (spin, then back off; fault and watchdog checks).
   void wait_done(Slot& s);
   // The launched slot's results -> idx / p (from the records or the output arrays).
@@ -307,6 +372,10 @@ class Engine {
   static constexpr int SIGNAL_STRIDE = 16;  // 64 bytes: one cache line per slot
   InlineBatch inline_{};        // guarded by launch_mu_
   std::mutex launch_mu_;        // launch_batch: batcher thread and run_idle callers
+
+  std::mutex lanes_mu_;
+  std::vector<std::unique_ptr<Lane>> lanes_;
+  std::vector<Lane*> free_lanes_;
 
   std::vector<std::thread> batchers_;
   std::vector<std::thread> completers_;

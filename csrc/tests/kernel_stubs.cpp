@@ -32,7 +32,7 @@ void launch_linear_split(int, const void*, int64_t, const void*, const float*, i
                          void*, size_t, hipStream_t, RecOut, SplitRecOut, KernelLauncher*) {
   unreachable("launch_linear_split");
 }
-std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int, const std::string&, int, std::string* why) {
+std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int, const std::string&, int, std::string* why, int) {
   if (why) *why = "host-only build";
   return nullptr;
 }

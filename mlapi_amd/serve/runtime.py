@@ -63,6 +63,7 @@ class EngineHandle:
         ec.spin_us = config.spin_us
         ec.inline_args = bool(config.inline_args)
         ec.idle_inline_rows = int(config.idle_inline_rows)
+        ec.lanes = int(config.lanes)
         ec.completers = int(config.completers)
         ec.batchers = int(config.batchers)
         ec.gemv_record_rows = int(config.gemv_record_rows)

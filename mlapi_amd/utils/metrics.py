@@ -75,6 +75,10 @@ def render(engine_stats: Optional[dict] = None, server_stats: Optional[dict] = N
             out += ["# HELP mlapi_idle_path_batches_total Batches the submitting IO thread ran itself on an idle engine.",
                     "# TYPE mlapi_idle_path_batches_total counter"]
             _line(out, "mlapi_idle_path_batches_total", es["idle_batches"], labels)
+        if "lane_batches" in es:
+            out += ["# HELP mlapi_lane_batches_total Batches IO threads dispatched themselves through engine lanes.",
+                    "# TYPE mlapi_lane_batches_total counter"]
+            _line(out, "mlapi_lane_batches_total", es["lane_batches"], labels)
     if server_stats:
         out += ["# HELP mlapi_http_requests_total HTTP requests by path taken.",
                 "# TYPE mlapi_http_requests_total counter"]
