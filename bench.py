@@ -165,7 +165,8 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         cpu_util["loadgen_process"] = utilization(l0, cpu_by_group(lg.pid), elapsed).get("process_total", 0.0)
         s1, h1 = srv.runtime.handle.stats(), srv.http.stats()
         nreq = max(1, s1["requests"] - s0["requests"])
-        nbat = max(1, (s1["batches"] - s0["batches"]) - (s1["idle_batches"] - s0["idle_batches"]))
+        nbat = max(1, (s1["batches"] - s0["batches"]) - (s1["idle_batches"] - s0["idle_batches"])
+                   - (s1["lane_batches"] - s0["lane_batches"]))  # batches the batcher thread launched
         # where this rank's server CPU goes, per request (IO-thread stage clock, exclusive; "poll"
         # is epoll_wait + loop overhead, mostly idle blocking) and the server-side HTTP latency
         cpu_breakdown = {
@@ -211,6 +212,7 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
                                       s3["idle_batches"] - s2["idle_batches"]], info)
         barrier(info)
         paths = {k: s1["path_batches"][k] - s0["path_batches"][k] for k in s1["path_batches"]}
+        lane_batches = s1["lane_batches"] - s0["lane_batches"]
         idle = {"c64": int(per_rank[:, 8].sum()), "batch1": int(per_rank[:, 9].sum())}
     finally:
         if srv is not None:
@@ -234,6 +236,9 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         "kernel_batches": paths,
         # batches the IO thread launched itself on an idle engine (Engine::run_idle)
         "idle_path_batches": idle,
+        # batches launched by an IO thread through the lanes' combining launcher (no batcher /
+        # completer hop; rank 0)
+        "lane_batches_rank0": int(lane_batches),
         "backend": srv.runtime.handle.backend,
         "cpu_cores_busy_rank0": cpu_util,
         "cpu_breakdown_rank0": cpu_breakdown,
@@ -269,15 +274,17 @@ def bench_serve(args, info):
 
 
 def bench_serve_wide(args, info):
-    """Wide model on the /predict hot path: F=256, K classes (2 -> GEMV kernel, else the class-split
-    MFMA kernel for serving-sized batches / the tiles kernel for large ones). --wide-dtype f32
-    (default, the engine default): f32 operands, every body within rel 1e-6 of the fp64 oracle of
-    the f32-rounded model; bf16: within rel 1e-4 of the bf16-rounded oracle."""
+    """Wide model on the /predict hot path: F=--wide-features (256), K classes (2 -> binary).
+    --wide-dtype f32 (default, the engine default): f32 storage (binary: the f32 GEMV; multiclass:
+    the f64-accumulating wide kernel), every body within rel 1e-11 (multiclass) / 1e-6 (GEMV) of the
+    fp64 oracle of the f32-rounded model; f64: the reference's precision (f64 storage, f64 MFMA
+    accumulation), every body within rel 1e-12 of sklearn's float64 math; bf16: the bf16 GEMV /
+    MFMA GEMM kernels, within rel 1e-4 of the bf16-rounded oracle."""
     from mlapi_amd.models.linear import LinearModel
     from mlapi_amd.parallel.comm import broadcast_model
     from mlapi_amd.serve.loadgen import bf16_oracle
 
-    F, K = 256, args.wide_classes
+    F, K = args.wide_features, args.wide_classes
     names = [f"f{i}" for i in range(F)]
     model = LinearModel.random(F, K, seed=0, labels=[f"class_{i}" for i in range(K)]) if info.is_main else None
     model = broadcast_model(model, info)
@@ -285,9 +292,12 @@ def bench_serve_wide(args, info):
     if args.wide_dtype == "bf16":
         okw = {"rtol_oracle": 1e-4, "label_margin": 1e-3, "oracle": bf16_oracle(model, rows)}
         rel = 1e-5
+    elif args.wide_dtype == "f64":
+        okw = {"rtol_oracle": 1e-12, "label_margin": 1e-9}
+        rel = 0.0
     else:
         f32 = lambda a: np.asarray(a, dtype=np.float32).astype(np.float64)  # noqa: E731
-        okw = {"rtol_oracle": 1e-6, "label_margin": 1e-5,
+        okw = {"rtol_oracle": 1e-6 if K == 2 else 1e-11, "label_margin": 1e-5 if K == 2 else 1e-9,
                "oracle": (LinearModel(f32(model.W), f32(model.b), model.classes, model.kind), f32(rows))}
         rel = 1e-6
     return _serve_bench(args, info, model, names, rows, dtype_cfg={"wide_dtype": args.wide_dtype}, rel_tol=rel,
@@ -469,7 +479,8 @@ def main(argv=None) -> int:
                          "driver's 20 steps time >= 2 s even at 1.3 M req/s)")
     ap.add_argument("--workload-rows", type=int, default=1024, help="serve: distinct validated requests")
     ap.add_argument("--wide-classes", type=int, default=1000, help="serve_wide: 2 = binary GEMV, else softmax GEMM")
-    ap.add_argument("--wide-dtype", default="f32", choices=["f32", "bf16"], help="serve_wide: kernel operand dtype")
+    ap.add_argument("--wide-dtype", default="f32", choices=["f32", "bf16", "f64"], help="serve_wide: kernel operand dtype")
+    ap.add_argument("--wide-features", type=int, default=256, help="serve_wide: F")
     ap.add_argument("--client-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--io-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--max-batch", type=int, default=256)

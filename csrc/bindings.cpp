@@ -114,7 +114,7 @@ py::dict stats_dict(const EngineStats& s) {
   d["dropped"] = s.dropped;
   d["rejected"] = s.rejected;
   py::dict paths;
-  static const char* names[PATH_COUNT] = {"small", "gemv", "gemm", "generic"};
+  static const char* names[PATH_COUNT] = {"small", "gemv", "gemm", "generic", "wide"};
   for (int i = 0; i < PATH_COUNT; ++i) paths[names[i]] = s.path_batches[i];
   d["path_batches"] = paths;
   d["inline_batches"] = s.inline_batches;
@@ -122,6 +122,7 @@ py::dict stats_dict(const EngineStats& s) {
   d["direct_wide_batches"] = s.direct_wide_batches;
   d["idle_batches"] = s.idle_batches;
   d["lane_batches"] = s.lane_batches;
+  d["generic_models"] = s.generic_models;
   d["bar_batches"] = s.bar_batches;
   d["direct_dispatch"] = s.direct_dispatch;
   d["direct_device_kernargs"] = s.direct_device_kernargs;
@@ -201,6 +202,29 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("X"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"), py::arg("K"), py::arg("kind"),
       py::arg("out_idx"), py::arg("out_p"), py::arg("ws"), py::arg("ws_bytes"), py::arg("stream") = 0);
+  m.def(
+      "linear_wide_plan",
+      [](int dt, int F, int K) {
+        const WidePlan p = linear_wide_plan(dt, F, K);
+        py::dict d;
+        d["ncb"] = p.ncb;
+        d["nfs"] = p.nfs;
+        d["ldx"] = p.ldx;
+        d["fsteps"] = p.fsteps;
+        return d;
+      },
+      py::arg("dt"), py::arg("F"), py::arg("K"));
+  m.def("linear_wide_workspace", &linear_wide_workspace, py::arg("B"), py::arg("dt"), py::arg("F"), py::arg("K"));
+  m.def(
+      "linear_wide",
+      [](int dt, uintptr_t X, int64_t ldx, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind,
+         uintptr_t out_idx, uintptr_t out_p, uintptr_t ws, size_t ws_bytes, uintptr_t stream) {
+        launch_linear_wide(dt, ptr<void>(X), ldx, ptr<void>(W), ptr<double>(b), B, F, K, kind, ptr<int32_t>(out_idx),
+                           ptr<double>(out_p), ptr<void>(ws), ws_bytes, stream_of(stream));
+      },
+      py::arg("dt"), py::arg("X"), py::arg("ldx"), py::arg("W"), py::arg("b"), py::arg("B"), py::arg("F"),
+      py::arg("K"), py::arg("kind"), py::arg("out_idx"), py::arg("out_p"), py::arg("ws"), py::arg("ws_bytes"),
+      py::arg("stream") = 0);
   m.def("linear_split_supported", &linear_split_supported);
   m.def("linear_split_workspace", &linear_split_workspace);
   m.def("linear_split_xcd_err_offset", &linear_split_xcd_err_offset);
@@ -405,6 +429,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("inline_args", &EngineConfig::inline_args)
       .def_readwrite("idle_inline_rows", &EngineConfig::idle_inline_rows)
       .def_readwrite("lanes", &EngineConfig::lanes)
+      .def_readwrite("f32_split", &EngineConfig::f32_split)
       .def_readwrite("completers", &EngineConfig::completers)
       .def_readwrite("batchers", &EngineConfig::batchers)
       .def_readwrite("gemv_record_rows", &EngineConfig::gemv_record_rows)
@@ -446,7 +471,7 @@ PYBIND11_MODULE(_C, m) {
            })
       .def("model_path",
            [](Engine& e) -> std::string {
-             static const char* names[PATH_COUNT] = {"small", "gemv", "gemm", "generic"};
+             static const char* names[PATH_COUNT] = {"small", "gemv", "gemm", "generic", "wide"};
              auto mm = e.model();
              return mm ? names[mm->path] : "";
            })

@@ -37,6 +37,7 @@ void launch_linear_small(int dt, const void* X, int64_t ldx, const void* W, cons
 // packet. Only the (idx, p) results go back, written straight into host-mapped memory.
 constexpr int INLINE_X_BYTES = 3072;
 constexpr int INLINE_WB_BYTES = 512;
+constexpr int INLINE_MAX_ROWS = 128;  // one block of <= 128 threads
 struct InlineBatch {
   int32_t n, F, K, kind;
   int32_t* out_idx;
@@ -46,8 +47,13 @@ struct InlineBatch {
   // Per-row completion records (host-mapped, ServeRecord[n]); when set, each row's result AND the
   // batch's sequence number go out in ONE 16-byte store, with no fence and no done word.
   void* rec;
+  // Scatter mode (combined batches of the engine's lanes): rec is a record arena and row r's record
+  // goes to rec[rec_idx[r]] (each row back to its own IO thread's ring); `done` then gets the batch
+  // seq from lane 0 after its record, write-through, no fence (the launcher's in-flight count only).
+  int32_t rec_scatter;
   alignas(16) unsigned char wb[INLINE_WB_BYTES];  // W [K][F] then b [K] (dtype of the launch)
   alignas(16) unsigned char x[INLINE_X_BYTES];    // rows [n][F]
+  alignas(16) uint32_t rec_idx[INLINE_MAX_ROWS];  // scatter mode only (only n entries are copied)
 };
 // One row's result as the host polls it: seq last written by the batch that produced it.
 struct alignas(16) ServeRecord {
@@ -183,6 +189,36 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
                          int kind, int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes,
                          hipStream_t stream, RecOut ro = RecOut(), SplitRecOut sro = SplitRecOut(),
                          KernelLauncher* direct = nullptr);
+
+// ---- linear_wide.hip: f64-accumulating predict for wide models (linear_wide.h) ----------------
+// X, W stored as f64 or f32 (dt), row stride ldx >= plan.ldx with the columns F..ldx zero in both;
+// b: f64 [K]. Every kind (binary kinds: K = 1). Accumulation in f64 on the matrix cores
+// (v_mfma_f64_16x16x4_f64), so f32 storage loses nothing beyond the f32 rounding of its inputs.
+// Grid: plan.ncb 16-class blocks x plan.nfs feature splits x ceil(B / 32) row groups.
+struct WidePlan {
+  int ncb = 0;     // 16-class blocks
+  int nfs = 0;     // feature splits over blocks (their partial logits summed by the last arriver)
+  int ldx = 0;     // padded row width the kernel reads (multiple of the split unit)
+  int fsteps = 0;  // steps per wave per split
+};
+WidePlan linear_wide_plan(int dt, int F, int K);
+// workspace (zeroed once; tickets are re-armed in-kernel) for up to B rows
+size_t linear_wide_workspace(int64_t B, int dt, int F, int K);
+// Host class merge (serving, multiclass, B <= 32): block cb writes for row r two 16-byte units at
+// rec[(cb * 32 + r) * 2 + {0, 1}] = {seq, argmax, m (f64)}, {seq, 0, s (f64)} and the host merges
+// the plan.ncb blocks in block order (split_merge.h, merge_wide_records).
+struct alignas(16) WideRecord {
+  uint32_t seq;
+  int32_t v;  // argmax (unit 0), 0 (unit 1)
+  double x;   // m (unit 0), s (unit 1)
+};
+struct WideRecOut {
+  WideRecord* rec = nullptr;
+  uint32_t seq = 0;
+};
+void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const double* b, int64_t B, int F, int K,
+                        int kind, int32_t* out_idx, double* out_p, void* workspace, size_t ws_bytes, hipStream_t stream,
+                        RecOut ro = RecOut(), WideRecOut hro = WideRecOut(), KernelLauncher* direct = nullptr);
 
 // Multiclass training row stats (gemm_softmax.hip MODE 2), X_aug = [X | 0.. | 1 | 0 x 7] bf16
 // read through its row stride ldx (the first F columns); W: [K, F] bf16; b: [K] f32.

@@ -12,6 +12,7 @@
 #include "linear_rows.h"
 #include "gemv_binary.h"
 #include "linear_split.h"
+#include "linear_wide.h"
 
 namespace {
 
@@ -23,6 +24,13 @@ __device__ __forceinline__ void direct_inline() {
   else
     mlapi::rows::inline_batch_rows<T, FMAX, KMAX>(a);
   if (a->done == nullptr) return;  // uniform
+  if (a->rec_scatter) {            // uniform: in-flight accounting only (records are already out)
+    if (threadIdx.x == 0) {
+      const uint32_t v = a->seq;
+      asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(a->done), "v"(v) : "memory");
+    }
+    return;
+  }
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(a->done, a->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -95,3 +103,14 @@ MLAPI_SPLIT_ENTRIES(f32, float, 32)
   MLAPI_GEMV_ENTRY(TN, T, 64, 8, 1)
 MLAPI_GEMV_ENTRIES(bf16, uint16_t)
 MLAPI_GEMV_ENTRIES(f32, float)
+
+// The f64-accumulating wide predict (linear_wide.h) for wide f64 / f32 models: the entries of
+// linear_wide.hip's kernel, named mlapi_wide_<storage dtype>_nb<row tiles>.
+#define MLAPI_WIDE_ENTRY(TN, T, NB)                                                                      \
+  extern "C" __global__ __launch_bounds__(256) void mlapi_wide_##TN##_nb##NB(const mlapi::wide::WideArgs a) { \
+    mlapi::wide::wide_predict<T, NB>(a);                                                                 \
+  }
+MLAPI_WIDE_ENTRY(f64, double, 1)
+MLAPI_WIDE_ENTRY(f64, double, 2)
+MLAPI_WIDE_ENTRY(f32, float, 1)
+MLAPI_WIDE_ENTRY(f32, float, 2)

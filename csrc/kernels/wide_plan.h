@@ -1,0 +1,48 @@
+// Host plan of the f64-accumulating wide predict (linear_wide.h): pure arithmetic, shared by the
+// launcher (linear_wide.hip) and host-only builds (csrc/tests/kernel_stubs.cpp), where the engine
+// still plans models it then serves on the CPU backend.
+#pragma once
+#include <algorithm>
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+
+#include "mlapi/common.h"
+#include "mlapi/kernels.h"
+
+namespace mlapi {
+namespace wide_plan {
+
+constexpr int CB = 16;     // classes per block
+constexpr int RG = 32;     // rows per row group
+constexpr int WAVES = 4;   // waves per block (feature quarters)
+constexpr int SMAX = 32;   // wave steps per feature split before the features are split over blocks
+
+inline WidePlan plan(int dt, int F, int K) {
+  if (dt != DT_F64 && dt != DT_F32) throw std::invalid_argument("linear_wide: f64 or f32 storage");
+  if (F < 1 || K < 1) throw std::invalid_argument("linear_wide: empty model");
+  const int E = dt == DT_F64 ? 2 : 4;  // elements per 16-byte load
+  const int unit = WAVES * 4 * E;      // features one step of every wave covers
+  WidePlan p;
+  p.ncb = (K + CB - 1) / CB;
+  p.nfs = std::max(1, (F + unit * SMAX - 1) / (unit * SMAX));
+  const int per = unit * p.nfs;
+  p.ldx = (F + per - 1) / per * per;
+  p.fsteps = p.ldx / per;
+  return p;
+}
+
+inline int row_groups(int64_t B) { return (int)((std::max<int64_t>(B, 1) + RG - 1) / RG); }
+inline size_t counters_bytes(int rg, int ncb) { return (((size_t)rg * ncb + rg) * sizeof(unsigned) + 255) & ~size_t(255); }
+
+inline size_t workspace(int64_t B, int dt, int F, int K) {
+  const WidePlan p = plan(dt, F, K);
+  const int rg = row_groups(B);
+  size_t bytes = counters_bytes(rg, p.ncb);
+  if (p.nfs > 1) bytes += (size_t)rg * p.ncb * p.nfs * (2 * 4 * 64) * sizeof(double);
+  bytes += (size_t)rg * p.ncb * RG * 4 * sizeof(double);
+  return bytes;
+}
+
+}  // namespace wide_plan
+}  // namespace mlapi

@@ -70,7 +70,8 @@ hsa_status_t collect_split_kernels(hsa_executable_t, hsa_agent_t, hsa_executable
   std::string name(len, '\0');
   hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_NAME, &name[0]);
   if (name.size() > 3 && name.compare(name.size() - 3, 3, ".kd") == 0) name.resize(name.size() - 3);
-  if (name.rfind("mlapi_split_", 0) != 0 && name.rfind("mlapi_gemv_", 0) != 0) return HSA_STATUS_SUCCESS;
+  if (name.rfind("mlapi_split_", 0) != 0 && name.rfind("mlapi_gemv_", 0) != 0 && name.rfind("mlapi_wide_", 0) != 0)
+    return HSA_STATUS_SUCCESS;
   Kernel k;
   hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.object);
   hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.group);
@@ -241,6 +242,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     const size_t wb_end = offsetof(InlineBatch, wb) + (size_t)a.K * (a.F + 1) * es;
     std::memcpy(ka, &a, wb_end);
     std::memcpy(ka + offsetof(InlineBatch, x), a.x, (size_t)a.n * a.F * es);
+    if (a.rec_scatter) std::memcpy(ka + offsetof(InlineBatch, rec_idx), a.rec_idx, (size_t)a.n * sizeof(uint32_t));
     flush_kernargs();
     const uint16_t threads = a.n <= 64 ? 64 : 128;
     // Acquire at agent scope invalidates the caches the kernel reads its (host-written) kernarg

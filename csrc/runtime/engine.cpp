@@ -29,6 +29,7 @@ Model::~Model() {
     if (db) (void)hipFree(db);
     if (ws) (void)hipFree(ws);
     if (ws_split) (void)hipFree(ws_split);
+    if (ws_wide) (void)hipFree(ws_wide);
     (void)hipSetDevice(prev);
   }
 }
@@ -150,6 +151,9 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     MLAPI_HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi));
     slots_.resize(cfg_.slots);
     slot_row_bytes_ = padded_features(cfg_.max_features) * sizeof(double);
+    for (int f = 1; f <= cfg_.max_features; ++f)  // WIDE models' padded rows (plan width, either storage)
+      slot_row_bytes_ = std::max({slot_row_bytes_, (size_t)linear_wide_plan(DT_F64, f, 1).ldx * sizeof(double),
+                                  (size_t)linear_wide_plan(DT_F32, f, 1).ldx * sizeof(float)});
     const size_t xb = (size_t)cfg_.max_batch * slot_row_bytes_;
     const size_t done_bytes = sizeof(uint32_t) * SIGNAL_STRIDE * cfg_.slots;
     MLAPI_HIP_CHECK(hipHostMalloc((void**)&done_h_, done_bytes, hipHostMallocMapped | hipHostMallocCoherent));
@@ -160,8 +164,19 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     MLAPI_HIP_CHECK(hipDeviceSynchronize());
     if (cfg_.direct_dispatch && !cfg_.hsaco_path.empty()) {
       std::string why;
-      direct_ = make_direct_dispatcher(cfg_.device, cfg_.hsaco_path, cfg_.slots, &why, cfg_.lanes > 0 ? 64 : 0);
+      direct_ = make_direct_dispatcher(cfg_.device, cfg_.hsaco_path, cfg_.slots, &why);
       if (!direct_) std::fprintf(stderr, "[mlapi engine] direct dispatch off (%s): using hipLaunchKernel\n", why.c_str());
+    }
+    if (direct_ && cfg_.lanes > 0) {
+      // lanes' record rings (host-mapped, written by the kernels' write-through stores) and the
+      // combined batches' done words
+      const size_t ab = (size_t)MAX_LANES * Lane::RING * sizeof(ServeRecord);
+      MLAPI_HIP_CHECK(hipHostMalloc((void**)&arena_h_, ab, hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(arena_h_, 0, ab);
+      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&arena_d_, arena_h_, 0));
+      MLAPI_HIP_CHECK(hipHostMalloc((void**)&cdone_h_, CRING * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(cdone_h_, 0, CRING * sizeof(uint32_t));
+      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&cdone_d_, cdone_h_, 0));
     }
     for (int i = 0; i < cfg_.slots; ++i) {
       Slot& s = slots_[i];
@@ -178,7 +193,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.drec, s.hrec, 0));
       if (direct_ && cfg_.bar_rows > 0) s.xbar = direct_->bar_alloc((size_t)cfg_.bar_rows * slot_row_bytes_);
       if (cfg_.host_merge_rows > 0) {
-        const size_t sb = (size_t)64 * 32 * sizeof(SplitRecord);
+        // linear_split: [64 blocks][32 rows] SplitRecord; linear_wide: [64 blocks][32 rows][2] WideRecord
+        const size_t sb = (size_t)64 * 32 * 2 * sizeof(WideRecord);
         MLAPI_HIP_CHECK(hipHostMalloc((void**)&s.hsrec, sb, hipHostMallocMapped | hipHostMallocCoherent));
         std::memset(s.hsrec, 0, sb);
         MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.dsrec, s.hsrec, 0));
@@ -199,6 +215,22 @@ Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (done_h_) (void)hipHostFree(done_h_);
     if (sig_counter_) (void)hipFree(sig_counter_);
+    {
+      // lanes' rows still in flight write into the arena: wait for the combined batches (bounded)
+      std::lock_guard<std::mutex> lk(launch_mu_);
+      const int64_t until = now_ns() + 2000000000LL;
+      while (cin_n_ > 0 && now_ns() < until) {
+        const CBatch& b = cin_[cin_head_];
+        if (__atomic_load_n(cdone_h_ + b.seq % CRING, __ATOMIC_ACQUIRE) == b.seq) {
+          cin_head_ = (cin_head_ + 1) % CRING;
+          --cin_n_;
+        } else {
+          _mm_pause();
+        }
+      }
+    }
+    if (arena_h_) (void)hipHostFree(arena_h_);
+    if (cdone_h_) (void)hipHostFree(cdone_h_);
     for (Slot& s : slots_) {
       if (s.hx) (void)hipHostFree(s.hx);
       if (s.dstage) (void)hipFree(s.dstage);
@@ -258,17 +290,31 @@ uint64_t Engine::load_model(int kind, int F, int K, const double* W, const doubl
     m->path = PATH_GEMM;
     m->xdt = DT_BF16;
     m->ldx = (int)padded_features(F);
-  } else if (!binary && K >= 2 && cfg_.wide_dtype == DT_F32 && F <= 512) {
-    // f32 MFMA class-split kernel at a power-of-two width (v_mfma_f32_16x16x4_f32)
+  } else if (!binary && K >= 2 && cfg_.wide_dtype == DT_F32 && F <= 512 && cfg_.f32_split) {
+    // f32-accumulating class-split kernel at a power-of-two width (v_mfma_f32_16x16x4_f32)
     m->path = PATH_GEMM;
     m->xdt = DT_F32;
     m->ldx = (int)padded_features(F);
+  } else if (binary ? K == 1 : K >= 2) {
+    // f64 accumulation on the matrix cores, any width: f64 storage (wide_dtype f64) or f32 (bf16
+    // models beyond the bf16 kernels' F <= 4096 are stored f32 here: more precision, not less)
+    m->path = PATH_WIDE;
+    m->xdt = cfg_.wide_dtype == DT_F64 ? DT_F64 : DT_F32;
+    m->wplan = linear_wide_plan(m->xdt, F, K);
+    m->ldx = m->wplan.ldx;
   } else {
     m->path = PATH_GENERIC;
     m->xdt = cfg_.wide_dtype == DT_F64 ? DT_F64 : DT_F32;
     m->ldx = F;
   }
+  if (m->path == PATH_GENERIC) {
+    std::fprintf(stderr, "[mlapi engine] warning: model kind %d F=%d K=%d runs on the scalar GENERIC kernel\n", kind, F,
+                 K);
+    std::lock_guard<std::mutex> lk(st_mu_);
+    stats_.generic_models++;
+  }
   m->pdt = (m->path == PATH_GEMV || m->path == PATH_GEMM) ? DT_F32 : m->xdt;
+  if (m->path == PATH_WIDE) m->pdt = DT_F64;
   m->bias0 = (float)b[0];
   m->version = next_version_.fetch_add(1);
   if (cfg_.device >= 0) {
@@ -290,10 +336,15 @@ uint64_t Engine::load_model(int kind, int F, int K, const double* W, const doubl
       }
     MLAPI_HIP_CHECK(hipMalloc(&m->dW, wbuf.size()));
     MLAPI_HIP_CHECK(hipMemcpy(m->dW, wbuf.data(), wbuf.size(), hipMemcpyHostToDevice));
-    // bias: xdt for SMALL / GENERIC (the kernels' T), f32 for GEMM (GEMV takes a scalar)
-    const int bdt = m->path == PATH_SMALL || m->path == PATH_GENERIC ? m->xdt : DT_F32;
+    // bias: xdt for SMALL / GENERIC (the kernels' T), f64 for WIDE, f32 for GEMM (GEMV takes a scalar)
+    const int bdt = m->path == PATH_SMALL || m->path == PATH_GENERIC ? m->xdt : m->path == PATH_WIDE ? DT_F64 : DT_F32;
     MLAPI_HIP_CHECK(hipMalloc(&m->db, (size_t)K * dtype_size(bdt)));
-    if (bdt == DT_F64) {
+    if (bdt == DT_F64 && m->path == PATH_WIDE && m->xdt == DT_F32) {
+      // f32 storage: the intercept is rounded like W and the rows (the f32 model, exactly)
+      std::vector<double> bd(K);
+      for (int k = 0; k < K; ++k) bd[k] = (double)(float)b[k];
+      MLAPI_HIP_CHECK(hipMemcpy(m->db, bd.data(), (size_t)K * 8, hipMemcpyHostToDevice));
+    } else if (bdt == DT_F64) {
       MLAPI_HIP_CHECK(hipMemcpy(m->db, b, (size_t)K * 8, hipMemcpyHostToDevice));
     } else {
       std::vector<float> bf(b, b + K);
@@ -313,6 +364,11 @@ uint64_t Engine::load_model(int kind, int F, int K, const double* W, const doubl
         MLAPI_HIP_CHECK(hipMalloc(&m->ws_split, m->ws_split_bytes));
         MLAPI_HIP_CHECK(hipMemset(m->ws_split, 0, m->ws_split_bytes));
       }
+    }
+    if (m->path == PATH_WIDE) {
+      m->ws_wide_bytes = linear_wide_workspace(cfg_.max_batch, m->xdt, F, K);
+      MLAPI_HIP_CHECK(hipMalloc(&m->ws_wide, m->ws_wide_bytes));
+      MLAPI_HIP_CHECK(hipMemset(m->ws_wide, 0, m->ws_wide_bytes));
     }
     MLAPI_HIP_CHECK(hipDeviceSynchronize());
   }
@@ -576,6 +632,7 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     s.rec_mode = cfg_.record_completion ? REC_ROWS : 0;
     a.done = s.rec_mode ? nullptr : sig.done;
     a.rec = s.rec_mode ? s.drec : nullptr;
+    a.rec_scatter = 0;
     a.seq = sig.seq;
     fill_inline(
         a, m, n,
@@ -605,7 +662,8 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
   // +4 us on the GPU leg for a 1 MB f32 K = 1000 model, which outweighs the ~2 us of batcher time
   // saved (profiles/r3_direct_wide/)
   const size_t w_bytes = (size_t)(m.path == PATH_GEMV ? 1 : m.K) * m.ldx * dtype_size(m.xdt);
-  const bool direct_wide = direct_ && cfg_.direct_wide && cfg_.record_completion && (split_path || gemv_rec) &&
+  const bool direct_wide = direct_ && cfg_.direct_wide && cfg_.record_completion &&
+                           (split_path || gemv_rec || m.path == PATH_WIDE) &&
                            w_bytes <= (size_t)cfg_.direct_wide_max_weight_bytes;
   const int64_t t_p0 = now_ns();
   pack_rows(s, xs, m, bar ? s.xbar : s.hx);
@@ -651,7 +709,27 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     } dl;
     dl.d = direct_.get();
     dl.flush_on_miss = bar;
-    if (m.path == PATH_GEMV)
+    if (m.path == PATH_WIDE) {
+      // f64 accumulation; serving-sized multiclass batches end in per-(class block, row) records the
+      // completer merges (no in-kernel class merge), the rest in per-row records
+      WideRecOut hro;
+      const bool binary = m.kind == KIND_BINARY || m.kind == KIND_BINARY_SOFTMAX;
+      if (cfg_.record_completion && s.hsrec != nullptr && !binary && n <= cfg_.host_merge_rows && n <= 32 &&
+          m.wplan.ncb > 1 && m.wplan.ncb <= 64) {
+        hro.rec = reinterpret_cast<WideRecord*>(s.dsrec);
+        hro.seq = sig.seq;
+        ro = RecOut();
+        s.rec_mode = REC_WIDE;
+        s.rec_nsplit = m.wplan.ncb;
+      } else if (cfg_.record_completion) {
+        ro.rec = s.drec;
+        ro.seq = sig.seq;
+        s.rec_mode = REC_ROWS;
+      }
+      launch_linear_wide(m.xdt, X, m.ldx, m.dW, static_cast<const double*>(m.db), n, m.F, m.K, m.kind, s.didx,
+                         static_cast<double*>(s.dp), m.ws_wide, m.ws_wide_bytes, stream_, ro, hro,
+                         direct_wide ? &dl : nullptr);
+    } else if (m.path == PATH_GEMV)
       launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_, ro,
                          direct_wide && ro.rec != nullptr ? &dl : nullptr);
     else if (m.ws_split != nullptr && (m.xdt == DT_F32 || n <= cfg_.split_max_rows)) {
@@ -816,9 +894,19 @@ void Engine::wait_done(Slot& s) {
   const int64_t t0 = now_ns();
   uint32_t spins = 0;
   int next_row = 0;  // record mode: rows [0, next_row) seen complete
-  const int nrec = s.rec_mode == REC_SPLITS ? s.rec_nsplit * s.n : s.n;
+  const int nrec = s.rec_mode == REC_SPLITS ? s.rec_nsplit * s.n : s.rec_mode == REC_WIDE ? 2 * s.rec_nsplit * s.n : s.n;
   auto done = [&]() -> bool {
     if (!s.rec_mode) return __atomic_load_n(dw, __ATOMIC_ACQUIRE) == s.seq;
+    if (s.rec_mode == REC_WIDE) {  // unit k: block k / (2n), row (k / 2) % n, half k % 2 (at [block][32][2])
+      const WideRecord* base = reinterpret_cast<const WideRecord*>(s.hsrec);
+      while (next_row < nrec) {
+        const int cb = next_row / (2 * s.n), rem = next_row - cb * 2 * s.n;
+        const WideRecord* r = base + ((size_t)cb * 32 + rem / 2) * 2 + (rem & 1);
+        if ((uint32_t)_mm_cvtsi128_si32(load_record(reinterpret_cast<const ServeRecord*>(r))) != s.seq) break;
+        ++next_row;
+      }
+      return next_row == nrec;
+    }
     if (s.rec_mode == REC_SPLITS) {  // record k: split k / n, row k % n (at [split][32])
       while (next_row < nrec) {
         const int sp = next_row / s.n, row = next_row - sp * s.n;
@@ -863,6 +951,22 @@ const int32_t* Engine::collect(Slot& s, std::vector<int32_t>& st, std::vector<do
     std::fill(st.begin(), st.end(), (int32_t)ST_DEVICE_ERROR);
     std::fill(pd.begin(), pd.end(), 0.0);
     idx.assign(n, 0);
+    return idx.data();
+  }
+  if (s.rec_mode == REC_WIDE) {
+    // host merge of linear_wide's per-class-block f64 states, in block order
+    idx.resize(n);
+    const bool ovr = s.model->kind == KIND_OVR;
+    const int ncb = s.rec_nsplit;
+    const WideRecord* base = reinterpret_cast<const WideRecord*>(s.hsrec);
+    for (size_t i = 0; i < n; ++i) {
+      alignas(16) WideRecord r[128];
+      for (int cb = 0; cb < ncb; ++cb)
+        for (int u = 0; u < 2; ++u)
+          _mm_store_si128(reinterpret_cast<__m128i*>(&r[2 * cb + u]),
+                          load_record(reinterpret_cast<const ServeRecord*>(base + ((size_t)cb * 32 + i) * 2 + u)));
+      pd[i] = merge_wide_records(r, ncb, ovr, &idx[i]);
+    }
     return idx.data();
   }
   if (s.rec_mode == REC_SPLITS) {
@@ -1060,22 +1164,19 @@ void Engine::completer_loop() {
   }
 }
 
-// ---- per-IO-thread dispatch lanes ---------------------------------------------------------------
+// ---- per-IO-thread lanes: flat-combining launcher --------------------------------------------------
 Lane* Engine::open_lane() {
-  if (cfg_.device < 0 || cfg_.lanes <= 0 || !direct_ || !cfg_.record_completion || !cfg_.inline_args) return nullptr;
-  {
-    std::lock_guard<std::mutex> lk(lanes_mu_);
-    if (!free_lanes_.empty()) {
-      Lane* l = free_lanes_.back();
-      free_lanes_.pop_back();
-      return l;
-    }
-  }
-  const int p = direct_->add_producer();
-  if (p < 0) return nullptr;
-  std::unique_ptr<Lane> l(new Lane(this, p));
+  if (cfg_.device < 0 || cfg_.lanes <= 0 || !direct_ || !cfg_.record_completion || !cfg_.inline_args ||
+      arena_h_ == nullptr)
+    return nullptr;
   std::lock_guard<std::mutex> lk(lanes_mu_);
-  lanes_.push_back(std::move(l));
+  if (!free_lanes_.empty()) {
+    Lane* l = free_lanes_.back();
+    free_lanes_.pop_back();
+    return l;
+  }
+  if ((int)lanes_.size() >= MAX_LANES) return nullptr;
+  lanes_.push_back(std::unique_ptr<Lane>(new Lane(this, (uint32_t)lanes_.size() * Lane::RING)));
   return lanes_.back().get();
 }
 
@@ -1084,153 +1185,241 @@ void Engine::close_lane(Lane* lane) {
   std::vector<Completion> c;
   std::vector<Lane::Seg> segs;
   const int64_t until = now_ns() + 2000000000LL;
-  while (lane->poll(c, segs) > 0 && now_ns() < until) _mm_pause();
-  if (lane->inflight() > 0) return;  // still running after 2 s: never reuse it (its records may be written)
+  while (lane->poll(c, segs) > 0 && now_ns() < until) {
+    c.clear();
+    segs.clear();
+    _mm_pause();
+  }
+  if (lane->inflight() > 0) return;  // still pending after 2 s: never reuse it (its records may be written)
   std::lock_guard<std::mutex> lk(lanes_mu_);
   free_lanes_.push_back(lane);
 }
 
-namespace {
-constexpr int LANE_MAX_ROWS = 128;  // the inline kernels run one block of <= 128 threads
-}
-
-Lane::Lane(Engine* e, int producer) : eng_(e), producer_(producer) {
-  // distinct sequence numbers per lane (a slot's records never carry a stale match)
-  seq_base_ = (uint32_t)producer << 24;
-  MLAPI_HIP_CHECK(hipSetDevice(e->cfg_.device));
-  for (LSlot& s : slots_) {
-    const size_t rb = (size_t)LANE_MAX_ROWS * sizeof(ServeRecord);
-    MLAPI_HIP_CHECK(hipHostMalloc((void**)&s.hrec, rb, hipHostMallocMapped | hipHostMallocCoherent));
-    std::memset(s.hrec, 0, rb);
-    MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&s.drec, s.hrec, 0));
-    s.tags.reserve(LANE_MAX_ROWS);
-    s.pre.reserve(LANE_MAX_ROWS);
-  }
-}
-
-Lane::~Lane() {
-  // a kernel still in flight writes into these records: wait for it (bounded) before freeing
-  const int64_t until = now_ns() + 2000000000LL;
-  for (int k = 0; k < SLOTS; ++k) {
-    LSlot& s = slots_[k];
-    if (!s.busy || s.failed) continue;
-    for (int i = 0; i < s.n && now_ns() < until; ++i)
-      while (__atomic_load_n(&s.hrec[i].seq, __ATOMIC_ACQUIRE) != s.seq && now_ns() < until) _mm_pause();
-  }
-  (void)hipSetDevice(eng_->cfg_.device);
-  for (LSlot& s : slots_)
-    if (s.hrec) (void)hipHostFree(s.hrec);
+Lane::Lane(Engine* e, uint32_t arena_base) : eng_(e), base_(arena_base) {
+  for (uint32_t i = 0; i < RING; ++i) ring_[i].rec = base_ + i;
+  ptrs_.reserve(INLINE_MAX_ROWS);
 }
 
 bool Lane::submit(const double* X, int n, int nf, const uint64_t* tags) {
   Engine& e = *eng_;
-  if (n <= 0 || n > LANE_MAX_ROWS || inflight_ == SLOTS) return false;
+  if (n <= 0 || n > INLINE_MAX_ROWS || head_ - tail_ + (uint64_t)n > RING) return false;
   if (nf < 0 || nf > e.cfg_.max_features) return false;
   if (e.drop_.load(std::memory_order_relaxed) || e.cfg_.fail_every > 0 || e.cfg_.delay_us > 0) return false;
   if (e.direct_->faulted()) return false;
-  std::shared_ptr<const Model> m = e.model();
-  if (!m || m->path != PATH_SMALL || !linear_inline_fits(m->xdt, n, m->F, m->K)) return false;
-  const int64_t t = now_ns();
-  LSlot& s = slots_[(next_ + inflight_) % SLOTS];
-  s.n = n;
-  s.tags.assign(tags, tags + n);
-  s.pre.assign((size_t)n, ST_OK);
-  s.seen = 0;
-  s.failed = false;
-  uint32_t sq = ++seq_base_;
-  if (sq == 0) sq = ++seq_base_;  // 0 is the records' initial value
-  s.seq = sq;
-  InlineBatch& a = batch_;
-  a.out_idx = nullptr;
-  a.out_p = nullptr;
-  a.done = nullptr;
-  a.rec = s.drec;
-  a.seq = s.seq;
-  fill_inline(
-      a, *m, n, [&](int64_t i) -> const double* { return nf == m->F ? X + i * nf : nullptr; }, s.pre.data());
-  try {
-    TraceRange tr("mlapi.lane.launch");
-    e.direct_->launch(m->xdt, a, producer_);
-  } catch (const std::exception&) {
-    e.healthy_.store(false);
-    return false;  // nothing was published: the caller's queued submit answers the rows
+  {
+    const std::shared_ptr<const Model> m = e.model();
+    if (!m || m->path != PATH_SMALL || !linear_inline_fits(m->xdt, n, m->F, m->K)) return false;
   }
-  s.t_enq = t;
-  s.t_launch = now_ns();
-  s.model = std::move(m);
-  s.busy = true;
-  ++inflight_;
+  const int64_t t = now_ns();
+  ptrs_.clear();
+  for (int i = 0; i < n; ++i) {
+    LaneEntry& en = ring_[(head_ + (uint64_t)i) % RING];
+    en.expect.store(0, std::memory_order_relaxed);
+    en.pre = ST_OK;
+    en.tag = tags[i];
+    en.t_enq = t;
+    ptrs_.push_back(&en);
+  }
+  head_ += (uint64_t)n;
+  {
+    std::lock_guard<std::mutex> lk(e.cq_mu_);
+    e.cq_x_.insert(e.cq_x_.end(), X, X + (size_t)n * nf);
+    e.cq_nf_.insert(e.cq_nf_.end(), (size_t)n, (int32_t)nf);
+    e.cq_e_.insert(e.cq_e_.end(), ptrs_.begin(), ptrs_.end());
+    e.cq_n_.store((int)e.cq_e_.size(), std::memory_order_release);
+  }
+  e.combine();
   return true;
 }
 
 int Lane::poll(std::vector<Completion>& out, std::vector<Seg>& segs) {
   Engine& e = *eng_;
-  while (inflight_ > 0) {
-    LSlot& s = slots_[next_];
-    if (!s.failed) {
-      while (s.seen < s.n && (uint32_t)_mm_cvtsi128_si32(load_record(s.hrec + s.seen)) == s.seq) ++s.seen;
-      if (s.seen < s.n) {
-        const int64_t waited = now_ns() - s.t_launch;
-        const int64_t wd = (int64_t)e.cfg_.watchdog_ms * 1000000;
-        if (e.direct_->faulted()) {
-          s.failed = true;
-          e.healthy_.store(false);
-        } else if (wd > 0 && waited > wd) {
-          e.healthy_.store(false);
-          if (waited > 10 * wd) s.failed = true;
-        }
-        if (!s.failed) return inflight_;
-      }
+  if (head_ == tail_) return 0;
+  if (e.cq_n_.load(std::memory_order_acquire) > 0) e.combine();
+  const int64_t now = now_ns();
+  const int64_t wd = (int64_t)e.cfg_.watchdog_ms * 1000000;
+  const bool faulted = e.direct_->faulted();
+  int done = 0, errors = 0;
+  double lat_sum = 0;
+  uint64_t lat_hist[24] = {0};
+  const Model* last = nullptr;
+  // rows complete in launch order per batch but batches may finish out of order: scan every pending
+  // row, retire the finished prefix of the ring
+  for (uint64_t pos = tail_; pos != head_; ++pos) {
+    LaneEntry& en = ring_[pos % RING];
+    if (en.tag == ~uint64_t(0)) continue;  // already delivered (out of order)
+    const uint32_t seq = en.expect.load(std::memory_order_acquire);
+    bool fin = false, fail = false;
+    alignas(16) ServeRecord r{};
+    if (seq != 0) {
+      _mm_store_si128(reinterpret_cast<__m128i*>(&r), load_record(e.arena_h_ + en.rec));
+      fin = r.seq == seq;
     }
-    const int64_t now = now_ns();
-    const size_t base = out.size();
-    segs.push_back(Seg{base, s.model});
-    int errors = 0;
-    for (int i = 0; i < s.n; ++i) {
-      int32_t st = s.pre[i], idx = 0;
-      double p = 0.0;
-      if (s.failed) {
-        st = ST_DEVICE_ERROR;
-      } else {
-        alignas(16) ServeRecord r;
-        _mm_store_si128(reinterpret_cast<__m128i*>(&r), load_record(s.hrec + i));
-        idx = r.idx;
-        p = r.p;
-        if (st == ST_OK && !std::isfinite(p)) st = ST_NONFINITE;
+    if (!fin) {
+      const int64_t waited = now - en.t_enq;
+      if (faulted || (wd > 0 && waited > 10 * wd)) {
+        fin = fail = true;  // the record may still land later: this ring slot is written off below
+      } else if (wd > 0 && waited > wd) {
+        e.healthy_.store(false);
       }
-      errors += st != ST_OK;
-      out.push_back(Completion{s.tags[i], idx, st, p, now - s.t_enq});
+      if (!fin) continue;
     }
-    e.record_lane(s, errors, now);
-    s.busy = false;
-    s.model.reset();
-    next_ = (next_ + 1) % SLOTS;
-    --inflight_;
+    int32_t st = fail ? (int32_t)ST_DEVICE_ERROR : en.pre;
+    const int32_t idx = fail ? 0 : r.idx;
+    const double p = fail ? 0.0 : r.p;
+    if (st == ST_OK && !std::isfinite(p)) st = ST_NONFINITE;
+    if (fail) e.healthy_.store(false);
+    errors += st != ST_OK;
+    if (en.model.get() != last || segs.empty()) {
+      segs.push_back(Seg{out.size(), en.model});
+      last = en.model.get();
+    }
+    const int64_t lat = now - en.t_enq;
+    out.push_back(Completion{en.tag, idx, st, p, lat});
+    const double us = (double)lat * 1e-3;
+    lat_sum += us;
+    int b = 0;
+    while (b < 23 && (double)(int64_t(1) << b) <= us) ++b;
+    lat_hist[b]++;
+    ++done;
+    en.model.reset();
+    en.tag = ~uint64_t(0);  // delivered
+    if (fail) en.rec = ~0u;  // a late record could still land in it: the slot is never reused
   }
-  return 0;
+  while (tail_ != head_ && ring_[tail_ % RING].tag == ~uint64_t(0) && ring_[tail_ % RING].rec != ~0u) ++tail_;
+  if (done > 0) {
+    std::lock_guard<std::mutex> lk(e.st_mu_);
+    e.stats_.requests += (uint64_t)done;
+    e.stats_.errors += (uint64_t)errors;
+    e.stats_.latency_sum_us += lat_sum;
+    for (int b = 0; b < 24; ++b) e.stats_.latency_hist[b] += lat_hist[b];
+  }
+  return (int)(head_ - tail_);
 }
 
-void Engine::record_lane(const Lane::LSlot& s, int errors, int64_t now) {
-  const double lat_us = (double)(now - s.t_enq) * 1e-3;
-  int lb = 0;
-  while (lb < 23 && (double)(int64_t(1) << lb) <= lat_us) ++lb;
-  int bb = 0;
-  while ((1 << (bb + 1)) <= s.n && bb < 11) ++bb;
-  std::lock_guard<std::mutex> lk(st_mu_);
-  stats_.requests += (uint64_t)s.n;
-  stats_.errors += (uint64_t)errors;
-  stats_.latency_sum_us += lat_us * s.n;
-  stats_.latency_hist[lb] += (uint64_t)s.n;
-  stats_.batches++;
-  stats_.batch_hist[bb]++;
-  stats_.lane_batches++;
-  if (!s.failed) {
+void Engine::combine_on_host(const std::shared_ptr<const Model>& m, LaneEntry** e, const double* X, const int32_t* nf,
+                             int n, uint32_t seq, int32_t status) {
+  size_t off = 0;
+  for (int i = 0; i < n; ++i) {
+    int32_t st = status, idx = 0;
+    double p = 0.0;
+    if (st == ST_OK) {
+      if (nf[i] != m->F)
+        st = ST_SHAPE;
+      else
+        cpu_linear_predict(*m, X + off, 1, &idx, &p);
+    }
+    off += (size_t)nf[i];
+    e[i]->pre = st;
+    e[i]->model = m;
+    ServeRecord* r = arena_h_ + e[i]->rec;
+    r->idx = idx;
+    r->p = p;
+    __atomic_store_n(&r->seq, seq, __ATOMIC_RELEASE);
+    e[i]->expect.store(seq, std::memory_order_release);
+  }
+}
+
+void Engine::combine() {
+  if (cq_n_.load(std::memory_order_acquire) == 0) return;
+  std::unique_lock<std::mutex> lk(launch_mu_, std::try_to_lock);
+  if (!lk.owns_lock()) return;  // the holder launches what is queued (it re-checks the queue)
+  const int64_t wd = (int64_t)cfg_.watchdog_ms * 1000000;
+  for (;;) {
+    // retire finished combined batches (done word = seq), or ones past the watchdog
+    const int64_t now = now_ns();
+    while (cin_n_ > 0) {
+      const CBatch& b = cin_[cin_head_];
+      const uint32_t d = __atomic_load_n(cdone_h_ + b.seq % CRING, __ATOMIC_ACQUIRE);
+      if (d != b.seq && !(wd > 0 && now - b.t_launch > wd)) break;
+      {
+        std::lock_guard<std::mutex> sl(st_mu_);
+        stats_.device_us_sum += (double)(now - b.t_launch) * 1e-3;
+      }
+      cin_head_ = (cin_head_ + 1) % CRING;
+      --cin_n_;
+    }
+    if (cin_n_ >= std::max(1, std::min(cfg_.lane_inflight, CRING / 2))) return;  // coalesce: the next batch takes them
+    const std::shared_ptr<const Model> m = model();
+    cx_.clear();
+    cnf_.clear();
+    ce_.clear();
+    {
+      std::lock_guard<std::mutex> ql(cq_mu_);
+      if (cq_e_.empty()) return;
+      // as many rows as one argument block holds
+      size_t take = cq_e_.size();
+      if (m && m->path == PATH_SMALL)
+        while (take > 1 && !linear_inline_fits(m->xdt, (int64_t)take, m->F, m->K)) take = take / 2;
+      take = std::min<size_t>(take, INLINE_MAX_ROWS);
+      size_t xoff = 0;
+      for (size_t i = 0; i < take; ++i) xoff += (size_t)cq_nf_[i];
+      cx_.assign(cq_x_.begin(), cq_x_.begin() + (ptrdiff_t)xoff);
+      cnf_.assign(cq_nf_.begin(), cq_nf_.begin() + (ptrdiff_t)take);
+      ce_.assign(cq_e_.begin(), cq_e_.begin() + (ptrdiff_t)take);
+      cq_x_.erase(cq_x_.begin(), cq_x_.begin() + (ptrdiff_t)xoff);
+      cq_nf_.erase(cq_nf_.begin(), cq_nf_.begin() + (ptrdiff_t)take);
+      cq_e_.erase(cq_e_.begin(), cq_e_.begin() + (ptrdiff_t)take);
+      cq_n_.store((int)cq_e_.size(), std::memory_order_release);
+    }
+    const int n = (int)ce_.size();
+    uint32_t seq = ++cseq_;
+    if (seq == 0) seq = ++cseq_;
+    if (!m || m->path != PATH_SMALL || !linear_inline_fits(m->xdt, n, m->F, m->K)) {
+      // the model changed under the queued rows (hot reload to a wide model, unload): answer them
+      // on the host - float64 oracle records, or ST_NO_MODEL
+      combine_on_host(m, ce_.data(), cx_.data(), cnf_.data(), n, seq, m ? ST_OK : ST_NO_MODEL);
+      continue;
+    }
+    InlineBatch& a = inline_;
+    a.out_idx = nullptr;
+    a.out_p = nullptr;
+    a.rec = arena_d_;
+    a.rec_scatter = 1;
+    a.done = cdone_d_ + seq % CRING;
+    a.seq = seq;
+    {
+      thread_local std::vector<const double*> rows;
+      thread_local std::vector<int32_t> st;
+      rows.assign((size_t)n, nullptr);
+      st.assign((size_t)n, ST_OK);
+      size_t off = 0;
+      for (int i = 0; i < n; ++i) {
+        rows[i] = cnf_[i] == m->F ? &cx_[off] : nullptr;
+        off += (size_t)cnf_[i];
+      }
+      fill_inline(a, *m, n, [&](int64_t i) -> const double* { return rows[i]; }, st.data());
+      for (int i = 0; i < n; ++i) {
+        a.rec_idx[i] = ce_[i]->rec;
+        ce_[i]->pre = st[i];
+        ce_[i]->model = m;
+        ce_[i]->expect.store(seq, std::memory_order_release);
+      }
+    }
+    const int64_t t_l = now_ns();
+    try {
+      TraceRange tr("mlapi.lane.launch");
+      direct_->launch(m->xdt, a);
+    } catch (const std::exception&) {
+      healthy_.store(false);
+      combine_on_host(m, ce_.data(), cx_.data(), cnf_.data(), n, seq, ST_DEVICE_ERROR);
+      continue;
+    }
+    cin_[(cin_head_ + cin_n_) % CRING] = CBatch{seq, t_l};
+    ++cin_n_;
+    double qw = 0;
+    for (int i = 0; i < n; ++i) qw += (double)(t_l - ce_[i]->t_enq);
+    int bb = 0;
+    while ((1 << (bb + 1)) <= n && bb < 11) ++bb;
+    std::lock_guard<std::mutex> sl(st_mu_);
+    stats_.batches++;
+    stats_.batch_hist[bb]++;
+    stats_.lane_batches++;
     stats_.path_batches[PATH_SMALL]++;
     stats_.inline_batches++;
     stats_.direct_batches++;
+    stats_.queue_wait_us_sum += qw * 1e-3;
   }
-  stats_.device_us_sum += (double)(now - s.t_launch) * 1e-3;
-  stats_.queue_wait_us_sum += (double)(s.t_launch - s.t_enq) * 1e-3 * s.n;
 }
 
 EngineStats Engine::stats() const {

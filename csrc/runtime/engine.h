@@ -57,9 +57,14 @@ enum Status : int32_t {
   ST_SHUTDOWN = 5,
 };
 
-enum RecMode : int { REC_ROWS = 1, REC_SPLITS = 2 };  // how a launched batch completes (Slot::rec_mode)
+// how a launched batch completes (Slot::rec_mode): per-row records, class-split records merged on
+// the host (linear_split), f64 class-block records merged on the host (linear_wide)
+enum RecMode : int { REC_ROWS = 1, REC_SPLITS = 2, REC_WIDE = 3 };
 
-enum ServePath : int32_t { PATH_SMALL = 0, PATH_GEMV = 1, PATH_GEMM = 2, PATH_GENERIC = 3, PATH_COUNT = 4 };
+// WIDE: linear_wide.h, f64 accumulation on the matrix cores for f64 / f32 storage, any F and K
+enum ServePath : int32_t {
+  PATH_SMALL = 0, PATH_GEMV = 1, PATH_GEMM = 2, PATH_GENERIC = 3, PATH_WIDE = 4, PATH_COUNT = 5
+};
 
 struct Model {
   int kind = KIND_MULTINOMIAL;
@@ -81,6 +86,9 @@ struct Model {
   size_t ws_bytes = 0;
   void* ws_split = nullptr;  // GEMM: linear_split workspace (small batches; every f32 batch)
   size_t ws_split_bytes = 0;
+  WidePlan wplan{};          // WIDE: the kernel's plan (class blocks, feature splits, padded width)
+  void* ws_wide = nullptr;   // WIDE: linear_wide workspace (zeroed once)
+  size_t ws_wide_bytes = 0;
   ~Model();
 };
 
@@ -94,54 +102,53 @@ struct Completion {
 
 class Engine;
 
-// Per-IO-thread dispatch lane (take the engine hop out of the request path).
-// An HTTP IO thread that parsed an epoll round's rows dispatches them itself - one AQL packet into
-// the engine's HSA queue (multi-producer: InlineDispatcher::launch's producer id), rows + W + b in
-// the kernel-argument block - and polls the batch's per-row completion records in its own event
-// loop, so a request never waits for the batcher thread (queue + futex wake) or the completer
-// thread (delivery + eventfd wake). SMALL-path models whose batch fits the argument block; the
-// engine queue remains the path for everything else (wide models, lane slots all busy, fault
-// injection, no direct dispatcher). One thread per lane.
+// Per-IO-thread lane (take the engine hop out of the request path). A lane is
+// a ring of result records that belongs to one HTTP IO thread. The thread that parsed an epoll
+// round's rows queues them with Lane::submit and then tries to become the engine's launcher
+// (flat combining: try-lock of the launch lock); whoever holds it dispatches EVERY queued row of
+// every lane as one kernel-argument batch - one AQL packet - whose kernel writes each row's
+// {seq, idx, p} record straight into its owner's ring (InlineBatch::rec_scatter). Each IO thread
+// polls its own ring in its event loop, so a request never waits for the batcher thread (queue +
+// futex wake) or the completer thread (delivery + eventfd wake). Coalescing is kept: one HSA queue
+// takes only ~0.7 M tiny dispatches/s (tools/dispatch_rate_probe.cpp), so at most
+// EngineConfig::lane_inflight combined batches are in flight and rows that arrive meanwhile ride
+// in the next one. SMALL-path models whose batch fits the argument block; everything else keeps
+// the engine queue. One thread per lane.
+struct LaneEntry {
+  std::atomic<uint32_t> expect{0};  // seq of the batch the row was launched in (0: still queued)
+  int32_t pre = 0;                  // status decided at launch (ST_SHAPE, ST_DEVICE_ERROR, ...)
+  uint32_t rec = 0;                 // arena index of the row's record
+  uint64_t tag = 0;
+  int64_t t_enq = 0;
+  std::shared_ptr<const Model> model;  // the batch's model (written by the launcher before expect)
+};
+
 class Lane {
  public:
-  ~Lane();
   Lane(const Lane&) = delete;
   Lane& operator=(const Lane&) = delete;
-  // Launch n rows (nf features each) from the calling thread. true = dispatched, completions come
-  // from poll(); false = not eligible now (the caller submits the rows to the engine queue).
+  // Queue n rows (nf features each) and try to launch. true = accepted (completions come from
+  // poll()); false = not eligible now (model not on the kernel-argument path, ring full, fault
+  // injection on): the caller submits them to the engine queue.
   bool submit(const double* X, int n, int nf, const uint64_t* tags);
   struct Seg {
-    size_t begin;  // first completion of the batch in poll()'s output
+    size_t begin;  // first completion of a run of one model in poll()'s output
     std::shared_ptr<const Model> model;
   };
-  // Appends the completions of finished batches (oldest first) to `out`, one Seg per batch, and
-  // returns the number of batches still in flight. Checks the watchdog and queue faults.
+  // Launches queued rows if the launcher is free, then appends the completions of this lane's
+  // finished rows to `out` (runs of one model in segs). Returns the rows still pending.
   int poll(std::vector<Completion>& out, std::vector<Seg>& segs);
-  int inflight() const { return inflight_; }
+  int inflight() const { return (int)(head_ - tail_); }
 
  private:
   friend class Engine;
-  explicit Lane(Engine* e, int producer);
-  struct LSlot {
-    ServeRecord* hrec = nullptr;
-    ServeRecord* drec = nullptr;
-    uint32_t seq = 0;
-    int n = 0;
-    int seen = 0;  // rows [0, seen) have their record
-    bool busy = false, failed = false;
-    int64_t t_enq = 0, t_launch = 0;
-    std::vector<uint64_t> tags;
-    std::vector<int32_t> pre;
-    std::shared_ptr<const Model> model;
-  };
-  static constexpr int SLOTS = 4;
+  Lane(Engine* e, uint32_t arena_base);
+  static constexpr uint32_t RING = 256;
   Engine* eng_;
-  int producer_;
-  int inflight_ = 0;
-  int next_ = 0;         // oldest busy slot (completion order = launch order)
-  uint32_t seq_base_;    // lane-distinct sequence numbers
-  LSlot slots_[SLOTS];
-  InlineBatch batch_;    // argument block under construction
+  uint32_t base_;             // first arena record of this lane
+  uint64_t head_ = 0, tail_ = 0;  // ring positions: [tail_, head_) pending
+  LaneEntry ring_[RING];
+  std::vector<LaneEntry*> ptrs_;  // submit scratch
 };
 
 class Sink {
@@ -157,9 +164,12 @@ struct EngineConfig {
   int max_wait_us = 0;    // 0 = continuous batching; >0 = also wait up to this long to fill a batch
   int slots = 4;          // batches in flight
   int dtype = DT_F64;     // SMALL-path compute dtype (f64 = bit parity with sklearn, or f32)
-  int wide_dtype = DT_F32;   // dtype of models too wide for the SMALL path: f32 -> GEMV (binary) /
-                             // f32 MFMA class-split kernel (multiclass, F <= 512); bf16 -> GEMV /
-                             // bf16 MFMA GEMM kernels; f64 (or f32 beyond F = 512) -> GENERIC
+  int wide_dtype = DT_F32;   // dtype of models too wide for the SMALL path: f64 -> WIDE (f64 storage,
+                             // f64 MFMA accumulation: the reference's precision, any F / K / kind);
+                             // f32 -> GEMV (binary, F <= 2048) or WIDE (f32 storage, f64
+                             // accumulation); bf16 -> GEMV / bf16 MFMA GEMM (F <= 4096), WIDE beyond
+  bool f32_split = false;    // f32 multiclass F <= 512: the f32-accumulating class-split kernel
+                             // (linear_split) instead of WIDE (measurement / A-B)
   int bar_rows = 32;         // wide paths: batches of at most this many rows are written straight into
                              // device HBM through the BAR (direct dispatch's HDP-flushed mapping) instead
                              // of being read by every wave over the host link (0 = off)
@@ -201,8 +211,9 @@ struct EngineConfig {
   // wake-ups (two futex hand-offs on a batch=1 request). SMALL-path models, batches of at most
   // this many rows; 0 = off. On the CPU backend the calling thread runs the float64 oracle.
   int idle_inline_rows = 8;
-  // IO threads dispatch SMALL-path batches themselves through lanes (open_lane); 0 = off
+  // IO threads queue SMALL-path rows on lanes and launch them by flat combining (open_lane); 0 = off
   int lanes = 1;
+  int lane_inflight = 3;  // combined lane batches in flight at most (the rest coalesce into the next)
 };
 
 struct EngineStats {
@@ -216,6 +227,7 @@ struct EngineStats {
   uint64_t direct_wide_batches = 0; // class-split (wide multiclass) batches dispatched into that queue
   uint64_t idle_batches = 0;        // batches run by the submitting thread (run_idle)
   uint64_t lane_batches = 0;        // batches dispatched by IO threads through lanes (Lane::submit)
+  uint64_t generic_models = 0;      // models loaded onto the scalar GENERIC kernel (a warning is logged)
   uint64_t bar_batches = 0;         // wide batches whose rows were written into HBM through the BAR
   bool direct_dispatch = false;     // the direct queue is up
   bool direct_device_kernargs = false;  // ... and its kernarg ring is in device memory
@@ -333,8 +345,11 @@ class Engine {
                const std::shared_ptr<const Model>& m, int64_t now);
   void record_batch(size_t n);
   friend class Lane;
-  // Lane batch bookkeeping (stats under st_mu_)
-  void record_lane(const Lane::LSlot& s, int errors, int64_t now);
+  // Flat-combining launcher of the lanes' queued rows (try-lock; no-op if another thread holds it)
+  void combine();
+  // rows of the combine queue that cannot run as a kernel-argument batch: host float64 records
+  void combine_on_host(const std::shared_ptr<const Model>& m, LaneEntry** e, const double* X, const int32_t* nf, int n,
+                       uint32_t seq, int32_t status);
   // Wait for a launched slot's done word (spin, then back off; fault and watchdog checks).
   void wait_done(Slot& s);
   // The launched slot's results -> idx / p (from the records or the output arrays).
@@ -376,6 +391,29 @@ class Engine {
   std::mutex lanes_mu_;
   std::vector<std::unique_ptr<Lane>> lanes_;
   std::vector<Lane*> free_lanes_;
+  static constexpr int MAX_LANES = 64;
+  ServeRecord* arena_h_ = nullptr;  // lanes' record rings [MAX_LANES][Lane::RING], host-mapped
+  ServeRecord* arena_d_ = nullptr;
+  // combine queue (rows of every lane waiting for the launcher)
+  std::mutex cq_mu_;
+  std::vector<double> cq_x_;
+  std::vector<int32_t> cq_nf_;
+  std::vector<LaneEntry*> cq_e_;
+  std::atomic<int> cq_n_{0};
+  // launcher state (guarded by launch_mu_): combined batches in flight, done words
+  static constexpr int CRING = 16;
+  uint32_t* cdone_h_ = nullptr;
+  uint32_t* cdone_d_ = nullptr;
+  uint32_t cseq_ = 0;
+  struct CBatch {
+    uint32_t seq;
+    int64_t t_launch;
+  };
+  CBatch cin_[CRING];
+  int cin_head_ = 0, cin_n_ = 0;
+  std::vector<double> cx_;  // launcher scratch: taken rows
+  std::vector<int32_t> cnf_;
+  std::vector<LaneEntry*> ce_;
 
   std::vector<std::thread> batchers_;
   std::vector<std::thread> completers_;

@@ -33,4 +33,32 @@ inline double merge_split_records(const SplitRecord* r, int ns, bool ovr, int32_
   return ovr ? (1.0 / (1.0 + std::exp(-M))) / S : 1.0 / S;
 }
 
+// Host class merge of linear_wide's per-block row states (WideRecOut): ncb blocks x 2 units of
+// one row, r[2 * cb] = {seq, argmax, m}, r[2 * cb + 1] = {seq, 0, s}, all f64, merged in block
+// order exactly as the kernel's in-kernel merge does (wide::wmerge).
+inline double merge_wide_records(const WideRecord* r, int ncb, bool ovr, int32_t* label) {
+  double M = -INFINITY, S = 0.0;
+  int bi = 0x7fffffff;
+  for (int b = 0; b < ncb; ++b) {
+    const double m = r[2 * b].x, s = r[2 * b + 1].x;
+    const int i = r[2 * b].v;
+    const bool take = (m > M) || (m == M && i < bi);
+    const double nm = take ? m : M;
+    if (ovr) {
+      S = S + s;
+    } else {
+      const double sa = M == -INFINITY ? 0.0 : S * std::exp(M - nm);
+      const double sb = m == -INFINITY ? 0.0 : s * std::exp(m - nm);
+      S = sa + sb;
+    }
+    if (take) {
+      M = m;
+      bi = i;
+    }
+    if (std::isnan(m)) M = m;  // a NaN state poisons the row (the kernel's merge does the same)
+  }
+  *label = bi;
+  return ovr ? (1.0 / (1.0 + std::exp(-M))) / S : 1.0 / S;
+}
+
 }  // namespace mlapi

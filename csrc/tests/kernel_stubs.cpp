@@ -4,6 +4,7 @@
 
 #include "mlapi/kernels.h"
 #include "../runtime/direct_dispatch.h"
+#include "../kernels/wide_plan.h"
 
 namespace mlapi {
 [[noreturn]] static void unreachable(const char* what) {
@@ -31,6 +32,12 @@ int linear_split_nsplit(int K) { return (K + 63) / 64; }
 void launch_linear_split(int, const void*, int64_t, const void*, const float*, int64_t, int, int, int, int32_t*, float*,
                          void*, size_t, hipStream_t, RecOut, SplitRecOut, KernelLauncher*) {
   unreachable("launch_linear_split");
+}
+WidePlan linear_wide_plan(int dt, int F, int K) { return wide_plan::plan(dt, F, K); }
+size_t linear_wide_workspace(int64_t B, int dt, int F, int K) { return wide_plan::workspace(B, dt, F, K); }
+void launch_linear_wide(int, const void*, int64_t, const void*, const double*, int64_t, int, int, int, int32_t*, double*,
+                        void*, size_t, hipStream_t, RecOut, WideRecOut, KernelLauncher*) {
+  unreachable("launch_linear_wide");
 }
 std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int, const std::string&, int, std::string* why, int) {
   if (why) *why = "host-only build";

@@ -34,6 +34,7 @@ SOURCES = [
     "kernels/gemv_binary.hip",
     "kernels/gemm_softmax.hip",
     "kernels/linear_split.hip",
+    "kernels/linear_wide.hip",
     "kernels/train.hip",
     "kernels/pack.hip",
     "kernels/shard.hip",

@@ -167,6 +167,45 @@ def linear_split(X, W, b, kind: int = Kind.MULTINOMIAL):
     return LinearSplit(X.shape[0], W.shape[0], X.device)(X, W, b, kind)
 
 
+class LinearWide:
+    """Wide-model predict with float64 accumulation on the matrix cores
+    (csrc/kernels/linear_wide.h, v_mfma_f64_16x16x4_f64): X, W stored as f64 or f32 (same
+    dtype), b f64; any F (zero-padded here to the plan's width), any K, every kind (binary kinds:
+    W is [1, F]). Returns (int32 label index, f64 p_max)."""
+
+    def __init__(self, max_batch: int, n_features: int, n_classes: int, dtype: torch.dtype, device):
+        self.dt = _DT[dtype]
+        self.plan = C().linear_wide_plan(self.dt, n_features, n_classes)
+        self.ws = torch.zeros(max(256, C().linear_wide_workspace(max_batch, self.dt, n_features, n_classes)),
+                              dtype=torch.uint8, device=device)
+
+    def __call__(self, X, W, b, kind: int = Kind.MULTINOMIAL, out=None):
+        _check(X, W, b)
+        if X.dtype not in (torch.float64, torch.float32) or W.dtype != X.dtype or b.dtype != torch.float64:
+            raise TypeError("linear_wide: X, W f64 or f32 (same dtype), b f64")
+        B, F = X.shape
+        K = W.shape[0]
+        if W.shape[1] != F or b.numel() != K:
+            raise ValueError("linear_wide: W must be [K, F] and b [K]")
+        ld = self.plan["ldx"]
+        if ld != F:
+            X = torch.nn.functional.pad(X, (0, ld - F)).contiguous()
+            W = torch.nn.functional.pad(W, (0, ld - F)).contiguous()
+        need = C().linear_wide_workspace(B, self.dt, F, K)
+        if need > self.ws.numel():
+            self.ws = torch.zeros(need, dtype=torch.uint8, device=X.device)
+        if out is None:
+            out = (torch.empty(B, dtype=torch.int32, device=X.device), torch.empty(B, dtype=torch.float64, device=X.device))
+        idx, p = out
+        C().linear_wide(self.dt, X.data_ptr(), ld, W.data_ptr(), b.data_ptr(), B, F, K, int(kind), idx.data_ptr(),
+                        p.data_ptr(), self.ws.data_ptr(), self.ws.numel(), _stream())
+        return idx, p
+
+
+def linear_wide(X, W, b, kind: int = Kind.MULTINOMIAL):
+    return LinearWide(X.shape[0], X.shape[1], W.shape[0], X.dtype, X.device)(X, W, b, kind)
+
+
 def gemm_softmax(X, W, b, kind: int = Kind.MULTINOMIAL):
     return GemmSoftmax(X.shape[0], W.shape[0], X.shape[1], X.device)(X, W, b, kind)
 

@@ -53,6 +53,7 @@ class Config:
     batchers: int = 1                         # batcher threads (queue take + launch; launches serialised)
     gemv_record_rows: int = 2                 # GEMV batches >= this many rows complete via records (0 = never)
     idle_inline_rows: int = 8                 # GPU: idle engine -> the IO thread launches <= this many rows itself (0 = off)
+    f32_split: bool = False                   # GPU: f32 multiclass F <= 512 on the f32-accumulating split kernel (A/B)
     lanes: int = 1                            # GPU: IO threads dispatch SMALL-model batches themselves (engine lanes; 0 = off)
     direct_dispatch: bool = True              # GPU: ... written as AQL packets into the engine's own HSA queue
     direct_wide: bool = True                  # GPU: class-split / record GEMV batches into that queue too ...

@@ -75,6 +75,10 @@ def render(engine_stats: Optional[dict] = None, server_stats: Optional[dict] = N
             out += ["# HELP mlapi_idle_path_batches_total Batches the submitting IO thread ran itself on an idle engine.",
                     "# TYPE mlapi_idle_path_batches_total counter"]
             _line(out, "mlapi_idle_path_batches_total", es["idle_batches"], labels)
+        if "generic_models" in es:
+            out += ["# HELP mlapi_generic_path_models Models loaded onto the scalar GENERIC kernel (no MFMA path for the shape).",
+                    "# TYPE mlapi_generic_path_models counter"]
+            _line(out, "mlapi_generic_path_models", es["generic_models"], labels)
         if "lane_batches" in es:
             out += ["# HELP mlapi_lane_batches_total Batches IO threads dispatched themselves through engine lanes.",
                     "# TYPE mlapi_lane_batches_total counter"]

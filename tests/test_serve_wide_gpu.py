@@ -68,11 +68,15 @@ def _engine(native, **kw):
     (512, 300, Kind.MULTINOMIAL, "bf16", "gemm"),
     (1024, 200, Kind.MULTINOMIAL, "bf16", "gemm"),  # row-group kernel (F looped in slices)
     (700, 30, Kind.OVR, "bf16", "gemm"),            # F padded to 1024
-    (48, 40, Kind.MULTINOMIAL, "f32", "gemm"),     # f32 MFMA class-split kernel, F padded to 64
-    (256, 1000, Kind.MULTINOMIAL, "f32", "gemm"),
-    (100, 10, Kind.OVR, "f32", "gemm"),
-    (700, 30, Kind.MULTINOMIAL, "f32", "generic"),  # f32 beyond F = 512
-    (48, 40, Kind.OVR, "f64", "generic"),
+    (48, 40, Kind.MULTINOMIAL, "f32", "wide"),     # f32 storage, f64 MFMA accumulation (linear_wide.h)
+    (256, 1000, Kind.MULTINOMIAL, "f32", "wide"),
+    (100, 10, Kind.OVR, "f32", "wide"),
+    (700, 30, Kind.MULTINOMIAL, "f32", "wide"),
+    (3000, 2, Kind.BINARY, "f32", "wide"),          # f32 binary beyond the GEMV's F = 2048
+    (48, 40, Kind.OVR, "f64", "wide"),
+    (256, 2, Kind.BINARY_SOFTMAX, "f64", "wide"),
+    (1024, 300, Kind.MULTINOMIAL, "f64", "wide"),   # feature splits over blocks
+    (5000, 20, Kind.MULTINOMIAL, "bf16", "wide"),   # beyond the bf16 kernels' F = 4096: f32 storage
 ])
 def test_engine_wide_paths_match_oracle(native, F, K, kind, wide, path, stage):
     m = LinearModel.random(F, K, seed=F + K, kind=kind)
@@ -83,29 +87,34 @@ def test_engine_wide_paths_match_oracle(native, F, K, kind, wide, path, stage):
         X = np.random.default_rng(F * K).standard_normal((3000, F))
         idx, p, st = e.predict(X)
         assert (st == 0).all()
-        check(m, X, idx, p, "f64" if path == "generic" and wide == "f64" else wide,
-              rtol=1e-12 if wide == "f64" else (1e-6 if wide == "f32" and path == "gemm" else 1e-4))
+        xdt = ("f32" if wide == "bf16" else wide) if path == "wide" else wide
+        # WIDE accumulates in f64: only the rounding of the stored inputs separates it from the oracle
+        check(m, X, idx, p, xdt, rtol=1e-11 if path == "wide" else 1e-4)
         s = e.stats()
         assert s["path_batches"][path] == s["batches"] and s["requests"] == 3000
     finally:
         e.stop()
 
 
-@pytest.mark.parametrize("wide", ["bf16", "f32"])
+@pytest.mark.parametrize("wide", ["bf16", "f32", "f32split"])
 def test_engine_small_multiclass_batches_take_split_kernel(native, wide):
-    """Serving-sized multiclass batches (1..32 rows) run the class-split kernel (linear_split.h)
-    with completion records; results match the oracle batch by batch."""
+    """Serving-sized multiclass batches (1..32 rows): bf16 and f32_split run the class-split kernel
+    (linear_split.h), f32 the f64-accumulating wide kernel (host-merged records up to 16 rows);
+    results match the oracle batch by batch."""
     F, K = 256, 1000
     m = LinearModel.random(F, K, seed=5, kind=Kind.MULTINOMIAL)
-    e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide])
+    e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide[:4] if wide != "bf16" else wide],
+                f32_split=wide == "f32split")
     try:
         e.load_model(int(m.kind), m.W, m.b, m.label_json())
+        assert e.model_path() == ("wide" if wide == "f32" else "gemm")
         rng = np.random.default_rng(9)
         for n in (1, 2, 5, 8, 16, 31, 32, 33):
             X = rng.standard_normal((n, F))
             idx, p, st = e.predict(X)
             assert (st == 0).all()
-            check(m, X, idx, p, wide, rtol=1e-6 if wide == "f32" else 1e-4)
+            check(m, X, idx, p, wide[:4] if wide != "bf16" else wide,
+                  rtol={"f32": 1e-11, "f32split": 1e-5, "bf16": 1e-4}[wide])
     finally:
         e.stop()
 
@@ -134,7 +143,7 @@ def test_bar_staged_rows_match_zero_copy(native, wide, K):
             e.stop()
     np.testing.assert_array_equal(outs[32][0], outs[0][0])
     np.testing.assert_array_equal(outs[32][1], outs[0][1])
-    check(m, X, outs[32][0], outs[32][1], wide, rtol=1e-6 if (wide == "f32" and K > 2) else 1e-4)
+    check(m, X, outs[32][0], outs[32][1], wide, rtol=1e-11 if (wide == "f32" and K > 2) else 1e-4)
 
 @pytest.mark.parametrize("wide", ["bf16", "f32"])
 @pytest.mark.parametrize("F,kind", [(256, Kind.BINARY), (64, Kind.BINARY_SOFTMAX), (1024, Kind.BINARY)])
@@ -195,7 +204,7 @@ def test_direct_dispatched_split_batches_match_hip_launch(native, wide, F, K, ki
             assert st["direct_dispatch"], "the serving code object did not load"
             if mode == "hip":
                 assert st["direct_wide_batches"] == 0
-            else:  # f32: every batch is class-split; bf16: beyond split_max_rows the tiles kernel
+            else:  # f32: every batch is the wide kernel; bf16: beyond split_max_rows the tiles kernel
                 assert st["direct_wide_batches"] > 0
                 assert wide != "f32" or st["direct_wide_batches"] == st["batches"]
             outs[mode] = (np.concatenate([r[0] for r in res]), np.concatenate([r[1] for r in res]))
@@ -208,7 +217,7 @@ def test_direct_dispatched_split_batches_match_hip_launch(native, wide, F, K, ki
         np.testing.assert_array_equal(outs[mode][0], outs["hip"][0])
         np.testing.assert_allclose(outs[mode][1], outs["hip"][1], rtol=1e-6, atol=0)
     check(m, np.concatenate(Xs), outs["direct"][0], outs["direct"][1], wide,
-          rtol=1e-6 if wide == "f32" else 1e-4)
+          rtol=1e-11 if wide == "f32" else 1e-4)
 
 
 
@@ -260,10 +269,10 @@ def test_native_server_wide_model_every_response(native, K, kind):
         got = [json.loads(b) for _, b in res]
         idx = np.array([int(g["prediction"][1:]) for g in got])
         p = np.array([g["probability"] for g in got])
-        # the default wide dtype is f32 (bf16 is opt-in): f32 GEMV / f32-MFMA class-split kernel
-        check(m, X, idx, p, "f32", rtol=1e-6 if K > 2 else 1e-5)
+        # the default wide dtype is f32 (bf16 is opt-in): f32 GEMV / f64-accumulating wide kernel
+        check(m, X, idx, p, "f32", rtol=1e-11 if K > 2 else 1e-5)
         st = srv.runtime.handle.stats()
-        path = "gemv" if K == 2 else "gemm"
+        path = "gemv" if K == 2 else "wide"
         assert st["path_batches"][path] >= 1 and st["path_batches"]["generic"] == 0
         assert st["batches"] < st["requests"]
         assert srv.http.stats()["fast"] >= 1024  # no request fell back to the Python slow path
@@ -311,4 +320,4 @@ def test_idle_engine_fast_path(native, F, K, kind):
         np.testing.assert_array_equal(idx, ridx)
         np.testing.assert_allclose(p, rp, rtol=1e-12, atol=0)
     else:
-        check(m, X, idx, p, "f32", rtol=1e-6 if K > 2 else 1e-5)
+        check(m, X, idx, p, "f32", rtol=1e-11 if K > 2 else 1e-5)
