@@ -395,6 +395,21 @@ def bench_gemm(args, info):
              "features": F, "parallelism": f"dp{info.world}"})
 
 
+def _replica_evidence(tr, info) -> dict:
+    """DP replicas after the timed steps: a 48-bit hash of every rank's parameters, all-gathered
+    (equal on every rank = bitwise-identical replicas), and the P2P exchange's start-up self-test."""
+    import hashlib
+
+    from mlapi_amd.parallel.comm import all_gather_floats
+
+    tr.check()
+    raw = tr.params.detach().cpu().numpy().tobytes()
+    h = float(int.from_bytes(hashlib.sha256(raw).digest()[:6], "little"))
+    hs = all_gather_floats([h], info)[:, 0]
+    return {"replicas_bitwise_equal": bool((hs == hs[0]).all()),
+            "p2p_selftest": info.__dict__.get("p2p_selftest", "n/a")}
+
+
 def bench_train(args, info):
     from mlapi_amd.train.sgd import BinarySGDTrainer, synthetic_binary
 
@@ -411,9 +426,10 @@ def bench_train(args, info):
     run(args.warmup)
     elapsed, _ = _timed(info, lambda: run(args.steps))
     value = info.world * args.train_batch * args.steps / elapsed
-    return ("train_samples_per_sec", value, "samples/s", elapsed,
-            {"final_loss": tr.last_loss(), "dp_exchange": tr.dp_exchange,
-             "launches_per_step": 2 if tr.dp_exchange in ("fused-p2p", "local") else 3},
+    extra = {"final_loss": tr.last_loss(), "dp_exchange": tr.dp_exchange,
+             "launches_per_step": 2 if tr.dp_exchange in ("fused-p2p", "local") else 3}
+    extra.update(_replica_evidence(tr, info))
+    return ("train_samples_per_sec", value, "samples/s", elapsed, extra,
             {"model": "binary LogisticRegression F=256 (mini-batch SGD)", "global_batch": args.train_batch * info.world,
              "seq_len": 1, "features": F, "parallelism": f"dp{info.world}"})
 
@@ -438,9 +454,11 @@ def bench_train_softmax(args, info):
     elapsed, _ = _timed(info, lambda: run(args.steps))
     value = info.world * B * args.steps / elapsed
     flops = 3 * 2 * B * K * tr.F_aug * info.world * args.steps / elapsed  # 2 logits passes + dW
-    return ("train_softmax_samples_per_sec", value, "samples/s", elapsed,
-            {"final_loss": tr.last_loss(), "tflops_incl_recompute": flops / 1e12, "dp_exchange": tr.dp_exchange,
-             "launches_per_step": 3 if tr.dp_exchange in ("fused-p2p", "local") else 4},
+    extra = {"final_loss": tr.last_loss(), "tflops_incl_recompute": flops / 1e12, "dp_exchange": tr.dp_exchange,
+             "launches_per_step": 3 if tr.dp_exchange in ("fused-p2p", "local") else 4,
+             "two_shot": os.environ.get("MLAPI_DP_TWO_SHOT", "auto")}
+    extra.update(_replica_evidence(tr, info))
+    return ("train_softmax_samples_per_sec", value, "samples/s", elapsed, extra,
             {"model": f"{K}-class softmax LogisticRegression F={F} (mini-batch SGD)", "global_batch": B * info.world,
              "seq_len": 1, "features": F, "classes": K, "parallelism": f"dp{info.world}"})
 

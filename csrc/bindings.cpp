@@ -618,6 +618,10 @@ PYBIND11_MODULE(_C, m) {
            py::arg("buf"), py::arg("count"), py::arg("dtype"), py::arg("stream"), py::arg("timeout_ms") = 60000,
            py::call_guard<py::gil_scoped_release>())
       .def("status", &P2PAllReduce::status, py::call_guard<py::gil_scoped_release>())
+      .def("status_now", &P2PAllReduce::status_now)
+      .def("selftest_write", &P2PAllReduce::selftest_write, py::arg("corrupt") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("selftest_verify", &P2PAllReduce::selftest_verify, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("epoch", &P2PAllReduce::epoch)
       .def_property_readonly("max_bytes", &P2PAllReduce::max_bytes);
 

@@ -42,7 +42,15 @@ struct P2PBlockArgs {
   const float* peer[MAX_RANKS] = {};              // every rank's same half (peer[rank] == mine)
   uint32_t* peer_bflags[MAX_RANKS] = {};          // every rank's block-flag array
   const uint32_t* my_bflags = nullptr;
-  uint32_t* status = nullptr;                     // sticky: 1 = a peer did not arrive in time
+  // Two-shot exchange (large buffers, many ranks): block b's columns are reduced and updated by
+  // rank b % world only (reads N-1 peer slices of 1/N of the columns), which publishes the result
+  // into `mine + pub_off` and raises its phase-2 flag; the other ranks copy that one slice. Per
+  // rank 2 (N-1) / N of the buffer cross xGMI instead of (N-1) x.
+  uint32_t* peer_bflags2[MAX_RANKS] = {};         // every rank's phase-2 flag array
+  const uint32_t* my_bflags2 = nullptr;
+  int64_t pub_off = 0;                            // floats from `mine` / `peer[r]` to the published result
+  int two_shot = 0;
+  uint32_t* status = nullptr;                     // sticky: 1 = a peer did not arrive in time (host-mapped)
   int rank = 0, world = 1;
   uint32_t epoch = 0;
   uint64_t timeout_ticks = 0;                     // wall_clock64() ticks (100 MHz)
@@ -69,10 +77,21 @@ class P2PAllReduce {
   void all_reduce(void* buf, size_t count, int dtype, hipStream_t stream, int timeout_ms);
   // 0 = every call so far completed; 1 = a call timed out waiting for a peer (sticky). Syncs.
   int status();
+  // The same word as the kernels have published it so far, without synchronising (it lives in
+  // host-mapped memory): trainers check it every step and stop at the first missed exchange
+  // instead of running on with partly updated replicas.
+  int status_now() const;
+  // Start-up self-check of the IPC mappings (every rank, between the two calls a host barrier):
+  // selftest_write stores a rank-tagged pattern into this rank's buffer (corrupt != 0: a wrong one,
+  // for tests); selftest_verify reads every peer's pattern through the mappings with the same
+  // uncached / system-scope loads the exchange uses and returns the number of wrong words.
+  void selftest_write(int corrupt);
+  int selftest_verify();
   // One fused exchange for a kernel of `nblocks` blocks whose slices total `bytes` (advances the
   // epoch; every rank must issue the same sequence of calls).
   P2PBlockArgs block_exchange(size_t bytes, int nblocks, int timeout_ms);
   uint32_t epoch() const { return epoch_; }
+  int world() const { return world_; }
   size_t max_bytes() const { return max_bytes_; }
 
  private:
@@ -80,7 +99,10 @@ class P2PAllReduce {
   size_t max_bytes_;
   void* data_ = nullptr;        // 2 halves of max_bytes (uncached, IPC-exported)
   uint32_t* flags_ = nullptr;   // FLAG_WORDS_ALLREDUCE epoch words + block flags (uncached, IPC-exported)
-  uint32_t* status_ = nullptr;  // device word
+  uint32_t* status_ = nullptr;   // host-mapped word (status_d_ on the device)
+  uint32_t* status_d_ = nullptr;
+  uint32_t* selftest_h_ = nullptr;  // host-mapped mismatch counter of selftest_verify
+  uint32_t* selftest_d_ = nullptr;
   void* peer_data_[MAX_RANKS] = {};
   uint32_t* peer_flags_[MAX_RANKS] = {};
   bool opened_[MAX_RANKS] = {};
@@ -89,7 +111,9 @@ class P2PAllReduce {
 
  public:
   static constexpr size_t FLAG_WORDS_ALLREDUCE = 64;  // all_reduce(): one word per source rank
-  static constexpr size_t FLAG_BYTES = (FLAG_WORDS_ALLREDUCE + (size_t)MAX_RANKS * MAX_FLAG_BLOCKS) * 4;
+  // [all-reduce epoch words][phase-1 block flags][phase-2 block flags]
+  static constexpr size_t FLAG_BYTES = (FLAG_WORDS_ALLREDUCE + 2 * (size_t)MAX_RANKS * MAX_FLAG_BLOCKS) * 4;
+  static constexpr int SELFTEST_WORDS = 4096;
 };
 
 }  // namespace mlapi

@@ -1,6 +1,7 @@
 // One-shot P2P all-reduce over IPC-mapped peer buffers; protocol in p2p.h.
 #include "p2p.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -57,7 +58,7 @@ __device__ bool p2p_barrier(const P2PArgs& a) {
 // float32: float4 per thread and step, peers summed in rank order (identical on every rank).
 __global__ __launch_bounds__(THREADS) void p2p_allreduce_f32(P2PArgs a) {
   if (!p2p_barrier(a)) {
-    if (threadIdx.x == 0) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
   float* out = static_cast<float*>(a.out);
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(THREADS) void p2p_allreduce_f32(P2PArgs a) {
 // bfloat16: 8 elements (16 B) per thread and step, fp32 accumulation, one rounding at the end.
 __global__ __launch_bounds__(THREADS) void p2p_allreduce_bf16(P2PArgs a) {
   if (!p2p_barrier(a)) {
-    if (threadIdx.x == 0) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
   }
   uint16_t* out = static_cast<uint16_t*>(a.out);
@@ -124,6 +125,32 @@ __global__ __launch_bounds__(THREADS) void p2p_allreduce_bf16(P2PArgs a) {
   }
 }
 
+// Self-test: a rank-tagged pattern (exact in f32) into this rank's half 0, and a check of every
+// peer's pattern with the exchange's own load path (uncached buffer, system-scope acquire).
+__device__ __forceinline__ float selftest_word(int rank, int i) { return (float)(rank * 8192 + (i ^ 0x5a5)); }
+
+__global__ __launch_bounds__(THREADS) void p2p_selftest_write(float* mine, int rank, int corrupt, int nwords) {
+  for (int i = blockIdx.x * THREADS + threadIdx.x; i < nwords; i += gridDim.x * THREADS)
+    mine[i] = selftest_word(rank, i) + (corrupt && i == 77 ? 1.0f : 0.0f);
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+struct SelftestArgs {
+  const float* peer[P2PAllReduce::MAX_RANKS];
+  uint32_t* bad;
+  int world, nwords;
+};
+
+__global__ __launch_bounds__(THREADS) void p2p_selftest_verify(SelftestArgs a) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  uint32_t bad = 0;
+  for (int r = 0; r < a.world; ++r)
+    for (int i = blockIdx.x * THREADS + threadIdx.x; i < a.nwords; i += gridDim.x * THREADS)
+      bad += __hip_atomic_load(a.peer[r] + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != selftest_word(r, i);
+  if (bad) __hip_atomic_fetch_add(a.bad, bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
 
 P2PAllReduce::P2PAllReduce(int rank, int world, int device, size_t max_bytes)
@@ -135,10 +162,14 @@ P2PAllReduce::P2PAllReduce(int rank, int world, int device, size_t max_bytes)
   // Uncached: stores go to HBM, so a peer GPU reading over xGMI never sees a stale L2 line.
   MLAPI_HIP_CHECK(hipExtMallocWithFlags(&data_, 2 * max_bytes_, hipDeviceMallocUncached));
   MLAPI_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), FLAG_BYTES, hipDeviceMallocUncached));
-  MLAPI_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&status_), sizeof(uint32_t)));
+  MLAPI_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&status_), 64, hipHostMallocMapped | hipHostMallocCoherent));
+  MLAPI_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&status_d_), status_, 0));
+  MLAPI_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&selftest_h_), 64, hipHostMallocMapped | hipHostMallocCoherent));
+  MLAPI_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&selftest_d_), selftest_h_, 0));
+  std::memset(status_, 0, 64);
+  std::memset(selftest_h_, 0, 64);
   MLAPI_HIP_CHECK(hipMemset(data_, 0, 2 * max_bytes_));
   MLAPI_HIP_CHECK(hipMemset(flags_, 0, FLAG_BYTES));
-  MLAPI_HIP_CHECK(hipMemset(status_, 0, sizeof(uint32_t)));
   MLAPI_HIP_CHECK(hipDeviceSynchronize());
   peer_data_[rank] = data_;
   peer_flags_[rank] = flags_;
@@ -155,7 +186,33 @@ P2PAllReduce::~P2PAllReduce() {
   }
   (void)hipFree(data_);
   (void)hipFree(flags_);
-  (void)hipFree(status_);
+  (void)hipHostFree(status_);
+  (void)hipHostFree(selftest_h_);
+}
+
+int P2PAllReduce::status_now() const { return (int)__atomic_load_n(status_, __ATOMIC_ACQUIRE); }
+
+void P2PAllReduce::selftest_write(int corrupt) {
+  MLAPI_HIP_CHECK(hipSetDevice(device_));
+  const int nw = (int)std::min<size_t>(SELFTEST_WORDS, max_bytes_ / sizeof(float));
+  hipLaunchKernelGGL(p2p_selftest_write, dim3(4), dim3(THREADS), 0, 0, static_cast<float*>(data_), rank_, corrupt, nw);
+  MLAPI_HIP_CHECK(hipGetLastError());
+  MLAPI_HIP_CHECK(hipDeviceSynchronize());
+}
+
+int P2PAllReduce::selftest_verify() {
+  if (!ready_) throw std::runtime_error("P2PAllReduce: open_peers() first");
+  MLAPI_HIP_CHECK(hipSetDevice(device_));
+  SelftestArgs a{};
+  for (int j = 0; j < world_; ++j) a.peer[j] = static_cast<const float*>(peer_data_[j]);
+  a.bad = selftest_d_;
+  a.world = world_;
+  a.nwords = (int)std::min<size_t>(SELFTEST_WORDS, max_bytes_ / sizeof(float));
+  __atomic_store_n(selftest_h_, 0u, __ATOMIC_RELEASE);
+  hipLaunchKernelGGL(p2p_selftest_verify, dim3(4), dim3(THREADS), 0, 0, a);
+  MLAPI_HIP_CHECK(hipGetLastError());
+  MLAPI_HIP_CHECK(hipDeviceSynchronize());
+  return (int)__atomic_load_n(selftest_h_, __ATOMIC_ACQUIRE);
 }
 
 static std::string export_handle(void* p) {
@@ -208,7 +265,7 @@ void P2PAllReduce::all_reduce(void* buf, size_t count, int dtype, hipStream_t st
     a.peer_flags[j] = peer_flags_[j];
   }
   a.my_flags = flags_;
-  a.status = status_;
+  a.status = status_d_;
   a.out = buf;
   a.n = (int64_t)count;
   a.rank = rank_;
@@ -237,7 +294,9 @@ P2PBlockArgs P2PAllReduce::block_exchange(size_t bytes, int nblocks, int timeout
     a.peer_bflags[j] = peer_flags_[j] + FLAG_WORDS_ALLREDUCE;
   }
   a.my_bflags = flags_ + FLAG_WORDS_ALLREDUCE;
-  a.status = status_;
+  for (int j = 0; j < world_; ++j) a.peer_bflags2[j] = peer_flags_[j] + FLAG_WORDS_ALLREDUCE + (size_t)MAX_RANKS * MAX_FLAG_BLOCKS;
+  a.my_bflags2 = flags_ + FLAG_WORDS_ALLREDUCE + (size_t)MAX_RANKS * MAX_FLAG_BLOCKS;
+  a.status = status_d_;
   a.rank = rank_;
   a.world = world_;
   a.epoch = epoch_;
@@ -253,9 +312,7 @@ P2PBlockArgs P2PAllReduce::block_exchange(size_t bytes, int nblocks, int timeout
 int P2PAllReduce::status() {
   MLAPI_HIP_CHECK(hipSetDevice(device_));
   MLAPI_HIP_CHECK(hipDeviceSynchronize());
-  uint32_t s = 0;
-  MLAPI_HIP_CHECK(hipMemcpy(&s, status_, sizeof s, hipMemcpyDeviceToHost));
-  return (int)s;
+  return status_now();
 }
 
 }  // namespace mlapi

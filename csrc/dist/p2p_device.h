@@ -23,28 +23,36 @@
 
 namespace mlapi {
 
-__device__ inline bool p2p_block_sync(const P2PBlockArgs& a, int block) {
-  __shared__ int p2p_ok;
-  // Every thread's slice stores acknowledged. The exchange buffer is uncached (fine-grained UC):
-  // an acknowledged store is in memory, where peers read it, so no L2 write-back (a system-scope
-  // release = buffer_wbl2 of the whole XCD L2, per wave) is needed before the flag store.
-  // P2P_RELEASE_FENCE (mode bit 0) restores the fenced protocol for A/B measurements.
+// Publish this block's slice: every thread's stores acknowledged (the exchange buffer is uncached
+// fine-grained memory: an acknowledged store is in memory, where peers read it, so no L2
+// write-back is needed before the flag store; P2P_RELEASE_FENCE, mode bit 0, restores the fenced
+// protocol for A/B measurements), then one thread per rank stores the epoch into that rank's flag
+// word for (block, this rank). phase2: the two-shot result flags instead.
+__device__ inline void p2p_block_publish(const P2PBlockArgs& a, int block, bool phase2 = false) {
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (a.mode & 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if ((int)threadIdx.x < a.world) {
-    uint32_t* f = a.peer_bflags[threadIdx.x] + (size_t)block * P2PBlockArgs::MAX_RANKS + a.rank;
+    uint32_t* f = (phase2 ? a.peer_bflags2 : a.peer_bflags)[threadIdx.x] + (size_t)block * P2PBlockArgs::MAX_RANKS + a.rank;
     if (a.mode & 1)
       __hip_atomic_store(f, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     else
       __hip_atomic_store(f, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// Wait until every rank's flag for `block` (only_rank >= 0: that rank's) reached the epoch, with a
+// bounded spin (timeout: sticky status word, false), then a system-scope acquire so the peer reads
+// that follow see this epoch's slices. Every thread of the block calls it.
+__device__ inline bool p2p_block_wait(const P2PBlockArgs& a, int block, int only_rank = -1, bool phase2 = false) {
+  __shared__ int p2p_ok;
   if (threadIdx.x == 0) p2p_ok = 1;
   __syncthreads();
-  if ((int)threadIdx.x < a.world) {
+  const int r = only_rank >= 0 ? only_rank : (int)threadIdx.x;
+  if (only_rank >= 0 ? threadIdx.x == 0 : (int)threadIdx.x < a.world) {
     // poll with system-coherent relaxed loads (each acquire load would invalidate the L2 again);
     // one acquire fence after the loop orders the peer reads
-    const uint32_t* f = a.my_bflags + (size_t)block * P2PBlockArgs::MAX_RANKS + threadIdx.x;
+    const uint32_t* f = (phase2 ? a.my_bflags2 : a.my_bflags) + (size_t)block * P2PBlockArgs::MAX_RANKS + r;
     const uint64_t t0 = wall_clock64();
     for (;;) {
       const uint32_t v = (a.mode & 2) ? __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)
@@ -52,7 +60,7 @@ __device__ inline bool p2p_block_sync(const P2PBlockArgs& a, int block) {
       if ((int32_t)(v - a.epoch) >= 0) break;
       if (wall_clock64() - t0 > a.timeout_ticks) {
         p2p_ok = 0;
-        __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -63,6 +71,11 @@ __device__ inline bool p2p_block_sync(const P2PBlockArgs& a, int block) {
   // cacheable on this GPU) so the reads below see this epoch's slices
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   return p2p_ok != 0;
+}
+
+__device__ inline bool p2p_block_sync(const P2PBlockArgs& a, int block) {
+  p2p_block_publish(a, block);
+  return p2p_block_wait(a, block);
 }
 
 }  // namespace mlapi

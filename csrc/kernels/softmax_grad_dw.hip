@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -592,6 +593,80 @@ __global__ __launch_bounds__(256) void gdw_reduce_kernel(const f32x4_t* __restri
       s += __builtin_nontemporal_load(slabs + (int64_t)i * width4 + j);
     }
   }
+  // fused SGD update of the 4 parameters of column j from the reduced gradient s (sgd_update_2d's
+  // arithmetic); np / nm: the new parameters and momenta (published by two-shot owners)
+  auto update = [&](const f32x4_t& g, f32x4_t& np, f32x4_t& nm) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t e = 4 * (int64_t)j + q;
+      const int64_t row = e / upd.cols;
+      const int c = (int)(e - row * upd.cols);
+      float d = g[q] * upd.inv_n + (c < upd.pen_cols ? upd.l2 * upd.params[e] : 0.f);
+      if (upd.mom != nullptr) {
+        const float v = upd.momentum * upd.mom[e] + d;
+        upd.mom[e] = v;
+        nm[q] = v;
+        d = v;
+      }
+      np[q] = upd.params[e] - upd.lr * d;
+    }
+  };
+  // the new parameters (and momenta) of column j into the replica + its shadow copies
+  auto store_params = [&](const f32x4_t& np, const f32x4_t* nm) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t e = 4 * (int64_t)j + q;
+      const int64_t row = e / upd.cols;
+      const int c = (int)(e - row * upd.cols);
+      upd.params[e] = np[q];
+      if (nm != nullptr && upd.mom != nullptr) upd.mom[e] = (*nm)[q];
+      if (upd.shadow_w != nullptr && c < upd.pen_cols)
+        upd.shadow_w[row * upd.pen_cols + c] = __builtin_bit_cast(uint16_t, (__bf16)np[q]);
+      if (upd.shadow_b != nullptr && c == upd.pen_cols) upd.shadow_b[row] = np[q];
+    }
+  };
+  if (DP && dp.world > 1 && dp.two_shot) {
+    // two-shot: rank (b % world) reduces and updates these columns, the others copy its result
+    f32x4_t* mine = reinterpret_cast<f32x4_t*>(dp.mine);
+    if (active) mine[j] = s;
+    const int owner = (int)(blockIdx.x % (unsigned)dp.world);
+    p2p_block_publish(dp, blockIdx.x);
+    if (dp.rank == owner) {
+      if (!p2p_block_wait(dp, blockIdx.x)) return;  // peer missing: status recorded, no update
+      if (active) {
+        const f32x4_t own = s;
+        s = dp.rank == 0 ? own : reinterpret_cast<const f32x4_t*>(dp.peer[0])[j];
+        for (int r = 1; r < dp.world; ++r) s += r == dp.rank ? own : reinterpret_cast<const f32x4_t*>(dp.peer[r])[j];
+        out[j] = s;
+        f32x4_t* pub = reinterpret_cast<f32x4_t*>(dp.mine + dp.pub_off);  // [grad | params | momenta]
+        pub[j] = s;
+        if (upd.params != nullptr) {
+          f32x4_t np = {0.f, 0.f, 0.f, 0.f}, nm = {0.f, 0.f, 0.f, 0.f};
+          update(s, np, nm);
+          store_params(np, nullptr);
+          pub[width4 + j] = np;
+          if (upd.mom != nullptr) pub[2 * (int64_t)width4 + j] = nm;
+        }
+      }
+      p2p_block_publish(dp, blockIdx.x, true);
+    } else {
+      if (!p2p_block_wait(dp, blockIdx.x, owner, true)) return;
+      if (active) {
+        const f32x4_t* pub = reinterpret_cast<const f32x4_t*>(dp.peer[owner] + dp.pub_off);
+        out[j] = pub[j];
+        if (upd.params != nullptr) {
+          const f32x4_t np = pub[width4 + j];
+          if (upd.mom != nullptr) {
+            const f32x4_t nm = pub[2 * (int64_t)width4 + j];
+            store_params(np, &nm);
+          } else {
+            store_params(np, nullptr);
+          }
+        }
+      }
+    }
+    return;
+  }
   if (DP && dp.world > 1) {
     if (active) reinterpret_cast<f32x4_t*>(dp.mine)[j] = s;
     if (!p2p_block_sync(dp, blockIdx.x)) return;  // peer missing: status recorded, no update
@@ -604,24 +679,31 @@ __global__ __launch_bounds__(256) void gdw_reduce_kernel(const f32x4_t* __restri
   if (!active) return;
   out[j] = s;
   if (upd.params != nullptr) {  // uniform: the fused SGD update of these 4 parameters
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t e = 4 * (int64_t)j + q;
-      const int64_t row = e / upd.cols;
-      const int c = (int)(e - row * upd.cols);
-      float d = s[q] * upd.inv_n + (c < upd.pen_cols ? upd.l2 * upd.params[e] : 0.f);
-      if (upd.mom != nullptr) {
-        const float v = upd.momentum * upd.mom[e] + d;
-        upd.mom[e] = v;
-        d = v;
-      }
-      const float np = upd.params[e] - upd.lr * d;
-      upd.params[e] = np;
-      if (upd.shadow_w != nullptr && c < upd.pen_cols)
-        upd.shadow_w[row * upd.pen_cols + c] = __builtin_bit_cast(uint16_t, (__bf16)np);
-      if (upd.shadow_b != nullptr && c == upd.pen_cols) upd.shadow_b[row] = np;
-    }
+    f32x4_t np = {0.f, 0.f, 0.f, 0.f}, nm = {0.f, 0.f, 0.f, 0.f};
+    update(s, np, nm);
+    store_params(np, nullptr);
   }
+}
+
+// The block exchange of one gradient reduce: one-shot (every rank reads every peer's slice) or,
+// for large buffers over many ranks, two-shot (P2PBlockArgs). MLAPI_DP_TWO_SHOT: 1 on, 0 off,
+// default auto = world >= 4 and a gradient of >= 64 KiB; it needs the exchange buffer to hold the
+// published [grad | params | momenta] behind the gradient slice (else one-shot).
+P2PBlockArgs gdw_exchange(P2PAllReduce* dp, int width4, int nblocks, int timeout_ms, const Sgd2D* update) {
+  const size_t grad_bytes = ((size_t)width4 * 4 + 4) * sizeof(float);
+  const int64_t pub_off = ((int64_t)width4 * 4 + 4 + 3) / 4 * 4;  // floats; 16-byte aligned
+  const bool mom = update != nullptr && update->mom != nullptr;
+  const size_t two_bytes = (size_t)(pub_off + (int64_t)(mom ? 3 : 2) * width4 * 4) * sizeof(float);
+  static const int mode = [] {
+    const char* e = getenv("MLAPI_DP_TWO_SHOT");
+    return e ? atoi(e) : -1;
+  }();
+  bool two = dp->world() > 1 && (mode == 1 || (mode < 0 && dp->world() >= 4 && grad_bytes >= (64u << 10)));
+  if (two && two_bytes > dp->max_bytes()) two = false;
+  P2PBlockArgs a = dp->block_exchange(two ? two_bytes : grad_bytes, nblocks, timeout_ms);
+  a.two_shot = two ? 1 : 0;
+  a.pub_off = pub_off;
+  return a;
 }
 
 }  // namespace
@@ -635,7 +717,7 @@ void launch_gdw_reduce(const float* slabs, int nslabs, int K, int F_aug, float* 
   const int width4 = K * F_aug / 4;
   const int nblocks = (width4 + 255) / 256 + 1;
   if (dp != nullptr) {
-    const P2PBlockArgs a = dp->block_exchange(((size_t)width4 * 4 + 4) * sizeof(float), nblocks, dp_timeout_ms);
+    const P2PBlockArgs a = gdw_exchange(dp, width4, nblocks, dp_timeout_ms, update);
     hipLaunchKernelGGL(gdw_reduce_kernel<true>, dim3((unsigned)nblocks), dim3(256), 0, stream,
                        reinterpret_cast<const f32x4_t*>(slabs), nslabs, width4, reinterpret_cast<f32x4_t*>(dW_out),
                        stat_slabs, nstat, stats_out, update != nullptr ? *update : Sgd2D{}, a);
@@ -773,7 +855,7 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
     const int width4 = K * (F + 8) / 4;
     const int nblocks = (width4 + 255) / 256 + 1;
     if (dp != nullptr) {
-      const P2PBlockArgs a = dp->block_exchange(((size_t)width4 * 4 + 4) * sizeof(float), nblocks, dp_timeout_ms);
+      const P2PBlockArgs a = gdw_exchange(dp, width4, nblocks, dp_timeout_ms, update);
       hipLaunchKernelGGL(gdw_reduce_kernel<true>, dim3((unsigned)nblocks), dim3(256), 0, stream,
                          reinterpret_cast<const f32x4_t*>(args.dw_slabs), L.row_groups, width4,
                          reinterpret_cast<f32x4_t*>(dW_out), args.stat_slabs, L.row_groups * L.class_groups, stats_out,

@@ -74,37 +74,90 @@ class P2PAllReduce:
         if self.status() != 0:
             raise RuntimeError("P2PAllReduce: a peer did not arrive within the timeout")
 
+    def status_now(self) -> int:
+        """The sticky status word as the kernels have published it so far (host-mapped: no sync)."""
+        return int(self._p.status_now())
+
+    def check_now(self) -> None:
+        """Raise at the first exchange a peer missed, without synchronising: a timed-out block skips
+        its update while the others apply theirs, so the replicas are no longer identical and the
+        step loop must stop (restore from the last checkpoint)."""
+        if self._p.status_now() != 0:
+            raise RuntimeError("P2P exchange: a peer did not arrive within the timeout; replicas may "
+                               "have diverged in the last step (restore from a checkpoint)")
+
+    def selftest(self, store=None, generation="", timeout_s: float = 120.0) -> int:
+        """Start-up check that the IPC mappings carry data between these ranks: every rank writes a
+        rank-tagged pattern into its buffer, a store barrier, then every rank reads every peer's
+        pattern through the exchange's own load path. Returns this rank's count of wrong words
+        (0 = ok). ``MLAPI_P2P_SELFTEST_CORRUPT=<rank>`` makes that rank write a wrong word (tests)."""
+        import os
+
+        corrupt = int(os.environ.get("MLAPI_P2P_SELFTEST_CORRUPT", "-1")) == self.rank
+        self._p.selftest_write(1 if corrupt else 0)
+        if self.world > 1:
+            if store is None:
+                from mlapi_amd.parallel.rccl import default_store
+
+                store = default_store()
+            key = f"mlapi/p2p-selftest/{generation}/{{}}"
+            store.set(key.format(self.rank), "1")
+            store.wait([key.format(r) for r in range(self.world)], datetime.timedelta(seconds=timeout_s))
+        return int(self._p.selftest_verify())
+
 
 def dp_exchange(info, nbytes: int) -> Optional[P2PAllReduce]:
     """The rank's exchange for fused DP training steps (gradient reduction + all-reduce + update in
     one kernel, csrc/dist/p2p_device.h), or None when it does not apply: CPU ranks, ranks spread over
-    several hosts (IPC peers must share a host), or ``MLAPI_DP_FUSED=0``. One replica (world = 1)
-    gets one too, so the N = 1 step runs the same kernels as the N > 1 step. Collective: every rank
-    calls it with the same ``nbytes``. Reuses the communicator's P2P buffers when they are big
-    enough; otherwise a dedicated exchange is set up (its own store keys, ``dp<N>`` generation).
+    several hosts (IPC peers must share a host), ``MLAPI_DP_FUSED=0``, and one replica (world = 1:
+    the trainers' local step is the same kernels without the exchange arguments, so N = 1 pays
+    nothing for DP). Collective: every rank calls it with the same ``nbytes``. Reuses the
+    communicator's P2P buffers when they are big enough; otherwise a dedicated exchange is set up
+    (its own store keys, ``dp<N>`` generation). A new exchange is self-tested first
+    (:meth:`P2PAllReduce.selftest`, max over ranks): if any rank reads a wrong word through the IPC
+    mappings, every rank gets None and the step uses the RCCL all-reduce instead
+    (``info.p2p_selftest`` = "ok" / "failed").
     """
     import os
 
-    if info.device is None or os.environ.get("MLAPI_DP_FUSED", "1") == "0":
+    if info.device is None or os.environ.get("MLAPI_DP_FUSED", "1") == "0" or info.world == 1:
         return None
     if info.world > 1 and getattr(info, "local_world", info.world) != info.world:
         return None
     comm_p2p = getattr(info.comm, "p2p", None)
     if isinstance(comm_p2p, P2PAllReduce) and comm_p2p.max_bytes >= nbytes:
-        return comm_p2p
+        return comm_p2p if _selftested(comm_p2p, info, None, "comm") else None
     cache = info.__dict__.setdefault("_dp_exchanges", [])
     for ex in cache:
         if ex.max_bytes >= nbytes:
             return ex
-    store = None
-    if info.world > 1:
-        from mlapi_amd.parallel.rccl import default_store
+    from mlapi_amd.parallel.rccl import default_store
 
-        store = default_store()
+    store = default_store()
+    gen = f"dp{len(cache)}"
     ex = P2PAllReduce(info.rank, info.world, info.device, store=store, max_bytes=max(nbytes, 4096),
-                      generation=f"dp{len(cache)}")
+                      generation=gen)
+    if not _selftested(ex, info, store, gen):
+        return None
     cache.append(ex)
     return ex
+
+
+def _selftested(ex: P2PAllReduce, info, store, gen: str) -> bool:
+    """Run the exchange's start-up self-test once (collective) and record the verdict."""
+    if getattr(ex, "_selftest_ok", None) is None:
+        from mlapi_amd.parallel.comm import all_reduce_max
+
+        worst = all_reduce_max(float(ex.selftest(store=store, generation=gen)), info)
+        ex._selftest_ok = worst == 0
+        if worst != 0:
+            import logging
+
+            logging.getLogger("mlapi_amd.parallel").warning(
+                "P2P self-test failed (%d wrong words on the worst rank): DP steps use the RCCL all-reduce",
+                int(worst))
+    info.__dict__["p2p_selftest"] = "ok" if ex._selftest_ok else "failed"
+    return ex._selftest_ok
 
 
 def from_env(rank: int, world: int, device: torch.device, store=None, generation: int = 0) -> Optional[P2PAllReduce]:

@@ -146,6 +146,7 @@ class BinarySGDTrainer:
         B = X.shape[0]
         if self.on_gpu and self._dp is not None and self.info.world > 1:
             self._fused_step(X, y)
+            self._dp.check_now()  # a missed exchange stops the loop (no silent divergence)
             self.steps += 1
             self._n_seen = B * self.info.world
             return

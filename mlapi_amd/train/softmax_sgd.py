@@ -81,7 +81,8 @@ class SoftmaxSGDTrainer:
         if self.on_gpu:
             from mlapi_amd.parallel.p2p import dp_exchange
 
-            self._dp = dp_exchange(self.info, (n + 4) * 4)
+            # gradient slice + stats, then (two-shot exchange) the published [grad | params | momenta]
+            self._dp = dp_exchange(self.info, (4 * n + 16) * 4)
         self.dp_timeout_ms = 60_000
         self.steps = 0
         self._n_seen = 0
@@ -175,6 +176,8 @@ class SoftmaxSGDTrainer:
             self._graph[0].replay()
         elif self.on_gpu and (self._dp is not None or self.info.world == 1):
             self._local_grad(Xa, y, fused_update_n=Xa.shape[0] * self.info.world, dp=self._dp)
+            if self._dp is not None:
+                self._dp.check_now()  # a missed exchange stops the loop (no silent divergence)
         else:
             self._local_grad(Xa, y)
             all_reduce_sum_(self.grad, self.info)

@@ -28,7 +28,15 @@ if info.rank == 0:
         tr.check()
     except RuntimeError:
         raised = True
-    res = {"raised": raised, "params_unchanged": bool(torch.equal(before, tr.params)), "elapsed_s": time.time() - t0}
+    # the sticky status is host-mapped: the next step stops at once (no silent divergence)
+    next_raised = False
+    try:
+        tr.step(X, y)
+    except RuntimeError:
+        next_raised = True
+    torch.cuda.synchronize()
+    res = {"raised": raised, "params_unchanged": bool(torch.equal(before, tr.params)), "elapsed_s": time.time() - t0,
+           "next_step_raised": next_raised}
     json.dump(res, open(f"{out}/timeout_{info.rank}.json", "w"))
 barrier(info)
 shutdown(info)

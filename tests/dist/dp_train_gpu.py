@@ -20,7 +20,7 @@ info = init_distributed(use_gpu=True, comm="p2p")
 assert info.backend == "p2p+gloo"
 dev, out, r, w = info.device, os.environ["OUT"], info.rank, info.world
 fused = os.environ.get("MLAPI_DP_FUSED", "1") != "0"
-tag = "" if fused else "_unfused"
+tag = ("" if fused else "_unfused") + ("_two" if os.environ.get("MLAPI_DP_TWO_SHOT") == "1" else "")
 m = LinearModel.random(6, 5, seed=7, labels=["a", "b", "c", "d", "e"]) if r == 0 else None
 m = broadcast_model(m, info)
 B = 2048
@@ -28,7 +28,9 @@ per = B // w
 X, y = synthetic_binary(8192, 256, seed=5, dtype=torch.bfloat16)
 X, y = X.to(dev), y.to(dev)
 tr = BinarySGDTrainer(256, info=info, lr=0.5, l2=1e-3, momentum=0.9, device=dev)
-assert tr.dp_exchange == ("fused-p2p" if fused else ("local" if w == 1 else "rccl")), tr.dp_exchange
+# one replica: the local step (no exchange object); N > 1: the in-kernel exchange unless unfused
+assert tr.dp_exchange == ("local" if w == 1 else ("fused-p2p" if fused else "rccl")), tr.dp_exchange
+assert w == 1 or info.__dict__.get("p2p_selftest") == ("ok" if fused else None), info.__dict__.get("p2p_selftest")
 for s in range(20):
     lo = s * B % 8192
     sl = slice(lo + r * per, lo + (r + 1) * per)

@@ -105,6 +105,11 @@ def test_dp_sgd_on_gpu_with_p2p_allreduce(tmp_path):
     _torchrun(1, "dp_train_gpu.py", tmp_path)
     _torchrun(2, "dp_train_gpu.py", tmp_path)
     _torchrun(2, "dp_train_gpu.py", tmp_path, env={"MLAPI_DP_FUSED": "0"})
+    # two-shot exchange (the multiclass gradient: owner ranks reduce + update, the others copy)
+    _torchrun(2, "dp_train_gpu.py", tmp_path, env={"MLAPI_DP_TWO_SHOT": "1"})
+    for r in range(2):
+        assert np.array_equal(np.load(tmp_path / f"mc_params_2_{r}_two.npy"), np.load(tmp_path / f"mc_params_2_{r}.npy")), \
+            "two-shot exchange must give the one-shot replicas bitwise"
     for name in ("params", "mc_params"):
         a, b = np.load(tmp_path / f"{name}_2_0.npy"), np.load(tmp_path / f"{name}_2_1.npy")
         assert np.array_equal(a, b), f"{name}: DP replicas must stay bitwise identical"
@@ -124,6 +129,20 @@ def test_dp_fused_exchange_times_out_without_a_peer(tmp_path):
     _torchrun(2, "dp_fused_timeout.py", tmp_path)
     res = json.loads((tmp_path / "timeout_0.json").read_text())
     assert res["raised"] and res["params_unchanged"] and res["elapsed_s"] < 30
+    assert res["next_step_raised"], "the step after a missed exchange must stop the loop"
+
+
+def test_p2p_selftest_failure_falls_back(tmp_path):
+    """A rank whose IPC self-test pattern arrives wrong (MLAPI_P2P_SELFTEST_CORRUPT) makes every
+    rank drop the fused in-kernel exchange for the unfused all-reduce path; training still runs and
+    the replicas stay bitwise identical."""
+    import numpy as np
+
+    _torchrun(2, "p2p_selftest.py", tmp_path, env={"MLAPI_P2P_SELFTEST_CORRUPT": "1"})
+    for r in range(2):
+        res = json.loads((tmp_path / f"selftest_{r}.json").read_text())
+        assert res["p2p_selftest"] == "failed" and res["dp_exchange"] == "rccl", res
+    assert np.array_equal(np.load(tmp_path / "st_params_0.npy"), np.load(tmp_path / "st_params_1.npy"))
 
 
 @pytest.mark.parametrize("mode", ["serve", "serve_wide"])
