@@ -429,6 +429,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("inline_args", &EngineConfig::inline_args)
       .def_readwrite("idle_inline_rows", &EngineConfig::idle_inline_rows)
       .def_readwrite("lanes", &EngineConfig::lanes)
+      .def_readwrite("lane_inflight", &EngineConfig::lane_inflight)
       .def_readwrite("f32_split", &EngineConfig::f32_split)
       .def_readwrite("completers", &EngineConfig::completers)
       .def_readwrite("batchers", &EngineConfig::batchers)

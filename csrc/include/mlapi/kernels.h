@@ -86,8 +86,11 @@ __device__ __forceinline__ void put_record(ServeRecord* dst, uint32_t seq, int32
   const uint64_t pb = __builtin_bit_cast(uint64_t, p);
   typedef __attribute__((ext_vector_type(4))) uint32_t rec_u32x4_t;
   const rec_u32x4_t v = {seq, (uint32_t)idx, (uint32_t)pb, (uint32_t)(pb >> 32)};
-  // write-through vector store (sc0 sc1): visible to the host without a fence or a flush
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
+  // write-through vector store (sc0 sc1): visible to the host without a fence or a flush. The
+  // s_nop: a store of more than 64 bits reads its data VGPRs after issue, so a VALU write to them
+  // right behind it needs a wait state - hipcc inserts it for its own stores, never inside asm
+  // (linear_wide's partials were clobbered by the next store's address computation without it)
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
 }
 __device__ __forceinline__ void put_result(int32_t* out_idx, float* out_p, const RecOut& ro, int64_t row,
                                            int32_t idx, float p) {

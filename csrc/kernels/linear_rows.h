@@ -134,7 +134,7 @@ __device__ __forceinline__ void inline_batch_rows(const InlineBatch* a) {
       // compiler emits the same bits for a 4/8-byte system-scope atomic store; there is no 16-byte
       // atomic, hence the asm.
       ServeRecord* dst = static_cast<ServeRecord*>(a->rec) + (a->rec_scatter ? a->rec_idx[r] : (uint32_t)r);
-      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
+      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
     } else {
       a->out_idx[r] = idx;
       static_cast<T*>(a->out_p)[r] = p;
@@ -162,7 +162,7 @@ __device__ __forceinline__ void inline_batch_rows_exact(const InlineBatch* a) {
     typedef __attribute__((ext_vector_type(4))) uint32_t u32x4_t;
     const u32x4_t v = {a->seq, (uint32_t)idx, (uint32_t)pb, (uint32_t)(pb >> 32)};
     ServeRecord* dst = static_cast<ServeRecord*>(a->rec) + (a->rec_scatter ? a->rec_idx[r] : (uint32_t)r);
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
   } else {
     a->out_idx[r] = idx;
     static_cast<T*>(a->out_p)[r] = p;

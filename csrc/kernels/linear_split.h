@@ -199,7 +199,7 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
       const su32x4_t r = {a.rec_seq, (uint32_t)S.bi, __float_as_uint(S.m), __float_as_uint(S.s)};
       uint4* dst = a.hrec + (int64_t)split * ROWS_PER_GROUP + l;
       // write-through (sc0 sc1): visible to the host poller without a fence, as one 16-byte unit
-      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(r) : "memory");
+      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(dst), "v"(r) : "memory");
     }
     return;
   }

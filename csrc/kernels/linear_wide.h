@@ -55,9 +55,12 @@ struct WideArgs {
   RecOut ro;               // ... or serving records (in-kernel class merge)
   uint4* hrec;             // host class merge: [ncb][32 rows][2] 16-byte units {seq, bi, m} {seq, 0, s}
   uint32_t hseq;
-  unsigned int* counters;  // [row groups][ncb] split tickets, then [row groups] class tickets; zero, re-armed
-  double* partials;        // [row groups][ncb][nfs][NB * 4 * 64] split partial tiles
-  double* states;          // [row groups][ncb][32 rows][4] {m, s, bi bits, 0} class-block row states
+  // Workspace, one region per row group (the layout does not depend on B, so launches of any size
+  // share it): [ncb split tickets | 1 class ticket] (zero, re-armed by the last arrivers), then
+  // [ncb][nfs][2 * 4 * 64] f64 split partial tiles (nfs > 1), then [ncb][32 rows][4] f64 row
+  // states {m, s, argmax bits, 0}.
+  unsigned char* ws;
+  int64_t rg_bytes, cnt_bytes, part_bytes;
   int32_t row_groups;
 };
 
@@ -98,10 +101,10 @@ __device__ __forceinline__ double wsigmoid(double z) { return 1.0 / (1.0 + exp(-
 
 // write-through 16-byte store (device-internal hand-off: sc1; host records: sc0 sc1)
 __device__ __forceinline__ void st16_sc1(void* dst, wu4_t v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
 }
 __device__ __forceinline__ void st16_host(void* dst, wu4_t v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
 }
 __device__ __forceinline__ wu4_t pack2(uint32_t a, uint32_t b, double d) {
   const uint64_t u = __builtin_bit_cast(uint64_t, d);
@@ -186,17 +189,18 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   // ---- feature splits: the last-arriving block of (row group, class block) sums them in order
   if (a.nfs > 1) {
     typedef __attribute__((address_space(1))) unsigned int gu32_t;
-    double* part = a.partials + (((int64_t)rgi * a.ncb + cb) * a.nfs) * (NB * 4 * 64);
+    unsigned char* rgw = a.ws + (int64_t)rgi * a.rg_bytes;
+    double* part = reinterpret_cast<double*>(rgw + a.cnt_bytes) + ((int64_t)cb * a.nfs) * (2 * 4 * 64);
     if (wave == 0) {
 #pragma unroll
       for (int t = 0; t < NB; ++t) {
-        double* dst = part + (int64_t)fs * (NB * 4 * 64) + t * 256 + lane * 4;
+        double* dst = part + (int64_t)fs * (2 * 4 * 64) + t * 256 + lane * 4;
         st16_sc1(dst, __builtin_bit_cast(wu4_t, wd2_t{acc[t][0], acc[t][1]}));
         st16_sc1(dst + 2, __builtin_bit_cast(wu4_t, wd2_t{acc[t][2], acc[t][3]}));
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every partial acknowledged before the ticket
       if (lane == 0) {
-        gu32_t* ctr = (gu32_t*)(a.counters + (int64_t)rgi * a.ncb + cb);
+        gu32_t* ctr = (gu32_t*)(reinterpret_cast<unsigned int*>(rgw) + cb);
         const unsigned tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool last = tk == (unsigned)a.nfs - 1;
         if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
@@ -213,7 +217,7 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
       for (int f = 0; f < a.nfs; ++f) {  // split order: deterministic
 #pragma unroll
         for (int t = 0; t < NB; ++t) {
-          const double* src = part + (int64_t)f * (NB * 4 * 64) + t * 256 + lane * 4;
+          const double* src = part + (int64_t)f * (2 * 4 * 64) + t * 256 + lane * 4;
           const wd4_t v = *reinterpret_cast<const wd4_t*>(src);
           acc[t] += v;
         }
@@ -294,7 +298,8 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     }
   }
   // ---- class blocks: the last-arriving block of the row group merges them in block order
-  double* states = a.states + (int64_t)rgi * a.ncb * RG * 4;
+  unsigned char* rgw2 = a.ws + (int64_t)rgi * a.rg_bytes;
+  double* states = reinterpret_cast<double*>(rgw2 + a.cnt_bytes + a.part_bytes);
   if (wave == 0) {
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
@@ -308,7 +313,7 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
       typedef __attribute__((address_space(1))) unsigned int gu32_t;
-      gu32_t* ctr = (gu32_t*)(a.counters + (int64_t)a.row_groups * a.ncb + rgi);
+      gu32_t* ctr = (gu32_t*)(reinterpret_cast<unsigned int*>(rgw2) + a.ncb);
       const unsigned tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool last = tk == (unsigned)a.ncb - 1;
       if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -20,7 +20,6 @@ __global__ __launch_bounds__(256) void linear_wide_kernel(wide::WideArgs a) {
 
 static_assert(wide::CB == wide_plan::CB && wide::RG == wide_plan::RG && wide::WAVES == wide_plan::WAVES,
               "linear_wide.h and wide_plan.h disagree on the geometry");
-using wide_plan::counters_bytes;
 using wide_plan::row_groups;
 
 }  // namespace
@@ -64,12 +63,11 @@ void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const
   a.hrec = reinterpret_cast<uint4*>(hro.rec);
   a.hseq = hro.seq;
   a.row_groups = rg;
-  unsigned char* w = static_cast<unsigned char*>(workspace);
-  a.counters = reinterpret_cast<unsigned*>(w);
-  size_t off = counters_bytes(rg, p.ncb);
-  a.partials = reinterpret_cast<double*>(w + off);
-  if (p.nfs > 1) off += (size_t)rg * p.ncb * p.nfs * (2 * 4 * 64) * sizeof(double);
-  a.states = reinterpret_cast<double*>(w + off);
+  const wide_plan::Layout lay = wide_plan::layout(p);
+  a.ws = static_cast<unsigned char*>(workspace);
+  a.rg_bytes = (int64_t)lay.rg_bytes;
+  a.cnt_bytes = (int64_t)lay.cnt_bytes;
+  a.part_bytes = (int64_t)lay.part_bytes;
   const dim3 grid((unsigned)(p.ncb * p.nfs), (unsigned)rg);
   const bool nb2 = B > 16;
   if (direct != nullptr) {

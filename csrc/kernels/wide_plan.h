@@ -33,15 +33,21 @@ inline WidePlan plan(int dt, int F, int K) {
 }
 
 inline int row_groups(int64_t B) { return (int)((std::max<int64_t>(B, 1) + RG - 1) / RG); }
-inline size_t counters_bytes(int rg, int ncb) { return (((size_t)rg * ncb + rg) * sizeof(unsigned) + 255) & ~size_t(255); }
+
+// one region per row group (linear_wide.h WideArgs): tickets | split partials | row states
+struct Layout {
+  size_t cnt_bytes, part_bytes, rg_bytes;
+};
+inline Layout layout(const WidePlan& p) {
+  Layout l;
+  l.cnt_bytes = (((size_t)p.ncb + 1) * sizeof(unsigned) + 255) & ~size_t(255);
+  l.part_bytes = p.nfs > 1 ? (size_t)p.ncb * p.nfs * (2 * 4 * 64) * sizeof(double) : 0;
+  l.rg_bytes = l.cnt_bytes + l.part_bytes + (size_t)p.ncb * RG * 4 * sizeof(double);
+  return l;
+}
 
 inline size_t workspace(int64_t B, int dt, int F, int K) {
-  const WidePlan p = plan(dt, F, K);
-  const int rg = row_groups(B);
-  size_t bytes = counters_bytes(rg, p.ncb);
-  if (p.nfs > 1) bytes += (size_t)rg * p.ncb * p.nfs * (2 * 4 * 64) * sizeof(double);
-  bytes += (size_t)rg * p.ncb * RG * 4 * sizeof(double);
-  return bytes;
+  return (size_t)row_groups(B) * layout(plan(dt, F, K)).rg_bytes;
 }
 
 }  // namespace wide_plan

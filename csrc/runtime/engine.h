@@ -211,8 +211,11 @@ struct EngineConfig {
   // wake-ups (two futex hand-offs on a batch=1 request). SMALL-path models, batches of at most
   // this many rows; 0 = off. On the CPU backend the calling thread runs the float64 oracle.
   int idle_inline_rows = 8;
-  // IO threads queue SMALL-path rows on lanes and launch them by flat combining (open_lane); 0 = off
-  int lanes = 1;
+  // IO threads queue SMALL-path rows on lanes and launch them by flat combining (open_lane); 0 = off.
+  // Off by default: measured against the batcher / completer threads on the c = 64 headline it
+  // cut the server-side latency but raised CPU per request and the tail (docs/PERFORMANCE.md,
+  // profiles/r4_lanes/)
+  int lanes = 0;
   int lane_inflight = 3;  // combined lane batches in flight at most (the rest coalesce into the next)
 };
 

@@ -64,6 +64,7 @@ class EngineHandle:
         ec.inline_args = bool(config.inline_args)
         ec.idle_inline_rows = int(config.idle_inline_rows)
         ec.lanes = int(config.lanes)
+        ec.lane_inflight = int(config.lane_inflight)
         ec.f32_split = bool(config.f32_split)
         ec.completers = int(config.completers)
         ec.batchers = int(config.batchers)

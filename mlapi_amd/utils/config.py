@@ -54,7 +54,8 @@ class Config:
     gemv_record_rows: int = 2                 # GEMV batches >= this many rows complete via records (0 = never)
     idle_inline_rows: int = 8                 # GPU: idle engine -> the IO thread launches <= this many rows itself (0 = off)
     f32_split: bool = False                   # GPU: f32 multiclass F <= 512 on the f32-accumulating split kernel (A/B)
-    lanes: int = 1                            # GPU: IO threads dispatch SMALL-model batches themselves (engine lanes; 0 = off)
+    lane_inflight: int = 3                    # GPU: combined lane batches in flight at most (rows coalesce behind them)
+    lanes: int = 0                            # GPU: IO threads launch SMALL-model rows by flat combining (engine lanes; opt-in, measured slower)
     direct_dispatch: bool = True              # GPU: ... written as AQL packets into the engine's own HSA queue
     direct_wide: bool = True                  # GPU: class-split / record GEMV batches into that queue too ...
     direct_wide_max_weight_bytes: int = 256 << 10  # ... for models with at most this many bytes of W
