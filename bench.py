@@ -373,7 +373,7 @@ def bench_gemm(args, info):
             X, W = X.float(), W.float()
         op = ops.LinearSplit(B, K, info.device)
     else:
-        forced = {"tiles": 1, "rows": 2, "t32": 3, "ws": 4}.get(args.gemm_kernel, 0)
+        forced = {"tiles": 1, "rows": 2, "t32": 3}.get(args.gemm_kernel, 0)
         if forced:
             from mlapi_amd._native import C
 
@@ -507,9 +507,9 @@ def main(argv=None) -> int:
     ap.add_argument("--c1-requests", type=int, default=3000)
     ap.add_argument("--rows", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=1024)
-    ap.add_argument("--gemm-kernel", default="auto", choices=["auto", "split", "tiles", "rows", "t32", "ws"],
+    ap.add_argument("--gemm-kernel", default="auto", choices=["auto", "split", "tiles", "rows", "t32"],
                     help="gemm: auto = the planner's choice; split = the class-split small-batch kernel; "
-                         "tiles / rows / t32 / ws = that gemm_softmax kernel forced (measurement)")
+                         "tiles / rows / t32 = that gemm_softmax kernel forced (measurement)")
     ap.add_argument("--gemm-dtype", default="bf16", choices=["bf16", "f32"], help="gemm: f32 runs the split kernel")
     ap.add_argument("--launch", default="graph", choices=["graph", "eager"],
                     help="gemv/gemm: the timed K calls replayed from one captured HIP graph (GPU time) or "

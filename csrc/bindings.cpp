@@ -178,18 +178,6 @@ PYBIND11_MODULE(_C, m) {
       py::arg("dt"), py::arg("X"), py::arg("w"), py::arg("bias"), py::arg("B"), py::arg("F"), py::arg("kind"),
       py::arg("out_idx"), py::arg("out_p"), py::arg("stream") = 0);
   m.def("gemm_softmax_workspace", &gemm_softmax_workspace);
-  m.def("gemm_softmax_ws_plan", [](int64_t B, int K, int F, int cus_per_xcd) -> py::object {
-    int ns = 0, sc = 0, gpx = 0;
-    int64_t tpg = 0, grid = 0;
-    if (!gemm_softmax_ws_plan(B, K, F, cus_per_xcd, &ns, &sc, &gpx, &tpg, &grid)) return py::none();
-    py::dict d;
-    d["slices"] = ns;
-    d["slice_classes"] = sc;
-    d["groups_per_xcd"] = gpx;
-    d["tiles_per_group"] = tpg;
-    d["grid"] = grid;
-    return d;
-  });
   m.def("gemm_softmax_force_plan", &gemm_softmax_force_plan, py::arg("nt") = 0, py::arg("splits") = 0,
         py::arg("kernel") = 0);
   m.def("gemm_softmax_set_stamps", [](uintptr_t p) { gemm_softmax_set_stamps(reinterpret_cast<void*>(p)); });
@@ -431,6 +419,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("lanes", &EngineConfig::lanes)
       .def_readwrite("lane_inflight", &EngineConfig::lane_inflight)
       .def_readwrite("f32_split", &EngineConfig::f32_split)
+      .def_readwrite("wide_host_merge_blocks", &EngineConfig::wide_host_merge_blocks)
       .def_readwrite("completers", &EngineConfig::completers)
       .def_readwrite("batchers", &EngineConfig::batchers)
       .def_readwrite("gemv_record_rows", &EngineConfig::gemv_record_rows)

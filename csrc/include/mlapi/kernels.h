@@ -118,10 +118,6 @@ void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_
 // width: the row-group kernel loops F in 256-feature slices). Workspace: gemm_softmax_workspace()
 // (0 when the row-group kernel serves the shape).
 size_t gemm_softmax_workspace(int64_t B, int K, int F);
-// Host plan of the W-stationary kernel (gemm_softmax_ws_kernel) for a device with cus_per_xcd CUs
-// per XCD: false if it does not apply (F not 128 / 256, more slices than CUs per XCD, B > 524288).
-bool gemm_softmax_ws_plan(int64_t B, int K, int F, int cus_per_xcd, int* slices, int* slice_classes,
-                          int* groups_per_xcd, int64_t* tiles_per_group, int64_t* grid);
 // Benchmark hook: force the tiles kernel's (rows-per-wave tiles, class splits) plan and the
 // kernel (0 automatic, 1 tiles 16x16x32, 2 row-group, 3 tiles 32x32x16); all 0 = automatic.
 void gemm_softmax_force_plan(int nt, int splits, int kernel = 0);

@@ -48,8 +48,8 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 constexpr int CLASS_CHUNK = 64;
 constexpr float LOG2E_F = 1.4426950408889634f;
 constexpr float LN2_F = 0.6931471805599453f;
-// Arrival counters live at the start of the workspace (split plans: one per row block; the
-// W-stationary plan: one per 32-row tile, B <= 524288); every plan re-arms its counters to 0 and
+// Arrival counters live at the start of the workspace (split plans: one per row block); every plan
+// re-arms its counters to 0 and
 // the partials always start after this region, so plans of different batch sizes can share one
 // zero-initialised workspace.
 constexpr int COUNTER_BYTES = 65536;
@@ -125,9 +125,6 @@ struct GemmArgs {
   float4* rowstate;        // MODE 4 output: {max, sum, argmax bits, 0} (class-sharded TP)
   unsigned long long* stamps;  // profiling (tools/gemm_phase_probe.py): 8 s_memtime slots per wave
   int xcd_local;               // split merge meets in one XCD's L2 (grid.x % 8 == 0; see xcd_put_partial)
-  int ws_slices;               // W-stationary kernel: class slices (NS), row groups per XCD, tiles per group
-  int ws_groups_per_xcd;
-  int64_t ws_tiles_per_group;
 };
 
 // ---- split-merge protocol (tiles kernels). Default (agent scope): partials stored write-through
@@ -1154,182 +1151,6 @@ gemm_softmax32_kernel(GemmArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// W-stationary persistent kernel (v7, large batches). The 32x32 kernel above re-streams every
-// 64-class W chunk through LDS for every 128-row block: one LDS-DMA + block barrier per chunk, all
-// 4 waves in lockstep, and every block starts by pulling its X rows from HBM with the MFMA pipe
-// idle (phase probe at B = 262144: prologue 11k of a 65k-cycle wave life, loop 52.6k against 32.8k
-// of MFMA; profiles/r2_gemm/phase_probe.log). Here the roles flip:
-//  * one 512-thread block per CU keeps a 128 KiB class SLICE of W (256 classes at F = 256) resident
-//    in LDS, DMA'd once; after that single barrier the 8 waves never synchronise again;
-//  * each wave streams its own 32-row X tiles into registers and runs the slice's chunks with the
-//    same pipelined MFMA + softmax-epilogue step as the 32x32 kernel; the two waves of a SIMD are
-//    free-running, so one wave's X fetch hides under its partner's MFMAs;
-//  * the grid is persistent and XCD-aware: blocks i, i+8, ... share an XCD (round-robin
-//    dispatch); the NS slice blocks of a row group sit on ONE XCD and walk the same tiles in the
-//    same order, so a tile's X comes from HBM once and from that XCD's L2 for the other slices;
-//  * per tile, each slice publishes its rows' online-softmax states {max, sum, argmax}; the wave
-//    whose arrival ticket completes the tile merges the NS states in slice order (first max
-//    wins: exact labels) and writes the outputs. No second launch, no spinning.
-// F in {128, 256} (KS 4, 8; X takes 4 * KS VGPRs): SLICE = 32 / KS chunks (128 KiB of LDS),
-// NS = ceil(K / SLICE) slices.
-constexpr int WS_WAVES = 8;
-constexpr int WS_SLICE_BYTES = 128 * 1024;
-
-template <int KS>
-constexpr int ws_slice_chunks() {
-  return WS_SLICE_BYTES / (CLASS_CHUNK * lds_row_stride<KS>());
-}
-
-template <int MODE>
-__device__ __forceinline__ void emit_row(const GemmArgs& a, int64_t row, const RowState& R, bool ovr) {
-  if constexpr (MODE == 0) {
-    put_result(a.out_idx, a.out_p, a.ro, row, R.bi, ovr ? sigmoidf_(R.m) / R.s : 1.f / R.s);
-  } else if constexpr (MODE == 4) {
-    a.rowstate[row] = make_float4(R.m, R.s, __int_as_float(R.bi), 0.f);
-  } else {
-    a.rowstat[row] = make_float2(R.m + __logf(R.s), __int_as_float(R.bi));
-  }
-}
-
-template <int KS, int MODE, bool OVR>
-__global__ __launch_bounds__(64 * WS_WAVES) __attribute__((amdgpu_waves_per_eu(2, 2))) void
-gemm_softmax_ws_kernel(GemmArgs a) {
-  static_assert(MODE == 0 || MODE == 2 || MODE == 4, "predict / row stats / row state modes");
-  constexpr int K2 = 2 * KS;
-  constexpr int NTHR = 64 * WS_WAVES;
-  constexpr int F_ = KS * 32;
-  constexpr int NCH = F_ / 8;  // 16-byte pieces per W row
-  constexpr int W_BYTES = CLASS_CHUNK * lds_row_stride<KS>();
-  constexpr int BUF_BYTES = W_BYTES + CLASS_CHUNK * 4;  // [W chunk image | its 64 biases]
-  constexpr int NQ = ws_slice_chunks<KS>();
-  constexpr int PIECES = CLASS_CHUNK * NCH / NTHR;
-  static_assert(PIECES >= 1 && CLASS_CHUNK * NCH % NTHR == 0, "W chunk must split evenly over the block");
-  static_assert(NQ * BUF_BYTES <= 160 * 1024 - 1024, "slice must fit the LDS");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[NQ * BUF_BYTES];
-
-  const int NS = a.ws_slices;
-  const int xcd = blockIdx.x & 7;
-  const int j = blockIdx.x >> 3;
-  const int slice = j % NS;
-  const int gx = j / NS;
-  if (gx >= a.ws_groups_per_xcd) return;  // uniform per block: CUs left over by NS
-  const int group = gx * 8 + xcd;
-  const int64_t B = a.B;
-  const int K = a.K;
-  const int c_begin = slice * NQ * CLASS_CHUNK;
-  const int c_end = min(K, c_begin + NQ * CLASS_CHUNK);
-  const int nq = (c_end - c_begin + CLASS_CHUNK - 1) / CLASS_CHUNK;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int h = lane >> 5;
-  const int col = lane & 31;
-  constexpr bool ovr = OVR;
-
-  // the slice -> LDS, once (rows >= K read as 0 through the range-checked descriptor; bias32
-  // maps their classes to -inf)
-  {
-    const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, K * F_ * 2, 0x00020000);
-    const auto brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.bias, 0, K * 4, 0x00020000);
-    for (int q = 0; q < nq; ++q) {
-#pragma unroll
-      for (int i = 0; i < PIECES; ++i) {
-        const int p = tid + i * NTHR;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            wrsrc, (lds_void_t*)(smem + q * BUF_BYTES + (i * NTHR + wave * 64) * 16), 16,
-            (uint32_t)(((p / NCH) * F_ + lds_pos<KS>(p / NCH, p % NCH) * 8) * 2), (c_begin + q * CLASS_CHUNK) * F_ * 2,
-            0, 0);
-      }
-      if (wave == (q & 7))
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void_t*)(smem + q * BUF_BYTES + W_BYTES), 4,
-                                                 (uint32_t)lane * 4, (c_begin + q * CLASS_CHUNK) * 4, 0, 0);
-    }
-    __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
-    asm volatile("" ::: "memory");
-    __syncthreads();
-    asm volatile("" ::: "memory");
-  }
-
-  const int64_t T = (B + 31) / 32;
-  const int64_t t_begin = (int64_t)group * a.ws_tiles_per_group;
-  const int64_t t_end = min(T, t_begin + a.ws_tiles_per_group);
-  const FragOff<KS> fo = frag_offsets<KS>(h, col);
-  for (int64_t tile = t_begin + wave; tile < t_end; tile += WS_WAVES) {
-    bf16x8_t xf[1][K2];
-    {
-      int64_t r = tile * 32 + col;
-      r = r < B ? r : B - 1;
-      const uint16_t* xr = a.X + r * a.ldx + 8 * h;
-#pragma unroll
-      for (int k = 0; k < K2; ++k) xf[0][k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + k * 16));
-    }
-    TileState ts[1];
-    tile_init(ts[0]);
-    f32x16_t accA[1][2], accB[1][2];
-    mfma32_chunk<KS, 1>(smem, xf, c_begin, c_end, h, col, accA);
-    // chunk q's MFMAs with chunk q-1's epilogue; accumulators alternate A/B by parity
-    static_for<NQ>([&](auto qc) {
-      constexpr int q = decltype(qc)::value;
-      if constexpr (q >= 1) {
-        if (q < nq) {
-          if constexpr (q & 1)
-            fused32_step<KS, 1, OVR, q, BUF_BYTES>(smem, fo, xf, c_begin + q * CLASS_CHUNK, c_end, h, accB, accA,
-                                                   c_begin + (q - 1) * CLASS_CHUNK, ts);
-          else
-            fused32_step<KS, 1, OVR, q, BUF_BYTES>(smem, fo, xf, c_begin + q * CLASS_CHUNK, c_end, h, accA, accB,
-                                                   c_begin + (q - 1) * CLASS_CHUNK, ts);
-        } else if (q == nq) {  // last slice, fewer chunks: the final epilogue
-          if constexpr ((q - 1) & 1)
-            epilogue32<OVR, 1>(accB, c_begin + (q - 1) * CLASS_CHUNK, ts);
-          else
-            epilogue32<OVR, 1>(accA, c_begin + (q - 1) * CLASS_CHUNK, ts);
-        }
-      }
-    });
-    if (nq == NQ) {
-      if constexpr ((NQ - 1) & 1)
-        epilogue32<OVR, 1>(accB, c_begin + (NQ - 1) * CLASS_CHUNK, ts);
-      else
-        epilogue32<OVR, 1>(accA, c_begin + (NQ - 1) * CLASS_CHUNK, ts);
-    }
-    RowState S = tile_result32(ts[0], h);
-    S = merge_state(S, shfl_state(S, 32), ovr);
-    const int64_t row = tile * 32 + col;
-    if (NS == 1) {
-      if (h == 0 && row < B) emit_row<MODE>(a, row, S, ovr);
-      continue;
-    }
-    // publish this slice's states; the tile's last-arriving slice wave merges them
-    if (h == 0 && row < B) {
-      typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-      typedef __attribute__((address_space(1))) unsigned int gu32_t;
-      float4* dst = a.partials + (int64_t)slice * B + row;
-      const unsigned long long ms =
-          (unsigned long long)__float_as_uint(S.m) | ((unsigned long long)__float_as_uint(S.s) << 32);
-      __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S.bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned ticket = 0;
-    if (lane == 0) ticket = __hip_atomic_fetch_add(&a.counters[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ticket = (unsigned)__builtin_amdgcn_readfirstlane((int)ticket);
-    if (ticket != (unsigned)NS - 1) continue;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (lane == 0) __hip_atomic_store(&a.counters[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (h == 0 && row < B) {
-      const float4 p0 = a.partials[row];
-      RowState R{p0.x, p0.y, __float_as_int(p0.z)};
-      for (int sp = 1; sp < NS; ++sp) {
-        const float4 pq = a.partials[(int64_t)sp * B + row];
-        R = merge_state(R, RowState{pq.x, pq.y, __float_as_int(pq.z)}, ovr);
-      }
-      emit_row<MODE>(a, row, R, ovr);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // Row-group kernel (small / medium batches, and any F): one block owns 16 * NT batch rows and
 // ALL classes. Its nw waves split the 64-class chunks round-robin; every wave streams its W
 // fragments straight from L2 into VGPRs (no LDS staging, no barrier per chunk: for a small batch
@@ -1478,7 +1299,7 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
 // Which kernel serves (B, K, F): the row-group kernel only where the tiles kernel has no
 // instantiation (F > 512, the only kernel that loops F). At F <= 512 the tiles kernel with class
 // splits is faster at every B (profiles/r2_gemm/sweep.log: B <= 4096 rows 17-19 us vs tiles 7-10).
-int g_force_kernel = 0;  // benchmark hook: 0 automatic, 1 tiles 16x16, 2 row-group, 3 tiles 32x32, 4 W-stationary
+int g_force_kernel = 0;  // benchmark hook: 0 automatic, 1 tiles 16x16, 2 row-group, 3 tiles 32x32
                          // (measurement only: 5 32x32 with the epilogue compiled out, 6 / 7 with
                          // W fragments 1 / 3 k-steps ahead instead of 2)
 
@@ -1542,9 +1363,6 @@ RowsArgs rows_args(const void* X, int64_t ldx, const void* W, const float* b, in
 }
 
 struct Plan {
-  int ws = 0;             // 1: the W-stationary persistent kernel (fields below)
-  int ws_slices = 0, ws_groups_per_xcd = 0;
-  int64_t ws_tiles_per_group = 0;
   int k32 = 0;            // > 0: the 32x32x16 kernel with this many waves per block
   int rt32 = 1;           // its 32-row tiles per wave
   int nt;                 // 16-row tiles per wave (16x16x32 kernel)
@@ -1577,38 +1395,9 @@ int cus_per_xcd() {  // CUs of the current device / 8 XCDs (the dispatcher round
   return cache[dev];
 }
 
-// W-stationary plan: class slices of 128 KiB, as many row groups per XCD as whole slice sets fit
-bool ws_plan_for(int64_t B, int K, int F, int cus_xcd, Plan& p) {
-  if (F != 128 && F != 256) return false;  // F = 64 spills SGPRs at 16 chunks per slice: the 32x32 kernel
-  const int slice = (WS_SLICE_BYTES / (F * 2) / CLASS_CHUNK) * CLASS_CHUNK;
-  const int ns = (K + slice - 1) / slice;
-  const int gpx = cus_xcd / ns;
-  const int64_t tiles = (B + 31) / 32;
-  if (gpx < 1 || tiles * 4 > COUNTER_BYTES) return false;
-  p.ws = 1;
-  p.ws_slices = ns;
-  p.ws_groups_per_xcd = gpx;
-  const int64_t groups = 8LL * gpx;
-  p.ws_tiles_per_group = (tiles + groups - 1) / groups;
-  p.splits = ns;
-  p.classes_per_split = slice;
-  p.row_blocks = 8LL * gpx * ns;  // the grid
-  return true;
-}
-
-bool ws_plan(int64_t B, int K, int F, Plan& p) { return ws_plan_for(B, K, F, cus_per_xcd(), p); }
-
 // allow32 = false for the logits mode (only the 16x16 kernel writes Z)
 Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   Plan p;
-  // W-stationary kernel: forced (4), or automatic for large batches once enabled (MLAPI_GEMM_WS=1;
-  // off by default until its A/B against the 32x32 kernel is measured on the box)
-  static const bool ws_auto = [] {
-    const char* e = getenv("MLAPI_GEMM_WS");
-    return e != nullptr && atoi(e) != 0;
-  }();
-  if (allow32 && (g_force_kernel == 4 || (g_force_kernel == 0 && ws_auto && B >= 16384)) && ws_plan(B, K, F, p))
-    return p;
   if (allow32 && t32_supported(F)) {
     if (g_force_kernel == 3 || g_force_kernel >= 5) p.k32 = 4;  // 5-8: 32x32 measurement variants
     else if (g_force_kernel == 0 && B >= 16384) p.k32 = 4;
@@ -1679,30 +1468,10 @@ void launch32(const GemmArgs& args, const dim3& grid, int rt, hipStream_t stream
 
 void* g_stamps = nullptr;  // profiling hook (gemm_softmax_set_stamps)
 
-template <int MODE, int KS>
-void launch_ws(const GemmArgs& args, unsigned blocks, hipStream_t stream) {
-  if constexpr (MODE != 1) {
-    if (args.kind == KIND_OVR)
-      hipLaunchKernelGGL((gemm_softmax_ws_kernel<KS, MODE, true>), dim3(blocks), dim3(64 * WS_WAVES), 0, stream, args);
-    else
-      hipLaunchKernelGGL((gemm_softmax_ws_kernel<KS, MODE, false>), dim3(blocks), dim3(64 * WS_WAVES), 0, stream, args);
-  }
-}
-
 template <int MODE>
 void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
   args.classes_per_split = plan.classes_per_split;
   args.stamps = static_cast<unsigned long long*>(g_stamps);
-  if (MODE != 1 && plan.ws) {
-    args.ws_slices = plan.ws_slices;
-    args.ws_groups_per_xcd = plan.ws_groups_per_xcd;
-    args.ws_tiles_per_group = plan.ws_tiles_per_group;
-    const unsigned blocks = (unsigned)plan.row_blocks;
-    if (F == 128) launch_ws<MODE, 4>(args, blocks, stream);
-    else launch_ws<MODE, 8>(args, blocks, stream);
-    MLAPI_HIP_CHECK(hipGetLastError());
-    return;
-  }
   // XCD-local split merge (put_partial / xcd_verify): on by default, MLAPI_GEMM_XCD=0 selects the
   // agent-scope protocol. The grid's x extent is padded to a multiple of 8 (blocks past the batch
   // return at once) so that every split of a row block lands on the same XCD.
@@ -1772,18 +1541,6 @@ GemmArgs base_args(const void* X, const void* W, int64_t B, int F, int K, int ki
 void gemm_softmax_set_stamps(void* stamps) { g_stamps = stamps; }
 
 size_t gemm_softmax_xcd_err_offset() { return (size_t)XCD_ERR_SLOT * 4; }
-
-bool gemm_softmax_ws_plan(int64_t B, int K, int F, int cus_per_xcd, int* slices, int* slice_classes,
-                          int* groups_per_xcd, int64_t* tiles_per_group, int64_t* grid) {
-  Plan p;
-  if (!ws_plan_for(B, K, F, cus_per_xcd, p)) return false;
-  *slices = p.ws_slices;
-  *slice_classes = p.classes_per_split;
-  *groups_per_xcd = p.ws_groups_per_xcd;
-  *tiles_per_group = p.ws_tiles_per_group;
-  *grid = p.row_blocks;
-  return true;
-}
 
 void gemm_softmax_force_plan(int nt, int splits, int kernel) {
   g_force_nt = nt;

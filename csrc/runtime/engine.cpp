@@ -715,7 +715,7 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
       WideRecOut hro;
       const bool binary = m.kind == KIND_BINARY || m.kind == KIND_BINARY_SOFTMAX;
       if (cfg_.record_completion && s.hsrec != nullptr && !binary && n <= cfg_.host_merge_rows && n <= 32 &&
-          m.wplan.ncb > 1 && m.wplan.ncb <= 64) {
+          m.wplan.ncb > 1 && m.wplan.ncb <= std::min(64, cfg_.wide_host_merge_blocks)) {
         hro.rec = reinterpret_cast<WideRecord*>(s.dsrec);
         hro.seq = sig.seq;
         ro = RecOut();

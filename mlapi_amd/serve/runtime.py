@@ -66,6 +66,7 @@ class EngineHandle:
         ec.lanes = int(config.lanes)
         ec.lane_inflight = int(config.lane_inflight)
         ec.f32_split = bool(config.f32_split)
+        ec.wide_host_merge_blocks = int(config.wide_host_merge_blocks)
         ec.completers = int(config.completers)
         ec.batchers = int(config.batchers)
         ec.gemv_record_rows = int(config.gemv_record_rows)

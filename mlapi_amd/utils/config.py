@@ -53,6 +53,7 @@ class Config:
     batchers: int = 1                         # batcher threads (queue take + launch; launches serialised)
     gemv_record_rows: int = 2                 # GEMV batches >= this many rows complete via records (0 = never)
     idle_inline_rows: int = 8                 # GPU: idle engine -> the IO thread launches <= this many rows itself (0 = off)
+    wide_host_merge_blocks: int = 0           # GPU: WIDE batches merge class blocks on the host up to this many blocks (0 = in-kernel)
     f32_split: bool = False                   # GPU: f32 multiclass F <= 512 on the f32-accumulating split kernel (A/B)
     lane_inflight: int = 3                    # GPU: combined lane batches in flight at most (rows coalesce behind them)
     lanes: int = 0                            # GPU: IO threads launch SMALL-model rows by flat combining (engine lanes; opt-in, measured slower)

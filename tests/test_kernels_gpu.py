@@ -84,16 +84,13 @@ def test_gemv_binary_large_stream():
     torch.testing.assert_close(p, torch.sigmoid(z.abs()), rtol=1e-4, atol=1e-4)
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["auto", "tiles", "rows", "t32", "ws"])
+@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "tiles", "rows", "t32"])
 def gemm_kernel(request):
     """Run a multiclass test under the automatic plan and with each kernel forced (tiles: the
     LDS-staged, chunk-pipelined 16x16x32 kernel; rows: the row-group kernel; t32: the 32x32x16
-    large-batch kernel, F in {64, 128, 256}, else tiles; ws: the W-stationary persistent kernel,
-    F in {128, 256}, else tiles)."""
+    large-batch kernel, F in {64, 128, 256}, else tiles)."""
     from mlapi_amd._native import C
 
-    if request.param == 4 and os.environ.get("MLAPI_GEMM_WS", "0") == "0":
-        pytest.skip("W-stationary kernel is opt-in (MLAPI_GEMM_WS=1): measured slower than the tiles kernel, profiles/r3_ws")
     C().gemm_softmax_force_plan(0, 0, request.param)
     yield request.param
     C().gemm_softmax_force_plan(0, 0, 0)

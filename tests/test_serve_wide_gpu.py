@@ -103,7 +103,7 @@ def test_engine_small_multiclass_batches_take_split_kernel(native, wide):
     results match the oracle batch by batch."""
     F, K = 256, 1000
     m = LinearModel.random(F, K, seed=5, kind=Kind.MULTINOMIAL)
-    e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide[:4] if wide != "bf16" else wide],
+    e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide[:3] if wide != "bf16" else wide],
                 f32_split=wide == "f32split")
     try:
         e.load_model(int(m.kind), m.W, m.b, m.label_json())
@@ -113,7 +113,7 @@ def test_engine_small_multiclass_batches_take_split_kernel(native, wide):
             X = rng.standard_normal((n, F))
             idx, p, st = e.predict(X)
             assert (st == 0).all()
-            check(m, X, idx, p, wide[:4] if wide != "bf16" else wide,
+            check(m, X, idx, p, wide[:3] if wide != "bf16" else wide,
                   rtol={"f32": 1e-11, "f32split": 1e-5, "bf16": 1e-4}[wide])
     finally:
         e.stop()

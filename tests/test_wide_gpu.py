@@ -116,7 +116,8 @@ def test_engine_f64_wide_models_match_sklearn_math(native, F, K, merge):
     merge) agrees with the float64 oracle to rel 1e-12 and exact labels."""
     kind = Kind.BINARY if K == 2 else Kind.MULTINOMIAL
     m = LinearModel.random(F, K, seed=F + K, kind=kind)
-    e = _engine(native, max_batch=64, max_features=F, wide_dtype=0, host_merge_rows=16 if merge == "host" else 0)
+    e = _engine(native, max_batch=64, max_features=F, wide_dtype=0, host_merge_rows=16 if merge == "host" else 0,
+                wide_host_merge_blocks=64 if merge == "host" else 0)
     try:
         e.load_model(int(m.kind), m.W, m.b, m.label_json())
         assert e.model_path() == "wide"
