@@ -202,6 +202,7 @@ PYBIND11_MODULE(_C, m) {
         return d;
       },
       py::arg("dt"), py::arg("F"), py::arg("K"));
+  m.def("linear_wide_set_probe", &linear_wide_set_probe, py::arg("probe"));
   m.def("linear_wide_workspace", &linear_wide_workspace, py::arg("B"), py::arg("dt"), py::arg("F"), py::arg("K"));
   m.def(
       "linear_wide",

@@ -201,6 +201,8 @@ struct WidePlan {
   int fsteps = 0;  // steps per wave per split
 };
 WidePlan linear_wide_plan(int dt, int F, int K);
+// measurement hook: later launches stop early (1: after the MFMA loop, 2: before the class merge)
+void linear_wide_set_probe(int probe);
 // workspace (zeroed once; tickets are re-armed in-kernel) for up to B rows
 size_t linear_wide_workspace(int64_t B, int dt, int F, int K);
 // Host class merge (serving, multiclass, B <= 32): block cb writes for row r two 16-byte units at
@@ -215,9 +217,12 @@ struct WideRecOut {
   WideRecord* rec = nullptr;
   uint32_t seq = 0;
 };
+// ws_private: no other launch in flight uses this workspace (the engine gives every batch slot its
+// own), so a direct-dispatched launch may overlap the ones before it (unordered packet).
 void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const double* b, int64_t B, int F, int K,
                         int kind, int32_t* out_idx, double* out_p, void* workspace, size_t ws_bytes, hipStream_t stream,
-                        RecOut ro = RecOut(), WideRecOut hro = WideRecOut(), KernelLauncher* direct = nullptr);
+                        RecOut ro = RecOut(), WideRecOut hro = WideRecOut(), KernelLauncher* direct = nullptr,
+                        bool ws_private = false);
 
 // Multiclass training row stats (gemm_softmax.hip MODE 2), X_aug = [X | 0.. | 1 | 0 x 7] bf16
 // read through its row stride ldx (the first F columns); W: [K, F] bf16; b: [K] f32.

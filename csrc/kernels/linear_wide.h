@@ -62,6 +62,8 @@ struct WideArgs {
   unsigned char* ws;
   int64_t rg_bytes, cnt_bytes, part_bytes;
   int32_t row_groups;
+  int32_t probe;  // measurement only (linear_wide_set_probe): 1 = stop after the MFMA loop, 2 = after
+                  // the block's row states (before the class merge)
 };
 
 template <typename T>
@@ -178,6 +180,10 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     mma(w1, x1, s0 + U);
   }
 
+  if (a.probe == 1) {  // measurement: keep the accumulators alive, store nothing
+    if (acc[0][0] == 12345.678) a.out_p[0] = acc[0][1];
+    return;
+  }
   // ---- the block's tile: the 4 waves' quarters, summed in wave order
 #pragma unroll
   for (int t = 0; t < NB; ++t) red[wave][t][lane] = acc[t];
@@ -227,7 +233,7 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   const bool ovr = a.kind == KIND_OVR;
   const bool binary = a.kind == KIND_BINARY || a.kind == KIND_BINARY_SOFTMAX;
   // the other waves are only needed for an in-kernel class merge (they join its barriers)
-  if (wave != 0 && (binary || a.ncb == 1 || a.hrec != nullptr)) return;
+  if (wave != 0 && (binary || a.ncb == 1 || a.hrec != nullptr || a.probe == 2)) return;
   // ---- epilogue (wave 0): lane holds classes c0 + g + 4r of row r16 of each tile
   WState st[NB];
   if (wave == 0) {
@@ -276,6 +282,10 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
       st[t] = S0;
     }
     if (binary) return;
+    if (a.probe == 2) {
+      if (st[0].m == 12345.678) a.out_p[0] = st[0].s;
+      return;
+    }
     if (a.hrec != nullptr) {  // host merge: one 32-byte record per (class block, row)
 #pragma unroll
       for (int t = 0; t < NB; ++t) {

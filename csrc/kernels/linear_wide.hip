@@ -24,13 +24,17 @@ using wide_plan::row_groups;
 
 }  // namespace
 
+int g_probe = 0;  // measurement hook (linear_wide_set_probe)
+
 WidePlan linear_wide_plan(int dt, int F, int K) { return wide_plan::plan(dt, F, K); }
+
+void linear_wide_set_probe(int probe) { g_probe = probe; }
 
 size_t linear_wide_workspace(int64_t B, int dt, int F, int K) { return wide_plan::workspace(B, dt, F, K); }
 
 void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const double* b, int64_t B, int F, int K,
                         int kind, int32_t* out_idx, double* out_p, void* workspace, size_t ws_bytes, hipStream_t stream,
-                        RecOut ro, WideRecOut hro, KernelLauncher* direct) {
+                        RecOut ro, WideRecOut hro, KernelLauncher* direct, bool ws_private) {
   if (B <= 0) return;
   const WidePlan p = linear_wide_plan(dt, F, K);
   const bool binary = kind == KIND_BINARY || kind == KIND_BINARY_SOFTMAX;
@@ -63,6 +67,7 @@ void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const
   a.hrec = reinterpret_cast<uint4*>(hro.rec);
   a.hseq = hro.seq;
   a.row_groups = rg;
+  a.probe = g_probe;
   const wide_plan::Layout lay = wide_plan::layout(p);
   a.ws = static_cast<unsigned char*>(workspace);
   a.rg_bytes = (int64_t)lay.rg_bytes;
@@ -73,8 +78,9 @@ void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const
   if (direct != nullptr) {
     char name[48];
     std::snprintf(name, sizeof name, "mlapi_wide_%s_nb%d", dt == DT_F64 ? "f64" : "f32", nb2 ? 2 : 1);
-    // the workspace's tickets are re-armed by the kernel: launches that use them stay in order
-    if (direct->launch_kernel(name, &a, sizeof a, grid.x, grid.y, 256, needs_ws)) return;
+    // the workspace's tickets are re-armed by the kernel: launches that share them stay in order
+    // (a workspace private to this launch lets it overlap the previous ones)
+    if (direct->launch_kernel(name, &a, sizeof a, grid.x, grid.y, 256, needs_ws && !ws_private)) return;
   }
   if (dt == DT_F64) {
     if (nb2)

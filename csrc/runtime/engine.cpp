@@ -366,9 +366,12 @@ uint64_t Engine::load_model(int kind, int F, int K, const double* W, const doubl
       }
     }
     if (m->path == PATH_WIDE) {
-      m->ws_wide_bytes = linear_wide_workspace(cfg_.max_batch, m->xdt, F, K);
-      MLAPI_HIP_CHECK(hipMalloc(&m->ws_wide, m->ws_wide_bytes));
-      MLAPI_HIP_CHECK(hipMemset(m->ws_wide, 0, m->ws_wide_bytes));
+      // one workspace per batch slot (256-byte aligned): batches in flight never share tickets, so
+      // their direct-dispatched packets need no barrier and overlap on the GPU
+      m->ws_wide_bytes = (linear_wide_workspace(cfg_.max_batch, m->xdt, F, K) + 255) & ~size_t(255);
+      const size_t total = m->ws_wide_bytes * (size_t)std::max(1, cfg_.slots);
+      MLAPI_HIP_CHECK(hipMalloc(&m->ws_wide, total));
+      MLAPI_HIP_CHECK(hipMemset(m->ws_wide, 0, total));
     }
     MLAPI_HIP_CHECK(hipDeviceSynchronize());
   }
@@ -727,8 +730,8 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
         s.rec_mode = REC_ROWS;
       }
       launch_linear_wide(m.xdt, X, m.ldx, m.dW, static_cast<const double*>(m.db), n, m.F, m.K, m.kind, s.didx,
-                         static_cast<double*>(s.dp), m.ws_wide, m.ws_wide_bytes, stream_, ro, hro,
-                         direct_wide ? &dl : nullptr);
+                         static_cast<double*>(s.dp), static_cast<unsigned char*>(m.ws_wide) + (size_t)si * m.ws_wide_bytes,
+                         m.ws_wide_bytes, stream_, ro, hro, direct_wide ? &dl : nullptr, /*ws_private=*/true);
     } else if (m.path == PATH_GEMV)
       launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_, ro,
                          direct_wide && ro.rec != nullptr ? &dl : nullptr);
