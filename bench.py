@@ -374,7 +374,7 @@ def bench_gemm(args, info):
             X, W = X.float(), W.float()
         op = ops.LinearSplit(B, K, info.device)
     else:
-        forced = {"tiles": 1, "rows": 2, "t32": 3}.get(args.gemm_kernel, 0)
+        forced = {"tiles": 1, "rows": 2, "t32": 3, "t32pk": 9}.get(args.gemm_kernel, 0)
         if forced:
             from mlapi_amd._native import C
 
@@ -508,7 +508,7 @@ def main(argv=None) -> int:
     ap.add_argument("--c1-requests", type=int, default=3000)
     ap.add_argument("--rows", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=1024)
-    ap.add_argument("--gemm-kernel", default="auto", choices=["auto", "split", "tiles", "rows", "t32"],
+    ap.add_argument("--gemm-kernel", default="auto", choices=["auto", "split", "tiles", "rows", "t32", "t32pk"],
                     help="gemm: auto = the planner's choice; split = the class-split small-batch kernel; "
                          "tiles / rows / t32 = that gemm_softmax kernel forced (measurement)")
     ap.add_argument("--gemm-dtype", default="bf16", choices=["bf16", "f32"], help="gemm: f32 runs the split kernel")

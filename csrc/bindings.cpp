@@ -123,6 +123,7 @@ py::dict stats_dict(const EngineStats& s) {
   d["idle_batches"] = s.idle_batches;
   d["lane_batches"] = s.lane_batches;
   d["generic_models"] = s.generic_models;
+  d["xcd_errors"] = s.xcd_errors;
   d["bar_batches"] = s.bar_batches;
   d["direct_dispatch"] = s.direct_dispatch;
   d["direct_device_kernargs"] = s.direct_device_kernargs;
@@ -220,6 +221,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_softmax_xcd_err_offset", &gemm_softmax_xcd_err_offset);
   m.def("xcd_placement_state", &xcd_placement_state, py::arg("device") = 0);
   m.def("xcd_placement_mismatches", &xcd_placement_mismatches, py::arg("device") = 0);
+  m.def("xcd_local_errors", &xcd_local_errors, py::arg("device") = 0);
+  m.def("xcd_local_inject", &xcd_local_inject, py::arg("launches"));
   m.def(
       "linear_split",
       [](int dt, uintptr_t X, int64_t ldx, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind,

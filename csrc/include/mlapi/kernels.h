@@ -180,7 +180,21 @@ size_t gemm_softmax_xcd_err_offset();
 bool xcd_local_allowed(hipStream_t stream);
 int xcd_placement_state(int device);
 int xcd_placement_mismatches(int device);
+// A serving row whose XCD-local merge read a partial written on another XCD comes back with this
+// label (and p = NaN) instead of a silently wrong answer; the engine fails the row and calls
+// xcd_local_report_error, which switches the XCD-local protocol off for the device (the
+// agent-scope protocol from the next launch on) and counts the event (xcd_local_errors).
+constexpr int32_t XCD_BAD_IDX = -2;
+// linear_wide: a row whose class merge waited over 1 s for a class block's state (never expected:
+// the blocks of a launch are co-resident) fails with this label and p = NaN
+constexpr int32_t WIDE_TIMEOUT_IDX = -3;
+void xcd_local_report_error(int device);
+uint64_t xcd_local_errors(int device);
+// test hook: the next `launches` XCD-local launches report every merged row as misplaced
+void xcd_local_inject(int launches);
+int xcd_local_take_inject();
 int linear_split_nsplit(int K);
+constexpr int64_t LINEAR_SPLIT_MAX_ROWS = 2048;  // rows per launch_linear_split call
 // direct: launch through that queue instead of `stream` (the caller keeps every launch that shares
 // the workspace on one of the two; serving completes through records, so nothing else needs the
 // stream's order)

@@ -125,6 +125,7 @@ struct GemmArgs {
   float4* rowstate;        // MODE 4 output: {max, sum, argmax bits, 0} (class-sharded TP)
   unsigned long long* stamps;  // profiling (tools/gemm_phase_probe.py): 8 s_memtime slots per wave
   int xcd_local;               // split merge meets in one XCD's L2 (grid.x % 8 == 0; see xcd_put_partial)
+  int xcd_inject;              // test hook (xcd_local_inject): every merged row reports a misplaced partial
 };
 
 // ---- split-merge protocol (tiles kernels). Default (agent scope): partials stored write-through
@@ -179,13 +180,15 @@ __device__ __forceinline__ float4 get_partial(const GemmArgs& a, int64_t idx) {
   return a.partials[idx];
 }
 // merging block, XCD-local protocol: every partial it merges came from its own XCD's L2
-__device__ __forceinline__ void xcd_verify(const GemmArgs& a, const float4 (&p)[MERGE_MAX], unsigned ns) {
-  if (!a.xcd_local) return;
+// (true: the row's merged state cannot be trusted - MODE 0 then returns XCD_BAD_IDX / NaN for it)
+__device__ __forceinline__ bool xcd_verify(const GemmArgs& a, const float4 (&p)[MERGE_MAX], unsigned ns) {
+  if (!a.xcd_local) return false;
   const unsigned me = my_xcc();
-  bool bad = false;
+  bool bad = a.xcd_inject != 0;
 #pragma unroll
   for (int sp = 0; sp < MERGE_MAX; ++sp) bad |= (unsigned)sp < ns && __float_as_uint(p[sp].w) != me;
   if (bad) __hip_atomic_fetch_or(a.counters + XCD_ERR_SLOT, 1u << me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return bad;
 }
 // the first MERGE_MAX splits' partials of `row`, every load issued before the first use (one
 // round trip; the protocol branch sits outside the loads so none of them waits on another)
@@ -736,7 +739,7 @@ gemm_softmax_kernel(GemmArgs a) {
         const unsigned ns = gridDim.y;
         float4 p[MERGE_MAX];
         get_partials(a, row, ns, p);  // clamped: unconditional
-        xcd_verify(a, p, ns);
+        const bool xbad = xcd_verify(a, p, ns);
         RowState S{p[0].x, p[0].y, __float_as_int(p[0].z)};
 #pragma unroll
         for (int sp = 1; sp < MERGE_MAX; ++sp)  // fixed split order: deterministic
@@ -746,7 +749,8 @@ gemm_softmax_kernel(GemmArgs a) {
           S = merge_state(S, RowState{q.x, q.y, __float_as_int(q.z)}, ovr);
         }
         if constexpr (MODE == 0) {
-          put_result(a.out_idx, a.out_p, a.ro, row, S.bi, ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s);
+          put_result(a.out_idx, a.out_p, a.ro, row, xbad ? XCD_BAD_IDX : S.bi,
+                     xbad ? __builtin_nanf("") : ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s);
         } else if constexpr (MODE == 4) {
           a.rowstate[row] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
         } else {
@@ -786,7 +790,21 @@ struct TileTmp7 {
   unsigned mask;
 };
 
-template <bool OVR>
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+// packed FP32 VALU (measurement variant PK): one v_pk_fma_f32 / v_pk_add_f32
+// per element pair in place of two single-lane ops (asm: the instruction is the experiment)
+__device__ __forceinline__ f32x2_t pk_fma(f32x2_t a, f32x2_t b, f32x2_t c) {
+  f32x2_t d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ f32x2_t pk_add(f32x2_t a, f32x2_t b) {
+  f32x2_t d;
+  asm("v_pk_add_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+
+template <bool OVR, bool PK = false>
 __device__ __forceinline__ void tile_stage7(int stage, const float (&v)[16], int c0, TileState& S, TileTmp7& T) {
   if (stage == 0) {
     float cm = vmax(v[0], v[1]);
@@ -806,14 +824,24 @@ __device__ __forceinline__ void tile_stage7(int stage, const float (&v)[16], int
   } else {
     const int i0 = (stage - 3) * 4;
     float e[4];
+    if constexpr (PK && !OVR) {  // 2 v_pk_fma_f32 + 1 v_pk_add_f32 for 4 fma + 2 adds
+      const f32x2_t l2 = {LOG2E_F, LOG2E_F}, nm = {-T.m2, -T.m2};
+      const f32x2_t t01 = pk_fma(f32x2_t{v[i0], v[i0 + 1]}, l2, nm);
+      const f32x2_t t23 = pk_fma(f32x2_t{v[i0 + 2], v[i0 + 3]}, l2, nm);
+      const f32x2_t e01 = {__builtin_amdgcn_exp2f(t01[0]), __builtin_amdgcn_exp2f(t01[1])};
+      const f32x2_t e23 = {__builtin_amdgcn_exp2f(t23[0]), __builtin_amdgcn_exp2f(t23[1])};
+      const f32x2_t s = pk_add(e01, e23);
+      T.part += s[0] + s[1];
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if constexpr (OVR)
-        e[i] = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-v[i0 + i] * LOG2E_F));
-      else
-        e[i] = __builtin_amdgcn_exp2f(fmaf(v[i0 + i], LOG2E_F, -T.m2));
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (OVR)
+          e[i] = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-v[i0 + i] * LOG2E_F));
+        else
+          e[i] = __builtin_amdgcn_exp2f(fmaf(v[i0 + i], LOG2E_F, -T.m2));
+      }
+      T.part += (e[0] + e[1]) + (e[2] + e[3]);
     }
-    T.part += (e[0] + e[1]) + (e[2] + e[3]);
     if (stage == 6) {
       if constexpr (OVR) {
         S.s += T.part;
@@ -895,7 +923,8 @@ __device__ __forceinline__ bf16x8_t frag32(const unsigned char* smem, const Frag
 
 // MFMAs of chunk cn (LDS buffer BUF -> nxt) with the epilogue of chunk c0 (acc -> S) spread over
 // the k-steps
-template <int KS, int RT, bool OVR, int BUF, int BUF_BYTES, bool EPI = true, int AHEAD = 2, bool PRIO = false>
+template <int KS, int RT, bool OVR, int BUF, int BUF_BYTES, bool EPI = true, int AHEAD = 2, bool PRIO = false,
+          bool PK = false>
 __device__ __forceinline__ void fused32_step(const unsigned char* smem, const FragOff<KS>& fo,
                                              const bf16x8_t (&xf)[RT][2 * KS], int cn, int c_end, int h,
                                              f32x16_t (&nxt)[RT][2], const f32x16_t (&acc)[RT][2], int c0,
@@ -950,7 +979,7 @@ __device__ __forceinline__ void fused32_step(const unsigned char* smem, const Fr
       constexpr int j = decltype(jc)::value;
       if constexpr ((j * K2) / NSTAGE == k) {
         constexpr int rt = j / 14, t = (j % 14) / 7, stg = j % 7;
-        if constexpr (EPI) tile_stage7<OVR>(stg, v[rt][t], c0 + 32 * t, S[rt], T[rt][t]);
+        if constexpr (EPI) tile_stage7<OVR, PK>(stg, v[rt][t], c0 + 32 * t, S[rt], T[rt][t]);
       }
     });
     __builtin_amdgcn_sched_barrier(0);
@@ -978,7 +1007,8 @@ __device__ __forceinline__ void epilogue32(const f32x16_t (&acc)[RT][2], int c0,
 // tools/gemm_phase_probe.py; its outputs are meaningless). It splits the class loop's time into the
 // MFMA / LDS feed and the epilogue: 44.4k of 52.2k cycles per wave are the feed
 // (profiles/r2_gemm/phase_probe_noepi.log).
-template <int KS, int WV, int RT, int MODE, bool OVR, bool EPI = true, int AHEAD = 2, bool PRIO = false>
+template <int KS, int WV, int RT, int MODE, bool OVR, bool EPI = true, int AHEAD = 2, bool PRIO = false,
+          bool PK = false>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(RT == 2 ? 1 : 2, RT == 2 ? 1 : 2))) void
 gemm_softmax32_kernel(GemmArgs a) {
   static_assert(MODE == 0 || MODE == 2 || MODE == 4, "logits mode runs the 16x16 kernel");
@@ -1070,7 +1100,7 @@ gemm_softmax32_kernel(GemmArgs a) {
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 0)
-    fused32_step<KS, RT, OVR, 1, BUF_BYTES, EPI, AHEAD, PRIO>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0,
+    fused32_step<KS, RT, OVR, 1, BUF_BYTES, EPI, AHEAD, PRIO, PK>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0,
                                                         ts);
     c0 += CLASS_CHUNK;
     if (c0 + CLASS_CHUNK >= c_end) {
@@ -1079,7 +1109,7 @@ gemm_softmax32_kernel(GemmArgs a) {
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 1)
-    fused32_step<KS, RT, OVR, 0, BUF_BYTES, EPI, AHEAD, PRIO>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0,
+    fused32_step<KS, RT, OVR, 0, BUF_BYTES, EPI, AHEAD, PRIO, PK>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0,
                                                         ts);
     c0 += CLASS_CHUNK;
   }
@@ -1130,7 +1160,7 @@ gemm_softmax32_kernel(GemmArgs a) {
       const unsigned ns = gridDim.y;
       float4 p[MERGE_MAX];
       get_partials(a, mrow, ns, p);
-      xcd_verify(a, p, ns);
+      const bool xbad = xcd_verify(a, p, ns);
       RowState R{p[0].x, p[0].y, __float_as_int(p[0].z)};
 #pragma unroll
       for (int sp = 1; sp < MERGE_MAX; ++sp)
@@ -1140,7 +1170,8 @@ gemm_softmax32_kernel(GemmArgs a) {
         R = merge_state(R, RowState{pq.x, pq.y, __float_as_int(pq.z)}, ovr);
       }
       if constexpr (MODE == 0) {
-        put_result(a.out_idx, a.out_p, a.ro, mrow, R.bi, ovr ? sigmoidf_(R.m) / R.s : 1.f / R.s);
+        put_result(a.out_idx, a.out_p, a.ro, mrow, xbad ? XCD_BAD_IDX : R.bi,
+                   xbad ? __builtin_nanf("") : ovr ? sigmoidf_(R.m) / R.s : 1.f / R.s);
       } else if constexpr (MODE == 4) {
         a.rowstate[mrow] = make_float4(R.m, R.s, __int_as_float(R.bi), 0.f);
       } else {
@@ -1399,7 +1430,7 @@ int cus_per_xcd() {  // CUs of the current device / 8 XCDs (the dispatcher round
 Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   Plan p;
   if (allow32 && t32_supported(F)) {
-    if (g_force_kernel == 3 || g_force_kernel >= 5) p.k32 = 4;  // 5-8: 32x32 measurement variants
+    if (g_force_kernel == 3 || g_force_kernel >= 5) p.k32 = 4;  // 5-9: 32x32 measurement variants
     else if (g_force_kernel == 0 && B >= 16384) p.k32 = 4;
   }
   // 32 rows per wave (NT = 2) halve the LDS fragment reads per MFMA. It pays once the register
@@ -1453,6 +1484,11 @@ void launch32(const GemmArgs& args, const dim3& grid, int rt, hipStream_t stream
                            args);
         return;
       }
+      if (!o && g_force_kernel == 9) {  // measurement: packed FP32 VALU in the softmax epilogue
+        hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, true, 2, false, true>), grid, dim3(256), 0,
+                           stream, args);
+        return;
+      }
       if (!o && (g_force_kernel == 6 || g_force_kernel == 7)) {  // measurement: fragment prefetch depth 1 / 3
         if (g_force_kernel == 6)
           hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, true, 1>), grid, dim3(256), 0, stream, args);
@@ -1484,6 +1520,7 @@ void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
                     (uint64_t)plan.splits * (uint64_t)args.B * 16u < 0x7fffffffu && xcd_local_allowed(stream))
                        ? 1
                        : 0;
+  args.xcd_inject = args.xcd_local ? xcd_local_take_inject() : 0;
   const dim3 grid((unsigned)(args.xcd_local ? rb_pad : plan.row_blocks), (unsigned)plan.splits);
   if (MODE != 1 && plan.k32) {
     if (F == 64) launch32<MODE, 2>(args, grid, plan.rt32, stream);

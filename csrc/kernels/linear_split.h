@@ -56,6 +56,7 @@ struct SplitArgs {
   float4* partials;        // [row groups][nsplit][32] {m, s, argmax bits, 0}
   unsigned int* xcd_err;   // xcd_local: bit x set when a merging block on XCD x read a partial written elsewhere
   int32_t xcd_local;        // 1-D XCD-ordered grid + L2-local merge protocol (see the header)
+  int32_t xcd_inject;       // test hook (xcd_local_inject): every merged row reports a misplaced partial
   int32_t row_groups;
   int32_t probe;           // measurement only (MLAPI_SPLIT_PROBE): 1 = stop after the block merge, 2 = after the partial stores
   // Host merge (serving, one row group): each block publishes its per-row states as 16-byte
@@ -184,6 +185,7 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
   const int64_t row = row0 + l;
   const bool live = l < NB * 16 && row < a.B;
   SState S{-INFINITY, 0.f, 0x7fffffff};
+  bool xbad = false;  // XCD-local merge read a partial written on another XCD (or the test hook)
   if (l < NB * 16) {
     const float4 v0 = red[0][l];
     S = SState{v0.x, v0.y, __float_as_int(v0.z)};
@@ -262,16 +264,19 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
         unsigned me;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(me));
         me &= 15;
-        bool bad = false;
+        bool bad = a.xcd_inject != 0;
 #pragma unroll
         for (int u = 0; u < 16; ++u) bad |= sp0 + u < a.nsplit && __float_as_uint(v[u].w) != me;
         if (bad) __hip_atomic_fetch_or(a.xcd_err, 1u << me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        xbad |= bad;
       }
     }
   }
   if (!live) return;
   const float p = OVR ? ssigmoid(S.m) / S.s : 1.f / S.s;
-  put_result(a.out_idx, a.out_p, a.ro, row, S.bi, p);
+  // a misplaced merge never answers: the row comes back as XCD_BAD_IDX / NaN (the engine fails it
+  // and switches the XCD-local protocol off)
+  put_result(a.out_idx, a.out_p, a.ro, row, xbad ? XCD_BAD_IDX : S.bi, xbad ? __builtin_nanf("") : p);
 }
 
 }  // namespace split

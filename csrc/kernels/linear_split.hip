@@ -15,6 +15,7 @@ namespace {
 // workspace: [64 row-group counters (B <= 2048)] [xcd error word at byte 256] [pad] [partials]
 constexpr size_t COUNTER_REGION = 512;
 constexpr size_t MAX_ROW_GROUPS = 64;
+static_assert(MAX_ROW_GROUPS * split::ROWS_PER_GROUP == (size_t)LINEAR_SPLIT_MAX_ROWS, "split row cap");
 constexpr size_t XCD_ERR_OFFSET = 256;
 
 template <typename T, int KS, int NB, bool OVR>
@@ -81,7 +82,7 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
     throw std::invalid_argument("linear_split: X and W must be 16-byte aligned");
   const int rg = row_groups(B), ns = nsplits(K);
   if (rg > (int)MAX_ROW_GROUPS)
-    throw std::invalid_argument("linear_split: B too large (<= 2048 rows per launch)");
+    throw std::invalid_argument("linear_split: B too large (<= LINEAR_SPLIT_MAX_ROWS rows per launch)");
   if (sro.rec != nullptr && rg != 1) throw std::invalid_argument("linear_split: host merge needs B <= 32");
   if (sro.rec == nullptr && ns > 1 && ws_bytes < linear_split_workspace(B, K))
     throw std::invalid_argument("linear_split: workspace too small (zero it once)");
@@ -112,6 +113,7 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
     return e ? atoi(e) : 1;
   }();
   a.xcd_local = (xcd_env != 0 && ns > 1 && sro.rec == nullptr && xcd_local_allowed(stream)) ? 1 : 0;
+  a.xcd_inject = a.xcd_local ? xcd_local_take_inject() : 0;
   a.row_groups = rg;
   a.xcd_err = reinterpret_cast<unsigned int*>(static_cast<unsigned char*>(workspace) + XCD_ERR_OFFSET);
   // XCD-ordered 1-D grid: 8 XCDs x ceil(rg / 8) row groups x ns splits (blocks past rg exit at once)

@@ -15,14 +15,15 @@
 //    for the e-th MFMA of the step - the same k permutation for A (W) and B (X);
 //  * loads in chunks of U = 4 steps, two chunks in flight (double buffer);
 //  * the 4 waves' tiles are summed through LDS in fixed order; feature splits (nfs > 1) are summed
-//    by the last-arriving block of the class block (write-through partials, one ticket, one
-//    agent-scope acquire: Guideline 16), in split order;
+//    by the last-arriving block of the class block (write-through partials, one ticket, and
+//    agent-coherent sc1 loads of them - or one agent-scope acquire: Guideline 16), in split order;
 //  * epilogue per row: bias, then the sklearn epilogue of `kind` (K = 1 binary kinds: z > 0 and
 //    sigma(|z|) / the two-class softmax, exactly as linear_rows.h); multiclass kinds reduce the
 //    block's 16 classes to a row state {max, sum exp(z - max) | sum sigmoid(z), first argmax} and
 //    class blocks are merged either on the host (one 32-byte record per block and row, the
 //    engine's completer merges in double in block order) or in-kernel by the last-arriving block
-//    of the row group (ticket + acquire), in block order. Everything in f64.
+//    of the row group (ticket + sc1 loads), 8 lanes per row: max by compares first, then every
+//    block's rescaled sum in parallel and a fixed-order sum tree. Everything in f64.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -56,12 +57,14 @@ struct WideArgs {
   uint4* hrec;             // host class merge: [ncb][32 rows][2] 16-byte units {seq, bi, m} {seq, 0, s}
   uint32_t hseq;
   // Workspace, one region per row group (the layout does not depend on B, so launches of any size
-  // share it): [ncb split tickets | 1 class ticket] (zero, re-armed by the last arrivers), then
-  // [ncb][nfs][2 * 4 * 64] f64 split partial tiles (nfs > 1), then [ncb][32 rows][4] f64 row
-  // states {m, s, argmax bits, 0}.
+  // share it): [ncb split tickets | 1 spare] (zero, re-armed by the last arrivers), then
+  // [ncb][nfs][2 * 4 * 64] f64 split partial tiles (nfs > 1), then [ncb][32 rows] 32-byte row
+  // state granules {m, argmax, epoch} {s, epoch, 0}.
   unsigned char* ws;
   int64_t rg_bytes, cnt_bytes, part_bytes;
   int32_t row_groups;
+  int32_t sc1_loads;  // feature-split partials: agent-coherent sc1 loads instead of an acquire
+  uint32_t epoch;     // != 0, distinct per launch: the tag of this launch's class-merge granules
   int32_t probe;  // measurement only (linear_wide_set_probe): 1 = stop after the MFMA loop, 2 = after
                   // the block's row states (before the class merge)
 };
@@ -97,6 +100,17 @@ __device__ __forceinline__ WState wmerge(WState a, WState b, bool ovr) {
 
 __device__ __forceinline__ WState wshfl(WState a, int off) {
   return WState{__shfl_xor(a.m, off, 64), __shfl_xor(a.s, off, 64), __shfl_xor(a.bi, off, 64)};
+}
+
+typedef __attribute__((address_space(1))) unsigned int gu32_t;
+typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+
+// agent-coherent 8-byte load (global_load_dwordx2 sc1): bypasses this CU's L1, so bytes another
+// workgroup stored sc1 and drained before its ticket add need no acquire fence (MI355X_MICROARCH.md
+// visibility table, first row: sc1 stores, one agent-scope ticket counter, last arriver loads)
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load((gu64_t*)const_cast<double*>(p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
 }
 
 __device__ __forceinline__ double wsigmoid(double z) { return 1.0 / (1.0 + exp(-z)); }
@@ -142,6 +156,10 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   for (int t = 0; t < NB; ++t)
     xp[t] = static_cast<const T*>(a.X) + min(row0 + t * 16 + r16, (int64_t)a.B - 1) * a.ldx + f0;
 
+  // the bias of this lane's classes, loaded now so its latency hides under the MFMA loop
+  double bz[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bz[r] = a.bias[min(c0 + g + 4 * r, a.K - 1)];
   wd4_t acc[NB];
 #pragma unroll
   for (int t = 0; t < NB; ++t) acc[t] = wd4_t{0.0, 0.0, 0.0, 0.0};
@@ -194,7 +212,6 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   }
   // ---- feature splits: the last-arriving block of (row group, class block) sums them in order
   if (a.nfs > 1) {
-    typedef __attribute__((address_space(1))) unsigned int gu32_t;
     unsigned char* rgw = a.ws + (int64_t)rgi * a.rg_bytes;
     double* part = reinterpret_cast<double*>(rgw + a.cnt_bytes) + ((int64_t)cb * a.nfs) * (2 * 4 * 64);
     if (wave == 0) {
@@ -215,16 +232,24 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     }
     __syncthreads();
     if (!bcast) return;  // uniform per block
-    if (wave == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (wave == 0) {  // only wave 0 (the adder) reads the partials
+      if (!a.sc1_loads) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
 #pragma unroll
       for (int t = 0; t < NB; ++t) acc[t] = wd4_t{0.0, 0.0, 0.0, 0.0};
       for (int f = 0; f < a.nfs; ++f) {  // split order: deterministic
 #pragma unroll
         for (int t = 0; t < NB; ++t) {
           const double* src = part + (int64_t)f * (2 * 4 * 64) + t * 256 + lane * 4;
-          const wd4_t v = *reinterpret_cast<const wd4_t*>(src);
+          wd4_t v;
+          if (a.sc1_loads) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = ld_sc1(src + k);
+          } else {
+            v = *reinterpret_cast<const wd4_t*>(src);
+          }
           acc[t] += v;
         }
       }
@@ -233,8 +258,11 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   const bool ovr = a.kind == KIND_OVR;
   const bool binary = a.kind == KIND_BINARY || a.kind == KIND_BINARY_SOFTMAX;
   // the other waves are only needed for an in-kernel class merge (they join its barriers)
-  if (wave != 0 && (binary || a.ncb == 1 || a.hrec != nullptr || a.probe == 2)) return;
-  // ---- epilogue (wave 0): lane holds classes c0 + g + 4r of row r16 of each tile
+  if (wave != 0 && (binary || a.ncb == 1 || a.hrec != nullptr || a.probe == 2 || cb != 0)) return;
+  // ---- epilogue (wave 0): lane holds classes c0 + g + 4r of row r16 of each tile. The row's
+  // block state {max, sum over the block's classes of exp(z - max) | sigmoid(z), first argmax}:
+  // the max (and argmax) first, by compares only, then the 16 exponentials in parallel against
+  // it and a fixed-order sum - no dependent chain of exponentials.
   WState st[NB];
   if (wave == 0) {
 #pragma unroll
@@ -242,7 +270,7 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
       const int64_t row = row0 + t * 16 + r16;
       if (binary) {
         if (g == 0 && row < a.B) {  // class 0 = the single logit
-          const double z = acc[t][0] + a.bias[0];
+          const double z = acc[t][0] + bz[0];
           double pm;
           if (a.kind == KIND_BINARY) {
             const double p1 = 1.0 / (1.0 + exp(-z)), p0 = 1.0 - p1;
@@ -260,26 +288,35 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
       bool nan = false;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int c = c0 + g + 4 * r;
-        z[r] = c < a.K ? acc[t][r] + a.bias[c] : -INFINITY;
+        z[r] = c0 + g + 4 * r < a.K ? acc[t][r] + bz[r] : -INFINITY;
         nan |= isnan(z[r]);
       }
-      WState S0{z[0], 0.0, c0 + g};
+      double m = z[0];
+      int bi = c0 + g;
 #pragma unroll
       for (int r = 1; r < 4; ++r)
-        if (z[r] > S0.m) {
-          S0.m = z[r];
-          S0.bi = c0 + g + 4 * r;
+        if (z[r] > m) {
+          m = z[r];
+          bi = c0 + g + 4 * r;
         }
+#pragma unroll
+      for (int off = 16; off <= 32; off <<= 1) {  // the row's 16 classes sit in lanes r16 + 16 g
+        const double om = __shfl_xor(m, off, 64);
+        const int ob = __shfl_xor(bi, off, 64);
+        if (om > m || (om == m && ob < bi)) {
+          m = om;
+          bi = ob;
+        }
+      }
       double s = 0.0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) s += ovr ? (z[r] == -INFINITY ? 0.0 : wsigmoid(z[r])) : (S0.m == -INFINITY ? 0.0 : exp(z[r] - S0.m));
-      S0.s = s;
-      if (S0.m == -INFINITY) S0.bi = 0x7fffffff;
-      if (nan) S0.m = NAN;  // a NaN logit makes the row's probability NaN (500, like sklearn -> json)
-      S0 = wmerge(S0, wshfl(S0, 16), ovr);
-      S0 = wmerge(S0, wshfl(S0, 32), ovr);
-      st[t] = S0;
+      for (int r = 0; r < 4; ++r) s += ovr ? wsigmoid(z[r]) : exp(z[r] - m);  // masked classes: z = -inf -> 0
+      // a NaN logit makes the row's probability NaN (500, like sklearn -> json)
+      const uint64_t nanm = __ballot(nan) >> r16;
+      if (nanm & 0x0001000100010001ull) s = NAN;
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      st[t] = WState{m, s, bi};
     }
     if (binary) return;
     if (a.probe == 2) {
@@ -307,7 +344,11 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
       return;
     }
   }
-  // ---- class blocks: the last-arriving block of the row group merges them in block order
+  // ---- class blocks: every block publishes its rows' states as two tagged 16-byte granules
+  // {m, argmax, epoch} {s, epoch, 0} (write-through sc1 stores; the data is the flag, so no drain,
+  // ticket or fence: Guideline 16 R2), and block 0 of the row group polls them with sc1 loads
+  // and merges. All blocks of a serving launch are co-resident (<= a few hundred blocks of 4
+  // waves), and the poll is bounded (1 s, then the rows fail with WIDE_TIMEOUT_IDX).
   unsigned char* rgw2 = a.ws + (int64_t)rgi * a.rg_bytes;
   double* states = reinterpret_cast<double*>(rgw2 + a.cnt_bytes + a.part_bytes);
   if (wave == 0) {
@@ -316,56 +357,115 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
       const int rl = t * 16 + r16;
       if (g == 0) {
         double* dst = states + ((int64_t)cb * RG + rl) * 4;
-        st16_sc1(dst, __builtin_bit_cast(wu4_t, wd2_t{st[t].m, st[t].s}));
-        st16_sc1(dst + 2, wu4_t{(uint32_t)st[t].bi, 0u, 0u, 0u});
+        const uint64_t mu = __builtin_bit_cast(uint64_t, st[t].m), su = __builtin_bit_cast(uint64_t, st[t].s);
+        st16_sc1(dst, wu4_t{(uint32_t)mu, (uint32_t)(mu >> 32), (uint32_t)st[t].bi, a.epoch});
+        st16_sc1(dst + 2, wu4_t{(uint32_t)su, (uint32_t)(su >> 32), 0u, a.epoch});
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      typedef __attribute__((address_space(1))) unsigned int gu32_t;
-      gu32_t* ctr = (gu32_t*)(reinterpret_cast<unsigned int*>(rgw2) + a.ncb);
-      const unsigned tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = tk == (unsigned)a.ncb - 1;
-      if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      bcast = last;
-    }
   }
-  __syncthreads();
-  if (!bcast) return;
-  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // 256 threads: row = tid & 31, part = tid >> 5 merges class blocks part, part + 8, ... in order
-  __shared__ double mrg[8][RG][3];
-  const int rl = threadIdx.x & 31, part = threadIdx.x >> 5;
-  WState M{-INFINITY, 0.0, 0x7fffffff};
-  for (int b0 = part; b0 < a.ncb; b0 += 8 * 8) {
-    wd2_t ms[8];
-    uint32_t bis[8];
+  if (cb != 0) return;
+  // block 0, 256 threads: row rl = tid >> 3 (8 rows per wave), part = tid & 7 takes class blocks
+  // part, part + 8, ...: the row max by compares and 3 xor shuffles, then every block's
+  // s * exp(m - max) in parallel, summed per lane in block order and over the 8 lanes in a
+  // fixed xor tree (deterministic).
+  const int rows = (int)min<int64_t>((int64_t)a.B - row0, 16 * NB);
+  if (8 * wave >= rows) return;  // wave-uniform: no rows of this wave in the launch
+  const int rl = threadIdx.x >> 3, part = threadIdx.x & 7;
+  const bool live = rl < rows;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)states, 0, a.ncb * RG * 32, 0x00020000);
+  auto ldg = [&](int b, int h) -> wu4_t {  // sc1 (aux 16): past this CU's L1, agent-coherent
+    return __builtin_bit_cast(wu4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, (b * RG + rl) * 32 + h * 16, 0, 16));
+  };
+  constexpr int MU = 8;  // states per lane held in registers (ncb <= 64: one pass)
+  const uint64_t t0 = wall_clock64();
+  bool timeout = false;
+  // wait until every granule this wave merges carries this launch's epoch
+  wu4_t g1[MU], g2[MU];
+  for (int b0 = 0; b0 < a.ncb; b0 += 8 * MU) {
+    for (;;) {
+      bool ok = true;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int b = min(b0 + u * 8, a.ncb - 1);
-      const double* src = states + ((int64_t)b * RG + rl) * 4;
-      ms[u] = *reinterpret_cast<const wd2_t*>(src);
-      bis[u] = *reinterpret_cast<const uint32_t*>(src + 2);
+      for (int u = 0; u < MU; ++u) {
+        const int b = b0 + part + 8 * u;
+        if (live && b < a.ncb) {
+          g1[u] = ldg(b, 0);
+          g2[u] = ldg(b, 1);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < MU; ++u) {
+        const int b = b0 + part + 8 * u;
+        if (live && b < a.ncb) ok &= g1[u][3] == a.epoch && g2[u][3] == a.epoch;
+      }
+      if (__all(ok)) break;
+      if (wall_clock64() - t0 > 100000000ull) {  // 1 s at 100 MHz: a block never ran
+        timeout = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");  // the next pass loads again
     }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (b0 + u * 8 < a.ncb) M = wmerge(M, WState{ms[u][0], ms[u][1], (int)bis[u]}, ovr);
+    if (timeout) break;
   }
-  mrg[part][rl][0] = M.m;
-  mrg[part][rl][1] = M.s;
-  mrg[part][rl][2] = __builtin_bit_cast(double, (uint64_t)(uint32_t)M.bi);
-  __syncthreads();
-  if (threadIdx.x >= RG) return;
-  // parts hold interleaved block sets; merging them in part order is a fixed order (deterministic)
-  WState R{mrg[0][rl][0], mrg[0][rl][1], (int)(uint32_t)__builtin_bit_cast(uint64_t, mrg[0][rl][2])};
+  auto gm = [](const wu4_t& v) { return __builtin_bit_cast(double, (uint64_t)v[0] | ((uint64_t)v[1] << 32)); };
+  double M = -INFINITY, SS = 0.0;
+  int BI = 0x7fffffff;
+  bool nan = false;
+  auto reduce_max = [&]() {
 #pragma unroll
-  for (int p = 1; p < 8; ++p)
-    R = wmerge(R, WState{mrg[p][rl][0], mrg[p][rl][1], (int)(uint32_t)__builtin_bit_cast(uint64_t, mrg[p][rl][2])},
-               ovr);
+    for (int off = 1; off <= 4; off <<= 1) {
+      const double om = __shfl_xor(M, off, 64);
+      const int ob = __shfl_xor(BI, off, 64);
+      if (om > M || (om == M && ob < BI)) {
+        M = om;
+        BI = ob;
+      }
+    }
+  };
+  if (a.ncb <= 8 * MU) {  // the last poll's granules are the states
+#pragma unroll
+    for (int u = 0; u < MU; ++u) {
+      const int b = part + 8 * u;
+      if (live && b < a.ncb) {
+        const double m = gm(g1[u]);
+        const int bi = (int)g1[u][2];
+        nan |= isnan(m);
+        if (m > M || (m == M && bi < BI)) {
+          M = m;
+          BI = bi;
+        }
+      }
+    }
+    reduce_max();
+#pragma unroll
+    for (int u = 0; u < MU; ++u)
+      if (live && part + 8 * u < a.ncb) SS += ovr ? gm(g2[u]) : gm(g2[u]) * exp(gm(g1[u]) - M);
+  } else if (live) {  // very wide K: every granule has arrived; a max pass, then a sum pass
+    for (int b = part; b < a.ncb; b += 8) {
+      const wu4_t v = ldg(b, 0);
+      const double m = gm(v);
+      nan |= isnan(m);
+      if (m > M || (m == M && (int)v[2] < BI)) {
+        M = m;
+        BI = (int)v[2];
+      }
+    }
+    reduce_max();
+    for (int b = part; b < a.ncb; b += 8) SS += ovr ? gm(ldg(b, 1)) : gm(ldg(b, 1)) * exp(gm(ldg(b, 0)) - M);
+  } else {
+    reduce_max();
+  }
+  if (nan) SS = NAN;
+  SS += __shfl_xor(SS, 1, 64);
+  SS += __shfl_xor(SS, 2, 64);
+  SS += __shfl_xor(SS, 4, 64);
   const int64_t row = row0 + rl;
-  if (row < a.B) finish_row(a, row, R.bi, ovr ? wsigmoid(R.m) / R.s : 1.0 / R.s);
+  if (part == 0 && live) {
+    if (timeout)
+      finish_row(a, row, WIDE_TIMEOUT_IDX, NAN);
+    else
+      finish_row(a, row, BI, ovr ? wsigmoid(M) / SS : 1.0 / SS);
+  }
 }
 
 }  // namespace wide

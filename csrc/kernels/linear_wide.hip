@@ -2,7 +2,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "linear_wide.h"
@@ -25,6 +27,16 @@ using wide_plan::row_groups;
 }  // namespace
 
 int g_probe = 0;  // measurement hook (linear_wide_set_probe)
+
+// MLAPI_WIDE_ACQUIRE=1: read the in-launch hand-offs behind an agent acquire fence instead of
+// with sc1 loads (the A/B of docs/PERFORMANCE.md)
+static int sc1_loads() {
+  static const int v = [] {
+    const char* e = std::getenv("MLAPI_WIDE_ACQUIRE");
+    return (e != nullptr && e[0] == '1') ? 0 : 1;
+  }();
+  return v;
+}
 
 WidePlan linear_wide_plan(int dt, int F, int K) { return wide_plan::plan(dt, F, K); }
 
@@ -68,6 +80,10 @@ void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const
   a.hseq = hro.seq;
   a.row_groups = rg;
   a.probe = g_probe;
+  a.sc1_loads = sc1_loads();
+  static std::atomic<uint32_t> epochs{0};  // class-merge granule tags: distinct per launch, never 0
+  a.epoch = epochs.fetch_add(1, std::memory_order_relaxed) + 1;
+  if (a.epoch == 0) a.epoch = epochs.fetch_add(1, std::memory_order_relaxed) + 1;
   const wide_plan::Layout lay = wide_plan::layout(p);
   a.ws = static_cast<unsigned char*>(workspace);
   a.rg_bytes = (int64_t)lay.rg_bytes;

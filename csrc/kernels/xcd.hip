@@ -66,6 +66,29 @@ bool xcd_local_allowed(hipStream_t stream) {
   return g_state[dev].load() == 1;
 }
 
+std::atomic<uint64_t> g_errors[MAX_DEVICES];
+std::atomic<int> g_inject{0};
+
+void xcd_local_report_error(int device) {
+  if (device < 0 || device >= MAX_DEVICES) return;
+  g_state[device].store(2, std::memory_order_release);
+  g_errors[device].fetch_add(1);
+}
+
+uint64_t xcd_local_errors(int device) {
+  if (device < 0 || device >= MAX_DEVICES) return 0;
+  return g_errors[device].load();
+}
+
+void xcd_local_inject(int launches) { g_inject.store(launches); }
+
+int xcd_local_take_inject() {
+  int v = g_inject.load(std::memory_order_relaxed);
+  while (v > 0 && !g_inject.compare_exchange_weak(v, v - 1)) {
+  }
+  return v > 0 ? 1 : 0;
+}
+
 int xcd_placement_state(int device) {
   if (device < 0 || device >= MAX_DEVICES) return 0;
   return g_state[device].load();

@@ -747,9 +747,17 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
         s.rec_mode = REC_SPLITS;
         s.rec_nsplit = ns;
       }
-      launch_linear_split(m.xdt, X, m.ldx, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
-                          static_cast<float*>(s.dp), m.ws_split, m.ws_split_bytes, stream_, ro, sro,
-                          direct_wide ? &dl : nullptr);
+      // one launch covers at most LINEAR_SPLIT_MAX_ROWS rows (its ticket region): larger batches
+      // (max_batch above it) go in row chunks, in order on one queue, sharing the workspace
+      for (int64_t r0 = 0; r0 < n; r0 += LINEAR_SPLIT_MAX_ROWS) {
+        const int64_t nb = std::min<int64_t>(LINEAR_SPLIT_MAX_ROWS, n - r0);
+        RecOut roc = ro;
+        if (roc.rec != nullptr) roc.rec += r0;
+        launch_linear_split(m.xdt, static_cast<const unsigned char*>(X) + (size_t)r0 * m.ldx * dtype_size(m.xdt),
+                            m.ldx, m.dW, static_cast<const float*>(m.db), nb, m.ldx, m.K, m.kind, s.didx + r0,
+                            static_cast<float*>(s.dp) + r0, m.ws_split, m.ws_split_bytes, stream_, roc, sro,
+                            direct_wide ? &dl : nullptr);
+      }
     } else
       launch_gemm_softmax(X, m.dW, static_cast<const float*>(m.db), n, m.ldx, m.K, m.kind, s.didx,
                           static_cast<float*>(s.dp), m.ws, m.ws_bytes, stream_, ro);
@@ -995,6 +1003,7 @@ const int32_t* Engine::collect(Slot& s, std::vector<int32_t>& st, std::vector<do
       idx[i] = r.idx;
       pd[i] = r.p;
     }
+    xcd_check(idx.data(), st, pd);
     return idx.data();
   }
   if (s.model->pdt == DT_F64) {
@@ -1003,7 +1012,29 @@ const int32_t* Engine::collect(Slot& s, std::vector<int32_t>& st, std::vector<do
     const float* pf = static_cast<const float*>(s.hp);
     for (size_t i = 0; i < n; ++i) pd[i] = pf[i];
   }
+  xcd_check(s.hidx, st, pd);
   return s.hidx;
+}
+
+// Rows an XCD-local split merge marked as misplaced (XCD_BAD_IDX: a partial came from another
+// XCD's L2, so the merged state may be stale) fail with ST_DEVICE_ERROR instead of answering, and
+// the protocol is switched off for the device: every later launch uses the agent-scope merge.
+void Engine::xcd_check(const int32_t* idx, std::vector<int32_t>& st, std::vector<double>& pd) {
+  uint64_t bad = 0, timeouts = 0;
+  for (size_t i = 0; i < st.size(); ++i)
+    if (idx[i] == XCD_BAD_IDX || idx[i] == WIDE_TIMEOUT_IDX) {
+      st[i] = ST_DEVICE_ERROR;
+      pd[i] = 0.0;
+      ++(idx[i] == XCD_BAD_IDX ? bad : timeouts);
+    }
+  if (timeouts != 0)
+    std::fprintf(stderr, "[mlapi] wide class merge timed out: %llu row(s) failed\n", (unsigned long long)timeouts);
+  if (bad == 0) return;
+  xcd_local_report_error(cfg_.device);
+  std::fprintf(stderr, "[mlapi] XCD-local split merge read a misplaced partial: %llu row(s) failed, protocol off\n",
+               (unsigned long long)bad);
+  std::lock_guard<std::mutex> lk(st_mu_);
+  stats_.xcd_errors += bad;
 }
 
 namespace {

@@ -237,6 +237,8 @@ struct EngineStats {
   uint64_t idle_batches = 0;        // batches run by the submitting thread (run_idle)
   uint64_t lane_batches = 0;        // batches dispatched by IO threads through lanes (Lane::submit)
   uint64_t generic_models = 0;      // models loaded onto the scalar GENERIC kernel (a warning is logged)
+  uint64_t xcd_errors = 0;          // rows failed because an XCD-local split merge read a misplaced partial
+                                    // (the protocol is then off for the device: linear_split.h, xcd.hip)
   uint64_t bar_batches = 0;         // wide batches whose rows were written into HBM through the BAR
   bool direct_dispatch = false;     // the direct queue is up
   bool direct_device_kernargs = false;  // ... and its kernarg ring is in device memory
@@ -363,6 +365,7 @@ class Engine {
   void wait_done(Slot& s);
   // The launched slot's results -> idx / p (from the records or the output arrays).
   const int32_t* collect(Slot& s, std::vector<int32_t>& st, std::vector<double>& pd, std::vector<int32_t>& idx);
+  void xcd_check(const int32_t* idx, std::vector<int32_t>& st, std::vector<double>& pd);
 
   EngineConfig cfg_;
   std::shared_ptr<const Model> model_;

@@ -29,6 +29,7 @@ void launch_gemm_softmax(const void*, const void*, const float*, int64_t, int, i
 bool linear_split_supported(int, int) { return false; }
 size_t linear_split_workspace(int64_t, int) { return 0; }
 int linear_split_nsplit(int K) { return (K + 63) / 64; }
+void xcd_local_report_error(int) {}
 void launch_linear_split(int, const void*, int64_t, const void*, const float*, int64_t, int, int, int, int32_t*, float*,
                          void*, size_t, hipStream_t, RecOut, SplitRecOut, KernelLauncher*) {
   unreachable("launch_linear_split");

@@ -79,6 +79,10 @@ def render(engine_stats: Optional[dict] = None, server_stats: Optional[dict] = N
             out += ["# HELP mlapi_generic_path_models Models loaded onto the scalar GENERIC kernel (no MFMA path for the shape).",
                     "# TYPE mlapi_generic_path_models counter"]
             _line(out, "mlapi_generic_path_models", es["generic_models"], labels)
+        if "xcd_errors" in es:
+            out += ["# HELP mlapi_xcd_merge_errors_total Rows failed because an XCD-local split merge read a misplaced partial.",
+                    "# TYPE mlapi_xcd_merge_errors_total counter"]
+            _line(out, "mlapi_xcd_merge_errors_total", es["xcd_errors"], labels)
         if "lane_batches" in es:
             out += ["# HELP mlapi_lane_batches_total Batches IO threads dispatched themselves through engine lanes.",
                     "# TYPE mlapi_lane_batches_total counter"]

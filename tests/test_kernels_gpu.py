@@ -84,11 +84,12 @@ def test_gemv_binary_large_stream():
     torch.testing.assert_close(p, torch.sigmoid(z.abs()), rtol=1e-4, atol=1e-4)
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "tiles", "rows", "t32"])
+@pytest.fixture(params=[0, 1, 2, 3, 9], ids=["auto", "tiles", "rows", "t32", "t32pk"])
 def gemm_kernel(request):
     """Run a multiclass test under the automatic plan and with each kernel forced (tiles: the
     LDS-staged, chunk-pipelined 16x16x32 kernel; rows: the row-group kernel; t32: the 32x32x16
-    large-batch kernel, F in {64, 128, 256}, else tiles)."""
+    large-batch kernel, F in {64, 128, 256}, else tiles; t32pk: its packed-FP32-epilogue
+    measurement variant at F = 256, multinomial - otherwise t32)."""
     from mlapi_amd._native import C
 
     C().gemm_softmax_force_plan(0, 0, request.param)

@@ -10,7 +10,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").environ.get("GRAFT_REPO_ROOT", "."))
 from mlapi_amd._native import C  # noqa: E402
 from mlapi_amd.models.linear import Kind, LinearModel  # noqa: E402
 from mlapi_amd.ops.linear import LinearWide  # noqa: E402
