@@ -455,8 +455,12 @@ def bench_train_softmax(args, info):
     elapsed, _ = _timed(info, lambda: run(args.steps))
     value = info.world * B * args.steps / elapsed
     flops = 3 * 2 * B * K * tr.F_aug * info.world * args.steps / elapsed  # 2 logits passes + dW
+    # F <= 512: row stats + fused G/dW + slab sum/update; wider: row stats with G (softmax_rows_kernel
+    # MODE 5) + G^T X_aug + slab sum/update (MLAPI_WIDE_TRAIN_5L=1: round 3's five launches)
+    launches = 5 if tr.Fk > 512 and os.environ.get("MLAPI_WIDE_TRAIN_5L") == "1" else 3
     extra = {"final_loss": tr.last_loss(), "tflops_incl_recompute": flops / 1e12, "dp_exchange": tr.dp_exchange,
-             "launches_per_step": 3 if tr.dp_exchange in ("fused-p2p", "local") else 4,
+             "launches_per_step": launches + (0 if tr.dp_exchange in ("fused-p2p", "local") else 1),
+             "kernel_width": tr.Fk,
              "two_shot": os.environ.get("MLAPI_DP_TWO_SHOT", "auto")}
     extra.update(_replica_evidence(tr, info))
     return ("train_softmax_samples_per_sec", value, "samples/s", elapsed, extra,
@@ -518,7 +522,7 @@ def main(argv=None) -> int:
     ap.add_argument("--train-batch", type=int, default=1 << 18)
     ap.add_argument("--shards", type=int, default=8)
     ap.add_argument("--softmax-batch", type=int, default=1 << 16)
-    ap.add_argument("--softmax-features", type=int, default=256, help="train_softmax: F (<= 512)")
+    ap.add_argument("--softmax-features", type=int, default=256, help="train_softmax: F (any: <= 512 the fused G/dW kernel, wider the 3-launch wide path)")
     ap.add_argument("--cpu", action="store_true", help="force the CPU backend (testing without a GPU)")
     ap.add_argument("--pin", default="auto", choices=["auto", "on", "off"],
                     help="pin this rank to its share of physical cores on its GPU's NUMA node, server "

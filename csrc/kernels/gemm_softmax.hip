@@ -1190,7 +1190,11 @@ gemm_softmax32_kernel(GemmArgs a) {
 // at the end, in wave order (deterministic). The feature dimension is looped in slices of KS * 32
 // (F <= 256: one slice, X kept in registers; wider F: 256-feature slices with X reloaded per slice
 // from L2), so any F that is a multiple of 256 (or a power of two <= 256) runs in ONE launch with
-// no split-K partials and no extra merge pass. MODE: 0 predict, 1 logits, 2 row stats, 4 row state.
+// no split-K partials and no extra merge pass. MODE: 0 predict, 1 logits, 2 row stats, 4 row state,
+// 5 training G: the row stats, then (same block, LDS-held lse) a second pass over the class chunks
+// that recomputes the logits and writes G = softmax(z) - onehot(y) (OvR: sigmoid(z) - onehot) as
+// bf16 [B][Kp] plus the block's {loss, correct} - the wide-F training step's first launch, so the
+// B x K logits never go through HBM (softmax_grad_wide.hip).
 constexpr int ROWS_MAX_WAVES = 8;
 
 struct RowsArgs {
@@ -1207,13 +1211,24 @@ struct RowsArgs {
   float* Z;
   float2* rowstat;
   float4* rowstate;
+  // MODE 5
+  const int32_t* y;
+  uint16_t* G;  // [B][Kp] bf16, columns K..Kp-1 written 0
+  int Kp;
+  float* stat_slabs;  // [gridDim.x][2] {loss, correct}
 };
+
+__device__ __forceinline__ uint16_t bf16_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
 
 template <int KS, int NT, int MODE, bool OVR>
 __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
   constexpr int ROWS = 16 * NT;
   constexpr int SLICE = KS * 32;
   __shared__ float4 part[ROWS_MAX_WAVES][ROWS];
+  __shared__ float lse_s[MODE == 5 ? ROWS : 1], hit_s[MODE == 5 ? ROWS : 1], wsum_s[MODE == 5 ? ROWS_MAX_WAVES : 1];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = blockDim.x >> 6;
@@ -1241,9 +1256,9 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) st[t] = RowState{-INFINITY, 0.f, 0x7fffffff};
 
-  for (int c = wave; c < nchunks; c += nw) {
-    const int c0 = c * CLASS_CHUNK;
-    f32x4_t acc[NT][4];
+  // logits of class chunk c0 (bias included) for the block's rows: acc[t][mt] = classes
+  // c0 + mt*16 + q*4 + r of batch row (t, col)
+  auto chunk_logits = [&](int c0, f32x4_t (&acc)[NT][4]) {
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       const int cb = c0 + mt * 16 + q * 4;
@@ -1270,6 +1285,11 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
           for (int mt = 0; mt < 4; ++mt)
             acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt][ks], xf[t][ks], acc[t][mt], 0, 0, 0);
     }
+  };
+  for (int c = wave; c < nchunks; c += nw) {
+    const int c0 = c * CLASS_CHUNK;
+    f32x4_t acc[NT][4];
+    chunk_logits(c0, acc);
     // epilogue: lane owns classes c0 + mt*16 + q*4 + r of batch row (t, col)
     const bool partial = c0 + CLASS_CHUNK > K;
 #pragma unroll
@@ -1314,15 +1334,78 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
         S = merge_state(S, RowState{pw.x, pw.y, __float_as_int(pw.z)}, OVR);
       }
       const int64_t row = row0 + r;
+      if constexpr (MODE == 5) {
+        lse_s[r] = S.m + __logf(S.s);
+        hit_s[r] = row < B && S.bi == a.y[row] ? 1.f : 0.f;
+      }
       if (row < B) {
         if constexpr (MODE == 0) {
           put_result(a.out_idx, a.out_p, a.ro, row, S.bi, OVR ? sigmoidf_(S.m) / S.s : 1.f / S.s);
         } else if constexpr (MODE == 4) {
           a.rowstate[row] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
-        } else {
+        } else if constexpr (MODE == 2) {
           a.rowstat[row] = make_float2(S.m + __logf(S.s), __int_as_float(S.bi));
         }
       }
+    }
+  }
+  if constexpr (MODE == 5) {
+    __syncthreads();  // lse_s / hit_s
+    float lse[NT];
+    int yr[NT];
+    bool live[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int64_t row = row0 + t * 16 + col;
+      live[t] = row < B;
+      lse[t] = lse_s[t * 16 + col];
+      yr[t] = live[t] ? a.y[row] : -1;
+    }
+    float loss = 0.f;
+    const int nchunks_p = a.Kp / CLASS_CHUNK;  // G's padded columns are written too (zeros)
+    for (int c = wave; c < nchunks_p; c += nw) {
+      const int c0 = c * CLASS_CHUNK;
+      f32x4_t acc[NT][4];
+      chunk_logits(c0, acc);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        if (!live[t]) continue;
+        uint16_t* gr = a.G + (row0 + t * 16 + col) * (int64_t)a.Kp + c0 + q * 4;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          uint16_t gb[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int cls = c0 + mt * 16 + q * 4 + r;
+            const float z = acc[t][mt][r];
+            float g = 0.f;
+            if (cls < K) {
+              const bool is_y = cls == yr[t];
+              const float p = OVR ? 1.f / (1.f + __expf(-z)) : __expf(z - lse[t]);
+              g = p - (is_y ? 1.f : 0.f);
+              if constexpr (OVR) loss += fmaxf(z, 0.f) - (is_y ? z : 0.f) + log1pf(__expf(-fabsf(z)));
+              else if (is_y) loss += lse[t] - z;
+            }
+            gb[r] = bf16_rne(g);
+          }
+          uint2 pk;
+          pk.x = (uint32_t)gb[0] | ((uint32_t)gb[1] << 16);
+          pk.y = (uint32_t)gb[2] | ((uint32_t)gb[3] << 16);
+          *reinterpret_cast<uint2*>(gr + mt * 16) = pk;
+        }
+      }
+    }
+    // the block's {loss, correct}: lanes, then waves in order (deterministic)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) loss += __shfl_xor(loss, off, 64);
+    if (lane == 0) wsum_s[wave] = loss;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float l = 0.f, h = 0.f;
+      for (int w = 0; w < nw; ++w) l += wsum_s[w];
+      for (int r = 0; r < ROWS; ++r) h += hit_s[r];
+      a.stat_slabs[2 * (int64_t)blockIdx.x] = l;
+      a.stat_slabs[2 * (int64_t)blockIdx.x + 1] = h;
     }
   }
 }
@@ -1671,6 +1754,25 @@ void launch_gemm_rowstate(const void* X, const void* W, const float* b, int64_t 
     args.partials = reinterpret_cast<float4*>(static_cast<unsigned char*>(workspace) + COUNTER_BYTES);
   }
   launch_mode<4>(args, F, plan, stream);
+}
+
+int softmax_rows_g_blocks(int64_t B) {
+  const int nt = B >= 16384 ? 2 : 1;  // launch_rows' row tiles per block
+  return (int)((B + 16 * nt - 1) / (16 * nt));
+}
+
+void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y, int64_t B,
+                           int F, int K, int kind, uint16_t* G, int Kp, float* stat_slabs, hipStream_t stream) {
+  if (B <= 0) return;
+  if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
+    throw std::invalid_argument("softmax_rows_g: multiclass kinds only");
+  if (Kp % CLASS_CHUNK != 0 || Kp < K) throw std::invalid_argument("softmax_rows_g: Kp must be K rounded up to 64");
+  RowsArgs ra = rows_args(X_aug, ldx, W, b, B, F, K);
+  ra.y = y;
+  ra.G = G;
+  ra.Kp = Kp;
+  ra.stat_slabs = stat_slabs;
+  launch_rows<5>(ra, kind, stream);
 }
 
 void launch_gemm_logits_ld(const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K, float* Z,

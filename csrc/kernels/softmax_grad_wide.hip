@@ -2,21 +2,25 @@
 // LogisticRegression.fit on any F, `Logistic Regression.ipynb:33-34`).
 //
 // The fused kernel (softmax_grad_dw.hip) keeps a 64-row X tile and a wave's 16 W rows in LDS /
-// registers for the whole F, which stops at F = 512. Beyond it the step is five launches, all
+// registers for the whole F, which stops at F = 512. Beyond it the step is three launches, all
 // hand-written (no vendor GEMM):
-//   1. row stats {lse, argmax} (row-group kernel, gemm_softmax.hip MODE 2);
-//   2. logits Z = X W^T + b, f32 (row-group kernel MODE 1);
-//   3. softmax_g_kernel: one wave per row - G = softmax(z) - onehot(y) (OvR: sigmoid(z) - onehot)
-//      as bf16 [B][Kp] (Kp = K rounded up to 64, zero padded) plus per-block {loss, correct};
-//   4. gdw_gemm_kernel: dW slabs[row group][K][F_aug] = G^T X_aug over the group's rows -
+//   1. softmax_rows_kernel MODE 5 (gemm_softmax.hip): a block owns 16-32 rows and ALL classes -
+//      the row stats {lse, argmax} over the class chunks, then (lse held in LDS) the logits again,
+//      chunk by chunk, straight into G = softmax(z) - onehot(y) (OvR: sigmoid(z) - onehot) as bf16
+//      [B][Kp] (Kp = K rounded up to 64, zero padded) plus the block's {loss, correct}: the B x K
+//      f32 logits never reach HBM (round 3 wrote and re-read them between two more launches);
+//   2. gdw_gemm_kernel: dW slabs[row group][K][F_aug] = G^T X_aug over the group's rows -
 //      v_mfma_f32_16x16x32_bf16 with M = classes, N = features, K = rows: both operands are
 //      row-major [rows][*] tiles, so each is staged in LDS (32 rows x 64 columns, one 16-byte load
 //      per thread) and read transposed with ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane
 //      group, two reads = the 8 rows of a lane's k-slice);
-//   5. launch_gdw_reduce: deterministic slab sum + fused SGD update (+ in-kernel DP exchange).
+//   3. launch_gdw_reduce: deterministic slab sum + fused SGD update (+ in-kernel DP exchange).
+// softmax_g_kernel below is the round-3 G pass (one wave per row, from f32 logits), kept for
+// MLAPI_WIDE_TRAIN_5L=1 (the A/B against the fused first launch).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "mlapi/common.h"
@@ -159,7 +163,7 @@ WideLayout wide_layout(int64_t B, int K, int F) {
   if (rg < 1) rg = 1;
   L.rows_per_group = ((B + rg - 1) / rg + TILE_ROWS - 1) / TILE_ROWS * TILE_ROWS;
   L.row_groups = (int)((B + L.rows_per_group - 1) / L.rows_per_group);
-  L.g_blocks = (int)((B + G_ROWS_PER_BLOCK - 1) / G_ROWS_PER_BLOCK);
+  L.g_blocks = (int)((B + G_ROWS_PER_BLOCK - 1) / G_ROWS_PER_BLOCK);  // >= softmax_rows_g_blocks(B)
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   size_t o = 0;
   L.rowstat_off = o;
@@ -203,21 +207,31 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
   uint16_t* G = reinterpret_cast<uint16_t*>(ws + L.g_off);
   float* slabs = reinterpret_cast<float*>(ws + L.dw_off);
   float* stat_slabs = reinterpret_cast<float*>(ws + L.stat_off);
-  launch_softmax_rowstats(X_aug, ldx, W, b, B, F, K, kind, rowstat, nullptr, 0, stream);
-  launch_gemm_logits_ld(X_aug, ldx, W, b, B, F, K, Z, stream);
-  if (kind == KIND_OVR)
-    hipLaunchKernelGGL(softmax_g_kernel<true>, dim3((unsigned)L.g_blocks), dim3(64 * G_ROWS_PER_BLOCK), 0, stream, Z,
-                       rowstat, y, B, K, L.Kp, G, stat_slabs);
-  else
-    hipLaunchKernelGGL(softmax_g_kernel<false>, dim3((unsigned)L.g_blocks), dim3(64 * G_ROWS_PER_BLOCK), 0, stream, Z,
-                       rowstat, y, B, K, L.Kp, G, stat_slabs);
-  MLAPI_HIP_CHECK(hipGetLastError());
+  static const bool five = [] {
+    const char* e = std::getenv("MLAPI_WIDE_TRAIN_5L");
+    return e != nullptr && e[0] == '1';
+  }();
+  int g_blocks = L.g_blocks;
+  if (five) {  // round 3: row stats, f32 logits through HBM, the G pass
+    launch_softmax_rowstats(X_aug, ldx, W, b, B, F, K, kind, rowstat, nullptr, 0, stream);
+    launch_gemm_logits_ld(X_aug, ldx, W, b, B, F, K, Z, stream);
+    if (kind == KIND_OVR)
+      hipLaunchKernelGGL(softmax_g_kernel<true>, dim3((unsigned)L.g_blocks), dim3(64 * G_ROWS_PER_BLOCK), 0, stream, Z,
+                         rowstat, y, B, K, L.Kp, G, stat_slabs);
+    else
+      hipLaunchKernelGGL(softmax_g_kernel<false>, dim3((unsigned)L.g_blocks), dim3(64 * G_ROWS_PER_BLOCK), 0, stream, Z,
+                         rowstat, y, B, K, L.Kp, G, stat_slabs);
+    MLAPI_HIP_CHECK(hipGetLastError());
+  } else {
+    launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, stream);
+    g_blocks = softmax_rows_g_blocks(B);
+  }
   const int F_aug = F + 8;
   const dim3 grid((unsigned)(L.Kp / TILE_COLS), (unsigned)((F_aug + TILE_COLS - 1) / TILE_COLS), (unsigned)L.row_groups);
   hipLaunchKernelGGL(gdw_gemm_kernel, grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug), ldx,
                      F_aug, B, K, L.rows_per_group, slabs);
   MLAPI_HIP_CHECK(hipGetLastError());
-  launch_gdw_reduce(slabs, L.row_groups, K, F_aug, dW_out, stat_slabs, L.g_blocks, stats_out, update, dp,
+  launch_gdw_reduce(slabs, L.row_groups, K, F_aug, dW_out, stat_slabs, g_blocks, stats_out, update, dp,
                     dp_timeout_ms, stream);
 }
 
