@@ -223,6 +223,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("xcd_placement_mismatches", &xcd_placement_mismatches, py::arg("device") = 0);
   m.def("xcd_local_errors", &xcd_local_errors, py::arg("device") = 0);
   m.def("xcd_local_inject", &xcd_local_inject, py::arg("launches"));
+  m.def("xcd_local_reset", &xcd_local_reset, py::arg("device") = 0);
   m.def(
       "linear_split",
       [](int dt, uintptr_t X, int64_t ldx, uintptr_t W, uintptr_t b, int64_t B, int F, int K, int kind,

@@ -192,6 +192,7 @@ void xcd_local_report_error(int device);
 uint64_t xcd_local_errors(int device);
 // test hook: the next `launches` XCD-local launches report every merged row as misplaced
 void xcd_local_inject(int launches);
+void xcd_local_reset(int device);  // forget the decision: the next launch probes again
 int xcd_local_take_inject();
 int linear_split_nsplit(int K);
 constexpr int64_t LINEAR_SPLIT_MAX_ROWS = 2048;  // rows per launch_linear_split call

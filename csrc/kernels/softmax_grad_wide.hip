@@ -103,9 +103,12 @@ __global__ __launch_bounds__(256) void gdw_gemm_kernel(const uint16_t* __restric
   // transposed reads: lane 4q + p of group g supplies row 8g + q (+4), columns base + 4p
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   wf32x4_t acc[4] = {};
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += TILE_ROWS) {
+  // the next tile's 16-byte loads are issued before this tile's LDS reads and MFMAs (register
+  // double buffer): the global round trip overlaps the MFMAs instead of preceding them
+  auto load_tile = [&](int64_t r0, uint4& gv, uint4& xv) {
     const int64_t r = r0 + sr;
-    uint4 gv = {0, 0, 0, 0}, xv = {0, 0, 0, 0};
+    gv = uint4{0, 0, 0, 0};
+    xv = uint4{0, 0, 0, 0};
     if (r < r_end) {
       gv = *reinterpret_cast<const uint4*>(G + r * Kp + c0 + sc);  // Kp % 64 == 0: always in bounds
       if (f0 + sc + 8 <= ldx) {
@@ -116,6 +119,12 @@ __global__ __launch_bounds__(256) void gdw_gemm_kernel(const uint16_t* __restric
         __builtin_memcpy(&xv, tmp, sizeof xv);
       }
     }
+  };
+  uint4 gn, xn;
+  load_tile(r_begin, gn, xn);
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += TILE_ROWS) {
+    const uint4 gv = gn, xv = xn;
+    if (r0 + TILE_ROWS < r_end) load_tile(r0 + TILE_ROWS, gn, xn);
     __syncthreads();  // the previous tile's reads are done
     *reinterpret_cast<uint4*>(&gt[sr][sc]) = gv;
     *reinterpret_cast<uint4*>(&xt[sr][sc]) = xv;

@@ -82,6 +82,10 @@ uint64_t xcd_local_errors(int device) {
 
 void xcd_local_inject(int launches) { g_inject.store(launches); }
 
+void xcd_local_reset(int device) {
+  if (device >= 0 && device < MAX_DEVICES) g_state[device].store(0);
+}
+
 int xcd_local_take_inject() {
   int v = g_inject.load(std::memory_order_relaxed);
   while (v > 0 && !g_inject.compare_exchange_weak(v, v - 1)) {

@@ -53,14 +53,21 @@ def test_misplaced_xcd_merge_fails_rows_then_falls_back(native):
         e0 = native.xcd_local_errors(0)
         native.xcd_local_inject(1)
         idx, p, st = e.predict(X)
-        assert (st == ST_DEVICE_ERROR).all(), st  # never a silently wrong answer
-        assert e.stats()["xcd_errors"] == len(X)
+        # the injected launch's rows fail (never a silently wrong answer); rows the batcher put in
+        # later batches already take the agent-scope merge and are right
+        bad = st == ST_DEVICE_ERROR
+        assert bad.any() and ((st == ST_OK) | bad).all(), st
+        ok = st == ST_OK
+        if ok.any():
+            _check(m, X[ok], idx[ok], p[ok])
+        assert e.stats()["xcd_errors"] == int(bad.sum())
         assert native.xcd_local_errors(0) == e0 + 1 and native.xcd_placement_state(0) == 2
         idx, p, st = e.predict(X)  # agent-scope merge from now on
         assert (st == ST_OK).all()
         _check(m, X, idx, p)
     finally:
         native.xcd_local_inject(0)
+        native.xcd_local_reset(0)  # later tests of this process probe the placement afresh
         e.stop()
 
 

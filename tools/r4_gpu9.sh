@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/r4_s9; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "softmax_grad_wide or wide_multiclass_estimator or softmax_train" > $O/pytest_train.log 2>&1 || { echo "train tests failed"; tail -30 $O/pytest_train.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_xcd_fallback_gpu.py -k "softmax_grad_wide or wide_multiclass_estimator or softmax_train or xcd or split" > $O/pytest_train.log 2>&1 || { echo "train tests failed"; tail -30 $O/pytest_train.log; exit 1; }
 tail -1 $O/pytest_train.log
 for i in 1 2; do
   timeout -k 10 150 python bench.py --mode train_softmax --softmax-features 1024 --steps 20 --warmup 3 > $O/tsm_f1024_3l_$i.json 2> $O/tsm_f1024_3l_$i.err || { echo "3l failed"; tail -5 $O/tsm_f1024_3l_$i.err; exit 1; }
