@@ -258,7 +258,7 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   const bool ovr = a.kind == KIND_OVR;
   const bool binary = a.kind == KIND_BINARY || a.kind == KIND_BINARY_SOFTMAX;
   // the other waves are only needed for an in-kernel class merge (they join its barriers)
-  if (wave != 0 && (binary || a.ncb == 1 || a.hrec != nullptr || a.probe == 2 || cb != 0)) return;
+  if (wave != 0 && (binary || a.ncb == 1 || a.hrec != nullptr || a.probe == 2 || cb != a.ncb - 1)) return;
   // ---- epilogue (wave 0): lane holds classes c0 + g + 4r of row r16 of each tile. The row's
   // block state {max, sum over the block's classes of exp(z - max) | sigmoid(z), first argmax}:
   // the max (and argmax) first, by compares only, then the 16 exponentials in parallel against
@@ -346,7 +346,7 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   }
   // ---- class blocks: every block publishes its rows' states as two tagged 16-byte granules
   // {m, argmax, epoch} {s, epoch, 0} (write-through sc1 stores; the data is the flag, so no drain,
-  // ticket or fence: Guideline 16 R2), and block 0 of the row group polls them with sc1 loads
+  // ticket or fence: Guideline 16 R2), and the row group's LAST class block polls them with sc1 loads
   // and merges. All blocks of a serving launch are co-resident (<= a few hundred blocks of 4
   // waves), and the poll is bounded (1 s, then the rows fail with WIDE_TIMEOUT_IDX).
   unsigned char* rgw2 = a.ws + (int64_t)rgi * a.rg_bytes;
@@ -363,8 +363,11 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
       }
     }
   }
-  if (cb != 0) return;
-  // block 0, 256 threads: row rl = tid >> 3 (8 rows per wave), part = tid & 7 takes class blocks
+  // the merger is the highest block index of the row group: blocks are dispatched in index order in
+  // practice, so its producers are already resident when it starts, and a grid far larger than the
+  // chip (library calls with huge B) never parks a spinning merger ahead of its own producers
+  if (cb != a.ncb - 1) return;
+  // merging block, 256 threads: row rl = tid >> 3 (8 rows per wave), part = tid & 7 takes class blocks
   // part, part + 8, ...: the row max by compares and 3 xor shuffles, then every block's
   // s * exp(m - max) in parallel, summed per lane in block order and over the 8 lanes in a
   // fixed xor tree (deterministic).

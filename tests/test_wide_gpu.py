@@ -62,6 +62,24 @@ def test_linear_wide_matches_fp64_oracle(dtype, F, K, kind):
         _oracle_check(om, Xo, idx.cpu().numpy(), p.cpu().numpy())
 
 
+def test_linear_wide_grid_far_beyond_the_chip():
+    """B = 6000 rows x K = 1000: 188 row groups x 63 class blocks = 11,844 blocks, ~6x what the chip
+    holds at once - every row group's merging block still sees all its producers' granules (none
+    times out), and the answers match the oracle."""
+    from mlapi_amd.ops.linear import LinearWide
+
+    F, K, B = 256, 1000, 6000
+    m = LinearModel.random(F, K, seed=77)
+    X = np.round(np.random.default_rng(8).standard_normal((B, F)), 3)
+    op = LinearWide(B, F, K, torch.float64, "cuda")
+    for _ in range(2):
+        idx, p = op(torch.tensor(X, device="cuda"), torch.tensor(m.W, device="cuda"), torch.tensor(m.b, device="cuda"))
+        torch.cuda.synchronize()
+        idx = idx.cpu().numpy()
+        assert (idx >= 0).all(), "a class merge timed out"
+        _oracle_check(m, X, idx, p.cpu().numpy())
+
+
 def test_linear_wide_is_deterministic_and_tie_first():
     """Repeated launches are bitwise identical (fixed merge orders) and exact ties go to the lowest
     class index across class blocks (numpy argmax)."""
