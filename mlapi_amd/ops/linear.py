@@ -171,7 +171,16 @@ class LinearWide:
     """Wide-model predict with float64 accumulation on the matrix cores
     (csrc/kernels/linear_wide.h, v_mfma_f64_16x16x4_f64): X, W stored as f64 or f32 (same
     dtype), b f64; any F (zero-padded here to the plan's width), any K, every kind (binary kinds:
-    W is [1, F]). Returns (int32 label index, f64 p_max)."""
+    W is [1, F]). Returns (int32 label index, f64 p_max). A row whose in-kernel class merge gave up
+    waiting (1 s: a class block never ran - not expected, the launch's blocks are dispatched in
+    order) comes back as index WIDE_TIMEOUT_IDX (-3) and p NaN; :meth:`failed` counts them (it
+    synchronises)."""
+
+    WIDE_TIMEOUT_IDX = -3
+
+    @staticmethod
+    def failed(idx: torch.Tensor) -> int:
+        return int((idx < 0).sum().item())
 
     def __init__(self, max_batch: int, n_features: int, n_classes: int, dtype: torch.dtype, device):
         self.dt = _DT[dtype]

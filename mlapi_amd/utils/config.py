@@ -31,8 +31,9 @@ class Config:
     # device / engine
     device: str = "auto"                      # "auto" | "cpu" | "cuda" | "cuda:N" | "N"
     dtype: str = "f64"                        # small-model (F<=32, K<=16) compute dtype: f64 (sklearn parity) | f32
-    wide_dtype: str = "f32"                   # wider models: f32 (GEMV / f32-MFMA class-split kernel; F <= 512
-                                              # multiclass) | bf16 (opt-in: bf16 GEMV / MFMA GEMM) | f64 (GENERIC)
+    wide_dtype: str = "f32"                   # wider models: f32 storage (f32 GEMV for binary F <= 2048, else the
+                                              # f64-accumulating WIDE kernel) | f64 (WIDE kernel, sklearn's dtype)
+                                              # | bf16 (opt-in: bf16 GEMV / MFMA GEMM)
     split_max_rows: int = 32                  # bf16 multiclass: batches <= this many rows take the class-split kernel
     bar_rows: int = 32                        # GPU wide paths: batches <= this many rows go to HBM through the BAR (0 = off)
     host_merge_rows: int = 16                 # GPU multiclass: class-split batches <= this many rows merge on the host

@@ -321,3 +321,45 @@ def test_idle_engine_fast_path(native, F, K, kind):
         np.testing.assert_allclose(p, rp, rtol=1e-12, atol=0)
     else:
         check(m, X, idx, p, "f32", rtol=1e-11 if K > 2 else 1e-5)
+
+
+@pytest.mark.parametrize("F,K,kind", [(256, 2, Kind.BINARY), (256, 40, Kind.MULTINOMIAL),
+                                      (1024, 1000, Kind.MULTINOMIAL), (4096, 40, Kind.OVR)])
+def test_native_server_f64_wide_models(native, F, K, kind):
+    """wide_dtype = f64 (the reference's dtype) over HTTP: every body is the engine's own answer
+    rendered byte for byte, labels are the float64 oracle's away from 1e-9 ties and p is within
+    rel 1e-12 of it; every batch ran the WIDE kernel (never GENERIC)."""
+    from mlapi_amd.serve.loadgen import render_response
+    from mlapi_amd.serve.server import NativeServer
+    from mlapi_amd.utils.config import Config
+
+    names = [f"f{i}" for i in range(F)]
+    m = LinearModel.random(F, K, seed=F + K, kind=kind, labels=[f"c{i}" for i in range(K)])
+    cfg = Config.from_env(port=0, device="cuda:0", feature_names=names, reload="off", missing_model="keep",
+                          model_path="/nonexistent/wide64.pkl", io_threads=4, wide_dtype="f64")
+    srv = NativeServer(cfg)
+    srv.runtime.handle.load(m)
+    srv.start()
+    try:
+        X = np.round(np.random.default_rng(F).standard_normal((256, F)), 3)
+        bodies = [json.dumps(dict(zip(names, map(float, row))), separators=(",", ":")).encode() for row in X]
+        with ThreadPoolExecutor(8) as ex:
+            parts = list(ex.map(lambda j: _post(srv.port, bodies[j::8]), range(8)))
+        res = [None] * len(bodies)
+        for j, part in enumerate(parts):
+            for i, r in enumerate(part):
+                res[j + 8 * i] = r
+        assert all(st == 200 for st, _ in res)
+        eidx, ep, est = srv.runtime.handle.engine.predict(X)
+        assert (est == 0).all()
+        for r, (_, body) in enumerate(res):
+            assert body == render_response(m, eidx[r], ep[r]), r
+        ridx, rp = m.predict_max(X)
+        z = m.decision_function(X)
+        margin = np.abs(z) if z.ndim == 1 else np.diff(np.sort(z, axis=1)[:, -2:], axis=1)[:, 0]
+        assert not ((eidx != ridx) & (margin > 1e-9)).any()
+        np.testing.assert_allclose(ep, rp, rtol=1e-12, atol=0)
+        st = srv.runtime.handle.stats()
+        assert st["path_batches"]["wide"] >= 1 and st["path_batches"]["generic"] == 0
+    finally:
+        srv.stop()

@@ -75,8 +75,8 @@ def test_linear_wide_grid_far_beyond_the_chip():
     for _ in range(2):
         idx, p = op(torch.tensor(X, device="cuda"), torch.tensor(m.W, device="cuda"), torch.tensor(m.b, device="cuda"))
         torch.cuda.synchronize()
+        assert op.failed(idx) == 0, "a class merge timed out"
         idx = idx.cpu().numpy()
-        assert (idx >= 0).all(), "a class merge timed out"
         _oracle_check(m, X, idx, p.cpu().numpy())
 
 
