@@ -1427,6 +1427,18 @@ bool use_rows(int64_t B, int F) {
   return g_force_kernel == 2 && rows_supported(F);
 }
 
+// 16-row tiles per block of the row-group kernel. Wide F (> 256) at large B: 4 tiles in 128-feature
+// slices (KS = 4) - every block streams all of W through its waves, so 64 rows per block halve that
+// L2 traffic against 32 (MLAPI_ROWS_NT4=0: 2 tiles in 256-feature slices, round 3)
+int rows_nt(int64_t B, int F) {
+  static const bool nt4 = [] {
+    const char* e = std::getenv("MLAPI_ROWS_NT4");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (B < 16384) return 1;
+  return (F > 256 && nt4) ? 4 : 2;
+}
+
 template <int MODE>
 void launch_rows(RowsArgs a, int kind, hipStream_t stream) {
   if (!rows_supported(a.F))
@@ -1435,7 +1447,7 @@ void launch_rows(RowsArgs a, int kind, hipStream_t stream) {
     throw std::invalid_argument("gemm_softmax: X rows and W must be 16-byte aligned");
   const int nchunks = (a.K + CLASS_CHUNK - 1) / CLASS_CHUNK;
   const int nw = nchunks < ROWS_MAX_WAVES ? nchunks : ROWS_MAX_WAVES;
-  const int nt = a.B >= 16384 ? 2 : 1;
+  const int nt = rows_nt(a.B, a.F);
   const dim3 grid((unsigned)((a.B + 16 * nt - 1) / (16 * nt))), block(64 * nw);
   const bool ovr = kind == KIND_OVR;
 #define MLAPI_ROWS_LAUNCH(KSV, NTV)                                                                \
@@ -1456,6 +1468,8 @@ void launch_rows(RowsArgs a, int kind, hipStream_t stream) {
     MLAPI_ROWS_NT(2)
   } else if (a.F == 128) {
     MLAPI_ROWS_NT(4)
+  } else if (nt == 4) {
+    MLAPI_ROWS_LAUNCH(4, 4);
   } else {
     MLAPI_ROWS_NT(8)
   }
@@ -1756,8 +1770,8 @@ void launch_gemm_rowstate(const void* X, const void* W, const float* b, int64_t 
   launch_mode<4>(args, F, plan, stream);
 }
 
-int softmax_rows_g_blocks(int64_t B) {
-  const int nt = B >= 16384 ? 2 : 1;  // launch_rows' row tiles per block
+int softmax_rows_g_blocks(int64_t B, int F) {
+  const int nt = rows_nt(B, F);  // launch_rows' row tiles per block
   return (int)((B + 16 * nt - 1) / (16 * nt));
 }
 

@@ -233,7 +233,7 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
     MLAPI_HIP_CHECK(hipGetLastError());
   } else {
     launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, stream);
-    g_blocks = softmax_rows_g_blocks(B);
+    g_blocks = softmax_rows_g_blocks(B, F);
   }
   const int F_aug = F + 8;
   const dim3 grid((unsigned)(L.Kp / TILE_COLS), (unsigned)((F_aug + TILE_COLS - 1) / TILE_COLS), (unsigned)L.row_groups);

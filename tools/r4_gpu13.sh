@@ -15,6 +15,14 @@ for r in rows[:6]:
 PY
   echo "-- $n done"
 }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "softmax_grad_wide or wide_multiclass or gemm_softmax" > $O/pytest_rows.log 2>&1 || { echo "rows tests failed"; tail -30 $O/pytest_rows.log; exit 1; }
+tail -1 $O/pytest_rows.log
+for i in 1 2; do
+  for v in 1 0; do
+    MLAPI_ROWS_NT4=$v timeout -k 10 150 python bench.py --mode train_softmax --softmax-features 1024 --steps 20 --warmup 3 > $O/tsm_f1024_nt4_${v}_$i.json 2> $O/tsm_f1024_nt4_${v}_$i.err || { echo "tsm failed"; exit 1; }
+    echo "nt4=$v $i $(python3 -c "import json; d=json.loads(open('$O/tsm_f1024_nt4_${v}_$i.json').read().strip().splitlines()[-1]); print(d['ms_per_step'], round(d['tflops_incl_recompute'],1))")"
+  done
+done
 prof serve 300 --steps 10 --warmup 2
 prof serve_wide_f1024 300 --mode serve_wide --wide-features 1024 --steps 6 --warmup 2
 prof serve_wide_f64 300 --mode serve_wide --wide-dtype f64 --steps 6 --warmup 2
