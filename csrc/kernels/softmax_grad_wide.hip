@@ -155,6 +155,112 @@ __global__ __launch_bounds__(256) void gdw_gemm_kernel(const uint16_t* __restric
   }
 }
 
+// ---- 4'. the same G^T X_aug with 128 x 128 block tiles (default): a wave owns 64 classes x 64
+// features (4 x 4 MFMA tiles, 64 accumulator VGPRs), so each 16-byte element staged through LDS
+// feeds twice the MFMAs of the 64 x 64 kernel and G / X are re-read from L2 half as often (the
+// 64 x 64 kernel is L2-bandwidth bound: G is read once per feature tile, X once per class tile).
+// LDS double buffered (one barrier per 32-row k-step); rows padded to 136 elements.
+constexpr int T128 = 128;
+constexpr int LDS_ROW = T128 + 8;
+
+__global__ __launch_bounds__(256) void gdw_gemm128_kernel(const uint16_t* __restrict__ G, int Kp,
+                                                          const uint16_t* __restrict__ X, int64_t ldx, int F_aug,
+                                                          int64_t B, int K, int64_t rows_per_group,
+                                                          float* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(16))) uint16_t gt[2][TILE_ROWS][LDS_ROW];
+  __shared__ __attribute__((aligned(16))) uint16_t xt[2][TILE_ROWS][LDS_ROW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wc = wave & 1, wf = wave >> 1;  // the wave's class half / feature half
+  const int c0 = blockIdx.x * T128, f0 = blockIdx.y * T128;
+  const int64_t r_begin = (int64_t)blockIdx.z * rows_per_group;
+  const int64_t r_end = min(B, r_begin + rows_per_group);
+  // staging: 32 rows x 16 chunks of 8 columns per array; thread t moves chunks t and t + 256
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  auto load_tile = [&](int64_t r0, uint4 (&gv)[2], uint4 (&xv)[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = (int)threadIdx.x + 256 * j, sr = k >> 4, sc = (k & 15) * 8;
+      const int64_t r = r0 + sr;
+      gv[j] = uint4{0, 0, 0, 0};
+      xv[j] = uint4{0, 0, 0, 0};
+      if (r < r_end) {
+        gv[j] = *reinterpret_cast<const uint4*>(G + r * Kp + c0 + sc);  // Kp % 128 == 0: in bounds
+        if (f0 + sc + 8 <= ldx) {
+          xv[j] = *reinterpret_cast<const uint4*>(X + r * ldx + f0 + sc);
+        } else {
+          uint16_t tmp[8];
+          for (int e = 0; e < 8; ++e) tmp[e] = f0 + sc + e < ldx ? X[r * ldx + f0 + sc + e] : 0;
+          __builtin_memcpy(&xv[j], tmp, sizeof(uint4));
+        }
+      }
+    }
+  };
+  auto store_tile = [&](int buf, const uint4 (&gv)[2], const uint4 (&xv)[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = (int)threadIdx.x + 256 * j, sr = k >> 4, sc = (k & 15) * 8;
+      *reinterpret_cast<uint4*>(&gt[buf][sr][sc]) = gv[j];
+      *reinterpret_cast<uint4*>(&xt[buf][sr][sc]) = xv[j];
+    }
+  };
+  wf32x4_t acc[4][4] = {};
+  uint4 gv[2], xv[2];
+  load_tile(r_begin, gv, xv);
+  store_tile(0, gv, xv);
+  __syncthreads();
+  int buf = 0;
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += TILE_ROWS) {
+    const bool more = r0 + TILE_ROWS < r_end;
+    if (more) load_tile(r0 + TILE_ROWS, gv, xv);  // in flight under this step's MFMAs
+    wbf16x8_t a[4], b[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {  // A: 16 classes x 8 rows per 16-lane group (transposed reads)
+      const int cc = wc * 64 + m * 16 + 4 * p;
+      const wi16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&gt[buf][8 * g + q][cc]);
+      const wi16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&gt[buf][8 * g + 4 + q][cc]);
+      const wi16x4_t v[2] = {lo, hi};
+      a[m] = __builtin_bit_cast(wbf16x8_t, v);
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int ff = wf * 64 + n * 16 + 4 * p;
+      const wi16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&xt[buf][8 * g + q][ff]);
+      const wi16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&xt[buf][8 * g + 4 + q][ff]);
+      const wi16x4_t v[2] = {lo, hi};
+      b[n] = __builtin_bit_cast(wbf16x8_t, v);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], b[n], acc[m][n], 0, 0, 0);
+    if (more) store_tile(buf ^ 1, gv, xv);  // the other buffer was last read before the previous barrier
+    __syncthreads();
+    buf ^= 1;
+  }
+  // C layout: class c0 + wc*64 + 16m + 4g + i (register i), feature f0 + wf*64 + 16n + (lane & 15)
+  float* slab = slabs + (int64_t)blockIdx.z * K * F_aug;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int f = f0 + wf * 64 + n * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = c0 + wc * 64 + m * 16 + 4 * g + i;
+        if (c < K && f < F_aug) slab[(int64_t)c * F_aug + f] = acc[m][n][i];
+      }
+    }
+}
+
+// 128 x 128 G^T X tiles unless MLAPI_GDW_TILE=64 (the round-3 kernel, for the A/B)
+bool gdw_tile128() {
+  static const bool v = [] {
+    const char* e = std::getenv("MLAPI_GDW_TILE");
+    return e == nullptr || std::atoi(e) != 64;
+  }();
+  return v;
+}
+
 struct WideLayout {
   size_t rowstat_off, z_off, g_off, dw_off, stat_off, total;
   int Kp, row_groups, g_blocks;
@@ -164,8 +270,9 @@ struct WideLayout {
 WideLayout wide_layout(int64_t B, int K, int F) {
   WideLayout L{};
   const int F_aug = F + 8;
-  L.Kp = (K + TILE_COLS - 1) / TILE_COLS * TILE_COLS;
-  const int tiles = (L.Kp / TILE_COLS) * ((F_aug + TILE_COLS - 1) / TILE_COLS);
+  const int T = gdw_tile128() ? T128 : TILE_COLS;  // G's columns padded to the class tile
+  L.Kp = (K + T - 1) / T * T;
+  const int tiles = (L.Kp / T) * ((F_aug + T - 1) / T);
   int64_t rg = (2048 + tiles - 1) / tiles;
   const int64_t max_rg = (B + 255) / 256;
   if (rg > max_rg) rg = max_rg;
@@ -236,9 +343,15 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
     g_blocks = softmax_rows_g_blocks(B, F);
   }
   const int F_aug = F + 8;
-  const dim3 grid((unsigned)(L.Kp / TILE_COLS), (unsigned)((F_aug + TILE_COLS - 1) / TILE_COLS), (unsigned)L.row_groups);
-  hipLaunchKernelGGL(gdw_gemm_kernel, grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug), ldx,
-                     F_aug, B, K, L.rows_per_group, slabs);
+  if (gdw_tile128()) {
+    const dim3 grid((unsigned)(L.Kp / T128), (unsigned)((F_aug + T128 - 1) / T128), (unsigned)L.row_groups);
+    hipLaunchKernelGGL(gdw_gemm128_kernel, grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug),
+                       ldx, F_aug, B, K, L.rows_per_group, slabs);
+  } else {
+    const dim3 grid((unsigned)(L.Kp / TILE_COLS), (unsigned)((F_aug + TILE_COLS - 1) / TILE_COLS), (unsigned)L.row_groups);
+    hipLaunchKernelGGL(gdw_gemm_kernel, grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug), ldx,
+                       F_aug, B, K, L.rows_per_group, slabs);
+  }
   MLAPI_HIP_CHECK(hipGetLastError());
   launch_gdw_reduce(slabs, L.row_groups, K, F_aug, dW_out, stat_slabs, g_blocks, stats_out, update, dp,
                     dp_timeout_ms, stream);
