@@ -280,7 +280,7 @@ void launch_gdw_reduce(const float* slabs, int nslabs, int K, int F_aug, float* 
 // Row stats + training G in one launch (row-group kernel MODE 5): G = softmax(z) - onehot(y) (OvR:
 // sigmoid(z) - onehot) as bf16 [B][Kp] (zero columns K..Kp-1) and per-block {loss, correct} in
 // stat_slabs[softmax_rows_g_blocks(B)][2]. F: a multiple of 256 (or a power of two <= 256).
-int softmax_rows_g_blocks(int64_t B, int F);
+int softmax_rows_g_blocks(int64_t B, int F, int K);
 void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y, int64_t B,
                            int F, int K, int kind, uint16_t* G, int Kp, float* stat_slabs, hipStream_t stream);
 void launch_gemm_logits_ld(const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K, float* Z,

@@ -1427,16 +1427,19 @@ bool use_rows(int64_t B, int F) {
   return g_force_kernel == 2 && rows_supported(F);
 }
 
-// 16-row tiles per block of the row-group kernel. Wide F (> 256) at large B: 4 tiles in 128-feature
-// slices (KS = 4) - every block streams all of W through its waves, so 64 rows per block halve that
-// L2 traffic against 32 (MLAPI_ROWS_NT4=0: 2 tiles in 256-feature slices, round 3)
-int rows_nt(int64_t B, int F) {
-  static const bool nt4 = [] {
-    const char* e = std::getenv("MLAPI_ROWS_NT4");
-    return e == nullptr || e[0] != '0';
+// 16-row tiles per block of the row-group kernel. Wide F (> 256) at large B: every block streams all
+// of W through its waves, so more rows per block mean less L2 traffic - 4 tiles in 128-feature
+// slices (KS = 4: 64 rows, half of round 3's 32-row blocks' W traffic), or 6 tiles in 64-feature
+// slices (KS = 2, 96 rows; needs >= 2 class chunks: the row merge takes one thread per row).
+// MLAPI_ROWS_NT = 2 / 4 / 6 picks (2: round 3's 256-feature slices).
+int rows_nt(int64_t B, int F, int K) {
+  static const int want = [] {
+    const char* e = std::getenv("MLAPI_ROWS_NT");
+    return e != nullptr ? std::atoi(e) : 6;  // 6 vs 4: 0.99-1.01 vs 1.05-1.06 ms per F = 1024 step
   }();
   if (B < 16384) return 1;
-  return (F > 256 && nt4) ? 4 : 2;
+  if (F <= 256 || want <= 2) return 2;
+  return (want >= 6 && K > CLASS_CHUNK) ? 6 : 4;
 }
 
 template <int MODE>
@@ -1447,7 +1450,7 @@ void launch_rows(RowsArgs a, int kind, hipStream_t stream) {
     throw std::invalid_argument("gemm_softmax: X rows and W must be 16-byte aligned");
   const int nchunks = (a.K + CLASS_CHUNK - 1) / CLASS_CHUNK;
   const int nw = nchunks < ROWS_MAX_WAVES ? nchunks : ROWS_MAX_WAVES;
-  const int nt = rows_nt(a.B, a.F);
+  const int nt = rows_nt(a.B, a.F, a.K);
   const dim3 grid((unsigned)((a.B + 16 * nt - 1) / (16 * nt))), block(64 * nw);
   const bool ovr = kind == KIND_OVR;
 #define MLAPI_ROWS_LAUNCH(KSV, NTV)                                                                \
@@ -1468,6 +1471,8 @@ void launch_rows(RowsArgs a, int kind, hipStream_t stream) {
     MLAPI_ROWS_NT(2)
   } else if (a.F == 128) {
     MLAPI_ROWS_NT(4)
+  } else if (nt == 6) {
+    MLAPI_ROWS_LAUNCH(2, 6);
   } else if (nt == 4) {
     MLAPI_ROWS_LAUNCH(4, 4);
   } else {
@@ -1770,8 +1775,8 @@ void launch_gemm_rowstate(const void* X, const void* W, const float* b, int64_t 
   launch_mode<4>(args, F, plan, stream);
 }
 
-int softmax_rows_g_blocks(int64_t B, int F) {
-  const int nt = rows_nt(B, F);  // launch_rows' row tiles per block
+int softmax_rows_g_blocks(int64_t B, int F, int K) {
+  const int nt = rows_nt(B, F, K);  // launch_rows' row tiles per block
   return (int)((B + 16 * nt - 1) / (16 * nt));
 }
 

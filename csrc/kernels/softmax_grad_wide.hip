@@ -340,7 +340,7 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
     MLAPI_HIP_CHECK(hipGetLastError());
   } else {
     launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, stream);
-    g_blocks = softmax_rows_g_blocks(B, F);
+    g_blocks = softmax_rows_g_blocks(B, F, K);
   }
   const int F_aug = F + 8;
   if (gdw_tile128()) {
