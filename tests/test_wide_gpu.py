@@ -32,6 +32,8 @@ SHAPES = [  # F, K, kind
     (1500, 33, Kind.OVR),
     (4096, 1000, Kind.MULTINOMIAL),
     (5000, 7, Kind.MULTINOMIAL),
+    (512, 3000, Kind.MULTINOMIAL),  # 188 class blocks: the merge's two-pass path (> 64 blocks)
+    (300, 1100, Kind.OVR),
     (256, 1, Kind.BINARY),
     (4096, 1, Kind.BINARY),
     (300, 1, Kind.BINARY_SOFTMAX),
