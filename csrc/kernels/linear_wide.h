@@ -65,8 +65,9 @@ struct WideArgs {
   int32_t row_groups;
   int32_t sc1_loads;  // feature-split partials: agent-coherent sc1 loads instead of an acquire
   uint32_t epoch;     // != 0, distinct per launch: the tag of this launch's class-merge granules
-  int32_t probe;  // measurement only (linear_wide_set_probe): 1 = stop after the MFMA loop, 2 = after
-                  // the block's row states (before the class merge)
+  int32_t probe;  // linear_wide_set_probe: measurement 1 = stop after the MFMA loop, 2 = after the
+                  // block's row states (before the class merge); fault injection 3 = the merging
+                  // block never sees the states (its rows time out after 1 s)
 };
 
 template <typename T>
@@ -400,7 +401,7 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
         const int b = b0 + part + 8 * u;
         if (live && b < a.ncb) ok &= g1[u][3] == a.epoch && g2[u][3] == a.epoch;
       }
-      if (__all(ok)) break;
+      if (__all(ok) && a.probe != 3) break;  // probe 3 (fault injection): the states never arrive
       if (wall_clock64() - t0 > 100000000ull) {  // 1 s at 100 MHz: a block never ran
         timeout = true;
         break;

@@ -171,3 +171,35 @@ def test_engine_f32_k40_model_meets_1e6(native):
                       oracle=(LinearModel(f32(m.W), f32(m.b), m.classes, m.kind), f32(rows)))
     finally:
         e.stop()
+
+
+def test_class_merge_timeout_fails_rows_not_answers(native):
+    """Fault injection (linear_wide_set_probe(3)): the merging block never sees the other blocks'
+    states. After its bounded 1 s poll every row comes back as WIDE_TIMEOUT_IDX / NaN from the op,
+    and through the engine as a failed row (ST_DEVICE_ERROR -> HTTP 500), never as an answer; the
+    next launch is normal again."""
+    from mlapi_amd.ops.linear import LinearWide
+
+    F, K = 64, 200
+    m = LinearModel.random(F, K, seed=4)
+    X = np.random.default_rng(1).standard_normal((5, F))
+    op = LinearWide(5, F, K, torch.float64, "cuda")
+    args = [torch.tensor(a, device="cuda") for a in (X, m.W, m.b)]
+    native.linear_wide_set_probe(3)
+    try:
+        idx, p = op(*args)
+        torch.cuda.synchronize()
+        assert op.failed(idx) == 5 and (idx == LinearWide.WIDE_TIMEOUT_IDX).all() and torch.isnan(p).all()
+        e = _engine(native, max_batch=16, max_features=F, wide_dtype=0)
+        try:
+            e.load_model(int(m.kind), m.W, m.b, m.label_json())
+            _, _, st = e.predict(X)
+            assert (st == 4).all(), st
+        finally:
+            e.stop()
+    finally:
+        native.linear_wide_set_probe(0)
+    idx, p = op(*args)
+    torch.cuda.synchronize()
+    assert op.failed(idx) == 0
+    _oracle_check(m, X, idx.cpu().numpy(), p.cpu().numpy())
