@@ -360,6 +360,7 @@ class IoThread : public Sink {
       }
     }
     const int r = srv_->engine()->submit_many(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), this);
+    if (r > 0) outstanding_ += r;
     if (r != n) {
       // rows [0, r) were queued; the rest: overloaded -> 503 + Retry-After, engine stopping -> 500
       for (int i = r > 0 ? r : 0; i < n; ++i) {
@@ -393,6 +394,7 @@ class IoThread : public Sink {
     const int64_t always_spin_ns = (int64_t)srv_->config().io_spin_us * 1000;
     const int64_t lowload_spin_ns = (int64_t)srv_->config().io_spin_lowload_us * 1000;
     const int lowload_conns = srv_->config().io_spin_max_conns;
+    const int64_t wait_spin_ns = (int64_t)srv_->config().io_wait_spin_us * 1000;
     int64_t last_active = 0;
     lane_ = srv_->engine() != nullptr ? srv_->engine()->open_lane() : nullptr;
     while (!stop_.load()) {
@@ -422,6 +424,17 @@ class IoThread : public Sink {
       }
       if (lane_ != nullptr && lane_->inflight() > 0) timeout = 0;  // poll the lane's records
       stage(SS_POLL);
+      if (timeout != 0 && wait_spin_ns > 0 && outstanding_ > 0 && !spinning_.load(std::memory_order_relaxed)) {
+        // rows of this thread are in the engine: watch for their hand-off in user space for a
+        // bounded while before blocking (the completer then skips the eventfd write and this
+        // thread its wake-up); `spinning_` tells wake() not to write it, and is cleared before
+        // blocked_ is set below, so a hand-off that raced with the end of the spin is still seen
+        spinning_.store(true);
+        const int64_t until = mono_ns() + wait_spin_ns;
+        while (!pending_.load(std::memory_order_acquire) && mono_ns() < until) _mm_pause();
+        spinning_.store(false);
+        if (pending_.load()) timeout = 0;
+      }
       if (timeout != 0) {
         blocked_.store(true);
         if (pending_.load()) timeout = 0;  // a hand-off that did not write the eventfd
@@ -744,6 +757,7 @@ class IoThread : public Sink {
       getpeername(fd, reinterpret_cast<sockaddr*>(&ss), &sl);
       register_conn(fd, ss);
     }
+    outstanding_ = std::max<int64_t>(0, outstanding_ - (int64_t)fast_c.size());
     for (size_t k = 0; k < fast_seg.size(); ++k) {
       const size_t b = fast_seg[k].begin, e = k + 1 < fast_seg.size() ? fast_seg[k + 1].begin : fast_c.size();
       render_fast(fast_seg[k].model, fast_c.data() + b, e - b);
@@ -1126,6 +1140,7 @@ class IoThread : public Sink {
   std::vector<FastSeg> spare_seg_;
   std::vector<Completion> idle_done_;  // run_idle completions (this thread only)
   Lane* lane_ = nullptr;               // this thread's dispatch lane (engine-owned), or none
+  int64_t outstanding_ = 0;            // rows this thread queued in the engine, not yet handed back
   std::vector<Completion> lane_c_;     // harvest_lane scratch (this thread only)
   std::vector<Lane::Seg> lane_seg_;
   std::string body_;                   // response body scratch (this thread only)

@@ -53,6 +53,10 @@ struct ServerConfig {
   // queue for this long before blocking, and the engine's completer then hands it batches
   // without an eventfd write (no wake-up on the request path). 0 = always block.
   int io_spin_us = 0;
+  // Wait-spin: an IO thread with rows in the engine watches its hand-off flag in user space for up
+  // to this long before blocking in epoll_wait (no eventfd write for the completer, no wake-up on
+  // the request path). 0 = off.
+  int io_wait_spin_us = 0;
   // Low-load busy-poll: while the whole server holds at most io_spin_max_conns open connections
   // (a batch=1 client), an IO thread that just had activity polls for this long before blocking,
   // so the client's next request does not pay an idle-thread wake-up. Under concurrency (more
