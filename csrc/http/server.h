@@ -55,8 +55,9 @@ struct ServerConfig {
   int io_spin_us = 0;
   // Wait-spin: an IO thread with rows in the engine watches its hand-off flag in user space for up
   // to this long before blocking in epoll_wait (no eventfd write for the completer, no wake-up on
-  // the request path). 0 = off.
-  int io_wait_spin_us = 0;
+  // the request path). 0 = off. 1-5 us measured +4-21 % c=64 req/s over 0 on three boxes, 15-30
+  // us lost (the spinning threads take the load generator's CPU): profiles/r4_waitspin/.
+  int io_wait_spin_us = 3;
   // Low-load busy-poll: while the whole server holds at most io_spin_max_conns open connections
   // (a batch=1 client), an IO thread that just had activity polls for this long before blocking,
   // so the client's next request does not pay an idle-thread wake-up. Under concurrency (more

@@ -45,8 +45,9 @@ class Config:
     delay_us: int = 0                         # fault injection: delay every batch
     spin_us: int = 0                          # batcher / completer spin before sleeping (0 = always sleep)
     io_spin_us: int = 0                       # IO threads busy-poll this long after activity (0 = block)
-    io_wait_spin_us: int = 0                  # IO threads with rows in the engine watch for the hand-off this
-                                              # long in user space before blocking (0 = off)
+    io_wait_spin_us: int = 3                  # IO threads with rows in the engine watch for the hand-off this
+                                              # long in user space before blocking (0 = off; 1-5 us measured
+                                              # best, profiles/r4_waitspin/)
     io_spin_lowload_us: int = 50              # ... only while <= io_spin_max_conns connections are open (batch=1 clients)
     io_spin_max_conns: int = 2
     max_queue: int = 1 << 20                  # backpressure: queued rows beyond this -> HTTP 503
