@@ -155,36 +155,45 @@ __global__ __launch_bounds__(256) void gdw_gemm_kernel(const uint16_t* __restric
   }
 }
 
-// ---- 4'. the same G^T X_aug with 128 x 128 block tiles (default): a wave owns 64 classes x 64
-// features (4 x 4 MFMA tiles, 64 accumulator VGPRs), so each 16-byte element staged through LDS
-// feeds twice the MFMAs of the 64 x 64 kernel and G / X are re-read from L2 half as often (the
-// 64 x 64 kernel is L2-bandwidth bound: G is read once per feature tile, X once per class tile).
-// LDS double buffered (one barrier per 32-row k-step); rows padded to 136 elements.
-constexpr int T128 = 128;
-constexpr int LDS_ROW = T128 + 8;
+// ---- 4'. the same G^T X_aug with (64 WC) x 128 block tiles (default): a wave owns 64 classes x 64
+// features (4 x 4 MFMA tiles, 64 accumulator VGPRs), the block 2 WC waves, so each 16-byte element
+// staged through LDS feeds 2-4x the MFMAs of the 64 x 64 kernel and G / X are re-read from L2
+// correspondingly less often (the 64 x 64 kernel is L2-bandwidth bound: G is read once per feature
+// tile, X once per class tile). LDS double buffered (one barrier per 32-row k-step); rows padded
+// by 8 elements. WC = 2 (128 x 128 tiles, 256 threads) is the one launched: WC = 4 (256 x 128, 512
+// threads) measured 1.05 vs 0.99 ms per F = 1024 training step (profiles/r4_train/tsm_f1024_t256_*).
+constexpr int TF128 = 128;
+constexpr int XROW = TF128 + 8;
 
-__global__ __launch_bounds__(256) void gdw_gemm128_kernel(const uint16_t* __restrict__ G, int Kp,
-                                                          const uint16_t* __restrict__ X, int64_t ldx, int F_aug,
-                                                          int64_t B, int K, int64_t rows_per_group,
-                                                          float* __restrict__ slabs) {
-  __shared__ __attribute__((aligned(16))) uint16_t gt[2][TILE_ROWS][LDS_ROW];
-  __shared__ __attribute__((aligned(16))) uint16_t xt[2][TILE_ROWS][LDS_ROW];
+template <int WC>
+__global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* __restrict__ G, int Kp,
+                                                               const uint16_t* __restrict__ X, int64_t ldx, int F_aug,
+                                                               int64_t B, int K, int64_t rows_per_group,
+                                                               float* __restrict__ slabs) {
+  constexpr int TC = 64 * WC, NTHR = 128 * WC, GROW = TC + 8;
+  constexpr int JX = 512 / NTHR;  // X chunks per thread (32 rows x 16 chunks of 8 columns)
+  static_assert(32 * TC / 8 == 2 * NTHR, "two G chunks per thread");
+  __shared__ __attribute__((aligned(16))) uint16_t gt[2][TILE_ROWS][GROW];
+  __shared__ __attribute__((aligned(16))) uint16_t xt[2][TILE_ROWS][XROW];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wc = wave & 1, wf = wave >> 1;  // the wave's class half / feature half
-  const int c0 = blockIdx.x * T128, f0 = blockIdx.y * T128;
+  const int wc = wave % WC, wf = wave / WC;  // the wave's 64-class slice / 64-feature half
+  const int c0 = blockIdx.x * TC, f0 = blockIdx.y * TF128;
   const int64_t r_begin = (int64_t)blockIdx.z * rows_per_group;
   const int64_t r_end = min(B, r_begin + rows_per_group);
-  // staging: 32 rows x 16 chunks of 8 columns per array; thread t moves chunks t and t + 256
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  auto load_tile = [&](int64_t r0, uint4 (&gv)[2], uint4 (&xv)[2]) {
+  auto load_tile = [&](int64_t r0, uint4 (&gv)[2], uint4 (&xv)[JX]) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int k = (int)threadIdx.x + 256 * j, sr = k >> 4, sc = (k & 15) * 8;
+      const int k = (int)threadIdx.x + NTHR * j, sr = k / (TC / 8), sc = (k % (TC / 8)) * 8;
       const int64_t r = r0 + sr;
-      gv[j] = uint4{0, 0, 0, 0};
+      gv[j] = r < r_end ? *reinterpret_cast<const uint4*>(G + r * Kp + c0 + sc) : uint4{0, 0, 0, 0};  // Kp % TC == 0
+    }
+#pragma unroll
+    for (int j = 0; j < JX; ++j) {
+      const int k = (int)threadIdx.x + NTHR * j, sr = k >> 4, sc = (k & 15) * 8;
+      const int64_t r = r0 + sr;
       xv[j] = uint4{0, 0, 0, 0};
       if (r < r_end) {
-        gv[j] = *reinterpret_cast<const uint4*>(G + r * Kp + c0 + sc);  // Kp % 128 == 0: in bounds
         if (f0 + sc + 8 <= ldx) {
           xv[j] = *reinterpret_cast<const uint4*>(X + r * ldx + f0 + sc);
         } else {
@@ -195,16 +204,20 @@ __global__ __launch_bounds__(256) void gdw_gemm128_kernel(const uint16_t* __rest
       }
     }
   };
-  auto store_tile = [&](int buf, const uint4 (&gv)[2], const uint4 (&xv)[2]) {
+  auto store_tile = [&](int buf, const uint4 (&gv)[2], const uint4 (&xv)[JX]) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int k = (int)threadIdx.x + 256 * j, sr = k >> 4, sc = (k & 15) * 8;
+      const int k = (int)threadIdx.x + NTHR * j, sr = k / (TC / 8), sc = (k % (TC / 8)) * 8;
       *reinterpret_cast<uint4*>(&gt[buf][sr][sc]) = gv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < JX; ++j) {
+      const int k = (int)threadIdx.x + NTHR * j, sr = k >> 4, sc = (k & 15) * 8;
       *reinterpret_cast<uint4*>(&xt[buf][sr][sc]) = xv[j];
     }
   };
   wf32x4_t acc[4][4] = {};
-  uint4 gv[2], xv[2];
+  uint4 gv[2], xv[JX];
   load_tile(r_begin, gv, xv);
   store_tile(0, gv, xv);
   __syncthreads();
@@ -252,11 +265,11 @@ __global__ __launch_bounds__(256) void gdw_gemm128_kernel(const uint16_t* __rest
     }
 }
 
-// 128 x 128 G^T X tiles unless MLAPI_GDW_TILE=64 (the round-3 kernel, for the A/B)
-bool gdw_tile128() {
-  static const bool v = [] {
+// G^T X class-tile width: 128 (default); MLAPI_GDW_TILE=64 = the round-3 kernel (for the A/B)
+int gdw_tile() {
+  static const int v = [] {
     const char* e = std::getenv("MLAPI_GDW_TILE");
-    return e == nullptr || std::atoi(e) != 64;
+    return e != nullptr && std::atoi(e) == 64 ? 64 : 128;
   }();
   return v;
 }
@@ -270,9 +283,10 @@ struct WideLayout {
 WideLayout wide_layout(int64_t B, int K, int F) {
   WideLayout L{};
   const int F_aug = F + 8;
-  const int T = gdw_tile128() ? T128 : TILE_COLS;  // G's columns padded to the class tile
+  const int T = gdw_tile();  // G's columns padded to the class tile
   L.Kp = (K + T - 1) / T * T;
-  const int tiles = (L.Kp / T) * ((F_aug + T - 1) / T);
+  const int TFw = T == TILE_COLS ? TILE_COLS : TF128;  // feature tile width
+  const int tiles = (L.Kp / T) * ((F_aug + TFw - 1) / TFw);
   int64_t rg = (2048 + tiles - 1) / tiles;
   const int64_t max_rg = (B + 255) / 256;
   if (rg > max_rg) rg = max_rg;
@@ -343,14 +357,15 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
     g_blocks = softmax_rows_g_blocks(B, F, K);
   }
   const int F_aug = F + 8;
-  if (gdw_tile128()) {
-    const dim3 grid((unsigned)(L.Kp / T128), (unsigned)((F_aug + T128 - 1) / T128), (unsigned)L.row_groups);
-    hipLaunchKernelGGL(gdw_gemm128_kernel, grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug),
-                       ldx, F_aug, B, K, L.rows_per_group, slabs);
-  } else {
+  const int T = gdw_tile();
+  if (T == 64) {
     const dim3 grid((unsigned)(L.Kp / TILE_COLS), (unsigned)((F_aug + TILE_COLS - 1) / TILE_COLS), (unsigned)L.row_groups);
     hipLaunchKernelGGL(gdw_gemm_kernel, grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug), ldx,
                        F_aug, B, K, L.rows_per_group, slabs);
+  } else {
+    const dim3 grid((unsigned)(L.Kp / T), (unsigned)((F_aug + TF128 - 1) / TF128), (unsigned)L.row_groups);
+    hipLaunchKernelGGL(gdw_gemm_big_kernel<2>, grid, dim3(256), 0, stream, G, L.Kp,
+                       static_cast<const uint16_t*>(X_aug), ldx, F_aug, B, K, L.rows_per_group, slabs);
   }
   MLAPI_HIP_CHECK(hipGetLastError());
   launch_gdw_reduce(slabs, L.row_groups, K, F_aug, dW_out, stat_slabs, g_blocks, stats_out, update, dp,
