@@ -713,8 +713,8 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     dl.d = direct_.get();
     dl.flush_on_miss = bar;
     if (m.path == PATH_WIDE) {
-      // f64 accumulation; serving-sized multiclass batches end in per-(class block, row) records the
-      // completer merges (no in-kernel class merge), the rest in per-row records
+      // f64 accumulation; per-row records from the kernel's in-kernel class merge (default), or -
+      // with wide_host_merge_blocks set - per-(class block, row) records the completer merges
       WideRecOut hro;
       const bool binary = m.kind == KIND_BINARY || m.kind == KIND_BINARY_SOFTMAX;
       if (cfg_.record_completion && s.hsrec != nullptr && !binary && n <= cfg_.host_merge_rows && n <= 32 &&

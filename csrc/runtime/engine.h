@@ -53,7 +53,8 @@ enum Status : int32_t {
   ST_NONFINITE = 1,     // NaN / inf probability (reference: json.dumps raises -> HTTP 500)
   ST_NO_MODEL = 2,      // checkpoint missing (reference: open() raises -> HTTP 500)
   ST_SHAPE = 3,         // feature count mismatch
-  ST_DEVICE_ERROR = 4,  // launch failure / injected fault
+  ST_DEVICE_ERROR = 4,  // launch failure / injected fault / a row the kernel refused to answer
+                        // (misplaced XCD-local merge, wide class-merge timeout)
   ST_SHUTDOWN = 5,
 };
 
