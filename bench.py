@@ -297,7 +297,8 @@ def bench_serve_wide(args, info):
         rel = 0.0
     else:
         f32 = lambda a: np.asarray(a, dtype=np.float32).astype(np.float64)  # noqa: E731
-        f32acc = K == 2 or os.environ.get("MLAPI_F32_SPLIT", "0") not in ("0", "", "false")  # f32-accumulating kernels
+        on = lambda v: os.environ.get(v, "0") not in ("0", "", "false")  # noqa: E731
+        f32acc = on("MLAPI_F32_SPLIT") or (K == 2 and on("MLAPI_F32_GEMV"))  # the f32-accumulating kernels (A/B)
         okw = {"rtol_oracle": 1e-6 if f32acc else 1e-11, "label_margin": 1e-5 if f32acc else 1e-9,
                "oracle": (LinearModel(f32(model.W), f32(model.b), model.classes, model.kind), f32(rows))}
         rel = 1e-6

@@ -424,6 +424,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("lanes", &EngineConfig::lanes)
       .def_readwrite("lane_inflight", &EngineConfig::lane_inflight)
       .def_readwrite("f32_split", &EngineConfig::f32_split)
+      .def_readwrite("f32_gemv", &EngineConfig::f32_gemv)
       .def_readwrite("wide_host_merge_blocks", &EngineConfig::wide_host_merge_blocks)
       .def_readwrite("completers", &EngineConfig::completers)
       .def_readwrite("batchers", &EngineConfig::batchers)

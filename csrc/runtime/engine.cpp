@@ -278,8 +278,10 @@ uint64_t Engine::load_model(int kind, int F, int K, const double* W, const doubl
     m->path = PATH_SMALL;
     m->xdt = cfg_.dtype;
     m->ldx = F;
-  } else if (binary && K == 1 && cfg_.wide_dtype != DT_F64 &&
-             F <= (cfg_.wide_dtype == DT_BF16 ? 4096 : 2048)) {
+  } else if (binary && K == 1 && (cfg_.wide_dtype == DT_BF16 ? F <= 4096 : cfg_.wide_dtype == DT_F32 && cfg_.f32_gemv && F <= 2048)) {
+    // bf16 binary models (and f32 ones with f32_gemv): the GEMV kernel, f32 accumulation; f32 / f64
+    // storage otherwise takes WIDE below (f64 accumulation: rel 1e-11 / 1e-12 of the oracle, and
+    // measured no slower at serving batch sizes: profiles/r4_s20/)
     m->path = PATH_GEMV;
     m->xdt = cfg_.wide_dtype;
     const int ne = cfg_.wide_dtype == DT_BF16 ? 8 : 4;  // elements per 16-byte chunk

@@ -167,14 +167,16 @@ struct EngineConfig {
   int dtype = DT_F64;     // SMALL-path compute dtype (f64 = bit parity with sklearn, or f32)
   int wide_dtype = DT_F32;   // dtype of models too wide for the SMALL path: f64 -> WIDE (f64 storage,
                              // f64 MFMA accumulation: the reference's precision, any F / K / kind);
-                             // f32 -> GEMV (binary, F <= 2048) or WIDE (f32 storage, f64
-                             // accumulation); bf16 -> GEMV / bf16 MFMA GEMM (F <= 4096), WIDE beyond
+                             // f32 -> WIDE (f32 storage, f64 accumulation; f32_gemv: binary
+                             // F <= 2048 on the f32 GEMV); bf16 -> GEMV / bf16 MFMA GEMM (F <= 4096),
+                             // WIDE beyond
   // WIDE multiclass batches of <= host_merge_rows rows from models with at most this many 16-class
   // blocks end in per-block records merged by the completer; 0 (default) = always the in-kernel
   // class merge. Off: the completer polls 2 records per block and row (126 per row at K = 1000;
   // measured 52 us GPU legs, profiles/r4_s4/), and the served p_max then depends on the batch
   // size (host vs device exp, another merge order), which breaks the f64 path's byte-exact bodies.
   int wide_host_merge_blocks = 0;
+  bool f32_gemv = false;     // f32 binary F <= 2048: the f32-accumulating GEMV instead of WIDE (A/B)
   bool f32_split = false;    // f32 multiclass F <= 512: the f32-accumulating class-split kernel
                              // (linear_split) instead of WIDE (measurement / A-B)
   int bar_rows = 32;         // wide paths: batches of at most this many rows are written straight into

@@ -66,6 +66,7 @@ class EngineHandle:
         ec.lanes = int(config.lanes)
         ec.lane_inflight = int(config.lane_inflight)
         ec.f32_split = bool(config.f32_split)
+        ec.f32_gemv = bool(config.f32_gemv)
         ec.wide_host_merge_blocks = int(config.wide_host_merge_blocks)
         ec.completers = int(config.completers)
         ec.batchers = int(config.batchers)

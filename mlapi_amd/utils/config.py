@@ -31,8 +31,8 @@ class Config:
     # device / engine
     device: str = "auto"                      # "auto" | "cpu" | "cuda" | "cuda:N" | "N"
     dtype: str = "f64"                        # small-model (F<=32, K<=16) compute dtype: f64 (sklearn parity) | f32
-    wide_dtype: str = "f32"                   # wider models: f32 storage (f32 GEMV for binary F <= 2048, else the
-                                              # f64-accumulating WIDE kernel) | f64 (WIDE kernel, sklearn's dtype)
+    wide_dtype: str = "f32"                   # wider models: f32 storage (the f64-accumulating WIDE kernel)
+                                              # | f64 (WIDE kernel, sklearn's dtype)
                                               # | bf16 (opt-in: bf16 GEMV / MFMA GEMM)
     split_max_rows: int = 32                  # bf16 multiclass: batches <= this many rows take the class-split kernel
     bar_rows: int = 32                        # GPU wide paths: batches <= this many rows go to HBM through the BAR (0 = off)
@@ -58,6 +58,7 @@ class Config:
     gemv_record_rows: int = 2                 # GEMV batches >= this many rows complete via records (0 = never)
     idle_inline_rows: int = 8                 # GPU: idle engine -> the IO thread launches <= this many rows itself (0 = off)
     wide_host_merge_blocks: int = 0           # GPU: WIDE batches merge class blocks on the host up to this many blocks (0 = in-kernel)
+    f32_gemv: bool = False                    # GPU: f32 binary F <= 2048 on the f32-accumulating GEMV (A/B)
     f32_split: bool = False                   # GPU: f32 multiclass F <= 512 on the f32-accumulating split kernel (A/B)
     lane_inflight: int = 3                    # GPU: combined lane batches in flight at most (rows coalesce behind them)
     lanes: int = 0                            # GPU: IO threads launch SMALL-model rows by flat combining (engine lanes; opt-in, measured slower)

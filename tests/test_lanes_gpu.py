@@ -60,8 +60,8 @@ def test_lanes_batch1_every_request_on_its_lane(native):
 
 
 def test_lanes_skip_wide_models(native):
-    """A model off the kernel-argument path (F = 64: GEMV) never takes a lane: the queued path
-    answers it, with the same bytes."""
+    """A model off the kernel-argument path (F = 64 binary: the WIDE kernel) never takes a lane: the
+    queued path answers it, with the same bytes."""
     F = 64
     names = [f"f{i}" for i in range(F)]
     m = LinearModel.random(F, 2, seed=2)

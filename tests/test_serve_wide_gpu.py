@@ -61,7 +61,7 @@ def _engine(native, **kw):
     (256, 2, Kind.BINARY, "bf16", "gemv"),
     (256, 2, Kind.BINARY_SOFTMAX, "bf16", "gemv"),
     (100, 2, Kind.BINARY, "bf16", "gemv"),        # F padded to 104
-    (256, 2, Kind.BINARY, "f32", "gemv"),
+    (256, 2, Kind.BINARY, "f32", "wide"),     # f32 storage, f64 accumulation (f32_gemv: the GEMV)
     (256, 1000, Kind.MULTINOMIAL, "bf16", "gemm"),
     (256, 50, Kind.OVR, "bf16", "gemm"),
     (100, 10, Kind.MULTINOMIAL, "bf16", "gemm"),  # F padded to 128
@@ -143,7 +143,7 @@ def test_bar_staged_rows_match_zero_copy(native, wide, K):
             e.stop()
     np.testing.assert_array_equal(outs[32][0], outs[0][0])
     np.testing.assert_array_equal(outs[32][1], outs[0][1])
-    check(m, X, outs[32][0], outs[32][1], wide, rtol=1e-11 if (wide == "f32" and K > 2) else 1e-4)
+    check(m, X, outs[32][0], outs[32][1], wide, rtol=1e-11 if wide == "f32" else 1e-4)
 
 @pytest.mark.parametrize("wide", ["bf16", "f32"])
 @pytest.mark.parametrize("F,kind", [(256, Kind.BINARY), (64, Kind.BINARY_SOFTMAX), (1024, Kind.BINARY)])
@@ -158,7 +158,7 @@ def test_direct_dispatched_gemv_batches_match_hip_launch(native, wide, F, kind):
     Xs = [rng.standard_normal((n, F)) for n in (1, 2, 3, 8, 1, 64, 250, 5)]
     outs = {}
     for mode in ("direct", "direct_nobar", "hip"):
-        e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide],
+        e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide], f32_gemv=True,
                     hsaco_path=str(hsaco_path()), direct_wide=(mode != "hip"),
                     direct_wide_max_weight_bytes=1 << 30, bar_rows=0 if mode == "direct_nobar" else 32)
         try:
@@ -269,10 +269,10 @@ def test_native_server_wide_model_every_response(native, K, kind):
         got = [json.loads(b) for _, b in res]
         idx = np.array([int(g["prediction"][1:]) for g in got])
         p = np.array([g["probability"] for g in got])
-        # the default wide dtype is f32 (bf16 is opt-in): f32 GEMV / f64-accumulating wide kernel
-        check(m, X, idx, p, "f32", rtol=1e-11 if K > 2 else 1e-5)
+        # the default wide dtype is f32 (bf16 is opt-in): the f64-accumulating wide kernel
+        check(m, X, idx, p, "f32", rtol=1e-11)
         st = srv.runtime.handle.stats()
-        path = "gemv" if K == 2 else "wide"
+        path = "wide"
         assert st["path_batches"][path] >= 1 and st["path_batches"]["generic"] == 0
         assert st["batches"] < st["requests"]
         assert srv.http.stats()["fast"] >= 1024  # no request fell back to the Python slow path
