@@ -17,9 +17,9 @@
 //    chunk. Without staging registers a wave can hold 32 rows (NT = 2), halving the LDS fragment
 //    reads per MFMA (B=262144: 230 -> 172 us);
 //  * small batches (B=1024 -> 16 row blocks) split the class range over gridDim.y so the launch
-//    fills the chip; the splits are merged IN THE SAME LAUNCH by the last-arriving block of each
-//    row block (partials stored write-through (sc1) + relaxed ticket, acquire fence in the reducer:
-//    Guideline 16 R1), replacing v1's separate merge kernel (7.3 us of a 18.6 us total);
+//    fills the chip; the splits are merged IN THE SAME LAUNCH by the last split's block of each
+//    row block, which polls the others' tagged 16-byte state granules (Guideline 16 R2; round 3
+//    took a ticket, round 1 ran a separate merge kernel: 7.3 us of a 18.6 us total);
 //  * the epilogue is branch-free per element (kind is a template parameter; a split's partial
 //    last chunk is masked to -inf) and uses exp2/rcp; accumulators start at the bias.
 //
@@ -30,6 +30,7 @@
 // ldx >= F; the forward reads only its first F columns).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <type_traits>
@@ -48,10 +49,9 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 constexpr int CLASS_CHUNK = 64;
 constexpr float LOG2E_F = 1.4426950408889634f;
 constexpr float LN2_F = 0.6931471805599453f;
-// Arrival counters live at the start of the workspace (split plans: one per row block); every plan
-// re-arms its counters to 0 and
-// the partials always start after this region, so plans of different batch sizes can share one
-// zero-initialised workspace.
+// The workspace starts with a counter region (its last slot: the XCD-local merge's error bits) and
+// the partial-state granules always start after it; granules carry a per-launch tag, so plans of
+// different batch sizes can share one zero-initialised workspace.
 constexpr int COUNTER_BYTES = 65536;
 constexpr int MERGE_MAX = 16;        // split partials the merging block loads at once (automatic plans: <= 16)
 
@@ -124,88 +124,149 @@ struct GemmArgs {
   float2* rowstat;         // MODE 2 output: {lse, argmax bits}
   float4* rowstate;        // MODE 4 output: {max, sum, argmax bits, 0} (class-sharded TP)
   unsigned long long* stamps;  // profiling (tools/gemm_phase_probe.py): 8 s_memtime slots per wave
-  int xcd_local;               // split merge meets in one XCD's L2 (grid.x % 8 == 0; see xcd_put_partial)
+  int xcd_local;               // split merge meets in one XCD's L2 (grid.x % 8 == 0; see put_granule)
   int xcd_inject;              // test hook (xcd_local_inject): every merged row reports a misplaced partial
+  unsigned epoch;              // split merge: this launch's granule tag (1 .. 2^28 - 1, see put_granule)
 };
 
-// ---- split-merge protocol (tiles kernels). Default (agent scope): partials stored write-through
-// (sc1), the ticket, and an agent-scope acquire (buffer_inv sc1) in the merging block. XCD-local
-// (a.xcd_local, chosen by the host when gridDim.x % 8 == 0): hardware blocks are dealt round-robin
-// over the 8 XCDs, so block b = y * gridDim.x + x runs on XCD (c + b) % 8 = (c + x) % 8 - c is
-// wherever the dispatcher's rotation stood when the launch began - and every split of row block
-// x runs on ONE XCD: the partials, the ticket and the merging block's loads all meet in that
-// XCD's L2 (plain stores, an L2 atomic and L1-bypassing sc0 loads; no write-through, no L2
-// invalidate). Each partial carries the XCD that wrote it (HW_REG_XCC_ID, 4th word); the merging
-// block checks them against its own and flags a mismatch in the last counter slot (bit = XCD).
+// ---- split-merge protocol (tiles kernels): tagged granules (cdna_hip_programming.md Guideline 16
+// R2, "the data is the flag", as in the WIDE kernel). Every class split but the last publishes each
+// of its rows' states as ONE 16-byte granule {m, s, argmax, tag = epoch << 4 | XCD} and exits: no
+// drain, ticket, barrier or fence on the producers. The last split's block of a row block (the
+// highest block index of the row block: dispatched after its producers) polls those granules with
+// sc1 loads until every tag carries this launch's epoch, merges them with its own state in
+// a fixed order, and clears the tags it consumed, so a HIP-graph replay (same epoch in its baked
+// arguments) never reads the previous replay's partials.
+// XCD-local (a.xcd_local, chosen by the host when gridDim.x % 8 == 0): hardware blocks are dealt
+// round-robin over the 8 XCDs, so block b = y * gridDim.x + x runs on XCD (c + b) % 8 = (c + x) % 8
+// - c is wherever the dispatcher's rotation stood when the launch began - and every split of row
+// block x runs on ONE XCD: the granules are plain stores into that XCD's L2 (no write-through).
+// The poll must not use sc0 loads: those are workgroup scope, the first pass leaves the stale line
+// in the CU's L1 and every later pass hits it (measured: every merge timed out, and buffer_inv sc0
+// between passes did not help; sc1 loads, or sc0 loads after buffer_inv sc1, saw the plain stores,
+// tools/dbg/gemm_merge_dbg.py). The tag's XCD field lets the merger check the placement; a
+// misplaced partial (or a poll that never completes, which is what a misplaced plain store looks
+// like) answers XCD_BAD_IDX and flags the last counter slot (bit = XCD), and the engine then turns
+// the protocol off. Agent scope: sc1 write-through stores; a poll that does not complete within 1 s
+// answers WIDE_TIMEOUT_IDX.
 constexpr int XCD_ERR_SLOT = COUNTER_BYTES / 4 - 1;
+constexpr int MERGE_OK = 0, MERGE_MISPLACED = 1, MERGE_TIMEOUT = 2;
 
 __device__ __forceinline__ unsigned my_xcc() {
   unsigned hw;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
   return hw & 15;
 }
-__device__ __forceinline__ void put_partial(const GemmArgs& a, int64_t idx, const RowState& S) {
-  float4* dst = a.partials + idx;
-  if (a.xcd_local) {
-    *dst = make_float4(S.m, S.s, __int_as_float(S.bi), __uint_as_float(my_xcc()));
-    return;
-  }
-  typedef __attribute__((address_space(1))) unsigned long long gu64_t;
-  typedef __attribute__((address_space(1))) unsigned int gu32_t;
-  const unsigned long long ms = (unsigned long long)__float_as_uint(S.m) | ((unsigned long long)__float_as_uint(S.s) << 32);
-  __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S.bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void put_granule(const GemmArgs& a, int64_t idx, const RowState& S) {
+  const u32x4_t v{__float_as_uint(S.m), __float_as_uint(S.s), (unsigned)S.bi,
+                  (a.epoch << 4) | (a.xcd_local ? my_xcc() : 0u)};
+  if (a.xcd_local)
+    *reinterpret_cast<u32x4_t*>(a.partials + idx) = v;
+  else
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(a.partials + idx), "v"(v) : "memory");
 }
-__device__ __forceinline__ unsigned take_ticket(const GemmArgs& a, unsigned slot) {
-  return a.xcd_local ? __hip_atomic_fetch_add(a.counters + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                     : __hip_atomic_fetch_add(a.counters + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// merging block: acquire (agent protocol only) and re-arm the counter
-__device__ __forceinline__ void merge_begin(const GemmArgs& a, unsigned slot) {
-  if (a.xcd_local) {
-    __hip_atomic_store(a.counters + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_store(a.counters + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// partial idx (float4 units) as seen by the merging block
-__device__ __forceinline__ float4 get_partial(const GemmArgs& a, int64_t idx) {
-  if (a.xcd_local) {  // cache policy sc0: miss this CU's L1, read the XCD's L2 (host: < 2^31 bytes)
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.partials, 0, 0x7fffffff, 0x00020000);
-    const f32x4_t t = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(idx * 16), 0, 1));
-    return make_float4(t[0], t[1], t[2], t[3]);
-  }
-  return a.partials[idx];
-}
-// merging block, XCD-local protocol: every partial it merges came from its own XCD's L2
-// (true: the row's merged state cannot be trusted - MODE 0 then returns XCD_BAD_IDX / NaN for it)
-__device__ __forceinline__ bool xcd_verify(const GemmArgs& a, const float4 (&p)[MERGE_MAX], unsigned ns) {
-  if (!a.xcd_local) return false;
-  const unsigned me = my_xcc();
-  bool bad = a.xcd_inject != 0;
-#pragma unroll
-  for (int sp = 0; sp < MERGE_MAX; ++sp) bad |= (unsigned)sp < ns && __float_as_uint(p[sp].w) != me;
-  if (bad) __hip_atomic_fetch_or(a.counters + XCD_ERR_SLOT, 1u << me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return bad;
-}
-// the first MERGE_MAX splits' partials of `row`, every load issued before the first use (one
-// round trip; the protocol branch sits outside the loads so none of them waits on another)
-__device__ __forceinline__ void get_partials(const GemmArgs& a, int64_t row, unsigned ns, float4 (&p)[MERGE_MAX]) {
+
+// Merging block: called by every lane of a wave. LPR lanes (lane offsets 64 / LPR apart) hold the
+// own state `own` of one row; lane qi of them takes splits qi, qi + LPR, ... (the first LPR * SL
+// splits' granules loaded together, one poll round trip; forced plans with more splits poll the
+// rest one by one). The merged state is the same on the row's LPR lanes; fail: MERGE_*.
+template <int LPR, int SL>
+__device__ __forceinline__ RowState granule_merge(const GemmArgs& a, int64_t row, int qi, const RowState& own,
+                                                  bool live, bool ovr, int& fail) {
+  const unsigned ns = gridDim.y;
   const int64_t B = a.B;
-  if (a.xcd_local) {
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.partials, 0, 0x7fffffff, 0x00020000);
-    f32x4_t t[MERGE_MAX];
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.partials, 0, 0x7fffffff, 0x00020000);
+  auto ld = [&](unsigned sp) -> u32x4_t {
+    return __builtin_bit_cast(u32x4_t,
+                              __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(((int64_t)sp * B + row) * 16), 0, 16));
+  };
+  const uint64_t t0 = wall_clock64();
+  bool timeout = false;
+  u32x4_t g[SL];
+  for (;;) {
+    bool ok = true;
 #pragma unroll
-    for (int sp = 0; sp < MERGE_MAX; ++sp)
-      t[sp] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                              rs, (uint32_t)(((int64_t)min((unsigned)sp, ns - 1) * B + row) * 16), 0, 1));
+    for (int u = 0; u < SL; ++u) {
+      const unsigned sp = qi + LPR * u;
+      if (live && sp + 1 < ns) g[u] = ld(sp);
+    }
 #pragma unroll
-    for (int sp = 0; sp < MERGE_MAX; ++sp) p[sp] = make_float4(t[sp][0], t[sp][1], t[sp][2], t[sp][3]);
+    for (int u = 0; u < SL; ++u) {
+      const unsigned sp = qi + LPR * u;
+      if (live && sp + 1 < ns) ok &= (g[u][3] >> 4) == a.epoch;
+    }
+    if (__all(ok)) break;
+    if (wall_clock64() - t0 > 100000000ull) {  // 1 s at 100 MHz: a producer never published
+      timeout = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");  // the next pass loads again
+  }
+  const unsigned me = a.xcd_local ? my_xcc() : 0u;
+  bool bad = a.xcd_inject != 0;
+  RowState S{-INFINITY, 0.f, 0x7fffffff};  // identity of merge_state (exact)
+  auto take = [&](unsigned sp, const u32x4_t& v) {
+    if (sp + 1 == ns) {
+      S = merge_state(S, own, ovr);
+      return;
+    }
+    bad |= a.xcd_local && (v[3] & 15u) != me;
+    S = merge_state(S, RowState{__uint_as_float(v[0]), __uint_as_float(v[1]), (int)v[2]}, ovr);
+  };
+#pragma unroll
+  for (int u = 0; u < SL; ++u) {
+    const unsigned sp = qi + LPR * u;
+    if (sp < ns) take(sp, g[u]);
+  }
+  for (unsigned sp = qi + LPR * SL; sp < ns; sp += LPR) {  // forced plans beyond MERGE_MAX splits
+    u32x4_t v{0u, 0u, 0u, 0u};
+    if (sp + 1 < ns && live && !timeout) {
+      for (;;) {
+        v = ld(sp);
+        if ((v[3] >> 4) == a.epoch) break;
+        if (wall_clock64() - t0 > 100000000ull) {
+          timeout = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+      }
+    }
+    take(sp, v);
+  }
+  // consumed: clear the tags (plain stores; the next launch's producers publish after this kernel)
+  if (live) {
+    unsigned* const base = reinterpret_cast<unsigned*>(a.partials);
+    for (unsigned sp = qi; sp + 1 < ns; sp += LPR) base[((int64_t)sp * B + row) * 4 + 3] = 0u;
+  }
+  int f = timeout ? 2 : bad ? 1 : 0;
+#pragma unroll
+  for (int off = 64 / LPR; off < 64; off <<= 1) {
+    S = merge_state(S, shfl_state(S, off), ovr);  // commutative: every lane of the row ends identical
+    f |= __shfl_xor(f, off, 64);
+  }
+  fail = f == 0 ? MERGE_OK : (a.xcd_local || (f & 1)) ? MERGE_MISPLACED : MERGE_TIMEOUT;
+  if (fail == MERGE_MISPLACED && live && qi == 0)
+    __hip_atomic_fetch_or(a.counters + XCD_ERR_SLOT, 1u << me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return S;
+}
+
+// a merged row's output; a failed merge answers XCD_BAD_IDX / WIDE_TIMEOUT_IDX with p NaN (MODE 0) or
+// NaN statistics (MODE 2 / 4: the loss turns NaN instead of training on a stale state)
+template <int MODE>
+__device__ __forceinline__ void finish_merged(const GemmArgs& a, int64_t row, const RowState& S, int fail, bool ovr) {
+  const float nan = __builtin_nanf("");
+  if constexpr (MODE == 0) {
+    if (fail != MERGE_OK)
+      put_result(a.out_idx, a.out_p, a.ro, row, fail == MERGE_MISPLACED ? XCD_BAD_IDX : WIDE_TIMEOUT_IDX, nan);
+    else
+      put_result(a.out_idx, a.out_p, a.ro, row, S.bi, ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s);
+  } else if constexpr (MODE == 4) {
+    a.rowstate[row] = fail != MERGE_OK ? make_float4(nan, nan, __int_as_float(S.bi), 0.f)
+                                       : make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
   } else {
-#pragma unroll
-    for (int sp = 0; sp < MERGE_MAX; ++sp) p[sp] = a.partials[(int64_t)min((unsigned)sp, ns - 1) * B + row];
+    a.rowstat[row] = make_float2(fail != MERGE_OK ? nan : S.m + __logf(S.s), __int_as_float(S.bi));
   }
 }
 
@@ -558,8 +619,7 @@ gemm_softmax_kernel(GemmArgs a) {
   // W chunk buffers: 8-wave blocks (one per CU) have the LDS for a third, which gives every DMA
   // two iterations to land instead of one; logits mode (stores in the loop) keeps two.
   constexpr int NBUF = (WV == 8 && MODE != 1) ? 3 : 2;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * BUF_BYTES + 16];
-  int* const flag = reinterpret_cast<int*>(smem + NBUF * BUF_BYTES);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * BUF_BYTES];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -712,51 +772,21 @@ gemm_softmax_kernel(GemmArgs a) {
       }
       return;
     }
-    // ---- split classes: publish partials, last-arriving block of this row block merges them.
-    // Agent protocol: partials stored write-through (sc1: agent-scope atomic stores into global
-    // memory), so no release fence (buffer_wbl2, ~1.7 us per block on the critical path) is needed
-    // before the ticket: every storing wave drains (vmcnt(0)), the workgroup barrier orders the
-    // waves, then one lane takes the ticket; the merging block keeps its agent acquire
-    // (cdna_hip_programming.md Guideline 16, R1). XCD-local protocol: see put_partial.
+    // ---- split classes: tagged-granule merge (put_granule / granule_merge)
+    if (blockIdx.y + 1 < gridDim.y) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int64_t row = row0 + t * 16 + col;
+        if (q == 0 && row < B) put_granule(a, (int64_t)blockIdx.y * B + row, st[t]);
+      }
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int64_t row = row0 + t * 16 + col;
-      if (q == 0 && row < B) put_partial(a, (int64_t)blockIdx.y * B + row, st[t]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-    __syncthreads();
-    if (tid == 0) *flag = take_ticket(a, blockIdx.x) == gridDim.y - 1;
-    __syncthreads();
-    if (*flag == 0) return;
-    if (tid == 0) merge_begin(a, blockIdx.x);
-    __syncthreads();
-    if (tid < ROWS_PER_BLOCK) {
-      const int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + tid;
-      if (row < B) {
-        // All splits' partials are issued before the first merge: a load-merge-load chain made each
-        // split one more dependent round trip to the memory-side cache (the partials were written
-        // by CUs of other XCDs), ~7 of them at B=1024.
-        const unsigned ns = gridDim.y;
-        float4 p[MERGE_MAX];
-        get_partials(a, row, ns, p);  // clamped: unconditional
-        const bool xbad = xcd_verify(a, p, ns);
-        RowState S{p[0].x, p[0].y, __float_as_int(p[0].z)};
-#pragma unroll
-        for (int sp = 1; sp < MERGE_MAX; ++sp)  // fixed split order: deterministic
-          if ((unsigned)sp < ns) S = merge_state(S, RowState{p[sp].x, p[sp].y, __float_as_int(p[sp].z)}, ovr);
-        for (unsigned sp = MERGE_MAX; sp < ns; ++sp) {  // plans with more splits (forced sweeps)
-          const float4 q = get_partial(a, (int64_t)sp * B + row);
-          S = merge_state(S, RowState{q.x, q.y, __float_as_int(q.z)}, ovr);
-        }
-        if constexpr (MODE == 0) {
-          put_result(a.out_idx, a.out_p, a.ro, row, xbad ? XCD_BAD_IDX : S.bi,
-                     xbad ? __builtin_nanf("") : ovr ? sigmoidf_(S.m) / S.s : 1.f / S.s);
-        } else if constexpr (MODE == 4) {
-          a.rowstate[row] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
-        } else {
-          a.rowstat[row] = make_float2(S.m + __logf(S.s), __int_as_float(S.bi));
-        }
-      }
+      int fail;
+      const RowState S = granule_merge<4, 4>(a, row, q, st[t], row < B, ovr, fail);
+      if (q == 0 && row < B) finish_merged<MODE>(a, row, S, fail, ovr);
     }
   }
 }
@@ -1029,8 +1059,7 @@ gemm_softmax32_kernel(GemmArgs a) {
   constexpr int PIECES = CLASS_CHUNK * NCH / NTHR;
   constexpr int NBUF = 2;
   static_assert(PIECES >= 1 && CLASS_CHUNK * NCH % NTHR == 0, "W chunk must split evenly over the block");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * BUF_BYTES + 16];
-  int* const flag = reinterpret_cast<int*>(smem + NBUF * BUF_BYTES);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NBUF * BUF_BYTES];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1141,43 +1170,21 @@ gemm_softmax32_kernel(GemmArgs a) {
     }
     return;
   }
-  // split classes: the 16x16 kernel's publish / last-arriver merge (see there)
+  // split classes: the 16x16 kernel's tagged-granule merge (see put_granule / granule_merge)
+  if (blockIdx.y + 1 < gridDim.y) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int64_t row = row0 + rt * 32 + col;
+      if (h == 0 && row < B) put_granule(a, (int64_t)blockIdx.y * B + row, S[rt]);
+    }
+    return;
+  }
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     const int64_t row = row0 + rt * 32 + col;
-    if (h == 0 && row < B) put_partial(a, (int64_t)blockIdx.y * B + row, S[rt]);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) *flag = take_ticket(a, blockIdx.x) == gridDim.y - 1;
-  __syncthreads();
-  if (*flag == 0) return;
-  if (tid == 0) merge_begin(a, blockIdx.x);
-  __syncthreads();
-  for (int mr = tid; mr < ROWS_PER_BLOCK; mr += NTHR) {
-    const int64_t mrow = (int64_t)blockIdx.x * ROWS_PER_BLOCK + mr;
-    if (mrow < B) {
-      const unsigned ns = gridDim.y;
-      float4 p[MERGE_MAX];
-      get_partials(a, mrow, ns, p);
-      const bool xbad = xcd_verify(a, p, ns);
-      RowState R{p[0].x, p[0].y, __float_as_int(p[0].z)};
-#pragma unroll
-      for (int sp = 1; sp < MERGE_MAX; ++sp)
-        if ((unsigned)sp < ns) R = merge_state(R, RowState{p[sp].x, p[sp].y, __float_as_int(p[sp].z)}, ovr);
-      for (unsigned sp = MERGE_MAX; sp < ns; ++sp) {
-        const float4 pq = get_partial(a, (int64_t)sp * B + mrow);
-        R = merge_state(R, RowState{pq.x, pq.y, __float_as_int(pq.z)}, ovr);
-      }
-      if constexpr (MODE == 0) {
-        put_result(a.out_idx, a.out_p, a.ro, mrow, xbad ? XCD_BAD_IDX : R.bi,
-                   xbad ? __builtin_nanf("") : ovr ? sigmoidf_(R.m) / R.s : 1.f / R.s);
-      } else if constexpr (MODE == 4) {
-        a.rowstate[mrow] = make_float4(R.m, R.s, __int_as_float(R.bi), 0.f);
-      } else {
-        a.rowstat[mrow] = make_float2(R.m + __logf(R.s), __int_as_float(R.bi));
-      }
-    }
+    int fail;
+    const RowState R = granule_merge<2, 4>(a, row, h, S[rt], row < B, ovr, fail);
+    if (h == 0 && row < B) finish_merged<MODE>(a, row, R, fail, ovr);
   }
 }
 
@@ -1533,7 +1540,9 @@ Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   Plan p;
   if (allow32 && t32_supported(F)) {
     if (g_force_kernel == 3 || g_force_kernel >= 5) p.k32 = 4;  // 5-9: 32x32 measurement variants
-    else if (g_force_kernel == 0 && B >= 16384) p.k32 = 4;
+    // B = 8192, K = 1000: 32x32 with 4 splits 10.2-10.4 us vs 16x16 10.8; at K = 100 (2 chunks)
+    // the 16x16 kernel keeps it (5.2-5.5 vs 6.7 us; profiles/r4_gemm_merge/)
+    else if (g_force_kernel == 0 && (B >= 16384 || (B >= 8192 && K >= 512))) p.k32 = 4;
   }
   // 32 rows per wave (NT = 2) halve the LDS fragment reads per MFMA. It pays once the register
   // staging is gone (LDS-DMA): B=262144 230 -> 172 us, B=8192 about even, B=1024 worse
@@ -1554,10 +1563,14 @@ Plan make_plan(int64_t B, int K, int F, bool training, bool allow32 = true) {
   const int rows_per_block = p.k32 ? 32 * p.rt32 * p.k32 : block_rows(F, p.nt);
   p.row_blocks = (B + rows_per_block - 1) / rows_per_block;
   const int chunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
-  // measured best: B=1024 -> 8 splits (128 blocks), B=8192 -> 4 (512 blocks): fill the chip, but
-  // keep >= 2 chunks per block so the LDS double buffer overlaps (the split merge is not free).
-  int64_t want = (512 + p.row_blocks - 1) / p.row_blocks;
-  if (want > chunks / 2) want = chunks / 2;
+  // Splits per row block, measured with the granule merge (profiles/r4_gemm_merge/, F = 256,
+  // K = 1000): one block per CU up to 64 row blocks (B = 1024: 16 splits of one 64-class chunk,
+  // 6.0 us vs 6.5 at 8 splits; B = 2048: 8), two per CU beyond (B = 8192: 4 splits); the 32x32
+  // kernel (128-row blocks) one per CU up to 128 row blocks (B = 16384: 2 splits, 15.4 vs 16.1 us).
+  // The round-3 ticket merge wanted >= 2 chunks per block (LDS double buffer) and 2 blocks per CU.
+  const int64_t one_per_cu = p.k32 ? 128 : 64;
+  int64_t want = p.row_blocks <= one_per_cu ? (256 + p.row_blocks - 1) / p.row_blocks
+                                            : (512 + p.row_blocks - 1) / p.row_blocks;
   int splits = (int)(want < 1 ? 1 : (want > chunks ? chunks : want));
   const int chunks_per_split = (chunks + splits - 1) / splits;
   p.classes_per_split = chunks_per_split * CLASS_CHUNK;
@@ -1606,11 +1619,20 @@ void launch32(const GemmArgs& args, const dim3& grid, int rt, hipStream_t stream
 
 void* g_stamps = nullptr;  // profiling hook (gemm_softmax_set_stamps)
 
+// split-merge granule tags: 28 bits, never 0 (a zero-initialised or cleared granule is never live)
+unsigned next_merge_epoch() {
+  static std::atomic<unsigned> e{0};
+  unsigned v;
+  do v = (e.fetch_add(1, std::memory_order_relaxed) + 1) & 0x0fffffffu;
+  while (v == 0);
+  return v;
+}
+
 template <int MODE>
 void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
   args.classes_per_split = plan.classes_per_split;
   args.stamps = static_cast<unsigned long long*>(g_stamps);
-  // XCD-local split merge (put_partial / xcd_verify): on by default, MLAPI_GEMM_XCD=0 selects the
+  // XCD-local split merge (put_granule / granule_merge): on by default, MLAPI_GEMM_XCD=0 selects the
   // agent-scope protocol. The grid's x extent is padded to a multiple of 8 (blocks past the batch
   // return at once) so that every split of a row block lands on the same XCD.
   static const int xcd_env = [] {
@@ -1623,6 +1645,12 @@ void launch_mode(GemmArgs args, int F, const Plan& plan, hipStream_t stream) {
                        ? 1
                        : 0;
   args.xcd_inject = args.xcd_local ? xcd_local_take_inject() : 0;
+  if (MODE != 1 && plan.splits > 1) {
+    // granule offsets are 32-bit buffer offsets (automatic plans split only below 512 row blocks)
+    if ((uint64_t)plan.splits * (uint64_t)args.B * 16u >= 0x7fffffffu)
+      throw std::invalid_argument("gemm_softmax: split plan's partials exceed 2 GiB");
+    args.epoch = next_merge_epoch();
+  }
   const dim3 grid((unsigned)(args.xcd_local ? rb_pad : plan.row_blocks), (unsigned)plan.splits);
   if (MODE != 1 && plan.k32) {
     if (F == 64) launch32<MODE, 2>(args, grid, plan.rt32, stream);

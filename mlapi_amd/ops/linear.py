@@ -90,8 +90,8 @@ class GemmSoftmax:
     def __init__(self, max_batch: int, n_classes: int, n_features: int, device):
         self.max_batch, self.K, self.F = max_batch, n_classes, n_features
         nbytes = C().gemm_softmax_workspace(max_batch, n_classes, n_features)
-        # zero-initialised once: the in-kernel split merge uses arrival counters at the start of
-        # the workspace, which the last-arriving block re-arms to 0 after every launch.
+        # zero-initialised once: the in-kernel split merge publishes tagged state granules here and
+        # the merging block clears the tags it consumed, so graph replays (one baked tag) stay exact.
         self.ws = torch.zeros(max(nbytes, 16), dtype=torch.uint8, device=device)
 
     def __call__(self, X, W, b, kind: int = Kind.MULTINOMIAL, out=None):
@@ -116,8 +116,9 @@ class GemmSoftmax:
         return idx, p
 
     def xcd_errors(self) -> int:
-        """Bit mask of XCDs whose merging block read a partial written on another XCD during an
-        XCD-local split merge (gemm_softmax.hip, xcd_verify); 0 while every merge stayed in one L2."""
+        """Bit mask of XCDs whose merging block read a partial written on another XCD (or never saw
+        one) during an XCD-local split merge (gemm_softmax.hip, granule_merge); 0 while every merge
+        stayed in one L2."""
         o = C().gemm_softmax_xcd_err_offset()
         if self.ws.numel() < o + 4:
             return 0  # no split plan has run: nothing was checked
@@ -174,7 +175,8 @@ class LinearWide:
     W is [1, F]). Returns (int32 label index, f64 p_max). A row whose in-kernel class merge gave up
     waiting (1 s: a class block never ran - not expected, the launch's blocks are dispatched in
     order) comes back as index WIDE_TIMEOUT_IDX (-3) and p NaN; :meth:`failed` counts them (it
-    synchronises)."""
+    synchronises). Eager launches only: every call tags its class-merge granules with a fresh epoch,
+    which a captured HIP graph would freeze."""
 
     WIDE_TIMEOUT_IDX = -3
 

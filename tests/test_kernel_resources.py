@@ -5,7 +5,8 @@ performance regression the numerics tests cannot see. The budgets are the ones t
 designed for (docs/PERFORMANCE.md, MI355X_MICROARCH.md register table): two waves per SIMD
 (<= 256 VGPRs incl. AGPRs) for the 32x32 gemm_softmax kernel; no scratch at all in the class-split
 and wide (f64 MFMA) serving kernels; no scratch access inside the MFMA loop of the 32x32 kernel (its
-OvR instantiations spill 12 bytes around the loop, not in it).
+KS = 8 OvR instantiations spill 28 bytes around the loop - stored before it, reloaded for the split
+merge after it - not in it).
 """
 import re
 import shutil
@@ -45,11 +46,23 @@ def _pick(res: dict, pattern: str) -> dict:
 
 
 def _mfma_loop_blocks(text: str, kernel: str):
-    """Basic blocks of `kernel` that issue >= 16 MFMAs (the pipelined class loop: 2 x F/16 per chunk)."""
+    """Basic blocks of `kernel` inside a loop (between a label and a later branch back to it) that
+    issue >= 16 MFMAs: the pipelined class loop (2 x F/16 per chunk), not the prologue's first chunk."""
     start = text.index(kernel + ":")
     body = text[start:text.index(".Lfunc_end", start)]
-    for blk in re.split(r"\n\.LBB\w+:", body):
-        if blk.count("v_mfma") >= 16:
+    parts = re.split(r"\n(\.LBB\w+):", body)
+    labels = [None] + parts[1::2]
+    blocks = [parts[0]] + parts[2::2]
+    pos = {lab: i for i, lab in enumerate(labels) if lab}
+    in_loop = [False] * len(blocks)
+    for j, blk in enumerate(blocks):
+        for target in re.findall(r"s_c?branch\w*\s+(\.LBB\w+)", blk):
+            i = pos.get(target)
+            if i is not None and i <= j:
+                for k in range(i, j + 1):
+                    in_loop[k] = True
+    for blk, loop in zip(blocks, in_loop):
+        if loop and blk.count("v_mfma") >= 16:
             yield blk
 
 
