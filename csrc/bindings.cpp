@@ -530,6 +530,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("pipeline_cap", &ServerConfig::pipeline_cap)
       .def_readwrite("io_spin_us", &ServerConfig::io_spin_us)
       .def_readwrite("io_wait_spin_us", &ServerConfig::io_wait_spin_us)
+      .def_readwrite("idle_max_conns", &ServerConfig::idle_max_conns)
       .def_readwrite("io_spin_lowload_us", &ServerConfig::io_spin_lowload_us)
       .def_readwrite("io_spin_max_conns", &ServerConfig::io_spin_max_conns)
       .def_readwrite("access_log", &ServerConfig::access_log)

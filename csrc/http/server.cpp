@@ -345,9 +345,11 @@ class IoThread : public Sink {
       idle_done_.clear();
       std::shared_ptr<const Model> m;
       // wide models too while the server is at low load (a batch=1 client)
-      const bool low = srv_->open_conns.load(std::memory_order_relaxed) <= srv_->config().io_spin_max_conns;
-      bool ran;
-      {
+      const int conns = srv_->open_conns.load(std::memory_order_relaxed);
+      const bool low = conns <= srv_->config().io_spin_max_conns;
+      const int idle_max = srv_->config().idle_max_conns;
+      bool ran = false;
+      if (idle_max <= 0 || conns <= idle_max) {
         Stage sg2(this, SS_IDLE_GPU);
         ran = srv_->engine()->run_idle(pend_x_.data(), n, (int)nfeat_, pend_tags_.data(), idle_done_, m, low);
       }

@@ -58,6 +58,7 @@ struct ServerConfig {
   // the request path). 0 = off. 1-5 us measured +4-21 % c=64 req/s over 0 on three boxes, 15-30
   // us lost (the spinning threads take the load generator's CPU): profiles/r4_waitspin/.
   int io_wait_spin_us = 3;
+  int idle_max_conns = 0;  // idle-engine path only while <= this many connections are open (0 = any)
   // Low-load busy-poll: while the whole server holds at most io_spin_max_conns open connections
   // (a batch=1 client), an IO thread that just had activity polls for this long before blocking,
   // so the client's next request does not pay an idle-thread wake-up. Under concurrency (more

@@ -48,6 +48,7 @@ class Config:
     io_wait_spin_us: int = 3                  # IO threads with rows in the engine watch for the hand-off this
                                               # long in user space before blocking (0 = off; 1-5 us measured
                                               # best, profiles/r4_waitspin/)
+    idle_max_conns: int = 0                   # idle-engine path only while <= this many connections are open (0 = any)
     io_spin_lowload_us: int = 50              # ... only while <= io_spin_max_conns connections are open (batch=1 clients)
     io_spin_max_conns: int = 2
     max_queue: int = 1 << 20                  # backpressure: queued rows beyond this -> HTTP 503

@@ -161,7 +161,7 @@ def test_gemm_softmax_large_batch_and_rearm():
 @pytest.mark.parametrize("B", [1024, 8192])
 def test_gemm_softmax_xcd_local_merge_repeated(B, kind):
     """BASELINE config 3 (B = 1024, K = 1000, F = 256) and a 4-split plan: the row blocks' splits meet
-    in one XCD's L2 (gemm_softmax.hip, put_partial). Twenty back-to-back launches on fresh inputs all
+    in one XCD's L2 (gemm_softmax.hip, put_granule). Twenty back-to-back launches on fresh inputs all
     match the oracle, and every merged partial came from the merging block's XCD."""
     F, K = 256, 1000
     W = _rand((K, F), torch.bfloat16, 61, scale=1 / 16)
@@ -183,6 +183,39 @@ def test_gemm_softmax_xcd_local_merge_repeated(B, kind):
         assert torch.equal(idx[clear].cpu(), ridx[clear].cpu())
         torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=2e-4, atol=2e-5)
     assert op.xcd_errors() == 0
+
+
+@pytest.mark.parametrize("B", [100, 1024, 8192])
+def test_gemm_softmax_split_merge_graph_replay(B):
+    """A HIP graph bakes the split merge's granule tag into its arguments: every replay runs with
+    the same epoch, so the merging block must clear the tags it consumed or the next replay would
+    merge the previous replay's partials. Five replays on new inputs copied into the captured
+    tensor all match the oracle."""
+    F, K = 256, 1000
+    W = _rand((K, F), torch.bfloat16, 71, scale=1 / 16)
+    b = _rand((K,), torch.float32, 72, scale=0.1)
+    op = ops.GemmSoftmax(B, K, F, DEV)
+    X = _rand((B, F), torch.bfloat16, 73)
+    out = (torch.empty(B, dtype=torch.int32, device=DEV), torch.empty(B, dtype=torch.float32, device=DEV))
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        op(X, W, b, Kind.MULTINOMIAL, out=out)  # warm-up outside the capture
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        op(X, W, b, Kind.MULTINOMIAL, out=out)
+    for i in range(5):
+        Xi = _rand((B, F), torch.bfloat16, 300 + i)
+        X.copy_(Xi)
+        g.replay()
+        torch.cuda.synchronize()
+        Z = ref.logits_ref(Xi, W, b, dtype=torch.float64)
+        ridx, rp = ref.predict_ref(Xi, W, b, Kind.MULTINOMIAL)
+        top2 = torch.topk(Z, 2, dim=1).values
+        clear = (top2[:, 0] - top2[:, 1]) > 1e-3
+        assert torch.equal(out[0][clear].cpu(), ridx[clear].cpu()), i
+        torch.testing.assert_close(out[1].double().cpu(), rp.cpu(), rtol=2e-4, atol=2e-5)
 
 
 @pytest.mark.parametrize("kernel", [1, 2])
