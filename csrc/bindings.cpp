@@ -179,6 +179,18 @@ PYBIND11_MODULE(_C, m) {
       py::arg("dt"), py::arg("X"), py::arg("w"), py::arg("bias"), py::arg("B"), py::arg("F"), py::arg("kind"),
       py::arg("out_idx"), py::arg("out_p"), py::arg("stream") = 0);
   m.def("gemm_softmax_workspace", &gemm_softmax_workspace);
+  m.def("gemm_softmax_plan", [](int64_t B, int K, int F) {
+    int64_t o[5];
+    gemm_softmax_plan_info(B, K, F, o);
+    static const char* kernels[] = {"tiles", "t32", "rows"};
+    py::dict d;
+    d["kernel"] = kernels[o[0]];
+    d["nt"] = o[1];
+    d["splits"] = o[2];
+    d["classes_per_split"] = o[3];
+    d["row_blocks"] = o[4];
+    return d;
+  });
   m.def("gemm_softmax_force_plan", &gemm_softmax_force_plan, py::arg("nt") = 0, py::arg("splits") = 0,
         py::arg("kernel") = 0);
   m.def("gemm_softmax_set_stamps", [](uintptr_t p) { gemm_softmax_set_stamps(reinterpret_cast<void*>(p)); });

@@ -118,6 +118,9 @@ void launch_gemv_binary(int dt, const void* X, const void* w, float bias, int64_
 // width: the row-group kernel loops F in 256-feature slices). Workspace: gemm_softmax_workspace()
 // (0 when the row-group kernel serves the shape).
 size_t gemm_softmax_workspace(int64_t B, int K, int F);
+// The automatic plan of a gemm_softmax call (host only): out = {kernel (0 16x16 tiles, 1 32x32,
+// 2 row-group), 16-row tiles per wave, class splits, classes per split, row blocks}.
+void gemm_softmax_plan_info(int64_t B, int K, int F, int64_t out[5]);
 // Benchmark hook: force the tiles kernel's (rows-per-wave tiles, class splits) plan and the
 // kernel (0 automatic, 1 tiles 16x16x32, 2 row-group, 3 tiles 32x32x16); all 0 = automatic.
 void gemm_softmax_force_plan(int nt, int splits, int kernel = 0);

@@ -1744,6 +1744,15 @@ void launch_softmax_rowstats(const void* X_aug, int64_t ldx, const void* W, cons
   launch_mode<2>(args, F, plan, stream);
 }
 
+void gemm_softmax_plan_info(int64_t B, int K, int F, int64_t out[5]) {
+  if (use_rows(B, F)) {
+    out[0] = 2, out[1] = 0, out[2] = 1, out[3] = K, out[4] = 0;
+    return;
+  }
+  const Plan p = make_plan(B, K, F, false);
+  out[0] = p.k32 ? 1 : 0, out[1] = p.nt, out[2] = p.splits, out[3] = p.classes_per_split, out[4] = p.row_blocks;
+}
+
 size_t gemm_softmax_workspace(int64_t B, int K, int F) {
   if (use_rows(B, F)) return 0;
   const Plan p = make_plan(B, K, F, false);

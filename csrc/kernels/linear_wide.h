@@ -459,6 +459,16 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   } else {
     reduce_max();
   }
+  // consumed: clear the granules' tags with write-through stores (no dirty line is left behind to
+  // be written back over a later launch's granule), so a HIP-graph replay - one epoch baked into
+  // its arguments - never merges the previous replay's states
+  if (live && !timeout) {
+    for (int b = part; b < a.ncb; b += 8) {
+      gu32_t* const t = (gu32_t*)(states + ((int64_t)b * RG + rl) * 4);
+      __hip_atomic_store(t + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(t + 7, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   if (nan) SS = NAN;
   SS += __shfl_xor(SS, 1, 64);
   SS += __shfl_xor(SS, 2, 64);

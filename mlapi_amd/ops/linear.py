@@ -175,8 +175,8 @@ class LinearWide:
     W is [1, F]). Returns (int32 label index, f64 p_max). A row whose in-kernel class merge gave up
     waiting (1 s: a class block never ran - not expected, the launch's blocks are dispatched in
     order) comes back as index WIDE_TIMEOUT_IDX (-3) and p NaN; :meth:`failed` counts them (it
-    synchronises). Eager launches only: every call tags its class-merge granules with a fresh epoch,
-    which a captured HIP graph would freeze."""
+    synchronises). HIP-graph capture is safe: the merging block clears the tags of the granules it
+    consumed, so replays (one epoch baked into the graph) never see the previous replay's states."""
 
     WIDE_TIMEOUT_IDX = -3
 

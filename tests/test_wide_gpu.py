@@ -203,3 +203,34 @@ def test_class_merge_timeout_fails_rows_not_answers(native):
     torch.cuda.synchronize()
     assert op.failed(idx) == 0
     _oracle_check(m, X, idx.cpu().numpy(), p.cpu().numpy())
+
+
+@pytest.mark.parametrize("B", [8, 100])
+def test_linear_wide_graph_replay(B):
+    """A captured HIP graph replays the WIDE launch with ONE class-merge epoch baked in: the merging
+    block clears the tags it consumed, so five replays on new rows copied into the captured input
+    all match the oracle (without the clear, replay k would merge replay k - 1's states)."""
+    from mlapi_amd.ops.linear import LinearWide
+
+    F, K = 256, 1000
+    m = LinearModel.random(F, K, seed=91, kind=Kind.MULTINOMIAL)
+    op = LinearWide(B, F, K, torch.float64, "cuda")
+    Wg = torch.tensor(m.W, device="cuda", dtype=torch.float64).contiguous()
+    bg = torch.tensor(m.b, device="cuda", dtype=torch.float64)
+    X = torch.zeros(B, F, device="cuda", dtype=torch.float64)
+    out = (torch.empty(B, dtype=torch.int32, device="cuda"), torch.empty(B, dtype=torch.float64, device="cuda"))
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        op(X, Wg, bg, int(Kind.MULTINOMIAL), out=out)  # warm-up outside the capture
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        op(X, Wg, bg, int(Kind.MULTINOMIAL), out=out)
+    rng = np.random.default_rng(92)
+    for i in range(5):
+        Xn = rng.standard_normal((B, F))
+        X.copy_(torch.tensor(Xn, device="cuda"))
+        g.replay()
+        torch.cuda.synchronize()
+        _oracle_check(m, Xn, out[0].cpu().numpy(), out[1].cpu().numpy())
