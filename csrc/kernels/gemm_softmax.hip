@@ -235,10 +235,13 @@ __device__ __forceinline__ RowState granule_merge(const GemmArgs& a, int64_t row
     }
     take(sp, v);
   }
-  // consumed: clear the tags (plain stores; the next launch's producers publish after this kernel)
-  if (live) {
-    unsigned* const base = reinterpret_cast<unsigned*>(a.partials);
-    for (unsigned sp = qi; sp + 1 < ns; sp += LPR) base[((int64_t)sp * B + row) * 4 + 3] = 0u;
+  // consumed: clear the tags (write-through: no dirty line is left to be written back over a later
+  // launch's granule)
+  if (live && !timeout) {
+    typedef __attribute__((address_space(1))) unsigned int gu32_t;
+    gu32_t* const base = (gu32_t*)a.partials;
+    for (unsigned sp = qi; sp + 1 < ns; sp += LPR)
+      __hip_atomic_store(base + ((int64_t)sp * B + row) * 4 + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   int f = timeout ? 2 : bad ? 1 : 0;
 #pragma unroll

@@ -15,17 +15,16 @@
 //  * epilogue in registers: a lane holds 4 classes of one row; 2 xor-shuffles merge the 4 lane
 //    groups, the 4 waves merge through 512 B of LDS in fixed order (first max wins: ties go to the
 //    lower class index, like numpy's argmax);
-//  * split merge with ONE cross-block round trip: wave 0 stores the block's row states
-//    write-through (sc1), drains them (vmcnt(0)), and takes a ticket on its row group's counter;
-//    the last arriver (agent-scope acquire) loads every split's state in fixed split order and
-//    writes (label, p_max) - or the serving completion record.
+//  * split merge with ONE cross-block round trip (round 4: tagged granules): wave 0 of every split
+//    but the last stores the block's row states as 16-byte granules tagged with the launch's epoch
+//    and exits; the row group's last split polls them, merges in fixed split order and writes
+//    (label, p_max) - or the serving completion record. (Round 3: a drained store, a ticket and an
+//    acquire in the last arriver.)
 //  * XCD-local merge (xcd_local): the grid is 1-D and ordered so that every split of a row group
 //    runs on ONE XCD (blocks are dealt round-robin over the 8 XCDs, starting wherever the
 //    dispatcher's rotation stood: block b runs on XCD (c + b) % 8, and the splits of row group r
-//    are the blocks with b % 8 == r % 8). All of the protocol's traffic - partial stores, the
-//    ticket, the last arriver's loads - then meets in that XCD's L2: plain stores, an L2 atomic and
-//    L1-bypassing (sc0) loads, with no write-through to HBM and no agent-scope L2 invalidate
-//    (buffer_inv sc1) on the merge path. Each partial carries the XCD that wrote it
+//    are the blocks with b % 8 == r % 8). The granules are then plain stores into that XCD's L2
+//    (no write-through to HBM), polled with sc1 loads. Each granule carries the XCD that wrote it
 //    (HW_REG_XCC_ID); the merging block checks them and flags a mismatch in the error word.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -52,8 +51,8 @@ struct SplitArgs {
   int32_t* out_idx;
   float* out_p;
   RecOut ro;            // serving: per-row completion records instead of out_idx / out_p
-  unsigned int* counters;  // [row groups], zero between launches (re-armed by the merging block)
-  float4* partials;        // [row groups][nsplit][32] {m, s, argmax bits, 0}
+  unsigned int* counters;  // start of the workspace (its error word: xcd_err)
+  float4* partials;        // [row groups][nsplit][32] state granules {m, s, argmax bits, epoch << 4 | XCD}
   unsigned int* xcd_err;   // xcd_local: bit x set when a merging block on XCD x read a partial written elsewhere
   int32_t xcd_local;        // 1-D XCD-ordered grid + L2-local merge protocol (see the header)
   int32_t xcd_inject;       // test hook (xcd_local_inject): every merged row reports a misplaced partial
@@ -65,6 +64,7 @@ struct SplitArgs {
   // split order (csrc/runtime/engine.cpp, collect()).
   uint4* hrec;
   uint32_t rec_seq;
+  uint32_t epoch;  // split merge: this launch's granule tag (1 .. 2^28 - 1)
 };
 
 struct SState {
@@ -185,7 +185,6 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
   const int64_t row = row0 + l;
   const bool live = l < NB * 16 && row < a.B;
   SState S{-INFINITY, 0.f, 0x7fffffff};
-  bool xbad = false;  // XCD-local merge read a partial written on another XCD (or the test hook)
   if (l < NB * 16) {
     const float4 v0 = red[0][l];
     S = SState{v0.x, v0.y, __float_as_int(v0.z)};
@@ -205,78 +204,84 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
     }
     return;
   }
+  int fail = 0;  // 1: misplaced (XCD-local) partial, 2: the poll gave up
   if (a.nsplit > 1) {
-    // one cross-block round trip: partials, drained, then the row group's ticket
-    typedef __attribute__((address_space(1))) unsigned long long gu64_t;
+    // Tagged granules (cdna_hip_programming.md Guideline 16 R2; the protocol of gemm_softmax.hip):
+    // every split but the last stores its rows' states as ONE 16-byte granule {m, s, argmax,
+    // epoch << 4 | XCD} and exits - no drain, ticket or fence; the row group's last split (its
+    // highest block index in both grid orders: dispatched after its producers) polls them with sc1
+    // loads, merges in split order and clears the tags it consumed (graph replays re-use one epoch).
+    typedef __attribute__((ext_vector_type(4))) uint32_t su32x4_t;
     typedef __attribute__((address_space(1))) unsigned int gu32_t;
     float4* part = a.partials + ((int64_t)rgi * a.nsplit) * ROWS_PER_GROUP;
-    unsigned int* ctr = a.counters + rgi;
-    if (live) {
-      float4* dst = part + (int64_t)split * ROWS_PER_GROUP + l;
-      if (a.xcd_local) {  // plain store: L1 is write-through, the row group's L2 is the meeting point
-        unsigned hw;      // 4th word: the XCD that wrote it (checked by the merging block)
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
-        *dst = make_float4(S.m, S.s, __int_as_float(S.bi), __uint_as_float(hw & 15));
-      } else {  // write-through past this XCD's L2
-        const unsigned long long ms =
-            (unsigned long long)__float_as_uint(S.m) | ((unsigned long long)__float_as_uint(S.s) << 32);
-        __hip_atomic_store((gu64_t*)dst, ms, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gu32_t*)dst + 2, (unsigned)S.bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stores are acknowledged before the ticket
-    if (a.probe == 2) return;
-    unsigned ticket = 0;
-    if (l == 0)
-      ticket = a.xcd_local ? __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                           : __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ticket = __shfl(ticket, 0, 64);
-    if (ticket != (unsigned)a.nsplit - 1) return;
+    unsigned me = 0;
     if (a.xcd_local) {
-      if (l == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      if (l == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(me));
+      me &= 15;
     }
-    if (!live) return;
-    // fixed split order (deterministic); 16 states in flight per batch of loads
-    const float4* src = part + l;
-    float4 v[16];
+    if (split + 1 < a.nsplit) {
+      if (live) {
+        const su32x4_t v = {__float_as_uint(S.m), __float_as_uint(S.s), (uint32_t)S.bi, (a.epoch << 4) | me};
+        float4* dst = part + (int64_t)split * ROWS_PER_GROUP + l;
+        if (a.xcd_local)  // plain store: L1 is write-through, the row group's L2 is the meeting point
+          *reinterpret_cast<su32x4_t*>(dst) = v;
+        else  // write-through past this XCD's L2
+          asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(v) : "memory");
+      }
+      return;
+    }
+    if (a.probe == 2) return;
+    // sc1 loads (agent scope: past the CU's L1, which would keep serving a stale line to an sc0 poll)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, a.nsplit * ROWS_PER_GROUP * 16, 0x00020000);
+    const SState own = S;
     S = SState{-INFINITY, 0.f, 0x7fffffff};
-    for (int sp0 = 0; sp0 < a.nsplit; sp0 += 16) {
-      if (a.xcd_local) {  // cache policy sc0: miss this CU's L1, read the row group's L2
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)part, 0, a.nsplit * ROWS_PER_GROUP * 16, 0x00020000);
+    bool bad = a.xcd_inject != 0, timeout = false;
+    const uint64_t t0 = wall_clock64();
+    su32x4_t v[16];
+    for (int sp0 = 0; sp0 < a.nsplit && !timeout; sp0 += 16) {
+      for (;;) {  // 16 granules in flight per pass
+        bool ok = true;
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const sf32x4_t t = __builtin_bit_cast(
-              sf32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-                            rs, (uint32_t)((min(sp0 + u, a.nsplit - 1) * ROWS_PER_GROUP + l) * 16), 0, 1));
-          v[u] = make_float4(t[0], t[1], t[2], t[3]);
+        for (int u = 0; u < 16; ++u)
+          if (live && sp0 + u + 1 < a.nsplit)
+            v[u] = __builtin_bit_cast(su32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    rs, (uint32_t)(((sp0 + u) * ROWS_PER_GROUP + l) * 16), 0, 16));
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (live && sp0 + u + 1 < a.nsplit) ok &= (v[u][3] >> 4) == a.epoch;
+        if (__all(ok)) break;
+        if (wall_clock64() - t0 > 100000000ull) {  // 1 s at 100 MHz: a split never published
+          timeout = true;
+          break;
         }
-      } else {
-#pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = src[(int64_t)min(sp0 + u, a.nsplit - 1) * ROWS_PER_GROUP];
+        __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");  // the next pass loads again
       }
 #pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (sp0 + u < a.nsplit) S = smerge(S, SState{v[u].x, v[u].y, __float_as_int(v[u].z)}, OVR);
-      if (a.xcd_local) {  // every merged state came from this XCD's L2
-        unsigned me;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(me));
-        me &= 15;
-        bool bad = a.xcd_inject != 0;
-#pragma unroll
-        for (int u = 0; u < 16; ++u) bad |= sp0 + u < a.nsplit && __float_as_uint(v[u].w) != me;
-        if (bad) __hip_atomic_fetch_or(a.xcd_err, 1u << me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        xbad |= bad;
+      for (int u = 0; u < 16; ++u) {  // fixed split order (deterministic)
+        const int sp = sp0 + u;
+        if (sp + 1 == a.nsplit) {
+          S = smerge(S, own, OVR);
+        } else if (sp + 1 < a.nsplit) {
+          bad |= a.xcd_local && (v[u][3] & 15u) != me;
+          S = smerge(S, SState{__uint_as_float(v[u][0]), __uint_as_float(v[u][1]), (int)v[u][2]}, OVR);
+        }
       }
     }
+    if (live && !timeout)  // consumed: clear the tags (write-through: no dirty line left behind)
+      for (int sp = 0; sp + 1 < a.nsplit; ++sp)
+        __hip_atomic_store((gu32_t*)(part + (int64_t)sp * ROWS_PER_GROUP + l) + 3, 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    bad = live && bad;
+    fail = (bad || (timeout && a.xcd_local)) ? 1 : timeout ? 2 : 0;
+    if (fail == 1) __hip_atomic_fetch_or(a.xcd_err, 1u << me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (!live) return;
   const float p = OVR ? ssigmoid(S.m) / S.s : 1.f / S.s;
   // a misplaced merge never answers: the row comes back as XCD_BAD_IDX / NaN (the engine fails it
-  // and switches the XCD-local protocol off)
-  put_result(a.out_idx, a.out_p, a.ro, row, xbad ? XCD_BAD_IDX : S.bi, xbad ? __builtin_nanf("") : p);
+  // and switches the XCD-local protocol off); a poll that gave up, WIDE_TIMEOUT_IDX / NaN
+  put_result(a.out_idx, a.out_p, a.ro, row, fail == 1 ? XCD_BAD_IDX : fail == 2 ? WIDE_TIMEOUT_IDX : S.bi,
+             fail ? __builtin_nanf("") : p);
 }
 
 }  // namespace split

@@ -1,6 +1,7 @@
 // Host launchers of the class-split multiclass predict (linear_split.h).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
@@ -114,6 +115,9 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
   }();
   a.xcd_local = (xcd_env != 0 && ns > 1 && sro.rec == nullptr && xcd_local_allowed(stream)) ? 1 : 0;
   a.xcd_inject = a.xcd_local ? xcd_local_take_inject() : 0;
+  static std::atomic<uint32_t> epochs{0};  // split-merge granule tags: 28 bits, never 0
+  do a.epoch = (epochs.fetch_add(1, std::memory_order_relaxed) + 1) & 0x0fffffffu;
+  while (a.epoch == 0);
   a.row_groups = rg;
   a.xcd_err = reinterpret_cast<unsigned int*>(static_cast<unsigned char*>(workspace) + XCD_ERR_OFFSET);
   // XCD-ordered 1-D grid: 8 XCDs x ceil(rg / 8) row groups x ns splits (blocks past rg exit at once)
