@@ -235,13 +235,14 @@ __device__ __forceinline__ RowState granule_merge(const GemmArgs& a, int64_t row
     }
     take(sp, v);
   }
-  // consumed: clear the tags (write-through: no dirty line is left to be written back over a later
-  // launch's granule)
+  // consumed: clear the tags. Plain stores: this kernel is only launched on HIP streams, whose
+  // system-scope release at kernel end writes dirty L2 lines back before the next launch (the
+  // direct-dispatched serving kernels, which may run without that release, clear write-through).
+  // Measured: B = 1024 5.72 vs 5.82 us, B = 8192 9.8 vs 10.0 us with write-through clears
+  // (profiles/r4_gemm_merge/s34/).
   if (live && !timeout) {
-    typedef __attribute__((address_space(1))) unsigned int gu32_t;
-    gu32_t* const base = (gu32_t*)a.partials;
-    for (unsigned sp = qi; sp + 1 < ns; sp += LPR)
-      __hip_atomic_store(base + ((int64_t)sp * B + row) * 4 + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned* const base = reinterpret_cast<unsigned*>(a.partials);
+    for (unsigned sp = qi; sp + 1 < ns; sp += LPR) base[((int64_t)sp * B + row) * 4 + 3] = 0u;
   }
   int f = timeout ? 2 : bad ? 1 : 0;
 #pragma unroll
