@@ -20,17 +20,18 @@ NAMES = ["sepal_length", "sepal_width", "petal_length", "petal_width"]
 A1 = b'{"sepal_length":5.1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}'
 
 
-@pytest.fixture(params=[(0, 0), (200, 0), (0, 20)], ids=["block", "spin", "waitspin"])
+@pytest.fixture(params=[(0, 0, 0), (200, 0, 0), (0, 20, 0), (0, 3, 1)], ids=["block", "spin", "waitspin", "idlegate"])
 def server(iris_cwd, request):
     """Blocking IO threads; busy-polling IO threads + spinning batcher / completer (the completion
     hand-off then skips the eventfd); IO threads that watch for their rows' hand-off for a bounded
-    while before blocking (io_wait_spin_us)."""
+    while before blocking (io_wait_spin_us); the idle-engine path only while one connection is open
+    (idle_max_conns)."""
     from mlapi_amd.serve.server import NativeServer
     from mlapi_amd.utils.config import Config
 
-    spin, wait_spin = request.param
+    spin, wait_spin, idle_max = request.param
     srv = NativeServer(Config.from_env(port=0, device="cpu", io_threads=2, io_spin_us=spin, spin_us=spin,
-                                       io_wait_spin_us=wait_spin)).start()
+                                       io_wait_spin_us=wait_spin, idle_max_conns=idle_max)).start()
     yield srv
     srv.stop()
 
