@@ -65,6 +65,7 @@ struct SplitArgs {
   uint4* hrec;
   uint32_t rec_seq;
   uint32_t epoch;  // split merge: this launch's granule tag (1 .. 2^28 - 1)
+  int32_t clear_tags;  // the merger clears the tags it consumed (set for HIP-graph captures only)
 };
 
 struct SState {
@@ -268,7 +269,7 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
         }
       }
     }
-    if (live && !timeout)  // consumed: clear the tags (write-through: no dirty line left behind)
+    if (a.clear_tags && live && !timeout)  // graph captures: clear the tags (write-through: no dirty line)
       for (int sp = 0; sp + 1 < a.nsplit; ++sp)
         __hip_atomic_store((gu32_t*)(part + (int64_t)sp * ROWS_PER_GROUP + l) + 3, 0u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);

@@ -118,6 +118,11 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
   static std::atomic<uint32_t> epochs{0};  // split-merge granule tags: 28 bits, never 0
   do a.epoch = (epochs.fetch_add(1, std::memory_order_relaxed) + 1) & 0x0fffffffu;
   while (a.epoch == 0);
+  {  // a launch being captured into a HIP graph replays its epoch: its merger clears the tags
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (direct == nullptr && hipStreamIsCapturing(stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+    a.clear_tags = cs == hipStreamCaptureStatusActive ? 1 : 0;
+  }
   a.row_groups = rg;
   a.xcd_err = reinterpret_cast<unsigned int*>(static_cast<unsigned char*>(workspace) + XCD_ERR_OFFSET);
   // XCD-ordered 1-D grid: 8 XCDs x ceil(rg / 8) row groups x ns splits (blocks past rg exit at once)

@@ -64,6 +64,7 @@ struct WideArgs {
   int64_t rg_bytes, cnt_bytes, part_bytes;
   int32_t row_groups;
   int32_t sc1_loads;  // feature-split partials: agent-coherent sc1 loads instead of an acquire
+  int32_t clear_tags; // the merger clears the tags it consumed (set for HIP-graph captures only)
   uint32_t epoch;     // != 0, distinct per launch: the tag of this launch's class-merge granules
   int32_t probe;  // linear_wide_set_probe: measurement 1 = stop after the MFMA loop, 2 = after the
                   // block's row states (before the class merge); fault injection 3 = the merging
@@ -461,8 +462,10 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   }
   // consumed: clear the granules' tags with write-through stores (no dirty line is left behind to
   // be written back over a later launch's granule), so a HIP-graph replay - one epoch baked into
-  // its arguments - never merges the previous replay's states
-  if (live && !timeout) {
+  // its arguments - never merges the previous replay's states. Captured launches only: an eager
+  // launch has an epoch of its own, and the kernel's end waits for these stores (+1.1 us at B = 8,
+  // profiles/r4_wide_merge/s39_summary.txt)
+  if (a.clear_tags && live && !timeout) {
     for (int b = part; b < a.ncb; b += 8) {
       gu32_t* const t = (gu32_t*)(states + ((int64_t)b * RG + rl) * 4);
       __hip_atomic_store(t + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

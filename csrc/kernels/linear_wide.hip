@@ -81,6 +81,11 @@ void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const
   a.row_groups = rg;
   a.probe = g_probe;
   a.sc1_loads = sc1_loads();
+  {  // a launch being captured into a HIP graph replays its epoch: its merger clears the tags
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (direct == nullptr && hipStreamIsCapturing(stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+    a.clear_tags = cs == hipStreamCaptureStatusActive ? 1 : 0;
+  }
   static std::atomic<uint32_t> epochs{0};  // class-merge granule tags: distinct per launch, never 0
   a.epoch = epochs.fetch_add(1, std::memory_order_relaxed) + 1;
   if (a.epoch == 0) a.epoch = epochs.fetch_add(1, std::memory_order_relaxed) + 1;
