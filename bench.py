@@ -165,12 +165,14 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         cpu_util["loadgen_process"] = utilization(l0, cpu_by_group(lg.pid), elapsed).get("process_total", 0.0)
         s1, h1 = srv.runtime.handle.stats(), srv.http.stats()
         nreq = max(1, s1["requests"] - s0["requests"])
-        nbat = max(1, (s1["batches"] - s0["batches"]) - (s1["idle_batches"] - s0["idle_batches"])
-                   - (s1["lane_batches"] - s0["lane_batches"]))  # batches the batcher thread launched
+        nbat = max(1, (s1["batches"] - s0["batches"]) - (s1["idle_batches"] - s0["idle_batches"]))  # batcher launches
         # where this rank's server CPU goes, per request (IO-thread stage clock, exclusive; "poll"
         # is epoll_wait + loop overhead, mostly idle blocking) and the server-side HTTP latency
         cpu_breakdown = {
             "server_cpu_us_per_req": cpu_util.get("process_total", 0.0) * elapsed / nreq * 1e6,
+            # requests this rank served per second of server CPU (all its threads): what decides the
+            # whole-node number when the ranks share the node's CPUs
+            "req_per_s_per_server_core": nreq / max(1e-9, cpu_util.get("process_total", 0.0) * elapsed),
             "io_stage_us_per_req": {k: (h1["stage_ns"][k] - h0["stage_ns"][k]) / nreq / 1e3 for k in h1["stage_ns"]},
             "engine_queue_wait_us_per_req": (s1["queue_wait_us_sum"] - s0["queue_wait_us_sum"]) / nreq,
             # engine threads, per GPU batch (launched by the batcher): where a batch's time goes
@@ -212,7 +214,10 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
                                       s3["idle_batches"] - s2["idle_batches"]], info)
         barrier(info)
         paths = {k: s1["path_batches"][k] - s0["path_batches"][k] for k in s1["path_batches"]}
-        lane_batches = s1["lane_batches"] - s0["lane_batches"]
+        resident = {"rows": s1["resident_rows"] - s0["resident_rows"],
+                    "stale": s1["resident_stale"] - s0["resident_stale"],
+                    "launches": s1["resident_launches"], "rings": s1["resident_rings"],
+                    "live": bool(s1["resident_live"])}
         idle = {"c64": int(per_rank[:, 8].sum()), "batch1": int(per_rank[:, 9].sum())}
     finally:
         if srv is not None:
@@ -236,13 +241,16 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         "kernel_batches": paths,
         # batches the IO thread launched itself on an idle engine (Engine::run_idle)
         "idle_path_batches": idle,
-        # batches launched by an IO thread through the lanes' combining launcher (no batcher /
-        # completer hop; rank 0)
-        "lane_batches_rank0": int(lane_batches),
+        # rows answered by the resident kernel through the IO threads' rings (rank 0; no packet,
+        # batcher or completer per request), bounced stale by a reload, instances launched, rings
+        "resident_rank0": resident,
         "backend": srv.runtime.handle.backend,
         "cpu_cores_busy_rank0": cpu_util,
         "cpu_breakdown_rank0": cpu_breakdown,
-        "threads": {"io": args.io_threads, "loadgen": args.client_threads, "pinned_cpus": args.pinned_cpus},
+        "threads": {"io": args.io_threads, "loadgen": args.client_threads, "pinned_cpus": args.pinned_cpus,
+                    # launcher placement of this rank (numa: its GPU's NUMA-node mask) and its mask size
+                    "placement": os.environ.get("MLAPI_PLACEMENT", "cores" if args.pinned_cpus else "none"),
+                    "affinity_cpus": len(os.sched_getaffinity(0))},
         "requests_per_step": args.reqs_per_conn * args.conns * info.world,
         "topology": ("one port for all ranks, connections dealt round robin by the group's acceptor "
                      "(csrc/http/dispatch.h); one out-of-process load generator per rank"),
@@ -275,11 +283,11 @@ def bench_serve(args, info):
 
 def bench_serve_wide(args, info):
     """Wide model on the /predict hot path: F=--wide-features (256), K classes (2 -> binary).
-    --wide-dtype f32 (default, the engine default): f32 storage (binary: the f32 GEMV; multiclass:
-    the f64-accumulating wide kernel), every body within rel 1e-11 (multiclass) / 1e-6 (GEMV) of the
-    fp64 oracle of the f32-rounded model; f64: the reference's precision (f64 storage, f64 MFMA
-    accumulation), every body within rel 1e-12 of sklearn's float64 math; bf16: the bf16 GEMV /
-    MFMA GEMM kernels, within rel 1e-4 of the bf16-rounded oracle."""
+    --wide-dtype f64 (default, the engine default): the reference's precision (f64 storage, f64 MFMA
+    accumulation), every body within rel 1e-12 of sklearn's float64 math and byte-compared (rel 0)
+    against the engine's own answers; f32: f32 storage on the same f64-accumulating kernel, within
+    rel 1e-11 of the fp64 oracle of the f32-rounded model; bf16: the bf16 GEMV / MFMA GEMM kernels,
+    within rel 1e-4 of the bf16-rounded oracle."""
     from mlapi_amd.models.linear import LinearModel
     from mlapi_amd.parallel.comm import broadcast_model
     from mlapi_amd.serve.loadgen import bf16_oracle
@@ -298,7 +306,7 @@ def bench_serve_wide(args, info):
     else:
         f32 = lambda a: np.asarray(a, dtype=np.float32).astype(np.float64)  # noqa: E731
         on = lambda v: os.environ.get(v, "0") not in ("0", "", "false")  # noqa: E731
-        f32acc = on("MLAPI_F32_SPLIT") or (K == 2 and on("MLAPI_F32_GEMV"))  # the f32-accumulating kernels (A/B)
+        f32acc = K == 2 and on("MLAPI_F32_GEMV")  # the f32-accumulating GEMV (A/B)
         okw = {"rtol_oracle": 1e-6 if f32acc else 1e-11, "label_margin": 1e-5 if f32acc else 1e-9,
                "oracle": (LinearModel(f32(model.W), f32(model.b), model.classes, model.kind), f32(rows))}
         rel = 1e-6
@@ -375,7 +383,7 @@ def bench_gemm(args, info):
             X, W = X.float(), W.float()
         op = ops.LinearSplit(B, K, info.device)
     else:
-        forced = {"tiles": 1, "rows": 2, "t32": 3, "t32pk": 9}.get(args.gemm_kernel, 0)
+        forced = {"tiles": 1, "rows": 2, "t32": 3}.get(args.gemm_kernel, 0)
         if forced:
             from mlapi_amd._native import C
 
@@ -457,8 +465,8 @@ def bench_train_softmax(args, info):
     value = info.world * B * args.steps / elapsed
     flops = 3 * 2 * B * K * tr.F_aug * info.world * args.steps / elapsed  # 2 logits passes + dW
     # F <= 512: row stats + fused G/dW + slab sum/update; wider: row stats with G (softmax_rows_kernel
-    # MODE 5) + G^T X_aug + slab sum/update (MLAPI_WIDE_TRAIN_5L=1: round 3's five launches)
-    launches = 5 if tr.Fk > 512 and os.environ.get("MLAPI_WIDE_TRAIN_5L") == "1" else 3
+    # MODE 5) + G^T X_aug + slab sum/update
+    launches = 3
     extra = {"final_loss": tr.last_loss(), "tflops_incl_recompute": flops / 1e12, "dp_exchange": tr.dp_exchange,
              "launches_per_step": launches + (0 if tr.dp_exchange in ("fused-p2p", "local") else 1),
              "kernel_width": tr.Fk,
@@ -486,7 +494,9 @@ def _self_launch(args, argv) -> int:
             return 2
     from mlapi_amd import launch
 
-    largv = ["--nproc", str(args.gpus)] + ([] if args.pin == "on" else ["--no-pin"])
+    # ranks on their GPU's NUMA node by default (a node mask, no core slices: core pinning lost at
+    # N = 1, profiles/r2_pin/); --pin on = disjoint core slices, off = unpinned
+    largv = ["--nproc", str(args.gpus), "--pin", {"auto": "numa", "on": "cores", "off": "off"}[args.pin]]
     return launch.main(largv + [os.path.abspath(__file__)] + list(argv))
 
 
@@ -503,7 +513,8 @@ def main(argv=None) -> int:
                          "driver's 20 steps time >= 2 s even at 1.3 M req/s)")
     ap.add_argument("--workload-rows", type=int, default=1024, help="serve: distinct validated requests")
     ap.add_argument("--wide-classes", type=int, default=1000, help="serve_wide: 2 = binary GEMV, else softmax GEMM")
-    ap.add_argument("--wide-dtype", default="f32", choices=["f32", "bf16", "f64"], help="serve_wide: kernel operand dtype")
+    ap.add_argument("--wide-dtype", default="f64", choices=["f64", "f32", "bf16"],
+                    help="serve_wide: kernel operand dtype (f64 = the engine default, sklearn's precision)")
     ap.add_argument("--wide-features", type=int, default=256, help="serve_wide: F")
     ap.add_argument("--client-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--io-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
@@ -513,7 +524,7 @@ def main(argv=None) -> int:
     ap.add_argument("--c1-requests", type=int, default=3000)
     ap.add_argument("--rows", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=1024)
-    ap.add_argument("--gemm-kernel", default="auto", choices=["auto", "split", "tiles", "rows", "t32", "t32pk"],
+    ap.add_argument("--gemm-kernel", default="auto", choices=["auto", "split", "tiles", "rows", "t32"],
                     help="gemm: auto = the planner's choice; split = the class-split small-batch kernel; "
                          "tiles / rows / t32 = that gemm_softmax kernel forced (measurement)")
     ap.add_argument("--gemm-dtype", default="bf16", choices=["bf16", "f32"], help="gemm: f32 runs the split kernel")
@@ -526,10 +537,11 @@ def main(argv=None) -> int:
     ap.add_argument("--softmax-features", type=int, default=256, help="train_softmax: F (any: <= 512 the fused G/dW kernel, wider the 3-launch wide path)")
     ap.add_argument("--cpu", action="store_true", help="force the CPU backend (testing without a GPU)")
     ap.add_argument("--pin", default="auto", choices=["auto", "on", "off"],
-                    help="pin this rank to its share of physical cores on its GPU's NUMA node, server "
-                         "and load generator on disjoint cores (auto = off: measured interleaved on "
-                         "one box, pinning cost c=64 throughput at N=1 (0.65-0.80 M vs 0.98-1.06 M "
-                         "req/s) and N=2 (0.83-0.85 M vs 0.92-1.02 M), profiles/r2_pin/)")
+                    help="on: pin this rank to its share of physical cores on its GPU's NUMA node, server "
+                         "and load generator on disjoint cores (measured interleaved on one box, core "
+                         "pinning cost c=64 throughput at N=1 (0.65-0.80 M vs 0.98-1.06 M req/s) and N=2 "
+                         "(0.83-0.85 M vs 0.92-1.02 M), profiles/r2_pin/); auto: N = 1 unpinned, N > 1 "
+                         "self-launched ranks on their GPU's NUMA node (node mask, mlapi_amd.launch); off")
     args = ap.parse_args(argv)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")

@@ -121,7 +121,11 @@ py::dict stats_dict(const EngineStats& s) {
   d["direct_batches"] = s.direct_batches;
   d["direct_wide_batches"] = s.direct_wide_batches;
   d["idle_batches"] = s.idle_batches;
-  d["lane_batches"] = s.lane_batches;
+  d["resident_rows"] = s.resident_rows;
+  d["resident_stale"] = s.resident_stale;
+  d["resident_launches"] = s.resident_launches;
+  d["resident_rings"] = s.resident_rings;
+  d["resident_live"] = s.resident_live;
   d["generic_models"] = s.generic_models;
   d["xcd_errors"] = s.xcd_errors;
   d["bar_batches"] = s.bar_batches;
@@ -230,6 +234,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_split_supported", &linear_split_supported);
   m.def("linear_split_workspace", &linear_split_workspace);
   m.def("linear_split_xcd_err_offset", &linear_split_xcd_err_offset);
+  m.def("linear_split_set_xcd", &linear_split_set_xcd);
   m.def("gemm_softmax_xcd_err_offset", &gemm_softmax_xcd_err_offset);
   m.def("xcd_placement_state", &xcd_placement_state, py::arg("device") = 0);
   m.def("xcd_placement_mismatches", &xcd_placement_mismatches, py::arg("device") = 0);
@@ -433,9 +438,11 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("host_merge_rows", &EngineConfig::host_merge_rows)
       .def_readwrite("inline_args", &EngineConfig::inline_args)
       .def_readwrite("idle_inline_rows", &EngineConfig::idle_inline_rows)
-      .def_readwrite("lanes", &EngineConfig::lanes)
-      .def_readwrite("lane_inflight", &EngineConfig::lane_inflight)
-      .def_readwrite("f32_split", &EngineConfig::f32_split)
+      .def_readwrite("resident", &EngineConfig::resident)
+      .def_readwrite("resident_depth", &EngineConfig::resident_depth)
+      .def_readwrite("resident_lease_ms", &EngineConfig::resident_lease_ms)
+      .def_readwrite("resident_idle_polls", &EngineConfig::resident_idle_polls)
+      .def_readwrite("resident_idle_sleep", &EngineConfig::resident_idle_sleep)
       .def_readwrite("f32_gemv", &EngineConfig::f32_gemv)
       .def_readwrite("wide_host_merge_blocks", &EngineConfig::wide_host_merge_blocks)
       .def_readwrite("completers", &EngineConfig::completers)
@@ -542,6 +549,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("pipeline_cap", &ServerConfig::pipeline_cap)
       .def_readwrite("io_spin_us", &ServerConfig::io_spin_us)
       .def_readwrite("io_wait_spin_us", &ServerConfig::io_wait_spin_us)
+      .def_readwrite("io_ring_spin_us", &ServerConfig::io_ring_spin_us)
       .def_readwrite("idle_max_conns", &ServerConfig::idle_max_conns)
       .def_readwrite("io_spin_lowload_us", &ServerConfig::io_spin_lowload_us)
       .def_readwrite("io_spin_max_conns", &ServerConfig::io_spin_max_conns)

@@ -316,15 +316,18 @@ class IoThread : public Sink {
     ++lat_n_;
   }
 
-  // Lane batches (rows this thread dispatched itself) whose records have landed: render them.
-  void harvest_lane() {
-    if (lane_ == nullptr || lane_->inflight() == 0) return;
-    lane_c_.clear();
-    lane_seg_.clear();
-    lane_->poll(lane_c_, lane_seg_);
-    for (size_t k = 0; k < lane_seg_.size(); ++k) {
-      const size_t b = lane_seg_[k].begin, e = k + 1 < lane_seg_.size() ? lane_seg_[k + 1].begin : lane_c_.size();
-      render_fast(lane_seg_[k].model, lane_c_.data() + b, e - b);
+  // Rows of this thread's resident-kernel ring whose records have landed: render them (rows bounced
+  // stale by a hot reload went to the engine queue: their answers come as hand-offs).
+  void harvest_ring() {
+    if (ring_ == nullptr || ring_->pending() == 0) return;
+    ring_c_.clear();
+    ring_seg_.clear();
+    int requeued = 0;
+    ring_->poll(ring_c_, ring_seg_, this, &requeued);
+    outstanding_ += requeued;
+    for (size_t k = 0; k < ring_seg_.size(); ++k) {
+      const size_t b = ring_seg_[k].begin, e = k + 1 < ring_seg_.size() ? ring_seg_[k + 1].begin : ring_c_.size();
+      render_fast(ring_seg_[k].model, ring_c_.data() + b, e - b);
     }
   }
 
@@ -332,9 +335,9 @@ class IoThread : public Sink {
     if (pend_tags_.empty()) return;
     Stage sg(this, SS_SUBMIT);
     const int n = (int)pend_tags_.size();
-    // this thread dispatches the round's rows itself (engine lane: no batcher / completer hop);
-    // not eligible (wide model, lane slots busy, ...) -> the idle path or the engine queue
-    if (lane_ != nullptr && lane_->submit(pend_x_.data(), n, (int)nfeat_, pend_tags_.data())) {
+    // the round's rows go into this thread's ring for the resident kernel (no packet, no batcher /
+    // completer hop); not eligible (wide model, no resident kernel, ...) -> the idle path or the queue
+    if (ring_ != nullptr && ring_->submit(pend_x_.data(), n, (int)nfeat_, pend_tags_.data())) {
       pend_x_.clear();
       pend_tags_.clear();
       return;
@@ -397,10 +400,12 @@ class IoThread : public Sink {
     const int64_t lowload_spin_ns = (int64_t)srv_->config().io_spin_lowload_us * 1000;
     const int lowload_conns = srv_->config().io_spin_max_conns;
     const int64_t wait_spin_ns = (int64_t)srv_->config().io_wait_spin_us * 1000;
+    const int64_t ring_spin_ns = (int64_t)srv_->config().io_ring_spin_us * 1000;
     int64_t last_active = 0;
-    lane_ = srv_->engine() != nullptr ? srv_->engine()->open_lane() : nullptr;
+    int last_n = 0;  // events of the previous epoll_wait
+    ring_ = srv_->engine() != nullptr ? srv_->engine()->open_ring() : nullptr;
     while (!stop_.load()) {
-      harvest_lane();
+      harvest_ring();
       flush_submits();
       flush_log();
       publish_clock();
@@ -424,7 +429,16 @@ class IoThread : public Sink {
         spinning_.store(false);  // left the low-load regime: hand-offs need the eventfd again
         if (pending_.load()) timeout = 0;
       }
-      if (lane_ != nullptr && lane_->inflight() > 0) timeout = 0;  // poll the lane's records
+      if (ring_ != nullptr && ring_->pending() > 0) {
+        // rows of this thread are on the GPU: no blocking wait. With nothing else to do (the last
+        // poll found no event), watch their records in user space for a while first - the GPU leg
+        // is a few us, an epoll_wait per check would be a syscall per pass
+        timeout = 0;
+        if (last_n == 0 && ring_spin_ns > 0 && !pending_.load(std::memory_order_relaxed)) {
+          Stage sg(this, SS_IDLE_GPU);
+          if (ring_->wait_any(ring_spin_ns)) continue;  // harvest first
+        }
+      }
       stage(SS_POLL);
       if (timeout != 0 && wait_spin_ns > 0 && outstanding_ > 0 && !spinning_.load(std::memory_order_relaxed)) {
         // rows of this thread are in the engine: watch for their hand-off in user space for a
@@ -443,6 +457,7 @@ class IoThread : public Sink {
       }
       const int n = epoll_wait(epfd_, evs, 256, timeout);
       blocked_.store(false);
+      last_n = n;
       const bool spin_enabled = always_spin_ns > 0 || lowload_spin_ns > 0;
       if (n > 0 && spin_enabled) last_active = mono_ns();
       // hand-offs posted while spinning come without an eventfd write (also the ones that raced
@@ -481,8 +496,8 @@ class IoThread : public Sink {
       }
       apply_listen_state();
     }
-    if (lane_ != nullptr) srv_->engine()->close_lane(lane_);
-    lane_ = nullptr;
+    if (ring_ != nullptr) srv_->engine()->close_ring(ring_);
+    ring_ = nullptr;
   }
 
   // Health-aware dispatch (SO_REUSEPORT group membership): an IO thread whose engine is unhealthy
@@ -1141,10 +1156,10 @@ class IoThread : public Sink {
   std::vector<Completion> spare_c_;  // drain_pending's side of the double buffer (this thread only)
   std::vector<FastSeg> spare_seg_;
   std::vector<Completion> idle_done_;  // run_idle completions (this thread only)
-  Lane* lane_ = nullptr;               // this thread's dispatch lane (engine-owned), or none
+  ServeRing* ring_ = nullptr;          // this thread's resident-kernel ring (engine-owned), or none
   int64_t outstanding_ = 0;            // rows this thread queued in the engine, not yet handed back
-  std::vector<Completion> lane_c_;     // harvest_lane scratch (this thread only)
-  std::vector<Lane::Seg> lane_seg_;
+  std::vector<Completion> ring_c_;     // harvest_ring scratch (this thread only)
+  std::vector<ServeRing::Seg> ring_seg_;
   std::string body_;                   // response body scratch (this thread only)
   std::vector<SlowResp> slow_;
   std::vector<double> pend_x_;      // fast-path rows parsed in this epoll round (IO thread only)

@@ -58,6 +58,9 @@ struct ServerConfig {
   // the request path). 0 = off. 1-5 us measured +4-21 % c=64 req/s over 0 on three boxes, 15-30
   // us lost (the spinning threads take the load generator's CPU): profiles/r4_waitspin/.
   int io_wait_spin_us = 3;
+  // Rows of this thread on the resident kernel (ServeRing) and no socket event: watch their records
+  // in user space this long before the next epoll_wait(0) (no syscall per check). 0 = never spin.
+  int io_ring_spin_us = 5;
   int idle_max_conns = 0;  // idle-engine path only while <= this many connections are open (0 = any)
   // Low-load busy-poll: while the whole server holds at most io_spin_max_conns open connections
   // (a batch=1 client), an IO thread that just had activity polls for this long before blocking,
@@ -91,7 +94,7 @@ enum ServerStage : int {
   SS_RECV,       // recv() syscalls
   SS_PARSE,      // HTTP + JSON parse of requests
   SS_SUBMIT,     // handing parsed rows to the engine (submit_many)
-  SS_IDLE_GPU,   // idle-engine path: launch + wait for the GPU in this thread (run_idle)
+  SS_IDLE_GPU,   // waiting for the GPU in this thread: idle-engine launches (run_idle), ring record watch
   SS_RENDER,     // JSON response rendering
   SS_SEND,       // send() syscalls
   SS_HANDOFF,    // completion / slow-path hand-offs drained from other threads

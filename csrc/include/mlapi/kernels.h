@@ -198,6 +198,8 @@ void xcd_local_inject(int launches);
 void xcd_local_reset(int device);  // forget the decision: the next launch probes again
 int xcd_local_take_inject();
 int linear_split_nsplit(int K);
+// test hook: force the XCD-local split merge on (1) / off (0), or back to MLAPI_SPLIT_XCD (-1)
+void linear_split_set_xcd(int mode);
 constexpr int64_t LINEAR_SPLIT_MAX_ROWS = 2048;  // rows per launch_linear_split call
 // direct: launch through that queue instead of `stream` (the caller keeps every launch that shares
 // the workspace on one of the two; serving completes through records, so nothing else needs the

@@ -240,7 +240,8 @@ __device__ __forceinline__ RowState granule_merge(const GemmArgs& a, int64_t row
   // direct-dispatched serving kernels, which may run without that release, clear write-through).
   // Measured: B = 1024 5.72 vs 5.82 us, B = 8192 9.8 vs 10.0 us with write-through clears
   // (profiles/r4_gemm_merge/s34/).
-  if (live && !timeout) {
+  // also after a timeout (the row already fails): no granule of this launch outlives it
+  if (live) {
     unsigned* const base = reinterpret_cast<unsigned*>(a.partials);
     for (unsigned sp = qi; sp + 1 < ns; sp += LPR) base[((int64_t)sp * B + row) * 4 + 3] = 0u;
   }
@@ -824,21 +825,7 @@ struct TileTmp7 {
   unsigned mask;
 };
 
-typedef __attribute__((ext_vector_type(2))) float f32x2_t;
-// packed FP32 VALU (measurement variant PK): one v_pk_fma_f32 / v_pk_add_f32
-// per element pair in place of two single-lane ops (asm: the instruction is the experiment)
-__device__ __forceinline__ f32x2_t pk_fma(f32x2_t a, f32x2_t b, f32x2_t c) {
-  f32x2_t d;
-  asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-  return d;
-}
-__device__ __forceinline__ f32x2_t pk_add(f32x2_t a, f32x2_t b) {
-  f32x2_t d;
-  asm("v_pk_add_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
-  return d;
-}
-
-template <bool OVR, bool PK = false>
+template <bool OVR>
 __device__ __forceinline__ void tile_stage7(int stage, const float (&v)[16], int c0, TileState& S, TileTmp7& T) {
   if (stage == 0) {
     float cm = vmax(v[0], v[1]);
@@ -858,24 +845,14 @@ __device__ __forceinline__ void tile_stage7(int stage, const float (&v)[16], int
   } else {
     const int i0 = (stage - 3) * 4;
     float e[4];
-    if constexpr (PK && !OVR) {  // 2 v_pk_fma_f32 + 1 v_pk_add_f32 for 4 fma + 2 adds
-      const f32x2_t l2 = {LOG2E_F, LOG2E_F}, nm = {-T.m2, -T.m2};
-      const f32x2_t t01 = pk_fma(f32x2_t{v[i0], v[i0 + 1]}, l2, nm);
-      const f32x2_t t23 = pk_fma(f32x2_t{v[i0 + 2], v[i0 + 3]}, l2, nm);
-      const f32x2_t e01 = {__builtin_amdgcn_exp2f(t01[0]), __builtin_amdgcn_exp2f(t01[1])};
-      const f32x2_t e23 = {__builtin_amdgcn_exp2f(t23[0]), __builtin_amdgcn_exp2f(t23[1])};
-      const f32x2_t s = pk_add(e01, e23);
-      T.part += s[0] + s[1];
-    } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if constexpr (OVR)
-          e[i] = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-v[i0 + i] * LOG2E_F));
-        else
-          e[i] = __builtin_amdgcn_exp2f(fmaf(v[i0 + i], LOG2E_F, -T.m2));
-      }
-      T.part += (e[0] + e[1]) + (e[2] + e[3]);
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (OVR)
+        e[i] = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-v[i0 + i] * LOG2E_F));
+      else
+        e[i] = __builtin_amdgcn_exp2f(fmaf(v[i0 + i], LOG2E_F, -T.m2));
     }
+    T.part += (e[0] + e[1]) + (e[2] + e[3]);
     if (stage == 6) {
       if constexpr (OVR) {
         S.s += T.part;
@@ -957,8 +934,7 @@ __device__ __forceinline__ bf16x8_t frag32(const unsigned char* smem, const Frag
 
 // MFMAs of chunk cn (LDS buffer BUF -> nxt) with the epilogue of chunk c0 (acc -> S) spread over
 // the k-steps
-template <int KS, int RT, bool OVR, int BUF, int BUF_BYTES, bool EPI = true, int AHEAD = 2, bool PRIO = false,
-          bool PK = false>
+template <int KS, int RT, bool OVR, int BUF, int BUF_BYTES, bool EPI = true, int AHEAD = 2, bool PRIO = false>
 __device__ __forceinline__ void fused32_step(const unsigned char* smem, const FragOff<KS>& fo,
                                              const bf16x8_t (&xf)[RT][2 * KS], int cn, int c_end, int h,
                                              f32x16_t (&nxt)[RT][2], const f32x16_t (&acc)[RT][2], int c0,
@@ -1013,7 +989,7 @@ __device__ __forceinline__ void fused32_step(const unsigned char* smem, const Fr
       constexpr int j = decltype(jc)::value;
       if constexpr ((j * K2) / NSTAGE == k) {
         constexpr int rt = j / 14, t = (j % 14) / 7, stg = j % 7;
-        if constexpr (EPI) tile_stage7<OVR, PK>(stg, v[rt][t], c0 + 32 * t, S[rt], T[rt][t]);
+        if constexpr (EPI) tile_stage7<OVR>(stg, v[rt][t], c0 + 32 * t, S[rt], T[rt][t]);
       }
     });
     __builtin_amdgcn_sched_barrier(0);
@@ -1041,8 +1017,7 @@ __device__ __forceinline__ void epilogue32(const f32x16_t (&acc)[RT][2], int c0,
 // tools/gemm_phase_probe.py; its outputs are meaningless). It splits the class loop's time into the
 // MFMA / LDS feed and the epilogue: 44.4k of 52.2k cycles per wave are the feed
 // (profiles/r2_gemm/phase_probe_noepi.log).
-template <int KS, int WV, int RT, int MODE, bool OVR, bool EPI = true, int AHEAD = 2, bool PRIO = false,
-          bool PK = false>
+template <int KS, int WV, int RT, int MODE, bool OVR, bool EPI = true, int AHEAD = 2, bool PRIO = false>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(RT == 2 ? 1 : 2, RT == 2 ? 1 : 2))) void
 gemm_softmax32_kernel(GemmArgs a) {
   static_assert(MODE == 0 || MODE == 2 || MODE == 4, "logits mode runs the 16x16 kernel");
@@ -1133,7 +1108,7 @@ gemm_softmax32_kernel(GemmArgs a) {
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 0)
-    fused32_step<KS, RT, OVR, 1, BUF_BYTES, EPI, AHEAD, PRIO, PK>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0,
+    fused32_step<KS, RT, OVR, 1, BUF_BYTES, EPI, AHEAD, PRIO>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accB, accA, c0,
                                                         ts);
     c0 += CLASS_CHUNK;
     if (c0 + CLASS_CHUNK >= c_end) {
@@ -1142,7 +1117,7 @@ gemm_softmax32_kernel(GemmArgs a) {
     }
     MLAPI_WAIT_BARRIER32()
     if (c0 + 2 * CLASS_CHUNK < c_end) MLAPI_DMA32(c0 + 2 * CLASS_CHUNK, 1)
-    fused32_step<KS, RT, OVR, 0, BUF_BYTES, EPI, AHEAD, PRIO, PK>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0,
+    fused32_step<KS, RT, OVR, 0, BUF_BYTES, EPI, AHEAD, PRIO>(smem, fo, xf, c0 + CLASS_CHUNK, c_end, h, accA, accB, c0,
                                                         ts);
     c0 += CLASS_CHUNK;
   }
@@ -1603,11 +1578,6 @@ void launch32(const GemmArgs& args, const dim3& grid, int rt, hipStream_t stream
                            args);
         return;
       }
-      if (!o && g_force_kernel == 9) {  // measurement: packed FP32 VALU in the softmax epilogue
-        hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, true, 2, false, true>), grid, dim3(256), 0,
-                           stream, args);
-        return;
-      }
       if (!o && (g_force_kernel == 6 || g_force_kernel == 7)) {  // measurement: fragment prefetch depth 1 / 3
         if (g_force_kernel == 6)
           hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, true, 1>), grid, dim3(256), 0, stream, args);
@@ -1763,6 +1733,10 @@ size_t gemm_softmax_workspace(int64_t B, int K, int F) {
   return p.splits > 1 ? (size_t)COUNTER_BYTES + (size_t)p.splits * (size_t)B * sizeof(float4) : 0;
 }
 
+// NOTE: every gemm_softmax launch goes through hipLaunchKernelGGL on `stream`; the split merge
+// clears its granule tags with plain stores, which is only safe because a HIP stream launch ends
+// with a system-scope release. A direct-dispatch path (KernelLauncher, packets without that
+// release) must switch these clears to write-through stores first.
 void launch_gemm_softmax(const void* X, const void* W, const float* b, int64_t B, int F, int K, int kind,
                          int32_t* out_idx, float* out_p, void* workspace, size_t ws_bytes, hipStream_t stream,
                          RecOut ro) {

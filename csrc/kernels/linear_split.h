@@ -269,7 +269,9 @@ __device__ __forceinline__ void split_predict(const SplitArgs& a) {
         }
       }
     }
-    if (a.clear_tags && live && !timeout)  // graph captures: clear the tags (write-through: no dirty line)
+    // graph captures: clear the tags (write-through: no dirty line) - also after a timeout (the
+    // rows already fail), so the next replay never reads this replay's granules as its own
+    if (a.clear_tags && live)
       for (int sp = 0; sp + 1 < a.nsplit; ++sp)
         __hip_atomic_store((gu32_t*)(part + (int64_t)sp * ROWS_PER_GROUP + l) + 3, 0u, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);

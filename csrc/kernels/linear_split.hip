@@ -24,8 +24,10 @@ __global__ __launch_bounds__(256) void linear_split_kernel(split::SplitArgs a) {
   split::split_predict<T, KS, NB, OVR>(a);
 }
 
+int g_split_xcd = -1;  // test hook (linear_split_set_xcd): -1 = MLAPI_SPLIT_XCD / default, 0 off, 1 on
+
 template <typename T, int KS>
-void launch_ks(const split::SplitArgs& a, dim3 grid, bool nb2, bool ovr, hipStream_t stream, KernelLauncher* direct) {
+void launch_ks(split::SplitArgs a, dim3 grid, bool nb2, bool ovr, hipStream_t stream, KernelLauncher* direct) {
   if (direct != nullptr) {
     // the same kernel, unmangled, in the serving code object (serve_direct.hip)
     char name[64];
@@ -34,6 +36,11 @@ void launch_ks(const split::SplitArgs& a, dim3 grid, bool nb2, bool ovr, hipStre
     // host merge (hrec): write-through records and no workspace - unordered; the in-kernel merge
     // re-arms the workspace counters for the next launch - ordered
     if (direct->launch_kernel(name, &a, sizeof a, grid.x, grid.y, 256, a.hrec == nullptr)) return;
+  }
+  {  // a launch being captured into a HIP graph replays its epoch: its merger clears the tags
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+    a.clear_tags = cs == hipStreamCaptureStatusActive ? 1 : 0;
   }
   if (nb2) {
     if (ovr)
@@ -61,6 +68,8 @@ bool linear_split_supported(int dt, int F) {
 }
 
 size_t linear_split_xcd_err_offset() { return XCD_ERR_OFFSET; }
+
+void linear_split_set_xcd(int mode) { g_split_xcd = mode; }
 
 size_t linear_split_workspace(int64_t B, int K) {
   const int rg = row_groups(B);
@@ -113,16 +122,20 @@ void launch_linear_split(int dt, const void* X, int64_t ldx, const void* W, cons
     const char* e = getenv("MLAPI_SPLIT_XCD");
     return e ? atoi(e) : 1;
   }();
-  a.xcd_local = (xcd_env != 0 && ns > 1 && sro.rec == nullptr && xcd_local_allowed(stream)) ? 1 : 0;
+  const int xcd_on = g_split_xcd >= 0 ? g_split_xcd : xcd_env;
+  a.xcd_local = (xcd_on != 0 && ns > 1 && sro.rec == nullptr && xcd_local_allowed(stream)) ? 1 : 0;
   a.xcd_inject = a.xcd_local ? xcd_local_take_inject() : 0;
-  static std::atomic<uint32_t> epochs{0};  // split-merge granule tags: 28 bits, never 0
+  // Split-merge granule tags: 28 bits, never 0, from one process-wide counter. Eager launches do
+  // not clear the tags they consumed, so a granule keeps the epoch of the last launch that wrote
+  // it; the counter wraps after 2^28 launches, and a granule left untouched for exactly that many
+  // launches would match again. Bound: the engine's serving launches are one row group (B <= 32,
+  // every split rewritten per launch, a workspace per model), so they never leave one behind;
+  // library callers that alternate large and small batches on one workspace over 2^28 launches
+  // should re-zero it (linear_split_workspace bytes) now and then. Graph captures clear their tags.
+  static std::atomic<uint32_t> epochs{0};
   do a.epoch = (epochs.fetch_add(1, std::memory_order_relaxed) + 1) & 0x0fffffffu;
   while (a.epoch == 0);
-  {  // a launch being captured into a HIP graph replays its epoch: its merger clears the tags
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (direct == nullptr && hipStreamIsCapturing(stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
-    a.clear_tags = cs == hipStreamCaptureStatusActive ? 1 : 0;
-  }
+  a.clear_tags = 0;  // direct-dispatched launches are never captured (launch_ks sets it for stream launches)
   a.row_groups = rg;
   a.xcd_err = reinterpret_cast<unsigned int*>(static_cast<unsigned char*>(workspace) + XCD_ERR_OFFSET);
   // XCD-ordered 1-D grid: 8 XCDs x ceil(rg / 8) row groups x ns splits (blocks past rg exit at once)

@@ -63,7 +63,6 @@ struct WideArgs {
   unsigned char* ws;
   int64_t rg_bytes, cnt_bytes, part_bytes;
   int32_t row_groups;
-  int32_t sc1_loads;  // feature-split partials: agent-coherent sc1 loads instead of an acquire
   int32_t clear_tags; // the merger clears the tags it consumed (set for HIP-graph captures only)
   uint32_t epoch;     // != 0, distinct per launch: the tag of this launch's class-merge granules
   int32_t probe;  // linear_wide_set_probe: measurement 1 = stop after the MFMA loop, 2 = after the
@@ -235,23 +234,15 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     __syncthreads();
     if (!bcast) return;  // uniform per block
     if (wave == 0) {  // only wave 0 (the adder) reads the partials
-      if (!a.sc1_loads) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
 #pragma unroll
       for (int t = 0; t < NB; ++t) acc[t] = wd4_t{0.0, 0.0, 0.0, 0.0};
       for (int f = 0; f < a.nfs; ++f) {  // split order: deterministic
 #pragma unroll
         for (int t = 0; t < NB; ++t) {
           const double* src = part + (int64_t)f * (2 * 4 * 64) + t * 256 + lane * 4;
-          wd4_t v;
-          if (a.sc1_loads) {
+          wd4_t v;  // agent-coherent sc1 loads: no acquire fence (the partials bypass this CU's L1)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = ld_sc1(src + k);
-          } else {
-            v = *reinterpret_cast<const wd4_t*>(src);
-          }
+          for (int k = 0; k < 4; ++k) v[k] = ld_sc1(src + k);
           acc[t] += v;
         }
       }
@@ -465,7 +456,9 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   // its arguments - never merges the previous replay's states. Captured launches only: an eager
   // launch has an epoch of its own, and the kernel's end waits for these stores (+1.1 us at B = 8,
   // profiles/r4_wide_merge/s39_summary.txt)
-  if (a.clear_tags && live && !timeout) {
+  // graph captures: clear the consumed tags - also after a timeout (the rows already fail), so the
+  // next replay never reads this replay's granules as its own
+  if (a.clear_tags && live) {
     for (int b = part; b < a.ncb; b += 8) {
       gu32_t* const t = (gu32_t*)(states + ((int64_t)b * RG + rl) * 4);
       __hip_atomic_store(t + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

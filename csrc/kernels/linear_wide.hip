@@ -28,16 +28,6 @@ using wide_plan::row_groups;
 
 int g_probe = 0;  // measurement hook (linear_wide_set_probe)
 
-// MLAPI_WIDE_ACQUIRE=1: read the in-launch hand-offs behind an agent acquire fence instead of
-// with sc1 loads (the A/B of docs/PERFORMANCE.md)
-static int sc1_loads() {
-  static const int v = [] {
-    const char* e = std::getenv("MLAPI_WIDE_ACQUIRE");
-    return (e != nullptr && e[0] == '1') ? 0 : 1;
-  }();
-  return v;
-}
-
 WidePlan linear_wide_plan(int dt, int F, int K) { return wide_plan::plan(dt, F, K); }
 
 void linear_wide_set_probe(int probe) { g_probe = probe; }
@@ -80,12 +70,7 @@ void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const
   a.hseq = hro.seq;
   a.row_groups = rg;
   a.probe = g_probe;
-  a.sc1_loads = sc1_loads();
-  {  // a launch being captured into a HIP graph replays its epoch: its merger clears the tags
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (direct == nullptr && hipStreamIsCapturing(stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
-    a.clear_tags = cs == hipStreamCaptureStatusActive ? 1 : 0;
-  }
+  a.clear_tags = 0;  // direct-dispatched launches are never captured (set below for the stream launch)
   static std::atomic<uint32_t> epochs{0};  // class-merge granule tags: distinct per launch, never 0
   a.epoch = epochs.fetch_add(1, std::memory_order_relaxed) + 1;
   if (a.epoch == 0) a.epoch = epochs.fetch_add(1, std::memory_order_relaxed) + 1;
@@ -102,6 +87,11 @@ void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const
     // the workspace's tickets are re-armed by the kernel: launches that share them stay in order
     // (a workspace private to this launch lets it overlap the previous ones)
     if (direct->launch_kernel(name, &a, sizeof a, grid.x, grid.y, 256, needs_ws && !ws_private)) return;
+  }
+  {  // a launch being captured into a HIP graph replays its epoch: its merger clears the tags
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess) cs = hipStreamCaptureStatusNone;
+    a.clear_tags = cs == hipStreamCaptureStatusActive ? 1 : 0;
   }
   if (dt == DT_F64) {
     if (nb2)

@@ -13,6 +13,7 @@
 #include "gemv_binary.h"
 #include "linear_split.h"
 #include "linear_wide.h"
+#include "serve_resident.h"
 
 namespace {
 
@@ -114,3 +115,21 @@ MLAPI_WIDE_ENTRY(f64, double, 1)
 MLAPI_WIDE_ENTRY(f64, double, 2)
 MLAPI_WIDE_ENTRY(f32, float, 1)
 MLAPI_WIDE_ENTRY(f32, float, 2)
+
+// The resident SMALL-path kernel (serve_resident.h): one wave per IO thread's submission ring,
+// launched by the engine's supervisor onto a queue of its own. mlapi_resident_<dt>_r<LPE>_d<D>:
+// LPE lanes per row (F <= LPE), D host-memory polls in flight.
+#define MLAPI_RESIDENT_ENTRY(TN, T, LPE, D)                                                                      \
+  extern "C" __global__ __launch_bounds__(64) void mlapi_resident_##TN##_r##LPE##_d##D(const mlapi::ResidentArgs a) { \
+    mlapi::resident::resident_serve<T, LPE, D, 16>(a);                                                        \
+  }
+#define MLAPI_RESIDENT_ENTRIES(TN, T, LPE) \
+  MLAPI_RESIDENT_ENTRY(TN, T, LPE, 1)      \
+  MLAPI_RESIDENT_ENTRY(TN, T, LPE, 2)      \
+  MLAPI_RESIDENT_ENTRY(TN, T, LPE, 4)
+MLAPI_RESIDENT_ENTRIES(f64, double, 4)
+MLAPI_RESIDENT_ENTRIES(f64, double, 8)
+MLAPI_RESIDENT_ENTRIES(f64, double, 32)
+MLAPI_RESIDENT_ENTRIES(f32, float, 4)
+MLAPI_RESIDENT_ENTRIES(f32, float, 8)
+MLAPI_RESIDENT_ENTRIES(f32, float, 32)

@@ -15,8 +15,8 @@
 //      per thread) and read transposed with ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane
 //      group, two reads = the 8 rows of a lane's k-slice);
 //   3. launch_gdw_reduce: deterministic slab sum + fused SGD update (+ in-kernel DP exchange).
-// softmax_g_kernel below is the round-3 G pass (one wave per row, from f32 logits), kept for
-// MLAPI_WIDE_TRAIN_5L=1 (the A/B against the fused first launch).
+// (Round 3's five launches - row stats, f32 logits through HBM, a wave-per-row G pass - lost to
+// this path: 1.79 -> 1.0 ms per step at F = 1024, docs/PERFORMANCE.md; removed in round 5.)
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -34,58 +34,9 @@ typedef __attribute__((ext_vector_type(4))) short wi16x4_t;
 typedef __attribute__((ext_vector_type(4))) float wf32x4_t;
 typedef __attribute__((address_space(3))) wi16x4_t lds_i16x4_t;
 
-constexpr int G_ROWS_PER_BLOCK = 4;  // one wave per row
 constexpr int TILE_ROWS = 32;        // MFMA k-step (rows)
 constexpr int TILE_COLS = 64;        // classes / features per block tile
 
-__device__ __forceinline__ uint16_t to_bf16(float f) {  // round to nearest even
-  const uint32_t u = __float_as_uint(f);
-  return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
-}
-
-// ---- 3. G = P - Y (bf16) + loss / correct per block
-template <bool OVR>
-__global__ __launch_bounds__(64 * G_ROWS_PER_BLOCK) void softmax_g_kernel(const float* __restrict__ Z,
-                                                                          const float2* __restrict__ rowstat,
-                                                                          const int32_t* __restrict__ y, int64_t B,
-                                                                          int K, int Kp, uint16_t* __restrict__ G,
-                                                                          float* __restrict__ stat_slabs) {
-  __shared__ float red[G_ROWS_PER_BLOCK][2];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t row = (int64_t)blockIdx.x * G_ROWS_PER_BLOCK + wave;
-  float loss = 0.f, correct = 0.f;
-  if (row < B) {
-    const float2 rs = rowstat[row];
-    const float lse = rs.x;
-    const int yr = y[row];
-    const float* zr = Z + row * K;
-    uint16_t* gr = G + row * Kp;
-    for (int k = lane; k < Kp; k += 64) {
-      float g = 0.f;
-      if (k < K) {
-        const float z = zr[k];
-        const float p = OVR ? 1.f / (1.f + expf(-z)) : expf(z - lse);
-        g = p - (k == yr ? 1.f : 0.f);
-        if (OVR) loss += fmaxf(z, 0.f) - (k == yr ? z : 0.f) + log1pf(expf(-fabsf(z)));
-        else if (k == yr) loss += lse - z;
-      }
-      gr[k] = to_bf16(g);
-    }
-    if (lane == 0) correct = __float_as_int(rs.y) == yr ? 1.f : 0.f;
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) loss += __shfl_xor(loss, off, 64);
-  if (lane == 0) {
-    red[wave][0] = loss;
-    red[wave][1] = correct;
-  }
-  __syncthreads();
-  if (threadIdx.x < 2) {
-    float s = 0.f;
-    for (int w = 0; w < G_ROWS_PER_BLOCK; ++w) s += red[w][threadIdx.x];
-    stat_slabs[2 * (int64_t)blockIdx.x + threadIdx.x] = s;
-  }
-}
 
 // ---- 4. dW slabs = G^T X_aug per row group
 // grid (Kp / 64, ceil(F_aug / 64), row_groups); a wave owns 16 classes x 64 features (4 N-tiles).
@@ -275,7 +226,7 @@ int gdw_tile() {
 }
 
 struct WideLayout {
-  size_t rowstat_off, z_off, g_off, dw_off, stat_off, total;
+  size_t g_off, dw_off, stat_off, total;
   int Kp, row_groups, g_blocks;
   int64_t rows_per_group;
 };
@@ -293,13 +244,9 @@ WideLayout wide_layout(int64_t B, int K, int F) {
   if (rg < 1) rg = 1;
   L.rows_per_group = ((B + rg - 1) / rg + TILE_ROWS - 1) / TILE_ROWS * TILE_ROWS;
   L.row_groups = (int)((B + L.rows_per_group - 1) / L.rows_per_group);
-  L.g_blocks = (int)((B + G_ROWS_PER_BLOCK - 1) / G_ROWS_PER_BLOCK);  // >= softmax_rows_g_blocks(B)
+  L.g_blocks = softmax_rows_g_blocks(B, F, K);  // the row-stats launch's {loss, correct} slabs
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   size_t o = 0;
-  L.rowstat_off = o;
-  o = al(o + (size_t)B * sizeof(float2));
-  L.z_off = o;
-  o = al(o + (size_t)B * K * sizeof(float));
   L.g_off = o;
   o = al(o + (size_t)B * L.Kp * sizeof(uint16_t));
   L.dw_off = o;
@@ -332,30 +279,11 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
   const WideLayout L = wide_layout(B, K, F);
   if (ws_bytes < L.total) throw std::invalid_argument("softmax_grad_wide: workspace too small");
   unsigned char* ws = static_cast<unsigned char*>(workspace);
-  float2* rowstat = reinterpret_cast<float2*>(ws + L.rowstat_off);
-  float* Z = reinterpret_cast<float*>(ws + L.z_off);
   uint16_t* G = reinterpret_cast<uint16_t*>(ws + L.g_off);
   float* slabs = reinterpret_cast<float*>(ws + L.dw_off);
   float* stat_slabs = reinterpret_cast<float*>(ws + L.stat_off);
-  static const bool five = [] {
-    const char* e = std::getenv("MLAPI_WIDE_TRAIN_5L");
-    return e != nullptr && e[0] == '1';
-  }();
-  int g_blocks = L.g_blocks;
-  if (five) {  // round 3: row stats, f32 logits through HBM, the G pass
-    launch_softmax_rowstats(X_aug, ldx, W, b, B, F, K, kind, rowstat, nullptr, 0, stream);
-    launch_gemm_logits_ld(X_aug, ldx, W, b, B, F, K, Z, stream);
-    if (kind == KIND_OVR)
-      hipLaunchKernelGGL(softmax_g_kernel<true>, dim3((unsigned)L.g_blocks), dim3(64 * G_ROWS_PER_BLOCK), 0, stream, Z,
-                         rowstat, y, B, K, L.Kp, G, stat_slabs);
-    else
-      hipLaunchKernelGGL(softmax_g_kernel<false>, dim3((unsigned)L.g_blocks), dim3(64 * G_ROWS_PER_BLOCK), 0, stream, Z,
-                         rowstat, y, B, K, L.Kp, G, stat_slabs);
-    MLAPI_HIP_CHECK(hipGetLastError());
-  } else {
-    launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, stream);
-    g_blocks = softmax_rows_g_blocks(B, F, K);
-  }
+  launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, stream);
+  const int g_blocks = L.g_blocks;
   const int F_aug = F + 8;
   const int T = gdw_tile();
   if (T == 64) {

@@ -70,7 +70,8 @@ hsa_status_t collect_split_kernels(hsa_executable_t, hsa_agent_t, hsa_executable
   std::string name(len, '\0');
   hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_NAME, &name[0]);
   if (name.size() > 3 && name.compare(name.size() - 3, 3, ".kd") == 0) name.resize(name.size() - 3);
-  if (name.rfind("mlapi_split_", 0) != 0 && name.rfind("mlapi_gemv_", 0) != 0 && name.rfind("mlapi_wide_", 0) != 0)
+  if (name.rfind("mlapi_split_", 0) != 0 && name.rfind("mlapi_gemv_", 0) != 0 && name.rfind("mlapi_wide_", 0) != 0 &&
+      name.rfind("mlapi_resident_", 0) != 0)
     return HSA_STATUS_SUCCESS;
   Kernel k;
   hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.object);
@@ -108,10 +109,17 @@ hsa_status_t pick_device_pool(hsa_amd_memory_pool_t p, void* data) {
 }
 
 void queue_error(hsa_status_t, hsa_queue_t*, void* data);
+void resident_queue_error(hsa_status_t, hsa_queue_t*, void* data);
 
 class HsaInlineDispatcher final : public InlineDispatcher {
  public:
   ~HsaInlineDispatcher() override {
+    // a resident kernel still running (its owner waited and gave up): leave its queue and memory
+    // alone - destroying them under a live wave is what the lease rule exists to avoid
+    if (rqueue_ && !resident_wait(0)) rqueue_ = nullptr, rkernarg_ = nullptr, rsig_.handle = 0;
+    if (rqueue_) hsa_queue_destroy(rqueue_);
+    if (rkernarg_) hsa_amd_memory_pool_free(rkernarg_);
+    if (rsig_.handle) hsa_signal_destroy(rsig_);
     if (queue_) hsa_queue_destroy(queue_);
     if (kernargs_) hsa_amd_memory_pool_free(kernargs_);
     for (void* p : bar_bufs_) hsa_amd_memory_pool_free(p);
@@ -154,6 +162,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     hsa_amd_memory_pool_t pool{};
     if (hsa_amd_agent_iterate_memory_pools(s.cpu, pick_kernarg_pool, &pool) != HSA_STATUS_INFO_BREAK)
       return fail("no kernarg memory pool");
+    kpool_ = pool;
     std::ifstream f(path, std::ios::binary);
     if (!f) return fail("code object " + path + " not found");
     blob_.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
@@ -297,10 +306,78 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     (void)*reinterpret_cast<volatile uint32_t*>(hdp_flush_);  // the flush is posted: wait for it
   }
 
+  bool resident_launch(const char* name, const void* args, size_t bytes, unsigned grid_blocks, unsigned block) override {
+    const auto it = named_.find(name);
+    if (it == named_.end()) return false;
+    const Kernel& k = it->second;
+    if (bytes != k.kernarg || bytes > RESIDENT_KERNARG || block == 0 || block > 1024 || grid_blocks == 0) return false;
+    if (rqueue_ != nullptr && !resident_wait(0)) return false;  // one at a time
+    if (rqueue_ == nullptr) {
+      if (hsa_queue_create(gpu_, 64, HSA_QUEUE_TYPE_SINGLE, resident_queue_error, this, UINT32_MAX, UINT32_MAX, &rqueue_) !=
+          HSA_STATUS_SUCCESS) {
+        rqueue_ = nullptr;
+        return false;
+      }
+      if (hsa_amd_memory_pool_allocate(kpool_, RESIDENT_KERNARG, 0, (void**)&rkernarg_) != HSA_STATUS_SUCCESS ||
+          hsa_amd_agents_allow_access(1, &gpu_, nullptr, rkernarg_) != HSA_STATUS_SUCCESS ||
+          hsa_signal_create(0, 0, nullptr, &rsig_) != HSA_STATUS_SUCCESS) {
+        hsa_queue_destroy(rqueue_);
+        rqueue_ = nullptr;
+        if (rkernarg_) hsa_amd_memory_pool_free(rkernarg_);
+        rkernarg_ = nullptr;
+        rsig_.handle = 0;
+        return false;
+      }
+    }
+    // the previous resident kernel has ended (checked above): its argument block is free
+    std::memcpy(rkernarg_, args, bytes);
+    hsa_signal_store_screlease(rsig_, 1);
+    const uint64_t wi = hsa_queue_add_write_index_scacq_screl(rqueue_, 1);
+    auto* pkt = reinterpret_cast<hsa_kernel_dispatch_packet_t*>(rqueue_->base_address) + (wi & (rqueue_->size - 1));
+    pkt->workgroup_size_x = (uint16_t)block;
+    pkt->workgroup_size_y = 1;
+    pkt->workgroup_size_z = 1;
+    pkt->reserved0 = 0;
+    pkt->grid_size_x = grid_blocks * block;
+    pkt->grid_size_y = 1;
+    pkt->grid_size_z = 1;
+    pkt->private_segment_size = k.priv;
+    pkt->group_segment_size = k.group;
+    pkt->kernel_object = k.object;
+    pkt->kernarg_address = rkernarg_;
+    pkt->reserved2 = 0;
+    pkt->completion_signal = rsig_;
+    const uint16_t header = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                            (1 << HSA_PACKET_HEADER_BARRIER) |
+                            (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                            (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+    __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), (uint32_t)header | (1u << 16), __ATOMIC_RELEASE);
+    hsa_signal_store_relaxed(rqueue_->doorbell_signal, (hsa_signal_value_t)wi);
+    return true;
+  }
+
+  bool resident_wait(int timeout_ms) override {
+    if (rsig_.handle == 0) return true;
+    const uint64_t ns = (uint64_t)std::max(0, timeout_ms) * 1000000ull;
+    // blocked wait (interrupt signal): the supervisor sleeps while the kernel serves
+    return hsa_signal_wait_scacquire(rsig_, HSA_SIGNAL_CONDITION_LT, 1, ns == 0 ? 1 : ns,
+                                     ns == 0 ? HSA_WAIT_STATE_ACTIVE : HSA_WAIT_STATE_BLOCKED) < 1;
+  }
+
+  bool resident_faulted() const override { return rfault_.load(std::memory_order_relaxed); }
+
+  void resident_abandon() override {
+    rfault_.store(false);
+    rqueue_ = nullptr;
+    rkernarg_ = nullptr;
+    rsig_.handle = 0;
+  }
+
   bool faulted() const override { return fault_.load(std::memory_order_relaxed); }
   uint64_t named_launches() const override { return named_launches_; }
   bool device_kernargs() const override { return hdp_flush_ != nullptr; }
   void set_fault() { fault_.store(true); }
+  void set_resident_fault() { rfault_.store(true); }
 
  private:
   // One producer's part of the kernarg ring: `entries` argument blocks used round robin; wi[e] is
@@ -387,6 +464,11 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   }
 
   static constexpr uint32_t QUEUE_SIZE = 256;
+  static constexpr size_t RESIDENT_KERNARG = 4096;
+  hsa_amd_memory_pool_t kpool_{};  // host kernarg pool (the resident kernel's block: read once)
+  hsa_queue_t* rqueue_ = nullptr;  // resident kernel queue
+  void* rkernarg_ = nullptr;
+  hsa_signal_t rsig_{};
   uint32_t ka_slots_ = 64;
   bool hdp_readback_ = true;
   const uint32_t stride_ = (uint32_t)((sizeof(InlineBatch) + 255) / 256 * 256);
@@ -410,9 +492,13 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   std::atomic<int> next_producer_{0};
   alignas(64) std::atomic<uint64_t> published_{0};  // next packet id allowed to publish (lanes on)
   std::atomic<bool> fault_{false};
+  std::atomic<bool> rfault_{false};  // the resident queue reported an error
 };
 
 void queue_error(hsa_status_t, hsa_queue_t*, void* data) { static_cast<HsaInlineDispatcher*>(data)->set_fault(); }
+void resident_queue_error(hsa_status_t, hsa_queue_t*, void* data) {
+  static_cast<HsaInlineDispatcher*>(data)->set_resident_fault();
+}
 
 }  // namespace
 

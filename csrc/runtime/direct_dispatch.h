@@ -47,6 +47,19 @@ class InlineDispatcher : public KernelLauncher {
   virtual void* bar_alloc(size_t bytes) = 0;
   // Make BAR writes visible to the device: sfence, HDP flush, read-back. Call before the launch.
   virtual void bar_flush() = 0;
+  // Resident kernels (the SMALL path's serve_resident.h): a kernel of the code object that runs
+  // until its own stop / lease rule ends it, on a second HSA queue of its own (it must not sit in
+  // front of the serving packets), one at a time, with a completion signal. false: the kernel is
+  // not in the code object, the argument block does not match it, or the queue failed.
+  virtual bool resident_launch(const char* name, const void* args, size_t bytes, unsigned grid_blocks,
+                               unsigned block) = 0;
+  // Wait up to timeout_ms for the resident kernel to end: true = ended (or none running).
+  virtual bool resident_wait(int timeout_ms) = 0;
+  // A resident kernel that did not end when told to: forget it and its queue (neither is touched
+  // again; the queue is not destroyed under a live wave) so the next launch gets a fresh queue.
+  virtual void resident_abandon() = 0;
+  // the resident queue reported an error (its kernel faulted): abandon it and launch afresh
+  virtual bool resident_faulted() const = 0;
 };
 
 // Loads `hsaco_path` (csrc/kernels/serve_direct.hip) for the GPU behind HIP device `device` and

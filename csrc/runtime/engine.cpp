@@ -5,6 +5,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -167,16 +168,16 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       direct_ = make_direct_dispatcher(cfg_.device, cfg_.hsaco_path, cfg_.slots, &why);
       if (!direct_) std::fprintf(stderr, "[mlapi engine] direct dispatch off (%s): using hipLaunchKernel\n", why.c_str());
     }
-    if (direct_ && cfg_.lanes > 0) {
-      // lanes' record rings (host-mapped, written by the kernels' write-through stores) and the
-      // combined batches' done words
-      const size_t ab = (size_t)MAX_LANES * Lane::RING * sizeof(ServeRecord);
-      MLAPI_HIP_CHECK(hipHostMalloc((void**)&arena_h_, ab, hipHostMallocMapped | hipHostMallocCoherent));
-      std::memset(arena_h_, 0, ab);
-      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&arena_d_, arena_h_, 0));
-      MLAPI_HIP_CHECK(hipHostMalloc((void**)&cdone_h_, CRING * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent));
-      std::memset(cdone_h_, 0, CRING * sizeof(uint32_t));
-      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&cdone_d_, cdone_h_, 0));
+    if (direct_ && cfg_.resident > 0) {
+      // resident kernel: rings + records + control block in host-coherent memory the waves poll
+      const size_t rb = (size_t)RESIDENT_MAX_RINGS * RESIDENT_RING * RESIDENT_ENTRY_BYTES;
+      const size_t cb = (size_t)RESIDENT_MAX_RINGS * RESIDENT_RING * sizeof(ServeRecord);
+      MLAPI_HIP_CHECK(hipHostMalloc((void**)&res_rings_h_, rb, hipHostMallocMapped | hipHostMallocCoherent));
+      MLAPI_HIP_CHECK(hipHostMalloc((void**)&res_recs_h_, cb, hipHostMallocMapped | hipHostMallocCoherent));
+      MLAPI_HIP_CHECK(hipHostMalloc((void**)&res_ctl_h_, sizeof(ResidentCtl), hipHostMallocMapped | hipHostMallocCoherent));
+      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&res_rings_d_, res_rings_h_, 0));
+      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&res_recs_d_, res_recs_h_, 0));
+      MLAPI_HIP_CHECK(hipHostGetDevicePointer((void**)&res_ctl_d_, res_ctl_h_, 0));
     }
     for (int i = 0; i < cfg_.slots; ++i) {
       Slot& s = slots_[i];
@@ -203,6 +204,23 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       free_slots_.push_back(i);
     }
   }
+  if (cfg_.device < 0 && cfg_.resident > 0) {
+    // CPU backend: same layouts in plain memory, the supervisor thread plays the resident kernel
+    res_cpu_ = true;
+    const size_t rb = (size_t)RESIDENT_MAX_RINGS * RESIDENT_RING * RESIDENT_ENTRY_BYTES;
+    const size_t cb = (size_t)RESIDENT_MAX_RINGS * RESIDENT_RING * sizeof(ServeRecord);
+    res_rings_h_ = res_rings_d_ = static_cast<unsigned char*>(std::aligned_alloc(64, rb));
+    res_recs_h_ = res_recs_d_ = static_cast<ServeRecord*>(std::aligned_alloc(64, cb));
+    res_ctl_h_ = res_ctl_d_ = static_cast<ResidentCtl*>(std::aligned_alloc(64, sizeof(ResidentCtl)));
+  }
+  if (res_ctl_h_ != nullptr) {
+    // position 0xffffffff with meta 0 never matches a live row; records start with seq 0xffffffff
+    std::memset(res_rings_h_, 0xff, (size_t)RESIDENT_MAX_RINGS * RESIDENT_RING * RESIDENT_ENTRY_BYTES);
+    std::memset(res_recs_h_, 0xff, (size_t)RESIDENT_MAX_RINGS * RESIDENT_RING * sizeof(ServeRecord));
+    std::memset(res_ctl_h_, 0, sizeof(ResidentCtl));
+    if (!res_cpu_) resident_register(true);
+    res_thread_ = std::thread([this] { resident_loop(); });
+  }
   for (int i = 0; i < std::max(1, cfg_.batchers); ++i) batchers_.emplace_back([this] { batcher_loop(); });
   if (cfg_.device >= 0)
     for (int i = 0; i < std::max(1, cfg_.completers); ++i) completers_.emplace_back([this] { completer_loop(); });
@@ -210,27 +228,21 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
 
 Engine::~Engine() {
   stop();
+  if (res_cpu_) {
+    std::free(res_rings_h_);
+    std::free(res_recs_h_);
+    std::free(res_ctl_h_);
+  }
   if (cfg_.device >= 0) {
     (void)hipSetDevice(cfg_.device);
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (done_h_) (void)hipHostFree(done_h_);
     if (sig_counter_) (void)hipFree(sig_counter_);
-    {
-      // lanes' rows still in flight write into the arena: wait for the combined batches (bounded)
-      std::lock_guard<std::mutex> lk(launch_mu_);
-      const int64_t until = now_ns() + 2000000000LL;
-      while (cin_n_ > 0 && now_ns() < until) {
-        const CBatch& b = cin_[cin_head_];
-        if (__atomic_load_n(cdone_h_ + b.seq % CRING, __ATOMIC_ACQUIRE) == b.seq) {
-          cin_head_ = (cin_head_ + 1) % CRING;
-          --cin_n_;
-        } else {
-          _mm_pause();
-        }
-      }
+    if (res_ctl_h_ != nullptr && !res_leaked_) {  // the supervisor has stopped its instance (stop())
+      (void)hipHostFree(res_rings_h_);
+      (void)hipHostFree(res_recs_h_);
+      (void)hipHostFree(res_ctl_h_);
     }
-    if (arena_h_) (void)hipHostFree(arena_h_);
-    if (cdone_h_) (void)hipHostFree(cdone_h_);
     for (Slot& s : slots_) {
       if (s.hx) (void)hipHostFree(s.hx);
       if (s.dstage) (void)hipFree(s.dstage);
@@ -248,6 +260,13 @@ Engine::~Engine() {
 }
 
 void Engine::stop() {
+  {
+    std::lock_guard<std::mutex> lk(res_mu_);
+    res_stop_ = true;
+  }
+  res_cv_.notify_all();
+  if (res_thread_.joinable()) res_thread_.join();  // the resident instance has ended (or is abandoned)
+  if (res_ctl_h_ != nullptr && !res_cpu_) resident_register(false);
   {
     std::lock_guard<std::mutex> lk(q_mu_);
     stopping_ = true;
@@ -291,11 +310,6 @@ uint64_t Engine::load_model(int kind, int F, int K, const double* W, const doubl
     // multiple of 512 (it loops F in 256-feature slices inside one launch)
     m->path = PATH_GEMM;
     m->xdt = DT_BF16;
-    m->ldx = (int)padded_features(F);
-  } else if (!binary && K >= 2 && cfg_.wide_dtype == DT_F32 && F <= 512 && cfg_.f32_split) {
-    // f32-accumulating class-split kernel at a power-of-two width (v_mfma_f32_16x16x4_f32)
-    m->path = PATH_GEMM;
-    m->xdt = DT_F32;
     m->ldx = (int)padded_features(F);
   } else if (binary ? K == 1 : K >= 2) {
     // f64 accumulation on the matrix cores, any width: f64 storage (wide_dtype f64) or f32 (bf16
@@ -386,12 +400,24 @@ uint64_t Engine::load_model(int kind, int F, int K, const double* W, const doubl
     std::lock_guard<std::mutex> lk(st_mu_);
     stats_.model_version = m->version;
   }
+  kick_resident();
   return m->version;  // old model (cm) released here unless an in-flight batch still holds it
 }
 
 void Engine::unload_model() {
-  std::lock_guard<std::mutex> lk(model_mu_);
-  model_.reset();
+  {
+    std::lock_guard<std::mutex> lk(model_mu_);
+    model_.reset();
+  }
+  kick_resident();
+}
+
+void Engine::kick_resident() {
+  {
+    std::lock_guard<std::mutex> lk(res_mu_);
+    ++res_kick_;
+  }
+  res_cv_.notify_all();
 }
 
 std::shared_ptr<const Model> Engine::model() const {
@@ -660,7 +686,7 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
   // class-split and record-completing GEMV batches go into the direct dispatcher's own queue: ~0.1 us of batcher time instead of hipLaunchKernel's ~3 us, and that launch's HDP flush
   // also covers the BAR rows (no flush of their own)
   const bool split_path = m.path != PATH_SMALL && m.path != PATH_GENERIC && m.path != PATH_GEMV &&
-                          m.ws_split != nullptr && (m.xdt == DT_F32 || n <= cfg_.split_max_rows);
+                          m.ws_split != nullptr && n <= cfg_.split_max_rows;
   const bool gemv_rec = m.path == PATH_GEMV && cfg_.gemv_record_rows > 0 && n >= cfg_.gemv_record_rows;
   // ... for models whose weights stay small: the packet's agent-scope acquire (it covers the
   // kernarg block written through the BAR) invalidates L2, so every batch re-reads W - measured
@@ -737,8 +763,8 @@ void Engine::launch_batch(Slot& s, const Model& m, const std::vector<double>& xs
     } else if (m.path == PATH_GEMV)
       launch_gemv_binary(m.xdt, X, m.dW, m.bias0, n, m.ldx, m.kind, s.didx, static_cast<float*>(s.dp), stream_, ro,
                          direct_wide && ro.rec != nullptr ? &dl : nullptr);
-    else if (m.ws_split != nullptr && (m.xdt == DT_F32 || n <= cfg_.split_max_rows)) {
-      // small batches (and every f32 batch): the class-split kernel. Serving-sized batches end in
+    else if (m.ws_split != nullptr && n <= cfg_.split_max_rows) {
+      // small batches: the class-split kernel. Serving-sized batches end in
       // per-block records the completer merges; larger ones merge in-kernel (one round trip).
       SplitRecOut sro;
       const int ns = linear_split_nsplit(m.K);
@@ -1200,261 +1226,426 @@ void Engine::completer_loop() {
   }
 }
 
-// ---- per-IO-thread lanes: flat-combining launcher --------------------------------------------------
-Lane* Engine::open_lane() {
-  if (cfg_.device < 0 || cfg_.lanes <= 0 || !direct_ || !cfg_.record_completion || !cfg_.inline_args ||
-      arena_h_ == nullptr)
-    return nullptr;
-  std::lock_guard<std::mutex> lk(lanes_mu_);
-  if (!free_lanes_.empty()) {
-    Lane* l = free_lanes_.back();
-    free_lanes_.pop_back();
-    return l;
+// ---- resident SMALL-path kernel: per-IO-thread rings (ServeRing) and the supervisor ---------------
+namespace {
+// Engines with a resident kernel: a process that exits without stopping its engines (interpreter
+// exit with a server still up) halts their instances first, so no wave is still polling when the
+// HIP runtime tears the queues down (the lease rule would end it within resident_lease_ms anyway).
+std::mutex g_res_mu;
+std::vector<Engine*>& res_engines() {
+  static std::vector<Engine*>* v = new std::vector<Engine*>();  // never destroyed: used at exit
+  return *v;
+}
+void halt_residents_at_exit() {
+  std::lock_guard<std::mutex> lk(g_res_mu);
+  for (Engine* e : res_engines()) e->resident_halt(500);
+}
+}  // namespace
+
+void Engine::resident_register(bool on) {
+  static bool hooked = false;
+  std::lock_guard<std::mutex> lk(g_res_mu);
+  auto& v = res_engines();
+  if (on) {
+    v.push_back(this);
+    if (!hooked) {
+      hooked = true;
+      std::atexit(halt_residents_at_exit);
+    }
+  } else {
+    v.erase(std::remove(v.begin(), v.end(), this), v.end());
   }
-  if ((int)lanes_.size() >= MAX_LANES) return nullptr;
-  lanes_.push_back(std::unique_ptr<Lane>(new Lane(this, (uint32_t)lanes_.size() * Lane::RING)));
-  return lanes_.back().get();
 }
 
-void Engine::close_lane(Lane* lane) {
-  if (lane == nullptr) return;
+void Engine::resident_halt(int timeout_ms) {
+  res_halt_.store(true, std::memory_order_release);  // the supervisor launches nothing from now on
+  res_live_.store(false, std::memory_order_release);
+  if (res_ctl_h_ == nullptr) return;
+  __atomic_store_n(&res_ctl_h_->stop, 1u, __ATOMIC_RELEASE);
+  if (!res_cpu_ && direct_) (void)direct_->resident_wait(timeout_ms);
+}
+
+ServeRing* Engine::open_ring() {
+  if (cfg_.resident <= 0 || res_ctl_h_ == nullptr) return nullptr;
+  ServeRing* r = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(rings_mu_);
+    if (!free_rings_.empty()) {
+      r = free_rings_.back();
+      free_rings_.pop_back();
+    } else if ((int)rings_.size() < RESIDENT_MAX_RINGS) {
+      rings_.push_back(std::unique_ptr<ServeRing>(new ServeRing(this, (int)rings_.size())));
+      r = rings_.back().get();
+      rings_open_.store((int)rings_.size(), std::memory_order_release);
+    }
+  }
+  if (r != nullptr) kick_resident();  // a new ring: the instance's grid grows
+  return r;
+}
+
+void Engine::close_ring(ServeRing* ring) {
+  if (ring == nullptr) return;
   std::vector<Completion> c;
-  std::vector<Lane::Seg> segs;
+  std::vector<ServeRing::Seg> segs;
   const int64_t until = now_ns() + 2000000000LL;
-  while (lane->poll(c, segs) > 0 && now_ns() < until) {
+  int rq = 0;
+  while (ring->poll(c, segs, nullptr, &rq) > 0 && now_ns() < until) {
     c.clear();
     segs.clear();
     _mm_pause();
   }
-  if (lane->inflight() > 0) return;  // still pending after 2 s: never reuse it (its records may be written)
-  std::lock_guard<std::mutex> lk(lanes_mu_);
-  free_lanes_.push_back(lane);
+  std::lock_guard<std::mutex> lk(rings_mu_);
+  free_rings_.push_back(ring);  // pending rows past 2 s stay poisoned in it: the slots are never reused
 }
 
-Lane::Lane(Engine* e, uint32_t arena_base) : eng_(e), base_(arena_base) {
-  for (uint32_t i = 0; i < RING; ++i) ring_[i].rec = base_ + i;
-  ptrs_.reserve(INLINE_MAX_ROWS);
+ServeRing::ServeRing(Engine* e, int index) : eng_(e), idx_(index) {
+  ring_ = reinterpret_cast<ResidentGranule*>(e->res_rings_h_ + (size_t)index * RESIDENT_RING * RESIDENT_ENTRY_BYTES);
+  rec_ = e->res_recs_h_ + (size_t)index * RESIDENT_RING;
+  // positions continue from the ring's head (a pooled ring keeps next_ itself)
+  next_ = tail_ = __atomic_load_n(&e->res_ctl_h_->heads[index], __ATOMIC_ACQUIRE);
 }
 
-bool Lane::submit(const double* X, int n, int nf, const uint64_t* tags) {
+// A record is {seq, idx, p} from one 16-byte store (kernel) or p, idx then seq (CPU backend); its slot
+// is rewritten only after this thread consumed it, so seq (acquire) then idx / p is consistent.
+bool ServeRing::landed(uint32_t pos) const {
+  return __atomic_load_n(&rec_[pos & (RESIDENT_RING - 1)].seq, __ATOMIC_ACQUIRE) == pos;
+}
+
+bool ServeRing::submit(const double* X, int n, int nf, const uint64_t* tags) {
   Engine& e = *eng_;
-  if (n <= 0 || n > INLINE_MAX_ROWS || head_ - tail_ + (uint64_t)n > RING) return false;
-  if (nf < 0 || nf > e.cfg_.max_features) return false;
+  if (n <= 0 || n > RESIDENT_RING / 2 || next_ - tail_ + (uint32_t)n > (uint32_t)RESIDENT_RING) return false;
+  if (!e.res_live_.load(std::memory_order_acquire) || idx_ >= e.res_nrings_.load(std::memory_order_acquire)) return false;
   if (e.drop_.load(std::memory_order_relaxed) || e.cfg_.fail_every > 0 || e.cfg_.delay_us > 0) return false;
-  if (e.direct_->faulted()) return false;
-  {
-    const std::shared_ptr<const Model> m = e.model();
-    if (!m || m->path != PATH_SMALL || !linear_inline_fits(m->xdt, n, m->F, m->K)) return false;
-  }
+  std::shared_ptr<const Model> m = e.model();
+  const uint32_t mver = e.res_mver_.load(std::memory_order_acquire);
+  if (!m || m->path != PATH_SMALL || nf != m->F || resident_mver(m->version) != mver) return false;
+  // slots of given-up rows are never rewritten (the GPU may still answer them)
+  for (int i = 0; i < n; ++i)
+    if (pend_[(next_ + (uint32_t)i) & (RESIDENT_RING - 1)].poisoned) return false;
   const int64_t t = now_ns();
-  ptrs_.clear();
+  const uint32_t meta = mver << 8 | (uint32_t)nf;
   for (int i = 0; i < n; ++i) {
-    LaneEntry& en = ring_[(head_ + (uint64_t)i) % RING];
-    en.expect.store(0, std::memory_order_relaxed);
-    en.pre = ST_OK;
-    en.tag = tags[i];
-    en.t_enq = t;
-    ptrs_.push_back(&en);
+    const uint32_t pos = next_ + (uint32_t)i;
+    const uint32_t ei = pos & (RESIDENT_RING - 1);
+    Pend& p = pend_[ei];
+    p.tag = tags[i];
+    p.t_enq = t;
+    p.model = m;
+    p.nf = nf;
+    p.live = true;
+    // every granule {x_f, pos, meta}: the value, then its tag word (x86 stores become visible in
+    // program order, and the wave reads each 16-byte granule in one load, so a granule whose tag
+    // it sees carries this row's value); the wave accepts the row once all F tags carry this position
+    ResidentGranule* g = ring_ + (size_t)ei * RESIDENT_FMAX;
+    const uint64_t tag = (uint64_t)meta << 32 | pos;
+    for (int f = 0; f < nf; ++f) {
+      g[f].x = X[(size_t)i * nf + f];
+      __atomic_store_n(reinterpret_cast<uint64_t*>(&g[f].pos), tag, __ATOMIC_RELEASE);
+    }
   }
-  head_ += (uint64_t)n;
-  {
-    std::lock_guard<std::mutex> lk(e.cq_mu_);
-    e.cq_x_.insert(e.cq_x_.end(), X, X + (size_t)n * nf);
-    e.cq_nf_.insert(e.cq_nf_.end(), (size_t)n, (int32_t)nf);
-    e.cq_e_.insert(e.cq_e_.end(), ptrs_.begin(), ptrs_.end());
-    e.cq_n_.store((int)e.cq_e_.size(), std::memory_order_release);
-  }
-  e.combine();
+  next_ += (uint32_t)n;
   return true;
 }
 
-int Lane::poll(std::vector<Completion>& out, std::vector<Seg>& segs) {
+bool ServeRing::wait_any(int64_t ns) const {
+  if (tail_ == next_) return false;
+  const int64_t until = now_ns() + ns;
+  for (;;) {
+    for (uint32_t pos = tail_; pos != next_; ++pos) {
+      const Pend& p = pend_[pos & (RESIDENT_RING - 1)];
+      if (p.live && landed(pos)) return true;
+    }
+    if (now_ns() >= until) return false;
+    for (int i = 0; i < 8; ++i) _mm_pause();
+  }
+}
+
+int ServeRing::poll(std::vector<Completion>& out, std::vector<Seg>& segs, Sink* sink, int* requeued) {
   Engine& e = *eng_;
-  if (head_ == tail_) return 0;
-  if (e.cq_n_.load(std::memory_order_acquire) > 0) e.combine();
+  if (tail_ == next_) return 0;
   const int64_t now = now_ns();
   const int64_t wd = (int64_t)e.cfg_.watchdog_ms * 1000000;
-  const bool faulted = e.direct_->faulted();
-  int done = 0, errors = 0;
+  int done = 0, errors = 0, stale = 0;
   double lat_sum = 0;
   uint64_t lat_hist[24] = {0};
   const Model* last = nullptr;
-  // rows complete in launch order per batch but batches may finish out of order: scan every pending
-  // row, retire the finished prefix of the ring
-  for (uint64_t pos = tail_; pos != head_; ++pos) {
-    LaneEntry& en = ring_[pos % RING];
-    if (en.tag == ~uint64_t(0)) continue;  // already delivered (out of order)
-    const uint32_t seq = en.expect.load(std::memory_order_acquire);
-    bool fin = false, fail = false;
-    alignas(16) ServeRecord r{};
-    if (seq != 0) {
-      _mm_store_si128(reinterpret_cast<__m128i*>(&r), load_record(e.arena_h_ + en.rec));
-      fin = r.seq == seq;
+  for (uint32_t pos = tail_; pos != next_; ++pos) {
+    Pend& p = pend_[pos & (RESIDENT_RING - 1)];
+    if (!p.live) continue;
+    const ServeRecord* rp = rec_ + (pos & (RESIDENT_RING - 1));
+    ServeRecord r{};
+    r.seq = __atomic_load_n(&rp->seq, __ATOMIC_ACQUIRE);
+    if (r.seq == pos) {
+      r.idx = rp->idx;
+      r.p = rp->p;
     }
-    if (!fin) {
-      const int64_t waited = now - en.t_enq;
-      if (faulted || (wd > 0 && waited > 10 * wd)) {
-        fin = fail = true;  // the record may still land later: this ring slot is written off below
-      } else if (wd > 0 && waited > wd) {
-        e.healthy_.store(false);
+    bool fail = false;
+    if (r.seq != pos) {
+      const int64_t waited = now - p.t_enq;
+      if (wd > 0 && waited > 10 * wd) {
+        fail = true;  // the record may still land later: this slot is never written again
+      } else {
+        if (wd > 0 && waited > wd) e.healthy_.store(false);
+        continue;
       }
-      if (!fin) continue;
     }
-    int32_t st = fail ? (int32_t)ST_DEVICE_ERROR : en.pre;
+    if (!fail && r.idx == RESIDENT_STALE_IDX) {
+      // parsed for another model version: the engine queue answers it with the current model
+      ++stale;
+      const ResidentGranule* g = ring_ + (size_t)(pos & (RESIDENT_RING - 1)) * RESIDENT_FMAX;
+      double x[RESIDENT_FMAX];
+      for (int f = 0; f < p.nf; ++f) x[f] = g[f].x;
+      const uint64_t tag = p.tag;
+      p.live = false;
+      p.model.reset();
+      if (sink != nullptr) {
+        const int k = e.submit_many(x, 1, p.nf, &tag, sink);
+        if (k == 1) {
+          ++*requeued;
+          continue;
+        }
+      }
+      // not accepted (stopping / backpressure / no sink): answered as a device error
+      out.push_back(Completion{tag, 0, (int32_t)ST_DEVICE_ERROR, 0.0, now - p.t_enq});
+      if (segs.empty() || last != nullptr) {
+        segs.push_back(Seg{out.size() - 1, nullptr});
+        last = nullptr;
+      }
+      ++errors;
+      ++done;
+      continue;
+    }
+    int32_t st = fail ? (int32_t)ST_DEVICE_ERROR : (int32_t)ST_OK;
     const int32_t idx = fail ? 0 : r.idx;
-    const double p = fail ? 0.0 : r.p;
-    if (st == ST_OK && !std::isfinite(p)) st = ST_NONFINITE;
-    if (fail) e.healthy_.store(false);
-    errors += st != ST_OK;
-    if (en.model.get() != last || segs.empty()) {
-      segs.push_back(Seg{out.size(), en.model});
-      last = en.model.get();
+    const double pv = fail ? 0.0 : r.p;
+    if (st == ST_OK && !std::isfinite(pv)) st = ST_NONFINITE;
+    if (fail) {
+      e.healthy_.store(false);
+      p.poisoned = true;
     }
-    const int64_t lat = now - en.t_enq;
-    out.push_back(Completion{en.tag, idx, st, p, lat});
+    errors += st != ST_OK;
+    if (segs.empty() || p.model.get() != last) {
+      segs.push_back(Seg{out.size(), p.model});
+      last = p.model.get();
+    }
+    const int64_t lat = now - p.t_enq;
+    out.push_back(Completion{p.tag, idx, st, pv, lat});
     const double us = (double)lat * 1e-3;
     lat_sum += us;
     int b = 0;
     while (b < 23 && (double)(int64_t(1) << b) <= us) ++b;
     lat_hist[b]++;
     ++done;
-    en.model.reset();
-    en.tag = ~uint64_t(0);  // delivered
-    if (fail) en.rec = ~0u;  // a late record could still land in it: the slot is never reused
+    p.live = false;
+    p.model.reset();
   }
-  while (tail_ != head_ && ring_[tail_ % RING].tag == ~uint64_t(0) && ring_[tail_ % RING].rec != ~0u) ++tail_;
-  if (done > 0) {
+  while (tail_ != next_) {
+    const Pend& p = pend_[tail_ & (RESIDENT_RING - 1)];
+    if (p.live || p.poisoned) break;
+    ++tail_;
+  }
+  if (done > 0 || stale > 0) {
     std::lock_guard<std::mutex> lk(e.st_mu_);
     e.stats_.requests += (uint64_t)done;
     e.stats_.errors += (uint64_t)errors;
+    e.stats_.resident_rows += (uint64_t)(done - errors);
+    e.stats_.resident_stale += (uint64_t)stale;
     e.stats_.latency_sum_us += lat_sum;
     for (int b = 0; b < 24; ++b) e.stats_.latency_hist[b] += lat_hist[b];
   }
-  return (int)(head_ - tail_);
+  return (int)(next_ - tail_);
 }
 
-void Engine::combine_on_host(const std::shared_ptr<const Model>& m, LaneEntry** e, const double* X, const int32_t* nf,
-                             int n, uint32_t seq, int32_t status) {
-  size_t off = 0;
-  for (int i = 0; i < n; ++i) {
-    int32_t st = status, idx = 0;
-    double p = 0.0;
-    if (st == ST_OK) {
-      if (nf[i] != m->F)
-        st = ST_SHAPE;
-      else
-        cpu_linear_predict(*m, X + off, 1, &idx, &p);
+namespace {
+int resident_lpe(int F) { return F <= 4 ? 4 : F <= 8 ? 8 : 32; }
+}  // namespace
+
+bool Engine::resident_launch(const std::shared_ptr<const Model>& m, uint32_t mver, int nrings, bool bounce) {
+  if (res_cpu_) return true;  // the supervisor polls the rings itself
+  if (!direct_) return false;
+  ResidentArgs a{};
+  a.rings = res_rings_d_;
+  a.recs = res_recs_d_;
+  a.ctl = res_ctl_d_;
+  const int F = bounce ? 32 : m->F;
+  const int lpe = resident_lpe(F);
+  a.F = bounce ? lpe : m->F;
+  a.K = bounce ? 0 : m->K;
+  a.kind = bounce ? 0 : m->kind;
+  a.W = bounce ? nullptr : m->dW;
+  a.b = bounce ? nullptr : m->db;
+  a.mver = bounce ? 0u : mver;
+  a.lease_ticks = (uint64_t)std::max(20, cfg_.resident_lease_ms) * 100000ull;
+  a.idle_exit_ticks = bounce ? 1000000ull : 0ull;  // the bounce instance: 10 ms without a row
+  a.idle_polls = (uint32_t)std::max(1, cfg_.resident_idle_polls);
+  a.idle_sleep = (uint32_t)std::max(0, cfg_.resident_idle_sleep);
+  const int depth = cfg_.resident_depth >= 4 ? 4 : cfg_.resident_depth >= 2 ? 2 : 1;
+  const bool f64 = bounce ? true : m->xdt == DT_F64;
+  char name[64];
+  std::snprintf(name, sizeof name, "mlapi_resident_%s_r%d_d%d", f64 ? "f64" : "f32", lpe, depth);
+  __atomic_store_n(&res_ctl_h_->stop, 0u, __ATOMIC_RELEASE);
+  return direct_->resident_launch(name, &a, sizeof a, (unsigned)nrings, 64);
+}
+
+bool Engine::resident_stop_instance(int timeout_ms) {
+  __atomic_store_n(&res_ctl_h_->stop, 1u, __ATOMIC_RELEASE);
+  if (res_cpu_) return true;
+  if (direct_->resident_wait(timeout_ms)) return true;
+  // never ended: keep its memory alive and forget its queue (the lease rule ends it eventually)
+  std::fprintf(stderr, "[mlapi engine] resident kernel did not stop within %d ms: abandoned\n", timeout_ms);
+  direct_->resident_abandon();
+  res_leaked_ = true;
+  healthy_.store(false);
+  return false;
+}
+
+// CPU backend: one pass of the resident kernel's protocol over every ring (the same tag rules).
+int Engine::resident_cpu_poll(const std::shared_ptr<const Model>& m, uint32_t mver, int nrings, bool bounce) {
+  int rows = 0;
+  for (int r = 0; r < nrings; ++r) {
+    uint32_t head = __atomic_load_n(&res_ctl_h_->heads[r], __ATOMIC_ACQUIRE);
+    const ResidentGranule* ring =
+        reinterpret_cast<const ResidentGranule*>(res_rings_h_ + (size_t)r * RESIDENT_RING * RESIDENT_ENTRY_BYTES);
+    for (;;) {
+      const ResidentGranule* g = ring + (size_t)(head & (RESIDENT_RING - 1)) * RESIDENT_FMAX;
+      auto tag_of = [&](int f) {  // {pos, meta} of granule f (acquire: its value was written before)
+        return __atomic_load_n(reinterpret_cast<const uint64_t*>(&g[f].pos), __ATOMIC_ACQUIRE);
+      };
+      const uint64_t t0 = tag_of(0);
+      if ((uint32_t)t0 != head) break;
+      const uint32_t meta = (uint32_t)(t0 >> 32);
+      const int rf = (int)(meta & 0xffu);
+      double x[RESIDENT_FMAX];
+      bool full = rf >= 1 && rf <= RESIDENT_FMAX;
+      for (int f = 0; f < rf && full; ++f) {
+        full = (uint32_t)tag_of(f) == head;
+        if (full) x[f] = g[f].x;
+      }
+      if (!full) break;
+      int32_t idx = RESIDENT_STALE_IDX;
+      double p = 0.0;
+      if (!bounce && m && (meta >> 8) == mver && rf == m->F) cpu_linear_predict(*m, x, 1, &idx, &p);
+      ServeRecord* rc = res_recs_h_ + (size_t)r * RESIDENT_RING + (head & (RESIDENT_RING - 1));
+      rc->idx = idx;
+      rc->p = p;
+      __atomic_store_n(&rc->seq, head, __ATOMIC_RELEASE);
+      ++head;
+      ++rows;
     }
-    off += (size_t)nf[i];
-    e[i]->pre = st;
-    e[i]->model = m;
-    ServeRecord* r = arena_h_ + e[i]->rec;
-    r->idx = idx;
-    r->p = p;
-    __atomic_store_n(&r->seq, seq, __ATOMIC_RELEASE);
-    e[i]->expect.store(seq, std::memory_order_release);
+    __atomic_store_n(&res_ctl_h_->heads[r], head, __ATOMIC_RELEASE);
   }
+  return rows;
 }
 
-void Engine::combine() {
-  if (cq_n_.load(std::memory_order_acquire) == 0) return;
-  std::unique_lock<std::mutex> lk(launch_mu_, std::try_to_lock);
-  if (!lk.owns_lock()) return;  // the holder launches what is queued (it re-checks the queue)
-  const int64_t wd = (int64_t)cfg_.watchdog_ms * 1000000;
+void Engine::resident_loop() {
+  pthread_setname_np(pthread_self(), "mlapi-resid");
+  if (cfg_.device >= 0) (void)hipSetDevice(cfg_.device);
+  bool running = false;      // an instance is up
+  bool inst_bounce = false;  // ... answering every row stale (no SMALL model to serve)
+  uint32_t inst_mver = 0;
+  int inst_rings = 0;
+  std::shared_ptr<const Model> inst_model;
+  uint64_t seen_kick = ~uint64_t(0);
+  uint64_t last_hb = 0;
+  int64_t t_hb = now_ns(), t_retry = 0, t_row = 0;
+  bool served = false;  // an instance has served rows that a successor may have to bounce
+  auto set_live = [&](bool live) {
+    res_live_.store(live, std::memory_order_release);
+    std::lock_guard<std::mutex> lk(st_mu_);
+    stats_.resident_live = live;
+    stats_.resident_rings = running ? inst_rings : 0;
+  };
+  auto stop_inst = [&]() {
+    res_live_.store(false, std::memory_order_release);
+    if (running) resident_stop_instance(1000);
+    running = false;
+    inst_model.reset();
+    set_live(false);
+  };
   for (;;) {
-    // retire finished combined batches (done word = seq), or ones past the watchdog
-    const int64_t now = now_ns();
-    while (cin_n_ > 0) {
-      const CBatch& b = cin_[cin_head_];
-      const uint32_t d = __atomic_load_n(cdone_h_ + b.seq % CRING, __ATOMIC_ACQUIRE);
-      if (d != b.seq && !(wd > 0 && now - b.t_launch > wd)) break;
-      {
-        std::lock_guard<std::mutex> sl(st_mu_);
-        stats_.device_us_sum += (double)(now - b.t_launch) * 1e-3;
+    bool stopping;
+    {
+      std::unique_lock<std::mutex> lk(res_mu_);
+      if (res_cpu_ && running) {
+        lk.unlock();
+        const int64_t t = now_ns();
+        if (resident_cpu_poll(inst_model, inst_mver, inst_rings, inst_bounce) > 0 || t_row == 0) t_row = t;
+        if (inst_bounce && t - t_row > 10000000) {  // the bounce instance's idle exit
+          running = false;
+          served = false;
+          t_row = 0;
+        }
+        lk.lock();
+      } else {
+        res_cv_.wait_for(lk, std::chrono::milliseconds(10), [&] { return res_stop_ || res_kick_ != seen_kick; });
       }
-      cin_head_ = (cin_head_ + 1) % CRING;
-      --cin_n_;
+      stopping = res_stop_;
+      seen_kick = res_kick_;
     }
-    if (cin_n_ >= std::max(1, std::min(cfg_.lane_inflight, CRING / 2))) return;  // coalesce: the next batch takes them
+    __atomic_fetch_add(&res_ctl_h_->lease, 1u, __ATOMIC_RELEASE);
+    if (res_leaked_) {  // an instance that never stopped owns the rings: the resident path stays off
+      if (stopping) break;
+      continue;
+    }
+    if (running && !res_cpu_ && direct_->resident_wait(0)) {
+      // ended by itself: the bounce instance's idle exit, a lease expiry (this thread starved) or a fault
+      running = false;
+      if (direct_->resident_faulted()) {
+        std::fprintf(stderr, "[mlapi engine] resident kernel queue error: restarting on a fresh queue\n");
+        direct_->resident_abandon();
+        healthy_.store(false);
+      }
+      if (inst_bounce) served = false;
+      set_live(false);
+    }
+    if (stopping) {
+      stop_inst();
+      break;
+    }
     const std::shared_ptr<const Model> m = model();
-    cx_.clear();
-    cnf_.clear();
-    ce_.clear();
-    {
-      std::lock_guard<std::mutex> ql(cq_mu_);
-      if (cq_e_.empty()) return;
-      // as many rows as one argument block holds
-      size_t take = cq_e_.size();
-      if (m && m->path == PATH_SMALL)
-        while (take > 1 && !linear_inline_fits(m->xdt, (int64_t)take, m->F, m->K)) take = take / 2;
-      take = std::min<size_t>(take, INLINE_MAX_ROWS);
-      size_t xoff = 0;
-      for (size_t i = 0; i < take; ++i) xoff += (size_t)cq_nf_[i];
-      cx_.assign(cq_x_.begin(), cq_x_.begin() + (ptrdiff_t)xoff);
-      cnf_.assign(cq_nf_.begin(), cq_nf_.begin() + (ptrdiff_t)take);
-      ce_.assign(cq_e_.begin(), cq_e_.begin() + (ptrdiff_t)take);
-      cq_x_.erase(cq_x_.begin(), cq_x_.begin() + (ptrdiff_t)xoff);
-      cq_nf_.erase(cq_nf_.begin(), cq_nf_.begin() + (ptrdiff_t)take);
-      cq_e_.erase(cq_e_.begin(), cq_e_.begin() + (ptrdiff_t)take);
-      cq_n_.store((int)cq_e_.size(), std::memory_order_release);
-    }
-    const int n = (int)ce_.size();
-    uint32_t seq = ++cseq_;
-    if (seq == 0) seq = ++cseq_;
-    if (!m || m->path != PATH_SMALL || !linear_inline_fits(m->xdt, n, m->F, m->K)) {
-      // the model changed under the queued rows (hot reload to a wide model, unload): answer them
-      // on the host - float64 oracle records, or ST_NO_MODEL
-      combine_on_host(m, ce_.data(), cx_.data(), cnf_.data(), n, seq, m ? ST_OK : ST_NO_MODEL);
-      continue;
-    }
-    InlineBatch& a = inline_;
-    a.out_idx = nullptr;
-    a.out_p = nullptr;
-    a.rec = arena_d_;
-    a.rec_scatter = 1;
-    a.done = cdone_d_ + seq % CRING;
-    a.seq = seq;
-    {
-      thread_local std::vector<const double*> rows;
-      thread_local std::vector<int32_t> st;
-      rows.assign((size_t)n, nullptr);
-      st.assign((size_t)n, ST_OK);
-      size_t off = 0;
-      for (int i = 0; i < n; ++i) {
-        rows[i] = cnf_[i] == m->F ? &cx_[off] : nullptr;
-        off += (size_t)cnf_[i];
-      }
-      fill_inline(a, *m, n, [&](int64_t i) -> const double* { return rows[i]; }, st.data());
-      for (int i = 0; i < n; ++i) {
-        a.rec_idx[i] = ce_[i]->rec;
-        ce_[i]->pre = st[i];
-        ce_[i]->model = m;
-        ce_[i]->expect.store(seq, std::memory_order_release);
+    const bool small = m && m->path == PATH_SMALL && m->F <= RESIDENT_FMAX && m->K <= 16;
+    const uint32_t want = small ? resident_mver(m->version) : 0u;
+    const int nr = rings_open_.load(std::memory_order_acquire);
+    if (running && (inst_rings != nr || (inst_bounce ? small : want != inst_mver))) stop_inst();
+    const int64_t now = now_ns();
+    if (!running && nr > 0 && (small || served) && now >= t_retry && !res_halt_.load(std::memory_order_acquire)) {
+      const bool bounce = !small;
+      if (resident_launch(m, want, nr, bounce)) {
+        running = true;
+        inst_bounce = bounce;
+        inst_mver = want;
+        inst_rings = nr;
+        inst_model = m;
+        served = true;
+        last_hb = __atomic_load_n(&res_ctl_h_->heartbeat, __ATOMIC_ACQUIRE);
+        t_hb = now;
+        t_row = 0;
+        res_mver_.store(want, std::memory_order_release);
+        res_nrings_.store(nr, std::memory_order_release);
+        {
+          std::lock_guard<std::mutex> lk(st_mu_);
+          stats_.resident_launches++;
+        }
+        set_live(small);
+      } else {
+        // no resident kernel in the code object (or the queue failed): the batcher path serves
+        t_retry = now + 1000000000LL;
+        set_live(false);
       }
     }
-    const int64_t t_l = now_ns();
-    try {
-      TraceRange tr("mlapi.lane.launch");
-      direct_->launch(m->xdt, a);
-    } catch (const std::exception&) {
-      healthy_.store(false);
-      combine_on_host(m, ce_.data(), cx_.data(), cnf_.data(), n, seq, ST_DEVICE_ERROR);
-      continue;
+    if (running && !res_cpu_ && !inst_bounce && cfg_.watchdog_ms > 0) {
+      const uint64_t hb = __atomic_load_n(&res_ctl_h_->heartbeat, __ATOMIC_ACQUIRE);
+      if (hb != last_hb) {
+        last_hb = hb;
+        t_hb = now;
+      } else if (now - t_hb > (int64_t)cfg_.watchdog_ms * 1000000) {
+        // the waves stopped polling: off the request path, restart (a fresh queue if it never ends)
+        std::fprintf(stderr, "[mlapi engine] resident kernel heartbeat stalled: restarting\n");
+        healthy_.store(false);
+        stop_inst();
+        t_hb = now;
+      }
     }
-    cin_[(cin_head_ + cin_n_) % CRING] = CBatch{seq, t_l};
-    ++cin_n_;
-    double qw = 0;
-    for (int i = 0; i < n; ++i) qw += (double)(t_l - ce_[i]->t_enq);
-    int bb = 0;
-    while ((1 << (bb + 1)) <= n && bb < 11) ++bb;
-    std::lock_guard<std::mutex> sl(st_mu_);
-    stats_.batches++;
-    stats_.batch_hist[bb]++;
-    stats_.lane_batches++;
-    stats_.path_batches[PATH_SMALL]++;
-    stats_.inline_batches++;
-    stats_.direct_batches++;
-    stats_.queue_wait_us_sum += qw * 1e-3;
   }
 }
 

@@ -45,6 +45,7 @@
 #include "mlapi/common.h"
 #include "mlapi/kernels.h"
 #include "direct_dispatch.h"
+#include "mlapi/resident.h"
 
 namespace mlapi {
 
@@ -103,55 +104,6 @@ struct Completion {
 
 class Engine;
 
-// Per-IO-thread lane (take the engine hop out of the request path). A lane is
-// a ring of result records that belongs to one HTTP IO thread. The thread that parsed an epoll
-// round's rows queues them with Lane::submit and then tries to become the engine's launcher
-// (flat combining: try-lock of the launch lock); whoever holds it dispatches EVERY queued row of
-// every lane as one kernel-argument batch - one AQL packet - whose kernel writes each row's
-// {seq, idx, p} record straight into its owner's ring (InlineBatch::rec_scatter). Each IO thread
-// polls its own ring in its event loop, so a request never waits for the batcher thread (queue +
-// futex wake) or the completer thread (delivery + eventfd wake). Coalescing is kept: one HSA queue
-// takes only ~0.7 M tiny dispatches/s (tools/dispatch_rate_probe.cpp), so at most
-// EngineConfig::lane_inflight combined batches are in flight and rows that arrive meanwhile ride
-// in the next one. SMALL-path models whose batch fits the argument block; everything else keeps
-// the engine queue. One thread per lane.
-struct LaneEntry {
-  std::atomic<uint32_t> expect{0};  // seq of the batch the row was launched in (0: still queued)
-  int32_t pre = 0;                  // status decided at launch (ST_SHAPE, ST_DEVICE_ERROR, ...)
-  uint32_t rec = 0;                 // arena index of the row's record
-  uint64_t tag = 0;
-  int64_t t_enq = 0;
-  std::shared_ptr<const Model> model;  // the batch's model (written by the launcher before expect)
-};
-
-class Lane {
- public:
-  Lane(const Lane&) = delete;
-  Lane& operator=(const Lane&) = delete;
-  // Queue n rows (nf features each) and try to launch. true = accepted (completions come from
-  // poll()); false = not eligible now (model not on the kernel-argument path, ring full, fault
-  // injection on): the caller submits them to the engine queue.
-  bool submit(const double* X, int n, int nf, const uint64_t* tags);
-  struct Seg {
-    size_t begin;  // first completion of a run of one model in poll()'s output
-    std::shared_ptr<const Model> model;
-  };
-  // Launches queued rows if the launcher is free, then appends the completions of this lane's
-  // finished rows to `out` (runs of one model in segs). Returns the rows still pending.
-  int poll(std::vector<Completion>& out, std::vector<Seg>& segs);
-  int inflight() const { return (int)(head_ - tail_); }
-
- private:
-  friend class Engine;
-  Lane(Engine* e, uint32_t arena_base);
-  static constexpr uint32_t RING = 256;
-  Engine* eng_;
-  uint32_t base_;             // first arena record of this lane
-  uint64_t head_ = 0, tail_ = 0;  // ring positions: [tail_, head_) pending
-  LaneEntry ring_[RING];
-  std::vector<LaneEntry*> ptrs_;  // submit scratch
-};
-
 class Sink {
  public:
   virtual ~Sink() = default;
@@ -159,15 +111,62 @@ class Sink {
   virtual void on_complete(const Completion* c, size_t n, const std::shared_ptr<const Model>& model) = 0;
 };
 
+// Per-IO-thread submission ring of the resident SMALL-path kernel (csrc/include/mlapi/resident.h,
+// the request path without an HSA packet, a batcher or a completer). The IO
+// thread that parsed an epoll round's rows writes them into its ring (plain stores into host
+// memory: no lock, no syscall) and later finds each answer in the ring's record array from its
+// own event loop. The resident wave of that ring (one per IO thread) reads the rows, runs the
+// SMALL kernel's row code and writes the records. One thread per ring.
+class ServeRing {
+ public:
+  ServeRing(const ServeRing&) = delete;
+  ServeRing& operator=(const ServeRing&) = delete;
+  // Write n rows (nf features each) for the resident kernel. true = accepted (completions come
+  // from poll()); false = not eligible now (no resident kernel live for the current model, ring
+  // full, a row of another width, fault injection on): the caller submits them to the engine queue.
+  bool submit(const double* X, int n, int nf, const uint64_t* tags);
+  struct Seg {
+    size_t begin;  // first completion of a run of one model in poll()'s output
+    std::shared_ptr<const Model> model;
+  };
+  // Appends the completions of answered rows to `out` (runs of one model in segs). A row answered
+  // stale (a hot reload raced its submit) goes through the engine queue to `sink` instead; the
+  // number of those is added to *requeued. Returns the rows still pending.
+  int poll(std::vector<Completion>& out, std::vector<Seg>& segs, Sink* sink, int* requeued);
+  int pending() const { return (int)(next_ - tail_); }
+  // Spin (user space, no syscall) until a pending row's record lands or `ns` passed: true if one did.
+  bool wait_any(int64_t ns) const;
+
+ private:
+  friend class Engine;
+  ServeRing(Engine* e, int index);
+  bool landed(uint32_t pos) const;
+  Engine* eng_;
+  int idx_;
+  ResidentGranule* ring_;  // this ring's entries (host view)
+  ServeRecord* rec_;       // this ring's records (host view)
+  uint32_t next_ = 0, tail_ = 0;  // positions: [tail_, next_) submitted and not yet consumed
+  struct Pend {
+    uint64_t tag = 0;
+    int64_t t_enq = 0;
+    std::shared_ptr<const Model> model;
+    int32_t nf = 0;
+    bool live = false;      // submitted, answer not yet consumed
+    bool poisoned = false;  // given up on (watchdog): the slot is never written again
+  };
+  Pend pend_[RESIDENT_RING];
+};
+
+
 struct EngineConfig {
   int device = -1;        // HIP device ordinal, -1 = CPU backend
   int max_batch = 256;    // rows per launch
   int max_wait_us = 0;    // 0 = continuous batching; >0 = also wait up to this long to fill a batch
   int slots = 4;          // batches in flight
   int dtype = DT_F64;     // SMALL-path compute dtype (f64 = bit parity with sklearn, or f32)
-  int wide_dtype = DT_F32;   // dtype of models too wide for the SMALL path: f64 -> WIDE (f64 storage,
-                             // f64 MFMA accumulation: the reference's precision, any F / K / kind);
-                             // f32 -> WIDE (f32 storage, f64 accumulation; f32_gemv: binary
+  int wide_dtype = DT_F64;   // dtype of models too wide for the SMALL path: f64 (default) -> WIDE (f64
+                             // storage, f64 MFMA accumulation: the reference's precision, any F / K /
+                             // kind); f32 -> WIDE (f32 storage, f64 accumulation; f32_gemv: binary
                              // F <= 2048 on the f32 GEMV); bf16 -> GEMV / bf16 MFMA GEMM (F <= 4096),
                              // WIDE beyond
   // WIDE multiclass batches of <= host_merge_rows rows from models with at most this many 16-class
@@ -177,8 +176,6 @@ struct EngineConfig {
   // size (host vs device exp, another merge order), which breaks the f64 path's byte-exact bodies.
   int wide_host_merge_blocks = 0;
   bool f32_gemv = false;     // f32 binary F <= 2048: the f32-accumulating GEMV instead of WIDE (A/B)
-  bool f32_split = false;    // f32 multiclass F <= 512: the f32-accumulating class-split kernel
-                             // (linear_split) instead of WIDE (measurement / A-B)
   int bar_rows = 32;         // wide paths: batches of at most this many rows are written straight into
                              // device HBM through the BAR (direct dispatch's HDP-flushed mapping) instead
                              // of being read by every wave over the host link (0 = off)
@@ -220,12 +217,15 @@ struct EngineConfig {
   // wake-ups (two futex hand-offs on a batch=1 request). SMALL-path models, batches of at most
   // this many rows; 0 = off. On the CPU backend the calling thread runs the float64 oracle.
   int idle_inline_rows = 8;
-  // IO threads queue SMALL-path rows on lanes and launch them by flat combining (open_lane); 0 = off.
-  // Off by default: measured against the batcher / completer threads on the c = 64 headline it
-  // cut the server-side latency but raised CPU per request and the tail (docs/PERFORMANCE.md,
-  // profiles/r4_lanes/)
-  int lanes = 0;
-  int lane_inflight = 3;  // combined lane batches in flight at most (the rest coalesce into the next)
+  // The resident SMALL-path kernel (ServeRing, mlapi/resident.h): IO threads write SMALL-model rows
+  // into per-thread rings that resident waves poll, no packet or engine thread per request; 0 = off
+  // (every row through the batcher). Needs the direct dispatcher's code object on a GPU; on the CPU
+  // backend a host thread plays the kernel's part (tests).
+  int resident = 1;
+  int resident_depth = 2;        // host-memory polls in flight per wave (1, 2, 4)
+  int resident_lease_ms = 200;   // a wave exits when the supervisor's lease has not moved for this long
+  int resident_idle_polls = 20000;  // polls without a row before a wave slows down (an idle server)
+  int resident_idle_sleep = 4;      // ... to one poll per this many ~3.4 us sleeps
 };
 
 struct EngineStats {
@@ -238,7 +238,11 @@ struct EngineStats {
   uint64_t direct_batches = 0;      // ... of which written straight into the HSA queue
   uint64_t direct_wide_batches = 0; // class-split (wide multiclass) batches dispatched into that queue
   uint64_t idle_batches = 0;        // batches run by the submitting thread (run_idle)
-  uint64_t lane_batches = 0;        // batches dispatched by IO threads through lanes (Lane::submit)
+  uint64_t resident_rows = 0;       // rows answered by the resident kernel (ServeRing)
+  uint64_t resident_stale = 0;      // ... bounced to the engine queue (a hot reload raced them)
+  uint64_t resident_launches = 0;   // resident kernel instances launched (start, reload, restart)
+  int resident_rings = 0;           // rings the running instance polls (0: none running)
+  bool resident_live = false;       // IO threads may submit to their rings now
   uint64_t generic_models = 0;      // models loaded onto the scalar GENERIC kernel (a warning is logged)
   uint64_t xcd_errors = 0;          // rows failed because an XCD-local split merge read a misplaced partial
                                     // (the protocol is then off for the device: linear_split.h, xcd.hip)
@@ -296,12 +300,14 @@ class Engine {
   // Blocking convenience API (tests / bulk scoring through the batcher).
   void predict(const double* X, int64_t B, int F, int32_t* idx, double* p, int32_t* status);
 
-  // A dispatch lane for the calling IO thread (owned by the engine, valid until it is destroyed),
-  // or nullptr: CPU backend, lanes off, no direct dispatcher or no producer id left.
-  Lane* open_lane();
-  // The thread is done with the lane: its in-flight batches are waited for (bounded) and dropped,
-  // and the lane goes back to the engine's pool for the next open_lane().
-  void close_lane(Lane* lane);
+  // The calling IO thread's submission ring for the resident kernel (owned by the engine, valid until
+  // it is destroyed), or nullptr: resident off / unavailable, or every ring taken.
+  ServeRing* open_ring();
+  // The thread is done with the ring: its pending rows are waited for (bounded) and the ring goes
+  // back to the engine's pool for the next open_ring().
+  void close_ring(ServeRing* ring);
+  // Stop the resident kernel for good (process exit): no relaunch, wait up to timeout_ms for it.
+  void resident_halt(int timeout_ms);
 
   EngineStats stats() const;
   const EngineConfig& config() const { return cfg_; }
@@ -358,12 +364,16 @@ class Engine {
   void deliver(std::vector<Meta>& metas, const int32_t* idx, const double* p, const int32_t* st,
                const std::shared_ptr<const Model>& m, int64_t now);
   void record_batch(size_t n);
-  friend class Lane;
-  // Flat-combining launcher of the lanes' queued rows (try-lock; no-op if another thread holds it)
-  void combine();
-  // rows of the combine queue that cannot run as a kernel-argument batch: host float64 records
-  void combine_on_host(const std::shared_ptr<const Model>& m, LaneEntry** e, const double* X, const int32_t* nf, int n,
-                       uint32_t seq, int32_t status);
+  friend class ServeRing;
+  void kick_resident();  // reload / ring open: wake the supervisor
+  void resident_register(bool on);  // the at-exit halt list
+  // Resident kernel supervisor (one thread): launches an instance for the current SMALL model over
+  // the open rings, bumps the lease, restarts it on reload / new rings / a stalled heartbeat, and on
+  // the CPU backend plays the kernel itself (resident_cpu_poll).
+  void resident_loop();
+  bool resident_launch(const std::shared_ptr<const Model>& m, uint32_t mver, int nrings, bool bounce);
+  bool resident_stop_instance(int timeout_ms);
+  int resident_cpu_poll(const std::shared_ptr<const Model>& m, uint32_t mver, int nrings, bool bounce);
   // Wait for a launched slot's done word (spin, then back off; fault and watchdog checks).
   void wait_done(Slot& s);
   // The launched slot's results -> idx / p (from the records or the output arrays).
@@ -403,32 +413,29 @@ class Engine {
   InlineBatch inline_{};        // guarded by launch_mu_
   std::mutex launch_mu_;        // launch_batch: batcher thread and run_idle callers
 
-  std::mutex lanes_mu_;
-  std::vector<std::unique_ptr<Lane>> lanes_;
-  std::vector<Lane*> free_lanes_;
-  static constexpr int MAX_LANES = 64;
-  ServeRecord* arena_h_ = nullptr;  // lanes' record rings [MAX_LANES][Lane::RING], host-mapped
-  ServeRecord* arena_d_ = nullptr;
-  // combine queue (rows of every lane waiting for the launcher)
-  std::mutex cq_mu_;
-  std::vector<double> cq_x_;
-  std::vector<int32_t> cq_nf_;
-  std::vector<LaneEntry*> cq_e_;
-  std::atomic<int> cq_n_{0};
-  // launcher state (guarded by launch_mu_): combined batches in flight, done words
-  static constexpr int CRING = 16;
-  uint32_t* cdone_h_ = nullptr;
-  uint32_t* cdone_d_ = nullptr;
-  uint32_t cseq_ = 0;
-  struct CBatch {
-    uint32_t seq;
-    int64_t t_launch;
-  };
-  CBatch cin_[CRING];
-  int cin_head_ = 0, cin_n_ = 0;
-  std::vector<double> cx_;  // launcher scratch: taken rows
-  std::vector<int32_t> cnf_;
-  std::vector<LaneEntry*> ce_;
+  // resident kernel (ServeRing): host-coherent rings [RESIDENT_MAX_RINGS][RESIDENT_RING] entries,
+  // records, control block; the supervisor thread and its wake-up
+  unsigned char* res_rings_h_ = nullptr;
+  unsigned char* res_rings_d_ = nullptr;
+  ServeRecord* res_recs_h_ = nullptr;
+  ServeRecord* res_recs_d_ = nullptr;
+  ResidentCtl* res_ctl_h_ = nullptr;
+  ResidentCtl* res_ctl_d_ = nullptr;
+  bool res_cpu_ = false;              // CPU backend: the supervisor polls the rings itself
+  bool res_leaked_ = false;           // an instance never ended: its memory is not freed
+  std::mutex rings_mu_;
+  std::vector<std::unique_ptr<ServeRing>> rings_;
+  std::vector<ServeRing*> free_rings_;
+  std::atomic<int> rings_open_{0};    // rings handed out so far (the instance's grid)
+  std::mutex res_mu_;
+  std::condition_variable res_cv_;
+  bool res_stop_ = false;
+  uint64_t res_kick_ = 0;             // bumped on reload / ring open: the supervisor re-plans
+  std::atomic<bool> res_live_{false};
+  std::atomic<bool> res_halt_{false};   // resident_halt: never launch again
+  std::atomic<uint32_t> res_mver_{0};   // 24-bit version of the model the running instance serves
+  std::atomic<int> res_nrings_{0};      // rings the running instance polls
+  std::thread res_thread_;
 
   std::vector<std::thread> batchers_;
   std::vector<std::thread> completers_;

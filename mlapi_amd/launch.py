@@ -8,8 +8,10 @@ alternative to ``torchrun`` with what a serving node needs:
   init joins it as a client via ``TORCHELASTIC_USE_AGENT_STORE``);
 * exports RANK / WORLD_SIZE / LOCAL_RANK / LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT, so every
   entry point (``bench.py``, ``mlapi_amd.serve``, ``mlapi_amd.train``) runs unchanged;
-* pins each rank to a contiguous, disjoint slice of the CPUs it may use (the serving path is CPU
-  bound: HTTP parsing and JSON rendering run on these cores) and sizes OMP_NUM_THREADS to it; GPU
+* places each rank (``--pin``): at N > 1 by default on its GPU's NUMA node (``numa``: the node's
+  CPU list as the affinity mask, the scheduler balances the rank's threads over it and its pinned
+  host memory is first touched there), at N = 1 on a disjoint slice of physical cores (``cores``,
+  which also sizes OMP_NUM_THREADS); ``off`` / ``--no-pin`` leaves ranks unpinned. GPU
   ``local_rank`` is selected by the rank itself (all devices stay visible so RCCL can map peers);
 * supervises: the first rank that exits non-zero brings the others down (SIGTERM, then SIGKILL
   after ``--grace``) and its exit code becomes the launcher's; with ``--restart N`` a failed rank
@@ -30,7 +32,7 @@ import sys
 import time
 from typing import List, Optional
 
-from mlapi_amd.utils.affinity import core_order, cpu_slices  # noqa: F401 (re-exported)
+from mlapi_amd.utils.affinity import core_order, cpu_slices, gpu_numa_nodes, numa_rank_cpus  # noqa: F401
 
 
 def _free_port(host: str) -> int:
@@ -41,12 +43,30 @@ def _free_port(host: str) -> int:
     return port
 
 
+def rank_placement(mode: str, nproc: int, **sysfs) -> List[List[int]]:
+    """The CPU mask of every rank ([] = leave it unpinned) for --pin ``mode`` (numa / cores / off).
+    numa: GPU r's NUMA-node CPUs for rank r (:func:`numa_rank_cpus`; unknown node -> unpinned);
+    cores: disjoint physical-core slices of the CPU quota (:func:`cpu_slices`). ``sysfs`` overrides
+    the sysfs roots (tests: sys_kfd, sys_pci, sysnode, cpus)."""
+    if mode == "off":
+        return [[] for _ in range(nproc)]
+    if mode == "cores":
+        return cpu_slices(nproc)
+    cpus = sysfs.pop("cpus", None)
+    nodes = gpu_numa_nodes(**{k: v for k, v in sysfs.items() if k in ("sys_kfd", "sys_pci")})
+    kw = {"sysnode": sysfs["sysnode"]} if "sysnode" in sysfs else {}
+    return [numa_rank_cpus(r, nodes, cpus, **kw) for r in range(nproc)]
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="python -m mlapi_amd.launch", description=__doc__.split("\n\n")[0])
     ap.add_argument("--nproc", type=int, default=0, help="ranks (default: visible GPU count, at least 1)")
     ap.add_argument("--master-addr", default="127.0.0.1")
     ap.add_argument("--master-port", type=int, default=0, help="0 = pick a free port")
-    ap.add_argument("--no-pin", action="store_true", help="do not pin ranks to CPU slices")
+    ap.add_argument("--pin", default="auto", choices=["auto", "numa", "cores", "off"],
+                    help="rank placement: numa = its GPU's NUMA-node CPUs (mask), cores = a disjoint slice of "
+                         "physical cores, off = unpinned; auto = numa at N > 1, cores at N = 1")
+    ap.add_argument("--no-pin", action="store_true", help="same as --pin off")
     ap.add_argument("--grace", type=float, default=10.0, help="seconds between SIGTERM and SIGKILL on failure")
     ap.add_argument("--restart", type=int, default=0,
                     help="restart a rank that exits non-zero up to N times instead of stopping the job "
@@ -81,7 +101,10 @@ def main(argv=None) -> int:
     port = args.master_port or _free_port(args.master_addr)
     store = dist.TCPStore(args.master_addr, port, nproc, is_master=True, wait_for_workers=False,
                           use_libuv=True)
-    slices = cpu_slices(nproc)
+    mode = "off" if args.no_pin else args.pin
+    if mode == "auto":
+        mode = "numa" if nproc > 1 else "cores"
+    placement = rank_placement(mode, nproc)
 
     def _spawn(r: int, restart: int = 0) -> subprocess.Popen:
         env = dict(os.environ)
@@ -90,10 +113,12 @@ def main(argv=None) -> int:
                     "TORCHELASTIC_USE_AGENT_STORE": "True", "MLAPI_LAUNCHER": "1"})
         if restart:
             env["MLAPI_REPLICA_RESTART"] = str(restart)
-        cpus = slices[r]
-        if not args.no_pin:
+        cpus = placement[r]
+        if cpus and mode == "cores":
             env["OMP_NUM_THREADS"] = str(max(1, len(cpus)))
-        pre = (lambda c=cpus: os.sched_setaffinity(0, c)) if not args.no_pin else None
+        if cpus:
+            env["MLAPI_PLACEMENT"] = mode
+        pre = (lambda c=cpus: os.sched_setaffinity(0, c)) if cpus else None
         return subprocess.Popen(cmd, env=env, preexec_fn=pre)
 
     procs: List[subprocess.Popen] = [_spawn(r) for r in range(nproc)]

@@ -63,9 +63,9 @@ class EngineHandle:
         ec.spin_us = config.spin_us
         ec.inline_args = bool(config.inline_args)
         ec.idle_inline_rows = int(config.idle_inline_rows)
-        ec.lanes = int(config.lanes)
-        ec.lane_inflight = int(config.lane_inflight)
-        ec.f32_split = bool(config.f32_split)
+        res = str(config.resident).strip().lower()
+        ec.resident = 1 if res == "on" or (res == "auto" and self.device is not None) else 0
+        ec.resident_depth = int(config.resident_depth)
         ec.f32_gemv = bool(config.f32_gemv)
         ec.wide_host_merge_blocks = int(config.wide_host_merge_blocks)
         ec.completers = int(config.completers)

@@ -11,6 +11,13 @@ the MI355X hosts (``tools/probe_box.sh``, ``profiles/r1_session5/probe.txt``):
 So a rank is placed on ``quota / ranks`` distinct physical cores of its own GPU's NUMA node (the
 zero-copy request slots the kernel reads live in host memory of that node). Used by
 ``mlapi_amd.launch`` and by ``bench.py`` / ``mlapi_amd.serve`` under ``torchrun``.
+
+Without core pinning, a rank can still be kept on its GPU's NUMA node (:func:`numa_rank_cpus`, the
+launcher's default at N > 1): the node's whole CPU list as the mask, so the scheduler balances the
+rank's threads over the node while its pinned host memory (first touched by those threads) and the
+GPU's host link stay on one socket. The GPU -> node map comes from sysfs alone
+(:func:`gpu_numa_nodes`: KFD topology order = HIP device order, PCI ``numa_node``), so a launcher
+that must not initialise the GPU can compute it.
 """
 from __future__ import annotations
 
@@ -183,3 +190,75 @@ def pin_this_rank(local_rank: int, local_world: int, device_index: Optional[int]
         return cpus
     except (OSError, ValueError, IndexError):
         return []
+
+
+SYS_KFD = "/sys/class/kfd/kfd/topology/nodes"
+SYS_PCI = "/sys/bus/pci/devices"
+
+
+def _kv(text: Optional[str]) -> Dict[str, str]:
+    out: Dict[str, str] = {}
+    for line in (text or "").splitlines():
+        parts = line.split()
+        if len(parts) == 2:
+            out[parts[0]] = parts[1]
+    return out
+
+
+def kfd_gpu_bdfs(sys_kfd: str = SYS_KFD) -> List[str]:
+    """PCI addresses ("dddd:bb:dd.f") of the GPUs in KFD topology order - the order the ROCm runtime
+    (and so HIP) enumerates them - read from sysfs without touching the GPU. CPU nodes (no SIMDs)
+    are skipped."""
+    try:
+        nodes = sorted(int(d) for d in os.listdir(sys_kfd) if d.isdigit())
+    except OSError:
+        return []
+    out = []
+    for n in nodes:
+        p = _kv(_read(f"{sys_kfd}/{n}/properties"))
+        try:
+            if int(p.get("simd_count", "0")) <= 0:
+                continue
+            loc, dom = int(p["location_id"]), int(p.get("domain", "0"))
+        except (KeyError, ValueError):
+            continue
+        out.append(f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}")
+    return out
+
+
+def _visible(n: int) -> List[int]:
+    """Physical GPU indices behind HIP device ordinals 0.. (HIP/ROCR/CUDA_VISIBLE_DEVICES)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:
+            try:
+                idx = [int(x) for x in v.split(",") if x.strip() != ""]
+                return [i for i in idx if 0 <= i < n]
+            except ValueError:
+                return list(range(n))
+    return list(range(n))
+
+
+def gpu_numa_nodes(sys_kfd: str = SYS_KFD, sys_pci: str = SYS_PCI) -> List[Optional[int]]:
+    """NUMA node of each visible GPU, by HIP device ordinal (None where sysfs does not say)."""
+    bdfs = kfd_gpu_bdfs(sys_kfd)
+    out: List[Optional[int]] = []
+    for i in _visible(len(bdfs)):
+        s = _read(f"{sys_pci}/{bdfs[i]}/numa_node")
+        try:
+            node = int(s)
+        except (TypeError, ValueError):
+            node = -1
+        out.append(node if node >= 0 else None)
+    return out
+
+
+def numa_rank_cpus(local_rank: int, nodes: List[Optional[int]], cpus: Optional[List[int]] = None,
+                   sysnode: str = SYS_NODE) -> List[int]:
+    """The CPU mask of a rank kept on its GPU's NUMA node (GPU ``local_rank``): the node's CPUs
+    that the process may use - a node mask, not a core slice. [] when the node is unknown or has no
+    usable CPU (the caller then leaves the rank unpinned)."""
+    if local_rank >= len(nodes) or nodes[local_rank] is None:
+        return []
+    allowed = set(sorted(os.sched_getaffinity(0)) if cpus is None else cpus)
+    return [c for c in node_cpus(nodes[local_rank], sysnode) if c in allowed]

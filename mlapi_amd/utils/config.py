@@ -31,8 +31,8 @@ class Config:
     # device / engine
     device: str = "auto"                      # "auto" | "cpu" | "cuda" | "cuda:N" | "N"
     dtype: str = "f64"                        # small-model (F<=32, K<=16) compute dtype: f64 (sklearn parity) | f32
-    wide_dtype: str = "f32"                   # wider models: f32 storage (the f64-accumulating WIDE kernel)
-                                              # | f64 (WIDE kernel, sklearn's dtype)
+    wide_dtype: str = "f64"                   # wider models: f64 storage on the f64-accumulating WIDE kernel (sklearn's
+                                              # dtype: byte-exact bodies) | f32 (opt-in: f32 storage, same kernel)
                                               # | bf16 (opt-in: bf16 GEMV / MFMA GEMM)
     split_max_rows: int = 32                  # bf16 multiclass: batches <= this many rows take the class-split kernel
     bar_rows: int = 32                        # GPU wide paths: batches <= this many rows go to HBM through the BAR (0 = off)
@@ -60,9 +60,12 @@ class Config:
     idle_inline_rows: int = 8                 # GPU: idle engine -> the IO thread launches <= this many rows itself (0 = off)
     wide_host_merge_blocks: int = 0           # GPU: WIDE batches merge class blocks on the host up to this many blocks (0 = in-kernel)
     f32_gemv: bool = False                    # GPU: f32 binary F <= 2048 on the f32-accumulating GEMV (A/B)
-    f32_split: bool = False                   # GPU: f32 multiclass F <= 512 on the f32-accumulating split kernel (A/B)
-    lane_inflight: int = 3                    # GPU: combined lane batches in flight at most (rows coalesce behind them)
-    lanes: int = 0                            # GPU: IO threads launch SMALL-model rows by flat combining (engine lanes; opt-in, measured slower)
+    resident: str = "auto"                    # resident SMALL-path kernel (IO threads write rows into rings that GPU-
+                                              # resident waves poll): auto (on for a GPU) | on (CPU backend: a host
+                                              # thread plays the kernel, tests) | off (every row via the batcher)
+    resident_depth: int = 2                   # host-memory polls in flight per resident wave (1, 2, 4)
+    io_ring_spin_us: int = 5                  # IO threads with rows on the resident kernel watch their records this
+                                              # long in user space between epoll_wait(0) calls
     direct_dispatch: bool = True              # GPU: ... written as AQL packets into the engine's own HSA queue
     direct_wide: bool = True                  # GPU: class-split / record GEMV batches into that queue too ...
     direct_wide_max_weight_bytes: int = 256 << 10  # ... for models with at most this many bytes of W

@@ -74,3 +74,52 @@ def test_cgroup_quota(tmp_path):
     assert cgroup_cpu_quota(str(v1)) == 2.0
     assert effective_cpus(str(v1)) == min(2, len(os.sched_getaffinity(0)))
     assert cgroup_cpu_quota(str(tmp_path / "none")) is None
+
+
+def _fake_mi355x_node(tmp_path, gpu_nodes=(0, 0, 0, 0, 1, 1, 1, 1)):
+    """8 GPUs in KFD topology (after 2 CPU nodes), their PCI numa_node files, and 2 NUMA nodes of
+    128 CPUs each (node 0 = 0-63,128-191, node 1 = 64-127,192-255) - the MI355X host layout."""
+    kfd = tmp_path / "kfd"
+    pci = tmp_path / "pci"
+    node = tmp_path / "node"
+    for n in range(2):  # CPU agents first, as KFD lists them
+        (kfd / str(n)).mkdir(parents=True)
+        (kfd / str(n) / "properties").write_text("cpu_cores_count 128\nsimd_count 0\nlocation_id 0\ndomain 0\n")
+    for g, nn in enumerate(gpu_nodes):
+        bus = 0x05 + 0x10 * g
+        (kfd / str(2 + g)).mkdir(parents=True)
+        (kfd / str(2 + g) / "properties").write_text(f"simd_count 1024\nlocation_id {bus << 8}\ndomain 0\n")
+        d = pci / f"0000:{bus:02x}:00.0"
+        d.mkdir(parents=True)
+        (d / "numa_node").write_text(f"{nn}\n")
+    (node / "node0").mkdir(parents=True)
+    (node / "node1").mkdir(parents=True)
+    (node / "node0" / "cpulist").write_text("0-63,128-191\n")
+    (node / "node1" / "cpulist").write_text("64-127,192-255\n")
+    return str(kfd), str(pci), str(node)
+
+
+def test_launcher_numa_placement_is_the_gpus_node_mask(tmp_path, monkeypatch):
+    """at N > 1 every rank's mask is its GPU's whole NUMA node (not a core
+    slice), read from sysfs without touching the GPU."""
+    from mlapi_amd.launch import rank_placement
+    from mlapi_amd.utils.affinity import gpu_numa_nodes, kfd_gpu_bdfs
+
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    kfd, pci, node = _fake_mi355x_node(tmp_path)
+    assert kfd_gpu_bdfs(kfd)[:2] == ["0000:05:00.0", "0000:15:00.0"]
+    assert gpu_numa_nodes(kfd, pci) == [0, 0, 0, 0, 1, 1, 1, 1]
+    masks = rank_placement("numa", 8, sys_kfd=kfd, sys_pci=pci, sysnode=node, cpus=list(range(256)))
+    n0 = list(range(0, 64)) + list(range(128, 192))
+    n1 = list(range(64, 128)) + list(range(192, 256))
+    assert masks == [n0] * 4 + [n1] * 4
+    # the mask never exceeds what the process may use
+    masks = rank_placement("numa", 8, sys_kfd=kfd, sys_pci=pci, sysnode=node, cpus=list(range(0, 256, 2)))
+    assert all(c % 2 == 0 for m in masks for c in m) and len(masks[0]) == 64
+    # HIP_VISIBLE_DEVICES remaps ordinals: rank 0 drives physical GPU 5 (node 1)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "5,1")
+    assert gpu_numa_nodes(kfd, pci) == [1, 0]
+    # no topology (a container without KFD sysfs): ranks stay unpinned
+    assert rank_placement("numa", 2, sys_kfd=str(tmp_path / "none"), sys_pci=pci, sysnode=node) == [[], []]
+    assert rank_placement("off", 3) == [[], [], []]

@@ -154,6 +154,35 @@ def test_binary_and_ovr_checkpoints(tmp_path, monkeypatch, iris_data):
         assert body["probability"] == pytest.approx(est.predict_proba(x).max(), rel=1e-13)
 
 
+def wide_sklearn_checkpoint(tmp_path, F=64, K=10, seed=0, multi_class=None):
+    """A wide sklearn LogisticRegression pickle (F features, K classes) in tmp_path, and rows."""
+    from sklearn.linear_model import LogisticRegression
+
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((400, F))
+    y = np.array([f"c{i}" for i in range(K)], dtype=object)[np.argmax(X[:, :K] + 0.5 * rng.standard_normal((400, K)), 1)]
+    est = LogisticRegression(max_iter=200).fit(X, y) if multi_class is None else \
+        LogisticRegression(solver="liblinear").fit(X, y)
+    (tmp_path / "LRClassifier.pkl").write_bytes(pickle.dumps(est))
+    return est, [f"f{i}" for i in range(F)], np.round(rng.standard_normal((32, F)), 3)
+
+
+@pytest.mark.parametrize("ovr", [False, True])
+def test_wide_sklearn_checkpoint_served_at_float64(tmp_path, monkeypatch, ovr):
+    """Models wider than Iris are served at sklearn's precision by default (wide_dtype f64): the
+    label is sklearn's predict() and the probability its predict_proba().max() (float64 math; the
+    GPU twin is tests/test_serve_wide_gpu.py::test_wide_sklearn_pickle_over_http)."""
+    est, names, rows = wide_sklearn_checkpoint(tmp_path, multi_class="ovr" if ovr else None)
+    monkeypatch.chdir(tmp_path)
+    c = _client(feature_names=names)
+    for x in rows:
+        r = c.post("/predict", json=dict(zip(names, x.tolist())))
+        assert r.status_code == 200, r.text
+        body = r.json()
+        assert body["prediction"] == est.predict(x[None])[0]
+        assert body["probability"] == pytest.approx(est.predict_proba(x[None]).max(), rel=1e-13, abs=0)
+
+
 # ------------------------------------------------------------------ /files/ (main.py:29-39)
 def _files(client, csv: bytes, token="tok", **extra):
     from mlapi_amd.api.multipart import encode_multipart

@@ -112,13 +112,23 @@ def test_launcher_pins_and_runs_collectives(tmp_path):
 
     assert cpu_slices(3, list(range(8))) == [[0, 1, 2], [3, 4, 5], [6, 7]]
     launch = [sys.executable, "-m", "mlapi_amd.launch", "--nproc", "2"]
-    out = subprocess.run(launch + [str(ROOT / "tests" / "dist" / "affinity.py")], env={**ENV, "OUT": str(tmp_path)},
-                         capture_output=True, text=True, timeout=120)
+    out = subprocess.run(launch[:-2] + ["--nproc", "2", "--pin", "cores", str(ROOT / "tests" / "dist" / "affinity.py")],
+                         env={**ENV, "OUT": str(tmp_path)}, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     a = [json.loads((tmp_path / f"aff_{r}.json").read_text()) for r in range(2)]
     assert [x["rank"] for x in a] == [0, 1] and all(x["world"] == 2 for x in a)
     assert not set(a[0]["cpus"]) & set(a[1]["cpus"])
     assert a[0]["omp"] == str(len(a[0]["cpus"]))
+    # default at N > 1: each rank on its GPU's NUMA node (tests/test_affinity.py); without the KFD
+    # topology in sysfs (this container) the ranks are left unpinned rather than guessed
+    import os
+
+    if not os.path.isdir("/sys/class/kfd/kfd/topology/nodes"):
+        out = subprocess.run(launch + [str(ROOT / "tests" / "dist" / "affinity.py")], env={**ENV, "OUT": str(tmp_path)},
+                             capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr
+        a = [json.loads((tmp_path / f"aff_{r}.json").read_text()) for r in range(2)]
+        assert sorted(a[0]["cpus"]) == sorted(os.sched_getaffinity(0)) == sorted(a[1]["cpus"])
     out = subprocess.run(launch + [str(ROOT / "tests" / "dist" / "comm_semantics.py")],
                          env={**ENV, "OUT": str(tmp_path), "MLAPI_COMM": "fake"}, capture_output=True, text=True,
                          timeout=120)

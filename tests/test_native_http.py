@@ -408,7 +408,7 @@ def test_metrics_expose_http_latency_stages_and_rejections(iris_cwd):
         for name in ('mlapi_http_request_duration_seconds_bucket{rank="0",backend="cpu",le="+Inf"}',
                      "mlapi_http_request_duration_seconds_count", 'mlapi_server_stage_seconds_total{rank="0",'
                      'backend="cpu",stage="parse"}', "mlapi_requests_rejected_total", "mlapi_queue_wait_seconds_total",
-                     'mlapi_serving_dtype_info{rank="0",backend="cpu",small="f64",wide="f32"} 1'):
+                     'mlapi_serving_dtype_info{rank="0",backend="cpu",small="f64",wide="f64"} 1'):
             assert name in m, name
     finally:
         srv.stop()

@@ -1,0 +1,180 @@
+"""The resident SMALL-path kernel (csrc/include/mlapi/resident.h, ServeRing in csrc/runtime/engine.h):
+IO threads write parsed /predict rows into per-thread rings that resident waves poll, and render
+the answers from the rings' record arrays - no AQL packet, batcher or completer per request.
+
+Every body is checked byte for byte against the engine's answers (which make_workload first
+checks against the float64 oracle). The CPU variants run the same ring protocol with the engine's
+supervisor thread playing the kernel (resident="on" on the CPU backend); the GPU variants run the
+real kernel (serve_resident.h) on the MI355X."""
+import threading
+
+import numpy as np
+import pytest
+
+from mlapi_amd.models.linear import Kind, LinearModel
+
+IRIS = ["sepal_length", "sepal_width", "petal_length", "petal_width"]
+LABELS = ["Iris-setosa", "Iris-versicolor", "Iris-virginica"]
+DEVICES = [pytest.param("cpu", id="cpu"), pytest.param("cuda:0", id="gpu", marks=pytest.mark.gpu)]
+
+
+def _cfg(device, names, **kw):
+    from mlapi_amd.utils.config import Config
+
+    kw.setdefault("io_threads", 4)
+    kw.setdefault("resident", "on")
+    return Config.from_env(port=0, device=device, reload="off", missing_model="keep",
+                           model_path="/nonexistent/resident.pkl", feature_names=list(names), **kw)
+
+
+def _stats_delta(s0, s1):
+    return {k: s1[k] - s0[k] for k in ("requests", "batches", "idle_batches", "errors", "resident_rows",
+                                       "resident_stale", "resident_launches")}
+
+
+def _serve(native, device, model, names, X, *, conns, threads, reqs_per_conn, rtol=1e-12, **kw):
+    from mlapi_amd.serve.loadgen import make_workload
+    from mlapi_amd.serve.server import NativeServer
+
+    with NativeServer(_cfg(device, names, **kw)) as srv:
+        srv.runtime.handle.load(model)
+        reqs, exp = make_workload(srv.runtime.handle.engine, model, names, X, rtol_oracle=rtol, label_margin=1e-5)
+        lg = native.Loadgen("127.0.0.1", srv.port, reqs[0].decode(), conns, threads)
+        lg.set_workload([r.decode() for r in reqs], [e.decode() for e in exp], 0.0)
+        lg.run(20, False)  # warm: every IO thread has opened its ring, the instance covers them all
+        s0 = srv.runtime.handle.stats()
+        res = lg.run(reqs_per_conn, True)
+        lg.close()
+        s1 = srv.runtime.handle.stats()
+    return res, _stats_delta(s0, s1), s1
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_resident_concurrent_bodies_exact(native, device):
+    m = LinearModel.random(4, 3, seed=11, labels=LABELS)
+    X = np.round(np.random.default_rng(3).standard_normal((512, 4)) * 2 + 4, 1)
+    res, d, s1 = _serve(native, device, m, IRIS, X, conns=48, threads=3, reqs_per_conn=200)
+    n = 48 * 200
+    assert res["failed"] == 0 and res["errors"] == 0 and res["body_mismatches"] == 0, res
+    assert res["status_counts"] == {200: n}
+    assert d["requests"] == n and d["errors"] == 0, d
+    # every row went through the rings: no batch was launched for them
+    assert d["resident_rows"] == n and d["batches"] == 0, d
+    assert s1["resident_live"] and s1["resident_rings"] >= 1, s1
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_resident_many_rows_per_ring(native, device):
+    """64 connections on ONE IO thread: more rows pending than one poll's window (16 rows of 4
+    features) - the window slides as the leading rows are answered."""
+    m = LinearModel.random(4, 3, seed=12, labels=LABELS)
+    X = np.round(np.random.default_rng(4).standard_normal((256, 4)) * 2 + 4, 1)
+    res, d, _ = _serve(native, device, m, IRIS, X, conns=64, threads=2, reqs_per_conn=100, io_threads=1)
+    assert res["body_mismatches"] == 0 and res["status_counts"] == {200: 6400}, res
+    assert d["resident_rows"] == 6400, d
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("F,K,kind,dtype", [(8, 4, Kind.OVR, "f32"), (2, 1, Kind.BINARY, "f64"),
+                                            (32, 16, Kind.MULTINOMIAL, "f64"), (5, 1, Kind.BINARY_SOFTMAX, "f32")])
+def test_resident_shapes(native, device, F, K, kind, dtype):
+    """Every SMALL-path width class (4 / 8 / 32 lanes per row), kind and dtype, batch = 1 and
+    concurrent."""
+    names = [f"x{i}" for i in range(F)]
+    m = LinearModel.random(F, K if K > 1 else 2, seed=5, kind=kind)
+    X = np.random.default_rng(9).standard_normal((128, F))
+    rtol = 1e-12 if dtype == "f64" else 1e-5
+    res, d, _ = _serve(native, device, m, names, X, conns=1, threads=1, reqs_per_conn=300, rtol=rtol, dtype=dtype)
+    assert res["body_mismatches"] == 0 and res["status_counts"] == {200: 300}, res
+    assert d["resident_rows"] == 300 and d["idle_batches"] == 0 and d["batches"] == 0, d
+    res, d, _ = _serve(native, device, m, names, X, conns=24, threads=2, reqs_per_conn=50, rtol=rtol, dtype=dtype)
+    assert res["body_mismatches"] == 0 and res["status_counts"] == {200: 1200}, res
+    assert d["resident_rows"] == 1200, d
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_resident_skips_wide_models(native, device):
+    """A model off the SMALL path (F = 64: the WIDE kernel) never takes the rings: the queued path
+    answers it, with the same bytes."""
+    F = 64
+    names = [f"f{i}" for i in range(F)]
+    m = LinearModel.random(F, 2, seed=2)
+    X = np.round(np.random.default_rng(4).standard_normal((128, F)), 3)
+    res, d, s1 = _serve(native, device, m, names, X, conns=16, threads=2, reqs_per_conn=50, rtol=1e-5)
+    assert res["body_mismatches"] == 0 and res["status_counts"] == {200: 800}, res
+    assert d["resident_rows"] == 0 and d["requests"] == 800, d
+    assert not s1["resident_live"], s1
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_resident_off_same_bytes(native, device):
+    """resident = off: the batcher answers, byte-identical to the resident kernel's answers."""
+    m = LinearModel.random(4, 3, seed=11, labels=LABELS)
+    X = np.round(np.random.default_rng(3).standard_normal((256, 4)) * 2 + 4, 1)
+    res, d, _ = _serve(native, device, m, IRIS, X, conns=16, threads=2, reqs_per_conn=50, resident="off")
+    assert res["body_mismatches"] == 0 and res["status_counts"] == {200: 800}, res
+    assert d["resident_rows"] == 0 and d["requests"] == 800, d
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_resident_hot_reload_under_load(native, device):
+    """Models swapped while clients keep posting: every body is the answer of one of the two
+    models for its row (rows parsed for the old version are bounced stale and re-answered by the
+    engine queue with the current model), nothing fails, and each reload relaunches the instance."""
+    import http.client
+    import json
+
+    from mlapi_amd.serve.server import NativeServer
+
+    ma = LinearModel.random(4, 3, seed=1, labels=LABELS)
+    mb = LinearModel.random(4, 3, seed=2, labels=LABELS)
+    rows = np.round(np.random.default_rng(8).standard_normal((64, 4)) * 2 + 4, 1)
+    want = []
+    for m in (ma, mb):
+        idx, p = m.predict_max(rows)
+        want.append([(LABELS[i], float(q)) for i, q in zip(idx, p)])
+    errors, bad = [], []
+    stop = threading.Event()
+    with NativeServer(_cfg(device, IRIS)) as srv:
+        srv.runtime.handle.load(ma)
+        s0 = srv.runtime.handle.stats()
+
+        def client(k):
+            try:
+                c = http.client.HTTPConnection("127.0.0.1", srv.port, timeout=10)
+                i = k
+                while not stop.is_set():
+                    r = i % len(rows)
+                    body = json.dumps(dict(zip(IRIS, rows[r].tolist())))
+                    c.request("POST", "/predict", body, {"Content-Type": "application/json"})
+                    resp = c.getresponse()
+                    data = resp.read()
+                    if resp.status != 200:
+                        bad.append((resp.status, data))
+                        continue
+                    got = json.loads(data)
+                    cands = [w[r] for w in want]
+                    if not any(got["prediction"] == lab and abs(got["probability"] - p) <= 1e-12 * p for lab, p in cands):
+                        bad.append((r, got, cands))
+                    i += 7
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+
+        ts = [threading.Thread(target=client, args=(k,)) for k in range(6)]
+        for t in ts:
+            t.start()
+        import time
+
+        for j in range(8):
+            time.sleep(0.05)
+            srv.runtime.handle.load(mb if j % 2 == 0 else ma)
+        time.sleep(0.05)
+        stop.set()
+        for t in ts:
+            t.join()
+        s1 = srv.runtime.handle.stats()
+    assert not errors, errors[:3]
+    assert not bad, bad[:3]
+    d = _stats_delta(s0, s1)
+    assert d["resident_launches"] >= 8 and d["errors"] == 0, d
+    assert d["resident_rows"] > 0, d

@@ -96,15 +96,14 @@ def test_engine_wide_paths_match_oracle(native, F, K, kind, wide, path, stage):
         e.stop()
 
 
-@pytest.mark.parametrize("wide", ["bf16", "f32", "f32split"])
+@pytest.mark.parametrize("wide", ["bf16", "f32"])
 def test_engine_small_multiclass_batches_take_split_kernel(native, wide):
-    """Serving-sized multiclass batches (1..32 rows): bf16 and f32_split run the class-split kernel
+    """Serving-sized multiclass batches (1..32 rows): bf16 runs the class-split kernel
     (linear_split.h), f32 the f64-accumulating wide kernel (host-merged records up to 16 rows);
     results match the oracle batch by batch."""
     F, K = 256, 1000
     m = LinearModel.random(F, K, seed=5, kind=Kind.MULTINOMIAL)
-    e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide[:3] if wide != "bf16" else wide],
-                f32_split=wide == "f32split")
+    e = _engine(native, max_batch=256, max_features=F, wide_dtype=DT[wide])
     try:
         e.load_model(int(m.kind), m.W, m.b, m.label_json())
         assert e.model_path() == ("wide" if wide == "f32" else "gemm")
@@ -113,8 +112,7 @@ def test_engine_small_multiclass_batches_take_split_kernel(native, wide):
             X = rng.standard_normal((n, F))
             idx, p, st = e.predict(X)
             assert (st == 0).all()
-            check(m, X, idx, p, wide[:3] if wide != "bf16" else wide,
-                  rtol={"f32": 1e-11, "f32split": 1e-5, "bf16": 1e-4}[wide])
+            check(m, X, idx, p, wide, rtol={"f32": 1e-11, "bf16": 1e-4}[wide])
     finally:
         e.stop()
 

@@ -3,8 +3,8 @@ misplaced merge: a row whose merging block read a partial written on another XCD
 XCD_BAD_IDX, the engine fails it (ST_DEVICE_ERROR, counted in stats()["xcd_errors"]) and switches
 the protocol off for the device, so the next batches take the agent-scope merge and are right
 again. The misplacement is injected (xcd_local_inject: the next launch reports every merged row as
-misplaced). Also: f32 class-split models with max_batch above one launch's 2048-row cap run in
-row chunks instead of throwing."""
+misplaced). Also: class-split batches above one launch's 2048-row cap run in row chunks instead of
+throwing. The engine's class-split path serves bf16 models (split_max_rows)."""
 import numpy as np
 import pytest
 
@@ -23,24 +23,21 @@ def _engine(native, **kw):
     return native.Engine(cfg)
 
 
-def _f32_oracle(m):
-    f32 = lambda a: np.asarray(a, dtype=np.float32).astype(np.float64)  # noqa: E731
-    return LinearModel(f32(m.W), f32(m.b), m.classes, m.kind), f32
+def _check(m, X, idx, p, rtol=1e-4):
+    from mlapi_amd.serve.loadgen import bf16_oracle
 
-
-def _check(m, X, idx, p, rtol=1e-5):
-    om, f32 = _f32_oracle(m)
-    ridx, rp = om.predict_max(f32(X))
-    z = om.decision_function(f32(X))
+    om, Xb = bf16_oracle(m, X)  # the model and rows as the bf16 kernel reads them
+    ridx, rp = om.predict_max(Xb)
+    z = om.decision_function(Xb)
     margin = np.diff(np.sort(z, axis=1)[:, -2:], axis=1)[:, 0]
-    assert not ((idx != ridx) & (margin > 1e-4)).any()
+    assert not ((idx != ridx) & (margin > 1e-3)).any()
     np.testing.assert_allclose(p, rp, rtol=rtol, atol=0)
 
 
 def test_misplaced_xcd_merge_fails_rows_then_falls_back(native):
     F, K = 256, 200  # 4 class blocks: an in-kernel split merge
     m = LinearModel.random(F, K, seed=21)
-    e = _engine(native, max_batch=64, max_features=F, wide_dtype=1, f32_split=True, host_merge_rows=0)
+    e = _engine(native, max_batch=64, max_features=F, wide_dtype=2, split_max_rows=64, host_merge_rows=0)
     try:
         e.load_model(int(m.kind), m.W, m.b, m.label_json())
         rng = np.random.default_rng(5)
@@ -71,10 +68,10 @@ def test_misplaced_xcd_merge_fails_rows_then_falls_back(native):
         e.stop()
 
 
-def test_f32_split_batches_above_one_launch_run_in_chunks(native):
+def test_split_batches_above_one_launch_run_in_chunks(native):
     F, K = 128, 40
     m = LinearModel.random(F, K, seed=8)
-    e = _engine(native, max_batch=4096, max_features=F, wide_dtype=1, f32_split=True, max_wait_us=50000)
+    e = _engine(native, max_batch=4096, max_features=F, wide_dtype=2, split_max_rows=4096, max_wait_us=50000)
     try:
         e.load_model(int(m.kind), m.W, m.b, m.label_json())
         X = np.round(np.random.default_rng(2).standard_normal((3000, F)), 3)

@@ -8,6 +8,8 @@
 # steps:
 #   test          pytest -m gpu (whole GPU tier)          smoke      __graft_entry__.smoke()
 #   serve         headline bench (Iris /predict)           serve_wide F=256 /predict, K=1000 and K=2, f32 and bf16
+#   resident      resident SMALL-path kernel: its GPU tests (tests/test_resident.py)
+#   serve_res     the driver's serve command, resident kernel on / off, interleaved x3 (RES_ROUNDS)
 #   marker        rocprofv3 --marker-trace of serve / serve_wide with the roctx stage ranges on
 #   serve_ab      serve with kernel-argument batches on/off, interleaved x2 (box variance is large)
 #   serve_idle    serve with the idle-engine fast path on (8 rows) / off, interleaved x2
@@ -64,6 +66,13 @@ for s in $steps; do
     test) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke) run smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     serve) run bench_serve 300 python -u bench.py --steps 200 --warmup 20 ;;
+    resident) run pytest_resident 400 python -u -m pytest tests/test_resident.py -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    serve_res)  # the driver's exact command with the resident kernel on / off, interleaved
+      for r in $(seq 1 "${RES_ROUNDS:-3}"); do
+        for m in on off; do
+          MLAPI_RESIDENT=$m run "serve_res${m}_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+        done
+      done ;;
     serve_wide)
       for dt in f32 bf16; do
         run bench_serve_wide_k1000_$dt 300 python -u bench.py --mode serve_wide --wide-classes 1000 --wide-dtype $dt --steps 40 --warmup 5
@@ -178,6 +187,10 @@ for s in $steps; do
       for m in gemv gemm train train_softmax; do prof "$m" 300 --mode $m --steps 20 --warmup 2; done
       prof serve 300 --steps 20 --warmup 2 --reqs-per-conn 512
       prof serve_wide 300 --mode serve_wide --steps 10 --warmup 2 --reqs-per-conn 256 ;;
+    pmc_big)  # every counter group (one pass each) for the big kernels: gemm_softmax32 (B = 262,144),
+              # softmax_grad_dw (F = 256), softmax_rows MODE 5 + gdw_gemm128 (F = 1024)
+      PMC_BENCHES="gemm_big:--mode gemm --batch 262144 --steps 5 --warmup 1|tsm256:--mode train_softmax --steps 5 --warmup 1|tsm1024:--mode train_softmax --softmax-features 1024 --steps 5 --warmup 1" \
+        run pmc_big 1200 bash tools/pmc_profile.sh ;;
     pmc_gemm) PMC_BENCHES="gemm:--mode gemm --steps 5 --warmup 1|gemm_big:--mode gemm --batch 262144 --steps 5 --warmup 1" run pmc_gemm 600 bash tools/pmc_profile.sh ;;
     gemm_ws)  # W-stationary persistent kernel vs the 32x32 kernel: tests, interleaved benches, kernel stats
       MLAPI_GEMM_WS=1 run pytest_gemm 600 python -u -m pytest tests/test_kernels_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "gemm or softmax"
