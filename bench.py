@@ -417,7 +417,10 @@ def _replica_evidence(tr, info) -> dict:
     h = float(int.from_bytes(hashlib.sha256(raw).digest()[:6], "little"))
     hs = all_gather_floats([h], info)[:, 0]
     return {"replicas_bitwise_equal": bool((hs == hs[0]).all()),
-            "p2p_selftest": info.__dict__.get("p2p_selftest", "n/a")}
+            "p2p_selftest": info.__dict__.get("p2p_selftest", "n/a"),
+            # the fused exchange checked against the exact sum / ncclAllReduce at start-up and by
+            # the replica hash every MLAPI_DP_VERIFY_EVERY steps (mlapi_amd/parallel/p2p.py)
+            "p2p_verify": info.__dict__.get("p2p_verify", "n/a")}
 
 
 def bench_train(args, info):

@@ -374,6 +374,16 @@ PYBIND11_MODULE(_C, m) {
       py::arg("stream") = 0, py::arg("params") = 0, py::arg("mom") = 0, py::arg("shadow_w") = 0,
       py::arg("shadow_b") = 0, py::arg("pen_cols") = 0, py::arg("lr") = 0.f, py::arg("inv_n") = 0.f,
       py::arg("l2") = 0.f, py::arg("momentum") = 0.f, py::arg("p2p") = nullptr, py::arg("timeout_ms") = 60000);
+  m.def(
+      "gdw_reduce",
+      [](uintptr_t slabs, int nslabs, int K, int F_aug, uintptr_t dW_out, uintptr_t stat_slabs, int nstat,
+         uintptr_t stats_out, uintptr_t stream, P2PAllReduce* p2p, int timeout_ms) {
+        launch_gdw_reduce(ptr<float>(slabs), nslabs, K, F_aug, ptr<float>(dW_out), ptr<float>(stat_slabs), nstat,
+                          ptr<float>(stats_out), nullptr, p2p, timeout_ms, stream_of(stream));
+      },
+      py::arg("slabs"), py::arg("nslabs"), py::arg("K"), py::arg("F_aug"), py::arg("dW_out"), py::arg("stat_slabs"),
+      py::arg("nstat"), py::arg("stats_out"), py::arg("stream") = 0, py::arg("p2p") = nullptr,
+      py::arg("timeout_ms") = 60000);
   m.def("softmax_grad_wide_supported", &softmax_grad_wide_supported);
   m.def("softmax_grad_wide_workspace", &softmax_grad_wide_workspace);
   m.def(
@@ -550,6 +560,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("io_spin_us", &ServerConfig::io_spin_us)
       .def_readwrite("io_wait_spin_us", &ServerConfig::io_wait_spin_us)
       .def_readwrite("io_ring_spin_us", &ServerConfig::io_ring_spin_us)
+      .def_readwrite("io_ring_sleep_us", &ServerConfig::io_ring_sleep_us)
       .def_readwrite("idle_max_conns", &ServerConfig::idle_max_conns)
       .def_readwrite("io_spin_lowload_us", &ServerConfig::io_spin_lowload_us)
       .def_readwrite("io_spin_max_conns", &ServerConfig::io_spin_max_conns)
@@ -640,6 +651,7 @@ PYBIND11_MODULE(_C, m) {
       .def("selftest_write", &P2PAllReduce::selftest_write, py::arg("corrupt") = 0,
            py::call_guard<py::gil_scoped_release>())
       .def("selftest_verify", &P2PAllReduce::selftest_verify, py::call_guard<py::gil_scoped_release>())
+      .def("inject_skip_publish", &P2PAllReduce::inject_skip_publish)
       .def_property_readonly("epoch", &P2PAllReduce::epoch)
       .def_property_readonly("max_bytes", &P2PAllReduce::max_bytes);
 

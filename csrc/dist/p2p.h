@@ -55,6 +55,7 @@ struct P2PBlockArgs {
   uint32_t epoch = 0;
   uint64_t timeout_ticks = 0;                     // wall_clock64() ticks (100 MHz)
   uint32_t mode = 0;  // bit 0: release fence + release flag store; bit 1: acquire polling (A/B: MLAPI_P2P_MODE)
+  int fault_block = -1;  // fault injection (P2PAllReduce::inject_skip_publish): this block never publishes
 };
 
 class P2PAllReduce {
@@ -90,6 +91,9 @@ class P2PAllReduce {
   // One fused exchange for a kernel of `nblocks` blocks whose slices total `bytes` (advances the
   // epoch; every rank must issue the same sequence of calls).
   P2PBlockArgs block_exchange(size_t bytes, int nblocks, int timeout_ms);
+  // Fault injection for the exchange verification (mlapi_amd/parallel/p2p.py): the next
+  // block_exchange's block `block` skips its flag publish on this rank (a stale flag for its peers).
+  void inject_skip_publish(int block) { fault_next_ = block; }
   uint32_t epoch() const { return epoch_; }
   int world() const { return world_; }
   size_t max_bytes() const { return max_bytes_; }
@@ -101,6 +105,7 @@ class P2PAllReduce {
   uint32_t* flags_ = nullptr;   // FLAG_WORDS_ALLREDUCE epoch words + block flags (uncached, IPC-exported)
   uint32_t* status_ = nullptr;   // host-mapped word (status_d_ on the device)
   uint32_t* status_d_ = nullptr;
+  int fault_next_ = -1;
   uint32_t* selftest_h_ = nullptr;  // host-mapped mismatch counter of selftest_verify
   uint32_t* selftest_d_ = nullptr;
   void* peer_data_[MAX_RANKS] = {};

@@ -306,6 +306,8 @@ P2PBlockArgs P2PAllReduce::block_exchange(size_t bytes, int nblocks, int timeout
     return e ? (uint32_t)atoi(e) : 0u;
   }();
   a.mode = mode;
+  a.fault_block = fault_next_;
+  fault_next_ = -1;
   return a;
 }
 

@@ -31,6 +31,7 @@ namespace mlapi {
 __device__ inline void p2p_block_publish(const P2PBlockArgs& a, int block, bool phase2 = false) {
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  if (block == a.fault_block && !phase2) return;  // injected fault: the peers see a stale flag
   if (a.mode & 1) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   if ((int)threadIdx.x < a.world) {
     uint32_t* f = (phase2 ? a.peer_bflags2 : a.peer_bflags)[threadIdx.x] + (size_t)block * P2PBlockArgs::MAX_RANKS + a.rank;

@@ -11,6 +11,7 @@
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
+#include <sys/prctl.h>
 #include <sys/socket.h>
 #include <unistd.h>
 #include <x86intrin.h>
@@ -401,6 +402,9 @@ class IoThread : public Sink {
     const int lowload_conns = srv_->config().io_spin_max_conns;
     const int64_t wait_spin_ns = (int64_t)srv_->config().io_wait_spin_us * 1000;
     const int64_t ring_spin_ns = (int64_t)srv_->config().io_ring_spin_us * 1000;
+    const int64_t ring_sleep_ns = (int64_t)srv_->config().io_ring_sleep_us * 1000;
+    if (ring_sleep_ns > 0) prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // us-scale epoll_pwait2 timeouts
+    bool ring_sleep = false;  // this pass waits for the ring's records in epoll_pwait2
     int64_t last_active = 0;
     int last_n = 0;  // events of the previous epoll_wait
     ring_ = srv_->engine() != nullptr ? srv_->engine()->open_ring() : nullptr;
@@ -434,7 +438,11 @@ class IoThread : public Sink {
         // poll found no event), watch their records in user space for a while first - the GPU leg
         // is a few us, an epoll_wait per check would be a syscall per pass
         timeout = 0;
-        if (last_n == 0 && ring_spin_ns > 0 && !pending_.load(std::memory_order_relaxed)) {
+        if (last_n == 0 && ring_sleep_ns > 0 && !pending_.load(std::memory_order_relaxed)) {
+          // io_ring_sleep_us: sleep in the kernel for that long instead (a socket event still
+          // wakes the thread at once); costs a context switch, saves the spin's CPU
+          ring_sleep = true;
+        } else if (last_n == 0 && ring_spin_ns > 0 && !pending_.load(std::memory_order_relaxed)) {
           Stage sg(this, SS_IDLE_GPU);
           if (ring_->wait_any(ring_spin_ns)) continue;  // harvest first
         }
@@ -455,7 +463,14 @@ class IoThread : public Sink {
         blocked_.store(true);
         if (pending_.load()) timeout = 0;  // a hand-off that did not write the eventfd
       }
-      const int n = epoll_wait(epfd_, evs, 256, timeout);
+      int n;
+      if (ring_sleep) {
+        ring_sleep = false;
+        const timespec ts{0, (long)ring_sleep_ns};
+        n = epoll_pwait2(epfd_, evs, 256, &ts, nullptr);
+      } else {
+        n = epoll_wait(epfd_, evs, 256, timeout);
+      }
       blocked_.store(false);
       last_n = n;
       const bool spin_enabled = always_spin_ns > 0 || lowload_spin_ns > 0;

@@ -61,6 +61,9 @@ struct ServerConfig {
   // Rows of this thread on the resident kernel (ServeRing) and no socket event: watch their records
   // in user space this long before the next epoll_wait(0) (no syscall per check). 0 = never spin.
   int io_ring_spin_us = 5;
+  // ... or, when > 0, sleep in epoll_pwait2 for this long instead of spinning (a socket event
+  // still wakes the thread; timer slack set to 1 us): a context switch instead of a spin.
+  int io_ring_sleep_us = 0;
   int idle_max_conns = 0;  // idle-engine path only while <= this many connections are open (0 = any)
   // Low-load busy-poll: while the whole server holds at most io_spin_max_conns open connections
   // (a batch=1 client), an IO thread that just had activity polls for this long before blocking,

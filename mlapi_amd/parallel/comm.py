@@ -192,6 +192,18 @@ def _bcast(t: torch.Tensor, info: DistInfo, src: int) -> None:
         dist.broadcast(t, src)
 
 
+def broadcast_(t: torch.Tensor, info: DistInfo, src: int = 0) -> torch.Tensor:
+    """In-place broadcast of ``t`` from rank ``src`` (any device: staged through the collective's)."""
+    if info.world == 1:
+        return t
+    dev = _coll_device(info)
+    buf = t.detach().to(dev).contiguous()
+    _bcast(buf, info, src)
+    if buf is not t:
+        t.copy_(buf)
+    return t
+
+
 def _broadcast_bytes(payload: Optional[bytes], info: DistInfo, src: int = 0) -> bytes:
     dev = _coll_device(info)
     n = torch.tensor([len(payload) if payload is not None else 0], dtype=torch.int64, device=dev)

@@ -63,6 +63,7 @@ class NativeServer:
         sc.io_spin_us = int(config.io_spin_us)
         sc.io_wait_spin_us = int(config.io_wait_spin_us)
         sc.io_ring_spin_us = int(config.io_ring_spin_us)
+        sc.io_ring_sleep_us = int(config.io_ring_sleep_us)
         sc.idle_max_conns = int(config.idle_max_conns)
         sc.io_spin_lowload_us = int(config.io_spin_lowload_us)
         sc.io_spin_max_conns = int(config.io_spin_max_conns)

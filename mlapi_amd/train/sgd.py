@@ -66,6 +66,9 @@ class BinarySGDTrainer:
 
             self._dp = dp_exchange(self.info, (n_features + 3) * 4)
         self.dp_timeout_ms = 60_000
+        from mlapi_amd.parallel.p2p import verify_every
+
+        self.verify_every = verify_every()  # fused steps between replica checks (MLAPI_DP_VERIFY_EVERY)
         self.steps = 0
         self._stats = torch.zeros(2, dtype=torch.float64)
         self._n_seen = 0
@@ -122,6 +125,29 @@ class BinarySGDTrainer:
         if self._dp is not None:
             self._dp.check()
 
+    def verify_replicas(self) -> bool:
+        """Collective: every replica's parameter hash must match (the fused exchange keeps replicas
+        bitwise identical). On a mismatch the trainer leaves the fused exchange for the RCCL
+        all-reduce for good, re-syncs every replica to rank 0's parameters and records
+        ``info.p2p_verify = "failed:param-hash"``. True if they agreed."""
+        from mlapi_amd.parallel.p2p import replicas_agree
+
+        if replicas_agree(self.params, self.info):
+            return True
+        import logging
+
+        from mlapi_amd.parallel.comm import broadcast_
+
+        logging.getLogger("mlapi_amd.train").warning(
+            "DP replicas diverged at step %d (parameter hashes differ): fused exchange off, replicas re-synced "
+            "from rank 0", self.steps)
+        self._dp = None
+        self.info.__dict__["p2p_verify"] = "failed:param-hash"
+        broadcast_(self.params, self.info, 0)
+        if self.mom is not None:
+            broadcast_(self.mom, self.info, 0)
+        return False
+
     def capture(self, X: torch.Tensor, y: torch.Tensor) -> None:
         """Capture the one-replica step for (X, y) in a HIP graph; later ``step(X, y)`` calls with
         these exact tensors replay it (one host call for the whole step - small batches are
@@ -149,6 +175,8 @@ class BinarySGDTrainer:
             self._dp.check_now()  # a missed exchange stops the loop (no silent divergence)
             self.steps += 1
             self._n_seen = B * self.info.world
+            if self.verify_every > 0 and self.steps % self.verify_every == 0:
+                self.verify_replicas()
             return
         if self.on_gpu and self.info.world == 1:
             g = getattr(self, "_graph", None)

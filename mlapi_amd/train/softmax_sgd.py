@@ -82,8 +82,11 @@ class SoftmaxSGDTrainer:
             from mlapi_amd.parallel.p2p import dp_exchange
 
             # gradient slice + stats, then (two-shot exchange) the published [grad | params | momenta]
-            self._dp = dp_exchange(self.info, (4 * n + 16) * 4)
+            self._dp = dp_exchange(self.info, (4 * n + 16) * 4, width=n)
         self.dp_timeout_ms = 60_000
+        from mlapi_amd.parallel.p2p import verify_every
+
+        self.verify_every = verify_every()  # fused steps between replica checks (MLAPI_DP_VERIFY_EVERY)
         self.steps = 0
         self._n_seen = 0
 
@@ -130,6 +133,30 @@ class SoftmaxSGDTrainer:
         """Raise if a fused DP exchange timed out waiting for a peer (synchronises the device)."""
         if self._dp is not None:
             self._dp.check()
+
+    def verify_replicas(self) -> bool:
+        """Collective: every replica's parameter hash must match (the fused exchange keeps replicas
+        bitwise identical). On a mismatch the trainer leaves the fused exchange for the RCCL
+        all-reduce for good, re-syncs every replica to rank 0's parameters (and its bf16 / f32
+        shadows) and records ``info.p2p_verify = "failed:param-hash"``. True if they agreed."""
+        from mlapi_amd.parallel.p2p import replicas_agree
+
+        if replicas_agree(self.params, self.info):
+            return True
+        import logging
+
+        from mlapi_amd.parallel.comm import broadcast_
+
+        logging.getLogger("mlapi_amd.train").warning(
+            "DP replicas diverged at step %d (parameter hashes differ): fused exchange off, replicas re-synced "
+            "from rank 0", self.steps)
+        self._dp = None
+        self.info.__dict__["p2p_verify"] = "failed:param-hash"
+        broadcast_(self.params, self.info, 0)
+        if self.mom is not None:
+            broadcast_(self.mom, self.info, 0)
+        self._refresh_shadow()
+        return False
 
     def _local_grad(self, Xa: torch.Tensor, y: torch.Tensor, fused_update_n: int = 0, dp=None) -> None:
         """Gradient sums into self.grad; with ``fused_update_n`` the SGD update for that global
@@ -178,6 +205,8 @@ class SoftmaxSGDTrainer:
             self._local_grad(Xa, y, fused_update_n=Xa.shape[0] * self.info.world, dp=self._dp)
             if self._dp is not None:
                 self._dp.check_now()  # a missed exchange stops the loop (no silent divergence)
+                if self.verify_every > 0 and (self.steps + 1) % self.verify_every == 0:
+                    self.verify_replicas()
         else:
             self._local_grad(Xa, y)
             all_reduce_sum_(self.grad, self.info)

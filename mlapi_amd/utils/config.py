@@ -66,6 +66,7 @@ class Config:
     resident_depth: int = 2                   # host-memory polls in flight per resident wave (1, 2, 4)
     io_ring_spin_us: int = 5                  # IO threads with rows on the resident kernel watch their records this
                                               # long in user space between epoll_wait(0) calls
+    io_ring_sleep_us: int = 0                 # > 0: ... sleep that long in epoll_pwait2 instead of spinning (A/B)
     direct_dispatch: bool = True              # GPU: ... written as AQL packets into the engine's own HSA queue
     direct_wide: bool = True                  # GPU: class-split / record GEMV batches into that queue too ...
     direct_wide_max_weight_bytes: int = 256 << 10  # ... for models with at most this many bytes of W

@@ -142,6 +142,47 @@ def test_p2p_selftest_failure_falls_back(tmp_path):
     for r in range(2):
         res = json.loads((tmp_path / f"selftest_{r}.json").read_text())
         assert res["p2p_selftest"] == "failed" and res["dp_exchange"] == "rccl", res
+        assert res["p2p_verify"] == "failed:ipc-pattern", res
+    assert np.array_equal(np.load(tmp_path / "st_params_0.npy"), np.load(tmp_path / "st_params_1.npy"))
+
+
+def test_p2p_verify_passes_on_a_healthy_exchange(tmp_path):
+    """the fused exchange kernel itself, on a rank-tagged synthetic gradient, is
+    bitwise equal to the exact sum before the first step; the job keeps the fused exchange."""
+    import numpy as np
+
+    _torchrun(2, "p2p_selftest.py", tmp_path, env={"MLAPI_DP_VERIFY_EVERY": "2"})
+    for r in range(2):
+        res = json.loads((tmp_path / f"selftest_{r}.json").read_text())
+        assert res["p2p_verify"] == "ok" and res["dp_exchange"] == "fused-p2p", res
+    assert np.array_equal(np.load(tmp_path / "st_params_0.npy"), np.load(tmp_path / "st_params_1.npy"))
+
+
+def test_p2p_verify_stale_flag_falls_back(tmp_path):
+    """A rank that skips one block's flag publish in the verification launch (a stale flag for its
+    peer, MLAPI_P2P_VERIFY_FAULT): the peer's bounded wait times out, the verdict (max over ranks)
+    is 'failed:fused-timeout' on every rank and the job trains on the unfused all-reduce path,
+    replicas bitwise identical."""
+    import numpy as np
+
+    _torchrun(2, "p2p_selftest.py", tmp_path, env={"MLAPI_P2P_VERIFY_FAULT": "1", "MLAPI_P2P_VERIFY_TIMEOUT_MS": "500"})
+    for r in range(2):
+        res = json.loads((tmp_path / f"selftest_{r}.json").read_text())
+        assert res["p2p_verify"] == "failed:fused-timeout" and res["dp_exchange"] == "rccl", res
+    assert np.array_equal(np.load(tmp_path / "st_params_0.npy"), np.load(tmp_path / "st_params_1.npy"))
+
+
+def test_p2p_periodic_replica_check_resyncs(tmp_path):
+    """A replica that diverges mid-run (rank 1's parameters nudged after step 3) is caught by the
+    replica-hash check at step 4 (MLAPI_DP_VERIFY_EVERY=2): fused exchange off, every replica re-synced
+    to rank 0's parameters, training continues bitwise identical."""
+    import numpy as np
+
+    _torchrun(2, "p2p_selftest.py", tmp_path, env={"MLAPI_DP_VERIFY_EVERY": "2", "CORRUPT_AT_STEP": "3"})
+    for r in range(2):
+        res = json.loads((tmp_path / f"selftest_{r}.json").read_text())
+        assert res["dp_exchange_first"] == "fused-p2p", res
+        assert res["p2p_verify"] == "failed:param-hash" and res["dp_exchange"] == "rccl", res
     assert np.array_equal(np.load(tmp_path / "st_params_0.npy"), np.load(tmp_path / "st_params_1.npy"))
 
 

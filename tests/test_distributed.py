@@ -350,3 +350,10 @@ def test_launcher_restarts_a_crashed_replica(tmp_path, iris_pickle_bytes):
             p.kill()
             out, _ = p.communicate()
     assert "restart 1/1" in out, out[-3000:]
+
+
+def test_p2p_verify_cpu_twin(tmp_path):
+    """the CPU FakeComm twin of the fused-exchange verification (exact-sum check
+    of a rank-tagged synthetic gradient, corruption caught, replica hash + rank-0 re-sync)."""
+    run(2, str(ROOT / "tests" / "dist" / "p2p_verify_cpu.py"), {"OUT": str(tmp_path), "MLAPI_COMM": "fake"})
+    assert (tmp_path / "OK_0").exists() and (tmp_path / "OK_1").exists()

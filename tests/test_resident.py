@@ -50,10 +50,13 @@ def _serve(native, device, model, names, X, *, conns, threads, reqs_per_conn, rt
 
 
 @pytest.mark.parametrize("device", DEVICES)
-def test_resident_concurrent_bodies_exact(native, device):
+@pytest.mark.parametrize("sleep_us", [0, 3], ids=["spin", "sleep"])
+def test_resident_concurrent_bodies_exact(native, device, sleep_us):
+    """48 connections over 4 IO threads; the IO threads watch their records by spinning
+    (io_ring_spin_us) or by sleeping in epoll_pwait2 (io_ring_sleep_us)."""
     m = LinearModel.random(4, 3, seed=11, labels=LABELS)
     X = np.round(np.random.default_rng(3).standard_normal((512, 4)) * 2 + 4, 1)
-    res, d, s1 = _serve(native, device, m, IRIS, X, conns=48, threads=3, reqs_per_conn=200)
+    res, d, s1 = _serve(native, device, m, IRIS, X, conns=48, threads=3, reqs_per_conn=200, io_ring_sleep_us=sleep_us)
     n = 48 * 200
     assert res["failed"] == 0 and res["errors"] == 0 and res["body_mismatches"] == 0, res
     assert res["status_counts"] == {200: n}

@@ -72,6 +72,7 @@ for s in $steps; do
         for m in on off; do
           MLAPI_RESIDENT=$m run "serve_res${m}_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
         done
+        MLAPI_IO_RING_SLEEP_US=3 run "serve_ressleep_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
       done ;;
     serve_wide)
       for dt in f32 bf16; do
