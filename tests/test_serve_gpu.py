@@ -87,6 +87,8 @@ def test_native_server_gpu_end_to_end(iris_cwd, native):
         stats = srv.runtime.handle.stats()
         assert stats["requests"] >= 6400
         assert stats["batches"] < stats["requests"], "concurrent requests must be coalesced into batches"
+        # the Iris model is served by the resident kernel by default: rows, not launched batches
+        assert stats["resident_live"] and stats["resident_rows"] >= 6000, stats
 
 
 # ---- small-model launch modes: kernel-argument batches vs zero-copy pinned rows ------------------
