@@ -499,7 +499,7 @@ def _self_launch(args, argv) -> int:
 
     # ranks on their GPU's NUMA node by default (a node mask, no core slices: core pinning lost at
     # N = 1, profiles/r2_pin/); --pin on = disjoint core slices, off = unpinned
-    largv = ["--nproc", str(args.gpus), "--pin", {"auto": "numa", "on": "cores", "off": "off"}[args.pin]]
+    largv = ["--nproc", str(args.gpus), "--pin", {"auto": "numa", "numa": "numa", "on": "cores", "off": "off"}[args.pin]]
     return launch.main(largv + [os.path.abspath(__file__)] + list(argv))
 
 
@@ -539,12 +539,13 @@ def main(argv=None) -> int:
     ap.add_argument("--softmax-batch", type=int, default=1 << 16)
     ap.add_argument("--softmax-features", type=int, default=256, help="train_softmax: F (any: <= 512 the fused G/dW kernel, wider the 3-launch wide path)")
     ap.add_argument("--cpu", action="store_true", help="force the CPU backend (testing without a GPU)")
-    ap.add_argument("--pin", default="auto", choices=["auto", "on", "off"],
+    ap.add_argument("--pin", default="auto", choices=["auto", "on", "off", "numa"],
                     help="on: pin this rank to its share of physical cores on its GPU's NUMA node, server "
                          "and load generator on disjoint cores (measured interleaved on one box, core "
                          "pinning cost c=64 throughput at N=1 (0.65-0.80 M vs 0.98-1.06 M req/s) and N=2 "
-                         "(0.83-0.85 M vs 0.92-1.02 M), profiles/r2_pin/); auto: N = 1 unpinned, N > 1 "
-                         "self-launched ranks on their GPU's NUMA node (node mask, mlapi_amd.launch); off")
+                         "(0.83-0.85 M vs 0.92-1.02 M), profiles/r2_pin/); numa: this rank and its load "
+                         "generator on the GPU's NUMA node (a node mask); auto: numa (N = 1 here, N > 1 "
+                         "through mlapi_amd.launch); off: unpinned")
     args = ap.parse_args(argv)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -577,6 +578,20 @@ def main(argv=None) -> int:
         return 2
     local = int(os.environ.get("LOCAL_WORLD_SIZE", info.world))
     pinned = []
+    if args.pin == "auto" and info.world == 1 and info.device is not None:
+        args.pin = "numa"  # measured: numa 1.51-1.54 M vs unpinned 1.35-1.53 M req/s (profiles/r5_serve/)
+    if args.pin == "numa" and os.environ.get("MLAPI_PLACEMENT") != "numa":
+        # this rank and its load generator on the GPU's NUMA node (a node mask, not core slices):
+        # loopback TCP, the pinned request rings and the GPU's host link stay on one socket
+        from mlapi_amd.utils.affinity import gpu_numa_nodes, numa_rank_cpus
+
+        dev_index = info.local_rank if info.device is None else info.device.index
+        mask = numa_rank_cpus(dev_index, gpu_numa_nodes())
+        if mask:
+            os.sched_setaffinity(0, mask)
+            if getattr(args, "lg_proc", None) is not None:
+                args.lg_proc.pin(mask)
+            os.environ["MLAPI_PLACEMENT"] = "numa"
     if args.pin == "on":
         # before any native thread starts: the server / batcher / load-generator threads inherit it
         from mlapi_amd.utils.affinity import pin_this_rank
@@ -591,11 +606,14 @@ def main(argv=None) -> int:
         from mlapi_amd.utils.threads import effective_cpus
 
         per_rank = max(4, len(pinned) if pinned else effective_cpus() // max(1, local))
-        # measured on a 16-CPU share with the out-of-process load generator (profiles/r2_serve_threads/
-        # sweep_io*): io=10/client=4 -> 0.99-1.11 M req/s; 9/5 0.89-0.93 M; 8/6 0.75-0.94 M;
-        # 7/6 0.52-0.79 M; 11/3 0.66-0.83 M (two interleaved rounds)
+        # measured on a 16-CPU share with the out-of-process load generator. Resident SMALL path
+        # (round 5, profiles/r5_serve/): io=8/client=4 -> 1.51-1.54 M req/s at 4.8-4.9 us of server
+        # CPU per request; io=10/4 -> 0.97 M (10 spinning IO threads); io=6/4 -> 0.96-1.09 M. The
+        # batcher path (resident off) had io=10/4 best (profiles/r2_serve_threads/: 0.99-1.11 M;
+        # 9/5 0.89-0.93 M; 8/6 0.75-0.94 M)
         cl = max(2, min(6, per_rank // 4))
-        io = max(2, min(12, per_rank - cl - 2))
+        resident = os.environ.get("MLAPI_RESIDENT", "auto").lower() != "off" and info.device is not None
+        io = max(2, min(12, per_rank // 2 if resident else per_rank - cl - 2))
         args.io_threads = args.io_threads if args.io_threads > 0 else io
         args.client_threads = args.client_threads if args.client_threads > 0 else cl
     if pinned and getattr(args, "lg_proc", None) is not None and len(pinned) > args.io_threads + 3:

@@ -178,7 +178,10 @@ LoadgenResult Loadgen::run(int64_t requests_per_conn, bool record) {
     char buf[65536];
     int64_t last_progress = mono_ns();
     while (live > 0 && !failed.load()) {
-      const int n = epoll_wait(ep, evs, 256, 1000);
+      // spin_us: poll (timeout 0) for this long after the last response before sleeping in
+      // epoll_wait - a closed-loop client whose responses arrive every few us then never pays a
+      // sleep / wake-up per response (and the server's send() never has to wake it)
+      const int n = epoll_wait(ep, evs, 256, spin_ns_ > 0 && mono_ns() - last_progress < spin_ns_ ? 0 : 1000);
       if (n > 0) last_progress = mono_ns();
       if (n == 0 && mono_ns() - last_progress > (int64_t)timeout_s_ * 1000000000LL) {
         failed.store(2);  // no progress for timeout_s: give up

@@ -1,4 +1,5 @@
 #pragma once
+#include <cstdlib>
 #include <atomic>
 #include <cstdint>
 #include <memory>
@@ -42,6 +43,12 @@ class Loadgen {
   std::vector<std::string> expected_;
   double rel_tol_ = 0.0;
   double timeout_s_ = 30.0;
+  // MLAPI_LOADGEN_SPIN_US (default 0): each thread polls its sockets this long after its last
+  // response before it sleeps in epoll_wait (no sleep / wake-up per response in a closed loop)
+  int64_t spin_ns_ = [] {
+    const char* e = std::getenv("MLAPI_LOADGEN_SPIN_US");
+    return e ? (int64_t)std::atoll(e) * 1000 : (int64_t)0;
+  }();
   int threads_;
   std::vector<std::unique_ptr<LgConn>> conns_;
 };

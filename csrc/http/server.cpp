@@ -405,6 +405,7 @@ class IoThread : public Sink {
     const int64_t ring_sleep_ns = (int64_t)srv_->config().io_ring_sleep_us * 1000;
     if (ring_sleep_ns > 0) prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // us-scale epoll_pwait2 timeouts
     bool ring_sleep = false;  // this pass waits for the ring's records in epoll_pwait2
+    bool ring_spun = false;   // spun since the last epoll_wait: poll the sockets before spinning again
     int64_t last_active = 0;
     int last_n = 0;  // events of the previous epoll_wait
     ring_ = srv_->engine() != nullptr ? srv_->engine()->open_ring() : nullptr;
@@ -442,7 +443,10 @@ class IoThread : public Sink {
           // io_ring_sleep_us: sleep in the kernel for that long instead (a socket event still
           // wakes the thread at once); costs a context switch, saves the spin's CPU
           ring_sleep = true;
-        } else if (last_n == 0 && ring_spin_ns > 0 && !pending_.load(std::memory_order_relaxed)) {
+        } else if (last_n == 0 && !ring_spun && ring_spin_ns > 0 && !pending_.load(std::memory_order_relaxed)) {
+          // one spin per epoll_wait: a steady trickle of landing records must not keep this thread
+          // from reading its other connections' requests
+          ring_spun = true;
           Stage sg(this, SS_IDLE_GPU);
           if (ring_->wait_any(ring_spin_ns)) continue;  // harvest first
         }
@@ -471,6 +475,7 @@ class IoThread : public Sink {
       } else {
         n = epoll_wait(epfd_, evs, 256, timeout);
       }
+      ring_spun = false;
       blocked_.store(false);
       last_n = n;
       const bool spin_enabled = always_spin_ns > 0 || lowload_spin_ns > 0;

@@ -1313,6 +1313,13 @@ bool ServeRing::landed(uint32_t pos) const {
 
 bool ServeRing::submit(const double* X, int n, int nf, const uint64_t* tags) {
   Engine& e = *eng_;
+  // measurement: MLAPI_RESIDENT_SHADOW=1 keeps the resident kernel polling while every row takes the
+  // engine queue (the polling's cost to the host, isolated from the path itself)
+  static const bool shadow = [] {
+    const char* v = getenv("MLAPI_RESIDENT_SHADOW");
+    return v != nullptr && atoi(v) != 0;
+  }();
+  if (shadow) return false;
   if (n <= 0 || n > RESIDENT_RING / 2 || next_ - tail_ + (uint32_t)n > (uint32_t)RESIDENT_RING) return false;
   if (!e.res_live_.load(std::memory_order_acquire) || idx_ >= e.res_nrings_.load(std::memory_order_acquire)) return false;
   if (e.drop_.load(std::memory_order_relaxed) || e.cfg_.fail_every > 0 || e.cfg_.delay_us > 0) return false;

@@ -66,6 +66,7 @@ class EngineHandle:
         res = str(config.resident).strip().lower()
         ec.resident = 1 if res == "on" or (res == "auto" and self.device is not None) else 0
         ec.resident_depth = int(config.resident_depth)
+        ec.resident_idle_polls = int(config.resident_idle_polls)
         ec.f32_gemv = bool(config.f32_gemv)
         ec.wide_host_merge_blocks = int(config.wide_host_merge_blocks)
         ec.completers = int(config.completers)

@@ -64,6 +64,7 @@ class Config:
                                               # resident waves poll): auto (on for a GPU) | on (CPU backend: a host
                                               # thread plays the kernel, tests) | off (every row via the batcher)
     resident_depth: int = 2                   # host-memory polls in flight per resident wave (1, 2, 4)
+    resident_idle_polls: int = 20000          # polls without a row before a resident wave slows its polling
     io_ring_spin_us: int = 5                  # IO threads with rows on the resident kernel watch their records this
                                               # long in user space between epoll_wait(0) calls
     io_ring_sleep_us: int = 0                 # > 0: ... sleep that long in epoll_pwait2 instead of spinning (A/B)

@@ -67,12 +67,45 @@ for s in $steps; do
     smoke) run smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     serve) run bench_serve 300 python -u bench.py --steps 200 --warmup 20 ;;
     resident) run pytest_resident 400 python -u -m pytest tests/test_resident.py -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    serve_resv)  # resident-path variants, interleaved x RES_ROUNDS: off, spin 5 / 2 us, 1 poll in flight, sleep 3 us
+      for r in $(seq 1 "${RES_ROUNDS:-2}"); do
+        MLAPI_RESIDENT=off run "resv_off_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+        run "resv_spin5_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+        MLAPI_IO_RING_SPIN_US=2 run "resv_spin2_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+        MLAPI_RESIDENT_DEPTH=1 run "resv_d1_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+        MLAPI_IO_RING_SLEEP_US=3 run "resv_sleep3_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      done ;;
+    serve_resx)  # resident-path experiments: polling cost with rows on the queue (shadow), IO / loadgen splits
+      for r in $(seq 1 "${RES_ROUNDS:-2}"); do
+        MLAPI_RESIDENT=off run "resx_off_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+        MLAPI_RESIDENT_SHADOW=1 MLAPI_RESIDENT_IDLE_POLLS=1000000000 run "resx_shadow_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+        run "resx_on_io6_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads 6 --client-threads 4
+        run "resx_on_io8_lg6_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads 8 --client-threads 6
+        run "resx_on_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      done ;;
+    serve_lgspin)  # load-generator spin (MLAPI_LOADGEN_SPIN_US) x resident path x IO threads, interleaved
+      for r in $(seq 1 "${RES_ROUNDS:-2}"); do
+        MLAPI_RESIDENT=off run "lgs_off_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+        MLAPI_RESIDENT=off MLAPI_LOADGEN_SPIN_US=50 run "lgs_off_spin_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+        run "lgs_on_io6_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads 6 --client-threads 4
+        MLAPI_LOADGEN_SPIN_US=50 run "lgs_on_io6_spin_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads 6 --client-threads 4
+        MLAPI_LOADGEN_SPIN_US=50 run "lgs_on_io8_spin_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads 8 --client-threads 4
+        MLAPI_LOADGEN_SPIN_US=50 run "lgs_on_io10_spin_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      done ;;
+    serve_numa)  # NUMA-node placement of the rank + load generator (--pin numa) x resident path, interleaved
+      for r in $(seq 1 "${RES_ROUNDS:-2}"); do
+        MLAPI_RESIDENT=off run "numa_off_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --pin numa
+        run "numa_on_io8_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --pin numa --io-threads 8 --client-threads 4
+        MLAPI_LOADGEN_SPIN_US=50 run "numa_on_io8_spin_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --pin numa --io-threads 8 --client-threads 4
+        run "numa_on_io10_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --pin numa
+        run "nonuma_on_io8_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads 8 --client-threads 4
+        MLAPI_RESIDENT=off run "nonuma_off_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
+      done ;;
     serve_res)  # the driver's exact command with the resident kernel on / off, interleaved
       for r in $(seq 1 "${RES_ROUNDS:-3}"); do
         for m in on off; do
           MLAPI_RESIDENT=$m run "serve_res${m}_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
         done
-        MLAPI_IO_RING_SLEEP_US=3 run "serve_ressleep_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
       done ;;
     serve_wide)
       for dt in f32 bf16; do
