@@ -292,8 +292,11 @@ def test_idle_engine_fast_path(native, F, K, kind):
     bodies = [json.dumps(dict(zip(names, map(float, row))), separators=(",", ":")).encode() for row in X]
     out = {}
     for rows in (8, 0):
+        # resident off: SMALL models (F = 4) would otherwise take the resident kernel's rings
+        # (tests/test_resident.py), never the idle path this test is about
         cfg = Config.from_env(port=0, device="cuda:0", feature_names=names, reload="off", missing_model="keep",
-                              model_path="/nonexistent/idle.pkl", io_threads=2, idle_inline_rows=rows)
+                              model_path="/nonexistent/idle.pkl", io_threads=2, idle_inline_rows=rows,
+                              resident="off")
         srv = NativeServer(cfg)
         srv.runtime.handle.load(m)
         srv.start()
