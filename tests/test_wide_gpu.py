@@ -234,3 +234,67 @@ def test_linear_wide_graph_replay(B):
         g.replay()
         torch.cuda.synchronize()
         _oracle_check(m, Xn, out[0].cpu().numpy(), out[1].cpu().numpy())
+
+
+def test_wide_overlapping_launches_with_concurrent_training(native):
+    """the WIDE class merge waits for its row group's class blocks, which the
+    dispatcher placed before the merging block. Here several WIDE batches are in flight at once
+    (slot-private workspaces: unordered packets that overlap on the GPU) while a 1000-class training
+    step loop keeps the CUs busy from another thread - the case where block residency is not a
+    given. Every one of the served bodies must still be the engine's own f64 answer (checked against
+    the fp64 oracle first), with no merge timeout (500)."""
+    import threading
+
+    from mlapi_amd.serve.loadgen import make_workload
+    from mlapi_amd.serve.server import NativeServer
+    from mlapi_amd.train.softmax_sgd import SoftmaxSGDTrainer, synthetic_multiclass
+    from mlapi_amd.utils.config import Config
+
+    F, K = 256, 1000
+    names = [f"f{i}" for i in range(F)]
+    m = LinearModel.random(F, K, seed=77, kind=Kind.MULTINOMIAL, labels=[f"c{i}" for i in range(K)])
+    X = np.round(np.random.default_rng(78).standard_normal((256, F)), 3)
+    stop = threading.Event()
+    steps = [0]
+    errors = []
+
+    def train():
+        try:
+            dev = torch.device("cuda:0")
+            tr = SoftmaxSGDTrainer(256, 1000, lr=0.1, device=dev)
+            Xt, yt = synthetic_multiclass(16384, 256, 1000, seed=5)
+            Xa, yt = tr.prepare(Xt.to(dev)), yt.to(dev)
+            s = torch.cuda.Stream(dev)
+            with torch.cuda.stream(s):
+                while not stop.is_set():
+                    tr.step(Xa, yt)
+                    steps[0] += 1
+                    if steps[0] % 8 == 0:
+                        s.synchronize()
+            s.synchronize()
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    cfg = Config.from_env(port=0, device="cuda:0", feature_names=names, reload="off", missing_model="keep",
+                          model_path="/nonexistent/overlap.pkl", io_threads=4, wide_dtype="f64", slots=4)
+    with NativeServer(cfg) as srv:
+        srv.runtime.handle.load(m)
+        reqs, exp = make_workload(srv.runtime.handle.engine, m, names, X, rtol_oracle=1e-12, label_margin=1e-9)
+        th = threading.Thread(target=train)
+        th.start()
+        try:
+            lg = native.Loadgen("127.0.0.1", srv.port, reqs[0].decode(), 48, 3)
+            lg.set_workload([r.decode() for r in reqs], [e.decode() for e in exp], 0.0)
+            s0 = srv.runtime.handle.stats()
+            res = lg.run(60, True)
+            lg.close()
+            s1 = srv.runtime.handle.stats()
+        finally:
+            stop.set()
+            th.join()
+    assert not errors, errors
+    assert steps[0] > 0, "the training loop never ran alongside the serving batches"
+    assert res["failed"] == 0 and res["body_mismatches"] == 0 and res["status_counts"] == {200: 48 * 60}, res
+    nb = s1["batches"] - s0["batches"]
+    assert s1["path_batches"]["wide"] - s0["path_batches"]["wide"] == nb and nb < 48 * 60  # coalesced, WIDE
+    assert s1["errors"] == s0["errors"]
