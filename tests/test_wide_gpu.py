@@ -283,18 +283,25 @@ def test_wide_overlapping_launches_with_concurrent_training(native):
         th = threading.Thread(target=train)
         th.start()
         try:
+            import time
+
+            t_end = time.time() + 60
+            while steps[0] < 2 and not errors and time.time() < t_end:  # training is under way
+                time.sleep(0.01)
             lg = native.Loadgen("127.0.0.1", srv.port, reqs[0].decode(), 48, 3)
             lg.set_workload([r.decode() for r in reqs], [e.decode() for e in exp], 0.0)
             s0 = srv.runtime.handle.stats()
-            res = lg.run(60, True)
+            st0 = steps[0]
+            res = lg.run(400, True)
+            st1 = steps[0]
             lg.close()
             s1 = srv.runtime.handle.stats()
         finally:
             stop.set()
             th.join()
     assert not errors, errors
-    assert steps[0] > 0, "the training loop never ran alongside the serving batches"
-    assert res["failed"] == 0 and res["body_mismatches"] == 0 and res["status_counts"] == {200: 48 * 60}, res
+    assert st1 > st0, "the training loop did not run alongside the serving batches"
+    assert res["failed"] == 0 and res["body_mismatches"] == 0 and res["status_counts"] == {200: 48 * 400}, res
     nb = s1["batches"] - s0["batches"]
-    assert s1["path_batches"]["wide"] - s0["path_batches"]["wide"] == nb and nb < 48 * 60  # coalesced, WIDE
+    assert s1["path_batches"]["wide"] - s0["path_batches"]["wide"] == nb and nb < 48 * 400  # coalesced, WIDE
     assert s1["errors"] == s0["errors"]
