@@ -612,7 +612,10 @@ def main(argv=None) -> int:
         # batcher path (resident off) had io=10/4 best (profiles/r2_serve_threads/: 0.99-1.11 M;
         # 9/5 0.89-0.93 M; 8/6 0.75-0.94 M)
         cl = max(2, min(6, per_rank // 4))
-        resident = os.environ.get("MLAPI_RESIDENT", "auto").lower() != "off" and info.device is not None
+        # the resident kernel serves the headline's SMALL (Iris) model; serve_wide's F = 256 models
+        # take the batcher path
+        resident = (args.mode == "serve" and os.environ.get("MLAPI_RESIDENT", "auto").lower() != "off"
+                    and info.device is not None)
         io = max(2, min(12, per_rank // 2 if resident else per_rank - cl - 2))
         args.io_threads = args.io_threads if args.io_threads > 0 else io
         args.client_threads = args.client_threads if args.client_threads > 0 else cl

@@ -220,6 +220,8 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("dt"), py::arg("F"), py::arg("K"));
   m.def("linear_wide_set_probe", &linear_wide_set_probe, py::arg("probe"));
+  m.def("linear_wide_set_trace", [](uintptr_t p) { linear_wide_set_trace(reinterpret_cast<void*>(p)); },
+        py::arg("data_ptr"));
   m.def("linear_wide_workspace", &linear_wide_workspace, py::arg("B"), py::arg("dt"), py::arg("F"), py::arg("K"));
   m.def(
       "linear_wide",

@@ -223,6 +223,9 @@ struct WidePlan {
 WidePlan linear_wide_plan(int dt, int F, int K);
 // measurement hook: later launches stop early (1: after the MFMA loop, 2: before the class merge)
 void linear_wide_set_probe(int probe);
+// measurement: per-block wall-clock timeline of the wide kernel (8 x u64 per block, device memory;
+// nullptr = off)
+void linear_wide_set_trace(void* trace);
 // workspace (zeroed once; tickets are re-armed in-kernel) for up to B rows
 size_t linear_wide_workspace(int64_t B, int dt, int F, int K);
 // Host class merge (serving, multiclass, B <= 32): block cb writes for row r two 16-byte units at

@@ -14,16 +14,21 @@
 //    feature offset 4*E*step + (l >> 4)*E, and element e of its load is the MFMA's k = l >> 4
 //    for the e-th MFMA of the step - the same k permutation for A (W) and B (X);
 //  * loads in chunks of U = 4 steps, two chunks in flight (double buffer);
-//  * the 4 waves' tiles are summed through LDS in fixed order; feature splits (nfs > 1) are summed
-//    by the last-arriving block of the class block (write-through partials, one ticket, and
-//    agent-coherent sc1 loads of them - or one agent-scope acquire: Guideline 16), in split order;
-//  * epilogue per row: bias, then the sklearn epilogue of `kind` (K = 1 binary kinds: z > 0 and
-//    sigma(|z|) / the two-class softmax, exactly as linear_rows.h); multiclass kinds reduce the
-//    block's 16 classes to a row state {max, sum exp(z - max) | sum sigmoid(z), first argmax} and
-//    class blocks are merged either on the host (one 32-byte record per block and row, the
-//    engine's completer merges in double in block order) or in-kernel by the last-arriving block
-//    of the row group (ticket + sc1 loads), 8 lanes per row: max by compares first, then every
-//    block's rescaled sum in parallel and a fixed-order sum tree. Everything in f64.
+//  * the 4 waves' tiles meet in LDS; feature splits (nfs > 1) are summed by the last-arriving
+//    block of the class block (write-through partials, one ticket, agent-coherent sc1 loads of
+//    them: Guideline 16), in split order;
+//  * epilogue on every wave (the serving batch is latency bound, and one wave running it alone
+//    measured ~1.5 us of issue for the block's states and ~2.3 us for the class merge - the
+//    per-block timeline of tools/wide_trace.py): wave w takes 4 rows of each tile, one row per
+//    16-lane DPP row and one class per lane, so a row's max / first argmax / sum are 4-step DPP
+//    all-reductions and every lane evaluates one exponential. Then bias and the sklearn epilogue
+//    of `kind` (K = 1 binary kinds: z > 0 and sigma(|z|) / the two-class softmax, exactly as
+//    linear_rows.h); multiclass kinds reduce the block's 16 classes to a row state {max,
+//    sum exp(z - max) | sum sigmoid(z), first argmax}, and class blocks are merged either on the
+//    host (one 32-byte record per block and row, the engine's completer merges in double) or
+//    in-kernel by the row group's highest class blocks: one wave per 4 rows, lane cl of a row
+//    taking class blocks cl, cl + 16, ... (sc1 polls of tagged granules), the same DPP
+//    reductions, every block's rescaled sum in parallel. Everything in f64, fixed orders.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -68,7 +73,17 @@ struct WideArgs {
   int32_t probe;  // linear_wide_set_probe: measurement 1 = stop after the MFMA loop, 2 = after the
                   // block's row states (before the class merge); fault injection 3 = the merging
                   // block never sees the states (its rows time out after 1 s)
+  uint64_t* trace;  // linear_wide_set_trace (measurement, nullptr in production): per block 8 wall-clock
+                    // stamps (100 MHz) at entry, MFMA loop done, states published, merge poll begin /
+                    // end, rows written
 };
+
+// measurement timeline: lane 0 of the calling wave stamps slot i of its block (vector stores)
+__device__ __forceinline__ void wstamp(const WideArgs& a, int i) {
+  if (a.trace != nullptr && (threadIdx.x & 63) == 0)
+    a.trace[((int64_t)blockIdx.y * (a.ncb * a.nfs) + blockIdx.x) * 8 + i] = wall_clock64();  // no gridDim: the
+  // direct-dispatched entries read no implicit argument (direct_dispatch.cpp launch_kernel)
+}
 
 template <typename T>
 __device__ __forceinline__ double elem(const uint4& v, int e) {
@@ -84,23 +99,37 @@ struct WState {
   int bi;
 };
 
-__device__ __forceinline__ WState wmerge(WState a, WState b, bool ovr) {
-  const bool take_b = (b.m > a.m) || (b.m == a.m && b.bi < a.bi);
-  WState r;
-  r.m = take_b ? b.m : a.m;
-  r.bi = take_b ? b.bi : a.bi;
-  if (ovr) {
-    r.s = a.s + b.s;
-  } else {
-    const double sa = a.m == -INFINITY ? 0.0 : a.s * exp(a.m - r.m);
-    const double sb = b.m == -INFINITY ? 0.0 : b.s * exp(b.m - r.m);
-    r.s = sa + sb;
-  }
-  return r;
+// all-reductions over the 16 lanes of a DPP row (xor 1 and xor 2 in the quad, then rotations by 4
+// and 8 within the row): VALU data movement, no LDS round trip; every lane of the row ends with the
+// row's result, in a fixed order per lane (deterministic). Call with the whole wave active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
 }
-
-__device__ __forceinline__ WState wshfl(WState a, int off) {
-  return WState{__shfl_xor(a.m, off, 64), __shfl_xor(a.s, off, 64), __shfl_xor(a.bi, off, 64)};
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint64_t lo = dpp_u32<CTRL>((uint32_t)u), hi = dpp_u32<CTRL>((uint32_t)(u >> 32));
+  return __builtin_bit_cast(double, lo | (hi << 32));
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_ROR4 = 0x124, DPP_ROR8 = 0x128;
+__device__ __forceinline__ double row16_max(double v) {  // fmax: a NaN lane is skipped
+  v = fmax(v, dpp_f64<DPP_XOR1>(v));
+  v = fmax(v, dpp_f64<DPP_XOR2>(v));
+  v = fmax(v, dpp_f64<DPP_ROR4>(v));
+  return fmax(v, dpp_f64<DPP_ROR8>(v));
+}
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_f64<DPP_XOR1>(v);
+  v += dpp_f64<DPP_XOR2>(v);
+  v += dpp_f64<DPP_ROR4>(v);
+  return v + dpp_f64<DPP_ROR8>(v);
+}
+__device__ __forceinline__ int row16_min(int v) {
+  v = min(v, (int)dpp_u32<DPP_XOR1>((uint32_t)v));
+  v = min(v, (int)dpp_u32<DPP_XOR2>((uint32_t)v));
+  v = min(v, (int)dpp_u32<DPP_ROR4>((uint32_t)v));
+  return min(v, (int)dpp_u32<DPP_ROR8>((uint32_t)v));
 }
 
 typedef __attribute__((address_space(1))) unsigned int gu32_t;
@@ -142,13 +171,14 @@ template <typename T, int NB>
 __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   constexpr int E = 16 / (int)sizeof(T);  // features per 16-byte load
   constexpr int STEP = 4 * E;             // features per wave step
-  __shared__ wd4_t red[WAVES][NB][64];
+  __shared__ double red[WAVES][NB][64][4];
   __shared__ int bcast;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r16 = lane & 15;
   const int cb = blockIdx.x % a.ncb, fs = blockIdx.x / a.ncb, rgi = blockIdx.y;
   const int c0 = cb * CB;
   const int64_t row0 = (int64_t)rgi * RG;
+  if (threadIdx.x < 64) wstamp(a, 0);
   const int S = a.fsteps;
   const int64_t f0 = ((int64_t)fs * WAVES + wave) * S * STEP + g * E;
   const T* wp = static_cast<const T*>(a.W) + (int64_t)min(c0 + r16, a.K - 1) * a.ldx + f0;
@@ -158,9 +188,7 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     xp[t] = static_cast<const T*>(a.X) + min(row0 + t * 16 + r16, (int64_t)a.B - 1) * a.ldx + f0;
 
   // the bias of this lane's classes, loaded now so its latency hides under the MFMA loop
-  double bz[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) bz[r] = a.bias[min(c0 + g + 4 * r, a.K - 1)];
+  const double bcl = a.bias[min(c0 + (lane & 15), a.K - 1)];
   wd4_t acc[NB];
 #pragma unroll
   for (int t = 0; t < NB; ++t) acc[t] = wd4_t{0.0, 0.0, 0.0, 0.0};
@@ -199,18 +227,16 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     mma(w1, x1, s0 + U);
   }
 
+  if (wave == 0) wstamp(a, 1);
   if (a.probe == 1) {  // measurement: keep the accumulators alive, store nothing
     if (acc[0][0] == 12345.678) a.out_p[0] = acc[0][1];
     return;
   }
-  // ---- the block's tile: the 4 waves' quarters, summed in wave order
+  // ---- the block's tile: the waves' feature quarters meet in LDS
 #pragma unroll
-  for (int t = 0; t < NB; ++t) red[wave][t][lane] = acc[t];
+  for (int t = 0; t < NB; ++t) *reinterpret_cast<wd4_t*>(&red[wave][t][lane][0]) = acc[t];
   __syncthreads();
-  if (wave == 0) {
-#pragma unroll
-    for (int t = 0; t < NB; ++t) acc[t] = ((red[0][t][lane] + red[1][t][lane]) + red[2][t][lane]) + red[3][t][lane];
-  }
+  int nred = WAVES;  // partial tiles to sum per element
   // ---- feature splits: the last-arriving block of (row group, class block) sums them in order
   if (a.nfs > 1) {
     unsigned char* rgw = a.ws + (int64_t)rgi * a.rg_bytes;
@@ -218,9 +244,12 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     if (wave == 0) {
 #pragma unroll
       for (int t = 0; t < NB; ++t) {
+        wd4_t v = *reinterpret_cast<const wd4_t*>(&red[0][t][lane][0]);
+#pragma unroll
+        for (int w2 = 1; w2 < WAVES; ++w2) v += *reinterpret_cast<const wd4_t*>(&red[w2][t][lane][0]);
         double* dst = part + (int64_t)fs * (2 * 4 * 64) + t * 256 + lane * 4;
-        st16_sc1(dst, __builtin_bit_cast(wu4_t, wd2_t{acc[t][0], acc[t][1]}));
-        st16_sc1(dst + 2, __builtin_bit_cast(wu4_t, wd2_t{acc[t][2], acc[t][3]}));
+        st16_sc1(dst, __builtin_bit_cast(wu4_t, wd2_t{v[0], v[1]}));
+        st16_sc1(dst + 2, __builtin_bit_cast(wu4_t, wd2_t{v[2], v[3]}));
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every partial acknowledged before the ticket
       if (lane == 0) {
@@ -235,154 +264,142 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     if (!bcast) return;  // uniform per block
     if (wave == 0) {  // only wave 0 (the adder) reads the partials
 #pragma unroll
-      for (int t = 0; t < NB; ++t) acc[t] = wd4_t{0.0, 0.0, 0.0, 0.0};
-      for (int f = 0; f < a.nfs; ++f) {  // split order: deterministic
-#pragma unroll
-        for (int t = 0; t < NB; ++t) {
+      for (int t = 0; t < NB; ++t) {
+        wd4_t v = wd4_t{0.0, 0.0, 0.0, 0.0};
+        for (int f = 0; f < a.nfs; ++f) {  // split order: deterministic
           const double* src = part + (int64_t)f * (2 * 4 * 64) + t * 256 + lane * 4;
-          wd4_t v;  // agent-coherent sc1 loads: no acquire fence (the partials bypass this CU's L1)
+          wd4_t u;  // agent-coherent sc1 loads: no acquire fence (the partials bypass this CU's L1)
 #pragma unroll
-          for (int k = 0; k < 4; ++k) v[k] = ld_sc1(src + k);
-          acc[t] += v;
+          for (int k = 0; k < 4; ++k) u[k] = ld_sc1(src + k);
+          v += u;
         }
+        *reinterpret_cast<wd4_t*>(&red[0][t][lane][0]) = v;
       }
     }
+    __syncthreads();
+    nred = 1;
   }
+  // ---- epilogue, every wave: wave w takes rows 4w .. 4w + 3 of each 16-row tile, one row per
+  // 16-lane DPP row (rs = lane >> 4), one class per lane (cl = lane & 15). The tile element of
+  // (class cl, row r) sits in lane r + 16 (cl & 3), component cl >> 2, of each wave's accumulator.
   const bool ovr = a.kind == KIND_OVR;
   const bool binary = a.kind == KIND_BINARY || a.kind == KIND_BINARY_SOFTMAX;
-  // the other waves are only needed for an in-kernel class merge (they join its barriers)
-  if (wave != 0 && (binary || a.ncb == 1 || a.hrec != nullptr || a.probe == 2 || cb != a.ncb - 1)) return;
-  // ---- epilogue (wave 0): lane holds classes c0 + g + 4r of row r16 of each tile. The row's
-  // block state {max, sum over the block's classes of exp(z - max) | sigmoid(z), first argmax}:
-  // the max (and argmax) first, by compares only, then the 16 exponentials in parallel against
-  // it and a fixed-order sum - no dependent chain of exponentials.
-  WState st[NB];
-  if (wave == 0) {
+  const int rs = lane >> 4, cl = lane & 15;
+  const int rows = (int)min<int64_t>((int64_t)a.B - row0, 16 * NB);  // rows of this row group in the launch
+  const bool cvalid = c0 + cl < a.K;
+  double z[NB];
+#pragma unroll
+  for (int t = 0; t < NB; ++t) {
+    const int src = 4 * wave + rs + 16 * (cl & 3);
+    double v = red[0][t][src][cl >> 2];
+#pragma unroll
+    for (int w2 = 1; w2 < WAVES; ++w2)
+      if (w2 < nred) v += red[w2][t][src][cl >> 2];
+    z[t] = cvalid ? v + bcl : -INFINITY;
+  }
+  if (binary) {  // K = 1: class 0 is the single logit (z > 0 and the sklearn probabilities, as linear_rows.h)
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-      const int64_t row = row0 + t * 16 + r16;
-      if (binary) {
-        if (g == 0 && row < a.B) {  // class 0 = the single logit
-          const double z = acc[t][0] + bz[0];
-          double pm;
-          if (a.kind == KIND_BINARY) {
-            const double p1 = 1.0 / (1.0 + exp(-z)), p0 = 1.0 - p1;
-            pm = isnan(p1) ? p1 : (p0 > p1 ? p0 : p1);
-          } else {
-            const double mm = fabs(z), e0 = exp(-z - mm), e1 = exp(z - mm), s = e0 + e1;
-            const double q0 = e0 / s, q1 = e1 / s;
-            pm = isnan(s) ? s : (q0 > q1 ? q0 : q1);
-          }
-          finish_row(a, row, z > 0.0 ? 1 : 0, pm);
+      const int rl = t * 16 + 4 * wave + rs;
+      if (cl == 0 && rl < rows) {
+        double pm;
+        if (a.kind == KIND_BINARY) {
+          const double p1 = 1.0 / (1.0 + exp(-z[t])), p0 = 1.0 - p1;
+          pm = isnan(p1) ? p1 : (p0 > p1 ? p0 : p1);
+        } else {
+          const double mm = fabs(z[t]), e0 = exp(-z[t] - mm), e1 = exp(z[t] - mm), s = e0 + e1;
+          const double q0 = e0 / s, q1 = e1 / s;
+          pm = isnan(s) ? s : (q0 > q1 ? q0 : q1);
         }
-        continue;
+        finish_row(a, row0 + rl, z[t] > 0.0 ? 1 : 0, pm);
       }
-      double z[4];
-      bool nan = false;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        z[r] = c0 + g + 4 * r < a.K ? acc[t][r] + bz[r] : -INFINITY;
-        nan |= isnan(z[r]);
-      }
-      double m = z[0];
-      int bi = c0 + g;
-#pragma unroll
-      for (int r = 1; r < 4; ++r)
-        if (z[r] > m) {
-          m = z[r];
-          bi = c0 + g + 4 * r;
-        }
-#pragma unroll
-      for (int off = 16; off <= 32; off <<= 1) {  // the row's 16 classes sit in lanes r16 + 16 g
-        const double om = __shfl_xor(m, off, 64);
-        const int ob = __shfl_xor(bi, off, 64);
-        if (om > m || (om == m && ob < bi)) {
-          m = om;
-          bi = ob;
-        }
-      }
-      double s = 0.0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s += ovr ? wsigmoid(z[r]) : exp(z[r] - m);  // masked classes: z = -inf -> 0
-      // a NaN logit makes the row's probability NaN (500, like sklearn -> json)
-      const uint64_t nanm = __ballot(nan) >> r16;
-      if (nanm & 0x0001000100010001ull) s = NAN;
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      st[t] = WState{m, s, bi};
     }
-    if (binary) return;
-    if (a.probe == 2) {
-      if (st[0].m == 12345.678) a.out_p[0] = st[0].s;
-      return;
-    }
-    if (a.hrec != nullptr) {  // host merge: one 32-byte record per (class block, row)
+    return;
+  }
+  // the row's block state {max, sum over the block's classes of exp(z - max) | sigmoid(z), first
+  // argmax}: 16-lane DPP all-reductions in a fixed order (deterministic), one exponential per lane
+  // and tile. A NaN logit makes s NaN (fmax skips it), and the row's probability NaN (500, like
+  // sklearn -> json); masked classes (z = -inf) add 0.
+  WState st[NB];
 #pragma unroll
-      for (int t = 0; t < NB; ++t) {
-        const int rl = t * 16 + r16;
-        if (g == 0 && row0 + rl < a.B) {
-          uint4* dst = a.hrec + ((int64_t)cb * RG + rl) * 2;
-          st16_host(dst, pack2(a.hseq, (uint32_t)st[t].bi, st[t].m));
-          st16_host(dst + 1, pack2(a.hseq, 0u, st[t].s));
-        }
-      }
-      return;
-    }
-    if (a.ncb == 1) {
+  for (int t = 0; t < NB; ++t) {
+    const double m = row16_max(z[t]);
+    const int bi = row16_min(cvalid && z[t] == m ? c0 + cl : 0x7fffffff);
+    const double s = row16_sum(ovr ? wsigmoid(z[t]) : exp(z[t] - m));
+    st[t] = WState{m, s, bi};
+  }
+  if (a.probe == 2) {
+    if (st[0].m == 12345.678) a.out_p[0] = st[0].s;
+    return;
+  }
+  if (a.hrec != nullptr) {  // host merge: one 32-byte record per (class block, row)
 #pragma unroll
-      for (int t = 0; t < NB; ++t) {
-        const int64_t row = row0 + t * 16 + r16;
-        if (g == 0 && row < a.B) finish_row(a, row, st[t].bi, ovr ? wsigmoid(st[t].m) / st[t].s : 1.0 / st[t].s);
+    for (int t = 0; t < NB; ++t) {
+      const int rl = t * 16 + 4 * wave + rs;
+      if (cl == 0 && rl < rows) {
+        uint4* dst = a.hrec + ((int64_t)cb * RG + rl) * 2;
+        st16_host(dst, pack2(a.hseq, (uint32_t)st[t].bi, st[t].m));
+        st16_host(dst + 1, pack2(a.hseq, 0u, st[t].s));
       }
-      return;
     }
+    return;
+  }
+  if (a.ncb == 1) {
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const int rl = t * 16 + 4 * wave + rs;
+      if (cl == 0 && rl < rows) finish_row(a, row0 + rl, st[t].bi, ovr ? wsigmoid(st[t].m) / st[t].s : 1.0 / st[t].s);
+    }
+    return;
   }
   // ---- class blocks: every block publishes its rows' states as two tagged 16-byte granules
   // {m, argmax, epoch} {s, epoch, 0} (write-through sc1 stores; the data is the flag, so no drain,
-  // ticket or fence: Guideline 16 R2), and the row group's LAST class block polls them with sc1 loads
-  // and merges. All blocks of a serving launch are co-resident (<= a few hundred blocks of 4
-  // waves), and the poll is bounded (1 s, then the rows fail with WIDE_TIMEOUT_IDX).
+  // ticket or fence: Guideline 16 R2)
   unsigned char* rgw2 = a.ws + (int64_t)rgi * a.rg_bytes;
   double* states = reinterpret_cast<double*>(rgw2 + a.cnt_bytes + a.part_bytes);
-  if (wave == 0) {
 #pragma unroll
-    for (int t = 0; t < NB; ++t) {
-      const int rl = t * 16 + r16;
-      if (g == 0) {
-        double* dst = states + ((int64_t)cb * RG + rl) * 4;
-        const uint64_t mu = __builtin_bit_cast(uint64_t, st[t].m), su = __builtin_bit_cast(uint64_t, st[t].s);
-        st16_sc1(dst, wu4_t{(uint32_t)mu, (uint32_t)(mu >> 32), (uint32_t)st[t].bi, a.epoch});
-        st16_sc1(dst + 2, wu4_t{(uint32_t)su, (uint32_t)(su >> 32), 0u, a.epoch});
-      }
+  for (int t = 0; t < NB; ++t) {
+    const int rl = t * 16 + 4 * wave + rs;
+    if (cl == 0 && rl < rows) {
+      double* dst = states + ((int64_t)cb * RG + rl) * 4;
+      const uint64_t mu = __builtin_bit_cast(uint64_t, st[t].m), su = __builtin_bit_cast(uint64_t, st[t].s);
+      st16_sc1(dst, wu4_t{(uint32_t)mu, (uint32_t)(mu >> 32), (uint32_t)st[t].bi, a.epoch});
+      st16_sc1(dst + 2, wu4_t{(uint32_t)su, (uint32_t)(su >> 32), 0u, a.epoch});
     }
   }
-  // the merger is the highest block index of the row group: blocks are dispatched in index order in
-  // practice, so its producers are already resident when it starts, and a grid far larger than the
-  // chip (library calls with huge B) never parks a spinning merger ahead of its own producers
-  if (cb != a.ncb - 1) return;
-  // merging block, 256 threads: row rl = tid >> 3 (8 rows per wave), part = tid & 7 takes class blocks
-  // part, part + 8, ...: the row max by compares and 3 xor shuffles, then every block's
-  // s * exp(m - max) in parallel, summed per lane in block order and over the 8 lanes in a
-  // fixed xor tree (deterministic).
-  const int rows = (int)min<int64_t>((int64_t)a.B - row0, 16 * NB);
-  if (8 * wave >= rows) return;  // wave-uniform: no rows of this wave in the launch
-  const int rl = threadIdx.x >> 3, part = threadIdx.x & 7;
+  if (wave == 0) wstamp(a, 2);
+  // ---- the class merge, by the row group's highest class blocks: nm mergers x 4 waves, one wave
+  // per row quad q (rows 4q .. 4q + 3, one per 16-lane DPP row; lane cl takes class blocks cl,
+  // cl + 16, ...). Q <= 8 quads and nm = min(ncb, Q) >= 2 mergers cover them in one pass. The
+  // mergers sit at the highest block indices: blocks are dispatched in index order in practice, so
+  // their producers are already resident when they poll; the poll is bounded (1 s, then the rows
+  // fail with WIDE_TIMEOUT_IDX).
+  const int Q = (rows + 3) >> 2;
+  const int nm = min(a.ncb, Q);
+  const int j = a.ncb - 1 - cb;
+  if (j >= nm) return;
+  const int q = j + nm * wave;
+  if (q >= Q) return;  // wave-uniform
+  const int rl = 4 * q + rs;
   const bool live = rl < rows;
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)states, 0, a.ncb * RG * 32, 0x00020000);
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)states, 0, a.ncb * RG * 32, 0x00020000);
   auto ldg = [&](int b, int h) -> wu4_t {  // sc1 (aux 16): past this CU's L1, agent-coherent
-    return __builtin_bit_cast(wu4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, (b * RG + rl) * 32 + h * 16, 0, 16));
+    return __builtin_bit_cast(wu4_t, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (b * RG + rl) * 32 + h * 16, 0, 16));
   };
-  constexpr int MU = 8;  // states per lane held in registers (ncb <= 64: one pass)
+  auto gm = [](const wu4_t& v) { return __builtin_bit_cast(double, (uint64_t)v[0] | ((uint64_t)v[1] << 32)); };
+  constexpr int MU = 4;  // granule pairs per lane held in registers (ncb <= 64: one pass)
   const uint64_t t0 = wall_clock64();
+  if (wave == 0) wstamp(a, 3);
   bool timeout = false;
-  // wait until every granule this wave merges carries this launch's epoch
   wu4_t g1[MU], g2[MU];
-  for (int b0 = 0; b0 < a.ncb; b0 += 8 * MU) {
-    for (;;) {
+  double m = -INFINITY;  // lane-local first max over its blocks (increasing b), and its class
+  int bi = 0x7fffffff;
+  for (int b0 = 0; b0 < a.ncb && !timeout; b0 += 16 * MU) {
+    for (;;) {  // until every granule of this chunk carries this launch's epoch
       bool ok = true;
 #pragma unroll
       for (int u = 0; u < MU; ++u) {
-        const int b = b0 + part + 8 * u;
+        const int b = b0 + cl + 16 * u;
         if (live && b < a.ncb) {
           g1[u] = ldg(b, 0);
           g2[u] = ldg(b, 1);
@@ -390,7 +407,7 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
       }
 #pragma unroll
       for (int u = 0; u < MU; ++u) {
-        const int b = b0 + part + 8 * u;
+        const int b = b0 + cl + 16 * u;
         if (live && b < a.ncb) ok &= g1[u][3] == a.epoch && g2[u][3] == a.epoch;
       }
       if (__all(ok) && a.probe != 3) break;  // probe 3 (fault injection): the states never arrive
@@ -401,81 +418,47 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
       __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");  // the next pass loads again
     }
-    if (timeout) break;
-  }
-  auto gm = [](const wu4_t& v) { return __builtin_bit_cast(double, (uint64_t)v[0] | ((uint64_t)v[1] << 32)); };
-  double M = -INFINITY, SS = 0.0;
-  int BI = 0x7fffffff;
-  bool nan = false;
-  auto reduce_max = [&]() {
-#pragma unroll
-    for (int off = 1; off <= 4; off <<= 1) {
-      const double om = __shfl_xor(M, off, 64);
-      const int ob = __shfl_xor(BI, off, 64);
-      if (om > M || (om == M && ob < BI)) {
-        M = om;
-        BI = ob;
-      }
-    }
-  };
-  if (a.ncb <= 8 * MU) {  // the last poll's granules are the states
 #pragma unroll
     for (int u = 0; u < MU; ++u) {
-      const int b = part + 8 * u;
-      if (live && b < a.ncb) {
-        const double m = gm(g1[u]);
-        const int bi = (int)g1[u][2];
-        nan |= isnan(m);
-        if (m > M || (m == M && bi < BI)) {
-          M = m;
-          BI = bi;
-        }
-      }
+      const int b = b0 + cl + 16 * u;
+      const double mu = live && b < a.ncb ? gm(g1[u]) : -INFINITY;
+      const bool take = mu > m;
+      m = take ? mu : m;
+      bi = take ? (int)g1[u][2] : bi;
     }
-    reduce_max();
+  }
+  if (wave == 0) wstamp(a, 4);
+  const double M = row16_max(m);
+  const int BI = row16_min(m == M ? bi : 0x7fffffff);
+  double sl = 0.0;
+  if (a.ncb <= 16 * MU) {  // the last poll's granules are the states
 #pragma unroll
-    for (int u = 0; u < MU; ++u)
-      if (live && part + 8 * u < a.ncb) SS += ovr ? gm(g2[u]) : gm(g2[u]) * exp(gm(g1[u]) - M);
-  } else if (live) {  // very wide K: every granule has arrived; a max pass, then a sum pass
-    for (int b = part; b < a.ncb; b += 8) {
-      const wu4_t v = ldg(b, 0);
-      const double m = gm(v);
-      nan |= isnan(m);
-      if (m > M || (m == M && (int)v[2] < BI)) {
-        M = m;
-        BI = (int)v[2];
-      }
+    for (int u = 0; u < MU; ++u) {
+      const int b = cl + 16 * u;
+      if (live && b < a.ncb) sl += ovr ? gm(g2[u]) : gm(g2[u]) * exp(gm(g1[u]) - M);
     }
-    reduce_max();
-    for (int b = part; b < a.ncb; b += 8) SS += ovr ? gm(ldg(b, 1)) : gm(ldg(b, 1)) * exp(gm(ldg(b, 0)) - M);
-  } else {
-    reduce_max();
+  } else if (live && !timeout) {  // very wide K: every granule has arrived; the sums reloaded
+    for (int b = cl; b < a.ncb; b += 16) sl += ovr ? gm(ldg(b, 1)) : gm(ldg(b, 1)) * exp(gm(ldg(b, 0)) - M);
   }
-  // consumed: clear the granules' tags with write-through stores (no dirty line is left behind to
-  // be written back over a later launch's granule), so a HIP-graph replay - one epoch baked into
-  // its arguments - never merges the previous replay's states. Captured launches only: an eager
-  // launch has an epoch of its own, and the kernel's end waits for these stores (+1.1 us at B = 8,
-  // profiles/r4_wide_merge/s39_summary.txt)
-  // graph captures: clear the consumed tags - also after a timeout (the rows already fail), so the
-  // next replay never reads this replay's granules as its own
+  const double SS = row16_sum(sl);
+  // graph captures: clear the consumed tags with write-through stores (no dirty line is left behind
+  // to be written back over a later launch's granule) - also after a timeout (the rows already
+  // fail) - so the next replay, one epoch baked into its arguments, never merges this replay's
+  // states. Captured launches only: an eager launch has an epoch of its own.
   if (a.clear_tags && live) {
-    for (int b = part; b < a.ncb; b += 8) {
-      gu32_t* const t = (gu32_t*)(states + ((int64_t)b * RG + rl) * 4);
-      __hip_atomic_store(t + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(t + 7, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int b = cl; b < a.ncb; b += 16) {
+      gu32_t* const tg = (gu32_t*)(states + ((int64_t)b * RG + rl) * 4);
+      __hip_atomic_store(tg + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(tg + 7, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (nan) SS = NAN;
-  SS += __shfl_xor(SS, 1, 64);
-  SS += __shfl_xor(SS, 2, 64);
-  SS += __shfl_xor(SS, 4, 64);
-  const int64_t row = row0 + rl;
-  if (part == 0 && live) {
+  if (cl == 0 && live) {
     if (timeout)
-      finish_row(a, row, WIDE_TIMEOUT_IDX, NAN);
+      finish_row(a, row0 + rl, WIDE_TIMEOUT_IDX, NAN);
     else
-      finish_row(a, row, BI, ovr ? wsigmoid(M) / SS : 1.0 / SS);
+      finish_row(a, row0 + rl, BI, ovr ? wsigmoid(M) / SS : 1.0 / SS);
   }
+  if (wave == 0) wstamp(a, 5);
 }
 
 }  // namespace wide

@@ -26,11 +26,14 @@ using wide_plan::row_groups;
 
 }  // namespace
 
-int g_probe = 0;  // measurement hook (linear_wide_set_probe)
+int g_probe = 0;  // measurement hooks (linear_wide_set_probe / _set_trace)
+uint64_t* g_trace = nullptr;
 
 WidePlan linear_wide_plan(int dt, int F, int K) { return wide_plan::plan(dt, F, K); }
 
 void linear_wide_set_probe(int probe) { g_probe = probe; }
+
+void linear_wide_set_trace(void* trace) { g_trace = static_cast<uint64_t*>(trace); }
 
 size_t linear_wide_workspace(int64_t B, int dt, int F, int K) { return wide_plan::workspace(B, dt, F, K); }
 
@@ -70,6 +73,7 @@ void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const
   a.hseq = hro.seq;
   a.row_groups = rg;
   a.probe = g_probe;
+  a.trace = g_trace;
   a.clear_tags = 0;  // direct-dispatched launches are never captured (set below for the stream launch)
   static std::atomic<uint32_t> epochs{0};  // class-merge granule tags: distinct per launch, never 0
   a.epoch = epochs.fetch_add(1, std::memory_order_relaxed) + 1;

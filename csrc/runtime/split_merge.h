@@ -35,7 +35,8 @@ inline double merge_split_records(const SplitRecord* r, int ns, bool ovr, int32_
 
 // Host class merge of linear_wide's per-block row states (WideRecOut): ncb blocks x 2 units of
 // one row, r[2 * cb] = {seq, argmax, m}, r[2 * cb + 1] = {seq, 0, s}, all f64, merged in block
-// order exactly as the kernel's in-kernel merge does (wide::wmerge).
+// order (the kernel's in-kernel merge sums the same terms in its own fixed order: both within
+// float64 rounding of the oracle, tests/test_wide_gpu.py).
 inline double merge_wide_records(const WideRecord* r, int ncb, bool ovr, int32_t* label) {
   double M = -INFINITY, S = 0.0;
   int bi = 0x7fffffff;

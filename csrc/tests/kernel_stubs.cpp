@@ -36,6 +36,7 @@ void launch_linear_split(int, const void*, int64_t, const void*, const float*, i
 }
 WidePlan linear_wide_plan(int dt, int F, int K) { return wide_plan::plan(dt, F, K); }
 void linear_wide_set_probe(int) {}
+void linear_wide_set_trace(void*) {}
 size_t linear_wide_workspace(int64_t B, int dt, int F, int K) { return wide_plan::workspace(B, dt, F, K); }
 void launch_linear_wide(int, const void*, int64_t, const void*, const double*, int64_t, int, int, int, int32_t*, double*,
                         void*, size_t, hipStream_t, RecOut, WideRecOut, KernelLauncher*, bool) {

@@ -107,6 +107,10 @@ for s in $steps; do
           MLAPI_RESIDENT=$m run "serve_res${m}_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
         done
       done ;;
+    serve_wide64)  # wide models at the default f64 (sklearn's dtype): every body byte-compared (rel_tol 0)
+      for k in 2 40 1000; do
+        run "bench_serve_wide_k${k}_f64" 300 python -u bench.py --mode serve_wide --wide-classes $k --wide-dtype f64 --steps 20 --warmup 5
+      done ;;
     serve_wide)
       for dt in f32 bf16; do
         run bench_serve_wide_k1000_$dt 300 python -u bench.py --mode serve_wide --wide-classes 1000 --wide-dtype $dt --steps 40 --warmup 5
