@@ -6,9 +6,10 @@
 //
 // Geometry (serving batches are a few rows, so the kernel is latency bound: spread the weights
 // over many CUs and keep every MFMA chain short):
-//  * grid = (ncb class blocks x nfs feature splits, row groups of 32 rows); a block = 4 waves;
-//    a block owns 16 classes x 32 rows x one feature split, and its 4 waves split that range
-//    again, each accumulating the 16 x 16-row tiles of its quarter (NB tiles) in f64 MFMAs;
+//  * grid = (ncb class blocks x nfs feature splits, row groups of NB 16-row tiles: NB = 1 while
+//    that grid fits one block per CU, else 2); a block = 4 waves; a block owns 16 classes x
+//    16 NB rows x one feature split, and its 4 waves split that range again, each accumulating
+//    the 16 x 16-row tiles of its quarter in f64 MFMAs;
 //  * operands straight from memory to registers, 16 bytes per lane per load (f64: 2 features,
 //    f32: 4 features converted exactly to f64): lane l loads class (l & 15) and row (l & 15) at
 //    feature offset 4*E*step + (l >> 4)*E, and element e of its load is the MFMA's k = l >> 4
@@ -26,9 +27,10 @@
 //    linear_rows.h); multiclass kinds reduce the block's 16 classes to a row state {max,
 //    sum exp(z - max) | sum sigmoid(z), first argmax}, and class blocks are merged either on the
 //    host (one 32-byte record per block and row, the engine's completer merges in double) or
-//    in-kernel by the row group's highest class blocks: one wave per 4 rows, lane cl of a row
-//    taking class blocks cl, cl + 16, ... (sc1 polls of tagged granules), the same DPP
-//    reductions, every block's rescaled sum in parallel. Everything in f64, fixed orders.
+//    in-kernel by the row group's highest class blocks: 16 / 32 / 64 lanes per row by the number
+//    of class blocks (one block per lane at K = 1000; sc1 polls of tagged granules), DPP plus
+//    permlane-swap all-reductions, every block's rescaled sum in parallel. Everything in f64,
+//    fixed orders.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -46,7 +48,7 @@ typedef __attribute__((ext_vector_type(4))) float wf4_t;
 typedef __attribute__((ext_vector_type(4))) uint32_t wu4_t;
 
 constexpr int CB = 16;     // classes per block
-constexpr int RG = 32;     // rows per row group
+constexpr int RG = 32;     // row slots of a row group's workspace region (a launch's groups use 16 or 32)
 constexpr int WAVES = 4;   // waves per block (feature quarters)
 constexpr int U = 4;       // steps per load chunk
 
@@ -75,7 +77,7 @@ struct WideArgs {
                   // block never sees the states (its rows time out after 1 s)
   uint64_t* trace;  // linear_wide_set_trace (measurement, nullptr in production): per block 8 wall-clock
                     // stamps (100 MHz) at entry, MFMA loop done, states published, merge poll begin /
-                    // end, rows written
+                    // end, rows written, first operands landed, kernel arguments arrived
 };
 
 // measurement timeline: lane 0 of the calling wave stamps slot i of its block (vector stores)
@@ -131,6 +133,42 @@ __device__ __forceinline__ int row16_min(int v) {
   v = min(v, (int)dpp_u32<DPP_ROR4>((uint32_t)v));
   return min(v, (int)dpp_u32<DPP_ROR8>((uint32_t)v));
 }
+// the value of lane ^ 16 / lane ^ 32 (gfx950 v_permlane16/32_swap with both operands v: each lane
+// gets back its own value and its partner's, in an order the test below does not need to know)
+__device__ __forceinline__ uint32_t xchg16(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return r[0] == v ? r[1] : r[0];
+}
+__device__ __forceinline__ uint32_t xchg32(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return r[0] == v ? r[1] : r[0];
+}
+template <bool X32>
+__device__ __forceinline__ double xchg_f64(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint64_t lo = X32 ? xchg32((uint32_t)u) : xchg16((uint32_t)u);
+  const uint64_t hi = X32 ? xchg32((uint32_t)(u >> 32)) : xchg16((uint32_t)(u >> 32));
+  return __builtin_bit_cast(double, lo | (hi << 32));
+}
+// all-reductions over groups of lpr = 16 / 32 / 64 lanes (lpr wave-uniform)
+__device__ __forceinline__ double lanes_max(double v, int lpr) {
+  v = row16_max(v);
+  if (lpr >= 32) v = fmax(v, xchg_f64<false>(v));
+  if (lpr == 64) v = fmax(v, xchg_f64<true>(v));
+  return v;
+}
+__device__ __forceinline__ double lanes_sum(double v, int lpr) {
+  v = row16_sum(v);
+  if (lpr >= 32) v += xchg_f64<false>(v);
+  if (lpr == 64) v += xchg_f64<true>(v);
+  return v;
+}
+__device__ __forceinline__ int lanes_min(int v, int lpr) {
+  v = row16_min(v);
+  if (lpr >= 32) v = min(v, (int)xchg16((uint32_t)v));
+  if (lpr == 64) v = min(v, (int)xchg32((uint32_t)v));
+  return v;
+}
 
 typedef __attribute__((address_space(1))) unsigned int gu32_t;
 typedef __attribute__((address_space(1))) unsigned long long gu64_t;
@@ -177,8 +215,12 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   const int g = lane >> 4, r16 = lane & 15;
   const int cb = blockIdx.x % a.ncb, fs = blockIdx.x / a.ncb, rgi = blockIdx.y;
   const int c0 = cb * CB;
-  const int64_t row0 = (int64_t)rgi * RG;
+  const int64_t row0 = (int64_t)rgi * (16 * NB);  // a launch's row groups are its NB-tile groups
   if (threadIdx.x < 64) wstamp(a, 0);
+  if (a.trace != nullptr && threadIdx.x < 64) {  // measurement only: the kernel arguments arrived
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wstamp(a, 7);
+  }
   const int S = a.fsteps;
   const int64_t f0 = ((int64_t)fs * WAVES + wave) * S * STEP + g * E;
   const T* wp = static_cast<const T*>(a.W) + (int64_t)min(c0 + r16, a.K - 1) * a.ldx + f0;
@@ -189,6 +231,9 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
 
   // the bias of this lane's classes, loaded now so its latency hides under the MFMA loop
   const double bcl = a.bias[min(c0 + (lane & 15), a.K - 1)];
+  // one accumulator chain per tile: two chains (even / odd k) measured no faster - the SIMD's f64
+  // MFMA pipe, not the chain's dependency, paces the loop (16 MFMAs per wave ~0.88 us after the
+  // operands land at F = 256; tools/wide_trace.py, profiles/r5_wide/)
   wd4_t acc[NB];
 #pragma unroll
   for (int t = 0; t < NB; ++t) acc[t] = wd4_t{0.0, 0.0, 0.0, 0.0};
@@ -218,6 +263,10 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     }
   };
   load(w0, x0, 0);
+  if (a.trace != nullptr && wave == 0) {  // measurement only: the first chunk's operands landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wstamp(a, 6);
+  }
   for (int s0 = 0; s0 < S; s0 += 2 * U) {
     load(w1, x1, s0 + U);
     __builtin_amdgcn_sched_barrier(0);  // keep the next chunk's loads in flight over these MFMAs
@@ -325,7 +374,9 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
   for (int t = 0; t < NB; ++t) {
     const double m = row16_max(z[t]);
     const int bi = row16_min(cvalid && z[t] == m ? c0 + cl : 0x7fffffff);
-    const double s = row16_sum(ovr ? wsigmoid(z[t]) : exp(z[t] - m));
+    // one exponential per lane for either kind (OvR: sigmoid(z) = 1 / (1 + exp(-z)))
+    const double e = exp(ovr ? -z[t] : z[t] - m);
+    const double s = row16_sum(ovr ? 1.0 / (1.0 + e) : e);
     st[t] = WState{m, s, bi};
   }
   if (a.probe == 2) {
@@ -368,38 +419,42 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     }
   }
   if (wave == 0) wstamp(a, 2);
-  // ---- the class merge, by the row group's highest class blocks: nm mergers x 4 waves, one wave
-  // per row quad q (rows 4q .. 4q + 3, one per 16-lane DPP row; lane cl takes class blocks cl,
-  // cl + 16, ...). Q <= 8 quads and nm = min(ncb, Q) >= 2 mergers cover them in one pass. The
-  // mergers sit at the highest block indices: blocks are dispatched in index order in practice, so
-  // their producers are already resident when they poll; the poll is bounded (1 s, then the rows
-  // fail with WIDE_TIMEOUT_IDX).
-  const int Q = (rows + 3) >> 2;
-  const int nm = min(a.ncb, Q);
+  // ---- the class merge, by the row group's highest class blocks: lpr lanes per row (16 / 32 / 64
+  // by the number of class blocks, so a lane takes at most ceil(ncb / lpr) <= 4 blocks - one at
+  // K = 1000), lane lb of a row taking blocks lb, lb + lpr, ...; one wave per 64 / lpr rows, 4 waves
+  // per merging block, nm = min(ncb, ceil(waves / 4)) merging blocks (rows <= 32: enough, since lpr
+  // grows with ncb). The mergers sit at the highest block indices: blocks are dispatched in index
+  // order in practice, so their producers are already resident when they poll; the poll is bounded
+  // (1 s, then the rows fail with WIDE_TIMEOUT_IDX).
+  const int lpr = a.ncb > 32 ? 64 : (a.ncb > 16 ? 32 : 16);
+  const int rpw = 64 / lpr;
+  const int units = (rows + rpw - 1) / rpw;
+  const int nm = min(a.ncb, (units + WAVES - 1) / WAVES);
   const int j = a.ncb - 1 - cb;
   if (j >= nm) return;
-  const int q = j + nm * wave;
-  if (q >= Q) return;  // wave-uniform
-  const int rl = 4 * q + rs;
+  const int unit = j + nm * wave;
+  if (unit >= units) return;  // wave-uniform
+  const int lb = lane & (lpr - 1);
+  const int rl = unit * rpw + lane / lpr;
   const bool live = rl < rows;
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)states, 0, a.ncb * RG * 32, 0x00020000);
   auto ldg = [&](int b, int h) -> wu4_t {  // sc1 (aux 16): past this CU's L1, agent-coherent
     return __builtin_bit_cast(wu4_t, __builtin_amdgcn_raw_buffer_load_b128(rsrc, (b * RG + rl) * 32 + h * 16, 0, 16));
   };
   auto gm = [](const wu4_t& v) { return __builtin_bit_cast(double, (uint64_t)v[0] | ((uint64_t)v[1] << 32)); };
-  constexpr int MU = 4;  // granule pairs per lane held in registers (ncb <= 64: one pass)
+  constexpr int MU = 4;  // granule pairs per lane held in registers (ncb <= 4 lpr: one pass)
   const uint64_t t0 = wall_clock64();
   if (wave == 0) wstamp(a, 3);
   bool timeout = false;
   wu4_t g1[MU], g2[MU];
   double m = -INFINITY;  // lane-local first max over its blocks (increasing b), and its class
   int bi = 0x7fffffff;
-  for (int b0 = 0; b0 < a.ncb && !timeout; b0 += 16 * MU) {
+  for (int b0 = 0; b0 < a.ncb && !timeout; b0 += lpr * MU) {
     for (;;) {  // until every granule of this chunk carries this launch's epoch
       bool ok = true;
 #pragma unroll
       for (int u = 0; u < MU; ++u) {
-        const int b = b0 + cl + 16 * u;
+        const int b = b0 + lb + lpr * u;
         if (live && b < a.ncb) {
           g1[u] = ldg(b, 0);
           g2[u] = ldg(b, 1);
@@ -407,7 +462,7 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
       }
 #pragma unroll
       for (int u = 0; u < MU; ++u) {
-        const int b = b0 + cl + 16 * u;
+        const int b = b0 + lb + lpr * u;
         if (live && b < a.ncb) ok &= g1[u][3] == a.epoch && g2[u][3] == a.epoch;
       }
       if (__all(ok) && a.probe != 3) break;  // probe 3 (fault injection): the states never arrive
@@ -420,7 +475,7 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     }
 #pragma unroll
     for (int u = 0; u < MU; ++u) {
-      const int b = b0 + cl + 16 * u;
+      const int b = b0 + lb + lpr * u;
       const double mu = live && b < a.ncb ? gm(g1[u]) : -INFINITY;
       const bool take = mu > m;
       m = take ? mu : m;
@@ -428,35 +483,38 @@ __device__ __forceinline__ void wide_predict(const WideArgs& a) {
     }
   }
   if (wave == 0) wstamp(a, 4);
-  const double M = row16_max(m);
-  const int BI = row16_min(m == M ? bi : 0x7fffffff);
+  const double M = lanes_max(m, lpr);
+  const int BI = lanes_min(m == M ? bi : 0x7fffffff, lpr);
   double sl = 0.0;
-  if (a.ncb <= 16 * MU) {  // the last poll's granules are the states
+  if (a.ncb <= lpr * MU) {  // the last poll's granules are the states
 #pragma unroll
     for (int u = 0; u < MU; ++u) {
-      const int b = cl + 16 * u;
-      if (live && b < a.ncb) sl += ovr ? gm(g2[u]) : gm(g2[u]) * exp(gm(g1[u]) - M);
+      const int b = lb + lpr * u;
+      if (live && b < a.ncb) sl += ovr ? gm(g2[u]) : gm(g2[u]) * exp(gm(g1[u]) - M);  // OvR: no exp
     }
   } else if (live && !timeout) {  // very wide K: every granule has arrived; the sums reloaded
-    for (int b = cl; b < a.ncb; b += 16) sl += ovr ? gm(ldg(b, 1)) : gm(ldg(b, 1)) * exp(gm(ldg(b, 0)) - M);
+    for (int b = lb; b < a.ncb; b += lpr) sl += ovr ? gm(ldg(b, 1)) : gm(ldg(b, 1)) * exp(gm(ldg(b, 0)) - M);
   }
-  const double SS = row16_sum(sl);
+  const double SS = lanes_sum(sl, lpr);
   // graph captures: clear the consumed tags with write-through stores (no dirty line is left behind
   // to be written back over a later launch's granule) - also after a timeout (the rows already
   // fail) - so the next replay, one epoch baked into its arguments, never merges this replay's
   // states. Captured launches only: an eager launch has an epoch of its own.
   if (a.clear_tags && live) {
-    for (int b = cl; b < a.ncb; b += 16) {
+    for (int b = lb; b < a.ncb; b += lpr) {
       gu32_t* const tg = (gu32_t*)(states + ((int64_t)b * RG + rl) * 4);
       __hip_atomic_store(tg + 3, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(tg + 7, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (cl == 0 && live) {
-    if (timeout)
+  if (lb == 0 && live) {
+    if (timeout) {
       finish_row(a, row0 + rl, WIDE_TIMEOUT_IDX, NAN);
-    else
-      finish_row(a, row0 + rl, BI, ovr ? wsigmoid(M) / SS : 1.0 / SS);
+    } else if (ovr) {
+      finish_row(a, row0 + rl, BI, wsigmoid(M) / SS);
+    } else {  // a branch of its own: the softmax row does not also pay the OvR sigmoid's exp and division
+      finish_row(a, row0 + rl, BI, 1.0 / SS);
+    }
   }
   if (wave == 0) wstamp(a, 5);
 }

@@ -49,9 +49,10 @@ void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const
   const size_t es = dt == DT_F64 ? 8 : 4;
   if ((ldx * es) % 16 != 0 || reinterpret_cast<uintptr_t>(X) % 16 != 0 || reinterpret_cast<uintptr_t>(W) % 16 != 0)
     throw std::invalid_argument("linear_wide: X and W rows must be 16-byte aligned");
-  const int rg = row_groups(B);
+  const int nb = wide_plan::tiles_per_group(B, p);
+  const int rg = row_groups(B, nb);
   if (rg > 65535) throw std::invalid_argument("linear_wide: B too large for one launch");
-  if (hro.rec != nullptr && (rg != 1 || binary)) throw std::invalid_argument("linear_wide: host merge needs B <= 32, multiclass");
+  if (hro.rec != nullptr && (rg != 1 || binary)) throw std::invalid_argument("linear_wide: host merge needs one row group, multiclass");
   const bool needs_ws = p.nfs > 1 || (!binary && p.ncb > 1 && hro.rec == nullptr);
   if (needs_ws && ws_bytes < linear_wide_workspace(B, dt, F, K))
     throw std::invalid_argument("linear_wide: workspace too small (zero it once)");
@@ -84,7 +85,7 @@ void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const
   a.cnt_bytes = (int64_t)lay.cnt_bytes;
   a.part_bytes = (int64_t)lay.part_bytes;
   const dim3 grid((unsigned)(p.ncb * p.nfs), (unsigned)rg);
-  const bool nb2 = B > 16;
+  const bool nb2 = nb == 2;
   if (direct != nullptr) {
     char name[48];
     std::snprintf(name, sizeof name, "mlapi_wide_%s_nb%d", dt == DT_F64 ? "f64" : "f32", nb2 ? 2 : 1);

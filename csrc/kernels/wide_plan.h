@@ -14,7 +14,7 @@ namespace mlapi {
 namespace wide_plan {
 
 constexpr int CB = 16;     // classes per block
-constexpr int RG = 32;     // rows per row group
+constexpr int RG = 32;     // rows of a row group's workspace region (a launch's groups have 16 or 32)
 constexpr int WAVES = 4;   // waves per block (feature quarters)
 constexpr int SMAX = 32;   // wave steps per feature split before the features are split over blocks
 
@@ -32,7 +32,13 @@ inline WidePlan plan(int dt, int F, int K) {
   return p;
 }
 
-inline int row_groups(int64_t B) { return (int)((std::max<int64_t>(B, 1) + RG - 1) / RG); }
+// 16-row tiles per row group: one (NB = 1) while the grid of 16-row groups stays within one block
+// per CU - small serving batches then spread their MFMA work over twice the CUs (B = 24: 126
+// blocks of one tile instead of 63 of two; tools/wide_trace.py) - else two (W read once per 32 rows)
+inline int tiles_per_group(int64_t B, const WidePlan& p) {
+  return (std::max<int64_t>(B, 1) + 15) / 16 * p.ncb * p.nfs <= 256 ? 1 : 2;
+}
+inline int row_groups(int64_t B, int nb) { return (int)((std::max<int64_t>(B, 1) + 16 * nb - 1) / (16 * nb)); }
 
 // one region per row group (linear_wide.h WideArgs): tickets | split partials | row states
 struct Layout {
@@ -46,8 +52,9 @@ inline Layout layout(const WidePlan& p) {
   return l;
 }
 
+// enough for every launch of at most B rows (16-row groups are the most regions a launch uses)
 inline size_t workspace(int64_t B, int dt, int F, int K) {
-  return (size_t)row_groups(B) * layout(plan(dt, F, K)).rg_bytes;
+  return (size_t)row_groups(B, 1) * layout(plan(dt, F, K)).rg_bytes;
 }
 
 }  // namespace wide_plan

@@ -32,7 +32,9 @@ SHAPES = [  # F, K, kind
     (1500, 33, Kind.OVR),
     (4096, 1000, Kind.MULTINOMIAL),
     (5000, 7, Kind.MULTINOMIAL),
-    (512, 3000, Kind.MULTINOMIAL),  # 188 class blocks: the merge's two-pass path (> 64 blocks)
+    (128, 300, Kind.MULTINOMIAL),   # 19 class blocks: 32 lanes per row in the merge
+    (512, 3000, Kind.MULTINOMIAL),  # 188 class blocks: 64 lanes per row, 3 blocks per lane
+    (64, 4500, Kind.MULTINOMIAL),   # 282 class blocks: the merge's two-pass path (> 4 x 64 blocks)
     (300, 1100, Kind.OVR),
     (256, 1, Kind.BINARY),
     (4096, 1, Kind.BINARY),

@@ -49,9 +49,17 @@ for td in (torch.float64, torch.float32):
                 (mg[:, 3].max() - base) if len(mg) else 0,  # merger poll begin
                 (mg[:, 4].max() - base) if len(mg) else 0,  # merger poll end
                 (mg[:, 5].max() - base) if len(mg) else 0,  # rows written
+                (np.median(t[:, 0]) - base),        # median block entry
+                np.median(t[:, 1] - t[:, 0]),       # median per-block MFMA phase
+                np.max(t[:, 1] - t[:, 0]),          # longest per-block MFMA phase
+                np.median(t[:, 2] - t[:, 1]),       # median per-block epilogue
+                np.median(t[:, 7] - t[:, 0]),       # median entry -> kernel arguments arrived
+                np.median(t[:, 6] - t[:, 0]),       # median entry -> first operands landed
             ])
         c.linear_wide_set_trace(0)
         r = np.median(np.array(rows, dtype=np.float64), axis=0) / 100.0  # 100 MHz ticks -> us
         print(f"dtype={str(td)[6:]} F={F} K={K} B={B} blocks={len(t)}: last entry {r[0]:.2f}  mfma med {r[1]:.2f} "
-              f"last {r[2]:.2f}  states {r[3]:.2f}  poll begin {r[4]:.2f} end {r[5]:.2f}  rows {r[6]:.2f} us",
+              f"last {r[2]:.2f}  states {r[3]:.2f}  poll begin {r[4]:.2f} end {r[5]:.2f}  rows {r[6]:.2f} us"
+              f" | entry med {r[7]:.2f}  per-block mfma med {r[8]:.2f} max {r[9]:.2f}  epilogue med {r[10]:.2f}"
+              f"  kernargs +{r[11]:.2f} operands +{r[12]:.2f}",
               flush=True)
