@@ -607,16 +607,25 @@ def main(argv=None) -> int:
 
         per_rank = max(4, len(pinned) if pinned else effective_cpus() // max(1, local))
         # measured on a 16-CPU share with the out-of-process load generator. Resident SMALL path
-        # (round 5, profiles/r5_serve/): io=8/client=4 -> 1.51-1.54 M req/s at 4.8-4.9 us of server
-        # CPU per request; io=10/4 -> 0.97 M (10 spinning IO threads); io=6/4 -> 0.96-1.09 M. The
-        # batcher path (resident off) had io=10/4 best (profiles/r2_serve_threads/: 0.99-1.11 M;
-        # 9/5 0.89-0.93 M; 8/6 0.75-0.94 M)
+        # (round 5, profiles/r5_serve/ s22-s26, interleaved): equal IO and load-generator thread
+        # counts win - the acceptor deals connection k to IO thread k % io and the load generator
+        # gives it to its thread k % client, so with io == client each load-generator thread's
+        # connections sit on one IO thread (3.7-3.9 us of server CPU per request instead of 4.8-5.1):
+        # 8/8 -> 1.94 M req/s median of 9 (1.32-1.97), 10/5 1.76 M median of 11, 7/7 1.64, 6/6
+        # 1.67, 8/4 1.52; ratios that are not whole (8/5, 7/5, 9/3, 8/6) 0.95-1.23 M. The batcher
+        # path (resident off) had io=10/4 best (profiles/r2_serve_threads/: 0.99-1.11 M; 9/5
+        # 0.89-0.93 M; 8/6 0.75-0.94 M)
         cl = max(2, min(6, per_rank // 4))
         # the resident kernel serves the headline's SMALL (Iris) model; serve_wide's F = 256 models
         # take the batcher path
-        resident = (args.mode == "serve" and os.environ.get("MLAPI_RESIDENT", "auto").lower() != "off"
-                    and info.device is not None)
+        from mlapi_amd.parallel.comm import resident_auto_ok
+
+        res_env = os.environ.get("MLAPI_RESIDENT", "auto").lower()
+        resident = (args.mode == "serve" and info.device is not None
+                    and (res_env == "on" or (res_env == "auto" and resident_auto_ok())))
         io = max(2, min(12, per_rank // 2 if resident else per_rank - cl - 2))
+        if resident:
+            cl = io
         args.io_threads = args.io_threads if args.io_threads > 0 else io
         args.client_threads = args.client_threads if args.client_threads > 0 else cl
     if pinned and getattr(args, "lg_proc", None) is not None and len(pinned) > args.io_threads + 3:

@@ -128,10 +128,9 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     if (inited_) hsa_shut_down();
   }
 
-  bool init(int device, const std::string& path, int max_in_flight, std::string* why, int max_producers) {
+  bool init(int device, const std::string& path, int max_in_flight, std::string* why) {
     ka_slots_ = std::max<uint32_t>(64u, 8u * (uint32_t)std::max(1, max_in_flight));
-    max_lanes_ = std::max(0, std::min(max_producers, MAX_LANES));
-    const uint32_t ka_total = ka_slots_ + (uint32_t)max_lanes_ * LANE_KERNARGS;
+    const uint32_t ka_total = ka_slots_;
     if (const char* e = getenv("MLAPI_HDP_READBACK")) hdp_readback_ = atoi(e) != 0;
     auto fail = [&](const std::string& m) {
       if (why) *why = m;
@@ -186,7 +185,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
       if (k_[i].kernarg < sizeof(InlineBatch) || k_[i].kernarg > stride_) return fail("unexpected kernarg layout");
     }
     hsa_executable_iterate_agent_symbols(exe_, gpu_, collect_split_kernels, &named_);
-    if (hsa_queue_create(gpu_, QUEUE_SIZE, max_lanes_ > 0 ? HSA_QUEUE_TYPE_MULTI : HSA_QUEUE_TYPE_SINGLE, queue_error,
+    if (hsa_queue_create(gpu_, QUEUE_SIZE, HSA_QUEUE_TYPE_SINGLE, queue_error,
                          this, UINT32_MAX, UINT32_MAX, &queue_) != HSA_STATUS_SUCCESS)
       return fail("hsa_queue_create failed");
     // Kernarg ring: a buffer is rewritten KA_SLOTS launches later; the engine keeps at most
@@ -220,32 +219,19 @@ class HsaInlineDispatcher final : public InlineDispatcher {
          hsa_amd_agents_allow_access(1, &gpu_, nullptr, kernargs_) != HSA_STATUS_SUCCESS))
       return fail("kernarg allocation failed");
     std::memset(kernargs_, 0, (size_t)stride_ * ka_total);
-    prod_[0].base = kernargs_;
-    prod_[0].entries = ka_slots_;
-    prod_[0].wi.assign(ka_slots_, ~uint64_t(0));
-    for (int p = 1; p <= max_lanes_; ++p) {
-      prod_[p].base = kernargs_ + (size_t)stride_ * (ka_slots_ + (uint32_t)(p - 1) * LANE_KERNARGS);
-      prod_[p].entries = LANE_KERNARGS;
-      prod_[p].wi.assign(LANE_KERNARGS, ~uint64_t(0));
-    }
-    published_.store(hsa_queue_load_write_index_scacquire(queue_), std::memory_order_relaxed);
+    ring_.base = kernargs_;
+    ring_.entries = ka_slots_;
+    ring_.wi.assign(ka_slots_, ~uint64_t(0));
     return true;
   }
 
-  int add_producer() override {
-    const int p = next_producer_.fetch_add(1) + 1;
-    return p <= max_lanes_ ? p : -1;
-  }
-
-  void launch(int dt, const InlineBatch& a, int producer) override {
+  void launch(int dt, const InlineBatch& a) override {
     if (dt != DT_F64 && dt != DT_F32) throw std::invalid_argument("direct dispatch: f64 / f32 batches only");
-    if (producer < 0 || producer > max_lanes_) throw std::invalid_argument("direct dispatch: unknown producer");
     if (faulted()) throw std::runtime_error("direct dispatch: queue error");
     const Kernel& k = (a.F == 4 && a.K == 3) ? k_[dt == DT_F64 ? 4 : 5]  // exact shape: one load batch
                                               : k_[(dt == DT_F64 ? 0 : 2) + (a.F <= 8 && a.K <= 4 ? 0 : 1)];
-    Producer& pr = prod_[producer];
     uint64_t* wi_slot = nullptr;
-    char* ka = next_kernarg(pr, &wi_slot);
+    char* ka = next_kernarg(ring_, &wi_slot);
     // Only the bytes the kernel reads: header + W/b of this model + n rows.
     const size_t es = dt == DT_F64 ? 8 : 4;
     const size_t wb_end = offsetof(InlineBatch, wb) + (size_t)a.K * (a.F + 1) * es;
@@ -271,7 +257,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
       throw std::invalid_argument(std::string("direct dispatch: bad launch of ") + name);
     if (faulted()) throw std::runtime_error("direct dispatch: queue error");
     uint64_t* wi_slot = nullptr;
-    char* ka = next_kernarg(prod_[0], &wi_slot);
+    char* ka = next_kernarg(ring_, &wi_slot);
     std::memcpy(ka, args, bytes);
     flush_kernargs();
     // ordered: barrier bit (the kernel starts after every earlier packet of this queue has
@@ -380,9 +366,9 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   void set_resident_fault() { rfault_.store(true); }
 
  private:
-  // One producer's part of the kernarg ring: `entries` argument blocks used round robin; wi[e] is
-  // the packet id that last used entry e (~0: never).
-  struct alignas(64) Producer {
+  // The kernarg ring: `entries` argument blocks used round robin; wi[e] is the packet id that last
+  // used entry e (~0: never).
+  struct alignas(64) Ring {
     char* base = nullptr;
     uint32_t entries = 0;
     uint64_t launches = 0;
@@ -390,11 +376,11 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   };
 
   // Ring entry reuse: the packet that last used this entry must have been consumed by the packet
-  // processor (its read index passed it). With at most a few batches in flight per producer and
+  // processor (its read index passed it). With at most a few batches in flight and
   // the region several times deeper, its kernel has finished as well; after a watchdog failure (a
   // batch given up while its packet may still be queued) this wait is what keeps live arguments
   // from being overwritten.
-  char* next_kernarg(Producer& p, uint64_t** slot) {
+  char* next_kernarg(Ring& p, uint64_t** slot) {
     const uint32_t e = (uint32_t)(p.launches++ % p.entries);
     const uint64_t last = p.wi[e];
     if (last != ~uint64_t(0)) {
@@ -420,16 +406,14 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     if (hdp_readback_) (void)*reinterpret_cast<volatile uint32_t*>(hdp_flush_);
   }
 
-  // grid_x in work-items (AQL), grid_y in blocks of height 1. Multi-producer: the packet slot is
-  // reserved by an atomic add on the write index; the header store and the doorbell go out in
-  // reservation order (published_), so the packet processor never sees a valid header behind an
-  // unpublished one and the doorbell value never decreases.
+  // grid_x in work-items (AQL), grid_y in blocks of height 1. One producer at a time (the engine's
+  // launch lock): reserve the slot, fill the packet, publish the header, ring the doorbell.
   void submit(const Kernel& k, const char* ka, uint32_t grid_x, uint32_t grid_y, uint16_t block, bool barrier,
               int release_scope, uint64_t* wi_slot) {
     const uint64_t wi = hsa_queue_add_write_index_scacq_screl(queue_, 1);
     *wi_slot = wi;
     while (wi - hsa_queue_load_read_index_scacquire(queue_) >= queue_->size) {
-      // full (cannot happen with a few batches in flight per producer): wait for the packet processor
+      // full (cannot happen with a few batches in flight): wait for the packet processor
       _mm_pause();
     }
     auto* pkt = reinterpret_cast<hsa_kernel_dispatch_packet_t*>(queue_->base_address) + (wi & (queue_->size - 1));
@@ -451,16 +435,8 @@ class HsaInlineDispatcher final : public InlineDispatcher {
                             (HSA_FENCE_SCOPE_AGENT << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                             (release_scope << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
     const uint32_t setup = grid_y > 1 ? 2 : 1;  // grid dimensions
-    if (max_lanes_ > 0) {
-      // earlier reservations publish first (their owners are between the add and the header store:
-      // a few stores); yield if one was descheduled in that window
-      uint32_t spins = 0;
-      while (published_.load(std::memory_order_acquire) != wi)
-        if (++spins > 4096) std::this_thread::yield(); else _mm_pause();
-    }
     __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), (uint32_t)header | (setup << 16), __ATOMIC_RELEASE);
     hsa_signal_store_relaxed(queue_->doorbell_signal, (hsa_signal_value_t)wi);
-    if (max_lanes_ > 0) published_.store(wi + 1, std::memory_order_release);
   }
 
   static constexpr uint32_t QUEUE_SIZE = 256;
@@ -486,11 +462,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   hsa_amd_memory_pool_t dpool_{};
   hsa_agent_t cpu_{};
   std::vector<void*> bar_bufs_;
-  static constexpr int MAX_LANES = 64;
-  int max_lanes_ = 0;
-  Producer prod_[MAX_LANES + 1];
-  std::atomic<int> next_producer_{0};
-  alignas(64) std::atomic<uint64_t> published_{0};  // next packet id allowed to publish (lanes on)
+  Ring ring_;
   std::atomic<bool> fault_{false};
   std::atomic<bool> rfault_{false};  // the resident queue reported an error
 };
@@ -503,9 +475,9 @@ void resident_queue_error(hsa_status_t, hsa_queue_t*, void* data) {
 }  // namespace
 
 std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int device, const std::string& hsaco_path, int max_in_flight,
-                                                         std::string* why, int max_producers) {
+                                                         std::string* why) {
   auto d = std::make_unique<HsaInlineDispatcher>();
-  if (!d->init(device, hsaco_path, max_in_flight, why, max_producers)) return nullptr;
+  if (!d->init(device, hsaco_path, max_in_flight, why)) return nullptr;
   return d;
 }
 

@@ -25,15 +25,11 @@ class InlineDispatcher : public KernelLauncher {
  public:
   ~InlineDispatcher() override = default;
   // Enqueue one kernel-argument batch (dt: DT_F64 / DT_F32); completion is the batch's done word
-  // or its records. `producer` 0 is the engine's launch path (batcher / run_idle, serialised by the
-  // engine's launch lock, also the only user of launch_kernel); 1.. are the per-IO-thread lanes of
-  // add_producer(). Each producer owns its part of the kernarg ring, so producers only meet at the
-  // packet slot: slots are reserved with an atomic add on the queue's write index and published
-  // (header store + doorbell) in reservation order, so the doorbell value never moves backwards.
-  // Any thread, one thread per producer at a time. Throws on failure.
-  virtual void launch(int dt, const InlineBatch& a, int producer = 0) = 0;
-  // A new producer id for launch() (a lane), or -1 when the kernarg ring has no region left.
-  virtual int add_producer() = 0;
+  // or its records. One caller at a time: the engine's launch path (batcher / run_idle, serialised
+  // by the engine's launch lock; also the only user of launch_kernel). Round 4's per-IO-thread
+  // dispatch lanes (a multi-producer queue) lost their A/B (profiles/r4_lanes/) and were removed in
+  // round 5; the resident kernel replaced the per-batch packet instead. Throws on failure.
+  virtual void launch(int dt, const InlineBatch& a) = 0;
   // true once the queue reported an error (the engine then fails the batches instead of waiting)
   virtual bool faulted() const = 0;
   // launches made through launch_kernel (wide serving batches dispatched without hipLaunchKernel)
@@ -68,9 +64,7 @@ class InlineDispatcher : public KernelLauncher {
 // `max_in_flight`: the engine's slot count. The kernarg ring is sized to a multiple of it (at least
 // 64 entries), and an entry is rewritten only after the packet processor has consumed the packet
 // that last used it (bounded wait, then an error instead of overwriting live arguments).
-// `max_producers`: lanes that add_producer() can hand out (each gets LANE_KERNARGS ring entries).
-constexpr int LANE_KERNARGS = 16;
 std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int device, const std::string& hsaco_path, int max_in_flight,
-                                                         std::string* why, int max_producers = 0);
+                                                         std::string* why);
 
 }  // namespace mlapi

@@ -42,7 +42,7 @@ void launch_linear_wide(int, const void*, int64_t, const void*, const double*, i
                         void*, size_t, hipStream_t, RecOut, WideRecOut, KernelLauncher*, bool) {
   unreachable("launch_linear_wide");
 }
-std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int, const std::string&, int, std::string* why, int) {
+std::unique_ptr<InlineDispatcher> make_direct_dispatcher(int, const std::string&, int, std::string* why) {
   if (why) *why = "host-only build";
   return nullptr;
 }

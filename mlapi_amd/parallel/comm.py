@@ -62,6 +62,40 @@ class DistInfo:
         return self.rank == 0
 
 
+def gpu_shared_by_ranks() -> bool:
+    """True when this node runs more ranks than it has visible GPUs (MLAPI_COMM=p2p rehearsals put
+    several ranks on one device). Reads the launcher's env and torch.cuda.device_count(), which does
+    not initialise the GPU on this image."""
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    n = torch.cuda.device_count()
+    return n > 0 and local_world > n
+
+
+def per_rank_cpus() -> int:
+    """CPUs one rank of this node can keep busy: its affinity mask, capped by its share of the
+    cgroup quota (or of the machine) over the node's ranks."""
+    from mlapi_amd.utils.threads import cgroup_cpu_quota
+
+    local_world = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = os.cpu_count() or 1
+    q = cgroup_cpu_quota()
+    total = int(q) if q is not None else (os.cpu_count() or 1)
+    return max(1, min(aff, total // local_world))
+
+
+RESIDENT_MIN_CPUS = 12  # the resident path's IO threads poll their records: per_rank_cpus() / 2 of them
+
+
+def resident_auto_ok() -> bool:
+    """resident=auto turns the resident SMALL-path kernel on for a rank with a GPU of its own and
+    CPUs enough for its polling IO threads. Two ranks on one card measured at half the batcher
+    path's throughput (0.53 M vs 1.05-1.21 M req/s, profiles/r5_serve/README.md)."""
+    return not gpu_shared_by_ranks() and per_rank_cpus() >= RESIDENT_MIN_CPUS
+
+
 def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None,
                      comm: Optional[str] = None) -> DistInfo:
     """Initialise from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); no-op for 1 process."""

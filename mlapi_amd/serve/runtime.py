@@ -64,7 +64,10 @@ class EngineHandle:
         ec.inline_args = bool(config.inline_args)
         ec.idle_inline_rows = int(config.idle_inline_rows)
         res = str(config.resident).strip().lower()
-        ec.resident = 1 if res == "on" or (res == "auto" and self.device is not None) else 0
+        # auto: on for a GPU of this rank's own and CPUs for its polling IO threads (resident_auto_ok)
+        from mlapi_amd.parallel.comm import resident_auto_ok
+
+        ec.resident = 1 if res == "on" or (res == "auto" and self.device is not None and resident_auto_ok()) else 0
         ec.resident_depth = int(config.resident_depth)
         ec.resident_idle_polls = int(config.resident_idle_polls)
         ec.f32_gemv = bool(config.f32_gemv)

@@ -192,3 +192,42 @@ def test_resident_hot_reload_under_load(native, device):
     d = _stats_delta(s0, s1)
     assert d["resident_launches"] >= 8 and d["errors"] == 0, d
     assert d["resident_rows"] > 0, d
+
+
+def test_resident_auto_off_when_ranks_share_a_gpu(monkeypatch):
+    """resident=auto keeps the batcher path for ranks that share one device (p2p rehearsals): two
+    resident kernels on one card measured at half the batcher path's throughput."""
+    import torch
+
+    from mlapi_amd.parallel import comm
+
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert comm.gpu_shared_by_ranks()
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert not comm.gpu_shared_by_ranks()
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert not comm.gpu_shared_by_ranks()
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)  # CPU backend: nothing to share
+    assert not comm.gpu_shared_by_ranks()
+
+
+def test_per_rank_cpus_share_of_quota(monkeypatch):
+    """per_rank_cpus: the affinity mask, capped by the node's ranks' share of the cgroup quota."""
+    import os
+
+    from mlapi_amd.parallel import comm
+    from mlapi_amd.utils import threads
+
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(128)))
+    monkeypatch.setattr(threads, "cgroup_cpu_quota", lambda root="/sys/fs/cgroup": 16.0)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert comm.per_rank_cpus() == 8      # two ranks in a 16-CPU quota: resident stays off
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert comm.per_rank_cpus() == 16     # the 1-GPU box: on
+    monkeypatch.setattr(threads, "cgroup_cpu_quota", lambda root="/sys/fs/cgroup": None)
+    monkeypatch.setattr(os, "cpu_count", lambda: 256)
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(16)))
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert comm.per_rank_cpus() == 16     # 8 ranks pinned to 16 cores each on a 256-CPU node

@@ -1,7 +1,8 @@
 """Host plan of the f64-accumulating wide serving kernel (csrc/kernels/wide_plan.h, a CPU test):
 class blocks of 16, feature splits only when one split would need more than 32 wave steps, rows
 padded to a whole number of (4 waves x 16-byte loads x splits), 16-byte aligned, and one
-workspace region per 32-row group whose layout does not depend on B."""
+workspace region per row group (16 rows while the grid fits one block per CU, else 32) whose
+layout does not depend on B."""
 import pytest
 
 from mlapi_amd._native import C, available
@@ -32,8 +33,8 @@ def test_wide_workspace_is_per_row_group(dt):
     for F, K in ((256, 1000), (4096, 40), (300, 1)):
         one = C().linear_wide_workspace(1, dt, F, K)
         assert one % 256 == 0 and one >= (-(-K // 16)) * 32 * 32  # >= the row states of one group
-        for B in (1, 31, 32, 33, 100, 1000):
-            assert C().linear_wide_workspace(B, dt, F, K) == -(-B // 32) * one
+        for B in (1, 15, 16, 17, 31, 32, 33, 100, 1000):  # sized for 16-row groups: the most a launch uses
+            assert C().linear_wide_workspace(B, dt, F, K) == -(-B // 16) * one
 
 
 def test_wide_plan_rejects_other_dtypes():

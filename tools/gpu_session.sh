@@ -101,6 +101,20 @@ for s in $steps; do
         run "nonuma_on_io8_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads 8 --client-threads 4
         MLAPI_RESIDENT=off run "nonuma_off_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
       done ;;
+    serve_lgsplit)  # resident path: IO threads x load-generator threads (SPLITS="io:lg ..."), interleaved
+      for r in $(seq 1 "${RES_ROUNDS:-2}"); do
+        for sp in ${SPLITS:-8:4 8:5 7:5 8:6 7:6}; do
+          run "lgsplit_${sp/:/_}_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads ${sp%%:*} --client-threads ${sp##*:}
+        done
+      done ;;
+    serve_n2res)  # two ranks on the one GPU (P2P data plane): resident on / off x placement, interleaved
+      for r in $(seq 1 "${RES_ROUNDS:-2}"); do
+        for pin in auto on; do
+          for m in on off; do
+            MLAPI_COMM=p2p MLAPI_RESIDENT=$m run "n2_${m}_${pin}_r$r" 300 python -u bench.py --gpus 2 --steps 20 --warmup 3 --pin $pin
+          done
+        done
+      done ;;
     serve_res)  # the driver's exact command with the resident kernel on / off, interleaved
       for r in $(seq 1 "${RES_ROUNDS:-3}"); do
         for m in on off; do
