@@ -101,10 +101,10 @@ for s in $steps; do
         run "nonuma_on_io8_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads 8 --client-threads 4
         MLAPI_RESIDENT=off run "nonuma_off_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
       done ;;
-    serve_lgsplit)  # resident path: IO threads x load-generator threads (SPLITS="io:lg ..."), interleaved
+    serve_lgsplit)  # IO threads x load-generator threads (SPLITS="io:lg ...", LGARGS: extra bench args), interleaved
       for r in $(seq 1 "${RES_ROUNDS:-2}"); do
         for sp in ${SPLITS:-8:4 8:5 7:5 8:6 7:6}; do
-          run "lgsplit_${sp/:/_}_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads ${sp%%:*} --client-threads ${sp##*:}
+          run "lgsplit_${sp/:/_}_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads ${sp%%:*} --client-threads ${sp##*:} ${LGARGS:-}
         done
       done ;;
     serve_n2res)  # two ranks on the one GPU (P2P data plane): resident on / off x placement, interleaved
