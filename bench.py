@@ -152,7 +152,11 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         reqs, exp = make_workload(srv.runtime.handle.engine, model, names, rows, **oracle_kw)
         lg.workload(reqs, exp, rel_tol)
         barrier(info)  # every rank's listeners are in the group before any client connects
-        lg.connect("127.0.0.1", port, args.conns, args.client_threads)
+        # dispatch "source": this rank's load generator connects from an address of its own, so
+        # the acceptor keeps its connections together on one replica, in connect order (as client
+        # hosts of their own would be); "acceptor" deals every connection round robin over ranks
+        src = f"127.1.{info.rank // 250}.{info.rank % 250 + 1}" if args.dispatch == "source" else ""
+        lg.connect("127.0.0.1", port, args.conns, args.client_threads, source=src)
         if args.warmup:
             w = lg.run(args.warmup * args.reqs_per_conn, False)
             if w["failed"] or w["errors"]:
@@ -195,7 +199,7 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         barrier(info)
         s2 = srv.runtime.handle.stats()
         if info.is_main:
-            lg.connect("127.0.0.1", port, 1, 1)
+            lg.connect("127.0.0.1", port, 1, 1, source=src)
             lg.run(200, False)
             s2 = srv.runtime.handle.stats()
             r1 = lg.run(args.c1_requests, True)
@@ -252,8 +256,10 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
                     "placement": os.environ.get("MLAPI_PLACEMENT", "cores" if args.pinned_cpus else "none"),
                     "affinity_cpus": len(os.sched_getaffinity(0))},
         "requests_per_step": args.reqs_per_conn * args.conns * info.world,
-        "topology": ("one port for all ranks, connections dealt round robin by the group's acceptor "
-                     "(csrc/http/dispatch.h); one out-of-process load generator per rank"),
+        "topology": ("one port for all ranks, connections dealt by the group's acceptor "
+                     "(csrc/http/dispatch.h; dispatch=source: round robin over client addresses, a "
+                     "client address keeping its replica); one out-of-process load generator per "
+                     "rank, connecting from an address of its own"),
         "dispatch": srv.config.dispatch,
     }
     return ("requests_per_sec_whole_node", value, "req/s", elapsed, extra,
@@ -522,8 +528,10 @@ def main(argv=None) -> int:
     ap.add_argument("--client-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--io-threads", type=int, default=0, help="0 = auto from the CPUs per rank")
     ap.add_argument("--max-batch", type=int, default=256)
-    ap.add_argument("--dispatch", default="acceptor", choices=["acceptor", "reuseport"],
-                    help="serve: connections dealt round robin by one acceptor (default) or hashed by SO_REUSEPORT")
+    ap.add_argument("--dispatch", default="source", choices=["source", "acceptor", "reuseport"],
+                    help="serve: one acceptor deals connections round robin over client addresses, each "
+                         "rank's load generator connecting from its own (default: a client host keeps its "
+                         "replica), round robin per connection (acceptor), or hashed by SO_REUSEPORT")
     ap.add_argument("--c1-requests", type=int, default=3000)
     ap.add_argument("--rows", type=int, default=1 << 20)
     ap.add_argument("--batch", type=int, default=1024)

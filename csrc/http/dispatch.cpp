@@ -13,6 +13,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdint>
 #include <chrono>
 #include <cstddef>
 #include <cstring>
@@ -107,14 +108,15 @@ bool same_user(int fd) {
 }  // namespace
 
 ConnDispatcher::ConnDispatcher(std::string group, std::string host, int port, int backlog, int rank,
-                               std::function<void(int)> adopt, std::function<bool()> healthy)
+                               std::function<void(int)> adopt, std::function<bool()> healthy, bool source_affinity)
     : group_(std::move(group)),
       host_(std::move(host)),
       want_port_(port),
       backlog_(backlog),
       rank_(rank),
       adopt_(std::move(adopt)),
-      healthy_(std::move(healthy)) {
+      healthy_(std::move(healthy)),
+      source_affinity_(source_affinity) {
   wake_fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
   if (wake_fd_ < 0) throw std::runtime_error("dispatch: eventfd failed");
 }
@@ -286,32 +288,60 @@ bool ConnDispatcher::send_fd(Member& m, int fd) {
   }
 }
 
-// One connection to the next healthy target in round-robin order; a target whose channel fails
-// is dropped and the connection goes to the next one. No healthy target: the connection is closed
+// Hand fd to target i (0 = this process, i > 0 = members_[i - 1]) if it is healthy; a member
+// whose channel fails for good is dropped.
+bool ConnDispatcher::deliver(size_t i, int fd) {
+  if (i == 0) {
+    if (!self_healthy_) return false;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ++self_conns_;
+    }
+    received_.fetch_add(1, std::memory_order_relaxed);
+    adopt_(fd);
+    return true;
+  }
+  Member& m = members_[i - 1];
+  if (m.rank < 0 || !m.healthy) return false;
+  if (send_fd(m, fd)) {
+    std::lock_guard<std::mutex> lk(mu_);
+    ++m.conns;
+    close(fd);  // the member holds its own descriptor of the socket now
+    return true;
+  }
+  if (errno != EAGAIN && errno != EWOULDBLOCK) drop_member(i - 1);  // peer gone
+  return false;
+}
+
+// One connection to the next healthy target in round-robin order (source affinity: to the target
+// its client address already uses, while that one is healthy); a target whose channel fails is
+// dropped and the connection goes to the next one. No healthy target: the connection is closed
 // (what a client of an all-unhealthy SO_REUSEPORT group saw: refused).
-void ConnDispatcher::dispatch(int fd) {
+void ConnDispatcher::dispatch(int fd, const std::string& source) {
+  if (source_affinity_ && !source.empty()) {
+    const auto it = affinity_.find(source);
+    if (it != affinity_.end()) {
+      size_t i = 0;  // the target's current index (members come and go)
+      if (it->second >= 0) {
+        i = SIZE_MAX;
+        for (size_t k = 0; k < members_.size(); ++k)
+          if (members_[k].rank == it->second) i = k + 1;
+      }
+      if (i != SIZE_MAX && deliver(i, fd)) return;
+      affinity_.erase(it);  // gone or unhealthy: the address moves on with its next connection
+    }
+  }
   for (size_t attempt = 0; attempt < 2 * (members_.size() + 1) + 2; ++attempt) {
     const size_t n = members_.size() + 1;
     const size_t i = rr_++ % n;
-    if (i == 0) {
-      if (!self_healthy_) continue;
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        ++self_conns_;
+    const int rank = i == 0 ? -1 : members_[i - 1].rank;
+    if (deliver(i, fd)) {
+      if (source_affinity_ && !source.empty()) {
+        if (affinity_.size() >= 65536) affinity_.clear();  // bounded: a full table starts over
+        affinity_[source] = rank;
       }
-      received_.fetch_add(1, std::memory_order_relaxed);
-      adopt_(fd);
       return;
     }
-    Member& m = members_[i - 1];
-    if (m.rank < 0 || !m.healthy) continue;
-    if (send_fd(m, fd)) {
-      std::lock_guard<std::mutex> lk(mu_);
-      ++m.conns;
-      close(fd);  // the member holds its own descriptor of the socket now
-      return;
-    }
-    if (errno != EAGAIN && errno != EWOULDBLOCK) drop_member(i - 1);  // peer gone
   }
   close(fd);
 }
@@ -388,7 +418,16 @@ void ConnDispatcher::lead_loop() {
         if (c < 0) break;
         int one = 1;
         setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);  // never Nagle
-        dispatch(c);
+        std::string source;  // the client's address without its port (source affinity)
+        if (source_affinity_) {
+          char txt[INET6_ADDRSTRLEN] = {0};
+          if (ss.ss_family == AF_INET)
+            inet_ntop(AF_INET, &reinterpret_cast<sockaddr_in*>(&ss)->sin_addr, txt, sizeof txt);
+          else if (ss.ss_family == AF_INET6)
+            inet_ntop(AF_INET6, &reinterpret_cast<sockaddr_in6*>(&ss)->sin6_addr, txt, sizeof txt);
+          source = txt;
+        }
+        dispatch(c, source);
       }
     }
   }

@@ -17,6 +17,12 @@
 //  * member: recvmsg -> the fd goes to its next IO thread; it reports health changes as one byte
 //    ('H' healthy / 'U' unhealthy), so an unhealthy replica stops receiving connections and is
 //    re-admitted when its health probe succeeds (the round-2 leave/rejoin semantics).
+//  * source affinity (optional, `source_affinity`): the first connection from a client address
+//    takes the next target in round-robin order, and later connections from that address go to
+//    the same target while it stays healthy (IPVS's "source hashing", kept as a table: a client
+//    host's keep-alive connections land together, in their connect order). A host with many
+//    clients behind one address then loads one replica: off by default, `bench.py` turns it on
+//    with one source address per rank's load generator.
 //  * failover: a member whose channel breaks (the leader died or stopped) runs the election again;
 //    the winner re-binds the TCP port and the others re-join it. A restarted replica simply joins.
 //  * trust: both ends check SO_PEERCRED - a member must run as the leader's user (the abstract
@@ -30,6 +36,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 namespace mlapi {
@@ -45,7 +52,7 @@ class ConnDispatcher {
   // adopt(fd): give a connected TCP socket to this process's IO threads. healthy(): may this
   // process receive new connections.
   ConnDispatcher(std::string group, std::string host, int port, int backlog, int rank,
-                 std::function<void(int)> adopt, std::function<bool()> healthy);
+                 std::function<void(int)> adopt, std::function<bool()> healthy, bool source_affinity = false);
   ~ConnDispatcher();
   ConnDispatcher(const ConnDispatcher&) = delete;
   ConnDispatcher& operator=(const ConnDispatcher&) = delete;
@@ -72,7 +79,8 @@ class ConnDispatcher {
   void run();
   void lead_loop();
   void member_loop();
-  void dispatch(int fd);
+  void dispatch(int fd, const std::string& source);
+  bool deliver(size_t i, int fd);  // target i (0 = this process): true once the fd is handed over
   bool send_fd(Member& m, int fd);
   void drop_member(size_t i);
 
@@ -90,6 +98,8 @@ class ConnDispatcher {
   bool self_healthy_ = true;
   uint64_t self_conns_ = 0;
   size_t rr_ = 0;
+  bool source_affinity_ = false;
+  std::unordered_map<std::string, int> affinity_;  // client address -> target rank (-1 = leader)
   mutable std::mutex mu_;  // members_, self_* (read by targets())
   std::vector<Member> members_;
   std::thread th_;

@@ -46,7 +46,7 @@ struct LgConn {
 };
 
 Loadgen::Loadgen(const std::string& host, int port, const std::string& request, int conns, int threads,
-                 double timeout_s)
+                 double timeout_s, const std::string& source)
     : host_(host), port_(port), requests_{request}, timeout_s_(timeout_s) {
   if (conns < 1) conns = 1;
   if (threads < 1) threads = 1;
@@ -62,6 +62,17 @@ Loadgen::Loadgen(const std::string& host, int port, const std::string& request, 
   for (auto& c : conns_) {
     c = std::make_unique<LgConn>();
     c->fd = socket(res->ai_family, SOCK_STREAM | SOCK_CLOEXEC, IPPROTO_TCP);
+    if (c->fd >= 0 && !source.empty()) {
+      sockaddr_in src{};
+      src.sin_family = AF_INET;
+      src.sin_port = 0;
+      if (res->ai_family != AF_INET || inet_pton(AF_INET, source.c_str(), &src.sin_addr) != 1 ||
+          bind(c->fd, reinterpret_cast<sockaddr*>(&src), sizeof src) != 0) {
+        const int e = errno;
+        freeaddrinfo(res);
+        throw std::runtime_error("loadgen: bind to source " + source + " failed: " + strerror(e));
+      }
+    }
     if (c->fd < 0 || connect(c->fd, res->ai_addr, res->ai_addrlen) != 0) {
       const int e = errno;
       freeaddrinfo(res);

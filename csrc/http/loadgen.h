@@ -21,9 +21,12 @@ struct LgConn;
 
 class Loadgen {
  public:
-  // Opens `conns` keep-alive connections (distributed over `threads` epoll loops).
+  // Opens `conns` keep-alive connections (distributed over `threads` epoll loops: connection c on
+  // loop c % threads), one after the other, from local address `source` when it is not empty (an
+  // IPv4 literal: on loopback every 127.x.y.z works, so several load generators on one host look
+  // like several client hosts to a source-affinity dispatcher).
   Loadgen(const std::string& host, int port, const std::string& request, int conns, int threads,
-          double timeout_s = 30.0);
+          double timeout_s = 30.0, const std::string& source = "");
   ~Loadgen();
   // Distinct requests cycled per connection (connection c starts at entry c % n), each with the
   // exact response body it must produce; empty `expected` = status-only checking.

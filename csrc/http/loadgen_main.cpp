@@ -5,7 +5,7 @@
 //
 //   pin <cpu>,<cpu>,...                        sched_setaffinity (threads created later inherit it)
 //   workload <path> [rel_tol]                  "MLW1\n" then per entry "<req_len> <exp_len>\n" + bytes
-//   connect <host> <port> <conns> <threads> <timeout_s>
+//   connect <host> <port> <conns> <threads> <timeout_s> [<source address>]
 //   run <requests_per_conn> <record 0|1>       -> {"completed":..,"p50_ns":..,...}
 //   close | quit
 #include <sched.h>
@@ -102,9 +102,11 @@ int main() {
         std::string host;
         int port = 0, conns = 1, threads = 1;
         double timeout_s = 30;
+        std::string source;
         in >> host >> port >> conns >> threads >> timeout_s;
+        if (!(in >> source) || source == "-") source.clear();  // optional local (source) address
         if (req.empty()) throw std::runtime_error("connect before workload");
-        lg = std::make_unique<Loadgen>(host, port, req[0], conns, threads, timeout_s);
+        lg = std::make_unique<Loadgen>(host, port, req[0], conns, threads, timeout_s, source);
         lg->set_workload(req, exp, rel_tol);
         reply("{\"ok\":true}");
       } else if (cmd == "run") {

@@ -1248,14 +1248,14 @@ int HttpServer::listeners() const {
 void HttpServer::start() {
   if (started_) return;
   (void)tsc_ns_per_tick();  // calibrate the stage clock before any IO thread needs it
-  if (cfg_.dispatch == "acceptor") {
+  if (cfg_.dispatch == "acceptor" || cfg_.dispatch == "source") {
     acceptor_ = true;
     for (int i = 0; i < cfg_.io_threads; ++i) threads_.push_back(std::make_unique<IoThread>(this, i, -1));
     for (auto& t : threads_) t->start();
     dispatcher_ = std::make_unique<ConnDispatcher>(
         cfg_.dispatch_group, cfg_.host, cfg_.port, cfg_.backlog, cfg_.dispatch_rank,
         [this](int fd) { threads_[adopt_rr_.fetch_add(1, std::memory_order_relaxed) % threads_.size()]->adopt(fd); },
-        [this] { return accepting(); });
+        [this] { return accepting(); }, cfg_.dispatch == "source");
     try {
       dispatcher_->start();
     } catch (...) {
@@ -1269,7 +1269,7 @@ void HttpServer::start() {
     started_ = true;
     return;
   }
-  if (cfg_.dispatch != "reuseport") throw std::invalid_argument("dispatch must be acceptor or reuseport");
+  if (cfg_.dispatch != "reuseport") throw std::invalid_argument("dispatch must be acceptor, source or reuseport");
   int port = cfg_.port;
   std::vector<int> fds;
   try {

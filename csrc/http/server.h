@@ -73,8 +73,9 @@ struct ServerConfig {
   int io_spin_max_conns = 2;
   bool stage_timing = true;  // per-stage CPU accounting + HTTP latency histogram (a few rdtsc per request)
   // Connection dispatch (dispatch.h): "acceptor" (default) = one acceptor per serving group hands
-  // every new connection to the next healthy replica / IO thread, round robin; "reuseport" = every
-  // IO thread listens on the port itself and the kernel hashes connections over the listeners.
+  // every new connection to the next healthy replica / IO thread, round robin; "source" = the same
+  // with source-address affinity (a client address keeps its replica); "reuseport" = every IO
+  // thread listens on the port itself and the kernel hashes connections over the listeners.
   std::string dispatch = "acceptor";
   std::string dispatch_group;  // "" = named after host:port
   int dispatch_rank = 0;       // this replica's rank (reported to the group's leader)

@@ -132,8 +132,10 @@ class LoadgenProcess:
         finally:
             os.unlink(path)
 
-    def connect(self, host: str, port: int, conns: int, threads: int, timeout_s: float = 60.0) -> dict:
-        return self.cmd(f"connect {host} {int(port)} {int(conns)} {int(threads)} {timeout_s}")
+    def connect(self, host: str, port: int, conns: int, threads: int, timeout_s: float = 60.0,
+                source: str = "") -> dict:
+        """source: local IPv4 address to connect from ("" = the kernel's choice)."""
+        return self.cmd(f"connect {host} {int(port)} {int(conns)} {int(threads)} {timeout_s} {source or '-'}")
 
     def run(self, requests_per_conn: int, record: bool = True) -> dict:
         return self.cmd(f"run {int(requests_per_conn)} {1 if record else 0}")

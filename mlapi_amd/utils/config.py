@@ -89,7 +89,8 @@ class Config:
     access_log: bool = False                  # uvicorn-format access log lines on stderr
     health_dispatch: str = "auto"             # auto (DP, world > 1) | on | off: unhealthy ranks leave the port
     dispatch: str = "acceptor"                # acceptor: one acceptor per port hands connections round robin to
-                                              # the replicas / IO threads (csrc/http/dispatch.h) | reuseport: kernel hash
+                                              # the replicas / IO threads (csrc/http/dispatch.h) | source: the same,
+                                              # a client address keeping its replica | reuseport: kernel hash
     dispatch_group: str = ""                  # acceptor group name ("" = named after host:port)
     admin: str = "loopback"                   # POST /admin/*: loopback (local clients only) | on | off
     # observability

@@ -40,13 +40,13 @@ def _post(port, body=A1, keep=None):
     return int(head.split()[1]), s
 
 
-def _server(port, rank, io_threads=2, group=""):
+def _server(port, rank, io_threads=2, group="", dispatch="acceptor"):
     from mlapi_amd.serve.server import NativeServer
     from mlapi_amd.utils.config import Config
 
     os.environ["RANK"] = str(rank)  # the replica's rank, reported to the group's leader
     try:
-        srv = NativeServer(Config.from_env(port=port, device="cpu", io_threads=io_threads, dispatch="acceptor",
+        srv = NativeServer(Config.from_env(port=port, device="cpu", io_threads=io_threads, dispatch=dispatch,
                                            dispatch_group=group)).start()
     finally:
         os.environ.pop("RANK", None)
@@ -85,6 +85,50 @@ def test_acceptor_round_robin_over_replicas_and_threads(iris_cwd):
         assert [s.http.stats()["connections"] for s in srvs] == [10, 10, 10]
         for s in socks:
             s.close()
+    finally:
+        for s in srvs:
+            s.stop()
+
+
+def _post_from(port, source):
+    s = socket.socket()
+    s.bind((source, 0))
+    s.settimeout(10)
+    s.connect(("127.0.0.1", port))
+    return _post(port, keep=s)
+
+
+def test_source_affinity_keeps_a_client_address_on_one_replica(iris_cwd):
+    """dispatch=source: three client addresses x 8 connections, interleaved, over three replicas of
+    4 IO threads -> each address's 8 connections on ONE replica (a different one per address, in
+    first-seen round-robin order), and inside it on the IO threads in connect order (2 per thread:
+    a load generator with 4 threads keeps each thread's connections on one IO thread)."""
+    port = _free_port()
+    srvs = [_server(port, r, io_threads=4, dispatch="source") for r in range(3)]
+    try:
+        t0 = time.time()
+        while len(srvs[0].http.stats()["dispatch"]["targets"]) < 3:
+            assert time.time() - t0 < 10
+            time.sleep(0.01)
+        socks = []
+        for k in range(8):
+            for a in ("127.1.0.1", "127.1.0.2", "127.1.0.3"):
+                st, s = _post_from(port, a)
+                assert st == 200
+                socks.append(s)
+        tg = {r: n for r, n, _ in srvs[0].http.stats()["dispatch"]["targets"]}
+        assert tg == {0: 8, 1: 8, 2: 8}, tg
+        assert [s.http.stats()["connections"] for s in srvs] == [8, 8, 8]
+        for s in socks:
+            s.close()
+        # a new address takes the next replica in round-robin order (the fourth: replica 0 again);
+        # a known one stays on its replica (127.1.0.2, seen second: replica 1)
+        st, s = _post_from(port, "127.1.0.4")
+        s.close()
+        st, s2 = _post_from(port, "127.1.0.2")
+        s2.close()
+        tg = {r: n for r, n, _ in srvs[0].http.stats()["dispatch"]["targets"]}
+        assert tg == {0: 9, 1: 9, 2: 8}, tg
     finally:
         for s in srvs:
             s.stop()
@@ -190,7 +234,8 @@ def _bench(args, env=None, timeout=300):
 
 def test_bench_self_launches_n_ranks():
     """`python bench.py --cpu --gpus 4` (no torchrun): the bench starts 4 ranks itself; the line says
-    n_gpus 4 / dp4, every rank served an equal share (round-robin dispatch), and the communicator
+    n_gpus 4 / dp4, every rank served an equal share (source-affinity dispatch: one load generator per
+    replica), and the communicator
     evidence fields are present."""
     r = _bench(["--cpu", "--gpus", "4", "--steps", "3", "--warmup", "1", "--reqs-per-conn", "64",
                 "--c1-requests", "100"])
@@ -217,12 +262,12 @@ def test_bench_self_launches_n_ranks():
     # engine-thread stage clocks per GPU batch (zero on the CPU backend, which has no GPU batches)
     assert set(cb["batcher_us_per_batch"]) == {"take", "slot", "launch", "book"}
     assert set(cb["completer_us_per_batch"]) == {"wait_gpu", "deliver"}
-    assert d["dispatch"] == "acceptor"
+    assert d["dispatch"] == "source"  # each rank's load generator from an address of its own
 
 
 def test_bench_self_launches_eight_ranks():
     """The driver's whole-node shape, rehearsed on the CPU: `bench.py --cpu --gpus 8` starts 8
-    ranks (gloo), the acceptor deals connections round robin to all of them, and the line reports
+    ranks (gloo), the acceptor deals the load generators' client addresses round robin to all of them, and the line reports
     dp8 with 8 balanced per-rank counts."""
     r = _bench(["--cpu", "--gpus", "8", "--steps", "2", "--warmup", "1", "--reqs-per-conn", "16",
                 "--c1-requests", "50"], timeout=600)

@@ -15,7 +15,7 @@
 #   serve_idle    serve with the idle-engine fast path on (8 rows) / off, interleaved x2
 #   serve_abenv   serve with AB_VAR set to each of AB_VALS, interleaved x2
 #   serve_compl   serve with COMPLS completer threads (default "1 2"), interleaved x2
-#   dispatch_ab   serve with the round-robin acceptor vs SO_REUSEPORT dispatch, N=1 and N=2 (p2p), x2
+#   dispatch_ab   serve with source-affinity vs per-connection round-robin dispatch (DISPATCHES), N=1 and N=2 (p2p), x2
 #   serve_pin     serve with the rank pinned to physical cores (server / load generator apart) vs unpinned, x2
 #   serve_spin    serve with busy-polling IO threads / spinning batcher+completer (SPINS="0 50"), interleaved x2
 #   selfl         bench.py --gpus 2 self-launched (p2p on one device) + the refusal without p2p
@@ -177,9 +177,9 @@ for s in $steps; do
           MLAPI_COMPLETERS=$c run "serve_compl${c}_r$r" 300 python -u bench.py --steps 60 --warmup 5
         done
       done ;;
-    dispatch_ab)  # connection dispatch: round-robin acceptor vs SO_REUSEPORT hash, interleaved x2 (N=1 and p2p N=2)
+    dispatch_ab)  # connection dispatch (DISPATCHES, default "source acceptor"), interleaved x2 (N=1 and p2p N=2)
       for r in 1 2; do
-        for d in acceptor reuseport; do
+        for d in ${DISPATCHES:-source acceptor}; do
           run "serve_dispatch_${d}_r$r" 300 python -u bench.py --steps 60 --warmup 5 --dispatch $d
           MLAPI_COMM=p2p run "serve_dispatch_${d}_n2_r$r" 300 python -u bench.py --gpus 2 --steps 30 --warmup 3 --dispatch $d
         done
