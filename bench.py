@@ -586,8 +586,10 @@ def main(argv=None) -> int:
         return 2
     local = int(os.environ.get("LOCAL_WORLD_SIZE", info.world))
     pinned = []
-    if args.pin == "auto" and info.world == 1 and info.device is not None:
-        args.pin = "numa"  # measured: numa 1.51-1.54 M vs unpinned 1.35-1.53 M req/s (profiles/r5_serve/)
+    if args.pin == "auto" and info.device is not None:
+        # measured: numa 1.51-1.54 M vs unpinned 1.35-1.53 M req/s (profiles/r5_serve/); at N > 1
+        # under torchrun too (bench's own launcher already placed the rank: MLAPI_PLACEMENT set)
+        args.pin = "numa"
     if args.pin == "numa" and os.environ.get("MLAPI_PLACEMENT") != "numa":
         # this rank and its load generator on the GPU's NUMA node (a node mask, not core slices):
         # loopback TCP, the pinned request rings and the GPU's host link stay on one socket
@@ -611,9 +613,11 @@ def main(argv=None) -> int:
         # MI355X box share: 6 + 6 threads -> 519k req/s vs 3 + 3 -> 270k; tools/gpu_session.sh threads).
         # The CPU budget is the cgroup quota, not the affinity mask (a 1-GPU box: 256 CPUs in the
         # mask, cpu.max = 16 cores), shared by the ranks of this node.
-        from mlapi_amd.utils.threads import effective_cpus
+        from mlapi_amd.parallel.comm import per_rank_cpus
 
-        per_rank = max(4, len(pinned) if pinned else effective_cpus() // max(1, local))
+        # core slice: the rank's own; NUMA-node mask: shared by the ranks on that node; both capped
+        # by the rank's share of the cgroup quota
+        per_rank = max(4, len(pinned) if pinned else per_rank_cpus())
         # measured on a 16-CPU share with the out-of-process load generator. Resident SMALL path
         # (round 5, profiles/r5_serve/ s22-s26, interleaved): equal IO and load-generator thread
         # counts win - the acceptor deals connection k to IO thread k % io and the load generator

@@ -72,18 +72,27 @@ def gpu_shared_by_ranks() -> bool:
 
 
 def per_rank_cpus() -> int:
-    """CPUs one rank of this node can keep busy: its affinity mask, capped by its share of the
-    cgroup quota (or of the machine) over the node's ranks."""
+    """CPUs one rank of this host can keep busy: its share of its affinity mask (a core slice is the
+    rank's own; a NUMA-node mask is shared by the ranks whose GPUs sit on that node; an unpinned
+    mask by every rank), capped by its share of the cgroup quota (or of the machine)."""
     from mlapi_amd.utils.threads import cgroup_cpu_quota
 
     local_world = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     try:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         aff = os.cpu_count() or 1
+    placement = os.environ.get("MLAPI_PLACEMENT", "none")
+    if placement == "numa":
+        from mlapi_amd.utils.affinity import gpu_numa_nodes, ranks_on_node
+
+        share = ranks_on_node(local_rank, local_world, gpu_numa_nodes())
+    else:
+        share = 1 if placement == "cores" else local_world
     q = cgroup_cpu_quota()
     total = int(q) if q is not None else (os.cpu_count() or 1)
-    return max(1, min(aff, total // local_world))
+    return max(1, min(aff // share, total // local_world))
 
 
 RESIDENT_MIN_CPUS = 12  # the resident path's IO threads poll their records: per_rank_cpus() / 2 of them

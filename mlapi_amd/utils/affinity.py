@@ -262,3 +262,14 @@ def numa_rank_cpus(local_rank: int, nodes: List[Optional[int]], cpus: Optional[L
         return []
     allowed = set(sorted(os.sched_getaffinity(0)) if cpus is None else cpus)
     return [c for c in node_cpus(nodes[local_rank], sysnode) if c in allowed]
+
+
+def ranks_on_node(local_rank: int, local_world: int, nodes: List[Optional[int]]) -> int:
+    """How many of this host's ranks (rank r uses GPU r % len(nodes)) sit on local_rank's GPU's NUMA
+    node - the ranks that share its node mask under numa placement. local_world when the nodes are
+    unknown (every rank then shares one mask)."""
+    if not nodes or nodes[local_rank % len(nodes)] is None:
+        return max(1, local_world)
+    mine = nodes[local_rank % len(nodes)]
+    return max(1, sum(1 for r in range(local_world) if nodes[r % len(nodes)] == mine))
+

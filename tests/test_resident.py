@@ -230,4 +230,17 @@ def test_per_rank_cpus_share_of_quota(monkeypatch):
     monkeypatch.setattr(os, "cpu_count", lambda: 256)
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(16)))
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setenv("MLAPI_PLACEMENT", "cores")
     assert comm.per_rank_cpus() == 16     # 8 ranks pinned to 16 cores each on a 256-CPU node
+    # numa placement: a 96-CPU node mask shared by the 4 ranks whose GPUs sit on that node
+    from mlapi_amd.utils import affinity
+
+    monkeypatch.setattr(affinity, "gpu_numa_nodes", lambda *a, **k: [0, 0, 0, 0, 1, 1, 1, 1])
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(96)))
+    monkeypatch.setenv("MLAPI_PLACEMENT", "numa")
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    assert comm.per_rank_cpus() == 24
+    monkeypatch.setattr(threads, "cgroup_cpu_quota", lambda root="/sys/fs/cgroup": 128.0)
+    assert comm.per_rank_cpus() == 16     # capped by the rank's share of a 128-CPU quota
+    monkeypatch.delenv("MLAPI_PLACEMENT")
+    assert comm.per_rank_cpus() == 12     # unplaced: the 96-CPU mask shared by all 8 ranks
