@@ -9,11 +9,11 @@
 //      chunk by chunk, straight into G = softmax(z) - onehot(y) (OvR: sigmoid(z) - onehot) as bf16
 //      [B][Kp] (Kp = K rounded up to 64, zero padded) plus the block's {loss, correct}: the B x K
 //      f32 logits never reach HBM (round 3 wrote and re-read them between two more launches);
-//   2. gdw_gemm_kernel: dW slabs[row group][K][F_aug] = G^T X_aug over the group's rows -
+//   2. gdw_gemm_big_kernel: dW slabs[row group][K][F_aug] = G^T X_aug over the group's rows -
 //      v_mfma_f32_16x16x32_bf16 with M = classes, N = features, K = rows: both operands are
-//      row-major [rows][*] tiles, so each is staged in LDS (32 rows x 64 columns, one 16-byte load
-//      per thread) and read transposed with ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane
-//      group, two reads = the 8 rows of a lane's k-slice);
+//      row-major [rows][*] tiles, so each is staged in LDS (32 rows x 128 columns, 16-byte loads)
+//      and read transposed with ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group, two
+//      reads = the 8 rows of a lane's k-slice);
 //   3. launch_gdw_reduce: deterministic slab sum + fused SGD update (+ in-kernel DP exchange).
 // (Round 3's five launches - row stats, f32 logits through HBM, a wave-per-row G pass - lost to
 // this path: 1.79 -> 1.0 ms per step at F = 1024, docs/PERFORMANCE.md; removed in round 5.)
@@ -35,93 +35,29 @@ typedef __attribute__((ext_vector_type(4))) float wf32x4_t;
 typedef __attribute__((address_space(3))) wi16x4_t lds_i16x4_t;
 
 constexpr int TILE_ROWS = 32;        // MFMA k-step (rows)
-constexpr int TILE_COLS = 64;        // classes / features per block tile
 
 
-// ---- 4. dW slabs = G^T X_aug per row group
-// grid (Kp / 64, ceil(F_aug / 64), row_groups); a wave owns 16 classes x 64 features (4 N-tiles).
-__global__ __launch_bounds__(256) void gdw_gemm_kernel(const uint16_t* __restrict__ G, int Kp, const uint16_t* __restrict__ X,
-                                                       int64_t ldx, int F_aug, int64_t B, int K, int64_t rows_per_group,
-                                                       float* __restrict__ slabs) {
-  __shared__ __attribute__((aligned(16))) uint16_t gt[TILE_ROWS][TILE_COLS];
-  __shared__ __attribute__((aligned(16))) uint16_t xt[TILE_ROWS][TILE_COLS];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c0 = blockIdx.x * TILE_COLS, f0 = blockIdx.y * TILE_COLS;
-  const int64_t r_begin = (int64_t)blockIdx.z * rows_per_group;
-  const int64_t r_end = min(B, r_begin + rows_per_group);
-  // staging: thread t loads 16 B = 8 columns of row t / 8, column chunk t % 8
-  const int sr = threadIdx.x >> 3, sc = (threadIdx.x & 7) * 8;
-  // transposed reads: lane 4q + p of group g supplies row 8g + q (+4), columns base + 4p
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  wf32x4_t acc[4] = {};
-  // the next tile's 16-byte loads are issued before this tile's LDS reads and MFMAs (register
-  // double buffer): the global round trip overlaps the MFMAs instead of preceding them
-  auto load_tile = [&](int64_t r0, uint4& gv, uint4& xv) {
-    const int64_t r = r0 + sr;
-    gv = uint4{0, 0, 0, 0};
-    xv = uint4{0, 0, 0, 0};
-    if (r < r_end) {
-      gv = *reinterpret_cast<const uint4*>(G + r * Kp + c0 + sc);  // Kp % 64 == 0: always in bounds
-      if (f0 + sc + 8 <= ldx) {
-        xv = *reinterpret_cast<const uint4*>(X + r * ldx + f0 + sc);
-      } else {
-        uint16_t tmp[8];
-        for (int e = 0; e < 8; ++e) tmp[e] = f0 + sc + e < ldx ? X[r * ldx + f0 + sc + e] : 0;
-        __builtin_memcpy(&xv, tmp, sizeof xv);
-      }
-    }
-  };
-  uint4 gn, xn;
-  load_tile(r_begin, gn, xn);
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += TILE_ROWS) {
-    const uint4 gv = gn, xv = xn;
-    if (r0 + TILE_ROWS < r_end) load_tile(r0 + TILE_ROWS, gn, xn);
-    __syncthreads();  // the previous tile's reads are done
-    *reinterpret_cast<uint4*>(&gt[sr][sc]) = gv;
-    *reinterpret_cast<uint4*>(&xt[sr][sc]) = xv;
-    __syncthreads();
-    // A: 16 classes (wave * 16 + i) x 8 rows (8g + j)
-    const wi16x4_t a_lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&gt[8 * g + q][wave * 16 + 4 * p]);
-    const wi16x4_t a_hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&gt[8 * g + 4 + q][wave * 16 + 4 * p]);
-    const wi16x4_t av[2] = {a_lo, a_hi};
-    const wbf16x8_t a = __builtin_bit_cast(wbf16x8_t, av);
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const wi16x4_t b_lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&xt[8 * g + q][n * 16 + 4 * p]);
-      const wi16x4_t b_hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&xt[8 * g + 4 + q][n * 16 + 4 * p]);
-      const wi16x4_t bv[2] = {b_lo, b_hi};
-      acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(wbf16x8_t, bv), acc[n], 0, 0, 0);
-    }
-  }
-  // C layout: class c0 + wave * 16 + 4g + i (register i), feature f0 + 16n + (lane & 15)
-  float* slab = slabs + (int64_t)blockIdx.z * K * F_aug;
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int f = f0 + n * 16 + (lane & 15);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = c0 + wave * 16 + 4 * g + i;
-      if (c < K && f < F_aug) slab[(int64_t)c * F_aug + f] = acc[n][i];
-    }
-  }
-}
-
-// ---- 4'. the same G^T X_aug with (64 WC) x 128 block tiles (default): a wave owns 64 classes x 64
-// features (4 x 4 MFMA tiles, 64 accumulator VGPRs), the block 2 WC waves, so each 16-byte element
-// staged through LDS feeds 2-4x the MFMAs of the 64 x 64 kernel and G / X are re-read from L2
-// correspondingly less often (the 64 x 64 kernel is L2-bandwidth bound: G is read once per feature
-// tile, X once per class tile). LDS double buffered (one barrier per 32-row k-step); rows padded
-// by 8 elements. WC = 2 (128 x 128 tiles, 256 threads) is the one launched: WC = 4 (256 x 128, 512
-// threads) measured 1.05 vs 0.99 ms per F = 1024 training step (profiles/r4_train/tsm_f1024_t256_*).
+// ---- 4. dW slabs = G^T X_aug per row group, (64 WC) x 128 block tiles: a wave owns 64 classes x
+// 64 features (4 x 4 MFMA tiles, 64 accumulator VGPRs), the block 2 WC waves, so each 16-byte
+// element staged through LDS feeds 2-4x the MFMAs of round 3's 64 x 64 tiles (514 -> 357 us at
+// F = 1024; that kernel left the build in round 5) and G / X are re-read from L2 correspondingly
+// less often. LDS double buffered (one barrier per 32-row k-step). WC = 2 (128 x 128 tiles, 256
+// threads) is the one launched: WC = 4 (256 x 128, 512 threads) measured 1.05 vs 0.99 ms per
+// F = 1024 training step (profiles/r4_train/tsm_f1024_t256_*).
+// Rows padded by 8 elements. The counters show 1.6 LDS bank conflicts per LDS instruction
+// (profiles/r5_pmc/summary_big.md); padding rows to 16 elements instead (8 banks per row) left both
+// the count (1.600) and the F = 1024 step (0.971 vs 0.972 ms, interleaved x3) unchanged
+// (profiles/r5_train/s37_*), so the conflicts are not the row stride's and not on the critical path.
 constexpr int TF128 = 128;
-constexpr int XROW = TF128 + 8;
+constexpr int LDS_PAD = 8;
+constexpr int XROW = TF128 + LDS_PAD;
 
 template <int WC>
 __global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* __restrict__ G, int Kp,
                                                                const uint16_t* __restrict__ X, int64_t ldx, int F_aug,
                                                                int64_t B, int K, int64_t rows_per_group,
                                                                float* __restrict__ slabs) {
-  constexpr int TC = 64 * WC, NTHR = 128 * WC, GROW = TC + 8;
+  constexpr int TC = 64 * WC, NTHR = 128 * WC, GROW = TC + LDS_PAD;
   constexpr int JX = 512 / NTHR;  // X chunks per thread (32 rows x 16 chunks of 8 columns)
   static_assert(32 * TC / 8 == 2 * NTHR, "two G chunks per thread");
   __shared__ __attribute__((aligned(16))) uint16_t gt[2][TILE_ROWS][GROW];
@@ -216,15 +152,6 @@ __global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* 
     }
 }
 
-// G^T X class-tile width: 128 (default); MLAPI_GDW_TILE=64 = the round-3 kernel (for the A/B)
-int gdw_tile() {
-  static const int v = [] {
-    const char* e = std::getenv("MLAPI_GDW_TILE");
-    return e != nullptr && std::atoi(e) == 64 ? 64 : 128;
-  }();
-  return v;
-}
-
 struct WideLayout {
   size_t g_off, dw_off, stat_off, total;
   int Kp, row_groups, g_blocks;
@@ -234,9 +161,9 @@ struct WideLayout {
 WideLayout wide_layout(int64_t B, int K, int F) {
   WideLayout L{};
   const int F_aug = F + 8;
-  const int T = gdw_tile();  // G's columns padded to the class tile
+  const int T = 128;  // G's columns padded to the class tile
   L.Kp = (K + T - 1) / T * T;
-  const int TFw = T == TILE_COLS ? TILE_COLS : TF128;  // feature tile width
+  const int TFw = TF128;  // feature tile width
   const int tiles = (L.Kp / T) * ((F_aug + TFw - 1) / TFw);
   int64_t rg = (2048 + tiles - 1) / tiles;
   const int64_t max_rg = (B + 255) / 256;
@@ -285,16 +212,9 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
   launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, stream);
   const int g_blocks = L.g_blocks;
   const int F_aug = F + 8;
-  const int T = gdw_tile();
-  if (T == 64) {
-    const dim3 grid((unsigned)(L.Kp / TILE_COLS), (unsigned)((F_aug + TILE_COLS - 1) / TILE_COLS), (unsigned)L.row_groups);
-    hipLaunchKernelGGL(gdw_gemm_kernel, grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug), ldx,
-                       F_aug, B, K, L.rows_per_group, slabs);
-  } else {
-    const dim3 grid((unsigned)(L.Kp / T), (unsigned)((F_aug + TF128 - 1) / TF128), (unsigned)L.row_groups);
-    hipLaunchKernelGGL(gdw_gemm_big_kernel<2>, grid, dim3(256), 0, stream, G, L.Kp,
-                       static_cast<const uint16_t*>(X_aug), ldx, F_aug, B, K, L.rows_per_group, slabs);
-  }
+  const dim3 grid((unsigned)(L.Kp / 128), (unsigned)((F_aug + TF128 - 1) / TF128), (unsigned)L.row_groups);
+  hipLaunchKernelGGL(gdw_gemm_big_kernel<2>, grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug),
+                     ldx, F_aug, B, K, L.rows_per_group, slabs);
   MLAPI_HIP_CHECK(hipGetLastError());
   launch_gdw_reduce(slabs, L.row_groups, K, F_aug, dW_out, stat_slabs, g_blocks, stats_out, update, dp,
                     dp_timeout_ms, stream);

@@ -317,6 +317,11 @@ for s in $steps; do
           || stop "serve_newenv_r$r" $? "$O/serve_newenv_r$r.log"
         tail -1 "$O/serve_newenv_r$r.log" | cut -c1-200
       done ;;
+    prev_ab)  # interleaved x3: the previous build copied to ab_prev/ vs the working tree, same bench args (PREV_ARGS)
+      for r in 1 2 3; do
+        run "prev_old_r$r" 300 python -c "import sys, runpy; sys.path.insert(0, 'ab_prev'); sys.argv = ['bench.py'] + sys.argv[1:]; runpy.run_path('bench.py', run_name='__main__')" ${PREV_ARGS}
+        run "prev_new_r$r" 300 python -u bench.py ${PREV_ARGS}
+      done ;;
     gemm_ab)
       for r in 1 2 3; do
         run "gemm_old_r$r" 120 python -c "import sys, runpy; sys.path.insert(0, 'ab_old'); sys.argv = ['bench.py'] + sys.argv[1:]; runpy.run_path('bench.py', run_name='__main__')" \
