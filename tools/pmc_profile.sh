@@ -18,6 +18,7 @@ declare -A GROUPS_=(
   [active]="SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM"
   [l2]="TCC_HIT_sum TCC_MISS_sum"
   [ldswait]="SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_MISC SQ_INSTS_SALU"
+  [l2req]="TCP_TCC_READ_REQ_sum TCC_REQ_sum TCC_READ_sum"
 )
 GROUP_ORDER="${PMC_GROUPS:-fetch write mfma lds valu stall active l2 ldswait}"
 BENCHES="${PMC_BENCHES:-gemv:--mode gemv --steps 5 --warmup 1|gemm:--mode gemm --steps 5 --warmup 1|gemm_big:--mode gemm --batch 262144 --steps 5 --warmup 1|train:--mode train --steps 5 --warmup 1|train_softmax:--mode train_softmax --steps 5 --warmup 1}"

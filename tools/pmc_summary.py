@@ -82,3 +82,18 @@ print(" Kernel time here is measured under counter collection (serialised dispat
 print(" bf16 TFLOP/s = SQ_INSTS_VALU_MFMA_MOPS_BF16 x 512 / kernel time (dense peak ~2500).")
 print(" wait / active % = share of SQ_WAVE_CYCLES (summed over waves) spent waiting on anything /")
 print(" on instruction issue, or with a VALU / LDS / VMEM instruction in flight.")
+
+# L2 request rates (group l2req): vector-L1 -> L2 read requests and all L2 requests per µs, and the
+# bytes they imply at 128 B per request (gfx950 L2 line) - the L2 bandwidth a kernel draws
+rows = [(b, k, cs) for (b, k), cs in sorted(vals.items()) if "TCC_REQ_sum" in cs or "TCP_TCC_READ_REQ_sum" in cs]
+if rows:
+    print()
+    print("| bench | kernel | µs | L1->L2 read req / µs | L2 req / µs | L2 read req / µs | L1->L2 read GB/s @128 B |")
+    print("|---|---|---|---|---|---|---|")
+    for b, k, cs in rows:
+        us = mean(dur.get((b, k), []))
+        r1 = mean(cs.get("TCP_TCC_READ_REQ_sum", [])) / us
+        r2 = mean(cs.get("TCC_REQ_sum", [])) / us
+        r3 = mean(cs.get("TCC_READ_sum", [])) / us
+        print(f"| {b} | `{k[:60]}` | {us:.1f} | {r1:.0f} | {r2:.0f} | {r3:.0f} | {r1 * 128 / 1e3:.0f} |")
+
