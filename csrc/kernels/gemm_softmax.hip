@@ -1209,10 +1209,21 @@ __device__ __forceinline__ uint16_t bf16_rne(float f) {
   return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
 }
 
-template <int KS, int NT, int MODE, bool OVR>
+// XLDS (F in (512, XLDS_FMAX], large B): the block's X rows are staged in LDS ONCE (all F; 64 rows
+// x (F + 8) bf16 <= 132 KB) and every wave reads its slices from there, instead of each of the 8
+// waves re-loading each slice from L2 for each of its class chunks (16x the X traffic at F = 1024);
+// the registers that held X then double-buffer the W slices (the next slice's W loads are in
+// flight under this slice's MFMAs). The MODE 5 second pass reuses the staged X.
+constexpr int XLDS_ROWS = 64;
+constexpr int XLDS_FMAX = 1024;
+constexpr int XLDS_PITCH = XLDS_FMAX + 8;
+
+template <int KS, int NT, int MODE, bool OVR, bool XLDS = false>
 __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
   constexpr int ROWS = 16 * NT;
   constexpr int SLICE = KS * 32;
+  static_assert(!XLDS || ROWS == XLDS_ROWS, "XLDS stages 64 rows");
+  __shared__ __attribute__((aligned(16))) uint16_t xs[XLDS ? XLDS_ROWS : 1][XLDS ? XLDS_PITCH : 8];
   __shared__ float4 part[ROWS_MAX_WAVES][ROWS];
   __shared__ float lse_s[MODE == 5 ? ROWS : 1], hit_s[MODE == 5 ? ROWS : 1], wsum_s[MODE == 5 ? ROWS_MAX_WAVES : 1];
   const int lane = threadIdx.x & 63;
@@ -1230,13 +1241,29 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
   auto load_x = [&](int slice) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int64_t r = min(row0 + t * 16 + col, B - 1);
-      const uint16_t* xr = a.X + r * a.ldx + slice * SLICE + 8 * q;
+      if constexpr (XLDS) {
+        const uint16_t* xr = &xs[t * 16 + col][slice * SLICE + 8 * q];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) xf[t][ks] = *reinterpret_cast<const bf16x8_t*>(xr + ks * 32);
+        for (int ks = 0; ks < KS; ++ks) xf[t][ks] = *reinterpret_cast<const bf16x8_t*>(xr + ks * 32);
+      } else {
+        const int64_t r = min(row0 + t * 16 + col, B - 1);
+        const uint16_t* xr = a.X + r * a.ldx + slice * SLICE + 8 * q;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) xf[t][ks] = *reinterpret_cast<const bf16x8_t*>(xr + ks * 32);
+      }
     }
   };
-  if (nslices == 1) load_x(0);
+  if constexpr (XLDS) {  // stage the block's rows (clamped like load_x), 16 bytes per thread per step
+    const int cpr = a.F / 8;
+    for (int i = (int)threadIdx.x; i < ROWS * cpr; i += (int)blockDim.x) {
+      const int r = i / cpr, c = (i - r * cpr) * 8;
+      const int64_t row = min(row0 + r, B - 1);
+      *reinterpret_cast<uint4*>(&xs[r][c]) = *reinterpret_cast<const uint4*>(a.X + row * a.ldx + c);
+    }
+    __syncthreads();
+  } else if (nslices == 1) {
+    load_x(0);
+  }
 
   RowState st[NT];
 #pragma unroll
@@ -1253,9 +1280,7 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t][mt] = b0;
     }
-    for (int sl = 0; sl < nslices; ++sl) {
-      if (nslices > 1) load_x(sl);
-      bf16x8_t wf[4][KS];
+    auto load_w = [&](int sl, bf16x8_t(&wf)[4][KS]) {
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const int cls = min(c0 + mt * 16 + col, K - 1);  // classes past K: masked below
@@ -1263,6 +1288,8 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) wf[mt][ks] = *reinterpret_cast<const bf16x8_t*>(wr + ks * 32);
       }
+    };
+    auto mma = [&](const bf16x8_t(&wf)[4][KS]) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -1270,6 +1297,27 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)
             acc[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt][ks], xf[t][ks], acc[t][mt], 0, 0, 0);
+    };
+    if constexpr (XLDS) {  // nslices even (F a multiple of 256, SLICE 64): W double buffered
+      bf16x8_t w0[4][KS], w1[4][KS];
+      load_w(0, w0);
+      for (int sl = 0; sl < nslices; sl += 2) {
+        load_w(sl + 1, w1);
+        load_x(sl);
+        __builtin_amdgcn_sched_barrier(0);  // the next slice's W loads stay in flight over these MFMAs
+        mma(w0);
+        if (sl + 2 < nslices) load_w(sl + 2, w0);
+        load_x(sl + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(w1);
+      }
+    } else {
+      for (int sl = 0; sl < nslices; ++sl) {
+        if (nslices > 1) load_x(sl);
+        bf16x8_t wf[4][KS];
+        load_w(sl, wf);
+        mma(wf);
+      }
     }
   };
   for (int c = wave; c < nchunks; c += nw) {
@@ -1428,6 +1476,17 @@ int rows_nt(int64_t B, int F, int K) {
   return (want >= 6 && K > CLASS_CHUNK) ? 6 : 4;
 }
 
+// the LDS-staged-X variant of the row-group kernel: F in (512, 1024] (64 rows x F fit the LDS),
+// batches large enough for 64-row blocks, more than one class chunk (the row merge takes one thread
+// per row). MLAPI_ROWS_XLDS=0 keeps the register-X kernel (measurement)
+bool rows_xlds(int64_t B, int F, int K) {
+  static const bool on = [] {
+    const char* e = std::getenv("MLAPI_ROWS_XLDS");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on && F > 512 && F <= XLDS_FMAX && F % 256 == 0 && B >= 16384 && K > CLASS_CHUNK;
+}
+
 template <int MODE>
 void launch_rows(RowsArgs a, int kind, hipStream_t stream) {
   if (!rows_supported(a.F))
@@ -1436,9 +1495,18 @@ void launch_rows(RowsArgs a, int kind, hipStream_t stream) {
     throw std::invalid_argument("gemm_softmax: X rows and W must be 16-byte aligned");
   const int nchunks = (a.K + CLASS_CHUNK - 1) / CLASS_CHUNK;
   const int nw = nchunks < ROWS_MAX_WAVES ? nchunks : ROWS_MAX_WAVES;
+  const bool ovr = kind == KIND_OVR;
+  if (rows_xlds(a.B, a.F, a.K)) {
+    const dim3 grid((unsigned)((a.B + XLDS_ROWS - 1) / XLDS_ROWS)), block(64 * nw);
+    if (ovr)
+      hipLaunchKernelGGL((softmax_rows_kernel<2, 4, MODE, true, true>), grid, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((softmax_rows_kernel<2, 4, MODE, false, true>), grid, block, 0, stream, a);
+    MLAPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const int nt = rows_nt(a.B, a.F, a.K);
   const dim3 grid((unsigned)((a.B + 16 * nt - 1) / (16 * nt))), block(64 * nw);
-  const bool ovr = kind == KIND_OVR;
 #define MLAPI_ROWS_LAUNCH(KSV, NTV)                                                                \
   do {                                                                                             \
     if (ovr)                                                                                       \
@@ -1790,9 +1858,9 @@ void launch_gemm_rowstate(const void* X, const void* W, const float* b, int64_t 
   launch_mode<4>(args, F, plan, stream);
 }
 
-int softmax_rows_g_blocks(int64_t B, int F, int K) {
-  const int nt = rows_nt(B, F, K);  // launch_rows' row tiles per block
-  return (int)((B + 16 * nt - 1) / (16 * nt));
+int softmax_rows_g_blocks(int64_t B, int F, int K) {  // launch_rows' grid: one {loss, correct} slab per block
+  const int rows = rows_xlds(B, F, K) ? XLDS_ROWS : 16 * rows_nt(B, F, K);
+  return (int)((B + rows - 1) / rows);
 }
 
 void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y, int64_t B,

@@ -117,15 +117,16 @@ def test_gemm_softmax(B, F, K, kind, gemm_kernel):
     torch.testing.assert_close(p.double().cpu(), rp.cpu(), rtol=2e-4, atol=2e-5)
 
 
-@pytest.mark.parametrize("F", [1024, 4096])
-def test_predict_wide_multiclass_matches_fp64_oracle(F):
-    """ops.predict on F = 1024 / 4096 multiclass models against the float64
-    oracle of the same bf16-rounded operands."""
+@pytest.mark.parametrize("F,B", [(1024, 777), (4096, 777), (1024, 20000), (768, 16384)])
+def test_predict_wide_multiclass_matches_fp64_oracle(F, B):
+    """ops.predict on F = 768 / 1024 / 4096 multiclass models against the float64
+    oracle of the same bf16-rounded operands; B >= 16384 at F <= 1024 runs the row-group kernel
+    with X staged in LDS."""
     from mlapi_amd.models.linear import LinearModel
     from mlapi_amd.serve.loadgen import bf16_oracle
 
     m = LinearModel.random(F, 300, seed=F, kind=Kind.MULTINOMIAL)
-    Xn = np.random.default_rng(F).standard_normal((777, F))
+    Xn = np.random.default_rng(F).standard_normal((B, F))
     idx, p = ops.predict(torch.tensor(Xn, device=DEV, dtype=torch.bfloat16), torch.tensor(m.W, device=DEV),
                          torch.tensor(m.b, device=DEV), Kind.MULTINOMIAL)
     om, Xr = bf16_oracle(m, Xn)
@@ -371,7 +372,8 @@ def test_softmax_grad_dw_fused(B, F, K, kind, groups, nc, pipe):
 
 @pytest.mark.parametrize("B,F,K,kind", [(2048, 1024, 100, Kind.MULTINOMIAL), (777, 700, 37, Kind.OVR),
                                         (4099, 1024, 1000, Kind.MULTINOMIAL), (65, 2048, 3, Kind.MULTINOMIAL),
-                                        (20000, 1024, 130, Kind.OVR)])  # B >= 16384: 64-row blocks
+                                        (20000, 1024, 130, Kind.OVR),  # B >= 16384, F <= 1024: X staged in LDS
+                                        (16384, 768, 1000, Kind.MULTINOMIAL)])
 def test_softmax_grad_wide(B, F, K, kind):
     """Wide multiclass gradient (F > 512, softmax_grad_wide.hip: row stats + logits by the row-group
     kernel, G in bf16, G^T X_aug by the transposed-LDS MFMA kernel, slab sum) vs the fp32 oracle;
