@@ -104,14 +104,7 @@ __global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* 
     }
   };
   wf32x4_t acc[4][4] = {};
-  uint4 gv[2], xv[JX];
-  load_tile(r_begin, gv, xv);
-  store_tile(0, gv, xv);
-  __syncthreads();
-  int buf = 0;
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += TILE_ROWS) {
-    const bool more = r0 + TILE_ROWS < r_end;
-    if (more) load_tile(r0 + TILE_ROWS, gv, xv);  // in flight under this step's MFMAs
+  auto mma_step = [&](int buf) {
     wbf16x8_t a[4], b[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {  // A: 16 classes x 8 rows per 16-lane group (transposed reads)
@@ -133,6 +126,19 @@ __global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* 
     for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], b[n], acc[m][n], 0, 0, 0);
+  };
+  // one k-step of loads in flight. Two (a second register set: tile t + 2 loading while t + 1 waits)
+  // took the kernel from 140 to 236 VGPRs, 3 to 2 blocks per CU, and the F = 1024 step from 0.915 to
+  // 1.13 ms (profiles/r5_train/s42_depth/): the resident blocks' overlap hides more than the depth
+  uint4 gv[2], xv[JX];
+  load_tile(r_begin, gv, xv);
+  store_tile(0, gv, xv);
+  __syncthreads();
+  int buf = 0;
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += TILE_ROWS) {
+    const bool more = r0 + TILE_ROWS < r_end;
+    if (more) load_tile(r0 + TILE_ROWS, gv, xv);  // in flight under this step's MFMAs
+    mma_step(buf);
     if (more) store_tile(buf ^ 1, gv, xv);  // the other buffer was last read before the previous barrier
     __syncthreads();
     buf ^= 1;
@@ -213,7 +219,7 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
   const int g_blocks = L.g_blocks;
   const int F_aug = F + 8;
   const dim3 grid((unsigned)(L.Kp / 128), (unsigned)((F_aug + TF128 - 1) / TF128), (unsigned)L.row_groups);
-  hipLaunchKernelGGL(gdw_gemm_big_kernel<2>, grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug),
+  hipLaunchKernelGGL((gdw_gemm_big_kernel<2>), grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug),
                      ldx, F_aug, B, K, L.rows_per_group, slabs);
   MLAPI_HIP_CHECK(hipGetLastError());
   launch_gdw_reduce(slabs, L.row_groups, K, F_aug, dW_out, stat_slabs, g_blocks, stats_out, update, dp,
