@@ -32,6 +32,12 @@
 #   serve_ab_old  interleaved x3 serve bench: ab_old/ (previous build) vs the working tree
 #   serve_ab3     interleaved x2: ab_old/ vs the working tree vs the working tree with AB_ENV (e.g. MLAPI_KERNARG_HOST=1)
 #   gemm_ab       interleaved x3 gemm bench: ab_old/mlapi_amd (stashed previous build) vs the working tree
+#   prev_ab       interleaved x3: the previous build copied to ab_prev/ vs the working tree (PREV_ARGS)
+#   wide_trace    WIDE kernel timeline + rocprofv3 phase split (tools/wide_trace.py, tools/wide_probe.py)
+#   bench_abenv   any bench mode (BENCH_ARGS) with AB_VAR set to each of AB_VALS, interleaved x2
+#   serve_lgsplit IO threads x load-generator threads (SPLITS="io:lg ...", LGARGS), interleaved
+#   serve_n2res   two ranks on one GPU: resident on / off x placement
+#   serve_wide64  serve_wide at f64 for K = 2 / 40 / 1000
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
@@ -316,6 +322,19 @@ for s in $steps; do
         env ${AB_ENV:-MLAPI_NOTHING=1} timeout -k 10 300 python -u bench.py --steps 100 --warmup 10 > "$O/serve_newenv_r$r.log" 2>&1 \
           || stop "serve_newenv_r$r" $? "$O/serve_newenv_r$r.log"
         tail -1 "$O/serve_newenv_r$r.log" | cut -c1-200
+      done ;;
+    wide_trace)  # WIDE kernel: in-kernel timeline (tools/wide_trace.py) + rocprofv3 phase durations (tools/wide_probe.py)
+      run wide_trace 180 python3 -u tools/wide_trace.py 256 1000 200
+      run wide_probe_prof 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/wide_prof" -o prof -- python3 tools/wide_probe.py
+      python3 tools/wide_probe_summary.py "$(find "$O/wide_prof" -name '*kernel_trace.csv' -print -quit)" > "$O/wide_probe_summary.txt" 2>&1
+      cat "$O/wide_trace.log" "$O/wide_probe_summary.txt" ;;
+    bench_abenv)  # AB_VAR=<env var> AB_VALS="<v1> <v2>" BENCH_ARGS="<bench args>": interleaved x2
+      for r in 1 2; do
+        for v in $AB_VALS; do
+          env "$AB_VAR=$v" timeout -k 10 300 python -u bench.py ${BENCH_ARGS:-} > "$O/bench_${AB_VAR}_${v}_r$r.log" 2>&1 \
+            || stop "bench_${AB_VAR}_${v}_r$r" $? "$O/bench_${AB_VAR}_${v}_r$r.log"
+          grep '^{' "$O/bench_${AB_VAR}_${v}_r$r.log" | cut -c1-240
+        done
       done ;;
     prev_ab)  # interleaved x3: the previous build copied to ab_prev/ vs the working tree, same bench args (PREV_ARGS)
       for r in 1 2 3; do
