@@ -239,8 +239,12 @@ for s in $steps; do
         MLAPI_SPLIT_PROBE=$pr prof "split_probe${pr}_b1" 120 --mode gemm --batch 1 --steps 300 --warmup 5 --gemm-kernel split --launch eager
       done
       prof "tiles_b1" 120 --mode gemm --batch 1 --steps 300 --warmup 5 --launch eager ;;
-    kbench)
-      for m in gemv gemm train train_softmax; do run "bench_$m" 300 python -u bench.py --mode $m --steps 100 --warmup 10; done ;;
+    kbench)  # kernel benches; the training modes in steady state (200 warm-up steps: the GPU's clock ramp)
+      for m in gemv gemm; do run "bench_$m" 300 python -u bench.py --mode $m --steps 100 --warmup 10; done
+      for m in train train_softmax; do run "bench_$m" 300 python -u bench.py --mode $m --steps 500 --warmup 200; done
+      run bench_train_softmax_f1024 300 python -u bench.py --mode train_softmax --softmax-features 1024 --steps 100 --warmup 20 ;;
+    driver)  # the driver's exact headline command
+      run bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof)
       for m in gemv gemm train train_softmax; do prof "$m" 300 --mode $m --steps 20 --warmup 2; done
       prof serve 300 --steps 20 --warmup 2 --reqs-per-conn 512
