@@ -388,6 +388,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("timeout_ms") = 60000);
   m.def("softmax_grad_wide_supported", &softmax_grad_wide_supported);
   m.def("softmax_grad_wide_workspace", &softmax_grad_wide_workspace);
+  m.def("softmax_grad_wide_set_zbuf", &softmax_grad_wide_set_zbuf);
   m.def(
       "softmax_grad_wide",
       [](uintptr_t X_aug, int64_t ldx, uintptr_t W, uintptr_t b, uintptr_t y, int64_t B, int F, int K, int kind,

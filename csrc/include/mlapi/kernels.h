@@ -287,10 +287,13 @@ void launch_gdw_reduce(const float* slabs, int nslabs, int K, int F_aug, float* 
 // Full logits Z [B, K] f32 of X [B, F] (row stride ldx) through the row-group kernel.
 // Row stats + training G in one launch (row-group kernel MODE 5): G = softmax(z) - onehot(y) (OvR:
 // sigmoid(z) - onehot) as bf16 [B][Kp] (zero columns K..Kp-1) and per-block {loss, correct} in
-// stat_slabs[softmax_rows_g_blocks(B)][2]. F: a multiple of 256 (or a power of two <= 256).
+// stat_slabs[softmax_rows_g_blocks(B)][2]. F: a multiple of 256 (or a power of two <= 256). Zs
+// (optional, [B][Kp] f32): the first pass stores its logits there and the second reads them back
+// instead of recomputing them; null recomputes.
 int softmax_rows_g_blocks(int64_t B, int F, int K);
 void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y, int64_t B,
-                           int F, int K, int kind, uint16_t* G, int Kp, float* stat_slabs, hipStream_t stream);
+                           int F, int K, int kind, uint16_t* G, int Kp, float* stat_slabs, float* Zs,
+                           hipStream_t stream);
 void launch_gemm_logits_ld(const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K, float* Z,
                            hipStream_t stream);
 // Multiclass training gradient for wide models (softmax_grad_wide.hip): F a multiple of 256 above
@@ -298,6 +301,7 @@ void launch_gemm_logits_ld(const void* X, int64_t ldx, const void* W, const floa
 // the loss / correct stats, dW slabs = G^T X_aug by an MFMA kernel (LDS tiles read through
 // ds_read_b64_tr_b16), then launch_gdw_reduce. Workspace: softmax_grad_wide_workspace bytes.
 bool softmax_grad_wide_supported(int F);
+void softmax_grad_wide_set_zbuf(int mode);  // measurement / test hook: -1 env default, 0 recompute, 1 keep logits
 size_t softmax_grad_wide_workspace(int64_t B, int K, int F);
 void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y,
                               int64_t B, int F, int K, int kind, float* dW_out, float* stats_out, void* workspace,

@@ -1201,6 +1201,7 @@ struct RowsArgs {
   const int32_t* y;
   uint16_t* G;  // [B][Kp] bf16, columns K..Kp-1 written 0
   int Kp;
+  float* Zs;  // [B][Kp] f32: the first pass's logits, read back by the second (null: recomputed)
   float* stat_slabs;  // [gridDim.x][2] {loss, correct}
 };
 
@@ -1345,6 +1346,14 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
           }
         }
       } else {
+        if constexpr (MODE == 5) {  // keep the logits for the second pass (each lane re-reads its own)
+          const int64_t row = row0 + t * 16 + col;
+          if (a.Zs != nullptr && row < B) {
+            float* zr = a.Zs + row * (int64_t)a.Kp + c0 + q * 4;
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) *reinterpret_cast<f32x4_t*>(zr + mt * 16) = acc[t][mt];
+          }
+        }
         online_update<OVR>(v, c0, q, st[t]);
       }
     }
@@ -1400,7 +1409,16 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
     for (int c = wave; c < nchunks_p; c += nw) {
       const int c0 = c * CLASS_CHUNK;
       f32x4_t acc[NT][4];
-      chunk_logits(c0, acc);
+      if (a.Zs != nullptr) {  // the first pass's logits: no second GEMM (the X reads and MFMAs)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const float* zr = a.Zs + min(row0 + t * 16 + col, B - 1) * (int64_t)a.Kp + c0 + q * 4;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) acc[t][mt] = *reinterpret_cast<const f32x4_t*>(zr + mt * 16);
+        }
+      } else {
+        chunk_logits(c0, acc);
+      }
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         if (!live[t]) continue;
@@ -1864,7 +1882,8 @@ int softmax_rows_g_blocks(int64_t B, int F, int K) {  // launch_rows' grid: one 
 }
 
 void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y, int64_t B,
-                           int F, int K, int kind, uint16_t* G, int Kp, float* stat_slabs, hipStream_t stream) {
+                           int F, int K, int kind, uint16_t* G, int Kp, float* stat_slabs, float* Zs,
+                           hipStream_t stream) {
   if (B <= 0) return;
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("softmax_rows_g: multiclass kinds only");
@@ -1874,6 +1893,7 @@ void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const 
   ra.G = G;
   ra.Kp = Kp;
   ra.stat_slabs = stat_slabs;
+  ra.Zs = Zs;
   launch_rows<5>(ra, kind, stream);
 }
 

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* 
 }
 
 struct WideLayout {
-  size_t g_off, dw_off, stat_off, total;
+  size_t g_off, dw_off, stat_off, z_off, total;
   int Kp, row_groups, g_blocks;
   int64_t rows_per_group;
 };
@@ -186,11 +186,27 @@ WideLayout wide_layout(int64_t B, int K, int F) {
   o = al(o + (size_t)L.row_groups * K * F_aug * sizeof(float));
   L.stat_off = o;
   o = al(o + (size_t)L.g_blocks * 2 * sizeof(float));
+  L.z_off = o;  // the row-stats pass's logits, [B][Kp] f32 (zbuf_on())
+  o = al(o + (size_t)B * L.Kp * sizeof(float));
   L.total = o;
   return L;
 }
 
+int g_zbuf = -1;  // softmax_grad_wide_set_zbuf: -1 MLAPI_WIDE_ZBUF (default on), 0 off, 1 on
+
+// The first launch keeps its logits in the workspace for its second pass (off: recomputes them, a
+// second GEMM over X instead of a B x Kp f32 write + read)
+bool zbuf_on() {
+  static const bool env = [] {
+    const char* e = std::getenv("MLAPI_WIDE_ZBUF");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return g_zbuf < 0 ? env : g_zbuf != 0;
+}
+
 }  // namespace
+
+void softmax_grad_wide_set_zbuf(int mode) { g_zbuf = mode; }
 
 bool softmax_grad_wide_supported(int F) { return F > 512 && F % 256 == 0; }
 
@@ -215,7 +231,8 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
   uint16_t* G = reinterpret_cast<uint16_t*>(ws + L.g_off);
   float* slabs = reinterpret_cast<float*>(ws + L.dw_off);
   float* stat_slabs = reinterpret_cast<float*>(ws + L.stat_off);
-  launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, stream);
+  float* Zs = zbuf_on() ? reinterpret_cast<float*>(ws + L.z_off) : nullptr;
+  launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, Zs, stream);
   const int g_blocks = L.g_blocks;
   const int F_aug = F + 8;
   const dim3 grid((unsigned)(L.Kp / 128), (unsigned)((F_aug + TF128 - 1) / TF128), (unsigned)L.row_groups);

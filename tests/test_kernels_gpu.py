@@ -402,6 +402,16 @@ def test_softmax_grad_wide(B, F, K, kind):
     assert st2[0].item() == pytest.approx(loss_ref.item(), rel=1e-4)
     assert abs(st2[1].item() - corr_ref.item()) <= max(2, B // 2000)
     assert torch.all(dW2[:, F:Fk] == 0) and torch.all(dW2[:, Fk + 1:] == 0)
+    # the second pass reads the first pass's logits back (default) or recomputes them: same bits
+    from mlapi_amd._native import C
+
+    C().softmax_grad_wide_set_zbuf(0)
+    try:
+        dW3, st3 = ops.softmax_train_grad(Xa, Wb, b, y, kind, bufs=bufs)
+        torch.cuda.synchronize()
+    finally:
+        C().softmax_grad_wide_set_zbuf(-1)
+    assert torch.equal(dW2, dW3) and torch.equal(st2, st3)
 
 
 def test_sgd_wide_multiclass_estimator_one_gpu():
