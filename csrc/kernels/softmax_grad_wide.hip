@@ -56,7 +56,8 @@ template <int WC>
 __global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* __restrict__ G, int Kp,
                                                                const uint16_t* __restrict__ X, int64_t ldx, int F_aug,
                                                                int64_t B, int K, int64_t rows_per_group,
-                                                               float* __restrict__ slabs) {
+                                                               float* __restrict__ slabs, int xcd_tiles,
+                                                               int row_groups) {
   constexpr int TC = 64 * WC, NTHR = 128 * WC, GROW = TC + LDS_PAD;
   constexpr int JX = 512 / NTHR;  // X chunks per thread (32 rows x 16 chunks of 8 columns)
   static_assert(32 * TC / 8 == 2 * NTHR, "two G chunks per thread");
@@ -64,8 +65,23 @@ __global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* 
   __shared__ __attribute__((aligned(16))) uint16_t xt[2][TILE_ROWS][XROW];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wc = wave % WC, wf = wave / WC;  // the wave's 64-class slice / 64-feature half
-  const int c0 = blockIdx.x * TC, f0 = blockIdx.y * TF128;
-  const int64_t r_begin = (int64_t)blockIdx.z * rows_per_group;
+  // xcd_tiles > 0: a 1-D grid dealt over the 8 XCDs round-robin (block b runs on XCD b % 8, as the
+  // dispatcher deals them; a placement hint only, nothing depends on it for correctness): XCD x
+  // takes row groups x, x + 8, ..., each as its xcd_tiles = (class tiles x feature tiles) blocks in
+  // a row, so an XCD's L2 holds the G and X rows of ITS row groups - every tile of a row group
+  // re-reads them there - instead of every XCD streaming all of X (the 3-D grid put class tile x
+  // on XCD x: X came from the infinity cache / HBM 8 times)
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (xcd_tiles > 0) {
+    const int j = (int)blockIdx.x >> 3;
+    bz = ((int)blockIdx.x & 7) + 8 * (j / xcd_tiles);
+    if (bz >= row_groups) return;  // the grid's padding to whole rounds of 8 (uniform per block)
+    const int tile = j % xcd_tiles, ncb = Kp / TC;
+    bx = tile % ncb;
+    by = tile / ncb;
+  }
+  const int c0 = bx * TC, f0 = by * TF128;
+  const int64_t r_begin = (int64_t)bz * rows_per_group;
   const int64_t r_end = min(B, r_begin + rows_per_group);
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   auto load_tile = [&](int64_t r0, uint4 (&gv)[2], uint4 (&xv)[JX]) {
@@ -144,7 +160,7 @@ __global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* 
     buf ^= 1;
   }
   // C layout: class c0 + wc*64 + 16m + 4g + i (register i), feature f0 + wf*64 + 16n + (lane & 15)
-  float* slab = slabs + (int64_t)blockIdx.z * K * F_aug;
+  float* slab = slabs + (int64_t)bz * K * F_aug;
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -156,6 +172,15 @@ __global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* 
         if (c < K && f < F_aug) slab[(int64_t)c * F_aug + f] = acc[m][n][i];
       }
     }
+}
+
+// the G^T X launch's XCD-aware block order (gdw_gemm_big_kernel); MLAPI_GDW_XCD=0: the 3-D grid
+bool gdw_xcd_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MLAPI_GDW_XCD");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
 }
 
 struct WideLayout {
@@ -172,6 +197,7 @@ WideLayout wide_layout(int64_t B, int K, int F) {
   const int TFw = TF128;  // feature tile width
   const int tiles = (L.Kp / T) * ((F_aug + TFw - 1) / TFw);
   int64_t rg = (2048 + tiles - 1) / tiles;
+  if (gdw_xcd_on()) rg = (rg + 7) / 8 * 8;  // whole rounds of row groups over the 8 XCDs
   const int64_t max_rg = (B + 255) / 256;
   if (rg > max_rg) rg = max_rg;
   if (rg < 1) rg = 1;
@@ -235,9 +261,17 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
   launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, Zs, stream);
   const int g_blocks = L.g_blocks;
   const int F_aug = F + 8;
-  const dim3 grid((unsigned)(L.Kp / 128), (unsigned)((F_aug + TF128 - 1) / TF128), (unsigned)L.row_groups);
-  hipLaunchKernelGGL((gdw_gemm_big_kernel<2>), grid, dim3(256), 0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug),
-                     ldx, F_aug, B, K, L.rows_per_group, slabs);
+  const int ncb = L.Kp / 128, nfb = (F_aug + TF128 - 1) / TF128;
+  if (gdw_xcd_on()) {
+    const int rounds = (L.row_groups + 7) / 8;
+    hipLaunchKernelGGL((gdw_gemm_big_kernel<2>), dim3((unsigned)(8 * ncb * nfb * rounds)), dim3(256), 0, stream, G,
+                       L.Kp, static_cast<const uint16_t*>(X_aug), ldx, F_aug, B, K, L.rows_per_group, slabs, ncb * nfb,
+                       L.row_groups);
+  } else {
+    hipLaunchKernelGGL((gdw_gemm_big_kernel<2>), dim3((unsigned)ncb, (unsigned)nfb, (unsigned)L.row_groups), dim3(256),
+                       0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug), ldx, F_aug, B, K, L.rows_per_group,
+                       slabs, 0, L.row_groups);
+  }
   MLAPI_HIP_CHECK(hipGetLastError());
   launch_gdw_reduce(slabs, L.row_groups, K, F_aug, dW_out, stat_slabs, g_blocks, stats_out, update, dp,
                     dp_timeout_ms, stream);
