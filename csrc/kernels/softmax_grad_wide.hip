@@ -10,19 +10,21 @@
 //      into G = softmax(z) - onehot(y) (OvR: sigmoid(z) - onehot) as bf16 [B][Kp] (Kp = K rounded
 //      up to 128, zero padded) plus the block's {loss, correct} - a write + read of the logits
 //      instead of a second GEMM over X (F = 1024: 0.914 -> 0.764 ms per step, profiles/r5_train/);
-//   2. gdw_gemm_big_kernel: dW slabs[row group][K][F_aug] = G^T X_aug over the group's rows -
+//   2. gdw_gemm_dma_kernel: dW slabs[row group][K][F_aug] = G^T X_aug over the group's rows -
 //      v_mfma_f32_16x16x32_bf16 with M = classes, N = features, K = rows: both operands are
-//      row-major [rows][*] tiles, so each is staged in LDS (32 rows x 128 columns, 16-byte loads)
-//      and read transposed with ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group, two
-//      reads = the 8 rows of a lane's k-slice);
+//      row-major [rows][*] tiles, DMA'd into LDS (32 rows x 128 columns per k-step, 3 stages)
+//      and read transposed with ds_read_b64_tr_b16;
 //   3. launch_gdw_reduce: deterministic slab sum + fused SGD update (+ in-kernel DP exchange).
 // (Round 3's five launches - row stats, f32 logits through HBM, a wave-per-row G pass - lost to
 // this path: 1.79 -> 1.0 ms per step at F = 1024, docs/PERFORMANCE.md; removed in round 5.)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 #include "mlapi/common.h"
 #include "mlapi/kernels.h"
@@ -34,49 +36,50 @@ typedef __attribute__((ext_vector_type(8))) __bf16 wbf16x8_t;
 typedef __attribute__((ext_vector_type(4))) short wi16x4_t;
 typedef __attribute__((ext_vector_type(4))) float wf32x4_t;
 typedef __attribute__((address_space(3))) wi16x4_t lds_i16x4_t;
+typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int TILE_ROWS = 32;        // MFMA k-step (rows)
 
 
-// ---- 4. dW slabs = G^T X_aug per row group, (64 WC) x 128 block tiles: a wave owns 64 classes x
-// 64 features (4 x 4 MFMA tiles, 64 accumulator VGPRs), the block 2 WC waves, so each 16-byte
-// element staged through LDS feeds 2-4x the MFMAs of round 3's 64 x 64 tiles (514 -> 357 us at
-// F = 1024; that kernel left the build in round 5) and G / X are re-read from L2 correspondingly
-// less often. LDS double buffered (one barrier per 32-row k-step). WC = 2 (128 x 128 tiles, 256
-// threads) is the one launched: WC = 4 (256 x 128, 512 threads) measured 1.05 vs 0.99 ms per
-// F = 1024 training step (profiles/r4_train/tsm_f1024_t256_*).
-// Rows padded by 8 elements. The counters show 1.6 LDS bank conflicts per LDS instruction
-// (profiles/r5_pmc/summary_big.md); padding rows to 16 elements instead (8 banks per row) left both
-// the count (1.600) and the F = 1024 step (0.971 vs 0.972 ms, interleaved x3) unchanged
-// (profiles/r5_train/s37_*), so the conflicts are not the row stride's and not on the critical path.
+// ---- 2. dW slabs = G^T X_aug per row group, 128 x 128 block tiles: a wave owns 64 classes x 64
+// features (4 x 4 tiles of v_mfma_f32_16x16x32_bf16, 64 accumulators); M = classes, N = features,
+// K = rows, and both operands are row-major [rows][*] tiles, read transposed from LDS with
+// ds_read_b64_tr_b16 (4 rows x 16 columns per 16-lane group, two reads = a lane's 8-row k-slice).
+// The tiles arrive by LDS-DMA (`buffer_load_dwordx4 ... lds`), NS stages deep: NS - 1 k-steps
+// stream into LDS while the MFMAs read the oldest. Round 4's kernel staged them through registers
+// with one k-step in flight (a second cost registers and a resident block, profiles/r5_train/s42)
+// and its waves waited on memory 68 % of their cycles at 19 % MFMA busy (s54); F = 1024 step 0.737
+// -> 0.612 ms (s55). A stage is the k-step's G and X tiles, 32 rows x 128 columns
+// bf16 each, rows unpadded (the DMA writes 1 KB per wave-instruction, lane-linear); the 16-byte
+// chunks of row r sit XOR-permuted by s(r) = 2 (r & 3) + 8 ((r >> 3) & 1), so the transposed reads
+// (rows 8g + q (+4), two adjacent chunks per 16-column subtile) touch 64 distinct banks per
+// 32-lane group. The source is read through range-checked buffer descriptors: rows past B load 0.
 constexpr int TF128 = 128;
-constexpr int LDS_PAD = 8;
-constexpr int XROW = TF128 + LDS_PAD;
+constexpr int DMA_ROW_BYTES = TF128 * 2;                 // 256 B: a 128-column bf16 row
+constexpr int DMA_TILE_BYTES = TILE_ROWS * DMA_ROW_BYTES;  // 8 KB
+__device__ __forceinline__ int dma_swz(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3); }
 
-template <int WC>
-__global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* __restrict__ G, int Kp,
-                                                               const uint16_t* __restrict__ X, int64_t ldx, int F_aug,
-                                                               int64_t B, int K, int64_t rows_per_group,
-                                                               float* __restrict__ slabs, int xcd_tiles,
-                                                               int row_groups) {
-  constexpr int TC = 64 * WC, NTHR = 128 * WC, GROW = TC + LDS_PAD;
-  constexpr int JX = 512 / NTHR;  // X chunks per thread (32 rows x 16 chunks of 8 columns)
-  static_assert(32 * TC / 8 == 2 * NTHR, "two G chunks per thread");
-  __shared__ __attribute__((aligned(16))) uint16_t gt[2][TILE_ROWS][GROW];
-  __shared__ __attribute__((aligned(16))) uint16_t xt[2][TILE_ROWS][XROW];
+template <int NS>
+__global__ __launch_bounds__(256) void gdw_gemm_dma_kernel(const uint16_t* __restrict__ G, int Kp,
+                                                           const uint16_t* __restrict__ X, int64_t ldx, int F_aug,
+                                                           int64_t B, int K, int64_t rows_per_group,
+                                                           float* __restrict__ slabs, int xcd_tiles,
+                                                           int row_groups) {
+  constexpr int TC = 128;
+  __shared__ __attribute__((aligned(1024))) unsigned char sm[NS][2][DMA_TILE_BYTES];  // [stage][G, X]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wc = wave % WC, wf = wave / WC;  // the wave's 64-class slice / 64-feature half
-  // xcd_tiles > 0: a 1-D grid dealt over the 8 XCDs round-robin (block b runs on XCD b % 8, as the
-  // dispatcher deals them; a placement hint only, nothing depends on it for correctness): XCD x
-  // takes row groups x, x + 8, ..., each as its xcd_tiles = (class tiles x feature tiles) blocks in
-  // a row, so an XCD's L2 holds the G and X rows of ITS row groups - every tile of a row group
-  // re-reads them there - instead of every XCD streaming all of X (the 3-D grid put class tile x
-  // on XCD x: X came from the infinity cache / HBM 8 times)
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (xcd_tiles > 0) {
+  const int wc = wave & 1, wf = wave >> 1;
+  int bx, by, bz;
+  // a 1-D grid dealt over the 8 XCDs round-robin (block b runs on XCD b % 8, as the dispatcher
+  // deals them; a placement hint only, nothing depends on it for correctness): XCD x takes row
+  // groups x, x + 8, ..., each as its xcd_tiles = (class tiles x feature tiles) blocks in a row, so
+  // an XCD's L2 holds the G and X rows of ITS row groups - every tile of a row group re-reads them
+  // there - instead of every XCD streaming all of X (a 3-D grid put class tile x on XCD x: X came
+  // from the infinity cache / HBM 8 times; F = 1024 step 0.765 -> 0.737 ms, s52)
+  {
     const int j = (int)blockIdx.x >> 3;
     bz = ((int)blockIdx.x & 7) + 8 * (j / xcd_tiles);
-    if (bz >= row_groups) return;  // the grid's padding to whole rounds of 8 (uniform per block)
+    if (bz >= row_groups) return;
     const int tile = j % xcd_tiles, ncb = Kp / TC;
     bx = tile % ncb;
     by = tile / ncb;
@@ -84,82 +87,106 @@ __global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* 
   const int c0 = bx * TC, f0 = by * TF128;
   const int64_t r_begin = (int64_t)bz * rows_per_group;
   const int64_t r_end = min(B, r_begin + rows_per_group);
+  const int nk = (int)((r_end - r_begin + TILE_ROWS - 1) / TILE_ROWS);
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  auto load_tile = [&](int64_t r0, uint4 (&gv)[2], uint4 (&xv)[JX]) {
+  // the row group's own descriptors: they end at its last row (the tail k-step's rows past B read
+  // as zeros) and keep every offset within 32 bits (wide_layout caps a group's bytes)
+  const int64_t nrows = r_end - r_begin;
+  const auto grs = __builtin_amdgcn_make_buffer_rsrc((void*)(G + r_begin * Kp), 0, (int)(nrows * Kp * 2), 0x00020000);
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + r_begin * ldx), 0, (int)(nrows * ldx * 2), 0x00020000);
+  // this lane's DMA pieces: wave-instruction j of a tile covers rows 4 (2 wave + j) .. + 3, lane l
+  // writes the 16 bytes at chunk position l & 15 of row + (l >> 4), which holds logical chunk
+  // (l & 15) ^ s(row)
+  uint32_t goff[2], xoff[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r = 4 * (2 * wave + j) + (lane >> 4);
+    const int ch = (lane & 15) ^ dma_swz(r);
+    goff[j] = (uint32_t)(((int64_t)r * Kp + c0 + ch * 8) * 2);
+    xoff[j] = (uint32_t)(((int64_t)r * ldx + f0 + ch * 8) * 2);
+  }
+  const uint32_t gstep = (uint32_t)(TILE_ROWS * Kp * 2), xstep = (uint32_t)(TILE_ROWS * ldx * 2);
+  auto dma = [&](int k, int st) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int k = (int)threadIdx.x + NTHR * j, sr = k / (TC / 8), sc = (k % (TC / 8)) * 8;
-      const int64_t r = r0 + sr;
-      gv[j] = r < r_end ? *reinterpret_cast<const uint4*>(G + r * Kp + c0 + sc) : uint4{0, 0, 0, 0};  // Kp % TC == 0
-    }
-#pragma unroll
-    for (int j = 0; j < JX; ++j) {
-      const int k = (int)threadIdx.x + NTHR * j, sr = k >> 4, sc = (k & 15) * 8;
-      const int64_t r = r0 + sr;
-      xv[j] = uint4{0, 0, 0, 0};
-      if (r < r_end) {
-        if (f0 + sc + 8 <= ldx) {
-          xv[j] = *reinterpret_cast<const uint4*>(X + r * ldx + f0 + sc);
-        } else {
-          uint16_t tmp[8];
-          for (int e = 0; e < 8; ++e) tmp[e] = f0 + sc + e < ldx ? X[r * ldx + f0 + sc + e] : 0;
-          __builtin_memcpy(&xv[j], tmp, sizeof(uint4));
-        }
-      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(grs, (lds_void_t*)(&sm[st][0][(2 * wave + j) * 1024]), 16,
+                                               goff[j] + (uint32_t)k * gstep, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void_t*)(&sm[st][1][(2 * wave + j) * 1024]), 16,
+                                               xoff[j] + (uint32_t)k * xstep, 0, 0, 0);
     }
   };
-  auto store_tile = [&](int buf, const uint4 (&gv)[2], const uint4 (&xv)[JX]) {
+  // this lane's transposed-read byte offsets within a tile: rows 8g + q (lo) / + 4 (hi), 4 columns
+  // at 16m + 4p of its 64-column half (chunk 2m + (p >> 1) of the half, byte 8 (p & 1))
+  uint32_t rdo[2][4];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int k = (int)threadIdx.x + NTHR * j, sr = k / (TC / 8), sc = (k % (TC / 8)) * 8;
-      *reinterpret_cast<uint4*>(&gt[buf][sr][sc]) = gv[j];
-    }
+  for (int h = 0; h < 2; ++h) {
+    const int r = 8 * g + 4 * h + q;
 #pragma unroll
-    for (int j = 0; j < JX; ++j) {
-      const int k = (int)threadIdx.x + NTHR * j, sr = k >> 4, sc = (k & 15) * 8;
-      *reinterpret_cast<uint4*>(&xt[buf][sr][sc]) = xv[j];
+    for (int m = 0; m < 4; ++m) {
+      const int ch = (8 * 0 + 2 * m + (p >> 1)) ^ dma_swz(r);  // half offset added per operand below
+      rdo[h][m] = (uint32_t)(r * DMA_ROW_BYTES + ch * 16 + (p & 1) * 8);
     }
-  };
+  }
   wf32x4_t acc[4][4] = {};
-  auto mma_step = [&](int buf) {
+  // The transposed reads go through inline asm: the compiler cannot tell the intrinsic's LDS read
+  // from the DMA stages still in flight and drained them all (vmcnt(0)) before every read; one
+  // lgkmcnt(0) that passes the 16 results through is the reads' only wait.
+  const uint32_t sm0 = (uint32_t)(uintptr_t)(lds_void_t*)&sm[0][0][0];
+  auto mma_step = [&](int st) {
+    const uint32_t gt = sm0 + (uint32_t)(st * 2 * DMA_TILE_BYTES), xt = gt + DMA_TILE_BYTES;
+    wi16x4_t r[16];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)  // the half's chunks are 8 higher: XOR with s(r) < 16 keeps bit 3
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r[2 * m + h]) : "v"(gt + (rdo[h][m] ^ (wc << 7))));
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r[8 + 2 * n + h]) : "v"(xt + (rdo[h][n] ^ (wf << 7))));
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7]),
+                   "+v"(r[8]), "+v"(r[9]), "+v"(r[10]), "+v"(r[11]), "+v"(r[12]), "+v"(r[13]), "+v"(r[14]), "+v"(r[15]));
     wbf16x8_t a[4], b[4];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {  // A: 16 classes x 8 rows per 16-lane group (transposed reads)
-      const int cc = wc * 64 + m * 16 + 4 * p;
-      const wi16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&gt[buf][8 * g + q][cc]);
-      const wi16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&gt[buf][8 * g + 4 + q][cc]);
-      const wi16x4_t v[2] = {lo, hi};
+    for (int m = 0; m < 4; ++m) {
+      const wi16x4_t v[2] = {r[2 * m], r[2 * m + 1]};
       a[m] = __builtin_bit_cast(wbf16x8_t, v);
-    }
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int ff = wf * 64 + n * 16 + 4 * p;
-      const wi16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&xt[buf][8 * g + q][ff]);
-      const wi16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_t*)&xt[buf][8 * g + 4 + q][ff]);
-      const wi16x4_t v[2] = {lo, hi};
-      b[n] = __builtin_bit_cast(wbf16x8_t, v);
+      const wi16x4_t w[2] = {r[8 + 2 * m], r[8 + 2 * m + 1]};
+      b[m] = __builtin_bit_cast(wbf16x8_t, w);
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], b[n], acc[m][n], 0, 0, 0);
   };
-  // one k-step of loads in flight. Two (a second register set: tile t + 2 loading while t + 1 waits)
-  // took the kernel from 140 to 236 VGPRs, 3 to 2 blocks per CU, and the F = 1024 step from 0.915 to
-  // 1.13 ms (profiles/r5_train/s42_depth/): the resident blocks' overlap hides more than the depth
-  uint4 gv[2], xv[JX];
-  load_tile(r_begin, gv, xv);
-  store_tile(0, gv, xv);
-  __syncthreads();
-  int buf = 0;
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += TILE_ROWS) {
-    const bool more = r0 + TILE_ROWS < r_end;
-    if (more) load_tile(r0 + TILE_ROWS, gv, xv);  // in flight under this step's MFMAs
-    mma_step(buf);
-    if (more) store_tile(buf ^ 1, gv, xv);  // the other buffer was last read before the previous barrier
-    __syncthreads();
-    buf ^= 1;
+#pragma unroll
+  for (int s0 = 0; s0 < NS - 1; ++s0) dma(min(s0, nk - 1), s0);
+  // unrolled by the stages, so every stage index is a constant: with a run-time stage the compiler
+  // cannot tell the DMA's LDS target from the stage being read and drains every DMA (vmcnt(0))
+  // before the reads
+  auto step = [&](int k, auto stc) {
+    constexpr int st = decltype(stc)::value;
+    // this wave's pieces of step k have landed (NS - 2 later steps may still be in flight: 4 DMA
+    // instructions per step and wave, completed in order) ...
+    __builtin_amdgcn_s_waitcnt((NS - 2) * 4 == 0 ? ((7 << 4) | (15 << 8)) : (((NS - 2) * 4) | (7 << 4) | (15 << 8)));
+    // ... and every other wave's; past this barrier no wave reads step k - 1's stage any more
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    dma(min(k + NS - 1, nk - 1), (st + NS - 1) % NS);  // the tail re-reads the last step into a free stage
+    mma_step(st);
+  };
+  for (int k = 0; k < nk; k += NS) {
+    step(k, std::integral_constant<int, 0>{});
+    if (k + 1 < nk) step(k + 1, std::integral_constant<int, 1 % NS>{});
+    if constexpr (NS > 2)
+      if (k + 2 < nk) step(k + 2, std::integral_constant<int, 2 % NS>{});
+    if constexpr (NS > 3)
+      if (k + 3 < nk) step(k + 3, std::integral_constant<int, 3 % NS>{});
   }
+  __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));  // drain the tail's DMAs before the block exits
   // C layout: class c0 + wc*64 + 16m + 4g + i (register i), feature f0 + wf*64 + 16n + (lane & 15)
   float* slab = slabs + (int64_t)bz * K * F_aug;
 #pragma unroll
@@ -173,15 +200,6 @@ __global__ __launch_bounds__(128 * WC) void gdw_gemm_big_kernel(const uint16_t* 
         if (c < K && f < F_aug) slab[(int64_t)c * F_aug + f] = acc[m][n][i];
       }
     }
-}
-
-// the G^T X launch's XCD-aware block order (gdw_gemm_big_kernel); MLAPI_GDW_XCD=0: the 3-D grid
-bool gdw_xcd_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("MLAPI_GDW_XCD");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return on;
 }
 
 struct WideLayout {
@@ -198,7 +216,10 @@ WideLayout wide_layout(int64_t B, int K, int F) {
   const int TFw = TF128;  // feature tile width
   const int tiles = (L.Kp / T) * ((F_aug + TFw - 1) / TFw);
   int64_t rg = (2048 + tiles - 1) / tiles;
-  if (gdw_xcd_on()) rg = (rg + 7) / 8 * 8;  // whole rounds of row groups over the 8 XCDs
+  // a group's G / X bytes stay below 2^31 (the G^T X kernel's buffer offsets are 32-bit)
+  const int64_t cap_rows = ((int64_t)INT32_MAX / (2 * std::max<int64_t>(L.Kp, F_aug))) / TILE_ROWS * TILE_ROWS;
+  rg = std::max<int64_t>(rg, (B + cap_rows - 1) / cap_rows);
+  rg = (rg + 7) / 8 * 8;  // whole rounds of row groups over the 8 XCDs
   const int64_t max_rg = (B + 255) / 256;
   if (rg > max_rg) rg = max_rg;
   if (rg < 1) rg = 1;
@@ -263,16 +284,10 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
   const int g_blocks = L.g_blocks;
   const int F_aug = F + 8;
   const int ncb = L.Kp / 128, nfb = (F_aug + TF128 - 1) / TF128;
-  if (gdw_xcd_on()) {
-    const int rounds = (L.row_groups + 7) / 8;
-    hipLaunchKernelGGL((gdw_gemm_big_kernel<2>), dim3((unsigned)(8 * ncb * nfb * rounds)), dim3(256), 0, stream, G,
-                       L.Kp, static_cast<const uint16_t*>(X_aug), ldx, F_aug, B, K, L.rows_per_group, slabs, ncb * nfb,
-                       L.row_groups);
-  } else {
-    hipLaunchKernelGGL((gdw_gemm_big_kernel<2>), dim3((unsigned)ncb, (unsigned)nfb, (unsigned)L.row_groups), dim3(256),
-                       0, stream, G, L.Kp, static_cast<const uint16_t*>(X_aug), ldx, F_aug, B, K, L.rows_per_group,
-                       slabs, 0, L.row_groups);
-  }
+  const int rounds = (L.row_groups + 7) / 8;
+  hipLaunchKernelGGL((gdw_gemm_dma_kernel<3>), dim3((unsigned)(8 * ncb * nfb * rounds)), dim3(256), 0, stream, G, L.Kp,
+                     static_cast<const uint16_t*>(X_aug), ldx, F_aug, B, K, L.rows_per_group, slabs, ncb * nfb,
+                     L.row_groups);
   MLAPI_HIP_CHECK(hipGetLastError());
   launch_gdw_reduce(slabs, L.row_groups, K, F_aug, dW_out, stat_slabs, g_blocks, stats_out, update, dp,
                     dp_timeout_ms, stream);
