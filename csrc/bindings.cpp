@@ -347,8 +347,7 @@ PYBIND11_MODULE(_C, m) {
       py::arg("params"), py::arg("grad"), py::arg("mom"), py::arg("n"), py::arg("n_pen"), py::arg("lr"),
       py::arg("inv_n"), py::arg("l2"), py::arg("momentum"), py::arg("stream") = 0);
   m.def("softmax_grad_dw_supported", &softmax_grad_dw_supported);
-  m.def("softmax_grad_dw_force_plan", &softmax_grad_dw_force_plan, py::arg("row_groups") = 0, py::arg("nc") = 0,
-        py::arg("pipe") = 0);
+  m.def("softmax_grad_dw_force_plan", &softmax_grad_dw_force_plan, py::arg("row_groups") = 0, py::arg("nc") = 0);
   m.def("softmax_grad_dw_workspace", &softmax_grad_dw_workspace);
   m.def(
       "softmax_grad_dw",

@@ -259,7 +259,7 @@ void launch_softmax_rowstats(const void* X_aug, int64_t ldx, const void* W, cons
 // (narrower models are zero-padded by the caller), ldx = F + 8. Workspace:
 // softmax_grad_dw_workspace(B, K, F) bytes, zeroed once.
 bool softmax_grad_dw_supported(int F);
-void softmax_grad_dw_force_plan(int row_groups, int nc, int pipe);  // benchmark hook (0 = automatic)
+void softmax_grad_dw_force_plan(int row_groups, int nc);  // benchmark hook (0 = automatic)
 size_t softmax_grad_dw_workspace(int64_t B, int K, int F);
 // Optional SGD update fused into the final slab sum (one replica: no all-reduce between them):
 // params [K, cols] -= lr * (dW / N + l2 * params[:, :pen_cols]) with momentum, refreshing the bf16 /

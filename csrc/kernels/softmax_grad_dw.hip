@@ -128,9 +128,9 @@ struct GradDwArgs {
 // X fragment read from LDS feeds two MFMAs, halving the LDS bytes per MFMA (at NC = 1 both phases
 // need 256 B/clk/CU, the LDS array's peak).
 //
-// PIPE (NC = 2 only): a software pipeline across tiles with 3 LDS buffers. Iteration t computes the
-// logits of tile t+1 and the epilogue of tile t in one basic block, so the epilogue's VALU work
-// fills the MFMA issue gaps of the next tile's logits instead of running exposed at 1 wave/SIMD.
+// (A software pipeline across tiles with 3 LDS buffers - the logits of tile t+1 and the epilogue of
+// tile t in one basic block - measured equal, 136.9-137.3 vs 136.2-141.9 us per step
+// (profiles/r5_train/s35_pipe_ab.log), and left the build in round 5.)
 //
 // F = 512 (KS = 16): the double-buffered tile is 2 x 65 KB of LDS (one block per CU) and the 32
 // dW N-tiles alone take 128 accumulator registers, so it runs NC = 1 at one wave per SIMD
@@ -140,13 +140,12 @@ constexpr int gdw_waves_per_eu() {
   return KS >= 16 ? 1 : 3 - NC;
 }
 
-template <int KS, bool OVR, int NC, bool PIPE>
+template <int KS, bool OVR, int NC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gdw_waves_per_eu<KS, NC>(),
                                                                      gdw_waves_per_eu<KS, NC>()))) void
 softmax_grad_dw_kernel(GradDwArgs a) {
   static_assert(KS < 16 || NC == 1, "F = 512 runs 16 classes per wave");
-  static_assert(!PIPE || NC == 2, "the pipelined variant runs at 1 wave/SIMD (NC = 2)");
-  constexpr int NBUF = PIPE ? 3 : 2;
+  constexpr int NBUF = 2;
   constexpr int CLASSES = 4 * WAVE_CLASSES * NC;
   constexpr int F_ = KS * 32;
   constexpr int X_BYTES = (F_ / 128) * SUB_BYTES;
@@ -407,7 +406,7 @@ softmax_grad_dw_kernel(GradDwArgs a) {
   };
   const uint32_t smem_off = lds_off(smem);
 
-  if constexpr (!PIPE) {
+  {
     int buf = 0;
     MLAPI_DMA_TILE(t_begin, 0)
     if (t_begin + 1 < t_end) {
@@ -442,55 +441,6 @@ softmax_grad_dw_kernel(GradDwArgs a) {
         MLAPI_RAW_BARRIER()
       }
       buf ^= 1;
-    }
-  } else {
-    // prologue: tiles 0, 1, 2 in flight; 0 and 1 landed before the first logits
-    MLAPI_DMA_TILE(t_begin, 0)
-    if (t_begin + 1 < t_end) MLAPI_DMA_TILE(t_begin + 1, 1)
-    if (t_begin + 2 < t_end) {
-      MLAPI_DMA_TILE(t_begin + 2, 2)
-      __builtin_amdgcn_s_waitcnt(kWaitTile);
-    } else {
-      __builtin_amdgcn_s_waitcnt(kWaitAll);
-    }
-    MLAPI_RAW_BARRIER()
-    f32x4_t zc[NC][4];
-    init_z(zc);
-    logits(smem_off, zc, std::false_type{});
-    int bcur = 0;
-    for (int t = t_begin; t < t_end; ++t) {
-      const int bnext = bcur == NBUF - 1 ? 0 : bcur + 1;
-      const uint32_t xo = smem_off + bcur * BUF_BYTES;
-      const uint32_t xn = smem_off + bnext * BUF_BYTES;  // tile t+1 (stale data on the last tile: unused)
-      const int rows_left = (int)min<int64_t>(ROWS, B - (int64_t)t * ROWS);
-      read_meta(xo + X_BYTES);
-      wait_meta();
-      // logits of tile t+1 and the epilogue of tile t: one basic block per epilogue variant, so the
-      // scheduler can interleave the epilogue's VALU with the independent MFMAs
-      f32x4_t zn[NC][4];
-      init_z(zn);
-      if (rows_left == ROWS) {
-        logits(xn, zn, std::false_type{});
-        epilogue(std::false_type{}, zc, rows_left);
-      } else {
-        logits(xn, zn, std::false_type{});
-        epilogue(std::true_type{}, zc, rows_left);
-      }
-      row_stats(xo + X_BYTES, rows_left);
-      dw(xo);
-      if (t + 3 < t_end) {
-        MLAPI_RAW_BARRIER()  // every wave is done reading buffer bcur (tile t)
-        MLAPI_DMA_TILE(t + 3, bcur)
-        __builtin_amdgcn_s_waitcnt(kWaitTile);  // tile t+2 landed, t+3 flies
-      } else {
-        __builtin_amdgcn_s_waitcnt(kWaitAll);
-      }
-      MLAPI_RAW_BARRIER()
-#pragma unroll
-      for (int h = 0; h < NC; ++h)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) zc[h][mt] = zn[h][mt];
-      bcur = bnext;
     }
   }
 #undef MLAPI_RAW_BARRIER
@@ -738,7 +688,6 @@ struct GdwLayout {
 
 int g_force_row_groups = 0;  // benchmark hooks (softmax_grad_dw_force_plan)
 int g_force_nc = 0;
-int g_force_pipe = 0;  // 0 auto (off), 1 off, 2 on (NC = 2 only)
 
 int auto_nc(int K, int F) {
   if (F >= 512) return 1;
@@ -770,10 +719,9 @@ GdwLayout gdw_layout(int64_t B, int K, int F, int nc) {
 
 bool softmax_grad_dw_supported(int F) { return F == 128 || F == 256 || F == 512; }
 
-void softmax_grad_dw_force_plan(int row_groups, int nc, int pipe) {
+void softmax_grad_dw_force_plan(int row_groups, int nc) {
   g_force_row_groups = row_groups;
   g_force_nc = nc;
-  g_force_pipe = pipe;
 }
 
 size_t softmax_grad_dw_workspace(int64_t B, int K, int F) {  // enough for either class-tile plan
@@ -822,22 +770,10 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
   const bool ovr = kind == KIND_OVR;
   auto launch = [&](auto ks, auto nc) {
     constexpr int KS_ = decltype(ks)::value, NC_ = decltype(nc)::value;
-    // measured equal to the plain NC = 2 loop (127-130 us either way at B=65536, K=1000; the
-    // scheduler interleaves only part of the epilogue), so the simpler loop stays the default
-    const bool pipe = NC_ == 2 && g_force_pipe == 2;
-    if constexpr (NC_ == 2) {
-      if (pipe) {
-        if (ovr)
-          hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, true, 2, true>), grid, dim3(256), 0, stream, args);
-        else
-          hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, false, 2, true>), grid, dim3(256), 0, stream, args);
-        return;
-      }
-    }
     if (ovr)
-      hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, true, NC_, false>), grid, dim3(256), 0, stream, args);
+      hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, true, NC_>), grid, dim3(256), 0, stream, args);
     else
-      hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, false, NC_, false>), grid, dim3(256), 0, stream, args);
+      hipLaunchKernelGGL((softmax_grad_dw_kernel<KS_, false, NC_>), grid, dim3(256), 0, stream, args);
   };
   using I4 = std::integral_constant<int, 4>;
   using I8 = std::integral_constant<int, 8>;

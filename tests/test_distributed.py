@@ -33,15 +33,20 @@ def torchrun(nproc: int, script: str, env: dict, cwd=None, timeout=240, args=())
 
 
 def run(nproc, script, env, timeout=240, args=(), cwd=None):
-    p = torchrun(nproc, script, env, args=args, cwd=cwd)
-    try:
-        out, _ = p.communicate(timeout=timeout)
-    except subprocess.TimeoutExpired:
-        p.kill()
-        out, _ = p.communicate()
-        raise AssertionError("torchrun timed out:\n" + out[-3000:])
-    assert p.returncode == 0, out[-3000:]
-    return out
+    # free_port() releases its port before torchrun binds it: another process's ephemeral socket
+    # (gloo opens many) can take it in between. Only that rendezvous failure is retried, on a new port.
+    for attempt in range(3):
+        p = torchrun(nproc, script, env, args=args, cwd=cwd)
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+            raise AssertionError("torchrun timed out:\n" + out[-3000:])
+        if p.returncode != 0 and "EADDRINUSE" in out and attempt < 2:
+            continue
+        assert p.returncode == 0, out[-3000:]
+        return out
 
 
 def test_broadcast_and_dp_sgd_determinism(tmp_path):

@@ -36,18 +36,8 @@ def timed(fn, n=200):
 
 
 res = {}
-if os.environ.get("PIPE_AB"):  # fused-gradient cross-tile pipeline off (1) / on (2), streamed batches, interleaved
-    from mlapi_amd._native import C
-
-    for rnd in range(3):
-        for pipe in (1, 2):
-            C().softmax_grad_dw_force_plan(0, 2, pipe)
-            tr._bufs.clear()  # the workspace layout follows the forced plan
-            res[f"pipe{pipe}_two_shards_r{rnd}"] = timed(lambda s: tr.step(*shards[s % 2]))
-    C().softmax_grad_dw_force_plan(0, 0, 0)
-else:
-    res["eager_two_shards"] = timed(lambda s: tr.step(*shards[s % 2]))
-    res["eager_one_shard"] = timed(lambda s: tr.step(*shards[0]))
-    tr.capture(*shards[0])
-    res["graph_one_shard"] = timed(lambda s: tr.step(*shards[0]))
+res["eager_two_shards"] = timed(lambda s: tr.step(*shards[s % 2]))
+res["eager_one_shard"] = timed(lambda s: tr.step(*shards[0]))
+tr.capture(*shards[0])
+res["graph_one_shard"] = timed(lambda s: tr.step(*shards[0]))
 print(json.dumps({k: {"device_us": v[0], "host_us": v[1]} for k, v in res.items()}), flush=True)

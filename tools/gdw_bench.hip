@@ -4,9 +4,6 @@
 #ifndef MLAPI_GDW_NC
 #define MLAPI_GDW_NC 1
 #endif
-#ifndef MLAPI_GDW_PIPE
-#define MLAPI_GDW_PIPE false
-#endif
 #include "../csrc/kernels/softmax_grad_dw.hip"
 
 #include <cstdio>
@@ -66,14 +63,14 @@ int main() {
   hipEvent_t e0, e1;
   MLAPI_HIP_CHECK(hipEventCreate(&e0));
   MLAPI_HIP_CHECK(hipEventCreate(&e1));
-  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((softmax_grad_dw_kernel<8, false, MLAPI_GDW_NC, MLAPI_GDW_PIPE>), grid, dim3(256), 0, 0, a);
+  for (int i = 0; i < 5; ++i) hipLaunchKernelGGL((softmax_grad_dw_kernel<8, false, MLAPI_GDW_NC>), grid, dim3(256), 0, 0, a);
   const int n = 50;
   MLAPI_HIP_CHECK(hipEventRecord(e0));
-  for (int i = 0; i < n; ++i) hipLaunchKernelGGL((softmax_grad_dw_kernel<8, false, MLAPI_GDW_NC, MLAPI_GDW_PIPE>), grid, dim3(256), 0, 0, a);
+  for (int i = 0; i < n; ++i) hipLaunchKernelGGL((softmax_grad_dw_kernel<8, false, MLAPI_GDW_NC>), grid, dim3(256), 0, 0, a);
   MLAPI_HIP_CHECK(hipEventRecord(e1));
   MLAPI_HIP_CHECK(hipEventSynchronize(e1));
   float ms = 0.f;
   MLAPI_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-  printf("nc=%d pipe=%d exp=%d grid=%u kernel_us=%.2f\n", MLAPI_GDW_NC, (int)MLAPI_GDW_PIPE, MLAPI_GDW_EXP, grid.x, ms * 1e3f / n);
+  printf("nc=%d exp=%d grid=%u kernel_us=%.2f\n", MLAPI_GDW_NC, MLAPI_GDW_EXP, grid.x, ms * 1e3f / n);
   return 0;
 }

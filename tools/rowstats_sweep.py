@@ -48,7 +48,7 @@ ref = None
 for gp in GEMM:
     for rg in GROUPS:
         C().gemm_softmax_force_plan(*gp)
-        C().softmax_grad_dw_force_plan(rg, 0, 0)
+        C().softmax_grad_dw_force_plan(rg, 0)
         fb = ops.SoftmaxTrainBuffers(B, K, F, dev)  # the workspace layout depends on both plans
         out = torch.empty(K, Fa, device=dev)
         fn = lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=fb, dW_out=out, stats_out=stf)  # noqa: E731
@@ -58,4 +58,4 @@ for gp in GEMM:
         err = ((out - ref).abs().max() / ref.abs().max()).item()
         print(json.dumps({"gemm_plan": gp, "row_groups": rg, "us": round(us, 2), "max_rel_dw_err": err}), flush=True)
 C().gemm_softmax_force_plan(0, 0, 0)
-C().softmax_grad_dw_force_plan(0, 0, 0)
+C().softmax_grad_dw_force_plan(0, 0)

@@ -37,15 +37,15 @@ for F in (128, 256, 512):
     fb = ops.SoftmaxTrainBuffers(B, K, F, dev)
     res[f"F{F}_auto_us"] = timeit(lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=fb, dW_out=out, stats_out=stf))
     ref = out.clone()
-    plans = ((1, 0), (2, 1), (2, 2)) if F < 512 else ((1, 0),)
-    for nc, pipe in plans:
+    plans = (1, 2) if F < 512 else (1,)
+    for nc in plans:
         for groups in (0, 16, 32, 64):
-            C().softmax_grad_dw_force_plan(groups, nc, pipe)
+            C().softmax_grad_dw_force_plan(groups, nc)
             pb = ops.SoftmaxTrainBuffers(B, K, F, dev)  # the workspace layout depends on the forced plan
-            res[f"F{F}_nc{nc}_pipe{pipe}_groups{groups}_us"] = timeit(
+            res[f"F{F}_nc{nc}_groups{groups}_us"] = timeit(
                 lambda: ops.softmax_train_grad(X, W, bias, y, 2, bufs=pb, dW_out=out, stats_out=stf))
-            res[f"F{F}_nc{nc}_pipe{pipe}_groups{groups}_maxdiff"] = (out - ref).abs().max().item()
-    C().softmax_grad_dw_force_plan(0, 0, 0)
+            res[f"F{F}_nc{nc}_groups{groups}_maxdiff"] = (out - ref).abs().max().item()
+    C().softmax_grad_dw_force_plan(0, 0)
     res[f"F{F}_tflops_auto"] = 4 * B * K * Fa / res[f"F{F}_auto_us"] / 1e6  # rowstats + logits + dW
 for k, v in res.items():
     print(f"{k:36s} {v:10.3f}")
