@@ -250,7 +250,7 @@ for s in $steps; do
       prof serve 300 --steps 20 --warmup 2 --reqs-per-conn 512
       prof serve_wide 300 --mode serve_wide --steps 10 --warmup 2 --reqs-per-conn 256 ;;
     pmc_big)  # every counter group (one pass each) for the big kernels: gemm_softmax32 (B = 262,144),
-              # softmax_grad_dw (F = 256), softmax_rows MODE 5 + gdw_gemm128 (F = 1024)
+              # softmax_grad_dw (F = 256), softmax_rows MODE 5 + gdw_gemm_dma (F = 1024)
       PMC_BENCHES="gemm_big:--mode gemm --batch 262144 --steps 5 --warmup 1|tsm256:--mode train_softmax --steps 5 --warmup 1|tsm1024:--mode train_softmax --softmax-features 1024 --steps 5 --warmup 1" \
         run pmc_big 1200 bash tools/pmc_profile.sh ;;
     pmc_gemm) PMC_BENCHES="gemm:--mode gemm --steps 5 --warmup 1|gemm_big:--mode gemm --batch 262144 --steps 5 --warmup 1" run pmc_gemm 600 bash tools/pmc_profile.sh ;;
