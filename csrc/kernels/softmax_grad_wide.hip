@@ -215,7 +215,14 @@ WideLayout wide_layout(int64_t B, int K, int F) {
   L.Kp = (K + T - 1) / T * T;
   const int TFw = TF128;  // feature tile width
   const int tiles = (L.Kp / T) * ((F_aug + TFw - 1) / TFw);
-  int64_t rg = (2048 + tiles - 1) / tiles;
+  // ~1024 G^T X blocks (row groups x tiles): each row group adds a K x F_aug slab to the reduce.
+  // F = 1024, K = 1000 (72 tiles): 16 row groups 0.595 ms per step, 8: 0.605, 24: 0.597, 32: 0.613,
+  // 48: 0.642 (profiles/r5_train/s61, s62). MLAPI_GDW_TARGET overrides (measurement).
+  static const int target = [] {
+    const char* e = std::getenv("MLAPI_GDW_TARGET");
+    return e != nullptr ? std::atoi(e) : 1024;
+  }();
+  int64_t rg = (target + tiles - 1) / tiles;
   // a group's G / X bytes stay below 2^31 (the G^T X kernel's buffer offsets are 32-bit)
   const int64_t cap_rows = ((int64_t)INT32_MAX / (2 * std::max<int64_t>(L.Kp, F_aug))) / TILE_ROWS * TILE_ROWS;
   rg = std::max<int64_t>(rg, (B + cap_rows - 1) / cap_rows);
