@@ -18,11 +18,28 @@ pytestmark = pytest.mark.gpu
 ENV = {**os.environ, "PYTHONPATH": str(ROOT)}
 
 
+def _launch(nproc, script_args, env, cwd=None):
+    """torchrun on a free 127.0.0.1 port. The port is released before torchrun binds it, so another
+    process's ephemeral socket can take it in between: only that rendezvous failure (EADDRINUSE)
+    is retried, on a new port."""
+    import socket
+
+    for attempt in range(3):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", *script_args]
+        out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=cwd)
+        if out.returncode != 0 and "EADDRINUSE" in out.stdout + out.stderr and attempt < 2:
+            continue
+        return out
+
+
 def test_native_comm_semantics_world1(tmp_path):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-           "--master-addr=127.0.0.1", "--master-port=29731", str(ROOT / "tests" / "dist" / "comm_semantics.py")]
-    out = subprocess.run(cmd, env={**ENV, "OUT": str(tmp_path), "MLAPI_COMM": "native"}, capture_output=True,
-                         text=True, timeout=240)
+    out = _launch(1, [str(ROOT / "tests" / "dist" / "comm_semantics.py")],
+                  {**ENV, "OUT": str(tmp_path), "MLAPI_COMM": "native"})
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     assert (tmp_path / "OK_0").read_text() == "native-rccl"
 
@@ -63,16 +80,8 @@ def test_p2p_allreduce_multiprocess(tmp_path, world):
     exchanged over the TCP store, peers' buffers mapped, bitwise rank-order sums, double-buffered
     epochs, and a bounded wait (status 1, no hang) when a peer never arrives. On the 1-GPU box all
     ranks share the GPU (RCCL itself refuses that), which exercises the same code path."""
-    import socket
-
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", str(ROOT / "tests" / "dist" / "p2p_allreduce.py")]
-    out = subprocess.run(cmd, env={**ENV, "OUT": str(tmp_path), "OMP_NUM_THREADS": "1"}, capture_output=True,
-                         text=True, timeout=240, cwd=ROOT)
+    out = _launch(world, [str(ROOT / "tests" / "dist" / "p2p_allreduce.py")],
+                  {**ENV, "OUT": str(tmp_path), "OMP_NUM_THREADS": "1"}, cwd=ROOT)
     assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
     res = [json.loads((tmp_path / f"P2P_{r}.json").read_text()) for r in range(world)]
     assert all(x["checks"] == 7 for x in res)
@@ -81,17 +90,8 @@ def test_p2p_allreduce_multiprocess(tmp_path, world):
 
 
 def _torchrun(world, script, out_dir, args=(), env=None):
-    import socket
-
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     path = script if script.endswith("bench.py") else str(ROOT / "tests" / "dist" / script)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr=127.0.0.1", f"--master-port={port}", path, *args]
-    out = subprocess.run(cmd, env={**ENV, "OUT": str(out_dir), "OMP_NUM_THREADS": "1", **(env or {})},
-                         capture_output=True, text=True, timeout=240, cwd=ROOT)
+    out = _launch(world, [path, *args], {**ENV, "OUT": str(out_dir), "OMP_NUM_THREADS": "1", **(env or {})}, cwd=ROOT)
     assert out.returncode == 0, (out.stdout + out.stderr)[-3000:]
     return out.stdout
 
