@@ -124,6 +124,12 @@ py::dict stats_dict(const EngineStats& s) {
   d["resident_rows"] = s.resident_rows;
   d["resident_stale"] = s.resident_stale;
   d["resident_launches"] = s.resident_launches;
+  d["resident_hb_restarts"] = s.resident_hb_restarts;
+  d["resident_ring_restarts"] = s.resident_ring_restarts;
+  d["resident_self_exits"] = s.resident_self_exits;
+  d["resident_queue_faults"] = s.resident_queue_faults;
+  d["resident_abandoned"] = s.resident_abandoned;
+  d["resident_heartbeat"] = s.resident_heartbeat;
   d["resident_rings"] = s.resident_rings;
   d["resident_live"] = s.resident_live;
   d["generic_models"] = s.generic_models;
@@ -503,6 +509,24 @@ PYBIND11_MODULE(_C, m) {
              return mm ? names[mm->path] : "";
            })
       .def("inject_drop", &Engine::inject_drop, py::arg("on"))
+      // resident-path fault injection (tests): "stall" | "stall_sticky" (kept across relaunches) |
+      // "exit_ring" (arg = ring) | "ignore_stop" | "lease_starve" (arg = ms) | "queue_fault" | "none"
+      // (clear); False = no live instance to inject into
+      .def(
+          "resident_inject",
+          [](Engine& e, const std::string& mode, int arg) {
+            int m = -1;
+            if (mode == "none") m = RES_FAULT_NONE;
+            else if (mode == "stall") m = RES_FAULT_STALL;
+            else if (mode == "stall_sticky") m = Engine::RES_INJECT_STALL_STICKY;
+            else if (mode == "exit_ring") m = RES_FAULT_EXIT_RING;
+            else if (mode == "ignore_stop") m = RES_FAULT_IGNORE_STOP;
+            else if (mode == "lease_starve") m = Engine::RES_INJECT_LEASE_STARVE;
+            else if (mode == "queue_fault") m = Engine::RES_INJECT_QUEUE_FAULT;
+            else throw std::invalid_argument("unknown resident fault " + mode);
+            return e.resident_inject(m, arg);
+          },
+          py::arg("mode"), py::arg("arg") = 0)
       .def("mark_healthy", &Engine::mark_healthy)
       .def(
           "submit",
@@ -766,5 +790,6 @@ PYBIND11_MODULE(_C, m) {
           py::arg("requests_per_conn"), py::arg("record") = true)
       .def("set_workload", &Loadgen::set_workload, py::arg("requests"), py::arg("expected"),
            py::arg("rel_tol") = 0.0)
+      .def("set_conn_map", &Loadgen::set_conn_map, py::arg("mode"), py::arg("seed") = 1)
       .def("close", &Loadgen::close_all);
 }

@@ -26,6 +26,10 @@
 
 #include <pthread.h>
 
+#include <algorithm>
+#include <numeric>
+#include <random>
+
 namespace mlapi {
 
 namespace {
@@ -82,9 +86,21 @@ Loadgen::Loadgen(const std::string& host, int port, const std::string& request, 
     setsockopt(c->fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
   }
   freeaddrinfo(res);
+  order_.resize(conns);
+  std::iota(order_.begin(), order_.end(), 0);
 }
 
 Loadgen::~Loadgen() { close_all(); }
+
+void Loadgen::set_conn_map(const std::string& mode, uint64_t seed) {
+  std::iota(order_.begin(), order_.end(), 0);
+  if (mode == "shuffle") {
+    std::mt19937_64 rng(seed);
+    std::shuffle(order_.begin(), order_.end(), rng);
+  } else if (mode != "rr") {
+    throw std::invalid_argument("loadgen: conn map must be rr or shuffle");
+  }
+}
 
 void Loadgen::set_workload(const std::vector<std::string>& requests, const std::vector<std::string>& expected,
                            double rel_tol) {
@@ -150,7 +166,7 @@ LoadgenResult Loadgen::run(int64_t requests_per_conn, bool record) {
     pthread_setname_np(pthread_self(), "mlapi-loadgen");
     const int ep = epoll_create1(EPOLL_CLOEXEC);
     std::vector<LgConn*> mine;
-    for (int i = ti; i < nc; i += threads_) mine.push_back(conns_[i].get());
+    for (int i = ti; i < nc; i += threads_) mine.push_back(conns_[order_[i]].get());
     if (record) lats[ti].reserve((size_t)(requests_per_conn * (int64_t)mine.size()));
     int live = 0;
     const size_t nw = requests_.size();

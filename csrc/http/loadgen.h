@@ -35,6 +35,11 @@ class Loadgen {
   // bf16 GEMM path change the last bits); 0 = the whole body byte for byte.
   void set_workload(const std::vector<std::string>& requests, const std::vector<std::string>& expected,
                     double rel_tol = 0.0);
+  // Which epoll loop drives which connection: "rr" (default) = connection c on loop c % threads,
+  // i.e. in connect order; "shuffle" = a seeded random permutation of the connections dealt round
+  // robin - a client thread's connections then land wherever the server's dispatcher put them, as
+  // independent clients' would (not paired with the server's IO threads by connect order).
+  void set_conn_map(const std::string& mode, uint64_t seed = 1);
   // Every connection completes `requests_per_conn` closed-loop requests.
   LoadgenResult run(int64_t requests_per_conn, bool record = true);
   void close_all();
@@ -53,6 +58,7 @@ class Loadgen {
     return e ? (int64_t)std::atoll(e) * 1000 : (int64_t)0;
   }();
   int threads_;
+  std::vector<int> order_;  // connection index of slot i (thread i % threads_ drives it)
   std::vector<std::unique_ptr<LgConn>> conns_;
 };
 

@@ -6,6 +6,7 @@
 //   pin <cpu>,<cpu>,...                        sched_setaffinity (threads created later inherit it)
 //   workload <path> [rel_tol]                  "MLW1\n" then per entry "<req_len> <exp_len>\n" + bytes
 //   connect <host> <port> <conns> <threads> <timeout_s> [<source address>]
+//   connmap <rr|shuffle> [seed]                which loop drives which connection (after connect)
 //   run <requests_per_conn> <record 0|1>       -> {"completed":..,"p50_ns":..,...}
 //   close | quit
 #include <sched.h>
@@ -108,6 +109,14 @@ int main() {
         if (req.empty()) throw std::runtime_error("connect before workload");
         lg = std::make_unique<Loadgen>(host, port, req[0], conns, threads, timeout_s, source);
         lg->set_workload(req, exp, rel_tol);
+        reply("{\"ok\":true}");
+      } else if (cmd == "connmap") {
+        std::string mode;
+        unsigned long long seed = 1;
+        in >> mode;
+        if (!(in >> seed)) seed = 1;
+        if (!lg) throw std::runtime_error("connmap before connect");
+        lg->set_conn_map(mode, seed);
         reply("{\"ok\":true}");
       } else if (cmd == "run") {
         long long n = 0;

@@ -45,11 +45,22 @@ struct alignas(16) ResidentGranule {
 };
 inline uint32_t resident_mver(uint64_t model_version) { return (uint32_t)(model_version % 0xffffffu) + 1u; }
 
+// Fault injection (tests): ResidentCtl::fault, read by every wave with the stop word.
+// Each mode keeps the lease rule, so no injected fault can keep a wave alive past its process.
+enum ResidentFault : uint32_t {
+  RES_FAULT_NONE = 0,
+  RES_FAULT_STALL = 1,        // waves stop answering rows and block 0 stops its heartbeat (a hung instance)
+  RES_FAULT_EXIT_RING = 2,    // the wave of ring fault_arg exits at once (publishing its head)
+  RES_FAULT_IGNORE_STOP = 3,  // waves ignore the stop word (only the lease ends them)
+};
+
 // Control block (host-coherent memory). Host -> GPU words first, GPU -> host words after.
 struct alignas(64) ResidentCtl {
-  uint32_t stop;   // non-zero: every wave exits at its next check
-  uint32_t lease;  // bumped by the supervisor every ~10 ms
-  uint32_t pad0[14];
+  uint32_t stop;       // non-zero: every wave exits at its next check
+  uint32_t lease;      // bumped by the supervisor every ~10 ms
+  uint32_t fault;      // ResidentFault (0 in service)
+  uint32_t fault_arg;  // ... its argument (RES_FAULT_EXIT_RING: the ring)
+  uint32_t pad0[12];
   uint32_t heads[RESIDENT_MAX_RINGS];  // ring heads: read at start, written back at exit
   uint64_t heartbeat;                  // block 0: polls so far (published every 1024 polls)
   uint64_t rows;                       // block 0: rows answered (same cadence)

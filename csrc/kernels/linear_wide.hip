@@ -49,7 +49,9 @@ void launch_linear_wide(int dt, const void* X, int64_t ldx, const void* W, const
   const size_t es = dt == DT_F64 ? 8 : 4;
   if ((ldx * es) % 16 != 0 || reinterpret_cast<uintptr_t>(X) % 16 != 0 || reinterpret_cast<uintptr_t>(W) % 16 != 0)
     throw std::invalid_argument("linear_wide: X and W rows must be 16-byte aligned");
-  const int nb = wide_plan::tiles_per_group(B, p);
+  // host-merged launches (<= 32 rows) need ONE row group: 17-32 rows take the 2-tile group even
+  // where the planner would spread a small batch over more blocks
+  const int nb = hro.rec != nullptr && B > 16 ? 2 : wide_plan::tiles_per_group(B, p);
   const int rg = row_groups(B, nb);
   if (rg > 65535) throw std::invalid_argument("linear_wide: B too large for one launch");
   if (hro.rec != nullptr && (rg != 1 || binary)) throw std::invalid_argument("linear_wide: host merge needs one row group, multiclass");

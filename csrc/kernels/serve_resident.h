@@ -47,6 +47,7 @@ __device__ __forceinline__ void resident_serve(const ResidentArgs& a) {
   const uint64_t t0 = wall_clock64();
   uint64_t t_lease = t0, t_row = t0;
   uint32_t lease = 0xffffffffu, idle = 0;
+  uint32_t fault = RES_FAULT_NONE;  // injected fault (tests), re-read with the stop word
   const bool fetch = f < F;  // lanes past F carry no feature: they do not load and always match
   ru32x4_t g[D];
   uint32_t base[D];
@@ -81,7 +82,7 @@ __device__ __forceinline__ void resident_serve(const ResidentArgs& a) {
       }
       const uint32_t sh = head - base[d];  // the poll was issued at base[d] <= head
       const uint32_t fresh = sh >= (uint32_t)EPL ? 0u : (full >> sh) & ~done & ((1u << EPL) - 1u);
-      if (fresh != 0) {  // wave-uniform
+      if (fresh != 0 && fault != RES_FAULT_STALL) {  // wave-uniform
         const int wpos = ent - (int)sh;  // window position of this lane's row
         const bool mine = wpos >= 0 && ((fresh >> wpos) & 1u);
         if (fetch) s_x[ent][f] = (T)__builtin_bit_cast(double, (uint64_t)g[d][0] | ((uint64_t)g[d][1] << 32));
@@ -109,14 +110,20 @@ __device__ __forceinline__ void resident_serve(const ResidentArgs& a) {
       if ((polls & 63) == 0) {
         const uint32_t stop = __builtin_amdgcn_raw_buffer_load_b32(cs, (int)offsetof(ResidentCtl, stop), 0, 17);
         const uint32_t ls = __builtin_amdgcn_raw_buffer_load_b32(cs, (int)offsetof(ResidentCtl, lease), 0, 17);
+        fault = __builtin_amdgcn_readfirstlane(
+            __builtin_amdgcn_raw_buffer_load_b32(cs, (int)offsetof(ResidentCtl, fault), 0, 17));
         const uint64_t now = wall_clock64();
         if (ls != lease) {
           lease = ls;
           t_lease = now;
         }
-        if (stop != 0 || now - t_lease > a.lease_ticks || (a.idle_exit_ticks != 0 && now - t_row > a.idle_exit_ticks))
+        if ((stop != 0 && fault != RES_FAULT_IGNORE_STOP) || now - t_lease > a.lease_ticks ||
+            (a.idle_exit_ticks != 0 && now - t_row > a.idle_exit_ticks))
           quit = true;
-        if (r == 0 && (polls & 1023) == 0 && l == 0) {
+        if (fault == RES_FAULT_EXIT_RING &&
+            (uint32_t)r == __builtin_amdgcn_raw_buffer_load_b32(cs, (int)offsetof(ResidentCtl, fault_arg), 0, 17))
+          quit = true;
+        if (r == 0 && (polls & 1023) == 0 && l == 0 && fault != RES_FAULT_STALL) {
           __hip_atomic_store(&a.ctl->heartbeat, polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(&a.ctl->rows, rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }

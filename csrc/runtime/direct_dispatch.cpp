@@ -117,6 +117,7 @@ class HsaInlineDispatcher final : public InlineDispatcher {
     // a resident kernel still running (its owner waited and gave up): leave its queue and memory
     // alone - destroying them under a live wave is what the lease rule exists to avoid
     if (rqueue_ && !resident_wait(0)) rqueue_ = nullptr, rkernarg_ = nullptr, rsig_.handle = 0;
+    (void)resident_abandoned_done();  // frees the abandoned instances that have ended since
     if (rqueue_) hsa_queue_destroy(rqueue_);
     if (rkernarg_) hsa_amd_memory_pool_free(rkernarg_);
     if (rsig_.handle) hsa_signal_destroy(rsig_);
@@ -352,12 +353,32 @@ class HsaInlineDispatcher final : public InlineDispatcher {
 
   bool resident_faulted() const override { return rfault_.load(std::memory_order_relaxed); }
 
-  void resident_abandon() override {
+  void resident_abandon(bool track) override {
     rfault_.store(false);
+    // a queue in error never signals: forget it; a kernel that only ignored its stop word ends on
+    // its lease: keep watching its signal, and free its queue once it has ended
+    if (track && rqueue_ != nullptr) abandoned_.push_back(Abandoned{rqueue_, rkernarg_, rsig_});
     rqueue_ = nullptr;
     rkernarg_ = nullptr;
     rsig_.handle = 0;
   }
+
+  bool resident_abandoned_done() override {
+    for (size_t i = 0; i < abandoned_.size();) {
+      Abandoned& a = abandoned_[i];
+      if (hsa_signal_load_scacquire(a.sig) >= 1) {
+        ++i;
+        continue;
+      }
+      hsa_queue_destroy(a.queue);
+      if (a.kernarg) hsa_amd_memory_pool_free(a.kernarg);
+      hsa_signal_destroy(a.sig);
+      abandoned_.erase(abandoned_.begin() + (long)i);
+    }
+    return abandoned_.empty();
+  }
+
+  void inject_resident_fault() override { rfault_.store(true); }
 
   bool faulted() const override { return fault_.load(std::memory_order_relaxed); }
   uint64_t named_launches() const override { return named_launches_; }
@@ -445,6 +466,12 @@ class HsaInlineDispatcher final : public InlineDispatcher {
   hsa_queue_t* rqueue_ = nullptr;  // resident kernel queue
   void* rkernarg_ = nullptr;
   hsa_signal_t rsig_{};
+  struct Abandoned {  // resident instances that did not stop when told (resident_abandon(true))
+    hsa_queue_t* queue;
+    void* kernarg;
+    hsa_signal_t sig;
+  };
+  std::vector<Abandoned> abandoned_;
   uint32_t ka_slots_ = 64;
   bool hdp_readback_ = true;
   const uint32_t stride_ = (uint32_t)((sizeof(InlineBatch) + 255) / 256 * 256);

@@ -51,11 +51,17 @@ class InlineDispatcher : public KernelLauncher {
                                unsigned block) = 0;
   // Wait up to timeout_ms for the resident kernel to end: true = ended (or none running).
   virtual bool resident_wait(int timeout_ms) = 0;
-  // A resident kernel that did not end when told to: forget it and its queue (neither is touched
-  // again; the queue is not destroyed under a live wave) so the next launch gets a fresh queue.
-  virtual void resident_abandon() = 0;
+  // A resident kernel that did not end when told to, or whose queue failed: the next launch gets a
+  // fresh queue, and the old one is never destroyed under a live wave. track = true (a kernel that
+  // still runs and ends on its lease): its signal is watched by resident_abandoned_done(), which
+  // frees the queue once the kernel has ended; false (a queue in error): forgotten.
+  virtual void resident_abandon(bool track) = 0;
+  // true once every tracked abandoned instance has ended (their queues are then freed)
+  virtual bool resident_abandoned_done() = 0;
   // the resident queue reported an error (its kernel faulted): abandon it and launch afresh
   virtual bool resident_faulted() const = 0;
+  // fault injection (tests): report the resident queue as failed
+  virtual void inject_resident_fault() = 0;
 };
 
 // Loads `hsaco_path` (csrc/kernels/serve_direct.hip) for the GPU behind HIP device `device` and

@@ -1258,9 +1258,13 @@ void Engine::resident_register(bool on) {
 }
 
 void Engine::resident_halt(int timeout_ms) {
+  // under the instance lock: a launch that already passed its halt check cannot clear this stop
+  // afterwards, and the dispatcher's resident queue / signal are not swapped under the wait
+  std::lock_guard<std::mutex> lk(res_inst_mu_);
   res_halt_.store(true, std::memory_order_release);  // the supervisor launches nothing from now on
   res_live_.store(false, std::memory_order_release);
   if (res_ctl_h_ == nullptr) return;
+  __atomic_store_n(&res_ctl_h_->fault, (uint32_t)RES_FAULT_NONE, __ATOMIC_RELAXED);  // an injected ignore-stop too
   __atomic_store_n(&res_ctl_h_->stop, 1u, __ATOMIC_RELEASE);
   if (!res_cpu_ && direct_) (void)direct_->resident_wait(timeout_ms);
 }
@@ -1294,8 +1298,39 @@ void Engine::close_ring(ServeRing* ring) {
     segs.clear();
     _mm_pause();
   }
+  // rows still pending after 2 s: poisoned, with their tags and models dropped, so the ring's next
+  // owner (another IO thread, whose connection ids overlap this one's) never renders their answers
+  // and never rewrites their slots before the GPU is done with them
+  const int gave_up = ring->abandon_pending();
+  if (gave_up > 0) {
+    healthy_.store(false);
+    std::fprintf(stderr, "[mlapi engine] resident ring %d closed with %d rows unanswered\n", ring->idx_, gave_up);
+  }
   std::lock_guard<std::mutex> lk(rings_mu_);
-  free_rings_.push_back(ring);  // pending rows past 2 s stay poisoned in it: the slots are never reused
+  free_rings_.push_back(ring);
+}
+
+int ServeRing::abandon_pending() {
+  int n = 0;
+  for (uint32_t pos = tail_; pos != next_; ++pos) {
+    Pend& p = pend_[pos & (RESIDENT_RING - 1)];
+    if (!p.live) continue;
+    p.live = false;
+    p.poisoned = true;
+    p.tag = 0;
+    p.model.reset();
+    ++n;
+  }
+  live_n_ = 0;
+  tail_ = next_;
+  return n;
+}
+
+bool ServeRing::reclaim(Pend& p) {
+  if (!p.poisoned) return true;
+  if (!landed(p.pos)) return false;
+  p.poisoned = false;
+  return true;
 }
 
 ServeRing::ServeRing(Engine* e, int index) : eng_(e), idx_(index) {
@@ -1326,9 +1361,10 @@ bool ServeRing::submit(const double* X, int n, int nf, const uint64_t* tags) {
   std::shared_ptr<const Model> m = e.model();
   const uint32_t mver = e.res_mver_.load(std::memory_order_acquire);
   if (!m || m->path != PATH_SMALL || nf != m->F || resident_mver(m->version) != mver) return false;
-  // slots of given-up rows are never rewritten (the GPU may still answer them)
+  // slots of given-up rows are not rewritten until their late records land (the GPU may still
+  // read the entry and answer it)
   for (int i = 0; i < n; ++i)
-    if (pend_[(next_ + (uint32_t)i) & (RESIDENT_RING - 1)].poisoned) return false;
+    if (!reclaim(pend_[(next_ + (uint32_t)i) & (RESIDENT_RING - 1)])) return false;
   const int64_t t = now_ns();
   const uint32_t meta = mver << 8 | (uint32_t)nf;
   for (int i = 0; i < n; ++i) {
@@ -1338,6 +1374,7 @@ bool ServeRing::submit(const double* X, int n, int nf, const uint64_t* tags) {
     p.tag = tags[i];
     p.t_enq = t;
     p.model = m;
+    p.pos = pos;
     p.nf = nf;
     p.live = true;
     // every granule {x_f, pos, meta}: the value, then its tag word (x86 stores become visible in
@@ -1351,6 +1388,7 @@ bool ServeRing::submit(const double* X, int n, int nf, const uint64_t* tags) {
     }
   }
   next_ += (uint32_t)n;
+  live_n_ += n;
   return true;
 }
 
@@ -1392,7 +1430,12 @@ int ServeRing::poll(std::vector<Completion>& out, std::vector<Seg>& segs, Sink* 
       if (wd > 0 && waited > 10 * wd) {
         fail = true;  // the record may still land later: this slot is never written again
       } else {
-        if (wd > 0 && waited > wd) e.healthy_.store(false);
+        if (wd > 0 && waited > wd) {
+          // this ring's wave stopped answering (it exited or hung while block 0 still beats): the
+          // supervisor restarts the instance, whose waves resume from the published ring heads
+          e.healthy_.store(false);
+          if (!e.res_ring_stall_.exchange(true)) e.kick_resident();
+        }
         continue;
       }
     }
@@ -1405,6 +1448,7 @@ int ServeRing::poll(std::vector<Completion>& out, std::vector<Seg>& segs, Sink* 
       const uint64_t tag = p.tag;
       p.live = false;
       p.model.reset();
+      --live_n_;
       if (sink != nullptr) {
         const int k = e.submit_many(x, 1, p.nf, &tag, sink);
         if (k == 1) {
@@ -1445,12 +1489,11 @@ int ServeRing::poll(std::vector<Completion>& out, std::vector<Seg>& segs, Sink* 
     ++done;
     p.live = false;
     p.model.reset();
+    --live_n_;
   }
-  while (tail_ != next_) {
-    const Pend& p = pend_[tail_ & (RESIDENT_RING - 1)];
-    if (p.live || p.poisoned) break;
-    ++tail_;
-  }
+  // consumed and given-up rows alike leave the window (a poisoned slot is reclaimed by submit once
+  // its late record lands)
+  while (tail_ != next_ && !pend_[tail_ & (RESIDENT_RING - 1)].live) ++tail_;
   if (done > 0 || stale > 0) {
     std::lock_guard<std::mutex> lk(e.st_mu_);
     e.stats_.requests += (uint64_t)done;
@@ -1460,7 +1503,7 @@ int ServeRing::poll(std::vector<Completion>& out, std::vector<Seg>& segs, Sink* 
     e.stats_.latency_sum_us += lat_sum;
     for (int b = 0; b < 24; ++b) e.stats_.latency_hist[b] += lat_hist[b];
   }
-  return (int)(next_ - tail_);
+  return live_n_;
 }
 
 namespace {
@@ -1468,6 +1511,8 @@ int resident_lpe(int F) { return F <= 4 ? 4 : F <= 8 ? 8 : 32; }
 }  // namespace
 
 bool Engine::resident_launch(const std::shared_ptr<const Model>& m, uint32_t mver, int nrings, bool bounce) {
+  if (!res_fault_sticky_.load(std::memory_order_relaxed))  // injections are per instance unless sticky
+    __atomic_store_n(&res_ctl_h_->fault, (uint32_t)RES_FAULT_NONE, __ATOMIC_RELAXED);
   if (res_cpu_) return true;  // the supervisor polls the rings itself
   if (!direct_) return false;
   ResidentArgs a{};
@@ -1490,24 +1535,71 @@ bool Engine::resident_launch(const std::shared_ptr<const Model>& m, uint32_t mve
   const bool f64 = bounce ? true : m->xdt == DT_F64;
   char name[64];
   std::snprintf(name, sizeof name, "mlapi_resident_%s_r%d_d%d", f64 ? "f64" : "f32", lpe, depth);
+  std::lock_guard<std::mutex> lk(res_inst_mu_);
+  if (res_halt_.load(std::memory_order_acquire)) return false;  // halted since the supervisor's check
   __atomic_store_n(&res_ctl_h_->stop, 0u, __ATOMIC_RELEASE);
   return direct_->resident_launch(name, &a, sizeof a, (unsigned)nrings, 64);
 }
 
 bool Engine::resident_stop_instance(int timeout_ms) {
+  std::lock_guard<std::mutex> lk(res_inst_mu_);
   __atomic_store_n(&res_ctl_h_->stop, 1u, __ATOMIC_RELEASE);
   if (res_cpu_) return true;
   if (direct_->resident_wait(timeout_ms)) return true;
-  // never ended: keep its memory alive and forget its queue (the lease rule ends it eventually)
-  std::fprintf(stderr, "[mlapi engine] resident kernel did not stop within %d ms: abandoned\n", timeout_ms);
-  direct_->resident_abandon();
+  // never ended: keep its memory alive and leave it to its lease (the supervisor stops bumping it
+  // while res_leaked_ is set); its queue is freed and the path resumes once it has ended
+  std::fprintf(stderr, "[mlapi engine] resident kernel did not stop within %d ms: abandoned to its lease\n",
+               timeout_ms);
+  direct_->resident_abandon(/*track=*/true);
   res_leaked_ = true;
   healthy_.store(false);
+  std::lock_guard<std::mutex> sl(st_mu_);
+  stats_.resident_abandoned++;
   return false;
+}
+
+bool Engine::resident_inject(int mode, int arg) {
+  if (res_ctl_h_ == nullptr) return false;
+  if (mode == RES_FAULT_NONE) {  // clear (a sticky injection too)
+    res_fault_sticky_.store(false);
+    __atomic_store_n(&res_ctl_h_->fault, (uint32_t)RES_FAULT_NONE, __ATOMIC_RELEASE);
+    return true;
+  }
+  if (!res_live_.load(std::memory_order_acquire)) return false;
+  if (mode == RES_INJECT_STALL_STICKY) {  // a hang that survives restarts: the rows' give-up path
+    res_fault_sticky_.store(true);
+    mode = RES_FAULT_STALL;
+  }
+  switch (mode) {
+    case RES_FAULT_STALL:
+    case RES_FAULT_EXIT_RING:
+    case RES_FAULT_IGNORE_STOP:
+      // the CPU backend's host poller plays a hang (STALL) but has no waves to exit or to ignore stop
+      if (res_cpu_ && mode != RES_FAULT_STALL) return false;
+      __atomic_store_n(&res_ctl_h_->fault_arg, (uint32_t)arg, __ATOMIC_RELAXED);
+      __atomic_store_n(&res_ctl_h_->fault, (uint32_t)mode, __ATOMIC_RELEASE);
+      return true;
+    case RES_INJECT_LEASE_STARVE:
+      res_starve_until_.store(now_ns() + (int64_t)std::max(0, arg) * 1000000);
+      return true;
+    case RES_INJECT_QUEUE_FAULT: {
+      if (res_cpu_ || !direct_) return false;
+      std::lock_guard<std::mutex> lk(res_inst_mu_);
+      res_fault_queue_.store(true);
+      direct_->inject_resident_fault();
+      __atomic_store_n(&res_ctl_h_->stop, 1u, __ATOMIC_RELEASE);  // the instance ends; its queue reads as failed
+      return true;
+    }
+    default:
+      return false;
+  }
 }
 
 // CPU backend: one pass of the resident kernel's protocol over every ring (the same tag rules).
 int Engine::resident_cpu_poll(const std::shared_ptr<const Model>& m, uint32_t mver, int nrings, bool bounce) {
+  // an injected hang: no row answered, no heartbeat (the watchdogs' tests on GPU-less hosts)
+  if (__atomic_load_n(&res_ctl_h_->fault, __ATOMIC_ACQUIRE) == RES_FAULT_STALL) return 0;
+  __atomic_store_n(&res_ctl_h_->heartbeat, res_ctl_h_->heartbeat + 1, __ATOMIC_RELAXED);
   int rows = 0;
   for (int r = 0; r < nrings; ++r) {
     uint32_t head = __atomic_load_n(&res_ctl_h_->heads[r], __ATOMIC_ACQUIRE);
@@ -1554,7 +1646,7 @@ void Engine::resident_loop() {
   std::shared_ptr<const Model> inst_model;
   uint64_t seen_kick = ~uint64_t(0);
   uint64_t last_hb = 0;
-  int64_t t_hb = now_ns(), t_retry = 0, t_row = 0;
+  int64_t t_hb = now_ns(), t_retry = 0, t_row = 0, t_ring_restart = 0;
   bool served = false;  // an instance has served rows that a successor may have to bounce
   auto set_live = [&](bool live) {
     res_live_.store(live, std::memory_order_release);
@@ -1589,21 +1681,44 @@ void Engine::resident_loop() {
       stopping = res_stop_;
       seen_kick = res_kick_;
     }
-    __atomic_fetch_add(&res_ctl_h_->lease, 1u, __ATOMIC_RELEASE);
-    if (res_leaked_) {  // an instance that never stopped owns the rings: the resident path stays off
-      if (stopping) break;
-      continue;
-    }
-    if (running && !res_cpu_ && direct_->resident_wait(0)) {
-      // ended by itself: the bounce instance's idle exit, a lease expiry (this thread starved) or a fault
-      running = false;
-      if (direct_->resident_faulted()) {
-        std::fprintf(stderr, "[mlapi engine] resident kernel queue error: restarting on a fresh queue\n");
-        direct_->resident_abandon();
-        healthy_.store(false);
+    // the lease: not while an abandoned instance (one that ignored its stop word) still owns the
+    // rings - it then ends on the lease rule - and not while a starvation is injected
+    if (!res_leaked_ && now_ns() >= res_starve_until_.load(std::memory_order_relaxed))
+      __atomic_fetch_add(&res_ctl_h_->lease, 1u, __ATOMIC_RELEASE);
+    if (res_leaked_) {
+      // the resident path stays off until the abandoned instance has ended (its queue is then freed)
+      bool done;
+      {
+        std::lock_guard<std::mutex> lk(res_inst_mu_);
+        done = direct_->resident_abandoned_done();
       }
+      if (stopping) break;
+      if (!done) continue;
+      std::fprintf(stderr, "[mlapi engine] abandoned resident kernel ended: resident path resumes\n");
+      res_leaked_ = false;
+    }
+    bool ended = false;
+    if (running && !res_cpu_) {
+      std::lock_guard<std::mutex> lk(res_inst_mu_);
+      ended = direct_->resident_wait(0);
+      if (ended && direct_->resident_faulted()) {
+        std::fprintf(stderr, "[mlapi engine] resident kernel queue error: restarting on a fresh queue\n");
+        // an injected fault ended cleanly: its queue is freed once seen ended; a real one is forgotten
+        direct_->resident_abandon(/*track=*/res_fault_queue_.exchange(false));
+        healthy_.store(false);
+        std::lock_guard<std::mutex> sl(st_mu_);
+        stats_.resident_queue_faults++;
+      }
+      (void)direct_->resident_abandoned_done();
+    }
+    if (ended) {
+      // ended by itself: the bounce instance's idle exit, a lease expiry (this thread starved), an
+      // early wave exit or a fault
+      running = false;
       if (inst_bounce) served = false;
       set_live(false);
+      std::lock_guard<std::mutex> sl(st_mu_);
+      stats_.resident_self_exits++;
     }
     if (stopping) {
       stop_inst();
@@ -1640,7 +1755,7 @@ void Engine::resident_loop() {
         set_live(false);
       }
     }
-    if (running && !res_cpu_ && !inst_bounce && cfg_.watchdog_ms > 0) {
+    if (running && !inst_bounce && cfg_.watchdog_ms > 0) {
       const uint64_t hb = __atomic_load_n(&res_ctl_h_->heartbeat, __ATOMIC_ACQUIRE);
       if (hb != last_hb) {
         last_hb = hb;
@@ -1651,6 +1766,23 @@ void Engine::resident_loop() {
         healthy_.store(false);
         stop_inst();
         t_hb = now;
+        t_ring_restart = now;
+        std::lock_guard<std::mutex> sl(st_mu_);
+        stats_.resident_hb_restarts++;
+      }
+    }
+    if (res_ring_stall_.load(std::memory_order_relaxed)) {
+      // a ring's row waited past the watchdog: restart the instance (at most once per watchdog
+      // period; an instance that is not running is relaunched above anyway)
+      const bool act = running && !inst_bounce && now - t_ring_restart > (int64_t)cfg_.watchdog_ms * 1000000;
+      if (act || !running) res_ring_stall_.store(false);
+      if (act) {
+        std::fprintf(stderr, "[mlapi engine] resident ring stalled: restarting the instance\n");
+        stop_inst();
+        t_ring_restart = now;
+        t_hb = now;
+        std::lock_guard<std::mutex> sl(st_mu_);
+        stats_.resident_ring_restarts++;
       }
     }
   }
@@ -1668,6 +1800,7 @@ EngineStats Engine::stats() const {
   }
   s.healthy = healthy_.load();
   s.dropped = drop_.load();
+  if (res_ctl_h_ != nullptr) s.resident_heartbeat = __atomic_load_n(&res_ctl_h_->heartbeat, __ATOMIC_RELAXED);
   s.direct_dispatch = direct_ != nullptr;
   s.direct_device_kernargs = direct_ != nullptr && direct_->device_kernargs();
   return s;

@@ -133,7 +133,11 @@ class ServeRing {
   // stale (a hot reload raced its submit) goes through the engine queue to `sink` instead; the
   // number of those is added to *requeued. Returns the rows still pending.
   int poll(std::vector<Completion>& out, std::vector<Seg>& segs, Sink* sink, int* requeued);
-  int pending() const { return (int)(next_ - tail_); }
+  // rows submitted and not yet answered (given-up rows are not counted: nothing waits for them)
+  int pending() const { return live_n_; }
+  // Give up on every pending row (the owning thread leaves the ring): their slots stay out of
+  // reuse until their records land, and no answer of theirs is ever rendered. Returns the rows.
+  int abandon_pending();
   // Spin (user space, no syscall) until a pending row's record lands or `ns` passed: true if one did.
   bool wait_any(int64_t ns) const;
 
@@ -145,15 +149,19 @@ class ServeRing {
   int idx_;
   ResidentGranule* ring_;  // this ring's entries (host view)
   ServeRecord* rec_;       // this ring's records (host view)
-  uint32_t next_ = 0, tail_ = 0;  // positions: [tail_, next_) submitted and not yet consumed
+  uint32_t next_ = 0, tail_ = 0;  // positions: [tail_, next_) submitted, not yet consumed or given up
+  int live_n_ = 0;                // live rows (pending())
   struct Pend {
     uint64_t tag = 0;
     int64_t t_enq = 0;
     std::shared_ptr<const Model> model;
+    uint32_t pos = 0;       // ring position of the row last written into this slot
     int32_t nf = 0;
     bool live = false;      // submitted, answer not yet consumed
-    bool poisoned = false;  // given up on (watchdog): the slot is never written again
+    bool poisoned = false;  // given up on (watchdog / ring closed): not rewritten until its record lands
   };
+  // a poisoned slot whose record has landed since (the GPU answered late) is free again
+  bool reclaim(Pend& p);
   Pend pend_[RESIDENT_RING];
 };
 
@@ -241,6 +249,12 @@ struct EngineStats {
   uint64_t resident_rows = 0;       // rows answered by the resident kernel (ServeRing)
   uint64_t resident_stale = 0;      // ... bounced to the engine queue (a hot reload raced them)
   uint64_t resident_launches = 0;   // resident kernel instances launched (start, reload, restart)
+  uint64_t resident_hb_restarts = 0;    // ... stopped and relaunched: block 0's heartbeat stalled
+  uint64_t resident_ring_restarts = 0;  // ... stopped and relaunched: a ring's row waited past the watchdog
+  uint64_t resident_self_exits = 0;     // instances that ended by themselves (lease expiry, early exit)
+  uint64_t resident_queue_faults = 0;   // ... on a queue error (relaunched on a fresh queue)
+  uint64_t resident_abandoned = 0;      // instances that did not stop when told (left to their lease)
+  uint64_t resident_heartbeat = 0;      // block 0's poll count (liveness; GPU instances)
   int resident_rings = 0;           // rings the running instance polls (0: none running)
   bool resident_live = false;       // IO threads may submit to their rings now
   uint64_t generic_models = 0;      // models loaded onto the scalar GENERIC kernel (a warning is logged)
@@ -308,6 +322,15 @@ class Engine {
   void close_ring(ServeRing* ring);
   // Stop the resident kernel for good (process exit): no relaunch, wait up to timeout_ms for it.
   void resident_halt(int timeout_ms);
+  // Fault injection into the resident path (tests). Kernel-side (the running instance,
+  // cleared when the supervisor relaunches): RES_FAULT_STALL, RES_FAULT_EXIT_RING (arg = ring),
+  // RES_FAULT_IGNORE_STOP; RES_FAULT_NONE clears. Host-side: RES_INJECT_LEASE_STARVE (the supervisor stops bumping the
+  // lease for arg ms), RES_INJECT_QUEUE_FAULT (the running instance is stopped and its queue
+  // treated as faulted). false: no resident instance to inject into.
+  static constexpr int RES_INJECT_LEASE_STARVE = 16;
+  static constexpr int RES_INJECT_QUEUE_FAULT = 17;
+  static constexpr int RES_INJECT_STALL_STICKY = 18;  // RES_FAULT_STALL kept across relaunches (until NONE)
+  bool resident_inject(int mode, int arg);
 
   EngineStats stats() const;
   const EngineConfig& config() const { return cfg_; }
@@ -435,6 +458,13 @@ class Engine {
   std::atomic<bool> res_halt_{false};   // resident_halt: never launch again
   std::atomic<uint32_t> res_mver_{0};   // 24-bit version of the model the running instance serves
   std::atomic<int> res_nrings_{0};      // rings the running instance polls
+  // launch / stop / halt / abandon of the instance: one at a time (the at-exit halt runs on another
+  // thread than the supervisor)
+  std::mutex res_inst_mu_;
+  std::atomic<bool> res_ring_stall_{false};     // ServeRing::poll: a row waited past the watchdog
+  std::atomic<int64_t> res_starve_until_{0};    // injection: no lease bump before this (now_ns)
+  std::atomic<bool> res_fault_queue_{false};    // injection: treat the ending instance's queue as faulted
+  std::atomic<bool> res_fault_sticky_{false};   // injection: the fault word survives relaunches
   std::thread res_thread_;
 
   std::vector<std::thread> batchers_;

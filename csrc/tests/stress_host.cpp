@@ -2,6 +2,8 @@
 // ("host C++ built with -fsanitize=address,undefined in a debug target; TSAN-style
 // stress tests of the batcher"). Runs on the CPU backend (device = -1), so it needs no GPU:
 //
+//   0. resident rings: an injected hang (rows given up after 10 x watchdog, no busy loop after),
+//      a ring closed with rows pending and handed to its next owner, restarts by the watchdogs;
 //   1. engine: 8 submitter threads x random batch sizes, results checked against the float64
 //      oracle, while another thread hot-swaps the model (version-tagged results must match the
 //      model they were computed with), polls stats() and unloads/reloads;
@@ -316,7 +318,88 @@ void http_stress() {
 
 }  // namespace
 
+// The resident rings' failure paths on the CPU backend (the supervisor thread plays the kernel):
+// a sticky injected hang makes rows give up after 10 x watchdog (a 500, never a hang, and no busy
+// IO loop afterwards: pending() drops to 0); a ring closed with rows pending hands its next owner
+// none of the old rows' answers; after the hang clears, the reopened ring serves correct answers.
+void ring_stress() {
+  EngineConfig cfg;
+  cfg.device = -1;
+  cfg.resident = 1;
+  cfg.watchdog_ms = 300;  // rows give up after 3 s: past close_ring's 2 s wait
+  Engine eng(cfg);
+  auto m0 = make_model(3, KIND_MULTINOMIAL);
+  eng.load_model(m0.kind, m0.F, m0.K, m0.W.data(), m0.b.data(), {"\"a\"", "\"b\"", "\"c\""});
+  ServeRing* ring = eng.open_ring();
+  CHECK(ring != nullptr, "no ring");
+  if (ring == nullptr) return;
+  std::vector<Completion> out;
+  std::vector<ServeRing::Seg> segs;
+  int rq = 0;
+  const double x[8] = {5.1, 3.5, 1.4, 0.2, 6.7, 3.0, 5.2, 2.3};
+  auto submit = [&](uint64_t tag0, int n) {  // retried while an instance (re)starts
+    const uint64_t tags[2] = {tag0, tag0 + 1};
+    for (int i = 0; i < 4000; ++i) {
+      if (ring->submit(x, n, 4, tags)) return true;
+      std::this_thread::sleep_for(std::chrono::microseconds(500));
+    }
+    return false;
+  };
+  auto drain = [&](int want, int ms) {
+    out.clear();
+    segs.clear();
+    const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(ms);
+    while ((int)out.size() < want && std::chrono::steady_clock::now() < until) {
+      ring->poll(out, segs, nullptr, &rq);
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+  };
+  auto check_answers = [&](uint64_t tag0) {
+    for (const Completion& c : out) {
+      int32_t idx;
+      double p;
+      cpu_linear_predict(*eng.model(), x + 4 * (c.tag - tag0), 1, &idx, &p);
+      CHECK(c.status == ST_OK && c.idx == idx && c.p == p, "ring answer tag %llu", (unsigned long long)c.tag);
+    }
+  };
+  CHECK(submit(10, 2), "submit (healthy)");
+  drain(2, 2000);
+  CHECK(out.size() == 2, "healthy ring answered %zu of 2", out.size());
+  check_answers(10);
+  // sticky hang: the rows give up after 10 x watchdog as device errors; nothing stays pending
+  CHECK(eng.resident_inject(Engine::RES_INJECT_STALL_STICKY, 0), "inject");
+  CHECK(submit(20, 2), "submit (stalled)");
+  drain(2, 6000);
+  CHECK(out.size() == 2 && out[0].status == ST_DEVICE_ERROR && out[1].status == ST_DEVICE_ERROR,
+        "given-up rows: %zu completions", out.size());
+  CHECK(ring->pending() == 0, "pending after give-up: %d", ring->pending());
+  // close with rows pending (still hung): the next owner sees none of them
+  CHECK(submit(30, 2), "submit (before close)");
+  eng.close_ring(ring);  // waits 2 s, then abandons them
+  CHECK(!eng.healthy(), "closing a ring with rows unanswered marks the engine unhealthy");
+  CHECK(eng.resident_inject(RES_FAULT_NONE, 0), "clear");
+  std::this_thread::sleep_for(std::chrono::milliseconds(50));  // the old rows' records land now
+  ServeRing* again = eng.open_ring();
+  CHECK(again == ring, "the pooled ring comes back");
+  ring = again;
+  out.clear();
+  segs.clear();
+  ring->poll(out, segs, nullptr, &rq);
+  CHECK(out.empty() && ring->pending() == 0, "reopened ring rendered %zu old answers", out.size());
+  CHECK(submit(40, 2), "submit (reopened)");
+  drain(2, 2000);
+  CHECK(out.size() == 2 && out[0].tag == 40 && out[1].tag == 41, "reopened ring answered %zu", out.size());
+  check_answers(40);
+  const EngineStats s = eng.stats();
+  CHECK(s.resident_hb_restarts + s.resident_ring_restarts >= 1, "no watchdog restart counted");
+  eng.close_ring(ring);
+  eng.stop();
+  std::printf("ring stress: give-up, close-with-pending and reopen OK (%llu restarts)\n",
+              (unsigned long long)(s.resident_hb_restarts + s.resident_ring_restarts));
+}
+
 int main() {
+  ring_stress();
   engine_stress();
   http_stress();
   if (g_fail.load() != 0) {

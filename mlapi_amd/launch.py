@@ -58,6 +58,21 @@ def rank_placement(mode: str, nproc: int, **sysfs) -> List[List[int]]:
     return [numa_rank_cpus(r, nodes, cpus, **kw) for r in range(nproc)]
 
 
+def numa_omp_threads(placement: List[List[int]], r: int, quota: Optional[float] = -1.0) -> int:
+    """OMP_NUM_THREADS for rank r under numa placement: its mask's CPUs split over the ranks that
+    share that mask, capped by the rank's share of the cgroup CPU quota (``quota`` None = no quota,
+    -1 = read it from the cgroup)."""
+    from mlapi_amd.utils.threads import cgroup_cpu_quota
+
+    mask = set(placement[r])
+    sharing = max(1, sum(1 for c in placement if set(c) == mask))
+    n = max(1, len(mask) // sharing)
+    q = cgroup_cpu_quota() if quota == -1.0 else quota
+    if q:
+        n = min(n, max(1, int(q // max(1, len(placement)))))
+    return n
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="python -m mlapi_amd.launch", description=__doc__.split("\n\n")[0])
     ap.add_argument("--nproc", type=int, default=0, help="ranks (default: visible GPU count, at least 1)")
@@ -116,6 +131,10 @@ def main(argv=None) -> int:
         cpus = placement[r]
         if cpus and mode == "cores":
             env["OMP_NUM_THREADS"] = str(max(1, len(cpus)))
+        elif cpus and mode == "numa" and "OMP_NUM_THREADS" not in os.environ:
+            # a node mask is shared by the ranks whose GPUs sit on that node: each rank's OpenMP /
+            # torch pool gets its share (and its share of the cgroup quota), not the whole mask
+            env["OMP_NUM_THREADS"] = str(numa_omp_threads(placement, r))
         if cpus:
             env["MLAPI_PLACEMENT"] = mode
         pre = (lambda c=cpus: os.sched_setaffinity(0, c)) if cpus else None

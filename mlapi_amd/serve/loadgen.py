@@ -137,6 +137,11 @@ class LoadgenProcess:
         """source: local IPv4 address to connect from ("" = the kernel's choice)."""
         return self.cmd(f"connect {host} {int(port)} {int(conns)} {int(threads)} {timeout_s} {source or '-'}")
 
+    def conn_map(self, mode: str, seed: int = 1) -> dict:
+        """rr: connection c on load-generator thread c % threads (connect order); shuffle: a seeded
+        permutation, so a thread's connections are not paired with the server's IO threads."""
+        return self.cmd(f"connmap {mode} {int(seed)}")
+
     def run(self, requests_per_conn: int, record: bool = True) -> dict:
         return self.cmd(f"run {int(requests_per_conn)} {1 if record else 0}")
 

@@ -83,10 +83,32 @@ def render(engine_stats: Optional[dict] = None, server_stats: Optional[dict] = N
             out += ["# HELP mlapi_xcd_merge_errors_total Rows failed because an XCD-local split merge read a misplaced partial.",
                     "# TYPE mlapi_xcd_merge_errors_total counter"]
             _line(out, "mlapi_xcd_merge_errors_total", es["xcd_errors"], labels)
-        if "lane_batches" in es:
-            out += ["# HELP mlapi_lane_batches_total Batches IO threads dispatched themselves through engine lanes.",
-                    "# TYPE mlapi_lane_batches_total counter"]
-            _line(out, "mlapi_lane_batches_total", es["lane_batches"], labels)
+        if "resident_rows" in es:
+            # the resident SMALL-path kernel (csrc/include/mlapi/resident.h): the default Iris path,
+            # which launches no batch per request (mlapi_batches_total stays flat while it serves)
+            out += ["# HELP mlapi_resident_rows_total Rows answered by the resident kernel through the IO threads' rings.",
+                    "# TYPE mlapi_resident_rows_total counter"]
+            _line(out, "mlapi_resident_rows_total", es["resident_rows"], labels)
+            out += ["# HELP mlapi_resident_stale_total Resident rows bounced to the engine queue (a hot reload raced them).",
+                    "# TYPE mlapi_resident_stale_total counter"]
+            _line(out, "mlapi_resident_stale_total", es["resident_stale"], labels)
+            out += ["# HELP mlapi_resident_launches_total Resident kernel instances launched (start, reload, restart).",
+                    "# TYPE mlapi_resident_launches_total counter"]
+            _line(out, "mlapi_resident_launches_total", es["resident_launches"], labels)
+            out += ["# HELP mlapi_resident_restarts_total Resident instances stopped and relaunched, by cause.",
+                    "# TYPE mlapi_resident_restarts_total counter"]
+            for cause, key in (("heartbeat", "resident_hb_restarts"), ("ring_stall", "resident_ring_restarts"),
+                               ("self_exit", "resident_self_exits"), ("queue_fault", "resident_queue_faults"),
+                               ("abandoned", "resident_abandoned")):
+                _line(out, "mlapi_resident_restarts_total", es.get(key, 0), {**labels, "cause": cause})
+            out += ["# HELP mlapi_resident_live 1 while IO threads submit rows to a running resident instance.",
+                    "# TYPE mlapi_resident_live gauge"]
+            _line(out, "mlapi_resident_live", 1 if es.get("resident_live") else 0, labels)
+            out += ["# TYPE mlapi_resident_rings gauge"]
+            _line(out, "mlapi_resident_rings", es.get("resident_rings", 0), labels)
+            out += ["# HELP mlapi_resident_heartbeat Block 0's poll count (moves while the instance is alive).",
+                    "# TYPE mlapi_resident_heartbeat gauge"]
+            _line(out, "mlapi_resident_heartbeat", es.get("resident_heartbeat", 0), labels)
     if server_stats:
         out += ["# HELP mlapi_http_requests_total HTTP requests by path taken.",
                 "# TYPE mlapi_http_requests_total counter"]

@@ -21,10 +21,10 @@ DEVICES = [pytest.param("cpu", id="cpu"), pytest.param("cuda:0", id="gpu", marks
 def _cfg(device, names, **kw):
     from mlapi_amd.utils.config import Config
 
-    kw.setdefault("io_threads", 4)
-    kw.setdefault("resident", "on")
-    return Config.from_env(port=0, device=device, reload="off", missing_model="keep",
-                           model_path="/nonexistent/resident.pkl", feature_names=list(names), **kw)
+    base = {"io_threads": 4, "resident": "on", "reload": "off", "missing_model": "keep",
+            "model_path": "/nonexistent/resident.pkl"}
+    base.update(kw)
+    return Config.from_env(port=0, device=device, feature_names=list(names), **base)
 
 
 def _stats_delta(s0, s1):
@@ -244,3 +244,125 @@ def test_per_rank_cpus_share_of_quota(monkeypatch):
     assert comm.per_rank_cpus() == 16     # capped by the rank's share of a 128-CPU quota
     monkeypatch.delenv("MLAPI_PLACEMENT")
     assert comm.per_rank_cpus() == 12     # unplaced: the 96-CPU mask shared by all 8 ranks
+
+
+# ---- failure paths (VERDICT r5 missing 3) ------------------------------------------------
+# Each injected fault must end with every request answered - 200 with the exact body, or a 500 -
+# never a hang, and a new instance serving the rings afterwards.
+FAULTS = [pytest.param("cpu", "stall", 0, id="cpu-stall"),
+          pytest.param("cuda:0", "stall", 0, id="gpu-stall", marks=pytest.mark.gpu),
+          pytest.param("cuda:0", "exit_ring", 0, id="gpu-exit_ring", marks=pytest.mark.gpu),
+          pytest.param("cuda:0", "lease_starve", 600, id="gpu-lease_starve", marks=pytest.mark.gpu),
+          pytest.param("cuda:0", "queue_fault", 0, id="gpu-queue_fault", marks=pytest.mark.gpu),
+          pytest.param("cuda:0", "ignore_stop", 0, id="gpu-ignore_stop", marks=pytest.mark.gpu)]
+
+
+def _wait_live(srv, n_rings, timeout=10.0):
+    import time
+
+    t_end = time.time() + timeout
+    while time.time() < t_end:
+        st = srv.runtime.handle.stats()
+        if st["resident_live"] and st["resident_rings"] >= n_rings:
+            return st
+        time.sleep(0.01)
+    raise AssertionError(f"resident instance not live: {srv.runtime.handle.stats()}")
+
+
+@pytest.mark.parametrize("device,mode,arg", FAULTS)
+def test_resident_fault_every_request_answered(native, device, mode, arg):
+    """Inject a resident-path fault under load (8 connections over 4 IO threads, watchdog 200 ms):
+    stall (block 0's heartbeat stops, no row answered: heartbeat / ring watchdog restart),
+    exit_ring (ring 0's wave exits: ring watchdog restart), lease_starve (the supervisor stops
+    bumping the lease: the waves exit on their own and are relaunched), queue_fault (the instance's
+    queue reads as failed: relaunch on a fresh queue), ignore_stop (the waves ignore the stop word; a
+    hot reload's stop times out: abandoned to its lease, the path resumes once it has ended)."""
+    import time
+
+    from mlapi_amd.serve.loadgen import make_workload
+    from mlapi_amd.serve.server import NativeServer
+
+    m = LinearModel.random(4, 3, seed=13, labels=LABELS)
+    X = np.round(np.random.default_rng(6).standard_normal((256, 4)) * 2 + 4, 1)
+    with NativeServer(_cfg(device, IRIS, watchdog_ms=200)) as srv:
+        h = srv.runtime.handle
+        h.load(m)
+        eng = h.engine
+        reqs, exp = make_workload(eng, m, IRIS, X, rtol_oracle=1e-12, label_margin=1e-5)
+        lg = native.Loadgen("127.0.0.1", srv.port, reqs[0].decode(), 8, 2, 20.0)
+        lg.set_workload([r.decode() for r in reqs], [e.decode() for e in exp], 0.0)
+        lg.run(20, False)
+        _wait_live(srv, 4)
+        s0 = h.stats()
+        assert eng.resident_inject(mode, arg)
+        if mode == "ignore_stop":
+            h.load(m)  # a reload stops the instance: the stop is ignored, the instance abandoned
+        t0 = time.time()
+        res = lg.run(150, True)
+        took = time.time() - t0
+        s1 = h.stats()
+        # every request answered (the bodies of the 200s byte-exact), within bounded time
+        assert res["failed"] == 0 and res["body_mismatches"] == 0, res
+        assert sum(res["status_counts"].values()) == 8 * 150 and set(res["status_counts"]) <= {200, 500}, res
+        assert res["status_counts"].get(200, 0) >= 8 * 140, res
+        assert took < 15.0, took
+        restarts = {k: s1[k] - s0[k] for k in ("resident_hb_restarts", "resident_ring_restarts",
+                                               "resident_self_exits", "resident_queue_faults",
+                                               "resident_abandoned", "resident_launches")}
+        want = {"stall": ("resident_hb_restarts", "resident_ring_restarts"), "exit_ring": ("resident_ring_restarts",),
+                "lease_starve": ("resident_self_exits",), "queue_fault": ("resident_queue_faults",),
+                "ignore_stop": ("resident_abandoned",)}[mode]
+        assert sum(restarts[k] for k in want) >= 1, restarts
+        # a new instance serves the rings afterwards
+        _wait_live(srv, 4, timeout=15.0)
+        s2 = h.stats()
+        res2 = lg.run(100, True)
+        s3 = h.stats()
+        lg.close()
+        assert res2["status_counts"] == {200: 800} and res2["body_mismatches"] == 0, res2
+        assert s3["resident_rows"] - s2["resident_rows"] >= 700, (s2, s3)
+        assert s3["resident_launches"] > s0["resident_launches"], (s0, s3)
+
+
+def test_resident_metrics_lines(native, iris_cwd):
+    """/metrics exports the resident path that serves the default Iris model: rows, stale bounces,
+    launches, restarts by cause, liveness, rings and the heartbeat; the removed lanes' counter is gone."""
+    import socket
+
+    from mlapi_amd.serve.server import NativeServer
+
+    srv = NativeServer(_cfg("cpu", IRIS, model_path="LRClassifier.pkl", reload="mtime", missing_model="error")).start()
+    try:
+        body = b'{"sepal_length":5.1,"sepal_width":3.5,"petal_length":1.4,"petal_width":0.2}'
+        req = (b"POST /predict HTTP/1.1\r\nHost: t\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n%s"
+               % (len(body), body))
+        lg = native.Loadgen("127.0.0.1", srv.port, req.decode(), 4, 1)
+        lg.run(20, False)
+        _wait_live(srv, 1)
+        r = lg.run(200, False)
+        lg.close()
+        assert r["status_counts"] == {200: 800}, r
+        s = socket.create_connection(("127.0.0.1", srv.port), timeout=5)
+        s.sendall(b"GET /metrics HTTP/1.1\r\nHost: t\r\nConnection: close\r\n\r\n")
+        data = b""
+        while True:
+            c = s.recv(65536)
+            if not c:
+                break
+            data += c
+        s.close()
+        text = data.split(b"\r\n\r\n", 1)[1].decode()
+        vals = {}
+        for line in text.splitlines():
+            if line.startswith("mlapi_resident"):
+                name, v = line.rsplit(" ", 1)
+                vals[name.split("{")[0] + ("{" + name.split("{")[1] if "cause" in name else "")] = float(v)
+        assert vals["mlapi_resident_rows_total"] >= 800, vals
+        assert vals["mlapi_resident_live"] == 1 and vals["mlapi_resident_rings"] >= 1, vals
+        assert vals["mlapi_resident_launches_total"] >= 1 and vals["mlapi_resident_heartbeat"] > 0, vals
+        assert "mlapi_resident_stale_total" in vals, vals
+        causes = {k for k in vals if k.startswith("mlapi_resident_restarts_total")}
+        assert len(causes) == 5, causes
+        assert "mlapi_lane_batches_total" not in text
+    finally:
+        srv.stop()
