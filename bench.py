@@ -80,6 +80,10 @@ def _comm_probe(info, model=None) -> dict:
     kind = getattr(info.comm, "kind", info.backend)
     out["rccl_nranks"] = (info.comm_nranks() if kind in ("native-rccl", "torch-rccl") or info.backend == "nccl"
                           else None)
+    if info.world == 1:
+        # one rank: a broadcast / all-reduce moves nothing over xGMI - no latency worth reporting
+        out["collectives"] = "noop_world1"
+        return out
     if model is None:
         model = LinearModel.random(256, 1000, seed=3) if info.is_main else None
     barrier(info)
@@ -162,38 +166,59 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
             if w["failed"] or w["errors"]:
                 raise RuntimeError(f"warmup failed: {w}")
         barrier(info)  # every rank's warmup traffic has drained before the counters are read
-        s0, h0 = srv.runtime.handle.stats(), srv.http.stats()
-        c0, l0 = cpu_by_group(), cpu_by_group(lg.pid)
-        elapsed, res = _timed(info, lambda: lg.run(args.steps * args.reqs_per_conn, True))
-        cpu_util = utilization(c0, cpu_by_group(), elapsed)
-        cpu_util["loadgen_process"] = utilization(l0, cpu_by_group(lg.pid), elapsed).get("process_total", 0.0)
-        s1, h1 = srv.runtime.handle.stats(), srv.http.stats()
-        nreq = max(1, s1["requests"] - s0["requests"])
-        nbat = max(1, (s1["batches"] - s0["batches"]) - (s1["idle_batches"] - s0["idle_batches"]))  # batcher launches
-        # where this rank's server CPU goes, per request (IO-thread stage clock, exclusive; "poll"
-        # is epoll_wait + loop overhead, mostly idle blocking) and the server-side HTTP latency
-        cpu_breakdown = {
-            "server_cpu_us_per_req": cpu_util.get("process_total", 0.0) * elapsed / nreq * 1e6,
-            # requests this rank served per second of server CPU (all its threads): what decides the
-            # whole-node number when the ranks share the node's CPUs
-            "req_per_s_per_server_core": nreq / max(1e-9, cpu_util.get("process_total", 0.0) * elapsed),
-            "io_stage_us_per_req": {k: (h1["stage_ns"][k] - h0["stage_ns"][k]) / nreq / 1e3 for k in h1["stage_ns"]},
-            "engine_queue_wait_us_per_req": (s1["queue_wait_us_sum"] - s0["queue_wait_us_sum"]) / nreq,
-            # engine threads, per GPU batch (launched by the batcher): where a batch's time goes
-            "batcher_us_per_batch": {k: (s1["batcher_ns"][k] - s0["batcher_ns"][k]) / nbat / 1e3
-                                     for k in s1["batcher_ns"]},
-            "completer_us_per_batch": {k: (s1["completer_ns"][k] - s0["completer_ns"][k]) / nbat / 1e3
-                                       for k in s1["completer_ns"]},
-            # inside `launch`, zero-copy / BAR batches only (the wide models' paths), per such batch
-            "wide_launch_us_per_batch": {k: (s1["launch_ns"][k] - s0["launch_ns"][k]) / nbat / 1e3
-                                         for k in s1["launch_ns"]},
-            "server_http_latency_us_mean": (h1["http_latency_sum_ns"] - h0["http_latency_sum_ns"]) / 1e3
-            / max(1, h1["http_latency_count"] - h0["http_latency_count"]),
-        }
+
+        def phase(steps):
+            """One timed closed-loop phase: (elapsed, loadgen result, server CPU breakdown)."""
+            s0, h0 = srv.runtime.handle.stats(), srv.http.stats()
+            c0, l0 = cpu_by_group(), cpu_by_group(lg.pid)
+            elapsed, res = _timed(info, lambda: lg.run(steps * args.reqs_per_conn, True))
+            cpu_util = utilization(c0, cpu_by_group(), elapsed)
+            cpu_util["loadgen_process"] = utilization(l0, cpu_by_group(lg.pid), elapsed).get("process_total", 0.0)
+            s1, h1 = srv.runtime.handle.stats(), srv.http.stats()
+            nreq = max(1, s1["requests"] - s0["requests"])
+            nbat = max(1, (s1["batches"] - s0["batches"]) - (s1["idle_batches"] - s0["idle_batches"]))  # batcher launches
+            # where this rank's server CPU goes, per request (IO-thread stage clock, exclusive; "poll"
+            # is epoll_wait + loop overhead, mostly idle blocking) and the server-side HTTP latency
+            cpu_breakdown = {
+                "server_cpu_us_per_req": cpu_util.get("process_total", 0.0) * elapsed / nreq * 1e6,
+                # requests this rank served per second of server CPU (all its threads): what decides the
+                # whole-node number when the ranks share the node's CPUs
+                "req_per_s_per_server_core": nreq / max(1e-9, cpu_util.get("process_total", 0.0) * elapsed),
+                "io_stage_us_per_req": {k: (h1["stage_ns"][k] - h0["stage_ns"][k]) / nreq / 1e3 for k in h1["stage_ns"]},
+                "engine_queue_wait_us_per_req": (s1["queue_wait_us_sum"] - s0["queue_wait_us_sum"]) / nreq,
+                # engine threads, per GPU batch (launched by the batcher): where a batch's time goes
+                "batcher_us_per_batch": {k: (s1["batcher_ns"][k] - s0["batcher_ns"][k]) / nbat / 1e3
+                                         for k in s1["batcher_ns"]},
+                "completer_us_per_batch": {k: (s1["completer_ns"][k] - s0["completer_ns"][k]) / nbat / 1e3
+                                           for k in s1["completer_ns"]},
+                # inside `launch`, zero-copy / BAR batches only (the wide models' paths), per such batch
+                "wide_launch_us_per_batch": {k: (s1["launch_ns"][k] - s0["launch_ns"][k]) / nbat / 1e3
+                                             for k in s1["launch_ns"]},
+                "server_http_latency_us_mean": (h1["http_latency_sum_ns"] - h0["http_latency_sum_ns"]) / 1e3
+                / max(1, h1["http_latency_count"] - h0["http_latency_count"]),
+                "steered_conns": h1.get("steered", 0) - h0.get("steered", 0),
+            }
+            want = steps * args.reqs_per_conn * args.conns
+            if res["failed"] or res["errors"] or res["body_mismatches"] or res["ok200"] != want:
+                raise RuntimeError(f"load generator saw errors: {res}")
+            return elapsed, res, cpu_util, cpu_breakdown, s0, s1
+
+        elapsed, res, cpu_util, cpu_breakdown, s0, s1 = phase(args.steps)
+        shuffled = None
+        if args.shuffle_steps > 0:
+            # the same connections, dealt to the load generator's threads by a seeded permutation: a
+            # client thread's connections then sit on several IO threads (not paired by connect
+            # order), as independent clients' would. Measured after the headline phase, same run.
+            lg.conn_map("shuffle", 1000 + info.rank)
+            el2, res2, cu2, cb2, _, _ = phase(args.shuffle_steps)
+            lg.conn_map("rr")
+            tot2 = float(all_gather_floats([res2["completed"]], info)[:, 0].sum())
+            shuffled = {"req_per_s": tot2 / el2, "p50_latency_ms_c64": res2["p50_ns"] / 1e6,
+                        "p99_latency_ms_c64": res2["p99_ns"] / 1e6,
+                        "server_cpu_us_per_req": cb2["server_cpu_us_per_req"],
+                        "steered_conns": cb2["steered_conns"], "cpu_cores_busy_rank0": cu2,
+                        "io_stage_us_per_req": cb2["io_stage_us_per_req"]}
         lg.cmd("close")
-        want = args.steps * args.reqs_per_conn * args.conns
-        if res["failed"] or res["errors"] or res["body_mismatches"] or res["ok200"] != want:
-            raise RuntimeError(f"load generator saw errors: {res}")
         # batch = 1: one client, closed loop, measured by rank 0 alone (the other ranks idle)
         r1 = {"p50_ns": 0, "p99_ns": 0, "completed": 0, "elapsed_s": 1.0}
         barrier(info)
@@ -251,6 +276,9 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         "backend": srv.runtime.handle.backend,
         "cpu_cores_busy_rank0": cpu_util,
         "cpu_breakdown_rank0": cpu_breakdown,
+        # the shuffled-connection phase (see phase() above): whole-node req/s and rank 0's server CPU
+        "req_per_s_shuffled": None if shuffled is None else shuffled["req_per_s"],
+        "shuffled_rank0": shuffled,
         "threads": {"io": args.io_threads, "loadgen": args.client_threads, "pinned_cpus": args.pinned_cpus,
                     # launcher placement of this rank (numa: its GPU's NUMA-node mask) and its mask size
                     "placement": os.environ.get("MLAPI_PLACEMENT", "cores" if args.pinned_cpus else "none"),
@@ -521,6 +549,9 @@ def main(argv=None) -> int:
                     help="serve: one step = conns x this many requests per rank (~0.15-0.25 s, so the "
                          "driver's 20 steps time >= 2 s even at 1.3 M req/s)")
     ap.add_argument("--workload-rows", type=int, default=1024, help="serve: distinct validated requests")
+    ap.add_argument("--shuffle-steps", type=int, default=-1,
+                    help="serve: steps of the extra phase with the load generator's connections dealt to its "
+                         "threads by a seeded permutation (req_per_s_shuffled); -1 = --steps, 0 = skip")
     ap.add_argument("--wide-classes", type=int, default=1000, help="serve_wide: 2 = binary GEMV, else softmax GEMM")
     ap.add_argument("--wide-dtype", default="f64", choices=["f64", "f32", "bf16"],
                     help="serve_wide: kernel operand dtype (f64 = the engine default, sklearn's precision)")
@@ -557,6 +588,8 @@ def main(argv=None) -> int:
     args = ap.parse_args(argv)
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
+    if args.shuffle_steps < 0:
+        args.shuffle_steps = args.steps
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
         # `python bench.py --gpus N`: start the N rank processes ourselves (one per GPU) through the

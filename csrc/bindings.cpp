@@ -590,6 +590,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("idle_max_conns", &ServerConfig::idle_max_conns)
       .def_readwrite("io_spin_lowload_us", &ServerConfig::io_spin_lowload_us)
       .def_readwrite("io_spin_max_conns", &ServerConfig::io_spin_max_conns)
+      .def_readwrite("io_steer", &ServerConfig::io_steer)
+      .def_readwrite("steer_every", &ServerConfig::steer_every)
+      .def_readwrite("steer_stable", &ServerConfig::steer_stable)
       .def_readwrite("access_log", &ServerConfig::access_log)
       .def_readwrite("access_log_fd", &ServerConfig::access_log_fd)
       .def_readwrite("health_dispatch", &ServerConfig::health_dispatch)
@@ -735,6 +738,7 @@ PYBIND11_MODULE(_C, m) {
         d["errors"] = st.errors;
         d["bad_requests"] = st.bad_requests;
         d["listen_closes"] = st.listen_closes;
+        d["steered"] = st.steered;
         d["accepting"] = st.accepting;
         d["listeners"] = s.listeners();
         py::dict stg;

@@ -25,6 +25,7 @@
 #include <thread>
 
 #include <pthread.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <numeric>
@@ -164,6 +165,23 @@ LoadgenResult Loadgen::run(int64_t requests_per_conn, bool record) {
   const int64_t t0 = mono_ns();
   auto worker = [&](int ti) {
     pthread_setname_np(pthread_self(), "mlapi-loadgen");
+    if (pin_threads_) {
+      // each client thread on one CPU of the process's mask (thread i -> its i-th CPU): like a NIC
+      // whose RX queues are pinned, every connection's segments then arrive from one stable CPU
+      cpu_set_t set;
+      CPU_ZERO(&set);
+      if (sched_getaffinity(0, sizeof set, &set) == 0) {
+        int k = 0, pick = -1;
+        for (int c = 0; c < CPU_SETSIZE && pick < 0; ++c)
+          if (CPU_ISSET(c, &set) && k++ == ti) pick = c;
+        if (pick >= 0) {
+          cpu_set_t one;
+          CPU_ZERO(&one);
+          CPU_SET(pick, &one);
+          pthread_setaffinity_np(pthread_self(), sizeof one, &one);
+        }
+      }
+    }
     const int ep = epoll_create1(EPOLL_CLOEXEC);
     std::vector<LgConn*> mine;
     for (int i = ti; i < nc; i += threads_) mine.push_back(conns_[order_[i]].get());

@@ -57,6 +57,11 @@ class Loadgen {
     const char* e = std::getenv("MLAPI_LOADGEN_SPIN_US");
     return e ? (int64_t)std::atoll(e) * 1000 : (int64_t)0;
   }();
+  // MLAPI_LOADGEN_PIN_THREADS=1: thread i runs on the i-th CPU of the process's affinity mask
+  bool pin_threads_ = [] {
+    const char* e = std::getenv("MLAPI_LOADGEN_PIN_THREADS");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
   int threads_;
   std::vector<int> order_;  // connection index of slot i (thread i % threads_ drives it)
   std::vector<std::unique_ptr<LgConn>> conns_;

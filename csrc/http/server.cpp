@@ -124,6 +124,12 @@ struct Conn {
   int client_port = 0, server_port = 0;
   std::string req_line;       // access log: request line of the outstanding request
   uint64_t t_req = 0;         // rdtsc when the outstanding request was fully parsed
+  // io_steer
+  uint32_t nreq = 0;          // fast-path requests parsed on this connection
+  int in_cpu = -1;            // SO_INCOMING_CPU at the last sample ...
+  int same_n = 0;             // ... and on how many samples in a row
+  int move_to = -1;           // IO thread to hand the connection to once it is idle
+  int64_t moved_ns = 0;       // when it last moved (at most one move per 50 ms)
 };
 
 // A run of engine completions that share one model (render_fast's unit).
@@ -243,6 +249,15 @@ class IoThread : public Sink {
     wake();
   }
 
+  // io_steer: an idle connection handed over by another IO thread (a new id is assigned here)
+  void adopt_conn(std::unique_ptr<Conn> c) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      moved_in_.push_back(std::move(c));
+    }
+    wake();
+  }
+
   void post_slow(uint64_t conn_id, std::string&& bytes, bool close) {
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -252,6 +267,7 @@ class IoThread : public Sink {
   }
 
   std::atomic<uint64_t> n_fast{0}, n_slow{0}, n_resp{0}, n_conn{0}, n_err{0}, n_bad{0}, n_listen_close{0};
+  std::atomic<uint64_t> n_steered{0};
   // published copies of the stage clock / latency histogram (ticks; see ServerStats)
   std::atomic<uint64_t> pub_stage[SS_COUNT] = {};
   std::atomic<uint64_t> pub_lat[HTTP_LAT_BUCKETS] = {};
@@ -781,18 +797,30 @@ class IoThread : public Sink {
     fast_seg.clear();
     std::vector<SlowResp> slow;
     std::vector<int> adopted;
+    std::vector<std::unique_ptr<Conn>> moved;
     {
       std::lock_guard<std::mutex> lk(mu_);
       fast_c.swap(fast_c_);
       fast_seg.swap(fast_seg_);
       if (!slow_.empty()) slow.swap(slow_);
       if (!adopted_.empty()) adopted.swap(adopted_);
+      if (!moved_in_.empty()) moved.swap(moved_in_);
     }
     for (int fd : adopted) {
       sockaddr_storage ss{};
       socklen_t sl = sizeof ss;
       getpeername(fd, reinterpret_cast<sockaddr*>(&ss), &sl);
       register_conn(fd, ss);
+    }
+    for (auto& c : moved) {
+      // idle when it left its old thread; level-triggered EPOLLIN reports bytes that arrived meanwhile
+      c->id = next_id_++;
+      epoll_event ev{};
+      ev.events = EPOLLIN | EPOLLRDHUP;
+      ev.data.u64 = c->id;
+      epoll_ctl(epfd_, EPOLL_CTL_ADD, c->fd, &ev);
+      const uint64_t id = c->id;
+      conns_.emplace(id, std::move(c));
     }
     outstanding_ = std::max<int64_t>(0, outstanding_ - (int64_t)fast_c.size());
     for (size_t k = 0; k < fast_seg.size(); ++k) {
@@ -834,7 +862,47 @@ class IoThread : public Sink {
       c->paused = false;
       update_events(c);
     }
-    return flush(c);
+    if (!flush(c)) return false;
+    if (c->move_to >= 0 && !c->waiting && !c->close_after && c->in_pos == c->in.size() && c->out.empty() &&
+        !c->epollout)
+      return migrate(c);
+    return true;
+  }
+
+  // io_steer: sample the connection's incoming CPU every steer_every fast-path requests; seen twice
+  // in a row on a CPU another IO thread owns, the connection moves there once it is idle
+  void steer_sample(Conn* c) {
+    const int every = srv_->config().steer_every;
+    if (srv_->config().io_steer <= 0 || every <= 0 || ++c->nreq % (uint32_t)every != 0) return;
+    int cpu = -1;
+    socklen_t l = sizeof cpu;
+    if (getsockopt(c->fd, SOL_SOCKET, SO_INCOMING_CPU, &cpu, &l) != 0 || cpu < 0) return;
+    if (cpu != c->in_cpu) {
+      c->in_cpu = cpu;
+      c->same_n = 1;
+      return;
+    }
+    // only a CPU seen on steer_stable samples in a row counts (a client thread the scheduler keeps
+    // moving gives no stable CPU, and its connections stay where they are)
+    if (++c->same_n < std::max(2, srv_->config().steer_stable)) return;
+    const int t = srv_->steer_target(cpu, index_);
+    if (t != index_ && t >= 0 && mono_ns() - c->moved_ns > 50000000) c->move_to = t;
+  }
+
+  // hand an idle connection to another IO thread (returns false: it is no longer this thread's)
+  bool migrate(Conn* c) {
+    const int t = c->move_to;
+    c->move_to = -1;
+    if (t < 0 || t >= srv_->io_thread_count() || t == index_) return true;
+    epoll_ctl(epfd_, EPOLL_CTL_DEL, c->fd, nullptr);
+    auto it = conns_.find(c->id);
+    std::unique_ptr<Conn> up = std::move(it->second);
+    conns_.erase(it);
+    up->moved_ns = mono_ns();
+    up->nreq = 0;
+    n_steered.fetch_add(1, std::memory_order_relaxed);
+    srv_->io_thread(t)->adopt_conn(std::move(up));
+    return false;
   }
 
   static bool ieq(const char* a, size_t n, const char* lower_lit, size_t m) {
@@ -933,6 +1001,7 @@ class IoThread : public Sink {
     c->t_req = timing_ ? __rdtsc() : 0;
     pend_tags_.push_back(c->id);
     n_fast.fetch_add(1, std::memory_order_relaxed);
+    steer_sample(c);
     return 1;
   }
 
@@ -1109,6 +1178,7 @@ class IoThread : public Sink {
           c->t_req = timing_ ? __rdtsc() : 0;
           pend_tags_.push_back(c->id);
           n_fast.fetch_add(1, std::memory_order_relaxed);
+          steer_sample(c);
           return 1;
         }
         pend_x_.resize(at);
@@ -1164,6 +1234,7 @@ class IoThread : public Sink {
   std::atomic<bool> blocked_{true};    // in (or about to enter) a blocking epoll_wait: hand-offs need the eventfd
   std::mutex mu_;
   std::vector<int> adopted_;  // acceptor mode: connections handed over by the dispatcher
+  std::vector<std::unique_ptr<Conn>> moved_in_;  // io_steer: connections handed over by other IO threads
   bool timing_ = false;
   double ns_per_tick_ = 1.0;
   uint64_t st_acc_[SS_COUNT] = {};
@@ -1194,6 +1265,35 @@ class IoThread : public Sink {
 HttpServer::HttpServer(Engine* engine, const ServerConfig& cfg) : engine_(engine), cfg_(cfg) {
   if (cfg_.io_threads < 1) cfg_.io_threads = 1;
   if (cfg_.io_threads > 64) cfg_.io_threads = 64;
+  steer_ncpu_ = (int)std::min<long>(4096, std::max<long>(1, sysconf(_SC_NPROCESSORS_CONF)));
+  steer_.reset(new SteerSlot[(size_t)steer_ncpu_]);
+}
+
+int HttpServer::steer_target(int cpu, int self) {
+  if (cpu < 0 || cpu >= steer_ncpu_) return self;
+  constexpr int64_t kExpireMs = 1000;
+  const int64_t now = mono_ns() / 1000000;
+  SteerSlot& s = steer_[cpu];
+  int o = s.owner.load(std::memory_order_relaxed);
+  if (o >= 0 && now - s.seen_ms.load(std::memory_order_relaxed) < kExpireMs) {
+    s.seen_ms.store(now, std::memory_order_relaxed);
+    return o;
+  }
+  // unowned (or expired): the IO thread with the fewest live claims takes it (ties: the observer)
+  const int n = (int)threads_.size();
+  std::vector<int> load((size_t)n, 0);
+  for (int c = 0; c < steer_ncpu_; ++c) {
+    const int oc = steer_[c].owner.load(std::memory_order_relaxed);
+    if (oc >= 0 && oc < n && now - steer_[c].seen_ms.load(std::memory_order_relaxed) < kExpireMs) ++load[(size_t)oc];
+  }
+  int best = self;
+  for (int i = 0; i < n; ++i)
+    if (load[(size_t)i] < load[(size_t)best]) best = i;
+  if (s.owner.compare_exchange_strong(o, best)) {
+    s.seen_ms.store(now, std::memory_order_relaxed);
+    return best;
+  }
+  return s.owner.load(std::memory_order_relaxed);  // another IO thread claimed it meanwhile
 }
 
 HttpServer::~HttpServer() {
@@ -1367,6 +1467,7 @@ ServerStats HttpServer::stats() const {
     s.errors += t->n_err.load();
     s.bad_requests += t->n_bad.load();
     s.listen_closes += t->n_listen_close.load();
+    s.steered += t->n_steered.load();
   }
   s.listen_closes += leaves_.load();
   s.accepting = accepting_.load();

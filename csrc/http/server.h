@@ -71,6 +71,15 @@ struct ServerConfig {
   // connections) the threads block as usual and no CPU is spent spinning. 0 = off.
   int io_spin_lowload_us = 50;
   int io_spin_max_conns = 2;
+  // Connection steering by SO_INCOMING_CPU: every steer_every requests an IO thread reads the CPU
+  // that last processed a connection's incoming segments (for loopback, the client thread's CPU;
+  // for a NIC, its RX queue's). Each such CPU is owned by one IO thread (claimed by the thread with
+  // the fewest live claims), and an idle connection seen twice in a row on another thread's CPU
+  // moves to that thread: connections driven from one CPU share one IO thread, so a burst of their
+  // requests lands in one epoll round (one wake-up) instead of one per thread. 0 = off.
+  int io_steer = 0;
+  int steer_every = 32;
+  int steer_stable = 3;  // samples in a row on one CPU before a connection may move
   bool stage_timing = true;  // per-stage CPU accounting + HTTP latency histogram (a few rdtsc per request)
   // Connection dispatch (dispatch.h): "acceptor" (default) = one acceptor per serving group hands
   // every new connection to the next healthy replica / IO thread, round robin; "source" = the same
@@ -109,6 +118,7 @@ constexpr int HTTP_LAT_BUCKETS = 24;  // power-of-two microsecond buckets: <1us 
 
 struct ServerStats {
   uint64_t fast = 0, slow = 0, responses = 0, connections = 0, errors = 0, bad_requests = 0;
+  uint64_t steered = 0;        // connections moved between IO threads by io_steer
   uint64_t listen_closes = 0;  // health_dispatch: times this rank left its dispatch group
   bool accepting = true;
   uint64_t stage_ns[SS_COUNT] = {};
@@ -142,6 +152,11 @@ class HttpServer {
 
   // internal, used by IoThread
   void push_slow(SlowRequest&& r);
+  // io_steer: the IO thread that owns connections whose segments arrive on `cpu` (claimed for the
+  // least-loaded thread on first sight; claims not seen for a second expire)
+  int steer_target(int cpu, int self);
+  IoThread* io_thread(int i) const { return threads_[(size_t)i].get(); }
+  int io_thread_count() const { return (int)threads_.size(); }
   bool acceptor_mode() const { return acceptor_; }
   ConnDispatcher* dispatcher() const { return dispatcher_.get(); }
 
@@ -163,6 +178,12 @@ class HttpServer {
   std::unique_ptr<ConnDispatcher> dispatcher_;
   std::atomic<uint64_t> adopt_rr_{0};
   std::atomic<uint64_t> leaves_{0};  // acceptor mode: healthy -> unhealthy transitions
+  struct SteerSlot {
+    std::atomic<int> owner{-1};
+    std::atomic<int64_t> seen_ms{0};
+  };
+  std::unique_ptr<SteerSlot[]> steer_;
+  int steer_ncpu_ = 0;
 };
 
 // HTTP date (RFC 7231 IMF-fixdate), cached per second.

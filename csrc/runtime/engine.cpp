@@ -1730,7 +1730,9 @@ void Engine::resident_loop() {
     const int nr = rings_open_.load(std::memory_order_acquire);
     if (running && (inst_rings != nr || (inst_bounce ? small : want != inst_mver))) stop_inst();
     const int64_t now = now_ns();
-    if (!running && nr > 0 && (small || served) && now >= t_retry && !res_halt_.load(std::memory_order_acquire)) {
+    // (never next to an abandoned instance: it may still be polling the same rings)
+    if (!running && nr > 0 && (small || served) && now >= t_retry && !res_leaked_ &&
+        !res_halt_.load(std::memory_order_acquire)) {
       const bool bounce = !small;
       if (resident_launch(m, want, nr, bounce)) {
         running = true;

@@ -70,6 +70,7 @@ class EngineHandle:
         ec.resident = 1 if res == "on" or (res == "auto" and self.device is not None and resident_auto_ok()) else 0
         ec.resident_depth = int(config.resident_depth)
         ec.resident_idle_polls = int(config.resident_idle_polls)
+        ec.resident_lease_ms = int(config.resident_lease_ms)
         ec.f32_gemv = bool(config.f32_gemv)
         ec.wide_host_merge_blocks = int(config.wide_host_merge_blocks)
         ec.completers = int(config.completers)

@@ -67,6 +67,9 @@ class NativeServer:
         sc.idle_max_conns = int(config.idle_max_conns)
         sc.io_spin_lowload_us = int(config.io_spin_lowload_us)
         sc.io_spin_max_conns = int(config.io_spin_max_conns)
+        sc.io_steer = int(config.io_steer)
+        sc.steer_every = int(config.steer_every)
+        sc.steer_stable = int(config.steer_stable)
         sc.access_log_fd = int(access_log_fd)
         sc.dispatch = str(config.dispatch)
         sc.dispatch_group = str(config.dispatch_group)

@@ -51,6 +51,9 @@ class Config:
     idle_max_conns: int = 0                   # idle-engine path only while <= this many connections are open (0 = any)
     io_spin_lowload_us: int = 50              # ... only while <= io_spin_max_conns connections are open (batch=1 clients)
     io_spin_max_conns: int = 2
+    io_steer: int = 0                         # 1: move idle connections to the IO thread owning their SO_INCOMING_CPU
+    steer_every: int = 32                     # ... sampled every this many requests per connection
+    steer_stable: int = 3                     # ... moved only after this many samples in a row on one CPU
     max_queue: int = 1 << 20                  # backpressure: queued rows beyond this -> HTTP 503
     inline_args: bool = True                  # GPU: tiny batches travel in the kernel-argument block
     record_completion: bool = True            # GPU: kernel-argument batches complete through 16-B per-row records
@@ -65,6 +68,7 @@ class Config:
                                               # thread plays the kernel, tests) | off (every row via the batcher)
     resident_depth: int = 2                   # host-memory polls in flight per resident wave (1, 2, 4)
     resident_idle_polls: int = 20000          # polls without a row before a resident wave slows its polling
+    resident_lease_ms: int = 200              # a resident wave exits when its lease has not moved for this long
     io_ring_spin_us: int = 5                  # IO threads with rows on the resident kernel watch their records this
                                               # long in user space between epoll_wait(0) calls
     io_ring_sleep_us: int = 0                 # > 0: ... sleep that long in epoll_pwait2 instead of spinning (A/B)

@@ -284,7 +284,11 @@ def test_resident_fault_every_request_answered(native, device, mode, arg):
 
     m = LinearModel.random(4, 3, seed=13, labels=LABELS)
     X = np.round(np.random.default_rng(6).standard_normal((256, 4)) * 2 + 4, 1)
-    with NativeServer(_cfg(device, IRIS, watchdog_ms=200)) as srv:
+    # ignore_stop: a lease longer than the supervisor's 1 s stop wait (with the default 200 ms lease
+    # the waves end on it while the supervisor waits - the lease rule at work - and nothing is
+    # abandoned)
+    lease = 2000 if mode == "ignore_stop" else 200
+    with NativeServer(_cfg(device, IRIS, watchdog_ms=200, resident_lease_ms=lease)) as srv:
         h = srv.runtime.handle
         h.load(m)
         eng = h.engine
@@ -297,15 +301,21 @@ def test_resident_fault_every_request_answered(native, device, mode, arg):
         assert eng.resident_inject(mode, arg)
         if mode == "ignore_stop":
             h.load(m)  # a reload stops the instance: the stop is ignored, the instance abandoned
+        # traffic for at least a second across the fault (the lease and stop paths take ~0.2-1.2 s
+        # to play out; a fast instance answers 1,200 requests in about a millisecond)
         t0 = time.time()
-        res = lg.run(150, True)
-        took = time.time() - t0
+        counts, runs = {}, 0
+        while runs == 0 or time.time() - t0 < 1.5:
+            res = lg.run(50, False)
+            runs += 1
+            assert res["failed"] == 0 and res["body_mismatches"] == 0, res
+            for k, v in res["status_counts"].items():
+                counts[k] = counts.get(k, 0) + v
+            assert time.time() - t0 < 20.0, (runs, counts)
         s1 = h.stats()
         # every request answered (the bodies of the 200s byte-exact), within bounded time
-        assert res["failed"] == 0 and res["body_mismatches"] == 0, res
-        assert sum(res["status_counts"].values()) == 8 * 150 and set(res["status_counts"]) <= {200, 500}, res
-        assert res["status_counts"].get(200, 0) >= 8 * 140, res
-        assert took < 15.0, took
+        assert sum(counts.values()) == runs * 8 * 50 and set(counts) <= {200, 500}, counts
+        assert counts.get(200, 0) >= 0.9 * runs * 8 * 50, counts
         restarts = {k: s1[k] - s0[k] for k in ("resident_hb_restarts", "resident_ring_restarts",
                                                "resident_self_exits", "resident_queue_faults",
                                                "resident_abandoned", "resident_launches")}

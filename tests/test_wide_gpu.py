@@ -155,6 +155,27 @@ def test_engine_f64_wide_models_match_sklearn_math(native, F, K, merge):
         e.stop()
 
 
+@pytest.mark.parametrize("K", [40, 1000])
+def test_engine_f64_host_merge_17_to_32_rows(native, K):
+    """Host-merged WIDE batches of 17-32 rows (host_merge_rows = 32) run as ONE 32-row group even
+    where the planner would pick 16-row groups for a batch that small; answers match the float64
+    oracle (those batches used to throw in the launcher)."""
+    F = 256
+    m = LinearModel.random(F, K, seed=K + 5)
+    e = _engine(native, max_batch=64, max_features=F, wide_dtype=0, host_merge_rows=32, wide_host_merge_blocks=64)
+    try:
+        e.load_model(int(m.kind), m.W, m.b, m.label_json())
+        assert e.model_path() == "wide"
+        rng = np.random.default_rng(K)
+        for n in (17, 24, 32):
+            X = np.round(rng.standard_normal((n, F)), 3)
+            idx, p, st = e.predict(X)
+            assert (st == 0).all(), st
+            _oracle_check(m, X, idx, p)
+    finally:
+        e.stop()
+
+
 def test_engine_f32_k40_model_meets_1e6(native):
     """The K = 40 f32 model that missed rel 1e-6 on the f32-accumulating class-split kernel
     (profiles/r3_final4/prof_serve_wide_k40_f32_direct_failure.txt: 7 / 1024 rows, max 2.08e-6):

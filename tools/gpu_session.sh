@@ -38,6 +38,9 @@
 #   serve_lgsplit IO threads x load-generator threads (SPLITS="io:lg ...", LGARGS), interleaved
 #   serve_n2res   two ranks on one GPU: resident on / off x placement
 #   serve_wide64  serve_wide at f64 for K = 2 / 40 / 1000
+#   faults        resident-path fault injection tests + the 17-32-row wide host-merge test
+#   steer         paired + shuffled phases, io_steer 0 / 1 x SPLITS (default "8:8 8:5 8:6"), interleaved x RES_ROUNDS
+#   shuf_env      paired + shuffled phases with AB_VAR set to each of AB_VALS (SPLITS), interleaved x RES_ROUNDS
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
@@ -111,6 +114,29 @@ for s in $steps; do
       for r in $(seq 1 "${RES_ROUNDS:-2}"); do
         for sp in ${SPLITS:-8:4 8:5 7:5 8:6 7:6}; do
           run "lgsplit_${sp/:/_}_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --io-threads ${sp%%:*} --client-threads ${sp##*:} ${LGARGS:-}
+        done
+      done ;;
+    faults)
+      run pytest_faults 400 python -u -m pytest tests/test_resident.py tests/test_wide_gpu.py -m gpu -x -v -p no:cacheprovider \
+        --timeout 120 --timeout-method thread -k "fault or metrics or host_merge_17" ;;
+    steer)  # SO_INCOMING_CPU connection steering off / on, paired and shuffled clients
+      for r in $(seq 1 "${RES_ROUNDS:-2}"); do
+        for sp in ${SPLITS:-8:8 8:5 8:6}; do
+          for st in 0 1; do
+            MLAPI_IO_STEER=$st run "steer${st}_${sp/:/_}_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 \
+              --io-threads ${sp%%:*} --client-threads ${sp##*:} ${LGARGS:-}
+          done
+        done
+      done ;;
+    shuf_env)
+      for r in $(seq 1 "${RES_ROUNDS:-2}"); do
+        for sp in ${SPLITS:-8:8}; do
+          for v in ${AB_VALS}; do
+            export "$AB_VAR=$v"
+            run "env_${v}_${sp/:/_}_r$r" 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 \
+              --io-threads ${sp%%:*} --client-threads ${sp##*:} ${LGARGS:-}
+            unset "$AB_VAR"
+          done
         done
       done ;;
     serve_n2res)  # two ranks on the one GPU (P2P data plane): resident on / off x placement, interleaved
