@@ -115,6 +115,21 @@ def _comm_probe(info, model=None) -> dict:
     return out
 
 
+def _client_cpus(args, info) -> list:
+    """--client-pin: one CPU per load-generator thread, from this rank's mask (disjoint stretches for
+    ranks that share a NUMA-node mask); [] = the threads keep the process mask."""
+    if args.client_pin == "off":
+        return []
+    from mlapi_amd.utils.affinity import client_thread_cpus, gpu_numa_nodes
+
+    if getattr(args, "lg_mask", None):  # --pin on: the load generator has a core slice of its own
+        return client_thread_cpus(0, 1, args.client_threads, args.lg_mask)
+    mask = sorted(os.sched_getaffinity(0))
+    nodes = gpu_numa_nodes() if os.environ.get("MLAPI_PLACEMENT") == "numa" else None
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", info.world))
+    return client_thread_cpus(info.local_rank, local_world, args.client_threads, mask, nodes)
+
+
 def _share_port(port: int, info) -> int:
     """Rank 0's bound port, known to every rank (the shared SO_REUSEPORT port of the DP group)."""
     from mlapi_amd.parallel.comm import all_gather_floats
@@ -161,6 +176,8 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         # hosts of their own would be); "acceptor" deals every connection round robin over ranks
         src = f"127.1.{info.rank // 250}.{info.rank % 250 + 1}" if args.dispatch == "source" else ""
         lg.connect("127.0.0.1", port, args.conns, args.client_threads, source=src)
+        client_cpus = _client_cpus(args, info)
+        lg.thread_cpus(client_cpus)
         if args.warmup:
             w = lg.run(args.warmup * args.reqs_per_conn, False)
             if w["failed"] or w["errors"]:
@@ -197,6 +214,9 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
                 "server_http_latency_us_mean": (h1["http_latency_sum_ns"] - h0["http_latency_sum_ns"]) / 1e3
                 / max(1, h1["http_latency_count"] - h0["http_latency_count"]),
                 "steered_conns": h1.get("steered", 0) - h0.get("steered", 0),
+                "steer_pauses": h1.get("steer_pauses", 0) - h0.get("steer_pauses", 0),
+                "io_conns_per_thread": h1.get("conns_per_thread"),
+                "steer_plan": h1.get("steer_plan") or None,
             }
             want = steps * args.reqs_per_conn * args.conns
             if res["failed"] or res["errors"] or res["body_mismatches"] or res["ok200"] != want:
@@ -216,7 +236,9 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
             shuffled = {"req_per_s": tot2 / el2, "p50_latency_ms_c64": res2["p50_ns"] / 1e6,
                         "p99_latency_ms_c64": res2["p99_ns"] / 1e6,
                         "server_cpu_us_per_req": cb2["server_cpu_us_per_req"],
-                        "steered_conns": cb2["steered_conns"], "cpu_cores_busy_rank0": cu2,
+                        "steered_conns": cb2["steered_conns"], "steer_pauses": cb2["steer_pauses"],
+                        "io_conns_per_thread": cb2["io_conns_per_thread"], "steer_plan": cb2["steer_plan"],
+                        "cpu_cores_busy_rank0": cu2,
                         "io_stage_us_per_req": cb2["io_stage_us_per_req"]}
         lg.cmd("close")
         # batch = 1: one client, closed loop, measured by rank 0 alone (the other ranks idle)
@@ -280,6 +302,9 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         "req_per_s_shuffled": None if shuffled is None else shuffled["req_per_s"],
         "shuffled_rank0": shuffled,
         "threads": {"io": args.io_threads, "loadgen": args.client_threads, "pinned_cpus": args.pinned_cpus,
+                    # one CPU per load-generator thread (--client-pin): the loopback stand-in for NIC
+                    # RX queues with pinned interrupts, so each connection arrives from a stable CPU
+                    "client_cpus": client_cpus,
                     # launcher placement of this rank (numa: its GPU's NUMA-node mask) and its mask size
                     "placement": os.environ.get("MLAPI_PLACEMENT", "cores" if args.pinned_cpus else "none"),
                     "affinity_cpus": len(os.sched_getaffinity(0))},
@@ -549,6 +574,10 @@ def main(argv=None) -> int:
                     help="serve: one step = conns x this many requests per rank (~0.15-0.25 s, so the "
                          "driver's 20 steps time >= 2 s even at 1.3 M req/s)")
     ap.add_argument("--workload-rows", type=int, default=1024, help="serve: distinct validated requests")
+    ap.add_argument("--client-pin", default="on", choices=["on", "off"],
+                    help="serve: pin each load-generator thread to its own CPU of the rank's mask (on: like "
+                         "NIC RX queues with pinned interrupts, a connection's segments arrive from one CPU, "
+                         "which the server's SO_INCOMING_CPU steering groups by) or leave them floating")
     ap.add_argument("--shuffle-steps", type=int, default=-1,
                     help="serve: steps of the extra phase with the load generator's connections dealt to its "
                          "threads by a seeded permutation (req_per_s_shuffled); -1 = --steps, 0 = skip")
@@ -680,6 +709,7 @@ def main(argv=None) -> int:
         n_srv = args.io_threads + 2
         _os.sched_setaffinity(0, pinned[:n_srv])
         args.lg_proc.pin(pinned[n_srv:])
+        args.lg_mask = list(pinned[n_srv:])
     if args.mode != "serve" and info.device is None:
         print(f"mode {args.mode} needs a GPU", file=sys.stderr)
         return 2

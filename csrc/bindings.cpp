@@ -739,6 +739,9 @@ PYBIND11_MODULE(_C, m) {
         d["bad_requests"] = st.bad_requests;
         d["listen_closes"] = st.listen_closes;
         d["steered"] = st.steered;
+        d["steer_pauses"] = st.steer_pauses;
+        d["conns_per_thread"] = st.conns_per_thread;
+        d["steer_plan"] = st.steer_plan;
         d["accepting"] = st.accepting;
         d["listeners"] = s.listeners();
         py::dict stg;
@@ -795,5 +798,6 @@ PYBIND11_MODULE(_C, m) {
       .def("set_workload", &Loadgen::set_workload, py::arg("requests"), py::arg("expected"),
            py::arg("rel_tol") = 0.0)
       .def("set_conn_map", &Loadgen::set_conn_map, py::arg("mode"), py::arg("seed") = 1)
+      .def("set_thread_cpus", &Loadgen::set_thread_cpus, py::arg("cpus"))
       .def("close", &Loadgen::close_all);
 }

@@ -93,6 +93,12 @@ Loadgen::Loadgen(const std::string& host, int port, const std::string& request, 
 
 Loadgen::~Loadgen() { close_all(); }
 
+void Loadgen::set_thread_cpus(const std::vector<int>& cpus) {
+  for (int c : cpus)
+    if (c < 0 || c >= CPU_SETSIZE) throw std::invalid_argument("loadgen: bad CPU in the thread list");
+  thread_cpus_ = cpus;
+}
+
 void Loadgen::set_conn_map(const std::string& mode, uint64_t seed) {
   std::iota(order_.begin(), order_.end(), 0);
   if (mode == "shuffle") {
@@ -165,22 +171,13 @@ LoadgenResult Loadgen::run(int64_t requests_per_conn, bool record) {
   const int64_t t0 = mono_ns();
   auto worker = [&](int ti) {
     pthread_setname_np(pthread_self(), "mlapi-loadgen");
-    if (pin_threads_) {
-      // each client thread on one CPU of the process's mask (thread i -> its i-th CPU): like a NIC
-      // whose RX queues are pinned, every connection's segments then arrive from one stable CPU
-      cpu_set_t set;
-      CPU_ZERO(&set);
-      if (sched_getaffinity(0, sizeof set, &set) == 0) {
-        int k = 0, pick = -1;
-        for (int c = 0; c < CPU_SETSIZE && pick < 0; ++c)
-          if (CPU_ISSET(c, &set) && k++ == ti) pick = c;
-        if (pick >= 0) {
-          cpu_set_t one;
-          CPU_ZERO(&one);
-          CPU_SET(pick, &one);
-          pthread_setaffinity_np(pthread_self(), sizeof one, &one);
-        }
-      }
+    if (!thread_cpus_.empty()) {
+      // this client thread on its own CPU (like a NIC whose RX queues' interrupts are pinned: every
+      // connection's segments then arrive from one stable CPU)
+      cpu_set_t one;
+      CPU_ZERO(&one);
+      CPU_SET(thread_cpus_[(size_t)ti % thread_cpus_.size()], &one);
+      pthread_setaffinity_np(pthread_self(), sizeof one, &one);
     }
     const int ep = epoll_create1(EPOLL_CLOEXEC);
     std::vector<LgConn*> mine;

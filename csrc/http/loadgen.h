@@ -40,6 +40,8 @@ class Loadgen {
   // robin - a client thread's connections then land wherever the server's dispatcher put them, as
   // independent clients' would (not paired with the server's IO threads by connect order).
   void set_conn_map(const std::string& mode, uint64_t seed = 1);
+  // Thread i of the next run() pins itself to cpus[i % size] (empty: threads keep the process mask).
+  void set_thread_cpus(const std::vector<int>& cpus);
   // Every connection completes `requests_per_conn` closed-loop requests.
   LoadgenResult run(int64_t requests_per_conn, bool record = true);
   void close_all();
@@ -57,11 +59,7 @@ class Loadgen {
     const char* e = std::getenv("MLAPI_LOADGEN_SPIN_US");
     return e ? (int64_t)std::atoll(e) * 1000 : (int64_t)0;
   }();
-  // MLAPI_LOADGEN_PIN_THREADS=1: thread i runs on the i-th CPU of the process's affinity mask
-  bool pin_threads_ = [] {
-    const char* e = std::getenv("MLAPI_LOADGEN_PIN_THREADS");
-    return e != nullptr && std::atoi(e) != 0;
-  }();
+  std::vector<int> thread_cpus_;  // set_thread_cpus
   int threads_;
   std::vector<int> order_;  // connection index of slot i (thread i % threads_ drives it)
   std::vector<std::unique_ptr<LgConn>> conns_;

@@ -7,6 +7,7 @@
 //   workload <path> [rel_tol]                  "MLW1\n" then per entry "<req_len> <exp_len>\n" + bytes
 //   connect <host> <port> <conns> <threads> <timeout_s> [<source address>]
 //   connmap <rr|shuffle> [seed]                which loop drives which connection (after connect)
+//   threadcpus <cpu>,<cpu>,... | -             one CPU per client thread (after connect; - = none)
 //   run <requests_per_conn> <record 0|1>       -> {"completed":..,"p50_ns":..,...}
 //   close | quit
 #include <sched.h>
@@ -118,6 +119,17 @@ int main() {
         if (!lg) throw std::runtime_error("connmap before connect");
         lg->set_conn_map(mode, seed);
         reply("{\"ok\":true}");
+      } else if (cmd == "threadcpus") {
+        std::string list;
+        in >> list;
+        if (!lg) throw std::runtime_error("threadcpus before connect");
+        std::vector<int> cpus;
+        std::stringstream ss(list == "-" ? std::string() : list);
+        std::string tok;
+        while (std::getline(ss, tok, ','))
+          if (!tok.empty()) cpus.push_back(std::atoi(tok.c_str()));
+        lg->set_thread_cpus(cpus);
+        reply("{\"ok\":true,\"cpus\":" + std::to_string(cpus.size()) + "}");
       } else if (cmd == "run") {
         long long n = 0;
         int record = 1;

@@ -128,6 +128,11 @@ struct Conn {
   uint32_t nreq = 0;          // fast-path requests parsed on this connection
   int in_cpu = -1;            // SO_INCOMING_CPU at the last sample ...
   int same_n = 0;             // ... and on how many samples in a row
+  int stable_cpu = -1;        // the CPU it counts for in the steering plan
+  uint32_t key = 0;           // (reserved) a per-connection key that survives moves
+  int flips = 0;              // stable-CPU changes within 5 s of each other ...
+  int64_t flip_ns = 0;
+  int64_t unsteered_until = 0;  // ... 3 of them: not steered until then
   int move_to = -1;           // IO thread to hand the connection to once it is idle
   int64_t moved_ns = 0;       // when it last moved (at most one move per 50 ms)
 };
@@ -251,6 +256,7 @@ class IoThread : public Sink {
 
   // io_steer: an idle connection handed over by another IO thread (a new id is assigned here)
   void adopt_conn(std::unique_ptr<Conn> c) {
+    n_open_.fetch_add(1, std::memory_order_relaxed);  // counted now: io_steer's cap sees moves in flight
     {
       std::lock_guard<std::mutex> lk(mu_);
       moved_in_.push_back(std::move(c));
@@ -268,6 +274,7 @@ class IoThread : public Sink {
 
   std::atomic<uint64_t> n_fast{0}, n_slow{0}, n_resp{0}, n_conn{0}, n_err{0}, n_bad{0}, n_listen_close{0};
   std::atomic<uint64_t> n_steered{0};
+  int open_count() const { return n_open_.load(std::memory_order_relaxed); }
   // published copies of the stage clock / latency histogram (ticks; see ServerStats)
   std::atomic<uint64_t> pub_stage[SS_COUNT] = {};
   std::atomic<uint64_t> pub_lat[HTTP_LAT_BUCKETS] = {};
@@ -624,6 +631,12 @@ class IoThread : public Sink {
       auto c = std::make_unique<Conn>();
       c->fd = fd;
       c->id = next_id_++;
+      {  // a per-connection key that survives moves (splitmix64 of the fd and the clock)
+        uint64_t z = (uint64_t)fd * 0x9E3779B97F4A7C15ull + (uint64_t)mono_ns();
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        c->key = (uint32_t)(z ^ (z >> 31));
+      }
       addr_to_str(ss, c->client_host, c->client_port);
       sockaddr_storage ls{};
       socklen_t ll = sizeof ls;
@@ -634,15 +647,18 @@ class IoThread : public Sink {
       ev.data.u64 = c->id;
       epoll_ctl(epfd_, EPOLL_CTL_ADD, fd, &ev);
       conns_.emplace(c->id, std::move(c));
+      n_open_.fetch_add(1, std::memory_order_relaxed);
       n_conn.fetch_add(1, std::memory_order_relaxed);
       srv_->open_conns.fetch_add(1, std::memory_order_relaxed);
     }
   }
 
   void close_conn(Conn* c) {
+    if (c->stable_cpu >= 0) srv_->steer_count(c->stable_cpu, -1);
     epoll_ctl(epfd_, EPOLL_CTL_DEL, c->fd, nullptr);
     close(c->fd);
     conns_.erase(c->id);  // destroys c
+    n_open_.fetch_sub(1, std::memory_order_relaxed);
     srv_->open_conns.fetch_sub(1, std::memory_order_relaxed);
   }
 
@@ -820,7 +836,7 @@ class IoThread : public Sink {
       ev.data.u64 = c->id;
       epoll_ctl(epfd_, EPOLL_CTL_ADD, c->fd, &ev);
       const uint64_t id = c->id;
-      conns_.emplace(id, std::move(c));
+      conns_.emplace(id, std::move(c));  // n_open_ was counted by adopt_conn
     }
     outstanding_ = std::max<int64_t>(0, outstanding_ - (int64_t)fast_c.size());
     for (size_t k = 0; k < fast_seg.size(); ++k) {
@@ -885,8 +901,26 @@ class IoThread : public Sink {
     // only a CPU seen on steer_stable samples in a row counts (a client thread the scheduler keeps
     // moving gives no stable CPU, and its connections stay where they are)
     if (++c->same_n < std::max(2, srv_->config().steer_stable)) return;
-    const int t = srv_->steer_target(cpu, index_);
-    if (t != index_ && t >= 0 && mono_ns() - c->moved_ns > 50000000) c->move_to = t;
+    const int64_t now = mono_ns();
+    if (now < c->unsteered_until) return;
+    if (cpu != c->stable_cpu) {
+      // a connection whose client keeps changing CPU (an unpinned client thread the scheduler
+      // moves around) has no CPU to be grouped by: it leaves the plan for 10 s instead of chasing it
+      c->flips = now - c->flip_ns < 5000000000LL ? c->flips + 1 : 1;
+      c->flip_ns = now;
+      if (c->flips >= 3) {
+        srv_->steer_count(c->stable_cpu, -1);
+        c->stable_cpu = -1;
+        c->move_to = -1;
+        c->flips = 0;
+        c->unsteered_until = now + 10000000000LL;
+        return;
+      }
+      srv_->steer_count(c->stable_cpu, cpu);
+      c->stable_cpu = cpu;
+    }
+    const int t = srv_->steer_target(cpu, index_, c->key);
+    if (t != index_ && t >= 0 && now - c->moved_ns > 50000000) c->move_to = t;
   }
 
   // hand an idle connection to another IO thread (returns false: it is no longer this thread's)
@@ -898,9 +932,12 @@ class IoThread : public Sink {
     auto it = conns_.find(c->id);
     std::unique_ptr<Conn> up = std::move(it->second);
     conns_.erase(it);
+    n_open_.fetch_sub(1, std::memory_order_relaxed);
     up->moved_ns = mono_ns();
     up->nreq = 0;
+    up->same_n = 0;
     n_steered.fetch_add(1, std::memory_order_relaxed);
+    srv_->steer_moved();
     srv_->io_thread(t)->adopt_conn(std::move(up));
     return false;
   }
@@ -1235,6 +1272,7 @@ class IoThread : public Sink {
   std::mutex mu_;
   std::vector<int> adopted_;  // acceptor mode: connections handed over by the dispatcher
   std::vector<std::unique_ptr<Conn>> moved_in_;  // io_steer: connections handed over by other IO threads
+  std::atomic<int> n_open_{0};                   // connections this thread holds (io_steer's balance)
   bool timing_ = false;
   double ns_per_tick_ = 1.0;
   uint64_t st_acc_[SS_COUNT] = {};
@@ -1266,34 +1304,113 @@ HttpServer::HttpServer(Engine* engine, const ServerConfig& cfg) : engine_(engine
   if (cfg_.io_threads < 1) cfg_.io_threads = 1;
   if (cfg_.io_threads > 64) cfg_.io_threads = 64;
   steer_ncpu_ = (int)std::min<long>(4096, std::max<long>(1, sysconf(_SC_NPROCESSORS_CONF)));
-  steer_.reset(new SteerSlot[(size_t)steer_ncpu_]);
+  cpu_conns_.reset(new std::atomic<int>[(size_t)steer_ncpu_]);
+  plan_.reset(new std::atomic<uint64_t>[(size_t)steer_ncpu_]);
+  for (int c = 0; c < steer_ncpu_; ++c) {
+    cpu_conns_[c].store(0);
+    plan_[c].store(0);
+  }
 }
 
-int HttpServer::steer_target(int cpu, int self) {
-  if (cpu < 0 || cpu >= steer_ncpu_) return self;
-  constexpr int64_t kExpireMs = 1000;
-  const int64_t now = mono_ns() / 1000000;
-  SteerSlot& s = steer_[cpu];
-  int o = s.owner.load(std::memory_order_relaxed);
-  if (o >= 0 && now - s.seen_ms.load(std::memory_order_relaxed) < kExpireMs) {
-    s.seen_ms.store(now, std::memory_order_relaxed);
-    return o;
-  }
-  // unowned (or expired): the IO thread with the fewest live claims takes it (ties: the observer)
-  const int n = (int)threads_.size();
-  std::vector<int> load((size_t)n, 0);
+// io_steer plan: every CPU that drives connections is assigned to the least-loaded IO thread, and
+// a CPU whose connections exceed that thread's room spills into the next least-loaded ones (at most
+// three threads per CPU; water-filling by group size, ties to the lowest index, so equal counts give
+// an equal plan). A CPU keeps its previous first thread while that one still has room (a re-plan
+// with slightly different counts must not shuffle every group). Encoding per CPU: three owners + 1,
+// 8 bits each (0 = none).
+void HttpServer::steer_replan(int64_t now_ms) {
+  std::unique_lock<std::mutex> lk(plan_mu_, std::try_to_lock);
+  if (!lk.owns_lock()) return;
+  if (now_ms - plan_ms_.load(std::memory_order_relaxed) < 100) return;
+  plan_ms_.store(now_ms, std::memory_order_relaxed);
+  const int n = std::min(255, (int)threads_.size());
+  std::vector<std::pair<int, int>> groups;  // (count, cpu)
+  int total = 0;
   for (int c = 0; c < steer_ncpu_; ++c) {
-    const int oc = steer_[c].owner.load(std::memory_order_relaxed);
-    if (oc >= 0 && oc < n && now - steer_[c].seen_ms.load(std::memory_order_relaxed) < kExpireMs) ++load[(size_t)oc];
+    const int k = cpu_conns_[c].load(std::memory_order_relaxed);
+    if (k > 0) {
+      groups.emplace_back(k, c);
+      total += k;
+    }
   }
-  int best = self;
-  for (int i = 0; i < n; ++i)
-    if (load[(size_t)i] < load[(size_t)best]) best = i;
-  if (s.owner.compare_exchange_strong(o, best)) {
-    s.seen_ms.store(now, std::memory_order_relaxed);
-    return best;
+  std::sort(groups.begin(), groups.end(), [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
+    return a.first != b.first ? a.first > b.first : a.second < b.second;
+  });
+  const int share = std::max(1, (total + n - 1) / n);
+  steer_share_.store(share, std::memory_order_relaxed);
+  std::vector<int> load((size_t)n, 0);
+  std::vector<uint64_t> prev((size_t)steer_ncpu_);
+  for (int c = 0; c < steer_ncpu_; ++c) prev[(size_t)c] = plan_[c].exchange(0, std::memory_order_relaxed);
+  for (const auto& g : groups) {
+    int left = g.first;
+    uint64_t e = 0;
+    int used[3] = {-1, -1, -1};
+    for (int k = 0; k < 3 && left > 0; ++k) {
+      int t = -1;
+      const int p1 = (int)(prev[(size_t)g.second] & 0xff) - 1;
+      if (k == 0 && p1 >= 0 && p1 < n && load[(size_t)p1] < share) t = p1;
+      if (t < 0)
+        for (int i = 0; i < n; ++i)
+          if (i != used[0] && i != used[1] && (t < 0 || load[(size_t)i] < load[(size_t)t])) t = i;
+      const int room = std::max(1, share - load[(size_t)t]);
+      const int take = k == 2 ? left : std::min(left, room);
+      load[(size_t)t] += take;
+      left -= take;
+      used[k] = t;
+      e |= (uint64_t)(t + 1) << (8 * k);
+    }
+    plan_[g.second].store(e, std::memory_order_relaxed);
   }
-  return s.owner.load(std::memory_order_relaxed);  // another IO thread claimed it meanwhile
+}
+
+int HttpServer::steer_target(int cpu, int self, uint32_t key) {
+  (void)key;
+  if (cpu < 0 || cpu >= steer_ncpu_) return self;
+  const int64_t now = mono_ns() / 1000000;
+  if (now < steer_pause_until_ms_.load(std::memory_order_relaxed)) return self;  // churn guard
+  if (now - plan_ms_.load(std::memory_order_relaxed) >= 100) steer_replan(now);
+  const uint64_t e = plan_[cpu].load(std::memory_order_relaxed);
+  const int n = (int)threads_.size();
+  int owners[3], no = 0;
+  for (int k = 0; k < 3; ++k) {
+    const int o = (int)((e >> (8 * k)) & 0xff) - 1;
+    if (o >= 0 && o < n) owners[no++] = o;
+  }
+  if (no == 0) return self;  // not planned yet
+  const int share = steer_share_.load(std::memory_order_relaxed);
+  for (int k = 0; k < no; ++k)
+    if (owners[k] == self) {
+      // already on one of its CPU's threads: stays, unless this one is over its share and another
+      // of them is under it (the split then evens out)
+      if (threads_[(size_t)self]->open_count() > share)
+        for (int j = 0; j < no; ++j)
+          if (owners[j] != self && threads_[(size_t)owners[j]]->open_count() < share) return owners[j];
+      return self;
+    }
+  // the first of its CPU's threads with room (moves in flight counted by adopt_conn): connections of
+  // other CPUs parked there leave for their own threads as those make room
+  const int cap = share + 1;
+  for (int k = 0; k < no; ++k)
+    if (threads_[(size_t)owners[k]]->open_count() < cap) return owners[k];
+  return self;
+}
+
+void HttpServer::steer_count(int old_cpu, int new_cpu) {
+  if (old_cpu >= 0 && old_cpu < steer_ncpu_) cpu_conns_[old_cpu].fetch_sub(1, std::memory_order_relaxed);
+  if (new_cpu >= 0 && new_cpu < steer_ncpu_) cpu_conns_[new_cpu].fetch_add(1, std::memory_order_relaxed);
+}
+
+void HttpServer::steer_moved() {
+  // churn guard: a scheduler that keeps moving client threads between CPUs makes connections chase
+  // them; more than 2 moves per open connection in a second pauses steering for 5 s
+  const int64_t now = mono_ns() / 1000000;
+  int64_t w = steer_win_ms_.load(std::memory_order_relaxed);
+  if (now - w >= 1000 && steer_win_ms_.compare_exchange_strong(w, now)) steer_win_moves_.store(0);
+  if (steer_win_moves_.fetch_add(1) + 1 > 2 * (int64_t)std::max(8, open_conns.load(std::memory_order_relaxed))) {
+    steer_pause_until_ms_.store(now + 5000, std::memory_order_relaxed);
+    steer_pauses_.fetch_add(1, std::memory_order_relaxed);
+    steer_win_moves_.store(0);
+  }
 }
 
 HttpServer::~HttpServer() {
@@ -1468,6 +1585,14 @@ ServerStats HttpServer::stats() const {
     s.bad_requests += t->n_bad.load();
     s.listen_closes += t->n_listen_close.load();
     s.steered += t->n_steered.load();
+    s.conns_per_thread.push_back(t->open_count());
+  }
+  s.steer_pauses = steer_pauses_.load();
+  for (int c = 0; c < steer_ncpu_; ++c) {
+    const int k = cpu_conns_[c].load(std::memory_order_relaxed);
+    const uint64_t e = plan_[c].load(std::memory_order_relaxed);
+    if (k != 0 || e != 0)
+      s.steer_plan.push_back({c, k, (int)(e & 0xff) - 1, (int)((e >> 8) & 0xff) - 1, (int)((e >> 16) & 0xff) - 1});
   }
   s.listen_closes += leaves_.load();
   s.accepting = accepting_.load();

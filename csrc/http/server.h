@@ -73,11 +73,12 @@ struct ServerConfig {
   int io_spin_max_conns = 2;
   // Connection steering by SO_INCOMING_CPU: every steer_every requests an IO thread reads the CPU
   // that last processed a connection's incoming segments (for loopback, the client thread's CPU;
-  // for a NIC, its RX queue's). Each such CPU is owned by one IO thread (claimed by the thread with
-  // the fewest live claims), and an idle connection seen twice in a row on another thread's CPU
-  // moves to that thread: connections driven from one CPU share one IO thread, so a burst of their
-  // requests lands in one epoll round (one wake-up) instead of one per thread. 0 = off.
-  int io_steer = 0;
+  // for a NIC, its RX queue's). A plan (recomputed every 100 ms from the connections' stable CPUs)
+  // gives each such CPU one IO thread, or two when its connections exceed a thread's share, and an
+  // idle connection whose CPU is planned elsewhere moves there: connections driven from one CPU
+  // share one IO thread, so a burst of their requests lands in one epoll round (one wake-up)
+  // instead of one per thread. A churn guard pauses it when client CPUs keep moving. 0 = off.
+  int io_steer = 1;
   int steer_every = 32;
   int steer_stable = 3;  // samples in a row on one CPU before a connection may move
   bool stage_timing = true;  // per-stage CPU accounting + HTTP latency histogram (a few rdtsc per request)
@@ -119,6 +120,9 @@ constexpr int HTTP_LAT_BUCKETS = 24;  // power-of-two microsecond buckets: <1us 
 struct ServerStats {
   uint64_t fast = 0, slow = 0, responses = 0, connections = 0, errors = 0, bad_requests = 0;
   uint64_t steered = 0;        // connections moved between IO threads by io_steer
+  uint64_t steer_pauses = 0;   // ... times its churn guard paused it
+  std::vector<int> conns_per_thread;  // open connections per IO thread
+  std::vector<std::vector<int>> steer_plan;  // io_steer: {cpu, connections, thread 1, thread 2, thread 3}
   uint64_t listen_closes = 0;  // health_dispatch: times this rank left its dispatch group
   bool accepting = true;
   uint64_t stage_ns[SS_COUNT] = {};
@@ -154,7 +158,9 @@ class HttpServer {
   void push_slow(SlowRequest&& r);
   // io_steer: the IO thread that owns connections whose segments arrive on `cpu` (claimed for the
   // least-loaded thread on first sight; claims not seen for a second expire)
-  int steer_target(int cpu, int self);
+  int steer_target(int cpu, int self, uint32_t key);
+  void steer_moved();  // a connection moved (churn guard)
+  void steer_count(int old_cpu, int new_cpu);  // a connection's stable CPU changed (-1: none)
   IoThread* io_thread(int i) const { return threads_[(size_t)i].get(); }
   int io_thread_count() const { return (int)threads_.size(); }
   bool acceptor_mode() const { return acceptor_; }
@@ -178,11 +184,14 @@ class HttpServer {
   std::unique_ptr<ConnDispatcher> dispatcher_;
   std::atomic<uint64_t> adopt_rr_{0};
   std::atomic<uint64_t> leaves_{0};  // acceptor mode: healthy -> unhealthy transitions
-  struct SteerSlot {
-    std::atomic<int> owner{-1};
-    std::atomic<int64_t> seen_ms{0};
-  };
-  std::unique_ptr<SteerSlot[]> steer_;
+  void steer_replan(int64_t now_ms);
+  std::unique_ptr<std::atomic<int>[]> cpu_conns_;   // connections whose stable incoming CPU is c
+  std::unique_ptr<std::atomic<uint64_t>[]> plan_;   // per CPU: up to three IO threads (+1, 8 bits each)
+  std::atomic<int64_t> plan_ms_{0};
+  std::atomic<int> steer_share_{1};  // the plan's connections per IO thread
+  std::mutex plan_mu_;
+  std::atomic<int64_t> steer_win_ms_{0}, steer_win_moves_{0}, steer_pause_until_ms_{0};
+  std::atomic<uint64_t> steer_pauses_{0};
   int steer_ncpu_ = 0;
 };
 

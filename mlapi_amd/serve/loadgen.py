@@ -142,6 +142,10 @@ class LoadgenProcess:
         permutation, so a thread's connections are not paired with the server's IO threads."""
         return self.cmd(f"connmap {mode} {int(seed)}")
 
+    def thread_cpus(self, cpus: Sequence[int]) -> dict:
+        """Pin client thread i to cpus[i] for the following runs ([] = keep the process mask)."""
+        return self.cmd("threadcpus " + (",".join(str(c) for c in cpus) if cpus else "-"))
+
     def run(self, requests_per_conn: int, record: bool = True) -> dict:
         return self.cmd(f"run {int(requests_per_conn)} {1 if record else 0}")
 

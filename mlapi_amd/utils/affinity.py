@@ -273,3 +273,23 @@ def ranks_on_node(local_rank: int, local_world: int, nodes: List[Optional[int]])
     mine = nodes[local_rank % len(nodes)]
     return max(1, sum(1 for r in range(local_world) if nodes[r % len(nodes)] == mine))
 
+
+
+def client_thread_cpus(local_rank: int, local_world: int, nthreads: int, mask: List[int],
+                       nodes: Optional[List[Optional[int]]] = None, sysfs: str = SYS_CPU) -> List[int]:
+    """One CPU per load-generator thread of this rank (bench.py pins its client threads, the loopback
+    stand-in for NIC RX queues whose interrupts are pinned: every connection's segments then arrive
+    from one stable CPU, which the server's SO_INCOMING_CPU steering relies on). Distinct physical
+    cores of ``mask`` first, and ranks that share the mask (numa placement) take disjoint stretches
+    of it, so no two ranks' client threads stack on one CPU. [] when the mask is empty."""
+    if nthreads <= 0 or not mask:
+        return []
+    order = core_order(sorted(mask), sysfs)
+    if nodes:
+        mine = nodes[local_rank % len(nodes)]
+        slot = sum(1 for r in range(local_rank) if nodes[r % len(nodes)] == mine)
+        sharing = ranks_on_node(local_rank, max(local_world, local_rank + 1), nodes)
+    else:
+        slot, sharing = local_rank, max(1, local_world)
+    stride = max(nthreads, len(order) // max(1, sharing))
+    return [order[(slot * stride + i) % len(order)] for i in range(nthreads)]

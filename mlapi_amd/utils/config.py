@@ -51,7 +51,7 @@ class Config:
     idle_max_conns: int = 0                   # idle-engine path only while <= this many connections are open (0 = any)
     io_spin_lowload_us: int = 50              # ... only while <= io_spin_max_conns connections are open (batch=1 clients)
     io_spin_max_conns: int = 2
-    io_steer: int = 0                         # 1: move idle connections to the IO thread owning their SO_INCOMING_CPU
+    io_steer: int = 1                         # group connections on IO threads by their SO_INCOMING_CPU (0 = off)
     steer_every: int = 32                     # ... sampled every this many requests per connection
     steer_stable: int = 3                     # ... moved only after this many samples in a row on one CPU
     max_queue: int = 1 << 20                  # backpressure: queued rows beyond this -> HTTP 503

@@ -5,6 +5,8 @@
 //   ring_probe <mode> <threads> <outstanding per thread> <seconds> [hdr_only 0|1] [window]
 //     mode pingpong: each thread keeps `outstanding` rows in flight (1 = batch-1 ping-pong) and
 //                    prints the completion latency distribution and rows/s
+//   ring_probe v2 <waves> 0 <seconds> [depth]: poll-only waves (no rows ever written), e.g. the
+//                    host-memory polling load of 8 GPUs x 8 rings on one box
 //
 // One workgroup (one wave) per ring; ring t belongs to host thread t. A row is F = 4 granules of
 // 16 bytes {x_f (f64), pos (u32), 0}: every granule carries the row's ring position, so a wave
@@ -296,7 +298,9 @@ int main(int argc, char** argv) {
   const int opt = argc > 5 ? atoi(argv[5]) : (v2 ? 1 : 0);  // v1: hdr_only, v2: depth
   const int window = argc > 6 ? atoi(argv[6]) : (v2 ? 16 : 64);
   const int devmem = v2 && argc > 7 ? atoi(argv[7]) : 0;
-  if (T < 1 || T > 64 || OUT < 1 || OUT > N / 2 || (v2 && (window < 1 || window > 16))) return 2;
+  // v2 with outstanding 0: poll-only waves (no host writer threads) - the host-memory read load of
+  // T busy resident rings, e.g. 64 to stand in for 8 GPUs x 8 rings next to a serving process
+  if (T < 1 || T > 64 || OUT < (v2 ? 0 : 1) || OUT > N / 2 || (v2 && (window < 1 || window > 16))) return 2;
   if (v2 && opt != 1 && opt != 2 && opt != 4) return 2;
   Granule* in = nullptr;
   Rec* out;
@@ -354,7 +358,7 @@ int main(int argc, char** argv) {
   std::vector<std::vector<uint32_t>> lat(T);
   std::vector<uint64_t> done(T * 8, 0);
   std::vector<std::thread> th;
-  for (int t = 0; t < T; ++t) {
+  for (int t = 0; t < T && OUT > 0; ++t) {
     th.emplace_back([&, t] {
       Granule* ring = in + (size_t)t * N * F;
       volatile Rec* rec = out + (size_t)t * N;
