@@ -95,14 +95,18 @@ def per_rank_cpus() -> int:
     return max(1, min(aff // share, total // local_world))
 
 
-RESIDENT_MIN_CPUS = 12  # the resident path's IO threads poll their records: per_rank_cpus() / 2 of them
+RESIDENT_MIN_CPUS = 8  # the smallest per-rank CPU budget measured with the resident path (no loss there)
 
 
 def resident_auto_ok() -> bool:
-    """resident=auto turns the resident SMALL-path kernel on for a rank with a GPU of its own and
-    CPUs enough for its polling IO threads. Two ranks on one card measured at half the batcher
-    path's throughput (0.53 M vs 1.05-1.21 M req/s, profiles/r5_serve/README.md)."""
-    return not gpu_shared_by_ranks() and per_rank_cpus() >= RESIDENT_MIN_CPUS
+    """resident=auto turns the resident SMALL-path kernel on for a rank with a GPU and at least
+    RESIDENT_MIN_CPUS CPUs of its own. Measured on one MI355X (profiles/r6_resident_n/README.md):
+    ranks sharing one card gain from it (2 ranks, io 4 : client 4 each: 2.69-2.77 M req/s on vs
+    1.40-1.43 M off), a rank limited to 8 CPUs neither gains nor loses (1.14-1.15 vs 1.12-1.16 M),
+    and 56 extra polling waves - the host-memory reads of 8 GPUs x 8 rings - cost nothing measurable
+    (1.85 M median of 3 with and without). Round 5's 0.53 M two-rank collapse does not reproduce,
+    neither with round 5's own tree (1.75-1.78 M) nor with this one."""
+    return per_rank_cpus() >= RESIDENT_MIN_CPUS
 
 
 def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None,

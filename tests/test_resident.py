@@ -194,9 +194,21 @@ def test_resident_hot_reload_under_load(native, device):
     assert d["resident_rows"] > 0, d
 
 
-def test_resident_auto_off_when_ranks_share_a_gpu(monkeypatch):
-    """resident=auto keeps the batcher path for ranks that share one device (p2p rehearsals): two
-    resident kernels on one card measured at half the batcher path's throughput."""
+def test_resident_auto_rule(monkeypatch):
+    """resident=auto: on for every rank with at least RESIDENT_MIN_CPUS CPUs, whether or not ranks
+    share the device (profiles/r6_resident_n/: two ranks on one card 2.69-2.77 M req/s with the
+    resident kernel vs 1.40-1.43 M without; at 8 CPUs per rank on = off)."""
+    from mlapi_amd.parallel import comm
+
+    monkeypatch.setattr(comm, "per_rank_cpus", lambda: 16)
+    assert comm.resident_auto_ok()
+    monkeypatch.setattr(comm, "per_rank_cpus", lambda: 8)
+    assert comm.resident_auto_ok()      # two ranks on the 16-CPU box: on (measured faster)
+    monkeypatch.setattr(comm, "per_rank_cpus", lambda: 4)
+    assert not comm.resident_auto_ok()  # below anything measured: the batcher path
+
+
+def test_gpu_shared_by_ranks(monkeypatch):
     import torch
 
     from mlapi_amd.parallel import comm
@@ -223,7 +235,7 @@ def test_per_rank_cpus_share_of_quota(monkeypatch):
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(128)))
     monkeypatch.setattr(threads, "cgroup_cpu_quota", lambda root="/sys/fs/cgroup": 16.0)
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
-    assert comm.per_rank_cpus() == 8      # two ranks in a 16-CPU quota: resident stays off
+    assert comm.per_rank_cpus() == 8      # two ranks in a 16-CPU quota
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
     assert comm.per_rank_cpus() == 16     # the 1-GPU box: on
     monkeypatch.setattr(threads, "cgroup_cpu_quota", lambda root="/sys/fs/cgroup": None)

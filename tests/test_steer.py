@@ -88,8 +88,8 @@ def test_steering_off_keeps_the_acceptor_deal(native):
         lg.set_workload([r.decode() for r in reqs], [e.decode() for e in exp], 0.0)
         lg.set_conn_map("shuffle", 3)
         res = lg.run(300, False)
-        lg.close()
         st = srv.http.stats()
+        lg.close()
     assert res["status_counts"] == {200: 4800} and res["body_mismatches"] == 0, res
     assert st["steered"] == 0 and st["conns_per_thread"] == [4, 4, 4, 4], st
 
