@@ -291,6 +291,11 @@ void launch_gdw_reduce(const float* slabs, int nslabs, int K, int F_aug, float* 
 // (optional, [B][Kp] f32): the first pass stores its logits there and the second reads them back
 // instead of recomputing them; null recomputes.
 int softmax_rows_g_blocks(int64_t B, int F, int K);
+// true: launch_softmax_rows_g keeps the logits in registers (softmax_rows_g2_kernel) and never
+// touches Zs, so callers need no [B][Kp] f32 buffer for it
+bool softmax_rows_g_keeps_logits(int64_t B, int F, int K, int Kp);
+// measurement / tests: -1 = MLAPI_ROWS_G2 (default on), 0 = the XLDS kernel + logits buffer, 1 = on
+void gemm_softmax_set_rows_g2(int on);
 void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y, int64_t B,
                            int F, int K, int kind, uint16_t* G, int Kp, float* stat_slabs, float* Zs,
                            hipStream_t stream);

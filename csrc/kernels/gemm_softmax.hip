@@ -1462,6 +1462,199 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
   }
 }
 
+// MODE 5 with the logits in registers (wide-F training G, F in (512, 1024], K <= 1024): the XLDS
+// row-group kernel computed each wave's two class chunks one after the other and parked the first
+// pass's logits in an f32 [B][Kp] buffer for the G pass (2 x 268 MB of HBM traffic per F = 1024
+// step at B = 65,536). Here a wave accumulates BOTH its chunks in one sweep over F (2 x 64 f32 per
+// lane), so the logits never leave the registers: the row stats merge across the waves through LDS
+// as before, and the G pass reads the accumulators. The W fragments ping-pong between the two
+// chunks - the next fragment's loads are in flight under the other chunk's 32 MFMAs - and X comes
+// from the block's LDS copy (staged once, as XLDS).
+template <bool OVR>
+__global__ __launch_bounds__(512) void softmax_rows_g2_kernel(RowsArgs a) {
+  constexpr int NT = 4, KS = 2, ROWS = 16 * NT, SLICE = KS * 32;
+  static_assert(ROWS == XLDS_ROWS, "the X copy holds 64 rows");
+  __shared__ __attribute__((aligned(16))) uint16_t xs[XLDS_ROWS][XLDS_PITCH];
+  __shared__ float4 part[ROWS_MAX_WAVES][ROWS];
+  __shared__ float lse_s[ROWS], hit_s[ROWS], wsum_s[ROWS_MAX_WAVES];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = blockDim.x >> 6;
+  const int q = lane >> 4;
+  const int col = lane & 15;
+  const int64_t B = a.B;
+  const int K = a.K;
+  const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+  const int nslices = a.F / SLICE;
+  const int nchunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
+  const int cc[2] = {wave * CLASS_CHUNK, (wave + nw) * CLASS_CHUNK};
+  const bool has_b = wave + nw < nchunks;  // wave-uniform
+  {  // stage the block's rows (rows past B clamped to the last one)
+    const int cpr = a.F / 8;
+    for (int i = (int)threadIdx.x; i < ROWS * cpr; i += (int)blockDim.x) {
+      const int r = i / cpr, c = (i - r * cpr) * 8;
+      const int64_t row = min(row0 + r, B - 1);
+      *reinterpret_cast<uint4*>(&xs[r][c]) = *reinterpret_cast<const uint4*>(a.X + row * a.ldx + c);
+    }
+  }
+  f32x4_t acc[2][NT][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int cb = cc[h] + mt * 16 + q * 4;
+      const f32x4_t b0 = {a.bias[min(cb, K - 1)], a.bias[min(cb + 1, K - 1)], a.bias[min(cb + 2, K - 1)],
+                          a.bias[min(cb + 3, K - 1)]};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[h][t][mt] = b0;
+    }
+  __syncthreads();
+  bf16x8_t wa[4][KS], wb[4][KS];
+  // W through a range-checked descriptor: ONE per-lane offset (class col, feature group q), the
+  // chunk / slice / k-step part a scalar offset, classes past K read as zeros (masked in the
+  // epilogue) - no clamped 64-bit address per fragment (those cost the registers the accumulators need)
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, K * a.F * 2, 0x00020000);
+  const uint32_t wlane = (uint32_t)(col * a.F + 8 * q) * 2u;
+  // k-step major: the first k-step's MFMAs wait for its 4 fragments only (vmcnt counts in order)
+  auto load_w = [&](int c0, int sl, bf16x8_t(&wf)[4][KS]) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        wf[mt][ks] = __builtin_bit_cast(
+            bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
+                          wrs, wlane, (uint32_t)(((c0 + mt * 16) * a.F + sl * SLICE + ks * 32) * 2), 0));
+  };
+  // X fragments one k-step at a time from the LDS copy (16 registers, not 32: the 128 accumulators
+  // and both W fragments must fit 256 VGPRs at 2 waves per SIMD); the other wave covers the reads
+  auto mma = [&](int sl, const bf16x8_t(&wf)[4][KS], f32x4_t(&ac)[NT][4]) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8_t xk[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        xk[t] = *reinterpret_cast<const bf16x8_t*>(&xs[t * 16 + col][sl * SLICE + ks * 32 + 8 * q]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          ac[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[mt][ks], xk[t], ac[t][mt], 0, 0, 0);
+    }
+  };
+  // Branch-free: a branch around a load group makes the wait insertion fall back to vmcnt(0) at the
+  // join, which waits for the fragments just issued for the OTHER chunk and defeats the ping-pong.
+  // So the loads and MFMAs of chunk b run on every wave (past K the range-checked loads return
+  // zeros and chunk b's results are never read), and the last slice's look-ahead load of chunk a
+  // (out of range or the next class row's features, never used) is issued anyway.
+  load_w(cc[0], 0, wa);
+  for (int sl = 0; sl < nslices; ++sl) {
+    load_w(cc[1], sl, wb);  // in flight under chunk a's MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+    mma(sl, wa, acc[0]);
+    load_w(cc[0], sl + 1, wa);  // in flight under chunk b's MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+    mma(sl, wb, acc[1]);
+  }
+  // row stats: online (max, sum, first argmax) over the wave's chunks, then the lanes of a row, then
+  // the waves in order (deterministic)
+  RowState st[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) st[t] = RowState{-INFINITY, 0.f, 0x7fffffff};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h == 1 && !has_b) break;
+    const int c0 = cc[h];
+    const bool partial = c0 + CLASS_CHUNK > K;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = acc[h][t][i >> 2][i & 3];
+      if (partial) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = c0 + (i >> 2) * 16 + q * 4 + (i & 3) < K ? v[i] : -INFINITY;
+      }
+      online_update<OVR>(v, c0, q, st[t]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    RowState S = st[t];
+    S = merge_state(S, shfl_state(S, 16), OVR);
+    S = merge_state(S, shfl_state(S, 32), OVR);
+    if (q == 0) part[wave][t * 16 + col] = make_float4(S.m, S.s, __int_as_float(S.bi), 0.f);
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < ROWS) {
+    const int r = threadIdx.x;
+    const float4 p0 = part[0][r];
+    RowState S{p0.x, p0.y, __float_as_int(p0.z)};
+    for (int w = 1; w < nw; ++w) {
+      const float4 pw = part[w][r];
+      S = merge_state(S, RowState{pw.x, pw.y, __float_as_int(pw.z)}, OVR);
+    }
+    const int64_t row = row0 + r;
+    lse_s[r] = S.m + __logf(S.s);
+    hit_s[r] = row < B && S.bi == a.y[row] ? 1.f : 0.f;
+  }
+  __syncthreads();
+  // G = softmax(z) - onehot(y) (OvR: sigmoid(z) - onehot) as bf16 [B][Kp], from the accumulators
+  float lse[NT];
+  int yr[NT];
+  bool live[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int64_t row = row0 + t * 16 + col;
+    live[t] = row < B;
+    lse[t] = lse_s[t * 16 + col];
+    yr[t] = live[t] ? a.y[row] : -1;
+  }
+  float loss = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h == 1 && !has_b) break;
+    const int c0 = cc[h];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (!live[t]) continue;
+      uint16_t* gr = a.G + (row0 + t * 16 + col) * (int64_t)a.Kp + c0 + q * 4;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        uint16_t gb[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cls = c0 + mt * 16 + q * 4 + r;
+          const float z = acc[h][t][mt][r];
+          float g = 0.f;
+          if (cls < K) {
+            const bool is_y = cls == yr[t];
+            const float p = OVR ? 1.f / (1.f + __expf(-z)) : __expf(z - lse[t]);
+            g = p - (is_y ? 1.f : 0.f);
+            if constexpr (OVR) loss += fmaxf(z, 0.f) - (is_y ? z : 0.f) + log1pf(__expf(-fabsf(z)));
+            else if (is_y) loss += lse[t] - z;
+          }
+          gb[r] = bf16_rne(g);
+        }
+        uint2 pk;
+        pk.x = (uint32_t)gb[0] | ((uint32_t)gb[1] << 16);
+        pk.y = (uint32_t)gb[2] | ((uint32_t)gb[3] << 16);
+        *reinterpret_cast<uint2*>(gr + mt * 16) = pk;
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) loss += __shfl_xor(loss, off, 64);
+  if (lane == 0) wsum_s[wave] = loss;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float l = 0.f, h = 0.f;
+    for (int w = 0; w < nw; ++w) l += wsum_s[w];
+    for (int r = 0; r < ROWS; ++r) h += hit_s[r];
+    a.stat_slabs[2 * (int64_t)blockIdx.x] = l;
+    a.stat_slabs[2 * (int64_t)blockIdx.x + 1] = h;
+  }
+}
+
 // Which kernel serves (B, K, F): the row-group kernel only where the tiles kernel has no
 // instantiation (F > 512, the only kernel that loops F). At F <= 512 the tiles kernel with class
 // splits is faster at every B (profiles/r2_gemm/sweep.log: B <= 4096 rows 17-19 us vs tiles 7-10).
@@ -1503,6 +1696,21 @@ bool rows_xlds(int64_t B, int F, int K) {
     return e == nullptr || std::atoi(e) != 0;
   }();
   return on && F > 512 && F <= XLDS_FMAX && F % 256 == 0 && B >= 16384 && K > CLASS_CHUNK;
+}
+
+// softmax_rows_g2_kernel serves the wide-F training G launch where the XLDS kernel would (64-row
+// blocks, F in (512, 1024]) and every wave has at most two class chunks (K <= 1024) with no padded
+// chunk past them (Kp = K rounded up to 64). MLAPI_ROWS_G2=0 keeps the XLDS kernel + logits buffer.
+int g_rows_g2 = -1;  // gemm_softmax_set_rows_g2: -1 MLAPI_ROWS_G2 (default on), 0 off, 1 on
+
+bool rows_g2(int64_t B, int F, int K, int Kp) {
+  static const bool env = [] {
+    const char* e = std::getenv("MLAPI_ROWS_G2");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  const bool on = g_rows_g2 < 0 ? env : g_rows_g2 != 0;
+  const int nchunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
+  return on && rows_xlds(B, F, K) && nchunks <= 2 * ROWS_MAX_WAVES && Kp == nchunks * CLASS_CHUNK;
 }
 
 template <int MODE>
@@ -1881,6 +2089,10 @@ int softmax_rows_g_blocks(int64_t B, int F, int K) {  // launch_rows' grid: one 
   return (int)((B + rows - 1) / rows);
 }
 
+bool softmax_rows_g_keeps_logits(int64_t B, int F, int K, int Kp) { return rows_g2(B, F, K, Kp); }
+
+void gemm_softmax_set_rows_g2(int on) { g_rows_g2 = on; }
+
 void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y, int64_t B,
                            int F, int K, int kind, uint16_t* G, int Kp, float* stat_slabs, float* Zs,
                            hipStream_t stream) {
@@ -1894,6 +2106,17 @@ void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const 
   ra.Kp = Kp;
   ra.stat_slabs = stat_slabs;
   ra.Zs = Zs;
+  if (rows_g2(B, F, K, Kp)) {
+    // logits kept in registers (no Zs round trip): 8 waves x (at most) 2 class chunks
+    const int nchunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
+    const dim3 grid((unsigned)((B + XLDS_ROWS - 1) / XLDS_ROWS)), block(64 * std::min(nchunks, ROWS_MAX_WAVES));
+    if (kind == KIND_OVR)
+      hipLaunchKernelGGL(softmax_rows_g2_kernel<true>, grid, block, 0, stream, ra);
+    else
+      hipLaunchKernelGGL(softmax_rows_g2_kernel<false>, grid, block, 0, stream, ra);
+    MLAPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   launch_rows<5>(ra, kind, stream);
 }
 

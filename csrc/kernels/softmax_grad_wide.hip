@@ -241,8 +241,8 @@ WideLayout wide_layout(int64_t B, int K, int F) {
   o = al(o + (size_t)L.row_groups * K * F_aug * sizeof(float));
   L.stat_off = o;
   o = al(o + (size_t)L.g_blocks * 2 * sizeof(float));
-  L.z_off = o;  // the row-stats pass's logits, [B][Kp] f32 (zbuf_on())
-  o = al(o + (size_t)B * L.Kp * sizeof(float));
+  L.z_off = o;  // the row-stats pass's logits, [B][Kp] f32 (zbuf_on(), unless the kernel keeps them in registers)
+  if (!softmax_rows_g_keeps_logits(B, F, K, L.Kp)) o = al(o + (size_t)B * L.Kp * sizeof(float));
   L.total = o;
   return L;
 }
@@ -286,7 +286,7 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
   uint16_t* G = reinterpret_cast<uint16_t*>(ws + L.g_off);
   float* slabs = reinterpret_cast<float*>(ws + L.dw_off);
   float* stat_slabs = reinterpret_cast<float*>(ws + L.stat_off);
-  float* Zs = zbuf_on() ? reinterpret_cast<float*>(ws + L.z_off) : nullptr;
+  float* Zs = zbuf_on() && !softmax_rows_g_keeps_logits(B, F, K, L.Kp) ? reinterpret_cast<float*>(ws + L.z_off) : nullptr;
   launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, Zs, stream);
   const int g_blocks = L.g_blocks;
   const int F_aug = F + 8;

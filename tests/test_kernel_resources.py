@@ -77,6 +77,21 @@ def test_gemm_softmax_kernels_fit_two_waves_per_simd_without_spills(tmp_path):
         assert not any("scratch_" in blk for blk in loops), name
 
 
+def test_rows_g2_kernel_keeps_its_logits_without_spilling_in_the_loop(tmp_path):
+    """The wide-F training G kernel that holds two class chunks of logits in registers (128 VGPRs of
+    accumulators) fits 2 waves per SIMD; its few spilled registers live outside the MFMA loop."""
+    text = _compile("kernels/gemm_softmax.hip", tmp_path)
+    res = _resources(text)
+    got = _pick(res, r"softmax_rows_g2_kernel")
+    assert len(got) == 2, sorted(got)  # softmax / OvR
+    for name, r in got.items():
+        assert r.get("num_vgpr", 0) + r.get("num_agpr", 0) <= 256, (name, r)
+        assert r.get("private_seg_size", 0) <= 16, (name, r)
+        loops = list(_mfma_loop_blocks(text, name))
+        assert loops, name
+        assert not any("scratch_" in blk for blk in loops), name
+
+
 def test_class_split_serving_kernel_has_no_scratch(tmp_path):
     res = _resources(_compile("kernels/linear_split.hip", tmp_path))
     for name, r in _pick(res, r"linear_split_kernel").items():

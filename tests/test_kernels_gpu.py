@@ -412,6 +412,16 @@ def test_softmax_grad_wide(B, F, K, kind):
     finally:
         C().softmax_grad_wide_set_zbuf(-1)
     assert torch.equal(dW2, dW3) and torch.equal(st2, st3)
+    # logits kept in registers (softmax_rows_g2_kernel, where it applies) vs the XLDS kernel with the
+    # logits buffer: the same MFMA and merge order, so the same bits
+    C().gemm_softmax_set_rows_g2(0)
+    try:
+        bufs0 = ops.SoftmaxTrainBuffers(B, K, Fk, X.device)
+        dW4, st4 = ops.softmax_train_grad(Xa, Wb, b, y, kind, bufs=bufs0)
+        torch.cuda.synchronize()
+    finally:
+        C().gemm_softmax_set_rows_g2(-1)
+    assert torch.equal(dW2, dW4) and torch.equal(st2, st4)
 
 
 def test_sgd_wide_multiclass_estimator_one_gpu():
