@@ -373,7 +373,8 @@ def test_softmax_grad_dw_fused(B, F, K, kind, groups, nc):
 @pytest.mark.parametrize("B,F,K,kind", [(2048, 1024, 100, Kind.MULTINOMIAL), (777, 700, 37, Kind.OVR),
                                         (4099, 1024, 1000, Kind.MULTINOMIAL), (65, 2048, 3, Kind.MULTINOMIAL),
                                         (20000, 1024, 130, Kind.OVR),  # B >= 16384, F <= 1024: X staged in LDS
-                                        (16384, 768, 1000, Kind.MULTINOMIAL)])
+                                        (16384, 768, 1000, Kind.MULTINOMIAL),
+                                        (16400, 1024, 1000, Kind.MULTINOMIAL)])
 def test_softmax_grad_wide(B, F, K, kind):
     """Wide multiclass gradient (F > 512, softmax_grad_wide.hip: row stats + logits by the row-group
     kernel, G in bf16, G^T X_aug by the transposed-LDS MFMA kernel, slab sum) vs the fp32 oracle;
