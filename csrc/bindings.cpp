@@ -594,6 +594,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("io_steer", &ServerConfig::io_steer)
       .def_readwrite("steer_every", &ServerConfig::steer_every)
       .def_readwrite("steer_stable", &ServerConfig::steer_stable)
+      .def_readwrite("io_cpus", &ServerConfig::io_cpus)
       .def_readwrite("access_log", &ServerConfig::access_log)
       .def_readwrite("access_log_fd", &ServerConfig::access_log_fd)
       .def_readwrite("health_dispatch", &ServerConfig::health_dispatch)

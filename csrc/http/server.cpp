@@ -9,6 +9,8 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/prctl.h>
@@ -415,6 +417,17 @@ class IoThread : public Sink {
     char name[16];
     snprintf(name, sizeof name, "mlapi-io-%d", index_);
     pthread_setname_np(pthread_self(), name);
+    if (!srv_->config().io_cpus.empty()) {
+      const auto& cpus = srv_->config().io_cpus;
+      cpu_set_t set;
+      CPU_ZERO(&set);
+      const int cpu = cpus[(size_t)index_ % cpus.size()];
+      if (cpu >= 0 && cpu < CPU_SETSIZE) {
+        CPU_SET(cpu, &set);
+        if (pthread_setaffinity_np(pthread_self(), sizeof set, &set) != 0)
+          fprintf(stderr, "mlapi: io thread %d: cannot pin to cpu %d (left unpinned)\n", index_, cpu);
+      }
+    }
     timing_ = srv_->config().stage_timing;
     ns_per_tick_ = tsc_ns_per_tick();
     st_last_ = __rdtsc();

@@ -70,6 +70,7 @@ class NativeServer:
         sc.io_steer = int(config.io_steer)
         sc.steer_every = int(config.steer_every)
         sc.steer_stable = int(config.steer_stable)
+        sc.io_cpus = [int(c) for c in str(config.io_cpus).split(",") if c.strip()]
         sc.access_log_fd = int(access_log_fd)
         sc.dispatch = str(config.dispatch)
         sc.dispatch_group = str(config.dispatch_group)

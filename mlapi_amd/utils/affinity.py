@@ -293,3 +293,49 @@ def client_thread_cpus(local_rank: int, local_world: int, nthreads: int, mask: L
         slot, sharing = local_rank, max(1, local_world)
     stride = max(nthreads, len(order) // max(1, sharing))
     return [order[(slot * stride + i) % len(order)] for i in range(nthreads)]
+
+
+def _siblings(cpu: int, sysfs: str) -> List[int]:
+    s = _read(f"{sysfs}/cpu{cpu}/topology/thread_siblings_list")
+    return parse_cpulist(s) if s else [cpu]
+
+
+def _llc(cpu: int, sysfs: str) -> List[int]:
+    s = _read(f"{sysfs}/cpu{cpu}/cache/index3/shared_cpu_list")
+    return parse_cpulist(s) if s else []
+
+
+def serve_thread_cpus(local_rank: int, local_world: int, n_client: int, n_io: int, mask: List[int],
+                      nodes: Optional[List[Optional[int]]] = None, sysfs: str = SYS_CPU,
+                      mode: str = "cores") -> tuple:
+    """(client CPUs, IO-thread CPUs) of a serving rank: the load-generator threads' CPUs as
+    :func:`client_thread_cpus` picks them, and one CPU per server IO thread by ``mode``:
+
+    * ``cores``: the next ``n_io`` CPUs of the same stretch of ``mask`` - physical cores of their own;
+    * ``sibling``: IO thread i on the SMT sibling of client thread i's CPU (one core per pair);
+    * ``llc``: IO thread i on a free CPU sharing client thread i's last-level cache (another core of
+      its CCD first, its sibling last).
+
+    ([], []) for an empty mask."""
+    if not mask or n_client + n_io <= 0:
+        return [], []
+    if mode == "cores":
+        both = client_thread_cpus(local_rank, local_world, n_client + n_io, mask, nodes, sysfs)
+        return both[:n_client], both[n_client:]
+    cl = client_thread_cpus(local_rank, local_world, n_client, mask, nodes, sysfs)
+    allowed, used, io = set(mask), set(cl), []
+    for i in range(n_io):
+        c = cl[i % len(cl)] if cl else mask[0]
+        sib = [x for x in _siblings(c, sysfs) if x != c and x in allowed]
+        if mode == "sibling":
+            cands = sib
+        else:  # llc: first threads of other cores of the client's LLC, then any free CPU of it, then the sibling
+            llc = [x for x in _llc(c, sysfs) if x in allowed and x != c]
+            order = core_order(llc, sysfs)
+            cands = [x for x in order if x not in sib] + sib
+        pick = next((x for x in cands if x not in used), None)
+        if pick is None:
+            pick = next((x for x in core_order(sorted(allowed), sysfs) if x not in used), c)
+        used.add(pick)
+        io.append(pick)
+    return cl, io

@@ -33,6 +33,65 @@ def test_client_thread_cpus_disjoint_per_rank():
     assert client_thread_cpus(0, 1, 0, mask) == [] and client_thread_cpus(0, 1, 4, []) == []
 
 
+def test_serve_thread_cpus_give_io_threads_cores_of_their_own():
+    from mlapi_amd.utils.affinity import client_thread_cpus, serve_thread_cpus
+
+    mask = list(range(64))
+    sysfs = "/nonexistent"
+    cl, io = serve_thread_cpus(0, 2, 8, 8, mask, [0, 0], sysfs=sysfs)
+    assert cl == client_thread_cpus(0, 2, 8, mask, [0, 0], sysfs=sysfs)[:8] and len(io) == 8
+    assert not set(cl) & set(io) and len(set(io)) == 8
+    cl1, io1 = serve_thread_cpus(1, 2, 8, 8, mask, [0, 0], sysfs=sysfs)  # the other rank's stretch
+    assert not (set(cl) | set(io)) & (set(cl1) | set(io1))
+    assert serve_thread_cpus(0, 1, 4, 0, mask, sysfs=sysfs) == (client_thread_cpus(0, 1, 4, mask, sysfs=sysfs), [])
+    assert serve_thread_cpus(0, 1, 4, 4, []) == ([], [])
+
+
+def test_serve_thread_cpus_llc_and_sibling_modes(tmp_path):
+    """A fake topology: 8 cores x 2 threads (CPU c and c + 8 siblings), two 4-core LLCs."""
+    from mlapi_amd.utils.affinity import serve_thread_cpus
+
+    for c in range(16):
+        core = c % 8
+        d = tmp_path / f"cpu{c}"
+        (d / "topology").mkdir(parents=True)
+        (d / "cache" / "index3").mkdir(parents=True)
+        (d / "topology" / "core_id").write_text(str(core))
+        (d / "topology" / "physical_package_id").write_text("0")
+        (d / "topology" / "thread_siblings_list").write_text(f"{core},{core + 8}")
+        lo = 0 if core < 4 else 4
+        (d / "cache" / "index3" / "shared_cpu_list").write_text(f"{lo}-{lo + 3},{lo + 8}-{lo + 11}")
+    mask = list(range(16))
+    cl, io = serve_thread_cpus(0, 1, 2, 2, mask, sysfs=str(tmp_path), mode="sibling")
+    assert io == [c + 8 for c in cl]
+    cl, io = serve_thread_cpus(0, 1, 2, 2, mask, sysfs=str(tmp_path), mode="llc")
+    assert len(set(io)) == 2 and not set(io) & set(cl)
+    for c, i in zip(cl, io):
+        assert (c % 8 < 4) == (i % 8 < 4) and i % 8 != c % 8  # same LLC, another core
+
+
+@pytest.mark.skipif(len(os.sched_getaffinity(0)) < 2, reason="needs 2 CPUs")
+def test_io_cpus_pin_the_io_threads(native):
+    """Config.io_cpus: IO thread i runs on the i-th CPU of the list (bench.py --io-pin)."""
+    cpus = sorted(os.sched_getaffinity(0))[:2]
+    with _server(4, io_cpus=",".join(str(c) for c in cpus)) as srv:
+        srv.start()
+        seen = {}
+        deadline = time.time() + 10
+        while len(seen) < 4 and time.time() < deadline:
+            for tid in os.listdir("/proc/self/task"):
+                try:
+                    name = open(f"/proc/self/task/{tid}/comm").read().strip()
+                except OSError:
+                    continue
+                if name.startswith("mlapi-io-"):
+                    seen[int(name.rsplit("-", 1)[1])] = sorted(os.sched_getaffinity(int(tid)))
+            time.sleep(0.05)
+        assert sorted(seen) == [0, 1, 2, 3], seen
+        for i, aff in seen.items():
+            assert aff == [cpus[i % 2]], (i, aff)
+
+
 def _server(io_threads, **kw):
     from mlapi_amd.serve.server import NativeServer
     from mlapi_amd.utils.config import Config
