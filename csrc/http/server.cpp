@@ -417,11 +417,10 @@ class IoThread : public Sink {
     char name[16];
     snprintf(name, sizeof name, "mlapi-io-%d", index_);
     pthread_setname_np(pthread_self(), name);
-    if (!srv_->config().io_cpus.empty()) {
-      const auto& cpus = srv_->config().io_cpus;
+    if ((size_t)index_ < srv_->config().io_cpus.size()) {
       cpu_set_t set;
       CPU_ZERO(&set);
-      const int cpu = cpus[(size_t)index_ % cpus.size()];
+      const int cpu = srv_->config().io_cpus[(size_t)index_];
       if (cpu >= 0 && cpu < CPU_SETSIZE) {
         CPU_SET(cpu, &set);
         if (pthread_setaffinity_np(pthread_self(), sizeof set, &set) != 0)

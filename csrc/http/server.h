@@ -81,7 +81,7 @@ struct ServerConfig {
   int io_steer = 1;
   int steer_every = 32;
   int steer_stable = 3;  // samples in a row on one CPU before a connection may move
-  // IO thread i runs on CPU io_cpus[i % size] (empty = wherever the scheduler puts it). A NIC
+  // IO thread i runs on CPU io_cpus[i] (threads past the list: wherever the scheduler puts them). A NIC
   // deployment pins them next to the RX queues' CPUs; bench.py gives them physical cores of their
   // own beside the load generator's (an unpinned IO thread sharing a core with another one or a
   // client thread is what made the same binary measure 1.3 or 2.3 M req/s run to run).

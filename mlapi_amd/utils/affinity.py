@@ -316,7 +316,8 @@ def serve_thread_cpus(local_rank: int, local_world: int, n_client: int, n_io: in
     * ``llc``: IO thread i on a free CPU sharing client thread i's last-level cache (another core of
       its CCD first, its sibling last).
 
-    ([], []) for an empty mask."""
+    In the paired modes IO threads past the client threads get no CPU (the server leaves them
+    unpinned: a core of their own was measured the worst placement). ([], []) for an empty mask."""
     if not mask or n_client + n_io <= 0:
         return [], []
     if mode == "cores":
@@ -324,8 +325,8 @@ def serve_thread_cpus(local_rank: int, local_world: int, n_client: int, n_io: in
         return both[:n_client], both[n_client:]
     cl = client_thread_cpus(local_rank, local_world, n_client, mask, nodes, sysfs)
     allowed, used, io = set(mask), set(cl), []
-    for i in range(n_io):
-        c = cl[i % len(cl)] if cl else mask[0]
+    for i in range(min(n_io, len(cl))):
+        c = cl[i]
         sib = [x for x in _siblings(c, sysfs) if x != c and x in allowed]
         if mode == "sibling":
             cands = sib

@@ -54,7 +54,7 @@ class Config:
     io_steer: int = 1                         # group connections on IO threads by their SO_INCOMING_CPU (0 = off)
     steer_every: int = 32                     # ... sampled every this many requests per connection
     steer_stable: int = 3                     # ... moved only after this many samples in a row on one CPU
-    io_cpus: str = ""                          # IO thread i pinned to the i-th CPU of this comma list ("" = unpinned)
+    io_cpus: str = ""                          # IO thread i pinned to the i-th CPU of this comma list (threads past it unpinned)
     max_queue: int = 1 << 20                  # backpressure: queued rows beyond this -> HTTP 503
     inline_args: bool = True                  # GPU: tiny batches travel in the kernel-argument block
     record_completion: bool = True            # GPU: kernel-argument batches complete through 16-B per-row records

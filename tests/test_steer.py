@@ -64,6 +64,7 @@ def test_serve_thread_cpus_llc_and_sibling_modes(tmp_path):
     mask = list(range(16))
     cl, io = serve_thread_cpus(0, 1, 2, 2, mask, sysfs=str(tmp_path), mode="sibling")
     assert io == [c + 8 for c in cl]
+    assert serve_thread_cpus(0, 1, 2, 5, mask, sysfs=str(tmp_path), mode="sibling")[1] == io  # no pair: unpinned
     cl, io = serve_thread_cpus(0, 1, 2, 2, mask, sysfs=str(tmp_path), mode="llc")
     assert len(set(io)) == 2 and not set(io) & set(cl)
     for c, i in zip(cl, io):
@@ -88,8 +89,8 @@ def test_io_cpus_pin_the_io_threads(native):
                     seen[int(name.rsplit("-", 1)[1])] = sorted(os.sched_getaffinity(int(tid)))
             time.sleep(0.05)
         assert sorted(seen) == [0, 1, 2, 3], seen
-        for i, aff in seen.items():
-            assert aff == [cpus[i % 2]], (i, aff)
+        for i, aff in seen.items():  # threads past the list keep the process mask
+            assert aff == ([cpus[i]] if i < 2 else sorted(os.sched_getaffinity(0))), (i, aff)
 
 
 def _server(io_threads, **kw):
