@@ -308,35 +308,54 @@ def _llc(cpu: int, sysfs: str) -> List[int]:
 def serve_thread_cpus(local_rank: int, local_world: int, n_client: int, n_io: int, mask: List[int],
                       nodes: Optional[List[Optional[int]]] = None, sysfs: str = SYS_CPU,
                       mode: str = "cores") -> tuple:
-    """(client CPUs, IO-thread CPUs) of a serving rank: the load-generator threads' CPUs as
-    :func:`client_thread_cpus` picks them, and one CPU per server IO thread by ``mode``:
+    """(client CPUs, IO-thread CPUs) of a serving rank, by ``mode``:
 
-    * ``cores``: the next ``n_io`` CPUs of the same stretch of ``mask`` - physical cores of their own;
-    * ``sibling``: IO thread i on the SMT sibling of client thread i's CPU (one core per pair);
-    * ``llc``: IO thread i on a free CPU sharing client thread i's last-level cache (another core of
-      its CCD first, its sibling last).
+    * ``cores``: the load-generator threads' CPUs as :func:`client_thread_cpus` picks them, then the
+      next ``n_io`` CPUs of the same stretch - physical cores of their own;
+    * ``sibling``: the ranks sharing ``mask`` split its PHYSICAL cores into disjoint stretches; client
+      thread i takes the first hardware thread of core i of this rank's stretch and IO thread i its
+      SMT sibling (one core per pair, and no core shared between ranks);
+    * ``llc``: client threads as ``sibling``; IO thread i on a free CPU of client thread i's
+      last-level cache in the stretch (another core first, its sibling last).
 
     In the paired modes IO threads past the client threads get no CPU (the server leaves them
-    unpinned: a core of their own was measured the worst placement). ([], []) for an empty mask."""
+    unpinned: a core of their own was measured the worst placement), and client threads past the
+    stretch's cores take the stretch's second hardware threads (their IO partners then stay
+    unpinned). ([], []) for an empty mask."""
     if not mask or n_client + n_io <= 0:
         return [], []
     if mode == "cores":
         both = client_thread_cpus(local_rank, local_world, n_client + n_io, mask, nodes, sysfs)
         return both[:n_client], both[n_client:]
-    cl = client_thread_cpus(local_rank, local_world, n_client, mask, nodes, sysfs)
-    allowed, used, io = set(mask), set(cl), []
-    for i in range(min(n_io, len(cl))):
+    if nodes:
+        mine = nodes[local_rank % len(nodes)]
+        slot = sum(1 for r in range(local_rank) if nodes[r % len(nodes)] == mine)
+        sharing = ranks_on_node(local_rank, max(local_world, local_rank + 1), nodes)
+    else:
+        slot, sharing = local_rank, max(1, local_world)
+    cores = _cores(sorted(mask), sysfs)
+    stride = max(1, len(cores) // sharing)
+    start = (slot * stride) % len(cores)
+    mine_cores = [cores[(start + k) % len(cores)] for k in range(stride)]
+    if n_client <= 0:
+        return [], []
+    cl = [mine_cores[i][0] if i < len(mine_cores) else mine_cores[i % len(mine_cores)][-1]
+          for i in range(n_client)]
+    stretch = [c for core in mine_cores for c in core]
+    used, io = set(cl), []
+    for i in range(min(n_io, n_client)):
         c = cl[i]
-        sib = [x for x in _siblings(c, sysfs) if x != c and x in allowed]
+        core = next(k for k in mine_cores if c in k)
+        sib = [x for x in core if x != c]
         if mode == "sibling":
             cands = sib
-        else:  # llc: first threads of other cores of the client's LLC, then any free CPU of it, then the sibling
-            llc = [x for x in _llc(c, sysfs) if x in allowed and x != c]
-            order = core_order(llc, sysfs)
-            cands = [x for x in order if x not in sib] + sib
+        else:  # llc
+            llc = set(_llc(c, sysfs)) or set(stretch)
+            others = [x for x in _threads_first([k for k in mine_cores if k is not core]) if x in llc]
+            cands = others + sib
         pick = next((x for x in cands if x not in used), None)
         if pick is None:
-            pick = next((x for x in core_order(sorted(allowed), sysfs) if x not in used), c)
+            break  # no free partner: this and later IO threads stay unpinned
         used.add(pick)
         io.append(pick)
     return cl, io

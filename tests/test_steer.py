@@ -62,6 +62,16 @@ def test_serve_thread_cpus_llc_and_sibling_modes(tmp_path):
         lo = 0 if core < 4 else 4
         (d / "cache" / "index3" / "shared_cpu_list").write_text(f"{lo}-{lo + 3},{lo + 8}-{lo + 11}")
     mask = list(range(16))
+    # four ranks on the node: each a stretch of 2 physical cores, client + IO on the same core,
+    # no core shared between ranks (a stretch of LOGICAL CPUs would hand ranks 2-3 the siblings of
+    # ranks 0-1's cores, i.e. their IO threads' CPUs)
+    seen = set()
+    for r in range(4):
+        cl, io = serve_thread_cpus(r, 4, 2, 2, mask, [0, 0, 0, 0], sysfs=str(tmp_path), mode="sibling")
+        assert io == [c + 8 for c in cl] and len(cl) == 2
+        cores = {c % 8 for c in cl}
+        assert not cores & seen
+        seen |= cores
     cl, io = serve_thread_cpus(0, 1, 2, 2, mask, sysfs=str(tmp_path), mode="sibling")
     assert io == [c + 8 for c in cl]
     assert serve_thread_cpus(0, 1, 2, 5, mask, sysfs=str(tmp_path), mode="sibling")[1] == io  # no pair: unpinned
@@ -75,8 +85,7 @@ def test_serve_thread_cpus_llc_and_sibling_modes(tmp_path):
 def test_io_cpus_pin_the_io_threads(native):
     """Config.io_cpus: IO thread i runs on the i-th CPU of the list (bench.py --io-pin)."""
     cpus = sorted(os.sched_getaffinity(0))[:2]
-    with _server(4, io_cpus=",".join(str(c) for c in cpus)) as srv:
-        srv.start()
+    with _server(4, io_cpus=",".join(str(c) for c in cpus)):
         seen = {}
         deadline = time.time() + 10
         while len(seen) < 4 and time.time() < deadline:
