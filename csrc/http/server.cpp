@@ -19,6 +19,7 @@
 #include <x86intrin.h>
 
 #include <cerrno>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <algorithm>
@@ -1322,9 +1323,35 @@ HttpServer::HttpServer(Engine* engine, const ServerConfig& cfg) : engine_(engine
     cpu_conns_[c].store(0);
     plan_[c].store(0);
   }
+  // io_cpus: each CPU's home IO thread = the one pinned to a CPU of the same physical core (the CPU
+  // itself or its SMT sibling, from sysfs); the steering plan prefers it for that CPU's connections
+  home_.assign((size_t)steer_ncpu_, -1);
+  for (size_t i = 0; i < cfg_.io_cpus.size() && i < (size_t)cfg_.io_threads; ++i) {
+    const int cpu = cfg_.io_cpus[i];
+    if (cpu < 0 || cpu >= steer_ncpu_) continue;
+    std::vector<int> sib{cpu};
+    char path[96];
+    snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", cpu);
+    if (FILE* f = fopen(path, "r")) {
+      char buf[128];
+      if (fgets(buf, sizeof buf, f)) {
+        sib.clear();
+        for (char* tok = strtok(buf, ",\n"); tok; tok = strtok(nullptr, ",\n")) {
+          int a = 0, b = 0;
+          const int nf = sscanf(tok, "%d-%d", &a, &b);
+          if (nf == 1) b = a;
+          for (int c = a; nf >= 1 && c <= b; ++c) sib.push_back(c);
+        }
+      }
+      fclose(f);
+    }
+    for (int c : sib)
+      if (c >= 0 && c < steer_ncpu_ && home_[(size_t)c] < 0) home_[(size_t)c] = (int)i;
+  }
 }
 
-// io_steer plan: every CPU that drives connections is assigned to the least-loaded IO thread, and
+// io_steer plan: every CPU that drives connections is assigned to its home IO thread (io_cpus: the
+// one pinned on the same physical core) or else the least-loaded IO thread, and
 // a CPU whose connections exceed that thread's room spills into the next least-loaded ones (at most
 // three threads per CPU; water-filling by group size, ties to the lowest index, so equal counts give
 // an equal plan). A CPU keeps its previous first thread while that one still has room (a re-plan
@@ -1359,8 +1386,11 @@ void HttpServer::steer_replan(int64_t now_ms) {
     int used[3] = {-1, -1, -1};
     for (int k = 0; k < 3 && left > 0; ++k) {
       int t = -1;
+      // first choice: the CPU's home thread (pinned on its core), then its previous thread
+      const int home = home_[(size_t)g.second];
+      if (k == 0 && home >= 0 && home < n && load[(size_t)home] < share) t = home;
       const int p1 = (int)(prev[(size_t)g.second] & 0xff) - 1;
-      if (k == 0 && p1 >= 0 && p1 < n && load[(size_t)p1] < share) t = p1;
+      if (t < 0 && k == 0 && p1 >= 0 && p1 < n && load[(size_t)p1] < share) t = p1;
       if (t < 0)
         for (int i = 0; i < n; ++i)
           if (i != used[0] && i != used[1] && (t < 0 || load[(size_t)i] < load[(size_t)t])) t = i;

@@ -192,6 +192,7 @@ class HttpServer {
   void steer_replan(int64_t now_ms);
   std::unique_ptr<std::atomic<int>[]> cpu_conns_;   // connections whose stable incoming CPU is c
   std::unique_ptr<std::atomic<uint64_t>[]> plan_;   // per CPU: up to three IO threads (+1, 8 bits each)
+  std::vector<int> home_;  // per CPU: the IO thread pinned on its physical core (io_cpus), -1 = none
   std::atomic<int64_t> plan_ms_{0};
   std::atomic<int> steer_share_{1};  // the plan's connections per IO thread
   std::mutex plan_mu_;

@@ -150,6 +150,32 @@ def test_shuffled_pinned_clients_are_regrouped_by_cpu(native):
     assert sorted(st["conns_per_thread"]) == [4, 4, 4, 4], st
 
 
+@pytest.mark.skipif(len(os.sched_getaffinity(0)) < 2, reason="needs 2 CPUs")
+def test_steering_prefers_the_io_thread_pinned_on_the_clients_core(native):
+    """io_cpus gives every CPU a home IO thread (the one pinned on its physical core): the plan sends
+    a client CPU's connections there, even when connect order dealt them elsewhere."""
+    cpus = sorted(os.sched_getaffinity(0))[:2]
+    # IO thread 0 on the second client CPU, thread 1 on the first: the reverse of connect order
+    with _server(2, steer_every=8, steer_stable=2, io_cpus=f"{cpus[1]},{cpus[0]}") as srv:
+        reqs, exp = _workload(srv)
+        lg = native.Loadgen("127.0.0.1", srv.port, reqs[0].decode(), 8, 2)
+        lg.set_workload([r.decode() for r in reqs], [e.decode() for e in exp], 0.0)
+        lg.set_thread_cpus(cpus)
+        t_end = time.time() + 20
+        st = srv.http.stats()
+        while time.time() < t_end:
+            res = lg.run(100, False)
+            assert res["failed"] == 0 and res["body_mismatches"] == 0, res
+            st = srv.http.stats()
+            plan = {p[0]: p for p in st["steer_plan"] if p[1] > 0}
+            if set(plan) == set(cpus) and st["conns_per_thread"] == [4, 4] and st["steered"] >= 8:
+                break
+        lg.close()
+    plan = {p[0]: p for p in st["steer_plan"] if p[1] > 0}
+    assert plan[cpus[0]][2] == 1 and plan[cpus[1]][2] == 0, st["steer_plan"]
+    assert st["steered"] >= 8 and st["conns_per_thread"] == [4, 4], st
+
+
 def test_steering_off_keeps_the_acceptor_deal(native):
     with _server(4, io_steer=0) as srv:
         reqs, exp = _workload(srv)
