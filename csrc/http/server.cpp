@@ -1336,7 +1336,8 @@ HttpServer::HttpServer(Engine* engine, const ServerConfig& cfg) : engine_(engine
       char buf[128];
       if (fgets(buf, sizeof buf, f)) {
         sib.clear();
-        for (char* tok = strtok(buf, ",\n"); tok; tok = strtok(nullptr, ",\n")) {
+        char* save = nullptr;
+        for (char* tok = strtok_r(buf, ",\n", &save); tok; tok = strtok_r(nullptr, ",\n", &save)) {
           int a = 0, b = 0;
           const int nf = sscanf(tok, "%d-%d", &a, &b);
           if (nf == 1) b = a;
