@@ -713,6 +713,13 @@ def main(argv=None) -> int:
         io = max(2, min(12, per_rank // 2 if resident else per_rank - cl - 2))
         if resident:
             cl = io
+        elif args.mode == "serve_wide" and args.client_pin == "on" and args.io_pin != "off":
+            # the batcher path with paired placement: half the CPUs to IO threads, two to the batcher
+            # and completer, the rest to client threads (each paired with an IO thread on its core):
+            # 8 : 6 0.90-0.95 M req/s at 9.7-10.1 us of server CPU per request vs 10 : 4 0.85-0.90 M
+            # at 11.2-11.7 (profiles/r6_iopin/r6s18)
+            io = max(2, min(12, per_rank // 2))
+            cl = max(2, per_rank - io - 2)
         args.io_threads = args.io_threads if args.io_threads > 0 else io
         args.client_threads = args.client_threads if args.client_threads > 0 else cl
     if pinned and getattr(args, "lg_proc", None) is not None and len(pinned) > args.io_threads + 3:
