@@ -202,6 +202,7 @@ PYBIND11_MODULE(_C, m) {
     return d;
   });
   m.def("gemm_softmax_set_rows_g2", &gemm_softmax_set_rows_g2, py::arg("on"));
+  m.def("gemm_softmax_set_w_packed", &gemm_softmax_set_w_packed, py::arg("on"));
   m.def("gemm_softmax_force_plan", &gemm_softmax_force_plan, py::arg("nt") = 0, py::arg("splits") = 0,
         py::arg("kernel") = 0);
   m.def("gemm_softmax_set_stamps", [](uintptr_t p) { gemm_softmax_set_stamps(reinterpret_cast<void*>(p)); });

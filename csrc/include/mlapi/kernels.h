@@ -296,9 +296,14 @@ int softmax_rows_g_blocks(int64_t B, int F, int K);
 bool softmax_rows_g_keeps_logits(int64_t B, int F, int K, int Kp);
 // measurement / tests: -1 = MLAPI_ROWS_G2 (default on), 0 = the XLDS kernel + logits buffer, 1 = on
 void gemm_softmax_set_rows_g2(int on);
+// bytes of the fragment-ordered W copy the register-resident G kernel reads (0: it does not apply);
+// pass such a buffer (16-byte aligned) as w_packed, or null for the row-major reads
+size_t softmax_rows_g_wpack_bytes(int64_t B, int F, int K, int Kp);
+// measurement / tests: -1 = MLAPI_G2_PACKED (default on), 0 = row-major W reads, 1 = packed
+void gemm_softmax_set_w_packed(int on);
 void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y, int64_t B,
                            int F, int K, int kind, uint16_t* G, int Kp, float* stat_slabs, float* Zs,
-                           hipStream_t stream);
+                           void* w_packed, hipStream_t stream);
 void launch_gemm_logits_ld(const void* X, int64_t ldx, const void* W, const float* b, int64_t B, int F, int K, float* Z,
                            hipStream_t stream);
 // Multiclass training gradient for wide models (softmax_grad_wide.hip): F a multiple of 256 above

@@ -1324,7 +1324,28 @@ __global__ __launch_bounds__(512) void softmax_rows_kernel(RowsArgs a) {
 // as before, and the G pass reads the accumulators. The W fragments ping-pong between the two
 // chunks - the next fragment's loads are in flight under the other chunk's 32 MFMAs - and X comes
 // from the block's LDS copy (staged once, as XLDS).
-template <bool OVR>
+// W in MFMA-fragment order (pack_w_frag_kernel): the 16 classes x 32 features one fragment load
+// needs are ONE contiguous 1 KB block in lane order, block (class block cb, k-step kk) at
+// (cb * F / 32 + kk) KB. Each packed load touches 8 full 128-byte lines; the row-major load
+// touched 16 class rows x 64 B (16 lines, half of each used) - measured 326-336 -> 202-204 us for
+// the launch at F = 1024, K = 1000, B = 65,536 (the data was wrong in that probe; same bytes).
+__global__ __launch_bounds__(256) void pack_w_frag_kernel(const uint16_t* __restrict__ W, int K, int F,
+                                                          uint16_t* __restrict__ Wp, int64_t pieces) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= pieces) return;
+  const int lane = (int)(t & 63);
+  const int64_t blk = t >> 6;
+  const int nks = F >> 5;
+  const int cb = (int)(blk / nks), kk = (int)(blk - (int64_t)cb * nks);
+  const int cls = cb * 16 + (lane & 15);
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (cls < K) v = *reinterpret_cast<const uint4*>(W + (int64_t)cls * F + kk * 32 + 8 * (lane >> 4));
+  *reinterpret_cast<uint4*>(Wp + t * 8) = v;
+}
+
+__host__ __device__ inline size_t packed_w_bytes(int K, int F) { return (size_t)((K + 15) / 16) * (size_t)(F / 32) * 1024; }
+
+template <bool OVR, bool PACKED = false>
 __global__ __launch_bounds__(512) void softmax_rows_g2_kernel(RowsArgs a) {
   constexpr int NT = 4, KS = 2, ROWS = 16 * NT, SLICE = KS * 32;
   static_assert(ROWS == XLDS_ROWS, "the X copy holds 64 rows");
@@ -1361,8 +1382,11 @@ __global__ __launch_bounds__(512) void softmax_rows_g2_kernel(RowsArgs a) {
   // W through a range-checked descriptor: ONE per-lane offset (class col, feature group q), the
   // chunk / slice / k-step part a scalar offset, classes past K read as zeros (masked in the
   // epilogue) - no clamped 64-bit address per fragment (those cost the registers the accumulators need)
-  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, K * a.F * 2, 0x00020000);
-  const uint32_t wlane = (uint32_t)(col * a.F + 8 * q) * 2u;
+  const auto wrs = PACKED ? __builtin_amdgcn_make_buffer_rsrc((void*)a.Wp, 0, (int)packed_w_bytes(K, a.F), 0x00020000)
+                         : __builtin_amdgcn_make_buffer_rsrc((void*)a.W, 0, K * a.F * 2, 0x00020000);
+  // PACKED: one contiguous 1 KB per fragment load (lane-linear); classes past K are out of the
+  // packed range (or zero-filled in its last class block) and read as zeros either way
+  const uint32_t wlane = PACKED ? (uint32_t)lane * 16u : (uint32_t)(col * a.F + 8 * q) * 2u;
   // k-step major: the first k-step's MFMAs wait for its 4 fragments only (vmcnt counts in order)
   auto load_w = [&](int c0, int sl, bf16x8_t(&wf)[4][KS]) {
 #pragma unroll
@@ -1371,7 +1395,11 @@ __global__ __launch_bounds__(512) void softmax_rows_g2_kernel(RowsArgs a) {
       for (int mt = 0; mt < 4; ++mt)
         wf[mt][ks] = __builtin_bit_cast(
             bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
-                          wrs, wlane, (uint32_t)(((c0 + mt * 16) * a.F + sl * SLICE + ks * 32) * 2), 0));
+                          wrs, wlane,
+                          PACKED
+                              ? (uint32_t)((((c0 + mt * 16) >> 4) * (a.F >> 5) + sl * KS + ks) * 1024)
+                              : (uint32_t)(((c0 + mt * 16) * a.F + sl * SLICE + ks * 32) * 2),
+                          0));
   };
   // X fragments one k-step at a time from the LDS copy (16 registers, not 32: the 128 accumulators
   // and both W fragments must fit 256 VGPRs at 2 waves per SIMD); the other wave covers the reads
@@ -1941,9 +1969,25 @@ bool softmax_rows_g_keeps_logits(int64_t B, int F, int K, int Kp) { return rows_
 
 void gemm_softmax_set_rows_g2(int on) { g_rows_g2 = on; }
 
+int g_w_packed = -1;  // gemm_softmax_set_w_packed: -1 MLAPI_G2_PACKED (default on), 0 off, 1 on
+
+bool w_packed_on() {
+  static const bool env = [] {
+    const char* e = std::getenv("MLAPI_G2_PACKED");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return g_w_packed < 0 ? env : g_w_packed != 0;
+}
+
+size_t softmax_rows_g_wpack_bytes(int64_t B, int F, int K, int Kp) {
+  return rows_g2(B, F, K, Kp) ? packed_w_bytes(K, F) : 0;
+}
+
+void gemm_softmax_set_w_packed(int on) { g_w_packed = on; }
+
 void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const float* b, const int32_t* y, int64_t B,
                            int F, int K, int kind, uint16_t* G, int Kp, float* stat_slabs, float* Zs,
-                           hipStream_t stream) {
+                           void* w_packed, hipStream_t stream) {
   if (B <= 0) return;
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("softmax_rows_g: multiclass kinds only");
@@ -1958,10 +2002,25 @@ void launch_softmax_rows_g(const void* X_aug, int64_t ldx, const void* W, const 
     // logits kept in registers (no Zs round trip): 8 waves x (at most) 2 class chunks
     const int nchunks = (K + CLASS_CHUNK - 1) / CLASS_CHUNK;
     const dim3 grid((unsigned)((B + XLDS_ROWS - 1) / XLDS_ROWS)), block(64 * std::min(nchunks, ROWS_MAX_WAVES));
-    if (kind == KIND_OVR)
+    if (w_packed != nullptr && w_packed_on()) {
+      // W re-laid in fragment order first (K x F bf16 read once, ~2 MB at F = 1024), then every
+      // block's fragment loads are contiguous 1 KB reads
+      if (reinterpret_cast<uintptr_t>(w_packed) % 16 != 0)
+        throw std::invalid_argument("softmax_rows_g: packed W buffer must be 16-byte aligned");
+      const int64_t pieces = (int64_t)packed_w_bytes(K, F) / 16;
+      hipLaunchKernelGGL(pack_w_frag_kernel, dim3((unsigned)((pieces + 255) / 256)), dim3(256), 0, stream,
+                         static_cast<const uint16_t*>(W), K, F, static_cast<uint16_t*>(w_packed), pieces);
+      MLAPI_HIP_CHECK(hipGetLastError());
+      ra.Wp = static_cast<const uint16_t*>(w_packed);
+      if (kind == KIND_OVR)
+        hipLaunchKernelGGL((softmax_rows_g2_kernel<true, true>), grid, block, 0, stream, ra);
+      else
+        hipLaunchKernelGGL((softmax_rows_g2_kernel<false, true>), grid, block, 0, stream, ra);
+    } else if (kind == KIND_OVR) {
       hipLaunchKernelGGL(softmax_rows_g2_kernel<true>, grid, block, 0, stream, ra);
-    else
+    } else {
       hipLaunchKernelGGL(softmax_rows_g2_kernel<false>, grid, block, 0, stream, ra);
+    }
     MLAPI_HIP_CHECK(hipGetLastError());
     return;
   }

@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void gdw_gemm_dma_kernel(const uint16_t* __res
 }
 
 struct WideLayout {
-  size_t g_off, dw_off, stat_off, z_off, total;
+  size_t g_off, dw_off, stat_off, z_off, wp_off, total;
   int Kp, row_groups, g_blocks;
   int64_t rows_per_group;
 };
@@ -243,6 +243,8 @@ WideLayout wide_layout(int64_t B, int K, int F) {
   o = al(o + (size_t)L.g_blocks * 2 * sizeof(float));
   L.z_off = o;  // the row-stats pass's logits, [B][Kp] f32 (zbuf_on(), unless the kernel keeps them in registers)
   if (!softmax_rows_g_keeps_logits(B, F, K, L.Kp)) o = al(o + (size_t)B * L.Kp * sizeof(float));
+  L.wp_off = o;  // W in MFMA-fragment order for the register-resident G kernel (0 bytes when it does not run)
+  o = al(o + softmax_rows_g_wpack_bytes(B, F, K, L.Kp));
   L.total = o;
   return L;
 }
@@ -287,7 +289,8 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
   float* slabs = reinterpret_cast<float*>(ws + L.dw_off);
   float* stat_slabs = reinterpret_cast<float*>(ws + L.stat_off);
   float* Zs = zbuf_on() && !softmax_rows_g_keeps_logits(B, F, K, L.Kp) ? reinterpret_cast<float*>(ws + L.z_off) : nullptr;
-  launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, Zs, stream);
+  void* wp = softmax_rows_g_wpack_bytes(B, F, K, L.Kp) ? static_cast<void*>(ws + L.wp_off) : nullptr;
+  launch_softmax_rows_g(X_aug, ldx, W, b, y, B, F, K, kind, G, L.Kp, stat_slabs, Zs, wp, stream);
   const int g_blocks = L.g_blocks;
   const int F_aug = F + 8;
   const int ncb = L.Kp / 128, nfb = (F_aug + TF128 - 1) / TF128;

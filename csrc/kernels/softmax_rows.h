@@ -140,6 +140,7 @@ struct RowsArgs {
   int Kp;
   float* Zs;  // [B][Kp] f32: the first pass's logits, read back by the second (null: recomputed)
   float* stat_slabs;  // [gridDim.x][2] {loss, correct}
+  const uint16_t* Wp;  // W in MFMA-fragment order (softmax_rows_g2_kernel<., true>), null otherwise
 };
 
 __device__ __forceinline__ uint16_t bf16_rne(float f) {

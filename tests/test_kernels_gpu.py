@@ -423,6 +423,15 @@ def test_softmax_grad_wide(B, F, K, kind):
     finally:
         C().gemm_softmax_set_rows_g2(-1)
     assert torch.equal(dW2, dW4) and torch.equal(st2, st4)
+    # W read in MFMA-fragment order (the packed copy, default) vs row-major: the same fragments,
+    # so the same bits
+    C().gemm_softmax_set_w_packed(0)
+    try:
+        dW5, st5 = ops.softmax_train_grad(Xa, Wb, b, y, kind, bufs=bufs)
+        torch.cuda.synchronize()
+    finally:
+        C().gemm_softmax_set_w_packed(-1)
+    assert torch.equal(dW2, dW5) and torch.equal(st2, st5)
 
 
 def test_sgd_wide_multiclass_estimator_one_gpu():
