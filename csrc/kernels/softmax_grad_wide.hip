@@ -224,7 +224,9 @@ WideLayout wide_layout(int64_t B, int K, int F) {
   }();
   int64_t rg = (target + tiles - 1) / tiles;
   // a group's G / X bytes stay below 2^31 (the G^T X kernel's buffer offsets are 32-bit)
-  const int64_t cap_rows = ((int64_t)INT32_MAX / (2 * std::max<int64_t>(L.Kp, F_aug))) / TILE_ROWS * TILE_ROWS;
+  // (X rows may be padded to a 64-element multiple: augment_features on the wide path)
+  const int64_t cap_rows =
+      ((int64_t)INT32_MAX / (2 * std::max<int64_t>(L.Kp, (F_aug + 63) / 64 * 64))) / TILE_ROWS * TILE_ROWS;
   rg = std::max<int64_t>(rg, (B + cap_rows - 1) / cap_rows);
   rg = (rg + 7) / 8 * 8;  // whole rounds of row groups over the 8 XCDs
   const int64_t max_rg = (B + 255) / 256;
@@ -275,7 +277,8 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
                               int dp_timeout_ms) {
   if (B <= 0) return;
   if (!softmax_grad_wide_supported(F)) throw std::invalid_argument("softmax_grad_wide: F must be a multiple of 256 above 512");
-  if (ldx != F + 8) throw std::invalid_argument("softmax_grad_wide: X_aug row stride must be F + 8");
+  if (ldx < F + 8 || ldx % 8 != 0)
+    throw std::invalid_argument("softmax_grad_wide: X_aug row stride must be >= F + 8 and a multiple of 8");
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("softmax_grad_wide: multiclass kinds only");
   if (update != nullptr && (update->params == nullptr || update->cols != F + 8 || update->pen_cols > F))
@@ -284,6 +287,8 @@ void launch_softmax_grad_wide(const void* X_aug, int64_t ldx, const void* W, con
     throw std::invalid_argument("softmax_grad_wide: X_aug and W must be 16-byte aligned");
   const WideLayout L = wide_layout(B, K, F);
   if (ws_bytes < L.total) throw std::invalid_argument("softmax_grad_wide: workspace too small");
+  if (L.rows_per_group * ldx * 2 > (int64_t)INT32_MAX)
+    throw std::invalid_argument("softmax_grad_wide: X_aug row stride too large for a row group's 32-bit offsets");
   unsigned char* ws = static_cast<unsigned char*>(workspace);
   uint16_t* G = reinterpret_cast<uint16_t*>(ws + L.g_off);
   float* slabs = reinterpret_cast<float*>(ws + L.dw_off);

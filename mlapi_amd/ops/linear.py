@@ -309,11 +309,22 @@ def softmax_train_faug(F: int) -> int:
     return softmax_kernel_width(F) + 8
 
 
+def xaug_row_stride(F_aug: int) -> int:
+    """Row stride (elements) of an augmented feature matrix. The wide path (kernel width > 512)
+    pads rows to a multiple of 64 bf16 = 128 bytes, so every row starts on a cache line: at
+    F_aug = 1032 an unpadded row starts 16 bytes further into its line each time, and the G^T X
+    kernel's 256-byte row segments straddle three lines instead of two (MLAPI_XAUG_PAD=0: unpadded)."""
+    if F_aug - 8 > 512 and os.environ.get("MLAPI_XAUG_PAD", "1") != "0":
+        return (F_aug + 63) // 64 * 64
+    return F_aug
+
+
 def augment_features(X: torch.Tensor, F_aug: int) -> torch.Tensor:
     """[X | 0.. | 1 | 0...] in bf16, shape [B, F_aug], the ones column at F_aug - 8 (done once per
-    dataset, not per step)."""
+    dataset, not per step). Wide widths come back as a row-padded view (:func:`xaug_row_stride`)."""
     B, F = X.shape
-    out = torch.zeros(B, F_aug, dtype=torch.bfloat16, device=X.device)
+    ld = xaug_row_stride(F_aug)
+    out = torch.zeros(B, ld, dtype=torch.bfloat16, device=X.device)[:, :F_aug]
     out[:, :F] = X
     out[:, F_aug - 8] = 1.0
     return out
@@ -360,12 +371,21 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
     all-reduce of [dW_aug | loss | correct] runs inside that final slab sum too (p2p_device.h), so
     a DP step stays 3 launches at any world size.
     """
-    _check(X_aug, W, b, y)
+    _check(W, b, y)
+    if not isinstance(X_aug, torch.Tensor) or not X_aug.is_cuda:
+        raise ValueError("mlapi_amd.ops: inputs must be GPU tensors (no CPU fallback)")
     if X_aug.dtype != torch.bfloat16 or W.dtype != torch.bfloat16 or b.dtype != torch.float32 \
             or y.dtype != torch.int32:
         raise TypeError("softmax_train_grad: X_aug, W bf16, b f32 and y int32")
     B, F_aug = X_aug.shape
     K, F = W.shape
+    # rows may be padded (augment_features on the wide path): unit column stride, row stride a
+    # multiple of 8 elements (16-byte aligned rows); the narrow kernels take unpadded rows only
+    ldx = X_aug.stride(0) if B > 0 else F_aug
+    if X_aug.stride(1) != 1 or ldx < F_aug or ldx % 8 != 0 \
+            or (ldx != F_aug and not C().softmax_grad_wide_supported(F)):
+        raise ValueError("mlapi_amd.ops: X_aug rows must be contiguous (row stride F_aug, or padded to a "
+                         "multiple of 8 on the wide path)")
     if (F not in SOFTMAX_TRAIN_WIDTHS and not C().softmax_grad_wide_supported(F)) or F_aug != F + 8 \
             or b.numel() != K or y.numel() != B:
         raise ValueError("softmax_train_grad: shape mismatch (W must be [K, Fk], Fk in 128/256/512 or a multiple "
@@ -388,7 +408,7 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
                    inv_n=float(update["inv_n"]), l2=float(update.get("l2", 0.0)),
                    momentum=float(update.get("momentum", 0.0)))
     launch = C().softmax_grad_wide if bufs.wide else C().softmax_grad_dw  # F > 512: softmax_grad_wide.hip
-    launch(X_aug.data_ptr(), F_aug, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
+    launch(X_aug.data_ptr(), ldx, W.data_ptr(), b.data_ptr(), y.data_ptr(), B, F, K, int(kind),
            dW_out.data_ptr(), stats.data_ptr(), bufs.ws.data_ptr(), bufs.ws.numel(), _stream(), **upd,
            p2p=None if p2p is None else p2p.native, timeout_ms=int(timeout_ms))
     return dW_out, stats
