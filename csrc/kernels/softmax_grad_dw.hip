@@ -742,7 +742,8 @@ void launch_softmax_grad_dw(const void* X_aug, int64_t ldx, const void* W, const
     throw std::invalid_argument("softmax_grad_dw: F must be 128, 256 or 512 (pad narrower features)");
   if (K < 2 || (kind != KIND_MULTINOMIAL && kind != KIND_OVR))
     throw std::invalid_argument("softmax_grad_dw: multiclass kinds only");
-  if (ldx != F + 8) throw std::invalid_argument("softmax_grad_dw: X_aug row stride must be F + 8");
+  if (ldx < F + 8 || ldx % 8 != 0)
+    throw std::invalid_argument("softmax_grad_dw: X_aug row stride must be >= F + 8 and a multiple of 8");
   if (reinterpret_cast<uintptr_t>(X_aug) % 16 != 0 || reinterpret_cast<uintptr_t>(W) % 16 != 0)
     throw std::invalid_argument("softmax_grad_dw: X_aug and W must be 16-byte aligned");
   const GdwLayout L = gdw_layout(B, K, F, auto_nc(K, F));

@@ -310,18 +310,18 @@ def softmax_train_faug(F: int) -> int:
 
 
 def xaug_row_stride(F_aug: int) -> int:
-    """Row stride (elements) of an augmented feature matrix. The wide path (kernel width > 512)
-    pads rows to a multiple of 64 bf16 = 128 bytes, so every row starts on a cache line: at
-    F_aug = 1032 an unpadded row starts 16 bytes further into its line each time, and the G^T X
-    kernel's 256-byte row segments straddle three lines instead of two (MLAPI_XAUG_PAD=0: unpadded)."""
-    if F_aug - 8 > 512 and os.environ.get("MLAPI_XAUG_PAD", "1") != "0":
+    """Row stride (elements) of an augmented feature matrix: padded to a multiple of 64 bf16 = 128
+    bytes, so every row starts on a cache line. Unpadded (F_aug = Fk + 8) a row starts 16 bytes
+    further into its line each time, and the kernels' row segments straddle one line more
+    (the F = 1024 G^T X launch: 197.5 -> 182.8 us padded; MLAPI_XAUG_PAD=0: unpadded)."""
+    if os.environ.get("MLAPI_XAUG_PAD", "1") != "0":
         return (F_aug + 63) // 64 * 64
     return F_aug
 
 
 def augment_features(X: torch.Tensor, F_aug: int) -> torch.Tensor:
     """[X | 0.. | 1 | 0...] in bf16, shape [B, F_aug], the ones column at F_aug - 8 (done once per
-    dataset, not per step). Wide widths come back as a row-padded view (:func:`xaug_row_stride`)."""
+    dataset, not per step), as a row-padded view (:func:`xaug_row_stride`)."""
     B, F = X.shape
     ld = xaug_row_stride(F_aug)
     out = torch.zeros(B, ld, dtype=torch.bfloat16, device=X.device)[:, :F_aug]
@@ -379,13 +379,12 @@ def softmax_train_grad(X_aug: torch.Tensor, W: torch.Tensor, b: torch.Tensor, y:
         raise TypeError("softmax_train_grad: X_aug, W bf16, b f32 and y int32")
     B, F_aug = X_aug.shape
     K, F = W.shape
-    # rows may be padded (augment_features on the wide path): unit column stride, row stride a
-    # multiple of 8 elements (16-byte aligned rows); the narrow kernels take unpadded rows only
+    # rows may be padded (augment_features): unit column stride, row stride a multiple of 8
+    # elements (16-byte aligned rows)
     ldx = X_aug.stride(0) if B > 0 else F_aug
-    if X_aug.stride(1) != 1 or ldx < F_aug or ldx % 8 != 0 \
-            or (ldx != F_aug and not C().softmax_grad_wide_supported(F)):
-        raise ValueError("mlapi_amd.ops: X_aug rows must be contiguous (row stride F_aug, or padded to a "
-                         "multiple of 8 on the wide path)")
+    if X_aug.stride(1) != 1 or ldx < F_aug or ldx % 8 != 0:
+        raise ValueError("mlapi_amd.ops: X_aug rows must be contiguous with a row stride >= F_aug, a "
+                         "multiple of 8")
     if (F not in SOFTMAX_TRAIN_WIDTHS and not C().softmax_grad_wide_supported(F)) or F_aug != F + 8 \
             or b.numel() != K or y.numel() != B:
         raise ValueError("softmax_train_grad: shape mismatch (W must be [K, Fk], Fk in 128/256/512 or a multiple "
