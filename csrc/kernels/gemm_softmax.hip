@@ -912,7 +912,7 @@ __device__ __forceinline__ void epilogue32(const f32x16_t (&acc)[RT][2], int c0,
 // tools/gemm_phase_probe.py; its outputs are meaningless). It splits the class loop's time into the
 // MFMA / LDS feed and the epilogue: 44.4k of 52.2k cycles per wave are the feed
 // (profiles/r2_gemm/phase_probe_noepi.log).
-template <int KS, int WV, int RT, int MODE, bool OVR, bool EPI = true, int AHEAD = 2, bool PRIO = false>
+template <int KS, int WV, int RT, int MODE, bool OVR, bool EPI = true, int AHEAD = 2, bool PRIO = false, bool XNT = false>
 __global__ __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(RT == 2 ? 1 : 2, RT == 2 ? 1 : 2))) void
 gemm_softmax32_kernel(GemmArgs a) {
   static_assert(MODE == 0 || MODE == 2 || MODE == 4, "logits mode runs the 16x16 kernel");
@@ -975,7 +975,12 @@ gemm_softmax32_kernel(GemmArgs a) {
     const uint16_t* xr = X + r * a.ldx + 8 * h;
 #pragma unroll
     for (int k = 0; k < K2; ++k)
-      xf[rt][k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + k * 16));
+      // Plain loads: an X row's 512 bytes reach a wave as 16 instructions of 32 bytes per lane, so
+      // each 128-byte line is touched by 4 of them; with the nontemporal hint (XNT, measurement
+      // variant) the line was not kept for the other 3 - prologue 10.9k -> 6.8k cycles per wave,
+      // the B = 262,144 launch 166.9 -> 150.4 us under the phase stamps (profiles/r6_gemm/)
+      xf[rt][k] = XNT ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + k * 16))
+                      : *reinterpret_cast<const bf16x8_t*>(xr + k * 16);
   }
   constexpr int kWaitAll = (7 << 4) | (15 << 8);
   __builtin_amdgcn_s_waitcnt(kWaitAll);  // chunk 0 + X
@@ -1741,6 +1746,11 @@ void launch32(const GemmArgs& args, const dim3& grid, int rt, hipStream_t stream
     if constexpr (MODE == 0 && KS == 8) {
       if (!o && g_force_kernel == 5) {  // measurement: epilogue compiled out
         hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, false>), grid, dim3(256), 0, stream, args);
+        return;
+      }
+      if (!o && g_force_kernel == 9) {  // measurement: X loaded with the nontemporal hint (round 5's loads)
+        hipLaunchKernelGGL((gemm_softmax32_kernel<KS, 4, 1, MODE, false, true, 2, false, true>), grid, dim3(256), 0,
+                           stream, args);
         return;
       }
       if (!o && g_force_kernel == 8) {  // measurement: s_setprio around each k-step's MFMAs

@@ -16,7 +16,7 @@ from mlapi_amd.ops import linear as ops  # noqa: E402
 
 dev = torch.device("cuda", 0)
 F, K = 256, 1000
-PLANS = {"auto": (0, 0, 0), "t16_nt2": (2, 0, 1), "t32": (0, 0, 3), "t32_noepi": (0, 0, 5), "t32_ahead1": (0, 0, 6), "t32_ahead3": (0, 0, 7)}
+PLANS = {"auto": (0, 0, 0), "t16_nt2": (2, 0, 1), "t32": (0, 0, 3), "t32_noepi": (0, 0, 5), "t32_ahead1": (0, 0, 6), "t32_ahead3": (0, 0, 7), "t32_xnt": (0, 0, 9)}
 for B in tuple(int(a) for a in sys.argv[1:]) or (1024, 262144):
     X = torch.randn(B, F, device=dev).to(torch.bfloat16)
     W = (torch.randn(K, F, device=dev) / 16).to(torch.bfloat16)
