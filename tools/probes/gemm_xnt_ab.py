@@ -15,8 +15,12 @@ W = (torch.randn(K, F, device=dev) / 16).to(torch.bfloat16)
 b = torch.randn(K, device=dev) * 0.1
 out = (torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, device=dev))
 res = {}
+# default: plain vs nontemporal X; argv "all": also the W look-ahead (1 / 3 k-steps) and s_setprio variants
+VARIANTS = [("plain", 0), ("nontemporal", 9)]
+if "all" in sys.argv[1:]:
+    VARIANTS += [("ahead1", 6), ("ahead3", 7), ("setprio", 8)]
 for rnd in range(4):
-    for name, kern in (("plain", 0), ("nontemporal", 9)):
+    for name, kern in VARIANTS:
         C().gemm_softmax_force_plan(0, 0, kern)
         op = ops.GemmSoftmax(B, K, F, dev)
         for _ in range(10):
