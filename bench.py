@@ -156,9 +156,14 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
     device = "cpu" if info.device is None else f"cuda:{info.device.index}"
     client_cpus, io_cpus = _thread_cpus(args, info)
     args.io_cpus = io_cpus
+    # dispatch "source": this rank's load generator connects from an address of its own, and this
+    # rank's replica claims it - its clients (pinned next to this replica's IO threads) are served
+    # here from the first connection on, not by whichever replica the round robin reached first
+    src = f"127.1.{info.rank // 250}.{info.rank % 250 + 1}" if args.dispatch == "source" else ""
     mk = lambda port: Config.from_env(port=port, device=device, reload="off", missing_model="keep",  # noqa: E731
                                       io_threads=args.io_threads, max_batch=args.max_batch, reuseport=True,
                                       dispatch=args.dispatch, io_cpus=",".join(str(c) for c in io_cpus),
+                                      dispatch_claim=src,
                                       model_path="/nonexistent/bench.pkl", feature_names=list(names), **dtype_cfg)
     srv = None
     # everything from the server start on is inside the try: a failed workload pre-check (or any
@@ -177,10 +182,8 @@ def _serve_bench(args, info, model, names, rows, *, dtype_cfg, rel_tol, oracle_k
         reqs, exp = make_workload(srv.runtime.handle.engine, model, names, rows, **oracle_kw)
         lg.workload(reqs, exp, rel_tol)
         barrier(info)  # every rank's listeners are in the group before any client connects
-        # dispatch "source": this rank's load generator connects from an address of its own, so
-        # the acceptor keeps its connections together on one replica, in connect order (as client
-        # hosts of their own would be); "acceptor" deals every connection round robin over ranks
-        src = f"127.1.{info.rank // 250}.{info.rank % 250 + 1}" if args.dispatch == "source" else ""
+        # "acceptor" deals every connection round robin over ranks; "source" keeps this rank's
+        # connections together on the replica that claimed their address (see src above)
         lg.connect("127.0.0.1", port, args.conns, args.client_threads, source=src)
         lg.thread_cpus(client_cpus)
         if args.warmup:

@@ -604,7 +604,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("dispatch", &ServerConfig::dispatch)
       .def_readwrite("stage_timing", &ServerConfig::stage_timing)
       .def_readwrite("dispatch_group", &ServerConfig::dispatch_group)
-      .def_readwrite("dispatch_rank", &ServerConfig::dispatch_rank);
+      .def_readwrite("dispatch_rank", &ServerConfig::dispatch_rank)
+      .def_readwrite("dispatch_claim", &ServerConfig::dispatch_claim);
 
   // ---- native RCCL communicator (csrc/dist/comm.h)
   py::class_<RcclComm>(m, "RcclComm")

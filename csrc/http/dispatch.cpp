@@ -27,6 +27,7 @@ struct Hello {
   uint32_t magic;
   int32_t rank;
   int32_t pid;
+  char claim[48];  // client address this member claims (source affinity), "" = none
 };
 struct Reply {
   uint32_t magic;
@@ -108,7 +109,8 @@ bool same_user(int fd) {
 }  // namespace
 
 ConnDispatcher::ConnDispatcher(std::string group, std::string host, int port, int backlog, int rank,
-                               std::function<void(int)> adopt, std::function<bool()> healthy, bool source_affinity)
+                               std::function<void(int)> adopt, std::function<bool()> healthy, bool source_affinity,
+                               std::string claim)
     : group_(std::move(group)),
       host_(std::move(host)),
       want_port_(port),
@@ -116,6 +118,7 @@ ConnDispatcher::ConnDispatcher(std::string group, std::string host, int port, in
       rank_(rank),
       adopt_(std::move(adopt)),
       healthy_(std::move(healthy)),
+      claim_(claim.size() < sizeof(Hello::claim) ? std::move(claim) : std::string()),
       source_affinity_(source_affinity) {
   wake_fd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
   if (wake_fd_ < 0) throw std::runtime_error("dispatch: eventfd failed");
@@ -171,6 +174,10 @@ bool ConnDispatcher::try_lead() {
   port_.store(bound);
   leader_.store(true);
   elections_.fetch_add(1);
+  if (source_affinity_ && !claim_.empty()) {
+    std::lock_guard<std::mutex> lk(mu_);
+    affinity_[claim_] = -1;  // the leader's own clients stay here
+  }
   return true;
 }
 
@@ -185,7 +192,8 @@ bool ConnDispatcher::try_join() {
   }
   timeval tv{2, 0};
   setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
-  const Hello h{MAGIC, rank_, (int32_t)getpid()};
+  Hello h{MAGIC, rank_, (int32_t)getpid(), {}};
+  memcpy(h.claim, claim_.c_str(), claim_.size() + 1);
   Reply r{};
   if (send(c, &h, sizeof h, MSG_NOSIGNAL) != (ssize_t)sizeof h || recv(c, &r, sizeof r, 0) != (ssize_t)sizeof r ||
       r.magic != MAGIC) {
@@ -372,6 +380,15 @@ void ConnDispatcher::lead_loop() {
         Hello h{};
         const ssize_t r = recv(m.fd, &h, sizeof h, MSG_DONTWAIT);
         if (r == (ssize_t)sizeof h && h.magic == MAGIC) {
+          // a claimed client address goes to this member from its first connection on (the
+          // replica beside those clients: its IO threads run next to their CPUs). Recorded before
+          // the reply, so the claim is in place when the member's start() returns; a member that
+          // then fails leaves a claim to a rank no member has, which dispatch() drops
+          h.claim[sizeof h.claim - 1] = '\0';
+          if (source_affinity_ && h.claim[0] != '\0') {
+            std::lock_guard<std::mutex> lk(mu_);
+            affinity_[std::string(h.claim)] = h.rank;
+          }
           const Reply rep{MAGIC, port_.load()};
           if (send(m.fd, &rep, sizeof rep, MSG_NOSIGNAL) == (ssize_t)sizeof rep) {
             std::lock_guard<std::mutex> lk(mu_);

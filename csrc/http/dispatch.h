@@ -52,7 +52,8 @@ class ConnDispatcher {
   // adopt(fd): give a connected TCP socket to this process's IO threads. healthy(): may this
   // process receive new connections.
   ConnDispatcher(std::string group, std::string host, int port, int backlog, int rank,
-                 std::function<void(int)> adopt, std::function<bool()> healthy, bool source_affinity = false);
+                 std::function<void(int)> adopt, std::function<bool()> healthy, bool source_affinity = false,
+                 std::string claim = "");
   ~ConnDispatcher();
   ConnDispatcher(const ConnDispatcher&) = delete;
   ConnDispatcher& operator=(const ConnDispatcher&) = delete;
@@ -98,6 +99,7 @@ class ConnDispatcher {
   bool self_healthy_ = true;
   uint64_t self_conns_ = 0;
   size_t rr_ = 0;
+  std::string claim_;  // client address this process claims (source affinity; sent in its hello)
   bool source_affinity_ = false;
   std::unordered_map<std::string, int> affinity_;  // client address -> target rank (-1 = leader)
   mutable std::mutex mu_;  // members_, self_* (read by targets())

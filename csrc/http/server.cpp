@@ -1515,7 +1515,7 @@ void HttpServer::start() {
     dispatcher_ = std::make_unique<ConnDispatcher>(
         cfg_.dispatch_group, cfg_.host, cfg_.port, cfg_.backlog, cfg_.dispatch_rank,
         [this](int fd) { threads_[adopt_rr_.fetch_add(1, std::memory_order_relaxed) % threads_.size()]->adopt(fd); },
-        [this] { return accepting(); }, cfg_.dispatch == "source");
+        [this] { return accepting(); }, cfg_.dispatch == "source", cfg_.dispatch_claim);
     try {
       dispatcher_->start();
     } catch (...) {

@@ -94,6 +94,9 @@ struct ServerConfig {
   std::string dispatch = "acceptor";
   std::string dispatch_group;  // "" = named after host:port
   int dispatch_rank = 0;       // this replica's rank (reported to the group's leader)
+  // dispatch = source: a client address this replica claims - its connections come here from the
+  // first on (e.g. the co-located load generator's address), instead of round robin ("" = none)
+  std::string dispatch_claim;
 };
 
 struct SlowRequest {

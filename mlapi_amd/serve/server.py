@@ -74,6 +74,7 @@ class NativeServer:
         sc.access_log_fd = int(access_log_fd)
         sc.dispatch = str(config.dispatch)
         sc.dispatch_group = str(config.dispatch_group)
+        sc.dispatch_claim = str(config.dispatch_claim)
         sc.dispatch_rank = int(os.environ.get("RANK", "0"))
         hd = str(config.health_dispatch).lower()
         sc.health_dispatch = hd == "on" or (hd == "auto" and int(os.environ.get("WORLD_SIZE", "1")) > 1)

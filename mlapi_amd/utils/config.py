@@ -97,6 +97,7 @@ class Config:
                                               # the replicas / IO threads (csrc/http/dispatch.h) | source: the same,
                                               # a client address keeping its replica | reuseport: kernel hash
     dispatch_group: str = ""                  # acceptor group name ("" = named after host:port)
+    dispatch_claim: str = ""                   # dispatch=source: client address this replica claims ("" = none)
     admin: str = "loopback"                   # POST /admin/*: loopback (local clients only) | on | off
     # observability
     metrics: bool = True

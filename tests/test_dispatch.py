@@ -40,14 +40,14 @@ def _post(port, body=A1, keep=None):
     return int(head.split()[1]), s
 
 
-def _server(port, rank, io_threads=2, group="", dispatch="acceptor"):
+def _server(port, rank, io_threads=2, group="", dispatch="acceptor", claim=""):
     from mlapi_amd.serve.server import NativeServer
     from mlapi_amd.utils.config import Config
 
     os.environ["RANK"] = str(rank)  # the replica's rank, reported to the group's leader
     try:
         srv = NativeServer(Config.from_env(port=port, device="cpu", io_threads=io_threads, dispatch=dispatch,
-                                           dispatch_group=group)).start()
+                                           dispatch_group=group, dispatch_claim=claim)).start()
     finally:
         os.environ.pop("RANK", None)
     return srv
@@ -96,6 +96,37 @@ def _post_from(port, source):
     s.settimeout(10)
     s.connect(("127.0.0.1", port))
     return _post(port, keep=s)
+
+
+def test_claimed_client_address_goes_to_its_replica(iris_cwd):
+    """dispatch=source with claims: replica r claims 127.1.0.(r+1); the addresses then reach their own
+    replicas whatever order they first connect in (without claims the first-seen address takes the
+    leader) - the bench's rank-local load generators stay on their own rank's replica."""
+    port = _free_port()
+    srvs = [_server(port, r, io_threads=2, dispatch="source", claim=f"127.1.0.{r + 1}") for r in range(3)]
+    try:
+        t0 = time.time()
+        while len(srvs[0].http.stats()["dispatch"]["targets"]) < 3:
+            assert time.time() - t0 < 10
+            time.sleep(0.01)
+        socks = []
+        for k in range(4):
+            for a in ("127.1.0.3", "127.1.0.2", "127.1.0.1"):  # reverse of the claims' order
+                st, s = _post_from(port, a)
+                assert st == 200
+                socks.append(s)
+        assert [s.http.stats()["connections"] for s in srvs] == [4, 4, 4]
+        assert [s.http.stats()["dispatch"]["received"] for s in srvs] == [4, 4, 4]
+        # an unclaimed address still goes round robin
+        st, s = _post_from(port, "127.1.0.9")
+        assert st == 200
+        socks.append(s)
+        assert sum(x.http.stats()["connections"] for x in srvs) == 13
+        for s in socks:
+            s.close()
+    finally:
+        for s in srvs:
+            s.stop()
 
 
 def test_source_affinity_keeps_a_client_address_on_one_replica(iris_cwd):
