@@ -96,6 +96,7 @@ struct GemmArgs {
   int xcd_local;               // split merge meets in one XCD's L2 (grid.x % 8 == 0; see put_granule)
   int xcd_inject;              // test hook (xcd_local_inject): every merged row reports a misplaced partial
   unsigned epoch;              // split merge: this launch's granule tag (1 .. 2^28 - 1, see put_granule)
+  int x_nt;                    // 16x16 kernel, NT = 2: X with the nontemporal hint (MLAPI_GEMM_XNT16=1, measurement)
 };
 
 // ---- split-merge protocol (tiles kernels): tagged granules (cdna_hip_programming.md Guideline 16
@@ -581,10 +582,10 @@ gemm_softmax_kernel(GemmArgs a) {
     const uint16_t* xr = X + r * a.ldx + 8 * q;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      // Large batches (NT = 2) stream X once: non-temporal, keep the L2 for W. Small batches split
-      // the classes, and every split block of a row block (same XCD: blockIdx.x + 16y = x mod 8)
-      // re-reads the same X rows, so those loads stay cacheable.
-      if constexpr (NT == 2)
+      // Plain loads, as in the 32x32 kernel (where dropping the nontemporal hint took 147.7 ->
+      // 137.3 us); here neutral: F = 512, B = 262,144 514-517 vs 514-523 us with the hint
+      // (MLAPI_GEMM_XNT16=1, profiles/r6_gemm/xnt16/)
+      if (NT == 2 && a.x_nt)
         xf[t][ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(xr + ks * 32));
       else
         xf[t][ks] = *reinterpret_cast<const bf16x8_t*>(xr + ks * 32);
@@ -1854,6 +1855,11 @@ GemmArgs base_args(const void* X, const void* W, int64_t B, int F, int K, int ki
   a.B = B;
   a.K = K;
   a.kind = kind;
+  static const int xnt16 = [] {
+    const char* e = std::getenv("MLAPI_GEMM_XNT16");
+    return e != nullptr && std::atoi(e) != 0 ? 1 : 0;
+  }();
+  a.x_nt = xnt16;
   return a;
 }
 
