@@ -1621,6 +1621,8 @@ int Engine::resident_cpu_poll(const std::shared_ptr<const Model>& m, uint32_t mv
         if (full) x[f] = g[f].x;
       }
       if (!full) break;
+      // a hang injected while this call was already past its check answers nothing more
+      if (__atomic_load_n(&res_ctl_h_->fault, __ATOMIC_ACQUIRE) == RES_FAULT_STALL) break;
       int32_t idx = RESIDENT_STALE_IDX;
       double p = 0.0;
       if (!bounce && m && (meta >> 8) == mver && rf == m->F) cpu_linear_predict(*m, x, 1, &idx, &p);

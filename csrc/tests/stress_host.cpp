@@ -368,10 +368,12 @@ void ring_stress() {
   check_answers(10);
   // sticky hang: the rows give up after 10 x watchdog as device errors; nothing stays pending
   CHECK(eng.resident_inject(Engine::RES_INJECT_STALL_STICKY, 0), "inject");
+  std::this_thread::sleep_for(std::chrono::milliseconds(20));  // the poller has seen the hang
   CHECK(submit(20, 2), "submit (stalled)");
   drain(2, 6000);
   CHECK(out.size() == 2 && out[0].status == ST_DEVICE_ERROR && out[1].status == ST_DEVICE_ERROR,
-        "given-up rows: %zu completions", out.size());
+        "given-up rows: %zu completions (status %d, %d)", out.size(), out.empty() ? -1 : (int)out[0].status,
+        out.size() < 2 ? -1 : (int)out[1].status);
   CHECK(ring->pending() == 0, "pending after give-up: %d", ring->pending());
   // close with rows pending (still hung): the next owner sees none of them
   CHECK(submit(30, 2), "submit (before close)");
